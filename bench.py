@@ -1,0 +1,218 @@
+"""bench.py -- trellis cells/s of the MI355X Viterbi decode path (BASELINE.json metric).
+
+Workload (BASELINE.json configs[3]): synthetic HMM with N=256
+states, V=1,024 observations (bdims [32,32]), Dirichlet(1) rows in log10, iid uniform
+observations from splitmix64; T=512, B=65,536 sequences in total, f32 row-A0 trellis.
+The batch is sharded across ranks (strong scaling: total work fixed, B/N per GPU); one
+step = decode of the rank's shard (forward trellis kernel + backtrack + f64 re-score of
+every path) followed, for N>1, by an RCCL gather of paths, scores and statuses to rank 0
+over xGMI.  Inputs are resident in HBM before the timed region.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+       (N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N)
+Rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "consistent-viterbi_amd"))
+
+N_STATES, V_OBS, T_LEN, B_TOTAL, SEED = 256, 1024, 512, 65536, 20261015
+HBM_PEAK = 8.0e12            # B/s, MI355X_MICROARCH.md chip table (spec)
+VALU_PAIR_PEAK = 3.93e13     # (from,to) pairs/s: 256 CU x 4 SIMD x 32 lanes x 2.4 GHz / 2 VALU slots per pair
+WORKSPACE = 48 << 30         # delta workspace cap: one forward launch per step at N=1 (34.4 GB)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=10)
+    p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--batch", type=int, default=B_TOTAL, help="total sequences (default 65,536)")
+    p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    return p.parse_args()
+
+
+def cpu_baseline(pi, a, b, obs_rank, budget_s):
+    """Oracle (C restatement of the reference's CPSolver forward + backtrack, f64, CP
+    association = what main.rs:120 runs) timed on this host, 1 thread, on the first k
+    sequences of this rank's shard; k grows until ~budget_s of CPU work."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import c_oracle
+
+    def run(k):
+        off = np.arange(k + 1, dtype=np.int64) * T_LEN
+        t0 = time.perf_counter()
+        c_oracle.decode_batch(pi, a, b, off, obs_rank[: k * T_LEN], c_oracle.CP, np.float64, nthreads=1)
+        return time.perf_counter() - t0
+
+    k = 2
+    dt = run(k)
+    k = max(2, min(int(budget_s / max(dt / k, 1e-6)), 4096))
+    dt = run(k)
+    cells = k * T_LEN * N_STATES
+    return {"value": cells / dt, "unit": "trellis cells/s", "cores": 1, "kind": "port",
+            "sample": f"first {k} sequences of config 4 (N=256, T=512), f64 CP association "
+                      f"(cp.rs:95-125), oracle/cv_oracle.c single thread, {dt:.1f} s",
+            "seconds": dt}
+
+
+def load_traffic():
+    """Per-launch HBM bytes of the forward kernel from the committed rocprofv3 PMC summary."""
+    p = os.path.join(ROOT, "profiles", "pmc_trellis_fwd_c4.json")
+    if not os.path.exists(p):
+        return None
+    try:
+        with open(p) as f:
+            d = json.load(f)
+        return float(d["hbm_bytes_per_launch"])
+    except Exception:
+        return None
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    import cviterbi as cv
+    from cviterbi import synth
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    if not torch.cuda.is_available():
+        raise SystemExit("bench.py needs a GPU (MI355X); none visible")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    B = args.batch
+    per = (B + world - 1) // world
+    s0, s1 = min(rank * per, B), min((rank + 1) * per, B)
+    nloc = s1 - s0
+    pi, a, b = synth.random_hmm(N_STATES, V_OBS, seed=SEED)
+    obs = synth.iid_obs(V_OBS, nloc * T_LEN, SEED, start=s0 * T_LEN)
+    off = np.arange(nloc + 1, dtype=np.int64) * T_LEN
+
+    h = cv.HMM(pi, a, b.reshape(N_STATES, 32, 32), device=local)
+    stream = torch.cuda.Stream(dev)  # non-default stream shared by the decode and the gathers
+    torch.cuda.set_stream(stream)
+    off_d = torch.from_numpy(off).to(dev)
+    obs_d = torch.from_numpy(obs).to(dev)
+    path_d = torch.empty(nloc * T_LEN, dtype=torch.int32, device=dev)
+    score_d = torch.empty(nloc, dtype=torch.float64, device=dev)
+    status_d = torch.empty(nloc, dtype=torch.uint8, device=dev)
+    if world > 1 and rank == 0:
+        gpath = [torch.empty(per * T_LEN, dtype=torch.int32, device=dev) for _ in range(world)]
+        gscore = [torch.empty(per, dtype=torch.float64, device=dev) for _ in range(world)]
+        gstat = [torch.empty(per, dtype=torch.uint8, device=dev) for _ in range(world)]
+    else:
+        gpath = gscore = gstat = None
+
+    def pad(x, n):
+        if x.numel() == n:
+            return x
+        y = torch.zeros(n, dtype=x.dtype, device=dev)
+        y[: x.numel()] = x
+        return y
+
+    def step():
+        cv.decode_batch_device(h, off_d, obs_d, path_d, score_d, status_d, offsets_host=off,
+                               stream=stream.cuda_stream, workspace_bytes=WORKSPACE)
+        if world > 1:  # RCCL over xGMI: decoded paths, scores, statuses to rank 0
+            dist.gather(pad(path_d, per * T_LEN), gpath, dst=0)
+            dist.gather(pad(score_d, per), gscore, dst=0)
+            dist.gather(pad(status_d, per), gstat, dst=0)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    bad = int((status_d != 0).sum().item())
+    if bad:
+        raise SystemExit(f"rank {rank}: {bad} sequences did not decode cleanly")
+
+    # timed region: barrier + sync on both sides, exactly K steps
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    fwd_ms, bt_ms, launches = 0.0, 0.0, 0
+    for _ in range(args.steps):
+        step()
+        t = cv.last_timing(h)  # HIP events recorded around each kernel on `stream`
+        fwd_ms += t["fwd_ms"]
+        bt_ms += t["bt_ms"]
+        launches += t["launches"]
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        el = float(tt.item())
+
+    cells_total = B * T_LEN * N_STATES * args.steps
+    value = cells_total / el
+    ms_step = el * 1e3 / args.steps
+    # roofline of the dominant kernel (forward trellis) on THIS rank, per launch
+    steps_rank = nloc * T_LEN
+    alg_bytes = (9 * N_STATES + 8) * steps_rank + 8 * nloc
+    alg_read = (4 * N_STATES + 4) * steps_rank
+    fwd_launch_s = fwd_ms / max(launches, 1) * 1e-3
+    per_launch_bytes = alg_bytes / (launches / args.steps)
+    achieved = per_launch_bytes / fwd_launch_s
+    pairs_per_launch = N_STATES * N_STATES * (T_LEN - 1) * nloc / (launches / args.steps)
+    traffic = load_traffic()
+    out = {
+        "metric": "trellis cells/s (N*T*batch), N=256 T=512 batch=65536",
+        "value": value,
+        "unit": "trellis cells/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_step,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (Dirichlet(1) log10 HMM, splitmix64 iid observations; SURVEY.md §8d config 4)",
+        "config": {"workload": "config4: N=256 states, V=1024, T=512, batch=65536 sharded over ranks, f32 row-A0 "
+                               "trellis + backtrack + f64 re-score" + (", RCCL gather to rank 0" if world > 1 else ""),
+                   "global_batch": B, "seq_len": T_LEN, "states": N_STATES, "parallelism": f"batch-shard x{world}"},
+        "seqs_per_s": B * args.steps / el,
+        "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK, "traffic": traffic,
+                     "kernel": "trellis_fwd_f32<256>", "kernel_ms_per_launch": fwd_launch_s * 1e3,
+                     "alg_bytes_per_launch": per_launch_bytes,
+                     "read_only_frac": alg_read / (launches / args.steps) / fwd_launch_s / HBM_PEAK,
+                     "binding": "valu",
+                     "valu": {"achieved_pairs_per_s": pairs_per_launch / fwd_launch_s, "peak_pairs_per_s": VALU_PAIR_PEAK,
+                              "frac": pairs_per_launch / fwd_launch_s / VALU_PAIR_PEAK}},
+        "kernel_ms_per_step": {"forward": fwd_ms / args.steps, "backtrack_rescore": bt_ms / args.steps},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(pi, a, b, obs, args.cpu_seconds)
+        out["cpu_baseline"]["gpu_over_cpu"] = value / out["cpu_baseline"]["value"]
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,789 @@
+// cviterbi.cpp -- C ABI (include/cviterbi.h) over the MI355X trellis kernels.
+//
+// Host side of the drop-in boundary: the HMM handle mirrors struct HMM<D> and its
+// log-prob lookups (src/hmm/hmm.rs:10-18, 407-445), the batch decode replaces the
+// dense forward + backtrack of viterbi_solver (cp.rs:95-125, viterbi.rs:5-32,
+// dp.rs:94-209), and cv_solver_* mirrors `trait Solver` (viterbi_solver.rs:11-16).
+//
+// There is deliberately no CPU decode path here: every decode runs the HIP kernels
+// in kernels/trellis.hip and fails with CV_EDEVICE if no gfx950 device is usable.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <numeric>
+#include <string>
+#include <vector>
+
+#include "../../include/cviterbi.h"
+#include "hmm_json.hpp"
+#include "kernels/trellis.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+cv_status set_err(cv_status st, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return st;
+}
+
+#define HIP_TRY(expr)                                                                          \
+  do {                                                                                         \
+    hipError_t _e = (expr);                                                                    \
+    if (_e != hipSuccess)                                                                      \
+      return set_err(CV_EDEVICE, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(_e), __FILE__, \
+                     __LINE__);                                                                \
+  } while (0)
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  DevBuf() = default;
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+  ~DevBuf() { release(); }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+  }
+  cv_status ensure(size_t n) {
+    if (n <= bytes && p) return CV_OK;
+    release();
+    if (n == 0) n = 16;
+    hipError_t e = hipMalloc(&p, n);
+    if (e != hipSuccess) {
+      p = nullptr;
+      (void)hipGetLastError();
+      return set_err(CV_ENOMEM, "hipMalloc(%zu) failed: %s", n, hipGetErrorString(e));
+    }
+    bytes = n;
+    return CV_OK;
+  }
+  template <typename T>
+  T* as() const {
+    return static_cast<T*>(p);
+  }
+};
+
+cv_status upload(DevBuf& buf, const void* src, size_t bytes) {
+  cv_status st = buf.ensure(bytes);
+  if (st != CV_OK) return st;
+  HIP_TRY(hipMemcpy(buf.p, src, bytes, hipMemcpyHostToDevice));
+  return CV_OK;
+}
+
+constexpr uint64_t kDefaultWorkspace = 8ull << 30;
+
+}  // namespace
+
+struct cv_hmm {
+  int N = 0, D = 0;
+  std::vector<int64_t> bdims;
+  int64_t V = 0;
+  std::vector<double> pi, a, b;  // host log10, canonical (-0.0 -> +0.0); b state-major [N*V]
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::mutex mu;
+
+  // trellis kernel tables (f32, padded to NP)
+  int np = 0;
+  DevBuf t_aimg, t_pi, t_et, t_at;
+  // f64 tables (generic f64 kernel + re-scoring): pi[N], a[N*N], et[V][N]
+  bool f64_ready = false;
+  DevBuf d_pi64, d_a64, d_et64;
+  // f32 generic tables
+  bool g32_ready = false;
+  DevBuf d_pi32, d_a32, d_et32;
+  // workspace
+  DevBuf ws_main, ws_last, ws_order;
+  DevBuf st_off, st_obs, st_path, st_score, st_status;
+  std::vector<int32_t> order_host;
+  // timing events of the last call
+  std::vector<hipEvent_t> ev;  // 3 per launch: start, mid, end
+  int64_t last_launches = 0;
+  int32_t last_kernel = 0;
+  int32_t last_np = 0;
+
+  ~cv_hmm() {
+    for (auto e : ev) (void)hipEventDestroy(e);
+    if (stream) (void)hipStreamDestroy(stream);
+  }
+};
+
+namespace {
+
+cv_status set_device(cv_hmm* h) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) {
+    (void)hipGetLastError();
+    return set_err(CV_EDEVICE, "no HIP device available");
+  }
+  if (h->device < 0 || h->device >= n) return set_err(CV_EDEVICE, "device %d out of range (%d devices)", h->device, n);
+  HIP_TRY(hipSetDevice(h->device));
+  if (!h->stream) HIP_TRY(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+  return CV_OK;
+}
+
+float f32(double x) { return (float)x; }
+
+// Trellis tables.  a_img: float4 per (wave w, pair q, lane): rows r0 = rg*R + 2q, r0+1 and
+// columns j0 = 16w + 2cp, j0+1 with rg = lane&7, cp = lane>>3 (trellis_fwd_f32 layout).
+cv_status ensure_trellis_tables(cv_hmm* h) {
+  const int np = cvk::trellis_padded_states(h->N);
+  if (!np) return set_err(CV_EUNSUPPORTED, "trellis kernel covers 1 <= N <= 256 (N=%d)", h->N);
+  if (h->np == np) return CV_OK;
+  const int N = h->N;
+  const int64_t V = h->V;
+  const int R = np / 8;
+  const float NI = -INFINITY;
+  auto A = [&](int i, int j) -> float { return (i < N && j < N) ? f32(h->a[(size_t)i * N + j]) : NI; };
+  std::vector<float> img((size_t)np * np);
+  for (int w = 0; w < np / 16; ++w)
+    for (int q = 0; q < R / 2; ++q)
+      for (int lane = 0; lane < 64; ++lane) {
+        const int rg = lane & 7, cp = lane >> 3, j0 = 16 * w + 2 * cp, r0 = rg * R + 2 * q;
+        float* dst = &img[(((size_t)w * (R / 2) + q) * 64 + lane) * 4];
+        dst[0] = A(r0, j0);
+        dst[1] = A(r0, j0 + 1);
+        dst[2] = A(r0 + 1, j0);
+        dst[3] = A(r0 + 1, j0 + 1);
+      }
+  std::vector<float> pi(np, NI), at((size_t)np * np, NI), et((size_t)V * np, NI);
+  for (int j = 0; j < N; ++j) pi[j] = f32(h->pi[j]);
+  for (int i = 0; i < N; ++i)
+    for (int j = 0; j < N; ++j) at[(size_t)j * np + i] = f32(h->a[(size_t)i * N + j]);
+  for (int j = 0; j < N; ++j)
+    for (int64_t o = 0; o < V; ++o) et[(size_t)o * np + j] = f32(h->b[(size_t)j * V + o]);
+  cv_status st;
+  if ((st = upload(h->t_aimg, img.data(), img.size() * 4)) != CV_OK) return st;
+  if ((st = upload(h->t_pi, pi.data(), pi.size() * 4)) != CV_OK) return st;
+  if ((st = upload(h->t_at, at.data(), at.size() * 4)) != CV_OK) return st;
+  if ((st = upload(h->t_et, et.data(), et.size() * 4)) != CV_OK) return st;
+  h->np = np;
+  return CV_OK;
+}
+
+cv_status ensure_f64_tables(cv_hmm* h) {
+  if (h->f64_ready) return CV_OK;
+  const int N = h->N;
+  const int64_t V = h->V;
+  std::vector<double> et((size_t)V * N);
+  for (int j = 0; j < N; ++j)
+    for (int64_t o = 0; o < V; ++o) et[(size_t)o * N + j] = h->b[(size_t)j * V + o];
+  cv_status st;
+  if ((st = upload(h->d_pi64, h->pi.data(), (size_t)N * 8)) != CV_OK) return st;
+  if ((st = upload(h->d_a64, h->a.data(), (size_t)N * N * 8)) != CV_OK) return st;
+  if ((st = upload(h->d_et64, et.data(), et.size() * 8)) != CV_OK) return st;
+  h->f64_ready = true;
+  return CV_OK;
+}
+
+cv_status ensure_g32_tables(cv_hmm* h) {
+  if (h->g32_ready) return CV_OK;
+  const int N = h->N;
+  const int64_t V = h->V;
+  std::vector<float> pi(N), a((size_t)N * N), et((size_t)V * N);
+  for (int j = 0; j < N; ++j) pi[j] = f32(h->pi[j]);
+  for (size_t k = 0; k < a.size(); ++k) a[k] = f32(h->a[k]);
+  for (int j = 0; j < N; ++j)
+    for (int64_t o = 0; o < V; ++o) et[(size_t)o * N + j] = f32(h->b[(size_t)j * V + o]);
+  cv_status st;
+  if ((st = upload(h->d_pi32, pi.data(), pi.size() * 4)) != CV_OK) return st;
+  if ((st = upload(h->d_a32, a.data(), a.size() * 4)) != CV_OK) return st;
+  if ((st = upload(h->d_et32, et.data(), et.size() * 4)) != CV_OK) return st;
+  h->g32_ready = true;
+  return CV_OK;
+}
+
+cv_status validate_model(int N, int64_t V, const double* pi, const double* a, const double* b) {
+  auto bad = [](double x) { return std::isnan(x) || x == INFINITY; };
+  for (int i = 0; i < N; ++i)
+    if (bad(pi[i])) return set_err(CV_EINVAL, "pi[%d] is NaN or +inf (log10 probabilities must be <= 0 or -inf)", i);
+  for (int64_t k = 0; k < (int64_t)N * N; ++k)
+    if (bad(a[k])) return set_err(CV_EINVAL, "a[%lld] is NaN or +inf", (long long)k);
+  for (int64_t k = 0; k < (int64_t)N * V; ++k)
+    if (bad(b[k])) return set_err(CV_EINVAL, "b[%lld] is NaN or +inf", (long long)k);
+  return CV_OK;
+}
+
+cv_status make_hmm(int N, const std::vector<int64_t>& bdims, const double* pi, const double* a, const double* b,
+                   int device, cv_hmm** out) {
+  if (N <= 0) return set_err(CV_EINVAL, "nstates must be > 0");
+  if (bdims.empty()) return set_err(CV_EINVAL, "ndims must be > 0");
+  int64_t V = 1;
+  for (auto d : bdims) {
+    if (d <= 0) return set_err(CV_EINVAL, "bdims entries must be > 0");
+    V *= d;
+  }
+  if (V > (int64_t)1 << 31) return set_err(CV_EINVAL, "observation alphabet too large (%lld)", (long long)V);
+  if (!pi || !a || !b) return set_err(CV_EINVAL, "null model array");
+  cv_status st = validate_model(N, V, pi, a, b);
+  if (st != CV_OK) return st;
+  auto h = std::make_unique<cv_hmm>();
+  h->N = N;
+  h->D = (int)bdims.size();
+  h->bdims = bdims;
+  h->V = V;
+  auto canon = [](double x) { return x == 0.0 ? 0.0 : x; };  // -0.0 -> +0.0
+  h->pi.resize(N);
+  h->a.resize((size_t)N * N);
+  h->b.resize((size_t)N * V);
+  std::transform(pi, pi + N, h->pi.begin(), canon);
+  std::transform(a, a + (size_t)N * N, h->a.begin(), canon);
+  std::transform(b, b + (size_t)N * V, h->b.begin(), canon);
+  h->device = device;
+  *out = h.release();
+  return CV_OK;
+}
+
+cv_status check_batch(const cv_hmm* h, int64_t nseq, const int64_t* offsets) {
+  if (nseq < 0) return set_err(CV_EINVAL, "nseq < 0");
+  if (!offsets) return set_err(CV_EINVAL, "offsets is NULL");
+  if (offsets[0] < 0) return set_err(CV_EINVAL, "offsets[0] < 0");
+  for (int64_t s = 0; s < nseq; ++s) {
+    const int64_t T = offsets[s + 1] - offsets[s];
+    if (T < 0) return set_err(CV_EINVAL, "offsets not non-decreasing at %lld", (long long)s);
+    if (T > INT32_MAX) return set_err(CV_EINVAL, "sequence %lld too long", (long long)s);
+  }
+  (void)h;
+  return CV_OK;
+}
+
+hipEvent_t get_event(cv_hmm* h, size_t i) {
+  while (h->ev.size() <= i) {
+    hipEvent_t e;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    h->ev.push_back(e);
+  }
+  return h->ev[i];
+}
+
+// Core device-side decode.  All pointers are device pointers except offsets_host.
+cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, const int64_t* offsets_dev,
+                        const int32_t* obs_dev, const cv_opts& o, int32_t* path_dev, double* score_dev,
+                        uint8_t* status_dev, hipStream_t stream) {
+  if (o.dtype != CV_DTYPE_F32 && o.dtype != CV_DTYPE_F64) return set_err(CV_EINVAL, "bad dtype %d", o.dtype);
+  if (o.assoc < CV_ASSOC_VITERBI || o.assoc > CV_ASSOC_DECODE) return set_err(CV_EINVAL, "bad assoc %d", o.assoc);
+  const bool trellis_ok = o.dtype == CV_DTYPE_F32 && o.assoc == CV_ASSOC_VITERBI &&
+                          cvk::trellis_padded_states(h->N) != 0;
+  bool use_trellis;
+  if (o.kernel == CV_KERNEL_TRELLIS) {
+    if (!trellis_ok)
+      return set_err(CV_EUNSUPPORTED, "trellis kernel needs dtype f32, assoc VITERBI and N <= 256");
+    use_trellis = true;
+  } else if (o.kernel == CV_KERNEL_GENERIC || o.kernel == CV_KERNEL_AUTO) {
+    use_trellis = o.kernel == CV_KERNEL_AUTO && trellis_ok;
+  } else {
+    return set_err(CV_EINVAL, "bad kernel %d", o.kernel);
+  }
+  if (!use_trellis && h->N > cvk::generic_max_states(o.dtype == CV_DTYPE_F64 ? 8 : 4))
+    return set_err(CV_EUNSUPPORTED, "N=%d exceeds the generic kernel's LDS capacity", h->N);
+
+  std::vector<int64_t> off_copy;
+  if (!offsets_host) {
+    off_copy.resize((size_t)nseq + 1);
+    HIP_TRY(hipMemcpyAsync(off_copy.data(), offsets_dev, off_copy.size() * 8, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipStreamSynchronize(stream));
+    offsets_host = off_copy.data();
+  }
+  cv_status st = check_batch(h, nseq, offsets_host);
+  if (st != CV_OK) return st;
+
+  const bool need_f64 = (o.rescore_f64 && o.dtype == CV_DTYPE_F32) || o.dtype == CV_DTYPE_F64;
+  if (use_trellis && (st = ensure_trellis_tables(h)) != CV_OK) return st;
+  if (need_f64 && (st = ensure_f64_tables(h)) != CV_OK) return st;
+  if (!use_trellis && o.dtype == CV_DTYPE_F32 && (st = ensure_g32_tables(h)) != CV_OK) return st;
+
+  h->last_launches = 0;
+  h->last_kernel = use_trellis ? CV_KERNEL_TRELLIS : CV_KERNEL_GENERIC;
+  h->last_np = use_trellis ? h->np : 0;
+  if (nseq == 0) return CV_OK;
+  HIP_TRY(hipMemsetAsync(status_dev, 0, (size_t)nseq, stream));
+
+  // Per-element workspace bytes: trellis keeps f32 delta rows [NP]; generic keeps u16 psi [N].
+  const uint64_t cap = o.workspace_bytes ? o.workspace_bytes : kDefaultWorkspace;
+  const uint64_t per_elem = use_trellis ? (uint64_t)h->np * 4 : (uint64_t)h->N * 2;
+  const int real_bytes = o.dtype == CV_DTYPE_F64 ? 8 : 4;
+  // chunk the sequences (original order) so that a chunk's elements fit the workspace
+  std::vector<std::pair<int64_t, int64_t>> chunks;
+  {
+    int64_t s0 = 0;
+    while (s0 < nseq) {
+      int64_t s1 = s0;
+      uint64_t elems = 0;
+      while (s1 < nseq) {
+        const uint64_t T = (uint64_t)(offsets_host[s1 + 1] - offsets_host[s1]);
+        if (s1 > s0 && (elems + T) * per_elem > cap) break;
+        elems += T;
+        ++s1;
+        if (s1 - s0 >= (1 << 30)) break;
+      }
+      chunks.emplace_back(s0, s1);
+      s0 = s1;
+    }
+  }
+  uint64_t max_elems = 0;
+  int64_t max_seqs = 0;
+  bool varlen = false;
+  for (auto& c : chunks) {
+    max_elems = std::max<uint64_t>(max_elems, (uint64_t)(offsets_host[c.second] - offsets_host[c.first]));
+    max_seqs = std::max<int64_t>(max_seqs, c.second - c.first);
+  }
+  const int64_t T0 = offsets_host[1] - offsets_host[0];
+  for (int64_t s = 1; s < nseq && !varlen; ++s) varlen = (offsets_host[s + 1] - offsets_host[s]) != T0;
+  if ((st = h->ws_main.ensure(std::max<uint64_t>(max_elems, 1) * per_elem)) != CV_OK) return st;
+  if (!use_trellis && (st = h->ws_last.ensure((size_t)max_seqs * h->N * real_bytes)) != CV_OK) return st;
+  const int32_t* order_dev = nullptr;
+  if (varlen) {
+    // longest-first schedule inside each chunk so the tail of the grid is short sequences
+    h->order_host.resize((size_t)nseq);
+    for (auto& c : chunks) {
+      std::iota(h->order_host.begin() + c.first, h->order_host.begin() + c.second, (int32_t)c.first);
+      std::stable_sort(h->order_host.begin() + c.first, h->order_host.begin() + c.second, [&](int32_t x, int32_t y) {
+        return (offsets_host[x + 1] - offsets_host[x]) > (offsets_host[y + 1] - offsets_host[y]);
+      });
+    }
+    if ((st = h->ws_order.ensure((size_t)nseq * 4)) != CV_OK) return st;
+    HIP_TRY(hipMemcpyAsync(h->ws_order.p, h->order_host.data(), (size_t)nseq * 4, hipMemcpyHostToDevice, stream));
+    HIP_TRY(hipStreamSynchronize(stream));  // order_host may be rewritten by the next call
+    order_dev = h->ws_order.as<int32_t>();
+  }
+
+  size_t evi = 0;
+  for (auto& c : chunks) {
+    const int64_t n = c.second - c.first;
+    hipEvent_t e0 = get_event(h, evi++), em = get_event(h, evi++), e1 = get_event(h, evi++);
+    if (!e0 || !em || !e1) return set_err(CV_EDEVICE, "hipEventCreate failed");
+    HIP_TRY(hipEventRecord(e0, stream));
+    hipError_t err;
+    if (use_trellis) {
+      cvk::TrellisFwdArgs fa{};
+      fa.a_img = h->t_aimg.as<float>();
+      fa.pi = h->t_pi.as<float>();
+      fa.et = h->t_et.as<float>();
+      fa.offsets = offsets_dev;
+      fa.obs = obs_dev;
+      fa.order = order_dev;
+      fa.seq_begin = c.first;
+      fa.delta = h->ws_main.as<float>();
+      fa.delta_elem_base = offsets_host[c.first];
+      fa.status = status_dev;
+      fa.nobs = (int)h->V;
+      cvk::BacktrackArgs ba{};
+      ba.delta = fa.delta;
+      ba.delta_elem_base = fa.delta_elem_base;
+      ba.at = h->t_at.as<float>();
+      ba.offsets = offsets_dev;
+      ba.obs = obs_dev;
+      ba.order = order_dev;
+      ba.seq_begin = c.first;
+      ba.seq_end = c.second;
+      ba.nstates = h->N;
+      ba.path = path_dev;
+      ba.score = score_dev;
+      ba.score32 = nullptr;
+      ba.status = status_dev;
+      ba.rescore_f64 = o.rescore_f64 ? 1 : 0;
+      ba.pi64 = h->d_pi64.as<double>();
+      ba.a64 = h->d_a64.as<double>();
+      ba.et64 = h->d_et64.as<double>();
+      err = cvk::launch_trellis(h->np, fa, ba, n, stream, em);
+    } else if (o.dtype == CV_DTYPE_F64) {
+      cvk::GenericFwdArgs<double> fa{};
+      fa.a = h->d_a64.as<double>();
+      fa.pi = h->d_pi64.as<double>();
+      fa.et = h->d_et64.as<double>();
+      fa.offsets = offsets_dev;
+      fa.obs = obs_dev;
+      fa.order = order_dev;
+      fa.seq_begin = c.first;
+      fa.nstates = h->N;
+      fa.nobs = (int)h->V;
+      fa.assoc = o.assoc;
+      fa.psi = h->ws_main.as<uint16_t>();
+      fa.psi_elem_base = offsets_host[c.first];
+      fa.last_row = h->ws_last.as<double>();
+      fa.status = status_dev;
+      cvk::GenericBtArgs<double> ba{};
+      ba.psi = fa.psi;
+      ba.psi_elem_base = fa.psi_elem_base;
+      ba.last_row = fa.last_row;
+      ba.offsets = offsets_dev;
+      ba.obs = obs_dev;
+      ba.order = order_dev;
+      ba.seq_begin = c.first;
+      ba.seq_end = c.second;
+      ba.nstates = h->N;
+      ba.path = path_dev;
+      ba.score = score_dev;
+      ba.status = status_dev;
+      ba.obs = obs_dev;
+      ba.rescore_f64 = 0;  // the f64 kernel's own score is already reference numerics
+      ba.pi64 = h->d_pi64.as<double>();
+      ba.a64 = h->d_a64.as<double>();
+      ba.et64 = h->d_et64.as<double>();
+      err = cvk::launch_generic<double>(fa, ba, n, stream, em);
+    } else {
+      cvk::GenericFwdArgs<float> fa{};
+      fa.a = h->d_a32.as<float>();
+      fa.pi = h->d_pi32.as<float>();
+      fa.et = h->d_et32.as<float>();
+      fa.offsets = offsets_dev;
+      fa.obs = obs_dev;
+      fa.order = order_dev;
+      fa.seq_begin = c.first;
+      fa.nstates = h->N;
+      fa.nobs = (int)h->V;
+      fa.assoc = o.assoc;
+      fa.psi = h->ws_main.as<uint16_t>();
+      fa.psi_elem_base = offsets_host[c.first];
+      fa.last_row = h->ws_last.as<float>();
+      fa.status = status_dev;
+      cvk::GenericBtArgs<float> ba{};
+      ba.psi = fa.psi;
+      ba.psi_elem_base = fa.psi_elem_base;
+      ba.last_row = fa.last_row;
+      ba.offsets = offsets_dev;
+      ba.obs = obs_dev;
+      ba.order = order_dev;
+      ba.seq_begin = c.first;
+      ba.seq_end = c.second;
+      ba.nstates = h->N;
+      ba.path = path_dev;
+      ba.score = score_dev;
+      ba.status = status_dev;
+      ba.obs = obs_dev;
+      ba.rescore_f64 = o.rescore_f64 ? 1 : 0;
+      ba.pi64 = h->d_pi64.as<double>();
+      ba.a64 = h->d_a64.as<double>();
+      ba.et64 = h->d_et64.as<double>();
+      err = cvk::launch_generic<float>(fa, ba, n, stream, em);
+    }
+    if (err != hipSuccess) return set_err(CV_EDEVICE, "kernel launch failed: %s", hipGetErrorString(err));
+    HIP_TRY(hipEventRecord(e1, stream));
+    ++h->last_launches;
+  }
+  return CV_OK;
+}
+
+cv_opts default_opts() {
+  cv_opts o;
+  cv_opts_init(&o);
+  return o;
+}
+
+}  // namespace
+
+// ===================================================================================
+extern "C" {
+
+CV_API const char* cv_last_error(void) { return g_err.c_str(); }
+CV_API const char* cv_version(void) { return "cviterbi 0.1.0 (gfx950)"; }
+CV_API int32_t cv_abi_version(void) { return CV_ABI_VERSION; }
+CV_API int32_t cv_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  return n;
+}
+
+CV_API void cv_opts_init(cv_opts* o) {
+  if (!o) return;
+  std::memset(o, 0, sizeof *o);
+  o->dtype = CV_DTYPE_F32;
+  o->assoc = CV_ASSOC_VITERBI;
+  o->kernel = CV_KERNEL_AUTO;
+  o->rescore_f64 = 1;
+}
+
+CV_API cv_status cv_hmm_create(const cv_hmm_desc* d, cv_hmm** out) {
+  if (!d || !out) return set_err(CV_EINVAL, "null argument");
+  if (d->ndims <= 0 || !d->bdims) return set_err(CV_EINVAL, "ndims/bdims required");
+  std::vector<int64_t> bd(d->bdims, d->bdims + d->ndims);
+  return make_hmm(d->nstates, bd, d->pi, d->a, d->b, d->device, out);
+}
+
+CV_API cv_status cv_hmm_from_json(const char* path, int32_t device, cv_hmm** out) {
+  if (!path || !out) return set_err(CV_EINVAL, "null argument");
+  std::string text, err;
+  if (!cvh::read_file(path, text)) return set_err(CV_EIO, "cannot read %s", path);
+  cvh::HmmJson j;
+  if (!cvh::parse_hmm_json(text, j, err)) return set_err(CV_EPARSE, "%s", err.c_str());
+  return make_hmm(j.nstates, j.bdims, j.pi.data(), j.a.data(), j.b.data(), device, out);
+}
+
+CV_API cv_status cv_hmm_write_json(const cv_hmm* h, const char* path) {
+  if (!h || !path) return set_err(CV_EINVAL, "null argument");
+  const std::string s = cvh::format_hmm_json(h->N, h->bdims, h->pi.data(), h->a.data(), h->b.data());
+  FILE* f = fopen(path, "wb");
+  if (!f) return set_err(CV_EIO, "cannot write %s", path);
+  const size_t n = fwrite(s.data(), 1, s.size(), f);
+  fclose(f);
+  if (n != s.size()) return set_err(CV_EIO, "short write to %s", path);
+  return CV_OK;
+}
+
+CV_API void cv_hmm_destroy(cv_hmm* h) {
+  if (!h) return;
+  int n = 0;
+  if (hipGetDeviceCount(&n) == hipSuccess && h->device >= 0 && h->device < n) (void)hipSetDevice(h->device);
+  delete h;
+}
+
+CV_API int32_t cv_hmm_nstates(const cv_hmm* h) { return h ? h->N : -1; }
+CV_API int64_t cv_hmm_nobs(const cv_hmm* h) { return h ? h->V : -1; }
+CV_API int32_t cv_hmm_ndims(const cv_hmm* h) { return h ? h->D : -1; }
+CV_API cv_status cv_hmm_bdims(const cv_hmm* h, int64_t* out) {
+  if (!h || !out) return set_err(CV_EINVAL, "null argument");
+  std::copy(h->bdims.begin(), h->bdims.end(), out);
+  return CV_OK;
+}
+
+CV_API cv_status cv_obs_flatten(const cv_hmm* h, const int64_t* value, int64_t* flat) {
+  if (!h || !value || !flat) return set_err(CV_EINVAL, "null argument");
+  int64_t f = 0;
+  for (int d = 0; d < h->D; ++d) {
+    if (value[d] < 0 || value[d] >= h->bdims[d])
+      return set_err(CV_EINVAL, "observation component %d = %lld out of range [0,%lld)", d, (long long)value[d],
+                     (long long)h->bdims[d]);
+    f = f * h->bdims[d] + value[d];  // row-major, ndarray default (C) order
+  }
+  *flat = f;
+  return CV_OK;
+}
+
+static bool lookup_ok(const cv_hmm* h, int32_t s, int64_t o) {
+  return h && s >= 0 && s < h->N && o >= 0 && o < h->V;
+}
+
+CV_API double cv_hmm_init_prob(const cv_hmm* h, int32_t state, int64_t obs) {
+  if (!lookup_ok(h, state, obs)) return NAN;
+  return h->pi[state] + h->b[(size_t)state * h->V + obs];
+}
+CV_API cv_status cv_hmm_init_probs(const cv_hmm* h, int64_t obs, double* out) {
+  if (!lookup_ok(h, 0, obs) || !out) return set_err(CV_EINVAL, "bad argument");
+  for (int s = 0; s < h->N; ++s) out[s] = h->pi[s] + h->b[(size_t)s * h->V + obs];
+  return CV_OK;
+}
+CV_API double cv_hmm_transition_prob(const cv_hmm* h, int32_t from, int32_t to, int64_t obs) {
+  if (!lookup_ok(h, to, obs) || from < 0 || from >= h->N) return NAN;
+  return h->a[(size_t)from * h->N + to] + h->b[(size_t)to * h->V + obs];
+}
+CV_API cv_status cv_hmm_transitions_to(const cv_hmm* h, int32_t to, double* out) {
+  if (!h || to < 0 || to >= h->N || !out) return set_err(CV_EINVAL, "bad argument");
+  for (int s = 0; s < h->N; ++s) out[s] = h->a[(size_t)s * h->N + to];
+  return CV_OK;
+}
+CV_API double cv_hmm_emit_prob(const cv_hmm* h, int32_t state, int64_t obs) {
+  if (!lookup_ok(h, state, obs)) return NAN;
+  return h->b[(size_t)state * h->V + obs];
+}
+CV_API cv_status cv_hmm_emit_probs(const cv_hmm* h, int64_t obs, double* out) {
+  if (!lookup_ok(h, 0, obs) || !out) return set_err(CV_EINVAL, "bad argument");
+  for (int s = 0; s < h->N; ++s) out[s] = h->b[(size_t)s * h->V + obs];
+  return CV_OK;
+}
+
+CV_API cv_status cv_decode_batch_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host,
+                                        const int64_t* offsets_dev, const int32_t* obs_dev, const cv_opts* opts,
+                                        int32_t* path_dev, double* score_dev, uint8_t* status_dev) {
+  if (!h) return set_err(CV_EINVAL, "null handle");
+  if (nseq > 0 && (!offsets_dev || !obs_dev || !path_dev || !score_dev || !status_dev))
+    return set_err(CV_EINVAL, "null device buffer");
+  std::lock_guard<std::mutex> lk(h->mu);
+  cv_status st = set_device(h);
+  if (st != CV_OK) return st;
+  const cv_opts o = opts ? *opts : default_opts();
+  hipStream_t stream = o.stream ? (hipStream_t)o.stream : h->stream;
+  return decode_device(h, nseq, offsets_host, offsets_dev, obs_dev, o, path_dev, score_dev, status_dev, stream);
+}
+
+CV_API cv_status cv_decode_batch(cv_hmm* h, int64_t nseq, const int64_t* offsets, const int32_t* obs,
+                                 const cv_opts* opts, int32_t* path_out, double* score_out, uint8_t* status_out) {
+  if (!h) return set_err(CV_EINVAL, "null handle");
+  if (nseq < 0 || (nseq > 0 && (!offsets || !obs || !path_out || !score_out || !status_out)))
+    return set_err(CV_EINVAL, "null argument");
+  std::lock_guard<std::mutex> lk(h->mu);
+  cv_status st = set_device(h);
+  if (st != CV_OK) return st;
+  if (nseq == 0) return CV_OK;
+  if ((st = check_batch(h, nseq, offsets)) != CV_OK) return st;
+  const int64_t base = offsets[0];
+  const int64_t total = offsets[nseq];  // obs/path are indexed by absolute element offset
+  for (int64_t k = base; k < total; ++k)
+    if (obs[k] < 0 || obs[k] >= h->V)
+      return set_err(CV_EINVAL, "obs[%lld] = %d out of range [0,%lld)", (long long)k, obs[k], (long long)h->V);
+  cv_opts o = opts ? *opts : default_opts();
+  hipStream_t stream = o.stream ? (hipStream_t)o.stream : h->stream;
+  if ((st = h->st_off.ensure((size_t)(nseq + 1) * 8)) != CV_OK) return st;
+  if ((st = h->st_obs.ensure((size_t)std::max<int64_t>(total, 1) * 4)) != CV_OK) return st;
+  if ((st = h->st_path.ensure((size_t)std::max<int64_t>(total, 1) * 4)) != CV_OK) return st;
+  if ((st = h->st_score.ensure((size_t)nseq * 8)) != CV_OK) return st;
+  if ((st = h->st_status.ensure((size_t)nseq)) != CV_OK) return st;
+  HIP_TRY(hipMemcpyAsync(h->st_off.p, offsets, (size_t)(nseq + 1) * 8, hipMemcpyHostToDevice, stream));
+  if (total > base)
+    HIP_TRY(hipMemcpyAsync(h->st_obs.as<int32_t>() + base, obs + base, (size_t)(total - base) * 4,
+                           hipMemcpyHostToDevice, stream));
+  st = decode_device(h, nseq, offsets, h->st_off.as<int64_t>(), h->st_obs.as<int32_t>(), o, h->st_path.as<int32_t>(),
+                     h->st_score.as<double>(), h->st_status.as<uint8_t>(), stream);
+  if (st != CV_OK) {
+    (void)hipStreamSynchronize(stream);
+    return st;
+  }
+  if (total > base)
+    HIP_TRY(hipMemcpyAsync(path_out + base, h->st_path.as<int32_t>() + base, (size_t)(total - base) * 4,
+                           hipMemcpyDeviceToHost, stream));
+  HIP_TRY(hipMemcpyAsync(score_out, h->st_score.p, (size_t)nseq * 8, hipMemcpyDeviceToHost, stream));
+  HIP_TRY(hipMemcpyAsync(status_out, h->st_status.p, (size_t)nseq, hipMemcpyDeviceToHost, stream));
+  HIP_TRY(hipStreamSynchronize(stream));
+  return CV_OK;
+}
+
+CV_API cv_status cv_last_timing(cv_hmm* h, cv_timing* out) {
+  if (!h || !out) return set_err(CV_EINVAL, "null argument");
+  std::lock_guard<std::mutex> lk(h->mu);
+  std::memset(out, 0, sizeof *out);
+  out->launches = h->last_launches;
+  out->kernel = h->last_kernel;
+  out->padded_states = h->last_np;
+  if (h->last_launches == 0) return CV_OK;
+  HIP_TRY(hipSetDevice(h->device));
+  HIP_TRY(hipEventSynchronize(h->ev[3 * h->last_launches - 1]));
+  for (int64_t c = 0; c < h->last_launches; ++c) {
+    float f = 0, b = 0;
+    HIP_TRY(hipEventElapsedTime(&f, h->ev[3 * c], h->ev[3 * c + 1]));
+    HIP_TRY(hipEventElapsedTime(&b, h->ev[3 * c + 1], h->ev[3 * c + 2]));
+    out->fwd_ms += f;
+    out->bt_ms += b;
+  }
+  float tot = 0;
+  HIP_TRY(hipEventElapsedTime(&tot, h->ev[0], h->ev[3 * h->last_launches - 1]));
+  out->total_ms = tot;
+  return CV_OK;
+}
+
+CV_API cv_status cv_viterbi_decode(cv_hmm* h, int64_t T, const int32_t* obs, int32_t* path_out) {
+  if (!h || T < 0 || (T > 0 && (!obs || !path_out))) return set_err(CV_EINVAL, "bad argument");
+  if (T == 0) return CV_OK;
+  const int64_t off[2] = {0, T};
+  double score;
+  uint8_t status;
+  cv_opts o;
+  cv_opts_init(&o);
+  o.dtype = CV_DTYPE_F64;
+  o.assoc = CV_ASSOC_DECODE;
+  o.rescore_f64 = 0;
+  return cv_decode_batch(h, 1, off, obs, &o, path_out, &score, &status);
+}
+
+// ---- trait Solver ------------------------------------------------------------------
+struct cv_solver {
+  std::string kind;
+  cv_hmm* hmm = nullptr;
+  cv_opts opts{};
+  int64_t nseq = 0;
+  std::vector<int64_t> offsets;
+  std::vector<int32_t> obs;
+  bool constrained = false;
+  std::vector<int32_t> solution;
+  std::vector<double> scores;
+  std::vector<uint8_t> status;
+  double objective = -INFINITY;
+  uint64_t explored = 0;
+};
+
+CV_API cv_status cv_solver_create(const char* kind, cv_hmm* h, const cv_superseq_desc* d, cv_solver** out) {
+  if (!kind || !h || !d || !out) return set_err(CV_EINVAL, "null argument");
+  if (d->nseq < 0 || (d->nseq > 0 && (!d->offsets || !d->obs))) return set_err(CV_EINVAL, "bad super-sequence");
+  auto s = std::make_unique<cv_solver>();
+  s->kind = kind;
+  s->hmm = h;
+  cv_opts_init(&s->opts);
+  if (s->kind == "gpu") {
+  } else if (s->kind == "gpu-f64") {
+    s->opts.dtype = CV_DTYPE_F64;
+  } else if (s->kind == "gpu-cp") {
+    s->opts.dtype = CV_DTYPE_F64;
+    s->opts.assoc = CV_ASSOC_CP;
+    s->opts.rescore_f64 = 0;
+  } else if (s->kind == "gpu-dp") {
+    s->opts.dtype = CV_DTYPE_F64;
+    s->opts.assoc = CV_ASSOC_DP;
+    s->opts.rescore_f64 = 0;
+  } else {
+    return set_err(CV_EINVAL, "unknown solver kind '%s' (gpu, gpu-f64, gpu-cp, gpu-dp)", kind);
+  }
+  s->nseq = d->nseq;
+  s->offsets.assign(d->offsets, d->offsets + d->nseq + 1);
+  if (s->offsets.empty()) s->offsets.push_back(0);
+  cv_status st = check_batch(h, s->nseq, s->offsets.data());
+  if (st != CV_OK) return st;
+  if (s->offsets[0] != 0) return set_err(CV_EINVAL, "super-sequence offsets must start at 0");
+  const int64_t total = s->offsets.back();
+  s->obs.assign(d->obs, d->obs + total);
+  if (d->active && d->component)
+    for (int64_t k = 0; k < total; ++k)
+      if (d->active[k] && d->component[k] >= 0) s->constrained = true;
+  *out = s.release();
+  return CV_OK;
+}
+
+CV_API cv_status cv_solver_solve(cv_solver* s) {
+  if (!s) return set_err(CV_EINVAL, "null solver");
+  if (s->constrained)
+    return set_err(CV_EUNSUPPORTED, "active consistency constraints are not supported by this ABI version");
+  const int64_t total = s->offsets.back();
+  s->solution.assign((size_t)total, 0);
+  s->scores.assign((size_t)s->nseq, 0.0);
+  s->status.assign((size_t)s->nseq, 0);
+  cv_status st = cv_decode_batch(s->hmm, s->nseq, s->offsets.data(), s->obs.data(), &s->opts, s->solution.data(),
+                                 s->scores.data(), s->status.data());
+  if (st != CV_OK) return st;
+  // objective of an unconstrained super-sequence = sum of per-sequence optima (row A6)
+  double obj = 0.0;
+  for (int64_t k = 0; k < s->nseq; ++k) {
+    if (s->status[k] == CV_SEQ_INFEASIBLE) {
+      s->objective = -INFINITY;
+      return set_err(CV_EINFEASIBLE, "sequence %lld has no finite-probability path", (long long)k);
+    }
+    obj += s->scores[k];
+  }
+  s->objective = obj;
+  s->explored = 0;  // CPSolver explores no B&B node without constraints (cp.rs:169-174)
+  return CV_OK;
+}
+
+CV_API cv_status cv_solver_get_solution(const cv_solver* s, const int32_t** sol, int64_t* len) {
+  if (!s || !sol || !len) return set_err(CV_EINVAL, "null argument");
+  *sol = s->solution.data();
+  *len = (int64_t)s->solution.size();
+  return CV_OK;
+}
+CV_API cv_status cv_solver_get_objective(const cv_solver* s, double* obj) {
+  if (!s || !obj) return set_err(CV_EINVAL, "null argument");
+  *obj = s->objective;
+  return CV_OK;
+}
+CV_API const char* cv_solver_get_name(const cv_solver* s) { return s ? s->kind.c_str() : ""; }
+CV_API cv_status cv_solver_get_explored_nodes(const cv_solver* s, uint64_t* n) {
+  if (!s || !n) return set_err(CV_EINVAL, "null argument");
+  *n = s->explored;
+  return CV_OK;
+}
+CV_API void cv_solver_destroy(cv_solver* s) { delete s; }
+
+}  // extern "C"

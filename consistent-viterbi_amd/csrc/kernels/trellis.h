@@ -1,0 +1,88 @@
+// trellis.h -- argument blocks and launchers of the HIP trellis kernels (trellis.hip).
+// Internal to libcviterbi; the public boundary is include/cviterbi.h.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace cvk {
+
+enum { CVK_SEQ_OK = 0, CVK_SEQ_INFEASIBLE = 1, CVK_SEQ_EMPTY = 2, CVK_SEQ_BADOBS = 3 };
+enum { CVK_ASSOC_VITERBI = 0, CVK_ASSOC_CP = 1, CVK_ASSOC_DP = 2, CVK_ASSOC_DECODE = 3 };
+
+struct TrellisFwdArgs {
+  const float* a_img;      // register image of A, NP*NP floats (see trellis_fwd_f32)
+  const float* pi;         // [NP], -inf padded
+  const float* et;         // [V][NP] emission transposed, -inf padded
+  const int64_t* offsets;  // [nseq_total+1] element offsets
+  const int32_t* obs;      // [sum T] flattened observation indices
+  const int32_t* order;    // optional schedule: slot -> sequence id
+  int64_t seq_begin;       // first schedule slot of this launch
+  float* delta;            // [(elements of chunk)][NP] delta rows for the backtrack
+  int64_t delta_elem_base; // element offset that maps to delta row 0
+  uint8_t* status;         // [nseq_total] per-sequence status (pre-zeroed)
+  int nobs;                // V
+};
+
+struct BacktrackArgs {
+  const float* delta;
+  int64_t delta_elem_base;
+  const float* at;         // [NP][NP]: at[j*NP + i] = A[i][j]
+  const int64_t* offsets;
+  const int32_t* obs;
+  const int32_t* order;
+  int64_t seq_begin, seq_end;
+  int nstates;             // real N
+  int32_t* path;           // [sum T]
+  double* score;           // [nseq_total]
+  float* score32;          // optional [nseq_total]
+  uint8_t* status;
+  int rescore_f64;
+  const double* pi64;      // [N]
+  const double* a64;       // [N*N]
+  const double* et64;      // [V][N]
+};
+
+template <typename REAL>
+struct GenericFwdArgs {
+  const REAL* a;           // [N*N]
+  const REAL* pi;          // [N]
+  const REAL* et;          // [V][N]
+  const int64_t* offsets;
+  const int32_t* obs;
+  const int32_t* order;
+  int64_t seq_begin;
+  int nstates, nobs, assoc;
+  uint16_t* psi;           // [(elements of chunk)][N]
+  int64_t psi_elem_base;
+  REAL* last_row;          // [(seqs of chunk)][N]
+  uint8_t* status;
+};
+
+template <typename REAL>
+struct GenericBtArgs {
+  const uint16_t* psi;
+  int64_t psi_elem_base;
+  const REAL* last_row;
+  const int64_t* offsets;
+  const int32_t* order;
+  int64_t seq_begin, seq_end;
+  int nstates;
+  int32_t* path;
+  double* score;
+  uint8_t* status;
+  const int32_t* obs;      // for the f64 re-score
+  int rescore_f64;         // f32 kernels only: score = f64 VITERBI re-score of the path
+  const double* pi64;
+  const double* a64;
+  const double* et64;
+};
+
+int trellis_padded_states(int n);  // 0 if the trellis kernel does not cover n
+hipError_t launch_trellis(int np, const TrellisFwdArgs& fa, const BacktrackArgs& ba, int64_t nseq,
+                          hipStream_t stream, hipEvent_t ev_mid);
+template <typename REAL>
+hipError_t launch_generic(const GenericFwdArgs<REAL>& fa, const GenericBtArgs<REAL>& ba, int64_t nseq,
+                          hipStream_t stream, hipEvent_t ev_mid);
+int generic_max_states(int real_bytes);
+
+}  // namespace cvk

@@ -1,0 +1,10 @@
+"""cviterbi -- MI355X-native Viterbi decode path behind the consistent-viterbi solver API.
+
+Host mirror of the reference's hmm::HMM and viterbi_solver interfaces over the C ABI
+in include/cviterbi.h (libcviterbi.so: hand-written gfx950 HIP kernels).
+"""
+from ._lib import CVError, EXPORTS, LIB_PATH  # noqa: F401
+from .hmm import HMM  # noqa: F401
+from .decode import decode, decode_batch, decode_batch_device, last_timing  # noqa: F401
+from .solver import (Constraints, GpuSolver, Solver, SuperSequence, load_sequences, load_tags,  # noqa: F401
+                     write_output)

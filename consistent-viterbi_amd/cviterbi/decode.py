@@ -1,0 +1,77 @@
+"""Batch Viterbi decode on MI355X (cv_decode_batch / cv_decode_batch_device).
+
+Replaces, per sequence, the dense forward + backtrack of the reference's solvers:
+CPSolver::init_viterbi + backtrack (viterbi_solver/cp.rs:95-125), viterbi::decode
+(viterbi.rs:5-32) and DPSolver::solve (dp.rs:94-209); see include/cviterbi.h.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _lib as L
+from .hmm import HMM
+
+_DT = {"f32": L.DTYPE_F32, "f64": L.DTYPE_F64, np.float32: L.DTYPE_F32, np.float64: L.DTYPE_F64}
+_ASSOC = {"viterbi": L.ASSOC_VITERBI, "cp": L.ASSOC_CP, "dp": L.ASSOC_DP, "decode": L.ASSOC_DECODE}
+_KERNEL = {"auto": L.KERNEL_AUTO, "trellis": L.KERNEL_TRELLIS, "generic": L.KERNEL_GENERIC}
+
+
+def _p(x):
+    return x.ctypes.data_as(ctypes.c_void_p)
+
+
+def make_opts(dtype="f32", assoc="viterbi", kernel="auto", rescore_f64=True, stream=None, workspace_bytes=0):
+    return L.opts(_DT.get(dtype, dtype), _ASSOC.get(assoc, assoc), _KERNEL.get(kernel, kernel), rescore_f64, stream,
+                  workspace_bytes)
+
+
+def decode_batch(hmm: HMM, offsets, obs, dtype="f32", assoc="viterbi", kernel="auto", rescore_f64=True,
+                 workspace_bytes=0):
+    """Decode CSR sequences (offsets[B+1], flat obs) -> (path int32[sum T], score f64[B], status u8[B])."""
+    offsets = np.ascontiguousarray(offsets, np.int64)
+    obs = np.ascontiguousarray(obs, np.int32)
+    nseq = offsets.shape[0] - 1
+    total = int(offsets[-1]) if nseq >= 0 else 0
+    path = np.zeros(max(total, 0), np.int32)
+    score = np.zeros(max(nseq, 0), np.float64)
+    status = np.zeros(max(nseq, 0), np.uint8)
+    o = make_opts(dtype, assoc, kernel, rescore_f64, None, workspace_bytes)
+    L.check(L.lib().cv_decode_batch(hmm.handle, nseq, _p(offsets), _p(obs), ctypes.byref(o), _p(path), _p(score),
+                                    _p(status)))
+    return path, score, status
+
+
+def decode_batch_device(hmm: HMM, offsets_dev, obs_dev, path_dev, score_dev, status_dev, offsets_host=None,
+                        dtype="f32", assoc="viterbi", kernel="auto", rescore_f64=True, stream=None,
+                        workspace_bytes=0):
+    """Device-pointer decode (ints or objects with data_ptr(), e.g. torch tensors); async on `stream`."""
+    def ptr(x):
+        if x is None:
+            return None
+        return x.data_ptr() if hasattr(x, "data_ptr") else int(x)
+
+    nseq = (len(offsets_host) if offsets_host is not None else offsets_dev.numel()) - 1
+    oh = None
+    if offsets_host is not None:
+        oh = np.ascontiguousarray(offsets_host, np.int64)
+    o = make_opts(dtype, assoc, kernel, rescore_f64, stream, workspace_bytes)
+    L.check(L.lib().cv_decode_batch_device(hmm.handle, nseq, _p(oh) if oh is not None else None, ptr(offsets_dev),
+                                           ptr(obs_dev), ctypes.byref(o), ptr(path_dev), ptr(score_dev),
+                                           ptr(status_dev)))
+
+
+def last_timing(hmm: HMM) -> dict:
+    t = L.Timing()
+    L.check(L.lib().cv_last_timing(hmm.handle, ctypes.byref(t)))
+    return dict(fwd_ms=t.fwd_ms, bt_ms=t.bt_ms, total_ms=t.total_ms, launches=t.launches,
+                kernel={1: "trellis", 2: "generic"}.get(t.kernel, "none"), padded_states=t.padded_states)
+
+
+def decode(sequence, hmm: HMM):
+    """viterbi::decode (viterbi.rs:5): sequence of [usize; D] (or flat ints) -> path (row 0 = 0.0 semantics)."""
+    obs = np.ascontiguousarray([hmm.flat(o) for o in sequence], np.int32)
+    path = np.zeros(obs.shape[0], np.int32)
+    L.check(L.lib().cv_viterbi_decode(hmm.handle, obs.shape[0], _p(obs), _p(path)))
+    return path

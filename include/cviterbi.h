@@ -1,0 +1,184 @@
+/*
+ * cviterbi.h -- C ABI of the MI355X-native consistent-viterbi decode path.
+ *
+ * This is the drop-in boundary for the reference's viterbi_solver forward pass over
+ * hmm::HMM (AlexandreDubray/consistent-viterbi).  The reference is a Rust crate with
+ * no FFI of its own; every entry point below names the Rust item it replaces, so a
+ * Rust `extern "C"` binding can stand in for it.  Plain pointers and
+ * sizes only; no torch or HIP types in the signatures (streams are opaque void*).
+ *
+ * Conventions
+ *  - Probabilities are log10 doubles, -inf for zero (src/hmm/hmm.rs:392-405); JSON
+ *    `null` reads as -inf (hmm.rs:448-464).
+ *  - a[from*N + to] (hmm.rs:420-426), b[state*V + obs] with obs flattened row-major
+ *    over bdims exactly as ndarray indexes `b[state][&obs[..]]` (hmm.rs:428-430).
+ *  - Sequences are CSR: offsets[nseq+1] (int64, element offsets), obs[offsets[nseq]]
+ *    (int32 flattened observation indices).  Paths are int32 per element.
+ *  - Functions return cv_status; cv_last_error() has a message for the calling thread.
+ *    Nothing aborts (the reference panics: cp.rs:119, dp.rs:184-186, unwraps).
+ */
+#ifndef CVITERBI_H
+#define CVITERBI_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CV_API __attribute__((visibility("default")))
+#define CV_ABI_VERSION 1
+
+typedef enum cv_status {
+  CV_OK = 0,
+  CV_EINVAL = 1,        /* bad argument (shape, range, NaN/+inf log-prob, obs out of range) */
+  CV_EDEVICE = 2,       /* HIP runtime error or no usable gfx950 device */
+  CV_ENOMEM = 3,        /* host or device allocation failed */
+  CV_EINFEASIBLE = 4,   /* at least one sequence has no finite-probability path */
+  CV_EIO = 5,           /* file could not be read / written */
+  CV_EPARSE = 6,        /* malformed hmm.json */
+  CV_EUNSUPPORTED = 7,  /* valid request this build does not implement */
+  CV_EINTERNAL = 8
+} cv_status;
+
+/* per-sequence status_out values */
+enum { CV_SEQ_OK = 0, CV_SEQ_INFEASIBLE = 1, CV_SEQ_EMPTY = 2, CV_SEQ_BADOBS = 3 };
+
+/* arithmetic type of the trellis recurrence */
+enum { CV_DTYPE_F32 = 0, CV_DTYPE_F64 = 1 };
+
+/* association of the recurrence:
+ *  VITERBI  d' = max_i(d[i] + a[i,j]) + b[j,o]      viterbi.rs:13-18 order, pi init cp.rs:98-100
+ *  CP       d' = d[psi] + (a[psi,j] + b[j,o])       CPSolver::init_viterbi cp.rs:95-115
+ *  DP       d' = max_i((a[i,j] + b[j,o]) + d[i])    DPSolver::solve dp.rs:127-182 (first index)
+ *  DECODE   VITERBI with row 0 = 0.0                viterbi::decode viterbi.rs:5-32 */
+enum { CV_ASSOC_VITERBI = 0, CV_ASSOC_CP = 1, CV_ASSOC_DP = 2, CV_ASSOC_DECODE = 3 };
+
+/* kernel choice: AUTO picks TRELLIS (register-resident A, f32, VITERBI, N <= 256) when
+ * it applies, else GENERIC (inline argmax, f32/f64, any association, N <= 4096). */
+enum { CV_KERNEL_AUTO = 0, CV_KERNEL_TRELLIS = 1, CV_KERNEL_GENERIC = 2 };
+
+typedef struct cv_hmm cv_hmm;
+typedef struct cv_solver cv_solver;
+
+/* Model description; arrays are copied.  Replaces the fields of struct HMM<D>
+ * (hmm.rs:10-18: a: Array2<f64>, b: Array1<ArrayD<f64>>, pi: Array1<f64>). */
+typedef struct cv_hmm_desc {
+  int32_t nstates;       /* N */
+  int32_t ndims;         /* D (const generic of HMM<D>) */
+  const int64_t* bdims;  /* [D] shape of each state's emission array (hmm.rs:225) */
+  const double* pi;      /* [N]   log10 */
+  const double* a;       /* [N*N] log10, from-major */
+  const double* b;       /* [N*V] log10, V = prod(bdims) */
+  int32_t device;        /* HIP device ordinal */
+} cv_hmm_desc;
+
+typedef struct cv_opts {
+  int32_t dtype;         /* CV_DTYPE_F32 (default) */
+  int32_t assoc;         /* CV_ASSOC_VITERBI (default) */
+  int32_t kernel;        /* CV_KERNEL_AUTO (default) */
+  int32_t rescore_f64;   /* 1 (default): score_out = f64 re-score of the decoded path with
+                            the VITERBI association (what the f64 reference computes along
+                            that path); 0: the kernel's own score (f32 widened for F32) */
+  void* stream;          /* hipStream_t for the *_device entry points; NULL = handle stream */
+  uint64_t workspace_bytes; /* delta/psi workspace cap; 0 = default (8 GiB) */
+  uint32_t flags;        /* reserved, 0 */
+} cv_opts;
+
+typedef struct cv_timing {
+  double fwd_ms;         /* forward kernel(s), device time, last decode call */
+  double bt_ms;          /* backtrack (+ f64 re-score) kernel(s) */
+  double total_ms;       /* first kernel start to last kernel end (device) */
+  int64_t launches;      /* forward launches (chunks) */
+  int32_t kernel;        /* CV_KERNEL_TRELLIS or CV_KERNEL_GENERIC actually used */
+  int32_t padded_states; /* NP of the trellis kernel (0 for generic) */
+} cv_timing;
+
+typedef struct cv_superseq_desc {
+  /* The super-sequence of viterbi_solver/utils.rs:265-274 in element order: sequences
+   * concatenated (after reordering), each element carrying MetaElements fields. */
+  int64_t nseq;
+  const int64_t* offsets;    /* [nseq+1] */
+  const int32_t* obs;        /* [offsets[nseq]] flattened observation index (value) */
+  const int64_t* seq_id;     /* [nseq] original sequence id (MetaElements::seq) or NULL = 0..nseq-1 */
+  const int32_t* component;  /* [elements] constraint_component, -1 = none; NULL = none */
+  const uint8_t* active;     /* [elements] active_cstr; NULL = all inactive */
+} cv_superseq_desc;
+
+/* ---- library ---------------------------------------------------------------------- */
+CV_API const char* cv_last_error(void);
+CV_API const char* cv_version(void);
+CV_API int32_t cv_abi_version(void);
+CV_API int32_t cv_device_count(void);
+CV_API void cv_opts_init(cv_opts* opts);
+
+/* ---- hmm::HMM (src/hmm/hmm.rs) ------------------------------------------------------- */
+/* HMM struct construction (hmm.rs:10-18). */
+CV_API cv_status cv_hmm_create(const cv_hmm_desc* desc, cv_hmm** out);
+/* HMM::from_json (hmm.rs:442-445 + null->-inf parsers 448-464). */
+CV_API cv_status cv_hmm_from_json(const char* path, int32_t device, cv_hmm** out);
+/* HMM::write (hmm.rs:436-440): serde_json layout, -inf written as null. */
+CV_API cv_status cv_hmm_write_json(const cv_hmm* h, const char* path);
+CV_API void cv_hmm_destroy(cv_hmm* h);
+/* HMM::nstates (hmm.rs:407-409). */
+CV_API int32_t cv_hmm_nstates(const cv_hmm* h);
+CV_API int64_t cv_hmm_nobs(const cv_hmm* h);                   /* V = prod(bdims) */
+CV_API int32_t cv_hmm_ndims(const cv_hmm* h);
+CV_API cv_status cv_hmm_bdims(const cv_hmm* h, int64_t* bdims_out /*[D]*/);
+/* flatten one D-dim observation value ([usize; D]) to the index used everywhere else. */
+CV_API cv_status cv_obs_flatten(const cv_hmm* h, const int64_t* value /*[D]*/, int64_t* flat_out);
+/* HMM::init_prob (hmm.rs:411-413) */
+CV_API double cv_hmm_init_prob(const cv_hmm* h, int32_t state, int64_t obs);
+/* HMM::init_probs (hmm.rs:415-418) -> out[N] */
+CV_API cv_status cv_hmm_init_probs(const cv_hmm* h, int64_t obs, double* out);
+/* HMM::transition_prob (hmm.rs:420-422) */
+CV_API double cv_hmm_transition_prob(const cv_hmm* h, int32_t from, int32_t to, int64_t obs);
+/* HMM::transitions_to (hmm.rs:424-426) -> out[N] = a[:, to] */
+CV_API cv_status cv_hmm_transitions_to(const cv_hmm* h, int32_t to, double* out);
+/* HMM::emit_prob (hmm.rs:428-430) */
+CV_API double cv_hmm_emit_prob(const cv_hmm* h, int32_t state, int64_t obs);
+/* HMM::emit_probs (hmm.rs:432-434) -> out[N] */
+CV_API cv_status cv_hmm_emit_probs(const cv_hmm* h, int64_t obs, double* out);
+
+/* ---- batch decode: the trellis forward pass + backtrack -------------------------------
+ * Replaces, per sequence, the dense forward of CPSolver::init_viterbi (cp.rs:95-115) /
+ * viterbi::decode (viterbi.rs:9-23) / DPSolver::solve (dp.rs:127-182) plus the backtrack
+ * (cp.rs:117-125, viterbi.rs:24-31, dp.rs:71-89).  Host pointers; synchronous. */
+CV_API cv_status cv_decode_batch(cv_hmm* h, int64_t nseq, const int64_t* offsets, const int32_t* obs,
+                                 const cv_opts* opts, int32_t* path_out, double* score_out,
+                                 uint8_t* status_out);
+/* Same on device-resident buffers, enqueued on opts->stream (or the handle's stream);
+ * returns after enqueueing.  offsets_host (nullable) is a host copy of offsets used for
+ * chunking; without it the offsets are copied back once.  Observation indices are
+ * range-checked on the device: a bad one sets status CV_SEQ_BADOBS. */
+CV_API cv_status cv_decode_batch_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host,
+                                        const int64_t* offsets_dev, const int32_t* obs_dev,
+                                        const cv_opts* opts, int32_t* path_dev, double* score_dev,
+                                        uint8_t* status_dev);
+/* Device timings of the last decode call on this handle (synchronizes its events). */
+CV_API cv_status cv_last_timing(cv_hmm* h, cv_timing* out);
+/* viterbi::decode (viterbi.rs:5): one sequence, reference decode() semantics (row 0 = 0.0,
+ * f64), path only. */
+CV_API cv_status cv_viterbi_decode(cv_hmm* h, int64_t T, const int32_t* obs, int32_t* path_out);
+
+/* ---- trait Solver (viterbi_solver.rs:11-16) -------------------------------------------
+ * kind: "gpu"      f32 trellis kernel, VITERBI association, f64 re-scored objective
+ *       "gpu-f64"  f64, VITERBI association (reference numerics, row A0)
+ *       "gpu-cp"   f64, CP association = CPSolver (cp.rs), what main.rs:120 runs
+ *       "gpu-dp"   f64, DP association = DPSolver (dp.rs), ascending-index ties
+ * Unconstrained super-sequences decode per sequence: objective =
+ * sum of per-sequence scores (sequence order), solution in element order.  Active
+ * constraints return CV_EUNSUPPORTED in this ABI version. */
+CV_API cv_status cv_solver_create(const char* kind, cv_hmm* h, const cv_superseq_desc* seq, cv_solver** out);
+CV_API cv_status cv_solver_solve(cv_solver* s);                                   /* Solver::solve */
+CV_API cv_status cv_solver_get_solution(const cv_solver* s, const int32_t** sol, int64_t* len); /* get_solution */
+CV_API cv_status cv_solver_get_objective(const cv_solver* s, double* obj);        /* get_objective */
+CV_API const char* cv_solver_get_name(const cv_solver* s);                        /* get_name */
+CV_API cv_status cv_solver_get_explored_nodes(const cv_solver* s, uint64_t* n);   /* CPSolver::get_explored_nodes cp.rs:128 */
+CV_API void cv_solver_destroy(cv_solver* s);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CVITERBI_H */

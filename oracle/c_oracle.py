@@ -1,0 +1,87 @@
+"""ctypes loader for the C oracle (oracle/build/libcv_oracle.so).
+
+TEST INFRASTRUCTURE ONLY -- imported by tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg, never by the product package.  See cv_oracle.h for
+the semantics and the parity status ("parity unpinned": pinned by KATs and
+exhaustive enumeration, not by reference fixtures, which do not exist).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+VITERBI, CP, DP, DECODE = 0, 1, 2, 3
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = os.path.join(_HERE, "build", "libcv_oracle.so")
+_lib = None
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", _HERE])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB):
+            build()
+        L = ctypes.CDLL(_LIB)
+        P = ctypes.c_void_p
+        for name in ("cvo_decode_batch_f64", "cvo_decode_batch_f32"):
+            f = getattr(L, name)
+            f.argtypes = [ctypes.c_int, ctypes.c_int, P, P, P, ctypes.c_int64, P, P, ctypes.c_int, P, P, P,
+                          ctypes.c_int]
+            f.restype = ctypes.c_int
+        L.cvo_rescore_f64.argtypes = [ctypes.c_int, ctypes.c_int, P, P, P, ctypes.c_int, P, P]
+        L.cvo_rescore_f64.restype = ctypes.c_double
+        L.cvo_cp_superseq_f64.argtypes = [ctypes.c_int, ctypes.c_int, P, P, P, ctypes.c_int64, P, P, P]
+        L.cvo_cp_superseq_f64.restype = ctypes.c_double
+        _lib = L
+    return _lib
+
+
+def _p(x):
+    return x.ctypes.data_as(ctypes.c_void_p)
+
+
+def decode_batch(pi, a, b, offsets, obs, assoc=VITERBI, dtype=np.float64, nthreads=1):
+    """Returns (path int32[sum T], score f64[B], status u8[B])."""
+    dt = np.dtype(dtype)
+    pi = np.ascontiguousarray(pi, dt)
+    a = np.ascontiguousarray(a, dt)
+    b = np.ascontiguousarray(b, dt)
+    offsets = np.ascontiguousarray(offsets, np.int64)
+    obs = np.ascontiguousarray(obs, np.int32)
+    n, v = a.shape[0], b.shape[1]
+    nseq = offsets.shape[0] - 1
+    path = np.zeros(int(offsets[-1]), np.int32)
+    score = np.zeros(nseq, np.float64)
+    status = np.zeros(nseq, np.uint8)
+    fn = lib().cvo_decode_batch_f64 if dt == np.float64 else lib().cvo_decode_batch_f32
+    fn(n, v, _p(pi), _p(a), _p(b), nseq, _p(offsets), _p(obs), assoc, _p(path), _p(score), _p(status),
+       int(nthreads))
+    return path, score, status
+
+
+def rescore_f64(pi, a, b, obs, path):
+    pi = np.ascontiguousarray(pi, np.float64)
+    a = np.ascontiguousarray(a, np.float64)
+    b = np.ascontiguousarray(b, np.float64)
+    obs = np.ascontiguousarray(obs, np.int32)
+    path = np.ascontiguousarray(path, np.int32)
+    return lib().cvo_rescore_f64(a.shape[0], b.shape[1], _p(pi), _p(a), _p(b), obs.shape[0], _p(obs), _p(path))
+
+
+def cp_superseq_f64(pi, a, b, offsets, obs):
+    pi = np.ascontiguousarray(pi, np.float64)
+    a = np.ascontiguousarray(a, np.float64)
+    b = np.ascontiguousarray(b, np.float64)
+    offsets = np.ascontiguousarray(offsets, np.int64)
+    obs = np.ascontiguousarray(obs, np.int32)
+    path = np.zeros(int(offsets[-1] - offsets[0]), np.int32)
+    obj = lib().cvo_cp_superseq_f64(a.shape[0], b.shape[1], _p(pi), _p(a), _p(b), offsets.shape[0] - 1,
+                                    _p(offsets), _p(obs), _p(path))
+    return path, obj

@@ -1,0 +1,79 @@
+/*
+ * cv_oracle.h -- CPU restatement of the reference Viterbi decode path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Nothing under oracle/ is linked into, loaded by or
+ * called from the product library (consistent-viterbi_amd/csrc).  Only tests/,
+ * __graft_entry__.smoke() and bench.py's cpu_baseline leg may use it, and only
+ * as the checker / the timed CPU baseline.
+ *
+ * PARITY STATUS: "parity unpinned" w.r.t. the reference binary.  The reference
+ * is a Rust crate that cannot be built here (no rustc/cargo, no crate registry,
+ * Gurobi licence) and ships no tests, fixtures or golden vectors
+ * (SURVEY.md §4).  This restatement is pinned instead by hand-derived known
+ * answers and by exhaustive path enumeration (tests/test_oracle_*.py), and it is
+ * cross-checked against an independent numpy restatement (oracle/np_oracle.py).
+ *
+ * Model (reference src/hmm/hmm.rs:10-18): log10 probabilities, -inf for zero.
+ *   pi[N]        initial log-probs                         (hmm.rs:211-218)
+ *   a[N*N]       a[from*N + to]                            (hmm.rs:220-226)
+ *   b[N*V]       b[state*V + obs], obs flattened row-major (hmm.rs:228-234)
+ *
+ * Association / semantics modes:
+ *   CVO_ASSOC_VITERBI  row A0: d0 = pi + b[:,o0]; s_i = d[i] + a[i,j];
+ *                      psi = first argmax s; d'[j] = max(s) + b[j,o]
+ *                      (viterbi.rs:13-18 order, cp.rs:98-100 init)
+ *   CVO_ASSOC_CP       CPSolver::init_viterbi (cp.rs:95-115):
+ *                      psi = first argmax(d + a[:,j]); d'[j] = d[psi] + (a[psi,j] + b[j,o])
+ *                      (arc_p utils.rs:240-246 -> transition_prob hmm.rs:420-422)
+ *   CVO_ASSOC_DP       DPSolver unconstrained branch (dp.rs:127-182): candidates
+ *                      c_i = (a[i,j] + b[j,o]) + d[i] over finite d[i], finite arc;
+ *                      keep strictly greater -> first index in ascending i (the
+ *                      reference iterates a HashMap; ascending order is our
+ *                      deterministic choice).
+ *   CVO_ASSOC_DECODE   viterbi::decode (viterbi.rs:5-32): row 0 = 0.0 (no pi, no
+ *                      first emission), otherwise as VITERBI.
+ * Final state = first argmax of the last row (cp.rs:117-125, viterbi.rs:24);
+ * score = max of the last row.
+ */
+#ifndef CV_ORACLE_H
+#define CV_ORACLE_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum { CVO_ASSOC_VITERBI = 0, CVO_ASSOC_CP = 1, CVO_ASSOC_DP = 2, CVO_ASSOC_DECODE = 3 };
+enum { CVO_SEQ_OK = 0, CVO_SEQ_INFEASIBLE = 1, CVO_SEQ_EMPTY = 2 };
+
+/* One sequence.  Returns CVO_SEQ_*; path[T] and *score always written. */
+int cvo_decode_f64(int N, int V, const double* pi, const double* a, const double* b, int T,
+                   const int32_t* obs, int assoc, int32_t* path, double* score);
+int cvo_decode_f32(int N, int V, const float* pi, const float* a, const float* b, int T,
+                   const int32_t* obs, int assoc, int32_t* path, float* score);
+
+/* Batch over CSR sequences offsets[nseq+1]; nthreads<=1 -> single thread.
+ * score_out is double for both precisions (f32 scores widened exactly). */
+int cvo_decode_batch_f64(int N, int V, const double* pi, const double* a, const double* b,
+                         int64_t nseq, const int64_t* offsets, const int32_t* obs, int assoc,
+                         int32_t* path, double* score, uint8_t* status, int nthreads);
+int cvo_decode_batch_f32(int N, int V, const float* pi, const float* a, const float* b,
+                         int64_t nseq, const int64_t* offsets, const int32_t* obs, int assoc,
+                         int32_t* path, double* score, uint8_t* status, int nthreads);
+
+/* f64 score of a fixed path with the row-A0 association:
+ * d = pi[p0] + b[p0,o0]; d = (d + a[p_{t-1},p_t]) + b[p_t,o_t]. */
+double cvo_rescore_f64(int N, int V, const double* pi, const double* a, const double* b, int T,
+                       const int32_t* obs, const int32_t* path);
+
+/* CPSolver over a whole super-sequence (cp.rs:95-115 + utils.rs:240-254):
+ * sequences concatenated, t==0 elements use the constant pi[to] transition
+ * vector.  Unconstrained only.  Returns objective; path[total] in element order. */
+double cvo_cp_superseq_f64(int N, int V, const double* pi, const double* a, const double* b,
+                           int64_t nseq, const int64_t* offsets, const int32_t* obs,
+                           int32_t* path);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

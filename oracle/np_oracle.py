@@ -1,0 +1,142 @@
+"""numpy restatement of the reference Viterbi decode path + exhaustive enumerator.
+
+TEST INFRASTRUCTURE ONLY: used in this container to cross-check the C oracle
+(oracle/cv_oracle.c) and to generate the committed golden fixtures under
+tests/golden/.  Never imported by the product package.
+
+Parity status: "parity unpinned" against the reference binary (a Rust crate that
+cannot be built or run here, with no tests or fixtures of its own; SURVEY.md §4,
+§8c).  Pinned instead by exhaustive enumeration (`brute_force`) and hand-derived
+known answers (tests/test_oracle_kat.py).
+
+Semantics follow SURVEY.md §8a (file:line into /root/reference/src):
+  VITERBI (row A0)  d0 = pi + b[:,o0] (hmm/hmm.rs:415-418, viterbi_solver/cp.rs:98-100);
+                    s = d[:,None] + a; psi = first argmax; d' = max(s) + b[:,o]
+                    (viterbi_solver/viterbi.rs:13-18).
+  CP                psi as above; d'[j] = d[psi] + (a[psi,j] + b[j,o])
+                    (cp.rs:102-110 via utils.rs:240-246 -> hmm.rs:420-422).
+  DP                c = (a + b[None,:,o]) + d[:,None] over finite entries; first max
+                    (dp.rs:127-177, ascending-index iteration instead of HashMap order).
+  DECODE            viterbi.rs:5-32: row 0 = 0.0, -inf emission -> -inf, bt 0.
+"""
+from __future__ import annotations
+
+import itertools
+
+import numpy as np
+
+VITERBI, CP, DP, DECODE = 0, 1, 2, 3
+SEQ_OK, SEQ_INFEASIBLE, SEQ_EMPTY = 0, 1, 2
+
+
+def decode(pi, a, b, obs, assoc=VITERBI, dtype=np.float64):
+    """Decode one sequence. pi[N], a[N,N] (from,to), b[N,V]; returns (path, score, status)."""
+    pi = np.asarray(pi, dtype=dtype)
+    a = np.asarray(a, dtype=dtype)
+    b = np.asarray(b, dtype=dtype)
+    obs = np.asarray(obs, dtype=np.int64)
+    n = a.shape[0]
+    T = obs.shape[0]
+    if T == 0:
+        return np.zeros(0, np.int32), dtype(0), SEQ_EMPTY
+    ninf = dtype(-np.inf)
+    e0 = b[:, obs[0]]
+    if assoc == DECODE:
+        prev = np.zeros(n, dtype)
+    elif assoc == DP:
+        prev = np.where(e0 > ninf, pi + e0, ninf).astype(dtype)
+    else:
+        prev = (pi + e0).astype(dtype)
+    bt = np.zeros((T, n), np.int32)
+    cols = np.arange(n)
+    for t in range(1, T):
+        e = b[:, obs[t]]
+        if assoc == DP:
+            arc = a + e[None, :]
+            c = arc + prev[:, None]
+            c = np.where(np.isfinite(prev)[:, None] & (arc > ninf), c, ninf)
+            arg = np.argmax(c, axis=0)
+            cur = c[arg, cols]
+            cur = np.where(e > ninf, cur, ninf)
+            arg = np.where(e > ninf, arg, 0)
+        else:
+            s = prev[:, None] + a
+            arg = np.argmax(s, axis=0)  # first maximal index, like ndarray-stats argmax
+            m = s[arg, cols]
+            if assoc == CP:
+                cur = prev[arg] + (a[arg, cols] + e)
+            else:
+                cur = m + e
+            if assoc == DECODE:
+                dead = ~(e > ninf)
+                cur = np.where(dead, ninf, cur)
+                arg = np.where(dead, 0, arg)
+        bt[t] = arg
+        prev = cur.astype(dtype)
+    end = int(np.argmax(prev))
+    best = prev[end]
+    path = np.zeros(T, np.int32)
+    if not best > ninf:
+        return path, ninf, SEQ_INFEASIBLE
+    cs = end
+    for t in range(T - 1, -1, -1):
+        path[t] = cs
+        cs = bt[t, cs]
+    return path, best, SEQ_OK
+
+
+def decode_batch(pi, a, b, offsets, obs, assoc=VITERBI, dtype=np.float64):
+    nseq = len(offsets) - 1
+    path = np.zeros(int(offsets[-1]), np.int32)
+    score = np.zeros(nseq, np.float64)
+    status = np.zeros(nseq, np.uint8)
+    for s in range(nseq):
+        lo, hi = int(offsets[s]), int(offsets[s + 1])
+        p, sc, st = decode(pi, a, b, obs[lo:hi], assoc, dtype)
+        path[lo:hi] = p
+        score[s] = float(sc)
+        status[s] = st
+    return path, score, status
+
+
+def path_score(pi, a, b, obs, path, dtype=np.float64):
+    """Row-A0 float score of a fixed path: d=(d + a[p,q]) + b[q,o], sequential rounding."""
+    pi = np.asarray(pi, dtype)
+    a = np.asarray(a, dtype)
+    b = np.asarray(b, dtype)
+    d = pi[path[0]] + b[path[0], obs[0]]
+    for t in range(1, len(obs)):
+        d = d + a[path[t - 1], path[t]]
+        d = d + b[path[t], obs[t]]
+    return d
+
+
+def brute_force(pi, a, b, obs, dtype=np.float64):
+    """Exhaustive Viterbi: max float score over all N^T paths (row-A0 per-path rounding).
+
+    Float addition is monotone, so the DP's delta equals this maximum exactly.  The DP
+    backtrack's tie rule (first argmax at the end, then first argmax of each
+    predecessor sum) selects, among optimal paths, the one whose REVERSED state
+    sequence is lexicographically smallest -- exactly so whenever the arithmetic is
+    exact (dyadic test values); with rounded arithmetic two paths whose pre-emission
+    sums differ can still round to one total, so callers compare paths only when
+    `n_opt == 1` or the values are dyadic.  Returns (path, score, status, n_opt).
+    """
+    pi = np.asarray(pi, dtype)
+    a = np.asarray(a, dtype)
+    b = np.asarray(b, dtype)
+    n = a.shape[0]
+    T = len(obs)
+    paths = np.array(list(itertools.product(range(n), repeat=T)), dtype=np.int64)
+    d = pi[paths[:, 0]] + b[paths[:, 0], obs[0]]
+    for t in range(1, T):
+        d = d + a[paths[:, t - 1], paths[:, t]]
+        d = d + b[paths[:, t], obs[t]]
+    best = d.max()
+    if not best > -np.inf:
+        return np.zeros(T, np.int32), dtype(-np.inf), SEQ_INFEASIBLE, 0
+    cand = paths[d == best]
+    # np.lexsort(keys) sorts by keys[-1] first; cand.T rows are t=0..T-1, so the primary
+    # key is t=T-1, then T-2, ...: lexicographic order of the reversed sequence.
+    order = np.lexsort(cand.T)
+    return cand[order[0]].astype(np.int32), best, SEQ_OK, int(cand.shape[0])
