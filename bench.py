@@ -99,9 +99,10 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
 
+    from cviterbi import dist as cvd
+
     B = args.batch
-    per = (B + world - 1) // world
-    s0, s1 = min(rank * per, B), min((rank + 1) * per, B)
+    s0, s1, per = cvd.shard_range(B, world, rank)
     nloc = s1 - s0
     pi, a, b = synth.random_hmm(N_STATES, V_OBS, seed=SEED)
     obs = synth.iid_obs(V_OBS, nloc * T_LEN, SEED, start=s0 * T_LEN)
@@ -115,27 +116,11 @@ def main():
     path_d = torch.empty(nloc * T_LEN, dtype=torch.int32, device=dev)
     score_d = torch.empty(nloc, dtype=torch.float64, device=dev)
     status_d = torch.empty(nloc, dtype=torch.uint8, device=dev)
-    if world > 1 and rank == 0:
-        gpath = [torch.empty(per * T_LEN, dtype=torch.int32, device=dev) for _ in range(world)]
-        gscore = [torch.empty(per, dtype=torch.float64, device=dev) for _ in range(world)]
-        gstat = [torch.empty(per, dtype=torch.uint8, device=dev) for _ in range(world)]
-    else:
-        gpath = gscore = gstat = None
-
-    def pad(x, n):
-        if x.numel() == n:
-            return x
-        y = torch.zeros(n, dtype=x.dtype, device=dev)
-        y[: x.numel()] = x
-        return y
-
     def step():
         cv.decode_batch_device(h, off_d, obs_d, path_d, score_d, status_d, offsets_host=off,
                                stream=stream.cuda_stream, workspace_bytes=WORKSPACE)
         if world > 1:  # RCCL over xGMI: decoded paths, scores, statuses to rank 0
-            dist.gather(pad(path_d, per * T_LEN), gpath, dst=0)
-            dist.gather(pad(score_d, per), gscore, dst=0)
-            dist.gather(pad(status_d, per), gstat, dst=0)
+            cvd.gather_to_root([path_d, score_d, status_d], [per * T_LEN, per, per], dist)
 
     for _ in range(args.warmup):
         step()
