@@ -94,12 +94,13 @@ struct cv_hmm {
   int64_t V = 0;
   std::vector<double> pi, a, b;  // host log10, canonical (-0.0 -> +0.0); b state-major [N*V]
   int device = 0;
-  hipStream_t stream = nullptr;
+  hipStream_t stream = nullptr;     // default stream of the handle
+  hipStream_t bt_stream = nullptr;  // backtrack stream (overlaps the next chunk's forward)
   std::mutex mu;
 
   // trellis kernel tables (f32, padded to NP)
   int np = 0;
-  DevBuf t_aimg, t_pi, t_et, t_at;
+  DevBuf t_aimg, t_aimg_mfma, t_pi, t_et, t_at;
   // f64 tables (generic f64 kernel + re-scoring): pi[N], a[N*N], et[V][N]
   bool f64_ready = false;
   DevBuf d_pi64, d_a64, d_et64;
@@ -111,14 +112,16 @@ struct cv_hmm {
   DevBuf st_off, st_obs, st_path, st_score, st_status;
   std::vector<int32_t> order_host;
   // timing events of the last call
-  std::vector<hipEvent_t> ev;  // 3 per launch: start, mid, end
+  std::vector<hipEvent_t> ev;  // 4 per chunk: fwd start/end (main stream), bt start/end
   int64_t last_launches = 0;
   int32_t last_kernel = 0;
   int32_t last_np = 0;
+  int32_t last_mt = -1;
 
   ~cv_hmm() {
     for (auto e : ev) (void)hipEventDestroy(e);
     if (stream) (void)hipStreamDestroy(stream);
+    if (bt_stream) (void)hipStreamDestroy(bt_stream);
   }
 };
 
@@ -133,6 +136,7 @@ cv_status set_device(cv_hmm* h) {
   if (h->device < 0 || h->device >= n) return set_err(CV_EDEVICE, "device %d out of range (%d devices)", h->device, n);
   HIP_TRY(hipSetDevice(h->device));
   if (!h->stream) HIP_TRY(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+  if (!h->bt_stream) HIP_TRY(hipStreamCreateWithFlags(&h->bt_stream, hipStreamNonBlocking));
   return CV_OK;
 }
 
@@ -160,6 +164,16 @@ cv_status ensure_trellis_tables(cv_hmm* h) {
         dst[2] = A(r0 + 1, j0);
         dst[3] = A(r0 + 1, j0 + 1);
       }
+  // MFMA-assisted kernel: [wave w][tile t][quad q][lane][4] in the 32x32 C/D layout:
+  // lane l, reg r = 4q + c -> row 32t + c + 8q + 4(l>>5), column 32w + (l&31).
+  std::vector<float> img2((size_t)np * np);
+  for (int w = 0; w < np / 32; ++w)
+    for (int t = 0; t < np / 32; ++t)
+      for (int q = 0; q < 4; ++q)
+        for (int lane = 0; lane < 64; ++lane)
+          for (int c = 0; c < 4; ++c)
+            img2[((((size_t)w * (np / 32) + t) * 4 + q) * 64 + lane) * 4 + c] =
+                A(32 * t + c + 8 * q + 4 * (lane >> 5), 32 * w + (lane & 31));
   std::vector<float> pi(np, NI), at((size_t)np * np, NI), et((size_t)V * np, NI);
   for (int j = 0; j < N; ++j) pi[j] = f32(h->pi[j]);
   for (int i = 0; i < N; ++i)
@@ -168,6 +182,7 @@ cv_status ensure_trellis_tables(cv_hmm* h) {
     for (int64_t o = 0; o < V; ++o) et[(size_t)o * np + j] = f32(h->b[(size_t)j * V + o]);
   cv_status st;
   if ((st = upload(h->t_aimg, img.data(), img.size() * 4)) != CV_OK) return st;
+  if ((st = upload(h->t_aimg_mfma, img2.data(), img2.size() * 4)) != CV_OK) return st;
   if ((st = upload(h->t_pi, pi.data(), pi.size() * 4)) != CV_OK) return st;
   if ((st = upload(h->t_at, at.data(), at.size() * 4)) != CV_OK) return st;
   if ((st = upload(h->t_et, et.data(), et.size() * 4)) != CV_OK) return st;
@@ -306,9 +321,22 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
   if (need_f64 && (st = ensure_f64_tables(h)) != CV_OK) return st;
   if (!use_trellis && o.dtype == CV_DTYPE_F32 && (st = ensure_g32_tables(h)) != CV_OK) return st;
 
+  // trellis variant: MFMA-assisted unless asked for the all-VALU kernel (or NP = 32)
+  const bool use_mfma = use_trellis && !(o.flags & CV_FLAG_VALU_TRELLIS) && h->np >= 64;
+  int mt = -1;
+  if (use_mfma) {
+    const int req = (int)((o.flags >> 8) & 0xFF) - 1;
+    mt = req >= 0 ? req : cvk::mfma_default_mt(h->np);
+    if (h->np != 256 && req >= 0 && req != cvk::mfma_default_mt(h->np))
+      return set_err(CV_EUNSUPPORTED, "MFMA tile override is only built for N in (224,256]");
+    if (h->np == 256 && !(mt == 0 || (mt >= 4 && mt <= 8)))
+      return set_err(CV_EINVAL, "MFMA tiles per wave must be 0 or 4..8 (got %d)", mt);
+    if (h->np != 256) mt = cvk::mfma_default_mt(h->np);
+  }
   h->last_launches = 0;
   h->last_kernel = use_trellis ? CV_KERNEL_TRELLIS : CV_KERNEL_GENERIC;
   h->last_np = use_trellis ? h->np : 0;
+  h->last_mt = use_mfma ? mt : -1;
   if (nseq == 0) return CV_OK;
   HIP_TRY(hipMemsetAsync(status_dev, 0, (size_t)nseq, stream));
 
@@ -316,7 +344,17 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
   const uint64_t cap = o.workspace_bytes ? o.workspace_bytes : kDefaultWorkspace;
   const uint64_t per_elem = use_trellis ? (uint64_t)h->np * 4 : (uint64_t)h->N * 2;
   const int real_bytes = o.dtype == CV_DTYPE_F64 ? 8 : 4;
-  // chunk the sequences (original order) so that a chunk's elements fit the workspace
+  const uint64_t total_elems = (uint64_t)(offsets_host[nseq] - offsets_host[0]);
+  // Chunks (contiguous in the original order) are pipelined over two streams: the forward
+  // pass of chunk k+1 runs while chunk k backtracks, out of a double-buffered workspace.
+  // At least ~2,048 sequences per chunk (8 per CU), at most 8 chunks unless the
+  // workspace cap forces more.
+  const bool serial = (o.flags & CV_FLAG_SERIAL) != 0;
+  const uint64_t half_cap = std::max<uint64_t>(serial ? cap : cap / 2, per_elem);
+  uint64_t nchunks = std::max<uint64_t>(1, (total_elems * per_elem + half_cap - 1) / half_cap);
+  if (!serial) nchunks = std::max<uint64_t>(nchunks, std::min<uint64_t>(8, (uint64_t)(nseq / 2048)));
+  const uint64_t target = std::max<uint64_t>(1, (total_elems + nchunks - 1) / nchunks);
+  const uint64_t elem_cap = std::max<uint64_t>(half_cap / per_elem, 1);
   std::vector<std::pair<int64_t, int64_t>> chunks;
   {
     int64_t s0 = 0;
@@ -325,7 +363,7 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
       uint64_t elems = 0;
       while (s1 < nseq) {
         const uint64_t T = (uint64_t)(offsets_host[s1 + 1] - offsets_host[s1]);
-        if (s1 > s0 && (elems + T) * per_elem > cap) break;
+        if (s1 > s0 && (elems + T > elem_cap || elems + T > target)) break;
         elems += T;
         ++s1;
         if (s1 - s0 >= (1 << 30)) break;
@@ -341,10 +379,13 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
     max_elems = std::max<uint64_t>(max_elems, (uint64_t)(offsets_host[c.second] - offsets_host[c.first]));
     max_seqs = std::max<int64_t>(max_seqs, c.second - c.first);
   }
+  const int nbuf = (chunks.size() > 1 && !serial) ? 2 : 1;
   const int64_t T0 = offsets_host[1] - offsets_host[0];
   for (int64_t s = 1; s < nseq && !varlen; ++s) varlen = (offsets_host[s + 1] - offsets_host[s]) != T0;
-  if ((st = h->ws_main.ensure(std::max<uint64_t>(max_elems, 1) * per_elem)) != CV_OK) return st;
-  if (!use_trellis && (st = h->ws_last.ensure((size_t)max_seqs * h->N * real_bytes)) != CV_OK) return st;
+  const size_t buf_bytes = ((std::max<uint64_t>(max_elems, 1) * per_elem + 255) / 256) * 256;
+  const size_t last_bytes = ((size_t)max_seqs * h->N * real_bytes + 255) / 256 * 256;
+  if ((st = h->ws_main.ensure(buf_bytes * nbuf)) != CV_OK) return st;
+  if (!use_trellis && (st = h->ws_last.ensure(last_bytes * nbuf)) != CV_OK) return st;
   const int32_t* order_dev = nullptr;
   if (varlen) {
     // longest-first schedule inside each chunk so the tail of the grid is short sequences
@@ -361,12 +402,19 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
     order_dev = h->ws_order.as<int32_t>();
   }
 
-  size_t evi = 0;
-  for (auto& c : chunks) {
+  hipStream_t bts = serial ? stream : h->bt_stream;
+  const size_t nev = 4 * chunks.size();
+  for (size_t i = 0; i < nev; ++i)
+    if (!get_event(h, i)) return set_err(CV_EDEVICE, "hipEventCreate failed");
+  for (size_t ci = 0; ci < chunks.size(); ++ci) {
+    const auto& c = chunks[ci];
     const int64_t n = c.second - c.first;
-    hipEvent_t e0 = get_event(h, evi++), em = get_event(h, evi++), e1 = get_event(h, evi++);
-    if (!e0 || !em || !e1) return set_err(CV_EDEVICE, "hipEventCreate failed");
-    HIP_TRY(hipEventRecord(e0, stream));
+    const int buf = nbuf == 2 ? (int)(ci % 2) : 0;
+    unsigned char* wsb = h->ws_main.as<unsigned char>() + buf * buf_bytes;
+    unsigned char* lrb = h->ws_last.as<unsigned char>() + buf * last_bytes;
+    hipEvent_t f0 = h->ev[4 * ci], f1 = h->ev[4 * ci + 1], b0 = h->ev[4 * ci + 2], b1 = h->ev[4 * ci + 3];
+    if (!serial && ci >= 2) HIP_TRY(hipStreamWaitEvent(stream, h->ev[4 * (ci - 2) + 3], 0));  // buffer reuse
+    HIP_TRY(hipEventRecord(f0, stream));
     hipError_t err;
     if (use_trellis) {
       cvk::TrellisFwdArgs fa{};
@@ -377,13 +425,59 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
       fa.obs = obs_dev;
       fa.order = order_dev;
       fa.seq_begin = c.first;
-      fa.delta = h->ws_main.as<float>();
+      fa.delta = reinterpret_cast<float*>(wsb);
       fa.delta_elem_base = offsets_host[c.first];
       fa.status = status_dev;
       fa.nobs = (int)h->V;
+      if (use_mfma) {
+        fa.a_img = h->t_aimg_mfma.as<float>();
+        err = cvk::launch_trellis_mfma(h->np, mt, fa, n, stream);
+      } else {
+        err = cvk::launch_trellis_fwd(h->np, fa, n, stream);
+      }
+    } else if (o.dtype == CV_DTYPE_F64) {
+      cvk::GenericFwdArgs<double> fa{};
+      fa.a = h->d_a64.as<double>();
+      fa.pi = h->d_pi64.as<double>();
+      fa.et = h->d_et64.as<double>();
+      fa.offsets = offsets_dev;
+      fa.obs = obs_dev;
+      fa.order = order_dev;
+      fa.seq_begin = c.first;
+      fa.nstates = h->N;
+      fa.nobs = (int)h->V;
+      fa.assoc = o.assoc;
+      fa.psi = reinterpret_cast<uint16_t*>(wsb);
+      fa.psi_elem_base = offsets_host[c.first];
+      fa.last_row = reinterpret_cast<double*>(lrb);
+      fa.status = status_dev;
+      err = cvk::launch_generic_fwd<double>(fa, n, stream);
+    } else {
+      cvk::GenericFwdArgs<float> fa{};
+      fa.a = h->d_a32.as<float>();
+      fa.pi = h->d_pi32.as<float>();
+      fa.et = h->d_et32.as<float>();
+      fa.offsets = offsets_dev;
+      fa.obs = obs_dev;
+      fa.order = order_dev;
+      fa.seq_begin = c.first;
+      fa.nstates = h->N;
+      fa.nobs = (int)h->V;
+      fa.assoc = o.assoc;
+      fa.psi = reinterpret_cast<uint16_t*>(wsb);
+      fa.psi_elem_base = offsets_host[c.first];
+      fa.last_row = reinterpret_cast<float*>(lrb);
+      fa.status = status_dev;
+      err = cvk::launch_generic_fwd<float>(fa, n, stream);
+    }
+    if (err != hipSuccess) return set_err(CV_EDEVICE, "forward launch failed: %s", hipGetErrorString(err));
+    HIP_TRY(hipEventRecord(f1, stream));
+    if (!serial) HIP_TRY(hipStreamWaitEvent(bts, f1, 0));
+    HIP_TRY(hipEventRecord(b0, bts));
+    if (use_trellis) {
       cvk::BacktrackArgs ba{};
-      ba.delta = fa.delta;
-      ba.delta_elem_base = fa.delta_elem_base;
+      ba.delta = reinterpret_cast<const float*>(wsb);
+      ba.delta_elem_base = offsets_host[c.first];
       ba.at = h->t_at.as<float>();
       ba.offsets = offsets_dev;
       ba.obs = obs_dev;
@@ -399,29 +493,13 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
       ba.pi64 = h->d_pi64.as<double>();
       ba.a64 = h->d_a64.as<double>();
       ba.et64 = h->d_et64.as<double>();
-      err = cvk::launch_trellis(h->np, fa, ba, n, stream, em);
+      err = cvk::launch_trellis_bt(h->np, ba, n, bts);
     } else if (o.dtype == CV_DTYPE_F64) {
-      cvk::GenericFwdArgs<double> fa{};
-      fa.a = h->d_a64.as<double>();
-      fa.pi = h->d_pi64.as<double>();
-      fa.et = h->d_et64.as<double>();
-      fa.offsets = offsets_dev;
-      fa.obs = obs_dev;
-      fa.order = order_dev;
-      fa.seq_begin = c.first;
-      fa.nstates = h->N;
-      fa.nobs = (int)h->V;
-      fa.assoc = o.assoc;
-      fa.psi = h->ws_main.as<uint16_t>();
-      fa.psi_elem_base = offsets_host[c.first];
-      fa.last_row = h->ws_last.as<double>();
-      fa.status = status_dev;
       cvk::GenericBtArgs<double> ba{};
-      ba.psi = fa.psi;
-      ba.psi_elem_base = fa.psi_elem_base;
-      ba.last_row = fa.last_row;
+      ba.psi = reinterpret_cast<const uint16_t*>(wsb);
+      ba.psi_elem_base = offsets_host[c.first];
+      ba.last_row = reinterpret_cast<const double*>(lrb);
       ba.offsets = offsets_dev;
-      ba.obs = obs_dev;
       ba.order = order_dev;
       ba.seq_begin = c.first;
       ba.seq_end = c.second;
@@ -434,29 +512,13 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
       ba.pi64 = h->d_pi64.as<double>();
       ba.a64 = h->d_a64.as<double>();
       ba.et64 = h->d_et64.as<double>();
-      err = cvk::launch_generic<double>(fa, ba, n, stream, em);
+      err = cvk::launch_generic_bt<double>(ba, n, bts);
     } else {
-      cvk::GenericFwdArgs<float> fa{};
-      fa.a = h->d_a32.as<float>();
-      fa.pi = h->d_pi32.as<float>();
-      fa.et = h->d_et32.as<float>();
-      fa.offsets = offsets_dev;
-      fa.obs = obs_dev;
-      fa.order = order_dev;
-      fa.seq_begin = c.first;
-      fa.nstates = h->N;
-      fa.nobs = (int)h->V;
-      fa.assoc = o.assoc;
-      fa.psi = h->ws_main.as<uint16_t>();
-      fa.psi_elem_base = offsets_host[c.first];
-      fa.last_row = h->ws_last.as<float>();
-      fa.status = status_dev;
       cvk::GenericBtArgs<float> ba{};
-      ba.psi = fa.psi;
-      ba.psi_elem_base = fa.psi_elem_base;
-      ba.last_row = fa.last_row;
+      ba.psi = reinterpret_cast<const uint16_t*>(wsb);
+      ba.psi_elem_base = offsets_host[c.first];
+      ba.last_row = reinterpret_cast<const float*>(lrb);
       ba.offsets = offsets_dev;
-      ba.obs = obs_dev;
       ba.order = order_dev;
       ba.seq_begin = c.first;
       ba.seq_end = c.second;
@@ -469,12 +531,14 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
       ba.pi64 = h->d_pi64.as<double>();
       ba.a64 = h->d_a64.as<double>();
       ba.et64 = h->d_et64.as<double>();
-      err = cvk::launch_generic<float>(fa, ba, n, stream, em);
+      err = cvk::launch_generic_bt<float>(ba, n, bts);
     }
-    if (err != hipSuccess) return set_err(CV_EDEVICE, "kernel launch failed: %s", hipGetErrorString(err));
-    HIP_TRY(hipEventRecord(e1, stream));
+    if (err != hipSuccess) return set_err(CV_EDEVICE, "backtrack launch failed: %s", hipGetErrorString(err));
+    HIP_TRY(hipEventRecord(b1, bts));
     ++h->last_launches;
   }
+  // the caller's stream sees the whole decode complete
+  if (!serial) HIP_TRY(hipStreamWaitEvent(stream, h->ev[4 * (chunks.size() - 1) + 3], 0));
   return CV_OK;
 }
 
@@ -660,18 +724,20 @@ CV_API cv_status cv_last_timing(cv_hmm* h, cv_timing* out) {
   out->launches = h->last_launches;
   out->kernel = h->last_kernel;
   out->padded_states = h->last_np;
+  out->mfma_tiles = h->last_mt;
   if (h->last_launches == 0) return CV_OK;
   HIP_TRY(hipSetDevice(h->device));
-  HIP_TRY(hipEventSynchronize(h->ev[3 * h->last_launches - 1]));
-  for (int64_t c = 0; c < h->last_launches; ++c) {
+  const int64_t L = h->last_launches;
+  HIP_TRY(hipEventSynchronize(h->ev[4 * (L - 1) + 3]));
+  for (int64_t c = 0; c < L; ++c) {
     float f = 0, b = 0;
-    HIP_TRY(hipEventElapsedTime(&f, h->ev[3 * c], h->ev[3 * c + 1]));
-    HIP_TRY(hipEventElapsedTime(&b, h->ev[3 * c + 1], h->ev[3 * c + 2]));
+    HIP_TRY(hipEventElapsedTime(&f, h->ev[4 * c], h->ev[4 * c + 1]));
+    HIP_TRY(hipEventElapsedTime(&b, h->ev[4 * c + 2], h->ev[4 * c + 3]));
     out->fwd_ms += f;
     out->bt_ms += b;
   }
   float tot = 0;
-  HIP_TRY(hipEventElapsedTime(&tot, h->ev[0], h->ev[3 * h->last_launches - 1]));
+  HIP_TRY(hipEventElapsedTime(&tot, h->ev[0], h->ev[4 * (L - 1) + 3]));
   out->total_ms = tot;
   return CV_OK;
 }

@@ -21,6 +21,11 @@ struct TrellisFwdArgs {
   int64_t delta_elem_base; // element offset that maps to delta row 0
   uint8_t* status;         // [nseq_total] per-sequence status (pre-zeroed)
   int nobs;                // V
+  // optional features (all null/0 on the plain decode path)
+  const int32_t* forced;   // [sum T] -1 free, else the state forced at that element
+  const int64_t* ranges;   // [nslot][2] explicit element ranges (begin, end); slot = sequence id
+  int reverse;             // 1: traverse each range from end-1 down to begin
+  float* last_row;         // [nslot][NP] final delta row of each slot (slot - seq_begin)
 };
 
 struct BacktrackArgs {
@@ -44,6 +49,7 @@ struct BacktrackArgs {
 
 template <typename REAL>
 struct GenericFwdArgs {
+  const int32_t* forced;   // [sum T] nullable: -1 free, else forced state
   const REAL* a;           // [N*N]
   const REAL* pi;          // [N]
   const REAL* et;          // [V][N]
@@ -78,11 +84,15 @@ struct GenericBtArgs {
 };
 
 int trellis_padded_states(int n);  // 0 if the trellis kernel does not cover n
-hipError_t launch_trellis(int np, const TrellisFwdArgs& fa, const BacktrackArgs& ba, int64_t nseq,
-                          hipStream_t stream, hipEvent_t ev_mid);
+hipError_t launch_trellis_fwd(int np, const TrellisFwdArgs& fa, int64_t nseq, hipStream_t stream);
+// MFMA-assisted forward (trellis_mfma_f32): A image in the 32x32 MFMA C/D layout; mt < 0 = default.
+hipError_t launch_trellis_mfma(int np, int mt, const TrellisFwdArgs& fa, int64_t nseq, hipStream_t stream);
+int mfma_default_mt(int np);
+hipError_t launch_trellis_bt(int np, const BacktrackArgs& ba, int64_t nseq, hipStream_t stream);
 template <typename REAL>
-hipError_t launch_generic(const GenericFwdArgs<REAL>& fa, const GenericBtArgs<REAL>& ba, int64_t nseq,
-                          hipStream_t stream, hipEvent_t ev_mid);
+hipError_t launch_generic_fwd(const GenericFwdArgs<REAL>& fa, int64_t nseq, hipStream_t stream);
+template <typename REAL>
+hipError_t launch_generic_bt(const GenericBtArgs<REAL>& ba, int64_t nseq, hipStream_t stream);
 int generic_max_states(int real_bytes);
 
 }  // namespace cvk

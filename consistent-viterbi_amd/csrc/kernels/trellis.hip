@@ -53,6 +53,27 @@ __device__ __forceinline__ float octet_max(float x) {
   return x;
 }
 
+// max of x over lane pairs (l, l^16) or (l, l^32).  permlane*_swap(u, u) may be lowered
+// with ONE register as both operands, which makes it a plain swap, so the lane's own
+// value is folded in explicitly: max3(x, r0, r1) is right for either lowering.
+__device__ __forceinline__ float swap_max(float x, bool sixteen) {
+  const unsigned u = __builtin_bit_cast(unsigned, x);
+  const auto r = sixteen ? __builtin_amdgcn_permlane16_swap(u, u, false, false)
+                         : __builtin_amdgcn_permlane32_swap(u, u, false, false);
+  return fmaxf(x, fmaxf(__builtin_bit_cast(float, r[0]), __builtin_bit_cast(float, r[1])));
+}
+
+// max over all 64 lanes, result in every lane: DPP inside rows of 16, then permlane swaps.
+__device__ __forceinline__ float wave_max(float x) {
+  x = octet_max(x);
+  asm volatile(
+      "s_nop 1\n\t"
+      "v_max_f32_dpp %0, %0, %0 row_mirror row_mask:0xf bank_mask:0xf"
+      : "+v"(x));
+  x = swap_max(x, true);
+  return swap_max(x, false);
+}
+
 // Workgroup barrier for LDS hand-offs only.  __syncthreads() also emits the workgroup
 // release fence, which waits (vmcnt) for this wave's outstanding GLOBAL stores -- the
 // delta row just written for the backtrack -- adding a store round trip to every step.
@@ -71,7 +92,25 @@ struct TrellisGeom {
   static_assert(NP % 32 == 0 && NP >= 32 && NP <= 256, "NP must be a multiple of 32 in [32,256]");
 };
 
-template <int NP>
+// slot -> (sequence id, first element, length): CSR offsets (+ optional schedule) or an
+// explicit element range per slot (constrained decode: prefixes / reversed suffixes).
+template <bool EXT>
+__device__ __forceinline__ void seq_range(const TrellisFwdArgs& args, int64_t slot, int64_t& seq, int64_t& e0,
+                                          int& T) {
+  if (EXT && args.ranges) {
+    seq = slot;
+    e0 = args.ranges[2 * slot];
+    T = (int)(args.ranges[2 * slot + 1] - e0);
+  } else {
+    seq = args.order ? (int64_t)args.order[slot] : slot;
+    e0 = args.offsets[seq];
+    T = (int)(args.offsets[seq + 1] - e0);
+  }
+}
+
+// EXT = false: the plain decode (no forced states, CSR ranges, forward order, no final-row
+// output) -- the extra features cost registers, so they are a separate instantiation.
+template <int NP, bool EXT>
 __global__ __launch_bounds__(NP * 4) void trellis_fwd_f32(TrellisFwdArgs args) {
   using G = TrellisGeom<NP>;
   constexpr int R = G::R;
@@ -85,14 +124,21 @@ __global__ __launch_bounds__(NP * 4) void trellis_fwd_f32(TrellisFwdArgs args) {
   const int j0 = 16 * w + 2 * cp;
 
   const int64_t slot = args.seq_begin + blockIdx.x;
-  const int64_t seq = args.order ? (int64_t)args.order[slot] : slot;
-  const int64_t e0 = args.offsets[seq];
-  const int T = (int)(args.offsets[seq + 1] - e0);
+  int64_t seq, e0;
+  int T;
+  seq_range<EXT>(args, slot, seq, e0, T);
   if (T <= 0) return;
   // constant address space: uniform loads become s_load (SMEM), off the vmcnt queue.
+  // A reversed range walks obs[end-1], obs[end-2], ... (ob_step = -1).
+  const bool rev = EXT && args.reverse;
+  const int ob_step = rev ? -1 : 1;
+  const int64_t ob0 = rev ? e0 + T - 1 : e0;
   const __attribute__((address_space(4))) int32_t* obs =
-      (const __attribute__((address_space(4))) int32_t*)(args.obs + e0);
-  float* __restrict__ drow = args.delta + (e0 - args.delta_elem_base) * NP + j0;
+      (const __attribute__((address_space(4))) int32_t*)(args.obs + ob0);
+  const __attribute__((address_space(4))) int32_t* frc =
+      (const __attribute__((address_space(4))) int32_t*)((EXT && args.forced) ? args.forced + ob0 : nullptr);
+  float* __restrict__ drow = (!EXT || args.delta) ? args.delta + (e0 - args.delta_elem_base) * NP + j0 : nullptr;
+  float* __restrict__ lrow = (EXT && args.last_row) ? args.last_row + (slot - args.seq_begin) * NP + j0 : nullptr;
   const float* __restrict__ etj = args.et + j0;
   const unsigned V = (unsigned)args.nobs;
 
@@ -116,11 +162,20 @@ __global__ __launch_bounds__(NP * 4) void trellis_fwd_f32(TrellisFwdArgs args) {
   // load leaves the table.
   unsigned bad = 0;
   auto obs_s = [&](int t) -> unsigned {
-    const unsigned o = (unsigned)obs[t];
+    const unsigned o = (unsigned)obs[t * ob_step];
     bad |= (o >= V);
     return o < V ? o : 0u;
   };
+  auto frc_s = [&](int t) -> int { return (EXT && frc) ? frc[t * ob_step] : -1; };
   auto et_row = [&](unsigned o) -> float2 { return *reinterpret_cast<const float2*>(etj + (size_t)o * NP); };
+  // forced state (consistency constraint): every other state of that element is impossible
+  auto force = [&](float2 d, int f) -> float2 {
+    if (EXT && f >= 0) {
+      d.x = (j0 == f) ? d.x : ninf_f();
+      d.y = (j0 + 1 == f) ? d.y : ninf_f();
+    }
+    return d;
+  };
 
   const int lds_w = (j0 / R) * S + (j0 % R);
   // ---- t = 0: d0 = pi + b[:,o0]  (hmm.rs:415-418, cp.rs:98-100) ----
@@ -129,11 +184,14 @@ __global__ __launch_bounds__(NP * 4) void trellis_fwd_f32(TrellisFwdArgs args) {
     float2 d0;
     d0.x = args.pi[j0] + e.x;
     d0.y = args.pi[j0 + 1] + e.y;
+    d0 = force(d0, frc_s(0));
     if (rg == 0) {
       *reinterpret_cast<float2*>(&lds_delta[0][lds_w]) = d0;
-      *reinterpret_cast<float2*>(drow) = d0;
+      if (!EXT || drow) *reinterpret_cast<float2*>(drow) = d0;
+      if (EXT && lrow && T == 1) *reinterpret_cast<float2*>(lrow) = d0;
     }
   }
+  int f_next = frc_s(T > 1 ? 1 : 0);
   unsigned o_next = obs_s(T > 1 ? 1 : 0);
   float2 eA = et_row(o_next);  // emission row of t = 1
   o_next = obs_s(T > 2 ? 2 : T - 1);
@@ -168,7 +226,9 @@ __global__ __launch_bounds__(NP * 4) void trellis_fwd_f32(TrellisFwdArgs args) {
         m1b = fmaxf(fmaxf(m1b, s21), s31);
       }
     }
+    const int f_use = f_next;
     o_next = obs_s(t + 2 < T ? t + 2 : T - 1);
+    f_next = frc_s(t + 1 < T ? t + 1 : T - 1);
     float m0 = fmaxf(m0a, m0b);
     float m1 = fmaxf(m1a, m1b);
     m0 = octet_max(m0);  // fold the 8 row groups of column j0
@@ -176,15 +236,213 @@ __global__ __launch_bounds__(NP * 4) void trellis_fwd_f32(TrellisFwdArgs args) {
     float2 dn;
     dn.x = m0 + e_use.x;  // (d + a) + b -- viterbi.rs:15-17 association
     dn.y = m1 + e_use.y;
+    dn = force(dn, f_use);
     if (rg == 0) {
       *reinterpret_cast<float2*>(&lds_delta[cur ^ 1][lds_w]) = dn;
-      *reinterpret_cast<float2*>(drow + (size_t)t * NP) = dn;
+      if (!EXT || drow) *reinterpret_cast<float2*>(drow + (size_t)t * NP) = dn;
+      if (EXT && lrow && t == T - 1) *reinterpret_cast<float2*>(lrow) = dn;
     }
     lds_barrier();
   };
 
   int t = 1;
   if ((T - 1) & 1) {  // odd number of steps: peel one so the pair loop is straight-line
+    step(t, eA, eB);
+    eA = eB;
+    ++t;
+  }
+  for (; t + 1 < T; t += 2) {
+    step(t, eA, eB);
+    step(t + 1, eB, eA);
+  }
+  if (bad && lane == 0 && w == 0) args.status[seq] = CVK_SEQ_BADOBS;
+}
+
+// ---------------------------------------------------------------------------------
+// trellis_mfma_f32<NP, MT>: the same recurrence with part of the pair adds on the MFMA pipe.
+//
+// v_mfma_f32_32x32x2_f32 computes D = fma(a1,b1, fma(a0,b0, C)) with one rounding per fma
+// (cdna_hip_programming.md §3 "FP32-input MFMA").  With a0 = d[i] (lanes 0-31), b0 = 1,
+// a1 = b1 = 0 (lanes 32-63) and C = the 32x32 transition tile, D[i][j] = fma(d_i, 1, a_ij)
+// = round(d_i + a_ij): bit-identical to the VALU add (no NaN: 0*0 = 0, +inf rejected).
+// The VALU then only takes maxima of those tiles (2 slots/pair -> 1 slot/pair), and does
+// add+max for the remaining TPW-MT tiles, so the matrix and vector pipes run side by side.
+//
+// Layout: wave w owns the 32 columns [32w, 32w+32) for ALL rows, as TPW = NP/32 tiles of
+// 32x32 held in the MFMA C/D register layout (lane l, reg r -> row (r&3) + 8(r>>2) +
+// 4(l>>5) of the tile, column l&31): 16 VGPRs per tile, 128 at NP = 256.  Column maxima
+// need only an in-lane fold and one v_permlane32_swap (no cross-wave partials).
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+template <int NP>
+struct MfmaGeom {
+  static constexpr int WAVES = NP / 32;
+  static constexpr int TPW = NP / 32;                 // row tiles per wave
+  static constexpr int LDS_FLOATS = 2 * NP + NP;      // two delta buffers + a zero block
+  static_assert(NP % 32 == 0 && NP >= 64 && NP <= 256, "NP must be a multiple of 32 in [64,256]");
+};
+
+template <int NP, int MT, bool EXT>
+__global__ __launch_bounds__(NP * 2) void trellis_mfma_f32(TrellisFwdArgs args) {
+  using G = MfmaGeom<NP>;
+  constexpr int TPW = G::TPW;
+  static_assert(MT >= 0 && MT <= TPW, "MT tiles per wave on the MFMA pipe");
+  __shared__ __attribute__((aligned(16))) float lds[G::LDS_FLOATS];
+
+  const int lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
+  const int h = lane >> 5;   // row half inside a tile
+  const int jl = lane & 31;  // column inside the wave's block
+  const int j = 32 * w + jl;
+
+  const int64_t slot = args.seq_begin + blockIdx.x;
+  int64_t seq, e0;
+  int T;
+  seq_range<EXT>(args, slot, seq, e0, T);
+  if (T <= 0) return;
+  const bool rev = EXT && args.reverse;
+  const int ob_step = rev ? -1 : 1;
+  const int64_t ob0 = rev ? e0 + T - 1 : e0;
+  const __attribute__((address_space(4))) int32_t* obs =
+      (const __attribute__((address_space(4))) int32_t*)(args.obs + ob0);
+  const __attribute__((address_space(4))) int32_t* frc =
+      (const __attribute__((address_space(4))) int32_t*)((EXT && args.forced) ? args.forced + ob0 : nullptr);
+  float* __restrict__ drow = (!EXT || args.delta) ? args.delta + (e0 - args.delta_elem_base) * NP + j : nullptr;
+  float* __restrict__ lrow = (EXT && args.last_row) ? args.last_row + (slot - args.seq_begin) * NP + j : nullptr;
+  const float* __restrict__ etj = args.et + j;
+  const unsigned V = (unsigned)args.nobs;
+
+  // transition tiles in the C/D layout: image [w][tile][reg/4][lane][4]
+  f32x16 at[TPW];
+  {
+    const float4* img = reinterpret_cast<const float4*>(args.a_img) + (size_t)w * TPW * 4 * 64 + lane;
+#pragma unroll
+    for (int t = 0; t < TPW; ++t)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float4 v = img[(t * 4 + q) * 64];
+        at[t][4 * q + 0] = v.x;
+        at[t][4 * q + 1] = v.y;
+        at[t][4 * q + 2] = v.z;
+        at[t][4 * q + 3] = v.w;
+      }
+  }
+  // zero block read by lanes 32-63 as the a1 = 0 MFMA operand
+  for (int i = threadIdx.x; i < NP; i += blockDim.x) lds[2 * NP + i] = 0.f;
+  const float bone = lane < 32 ? 1.0f : 0.0f;  // b0 = 1 (k = 0), b1 = 0 (k = 1)
+
+  unsigned bad = 0;
+  auto obs_s = [&](int t) -> unsigned {
+    const unsigned o = (unsigned)obs[t * ob_step];
+    bad |= (o >= V);
+    return o < V ? o : 0u;
+  };
+  auto frc_s = [&](int t) -> int { return (EXT && frc) ? frc[t * ob_step] : -1; };
+  auto et_row = [&](unsigned o) -> float { return etj[(size_t)o * NP]; };
+
+  {
+    const float e = et_row(obs_s(0));
+    float d0 = args.pi[j] + e;  // hmm.rs:415-418
+    const int f0 = frc_s(0);
+    if (EXT && f0 >= 0 && j != f0) d0 = ninf_f();
+    if (lane < 32) {
+      lds[j] = d0;
+      if (!EXT || drow) drow[0] = d0;
+      if (EXT && lrow && T == 1) lrow[0] = d0;
+    }
+  }
+  int f_next = frc_s(T > 1 ? 1 : 0);
+  unsigned o_next = obs_s(T > 1 ? 1 : 0);
+  float eA = et_row(o_next);
+  o_next = obs_s(T > 2 ? 2 : T - 1);
+  float eB;
+  lds_barrier();
+
+  auto step = [&](int t, float e_use, float& e_pref) {
+    e_pref = et_row(o_next);
+    const int cur = (t - 1) & 1;
+    const float* dbuf = lds + cur * NP;
+    // MFMA a-operand source: d[rb*32 + lane] for lanes 0-31, the zero block for 32-63
+    const float* asrc = lane < 32 ? dbuf + lane : lds + 2 * NP;
+    const float* vsrc = dbuf + 4 * h;  // VALU tiles: rows 8q + 4h + {0..3}
+    float m0 = ninf_f(), m1 = ninf_f(), m2 = ninf_f(), m3 = ninf_f();
+    // Software pipeline: two MFMA results in flight; between an MFMA's issue and the
+    // max over its result the wave runs half a VALU tile (8 adds + 4 max3), so the
+    // matrix and vector pipes overlap.  sched_barrier pins the order (hipcc would
+    // otherwise pad each MFMA->VALU dependency with s_nop).
+    float amf[MT > 0 ? MT : 1];
+#pragma unroll
+    for (int k = 0; k < MT; ++k) amf[k] = asrc[32 * k];
+    constexpr int NV = TPW - MT;  // VALU tiles, processed as 2*NV half tiles
+    auto vhalf = [&](int vh) {    // half tile vh: tile MT + vh/2, quads 2*(vh&1), +1
+      const int t2 = MT + (vh >> 1);
+#pragma unroll
+      for (int qq = 0; qq < 2; ++qq) {
+        const int q = 2 * (vh & 1) + qq;
+        const float4 dv = *reinterpret_cast<const float4*>(vsrc + 32 * t2 + 8 * q);
+        const float s0 = dv.x + at[t2][4 * q + 0];  // viterbi.rs:15
+        const float s1 = dv.y + at[t2][4 * q + 1];
+        const float s2 = dv.z + at[t2][4 * q + 2];
+        const float s3 = dv.w + at[t2][4 * q + 3];
+        if (qq) {
+          m2 = fmaxf(fmaxf(m2, s0), s1);
+          m3 = fmaxf(fmaxf(m3, s2), s3);
+        } else {
+          m0 = fmaxf(fmaxf(m0, s0), s1);
+          m1 = fmaxf(fmaxf(m1, s2), s3);
+        }
+      }
+    };
+    auto dmax = [&](const f32x16& d) {
+      m0 = fmaxf(fmaxf(m0, d[0]), d[1]);
+      m1 = fmaxf(fmaxf(m1, d[2]), d[3]);
+      m2 = fmaxf(fmaxf(m2, d[4]), d[5]);
+      m3 = fmaxf(fmaxf(m3, d[6]), d[7]);
+      m0 = fmaxf(fmaxf(m0, d[8]), d[9]);
+      m1 = fmaxf(fmaxf(m1, d[10]), d[11]);
+      m2 = fmaxf(fmaxf(m2, d[12]), d[13]);
+      m3 = fmaxf(fmaxf(m3, d[14]), d[15]);
+    };
+    f32x16 dA, dB;
+    if constexpr (MT > 0) dA = __builtin_amdgcn_mfma_f32_32x32x2f32(amf[0], bone, at[0], 0, 0, 0);
+    if constexpr (MT > 1) dB = __builtin_amdgcn_mfma_f32_32x32x2f32(amf[1], bone, at[1], 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    int vh = 0;
+#pragma unroll
+    for (int k = 0; k < MT; ++k) {
+      if (vh < 2 * NV) {
+        vhalf(vh);
+        ++vh;
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      if (k & 1) {
+        dmax(dB);
+        if (k + 2 < MT) dB = __builtin_amdgcn_mfma_f32_32x32x2f32(amf[k + 2], bone, at[k + 2], 0, 0, 0);
+      } else {
+        dmax(dA);
+        if (k + 2 < MT) dA = __builtin_amdgcn_mfma_f32_32x32x2f32(amf[k + 2], bone, at[k + 2], 0, 0, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (; vh < 2 * NV; ++vh) vhalf(vh);
+    const int f_use = f_next;
+    o_next = obs_s(t + 2 < T ? t + 2 : T - 1);
+    f_next = frc_s(t + 1 < T ? t + 1 : T - 1);
+    float m = fmaxf(fmaxf(m0, m1), fmaxf(m2, m3));
+    m = swap_max(m, false);  // fold the two row halves (lanes l and l+32) of each column
+    float dn = m + e_use;    // (d + a) + b -- viterbi.rs:15-17 association
+    if (EXT && f_use >= 0 && j != f_use) dn = ninf_f();
+    if (lane < 32) {
+      lds[(cur ^ 1) * NP + j] = dn;
+      if (!EXT || drow) drow[(size_t)t * NP] = dn;
+      if (EXT && lrow && t == T - 1) lrow[0] = dn;
+    }
+    lds_barrier();
+  };
+
+  int t = 1;
+  if ((T - 1) & 1) {
     step(t, eA, eB);
     eA = eB;
     ++t;
@@ -248,8 +506,12 @@ __device__ double rescore_path_f64(const int32_t* path, const int32_t* obs, int 
     }
     const int cnt = min(64, T - base);
     for (int k = 0; k < cnt; ++k) {
-      const double ak = __shfl(av, k);
-      const double bk = __shfl(bv, k);
+      const double ak = __builtin_bit_cast(
+          double, ((unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)(__builtin_bit_cast(unsigned long long, av) >> 32), k) << 32) |
+                      (unsigned)__builtin_amdgcn_readlane((int)__builtin_bit_cast(unsigned long long, av), k));
+      const double bk = __builtin_bit_cast(
+          double, ((unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)(__builtin_bit_cast(unsigned long long, bv) >> 32), k) << 32) |
+                      (unsigned)__builtin_amdgcn_readlane((int)__builtin_bit_cast(unsigned long long, bv), k));
       if (base + k == 0)
         d = ak + bk;  // pi[p0] + b[p0,o0]
       else
@@ -259,8 +521,14 @@ __device__ double rescore_path_f64(const int32_t* path, const int32_t* obs, int 
   return d;
 }
 
+// One wave per sequence.  delta rows are independent of the path, so they are prefetched
+// PF steps ahead into a register ring; only the transition column a[:, path[t]] is a
+// dependent (L2-resident) load.  First argmax = DPP/permlane wave max, then a ballot of
+// the lanes holding it (lowest lane of the lowest k = lowest state index).
 template <int NP>
 __global__ __launch_bounds__(256) void backtrack_f32(BacktrackArgs args) {
+  constexpr int KP = (NP + 63) / 64;
+  constexpr int PF = 8;
   const int lane = threadIdx.x & 63;
   const int64_t slot = args.seq_begin + (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (slot >= args.seq_end) return;
@@ -277,26 +545,30 @@ __global__ __launch_bounds__(256) void backtrack_f32(BacktrackArgs args) {
   }
   int32_t* __restrict__ path = args.path + e0;
   const float* __restrict__ drow = args.delta + (e0 - args.delta_elem_base) * NP;
-  constexpr int KP = (NP + 63) / 64;
-
-  // first argmax of the last row (cp.rs:117-118)
-  float bv = ninf_f();
-  int bi = 0x7fffffff;
-  {
-    const float* last = drow + (size_t)(T - 1) * NP;
+  bool valid[KP];
 #pragma unroll
-    for (int k = 0; k < KP; ++k) {
-      const int i = lane + 64 * k;
-      if (i < N) {
-        const float v = last[i];
-        if (bi == 0x7fffffff || v > bv) {  // ascending i: keeps the first maximum
-          bv = v;
-          bi = i;
-        }
-      }
+  for (int k = 0; k < KP; ++k) valid[k] = (lane + 64 * k) < N;
+  auto load_row = [&](int r, float (&dst)[KP]) {
+#pragma unroll
+    for (int k = 0; k < KP; ++k) dst[k] = (r >= 0 && valid[k]) ? drow[(size_t)r * NP + lane + 64 * k] : ninf_f();
+  };
+  // first argmax of the last row (cp.rs:117-118)
+  int cur;
+  float bv;
+  {
+    float last[KP];
+    load_row(T - 1, last);
+    float m = last[0];
+#pragma unroll
+    for (int k = 1; k < KP; ++k) m = fmaxf(m, last[k]);
+    bv = wave_max(m);
+    cur = 0;
+#pragma unroll
+    for (int k = KP - 1; k >= 0; --k) {
+      const unsigned long long mask = __ballot(valid[k] && last[k] == bv);
+      if (mask) cur = 64 * k + __builtin_ctzll(mask);
     }
   }
-  wave_argmax_first(bv, bi);
   const uint8_t prior = args.status[seq];
   if (!(bv > ninf_f()) || prior == CVK_SEQ_BADOBS) {
     for (int t = lane; t < T; t += 64) path[t] = 0;
@@ -307,41 +579,41 @@ __global__ __launch_bounds__(256) void backtrack_f32(BacktrackArgs args) {
     return;
   }
   const float score32 = bv;
-  int cur = bi;
   int pathreg = 0;
   if (lane == ((T - 1) & 63)) pathreg = cur;
-  if (((T - 1) & 63) == 0) {
-    if (lane == 0) path[T - 1] = cur;
-  }
+  if (((T - 1) & 63) == 0 && lane == 0) path[T - 1] = cur;
   const float* __restrict__ at = args.at;
-  for (int t = T - 1; t >= 1; --t) {
-    // s_i = d_{t-1}[i] + a[i, cur]  -- the forward pass's exact f32 add
-    const float* prow = drow + (size_t)(t - 1) * NP;
-    const float* acol = at + (size_t)cur * NP;
-    float v = ninf_f();
-    int vi = 0x7fffffff;
+  float ring[PF][KP];
 #pragma unroll
-    for (int k = 0; k < KP; ++k) {
-      const int i = lane + 64 * k;
-      if (i < N) {
-        const float s = prow[i] + acol[i];
-        if (vi == 0x7fffffff || s > v) {
-          v = s;
-          vi = i;
+  for (int u = 0; u < PF; ++u) load_row(T - 2 - u, ring[u]);
+  for (int base = T - 1; base >= 1; base -= PF) {
+#pragma unroll
+    for (int u = 0; u < PF; ++u) {
+      const int t = base - u;
+      if (t >= 1) {
+        // s_i = d_{t-1}[i] + a[i, cur]  -- the forward pass's exact f32 add
+        const float* acol = at + (size_t)cur * NP + lane;
+        float s[KP];
+#pragma unroll
+        for (int k = 0; k < KP; ++k) s[k] = valid[k] ? ring[u][k] + acol[64 * k] : ninf_f();
+        load_row(t - 1 - PF, ring[u]);  // refill: used again PF steps later
+        float m = s[0];
+#pragma unroll
+        for (int k = 1; k < KP; ++k) m = fmaxf(m, s[k]);
+        const float M = wave_max(m);
+        int nxt = 0;
+#pragma unroll
+        for (int k = KP - 1; k >= 0; --k) {
+          const unsigned long long mask = __ballot(valid[k] && s[k] == M);
+          if (mask) nxt = 64 * k + __builtin_ctzll(mask);
         }
+        cur = nxt;
+        const int tp = t - 1;
+        if (lane == (tp & 63)) pathreg = cur;
+        if ((tp & 63) == 0 && tp + lane < T) path[tp + lane] = pathreg;  // flush a 64-entry block
       }
     }
-    wave_argmax_first(v, vi);
-    cur = vi;
-    const int tp = t - 1;
-    if (lane == (tp & 63)) pathreg = cur;
-    if ((tp & 63) == 0) {
-      // flush the block [tp, min(tp+64, T)) written in pathreg
-      if (tp + lane < T) path[tp + lane] = pathreg;
-    }
   }
-  // Every 64-entry block is flushed when tp reaches its start (tp = 0 closes the last
-  // one); a top block starting exactly at T-1 was written before the loop.
   if (lane == 0) {
     args.status[seq] = CVK_SEQ_OK;
     if (!args.rescore_f64) args.score[seq] = (double)score32;
@@ -384,6 +656,7 @@ __global__ __launch_bounds__(256) void generic_fwd(GenericFwdArgs<REAL> args) {
         d = (e > ninf) ? (REAL)(args.pi[j] + e) : ninf;
       else
         d = args.pi[j] + e;
+      if (args.forced && args.forced[e0] >= 0 && j != args.forced[e0]) d = ninf;
       dbuf[j] = d;
     }
   }
@@ -428,6 +701,7 @@ __global__ __launch_bounds__(256) void generic_fwd(GenericFwdArgs<REAL> args) {
           arg = 0;
         }
       }
+      if (args.forced && args.forced[e0 + t] >= 0 && j != args.forced[e0 + t]) cur[j] = ninf;
       psi[(size_t)t * N + j] = (uint16_t)arg;
     }
     __syncthreads();
@@ -493,15 +767,22 @@ __global__ __launch_bounds__(256) void generic_backtrack(GenericBtArgs<REAL> arg
 }
 
 // ---------------------------------------------------------------------------------
-// Host-side launchers (called from the C-ABI layer).
+// Host-side launchers (called from the C-ABI layer).  Forward and backtrack are launched
+// separately so the host can run chunk k's backtrack beside chunk k+1's forward pass.
+static bool ext_args(const TrellisFwdArgs& fa) {
+  return fa.forced || fa.ranges || fa.reverse || fa.last_row || !fa.delta;
+}
+
 template <int NP>
-static hipError_t launch_trellis_np(const TrellisFwdArgs& fa, const BacktrackArgs& ba, int64_t nseq,
-                                    hipStream_t stream, hipEvent_t ev_mid) {
-  if (nseq <= 0) return hipSuccess;
-  hipLaunchKernelGGL(trellis_fwd_f32<NP>, dim3((unsigned)nseq), dim3(NP * 4), 0, stream, fa);
-  hipError_t err = hipGetLastError();
-  if (err != hipSuccess) return err;
-  if (ev_mid) (void)hipEventRecord(ev_mid, stream);
+static hipError_t trellis_fwd_np(const TrellisFwdArgs& fa, int64_t nseq, hipStream_t stream) {
+  if (ext_args(fa))
+    hipLaunchKernelGGL((trellis_fwd_f32<NP, true>), dim3((unsigned)nseq), dim3(NP * 4), 0, stream, fa);
+  else
+    hipLaunchKernelGGL((trellis_fwd_f32<NP, false>), dim3((unsigned)nseq), dim3(NP * 4), 0, stream, fa);
+  return hipGetLastError();
+}
+template <int NP>
+static hipError_t trellis_bt_np(const BacktrackArgs& ba, int64_t nseq, hipStream_t stream) {
   hipLaunchKernelGGL(backtrack_f32<NP>, dim3((unsigned)((nseq + 3) / 4)), dim3(256), 0, stream, ba);
   return hipGetLastError();
 }
@@ -511,38 +792,87 @@ int trellis_padded_states(int n) {
   return ((n + 31) / 32) * 32;
 }
 
-hipError_t launch_trellis(int np, const TrellisFwdArgs& fa, const BacktrackArgs& ba, int64_t nseq,
-                          hipStream_t stream, hipEvent_t ev_mid) {
+#define CVK_NP_SWITCH(np, CALL)     \
+  switch (np) {                     \
+    case 32: return CALL(32);       \
+    case 64: return CALL(64);       \
+    case 96: return CALL(96);       \
+    case 128: return CALL(128);     \
+    case 160: return CALL(160);     \
+    case 192: return CALL(192);     \
+    case 224: return CALL(224);     \
+    case 256: return CALL(256);     \
+    default: return hipErrorInvalidValue; \
+  }
+
+hipError_t launch_trellis_fwd(int np, const TrellisFwdArgs& fa, int64_t nseq, hipStream_t stream) {
+  if (nseq <= 0) return hipSuccess;
+#define CVK_FWD(NP) trellis_fwd_np<NP>(fa, nseq, stream)
+  CVK_NP_SWITCH(np, CVK_FWD)
+#undef CVK_FWD
+}
+
+// MFMA-assisted variant: default MFMA tiles per wave = 3/4 of the wave's row tiles
+// (pipe-balance model in DESIGN.md §3); NP = 32 has no MFMA variant.
+int mfma_default_mt(int np) { return (3 * (np / 32) + 2) / 4; }
+
+// The MFMA variant is built for the plain decode only (its EXT instantiation spills at
+// NP = 256); forced / ranged / reversed passes use the VALU kernel (launch_trellis_fwd).
+template <int NP, int MT>
+static hipError_t mfma_np(const TrellisFwdArgs& fa, int64_t nseq, hipStream_t stream) {
+  if (ext_args(fa)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL((trellis_mfma_f32<NP, MT, false>), dim3((unsigned)nseq), dim3(NP * 2), 0, stream, fa);
+  return hipGetLastError();
+}
+
+hipError_t launch_trellis_mfma(int np, int mt, const TrellisFwdArgs& fa, int64_t nseq, hipStream_t stream) {
+  if (nseq <= 0) return hipSuccess;
+  if (mt < 0) mt = mfma_default_mt(np);
   switch (np) {
-    case 32: return launch_trellis_np<32>(fa, ba, nseq, stream, ev_mid);
-    case 64: return launch_trellis_np<64>(fa, ba, nseq, stream, ev_mid);
-    case 96: return launch_trellis_np<96>(fa, ba, nseq, stream, ev_mid);
-    case 128: return launch_trellis_np<128>(fa, ba, nseq, stream, ev_mid);
-    case 160: return launch_trellis_np<160>(fa, ba, nseq, stream, ev_mid);
-    case 192: return launch_trellis_np<192>(fa, ba, nseq, stream, ev_mid);
-    case 224: return launch_trellis_np<224>(fa, ba, nseq, stream, ev_mid);
-    case 256: return launch_trellis_np<256>(fa, ba, nseq, stream, ev_mid);
+    case 64: return mfma_np<64, 2>(fa, nseq, stream);
+    case 96: return mfma_np<96, 2>(fa, nseq, stream);
+    case 128: return mfma_np<128, 3>(fa, nseq, stream);
+    case 160: return mfma_np<160, 4>(fa, nseq, stream);
+    case 192: return mfma_np<192, 5>(fa, nseq, stream);
+    case 224: return mfma_np<224, 5>(fa, nseq, stream);
+    case 256:
+      switch (mt) {
+        case 0: return mfma_np<256, 0>(fa, nseq, stream);
+        case 4: return mfma_np<256, 4>(fa, nseq, stream);
+        case 5: return mfma_np<256, 5>(fa, nseq, stream);
+        case 6: return mfma_np<256, 6>(fa, nseq, stream);
+        case 7: return mfma_np<256, 7>(fa, nseq, stream);
+        case 8: return mfma_np<256, 8>(fa, nseq, stream);
+        default: return hipErrorInvalidValue;
+      }
     default: return hipErrorInvalidValue;
   }
 }
 
+hipError_t launch_trellis_bt(int np, const BacktrackArgs& ba, int64_t nseq, hipStream_t stream) {
+  if (nseq <= 0) return hipSuccess;
+#define CVK_BT(NP) trellis_bt_np<NP>(ba, nseq, stream)
+  CVK_NP_SWITCH(np, CVK_BT)
+#undef CVK_BT
+}
+
 template <typename REAL>
-hipError_t launch_generic(const GenericFwdArgs<REAL>& fa, const GenericBtArgs<REAL>& ba, int64_t nseq,
-                          hipStream_t stream, hipEvent_t ev_mid) {
+hipError_t launch_generic_fwd(const GenericFwdArgs<REAL>& fa, int64_t nseq, hipStream_t stream) {
   if (nseq <= 0) return hipSuccess;
   const size_t lds = sizeof(REAL) * 2 * (size_t)fa.nstates;
   hipLaunchKernelGGL(generic_fwd<REAL>, dim3((unsigned)nseq), dim3(256), lds, stream, fa);
-  hipError_t err = hipGetLastError();
-  if (err != hipSuccess) return err;
-  if (ev_mid) (void)hipEventRecord(ev_mid, stream);
+  return hipGetLastError();
+}
+template <typename REAL>
+hipError_t launch_generic_bt(const GenericBtArgs<REAL>& ba, int64_t nseq, hipStream_t stream) {
+  if (nseq <= 0) return hipSuccess;
   hipLaunchKernelGGL(generic_backtrack<REAL>, dim3((unsigned)((nseq + 3) / 4)), dim3(256), 0, stream, ba);
   return hipGetLastError();
 }
-
-template hipError_t launch_generic<float>(const GenericFwdArgs<float>&, const GenericBtArgs<float>&, int64_t,
-                                          hipStream_t, hipEvent_t);
-template hipError_t launch_generic<double>(const GenericFwdArgs<double>&, const GenericBtArgs<double>&, int64_t,
-                                           hipStream_t, hipEvent_t);
+template hipError_t launch_generic_fwd<float>(const GenericFwdArgs<float>&, int64_t, hipStream_t);
+template hipError_t launch_generic_fwd<double>(const GenericFwdArgs<double>&, int64_t, hipStream_t);
+template hipError_t launch_generic_bt<float>(const GenericBtArgs<float>&, int64_t, hipStream_t);
+template hipError_t launch_generic_bt<double>(const GenericBtArgs<double>&, int64_t, hipStream_t);
 
 // Generic kernel keeps 2*N REAL delta values in LDS.
 int generic_max_states(int real_bytes) { return (int)(65536 / (2 * real_bytes)); }

@@ -19,6 +19,12 @@ SEQ_OK, SEQ_INFEASIBLE, SEQ_EMPTY, SEQ_BADOBS = 0, 1, 2, 3
 DTYPE_F32, DTYPE_F64 = 0, 1
 ASSOC_VITERBI, ASSOC_CP, ASSOC_DP, ASSOC_DECODE = 0, 1, 2, 3
 KERNEL_AUTO, KERNEL_TRELLIS, KERNEL_GENERIC = 0, 1, 2
+FLAG_VALU_TRELLIS = 0x1
+FLAG_SERIAL = 0x2
+
+
+def FLAG_MFMA_TILES(n):
+    return (n + 1) << 8
 
 # every symbol include/cviterbi.h declares (checked by tests/test_abi.py)
 EXPORTS = [
@@ -51,7 +57,8 @@ class Opts(ctypes.Structure):
 
 class Timing(ctypes.Structure):
     _fields_ = [("fwd_ms", ctypes.c_double), ("bt_ms", ctypes.c_double), ("total_ms", ctypes.c_double),
-                ("launches", ctypes.c_int64), ("kernel", ctypes.c_int32), ("padded_states", ctypes.c_int32)]
+                ("launches", ctypes.c_int64), ("kernel", ctypes.c_int32), ("padded_states", ctypes.c_int32),
+                ("mfma_tiles", ctypes.c_int32)]
 
 
 class SuperSeqDesc(ctypes.Structure):
@@ -125,10 +132,11 @@ def check(status):
 
 
 def opts(dtype=DTYPE_F32, assoc=ASSOC_VITERBI, kernel=KERNEL_AUTO, rescore_f64=True, stream=None,
-         workspace_bytes=0):
+         workspace_bytes=0, flags=0):
     o = Opts()
     lib().cv_opts_init(ctypes.byref(o))
     o.dtype, o.assoc, o.kernel, o.rescore_f64 = dtype, assoc, kernel, int(bool(rescore_f64))
     o.stream = stream
     o.workspace_bytes = workspace_bytes
+    o.flags = flags
     return o

@@ -22,13 +22,22 @@ def _p(x):
     return x.ctypes.data_as(ctypes.c_void_p)
 
 
-def make_opts(dtype="f32", assoc="viterbi", kernel="auto", rescore_f64=True, stream=None, workspace_bytes=0):
+def make_opts(dtype="f32", assoc="viterbi", kernel="auto", rescore_f64=True, stream=None, workspace_bytes=0,
+              variant=None, mfma_tiles=None, serial=False):
+    """variant: None/"mfma" (MFMA-assisted trellis, default) or "valu" (all-VALU trellis);
+    mfma_tiles: tuning override of the MFMA tiles per wave (bit-identical results);
+    serial: no forward/backtrack stream overlap."""
+    flags = L.FLAG_SERIAL if serial else 0
+    if variant == "valu":
+        flags |= L.FLAG_VALU_TRELLIS
+    if mfma_tiles is not None:
+        flags |= L.FLAG_MFMA_TILES(mfma_tiles)
     return L.opts(_DT.get(dtype, dtype), _ASSOC.get(assoc, assoc), _KERNEL.get(kernel, kernel), rescore_f64, stream,
-                  workspace_bytes)
+                  workspace_bytes, flags)
 
 
 def decode_batch(hmm: HMM, offsets, obs, dtype="f32", assoc="viterbi", kernel="auto", rescore_f64=True,
-                 workspace_bytes=0):
+                 workspace_bytes=0, variant=None, mfma_tiles=None, serial=False):
     """Decode CSR sequences (offsets[B+1], flat obs) -> (path int32[sum T], score f64[B], status u8[B])."""
     offsets = np.ascontiguousarray(offsets, np.int64)
     obs = np.ascontiguousarray(obs, np.int32)
@@ -37,7 +46,7 @@ def decode_batch(hmm: HMM, offsets, obs, dtype="f32", assoc="viterbi", kernel="a
     path = np.zeros(max(total, 0), np.int32)
     score = np.zeros(max(nseq, 0), np.float64)
     status = np.zeros(max(nseq, 0), np.uint8)
-    o = make_opts(dtype, assoc, kernel, rescore_f64, None, workspace_bytes)
+    o = make_opts(dtype, assoc, kernel, rescore_f64, None, workspace_bytes, variant, mfma_tiles, serial)
     L.check(L.lib().cv_decode_batch(hmm.handle, nseq, _p(offsets), _p(obs), ctypes.byref(o), _p(path), _p(score),
                                     _p(status)))
     return path, score, status
@@ -45,7 +54,7 @@ def decode_batch(hmm: HMM, offsets, obs, dtype="f32", assoc="viterbi", kernel="a
 
 def decode_batch_device(hmm: HMM, offsets_dev, obs_dev, path_dev, score_dev, status_dev, offsets_host=None,
                         dtype="f32", assoc="viterbi", kernel="auto", rescore_f64=True, stream=None,
-                        workspace_bytes=0):
+                        workspace_bytes=0, variant=None, mfma_tiles=None, serial=False):
     """Device-pointer decode (ints or objects with data_ptr(), e.g. torch tensors); async on `stream`."""
     def ptr(x):
         if x is None:
@@ -56,7 +65,7 @@ def decode_batch_device(hmm: HMM, offsets_dev, obs_dev, path_dev, score_dev, sta
     oh = None
     if offsets_host is not None:
         oh = np.ascontiguousarray(offsets_host, np.int64)
-    o = make_opts(dtype, assoc, kernel, rescore_f64, stream, workspace_bytes)
+    o = make_opts(dtype, assoc, kernel, rescore_f64, stream, workspace_bytes, variant, mfma_tiles, serial)
     L.check(L.lib().cv_decode_batch_device(hmm.handle, nseq, _p(oh) if oh is not None else None, ptr(offsets_dev),
                                            ptr(obs_dev), ctypes.byref(o), ptr(path_dev), ptr(score_dev),
                                            ptr(status_dev)))
@@ -66,7 +75,8 @@ def last_timing(hmm: HMM) -> dict:
     t = L.Timing()
     L.check(L.lib().cv_last_timing(hmm.handle, ctypes.byref(t)))
     return dict(fwd_ms=t.fwd_ms, bt_ms=t.bt_ms, total_ms=t.total_ms, launches=t.launches,
-                kernel={1: "trellis", 2: "generic"}.get(t.kernel, "none"), padded_states=t.padded_states)
+                kernel={1: "trellis", 2: "generic"}.get(t.kernel, "none"), padded_states=t.padded_states,
+                mfma_tiles=t.mfma_tiles)
 
 
 def decode(sequence, hmm: HMM):

@@ -55,9 +55,17 @@ enum { CV_DTYPE_F32 = 0, CV_DTYPE_F64 = 1 };
  *  DECODE   VITERBI with row 0 = 0.0                viterbi::decode viterbi.rs:5-32 */
 enum { CV_ASSOC_VITERBI = 0, CV_ASSOC_CP = 1, CV_ASSOC_DP = 2, CV_ASSOC_DECODE = 3 };
 
-/* kernel choice: AUTO picks TRELLIS (register-resident A, f32, VITERBI, N <= 256) when
- * it applies, else GENERIC (inline argmax, f32/f64, any association, N <= 4096). */
+/* kernel choice: AUTO picks TRELLIS (register-resident A, f32, VITERBI, N <= 256; the
+ * MFMA-assisted variant for N > 32) when it applies, else GENERIC (inline argmax, f32/f64,
+ * any association, N <= 8192 f32 / 4096 f64). */
 enum { CV_KERNEL_AUTO = 0, CV_KERNEL_TRELLIS = 1, CV_KERNEL_GENERIC = 2 };
+
+/* cv_opts.flags */
+#define CV_FLAG_VALU_TRELLIS 0x1u /* all-VALU trellis kernel instead of the MFMA-assisted one */
+#define CV_FLAG_SERIAL 0x2u       /* one stream, fewest chunks: no forward/backtrack overlap */
+/* tuning knob: MFMA tiles per wave per step for the MFMA-assisted kernel (N in (224,256]:
+ * 0, 4..8; default 6).  Results are bit-identical for every value. */
+#define CV_FLAG_MFMA_TILES(n) ((uint32_t)((n) + 1) << 8)
 
 typedef struct cv_hmm cv_hmm;
 typedef struct cv_solver cv_solver;
@@ -83,7 +91,7 @@ typedef struct cv_opts {
                             that path); 0: the kernel's own score (f32 widened for F32) */
   void* stream;          /* hipStream_t for the *_device entry points; NULL = handle stream */
   uint64_t workspace_bytes; /* delta/psi workspace cap; 0 = default (8 GiB) */
-  uint32_t flags;        /* reserved, 0 */
+  uint32_t flags;        /* CV_FLAG_* (0 = defaults) */
 } cv_opts;
 
 typedef struct cv_timing {
@@ -93,6 +101,7 @@ typedef struct cv_timing {
   int64_t launches;      /* forward launches (chunks) */
   int32_t kernel;        /* CV_KERNEL_TRELLIS or CV_KERNEL_GENERIC actually used */
   int32_t padded_states; /* NP of the trellis kernel (0 for generic) */
+  int32_t mfma_tiles;    /* MFMA tiles per wave of the trellis kernel, -1 = all-VALU kernel */
 } cv_timing;
 
 typedef struct cv_superseq_desc {

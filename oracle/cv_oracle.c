@@ -26,7 +26,7 @@
  */
 #define CVO_DEFINE_DECODE(NAME, REAL, NEG_INF)                                                  \
   int NAME(int N, int V, const REAL* pi, const REAL* a, const REAL* b, int T,                  \
-           const int32_t* obs, int assoc, int32_t* path, REAL* score) {                        \
+           const int32_t* obs, const int32_t* forced, int assoc, int32_t* path, REAL* score) {  \
     (void)V;                                                                                    \
     if (T <= 0) {                                                                               \
       *score = (REAL)0;                                                                         \
@@ -48,6 +48,10 @@
         else                                                                                    \
           prev[j] = pi[j] + b[(int64_t)j * V + o];                                              \
       }                                                                                         \
+      /* forced state (consistency constraint, opti.rs:101-111): other states impossible */    \
+      if (forced && forced[0] >= 0)                                                             \
+        for (int j = 0; j < N; ++j)                                                             \
+          if (j != forced[0]) prev[j] = ninf;                                                   \
     }                                                                                           \
     for (int t = 1; t < T; ++t) {                                                               \
       const int64_t o = obs[t];                                                                 \
@@ -96,6 +100,9 @@
         else /* viterbi.rs:15-17: (prev + a) + b */                                             \
           cur[j] = m + e;                                                                       \
       }                                                                                         \
+      if (forced && forced[t] >= 0)                                                             \
+        for (int j = 0; j < N; ++j)                                                             \
+          if (j != forced[t]) cur[j] = ninf;                                                    \
       REAL* tmp = prev;                                                                         \
       prev = cur;                                                                               \
       cur = tmp;                                                                                \
@@ -128,19 +135,35 @@
     return status;                                                                              \
   }
 
-CVO_DEFINE_DECODE(cvo_decode_f64, double, -INFINITY)
-CVO_DEFINE_DECODE(cvo_decode_f32, float, -INFINITY)
+CVO_DEFINE_DECODE(cvo_decode_forced_f64, double, -INFINITY)
+CVO_DEFINE_DECODE(cvo_decode_forced_f32, float, -INFINITY)
+
+int cvo_decode_f64(int N, int V, const double* pi, const double* a, const double* b, int T, const int32_t* obs,
+                   int assoc, int32_t* path, double* score) {
+  return cvo_decode_forced_f64(N, V, pi, a, b, T, obs, NULL, assoc, path, score);
+}
+int cvo_decode_f32(int N, int V, const float* pi, const float* a, const float* b, int T, const int32_t* obs,
+                   int assoc, int32_t* path, float* score) {
+  return cvo_decode_forced_f32(N, V, pi, a, b, T, obs, NULL, assoc, path, score);
+}
 
 int cvo_decode_batch_f64(int N, int V, const double* pi, const double* a, const double* b,
                          int64_t nseq, const int64_t* offsets, const int32_t* obs, int assoc,
                          int32_t* path, double* score, uint8_t* status, int nthreads) {
+  return cvo_decode_batch_forced_f64(N, V, pi, a, b, nseq, offsets, obs, NULL, assoc, path, score, status,
+                                     nthreads);
+}
+
+int cvo_decode_batch_forced_f64(int N, int V, const double* pi, const double* a, const double* b,
+                                int64_t nseq, const int64_t* offsets, const int32_t* obs, const int32_t* forced,
+                                int assoc, int32_t* path, double* score, uint8_t* status, int nthreads) {
   if (nthreads < 1) nthreads = 1;
 #pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads)
   for (int64_t s = 0; s < nseq; ++s) {
     const int64_t o0 = offsets[s];
     const int T = (int)(offsets[s + 1] - o0);
     double sc;
-    int st = cvo_decode_f64(N, V, pi, a, b, T, obs + o0, assoc, path + o0, &sc);
+    int st = cvo_decode_forced_f64(N, V, pi, a, b, T, obs + o0, forced ? forced + o0 : NULL, assoc, path + o0, &sc);
     score[s] = sc;
     status[s] = (uint8_t)st;
   }
@@ -150,13 +173,20 @@ int cvo_decode_batch_f64(int N, int V, const double* pi, const double* a, const 
 int cvo_decode_batch_f32(int N, int V, const float* pi, const float* a, const float* b,
                          int64_t nseq, const int64_t* offsets, const int32_t* obs, int assoc,
                          int32_t* path, double* score, uint8_t* status, int nthreads) {
+  return cvo_decode_batch_forced_f32(N, V, pi, a, b, nseq, offsets, obs, NULL, assoc, path, score, status,
+                                     nthreads);
+}
+
+int cvo_decode_batch_forced_f32(int N, int V, const float* pi, const float* a, const float* b,
+                                int64_t nseq, const int64_t* offsets, const int32_t* obs, const int32_t* forced,
+                                int assoc, int32_t* path, double* score, uint8_t* status, int nthreads) {
   if (nthreads < 1) nthreads = 1;
 #pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads)
   for (int64_t s = 0; s < nseq; ++s) {
     const int64_t o0 = offsets[s];
     const int T = (int)(offsets[s + 1] - o0);
     float sc;
-    int st = cvo_decode_f32(N, V, pi, a, b, T, obs + o0, assoc, path + o0, &sc);
+    int st = cvo_decode_forced_f32(N, V, pi, a, b, T, obs + o0, forced ? forced + o0 : NULL, assoc, path + o0, &sc);
     score[s] = (double)sc;
     status[s] = (uint8_t)st;
   }

@@ -52,6 +52,20 @@ int cvo_decode_f64(int N, int V, const double* pi, const double* a, const double
 int cvo_decode_f32(int N, int V, const float* pi, const float* a, const float* b, int T,
                    const int32_t* obs, int assoc, int32_t* path, float* score);
 
+/* forced[T] (nullable): -1 = free, s >= 0 = state s forced at that element (every other
+ * state gets -inf after the row is computed) -- the consistency constraints of
+ * opti.rs:101-111 / dp.rs:157-164 once each component's state is chosen. */
+int cvo_decode_forced_f64(int N, int V, const double* pi, const double* a, const double* b, int T,
+                          const int32_t* obs, const int32_t* forced, int assoc, int32_t* path, double* score);
+int cvo_decode_forced_f32(int N, int V, const float* pi, const float* a, const float* b, int T,
+                          const int32_t* obs, const int32_t* forced, int assoc, int32_t* path, float* score);
+int cvo_decode_batch_forced_f64(int N, int V, const double* pi, const double* a, const double* b,
+                                int64_t nseq, const int64_t* offsets, const int32_t* obs, const int32_t* forced,
+                                int assoc, int32_t* path, double* score, uint8_t* status, int nthreads);
+int cvo_decode_batch_forced_f32(int N, int V, const float* pi, const float* a, const float* b,
+                                int64_t nseq, const int64_t* offsets, const int32_t* obs, const int32_t* forced,
+                                int assoc, int32_t* path, double* score, uint8_t* status, int nthreads);
+
 /* Batch over CSR sequences offsets[nseq+1]; nthreads<=1 -> single thread.
  * score_out is double for both precisions (f32 scores widened exactly). */
 int cvo_decode_batch_f64(int N, int V, const double* pi, const double* a, const double* b,

@@ -51,6 +51,32 @@ def test_trellis_f32_bit_exact(gpu, n):
             assert score[s] == O.rescore_f64(pi, a, b, obs[lo:hi], path[lo:hi])
 
 
+@pytest.mark.parametrize("n", [40, 64, 100, 128, 160, 200, 224, 256])
+@pytest.mark.parametrize("variant", ["valu", "mfma"])
+@pytest.mark.parametrize("serial", [False, True])
+def test_trellis_variants_bit_exact(gpu, n, variant, serial):
+    """Both trellis variants (all-VALU; MFMA-assisted, whose MFMA tiles compute
+    fma(d, 1, a) = d + a exactly) and both schedules (pipelined chunks / serial) give the
+    oracle's f32 result bit for bit."""
+    pi, a, b, off, obs = _case(n, 29, seed=300 + n, nseq=30, tmax=50, zero_frac=0.03)
+    h = cv.HMM(pi, a, b)
+    ref = O.decode_batch(pi, a, b, off, obs, O.VITERBI, np.float32)
+    got = cv.decode_batch(h, off, obs, rescore_f64=False, variant=variant, serial=serial,
+                          workspace_bytes=0 if serial else 256 * 4 * 300)
+    t = cv.last_timing(h)
+    assert (t["mfma_tiles"] >= 0) == (variant == "mfma" and t["padded_states"] >= 64)
+    _assert_same(got, ref, f"{variant} N={n} serial={serial}")
+
+
+@pytest.mark.parametrize("mt", [0, 4, 5, 6, 7, 8])
+def test_mfma_tile_counts_bit_exact(gpu, mt):
+    pi, a, b, off, obs = _case(256, 31, seed=77, nseq=12, tmax=60, zero_frac=0.02)
+    h = cv.HMM(pi, a, b)
+    got = cv.decode_batch(h, off, obs, rescore_f64=False, mfma_tiles=mt)
+    assert cv.last_timing(h)["mfma_tiles"] == mt
+    _assert_same(got, O.decode_batch(pi, a, b, off, obs, O.VITERBI, np.float32), f"mt={mt}")
+
+
 @pytest.mark.parametrize("dtype", ["f32", "f64"])
 @pytest.mark.parametrize("assoc", ["viterbi", "cp", "dp", "decode"])
 @pytest.mark.parametrize("n", [3, 45, 64, 300])
