@@ -101,6 +101,7 @@ struct cv_hmm {
   // trellis kernel tables (f32, padded to NP)
   int np = 0;
   DevBuf t_aimg, t_aimg_mfma, t_pi, t_et, t_at;
+  DevBuf t_aimg_T, t_pi0;  // reversed (backward) pass: VALU image of a^T, pi = 0
   // f64 tables (generic f64 kernel + re-scoring): pi[N], a[N*N], et[V][N]
   bool f64_ready = false;
   DevBuf d_pi64, d_a64, d_et64;
@@ -109,7 +110,8 @@ struct cv_hmm {
   DevBuf d_pi32, d_a32, d_et32;
   // workspace
   DevBuf ws_main, ws_last, ws_order;
-  DevBuf st_off, st_obs, st_path, st_score, st_status;
+  DevBuf st_off, st_obs, st_path, st_score, st_status, st_forced;
+  DevBuf cs_ranges, cs_delta, cs_g, cs_mu;  // constrained-decode scratch
   std::vector<int32_t> order_host;
   // timing events of the last call
   std::vector<hipEvent_t> ev;  // 4 per chunk: fwd start/end (main stream), bt start/end
@@ -117,6 +119,7 @@ struct cv_hmm {
   int32_t last_kernel = 0;
   int32_t last_np = 0;
   int32_t last_mt = -1;
+  uint64_t last_explored = 0;
 
   ~cv_hmm() {
     for (auto e : ev) (void)hipEventDestroy(e);
@@ -183,6 +186,24 @@ cv_status ensure_trellis_tables(cv_hmm* h) {
   cv_status st;
   if ((st = upload(h->t_aimg, img.data(), img.size() * 4)) != CV_OK) return st;
   if ((st = upload(h->t_aimg_mfma, img2.data(), img2.size() * 4)) != CV_OK) return st;
+  {  // the backward max-plus pass runs the same kernel on a^T with pi = 0
+    auto AT = [&](int i, int j) -> float { return A(j, i); };
+    std::vector<float> imgT((size_t)np * np);
+    for (int w = 0; w < np / 16; ++w)
+      for (int q = 0; q < R / 2; ++q)
+        for (int lane = 0; lane < 64; ++lane) {
+          const int rg = lane & 7, cp = lane >> 3, j0 = 16 * w + 2 * cp, r0 = rg * R + 2 * q;
+          float* dst = &imgT[(((size_t)w * (R / 2) + q) * 64 + lane) * 4];
+          dst[0] = AT(r0, j0);
+          dst[1] = AT(r0, j0 + 1);
+          dst[2] = AT(r0 + 1, j0);
+          dst[3] = AT(r0 + 1, j0 + 1);
+        }
+    std::vector<float> pi0(np, NI);
+    for (int j = 0; j < N; ++j) pi0[j] = 0.f;
+    if ((st = upload(h->t_aimg_T, imgT.data(), imgT.size() * 4)) != CV_OK) return st;
+    if ((st = upload(h->t_pi0, pi0.data(), pi0.size() * 4)) != CV_OK) return st;
+  }
   if ((st = upload(h->t_pi, pi.data(), pi.size() * 4)) != CV_OK) return st;
   if ((st = upload(h->t_at, at.data(), at.size() * 4)) != CV_OK) return st;
   if ((st = upload(h->t_et, et.data(), et.size() * 4)) != CV_OK) return st;
@@ -322,7 +343,7 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
   if (!use_trellis && o.dtype == CV_DTYPE_F32 && (st = ensure_g32_tables(h)) != CV_OK) return st;
 
   // trellis variant: MFMA-assisted unless asked for the all-VALU kernel (or NP = 32)
-  const bool use_mfma = use_trellis && !(o.flags & CV_FLAG_VALU_TRELLIS) && h->np >= 64;
+  const bool use_mfma = use_trellis && !(o.flags & CV_FLAG_VALU_TRELLIS) && h->np >= 64 && !o.forced;
   int mt = -1;
   if (use_mfma) {
     const int req = (int)((o.flags >> 8) & 0xFF) - 1;
@@ -429,6 +450,7 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
       fa.delta_elem_base = offsets_host[c.first];
       fa.status = status_dev;
       fa.nobs = (int)h->V;
+      fa.forced = o.forced;
       if (use_mfma) {
         fa.a_img = h->t_aimg_mfma.as<float>();
         err = cvk::launch_trellis_mfma(h->np, mt, fa, n, stream);
@@ -451,6 +473,7 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
       fa.psi_elem_base = offsets_host[c.first];
       fa.last_row = reinterpret_cast<double*>(lrb);
       fa.status = status_dev;
+      fa.forced = o.forced;
       err = cvk::launch_generic_fwd<double>(fa, n, stream);
     } else {
       cvk::GenericFwdArgs<float> fa{};
@@ -468,6 +491,7 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
       fa.psi_elem_base = offsets_host[c.first];
       fa.last_row = reinterpret_cast<float*>(lrb);
       fa.status = status_dev;
+      fa.forced = o.forced;
       err = cvk::launch_generic_fwd<float>(fa, n, stream);
     }
     if (err != hipSuccess) return set_err(CV_EDEVICE, "forward launch failed: %s", hipGetErrorString(err));
@@ -676,14 +700,10 @@ CV_API cv_status cv_decode_batch_device(cv_hmm* h, int64_t nseq, const int64_t* 
   return decode_device(h, nseq, offsets_host, offsets_dev, obs_dev, o, path_dev, score_dev, status_dev, stream);
 }
 
-CV_API cv_status cv_decode_batch(cv_hmm* h, int64_t nseq, const int64_t* offsets, const int32_t* obs,
-                                 const cv_opts* opts, int32_t* path_out, double* score_out, uint8_t* status_out) {
-  if (!h) return set_err(CV_EINVAL, "null handle");
-  if (nseq < 0 || (nseq > 0 && (!offsets || !obs || !path_out || !score_out || !status_out)))
-    return set_err(CV_EINVAL, "null argument");
-  std::lock_guard<std::mutex> lk(h->mu);
-  cv_status st = set_device(h);
-  if (st != CV_OK) return st;
+// Host-pointer decode; caller holds h->mu and has selected the device.
+static cv_status decode_host_locked(cv_hmm* h, int64_t nseq, const int64_t* offsets, const int32_t* obs, cv_opts o,
+                                    int32_t* path_out, double* score_out, uint8_t* status_out) {
+  cv_status st;
   if (nseq == 0) return CV_OK;
   if ((st = check_batch(h, nseq, offsets)) != CV_OK) return st;
   const int64_t base = offsets[0];
@@ -691,7 +711,6 @@ CV_API cv_status cv_decode_batch(cv_hmm* h, int64_t nseq, const int64_t* offsets
   for (int64_t k = base; k < total; ++k)
     if (obs[k] < 0 || obs[k] >= h->V)
       return set_err(CV_EINVAL, "obs[%lld] = %d out of range [0,%lld)", (long long)k, obs[k], (long long)h->V);
-  cv_opts o = opts ? *opts : default_opts();
   hipStream_t stream = o.stream ? (hipStream_t)o.stream : h->stream;
   if ((st = h->st_off.ensure((size_t)(nseq + 1) * 8)) != CV_OK) return st;
   if ((st = h->st_obs.ensure((size_t)std::max<int64_t>(total, 1) * 4)) != CV_OK) return st;
@@ -702,6 +721,16 @@ CV_API cv_status cv_decode_batch(cv_hmm* h, int64_t nseq, const int64_t* offsets
   if (total > base)
     HIP_TRY(hipMemcpyAsync(h->st_obs.as<int32_t>() + base, obs + base, (size_t)(total - base) * 4,
                            hipMemcpyHostToDevice, stream));
+  if (o.forced) {  // host forced[] -> device staging, indexed like obs
+    for (int64_t k = base; k < total; ++k)
+      if (o.forced[k] < -1 || o.forced[k] >= h->N)
+        return set_err(CV_EINVAL, "forced[%lld] = %d out of range [-1,%d)", (long long)k, o.forced[k], h->N);
+    if ((st = h->st_forced.ensure((size_t)std::max<int64_t>(total, 1) * 4)) != CV_OK) return st;
+    if (total > base)
+      HIP_TRY(hipMemcpyAsync(h->st_forced.as<int32_t>() + base, o.forced + base, (size_t)(total - base) * 4,
+                             hipMemcpyHostToDevice, stream));
+    o.forced = h->st_forced.as<int32_t>();
+  }
   st = decode_device(h, nseq, offsets, h->st_off.as<int64_t>(), h->st_obs.as<int32_t>(), o, h->st_path.as<int32_t>(),
                      h->st_score.as<double>(), h->st_status.as<uint8_t>(), stream);
   if (st != CV_OK) {
@@ -714,6 +743,155 @@ CV_API cv_status cv_decode_batch(cv_hmm* h, int64_t nseq, const int64_t* offsets
   HIP_TRY(hipMemcpyAsync(score_out, h->st_score.p, (size_t)nseq * 8, hipMemcpyDeviceToHost, stream));
   HIP_TRY(hipMemcpyAsync(status_out, h->st_status.p, (size_t)nseq, hipMemcpyDeviceToHost, stream));
   HIP_TRY(hipStreamSynchronize(stream));
+  return CV_OK;
+}
+
+CV_API cv_status cv_decode_batch(cv_hmm* h, int64_t nseq, const int64_t* offsets, const int32_t* obs,
+                                 const cv_opts* opts, int32_t* path_out, double* score_out, uint8_t* status_out) {
+  if (!h) return set_err(CV_EINVAL, "null handle");
+  if (nseq < 0 || (nseq > 0 && (!offsets || !obs || !path_out || !score_out || !status_out)))
+    return set_err(CV_EINVAL, "null argument");
+  std::lock_guard<std::mutex> lk(h->mu);
+  cv_status st = set_device(h);
+  if (st != CV_OK) return st;
+  return decode_host_locked(h, nseq, offsets, obs, opts ? *opts : default_opts(), path_out, score_out, status_out);
+}
+
+CV_API cv_status cv_decode_constrained(cv_hmm* h, int64_t nseq, const int64_t* offsets, const int32_t* obs,
+                                       const int32_t* component, int32_t ncomp, const cv_opts* opts,
+                                       int32_t* path_out, double* score_out, uint8_t* status_out,
+                                       int32_t* comp_state_out, double* objective_out) {
+  if (!h) return set_err(CV_EINVAL, "null handle");
+  if (nseq < 0 || ncomp < 0 || (nseq > 0 && (!offsets || !obs || !component || !path_out || !score_out ||
+                                             !status_out)) || (ncomp > 0 && !comp_state_out))
+    return set_err(CV_EINVAL, "null argument");
+  std::lock_guard<std::mutex> lk(h->mu);
+  cv_status st = set_device(h);
+  if (st != CV_OK) return st;
+  cv_opts o = opts ? *opts : default_opts();
+  if (o.dtype != CV_DTYPE_F32 || o.assoc != CV_ASSOC_VITERBI || !cvk::trellis_padded_states(h->N))
+    return set_err(CV_EUNSUPPORTED, "constrained decode runs on the f32 VITERBI trellis path (N <= 256)");
+  if (o.forced) return set_err(CV_EINVAL, "opts->forced is set by the constrained decode itself");
+  for (int32_t c = 0; c < ncomp; ++c) comp_state_out[c] = -1;
+  if (objective_out) *objective_out = 0.0;
+  if (nseq == 0) return CV_OK;
+  if ((st = check_batch(h, nseq, offsets)) != CV_OK) return st;
+  const int64_t base = offsets[0], total = offsets[nseq];
+  for (int64_t k = base; k < total; ++k) {
+    if (obs[k] < 0 || obs[k] >= h->V)
+      return set_err(CV_EINVAL, "obs[%lld] = %d out of range [0,%lld)", (long long)k, obs[k], (long long)h->V);
+    if (component[k] < -1 || component[k] >= ncomp)
+      return set_err(CV_EINVAL, "component[%lld] = %d out of range [-1,%d)", (long long)k, component[k], ncomp);
+  }
+  // constrained elements, in sequence order: (sequence, element, component)
+  struct Con { int64_t seq, elem; int32_t comp; };
+  std::vector<Con> cons;
+  for (int64_t s = 0; s < nseq; ++s) {
+    int found = 0;
+    for (int64_t e = offsets[s]; e < offsets[s + 1]; ++e)
+      if (component[e] >= 0) {
+        if (++found > 1)
+          return set_err(CV_EUNSUPPORTED, "sequence %lld holds more than one constrained element (pairwise "
+                                          "component terms are not implemented)", (long long)s);
+        cons.push_back({s, e, component[e]});
+      }
+  }
+  if ((st = ensure_trellis_tables(h)) != CV_OK) return st;
+  if ((st = ensure_f64_tables(h)) != CV_OK) return st;
+  const int np = h->np;
+  const int64_t ncon = (int64_t)cons.size();
+  hipStream_t stream = o.stream ? (hipStream_t)o.stream : h->stream;
+  std::vector<float> mu((size_t)ncon * np);
+  if (ncon > 0) {
+    if ((st = h->st_obs.ensure((size_t)std::max<int64_t>(total, 1) * 4)) != CV_OK) return st;
+    HIP_TRY(hipMemcpyAsync(h->st_obs.as<int32_t>() + base, obs + base, (size_t)(total - base) * 4,
+                           hipMemcpyHostToDevice, stream));
+    std::vector<int64_t> rg((size_t)ncon * 4);  // prefix ranges, then suffix ranges
+    for (int64_t i = 0; i < ncon; ++i) {
+      rg[2 * i] = offsets[cons[i].seq];
+      rg[2 * i + 1] = cons[i].elem + 1;
+      rg[2 * ncon + 2 * i] = cons[i].elem + 1;
+      rg[2 * ncon + 2 * i + 1] = offsets[cons[i].seq + 1];
+    }
+    if ((st = h->cs_ranges.ensure(rg.size() * 8)) != CV_OK) return st;
+    if ((st = h->cs_delta.ensure((size_t)ncon * np * 4)) != CV_OK) return st;
+    if ((st = h->cs_g.ensure((size_t)ncon * np * 4)) != CV_OK) return st;
+    if ((st = h->cs_mu.ensure((size_t)ncon * np * 4)) != CV_OK) return st;
+    if ((st = h->st_status.ensure((size_t)std::max<int64_t>(nseq, ncon))) != CV_OK) return st;
+    HIP_TRY(hipMemcpyAsync(h->cs_ranges.p, rg.data(), rg.size() * 8, hipMemcpyHostToDevice, stream));
+    cvk::TrellisFwdArgs fa{};
+    fa.a_img = h->t_aimg.as<float>();
+    fa.pi = h->t_pi.as<float>();
+    fa.et = h->t_et.as<float>();
+    fa.obs = h->st_obs.as<int32_t>();
+    fa.status = h->st_status.as<uint8_t>();
+    fa.nobs = (int)h->V;
+    fa.ranges = h->cs_ranges.as<int64_t>();
+    fa.last_row = h->cs_delta.as<float>();
+    hipError_t err = cvk::launch_trellis_fwd(np, fa, ncon, stream);  // delta_{t_k}: forward over the prefix
+    if (err == hipSuccess) {
+      fa.a_img = h->t_aimg_T.as<float>();  // g_{t_k+1}: backward pass = same kernel on a^T, pi = 0, reversed
+      fa.pi = h->t_pi0.as<float>();
+      fa.ranges = h->cs_ranges.as<int64_t>() + 2 * ncon;
+      fa.reverse = 1;
+      fa.last_row = h->cs_g.as<float>();
+      err = cvk::launch_trellis_fwd(np, fa, ncon, stream);
+    }
+    if (err == hipSuccess) {
+      cvk::MaxMarginalArgs ma{};
+      ma.delta = h->cs_delta.as<float>();
+      ma.g = h->cs_g.as<float>();
+      ma.ranges_suffix = h->cs_ranges.as<int64_t>() + 2 * ncon;
+      ma.at = h->t_at.as<float>();
+      ma.mu = h->cs_mu.as<float>();
+      err = cvk::launch_max_marginal(np, ma, ncon, stream);
+    }
+    if (err != hipSuccess) return set_err(CV_EDEVICE, "max-marginal launch failed: %s", hipGetErrorString(err));
+    HIP_TRY(hipMemcpyAsync(mu.data(), h->cs_mu.p, mu.size() * 4, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipStreamSynchronize(stream));
+  }
+  // exact per-component sums of the max-marginals, in units of 2^-64 (order independent)
+  const int N = h->N;
+  std::vector<__int128> acc((size_t)ncomp * N, 0);
+  std::vector<uint8_t> dead((size_t)ncomp * N, 0), used((size_t)ncomp, 0);
+  const double scale = 18446744073709551616.0;  // 2^64
+  for (int64_t i = 0; i < ncon; ++i) {
+    const int32_t c = cons[i].comp;
+    used[c] = 1;
+    for (int s = 0; s < N; ++s) {
+      const float m = mu[(size_t)i * np + s];
+      if (!(m > -INFINITY)) {
+        dead[(size_t)c * N + s] = 1;
+        continue;
+      }
+      acc[(size_t)c * N + s] += (__int128)std::nearbyint((double)m * scale);
+    }
+  }
+  uint64_t explored = 0;
+  for (int32_t c = 0; c < ncomp; ++c) {
+    if (!used[c]) continue;
+    int best = -1;
+    for (int s = 0; s < N; ++s) {
+      if (dead[(size_t)c * N + s]) continue;
+      if (best < 0 || acc[(size_t)c * N + s] > acc[(size_t)c * N + best]) best = s;
+    }
+    comp_state_out[c] = best;
+    explored += (uint64_t)N;
+  }
+  h->last_explored = explored;
+  // final decode with every constrained element forced to its component's state
+  std::vector<int32_t> forced((size_t)total, -1);
+  for (const auto& x : cons) forced[x.elem] = comp_state_out[x.comp] >= 0 ? comp_state_out[x.comp] : 0;
+  o.forced = forced.data();
+  if ((st = decode_host_locked(h, nseq, offsets, obs, o, path_out, score_out, status_out)) != CV_OK) return st;
+  double obj = 0.0;
+  for (const auto& x : cons)
+    if (comp_state_out[x.comp] < 0) {
+      status_out[x.seq] = CV_SEQ_INFEASIBLE;
+      score_out[x.seq] = -INFINITY;
+    }
+  for (int64_t s = 0; s < nseq; ++s) obj += status_out[s] == CV_SEQ_INFEASIBLE ? -INFINITY : score_out[s];
+  if (objective_out) *objective_out = obj;
   return CV_OK;
 }
 
@@ -765,6 +943,8 @@ struct cv_solver {
   std::vector<int64_t> offsets;
   std::vector<int32_t> obs;
   bool constrained = false;
+  std::vector<int32_t> comp;  // active constraint component per element, -1 = none
+  int32_t ncomp = 0;
   std::vector<int32_t> solution;
   std::vector<double> scores;
   std::vector<uint8_t> status;
@@ -801,17 +981,38 @@ CV_API cv_status cv_solver_create(const char* kind, cv_hmm* h, const cv_superseq
   if (s->offsets[0] != 0) return set_err(CV_EINVAL, "super-sequence offsets must start at 0");
   const int64_t total = s->offsets.back();
   s->obs.assign(d->obs, d->obs + total);
+  s->comp.assign((size_t)total, -1);
   if (d->active && d->component)
     for (int64_t k = 0; k < total; ++k)
-      if (d->active[k] && d->component[k] >= 0) s->constrained = true;
+      if (d->active[k] && d->component[k] >= 0) {
+        s->constrained = true;
+        s->comp[k] = d->component[k];
+        s->ncomp = std::max(s->ncomp, d->component[k] + 1);
+      }
   *out = s.release();
   return CV_OK;
 }
 
 CV_API cv_status cv_solver_solve(cv_solver* s) {
   if (!s) return set_err(CV_EINVAL, "null solver");
-  if (s->constrained)
-    return set_err(CV_EUNSUPPORTED, "active consistency constraints are not supported by this ABI version");
+  if (s->constrained) {
+    if (s->kind != "gpu")
+      return set_err(CV_EUNSUPPORTED, "constrained decode runs on the f32 trellis path (solver kind \"gpu\")");
+    const int64_t total = s->offsets.back();
+    s->solution.assign((size_t)total, 0);
+    s->scores.assign((size_t)s->nseq, 0.0);
+    s->status.assign((size_t)s->nseq, 0);
+    std::vector<int32_t> states((size_t)s->ncomp, -1);
+    double obj = 0;
+    cv_status st = cv_decode_constrained(s->hmm, s->nseq, s->offsets.data(), s->obs.data(), s->comp.data(), s->ncomp,
+                                         &s->opts, s->solution.data(), s->scores.data(), s->status.data(),
+                                         states.data(), &obj);
+    if (st != CV_OK) return st;
+    s->objective = obj;
+    s->explored = s->hmm->last_explored;
+    if (!(obj > -INFINITY)) return set_err(CV_EINFEASIBLE, "no assignment satisfies the constraints");
+    return CV_OK;
+  }
   const int64_t total = s->offsets.back();
   s->solution.assign((size_t)total, 0);
   s->scores.assign((size_t)s->nseq, 0.0);

@@ -83,6 +83,15 @@ struct GenericBtArgs {
   const double* et64;
 };
 
+struct MaxMarginalArgs {
+  const float* delta;          // [ncon][NP] forward row at the constrained position
+  const float* g;              // [ncon][NP] last row of the reversed suffix pass
+  const int64_t* ranges_suffix;// [ncon][2] suffix element range (empty -> beta = 0)
+  const float* at;             // [NP][NP] at[j*NP + i] = a[i][j]
+  float* mu;                   // [ncon][NP]
+};
+hipError_t launch_max_marginal(int np, const MaxMarginalArgs& a, int64_t ncon, hipStream_t stream);
+
 int trellis_padded_states(int n);  // 0 if the trellis kernel does not cover n
 hipError_t launch_trellis_fwd(int np, const TrellisFwdArgs& fa, int64_t nseq, hipStream_t stream);
 // MFMA-assisted forward (trellis_mfma_f32): A image in the 32x32 MFMA C/D layout; mt < 0 = default.

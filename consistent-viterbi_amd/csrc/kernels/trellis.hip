@@ -767,6 +767,52 @@ __global__ __launch_bounds__(256) void generic_backtrack(GenericBtArgs<REAL> arg
 }
 
 // ---------------------------------------------------------------------------------
+// Max-marginal at one constrained position (constrained decode):
+//   beta[i] = max_j(g[j] + a[i,j])   (g = last row of the reversed pass; 0 if no suffix)
+//   mu[i]   = delta_tk[i] + beta[i]
+// One workgroup of NP threads per constrained sequence; thread i reads at[j*NP + i] =
+// a[i][j], coalesced across i.
+template <int NP>
+__global__ __launch_bounds__(NP) void max_marginal_f32(MaxMarginalArgs args) {
+  __shared__ float g[NP];
+  const int i = threadIdx.x;
+  const int64_t c = blockIdx.x;
+  const bool suffix = args.ranges_suffix[2 * c + 1] > args.ranges_suffix[2 * c];
+  g[i] = suffix ? args.g[c * NP + i] : 0.f;
+  __syncthreads();
+  float beta = 0.f;
+  if (suffix) {
+    beta = ninf_f();
+#pragma unroll 8
+    for (int j = 0; j < NP; ++j) beta = fmaxf(beta, g[j] + args.at[(size_t)j * NP + i]);
+  }
+  args.mu[c * NP + i] = args.delta[c * NP + i] + beta;
+}
+
+template <int NP>
+static hipError_t mm_np(const MaxMarginalArgs& a, int64_t ncon, hipStream_t stream) {
+  hipLaunchKernelGGL(max_marginal_f32<NP>, dim3((unsigned)ncon), dim3(NP), 0, stream, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_max_marginal(int np, const MaxMarginalArgs& a, int64_t ncon, hipStream_t stream) {
+  if (ncon <= 0) return hipSuccess;
+#define CVK_MM(NP) mm_np<NP>(a, ncon, stream)
+  switch (np) {
+    case 32: return CVK_MM(32);
+    case 64: return CVK_MM(64);
+    case 96: return CVK_MM(96);
+    case 128: return CVK_MM(128);
+    case 160: return CVK_MM(160);
+    case 192: return CVK_MM(192);
+    case 224: return CVK_MM(224);
+    case 256: return CVK_MM(256);
+    default: return hipErrorInvalidValue;
+  }
+#undef CVK_MM
+}
+
+// ---------------------------------------------------------------------------------
 // Host-side launchers (called from the C-ABI layer).  Forward and backtrack are launched
 // separately so the host can run chunk k's backtrack beside chunk k+1's forward pass.
 static bool ext_args(const TrellisFwdArgs& fa) {

@@ -37,8 +37,9 @@ def make_opts(dtype="f32", assoc="viterbi", kernel="auto", rescore_f64=True, str
 
 
 def decode_batch(hmm: HMM, offsets, obs, dtype="f32", assoc="viterbi", kernel="auto", rescore_f64=True,
-                 workspace_bytes=0, variant=None, mfma_tiles=None, serial=False):
-    """Decode CSR sequences (offsets[B+1], flat obs) -> (path int32[sum T], score f64[B], status u8[B])."""
+                 workspace_bytes=0, variant=None, mfma_tiles=None, serial=False, forced=None):
+    """Decode CSR sequences (offsets[B+1], flat obs) -> (path int32[sum T], score f64[B], status u8[B]).
+    forced[sum T] (optional): -1 free, s >= 0 forces state s at that element."""
     offsets = np.ascontiguousarray(offsets, np.int64)
     obs = np.ascontiguousarray(obs, np.int32)
     nseq = offsets.shape[0] - 1
@@ -47,9 +48,33 @@ def decode_batch(hmm: HMM, offsets, obs, dtype="f32", assoc="viterbi", kernel="a
     score = np.zeros(max(nseq, 0), np.float64)
     status = np.zeros(max(nseq, 0), np.uint8)
     o = make_opts(dtype, assoc, kernel, rescore_f64, None, workspace_bytes, variant, mfma_tiles, serial)
+    if forced is not None:
+        forced = np.ascontiguousarray(forced, np.int32)
+        o.forced = forced.ctypes.data
     L.check(L.lib().cv_decode_batch(hmm.handle, nseq, _p(offsets), _p(obs), ctypes.byref(o), _p(path), _p(score),
                                     _p(status)))
     return path, score, status
+
+
+def decode_constrained(hmm: HMM, offsets, obs, component, ncomp=None, rescore_f64=True):
+    """Consistency-constrained decode (cv_decode_constrained): component[sum T] (-1 = free).
+    Returns (path, score, status, comp_state[ncomp], objective)."""
+    offsets = np.ascontiguousarray(offsets, np.int64)
+    obs = np.ascontiguousarray(obs, np.int32)
+    component = np.ascontiguousarray(component, np.int32)
+    if ncomp is None:
+        ncomp = int(component.max()) + 1 if component.size else 0
+    nseq = offsets.shape[0] - 1
+    path = np.zeros(int(offsets[-1]), np.int32)
+    score = np.zeros(nseq, np.float64)
+    status = np.zeros(nseq, np.uint8)
+    states = np.full(max(ncomp, 1), -1, np.int32)
+    obj = ctypes.c_double()
+    o = make_opts("f32", "viterbi", "auto", rescore_f64)
+    L.check(L.lib().cv_decode_constrained(hmm.handle, nseq, _p(offsets), _p(obs), _p(component), int(ncomp),
+                                          ctypes.byref(o), _p(path), _p(score), _p(status), _p(states),
+                                          ctypes.byref(obj)))
+    return path, score, status, states[:ncomp], obj.value
 
 
 def decode_batch_device(hmm: HMM, offsets_dev, obs_dev, path_dev, score_dev, status_dev, offsets_host=None,

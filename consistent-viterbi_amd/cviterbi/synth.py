@@ -5,6 +5,7 @@ corpora need the network), so these are synthetic by design:
   config 2  N=45,  V=50,000 Zipf(1.1)-shaped emissions, T~U[1,128], B=4,096, seed 2
   config 3  N=64,  V=256, T~U[32,1024], B=16,384, seed 3
   config 4  N=256, V=1,024 (bdims [32,32]), T=512, B=65,536, seed 20261015
+  config 5  config 4 + one constrained position in half the sequences, K=7 components
 Rows of A, B and pi are Dirichlet(alpha) samples turned into log10 probabilities
 with exact zeros mapped to -inf (reference hmm/hmm.rs:392-405 `log`).
 """
@@ -102,4 +103,22 @@ def config(name: str, nseq: int | None = None):
         off = offsets_from_lengths(uniform_lengths(rng, 32, 1024, B))
         obs = iid_obs(v, int(off[-1]), seed)
         return dict(pi=pi, a=a, b=b, offsets=off, obs=obs, bdims=(v, 1))
+    if name == "c5":
+        c = config("c4", nseq)
+        c["component"] = constraint_components(c["offsets"], seed=20261016)
+        return c
     raise ValueError(name)
+
+
+def constraint_components(offsets, seed, ncomp=7, prob=0.5):
+    """Config 5: each sequence gets, with probability `prob`, ONE constrained
+    position at a uniform t, with a component uniform in [0, ncomp) -- the reference's POS
+    pipeline puts one tagged position per sentence.  Returns component[sum T] (-1 = free)."""
+    offsets = np.asarray(offsets, np.int64)
+    rng = np.random.default_rng(seed)
+    comp = np.full(int(offsets[-1]), -1, np.int32)
+    for k in range(len(offsets) - 1):
+        T = int(offsets[k + 1] - offsets[k])
+        if T > 0 and rng.random() < prob:
+            comp[offsets[k] + rng.integers(0, T)] = rng.integers(0, ncomp)
+    return comp

@@ -92,6 +92,8 @@ typedef struct cv_opts {
   void* stream;          /* hipStream_t for the *_device entry points; NULL = handle stream */
   uint64_t workspace_bytes; /* delta/psi workspace cap; 0 = default (8 GiB) */
   uint32_t flags;        /* CV_FLAG_* (0 = defaults) */
+  const int32_t* forced; /* [sum T] nullable: -1 = free, s >= 0 = state s forced at that element
+                            (host pointer for cv_decode_batch, device pointer for *_device) */
 } cv_opts;
 
 typedef struct cv_timing {
@@ -167,6 +169,21 @@ CV_API cv_status cv_decode_batch_device(cv_hmm* h, int64_t nseq, const int64_t* 
                                         uint8_t* status_dev);
 /* Device timings of the last decode call on this handle (synchronizes its events). */
 CV_API cv_status cv_last_timing(cv_hmm* h, cv_timing* out);
+/* Consistency-constrained decode (the intended semantics of the reference's constrained
+ * solvers, opti.rs:101-111 / dp.rs:157-164 / cp.rs:95-126): every element with
+ * component[e] >= 0 takes the common state of its component, and the total log-likelihood
+ * is maximised.  Exact when each sequence holds at most one constrained element: per
+ * component, the max-marginals mu_k(s) at the constrained positions (forward + reversed
+ * backward trellis passes on the GPU) are summed exactly (integers in units of 2^-64, so
+ * the choice is independent of order and of how the batch is sharded), s_c = first argmax,
+ * then a forced decode.  f32 trellis path (N <= 256).  comp_state_out[ncomp] gets s_c (-1 if
+ * the component has no active element, or no feasible state); objective_out = sum of the
+ * per-sequence scores (f64 re-scored).  Sequences with two or more constrained elements
+ * return CV_EUNSUPPORTED. Host pointers; synchronous. */
+CV_API cv_status cv_decode_constrained(cv_hmm* h, int64_t nseq, const int64_t* offsets, const int32_t* obs,
+                                       const int32_t* component, int32_t ncomp, const cv_opts* opts,
+                                       int32_t* path_out, double* score_out, uint8_t* status_out,
+                                       int32_t* comp_state_out, double* objective_out);
 /* viterbi::decode (viterbi.rs:5): one sequence, reference decode() semantics (row 0 = 0.0,
  * f64), path only. */
 CV_API cv_status cv_viterbi_decode(cv_hmm* h, int64_t T, const int32_t* obs, int32_t* path_out);
@@ -178,7 +195,8 @@ CV_API cv_status cv_viterbi_decode(cv_hmm* h, int64_t T, const int32_t* obs, int
  *       "gpu-dp"   f64, DP association = DPSolver (dp.rs), ascending-index ties
  * Unconstrained super-sequences decode per sequence: objective =
  * sum of per-sequence scores (sequence order), solution in element order.  Active
- * constraints return CV_EUNSUPPORTED in this ABI version. */
+ * constraints go through cv_decode_constrained ("gpu" kind only); get_explored_nodes then
+ * reports the number of (component, state) candidates scored. */
 CV_API cv_status cv_solver_create(const char* kind, cv_hmm* h, const cv_superseq_desc* seq, cv_solver** out);
 CV_API cv_status cv_solver_solve(cv_solver* s);                                   /* Solver::solve */
 CV_API cv_status cv_solver_get_solution(const cv_solver* s, const int32_t** sol, int64_t* len); /* get_solution */

@@ -35,6 +35,15 @@ def lib():
             f.argtypes = [ctypes.c_int, ctypes.c_int, P, P, P, ctypes.c_int64, P, P, ctypes.c_int, P, P, P,
                           ctypes.c_int]
             f.restype = ctypes.c_int
+        for name in ("cvo_decode_batch_forced_f64", "cvo_decode_batch_forced_f32"):
+            f = getattr(L, name)
+            f.argtypes = [ctypes.c_int, ctypes.c_int, P, P, P, ctypes.c_int64, P, P, P, ctypes.c_int, P, P, P,
+                          ctypes.c_int]
+            f.restype = ctypes.c_int
+        for name in ("cvo_forward_row_f64", "cvo_forward_row_f32"):
+            f = getattr(L, name)
+            f.argtypes = [ctypes.c_int, ctypes.c_int, P, P, P, ctypes.c_int, P, P]
+            f.restype = None
         L.cvo_rescore_f64.argtypes = [ctypes.c_int, ctypes.c_int, P, P, P, ctypes.c_int, P, P]
         L.cvo_rescore_f64.restype = ctypes.c_double
         L.cvo_cp_superseq_f64.argtypes = [ctypes.c_int, ctypes.c_int, P, P, P, ctypes.c_int64, P, P, P]
@@ -47,8 +56,8 @@ def _p(x):
     return x.ctypes.data_as(ctypes.c_void_p)
 
 
-def decode_batch(pi, a, b, offsets, obs, assoc=VITERBI, dtype=np.float64, nthreads=1):
-    """Returns (path int32[sum T], score f64[B], status u8[B])."""
+def decode_batch(pi, a, b, offsets, obs, assoc=VITERBI, dtype=np.float64, nthreads=1, forced=None):
+    """Returns (path int32[sum T], score f64[B], status u8[B]); forced[sum T] optional (-1 free)."""
     dt = np.dtype(dtype)
     pi = np.ascontiguousarray(pi, dt)
     a = np.ascontiguousarray(a, dt)
@@ -60,10 +69,76 @@ def decode_batch(pi, a, b, offsets, obs, assoc=VITERBI, dtype=np.float64, nthrea
     path = np.zeros(int(offsets[-1]), np.int32)
     score = np.zeros(nseq, np.float64)
     status = np.zeros(nseq, np.uint8)
-    fn = lib().cvo_decode_batch_f64 if dt == np.float64 else lib().cvo_decode_batch_f32
-    fn(n, v, _p(pi), _p(a), _p(b), nseq, _p(offsets), _p(obs), assoc, _p(path), _p(score), _p(status),
-       int(nthreads))
+    if forced is None:
+        fn = lib().cvo_decode_batch_f64 if dt == np.float64 else lib().cvo_decode_batch_f32
+        fn(n, v, _p(pi), _p(a), _p(b), nseq, _p(offsets), _p(obs), assoc, _p(path), _p(score), _p(status),
+           int(nthreads))
+    else:
+        forced = np.ascontiguousarray(forced, np.int32)
+        fn = lib().cvo_decode_batch_forced_f64 if dt == np.float64 else lib().cvo_decode_batch_forced_f32
+        fn(n, v, _p(pi), _p(a), _p(b), nseq, _p(offsets), _p(obs), _p(forced), assoc, _p(path), _p(score),
+           _p(status), int(nthreads))
     return path, score, status
+
+
+def forward_row(pi, m, b, obs, dtype):
+    dt = np.dtype(dtype)
+    pi = np.ascontiguousarray(pi, dt)
+    m = np.ascontiguousarray(m, dt)
+    b = np.ascontiguousarray(b, dt)
+    obs = np.ascontiguousarray(obs, np.int32)
+    out = np.zeros(m.shape[0], dt)
+    fn = lib().cvo_forward_row_f64 if dt == np.float64 else lib().cvo_forward_row_f32
+    fn(m.shape[0], b.shape[1], _p(pi), _p(m), _p(b), obs.shape[0], _p(obs), _p(out))
+    return out
+
+
+def max_marginal(pi, a, b, obs, tk, dtype):
+    """Spec of np_oracle.max_marginal, C-accelerated."""
+    dt = np.dtype(dtype).type
+    a_ = np.asarray(a, dt)
+    d = forward_row(pi, a, b, obs[:tk + 1], dt)
+    if tk == len(obs) - 1:
+        beta = np.zeros(a_.shape[0], dt)
+    else:
+        g = forward_row(np.zeros(a_.shape[0]), np.ascontiguousarray(np.asarray(a).T), b, obs[tk + 1:][::-1], dt)
+        beta = (g[None, :] + a_).max(axis=1).astype(dt)
+    return (d + beta).astype(dt)
+
+
+def constrained_forced(pi, a, b, offsets, obs, component, dtype=np.float32):
+    """np_oracle.constrained_decode spec (exact 2^-64 integer sums), C-accelerated.
+    Returns (comp_state dict, forced[sum T])."""
+    import np_oracle as NO
+
+    offsets = np.asarray(offsets, np.int64)
+    component = np.asarray(component, np.int64)
+    n = np.asarray(a).shape[0]
+    sums = {}
+    for k in range(len(offsets) - 1):
+        lo, hi = offsets[k], offsets[k + 1]
+        pos = np.nonzero(component[lo:hi] >= 0)[0]
+        if len(pos) == 0:
+            continue
+        assert len(pos) == 1
+        tk = int(pos[0])
+        c = int(component[lo + tk])
+        mu = max_marginal(pi, a, b, np.asarray(obs[lo:hi]), tk, dtype)
+        acc = sums.setdefault(c, [0] * n)
+        for s in range(n):
+            u = NO.exact_units(mu[s])
+            acc[s] = None if (u is None or acc[s] is None) else acc[s] + u
+    comp_state = {}
+    for c, acc in sums.items():
+        best = None
+        for s in range(n):
+            if acc[s] is not None and (best is None or acc[s] > acc[best]):
+                best = s
+        comp_state[c] = -1 if best is None else best
+    forced = np.full(len(obs), -1, np.int32)
+    for e in np.nonzero(component >= 0)[0]:
+        forced[e] = max(comp_state[int(component[e])], 0)
+    return comp_state, forced
 
 
 def rescore_f64(pi, a, b, obs, path):

@@ -259,3 +259,32 @@ double cvo_cp_superseq_f64(int N, int V, const double* pi, const double* a, cons
   free(first);
   return obj;
 }
+
+/* Last delta row of the row-A0 forward recurrence over obs[0..T) with an arbitrary
+ * transition matrix m[from*N + to] (pass a^T and pi = 0 over reversed observations for
+ * the backward max-plus pass of the constrained decode spec, np_oracle.py). */
+#define CVO_DEFINE_ROW(NAME, REAL)                                                              \
+  void NAME(int N, int V, const REAL* pi, const REAL* m, const REAL* b, int T, const int32_t* obs, \
+            REAL* out) {                                                                        \
+    REAL* prev = (REAL*)malloc(sizeof(REAL) * (size_t)N);                                       \
+    REAL* cur = (REAL*)malloc(sizeof(REAL) * (size_t)N);                                        \
+    for (int j = 0; j < N; ++j) prev[j] = pi[j] + b[(int64_t)j * V + obs[0]];                   \
+    for (int t = 1; t < T; ++t) {                                                               \
+      for (int j = 0; j < N; ++j) {                                                             \
+        REAL mx = prev[0] + m[j];                                                               \
+        for (int i = 1; i < N; ++i) {                                                           \
+          const REAL s = prev[i] + m[(int64_t)i * N + j];                                       \
+          if (s > mx) mx = s;                                                                   \
+        }                                                                                       \
+        cur[j] = mx + b[(int64_t)j * V + obs[t]];                                               \
+      }                                                                                         \
+      REAL* tmp = prev;                                                                         \
+      prev = cur;                                                                               \
+      cur = tmp;                                                                                \
+    }                                                                                           \
+    for (int j = 0; j < N; ++j) out[j] = prev[j];                                               \
+    free(prev);                                                                                 \
+    free(cur);                                                                                  \
+  }
+CVO_DEFINE_ROW(cvo_forward_row_f64, double)
+CVO_DEFINE_ROW(cvo_forward_row_f32, float)

@@ -87,6 +87,12 @@ double cvo_cp_superseq_f64(int N, int V, const double* pi, const double* a, cons
                            int64_t nseq, const int64_t* offsets, const int32_t* obs,
                            int32_t* path);
 
+/* Last delta row of the row-A0 recurrence with transition matrix m (constrained spec). */
+void cvo_forward_row_f64(int N, int V, const double* pi, const double* m, const double* b, int T,
+                         const int32_t* obs, double* out);
+void cvo_forward_row_f32(int N, int V, const float* pi, const float* m, const float* b, int T,
+                         const int32_t* obs, float* out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -140,3 +140,135 @@ def brute_force(pi, a, b, obs, dtype=np.float64):
     # key is t=T-1, then T-2, ...: lexicographic order of the reversed sequence.
     order = np.lexsort(cand.T)
     return cand[order[0]].astype(np.int32), best, SEQ_OK, int(cand.shape[0])
+
+
+# ---------------------------------------------------------------------------------------
+# Consistency-constrained decode (intended semantics of
+# opti.rs:101-111 / dp.rs:157-164): every ACTIVE position of a component decodes to one
+# common state; maximise the total log-likelihood.  Spec used by the GPU path when each
+# sequence has at most one active constrained position (the components then decouple):
+#   mu_k(s)  = delta_{t_k}(s) + beta_{t_k}(s)           (max-marginal at the position)
+#     delta  : row-A0 forward over elements 0..t_k            (dtype)
+#     g      : the same recurrence run BACKWARD with a^T and pi = 0 over T-1..t_k+1,
+#              g_t[i] = max_j(g_{t+1}[j] + a[i,j]) + b[i,o_t]  (dtype)
+#     beta   : max_j(g_{t_k+1}[j] + a[i,j]), 0 when t_k = T-1  (dtype)
+#   U_c(s)   = sum over the component's sequences of round(mu_k(s) * 2^64) as exact
+#              integers (order- and rank-count independent); -inf terms exclude s
+#   s_c      = first argmax of U_c; then a forced decode with s_c at every active position.
+def forward_last_row(pi, a, b, obs, dtype):
+    pi = np.asarray(pi, dtype)
+    a = np.asarray(a, dtype)
+    b = np.asarray(b, dtype)
+    d = (pi + b[:, obs[0]]).astype(dtype)
+    for t in range(1, len(obs)):
+        d = ((d[:, None] + a).max(axis=0) + b[:, obs[t]]).astype(dtype)
+    return d
+
+
+def exact_units(x):
+    """mu (float) -> exact integer in units of 2^-64 (None for -inf)."""
+    x = float(x)
+    if x == -np.inf:
+        return None
+    return int(np.rint(x * 2.0 ** 64))
+
+
+def max_marginal(pi, a, b, obs, tk, dtype):
+    a_ = np.asarray(a, dtype)
+    d = forward_last_row(pi, a, b, obs[:tk + 1], dtype)
+    T = len(obs)
+    if tk == T - 1:
+        beta = np.zeros(a_.shape[0], dtype)
+    else:
+        g = forward_last_row(np.zeros(a_.shape[0]), np.asarray(a).T, b, obs[tk + 1:][::-1], dtype)
+        beta = (g[None, :] + a_).max(axis=1).astype(dtype)  # beta[i] = max_j g[j] + a[i,j]
+    return (d + beta).astype(dtype)
+
+
+def constrained_decode(pi, a, b, offsets, obs, component, dtype=np.float32):
+    """Returns (comp_state dict, path, score f64 (f64 re-score for f32), status, objective)."""
+    offsets = np.asarray(offsets, np.int64)
+    obs = np.asarray(obs, np.int64)
+    component = np.asarray(component, np.int64)
+    n = np.asarray(a).shape[0]
+    nseq = len(offsets) - 1
+    sums = {}
+    for k in range(nseq):
+        lo, hi = offsets[k], offsets[k + 1]
+        pos = np.nonzero(component[lo:hi] >= 0)[0]
+        if len(pos) == 0:
+            continue
+        assert len(pos) == 1, "spec covers one active constrained position per sequence"
+        tk = int(pos[0])
+        c = int(component[lo + tk])
+        mu = max_marginal(pi, a, b, obs[lo:hi], tk, dtype)
+        acc = sums.setdefault(c, [0] * n)
+        for s in range(n):
+            u = exact_units(mu[s])
+            if u is None or acc[s] is None:
+                acc[s] = None
+            else:
+                acc[s] += u
+    comp_state = {}
+    for c, acc in sums.items():
+        best = None
+        for s in range(n):
+            if acc[s] is not None and (best is None or acc[s] > acc[best]):
+                best = s
+        comp_state[c] = -1 if best is None else best
+    forced = np.full(len(obs), -1, np.int32)
+    for e in np.nonzero(component >= 0)[0]:
+        forced[e] = comp_state[int(component[e])]
+    return comp_state, forced
+
+
+def constrained_brute(pi, a, b, offsets, obs, component, dtype=np.float64):
+    """Exhaustive over component-state assignments: returns (assignment, objective)
+    maximising the sum of per-sequence forced-decode scores (dtype decode, f64 sum)."""
+    comps = sorted(set(int(c) for c in component if c >= 0))
+    n = np.asarray(a).shape[0]
+    best, best_obj = None, -np.inf
+    for assign in itertools.product(range(n), repeat=len(comps)):
+        st = dict(zip(comps, assign))
+        total = 0.0
+        for k in range(len(offsets) - 1):
+            lo, hi = offsets[k], offsets[k + 1]
+            f = np.array([st[int(c)] if c >= 0 else -1 for c in component[lo:hi]], np.int32)
+            _, sc, status = decode_forced(pi, a, b, obs[lo:hi], f, dtype)
+            total += float(sc) if status == SEQ_OK else -np.inf
+        if total > best_obj:
+            best, best_obj = st, total
+    return best, best_obj
+
+
+def decode_forced(pi, a, b, obs, forced, dtype=np.float64):
+    """Row-A0 decode with forced states (-1 = free)."""
+    pi = np.asarray(pi, dtype)
+    a = np.asarray(a, dtype)
+    b = np.asarray(b, dtype)
+    n, T = a.shape[0], len(obs)
+    if T == 0:
+        return np.zeros(0, np.int32), dtype(0), SEQ_EMPTY
+    ninf = dtype(-np.inf)
+    prev = (pi + b[:, obs[0]]).astype(dtype)
+    if forced[0] >= 0:
+        prev = np.where(np.arange(n) == forced[0], prev, ninf)
+    bt = np.zeros((T, n), np.int32)
+    cols = np.arange(n)
+    for t in range(1, T):
+        s = prev[:, None] + a
+        arg = np.argmax(s, axis=0)
+        cur = (s[arg, cols] + b[:, obs[t]]).astype(dtype)
+        if forced[t] >= 0:
+            cur = np.where(cols == forced[t], cur, ninf)
+        bt[t] = arg
+        prev = cur
+    end = int(np.argmax(prev))
+    if not prev[end] > ninf:
+        return np.zeros(T, np.int32), ninf, SEQ_INFEASIBLE
+    path = np.zeros(T, np.int32)
+    cs = end
+    for t in range(T - 1, -1, -1):
+        path[t] = cs
+        cs = bt[t, cs]
+    return path, prev[end], SEQ_OK

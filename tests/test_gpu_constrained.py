@@ -1,0 +1,79 @@
+"""GPU: forced-state decoding and the consistency-constrained decode (config 5) against
+the oracle spec (oracle/np_oracle.py constrained_decode, C-accelerated in c_oracle):
+component states identical, paths bit-exact (f32), scores = f64 re-score of the path."""
+import numpy as np
+import pytest
+
+import c_oracle as O
+import cviterbi as cv
+from cviterbi import synth
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("n", [5, 45, 64, 200, 256])
+@pytest.mark.parametrize("variant", ["valu", "mfma"])
+def test_forced_decode_bit_exact(gpu, n, variant):
+    pi, a, b = synth.random_hmm(n, 19, seed=n)
+    rng = np.random.default_rng(n)
+    off = synth.offsets_from_lengths(rng.integers(1, 60, size=20))
+    obs = rng.integers(0, 19, size=int(off[-1])).astype(np.int32)
+    forced = np.where(rng.random(len(obs)) < 0.05, rng.integers(0, n, size=len(obs)), -1).astype(np.int32)
+    h = cv.HMM(pi, a, b)
+    got = cv.decode_batch(h, off, obs, rescore_f64=False, forced=forced, variant=variant)
+    ref = O.decode_batch(pi, a, b, off, obs, O.VITERBI, np.float32, forced=forced)
+    for x, y, what in zip(got, ref, ("path", "score", "status")):
+        assert np.array_equal(x, y), what
+
+
+def _check(h, pi, a, b, off, obs, comp):
+    path, score, status, states, obj = cv.decode_constrained(h, off, obs, comp)
+    ref_states, forced = O.constrained_forced(pi, a, b, off, obs, comp, np.float32)
+    for c, s in ref_states.items():
+        assert states[c] == s, (c, states[c], s)
+    rp, rs, rst = O.decode_batch(pi, a, b, off, obs, O.VITERBI, np.float32, forced=forced)
+    assert np.array_equal(status, rst)
+    assert np.array_equal(path, rp)
+    for k in range(len(off) - 1):
+        if status[k] == 0:
+            assert score[k] == O.rescore_f64(pi, a, b, obs[off[k]:off[k + 1]], path[off[k]:off[k + 1]])
+    assert obj == pytest.approx(float(np.sum(score)), rel=1e-12)
+    for e in np.nonzero(comp >= 0)[0]:
+        assert path[e] == states[comp[e]]
+
+
+@pytest.mark.parametrize("n", [4, 33, 64, 256])
+def test_constrained_small(gpu, n):
+    pi, a, b = synth.random_hmm(n, 11, seed=50 + n)
+    rng = np.random.default_rng(n)
+    off = synth.offsets_from_lengths(rng.integers(1, 40, size=24))
+    obs = rng.integers(0, 11, size=int(off[-1])).astype(np.int32)
+    comp = synth.constraint_components(off, seed=n, ncomp=3, prob=0.6)
+    _check(cv.HMM(pi, a, b), pi, a, b, off, obs, comp)
+
+
+def test_constrained_config5_subset(gpu):
+    c = synth.config("c5", nseq=48)
+    _check(cv.HMM(c["pi"], c["a"], c["b"]), c["pi"], c["a"], c["b"], c["offsets"], c["obs"], c["component"])
+
+
+def test_constrained_solver_api(gpu):
+    pi, a, b = synth.random_hmm(10, 8, seed=9)
+    rng = np.random.default_rng(9)
+    seqs = [[int(x) for x in rng.integers(0, 8, size=int(t))] for t in rng.integers(2, 20, size=12)]
+    tags = [[(int(rng.integers(0, 3)) if (t == 0 and rng.random() < 0.6) else None) for t in range(len(s))]
+            for s in seqs]
+    h = cv.HMM(pi, a, b)
+    ss = cv.SuperSequence(seqs, cv.Constraints.from_tags(tags), h)
+    ss.recompute_constraints(1.0)
+    s = cv.GpuSolver(h, ss, "gpu")
+    s.solve()
+    sol = s.get_solution()
+    assert s.get_explored_nodes() == 10 * ss.number_constraints()
+    # every active element of a component decodes to one state
+    for c in set(ss.component[ss.active == 1].tolist()):
+        assert len(set(sol[(ss.component == c) & (ss.active == 1)].tolist())) == 1
+    offsets, obs, _ = ss.sequence_blocks()
+    comp = np.where(ss.active == 1, ss.component, -1).astype(np.int32)
+    _, _, _, _, obj = cv.decode_constrained(h, offsets, obs, comp)
+    assert s.get_objective() == pytest.approx(obj, rel=1e-12)

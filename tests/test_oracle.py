@@ -163,3 +163,59 @@ def test_cp_superseq_vs_per_sequence():
     p, s, _ = C.decode_batch(pi, a, b, off, obs, C.CP, np.float64)
     assert obj == pytest.approx(float(np.sum(s)), rel=1e-12)
     assert np.array_equal(path, p)
+
+
+# ---- consistency-constrained decode spec (np_oracle.constrained_decode) -------------------
+def _constrained_case(seed, n=3, v=4, nseq=6, tmax=6, ncomp=2, p=0.7):
+    pi, a, b = synth.random_hmm(n, v, seed=seed)
+    rng = np.random.default_rng(seed)
+    lengths = rng.integers(1, tmax, size=nseq)
+    off = synth.offsets_from_lengths(lengths)
+    obs = rng.integers(0, v, size=int(off[-1])).astype(np.int32)
+    comp = np.full(len(obs), -1, np.int32)
+    for k in range(nseq):
+        if rng.random() < p:
+            comp[off[k] + rng.integers(0, lengths[k])] = rng.integers(0, ncomp)
+    return pi, a, b, off, obs, comp
+
+
+@pytest.mark.parametrize("seed", range(25))
+def test_constrained_spec_is_exact_optimum(seed):
+    """With one constrained position per sequence the components decouple, so summing the
+    max-marginals per component and forcing the best state gives the exhaustive optimum
+    over all component-state assignments (f64; equal objective, tolerance 1e-12 rel)."""
+    pi, a, b, off, obs, comp = _constrained_case(seed)
+    states, forced = NO.constrained_decode(pi, a, b, off, obs, comp, np.float64)
+    p, s, st = C.decode_batch(pi, a, b, off, obs, C.VITERBI, np.float64, forced=forced)
+    best, bobj = NO.constrained_brute(pi, a, b, off, obs, comp, np.float64)
+    obj = float(np.sum(np.where(st == 0, s, -np.inf)))
+    assert obj == pytest.approx(bobj, rel=1e-12)
+    for e in np.nonzero(comp >= 0)[0]:
+        k = np.searchsorted(off, e, side="right") - 1
+        assert p[e] == states[int(comp[e])]  # every constrained element takes its component's state
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_constrained_spec_numpy_vs_c(seed):
+    pi, a, b, off, obs, comp = _constrained_case(seed, n=6, v=5, nseq=9, tmax=12, ncomp=3)
+    for dt in (np.float32, np.float64):
+        s1, f1 = NO.constrained_decode(pi, a, b, off, obs, comp, dt)
+        s2, f2 = C.constrained_forced(pi, a, b, off, obs, comp, dt)
+        assert s1 == s2
+
+
+def test_forced_decode_c_vs_numpy():
+    pi, a, b = synth.random_hmm(7, 5, seed=3, zero_frac=0.1)
+    rng = np.random.default_rng(3)
+    off = synth.offsets_from_lengths(rng.integers(1, 15, size=10))
+    obs = rng.integers(0, 5, size=int(off[-1])).astype(np.int32)
+    forced = np.where(rng.random(len(obs)) < 0.2, rng.integers(0, 7, size=len(obs)), -1).astype(np.int32)
+    for dt in (np.float32, np.float64):
+        p, s, st = C.decode_batch(pi, a, b, off, obs, C.VITERBI, dt, forced=forced)
+        for k in range(10):
+            lo, hi = off[k], off[k + 1]
+            q, sc, sst = NO.decode_forced(pi, a, b, obs[lo:hi], forced[lo:hi], dt)
+            assert sst == st[k]
+            if sst == 0:
+                assert np.array_equal(q, p[lo:hi]) and float(sc) == s[k]
+                assert all(p[lo + t] == forced[lo + t] for t in range(hi - lo) if forced[lo + t] >= 0)
