@@ -7,8 +7,9 @@ Mirrors (file:line into /root/reference/src):
   Constraints::from_tags/from_file  viterbi_solver/constraints.rs:12-69
   load_sequences / load_tags        utils.rs:7-60
   main's output file                main.rs:111-133
-Unconstrained decoding goes through cv_solver_* (libcviterbi); constrained B&B/CSP
-search is not implemented in this round (CV_EUNSUPPORTED).
+Decoding goes through cv_solver_* (libcviterbi).  Active consistency constraints use
+cv_decode_constrained (exact when every sequence holds at most one active constrained
+element; more than one per sequence -> CV_EUNSUPPORTED).
 """
 from __future__ import annotations
 
@@ -19,6 +20,7 @@ import numpy as np
 
 from . import _lib as L
 from .hmm import HMM
+from .stdrng import StdRng
 
 
 def _p(x):
@@ -140,6 +142,7 @@ class SuperSequence:
         self.start = np.concatenate([[0], np.cumsum(self.orig_sizes)[:-1]]).astype(np.int64) if sequences else \
             np.zeros(0, np.int64)
         self._mark_last()
+        self.rng = StdRng(3019)  # utils.rs:101 StdRng::seed_from_u64(3019)
 
     def _mark_last(self):
         """utils.rs:104-115 / 168-179: last active element of each component, scanning backwards."""
@@ -184,16 +187,15 @@ class SuperSequence:
         self._mark_last()
 
     def recompute_constraints(self, proportion: float):
-        """utils.rs:168-177.  prop >= 1 activates every constrained element, prop <= 0
-        none (the reference draws ChaCha12(seed 3019) uniforms in [0,1), so prop=0 is
-        inactive except with probability 2^-53 per element).  0 < prop < 1 needs that
-        exact RNG stream: not implemented this round."""
-        if proportion >= 1.0:
-            self.active = (self.component != -1).astype(np.uint8)
-        elif proportion <= 0.0:
-            self.active[:] = 0
-        else:
-            raise NotImplementedError("0 < prop < 1 needs rand 0.8 StdRng(3019) bit-exact sampling")
+        """utils.rs:168-177: in element order, an element with a component is active iff
+        rng.gen::<f64>() <= proportion (one draw per such element, short-circuit: none for
+        free elements), then reorder().  The RNG stream persists across calls, as in
+        main.rs:107 + 113-115 (see stdrng.py for the restated StdRng)."""
+        has = self.component != -1
+        draws = self.rng.gen_f64(int(has.sum()))
+        act = np.zeros(len(self.component), np.uint8)
+        act[has] = (draws <= proportion).astype(np.uint8)
+        self.active = act
         self.reorder()
 
     def __len__(self):
@@ -283,8 +285,10 @@ class GpuSolver(Solver):
 
 def write_output(path, solver: Solver, sequence: SuperSequence, elapsed_ms: int, explored_nodes: int = 0):
     """main.rs:129-133: "objective explored\\nms\\n" then "seq state" per element."""
+    from .cli import rust_f64
+
     sol = solver.get_solution()
     with open(path, "w") as f:
-        f.write(f"{solver.get_objective()} {explored_nodes}\n{elapsed_ms}\n")
+        f.write(f"{rust_f64(solver.get_objective())} {explored_nodes}\n{elapsed_ms}\n")
         for k in range(len(sol)):
             f.write(f"{int(sequence.seq[k])} {int(sol[k])}\n")

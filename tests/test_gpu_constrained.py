@@ -77,3 +77,27 @@ def test_constrained_solver_api(gpu):
     comp = np.where(ss.active == 1, ss.component, -1).astype(np.int32)
     _, _, _, _, obj = cv.decode_constrained(h, offsets, obs, comp)
     assert s.get_objective() == pytest.approx(obj, rel=1e-12)
+
+
+def test_cli_end_to_end(gpu, tmp_path):
+    """main.rs workflow: input dir (sequences, tags, test_tags, hmm.json) -> output {prop}_0."""
+    from cviterbi import cli
+
+    pi, a, b = synth.random_hmm(6, 12, seed=2)
+    h = cv.HMM(pi, a, b.reshape(6, 4, 3))
+    h.write(tmp_path / "hmm.json")
+    rng = np.random.default_rng(2)
+    seqs, tags, test_tags = [], [], []
+    for sid in range(8):
+        T = int(rng.integers(2, 9))
+        seqs += [f"{sid} {rng.integers(0, 4)} {rng.integers(0, 3)}" for _ in range(T)]
+        tags += [f"{sid} {rng.integers(0, 6)}" for _ in range(T)]
+        test_tags += [f"{sid} {rng.integers(0, 2) if t == 0 and sid % 2 == 0 else -1}" for t in range(T)]
+    (tmp_path / "sequences").write_text("\n".join(seqs) + "\n")
+    (tmp_path / "tags").write_text("\n".join(tags) + "\n")
+    (tmp_path / "test_tags").write_text("\n".join(test_tags) + "\n")
+    assert cli.main(["-i", str(tmp_path), "-o", str(tmp_path / "out"), "-n", "6", "-b", "4", "3", "-p", "1"]) == 0
+    lines = (tmp_path / "out" / "1_0").read_text().splitlines()
+    obj, nodes = lines[0].split()
+    assert float(obj) < 0 and int(nodes) > 0 and int(lines[1]) >= 0
+    assert len(lines) == 2 + len(seqs)

@@ -61,8 +61,46 @@ def test_reorder_follows_reference_key(hmm):
     sol = np.arange(len(ss))
     per = ss.parse_solution(sol)
     assert [len(x) for x in per] == [2, 1, 3]
-    with pytest.raises(NotImplementedError):
-        ss.recompute_constraints(0.5)
+
+
+def test_stdrng_chacha_core_known_answer():
+    """The ChaCha core of the restated rand 0.8 StdRng reproduces the published all-zero
+    key / all-zero nonce ChaCha20 keystream block (djb layout, 64-bit counter)."""
+    from cviterbi.stdrng import chacha_blocks
+
+    blk = chacha_blocks([0] * 8, 0, 1, rounds=20)[0].astype("<u4").tobytes().hex()
+    assert blk == ("76b8e0ada0f13d90405d6ae55386bd28bdd219b8a08ded1aa836efcc8b770dc7"
+                   "da41597c5157488d7724e03fb8d84a376a43b8f41518a11cc387b669b2ee6586")
+
+
+def test_recompute_constraints_draws(hmm):
+    """utils.rs:168-177: one gen::<f64>() per element WITH a component, in element order,
+    stream continuing across calls; prop=1 activates all, prop=0 (practically) none."""
+    from cviterbi.stdrng import StdRng
+
+    seqs = [[(0, 0), (1, 1), (2, 0)], [(1, 1), (0, 1)], [(2, 1)]]
+    tags = [[1, None, 2], [None, 1], [2]]
+    ss = cv.SuperSequence(seqs, cv.Constraints.from_tags(tags), hmm)
+    ss.recompute_constraints(0.5)
+    ref = StdRng(3019).gen_f64(8)
+    # draws of the first call happen in the ORIGINAL element order (before reorder)
+    orig_comp = [0, -1, 1, -1, 0, 1]
+    act = [ref[i] <= 0.5 for i in range(4)]
+    k = 0
+    exp = {}
+    for e, c in enumerate(orig_comp):
+        if c != -1:
+            exp[e] = act[k]
+            k += 1
+    got = {}
+    for e in range(len(ss)):
+        seq, t = int(ss.seq[e]), int(ss.t[e])
+        oe = [0, 3, 5][seq] + t
+        if orig_comp[oe] != -1:
+            got[oe] = bool(ss.active[e])
+    assert got == exp
+    ss.recompute_constraints(1.0)
+    assert ss.active.tolist() == (ss.component != -1).astype(int).tolist()
 
 
 def test_write_output_format(tmp_path, hmm):
