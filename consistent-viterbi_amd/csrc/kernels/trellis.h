@@ -97,7 +97,7 @@ hipError_t launch_trellis_fwd(int np, const TrellisFwdArgs& fa, int64_t nseq, hi
 // MFMA-assisted forward (trellis_mfma_f32): A image in the 32x32 MFMA C/D layout; mt < 0 = default.
 hipError_t launch_trellis_mfma(int np, int mt, const TrellisFwdArgs& fa, int64_t nseq, hipStream_t stream);
 int mfma_default_mt(int np);
-hipError_t launch_trellis_bt(int np, const BacktrackArgs& ba, int64_t nseq, hipStream_t stream);
+hipError_t launch_trellis_bt(int np, const BacktrackArgs& ba, int64_t nseq, hipStream_t stream, int lds_reserve = 0);
 template <typename REAL>
 hipError_t launch_generic_fwd(const GenericFwdArgs<REAL>& fa, int64_t nseq, hipStream_t stream);
 template <typename REAL>

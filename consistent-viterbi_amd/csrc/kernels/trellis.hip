@@ -827,9 +827,21 @@ static hipError_t trellis_fwd_np(const TrellisFwdArgs& fa, int64_t nseq, hipStre
     hipLaunchKernelGGL((trellis_fwd_f32<NP, false>), dim3((unsigned)nseq), dim3(NP * 4), 0, stream, fa);
   return hipGetLastError();
 }
+// lds_reserve > 0: dynamic LDS the backtrack workgroup reserves but does not use, to cap how
+// many of them share a CU with the forward kernel of the next chunk (overlap mode): a
+// forward workgroup must always find its VGPRs free, or the pipeline stalls the forward.
 template <int NP>
-static hipError_t trellis_bt_np(const BacktrackArgs& ba, int64_t nseq, hipStream_t stream) {
-  hipLaunchKernelGGL(backtrack_f32<NP>, dim3((unsigned)((nseq + 3) / 4)), dim3(256), 0, stream, ba);
+static hipError_t trellis_bt_np(const BacktrackArgs& ba, int64_t nseq, hipStream_t stream, int lds_reserve) {
+  if (lds_reserve > 0) {
+    static bool attr = false;  // allow the large dynamic-LDS reservation
+    if (!attr) {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&backtrack_f32<NP>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      attr = true;
+    }
+  }
+  hipLaunchKernelGGL(backtrack_f32<NP>, dim3((unsigned)((nseq + 3) / 4)), dim3(256), (size_t)lds_reserve, stream,
+                     ba);
   return hipGetLastError();
 }
 
@@ -895,9 +907,9 @@ hipError_t launch_trellis_mfma(int np, int mt, const TrellisFwdArgs& fa, int64_t
   }
 }
 
-hipError_t launch_trellis_bt(int np, const BacktrackArgs& ba, int64_t nseq, hipStream_t stream) {
+hipError_t launch_trellis_bt(int np, const BacktrackArgs& ba, int64_t nseq, hipStream_t stream, int lds_reserve) {
   if (nseq <= 0) return hipSuccess;
-#define CVK_BT(NP) trellis_bt_np<NP>(ba, nseq, stream)
+#define CVK_BT(NP) trellis_bt_np<NP>(ba, nseq, stream, lds_reserve)
   CVK_NP_SWITCH(np, CVK_BT)
 #undef CVK_BT
 }
