@@ -761,24 +761,21 @@ CV_API cv_status cv_decode_batch(cv_hmm* h, int64_t nseq, const int64_t* offsets
   return decode_host_locked(h, nseq, offsets, obs, opts ? *opts : default_opts(), path_out, score_out, status_out);
 }
 
-CV_API cv_status cv_decode_constrained(cv_hmm* h, int64_t nseq, const int64_t* offsets, const int32_t* obs,
-                                       const int32_t* component, int32_t ncomp, const cv_opts* opts,
-                                       int32_t* path_out, double* score_out, uint8_t* status_out,
-                                       int32_t* comp_state_out, double* objective_out) {
-  if (!h) return set_err(CV_EINVAL, "null handle");
-  if (nseq < 0 || ncomp < 0 || (nseq > 0 && (!offsets || !obs || !component || !path_out || !score_out ||
-                                             !status_out)) || (ncomp > 0 && !comp_state_out))
-    return set_err(CV_EINVAL, "null argument");
-  std::lock_guard<std::mutex> lk(h->mu);
-  cv_status st = set_device(h);
-  if (st != CV_OK) return st;
-  cv_opts o = opts ? *opts : default_opts();
+// ---- consistency-constrained decode --------------------------------------------------------
+namespace {
+struct Con { int64_t seq, elem; int32_t comp; };
+
+// Validation + the device passes: mu[i][s] (f32, stride np) for each constrained element i.
+cv_status constrained_mu_locked(cv_hmm* h, int64_t nseq, const int64_t* offsets, const int32_t* obs,
+                                const int32_t* component, int32_t ncomp, cv_opts& o, std::vector<Con>& cons,
+                                std::vector<float>& mu) {
   if (o.dtype != CV_DTYPE_F32 || o.assoc != CV_ASSOC_VITERBI || !cvk::trellis_padded_states(h->N))
     return set_err(CV_EUNSUPPORTED, "constrained decode runs on the f32 VITERBI trellis path (N <= 256)");
   if (o.forced) return set_err(CV_EINVAL, "opts->forced is set by the constrained decode itself");
-  for (int32_t c = 0; c < ncomp; ++c) comp_state_out[c] = -1;
-  if (objective_out) *objective_out = 0.0;
+  cons.clear();
+  mu.clear();
   if (nseq == 0) return CV_OK;
+  cv_status st;
   if ((st = check_batch(h, nseq, offsets)) != CV_OK) return st;
   const int64_t base = offsets[0], total = offsets[nseq];
   for (int64_t k = base; k < total; ++k) {
@@ -787,9 +784,6 @@ CV_API cv_status cv_decode_constrained(cv_hmm* h, int64_t nseq, const int64_t* o
     if (component[k] < -1 || component[k] >= ncomp)
       return set_err(CV_EINVAL, "component[%lld] = %d out of range [-1,%d)", (long long)k, component[k], ncomp);
   }
-  // constrained elements, in sequence order: (sequence, element, component)
-  struct Con { int64_t seq, elem; int32_t comp; };
-  std::vector<Con> cons;
   for (int64_t s = 0; s < nseq; ++s) {
     int found = 0;
     for (int64_t e = offsets[s]; e < offsets[s + 1]; ++e)
@@ -804,99 +798,209 @@ CV_API cv_status cv_decode_constrained(cv_hmm* h, int64_t nseq, const int64_t* o
   if ((st = ensure_f64_tables(h)) != CV_OK) return st;
   const int np = h->np;
   const int64_t ncon = (int64_t)cons.size();
+  if (ncon == 0) return CV_OK;
   hipStream_t stream = o.stream ? (hipStream_t)o.stream : h->stream;
-  std::vector<float> mu((size_t)ncon * np);
-  if (ncon > 0) {
-    if ((st = h->st_obs.ensure((size_t)std::max<int64_t>(total, 1) * 4)) != CV_OK) return st;
-    HIP_TRY(hipMemcpyAsync(h->st_obs.as<int32_t>() + base, obs + base, (size_t)(total - base) * 4,
-                           hipMemcpyHostToDevice, stream));
-    std::vector<int64_t> rg((size_t)ncon * 4);  // prefix ranges, then suffix ranges
-    for (int64_t i = 0; i < ncon; ++i) {
-      rg[2 * i] = offsets[cons[i].seq];
-      rg[2 * i + 1] = cons[i].elem + 1;
-      rg[2 * ncon + 2 * i] = cons[i].elem + 1;
-      rg[2 * ncon + 2 * i + 1] = offsets[cons[i].seq + 1];
-    }
-    if ((st = h->cs_ranges.ensure(rg.size() * 8)) != CV_OK) return st;
-    if ((st = h->cs_delta.ensure((size_t)ncon * np * 4)) != CV_OK) return st;
-    if ((st = h->cs_g.ensure((size_t)ncon * np * 4)) != CV_OK) return st;
-    if ((st = h->cs_mu.ensure((size_t)ncon * np * 4)) != CV_OK) return st;
-    if ((st = h->st_status.ensure((size_t)std::max<int64_t>(nseq, ncon))) != CV_OK) return st;
-    HIP_TRY(hipMemcpyAsync(h->cs_ranges.p, rg.data(), rg.size() * 8, hipMemcpyHostToDevice, stream));
-    cvk::TrellisFwdArgs fa{};
-    fa.a_img = h->t_aimg.as<float>();
-    fa.pi = h->t_pi.as<float>();
-    fa.et = h->t_et.as<float>();
-    fa.obs = h->st_obs.as<int32_t>();
-    fa.status = h->st_status.as<uint8_t>();
-    fa.nobs = (int)h->V;
-    fa.ranges = h->cs_ranges.as<int64_t>();
-    fa.last_row = h->cs_delta.as<float>();
-    hipError_t err = cvk::launch_trellis_fwd(np, fa, ncon, stream);  // delta_{t_k}: forward over the prefix
-    if (err == hipSuccess) {
-      fa.a_img = h->t_aimg_T.as<float>();  // g_{t_k+1}: backward pass = same kernel on a^T, pi = 0, reversed
-      fa.pi = h->t_pi0.as<float>();
-      fa.ranges = h->cs_ranges.as<int64_t>() + 2 * ncon;
-      fa.reverse = 1;
-      fa.last_row = h->cs_g.as<float>();
-      err = cvk::launch_trellis_fwd(np, fa, ncon, stream);
-    }
-    if (err == hipSuccess) {
-      cvk::MaxMarginalArgs ma{};
-      ma.delta = h->cs_delta.as<float>();
-      ma.g = h->cs_g.as<float>();
-      ma.ranges_suffix = h->cs_ranges.as<int64_t>() + 2 * ncon;
-      ma.at = h->t_at.as<float>();
-      ma.mu = h->cs_mu.as<float>();
-      err = cvk::launch_max_marginal(np, ma, ncon, stream);
-    }
-    if (err != hipSuccess) return set_err(CV_EDEVICE, "max-marginal launch failed: %s", hipGetErrorString(err));
-    HIP_TRY(hipMemcpyAsync(mu.data(), h->cs_mu.p, mu.size() * 4, hipMemcpyDeviceToHost, stream));
-    HIP_TRY(hipStreamSynchronize(stream));
-  }
-  // exact per-component sums of the max-marginals, in units of 2^-64 (order independent)
-  const int N = h->N;
-  std::vector<__int128> acc((size_t)ncomp * N, 0);
-  std::vector<uint8_t> dead((size_t)ncomp * N, 0), used((size_t)ncomp, 0);
-  const double scale = 18446744073709551616.0;  // 2^64
+  mu.resize((size_t)ncon * np);
+  if ((st = h->st_obs.ensure((size_t)std::max<int64_t>(total, 1) * 4)) != CV_OK) return st;
+  HIP_TRY(hipMemcpyAsync(h->st_obs.as<int32_t>() + base, obs + base, (size_t)(total - base) * 4,
+                         hipMemcpyHostToDevice, stream));
+  std::vector<int64_t> rg((size_t)ncon * 4);  // prefix ranges, then suffix ranges
   for (int64_t i = 0; i < ncon; ++i) {
-    const int32_t c = cons[i].comp;
-    used[c] = 1;
+    rg[2 * i] = offsets[cons[i].seq];
+    rg[2 * i + 1] = cons[i].elem + 1;
+    rg[2 * ncon + 2 * i] = cons[i].elem + 1;
+    rg[2 * ncon + 2 * i + 1] = offsets[cons[i].seq + 1];
+  }
+  if ((st = h->cs_ranges.ensure(rg.size() * 8)) != CV_OK) return st;
+  if ((st = h->cs_delta.ensure((size_t)ncon * np * 4)) != CV_OK) return st;
+  if ((st = h->cs_g.ensure((size_t)ncon * np * 4)) != CV_OK) return st;
+  if ((st = h->cs_mu.ensure((size_t)ncon * np * 4)) != CV_OK) return st;
+  if ((st = h->st_status.ensure((size_t)std::max<int64_t>(nseq, ncon))) != CV_OK) return st;
+  HIP_TRY(hipMemcpyAsync(h->cs_ranges.p, rg.data(), rg.size() * 8, hipMemcpyHostToDevice, stream));
+  cvk::TrellisFwdArgs fa{};
+  fa.a_img = h->t_aimg.as<float>();
+  fa.pi = h->t_pi.as<float>();
+  fa.et = h->t_et.as<float>();
+  fa.obs = h->st_obs.as<int32_t>();
+  fa.status = h->st_status.as<uint8_t>();
+  fa.nobs = (int)h->V;
+  fa.ranges = h->cs_ranges.as<int64_t>();
+  fa.last_row = h->cs_delta.as<float>();
+  hipError_t err = cvk::launch_trellis_fwd(np, fa, ncon, stream);  // delta_{t_k}: forward over the prefix
+  if (err == hipSuccess) {
+    fa.a_img = h->t_aimg_T.as<float>();  // g_{t_k+1}: backward pass = same kernel on a^T, pi = 0, reversed
+    fa.pi = h->t_pi0.as<float>();
+    fa.ranges = h->cs_ranges.as<int64_t>() + 2 * ncon;
+    fa.reverse = 1;
+    fa.last_row = h->cs_g.as<float>();
+    err = cvk::launch_trellis_fwd(np, fa, ncon, stream);
+  }
+  if (err == hipSuccess) {
+    cvk::MaxMarginalArgs ma{};
+    ma.delta = h->cs_delta.as<float>();
+    ma.g = h->cs_g.as<float>();
+    ma.ranges_suffix = h->cs_ranges.as<int64_t>() + 2 * ncon;
+    ma.at = h->t_at.as<float>();
+    ma.mu = h->cs_mu.as<float>();
+    err = cvk::launch_max_marginal(np, ma, ncon, stream);
+  }
+  if (err != hipSuccess) return set_err(CV_EDEVICE, "max-marginal launch failed: %s", hipGetErrorString(err));
+  HIP_TRY(hipMemcpyAsync(mu.data(), h->cs_mu.p, mu.size() * 4, hipMemcpyDeviceToHost, stream));
+  HIP_TRY(hipStreamSynchronize(stream));
+  return CV_OK;
+}
+
+// Partials layout per component c (stride CV_PARTIAL_STRIDE(N) int64 words):
+//   [4N] base-2^32 limbs of the exact sum in units of 2^-64 (limb 3 signed), state-major
+//   [N]  count of -inf max-marginals per state, [1] count of constrained elements.
+// Every word is a plain sum over elements, so partials of disjoint shards add.
+void accumulate_partials(const std::vector<Con>& cons, const std::vector<float>& mu, int N, int np,
+                         int64_t* part) {
+  const int64_t stride = 5 * (int64_t)N + 1;
+  const double scale = 18446744073709551616.0;  // 2^64
+  for (size_t i = 0; i < cons.size(); ++i) {
+    int64_t* pc = part + (int64_t)cons[i].comp * stride;
+    pc[5 * N] += 1;
     for (int s = 0; s < N; ++s) {
-      const float m = mu[(size_t)i * np + s];
+      const float m = mu[i * np + s];
       if (!(m > -INFINITY)) {
-        dead[(size_t)c * N + s] = 1;
+        pc[4 * N + s] += 1;
         continue;
       }
-      acc[(size_t)c * N + s] += (__int128)std::nearbyint((double)m * scale);
+      const __int128 v = (__int128)std::nearbyint((double)m * scale);  // |m| < 2^24 -> < 2^88, exact
+      const unsigned __int128 u = (unsigned __int128)v;
+      pc[4 * s + 0] += (int64_t)(uint32_t)(u);
+      pc[4 * s + 1] += (int64_t)(uint32_t)(u >> 32);
+      pc[4 * s + 2] += (int64_t)(uint32_t)(u >> 64);
+      pc[4 * s + 3] += (int64_t)(v >> 96);  // arithmetic shift: signed top limb
     }
   }
-  uint64_t explored = 0;
+}
+
+void select_states(int32_t ncomp, int N, const int64_t* part, int32_t* comp_state_out, uint64_t* explored) {
+  const int64_t stride = 5 * (int64_t)N + 1;
+  uint64_t ex = 0;
   for (int32_t c = 0; c < ncomp; ++c) {
-    if (!used[c]) continue;
+    const int64_t* pc = part + (int64_t)c * stride;
+    comp_state_out[c] = -1;
+    if (pc[5 * N] == 0) continue;
+    ex += (uint64_t)N;
     int best = -1;
+    __int128 bv = 0;
     for (int s = 0; s < N; ++s) {
-      if (dead[(size_t)c * N + s]) continue;
-      if (best < 0 || acc[(size_t)c * N + s] > acc[(size_t)c * N + best]) best = s;
+      if (pc[4 * N + s] != 0) continue;
+      const __int128 v = (__int128)pc[4 * s] + ((__int128)pc[4 * s + 1] << 32) + ((__int128)pc[4 * s + 2] << 64) +
+                         ((__int128)pc[4 * s + 3] << 96);
+      if (best < 0 || v > bv) best = s, bv = v;
     }
     comp_state_out[c] = best;
-    explored += (uint64_t)N;
   }
-  h->last_explored = explored;
-  // final decode with every constrained element forced to its component's state
+  if (explored) *explored = ex;
+}
+// Final decode: every constrained element forced to its component's state; sequences whose
+// component has no feasible state are infeasible.  objective = sum of the f64 scores.
+cv_status forced_decode_locked(cv_hmm* h, int64_t nseq, const int64_t* offsets, const int32_t* obs,
+                               const int32_t* component, const int32_t* comp_state, cv_opts o, int32_t* path_out,
+                               double* score_out, uint8_t* status_out, double* objective_out) {
+  const int64_t base = offsets[0], total = offsets[nseq];
   std::vector<int32_t> forced((size_t)total, -1);
-  for (const auto& x : cons) forced[x.elem] = comp_state_out[x.comp] >= 0 ? comp_state_out[x.comp] : 0;
+  for (int64_t e = base; e < total; ++e)
+    if (component[e] >= 0) forced[e] = comp_state[component[e]] >= 0 ? comp_state[component[e]] : 0;
   o.forced = forced.data();
-  if ((st = decode_host_locked(h, nseq, offsets, obs, o, path_out, score_out, status_out)) != CV_OK) return st;
+  cv_status st = decode_host_locked(h, nseq, offsets, obs, o, path_out, score_out, status_out);
+  if (st != CV_OK) return st;
   double obj = 0.0;
-  for (const auto& x : cons)
-    if (comp_state_out[x.comp] < 0) {
-      status_out[x.seq] = CV_SEQ_INFEASIBLE;
-      score_out[x.seq] = -INFINITY;
-    }
-  for (int64_t s = 0; s < nseq; ++s) obj += status_out[s] == CV_SEQ_INFEASIBLE ? -INFINITY : score_out[s];
+  for (int64_t s = 0; s < nseq; ++s) {
+    for (int64_t e = offsets[s]; e < offsets[s + 1]; ++e)
+      if (component[e] >= 0 && comp_state[component[e]] < 0) {
+        status_out[s] = CV_SEQ_INFEASIBLE;
+        score_out[s] = -INFINITY;
+      }
+    obj += status_out[s] == CV_SEQ_INFEASIBLE ? -INFINITY : score_out[s];
+  }
   if (objective_out) *objective_out = obj;
   return CV_OK;
+}
+}  // namespace
+
+CV_API cv_status cv_constrained_partials(cv_hmm* h, int64_t nseq, const int64_t* offsets, const int32_t* obs,
+                                         const int32_t* component, int32_t ncomp, const cv_opts* opts,
+                                         int64_t* partials_out) {
+  if (!h) return set_err(CV_EINVAL, "null handle");
+  if (nseq < 0 || ncomp < 0 || (nseq > 0 && (!offsets || !obs || !component)) || (ncomp > 0 && !partials_out))
+    return set_err(CV_EINVAL, "null argument");
+  std::lock_guard<std::mutex> lk(h->mu);
+  cv_status st = set_device(h);
+  if (st != CV_OK) return st;
+  cv_opts o = opts ? *opts : default_opts();
+  std::vector<Con> cons;
+  std::vector<float> mu;
+  if ((st = constrained_mu_locked(h, nseq, offsets, obs, component, ncomp, o, cons, mu)) != CV_OK) return st;
+  std::memset(partials_out, 0, (size_t)ncomp * (5 * (size_t)h->N + 1) * 8);
+  accumulate_partials(cons, mu, h->N, h->np, partials_out);
+  return CV_OK;
+}
+
+CV_API cv_status cv_constrained_select(int32_t nstates, int32_t ncomp, const int64_t* partials,
+                                       int32_t* comp_state_out, uint64_t* explored_out) {
+  if (nstates <= 0 || ncomp < 0 || (ncomp > 0 && (!partials || !comp_state_out)))
+    return set_err(CV_EINVAL, "bad argument");
+  select_states(ncomp, nstates, partials, comp_state_out, explored_out);
+  return CV_OK;
+}
+
+CV_API cv_status cv_decode_constrained(cv_hmm* h, int64_t nseq, const int64_t* offsets, const int32_t* obs,
+                                       const int32_t* component, int32_t ncomp, const cv_opts* opts,
+                                       int32_t* path_out, double* score_out, uint8_t* status_out,
+                                       int32_t* comp_state_out, double* objective_out) {
+  if (!h) return set_err(CV_EINVAL, "null handle");
+  if (nseq < 0 || ncomp < 0 || (nseq > 0 && (!offsets || !obs || !component || !path_out || !score_out ||
+                                             !status_out)) || (ncomp > 0 && !comp_state_out))
+    return set_err(CV_EINVAL, "null argument");
+  std::lock_guard<std::mutex> lk(h->mu);
+  cv_status st = set_device(h);
+  if (st != CV_OK) return st;
+  cv_opts o = opts ? *opts : default_opts();
+  for (int32_t c = 0; c < ncomp; ++c) comp_state_out[c] = -1;
+  if (objective_out) *objective_out = 0.0;
+  std::vector<Con> cons;
+  std::vector<float> mu;
+  if ((st = constrained_mu_locked(h, nseq, offsets, obs, component, ncomp, o, cons, mu)) != CV_OK) return st;
+  if (nseq == 0) return CV_OK;
+  // exact per-component sums of the max-marginals (order and shard independent)
+  std::vector<int64_t> part((size_t)ncomp * (5 * (size_t)h->N + 1), 0);
+  accumulate_partials(cons, mu, h->N, h->np, part.data());
+  uint64_t explored = 0;
+  select_states(ncomp, h->N, part.data(), comp_state_out, &explored);
+  h->last_explored = explored;
+  return forced_decode_locked(h, nseq, offsets, obs, component, comp_state_out, o, path_out, score_out, status_out,
+                              objective_out);
+}
+
+CV_API cv_status cv_decode_forced_components(cv_hmm* h, int64_t nseq, const int64_t* offsets, const int32_t* obs,
+                                             const int32_t* component, int32_t ncomp, const int32_t* comp_state,
+                                             const cv_opts* opts, int32_t* path_out, double* score_out,
+                                             uint8_t* status_out, double* objective_out) {
+  if (!h) return set_err(CV_EINVAL, "null handle");
+  if (nseq < 0 || ncomp < 0 || (nseq > 0 && (!offsets || !obs || !component || !path_out || !score_out ||
+                                             !status_out)) || (ncomp > 0 && !comp_state))
+    return set_err(CV_EINVAL, "null argument");
+  std::lock_guard<std::mutex> lk(h->mu);
+  cv_status st = set_device(h);
+  if (st != CV_OK) return st;
+  cv_opts o = opts ? *opts : default_opts();
+  if (o.forced) return set_err(CV_EINVAL, "opts->forced is derived from component/comp_state");
+  if (objective_out) *objective_out = 0.0;
+  if (nseq == 0) return CV_OK;
+  if ((st = check_batch(h, nseq, offsets)) != CV_OK) return st;
+  for (int64_t k = offsets[0]; k < offsets[nseq]; ++k)
+    if (component[k] < -1 || component[k] >= ncomp)
+      return set_err(CV_EINVAL, "component[%lld] = %d out of range [-1,%d)", (long long)k, component[k], ncomp);
+  for (int32_t c = 0; c < ncomp; ++c)
+    if (comp_state[c] < -1 || comp_state[c] >= h->N)
+      return set_err(CV_EINVAL, "comp_state[%d] = %d out of range [-1,%lld)", c, comp_state[c], (long long)h->N);
+  return forced_decode_locked(h, nseq, offsets, obs, component, comp_state, o, path_out, score_out, status_out,
+                              objective_out);
 }
 
 CV_API cv_status cv_last_timing(cv_hmm* h, cv_timing* out) {

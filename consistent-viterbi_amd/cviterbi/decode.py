@@ -77,6 +77,53 @@ def decode_constrained(hmm: HMM, offsets, obs, component, ncomp=None, rescore_f6
     return path, score, status, states[:ncomp], obj.value
 
 
+def partial_stride(nstates: int) -> int:
+    """CV_PARTIAL_STRIDE: int64 words per component in the constrained partials."""
+    return 5 * int(nstates) + 1
+
+
+def constrained_partials(hmm: HMM, offsets, obs, component, ncomp):
+    """cv_constrained_partials: this shard's exact per-component sums, int64[ncomp, 5N+1];
+    partials of disjoint shards add (one all-reduce SUM)."""
+    offsets = np.ascontiguousarray(offsets, np.int64)
+    obs = np.ascontiguousarray(obs, np.int32)
+    component = np.ascontiguousarray(component, np.int32)
+    part = np.zeros((max(int(ncomp), 1), partial_stride(hmm.nstates())), np.int64)
+    o = make_opts("f32", "viterbi", "auto", True)
+    L.check(L.lib().cv_constrained_partials(hmm.handle, offsets.shape[0] - 1, _p(offsets), _p(obs), _p(component),
+                                            int(ncomp), ctypes.byref(o), _p(part)))
+    return part[:ncomp]
+
+
+def constrained_select(nstates: int, partials):
+    """cv_constrained_select (host only): (comp_state[ncomp], explored) from reduced partials."""
+    partials = np.ascontiguousarray(partials, np.int64)
+    ncomp = partials.shape[0]
+    states = np.full(max(ncomp, 1), -1, np.int32)
+    ex = ctypes.c_uint64()
+    L.check(L.lib().cv_constrained_select(int(nstates), ncomp, _p(partials), _p(states), ctypes.byref(ex)))
+    return states[:ncomp], ex.value
+
+
+def decode_forced_components(hmm: HMM, offsets, obs, component, comp_state, rescore_f64=True):
+    """cv_decode_forced_components: final decode of a shard given the component states.
+    Returns (path, score, status, objective)."""
+    offsets = np.ascontiguousarray(offsets, np.int64)
+    obs = np.ascontiguousarray(obs, np.int32)
+    component = np.ascontiguousarray(component, np.int32)
+    cs = np.ascontiguousarray(comp_state, np.int32)
+    nseq = offsets.shape[0] - 1
+    path = np.zeros(int(offsets[-1]), np.int32)
+    score = np.zeros(nseq, np.float64)
+    status = np.zeros(nseq, np.uint8)
+    obj = ctypes.c_double()
+    o = make_opts("f32", "viterbi", "auto", rescore_f64)
+    L.check(L.lib().cv_decode_forced_components(hmm.handle, nseq, _p(offsets), _p(obs), _p(component), len(cs),
+                                                _p(cs) if len(cs) else None, ctypes.byref(o), _p(path), _p(score),
+                                                _p(status), ctypes.byref(obj)))
+    return path, score, status, obj.value
+
+
 def decode_batch_device(hmm: HMM, offsets_dev, obs_dev, path_dev, score_dev, status_dev, offsets_host=None,
                         dtype="f32", assoc="viterbi", kernel="auto", rescore_f64=True, stream=None,
                         workspace_bytes=0, variant=None, mfma_tiles=None, serial=False):

@@ -4,6 +4,12 @@ The unconstrained decode is independent per sequence, so the batch is split into
 contiguous shards of ceil(B/world) sequences, one per rank (one process per GPU); the
 HMM is replicated.  The only collective is the gather of paths, scores and statuses to
 rank 0 -- RCCL over xGMI with the "nccl" backend on the GPU node, gloo in CPU tests.
+
+The consistency-constrained decode (config 5) has one real exchange step: the per-component
+sums of max-marginals.  Each rank reduces its shard to exact integer partials (int64 words,
+include/cviterbi.h CV_PARTIAL_STRIDE), one all-reduce SUM combines them -- bit-identical to
+the single-process choice whatever the shard boundaries -- and every rank selects the same
+component states and decodes its own shard.
 """
 from __future__ import annotations
 
@@ -47,3 +53,53 @@ def assemble(parts, lengths):
     import torch
 
     return torch.cat([p[:n] for p, n in zip(parts, lengths)])
+
+
+def allreduce_partials(partials, dist, device=None):
+    """All-reduce SUM of int64 constrained partials ([ncomp, 5N+1]); returns numpy int64.
+    Integer sums: exact and independent of reduction order."""
+    import torch
+
+    t = torch.from_numpy(np.ascontiguousarray(partials, np.int64)).to(device or "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return t.cpu().numpy()
+
+
+def constrained_decode_sharded(hmm, offsets, obs, component, ncomp, dist, device=None):
+    """Config 5 across ranks: shard sequences, exact partials, one all-reduce, select,
+    per-shard forced decode, gather to rank 0.  Returns (path, score, status, comp_state,
+    objective) on rank 0 and (None, None, None, comp_state, None) elsewhere."""
+    import torch
+
+    from .decode import constrained_partials, constrained_select, decode_forced_components
+
+    offsets = np.asarray(offsets, np.int64)
+    world, rank = dist.get_world_size(), dist.get_rank()
+    B = len(offsets) - 1
+    s0, s1, per = shard_range(B, world, rank)
+    lo, hi = int(offsets[s0]), int(offsets[s1])
+    off = shard_offsets(offsets, s0, s1)
+    ob = np.asarray(obs, np.int32)[lo:hi]
+    cp = np.asarray(component, np.int32)[lo:hi]
+    part = constrained_partials(hmm, off, ob, cp, ncomp)
+    part = allreduce_partials(part, dist, device)
+    states, _ = constrained_select(hmm.nstates(), part)
+    path, score, status, _ = decode_forced_components(hmm, off, ob, cp, states)
+    # gather: sequence counts and element counts differ per rank -> pad to capacities
+    counts = torch.tensor([s1 - s0, hi - lo], dtype=torch.int64, device=device or "cpu")
+    allc = [torch.zeros_like(counts) for _ in range(world)]
+    dist.all_gather(allc, counts)
+    ecap = max(int(c[1]) for c in allc)
+    dev = device or "cpu"
+    g = gather_to_root([torch.from_numpy(path).to(dev), torch.from_numpy(score).to(dev),
+                        torch.from_numpy(status.astype(np.int32)).to(dev)], [ecap, per, per], dist)
+    if rank != 0:
+        return None, None, None, states, None
+    ns = [int(c[0]) for c in allc]
+    ne = [int(c[1]) for c in allc]
+    path = assemble(g[0], ne).cpu().numpy()
+    score = assemble(g[1], ns).cpu().numpy()
+    status = assemble(g[2], ns).cpu().numpy().astype(np.uint8)
+    # sequential sum in sequence order, as cv_decode_constrained does (CV_SEQ_INFEASIBLE = 1)
+    objective = float(np.cumsum(np.where(status == 1, -np.inf, score))[-1]) if B else 0.0
+    return path, score, status, states, objective

@@ -184,6 +184,26 @@ CV_API cv_status cv_decode_constrained(cv_hmm* h, int64_t nseq, const int64_t* o
                                        const int32_t* component, int32_t ncomp, const cv_opts* opts,
                                        int32_t* path_out, double* score_out, uint8_t* status_out,
                                        int32_t* comp_state_out, double* objective_out);
+/* The same decode split at its one exchange step, for a batch sharded over processes/GPUs:
+ * 1. cv_constrained_partials: this shard's exact per-component sums as int64 words that
+ *    ADD across shards (one all-reduce SUM of ncomp * CV_PARTIAL_STRIDE(N) int64 words);
+ *    per component: 4N base-2^32 limbs (state-major) of the sum in units of 2^-64, N counts
+ *    of -inf max-marginals, 1 count of constrained elements.  Zeroes partials_out first.
+ * 2. cv_constrained_select (host only): comp_state_out[c] = first argmax over feasible states
+ *    of the reduced partials (-1: no element / no feasible state); explored = N per used one.
+ * 3. cv_decode_forced_components: the shard's final decode with every constrained element
+ *    forced to comp_state[component[e]]; objective_out = the shard's sum of scores.
+ * cv_decode_constrained == 1 + 2 + 3 on one process. */
+#define CV_PARTIAL_STRIDE(nstates) (5 * (int64_t)(nstates) + 1)
+CV_API cv_status cv_constrained_partials(cv_hmm* h, int64_t nseq, const int64_t* offsets, const int32_t* obs,
+                                         const int32_t* component, int32_t ncomp, const cv_opts* opts,
+                                         int64_t* partials_out);
+CV_API cv_status cv_constrained_select(int32_t nstates, int32_t ncomp, const int64_t* partials,
+                                       int32_t* comp_state_out, uint64_t* explored_out);
+CV_API cv_status cv_decode_forced_components(cv_hmm* h, int64_t nseq, const int64_t* offsets, const int32_t* obs,
+                                             const int32_t* component, int32_t ncomp, const int32_t* comp_state,
+                                             const cv_opts* opts, int32_t* path_out, double* score_out,
+                                             uint8_t* status_out, double* objective_out);
 /* viterbi::decode (viterbi.rs:5): one sequence, reference decode() semantics (row 0 = 0.0,
  * f64), path only. */
 CV_API cv_status cv_viterbi_decode(cv_hmm* h, int64_t T, const int32_t* obs, int32_t* path_out);

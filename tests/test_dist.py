@@ -98,3 +98,123 @@ def test_shard_range_covers_batch():
                 assert 0 <= s1 - s0 <= per
                 seen.extend(range(s0, s1))
             assert seen == list(range(total))
+
+
+# ---- config 5 exchange step: exact partials, all-reduce SUM, select -----------------------
+NC = 4
+
+
+def _pack_partials(mu_rows, comps, n, ncomp):
+    """Test-side packing of include/cviterbi.h's partial layout from oracle max-marginals."""
+    part = np.zeros((ncomp, 5 * n + 1), np.int64)
+    M = (1 << 32) - 1
+    for mu, c in zip(mu_rows, comps):
+        part[c, 5 * n] += 1
+        for s in range(n):
+            if not np.isfinite(mu[s]):
+                part[c, 4 * n + s] += 1
+                continue
+            import np_oracle as NO
+
+            v = NO.exact_units(float(mu[s]))
+            part[c, 4 * s:4 * s + 4] += [v & M, (v >> 32) & M, (v >> 64) & M, v >> 96]
+    return part
+
+
+def _constrained_data():
+    sys.path.insert(0, os.path.join(ROOT, "consistent-viterbi_amd"))
+    from cviterbi import synth
+
+    pi, a, b = synth.random_hmm(N, V, seed=11, zero_frac=0.2)
+    rng = np.random.default_rng(11)
+    lengths = rng.integers(1, T_MAX, size=B)
+    off = synth.offsets_from_lengths(lengths)
+    obs = rng.integers(0, V, size=int(off[-1])).astype(np.int32)
+    comp = np.full(len(obs), -1, np.int32)
+    for k in range(B):
+        if rng.random() < 0.8:
+            comp[off[k] + rng.integers(0, lengths[k])] = rng.integers(0, NC)
+    return pi, a, b, off, obs, comp
+
+
+def _shard_mu(pi, a, b, off, obs, comp, s0, s1):
+    import c_oracle
+
+    rows, comps = [], []
+    for k in range(s0, s1):
+        lo, hi = off[k], off[k + 1]
+        pos = np.nonzero(comp[lo:hi] >= 0)[0]
+        for t in pos:
+            rows.append(c_oracle.max_marginal(pi, a, b, obs[lo:hi], int(t), np.float32))
+            comps.append(int(comp[lo + t]))
+    return rows, comps
+
+
+def _partials_worker(rank, world, port, q):
+    for p in (os.path.join(ROOT, "consistent-viterbi_amd"), os.path.join(ROOT, "oracle")):
+        sys.path.insert(0, p)
+    import torch.distributed as dist
+
+    from cviterbi.decode import constrained_select
+    from cviterbi import dist as cvd
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    pi, a, b, off, obs, comp = _constrained_data()
+    s0, s1, _ = cvd.shard_range(B, world, rank)
+    part = _pack_partials(*_shard_mu(pi, a, b, off, obs, comp, s0, s1), N, NC)
+    red = cvd.allreduce_partials(part, dist)
+    states, explored = constrained_select(N, red)  # host-only C-ABI call
+    q.put((rank, states.tolist(), explored))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_constrained_partials_allreduce_matches_spec(world):
+    """Shard partials + all-reduce + cv_constrained_select == the single-process spec's
+    component states (np_oracle.constrained_decode, exact 2^-64 sums) on every rank."""
+    import c_oracle
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_partials_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    pi, a, b, off, obs, comp = _constrained_data()
+    spec, _ = c_oracle.constrained_forced(pi, a, b, off, obs, comp, np.float32)
+    want = [spec.get(c, -1) for c in range(NC)]
+    for _, states, explored in res:
+        assert states == want
+        assert explored == N * sum(1 for c in range(NC) if (comp == c).any())
+
+
+def test_constrained_select_limb_carries():
+    """cv_constrained_select reconstructs sums whose limbs carry (values near +-2^88)."""
+    sys.path.insert(0, os.path.join(ROOT, "consistent-viterbi_amd"))
+    from cviterbi.decode import constrained_select
+
+    M = (1 << 32) - 1
+    rng = np.random.default_rng(0)
+    n, ncomp = 5, 3
+    part = np.zeros((ncomp, 5 * n + 1), np.int64)
+    exact = np.zeros((ncomp, n), object)
+    for c in range(ncomp):
+        part[c, 5 * n] = 1
+        for s in range(n):
+            for _ in range(50):
+                v = int(rng.integers(-(1 << 62), 1 << 62)) * int(rng.integers(1, 1 << 24)) - (1 << 80) * (c % 2)
+                exact[c, s] += v
+                part[c, 4 * s:4 * s + 4] += [v & M, (v >> 32) & M, (v >> 64) & M, v >> 96]
+    part[1, 4 * n + 2] = 1  # state 2 of component 1 infeasible
+    states, ex = constrained_select(n, part)
+    for c in range(ncomp):
+        cand = [s for s in range(n) if not (c == 1 and s == 2)]
+        best = max(cand, key=lambda s: (exact[c, s], -s))
+        assert states[c] == best
+    assert ex == n * ncomp

@@ -101,3 +101,31 @@ def test_cli_end_to_end(gpu, tmp_path):
     obj, nodes = lines[0].split()
     assert float(obj) < 0 and int(nodes) > 0 and int(lines[1]) >= 0
     assert len(lines) == 2 + len(seqs)
+
+
+@pytest.mark.parametrize("nshards", [2, 5])
+def test_constrained_sharded_equals_single(gpu, nshards):
+    """The multi-GPU split (cv_constrained_partials per shard, integer SUM, select, per-shard
+    cv_decode_forced_components) reproduces cv_decode_constrained bit for bit, whatever the
+    shard boundaries (the exchange step of cviterbi.dist.constrained_decode_sharded)."""
+    from cviterbi import dist as cvdist
+
+    c = synth.config("c5", nseq=60)
+    h = cv.HMM(c["pi"], c["a"], c["b"])
+    off, obs, comp = c["offsets"], c["obs"], c["component"]
+    ncomp = int(comp.max()) + 1
+    path, score, status, states, obj = cv.decode_constrained(h, off, obs, comp, ncomp)
+    B = len(off) - 1
+    part = 0
+    shards = [cvdist.shard_range(B, nshards, r)[:2] for r in range(nshards)]
+    for s0, s1 in shards:
+        lo, hi = off[s0], off[s1]
+        part = part + cv.constrained_partials(h, cvdist.shard_offsets(off, s0, s1), obs[lo:hi], comp[lo:hi], ncomp)
+    got_states, explored = cv.constrained_select(h.nstates(), part)
+    assert np.array_equal(got_states, states)
+    assert explored == h.nstates() * len(set(comp[comp >= 0].tolist()))
+    for s0, s1 in shards:
+        lo, hi = off[s0], off[s1]
+        p, s, st, _ = cv.decode_forced_components(h, cvdist.shard_offsets(off, s0, s1), obs[lo:hi], comp[lo:hi],
+                                                  got_states)
+        assert np.array_equal(p, path[lo:hi]) and np.array_equal(s, score[s0:s1]) and np.array_equal(st, status[s0:s1])
