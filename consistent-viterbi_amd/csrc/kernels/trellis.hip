@@ -53,14 +53,18 @@ __device__ __forceinline__ float octet_max(float x) {
   return x;
 }
 
-// max of x over lane pairs (l, l^16) or (l, l^32).  permlane*_swap(u, u) may be lowered
-// with ONE register as both operands, which makes it a plain swap, so the lane's own
-// value is folded in explicitly: max3(x, r0, r1) is right for either lowering.
+// max of x over lane pairs (l, l^16) or (l, l^32).  Inline asm: hipcc (ROCm 7.2) folds
+// __builtin_amdgcn_permlane*_swap(x, x) to its first result only, which is right in half
+// of the lanes (tools/debug/reduce_check.hip measured it on the device).
 __device__ __forceinline__ float swap_max(float x, bool sixteen) {
-  const unsigned u = __builtin_bit_cast(unsigned, x);
-  const auto r = sixteen ? __builtin_amdgcn_permlane16_swap(u, u, false, false)
-                         : __builtin_amdgcn_permlane32_swap(u, u, false, false);
-  return fmaxf(x, fmaxf(__builtin_bit_cast(float, r[0]), __builtin_bit_cast(float, r[1])));
+  // a = vdst, b = src, both = x.  After the swap a holds the low half's values (row pair)
+  // in both halves and b the high half's, so max(a, b) = max(x[l], x[l^16|32]) in every lane.
+  float a = x, b = x;
+  if (sixteen)
+    asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+  else
+    asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+  return fmaxf(a, b);
 }
 
 // max over all 64 lanes, result in every lane: DPP inside rows of 16, then permlane swaps.

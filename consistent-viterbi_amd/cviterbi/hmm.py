@@ -53,8 +53,11 @@ class HMM:
 
     def __del__(self):
         h = getattr(self, "_h", None)
-        if h:
-            L.lib().cv_hmm_destroy(h)
+        if h and L is not None and L.lib is not None:  # module globals may be gone at interpreter exit
+            try:
+                L.lib().cv_hmm_destroy(h)
+            except TypeError:
+                pass
             self._h = None
 
     @property

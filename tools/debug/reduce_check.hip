@@ -18,10 +18,14 @@ __device__ __forceinline__ float octet_max(float x) {
   return x;
 }
 __device__ __forceinline__ float swap_max(float x, bool sixteen) {
-  const unsigned u = __builtin_bit_cast(unsigned, x);
-  const auto r = sixteen ? __builtin_amdgcn_permlane16_swap(u, u, false, false)
-                         : __builtin_amdgcn_permlane32_swap(u, u, false, false);
-  return fmaxf(x, fmaxf(__builtin_bit_cast(float, r[0]), __builtin_bit_cast(float, r[1])));
+  // a = vdst, b = src, both = x.  After the swap a holds the low half's values (row pair)
+  // in both halves and b the high half's, so max(a, b) = max(x[l], x[l^16|32]) in every lane.
+  float a = x, b = x;
+  if (sixteen)
+    asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+  else
+    asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+  return fmaxf(a, b);
 }
 __device__ __forceinline__ float swap_pair_only(float x, bool sixteen) {  // the round-1 form
   const unsigned u = __builtin_bit_cast(unsigned, x);
