@@ -342,8 +342,9 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
   if (need_f64 && (st = ensure_f64_tables(h)) != CV_OK) return st;
   if (!use_trellis && o.dtype == CV_DTYPE_F32 && (st = ensure_g32_tables(h)) != CV_OK) return st;
 
-  // trellis variant: MFMA-assisted unless asked for the all-VALU kernel (or NP = 32)
-  const bool use_mfma = use_trellis && !(o.flags & CV_FLAG_VALU_TRELLIS) && h->np >= 64 && !o.forced;
+  // trellis variant: all-VALU unless the (slower, experimental) MFMA-assisted one is asked for
+  const bool want_mfma = (o.flags & CV_FLAG_MFMA_TRELLIS) || ((o.flags >> 8) & 0xFF);
+  const bool use_mfma = use_trellis && want_mfma && h->np >= 64 && !o.forced;
   int mt = -1;
   if (use_mfma) {
     const int req = (int)((o.flags >> 8) & 0xFF) - 1;

@@ -19,7 +19,7 @@ SEQ_OK, SEQ_INFEASIBLE, SEQ_EMPTY, SEQ_BADOBS = 0, 1, 2, 3
 DTYPE_F32, DTYPE_F64 = 0, 1
 ASSOC_VITERBI, ASSOC_CP, ASSOC_DP, ASSOC_DECODE = 0, 1, 2, 3
 KERNEL_AUTO, KERNEL_TRELLIS, KERNEL_GENERIC = 0, 1, 2
-FLAG_VALU_TRELLIS = 0x1
+FLAG_MFMA_TRELLIS = 0x1
 FLAG_SERIAL = 0x2
 
 

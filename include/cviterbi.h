@@ -55,15 +55,17 @@ enum { CV_DTYPE_F32 = 0, CV_DTYPE_F64 = 1 };
  *  DECODE   VITERBI with row 0 = 0.0                viterbi::decode viterbi.rs:5-32 */
 enum { CV_ASSOC_VITERBI = 0, CV_ASSOC_CP = 1, CV_ASSOC_DP = 2, CV_ASSOC_DECODE = 3 };
 
-/* kernel choice: AUTO picks TRELLIS (register-resident A, f32, VITERBI, N <= 256; the
- * MFMA-assisted variant for N > 32) when it applies, else GENERIC (inline argmax, f32/f64,
- * any association, N <= 8192 f32 / 4096 f64). */
+/* kernel choice: AUTO picks TRELLIS (register-resident A, f32, VITERBI, N <= 256) when it
+ * applies, else GENERIC (inline argmax, f32/f64, any association, N <= 8192 f32 / 4096 f64). */
 enum { CV_KERNEL_AUTO = 0, CV_KERNEL_TRELLIS = 1, CV_KERNEL_GENERIC = 2 };
 
 /* cv_opts.flags */
-#define CV_FLAG_VALU_TRELLIS 0x1u /* all-VALU trellis kernel instead of the MFMA-assisted one */
+/* MFMA-assisted trellis (64 <= N <= 256) instead of the all-VALU one.  Bit-identical, but
+ * SLOWER on gfx950: f32 MFMA does not co-execute with VALU work on a SIMD
+ * (profiles/r01_mfma_overlap.txt), so it is kept as an experiment only. */
+#define CV_FLAG_MFMA_TRELLIS 0x1u
 #define CV_FLAG_SERIAL 0x2u       /* one stream, fewest chunks: no forward/backtrack overlap */
-/* tuning knob: MFMA tiles per wave per step for the MFMA-assisted kernel (N in (224,256]:
+/* MFMA tiles per wave per step for the MFMA-assisted kernel (implies it; N in (224,256]:
  * 0, 4..8; default 6).  Results are bit-identical for every value. */
 #define CV_FLAG_MFMA_TILES(n) ((uint32_t)((n) + 1) << 8)
 
