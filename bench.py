@@ -44,26 +44,50 @@ def parse():
 
 def cpu_baseline(pi, a, b, obs_rank, budget_s):
     """Oracle (C restatement of the reference's CPSolver forward + backtrack, f64, CP
-    association = what main.rs:120 runs) timed on this host, 1 thread, on the first k
-    sequences of this rank's shard; k grows until ~budget_s of CPU work."""
+    association = what main.rs:120 runs) timed on this host on the first k sequences of this
+    rank's shard; k grows until ~budget_s of CPU work.  `value` is the single-thread rate
+    (the reference is single-threaded); `all_cores` repeats it with OpenMP across sequences
+    on this process's CPU share."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import c_oracle
 
-    def run(k):
+    def run(k, threads):
         off = np.arange(k + 1, dtype=np.int64) * T_LEN
         t0 = time.perf_counter()
-        c_oracle.decode_batch(pi, a, b, off, obs_rank[: k * T_LEN], c_oracle.CP, np.float64, nthreads=1)
+        c_oracle.decode_batch(pi, a, b, off, obs_rank[: k * T_LEN], c_oracle.CP, np.float64, nthreads=threads)
         return time.perf_counter() - t0
 
-    k = 2
-    dt = run(k)
-    k = max(2, min(int(budget_s / max(dt / k, 1e-6)), 4096))
-    dt = run(k)
+    def sample(threads, budget):
+        k = 2 * threads
+        dt = run(k, threads)
+        k = max(2 * threads, min(int(budget / max(dt / k, 1e-6)), 4096 * threads))
+        return k, run(k, threads)
+
+    k, dt = sample(1, budget_s)
     cells = k * T_LEN * N_STATES
+    try:
+        share = len(os.sched_getaffinity(0))
+    except AttributeError:
+        share = os.cpu_count() or 1
+    nth = max(1, min(share, int(os.environ.get("OMP_NUM_THREADS", share)), 16))
+    km, dtm = sample(nth, budget_s / 2)
     return {"value": cells / dt, "unit": "trellis cells/s", "cores": 1, "kind": "port",
             "sample": f"first {k} sequences of config 4 (N=256, T=512), f64 CP association "
                       f"(cp.rs:95-125), oracle/cv_oracle.c single thread, {dt:.1f} s",
-            "seconds": dt}
+            "seconds": dt,
+            "all_cores": {"value": km * T_LEN * N_STATES / dtm, "cores": nth, "sequences": km, "seconds": dtm,
+                          "cpu": _cpu_model()}}
+
+
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
 
 
 def load_traffic():
