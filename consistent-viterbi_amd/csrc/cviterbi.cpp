@@ -21,6 +21,7 @@
 #include <vector>
 
 #include "../../include/cviterbi.h"
+#include "csp.hpp"
 #include "hmm_json.hpp"
 #include "kernels/trellis.h"
 
@@ -111,7 +112,7 @@ struct cv_hmm {
   // workspace
   DevBuf ws_main, ws_last, ws_order;
   DevBuf st_off, st_obs, st_path, st_score, st_status, st_forced;
-  DevBuf cs_ranges, cs_delta, cs_g, cs_mu;  // constrained-decode scratch
+  DevBuf cs_ranges, cs_delta, cs_g, cs_mu, cs_start, cs_zero;  // constrained-decode scratch
   std::vector<int32_t> order_host;
   // timing events of the last call
   std::vector<hipEvent_t> ev;  // 4 per chunk: fwd start/end (main stream), bt start/end
@@ -763,61 +764,101 @@ CV_API cv_status cv_decode_batch(cv_hmm* h, int64_t nseq, const int64_t* offsets
 }
 
 // ---- consistency-constrained decode --------------------------------------------------------
+// Spec: oracle/np_oracle.py constrained_decode; host search: csp.hpp.
 namespace {
-struct Con { int64_t seq, elem; int32_t comp; };
+constexpr uint64_t kCspNodeLimit = 20000000;  // branch-and-bound nodes per call
+constexpr int64_t kSegmentSlots = 65536;      // segment-table rows per launch (64 MiB of rows)
 
-// Validation + the device passes: mu[i][s] (f32, stride np) for each constrained element i.
-cv_status constrained_mu_locked(cv_hmm* h, int64_t nseq, const int64_t* offsets, const int32_t* obs,
-                                const int32_t* component, int32_t ncomp, cv_opts& o, std::vector<Con>& cons,
-                                std::vector<float>& mu) {
+struct ConSeq {
+  int64_t seq;
+  std::vector<int64_t> elems;  // constrained elements, ascending
+};
+
+cv_status constrained_validate(cv_hmm* h, int64_t nseq, const int64_t* offsets, const int32_t* obs,
+                               const int32_t* component, int32_t ncomp, const cv_opts& o, std::vector<ConSeq>& cs) {
   if (o.dtype != CV_DTYPE_F32 || o.assoc != CV_ASSOC_VITERBI || !cvk::trellis_padded_states(h->N))
     return set_err(CV_EUNSUPPORTED, "constrained decode runs on the f32 VITERBI trellis path (N <= 256)");
   if (o.forced) return set_err(CV_EINVAL, "opts->forced is set by the constrained decode itself");
-  cons.clear();
-  mu.clear();
+  cs.clear();
   if (nseq == 0) return CV_OK;
   cv_status st;
   if ((st = check_batch(h, nseq, offsets)) != CV_OK) return st;
-  const int64_t base = offsets[0], total = offsets[nseq];
-  for (int64_t k = base; k < total; ++k) {
+  for (int64_t k = offsets[0]; k < offsets[nseq]; ++k) {
     if (obs[k] < 0 || obs[k] >= h->V)
       return set_err(CV_EINVAL, "obs[%lld] = %d out of range [0,%lld)", (long long)k, obs[k], (long long)h->V);
     if (component[k] < -1 || component[k] >= ncomp)
       return set_err(CV_EINVAL, "component[%lld] = %d out of range [-1,%d)", (long long)k, component[k], ncomp);
   }
   for (int64_t s = 0; s < nseq; ++s) {
-    int found = 0;
+    ConSeq c{s, {}};
     for (int64_t e = offsets[s]; e < offsets[s + 1]; ++e)
-      if (component[e] >= 0) {
-        if (++found > 1)
-          return set_err(CV_EUNSUPPORTED, "sequence %lld holds more than one constrained element (pairwise "
-                                          "component terms are not implemented)", (long long)s);
-        cons.push_back({s, e, component[e]});
-      }
+      if (component[e] >= 0) c.elems.push_back(e);
+    if (!c.elems.empty()) cs.push_back(std::move(c));
   }
+  return CV_OK;
+}
+
+// Device passes of one shard + exact accumulation into its partials (csp.hpp layout;
+// `part` is zeroed by the caller).  Per sequence with constrained elements t_1 < .. < t_m:
+//   m == 1: mu = delta_{t_1} + beta  -> unary of c_1
+//   m >= 2: alpha = delta_{t_1} -> unary c_1; beta -> unary c_m; segment tables M_k -> the
+//           pair (c_k, c_{k+1}) (or the diagonal into the unary when c_k == c_{k+1}).
+cv_status constrained_partials_locked(cv_hmm* h, int64_t nseq, const int64_t* offsets, const int32_t* obs,
+                                      const int32_t* component, int32_t ncomp, const int32_t* pairs, int64_t npairs,
+                                      cv_opts& o, int64_t* part) {
+  std::vector<ConSeq> cs;
+  cv_status st = constrained_validate(h, nseq, offsets, obs, component, ncomp, o, cs);
+  if (st != CV_OK || cs.empty()) return st;
+  const int N = (int)h->N;
+  const int64_t uw = cvcsp::unary_words(N), pw = cvcsp::pair_words(N);
+  int64_t* pbase = part + (int64_t)ncomp * uw;
+  // pair lookups first: a missing pair is a caller error, found before any device work
+  std::vector<int64_t> seg_pair;  // per segment: pair index, or -1 for a same-component segment
+  for (const auto& c : cs)
+    for (size_t k = 0; k + 1 < c.elems.size(); ++k) {
+      const int32_t c1 = component[c.elems[k]], c2 = component[c.elems[k + 1]];
+      if (c1 == c2) {
+        seg_pair.push_back(-1);
+        continue;
+      }
+      const int64_t p = cvcsp::pair_index(pairs, npairs, std::min(c1, c2), std::max(c1, c2));
+      if (p < 0) return set_err(CV_EINVAL, "component pair (%d,%d) missing from the pair list", c1, c2);
+      seg_pair.push_back(p);
+    }
   if ((st = ensure_trellis_tables(h)) != CV_OK) return st;
   if ((st = ensure_f64_tables(h)) != CV_OK) return st;
   const int np = h->np;
-  const int64_t ncon = (int64_t)cons.size();
-  if (ncon == 0) return CV_OK;
   hipStream_t stream = o.stream ? (hipStream_t)o.stream : h->stream;
-  mu.resize((size_t)ncon * np);
+  const int64_t base = offsets[0], total = offsets[nseq];
   if ((st = h->st_obs.ensure((size_t)std::max<int64_t>(total, 1) * 4)) != CV_OK) return st;
   HIP_TRY(hipMemcpyAsync(h->st_obs.as<int32_t>() + base, obs + base, (size_t)(total - base) * 4,
                          hipMemcpyHostToDevice, stream));
-  std::vector<int64_t> rg((size_t)ncon * 4);  // prefix ranges, then suffix ranges
-  for (int64_t i = 0; i < ncon; ++i) {
-    rg[2 * i] = offsets[cons[i].seq];
-    rg[2 * i + 1] = cons[i].elem + 1;
-    rg[2 * ncon + 2 * i] = cons[i].elem + 1;
-    rg[2 * ncon + 2 * i + 1] = offsets[cons[i].seq + 1];
+
+  // ---- prefix / suffix passes for every constrained sequence (m == 1 ones first) ----
+  std::vector<const ConSeq*> order;
+  for (const auto& c : cs)
+    if (c.elems.size() == 1) order.push_back(&c);
+  const int64_t n1 = (int64_t)order.size();
+  for (const auto& c : cs)
+    if (c.elems.size() > 1) order.push_back(&c);
+  const int64_t nc = (int64_t)order.size();
+  std::vector<int64_t> rg((size_t)nc * 4);  // prefix ranges, then suffix ranges
+  for (int64_t i = 0; i < nc; ++i) {
+    const ConSeq& c = *order[i];
+    rg[2 * i] = offsets[c.seq];
+    rg[2 * i + 1] = c.elems.front() + 1;
+    rg[2 * nc + 2 * i] = c.elems.back() + 1;
+    rg[2 * nc + 2 * i + 1] = offsets[c.seq + 1];
   }
-  if ((st = h->cs_ranges.ensure(rg.size() * 8)) != CV_OK) return st;
-  if ((st = h->cs_delta.ensure((size_t)ncon * np * 4)) != CV_OK) return st;
-  if ((st = h->cs_g.ensure((size_t)ncon * np * 4)) != CV_OK) return st;
-  if ((st = h->cs_mu.ensure((size_t)ncon * np * 4)) != CV_OK) return st;
-  if ((st = h->st_status.ensure((size_t)std::max<int64_t>(nseq, ncon))) != CV_OK) return st;
+  const int64_t nslot_max = std::max<int64_t>(nc, std::min<int64_t>(kSegmentSlots, (int64_t)seg_pair.size() * N));
+  if ((st = h->cs_ranges.ensure(std::max(rg.size(), (size_t)nslot_max * 2) * 8)) != CV_OK) return st;
+  if ((st = h->cs_delta.ensure((size_t)nslot_max * np * 4)) != CV_OK) return st;
+  if ((st = h->cs_g.ensure((size_t)nc * np * 4)) != CV_OK) return st;
+  if ((st = h->cs_mu.ensure((size_t)nc * np * 4)) != CV_OK) return st;
+  if ((st = h->cs_zero.ensure((size_t)nc * np * 4)) != CV_OK) return st;
+  if ((st = h->st_status.ensure((size_t)std::max<int64_t>(nseq, nslot_max))) != CV_OK) return st;
   HIP_TRY(hipMemcpyAsync(h->cs_ranges.p, rg.data(), rg.size() * 8, hipMemcpyHostToDevice, stream));
+  HIP_TRY(hipMemsetAsync(h->cs_zero.p, 0, (size_t)nc * np * 4, stream));
   cvk::TrellisFwdArgs fa{};
   fa.a_img = h->t_aimg.as<float>();
   fa.pi = h->t_pi.as<float>();
@@ -827,77 +868,115 @@ cv_status constrained_mu_locked(cv_hmm* h, int64_t nseq, const int64_t* offsets,
   fa.nobs = (int)h->V;
   fa.ranges = h->cs_ranges.as<int64_t>();
   fa.last_row = h->cs_delta.as<float>();
-  hipError_t err = cvk::launch_trellis_fwd(np, fa, ncon, stream);  // delta_{t_k}: forward over the prefix
+  hipError_t err = cvk::launch_trellis_fwd(np, fa, nc, stream);  // delta_{t_1}: forward over the prefix
   if (err == hipSuccess) {
-    fa.a_img = h->t_aimg_T.as<float>();  // g_{t_k+1}: backward pass = same kernel on a^T, pi = 0, reversed
+    fa.a_img = h->t_aimg_T.as<float>();  // g_{t_m+1}: backward pass = same kernel on a^T, pi = 0, reversed
     fa.pi = h->t_pi0.as<float>();
-    fa.ranges = h->cs_ranges.as<int64_t>() + 2 * ncon;
+    fa.ranges = h->cs_ranges.as<int64_t>() + 2 * nc;
     fa.reverse = 1;
     fa.last_row = h->cs_g.as<float>();
-    err = cvk::launch_trellis_fwd(np, fa, ncon, stream);
+    err = cvk::launch_trellis_fwd(np, fa, nc, stream);
   }
-  if (err == hipSuccess) {
-    cvk::MaxMarginalArgs ma{};
+  cvk::MaxMarginalArgs ma{};
+  ma.g = h->cs_g.as<float>();
+  ma.ranges_suffix = h->cs_ranges.as<int64_t>() + 2 * nc;
+  ma.at = h->t_at.as<float>();
+  ma.mu = h->cs_mu.as<float>();
+  if (err == hipSuccess) {  // m == 1: mu = delta + beta
     ma.delta = h->cs_delta.as<float>();
-    ma.g = h->cs_g.as<float>();
-    ma.ranges_suffix = h->cs_ranges.as<int64_t>() + 2 * ncon;
-    ma.at = h->t_at.as<float>();
-    ma.mu = h->cs_mu.as<float>();
-    err = cvk::launch_max_marginal(np, ma, ncon, stream);
+    err = cvk::launch_max_marginal(np, ma, n1, stream);
+  }
+  if (err == hipSuccess && nc > n1) {  // m >= 2: beta alone (0 + beta is exact)
+    ma.delta = h->cs_zero.as<float>();
+    ma.g += n1 * np;
+    ma.ranges_suffix += 2 * n1;
+    ma.mu += n1 * np;
+    err = cvk::launch_max_marginal(np, ma, nc - n1, stream);
   }
   if (err != hipSuccess) return set_err(CV_EDEVICE, "max-marginal launch failed: %s", hipGetErrorString(err));
+  std::vector<float> dl((size_t)nc * np), mu((size_t)nc * np);
+  HIP_TRY(hipMemcpyAsync(dl.data(), h->cs_delta.p, dl.size() * 4, hipMemcpyDeviceToHost, stream));
   HIP_TRY(hipMemcpyAsync(mu.data(), h->cs_mu.p, mu.size() * 4, hipMemcpyDeviceToHost, stream));
   HIP_TRY(hipStreamSynchronize(stream));
+  for (int64_t i = 0; i < nc; ++i) {
+    const ConSeq& c = *order[i];
+    const int32_t c1 = component[c.elems.front()], cm = component[c.elems.back()];
+    for (int64_t e : c.elems) part[(int64_t)component[e] * uw + 5 * N] += 1;
+    int64_t* u1 = part + (int64_t)c1 * uw;
+    int64_t* um = part + (int64_t)cm * uw;
+    for (int s = 0; s < N; ++s) {
+      if (i < n1) {
+        cvcsp::add_exact(u1 + 4 * s, u1 + 4 * N + s, mu[(size_t)i * np + s]);
+      } else {
+        cvcsp::add_exact(u1 + 4 * s, u1 + 4 * N + s, dl[(size_t)i * np + s]);
+        cvcsp::add_exact(um + 4 * s, um + 4 * N + s, mu[(size_t)i * np + s]);
+      }
+    }
+  }
+
+  // ---- segment tables: one slot per (segment, start state), in batches ----
+  struct Seg { int64_t e0, e1; int32_t c1, c2; int64_t p; };
+  std::vector<Seg> segs;
+  {
+    size_t q = 0;  // seg_pair follows cs order, and so do the m >= 2 entries of `order`
+    for (int64_t i = n1; i < nc; ++i) {
+      const ConSeq& c = *order[i];
+      for (size_t k = 0; k + 1 < c.elems.size(); ++k, ++q)
+        segs.push_back({c.elems[k], c.elems[k + 1], component[c.elems[k]], component[c.elems[k + 1]], seg_pair[q]});
+    }
+  }
+  const int64_t nslots = (int64_t)segs.size() * N;
+  std::vector<int64_t> srg;
+  std::vector<int32_t> sst;
+  std::vector<float> rows;
+  for (int64_t b0 = 0; b0 < nslots; b0 += kSegmentSlots) {
+    const int64_t nb = std::min(kSegmentSlots, nslots - b0);
+    srg.resize((size_t)nb * 2);
+    sst.resize((size_t)nb);
+    for (int64_t k = 0; k < nb; ++k) {
+      const Seg& sg = segs[(b0 + k) / N];
+      srg[2 * k] = sg.e0;
+      srg[2 * k + 1] = sg.e1 + 1;
+      sst[k] = (int32_t)((b0 + k) % N);
+    }
+    if ((st = h->cs_start.ensure((size_t)nb * 4)) != CV_OK) return st;
+    HIP_TRY(hipMemcpyAsync(h->cs_ranges.p, srg.data(), srg.size() * 8, hipMemcpyHostToDevice, stream));
+    HIP_TRY(hipMemcpyAsync(h->cs_start.p, sst.data(), sst.size() * 4, hipMemcpyHostToDevice, stream));
+    cvk::TrellisFwdArgs sa{};
+    sa.a_img = h->t_aimg.as<float>();
+    sa.pi = h->t_pi.as<float>();
+    sa.et = h->t_et.as<float>();
+    sa.obs = h->st_obs.as<int32_t>();
+    sa.status = h->st_status.as<uint8_t>();
+    sa.nobs = (int)h->V;
+    sa.ranges = h->cs_ranges.as<int64_t>();
+    sa.start = h->cs_start.as<int32_t>();
+    sa.last_row = h->cs_delta.as<float>();
+    if ((err = cvk::launch_trellis_fwd(np, sa, nb, stream)) != hipSuccess)
+      return set_err(CV_EDEVICE, "segment-table launch failed: %s", hipGetErrorString(err));
+    rows.resize((size_t)nb * np);
+    HIP_TRY(hipMemcpyAsync(rows.data(), h->cs_delta.p, rows.size() * 4, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipStreamSynchronize(stream));
+    for (int64_t k = 0; k < nb; ++k) {
+      const Seg& sg = segs[(b0 + k) / N];
+      const int s = (int)((b0 + k) % N);
+      const float* r = &rows[(size_t)k * np];
+      if (sg.p < 0) {  // same component at both ends: only the diagonal is consistent
+        int64_t* u = part + (int64_t)sg.c1 * uw;
+        cvcsp::add_exact(u + 4 * s, u + 4 * N + s, r[s]);
+        continue;
+      }
+      int64_t* pp = pbase + sg.p * pw;
+      if (s == 0) pp[5 * (int64_t)N * N] += 1;
+      for (int s2 = 0; s2 < N; ++s2) {
+        const int64_t e = sg.c1 < sg.c2 ? (int64_t)s * N + s2 : (int64_t)s2 * N + s;
+        cvcsp::add_exact(pp + 4 * e, pp + 4 * (int64_t)N * N + e, r[s2]);
+      }
+    }
+  }
   return CV_OK;
 }
 
-// Partials layout per component c (stride CV_PARTIAL_STRIDE(N) int64 words):
-//   [4N] base-2^32 limbs of the exact sum in units of 2^-64 (limb 3 signed), state-major
-//   [N]  count of -inf max-marginals per state, [1] count of constrained elements.
-// Every word is a plain sum over elements, so partials of disjoint shards add.
-void accumulate_partials(const std::vector<Con>& cons, const std::vector<float>& mu, int N, int np,
-                         int64_t* part) {
-  const int64_t stride = 5 * (int64_t)N + 1;
-  const double scale = 18446744073709551616.0;  // 2^64
-  for (size_t i = 0; i < cons.size(); ++i) {
-    int64_t* pc = part + (int64_t)cons[i].comp * stride;
-    pc[5 * N] += 1;
-    for (int s = 0; s < N; ++s) {
-      const float m = mu[i * np + s];
-      if (!(m > -INFINITY)) {
-        pc[4 * N + s] += 1;
-        continue;
-      }
-      const __int128 v = (__int128)std::nearbyint((double)m * scale);  // |m| < 2^24 -> < 2^88, exact
-      const unsigned __int128 u = (unsigned __int128)v;
-      pc[4 * s + 0] += (int64_t)(uint32_t)(u);
-      pc[4 * s + 1] += (int64_t)(uint32_t)(u >> 32);
-      pc[4 * s + 2] += (int64_t)(uint32_t)(u >> 64);
-      pc[4 * s + 3] += (int64_t)(v >> 96);  // arithmetic shift: signed top limb
-    }
-  }
-}
-
-void select_states(int32_t ncomp, int N, const int64_t* part, int32_t* comp_state_out, uint64_t* explored) {
-  const int64_t stride = 5 * (int64_t)N + 1;
-  uint64_t ex = 0;
-  for (int32_t c = 0; c < ncomp; ++c) {
-    const int64_t* pc = part + (int64_t)c * stride;
-    comp_state_out[c] = -1;
-    if (pc[5 * N] == 0) continue;
-    ex += (uint64_t)N;
-    int best = -1;
-    __int128 bv = 0;
-    for (int s = 0; s < N; ++s) {
-      if (pc[4 * N + s] != 0) continue;
-      const __int128 v = (__int128)pc[4 * s] + ((__int128)pc[4 * s + 1] << 32) + ((__int128)pc[4 * s + 2] << 64) +
-                         ((__int128)pc[4 * s + 3] << 96);
-      if (best < 0 || v > bv) best = s, bv = v;
-    }
-    comp_state_out[c] = best;
-  }
-  if (explored) *explored = ex;
-}
 // Final decode: every constrained element forced to its component's state; sequences whose
 // component has no feasible state are infeasible.  objective = sum of the f64 scores.
 cv_status forced_decode_locked(cv_hmm* h, int64_t nseq, const int64_t* offsets, const int32_t* obs,
@@ -922,32 +1001,71 @@ cv_status forced_decode_locked(cv_hmm* h, int64_t nseq, const int64_t* offsets, 
   if (objective_out) *objective_out = obj;
   return CV_OK;
 }
+
+cv_status select_locked(int32_t nstates, int32_t ncomp, const int32_t* pairs, int64_t npairs,
+                        const int64_t* partials, int32_t* comp_state_out, uint64_t* explored_out) {
+  const cvcsp::SolveResult r = cvcsp::solve(nstates, ncomp, pairs, npairs, partials, comp_state_out, kCspNodeLimit);
+  if (explored_out) *explored_out = r.explored;
+  if (r.limit_hit)
+    return set_err(CV_ELIMIT, "component-state search exceeded %llu nodes", (unsigned long long)kCspNodeLimit);
+  return CV_OK;
+}
+
+bool pairs_sorted(const int32_t* pairs, int64_t npairs, int32_t ncomp) {
+  for (int64_t p = 0; p < npairs; ++p) {
+    if (pairs[2 * p] < 0 || pairs[2 * p] >= pairs[2 * p + 1] || pairs[2 * p + 1] >= ncomp) return false;
+    if (p > 0 && !(pairs[2 * p - 2] < pairs[2 * p] || (pairs[2 * p - 2] == pairs[2 * p] && pairs[2 * p - 1] <
+                                                                                             pairs[2 * p + 1])))
+      return false;
+  }
+  return true;
+}
 }  // namespace
 
+CV_API cv_status cv_constrained_pairs(int64_t nseq, const int64_t* offsets, const int32_t* component, int32_t ncomp,
+                                      int32_t* pairs_out, int64_t cap_pairs, int64_t* npairs_out) {
+  if (nseq < 0 || ncomp < 0 || !npairs_out || (nseq > 0 && (!offsets || !component)))
+    return set_err(CV_EINVAL, "bad argument");
+  *npairs_out = 0;
+  if (nseq == 0) return CV_OK;
+  for (int64_t s = 0; s < nseq; ++s)
+    if (offsets[s + 1] < offsets[s]) return set_err(CV_EINVAL, "offsets must be non-decreasing");
+  for (int64_t k = offsets[0]; k < offsets[nseq]; ++k)
+    if (component[k] < -1 || component[k] >= ncomp)
+      return set_err(CV_EINVAL, "component[%lld] = %d out of range [-1,%d)", (long long)k, component[k], ncomp);
+  const std::vector<int32_t> p = cvcsp::component_pairs(nseq, offsets, component);
+  *npairs_out = (int64_t)p.size() / 2;
+  if (pairs_out) {
+    if (cap_pairs < *npairs_out) return set_err(CV_EINVAL, "pairs_out holds %lld pairs, %lld needed",
+                                                (long long)cap_pairs, (long long)*npairs_out);
+    std::copy(p.begin(), p.end(), pairs_out);
+  }
+  return CV_OK;
+}
+
 CV_API cv_status cv_constrained_partials(cv_hmm* h, int64_t nseq, const int64_t* offsets, const int32_t* obs,
-                                         const int32_t* component, int32_t ncomp, const cv_opts* opts,
-                                         int64_t* partials_out) {
+                                         const int32_t* component, int32_t ncomp, int64_t npairs,
+                                         const int32_t* pairs, const cv_opts* opts, int64_t* partials_out) {
   if (!h) return set_err(CV_EINVAL, "null handle");
-  if (nseq < 0 || ncomp < 0 || (nseq > 0 && (!offsets || !obs || !component)) || (ncomp > 0 && !partials_out))
+  if (nseq < 0 || ncomp < 0 || npairs < 0 || (nseq > 0 && (!offsets || !obs || !component)) ||
+      (ncomp > 0 && !partials_out) || (npairs > 0 && !pairs))
     return set_err(CV_EINVAL, "null argument");
+  if (!pairs_sorted(pairs, npairs, ncomp)) return set_err(CV_EINVAL, "pairs must be sorted (c1 < c2) and unique");
   std::lock_guard<std::mutex> lk(h->mu);
   cv_status st = set_device(h);
   if (st != CV_OK) return st;
   cv_opts o = opts ? *opts : default_opts();
-  std::vector<Con> cons;
-  std::vector<float> mu;
-  if ((st = constrained_mu_locked(h, nseq, offsets, obs, component, ncomp, o, cons, mu)) != CV_OK) return st;
-  std::memset(partials_out, 0, (size_t)ncomp * (5 * (size_t)h->N + 1) * 8);
-  accumulate_partials(cons, mu, h->N, h->np, partials_out);
-  return CV_OK;
+  std::memset(partials_out, 0, (size_t)cvcsp::partial_words((int)h->N, ncomp, npairs) * 8);
+  return constrained_partials_locked(h, nseq, offsets, obs, component, ncomp, pairs, npairs, o, partials_out);
 }
 
-CV_API cv_status cv_constrained_select(int32_t nstates, int32_t ncomp, const int64_t* partials,
-                                       int32_t* comp_state_out, uint64_t* explored_out) {
-  if (nstates <= 0 || ncomp < 0 || (ncomp > 0 && (!partials || !comp_state_out)))
+CV_API cv_status cv_constrained_select(int32_t nstates, int32_t ncomp, int64_t npairs, const int32_t* pairs,
+                                       const int64_t* partials, int32_t* comp_state_out, uint64_t* explored_out) {
+  if (nstates <= 0 || ncomp < 0 || npairs < 0 || (ncomp > 0 && (!partials || !comp_state_out)) ||
+      (npairs > 0 && !pairs))
     return set_err(CV_EINVAL, "bad argument");
-  select_states(ncomp, nstates, partials, comp_state_out, explored_out);
-  return CV_OK;
+  if (!pairs_sorted(pairs, npairs, ncomp)) return set_err(CV_EINVAL, "pairs must be sorted (c1 < c2) and unique");
+  return select_locked(nstates, ncomp, pairs, npairs, partials, comp_state_out, explored_out);
 }
 
 CV_API cv_status cv_decode_constrained(cv_hmm* h, int64_t nseq, const int64_t* offsets, const int32_t* obs,
@@ -964,15 +1082,19 @@ CV_API cv_status cv_decode_constrained(cv_hmm* h, int64_t nseq, const int64_t* o
   cv_opts o = opts ? *opts : default_opts();
   for (int32_t c = 0; c < ncomp; ++c) comp_state_out[c] = -1;
   if (objective_out) *objective_out = 0.0;
-  std::vector<Con> cons;
-  std::vector<float> mu;
-  if ((st = constrained_mu_locked(h, nseq, offsets, obs, component, ncomp, o, cons, mu)) != CV_OK) return st;
+  std::vector<ConSeq> cs;
+  if ((st = constrained_validate(h, nseq, offsets, obs, component, ncomp, o, cs)) != CV_OK) return st;
   if (nseq == 0) return CV_OK;
-  // exact per-component sums of the max-marginals (order and shard independent)
-  std::vector<int64_t> part((size_t)ncomp * (5 * (size_t)h->N + 1), 0);
-  accumulate_partials(cons, mu, h->N, h->np, part.data());
+  const std::vector<int32_t> pairs = cvcsp::component_pairs(nseq, offsets, component);
+  const int64_t npairs = (int64_t)pairs.size() / 2;
+  std::vector<int64_t> part((size_t)cvcsp::partial_words((int)h->N, ncomp, npairs), 0);
+  if ((st = constrained_partials_locked(h, nseq, offsets, obs, component, ncomp, pairs.data(), npairs, o,
+                                        part.data())) != CV_OK)
+    return st;
   uint64_t explored = 0;
-  select_states(ncomp, h->N, part.data(), comp_state_out, &explored);
+  if ((st = select_locked((int32_t)h->N, ncomp, pairs.data(), npairs, part.data(), comp_state_out, &explored)) !=
+      CV_OK)
+    return st;
   h->last_explored = explored;
   return forced_decode_locked(h, nseq, offsets, obs, component, comp_state_out, o, path_out, score_out, status_out,
                               objective_out);

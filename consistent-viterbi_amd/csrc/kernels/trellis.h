@@ -26,6 +26,8 @@ struct TrellisFwdArgs {
   const int64_t* ranges;   // [nslot][2] explicit element ranges (begin, end); slot = sequence id
   int reverse;             // 1: traverse each range from end-1 down to begin
   float* last_row;         // [nslot][NP] final delta row of each slot (slot - seq_begin)
+  const int32_t* start;    // [nslot] (slot - seq_begin): s >= 0 starts the range in state s with
+                           // delta = 0 there (-inf elsewhere, no pi/emission term); -1: normal
 };
 
 struct BacktrackArgs {

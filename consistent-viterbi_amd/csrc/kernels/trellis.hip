@@ -188,6 +188,13 @@ __global__ __launch_bounds__(NP * 4) void trellis_fwd_f32(TrellisFwdArgs args) {
     float2 d0;
     d0.x = args.pi[j0] + e.x;
     d0.y = args.pi[j0 + 1] + e.y;
+    if (EXT && args.start) {  // segment table column: start in state s, score 0 (cfn.rs:11-34 pattern)
+      const int s = args.start[slot - args.seq_begin];
+      if (s >= 0) {
+        d0.x = (j0 == s) ? 0.0f : ninf_f();
+        d0.y = (j0 + 1 == s) ? 0.0f : ninf_f();
+      }
+    }
     d0 = force(d0, frc_s(0));
     if (rg == 0) {
       *reinterpret_cast<float2*>(&lds_delta[0][lds_w]) = d0;
@@ -820,7 +827,7 @@ hipError_t launch_max_marginal(int np, const MaxMarginalArgs& a, int64_t ncon, h
 // Host-side launchers (called from the C-ABI layer).  Forward and backtrack are launched
 // separately so the host can run chunk k's backtrack beside chunk k+1's forward pass.
 static bool ext_args(const TrellisFwdArgs& fa) {
-  return fa.forced || fa.ranges || fa.reverse || fa.last_row || !fa.delta;
+  return fa.forced || fa.ranges || fa.reverse || fa.last_row || fa.start || !fa.delta;
 }
 
 template <int NP>

@@ -12,9 +12,10 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libcviterbi.so")
 
-CV_OK, CV_EINVAL, CV_EDEVICE, CV_ENOMEM, CV_EINFEASIBLE, CV_EIO, CV_EPARSE, CV_EUNSUPPORTED, CV_EINTERNAL = range(9)
+(CV_OK, CV_EINVAL, CV_EDEVICE, CV_ENOMEM, CV_EINFEASIBLE, CV_EIO, CV_EPARSE, CV_EUNSUPPORTED, CV_EINTERNAL,
+ CV_ELIMIT) = range(10)
 STATUS_NAMES = {0: "CV_OK", 1: "CV_EINVAL", 2: "CV_EDEVICE", 3: "CV_ENOMEM", 4: "CV_EINFEASIBLE", 5: "CV_EIO",
-                6: "CV_EPARSE", 7: "CV_EUNSUPPORTED", 8: "CV_EINTERNAL"}
+                6: "CV_EPARSE", 7: "CV_EUNSUPPORTED", 8: "CV_EINTERNAL", 9: "CV_ELIMIT"}
 SEQ_OK, SEQ_INFEASIBLE, SEQ_EMPTY, SEQ_BADOBS = 0, 1, 2, 3
 DTYPE_F32, DTYPE_F64 = 0, 1
 ASSOC_VITERBI, ASSOC_CP, ASSOC_DP, ASSOC_DECODE = 0, 1, 2, 3
@@ -33,7 +34,7 @@ EXPORTS = [
     "cv_hmm_ndims", "cv_hmm_bdims", "cv_obs_flatten", "cv_hmm_init_prob", "cv_hmm_init_probs",
     "cv_hmm_transition_prob", "cv_hmm_transitions_to", "cv_hmm_emit_prob", "cv_hmm_emit_probs",
     "cv_decode_batch", "cv_decode_batch_device", "cv_last_timing", "cv_decode_constrained",
-    "cv_constrained_partials", "cv_constrained_select", "cv_decode_forced_components", "cv_viterbi_decode",
+    "cv_constrained_pairs", "cv_constrained_partials", "cv_constrained_select", "cv_decode_forced_components", "cv_viterbi_decode",
     "cv_solver_create", "cv_solver_solve", "cv_solver_get_solution", "cv_solver_get_objective",
     "cv_solver_get_name", "cv_solver_get_explored_nodes", "cv_solver_destroy",
 ]
@@ -111,8 +112,9 @@ def lib():
         "cv_decode_batch_device": ([P, I64, P, P, P, P, P, P, P], S),
         "cv_last_timing": ([P, P], S),
         "cv_decode_constrained": ([P, I64, P, P, P, I32, P, P, P, P, P, P], S),
-        "cv_constrained_partials": ([P, I64, P, P, P, I32, P, P], S),
-        "cv_constrained_select": ([I32, I32, P, P, P], S),
+        "cv_constrained_pairs": ([I64, P, P, I32, P, I64, P], S),
+        "cv_constrained_partials": ([P, I64, P, P, P, I32, I64, P, P, P], S),
+        "cv_constrained_select": ([I32, I32, I64, P, P, P, P], S),
         "cv_decode_forced_components": ([P, I64, P, P, P, I32, P, P, P, P, P, P], S),
         "cv_viterbi_decode": ([P, I64, P, P], S),
         "cv_solver_create": ([ctypes.c_char_p, P, P, P], S),

@@ -77,31 +77,53 @@ def decode_constrained(hmm: HMM, offsets, obs, component, ncomp=None, rescore_f6
     return path, score, status, states[:ncomp], obj.value
 
 
-def partial_stride(nstates: int) -> int:
-    """CV_PARTIAL_STRIDE: int64 words per component in the constrained partials."""
-    return 5 * int(nstates) + 1
+def partial_words(nstates: int, ncomp: int, npairs: int) -> int:
+    """CV_PARTIAL_WORDS: int64 words of the constrained partials."""
+    return int(ncomp) * (5 * int(nstates) + 1) + int(npairs) * (5 * int(nstates) ** 2 + 1)
 
 
-def constrained_partials(hmm: HMM, offsets, obs, component, ncomp):
-    """cv_constrained_partials: this shard's exact per-component sums, int64[ncomp, 5N+1];
-    partials of disjoint shards add (one all-reduce SUM)."""
+def constrained_pairs(offsets, component, ncomp):
+    """cv_constrained_pairs (host only): int32[npairs, 2] sorted component pairs (c1 < c2)
+    that are consecutive constrained elements of a sequence -- compute on the FULL batch."""
+    offsets = np.ascontiguousarray(offsets, np.int64)
+    component = np.ascontiguousarray(component, np.int32)
+    n = ctypes.c_int64()
+    nseq = offsets.shape[0] - 1
+    L.check(L.lib().cv_constrained_pairs(nseq, _p(offsets), _p(component), int(ncomp), None, 0, ctypes.byref(n)))
+    pairs = np.zeros((max(n.value, 1), 2), np.int32)
+    L.check(L.lib().cv_constrained_pairs(nseq, _p(offsets), _p(component), int(ncomp), _p(pairs), n.value,
+                                         ctypes.byref(n)))
+    return pairs[:n.value]
+
+
+def constrained_partials(hmm: HMM, offsets, obs, component, ncomp, pairs=None):
+    """cv_constrained_partials: this shard's exact unary + pairwise terms as int64 words
+    (partial_words long); partials of disjoint shards add (one all-reduce SUM).  `pairs`
+    must come from constrained_pairs on the full batch (default: this batch's own)."""
     offsets = np.ascontiguousarray(offsets, np.int64)
     obs = np.ascontiguousarray(obs, np.int32)
     component = np.ascontiguousarray(component, np.int32)
-    part = np.zeros((max(int(ncomp), 1), partial_stride(hmm.nstates())), np.int64)
+    if pairs is None:
+        pairs = constrained_pairs(offsets, component, ncomp)
+    pairs = np.ascontiguousarray(pairs, np.int32).reshape(-1, 2)
+    part = np.zeros(max(partial_words(hmm.nstates(), ncomp, len(pairs)), 1), np.int64)
     o = make_opts("f32", "viterbi", "auto", True)
     L.check(L.lib().cv_constrained_partials(hmm.handle, offsets.shape[0] - 1, _p(offsets), _p(obs), _p(component),
-                                            int(ncomp), ctypes.byref(o), _p(part)))
-    return part[:ncomp]
+                                            int(ncomp), len(pairs), _p(pairs) if len(pairs) else None,
+                                            ctypes.byref(o), _p(part)))
+    return part[:partial_words(hmm.nstates(), ncomp, len(pairs))]
 
 
-def constrained_select(nstates: int, partials):
+def constrained_select(nstates: int, ncomp: int, partials, pairs=None):
     """cv_constrained_select (host only): (comp_state[ncomp], explored) from reduced partials."""
     partials = np.ascontiguousarray(partials, np.int64)
-    ncomp = partials.shape[0]
+    pairs = np.zeros((0, 2), np.int32) if pairs is None else np.ascontiguousarray(pairs, np.int32).reshape(-1, 2)
+    if partials.size != partial_words(nstates, ncomp, len(pairs)):
+        raise ValueError("partials size does not match (nstates, ncomp, pairs)")
     states = np.full(max(ncomp, 1), -1, np.int32)
     ex = ctypes.c_uint64()
-    L.check(L.lib().cv_constrained_select(int(nstates), ncomp, _p(partials), _p(states), ctypes.byref(ex)))
+    L.check(L.lib().cv_constrained_select(int(nstates), int(ncomp), len(pairs), _p(pairs) if len(pairs) else None,
+                                          _p(partials), _p(states), ctypes.byref(ex)))
     return states[:ncomp], ex.value
 
 

@@ -5,11 +5,12 @@ contiguous shards of ceil(B/world) sequences, one per rank (one process per GPU)
 HMM is replicated.  The only collective is the gather of paths, scores and statuses to
 rank 0 -- RCCL over xGMI with the "nccl" backend on the GPU node, gloo in CPU tests.
 
-The consistency-constrained decode (config 5) has one real exchange step: the per-component
-sums of max-marginals.  Each rank reduces its shard to exact integer partials (int64 words,
-include/cviterbi.h CV_PARTIAL_STRIDE), one all-reduce SUM combines them -- bit-identical to
-the single-process choice whatever the shard boundaries -- and every rank selects the same
-component states and decodes its own shard.
+The consistency-constrained decode (config 5) has one real exchange step: the unary and
+pairwise component terms.  Every rank derives the same pair layout from the full batch
+(cv_constrained_pairs), reduces its shard to exact integer partials (int64 words,
+include/cviterbi.h CV_PARTIAL_WORDS), one all-reduce SUM combines them -- bit-identical to
+the single-process choice whatever the shard boundaries -- and every rank runs the same
+exact search and decodes its own shard.
 """
 from __future__ import annotations
 
@@ -56,7 +57,7 @@ def assemble(parts, lengths):
 
 
 def allreduce_partials(partials, dist, device=None):
-    """All-reduce SUM of int64 constrained partials ([ncomp, 5N+1]); returns numpy int64.
+    """All-reduce SUM of int64 constrained partials (CV_PARTIAL_WORDS); returns numpy int64.
     Integer sums: exact and independent of reduction order."""
     import torch
 
@@ -71,7 +72,7 @@ def constrained_decode_sharded(hmm, offsets, obs, component, ncomp, dist, device
     objective) on rank 0 and (None, None, None, comp_state, None) elsewhere."""
     import torch
 
-    from .decode import constrained_partials, constrained_select, decode_forced_components
+    from .decode import constrained_pairs, constrained_partials, constrained_select, decode_forced_components
 
     offsets = np.asarray(offsets, np.int64)
     world, rank = dist.get_world_size(), dist.get_rank()
@@ -81,9 +82,10 @@ def constrained_decode_sharded(hmm, offsets, obs, component, ncomp, dist, device
     off = shard_offsets(offsets, s0, s1)
     ob = np.asarray(obs, np.int32)[lo:hi]
     cp = np.asarray(component, np.int32)[lo:hi]
-    part = constrained_partials(hmm, off, ob, cp, ncomp)
+    pairs = constrained_pairs(offsets, component, ncomp)  # full batch: the same layout on every rank
+    part = constrained_partials(hmm, off, ob, cp, ncomp, pairs)
     part = allreduce_partials(part, dist, device)
-    states, _ = constrained_select(hmm.nstates(), part)
+    states, _ = constrained_select(hmm.nstates(), ncomp, part, pairs)
     path, score, status, _ = decode_forced_components(hmm, off, ob, cp, states)
     # gather: sequence counts and element counts differ per rank -> pad to capacities
     counts = torch.tensor([s1 - s0, hi - lo], dtype=torch.int64, device=device or "cpu")

@@ -39,7 +39,8 @@ typedef enum cv_status {
   CV_EIO = 5,           /* file could not be read / written */
   CV_EPARSE = 6,        /* malformed hmm.json */
   CV_EUNSUPPORTED = 7,  /* valid request this build does not implement */
-  CV_EINTERNAL = 8
+  CV_EINTERNAL = 8,
+  CV_ELIMIT = 9         /* search limit reached (constrained decode: branch-and-bound nodes) */
 } cv_status;
 
 /* per-sequence status_out values */
@@ -174,34 +175,43 @@ CV_API cv_status cv_last_timing(cv_hmm* h, cv_timing* out);
 /* Consistency-constrained decode (the intended semantics of the reference's constrained
  * solvers, opti.rs:101-111 / dp.rs:157-164 / cp.rs:95-126): every element with
  * component[e] >= 0 takes the common state of its component, and the total log-likelihood
- * is maximised.  Exact when each sequence holds at most one constrained element: per
- * component, the max-marginals mu_k(s) at the constrained positions (forward + reversed
- * backward trellis passes on the GPU) are summed exactly (integers in units of 2^-64, so
- * the choice is independent of order and of how the batch is sharded), s_c = first argmax,
- * then a forced decode.  f32 trellis path (N <= 256).  comp_state_out[ncomp] gets s_c (-1 if
- * the component has no active element, or no feasible state); objective_out = sum of the
- * per-sequence scores (f64 re-scored).  Sequences with two or more constrained elements
- * return CV_EUNSUPPORTED. Host pointers; synchronous. */
+ * is maximised.  The objective splits at the constrained positions of each sequence
+ * (cfn.rs:11-34 pattern): one position gives the max-marginal mu(s) = delta + beta; several
+ * give alpha(s_1) + sum_k M_k(s_k, s_k+1) + beta(s_m) with segment tables M_k (start in s at
+ * t_k with score 0, run to t_k+1) -- all computed by the trellis kernels.  Summed over
+ * sequences as exact integers (units of 2^-64: independent of order and sharding) this is
+ * a weighted CSP with unary and pairwise terms, solved exactly per connected group of
+ * components by branch and bound (ties: lexicographically smallest state vector in
+ * component order); then a forced decode.  f32 trellis path (N <= 256).  comp_state_out[ncomp]
+ * gets s_c (-1: no active element, or no feasible assignment of its group); objective_out =
+ * sum of the per-sequence scores (f64 re-scored).  CV_ELIMIT if the search exceeds its node
+ * limit.  Host pointers; synchronous. */
 CV_API cv_status cv_decode_constrained(cv_hmm* h, int64_t nseq, const int64_t* offsets, const int32_t* obs,
                                        const int32_t* component, int32_t ncomp, const cv_opts* opts,
                                        int32_t* path_out, double* score_out, uint8_t* status_out,
                                        int32_t* comp_state_out, double* objective_out);
 /* The same decode split at its one exchange step, for a batch sharded over processes/GPUs:
- * 1. cv_constrained_partials: this shard's exact per-component sums as int64 words that
- *    ADD across shards (one all-reduce SUM of ncomp * CV_PARTIAL_STRIDE(N) int64 words);
- *    per component: 4N base-2^32 limbs (state-major) of the sum in units of 2^-64, N counts
- *    of -inf max-marginals, 1 count of constrained elements.  Zeroes partials_out first.
- * 2. cv_constrained_select (host only): comp_state_out[c] = first argmax over feasible states
- *    of the reduced partials (-1: no element / no feasible state); explored = N per used one.
+ * 0. cv_constrained_pairs (host only) on the FULL batch: the sorted component pairs (c1 < c2)
+ *    that are consecutive constrained elements of some sequence -- the layout every rank
+ *    agrees on.  pairs_out may be null to query *npairs_out.
+ * 1. cv_constrained_partials: this shard's exact terms as CV_PARTIAL_WORDS int64 words that
+ *    ADD across shards (one all-reduce SUM).  Per component: 4N base-2^32 limbs (state-major)
+ *    of the unary sum in units of 2^-64, N counts of -inf terms, 1 count of constrained
+ *    elements; then per pair: 4N^2 limbs (entry s1*N+s2), N^2 -inf counts, 1 count.
+ * 2. cv_constrained_select (host only): the exact search on the reduced partials;
+ *    explored = (component, state) candidates scored.
  * 3. cv_decode_forced_components: the shard's final decode with every constrained element
  *    forced to comp_state[component[e]]; objective_out = the shard's sum of scores.
- * cv_decode_constrained == 1 + 2 + 3 on one process. */
-#define CV_PARTIAL_STRIDE(nstates) (5 * (int64_t)(nstates) + 1)
+ * cv_decode_constrained == 0 + 1 + 2 + 3 on one process. */
+#define CV_PARTIAL_WORDS(nstates, ncomp, npairs) \
+  ((int64_t)(ncomp) * (5 * (int64_t)(nstates) + 1) + (int64_t)(npairs) * (5 * (int64_t)(nstates) * (nstates) + 1))
+CV_API cv_status cv_constrained_pairs(int64_t nseq, const int64_t* offsets, const int32_t* component, int32_t ncomp,
+                                      int32_t* pairs_out, int64_t cap_pairs, int64_t* npairs_out);
 CV_API cv_status cv_constrained_partials(cv_hmm* h, int64_t nseq, const int64_t* offsets, const int32_t* obs,
-                                         const int32_t* component, int32_t ncomp, const cv_opts* opts,
-                                         int64_t* partials_out);
-CV_API cv_status cv_constrained_select(int32_t nstates, int32_t ncomp, const int64_t* partials,
-                                       int32_t* comp_state_out, uint64_t* explored_out);
+                                         const int32_t* component, int32_t ncomp, int64_t npairs,
+                                         const int32_t* pairs, const cv_opts* opts, int64_t* partials_out);
+CV_API cv_status cv_constrained_select(int32_t nstates, int32_t ncomp, int64_t npairs, const int32_t* pairs,
+                                       const int64_t* partials, int32_t* comp_state_out, uint64_t* explored_out);
 CV_API cv_status cv_decode_forced_components(cv_hmm* h, int64_t nseq, const int64_t* offsets, const int32_t* obs,
                                              const int32_t* component, int32_t ncomp, const int32_t* comp_state,
                                              const cv_opts* opts, int32_t* path_out, double* score_out,

@@ -107,38 +107,13 @@ def max_marginal(pi, a, b, obs, tk, dtype):
 
 
 def constrained_forced(pi, a, b, offsets, obs, component, dtype=np.float32):
-    """np_oracle.constrained_decode spec (exact 2^-64 integer sums), C-accelerated.
+    """np_oracle.constrained_decode spec with the C-accelerated max-marginal (one-position
+    sequences); several-position sequences use the numpy segment tables.
     Returns (comp_state dict, forced[sum T])."""
     import np_oracle as NO
 
-    offsets = np.asarray(offsets, np.int64)
-    component = np.asarray(component, np.int64)
-    n = np.asarray(a).shape[0]
-    sums = {}
-    for k in range(len(offsets) - 1):
-        lo, hi = offsets[k], offsets[k + 1]
-        pos = np.nonzero(component[lo:hi] >= 0)[0]
-        if len(pos) == 0:
-            continue
-        assert len(pos) == 1
-        tk = int(pos[0])
-        c = int(component[lo + tk])
-        mu = max_marginal(pi, a, b, np.asarray(obs[lo:hi]), tk, dtype)
-        acc = sums.setdefault(c, [0] * n)
-        for s in range(n):
-            u = NO.exact_units(mu[s])
-            acc[s] = None if (u is None or acc[s] is None) else acc[s] + u
-    comp_state = {}
-    for c, acc in sums.items():
-        best = None
-        for s in range(n):
-            if acc[s] is not None and (best is None or acc[s] > acc[best]):
-                best = s
-        comp_state[c] = -1 if best is None else best
-    forced = np.full(len(obs), -1, np.int32)
-    for e in np.nonzero(component >= 0)[0]:
-        forced[e] = max(comp_state[int(component[e])], 0)
-    return comp_state, forced
+    return NO.constrained_decode(pi, a, b, offsets, obs, component, dtype,
+                                 mm=lambda pi_, a_, b_, o, t, dt: max_marginal(pi_, a_, b_, np.asarray(o), t, dt))
 
 
 def rescore_f64(pi, a, b, obs, path):

@@ -155,6 +155,9 @@ def brute_force(pi, a, b, obs, dtype=np.float64):
 #   U_c(s)   = sum over the component's sequences of round(mu_k(s) * 2^64) as exact
 #              integers (order- and rank-count independent); -inf terms exclude s
 #   s_c      = first argmax of U_c; then a forced decode with s_c at every active position.
+# Several positions per sequence add alpha / segment-table / beta terms and pairwise terms
+# between components (constrained_terms below); the search is then exact over the
+# component groups they link (constrained_solve).
 def forward_last_row(pi, a, b, obs, dtype):
     pi = np.asarray(pi, dtype)
     a = np.asarray(a, dtype)
@@ -185,40 +188,133 @@ def max_marginal(pi, a, b, obs, tk, dtype):
     return (d + beta).astype(dtype)
 
 
-def constrained_decode(pi, a, b, offsets, obs, component, dtype=np.float32):
-    """Returns (comp_state dict, path, score f64 (f64 re-score for f32), status, objective)."""
+def suffix_beta(a, b, obs_after, dtype):
+    """beta[i] = best continuation score after a position in state i over the elements
+    obs_after (0 when empty): g from the reversed pass on a^T, then max_j(g[j] + a[i,j])."""
+    a_ = np.asarray(a, dtype)
+    if len(obs_after) == 0:
+        return np.zeros(a_.shape[0], dtype)
+    g = forward_last_row(np.zeros(a_.shape[0]), np.asarray(a).T, b, obs_after[::-1], dtype)
+    return (g[None, :] + a_).max(axis=1).astype(dtype)
+
+
+def segment_table(a, b, obs_seg, dtype):
+    """M[s, s'] = best score from state s at obs_seg[0] (score 0, no emission there) to
+    state s' at obs_seg[-1], row-A0 recurrence in dtype (the kernel's `start` mode)."""
+    a = np.asarray(a, dtype)
+    b = np.asarray(b, dtype)
+    n = a.shape[0]
+    D = np.full((n, n), -np.inf, dtype)
+    np.fill_diagonal(D, 0)
+    for t in range(1, len(obs_seg)):
+        D = ((D[:, :, None] + a[None, :, :]).max(axis=1) + b[None, :, obs_seg[t]]).astype(dtype)
+    return D
+
+
+def _acc(vec, vals):
+    """vec (list of int|None) += exact units of vals; None (-inf) is sticky."""
+    for s, x in enumerate(vals):
+        u = exact_units(x)
+        vec[s] = None if (u is None or vec[s] is None) else vec[s] + u
+
+
+def constrained_terms(pi, a, b, offsets, obs, component, dtype=np.float32, mm=None):
+    """Exact unary U[c][s] and pairwise P[(c1,c2)][s1][s2] terms (c1 < c2) of the
+    constrained objective (csp.hpp): per sequence with constrained positions t_1 < .. < t_m,
+      m == 1: U[c_1] += mu = dtype(delta_{t_1} + beta)
+      m >= 2: U[c_1] += alpha = delta_{t_1}; U[c_m] += beta; per segment k: M_k into
+              P[(c_k, c_k+1)] (oriented by component id) or its diagonal into U[c_k] when
+              c_k == c_k+1.
+    mm (optional) replaces max_marginal (e.g. a C-accelerated one)."""
     offsets = np.asarray(offsets, np.int64)
     obs = np.asarray(obs, np.int64)
     component = np.asarray(component, np.int64)
     n = np.asarray(a).shape[0]
-    nseq = len(offsets) - 1
-    sums = {}
-    for k in range(nseq):
-        lo, hi = offsets[k], offsets[k + 1]
-        pos = np.nonzero(component[lo:hi] >= 0)[0]
-        if len(pos) == 0:
+    mm = mm or max_marginal
+    U, P = {}, {}
+    for k in range(len(offsets) - 1):
+        lo, hi = int(offsets[k]), int(offsets[k + 1])
+        pos = [int(t) for t in np.nonzero(component[lo:hi] >= 0)[0]]
+        if not pos:
             continue
-        assert len(pos) == 1, "spec covers one active constrained position per sequence"
-        tk = int(pos[0])
-        c = int(component[lo + tk])
-        mu = max_marginal(pi, a, b, obs[lo:hi], tk, dtype)
-        acc = sums.setdefault(c, [0] * n)
-        for s in range(n):
-            u = exact_units(mu[s])
-            if u is None or acc[s] is None:
-                acc[s] = None
-            else:
-                acc[s] += u
-    comp_state = {}
-    for c, acc in sums.items():
-        best = None
-        for s in range(n):
-            if acc[s] is not None and (best is None or acc[s] > acc[best]):
-                best = s
-        comp_state[c] = -1 if best is None else best
-    forced = np.full(len(obs), -1, np.int32)
+        o = obs[lo:hi]
+        cs = [int(component[lo + t]) for t in pos]
+        for c in cs:
+            U.setdefault(c, [0] * n)
+        if len(pos) == 1:
+            _acc(U[cs[0]], mm(pi, a, b, o, pos[0], dtype))
+            continue
+        _acc(U[cs[0]], forward_last_row(pi, a, b, o[:pos[0] + 1], dtype))
+        _acc(U[cs[-1]], suffix_beta(a, b, o[pos[-1] + 1:], dtype))
+        for j in range(len(pos) - 1):
+            M = segment_table(a, b, o[pos[j]:pos[j + 1] + 1], dtype)
+            c1, c2 = cs[j], cs[j + 1]
+            if c1 == c2:
+                _acc(U[c1], np.diag(M))
+                continue
+            if c1 > c2:
+                c1, c2, M = c2, c1, M.T
+            tab = P.setdefault((c1, c2), [[0] * n for _ in range(n)])
+            for s1 in range(n):
+                _acc(tab[s1], M[s1])
+    return U, P
+
+
+def constrained_solve(U, P, n, limit=200000):
+    """Exact maximisation of sum U + sum P, brute force per connected group of components
+    (ascending ids); ties -> lexicographically smallest state vector; -1 for a group with
+    no feasible assignment.  Returns {component: state}."""
+    parent = {c: c for c in U}
+
+    def find(x):
+        while parent[x] != x:
+            x = parent[x]
+        return x
+
+    for c1, c2 in P:
+        parent[find(c1)] = find(c2)
+    groups = {}
+    for c in sorted(U):
+        groups.setdefault(find(c), []).append(c)
+    out = {}
+    for comps in groups.values():
+        assert n ** len(comps) <= limit, "oracle brute force is for small cases"
+        pairs = [(i, j, P[(ci, cj)]) for i, ci in enumerate(comps) for j, cj in enumerate(comps)
+                 if (ci, cj) in P]
+        best, best_v = None, None
+        for st in itertools.product(range(n), repeat=len(comps)):  # lexicographic order
+            v = 0
+            for i, c in enumerate(comps):
+                x = U[c][st[i]]
+                if x is None:
+                    v = None
+                    break
+                v += x
+            if v is None:
+                continue
+            for i, j, tab in pairs:
+                x = tab[st[i]][st[j]]
+                if x is None:
+                    v = None
+                    break
+                v += x
+            if v is not None and (best_v is None or v > best_v):
+                best, best_v = st, v
+        for i, c in enumerate(comps):
+            out[c] = -1 if best is None else best[i]
+    return out
+
+
+def constrained_decode(pi, a, b, offsets, obs, component, dtype=np.float32, mm=None):
+    """The constrained-decode spec: exact terms, exact search.  Returns (comp_state dict,
+    forced[sum T]) -- forced uses 0 for a component without a feasible state (its
+    sequences are then reported infeasible)."""
+    U, P = constrained_terms(pi, a, b, offsets, obs, component, dtype, mm)
+    comp_state = constrained_solve(U, P, np.asarray(a).shape[0])
+    component = np.asarray(component, np.int64)
+    forced = np.full(len(component), -1, np.int32)
     for e in np.nonzero(component >= 0)[0]:
-        forced[e] = comp_state[int(component[e])]
+        forced[e] = max(comp_state[int(component[e])], 0)
     return comp_state, forced
 
 

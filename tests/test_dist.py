@@ -164,7 +164,7 @@ def _partials_worker(rank, world, port, q):
     s0, s1, _ = cvd.shard_range(B, world, rank)
     part = _pack_partials(*_shard_mu(pi, a, b, off, obs, comp, s0, s1), N, NC)
     red = cvd.allreduce_partials(part, dist)
-    states, explored = constrained_select(N, red)  # host-only C-ABI call
+    states, explored = constrained_select(N, NC, red.reshape(-1))  # host-only C-ABI call
     q.put((rank, states.tolist(), explored))
     dist.barrier()
     dist.destroy_process_group()
@@ -212,7 +212,7 @@ def test_constrained_select_limb_carries():
                 exact[c, s] += v
                 part[c, 4 * s:4 * s + 4] += [v & M, (v >> 32) & M, (v >> 64) & M, v >> 96]
     part[1, 4 * n + 2] = 1  # state 2 of component 1 infeasible
-    states, ex = constrained_select(n, part)
+    states, ex = constrained_select(n, ncomp, part.reshape(-1))
     for c in range(ncomp):
         cand = [s for s in range(n) if not (c == 1 and s == 2)]
         best = max(cand, key=lambda s: (exact[c, s], -s))

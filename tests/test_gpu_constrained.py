@@ -116,12 +116,14 @@ def test_constrained_sharded_equals_single(gpu, nshards):
     ncomp = int(comp.max()) + 1
     path, score, status, states, obj = cv.decode_constrained(h, off, obs, comp, ncomp)
     B = len(off) - 1
+    pairs = cv.constrained_pairs(off, comp, ncomp)
     part = 0
     shards = [cvdist.shard_range(B, nshards, r)[:2] for r in range(nshards)]
     for s0, s1 in shards:
         lo, hi = off[s0], off[s1]
-        part = part + cv.constrained_partials(h, cvdist.shard_offsets(off, s0, s1), obs[lo:hi], comp[lo:hi], ncomp)
-    got_states, explored = cv.constrained_select(h.nstates(), part)
+        part = part + cv.constrained_partials(h, cvdist.shard_offsets(off, s0, s1), obs[lo:hi], comp[lo:hi], ncomp,
+                                              pairs)
+    got_states, explored = cv.constrained_select(h.nstates(), ncomp, part, pairs)
     assert np.array_equal(got_states, states)
     assert explored == h.nstates() * len(set(comp[comp >= 0].tolist()))
     for s0, s1 in shards:
@@ -129,3 +131,45 @@ def test_constrained_sharded_equals_single(gpu, nshards):
         p, s, st, _ = cv.decode_forced_components(h, cvdist.shard_offsets(off, s0, s1), obs[lo:hi], comp[lo:hi],
                                                   got_states)
         assert np.array_equal(p, path[lo:hi]) and np.array_equal(s, score[s0:s1]) and np.array_equal(st, status[s0:s1])
+
+
+def _multi_case(n, seed, nseq=16, tmax=24, ncomp=3, maxpos=3, v=7):
+    pi, a, b = synth.random_hmm(n, v, seed=seed)
+    rng = np.random.default_rng(seed)
+    lengths = rng.integers(1, tmax, size=nseq)
+    off = synth.offsets_from_lengths(lengths)
+    obs = rng.integers(0, v, size=int(off[-1])).astype(np.int32)
+    comp = np.full(len(obs), -1, np.int32)
+    for k in range(nseq):
+        m = int(rng.integers(0, maxpos + 1))
+        for t in rng.choice(lengths[k], size=min(m, lengths[k]), replace=False):
+            comp[off[k] + t] = rng.integers(0, ncomp)
+    return pi, a, b, off, obs, comp
+
+
+@pytest.mark.parametrize("n,seed", [(3, 1), (5, 2), (8, 3), (13, 4), (16, 5), (32, 6)])
+def test_constrained_multi_position(gpu, n, seed):
+    """Several constrained positions per sequence: alpha / segment tables (the trellis
+    kernel's `start` mode) / beta terms, pairwise component terms and the exact search;
+    component states equal the spec's, paths bit-exact, scores the f64 re-score."""
+    pi, a, b, off, obs, comp = _multi_case(n, seed, ncomp=3 if n <= 16 else 2)
+    _check(cv.HMM(pi, a, b), pi, a, b, off, obs, comp)
+
+
+def test_constrained_multi_position_sharded(gpu):
+    from cviterbi import dist as cvdist
+
+    pi, a, b, off, obs, comp = _multi_case(6, 9, nseq=30)
+    h = cv.HMM(pi, a, b)
+    ncomp = int(comp.max()) + 1
+    path, score, status, states, obj = cv.decode_constrained(h, off, obs, comp, ncomp)
+    pairs = cv.constrained_pairs(off, comp, ncomp)
+    assert len(pairs) > 0
+    part = 0
+    for r in range(3):
+        s0, s1, _ = cvdist.shard_range(len(off) - 1, 3, r)
+        lo, hi = off[s0], off[s1]
+        part = part + cv.constrained_partials(h, cvdist.shard_offsets(off, s0, s1), obs[lo:hi], comp[lo:hi], ncomp,
+                                              pairs)
+    got, _ = cv.constrained_select(h.nstates(), ncomp, part, pairs)
+    assert np.array_equal(got, states)

@@ -5,6 +5,7 @@ Parity status: the reference (Rust) cannot be built or imported here and has no 
 or fixtures of its own, so the oracle is "parity unpinned" against
 the binary; these tests pin it to the reference's stated semantics instead.
 """
+import itertools
 import math
 
 import numpy as np
@@ -166,7 +167,7 @@ def test_cp_superseq_vs_per_sequence():
 
 
 # ---- consistency-constrained decode spec (np_oracle.constrained_decode) -------------------
-def _constrained_case(seed, n=3, v=4, nseq=6, tmax=6, ncomp=2, p=0.7):
+def _constrained_case(seed, n=3, v=4, nseq=6, tmax=6, ncomp=2, p=0.7, maxpos=1):
     pi, a, b = synth.random_hmm(n, v, seed=seed)
     rng = np.random.default_rng(seed)
     lengths = rng.integers(1, tmax, size=nseq)
@@ -175,7 +176,9 @@ def _constrained_case(seed, n=3, v=4, nseq=6, tmax=6, ncomp=2, p=0.7):
     comp = np.full(len(obs), -1, np.int32)
     for k in range(nseq):
         if rng.random() < p:
-            comp[off[k] + rng.integers(0, lengths[k])] = rng.integers(0, ncomp)
+            m = int(rng.integers(1, maxpos + 1))
+            for t in rng.choice(lengths[k], size=min(m, lengths[k]), replace=False):
+                comp[off[k] + t] = rng.integers(0, ncomp)
     return pi, a, b, off, obs, comp
 
 
@@ -191,8 +194,42 @@ def test_constrained_spec_is_exact_optimum(seed):
     obj = float(np.sum(np.where(st == 0, s, -np.inf)))
     assert obj == pytest.approx(bobj, rel=1e-12)
     for e in np.nonzero(comp >= 0)[0]:
-        k = np.searchsorted(off, e, side="right") - 1
         assert p[e] == states[int(comp[e])]  # every constrained element takes its component's state
+
+
+@pytest.mark.parametrize("seed", range(30))
+def test_constrained_multi_position_spec_is_exact_optimum(seed):
+    """Several constrained positions per sequence (pairwise component terms, segment
+    tables): the spec's exact search reaches the exhaustive optimum over all component-state
+    assignments (f64 objective within 1e-12 rel), with 2-3 components linked in groups."""
+    pi, a, b, off, obs, comp = _constrained_case(seed, n=3, v=4, nseq=5, tmax=8, ncomp=3, p=0.9, maxpos=3)
+    states, forced = NO.constrained_decode(pi, a, b, off, obs, comp, np.float64)
+    p, s, st = C.decode_batch(pi, a, b, off, obs, C.VITERBI, np.float64, forced=forced)
+    _, bobj = NO.constrained_brute(pi, a, b, off, obs, comp, np.float64)
+    obj = float(np.sum(np.where(st == 0, s, -np.inf)))
+    if bobj == -np.inf:
+        assert obj == -np.inf
+    else:
+        assert obj == pytest.approx(bobj, rel=1e-12)
+    for e in np.nonzero(comp >= 0)[0]:
+        assert p[e] == states[int(comp[e])]
+
+
+def test_segment_table_matches_forced_decode():
+    """M[s, s'] (start in s with score 0, run to s') == the forced-decode score of the segment
+    with both ends forced minus nothing: checked against decode_forced with a zero-emission
+    first element (pi = 0 at s), f64."""
+    pi, a, b = synth.random_hmm(4, 5, seed=4)
+    obs = np.array([1, 3, 0, 4, 2], np.int32)
+    M = NO.segment_table(a, b, obs, np.float64)
+    for s in range(4):
+        for s2 in range(4):
+            best = -np.inf
+            for mid in itertools.product(range(4), repeat=len(obs) - 2):
+                path = (s,) + mid + (s2,)
+                v = sum(a[path[t - 1], path[t]] + b[path[t], obs[t]] for t in range(1, len(obs)))
+                best = max(best, v)
+            assert M[s, s2] == pytest.approx(best, abs=1e-12)
 
 
 @pytest.mark.parametrize("seed", range(8))
