@@ -410,14 +410,35 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
   if ((st = h->ws_main.ensure(buf_bytes * nbuf)) != CV_OK) return st;
   if (!use_trellis && (st = h->ws_last.ensure(last_bytes * nbuf)) != CV_OK) return st;
   const int32_t* order_dev = nullptr;
+  // Two equal-length sequences per forward workgroup (trellis_fwd2_f32) where possible:
+  // chunk slots [first, first + 2*npair) hold the pairs, the rest run one per workgroup.
+  const bool pairing = use_trellis && !use_mfma && !o.forced && !(o.flags & CV_FLAG_NO_PAIR) &&
+                       cvk::trellis_pair_supported(h->np);
+  std::vector<int64_t> npair(chunks.size(), 0);
   if (varlen) {
-    // longest-first schedule inside each chunk so the tail of the grid is short sequences
+    // longest-first schedule inside each chunk so the tail of the grid is short sequences;
+    // with pairing, equal-length neighbours are paired first and leftovers go last
     h->order_host.resize((size_t)nseq);
-    for (auto& c : chunks) {
-      std::iota(h->order_host.begin() + c.first, h->order_host.begin() + c.second, (int32_t)c.first);
-      std::stable_sort(h->order_host.begin() + c.first, h->order_host.begin() + c.second, [&](int32_t x, int32_t y) {
-        return (offsets_host[x + 1] - offsets_host[x]) > (offsets_host[y + 1] - offsets_host[y]);
-      });
+    std::vector<int32_t> tail;
+    for (size_t ci = 0; ci < chunks.size(); ++ci) {
+      const auto& c = chunks[ci];
+      auto b = h->order_host.begin() + c.first, e = h->order_host.begin() + c.second;
+      std::iota(b, e, (int32_t)c.first);
+      auto len = [&](int32_t x) { return offsets_host[x + 1] - offsets_host[x]; };
+      std::stable_sort(b, e, [&](int32_t x, int32_t y) { return len(x) > len(y); });
+      if (!pairing) continue;
+      tail.clear();
+      auto out = b;
+      for (auto it = b; it != e;) {
+        if (it + 1 != e && len(*it) == len(*(it + 1))) {
+          *out++ = *it++;
+          *out++ = *it++;
+        } else {
+          tail.push_back(*it++);
+        }
+      }
+      npair[ci] = (out - b) / 2;
+      std::copy(tail.begin(), tail.end(), out);
     }
     if ((st = h->ws_order.ensure((size_t)nseq * 4)) != CV_OK) return st;
     HIP_TRY(hipMemcpyAsync(h->ws_order.p, h->order_host.data(), (size_t)nseq * 4, hipMemcpyHostToDevice, stream));
@@ -457,7 +478,12 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
         fa.a_img = h->t_aimg_mfma.as<float>();
         err = cvk::launch_trellis_mfma(h->np, mt, fa, n, stream);
       } else {
-        err = cvk::launch_trellis_fwd(h->np, fa, n, stream);
+        const int64_t np2 = pairing ? (varlen ? npair[ci] : n / 2) : 0;
+        err = cvk::launch_trellis_fwd2(h->np, fa, np2, stream);
+        if (err == hipSuccess && n > 2 * np2) {
+          fa.seq_begin = c.first + 2 * np2;
+          err = cvk::launch_trellis_fwd(h->np, fa, n - 2 * np2, stream);
+        }
       }
     } else if (o.dtype == CV_DTYPE_F64) {
       cvk::GenericFwdArgs<double> fa{};

@@ -96,6 +96,10 @@ hipError_t launch_max_marginal(int np, const MaxMarginalArgs& a, int64_t ncon, h
 
 int trellis_padded_states(int n);  // 0 if the trellis kernel does not cover n
 hipError_t launch_trellis_fwd(int np, const TrellisFwdArgs& fa, int64_t nseq, hipStream_t stream);
+// Two equal-length sequences per workgroup (slots seq_begin + 2k, +2k+1), plain decode only;
+// NP in {64, 128, 192, 256}.
+bool trellis_pair_supported(int np);
+hipError_t launch_trellis_fwd2(int np, const TrellisFwdArgs& fa, int64_t npairs, hipStream_t stream);
 // MFMA-assisted forward (trellis_mfma_f32): A image in the 32x32 MFMA C/D layout; mt < 0 = default.
 hipError_t launch_trellis_mfma(int np, int mt, const TrellisFwdArgs& fa, int64_t nseq, hipStream_t stream);
 int mfma_default_mt(int np);

@@ -82,7 +82,16 @@ __device__ __forceinline__ float wave_max(float x) {
 // release fence, which waits (vmcnt) for this wave's outstanding GLOBAL stores -- the
 // delta row just written for the backtrack -- adding a store round trip to every step.
 // Nothing in the kernel reads those stores back, so only the LDS writes are drained.
-__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+// The wait is the s_waitcnt builtin (not inline asm) so the compiler's waitcnt pass knows
+// lgkmcnt is 0 after it -- otherwise a scalar load issued before the barrier makes it
+// insert lgkmcnt(0) after the next LDS reads; the empty asm statements keep the compiler
+// from moving memory operations across (the s_barrier builtin itself is not a fence).
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // gfx9 encoding: lgkmcnt(0), vmcnt/expcnt unconstrained
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
 
 // Padded LDS stride (floats) of one row-group block of delta: conflict-free
 // ds_read_b128 for the 8 row-group addresses of a lane group (checked exhaustively).
@@ -267,6 +276,170 @@ __global__ __launch_bounds__(NP * 4) void trellis_fwd_f32(TrellisFwdArgs args) {
     step(t + 1, eB, eA);
   }
   if (bad && lane == 0 && w == 0) args.status[seq] = CVK_SEQ_BADOBS;
+}
+
+// ---------------------------------------------------------------------------------
+// trellis_fwd2_f32<NP>: the same recurrence for TWO sequences (X, Y) of equal length per
+// workgroup, in alternating half-steps X(t), Y(t), one barrier after each.  Each half-step
+// reads the first half of the lane's delta rows from registers prefetched during the
+// previous half-step (the other sequence's data, complete since the last barrier), so the
+// LDS latency after a barrier -- the bubble of the one-sequence kernel, where all four
+// waves of a SIMD wait for their first ds_read together -- is hidden; the second half is
+// loaded at the start of the half-step behind the first half's adds.  Same registers as
+// the one-sequence kernel (A image 64 + delta 32 at NP = 256).  Plain decode only (no EXT
+// features); the host pairs equal-length sequences and runs leftovers through
+// trellis_fwd_f32.  NP % 64 == 0 so that each half is whole float4s.
+template <int NP>
+__global__ __launch_bounds__(NP * 4) void trellis_fwd2_f32(TrellisFwdArgs args) {
+  using G = TrellisGeom<NP>;
+  constexpr int R = G::R;
+  constexpr int S = G::S;
+  constexpr int H = R / 2;
+  static_assert(H % 4 == 0, "pair kernel needs NP % 64 == 0");
+  __shared__ __attribute__((aligned(16))) float lds[2][2][G::LDS_FLOATS];  // [X/Y][buffer]
+
+  const int lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
+  const int rg = lane & 7;
+  const int cp = lane >> 3;
+  const int j0 = 16 * w + 2 * cp;
+
+  const int64_t slot = args.seq_begin + 2 * (int64_t)blockIdx.x;
+  int64_t seq[2], e0[2];
+  int Ts[2];
+  seq_range<false>(args, slot, seq[0], e0[0], Ts[0]);
+  seq_range<false>(args, slot + 1, seq[1], e0[1], Ts[1]);
+  const int T = Ts[0];  // host guarantees Ts[0] == Ts[1]
+  if (T <= 0) return;
+  typedef const __attribute__((address_space(4))) int32_t* cobs_t;
+  const cobs_t obsX = (cobs_t)(args.obs + e0[0]);
+  const cobs_t obsY = (cobs_t)(args.obs + e0[1]);
+  // uniform row bases (SGPRs); the lane adds j0
+  float* const dX = args.delta + (e0[0] - args.delta_elem_base) * NP;
+  float* const dY = args.delta + (e0[1] - args.delta_elem_base) * NP;
+  const unsigned V = (unsigned)args.nobs;
+
+  float a_reg[2 * R];
+  {
+    const float4* img = reinterpret_cast<const float4*>(args.a_img) + (size_t)w * (R / 2) * 64 + lane;
+#pragma unroll
+    for (int q = 0; q < R / 2; ++q) {
+      const float4 v = img[q * 64];
+      a_reg[4 * q + 0] = v.x;
+      a_reg[4 * q + 1] = v.y;
+      a_reg[4 * q + 2] = v.z;
+      a_reg[4 * q + 3] = v.w;
+    }
+  }
+  unsigned bad = 0;  // bit 0: X, bit 1: Y
+  auto obs_x = [&](int t) -> unsigned {
+    const unsigned o = (unsigned)obsX[t];
+    bad |= (o >= V) ? 1u : 0u;
+    return o < V ? o : 0u;
+  };
+  auto obs_y = [&](int t) -> unsigned {
+    const unsigned o = (unsigned)obsY[t];
+    bad |= (o >= V) ? 2u : 0u;
+    return o < V ? o : 0u;
+  };
+  auto et_row = [&](unsigned o) -> float2 { return *reinterpret_cast<const float2*>(args.et + (size_t)o * NP + j0); };
+  const int lds_w = (j0 / R) * S + (j0 % R);
+  auto clampT = [&](int t) { return t < T ? t : T - 1; };
+
+  // ---- t = 0 for both sequences ----
+  {
+    const float2 ex = et_row(obs_x(0)), ey = et_row(obs_y(0));
+    const float p0 = args.pi[j0], p1 = args.pi[j0 + 1];
+    const float2 dx = make_float2(p0 + ex.x, p1 + ex.y), dy = make_float2(p0 + ey.x, p1 + ey.y);
+    if (rg == 0) {
+      *reinterpret_cast<float2*>(&lds[0][0][lds_w]) = dx;
+      *reinterpret_cast<float2*>(&lds[1][0][lds_w]) = dy;
+      *reinterpret_cast<float2*>(dX + j0) = dx;
+      *reinterpret_cast<float2*>(dY + j0) = dy;
+    }
+  }
+  // Emission rows are loaded one HALF-step ahead (during the other sequence's half-step):
+  // eX is loaded in Y(t-1) and used in X(t), eY loaded in X(t) and used in Y(t), so at each
+  // use exactly two newer vector-memory ops are in flight (vmcnt(2), no store drain).  The
+  // scalar obs loads are issued at the END of a half-step, so the barrier's lgkmcnt(0)
+  // retires them and the compiler's own wait for them (at the next emission load) comes
+  // before that half-step's LDS reads -- an SMEM load in flight would otherwise force an
+  // lgkmcnt(0) on the prefetched rows and expose the LDS latency again.
+  float2 eX = et_row(obs_x(clampT(1)));  // X at t = 1
+  float2 eY;
+  unsigned oY = obs_y(clampT(1));  // o_Y(t) for the coming X(t)
+  unsigned oX = obs_x(clampT(2));  // o_X(t+1) for the coming Y(t)
+  lds_barrier();
+  float4 P[H / 4];  // rows [0, H) of the next half-step's delta (prefetched)
+#pragma unroll
+  for (int q = 0; q < H / 4; ++q) P[q] = *reinterpret_cast<const float4*>(&lds[0][0][rg * S + 4 * q]);
+
+  // One half-step at step t: dsrc = this sequence's delta_{t-1} block, nsrc = the block the
+  // next half-step reads first (prefetched into P once P's rows are consumed); e_use = this
+  // half-step's emission row, e_load <- the next half-step's (row o_load); then o_load <-
+  // obs(t_obs) of the sequence `is_y`.
+  auto half = [&](const float* dsrc, const float* nsrc, float* ldst, float* drow, int t, const float2& e_use,
+                  float2& e_load, unsigned& o_load, bool is_y, int t_obs) {
+    e_load = et_row(o_load);
+    float4 Q[H / 4];
+#pragma unroll
+    for (int q = 0; q < H / 4; ++q) Q[q] = *reinterpret_cast<const float4*>(dsrc + H + 4 * q);
+    float m0a = ninf_f(), m0b = ninf_f(), m1a = ninf_f(), m1b = ninf_f();
+    auto rows4 = [&](const float4& dd, int k, bool first) {
+      // s_i = d[i] + a[i,j]  (viterbi.rs:15) for rows k..k+3 of this lane, columns j0, j0+1
+      const float s00 = dd.x + a_reg[2 * k + 0], s01 = dd.x + a_reg[2 * k + 1];
+      const float s10 = dd.y + a_reg[2 * k + 2], s11 = dd.y + a_reg[2 * k + 3];
+      const float s20 = dd.z + a_reg[2 * k + 4], s21 = dd.z + a_reg[2 * k + 5];
+      const float s30 = dd.w + a_reg[2 * k + 6], s31 = dd.w + a_reg[2 * k + 7];
+      if (first) {
+        m0a = fmaxf(s00, s10);
+        m1a = fmaxf(s01, s11);
+        m0b = fmaxf(s20, s30);
+        m1b = fmaxf(s21, s31);
+      } else {
+        m0a = fmaxf(fmaxf(m0a, s00), s10);
+        m1a = fmaxf(fmaxf(m1a, s01), s11);
+        m0b = fmaxf(fmaxf(m0b, s20), s30);
+        m1b = fmaxf(fmaxf(m1b, s21), s31);
+      }
+    };
+#pragma unroll
+    for (int q = 0; q < H / 4; ++q) rows4(P[q], 4 * q, q == 0);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int q = 0; q < H / 4; ++q) P[q] = *reinterpret_cast<const float4*>(nsrc + 4 * q);
+#pragma unroll
+    for (int q = 0; q < H / 4; ++q) rows4(Q[q], H + 4 * q, false);
+    float m0 = fmaxf(m0a, m0b);
+    float m1 = fmaxf(m1a, m1b);
+    m0 = octet_max(m0);  // fold the 8 row groups of column j0
+    m1 = octet_max(m1);
+    const float2 dn = make_float2(m0 + e_use.x, m1 + e_use.y);  // (d + a) + b, viterbi.rs:15-17
+    __builtin_amdgcn_sched_barrier(0);
+    o_load = is_y ? obs_y(t_obs) : obs_x(t_obs);
+    if (rg == 0) {
+      *reinterpret_cast<float2*>(ldst + lds_w) = dn;
+      *reinterpret_cast<float2*>(drow + (size_t)t * NP + j0) = dn;
+    }
+    lds_barrier();
+  };
+  // step t: X(t) prefetches Y's delta_{t-1} and loads e_Y(t); Y(t) prefetches X's delta_t and
+  // loads e_X(t+1)
+  auto step = [&](int t) {
+    const int cur = (t - 1) & 1, nxt = t & 1;
+    half(&lds[0][cur][rg * S], &lds[1][cur][rg * S], &lds[0][nxt][0], dX, t, eX, eY, oY, true, clampT(t + 1));
+    half(&lds[1][cur][rg * S], &lds[0][nxt][rg * S], &lds[1][nxt][0], dY, t, eY, eX, oX, false, clampT(t + 2));
+  };
+  int t = 1;
+  if ((T - 1) & 1) step(t++);
+  for (; t + 1 < T; t += 2) {
+    step(t);
+    step(t + 1);
+  }
+  if (bad && lane == 0 && w == 0) {
+    if (bad & 1u) args.status[seq[0]] = CVK_SEQ_BADOBS;
+    if (bad & 2u) args.status[seq[1]] = CVK_SEQ_BADOBS;
+  }
 }
 
 // ---------------------------------------------------------------------------------
@@ -873,6 +1046,26 @@ int trellis_padded_states(int n) {
     case 256: return CALL(256);     \
     default: return hipErrorInvalidValue; \
   }
+
+template <int NP>
+static hipError_t trellis_fwd2_np(const TrellisFwdArgs& fa, int64_t npairs, hipStream_t stream) {
+  if constexpr (NP % 64 != 0) {
+    return hipErrorInvalidValue;
+  } else {
+    if (ext_args(fa)) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(trellis_fwd2_f32<NP>, dim3((unsigned)npairs), dim3(NP * 4), 0, stream, fa);
+    return hipGetLastError();
+  }
+}
+
+bool trellis_pair_supported(int np) { return np >= 64 && np <= 256 && np % 64 == 0; }
+
+hipError_t launch_trellis_fwd2(int np, const TrellisFwdArgs& fa, int64_t npairs, hipStream_t stream) {
+  if (npairs <= 0) return hipSuccess;
+#define CVK_FWD2(NP) trellis_fwd2_np<NP>(fa, npairs, stream)
+  CVK_NP_SWITCH(np, CVK_FWD2)
+#undef CVK_FWD2
+}
 
 hipError_t launch_trellis_fwd(int np, const TrellisFwdArgs& fa, int64_t nseq, hipStream_t stream) {
   if (nseq <= 0) return hipSuccess;

@@ -21,6 +21,7 @@ DTYPE_F32, DTYPE_F64 = 0, 1
 ASSOC_VITERBI, ASSOC_CP, ASSOC_DP, ASSOC_DECODE = 0, 1, 2, 3
 KERNEL_AUTO, KERNEL_TRELLIS, KERNEL_GENERIC = 0, 1, 2
 FLAG_MFMA_TRELLIS = 0x1
+FLAG_NO_PAIR = 0x4
 FLAG_SERIAL = 0x2
 
 

@@ -52,7 +52,7 @@ def test_trellis_f32_bit_exact(gpu, n):
 
 
 @pytest.mark.parametrize("n", [40, 64, 100, 128, 160, 200, 224, 256])
-@pytest.mark.parametrize("variant", ["valu", "mfma"])
+@pytest.mark.parametrize("variant", ["valu", "valu1", "mfma"])
 @pytest.mark.parametrize("serial", [False, True])
 def test_trellis_variants_bit_exact(gpu, n, variant, serial):
     """Both trellis variants (all-VALU; MFMA-assisted, whose MFMA tiles compute
@@ -66,6 +66,29 @@ def test_trellis_variants_bit_exact(gpu, n, variant, serial):
     t = cv.last_timing(h)
     assert (t["mfma_tiles"] >= 0) == (variant == "mfma" and t["padded_states"] >= 64)
     _assert_same(got, ref, f"{variant} N={n} serial={serial}")
+
+
+@pytest.mark.parametrize("n", [45, 64, 128, 192, 256])
+@pytest.mark.parametrize("serial", [False, True])
+def test_pair_kernel_equal_and_ragged(gpu, n, serial):
+    """Two sequences per workgroup (trellis_fwd2_f32): lengths from a small set so most
+    sequences pair with an equal-length neighbour, an odd leftover per length, T = 1 and 2
+    (no or one step), zeros in A -- bit-identical to the oracle and to one per workgroup."""
+    pi, a, b = synth.random_hmm(n, 23, seed=n, zero_frac=0.02)
+    rng = np.random.default_rng(n)
+    off = synth.offsets_from_lengths(rng.choice([1, 2, 3, 17, 64], size=37))
+    obs = rng.integers(0, 23, size=int(off[-1])).astype(np.int32)
+    h = cv.HMM(pi, a, b)
+    ref = O.decode_batch(pi, a, b, off, obs, O.VITERBI, np.float32)
+    ws = 0 if serial else n * 4 * 400
+    for variant in ("valu", "valu1"):
+        got = cv.decode_batch(h, off, obs, rescore_f64=False, variant=variant, serial=serial, workspace_bytes=ws)
+        _assert_same(got, ref, f"{variant} N={n} serial={serial}")
+    # equal lengths, odd count: pairs (2k, 2k+1) straight from the CSR order, one single
+    off2 = synth.offsets_from_lengths(np.full(9, 33))
+    obs2 = rng.integers(0, 23, size=int(off2[-1])).astype(np.int32)
+    ref2 = O.decode_batch(pi, a, b, off2, obs2, O.VITERBI, np.float32)
+    _assert_same(cv.decode_batch(h, off2, obs2, rescore_f64=False, serial=serial), ref2, f"equal N={n}")
 
 
 @pytest.mark.parametrize("mt", [0, 4, 5, 6, 7, 8])

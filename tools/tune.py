@@ -18,6 +18,8 @@ from cviterbi import synth  # noqa: E402
 B = int(os.environ.get("TUNE_B", "65536"))
 ROUNDS = int(os.environ.get("TUNE_ROUNDS", "3"))
 VARIANTS = [
+    dict(name="valu1-serial", variant="valu1", serial=True),
+    dict(name="valu1-overlap", variant="valu1", serial=False),
     dict(name="valu-serial", variant="valu", serial=True),
     dict(name="valu-overlap", variant="valu", serial=False),
     dict(name="mfma0-serial", mfma_tiles=0, serial=True),
