@@ -303,6 +303,7 @@ __global__ __launch_bounds__(NP * 4) void trellis_fwd2_f32(TrellisFwdArgs args) 
   const int rg = lane & 7;
   const int cp = lane >> 3;
   const int j0 = 16 * w + 2 * cp;
+  const unsigned ju = (unsigned)j0;  // unsigned lane offset: uniform base (SGPRs) + 32-bit VGPR offset
 
   const int64_t slot = args.seq_begin + 2 * (int64_t)blockIdx.x;
   int64_t seq[2], e0[2];
@@ -342,7 +343,10 @@ __global__ __launch_bounds__(NP * 4) void trellis_fwd2_f32(TrellisFwdArgs args) 
     bad |= (o >= V) ? 2u : 0u;
     return o < V ? o : 0u;
   };
-  auto et_row = [&](unsigned o) -> float2 { return *reinterpret_cast<const float2*>(args.et + (size_t)o * NP + j0); };
+  auto et_row = [&](unsigned o) -> float2 {
+    const float* row = args.et + (size_t)o * NP;  // uniform
+    return *reinterpret_cast<const float2*>(row + ju);
+  };
   const int lds_w = (j0 / R) * S + (j0 % R);
   auto clampT = [&](int t) { return t < T ? t : T - 1; };
 
@@ -354,8 +358,8 @@ __global__ __launch_bounds__(NP * 4) void trellis_fwd2_f32(TrellisFwdArgs args) 
     if (rg == 0) {
       *reinterpret_cast<float2*>(&lds[0][0][lds_w]) = dx;
       *reinterpret_cast<float2*>(&lds[1][0][lds_w]) = dy;
-      *reinterpret_cast<float2*>(dX + j0) = dx;
-      *reinterpret_cast<float2*>(dY + j0) = dy;
+      *reinterpret_cast<float2*>(dX + ju) = dx;
+      *reinterpret_cast<float2*>(dY + ju) = dy;
     }
   }
   // Emission rows are loaded one HALF-step ahead (during the other sequence's half-step):
@@ -419,7 +423,8 @@ __global__ __launch_bounds__(NP * 4) void trellis_fwd2_f32(TrellisFwdArgs args) 
     o_load = is_y ? obs_y(t_obs) : obs_x(t_obs);
     if (rg == 0) {
       *reinterpret_cast<float2*>(ldst + lds_w) = dn;
-      *reinterpret_cast<float2*>(drow + (size_t)t * NP + j0) = dn;
+      float* row = drow + (size_t)t * NP;  // uniform
+      *reinterpret_cast<float2*>(row + ju) = dn;
     }
     lds_barrier();
   };
@@ -705,8 +710,8 @@ __device__ double rescore_path_f64(const int32_t* path, const int32_t* obs, int 
   return d;
 }
 
-// One wave per sequence.  delta rows are independent of the path, so they are prefetched
-// PF steps ahead into a register ring; only the transition column a[:, path[t]] is a
+// One wave per sequence.  delta rows are independent of the path, so they are loaded PF
+// rows at a time into a register ring; only the transition column a[:, path[t]] is a
 // dependent (L2-resident) load.  First argmax = DPP/permlane wave max, then a ballot of
 // the lanes holding it (lowest lane of the lowest k = lowest state index).
 template <int NP>
@@ -780,7 +785,6 @@ __global__ __launch_bounds__(256) void backtrack_f32(BacktrackArgs args) {
         float s[KP];
 #pragma unroll
         for (int k = 0; k < KP; ++k) s[k] = valid[k] ? ring[u][k] + acol[64 * k] : ninf_f();
-        load_row(t - 1 - PF, ring[u]);  // refill: used again PF steps later
         float m = s[0];
 #pragma unroll
         for (int k = 1; k < KP; ++k) m = fmaxf(m, s[k]);
@@ -797,6 +801,11 @@ __global__ __launch_bounds__(256) void backtrack_f32(BacktrackArgs args) {
         if ((tp & 63) == 0 && tp + lane < T) path[tp + lane] = pathreg;  // flush a 64-entry block
       }
     }
+    // Refill the whole ring once per block.  Vector-memory loads retire in order, so a
+    // per-step refill would make every step's dependent a-column load wait for the
+    // previous step's HBM row load; in bulk, only the block's first step waits for HBM.
+#pragma unroll
+    for (int u = 0; u < PF; ++u) load_row(base - PF - 1 - u, ring[u]);
   }
   if (lane == 0) {
     args.status[seq] = CVK_SEQ_OK;
