@@ -548,7 +548,8 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
       // overlap mode: at most ONE backtrack workgroup (one 64-VGPR wave per SIMD) per CU, so
       // the next forward workgroup (MFMA: 2 waves x 200 VGPRs per SIMD; VALU: 4 x 104) always
       // finds its registers free: reserve 100 KiB of LDS (2 x 100 > 160 KiB)
-      const int reserve = serial ? 0 : 100 * 1024;
+      // the last chunk's backtrack has the device to itself: full occupancy
+      const int reserve = (serial || ci + 1 == chunks.size()) ? 0 : 100 * 1024;
       err = cvk::launch_trellis_bt(h->np, ba, n, bts, reserve);
     } else if (o.dtype == CV_DTYPE_F64) {
       cvk::GenericBtArgs<double> ba{};

@@ -374,20 +374,28 @@ __global__ __launch_bounds__(NP * 4) void trellis_fwd2_f32(TrellisFwdArgs args) 
   unsigned oY = obs_y(clampT(1));  // o_Y(t) for the coming X(t)
   unsigned oX = obs_x(clampT(2));  // o_X(t+1) for the coming Y(t)
   lds_barrier();
-  float4 P[H / 4];  // rows [0, H) of the next half-step's delta (prefetched)
-#pragma unroll
-  for (int q = 0; q < H / 4; ++q) P[q] = *reinterpret_cast<const float4*>(&lds[0][0][rg * S + 4 * q]);
+  // delta rows stream through a rolling window of two 8-row blocks (P, Q): block k of the
+  // lane's R rows lives in P for even k, Q for odd k, and each block is refilled with block
+  // k+2 as soon as it is consumed, so a load always has the next block's adds to hide
+  // behind.  Block 0 of the NEXT half-step (the other sequence's delta, complete since the
+  // last barrier) goes into P while this half-step's last block is processed.  16 VGPRs of
+  // delta instead of 32: 4 waves x <=112 VGPRs leave a backtrack wave room on every SIMD.
+  constexpr int KB = R / 8;  // 8-row blocks per lane
+  static_assert(R % 8 == 0, "pair kernel needs NP % 64 == 0");
+  auto ld8 = [&](const float* src, float4 (&dst)[2]) {
+    dst[0] = *reinterpret_cast<const float4*>(src);
+    dst[1] = *reinterpret_cast<const float4*>(src + 4);
+  };
+  float4 P[2], Q[2];
+  ld8(&lds[0][0][rg * S], P);
 
   // One half-step at step t: dsrc = this sequence's delta_{t-1} block, nsrc = the block the
-  // next half-step reads first (prefetched into P once P's rows are consumed); e_use = this
-  // half-step's emission row, e_load <- the next half-step's (row o_load); then o_load <-
-  // obs(t_obs) of the sequence `is_y`.
+  // next half-step reads first; e_use = this half-step's emission row, e_load <- the next
+  // half-step's (row o_load); then o_load <- obs(t_obs) of the sequence `is_y`.
   auto half = [&](const float* dsrc, const float* nsrc, float* ldst, float* drow, int t, const float2& e_use,
                   float2& e_load, unsigned& o_load, bool is_y, int t_obs) {
     e_load = et_row(o_load);
-    float4 Q[H / 4];
-#pragma unroll
-    for (int q = 0; q < H / 4; ++q) Q[q] = *reinterpret_cast<const float4*>(dsrc + H + 4 * q);
+    if (KB > 1) ld8(dsrc + 8, Q);
     float m0a = ninf_f(), m0b = ninf_f(), m1a = ninf_f(), m1b = ninf_f();
     auto rows4 = [&](const float4& dd, int k, bool first) {
       // s_i = d[i] + a[i,j]  (viterbi.rs:15) for rows k..k+3 of this lane, columns j0, j0+1
@@ -408,12 +416,17 @@ __global__ __launch_bounds__(NP * 4) void trellis_fwd2_f32(TrellisFwdArgs args) 
       }
     };
 #pragma unroll
-    for (int q = 0; q < H / 4; ++q) rows4(P[q], 4 * q, q == 0);
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int q = 0; q < H / 4; ++q) P[q] = *reinterpret_cast<const float4*>(nsrc + 4 * q);
-#pragma unroll
-    for (int q = 0; q < H / 4; ++q) rows4(Q[q], H + 4 * q, false);
+    for (int k = 0; k < KB; ++k) {
+      float4(&B)[2] = (k & 1) ? Q : P;
+      rows4(B[0], 8 * k, k == 0);
+      rows4(B[1], 8 * k + 4, false);
+      __builtin_amdgcn_sched_barrier(0);
+      if (k + 2 < KB)
+        ld8(dsrc + 8 * (k + 2), B);
+      else if (!(k & 1) && (k + 2 == KB || k + 1 == KB))
+        ld8(nsrc, P);  // next half-step's block 0 (KB odd: no adds left to hide it)
+      __builtin_amdgcn_sched_barrier(0);
+    }
     float m0 = fmaxf(m0a, m0b);
     float m1 = fmaxf(m1a, m1b);
     m0 = octet_max(m0);  // fold the 8 row groups of column j0

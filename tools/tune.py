@@ -63,12 +63,12 @@ for r in range(ROUNDS + 1):
             for x, y in zip(out, ref):
                 assert np.array_equal(x, y), f"variant {v['name']} differs"
         if r > 0:
-            res[v["name"]].append((wall, t["fwd_ms"], t["bt_ms"], t["launches"], t["mfma_tiles"]))
+            res[v["name"]].append((wall, t["fwd_ms"], t["bt_ms"], t["launches"], t["mfma_tiles"], t["total_ms"]))
 summary = {}
 for name, rows in res.items():
     a = np.array(rows)
     summary[name] = dict(wall_ms=float(np.median(a[:, 0])), fwd_ms=float(np.median(a[:, 1])),
-                         bt_ms=float(np.median(a[:, 2])), launches=int(a[0, 3]), mfma_tiles=int(a[0, 4]))
+                         bt_ms=float(np.median(a[:, 2])), total_ms=float(np.median(a[:, 5])), launches=int(a[0, 3]), mfma_tiles=int(a[0, 4]))
     print(f"{name:16s} wall {summary[name]['wall_ms']:8.2f} ms  fwd {summary[name]['fwd_ms']:8.2f}  "
-          f"bt {summary[name]['bt_ms']:7.2f}  launches {summary[name]['launches']}", flush=True)
+          f"bt {summary[name]['bt_ms']:7.2f}  gpu-total {summary[name]['total_ms']:7.2f}  launches {summary[name]['launches']}", flush=True)
 print(json.dumps(dict(B=B, rounds=ROUNDS, results=summary)))
