@@ -95,6 +95,7 @@ struct cv_hmm {
   int64_t V = 0;
   std::vector<double> pi, a, b;  // host log10, canonical (-0.0 -> +0.0); b state-major [N*V]
   int device = 0;
+  int cus = 0;                      // compute units of the device (workgroup rounds)
   hipStream_t stream = nullptr;     // default stream of the handle
   hipStream_t bt_stream = nullptr;  // backtrack stream (overlaps the next chunk's forward)
   std::mutex mu;
@@ -139,6 +140,7 @@ cv_status set_device(cv_hmm* h) {
   }
   if (h->device < 0 || h->device >= n) return set_err(CV_EDEVICE, "device %d out of range (%d devices)", h->device, n);
   HIP_TRY(hipSetDevice(h->device));
+  if (!h->cus) HIP_TRY(hipDeviceGetAttribute(&h->cus, hipDeviceAttributeMultiprocessorCount, h->device));
   if (!h->stream) HIP_TRY(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
   if (!h->bt_stream) HIP_TRY(hipStreamCreateWithFlags(&h->bt_stream, hipStreamNonBlocking));
   return CV_OK;
@@ -373,6 +375,10 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
   // At least ~2,048 sequences per chunk (8 per CU), at most 8 chunks unless the
   // workspace cap forces more.
   const bool serial = (o.flags & CV_FLAG_SERIAL) != 0;
+  // Sequences per forward workgroup: 2 (trellis_fwd2_f32, equal-length pairs; default) or 1
+  // (trellis_fwd_f32: leftovers, EXT features, MFMA, N not a multiple of 64).
+  const bool plain = use_trellis && !use_mfma && !o.forced && cvk::trellis_pair_supported(h->np);
+  const int group = (!plain || (o.flags & CV_FLAG_NO_PAIR)) ? 1 : 2;
   const uint64_t half_cap = std::max<uint64_t>(serial ? cap : cap / 2, per_elem);
   uint64_t nchunks = std::max<uint64_t>(1, (total_elems * per_elem + half_cap - 1) / half_cap);
   if (!serial) nchunks = std::max<uint64_t>(nchunks, std::min<uint64_t>(8, (uint64_t)(nseq / 2048)));
@@ -395,6 +401,22 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
       s0 = s1;
     }
   }
+  {
+    // Equal lengths: whole rounds of workgroups (group x CUs sequences) per chunk, so only
+    // the last chunk ends on a partly filled round (a chunk's launch waits for the last).
+    const int64_t T0c = offsets_host[1] - offsets_host[0];
+    bool uniform = T0c > 0;
+    for (int64_t s = 1; s < nseq && uniform; ++s) uniform = (offsets_host[s + 1] - offsets_host[s]) == T0c;
+    const int64_t unit = group * (int64_t)std::max(h->cus, 1);
+    if (uniform && chunks.size() > 1) {
+      const int64_t cap_seqs = std::max<int64_t>((int64_t)(elem_cap / (uint64_t)T0c), 1);
+      int64_t per = (nseq + (int64_t)chunks.size() - 1) / (int64_t)chunks.size();
+      per = ((per + unit - 1) / unit) * unit;
+      if (per > cap_seqs) per = cap_seqs >= unit ? (cap_seqs / unit) * unit : cap_seqs;
+      chunks.clear();
+      for (int64_t s0 = 0; s0 < nseq; s0 += per) chunks.emplace_back(s0, std::min(nseq, s0 + per));
+    }
+  }
   uint64_t max_elems = 0;
   int64_t max_seqs = 0;
   bool varlen = false;
@@ -410,10 +432,9 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
   if ((st = h->ws_main.ensure(buf_bytes * nbuf)) != CV_OK) return st;
   if (!use_trellis && (st = h->ws_last.ensure(last_bytes * nbuf)) != CV_OK) return st;
   const int32_t* order_dev = nullptr;
-  // Two equal-length sequences per forward workgroup (trellis_fwd2_f32) where possible:
-  // chunk slots [first, first + 2*npair) hold the pairs, the rest run one per workgroup.
-  const bool pairing = use_trellis && !use_mfma && !o.forced && !(o.flags & CV_FLAG_NO_PAIR) &&
-                       cvk::trellis_pair_supported(h->np);
+  // group == 2: chunk slots [first, first + 2*npair) hold equal-length pairs, the rest run
+  // one per workgroup.
+  const bool pairing = group == 2;
   std::vector<int64_t> npair(chunks.size(), 0);
   if (varlen) {
     // longest-first schedule inside each chunk so the tail of the grid is short sequences;

@@ -89,7 +89,9 @@ __device__ __forceinline__ float wave_max(float x) {
 __device__ __forceinline__ void lds_barrier() {
   asm volatile("" ::: "memory");
   __builtin_amdgcn_s_waitcnt(0xC07F);  // gfx9 encoding: lgkmcnt(0), vmcnt/expcnt unconstrained
+#ifndef CVK_ABLATE_NOBAR  // tools/microbench/fwd_ablate.hip only: timing without the barrier
   __builtin_amdgcn_s_barrier();
+#endif
   asm volatile("" ::: "memory");
 }
 
@@ -121,6 +123,25 @@ __device__ __forceinline__ void seq_range(const TrellisFwdArgs& args, int64_t sl
   }
 }
 
+// Column fold of the forward kernels: a lane's two column partials are folded
+// together -- lanes rg < 4 end with column j0, rg >= 4 with column j0+1; the first level
+// (row_half_mirror pairs rg with 7-rg, i.e. the other half) brings in the other column --
+// so 3 DPP maxima + 2 selects replace octet_max on both columns (6 DPP maxima).
+__device__ __forceinline__ float dpp_max_mirror(float mine, float other) {
+  asm volatile("s_nop 1\n\tv_max_f32_dpp %0, %1, %0 row_half_mirror row_mask:0xf bank_mask:0xf"
+               : "+v"(mine)
+               : "v"(other));
+  return mine;
+}
+__device__ __forceinline__ float dpp_max_xor1(float x) {
+  asm volatile("s_nop 1\n\tv_max_f32_dpp %0, %0, %0 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf" : "+v"(x));
+  return x;
+}
+__device__ __forceinline__ float dpp_max_xor2(float x) {
+  asm volatile("s_nop 1\n\tv_max_f32_dpp %0, %0, %0 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf" : "+v"(x));
+  return x;
+}
+
 // EXT = false: the plain decode (no forced states, CSR ranges, forward order, no final-row
 // output) -- the extra features cost registers, so they are a separate instantiation.
 template <int NP, bool EXT>
@@ -135,6 +156,9 @@ __global__ __launch_bounds__(NP * 4) void trellis_fwd_f32(TrellisFwdArgs args) {
   const int rg = lane & 7;
   const int cp = lane >> 3;
   const int j0 = 16 * w + 2 * cp;
+  const bool hi = rg >= 4;  // column of this lane after the fold: j0 + hi
+  const int jw = j0 + (hi ? 1 : 0);
+  const bool writer = (rg & 3) == 0;  // rg 0 stores column j0, rg 4 column j0 + 1
 
   const int64_t slot = args.seq_begin + blockIdx.x;
   int64_t seq, e0;
@@ -150,9 +174,9 @@ __global__ __launch_bounds__(NP * 4) void trellis_fwd_f32(TrellisFwdArgs args) {
       (const __attribute__((address_space(4))) int32_t*)(args.obs + ob0);
   const __attribute__((address_space(4))) int32_t* frc =
       (const __attribute__((address_space(4))) int32_t*)((EXT && args.forced) ? args.forced + ob0 : nullptr);
-  float* __restrict__ drow = (!EXT || args.delta) ? args.delta + (e0 - args.delta_elem_base) * NP + j0 : nullptr;
-  float* __restrict__ lrow = (EXT && args.last_row) ? args.last_row + (slot - args.seq_begin) * NP + j0 : nullptr;
-  const float* __restrict__ etj = args.et + j0;
+  float* __restrict__ drow = (!EXT || args.delta) ? args.delta + (e0 - args.delta_elem_base) * NP + jw : nullptr;
+  float* __restrict__ lrow = (EXT && args.last_row) ? args.last_row + (slot - args.seq_begin) * NP + jw : nullptr;
+  const float* __restrict__ etj = args.et + jw;
   const unsigned V = (unsigned)args.nobs;
 
   // A register image: float4 q of a lane = (A[rg*R+2q][j0], A[rg*R+2q][j0+1],
@@ -180,54 +204,49 @@ __global__ __launch_bounds__(NP * 4) void trellis_fwd_f32(TrellisFwdArgs args) {
     return o < V ? o : 0u;
   };
   auto frc_s = [&](int t) -> int { return (EXT && frc) ? frc[t * ob_step] : -1; };
-  auto et_row = [&](unsigned o) -> float2 { return *reinterpret_cast<const float2*>(etj + (size_t)o * NP); };
+  auto et_row = [&](unsigned o) -> float { return etj[(size_t)o * NP]; };
   // forced state (consistency constraint): every other state of that element is impossible
-  auto force = [&](float2 d, int f) -> float2 {
-    if (EXT && f >= 0) {
-      d.x = (j0 == f) ? d.x : ninf_f();
-      d.y = (j0 + 1 == f) ? d.y : ninf_f();
-    }
-    return d;
-  };
+  auto force = [&](float d, int f) -> float { return (EXT && f >= 0 && jw != f) ? ninf_f() : d; };
 
-  const int lds_w = (j0 / R) * S + (j0 % R);
+  const int lds_w = (j0 / R) * S + (j0 % R) + (hi ? 1 : 0);
   // ---- t = 0: d0 = pi + b[:,o0]  (hmm.rs:415-418, cp.rs:98-100) ----
   {
-    const float2 e = et_row(obs_s(0));
-    float2 d0;
-    d0.x = args.pi[j0] + e.x;
-    d0.y = args.pi[j0 + 1] + e.y;
+    const float e = et_row(obs_s(0));
+    float d0 = args.pi[jw] + e;
     if (EXT && args.start) {  // segment table column: start in state s, score 0 (cfn.rs:11-34 pattern)
       const int s = args.start[slot - args.seq_begin];
-      if (s >= 0) {
-        d0.x = (j0 == s) ? 0.0f : ninf_f();
-        d0.y = (j0 + 1 == s) ? 0.0f : ninf_f();
-      }
+      if (s >= 0) d0 = (jw == s) ? 0.0f : ninf_f();
     }
     d0 = force(d0, frc_s(0));
-    if (rg == 0) {
-      *reinterpret_cast<float2*>(&lds_delta[0][lds_w]) = d0;
-      if (!EXT || drow) *reinterpret_cast<float2*>(drow) = d0;
-      if (EXT && lrow && T == 1) *reinterpret_cast<float2*>(lrow) = d0;
+    if (writer) {
+      lds_delta[0][lds_w] = d0;
+      if (!EXT || drow) *drow = d0;
+      if (EXT && lrow && T == 1) *lrow = d0;
     }
   }
   int f_next = frc_s(T > 1 ? 1 : 0);
   unsigned o_next = obs_s(T > 1 ? 1 : 0);
-  float2 eA = et_row(o_next);  // emission row of t = 1
+  float eA = et_row(o_next);  // emission row of t = 1
   o_next = obs_s(T > 2 ? 2 : T - 1);
-  float2 eB;
+  float eB;
   lds_barrier();
 
   // One trellis step t: consumes e_use (row of o_t, loaded one step earlier), issues the
   // load of the row of o_{t+1} into e_pref and the scalar load of o_{t+2}.
-  auto step = [&](int t, const float2& e_use, float2& e_pref) {
+  auto step = [&](int t, const float& e_use, float& e_pref) {
     e_pref = et_row(o_next);
     const int cur = (t - 1) & 1;
     const float* dsrc = &lds_delta[cur][rg * S];
     float m0a = ninf_f(), m0b = ninf_f(), m1a = ninf_f(), m1b = ninf_f();
+    // the lane's R delta rows stream through a window of three float4 blocks (block q+3 is
+    // loaded once block q is consumed) instead of R registers
+    constexpr int NB = R / 4;
+    float4 win[3];
 #pragma unroll
-    for (int q4 = 0; q4 < R / 4; ++q4) {
-      const float4 d = *reinterpret_cast<const float4*>(dsrc + 4 * q4);
+    for (int q = 0; q < 3 && q < NB; ++q) win[q] = *reinterpret_cast<const float4*>(dsrc + 4 * q);
+#pragma unroll
+    for (int q4 = 0; q4 < NB; ++q4) {
+      const float4 d = win[q4 % 3];
       const int k = 4 * q4;
       // s_i = d[i] + a[i,j]  (viterbi.rs:15) for rows k..k+3 of this lane, columns j0, j0+1
       const float s00 = d.x + a_reg[2 * k + 0], s01 = d.x + a_reg[2 * k + 1];
@@ -245,22 +264,27 @@ __global__ __launch_bounds__(NP * 4) void trellis_fwd_f32(TrellisFwdArgs args) {
         m0b = fmaxf(fmaxf(m0b, s20), s30);
         m1b = fmaxf(fmaxf(m1b, s21), s31);
       }
+      if (q4 + 3 < NB) {
+        // keep the block's adds here (inputs only: an asm output would be canonicalised)
+        asm volatile("" ::"v"(m0a), "v"(m0b), "v"(m1a), "v"(m1b));
+        win[q4 % 3] = *reinterpret_cast<const float4*>(dsrc + 4 * (q4 + 3));
+      }
     }
     const int f_use = f_next;
     o_next = obs_s(t + 2 < T ? t + 2 : T - 1);
     f_next = frc_s(t + 1 < T ? t + 1 : T - 1);
-    float m0 = fmaxf(m0a, m0b);
-    float m1 = fmaxf(m1a, m1b);
-    m0 = octet_max(m0);  // fold the 8 row groups of column j0
-    m1 = octet_max(m1);
-    float2 dn;
-    dn.x = m0 + e_use.x;  // (d + a) + b -- viterbi.rs:15-17 association
-    dn.y = m1 + e_use.y;
+    const float m0 = fmaxf(m0a, m0b);
+    const float m1 = fmaxf(m1a, m1b);
+    // fold the 8 row groups; column j0 + hi ends in this lane
+    float m = dpp_max_mirror(hi ? m1 : m0, hi ? m0 : m1);
+    m = dpp_max_xor1(m);
+    m = dpp_max_xor2(m);
+    float dn = m + e_use;  // (d + a) + b -- viterbi.rs:15-17 association
     dn = force(dn, f_use);
-    if (rg == 0) {
-      *reinterpret_cast<float2*>(&lds_delta[cur ^ 1][lds_w]) = dn;
-      if (!EXT || drow) *reinterpret_cast<float2*>(drow + (size_t)t * NP) = dn;
-      if (EXT && lrow && t == T - 1) *reinterpret_cast<float2*>(lrow) = dn;
+    if (writer) {
+      lds_delta[cur ^ 1][lds_w] = dn;
+      if (!EXT || drow) drow[(size_t)t * NP] = dn;
+      if (EXT && lrow && t == T - 1) *lrow = dn;
     }
     lds_barrier();
   };
@@ -303,7 +327,9 @@ __global__ __launch_bounds__(NP * 4) void trellis_fwd2_f32(TrellisFwdArgs args) 
   const int rg = lane & 7;
   const int cp = lane >> 3;
   const int j0 = 16 * w + 2 * cp;
-  const unsigned ju = (unsigned)j0;  // unsigned lane offset: uniform base (SGPRs) + 32-bit VGPR offset
+  const bool hi = rg >= 4;  // column of this lane after the fold: j0 + hi
+  const unsigned jw = (unsigned)(j0 + (hi ? 1 : 0));  // uniform base (SGPRs) + 32-bit VGPR offset
+  const bool writer = (rg & 3) == 0;                  // rg 0 stores column j0, rg 4 column j0 + 1
 
   const int64_t slot = args.seq_begin + 2 * (int64_t)blockIdx.x;
   int64_t seq[2], e0[2];
@@ -343,23 +369,23 @@ __global__ __launch_bounds__(NP * 4) void trellis_fwd2_f32(TrellisFwdArgs args) 
     bad |= (o >= V) ? 2u : 0u;
     return o < V ? o : 0u;
   };
-  auto et_row = [&](unsigned o) -> float2 {
+  auto et_row = [&](unsigned o) -> float {
     const float* row = args.et + (size_t)o * NP;  // uniform
-    return *reinterpret_cast<const float2*>(row + ju);
+    return row[jw];
   };
-  const int lds_w = (j0 / R) * S + (j0 % R);
+  const int lds_w = (j0 / R) * S + (j0 % R) + (hi ? 1 : 0);
   auto clampT = [&](int t) { return t < T ? t : T - 1; };
 
   // ---- t = 0 for both sequences ----
   {
-    const float2 ex = et_row(obs_x(0)), ey = et_row(obs_y(0));
-    const float p0 = args.pi[j0], p1 = args.pi[j0 + 1];
-    const float2 dx = make_float2(p0 + ex.x, p1 + ex.y), dy = make_float2(p0 + ey.x, p1 + ey.y);
-    if (rg == 0) {
-      *reinterpret_cast<float2*>(&lds[0][0][lds_w]) = dx;
-      *reinterpret_cast<float2*>(&lds[1][0][lds_w]) = dy;
-      *reinterpret_cast<float2*>(dX + ju) = dx;
-      *reinterpret_cast<float2*>(dY + ju) = dy;
+    const float ex = et_row(obs_x(0)), ey = et_row(obs_y(0));
+    const float p = args.pi[jw];
+    const float dx = p + ex, dy = p + ey;
+    if (writer) {
+      lds[0][0][lds_w] = dx;
+      lds[1][0][lds_w] = dy;
+      dX[jw] = dx;
+      dY[jw] = dy;
     }
   }
   // Emission rows are loaded one HALF-step ahead (during the other sequence's half-step):
@@ -369,8 +395,8 @@ __global__ __launch_bounds__(NP * 4) void trellis_fwd2_f32(TrellisFwdArgs args) 
   // retires them and the compiler's own wait for them (at the next emission load) comes
   // before that half-step's LDS reads -- an SMEM load in flight would otherwise force an
   // lgkmcnt(0) on the prefetched rows and expose the LDS latency again.
-  float2 eX = et_row(obs_x(clampT(1)));  // X at t = 1
-  float2 eY;
+  float eX = et_row(obs_x(clampT(1)));  // X at t = 1
+  float eY;
   unsigned oY = obs_y(clampT(1));  // o_Y(t) for the coming X(t)
   unsigned oX = obs_x(clampT(2));  // o_X(t+1) for the coming Y(t)
   lds_barrier();
@@ -392,8 +418,8 @@ __global__ __launch_bounds__(NP * 4) void trellis_fwd2_f32(TrellisFwdArgs args) 
   // One half-step at step t: dsrc = this sequence's delta_{t-1} block, nsrc = the block the
   // next half-step reads first; e_use = this half-step's emission row, e_load <- the next
   // half-step's (row o_load); then o_load <- obs(t_obs) of the sequence `is_y`.
-  auto half = [&](const float* dsrc, const float* nsrc, float* ldst, float* drow, int t, const float2& e_use,
-                  float2& e_load, unsigned& o_load, bool is_y, int t_obs) {
+  auto half = [&](const float* dsrc, const float* nsrc, float* ldst, float* drow, int t, const float& e_use,
+                  float& e_load, unsigned& o_load, bool is_y, int t_obs) {
     e_load = et_row(o_load);
     if (KB > 1) ld8(dsrc + 8, Q);
     float m0a = ninf_f(), m0b = ninf_f(), m1a = ninf_f(), m1b = ninf_f();
@@ -427,17 +453,19 @@ __global__ __launch_bounds__(NP * 4) void trellis_fwd2_f32(TrellisFwdArgs args) 
         ld8(nsrc, P);  // next half-step's block 0 (KB odd: no adds left to hide it)
       __builtin_amdgcn_sched_barrier(0);
     }
-    float m0 = fmaxf(m0a, m0b);
-    float m1 = fmaxf(m1a, m1b);
-    m0 = octet_max(m0);  // fold the 8 row groups of column j0
-    m1 = octet_max(m1);
-    const float2 dn = make_float2(m0 + e_use.x, m1 + e_use.y);  // (d + a) + b, viterbi.rs:15-17
+    const float m0 = fmaxf(m0a, m0b);
+    const float m1 = fmaxf(m1a, m1b);
+    // fold the 8 row groups; column j0 + hi ends in this lane
+    float m = dpp_max_mirror(hi ? m1 : m0, hi ? m0 : m1);
+    m = dpp_max_xor1(m);
+    m = dpp_max_xor2(m);
+    const float dn = m + e_use;  // (d + a) + b, viterbi.rs:15-17
     __builtin_amdgcn_sched_barrier(0);
     o_load = is_y ? obs_y(t_obs) : obs_x(t_obs);
-    if (rg == 0) {
-      *reinterpret_cast<float2*>(ldst + lds_w) = dn;
+    if (writer) {
+      ldst[lds_w] = dn;
       float* row = drow + (size_t)t * NP;  // uniform
-      *reinterpret_cast<float2*>(row + ju) = dn;
+      row[jw] = dn;
     }
     lds_barrier();
   };

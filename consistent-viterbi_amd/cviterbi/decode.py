@@ -24,8 +24,9 @@ def _p(x):
 
 def make_opts(dtype="f32", assoc="viterbi", kernel="auto", rescore_f64=True, stream=None, workspace_bytes=0,
               variant=None, mfma_tiles=None, serial=False):
-    """variant: None/"valu" (all-VALU trellis, two sequences per workgroup where possible,
-    default), "valu1" (one sequence per workgroup) or "mfma" (MFMA-assisted, slower);
+    """variant: None/"valu" (all-VALU trellis, two equal-length sequences per workgroup where
+    N % 64 == 0, default), "valu1" (one sequence per workgroup) or "mfma" (MFMA-assisted,
+    slower) -- all bit-identical;
     mfma_tiles: tuning override of the MFMA tiles per wave (bit-identical results);
     serial: no forward/backtrack stream overlap."""
     flags = L.FLAG_SERIAL if serial else 0

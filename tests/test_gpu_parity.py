@@ -55,7 +55,7 @@ def test_trellis_f32_bit_exact(gpu, n):
 @pytest.mark.parametrize("variant", ["valu", "valu1", "mfma"])
 @pytest.mark.parametrize("serial", [False, True])
 def test_trellis_variants_bit_exact(gpu, n, variant, serial):
-    """Both trellis variants (all-VALU; MFMA-assisted, whose MFMA tiles compute
+    """All trellis variants (all-VALU with 2 or 1 sequences per workgroup; MFMA-assisted, whose MFMA tiles compute
     fma(d, 1, a) = d + a exactly) and both schedules (pipelined chunks / serial) give the
     oracle's f32 result bit for bit."""
     pi, a, b, off, obs = _case(n, 29, seed=300 + n, nseq=30, tmax=50, zero_frac=0.03)
@@ -160,10 +160,11 @@ def test_chunked_workspace(gpu):
         assert np.array_equal(x, y)
 
 
-def test_device_api_badobs(gpu):
+@pytest.mark.parametrize("n", [32, 64, 256])
+def test_device_api_badobs(gpu, n):
     import torch
 
-    pi, a, b, off, obs = _case(32, 10, seed=9, nseq=6, tmax=30, tmin=5)
+    pi, a, b, off, obs = _case(n, 10, seed=9, nseq=6, tmax=30, tmin=5)
     obs = obs.copy()
     obs[off[2] + 3] = 10  # out of range on the device path
     h = cv.HMM(pi, a, b)
