@@ -181,6 +181,9 @@ __global__ __launch_bounds__(NP * 4) void trellis_fwd_f32(TrellisFwdArgs args) {
 
   // A register image: float4 q of a lane = (A[rg*R+2q][j0], A[rg*R+2q][j0+1],
   // A[rg*R+2q+1][j0], A[rg*R+2q+1][j0+1]); each wave-instruction reads 1 KiB contiguous.
+  // Forward waves win issue arbitration over co-resident backtrack waves (overlap mode):
+  // the backtrack has slack, the forward pass is the critical path.
+  __builtin_amdgcn_s_setprio(3);
   float a_reg[2 * R];
   {
     const float4* img = reinterpret_cast<const float4*>(args.a_img) + (size_t)w * (R / 2) * 64 + lane;
@@ -346,6 +349,9 @@ __global__ __launch_bounds__(NP * 4) void trellis_fwd2_f32(TrellisFwdArgs args) 
   float* const dY = args.delta + (e0[1] - args.delta_elem_base) * NP;
   const unsigned V = (unsigned)args.nobs;
 
+  // Forward waves win issue arbitration over co-resident backtrack waves (overlap mode):
+  // the backtrack has slack, the forward pass is the critical path.
+  __builtin_amdgcn_s_setprio(3);
   float a_reg[2 * R];
   {
     const float4* img = reinterpret_cast<const float4*>(args.a_img) + (size_t)w * (R / 2) * 64 + lane;
