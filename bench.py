@@ -205,7 +205,7 @@ def main():
         "seqs_per_s": B * args.steps / el,
         "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK, "traffic": traffic,
-                     "kernel": "trellis_fwd_f32<256>", "kernel_ms_per_launch": fwd_launch_s * 1e3,
+                     "kernel": "trellis_fwd2_f32<256>", "kernel_ms_per_launch": fwd_launch_s * 1e3,
                      "alg_bytes_per_launch": per_launch_bytes,
                      "read_only_frac": alg_read / (launches / args.steps) / fwd_launch_s / HBM_PEAK,
                      "binding": "valu",

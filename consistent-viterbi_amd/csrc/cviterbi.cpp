@@ -562,16 +562,28 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
       ba.score = score_dev;
       ba.score32 = nullptr;
       ba.status = status_dev;
-      ba.rescore_f64 = o.rescore_f64 ? 1 : 0;
-      ba.pi64 = h->d_pi64.as<double>();
-      ba.a64 = h->d_a64.as<double>();
-      ba.et64 = h->d_et64.as<double>();
       // overlap mode: at most ONE backtrack workgroup (one 64-VGPR wave per SIMD) per CU, so
       // the next forward workgroup (MFMA: 2 waves x 200 VGPRs per SIMD; VALU: 4 x 104) always
       // finds its registers free: reserve 100 KiB of LDS (2 x 100 > 160 KiB)
       // the last chunk's backtrack has the device to itself: full occupancy
       const int reserve = (serial || ci + 1 == chunks.size()) ? 0 : 100 * 1024;
       err = cvk::launch_trellis_bt(h->np, ba, n, bts, reserve);
+      if (err == hipSuccess && o.rescore_f64) {
+        cvk::RescoreArgs ra{};
+        ra.path = path_dev;
+        ra.obs = obs_dev;
+        ra.offsets = offsets_dev;
+        ra.order = order_dev;
+        ra.seq_begin = c.first;
+        ra.seq_end = c.second;
+        ra.nstates = h->N;
+        ra.pi64 = h->d_pi64.as<double>();
+        ra.a64 = h->d_a64.as<double>();
+        ra.et64 = h->d_et64.as<double>();
+        ra.status = status_dev;
+        ra.score = score_dev;
+        err = cvk::launch_rescore_f64(ra, n, bts, reserve);
+      }
     } else if (o.dtype == CV_DTYPE_F64) {
       cvk::GenericBtArgs<double> ba{};
       ba.psi = reinterpret_cast<const uint16_t*>(wsb);

@@ -43,11 +43,23 @@ struct BacktrackArgs {
   double* score;           // [nseq_total]
   float* score32;          // optional [nseq_total]
   uint8_t* status;
-  int rescore_f64;
+};
+
+// f64 re-score of decoded paths, one LANE per sequence (rescore_f64_lanes)
+struct RescoreArgs {
+  const int32_t* path;     // [sum T]
+  const int32_t* obs;      // [sum T]
+  const int64_t* offsets;
+  const int32_t* order;    // optional schedule: slot -> sequence id
+  int64_t seq_begin, seq_end;
+  int nstates;             // real N
   const double* pi64;      // [N]
   const double* a64;       // [N*N]
   const double* et64;      // [V][N]
+  const uint8_t* status;   // only CVK_SEQ_OK sequences are re-scored
+  double* score;           // [nseq_total]
 };
+hipError_t launch_rescore_f64(const RescoreArgs& r, int64_t nseq, hipStream_t stream, int lds_reserve = 0);
 
 template <typename REAL>
 struct GenericFwdArgs {

@@ -856,13 +856,185 @@ __global__ __launch_bounds__(256) void backtrack_f32(BacktrackArgs args) {
   }
   if (lane == 0) {
     args.status[seq] = CVK_SEQ_OK;
-    if (!args.rescore_f64) args.score[seq] = (double)score32;
+    args.score[seq] = (double)score32;  // f64 re-score: rescore_f64_lanes (after this kernel)
+    if (args.score32) args.score32[seq] = score32;
   }
-  if (args.rescore_f64) {
-    const double d = rescore_path_f64(path, args.obs + e0, T, args.pi64, args.a64, args.et64, N, lane);
-    if (lane == 0) args.score[seq] = d;
+}
+
+// backtrack_v_f32<NP> (NP % 64 == 0): the same backtrack with VL = NP/64 CONSECUTIVE states
+// per lane (lane l owns states VL*l .. VL*l+VL-1), so a delta row and a column of A^T are
+// one dwordx{VL} load per lane instead of VL dword loads: 4x fewer vector-memory
+// instructions at N = 256 and 16-byte requests.  First argmax: wave max, ballot of the lanes
+// holding it (lowest lane = lowest state block), then that lane's first k (readlane).
+template <int VL>
+__device__ __forceinline__ void ld_vl(const float* p, float (&d)[VL]) {
+  if constexpr (VL == 4) {
+    const float4 x = *reinterpret_cast<const float4*>(p);
+    d[0] = x.x, d[1] = x.y, d[2] = x.z, d[3] = x.w;
+  } else if constexpr (VL == 2) {
+    const float2 x = *reinterpret_cast<const float2*>(p);
+    d[0] = x.x, d[1] = x.y;
+  } else {
+#pragma unroll
+    for (int k = 0; k < VL; ++k) d[k] = p[k];
   }
-  if (args.score32 && lane == 0) args.score32[seq] = score32;
+}
+
+template <int VL>
+__device__ __forceinline__ int first_argmax_vl(const float (&s)[VL], float M, int lane) {
+  int fk = VL;
+#pragma unroll
+  for (int k = VL - 1; k >= 0; --k) fk = (s[k] == M) ? k : fk;
+  const unsigned long long mask = __ballot(fk < VL);
+  const int L = (int)__builtin_ctzll(mask);  // mask != 0: M is one of the s values
+  return VL * L + __builtin_amdgcn_readlane(fk, L);
+}
+
+template <int NP>
+__global__ __launch_bounds__(256) void backtrack_v_f32(BacktrackArgs args) {
+  constexpr int VL = NP / 64;
+  constexpr int PF = 8;
+  static_assert(NP % 64 == 0, "backtrack_v_f32 needs NP % 64 == 0");
+  const int lane = threadIdx.x & 63;
+  const int64_t slot = args.seq_begin + (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (slot >= args.seq_end) return;
+  const int64_t seq = args.order ? (int64_t)args.order[slot] : slot;
+  const int64_t e0 = args.offsets[seq];
+  const int T = (int)(args.offsets[seq + 1] - e0);
+  if (T <= 0) {
+    if (lane == 0) {
+      args.score[seq] = 0.0;
+      args.status[seq] = CVK_SEQ_EMPTY;
+    }
+    return;
+  }
+  int32_t* __restrict__ path = args.path + e0;
+  // padded states (>= N) hold -inf in delta and A^T, so they never win a feasible argmax
+  const float* __restrict__ drow = args.delta + (e0 - args.delta_elem_base) * NP + VL * lane;
+  auto load_row = [&](int r, float (&dst)[VL]) {
+    if (r >= 0) {
+      ld_vl<VL>(drow + (size_t)r * NP, dst);
+    } else {
+#pragma unroll
+      for (int k = 0; k < VL; ++k) dst[k] = ninf_f();
+    }
+  };
+  auto lane_max = [&](const float (&v)[VL]) {
+    float m = v[0];
+#pragma unroll
+    for (int k = 1; k < VL; ++k) m = fmaxf(m, v[k]);
+    return m;
+  };
+  // first argmax of the last row (cp.rs:117-118)
+  int cur;
+  float bv;
+  {
+    float last[VL];
+    load_row(T - 1, last);
+    bv = wave_max(lane_max(last));
+    cur = (bv > ninf_f()) ? first_argmax_vl<VL>(last, bv, lane) : 0;
+  }
+  const uint8_t prior = args.status[seq];
+  if (!(bv > ninf_f()) || prior == CVK_SEQ_BADOBS) {
+    for (int t = lane; t < T; t += 64) path[t] = 0;
+    if (lane == 0) {
+      args.score[seq] = (double)ninf_f();
+      args.status[seq] = prior == CVK_SEQ_BADOBS ? CVK_SEQ_BADOBS : CVK_SEQ_INFEASIBLE;
+    }
+    return;
+  }
+  const float score32 = bv;
+  int pathreg = 0;
+  if (lane == ((T - 1) & 63)) pathreg = cur;
+  if (((T - 1) & 63) == 0 && lane == 0) path[T - 1] = cur;
+  const float* __restrict__ at = args.at + VL * lane;
+  float ring[PF][VL];
+#pragma unroll
+  for (int u = 0; u < PF; ++u) load_row(T - 2 - u, ring[u]);
+  for (int base = T - 1; base >= 1; base -= PF) {
+#pragma unroll
+    for (int u = 0; u < PF; ++u) {
+      const int t = base - u;
+      if (t >= 1) {
+        // s_i = d_{t-1}[i] + a[i, cur]  -- the forward pass's exact f32 add
+        float acol[VL], sv[VL];
+        ld_vl<VL>(at + (size_t)cur * NP, acol);
+#pragma unroll
+        for (int k = 0; k < VL; ++k) sv[k] = ring[u][k] + acol[k];
+        const float M = wave_max(lane_max(sv));
+        cur = first_argmax_vl<VL>(sv, M, lane);
+        const int tp = t - 1;
+        if (lane == (tp & 63)) pathreg = cur;
+        if ((tp & 63) == 0 && tp + lane < T) path[tp + lane] = pathreg;  // flush a 64-entry block
+      }
+    }
+    // refill the whole ring once per block (in-order vmcnt: see backtrack_f32)
+#pragma unroll
+    for (int u = 0; u < PF; ++u) load_row(base - PF - 1 - u, ring[u]);
+  }
+  if (lane == 0) {
+    args.status[seq] = CVK_SEQ_OK;
+    args.score[seq] = (double)score32;  // f64 re-score: rescore_f64_lanes (after this kernel)
+    if (args.score32) args.score32[seq] = score32;
+  }
+}
+
+// rescore_f64_lanes: the f64 re-score of rescore_path_f64, but one LANE per sequence, so the
+// sequential fold (its rounding order is the definition) runs in 64 sequences at once per
+// wave instead of one lane of a wave doing 4 readlanes per step.  The path/obs reads and the
+// a/b gathers of 8 steps are issued before the 16 dependent adds that use them.
+__global__ __launch_bounds__(64) void rescore_f64_lanes(RescoreArgs r) {
+  const int64_t slot = r.seq_begin + (int64_t)blockIdx.x * 64 + threadIdx.x;
+  if (slot >= r.seq_end) return;
+  const int64_t seq = r.order ? (int64_t)r.order[slot] : slot;
+  if (r.status[seq] != CVK_SEQ_OK) return;
+  const int64_t e0 = r.offsets[seq];
+  const int T = (int)(r.offsets[seq + 1] - e0);
+  const int32_t* __restrict__ path = r.path + e0;
+  const int32_t* __restrict__ obs = r.obs + e0;
+  const int N = r.nstates;
+  int pp = path[0];
+  double d = r.pi64[pp] + r.et64[(size_t)obs[0] * N + pp];  // init_prob: pi + b (hmm.rs:415-418)
+  int t = 1;
+  constexpr int U = 8;
+  for (; t + U <= T; t += U) {
+    int p[U], o[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      p[k] = path[t + k];
+      o[k] = obs[t + k];
+    }
+    double av[U], bv[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      av[k] = r.a64[(size_t)(k ? p[k - 1] : pp) * N + p[k]];
+      bv[k] = r.et64[(size_t)o[k] * N + p[k]];
+    }
+#pragma unroll
+    for (int k = 0; k < U; ++k) d = (d + av[k]) + bv[k];  // (d + a) + b, viterbi.rs:15-17
+    pp = p[U - 1];
+  }
+  for (; t < T; ++t) {
+    const int p = path[t];
+    d = (d + r.a64[(size_t)pp * N + p]) + r.et64[(size_t)obs[t] * N + p];
+    pp = p;
+  }
+  r.score[seq] = d;
+}
+
+hipError_t launch_rescore_f64(const RescoreArgs& r, int64_t nseq, hipStream_t stream, int lds_reserve) {
+  if (nseq <= 0) return hipSuccess;
+  if (lds_reserve > 0) {  // overlap mode: at most one re-score wave per CU beside the forward pass
+    static bool attr = false;
+    if (!attr) {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&rescore_f64_lanes),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      attr = true;
+    }
+  }
+  hipLaunchKernelGGL(rescore_f64_lanes, dim3((unsigned)((nseq + 63) / 64)), dim3(64), (size_t)lds_reserve, stream,
+                     r);
+  return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------------
@@ -1075,13 +1247,21 @@ static hipError_t trellis_bt_np(const BacktrackArgs& ba, int64_t nseq, hipStream
   if (lds_reserve > 0) {
     static bool attr = false;  // allow the large dynamic-LDS reservation
     if (!attr) {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&backtrack_f32<NP>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      if constexpr (NP % 64 == 0)
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&backtrack_v_f32<NP>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      else
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&backtrack_f32<NP>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       attr = true;
     }
   }
-  hipLaunchKernelGGL(backtrack_f32<NP>, dim3((unsigned)((nseq + 3) / 4)), dim3(256), (size_t)lds_reserve, stream,
-                     ba);
+  if constexpr (NP % 64 == 0)
+    hipLaunchKernelGGL(backtrack_v_f32<NP>, dim3((unsigned)((nseq + 3) / 4)), dim3(256), (size_t)lds_reserve, stream,
+                       ba);
+  else
+    hipLaunchKernelGGL(backtrack_f32<NP>, dim3((unsigned)((nseq + 3) / 4)), dim3(256), (size_t)lds_reserve, stream,
+                       ba);
   return hipGetLastError();
 }
 
