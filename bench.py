@@ -5,8 +5,8 @@ states, V=1,024 observations (bdims [32,32]), Dirichlet(1) rows in log10, iid un
 observations from splitmix64; T=512, B=65,536 sequences in total, f32 row-A0 trellis.
 The batch is sharded across ranks (strong scaling: total work fixed, B/N per GPU); one
 step = decode of the rank's shard (forward trellis kernel + backtrack + f64 re-score of
-every path) followed, for N>1, by an RCCL gather of paths, scores and statuses to rank 0
-over xGMI.  Inputs are resident in HBM before the timed region.
+every path) followed, for N>1, by ONE RCCL gather (torch.distributed "nccl") of the paths
+(u8 states), scores and statuses to rank 0 over xGMI.  Inputs are resident in HBM before the timed region.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
        (N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N)
@@ -143,8 +143,8 @@ def main():
     def step():
         cv.decode_batch_device(h, off_d, obs_d, path_d, score_d, status_d, offsets_host=off,
                                stream=stream.cuda_stream, workspace_bytes=WORKSPACE)
-        if world > 1:  # RCCL over xGMI: decoded paths, scores, statuses to rank 0
-            cvd.gather_to_root([path_d, score_d, status_d], [per * T_LEN, per, per], dist)
+        if world > 1:  # RCCL over xGMI: decoded paths (u8 states), scores, statuses to rank 0, one gather
+            cvd.gather_packed_to_root(path_d, score_d, status_d, N_STATES, per * T_LEN, per, dist)
 
     for _ in range(args.warmup):
         step()

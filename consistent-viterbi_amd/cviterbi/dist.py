@@ -49,6 +49,40 @@ def gather_to_root(tensors, per_sizes, dist, device=None):
     return out if rank == 0 else None
 
 
+def gather_packed_to_root(path, score, status, nstates, elem_cap, seq_cap, dist):
+    """ONE gather of a rank's decode result to rank 0: states as u8 when nstates <= 256 (else
+    int32), f64 scores as raw bytes, u8 statuses, packed into one byte buffer padded to the
+    per-rank capacities (elem_cap path entries, seq_cap sequences).  At config 4 / 8 ranks
+    that is 4.2 MB per rank instead of 16.8 MB of int32 paths in three collectives.
+    Returns on rank 0 a list over ranks of (path int32, score f64, status u8) padded to the
+    capacities (trim with `assemble`); None elsewhere."""
+    import torch
+
+    pdt = torch.uint8 if nstates <= 256 else torch.int32
+    psz = 1 if pdt == torch.uint8 else 4
+    dev = path.device
+    nbytes = seq_cap * 8 + elem_cap * psz + seq_cap  # [scores | paths | statuses], views stay aligned
+    buf = torch.zeros(nbytes, dtype=torch.uint8, device=dev)
+    buf[: score.numel() * 8] = score.contiguous().view(torch.uint8)
+    o = seq_cap * 8
+    buf[o: o + path.numel() * psz] = path.to(pdt).view(torch.uint8)
+    o += elem_cap * psz
+    buf[o: o + status.numel()] = status.to(torch.uint8)
+    rank = dist.get_rank()
+    lst = [torch.empty(nbytes, dtype=torch.uint8, device=dev) for _ in range(dist.get_world_size())] \
+        if rank == 0 else None
+    dist.gather(buf, lst, dst=0)
+    if rank != 0:
+        return None
+    out = []
+    for b in lst:
+        sc = b[: seq_cap * 8].view(torch.float64)
+        p = b[seq_cap * 8: seq_cap * 8 + elem_cap * psz].view(pdt).to(torch.int32)
+        st = b[seq_cap * 8 + elem_cap * psz:]
+        out.append((p, sc, st))
+    return out
+
+
 def assemble(parts, lengths):
     """Concatenate per-rank gathered buffers, keeping the first lengths[r] entries of each."""
     import torch

@@ -57,11 +57,19 @@ def _worker(rank, world, port, q):
     cap = int(max(off[min((r + 1) * per, B)] - off[min(r * per, B)] for r in range(world)))
     got = cvd.gather_to_root([torch.from_numpy(path), torch.from_numpy(score), torch.from_numpy(status)],
                              [cap, per, per], dist)
+    # the packed single-collective form bench.py uses (u8 states, raw f64 scores, u8 status)
+    packed = cvd.gather_packed_to_root(torch.from_numpy(path), torch.from_numpy(score),
+                                       torch.from_numpy(status), N, cap, per, dist)
     if rank == 0:
         nel = [int(off[min((r + 1) * per, B)] - off[min(r * per, B)]) for r in range(world)]
         nsq = [min((r + 1) * per, B) - min(r * per, B) for r in range(world)]
-        q.put((cvd.assemble(got[0], nel).numpy(), cvd.assemble(got[1], nsq).numpy(),
-               cvd.assemble(got[2], nsq).numpy()))
+        res = (cvd.assemble(got[0], nel).numpy(), cvd.assemble(got[1], nsq).numpy(),
+               cvd.assemble(got[2], nsq).numpy())
+        res2 = (cvd.assemble([x[0] for x in packed], nel).numpy(), cvd.assemble([x[1] for x in packed], nsq).numpy(),
+                cvd.assemble([x[2] for x in packed], nsq).numpy())
+        for x, y in zip(res, res2):
+            assert np.array_equal(x, y.astype(x.dtype))
+        q.put(res)
     dist.barrier()
     dist.destroy_process_group()
 
