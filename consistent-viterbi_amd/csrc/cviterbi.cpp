@@ -13,11 +13,13 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <mutex>
 #include <numeric>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/cviterbi.h"
@@ -287,6 +289,47 @@ cv_status make_hmm(int N, const std::vector<int64_t>& bdims, const double* pi, c
   return CV_OK;
 }
 
+// Host worker threads for the O(elements) loops of the host API (validation, constraint
+// bookkeeping, exact accumulation): min(16, hardware threads), CV_HOST_THREADS overrides.
+int host_threads() {
+  static const int n = [] {
+    const char* e = getenv("CV_HOST_THREADS");
+    int v = e ? atoi(e) : (int)std::thread::hardware_concurrency();
+    return std::max(1, std::min(v > 0 ? v : 1, 16));
+  }();
+  return n;
+}
+
+// f(t, lo, hi) over [0, n) split into contiguous ranges, one per worker (t = worker index).
+template <typename F>
+void parallel_ranges(int64_t n, F&& f, int64_t min_per_thread = 1 << 16) {
+  const int nt = (int)std::max<int64_t>(1, std::min<int64_t>(host_threads(), n / std::max<int64_t>(min_per_thread, 1)));
+  if (nt <= 1) {
+    f(0, (int64_t)0, n);
+    return;
+  }
+  std::vector<std::thread> th;
+  th.reserve(nt);
+  for (int t = 0; t < nt; ++t) th.emplace_back([&, t] { f(t, n * t / nt, n * (t + 1) / nt); });
+  for (auto& x : th) x.join();
+}
+
+// First index k in [lo, hi) with bad(k), or -1 (parallel scan; the smallest index wins).
+template <typename P>
+int64_t first_bad(int64_t lo, int64_t hi, P&& bad) {
+  std::vector<int64_t> first((size_t)host_threads(), -1);
+  parallel_ranges(hi - lo, [&](int t, int64_t a, int64_t b) {
+    for (int64_t k = lo + a; k < lo + b; ++k)
+      if (bad(k)) {
+        first[t] = k;
+        return;
+      }
+  });
+  for (int64_t f : first)
+    if (f >= 0) return f;  // workers hold ascending ranges
+  return -1;
+}
+
 cv_status check_batch(const cv_hmm* h, int64_t nseq, const int64_t* offsets) {
   if (nseq < 0) return set_err(CV_EINVAL, "nseq < 0");
   if (!offsets) return set_err(CV_EINVAL, "offsets is NULL");
@@ -376,8 +419,8 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
   // workspace cap forces more.
   const bool serial = (o.flags & CV_FLAG_SERIAL) != 0;
   // Sequences per forward workgroup: 2 (trellis_fwd2_f32, equal-length pairs; default) or 1
-  // (trellis_fwd_f32: leftovers, EXT features, MFMA, N not a multiple of 64).
-  const bool plain = use_trellis && !use_mfma && !o.forced && cvk::trellis_pair_supported(h->np);
+  // (trellis_fwd_f32: leftovers, MFMA, N not a multiple of 64).
+  const bool plain = use_trellis && !use_mfma && cvk::trellis_pair_supported(h->np);
   const int group = (!plain || (o.flags & CV_FLAG_NO_PAIR)) ? 1 : 2;
   const uint64_t half_cap = std::max<uint64_t>(serial ? cap : cap / 2, per_elem);
   uint64_t nchunks = std::max<uint64_t>(1, (total_elems * per_elem + half_cap - 1) / half_cap);
@@ -767,16 +810,22 @@ CV_API cv_status cv_decode_batch_device(cv_hmm* h, int64_t nseq, const int64_t* 
 }
 
 // Host-pointer decode; caller holds h->mu and has selected the device.
+// obs_staged: h->st_obs already holds the (validated) observations of [offsets[0],
+// offsets[nseq]); forced_staged: o.forced is a validated DEVICE array indexed like obs.
 static cv_status decode_host_locked(cv_hmm* h, int64_t nseq, const int64_t* offsets, const int32_t* obs, cv_opts o,
-                                    int32_t* path_out, double* score_out, uint8_t* status_out) {
+                                    int32_t* path_out, double* score_out, uint8_t* status_out,
+                                    bool obs_staged = false, bool forced_staged = false) {
   cv_status st;
   if (nseq == 0) return CV_OK;
   if ((st = check_batch(h, nseq, offsets)) != CV_OK) return st;
   const int64_t base = offsets[0];
   const int64_t total = offsets[nseq];  // obs/path are indexed by absolute element offset
-  for (int64_t k = base; k < total; ++k)
-    if (obs[k] < 0 || obs[k] >= h->V)
+  if (!obs_staged) {
+    const int64_t V = h->V;
+    const int64_t k = first_bad(base, total, [&](int64_t i) { return obs[i] < 0 || obs[i] >= V; });
+    if (k >= 0)
       return set_err(CV_EINVAL, "obs[%lld] = %d out of range [0,%lld)", (long long)k, obs[k], (long long)h->V);
+  }
   hipStream_t stream = o.stream ? (hipStream_t)o.stream : h->stream;
   if ((st = h->st_off.ensure((size_t)(nseq + 1) * 8)) != CV_OK) return st;
   if ((st = h->st_obs.ensure((size_t)std::max<int64_t>(total, 1) * 4)) != CV_OK) return st;
@@ -784,13 +833,14 @@ static cv_status decode_host_locked(cv_hmm* h, int64_t nseq, const int64_t* offs
   if ((st = h->st_score.ensure((size_t)nseq * 8)) != CV_OK) return st;
   if ((st = h->st_status.ensure((size_t)nseq)) != CV_OK) return st;
   HIP_TRY(hipMemcpyAsync(h->st_off.p, offsets, (size_t)(nseq + 1) * 8, hipMemcpyHostToDevice, stream));
-  if (total > base)
+  if (total > base && !obs_staged)
     HIP_TRY(hipMemcpyAsync(h->st_obs.as<int32_t>() + base, obs + base, (size_t)(total - base) * 4,
                            hipMemcpyHostToDevice, stream));
-  if (o.forced) {  // host forced[] -> device staging, indexed like obs
-    for (int64_t k = base; k < total; ++k)
-      if (o.forced[k] < -1 || o.forced[k] >= h->N)
-        return set_err(CV_EINVAL, "forced[%lld] = %d out of range [-1,%d)", (long long)k, o.forced[k], h->N);
+  if (o.forced && !forced_staged) {  // host forced[] -> device staging, indexed like obs
+    const int32_t N = h->N;
+    const int32_t* fr = o.forced;
+    const int64_t k = first_bad(base, total, [&](int64_t i) { return fr[i] < -1 || fr[i] >= N; });
+    if (k >= 0) return set_err(CV_EINVAL, "forced[%lld] = %d out of range [-1,%d)", (long long)k, o.forced[k], h->N);
     if ((st = h->st_forced.ensure((size_t)std::max<int64_t>(total, 1) * 4)) != CV_OK) return st;
     if (total > base)
       HIP_TRY(hipMemcpyAsync(h->st_forced.as<int32_t>() + base, o.forced + base, (size_t)(total - base) * 4,
@@ -834,6 +884,39 @@ struct ConSeq {
   std::vector<int64_t> elems;  // constrained elements, ascending
 };
 
+// Constrained sequences in sequence order (per-worker lists concatenated in order).
+void build_conseq(int64_t nseq, const int64_t* offsets, const int32_t* component, std::vector<ConSeq>& cs) {
+  cs.clear();
+  std::vector<std::vector<ConSeq>> part((size_t)host_threads());
+  parallel_ranges(nseq, [&](int t, int64_t lo, int64_t hi) {
+    for (int64_t s = lo; s < hi; ++s) {
+      ConSeq c{s, {}};
+      for (int64_t e = offsets[s]; e < offsets[s + 1]; ++e)
+        if (component[e] >= 0) c.elems.push_back(e);
+      if (!c.elems.empty()) part[t].push_back(std::move(c));
+    }
+  }, 1024);
+  for (auto& p : part)
+    for (auto& c : p) cs.push_back(std::move(c));
+}
+
+// Pairs (c1 < c2) of different components at consecutive constrained elements, sorted and
+// unique -- cvcsp::component_pairs restricted to the constrained elements.
+std::vector<int32_t> conseq_pairs(const std::vector<ConSeq>& cs, const int32_t* component) {
+  std::vector<std::pair<int32_t, int32_t>> ps;
+  for (const auto& c : cs)
+    for (size_t k = 0; k + 1 < c.elems.size(); ++k) {
+      const int32_t a = component[c.elems[k]], b = component[c.elems[k + 1]];
+      if (a != b) ps.emplace_back(std::min(a, b), std::max(a, b));
+    }
+  std::sort(ps.begin(), ps.end());
+  ps.erase(std::unique(ps.begin(), ps.end()), ps.end());
+  std::vector<int32_t> out;
+  out.reserve(ps.size() * 2);
+  for (auto& p : ps) out.push_back(p.first), out.push_back(p.second);
+  return out;
+}
+
 cv_status constrained_validate(cv_hmm* h, int64_t nseq, const int64_t* offsets, const int32_t* obs,
                                const int32_t* component, int32_t ncomp, const cv_opts& o, std::vector<ConSeq>& cs) {
   if (o.dtype != CV_DTYPE_F32 || o.assoc != CV_ASSOC_VITERBI || !cvk::trellis_padded_states(h->N))
@@ -843,18 +926,16 @@ cv_status constrained_validate(cv_hmm* h, int64_t nseq, const int64_t* offsets, 
   if (nseq == 0) return CV_OK;
   cv_status st;
   if ((st = check_batch(h, nseq, offsets)) != CV_OK) return st;
-  for (int64_t k = offsets[0]; k < offsets[nseq]; ++k) {
-    if (obs[k] < 0 || obs[k] >= h->V)
+  {
+    const int64_t V = h->V;
+    int64_t k = first_bad(offsets[0], offsets[nseq], [&](int64_t i) { return obs[i] < 0 || obs[i] >= V; });
+    if (k >= 0)
       return set_err(CV_EINVAL, "obs[%lld] = %d out of range [0,%lld)", (long long)k, obs[k], (long long)h->V);
-    if (component[k] < -1 || component[k] >= ncomp)
+    k = first_bad(offsets[0], offsets[nseq], [&](int64_t i) { return component[i] < -1 || component[i] >= ncomp; });
+    if (k >= 0)
       return set_err(CV_EINVAL, "component[%lld] = %d out of range [-1,%d)", (long long)k, component[k], ncomp);
   }
-  for (int64_t s = 0; s < nseq; ++s) {
-    ConSeq c{s, {}};
-    for (int64_t e = offsets[s]; e < offsets[s + 1]; ++e)
-      if (component[e] >= 0) c.elems.push_back(e);
-    if (!c.elems.empty()) cs.push_back(std::move(c));
-  }
+  build_conseq(nseq, offsets, component, cs);
   return CV_OK;
 }
 
@@ -863,12 +944,18 @@ cv_status constrained_validate(cv_hmm* h, int64_t nseq, const int64_t* offsets, 
 //   m == 1: mu = delta_{t_1} + beta  -> unary of c_1
 //   m >= 2: alpha = delta_{t_1} -> unary c_1; beta -> unary c_m; segment tables M_k -> the
 //           pair (c_k, c_{k+1}) (or the diagonal into the unary when c_k == c_{k+1}).
+// `pre`: the caller's already validated constrained-sequence list (else validated here);
+// on return *obs_staged tells whether h->st_obs holds the batch's observations.
 cv_status constrained_partials_locked(cv_hmm* h, int64_t nseq, const int64_t* offsets, const int32_t* obs,
                                       const int32_t* component, int32_t ncomp, const int32_t* pairs, int64_t npairs,
-                                      cv_opts& o, int64_t* part) {
-  std::vector<ConSeq> cs;
-  cv_status st = constrained_validate(h, nseq, offsets, obs, component, ncomp, o, cs);
-  if (st != CV_OK || cs.empty()) return st;
+                                      cv_opts& o, int64_t* part, const std::vector<ConSeq>* pre = nullptr,
+                                      bool* obs_staged = nullptr) {
+  if (obs_staged) *obs_staged = false;
+  std::vector<ConSeq> own;
+  cv_status st = CV_OK;
+  if (!pre && (st = constrained_validate(h, nseq, offsets, obs, component, ncomp, o, own)) != CV_OK) return st;
+  const std::vector<ConSeq>& cs = pre ? *pre : own;
+  if (cs.empty()) return CV_OK;
   const int N = (int)h->N;
   const int64_t uw = cvcsp::unary_words(N), pw = cvcsp::pair_words(N);
   int64_t* pbase = part + (int64_t)ncomp * uw;
@@ -893,6 +980,7 @@ cv_status constrained_partials_locked(cv_hmm* h, int64_t nseq, const int64_t* of
   if ((st = h->st_obs.ensure((size_t)std::max<int64_t>(total, 1) * 4)) != CV_OK) return st;
   HIP_TRY(hipMemcpyAsync(h->st_obs.as<int32_t>() + base, obs + base, (size_t)(total - base) * 4,
                          hipMemcpyHostToDevice, stream));
+  if (obs_staged) *obs_staged = true;
 
   // ---- prefix / suffix passes for every constrained sequence (m == 1 ones first) ----
   std::vector<const ConSeq*> order;
@@ -958,21 +1046,25 @@ cv_status constrained_partials_locked(cv_hmm* h, int64_t nseq, const int64_t* of
   HIP_TRY(hipMemcpyAsync(dl.data(), h->cs_delta.p, dl.size() * 4, hipMemcpyDeviceToHost, stream));
   HIP_TRY(hipMemcpyAsync(mu.data(), h->cs_mu.p, mu.size() * 4, hipMemcpyDeviceToHost, stream));
   HIP_TRY(hipStreamSynchronize(stream));
-  for (int64_t i = 0; i < nc; ++i) {
-    const ConSeq& c = *order[i];
-    const int32_t c1 = component[c.elems.front()], cm = component[c.elems.back()];
-    for (int64_t e : c.elems) part[(int64_t)component[e] * uw + 5 * N] += 1;
-    int64_t* u1 = part + (int64_t)c1 * uw;
-    int64_t* um = part + (int64_t)cm * uw;
-    for (int s = 0; s < N; ++s) {
-      if (i < n1) {
-        cvcsp::add_exact(u1 + 4 * s, u1 + 4 * N + s, mu[(size_t)i * np + s]);
-      } else {
-        cvcsp::add_exact(u1 + 4 * s, u1 + 4 * N + s, dl[(size_t)i * np + s]);
-        cvcsp::add_exact(um + 4 * s, um + 4 * N + s, mu[(size_t)i * np + s]);
+  for (int64_t i = 0; i < nc; ++i)
+    for (int64_t e : order[i]->elems) part[(int64_t)component[e] * uw + 5 * N] += 1;
+  // exact accumulation, parallel over states: a worker owns the words of its states in
+  // every component, so no two workers touch the same word (integer sums: order-free)
+  parallel_ranges(N, [&](int, int64_t s0, int64_t s1) {
+    for (int64_t i = 0; i < nc; ++i) {
+      const ConSeq& c = *order[i];
+      int64_t* u1 = part + (int64_t)component[c.elems.front()] * uw;
+      int64_t* um = part + (int64_t)component[c.elems.back()] * uw;
+      for (int64_t s = s0; s < s1; ++s) {
+        if (i < n1) {
+          cvcsp::add_exact(u1 + 4 * s, u1 + 4 * N + s, mu[(size_t)i * np + s]);
+        } else {
+          cvcsp::add_exact(u1 + 4 * s, u1 + 4 * N + s, dl[(size_t)i * np + s]);
+          cvcsp::add_exact(um + 4 * s, um + 4 * N + s, mu[(size_t)i * np + s]);
+        }
       }
     }
-  }
+  }, 1);
 
   // ---- segment tables: one slot per (segment, start state), in batches ----
   struct Seg { int64_t e0, e1; int32_t c1, c2; int64_t p; };
@@ -1038,26 +1130,45 @@ cv_status constrained_partials_locked(cv_hmm* h, int64_t nseq, const int64_t* of
 }
 
 // Final decode: every constrained element forced to its component's state; sequences whose
-// component has no feasible state are infeasible.  objective = sum of the f64 scores.
+// component has no feasible state are infeasible.  objective = sum of the f64 scores.  The
+// forced-state array is built on the device (fill -1, scatter the constrained elements of
+// `cs`); obs_staged: h->st_obs already holds the batch's observations.
 cv_status forced_decode_locked(cv_hmm* h, int64_t nseq, const int64_t* offsets, const int32_t* obs,
-                               const int32_t* component, const int32_t* comp_state, cv_opts o, int32_t* path_out,
+                               const int32_t* component, const int32_t* comp_state, cv_opts o,
+                               const std::vector<ConSeq>& cs, bool obs_staged, int32_t* path_out,
                                double* score_out, uint8_t* status_out, double* objective_out) {
   const int64_t base = offsets[0], total = offsets[nseq];
-  std::vector<int32_t> forced((size_t)total, -1);
-  for (int64_t e = base; e < total; ++e)
-    if (component[e] >= 0) forced[e] = comp_state[component[e]] >= 0 ? comp_state[component[e]] : 0;
-  o.forced = forced.data();
-  cv_status st = decode_host_locked(h, nseq, offsets, obs, o, path_out, score_out, status_out);
-  if (st != CV_OK) return st;
-  double obj = 0.0;
-  for (int64_t s = 0; s < nseq; ++s) {
-    for (int64_t e = offsets[s]; e < offsets[s + 1]; ++e)
-      if (component[e] >= 0 && comp_state[component[e]] < 0) {
-        status_out[s] = CV_SEQ_INFEASIBLE;
-        score_out[s] = -INFINITY;
-      }
-    obj += status_out[s] == CV_SEQ_INFEASIBLE ? -INFINITY : score_out[s];
+  std::vector<int64_t> el;
+  std::vector<int32_t> sv;
+  for (const auto& c : cs)
+    for (int64_t e : c.elems) {
+      el.push_back(e);
+      sv.push_back(comp_state[component[e]] >= 0 ? comp_state[component[e]] : 0);
+    }
+  hipStream_t stream = o.stream ? (hipStream_t)o.stream : h->stream;
+  cv_status st;
+  if ((st = h->st_forced.ensure((size_t)std::max<int64_t>(total, 1) * 4)) != CV_OK) return st;
+  if ((st = h->cs_ranges.ensure(std::max<size_t>(el.size(), 1) * 8)) != CV_OK) return st;
+  if ((st = h->cs_start.ensure(std::max<size_t>(sv.size(), 1) * 4)) != CV_OK) return st;
+  if (total > base) HIP_TRY(hipMemsetAsync(h->st_forced.as<int32_t>() + base, 0xFF, (size_t)(total - base) * 4, stream));
+  if (!el.empty()) {
+    HIP_TRY(hipMemcpyAsync(h->cs_ranges.p, el.data(), el.size() * 8, hipMemcpyHostToDevice, stream));
+    HIP_TRY(hipMemcpyAsync(h->cs_start.p, sv.data(), sv.size() * 4, hipMemcpyHostToDevice, stream));
+    const hipError_t err = cvk::launch_scatter_forced(h->cs_ranges.as<int64_t>(), h->cs_start.as<int32_t>(),
+                                                      (int64_t)el.size(), h->st_forced.as<int32_t>(), stream);
+    if (err != hipSuccess) return set_err(CV_EDEVICE, "forced-state scatter failed: %s", hipGetErrorString(err));
   }
+  o.forced = h->st_forced.as<int32_t>();
+  st = decode_host_locked(h, nseq, offsets, obs, o, path_out, score_out, status_out, obs_staged, true);
+  if (st != CV_OK) return st;
+  for (const auto& c : cs)
+    for (int64_t e : c.elems)
+      if (comp_state[component[e]] < 0) {
+        status_out[c.seq] = CV_SEQ_INFEASIBLE;
+        score_out[c.seq] = -INFINITY;
+      }
+  double obj = 0.0;  // sequential, in sequence order (the f64 sum's rounding is part of the spec)
+  for (int64_t s = 0; s < nseq; ++s) obj += status_out[s] == CV_SEQ_INFEASIBLE ? -INFINITY : score_out[s];
   if (objective_out) *objective_out = obj;
   return CV_OK;
 }
@@ -1145,19 +1256,20 @@ CV_API cv_status cv_decode_constrained(cv_hmm* h, int64_t nseq, const int64_t* o
   std::vector<ConSeq> cs;
   if ((st = constrained_validate(h, nseq, offsets, obs, component, ncomp, o, cs)) != CV_OK) return st;
   if (nseq == 0) return CV_OK;
-  const std::vector<int32_t> pairs = cvcsp::component_pairs(nseq, offsets, component);
+  const std::vector<int32_t> pairs = conseq_pairs(cs, component);
   const int64_t npairs = (int64_t)pairs.size() / 2;
   std::vector<int64_t> part((size_t)cvcsp::partial_words((int)h->N, ncomp, npairs), 0);
+  bool obs_staged = false;
   if ((st = constrained_partials_locked(h, nseq, offsets, obs, component, ncomp, pairs.data(), npairs, o,
-                                        part.data())) != CV_OK)
+                                        part.data(), &cs, &obs_staged)) != CV_OK)
     return st;
   uint64_t explored = 0;
   if ((st = select_locked((int32_t)h->N, ncomp, pairs.data(), npairs, part.data(), comp_state_out, &explored)) !=
       CV_OK)
     return st;
   h->last_explored = explored;
-  return forced_decode_locked(h, nseq, offsets, obs, component, comp_state_out, o, path_out, score_out, status_out,
-                              objective_out);
+  return forced_decode_locked(h, nseq, offsets, obs, component, comp_state_out, o, cs, obs_staged, path_out,
+                              score_out, status_out, objective_out);
 }
 
 CV_API cv_status cv_decode_forced_components(cv_hmm* h, int64_t nseq, const int64_t* offsets, const int32_t* obs,
@@ -1176,14 +1288,19 @@ CV_API cv_status cv_decode_forced_components(cv_hmm* h, int64_t nseq, const int6
   if (objective_out) *objective_out = 0.0;
   if (nseq == 0) return CV_OK;
   if ((st = check_batch(h, nseq, offsets)) != CV_OK) return st;
-  for (int64_t k = offsets[0]; k < offsets[nseq]; ++k)
-    if (component[k] < -1 || component[k] >= ncomp)
+  {
+    const int64_t k =
+        first_bad(offsets[0], offsets[nseq], [&](int64_t i) { return component[i] < -1 || component[i] >= ncomp; });
+    if (k >= 0)
       return set_err(CV_EINVAL, "component[%lld] = %d out of range [-1,%d)", (long long)k, component[k], ncomp);
+  }
   for (int32_t c = 0; c < ncomp; ++c)
     if (comp_state[c] < -1 || comp_state[c] >= h->N)
       return set_err(CV_EINVAL, "comp_state[%d] = %d out of range [-1,%lld)", c, comp_state[c], (long long)h->N);
-  return forced_decode_locked(h, nseq, offsets, obs, component, comp_state, o, path_out, score_out, status_out,
-                              objective_out);
+  std::vector<ConSeq> cs;
+  build_conseq(nseq, offsets, component, cs);
+  return forced_decode_locked(h, nseq, offsets, obs, component, comp_state, o, cs, false, path_out, score_out,
+                              status_out, objective_out);
 }
 
 CV_API cv_status cv_last_timing(cv_hmm* h, cv_timing* out) {

@@ -106,6 +106,11 @@ struct MaxMarginalArgs {
 };
 hipError_t launch_max_marginal(int np, const MaxMarginalArgs& a, int64_t ncon, hipStream_t stream);
 
+// forced[elems[k]] = states[k] for k < n (the constrained decode's forced-state array,
+// built on the device from the compact list of constrained elements)
+hipError_t launch_scatter_forced(const int64_t* elems, const int32_t* states, int64_t n, int32_t* forced,
+                                 hipStream_t stream);
+
 int trellis_padded_states(int n);  // 0 if the trellis kernel does not cover n
 hipError_t launch_trellis_fwd(int np, const TrellisFwdArgs& fa, int64_t nseq, hipStream_t stream);
 // Two equal-length sequences per workgroup (slots seq_begin + 2k, +2k+1), plain decode only;

@@ -312,11 +312,11 @@ __global__ __launch_bounds__(NP * 4) void trellis_fwd_f32(TrellisFwdArgs args) {
 // previous half-step (the other sequence's data, complete since the last barrier), so the
 // LDS latency after a barrier -- the bubble of the one-sequence kernel, where all four
 // waves of a SIMD wait for their first ds_read together -- is hidden; the second half is
-// loaded at the start of the half-step behind the first half's adds.  Same registers as
-// the one-sequence kernel (A image 64 + delta 32 at NP = 256).  Plain decode only (no EXT
-// features); the host pairs equal-length sequences and runs leftovers through
-// trellis_fwd_f32.  NP % 64 == 0 so that each half is whole float4s.
-template <int NP>
+// loaded at the start of the half-step behind the first half's adds.  Plain decode, plus
+// forced states (FRC: the consistency-constrained final decode) -- no other EXT features;
+// the host pairs equal-length sequences and runs leftovers through trellis_fwd_f32.
+// NP % 64 == 0 so that the delta blocks are whole float4s.
+template <int NP, bool FRC>
 __global__ __launch_bounds__(NP * 4) void trellis_fwd2_f32(TrellisFwdArgs args) {
   using G = TrellisGeom<NP>;
   constexpr int R = G::R;
@@ -344,6 +344,8 @@ __global__ __launch_bounds__(NP * 4) void trellis_fwd2_f32(TrellisFwdArgs args) 
   typedef const __attribute__((address_space(4))) int32_t* cobs_t;
   const cobs_t obsX = (cobs_t)(args.obs + e0[0]);
   const cobs_t obsY = (cobs_t)(args.obs + e0[1]);
+  const cobs_t frcX = (cobs_t)(FRC ? args.forced + e0[0] : nullptr);
+  const cobs_t frcY = (cobs_t)(FRC ? args.forced + e0[1] : nullptr);
   // uniform row bases (SGPRs); the lane adds j0
   float* const dX = args.delta + (e0[0] - args.delta_elem_base) * NP;
   float* const dY = args.delta + (e0[1] - args.delta_elem_base) * NP;
@@ -381,12 +383,14 @@ __global__ __launch_bounds__(NP * 4) void trellis_fwd2_f32(TrellisFwdArgs args) 
   };
   const int lds_w = (j0 / R) * S + (j0 % R) + (hi ? 1 : 0);
   auto clampT = [&](int t) { return t < T ? t : T - 1; };
+  // forced state (consistency constraint): every other state of that element is impossible
+  auto force = [&](float d, int f) -> float { return (FRC && f >= 0 && (int)jw != f) ? ninf_f() : d; };
 
   // ---- t = 0 for both sequences ----
   {
     const float ex = et_row(obs_x(0)), ey = et_row(obs_y(0));
     const float p = args.pi[jw];
-    const float dx = p + ex, dy = p + ey;
+    const float dx = force(p + ex, FRC ? frcX[0] : -1), dy = force(p + ey, FRC ? frcY[0] : -1);
     if (writer) {
       lds[0][0][lds_w] = dx;
       lds[1][0][lds_w] = dy;
@@ -405,6 +409,8 @@ __global__ __launch_bounds__(NP * 4) void trellis_fwd2_f32(TrellisFwdArgs args) 
   float eY;
   unsigned oY = obs_y(clampT(1));  // o_Y(t) for the coming X(t)
   unsigned oX = obs_x(clampT(2));  // o_X(t+1) for the coming Y(t)
+  // forced state of the coming half-step, loaded (SMEM) at the end of the previous one
+  int f_nx = FRC ? frcX[clampT(1)] : -1;
   lds_barrier();
   // delta rows stream through a rolling window of two 8-row blocks (P, Q): block k of the
   // lane's R rows lives in P for even k, Q for odd k, and each block is refilled with block
@@ -426,6 +432,7 @@ __global__ __launch_bounds__(NP * 4) void trellis_fwd2_f32(TrellisFwdArgs args) 
   // half-step's (row o_load); then o_load <- obs(t_obs) of the sequence `is_y`.
   auto half = [&](const float* dsrc, const float* nsrc, float* ldst, float* drow, int t, const float& e_use,
                   float& e_load, unsigned& o_load, bool is_y, int t_obs) {
+    const int f_use = f_nx;
     e_load = et_row(o_load);
     if (KB > 1) ld8(dsrc + 8, Q);
     float m0a = ninf_f(), m0b = ninf_f(), m1a = ninf_f(), m1b = ninf_f();
@@ -465,9 +472,11 @@ __global__ __launch_bounds__(NP * 4) void trellis_fwd2_f32(TrellisFwdArgs args) 
     float m = dpp_max_mirror(hi ? m1 : m0, hi ? m0 : m1);
     m = dpp_max_xor1(m);
     m = dpp_max_xor2(m);
-    const float dn = m + e_use;  // (d + a) + b, viterbi.rs:15-17
+    const float dn = force(m + e_use, f_use);  // (d + a) + b, viterbi.rs:15-17
     __builtin_amdgcn_sched_barrier(0);
     o_load = is_y ? obs_y(t_obs) : obs_x(t_obs);
+    // X(t) is followed by Y(t), Y(t) by X(t+1)
+    if (FRC) f_nx = is_y ? frcY[clampT(t)] : frcX[clampT(t + 1)];
     if (writer) {
       ldst[lds_w] = dn;
       float* row = drow + (size_t)t * NP;  // uniform
@@ -1265,6 +1274,18 @@ static hipError_t trellis_bt_np(const BacktrackArgs& ba, int64_t nseq, hipStream
   return hipGetLastError();
 }
 
+__global__ void scatter_forced(const int64_t* elems, const int32_t* states, int64_t n, int32_t* forced) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < n) forced[elems[k]] = states[k];
+}
+
+hipError_t launch_scatter_forced(const int64_t* elems, const int32_t* states, int64_t n, int32_t* forced,
+                                 hipStream_t stream) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(scatter_forced, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, elems, states, n, forced);
+  return hipGetLastError();
+}
+
 int trellis_padded_states(int n) {
   if (n <= 0 || n > 256) return 0;
   return ((n + 31) / 32) * 32;
@@ -1288,8 +1309,11 @@ static hipError_t trellis_fwd2_np(const TrellisFwdArgs& fa, int64_t npairs, hipS
   if constexpr (NP % 64 != 0) {
     return hipErrorInvalidValue;
   } else {
-    if (ext_args(fa)) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(trellis_fwd2_f32<NP>, dim3((unsigned)npairs), dim3(NP * 4), 0, stream, fa);
+    if (fa.ranges || fa.reverse || fa.last_row || fa.start || !fa.delta) return hipErrorInvalidValue;
+    if (fa.forced)
+      hipLaunchKernelGGL((trellis_fwd2_f32<NP, true>), dim3((unsigned)npairs), dim3(NP * 4), 0, stream, fa);
+    else
+      hipLaunchKernelGGL((trellis_fwd2_f32<NP, false>), dim3((unsigned)npairs), dim3(NP * 4), 0, stream, fa);
     return hipGetLastError();
   }
 }

@@ -1,0 +1,64 @@
+"""Throughput of the other BASELINE.json configs on one MI355X (documentation lines for
+DESIGN.md; bench.py keeps config 4 as the headline):
+  c2  N=45,  V=50,000, T~U[1,128], B=4,096          (plain decode, f32 + f64 re-score)
+  c3  N=64,  V=256,    T~U[32,1024], B=16,384       (plain decode, length-sorted schedule)
+  c5  config 4 + one constrained position in half the sequences, K=7 (cv_decode_constrained)
+Inputs resident in HBM for c2/c3 (device API); c5 goes through the host API (its exact
+search runs on the host between the GPU passes), so its line includes PCIe transfers.
+Prints one JSON line per config."""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "consistent-viterbi_amd"))
+import torch  # noqa: E402
+
+import cviterbi as cv  # noqa: E402
+from cviterbi import synth  # noqa: E402
+
+REPS = int(os.environ.get("REPS", "5"))
+which = sys.argv[1:] or ["c2", "c3", "c5"]
+dev = torch.device("cuda:0")
+stream = torch.cuda.Stream(dev)
+torch.cuda.set_stream(stream)
+
+for name in which:
+    c = synth.config(name)
+    n = c["pi"].shape[0]
+    off, obs = c["offsets"], c["obs"]
+    B = len(off) - 1
+    cells = int(off[-1]) * n
+    h = cv.HMM(c["pi"], c["a"], c["b"])
+    if name in ("c2", "c3"):
+        o_d, ob_d = torch.from_numpy(off).to(dev), torch.from_numpy(obs).to(dev)
+        p_d = torch.empty(len(obs), dtype=torch.int32, device=dev)
+        s_d = torch.empty(B, dtype=torch.float64, device=dev)
+        st_d = torch.empty(B, dtype=torch.uint8, device=dev)
+
+        def run():
+            cv.decode_batch_device(h, o_d, ob_d, p_d, s_d, st_d, offsets_host=off, stream=stream.cuda_stream)
+    else:
+        comp = c["component"]
+
+        def run():
+            cv.decode_constrained(h, off, obs, comp, 7)
+    run()
+    run()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(REPS):
+        run()
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / REPS
+    t = cv.last_timing(h)
+    out = {"config": name, "states": n, "sequences": B, "elements": int(off[-1]), "ms_per_decode": dt * 1e3,
+           "cells_per_s": cells / dt, "seqs_per_s": B / dt, "last_call_timing": t}
+    if name in ("c2", "c3"):
+        alg = (9 * n + 8) * int(off[-1]) + 8 * B
+        out["alg_hbm_frac"] = alg / (t["fwd_ms"] * 1e-3) / 8.0e12 if t["fwd_ms"] else None
+        out["valu_pairs_frac"] = n * n * (int(off[-1]) - B) / (t["fwd_ms"] * 1e-3) / 3.93e13 if t["fwd_ms"] else None
+    print(json.dumps(out), flush=True)
