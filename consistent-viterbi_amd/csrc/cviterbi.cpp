@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -117,6 +118,7 @@ struct cv_hmm {
   DevBuf st_off, st_obs, st_path, st_score, st_status, st_forced;
   DevBuf cs_ranges, cs_delta, cs_g, cs_mu, cs_start, cs_zero;  // constrained-decode scratch
   std::vector<int32_t> order_host;
+  std::vector<float> host_dl, host_mu;  // constrained-decode term rows (kept: no per-call page faults)
   // timing events of the last call
   std::vector<hipEvent_t> ev;  // 4 per chunk: fwd start/end (main stream), bt start/end
   int64_t last_launches = 0;
@@ -287,6 +289,19 @@ cv_status make_hmm(int N, const std::vector<int64_t>& bdims, const double* pi, c
   h->device = device;
   *out = h.release();
   return CV_OK;
+}
+
+// CV_TRACE=1: host-side phase timestamps of the constrained decode on stderr (profiling aid).
+void trace_mark(const char* what) {
+  static const bool on = [] {
+    const char* e = getenv("CV_TRACE");
+    return e && *e && *e != '0';
+  }();
+  if (!on) return;
+  static thread_local auto last = std::chrono::steady_clock::now();
+  const auto now = std::chrono::steady_clock::now();
+  fprintf(stderr, "[cv] %-28s +%8.3f ms\n", what, std::chrono::duration<double, std::milli>(now - last).count());
+  last = now;
 }
 
 // Host worker threads for the O(elements) loops of the host API (validation, constraint
@@ -981,6 +996,7 @@ cv_status constrained_partials_locked(cv_hmm* h, int64_t nseq, const int64_t* of
   HIP_TRY(hipMemcpyAsync(h->st_obs.as<int32_t>() + base, obs + base, (size_t)(total - base) * 4,
                          hipMemcpyHostToDevice, stream));
   if (obs_staged) *obs_staged = true;
+  trace_mark("obs H2D enqueued");
 
   // ---- prefix / suffix passes for every constrained sequence (m == 1 ones first) ----
   std::vector<const ConSeq*> order;
@@ -1004,7 +1020,8 @@ cv_status constrained_partials_locked(cv_hmm* h, int64_t nseq, const int64_t* of
   if ((st = h->cs_g.ensure((size_t)nc * np * 4)) != CV_OK) return st;
   if ((st = h->cs_mu.ensure((size_t)nc * np * 4)) != CV_OK) return st;
   if ((st = h->cs_zero.ensure((size_t)nc * np * 4)) != CV_OK) return st;
-  if ((st = h->st_status.ensure((size_t)std::max<int64_t>(nseq, nslot_max))) != CV_OK) return st;
+  if ((st = h->st_status.ensure((size_t)std::max<int64_t>(nseq, std::max<int64_t>(nslot_max, 2 * nc)))) != CV_OK)
+    return st;
   HIP_TRY(hipMemcpyAsync(h->cs_ranges.p, rg.data(), rg.size() * 8, hipMemcpyHostToDevice, stream));
   HIP_TRY(hipMemsetAsync(h->cs_zero.p, 0, (size_t)nc * np * 4, stream));
   cvk::TrellisFwdArgs fa{};
@@ -1015,16 +1032,27 @@ cv_status constrained_partials_locked(cv_hmm* h, int64_t nseq, const int64_t* of
   fa.status = h->st_status.as<uint8_t>();
   fa.nobs = (int)h->V;
   fa.ranges = h->cs_ranges.as<int64_t>();
+  // one launch, longest range first: slots [0, nc) = prefixes, forward -> delta_{t_1};
+  // slots [nc, 2nc) = suffixes, the backward pass = same kernel on a^T with pi = 0,
+  // reversed -> g_{t_m+1}
   fa.last_row = h->cs_delta.as<float>();
-  hipError_t err = cvk::launch_trellis_fwd(np, fa, nc, stream);  // delta_{t_1}: forward over the prefix
-  if (err == hipSuccess) {
-    fa.a_img = h->t_aimg_T.as<float>();  // g_{t_m+1}: backward pass = same kernel on a^T, pi = 0, reversed
-    fa.pi = h->t_pi0.as<float>();
-    fa.ranges = h->cs_ranges.as<int64_t>() + 2 * nc;
-    fa.reverse = 1;
-    fa.last_row = h->cs_g.as<float>();
-    err = cvk::launch_trellis_fwd(np, fa, nc, stream);
+  fa.split = nc;
+  fa.a_img2 = h->t_aimg_T.as<float>();
+  fa.pi2 = h->t_pi0.as<float>();
+  fa.last_row2 = h->cs_g.as<float>();
+  {
+    std::vector<int32_t> so((size_t)2 * nc);
+    std::iota(so.begin(), so.end(), 0);
+    std::stable_sort(so.begin(), so.end(), [&](int32_t x, int32_t y) {
+      return rg[2 * x + 1] - rg[2 * x] > rg[2 * y + 1] - rg[2 * y];
+    });
+    if ((st = h->ws_order.ensure(so.size() * 4)) != CV_OK) return st;
+    HIP_TRY(hipMemcpyAsync(h->ws_order.p, so.data(), so.size() * 4, hipMemcpyHostToDevice, stream));
+    fa.slot_order = h->ws_order.as<int32_t>();
+    HIP_TRY(hipStreamSynchronize(stream));  // `so` is a local buffer
+    trace_mark("obs H2D + slot order");
   }
+  hipError_t err = cvk::launch_trellis_fwd(np, fa, 2 * nc, stream);
   cvk::MaxMarginalArgs ma{};
   ma.g = h->cs_g.as<float>();
   ma.ranges_suffix = h->cs_ranges.as<int64_t>() + 2 * nc;
@@ -1042,30 +1070,50 @@ cv_status constrained_partials_locked(cv_hmm* h, int64_t nseq, const int64_t* of
     err = cvk::launch_max_marginal(np, ma, nc - n1, stream);
   }
   if (err != hipSuccess) return set_err(CV_EDEVICE, "max-marginal launch failed: %s", hipGetErrorString(err));
-  std::vector<float> dl((size_t)nc * np), mu((size_t)nc * np);
-  HIP_TRY(hipMemcpyAsync(dl.data(), h->cs_delta.p, dl.size() * 4, hipMemcpyDeviceToHost, stream));
-  HIP_TRY(hipMemcpyAsync(mu.data(), h->cs_mu.p, mu.size() * 4, hipMemcpyDeviceToHost, stream));
+  trace_mark("term launches enqueued");
+  std::vector<float>& dl = h->host_dl;
+  std::vector<float>& mu = h->host_mu;
+  if (dl.size() < (size_t)nc * np) dl.resize((size_t)nc * np);
+  if (mu.size() < (size_t)nc * np) mu.resize((size_t)nc * np);
+  HIP_TRY(hipMemcpyAsync(dl.data(), h->cs_delta.p, (size_t)nc * np * 4, hipMemcpyDeviceToHost, stream));
+  HIP_TRY(hipMemcpyAsync(mu.data(), h->cs_mu.p, (size_t)nc * np * 4, hipMemcpyDeviceToHost, stream));
   HIP_TRY(hipStreamSynchronize(stream));
+  trace_mark("terms device + D2H");
   for (int64_t i = 0; i < nc; ++i)
     for (int64_t e : order[i]->elems) part[(int64_t)component[e] * uw + 5 * N] += 1;
-  // exact accumulation, parallel over states: a worker owns the words of its states in
-  // every component, so no two workers touch the same word (integer sums: order-free)
+  // exact accumulation, parallel over states into worker-local words (the components'
+  // word blocks are not cache-line aligned: writing `part` directly would false-share),
+  // added into `part` at the end (integer sums: order-free)
   parallel_ranges(N, [&](int, int64_t s0, int64_t s1) {
+    const int64_t ns = s1 - s0;
+    std::vector<int64_t> loc((size_t)ncomp * ns * 5, 0);  // [comp][state][4 limbs], then [comp][state] -inf counts
+    int64_t* lim = loc.data();
+    int64_t* cnt = loc.data() + (size_t)ncomp * ns * 4;
     for (int64_t i = 0; i < nc; ++i) {
       const ConSeq& c = *order[i];
-      int64_t* u1 = part + (int64_t)component[c.elems.front()] * uw;
-      int64_t* um = part + (int64_t)component[c.elems.back()] * uw;
+      const int64_t c1 = component[c.elems.front()], cm = component[c.elems.back()];
+      const float* mr = &mu[(size_t)i * np];
+      const float* dr = &dl[(size_t)i * np];
       for (int64_t s = s0; s < s1; ++s) {
+        const int64_t q1 = c1 * ns + (s - s0), qm = cm * ns + (s - s0);
         if (i < n1) {
-          cvcsp::add_exact(u1 + 4 * s, u1 + 4 * N + s, mu[(size_t)i * np + s]);
+          cvcsp::add_exact(lim + 4 * q1, cnt + q1, mr[s]);
         } else {
-          cvcsp::add_exact(u1 + 4 * s, u1 + 4 * N + s, dl[(size_t)i * np + s]);
-          cvcsp::add_exact(um + 4 * s, um + 4 * N + s, mu[(size_t)i * np + s]);
+          cvcsp::add_exact(lim + 4 * q1, cnt + q1, dr[s]);
+          cvcsp::add_exact(lim + 4 * qm, cnt + qm, mr[s]);
         }
       }
     }
+    for (int64_t c = 0; c < ncomp; ++c)
+      for (int64_t s = s0; s < s1; ++s) {
+        const int64_t q = c * ns + (s - s0);
+        int64_t* u = part + c * uw;
+        for (int k = 0; k < 4; ++k) u[4 * s + k] += lim[4 * q + k];
+        u[4 * N + s] += cnt[q];
+      }
   }, 1);
 
+  trace_mark("exact sums");
   // ---- segment tables: one slot per (segment, start state), in batches ----
   struct Seg { int64_t e0, e1; int32_t c1, c2; int64_t p; };
   std::vector<Seg> segs;
@@ -1158,9 +1206,11 @@ cv_status forced_decode_locked(cv_hmm* h, int64_t nseq, const int64_t* offsets, 
                                                       (int64_t)el.size(), h->st_forced.as<int32_t>(), stream);
     if (err != hipSuccess) return set_err(CV_EDEVICE, "forced-state scatter failed: %s", hipGetErrorString(err));
   }
+  trace_mark("forced array (device)");
   o.forced = h->st_forced.as<int32_t>();
   st = decode_host_locked(h, nseq, offsets, obs, o, path_out, score_out, status_out, obs_staged, true);
   if (st != CV_OK) return st;
+  trace_mark("forced decode (sync)");
   for (const auto& c : cs)
     for (int64_t e : c.elems)
       if (comp_state[component[e]] < 0) {
@@ -1253,8 +1303,10 @@ CV_API cv_status cv_decode_constrained(cv_hmm* h, int64_t nseq, const int64_t* o
   cv_opts o = opts ? *opts : default_opts();
   for (int32_t c = 0; c < ncomp; ++c) comp_state_out[c] = -1;
   if (objective_out) *objective_out = 0.0;
+  trace_mark("decode_constrained: start");
   std::vector<ConSeq> cs;
   if ((st = constrained_validate(h, nseq, offsets, obs, component, ncomp, o, cs)) != CV_OK) return st;
+  trace_mark("validate + constrained list");
   if (nseq == 0) return CV_OK;
   const std::vector<int32_t> pairs = conseq_pairs(cs, component);
   const int64_t npairs = (int64_t)pairs.size() / 2;
@@ -1263,11 +1315,13 @@ CV_API cv_status cv_decode_constrained(cv_hmm* h, int64_t nseq, const int64_t* o
   if ((st = constrained_partials_locked(h, nseq, offsets, obs, component, ncomp, pairs.data(), npairs, o,
                                         part.data(), &cs, &obs_staged)) != CV_OK)
     return st;
+  trace_mark("partials (device + exact sums)");
   uint64_t explored = 0;
   if ((st = select_locked((int32_t)h->N, ncomp, pairs.data(), npairs, part.data(), comp_state_out, &explored)) !=
       CV_OK)
     return st;
   h->last_explored = explored;
+  trace_mark("select");
   return forced_decode_locked(h, nseq, offsets, obs, component, comp_state_out, o, cs, obs_staged, path_out,
                               score_out, status_out, objective_out);
 }

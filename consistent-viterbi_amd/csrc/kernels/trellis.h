@@ -28,6 +28,15 @@ struct TrellisFwdArgs {
   float* last_row;         // [nslot][NP] final delta row of each slot (slot - seq_begin)
   const int32_t* start;    // [nslot] (slot - seq_begin): s >= 0 starts the range in state s with
                            // delta = 0 there (-inf elsewhere, no pi/emission term); -1: normal
+  // two passes in one launch (constrained terms: prefixes forward, suffixes reversed):
+  // ranged slots >= split use a_img2 / pi2, traverse reversed and write their final row to
+  // last_row2 + (slot - split) * NP; slot_order (optional) maps blockIdx -> ranged slot
+  // (longest first, so the ragged tail is short ranges)
+  int64_t split;
+  const float* a_img2;
+  const float* pi2;
+  float* last_row2;
+  const int32_t* slot_order;
 };
 
 struct BacktrackArgs {

@@ -160,14 +160,16 @@ __global__ __launch_bounds__(NP * 4) void trellis_fwd_f32(TrellisFwdArgs args) {
   const int jw = j0 + (hi ? 1 : 0);
   const bool writer = (rg & 3) == 0;  // rg 0 stores column j0, rg 4 column j0 + 1
 
-  const int64_t slot = args.seq_begin + blockIdx.x;
+  const int64_t slot =
+      (EXT && args.slot_order) ? (int64_t)args.slot_order[blockIdx.x] : args.seq_begin + (int64_t)blockIdx.x;
+  const bool second = EXT && args.split > 0 && slot >= args.split;  // second pass of a two-pass launch
   int64_t seq, e0;
   int T;
   seq_range<EXT>(args, slot, seq, e0, T);
   if (T <= 0) return;
   // constant address space: uniform loads become s_load (SMEM), off the vmcnt queue.
   // A reversed range walks obs[end-1], obs[end-2], ... (ob_step = -1).
-  const bool rev = EXT && args.reverse;
+  const bool rev = EXT && (args.reverse || second);
   const int ob_step = rev ? -1 : 1;
   const int64_t ob0 = rev ? e0 + T - 1 : e0;
   const __attribute__((address_space(4))) int32_t* obs =
@@ -175,7 +177,10 @@ __global__ __launch_bounds__(NP * 4) void trellis_fwd_f32(TrellisFwdArgs args) {
   const __attribute__((address_space(4))) int32_t* frc =
       (const __attribute__((address_space(4))) int32_t*)((EXT && args.forced) ? args.forced + ob0 : nullptr);
   float* __restrict__ drow = (!EXT || args.delta) ? args.delta + (e0 - args.delta_elem_base) * NP + jw : nullptr;
-  float* __restrict__ lrow = (EXT && args.last_row) ? args.last_row + (slot - args.seq_begin) * NP + jw : nullptr;
+  float* __restrict__ lrow = !EXT ? nullptr
+                             : second ? args.last_row2 + (slot - args.split) * NP + jw
+                             : args.last_row ? args.last_row + (slot - args.seq_begin) * NP + jw : nullptr;
+  const float* __restrict__ pi = second ? args.pi2 : args.pi;
   const float* __restrict__ etj = args.et + jw;
   const unsigned V = (unsigned)args.nobs;
 
@@ -186,7 +191,7 @@ __global__ __launch_bounds__(NP * 4) void trellis_fwd_f32(TrellisFwdArgs args) {
   __builtin_amdgcn_s_setprio(3);
   float a_reg[2 * R];
   {
-    const float4* img = reinterpret_cast<const float4*>(args.a_img) + (size_t)w * (R / 2) * 64 + lane;
+    const float4* img = reinterpret_cast<const float4*>(second ? args.a_img2 : args.a_img) + (size_t)w * (R / 2) * 64 + lane;
 #pragma unroll
     for (int q = 0; q < R / 2; ++q) {
       const float4 v = img[q * 64];
@@ -215,7 +220,7 @@ __global__ __launch_bounds__(NP * 4) void trellis_fwd_f32(TrellisFwdArgs args) {
   // ---- t = 0: d0 = pi + b[:,o0]  (hmm.rs:415-418, cp.rs:98-100) ----
   {
     const float e = et_row(obs_s(0));
-    float d0 = args.pi[jw] + e;
+    float d0 = pi[jw] + e;
     if (EXT && args.start) {  // segment table column: start in state s, score 0 (cfn.rs:11-34 pattern)
       const int s = args.start[slot - args.seq_begin];
       if (s >= 0) d0 = (jw == s) ? 0.0f : ninf_f();
@@ -1237,7 +1242,7 @@ hipError_t launch_max_marginal(int np, const MaxMarginalArgs& a, int64_t ncon, h
 // Host-side launchers (called from the C-ABI layer).  Forward and backtrack are launched
 // separately so the host can run chunk k's backtrack beside chunk k+1's forward pass.
 static bool ext_args(const TrellisFwdArgs& fa) {
-  return fa.forced || fa.ranges || fa.reverse || fa.last_row || fa.start || !fa.delta;
+  return fa.forced || fa.ranges || fa.reverse || fa.last_row || fa.start || !fa.delta || fa.split || fa.slot_order;
 }
 
 template <int NP>
