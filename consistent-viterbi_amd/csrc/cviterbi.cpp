@@ -105,7 +105,7 @@ struct cv_hmm {
 
   // trellis kernel tables (f32, padded to NP)
   int np = 0;
-  DevBuf t_aimg, t_aimg_mfma, t_pi, t_et, t_at;
+  DevBuf t_aimg, t_aimg_mfma, t_pi, t_et, t_at, t_arm;  // t_arm: row-major A (one-wave kernel)
   DevBuf t_aimg_T, t_pi0;  // reversed (backward) pass: VALU image of a^T, pi = 0
   // f64 tables (generic f64 kernel + re-scoring): pi[N], a[N*N], et[V][N]
   bool f64_ready = false;
@@ -184,10 +184,10 @@ cv_status ensure_trellis_tables(cv_hmm* h) {
           for (int c = 0; c < 4; ++c)
             img2[((((size_t)w * (np / 32) + t) * 4 + q) * 64 + lane) * 4 + c] =
                 A(32 * t + c + 8 * q + 4 * (lane >> 5), 32 * w + (lane & 31));
-  std::vector<float> pi(np, NI), at((size_t)np * np, NI), et((size_t)V * np, NI);
+  std::vector<float> pi(np, NI), at((size_t)np * np, NI), arm((size_t)np * np, NI), et((size_t)V * np, NI);
   for (int j = 0; j < N; ++j) pi[j] = f32(h->pi[j]);
   for (int i = 0; i < N; ++i)
-    for (int j = 0; j < N; ++j) at[(size_t)j * np + i] = f32(h->a[(size_t)i * N + j]);
+    for (int j = 0; j < N; ++j) at[(size_t)j * np + i] = arm[(size_t)i * np + j] = f32(h->a[(size_t)i * N + j]);
   for (int j = 0; j < N; ++j)
     for (int64_t o = 0; o < V; ++o) et[(size_t)o * np + j] = f32(h->b[(size_t)j * V + o]);
   cv_status st;
@@ -213,6 +213,7 @@ cv_status ensure_trellis_tables(cv_hmm* h) {
   }
   if ((st = upload(h->t_pi, pi.data(), pi.size() * 4)) != CV_OK) return st;
   if ((st = upload(h->t_at, at.data(), at.size() * 4)) != CV_OK) return st;
+  if ((st = upload(h->t_arm, arm.data(), arm.size() * 4)) != CV_OK) return st;
   if ((st = upload(h->t_et, et.data(), et.size() * 4)) != CV_OK) return st;
   h->np = np;
   return CV_OK;
@@ -367,6 +368,27 @@ hipEvent_t get_event(cv_hmm* h, size_t i) {
   return h->ev[i];
 }
 
+cvk::BacktrackArgs make_bt_args(cv_hmm* h, unsigned char* wsb, const int64_t* offsets_host,
+                                const int64_t* offsets_dev, const int32_t* obs_dev, const int32_t* order_dev,
+                                const std::pair<int64_t, int64_t>& c, int32_t* path_dev, double* score_dev,
+                                uint8_t* status_dev) {
+  cvk::BacktrackArgs ba{};
+  ba.delta = reinterpret_cast<const float*>(wsb);
+  ba.delta_elem_base = offsets_host[c.first];
+  ba.at = h->t_at.as<float>();
+  ba.offsets = offsets_dev;
+  ba.obs = obs_dev;
+  ba.order = order_dev;
+  ba.seq_begin = c.first;
+  ba.seq_end = c.second;
+  ba.nstates = h->N;
+  ba.path = path_dev;
+  ba.score = score_dev;
+  ba.score32 = nullptr;
+  ba.status = status_dev;
+  return ba;
+}
+
 // Core device-side decode.  All pointers are device pointers except offsets_host.
 cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, const int64_t* offsets_dev,
                         const int32_t* obs_dev, const cv_opts& o, int32_t* path_dev, double* score_dev,
@@ -432,10 +454,13 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
   // pass of chunk k+1 runs while chunk k backtracks, out of a double-buffered workspace.
   // At least ~2,048 sequences per chunk (8 per CU), at most 8 chunks unless the
   // workspace cap forces more.
-  const bool serial = (o.flags & CV_FLAG_SERIAL) != 0;
+  // N <= 64: one wave per sequence, forward and backtrack fused (trellis_wave64_f32); its
+  // chunks run back to back on one stream (nothing to overlap)
+  const bool wave = use_trellis && !use_mfma && h->np == 64 && !(o.flags & CV_FLAG_NO_WAVE);
+  const bool serial = (o.flags & CV_FLAG_SERIAL) != 0 || wave;
   // Sequences per forward workgroup: 2 (trellis_fwd2_f32, equal-length pairs; default) or 1
   // (trellis_fwd_f32: leftovers, MFMA, N not a multiple of 64).
-  const bool plain = use_trellis && !use_mfma && cvk::trellis_pair_supported(h->np);
+  const bool plain = use_trellis && !use_mfma && !wave && cvk::trellis_pair_supported(h->np);
   const int group = (!plain || (o.flags & CV_FLAG_NO_PAIR)) ? 1 : 2;
   const uint64_t half_cap = std::max<uint64_t>(serial ? cap : cap / 2, per_elem);
   uint64_t nchunks = std::max<uint64_t>(1, (total_elems * per_elem + half_cap - 1) / half_cap);
@@ -553,7 +578,12 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
       fa.status = status_dev;
       fa.nobs = (int)h->V;
       fa.forced = o.forced;
-      if (use_mfma) {
+      if (wave) {
+        fa.a_img = h->t_arm.as<float>();
+        err = cvk::launch_trellis_wave64(fa, make_bt_args(h, wsb, offsets_host, offsets_dev, obs_dev, order_dev, c,
+                                                          path_dev, score_dev, status_dev),
+                                         n, stream);
+      } else if (use_mfma) {
         fa.a_img = h->t_aimg_mfma.as<float>();
         err = cvk::launch_trellis_mfma(h->np, mt, fa, n, stream);
       } else {
@@ -606,26 +636,14 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
     if (!serial) HIP_TRY(hipStreamWaitEvent(bts, f1, 0));
     HIP_TRY(hipEventRecord(b0, bts));
     if (use_trellis) {
-      cvk::BacktrackArgs ba{};
-      ba.delta = reinterpret_cast<const float*>(wsb);
-      ba.delta_elem_base = offsets_host[c.first];
-      ba.at = h->t_at.as<float>();
-      ba.offsets = offsets_dev;
-      ba.obs = obs_dev;
-      ba.order = order_dev;
-      ba.seq_begin = c.first;
-      ba.seq_end = c.second;
-      ba.nstates = h->N;
-      ba.path = path_dev;
-      ba.score = score_dev;
-      ba.score32 = nullptr;
-      ba.status = status_dev;
+      const cvk::BacktrackArgs ba =
+          make_bt_args(h, wsb, offsets_host, offsets_dev, obs_dev, order_dev, c, path_dev, score_dev, status_dev);
       // overlap mode: at most ONE backtrack workgroup (one 64-VGPR wave per SIMD) per CU, so
       // the next forward workgroup (MFMA: 2 waves x 200 VGPRs per SIMD; VALU: 4 x 104) always
       // finds its registers free: reserve 100 KiB of LDS (2 x 100 > 160 KiB)
       // the last chunk's backtrack has the device to itself: full occupancy
       const int reserve = (serial || ci + 1 == chunks.size()) ? 0 : 100 * 1024;
-      err = cvk::launch_trellis_bt(h->np, ba, n, bts, reserve);
+      err = wave ? hipSuccess : cvk::launch_trellis_bt(h->np, ba, n, bts, reserve);  // wave: fused
       if (err == hipSuccess && o.rescore_f64) {
         cvk::RescoreArgs ra{};
         ra.path = path_dev;

@@ -137,6 +137,18 @@ __device__ __forceinline__ float dpp_max_xor1(float x) {
   asm volatile("s_nop 1\n\tv_max_f32_dpp %0, %0, %0 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf" : "+v"(x));
   return x;
 }
+__device__ __forceinline__ float dpp_max_xor1_other(float mine, float other) {
+  asm volatile("s_nop 1\n\tv_max_f32_dpp %0, %1, %0 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf"
+               : "+v"(mine)
+               : "v"(other));
+  return mine;
+}
+__device__ __forceinline__ float dpp_max_xor2_other(float mine, float other) {
+  asm volatile("s_nop 1\n\tv_max_f32_dpp %0, %1, %0 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf"
+               : "+v"(mine)
+               : "v"(other));
+  return mine;
+}
 __device__ __forceinline__ float dpp_max_xor2(float x) {
   asm volatile("s_nop 1\n\tv_max_f32_dpp %0, %0, %0 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf" : "+v"(x));
   return x;
@@ -904,27 +916,16 @@ __device__ __forceinline__ int first_argmax_vl(const float (&s)[VL], float M, in
   return VL * L + __builtin_amdgcn_readlane(fk, L);
 }
 
-template <int NP>
-__global__ __launch_bounds__(256) void backtrack_v_f32(BacktrackArgs args) {
-  constexpr int VL = NP / 64;
+// Backtrack of ONE sequence by one wave (lane l owns states VL*l .. VL*l+VL-1): drow / at
+// point at this lane's first state of delta row 0 / of A^T row 0; badobs: the forward pass
+// flagged the sequence.  Shared by backtrack_v_f32 and the fused small-N kernel.
+template <int VL, int NP>
+__device__ __forceinline__ void backtrack_one(const BacktrackArgs& args, int64_t seq, int64_t e0, int T, int lane,
+                                              const float* __restrict__ drow, const float* __restrict__ at,
+                                              bool badobs) {
   constexpr int PF = 8;
-  static_assert(NP % 64 == 0, "backtrack_v_f32 needs NP % 64 == 0");
-  const int lane = threadIdx.x & 63;
-  const int64_t slot = args.seq_begin + (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (slot >= args.seq_end) return;
-  const int64_t seq = args.order ? (int64_t)args.order[slot] : slot;
-  const int64_t e0 = args.offsets[seq];
-  const int T = (int)(args.offsets[seq + 1] - e0);
-  if (T <= 0) {
-    if (lane == 0) {
-      args.score[seq] = 0.0;
-      args.status[seq] = CVK_SEQ_EMPTY;
-    }
-    return;
-  }
   int32_t* __restrict__ path = args.path + e0;
   // padded states (>= N) hold -inf in delta and A^T, so they never win a feasible argmax
-  const float* __restrict__ drow = args.delta + (e0 - args.delta_elem_base) * NP + VL * lane;
   auto load_row = [&](int r, float (&dst)[VL]) {
     if (r >= 0) {
       ld_vl<VL>(drow + (size_t)r * NP, dst);
@@ -948,12 +949,11 @@ __global__ __launch_bounds__(256) void backtrack_v_f32(BacktrackArgs args) {
     bv = wave_max(lane_max(last));
     cur = (bv > ninf_f()) ? first_argmax_vl<VL>(last, bv, lane) : 0;
   }
-  const uint8_t prior = args.status[seq];
-  if (!(bv > ninf_f()) || prior == CVK_SEQ_BADOBS) {
+  if (!(bv > ninf_f()) || badobs) {
     for (int t = lane; t < T; t += 64) path[t] = 0;
     if (lane == 0) {
       args.score[seq] = (double)ninf_f();
-      args.status[seq] = prior == CVK_SEQ_BADOBS ? CVK_SEQ_BADOBS : CVK_SEQ_INFEASIBLE;
+      args.status[seq] = badobs ? CVK_SEQ_BADOBS : CVK_SEQ_INFEASIBLE;
     }
     return;
   }
@@ -961,7 +961,6 @@ __global__ __launch_bounds__(256) void backtrack_v_f32(BacktrackArgs args) {
   int pathreg = 0;
   if (lane == ((T - 1) & 63)) pathreg = cur;
   if (((T - 1) & 63) == 0 && lane == 0) path[T - 1] = cur;
-  const float* __restrict__ at = args.at + VL * lane;
   float ring[PF][VL];
 #pragma unroll
   for (int u = 0; u < PF; ++u) load_row(T - 2 - u, ring[u]);
@@ -991,6 +990,139 @@ __global__ __launch_bounds__(256) void backtrack_v_f32(BacktrackArgs args) {
     args.score[seq] = (double)score32;  // f64 re-score: rescore_f64_lanes (after this kernel)
     if (args.score32) args.score32[seq] = score32;
   }
+}
+
+template <int NP>
+__global__ __launch_bounds__(256) void backtrack_v_f32(BacktrackArgs args) {
+  constexpr int VL = NP / 64;
+  static_assert(NP % 64 == 0, "backtrack_v_f32 needs NP % 64 == 0");
+  const int lane = threadIdx.x & 63;
+  const int64_t slot = args.seq_begin + (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (slot >= args.seq_end) return;
+  const int64_t seq = args.order ? (int64_t)args.order[slot] : slot;
+  const int64_t e0 = args.offsets[seq];
+  const int T = (int)(args.offsets[seq + 1] - e0);
+  if (T <= 0) {
+    if (lane == 0) {
+      args.score[seq] = 0.0;
+      args.status[seq] = CVK_SEQ_EMPTY;
+    }
+    return;
+  }
+  backtrack_one<VL, NP>(args, seq, e0, T, lane, args.delta + (e0 - args.delta_elem_base) * NP + VL * lane,
+                        args.at + VL * lane, args.status[seq] == CVK_SEQ_BADOBS);
+}
+
+// ---------------------------------------------------------------------------------
+// trellis_wave64_f32<FRC>: small N (NP = 64) -- ONE WAVE per sequence, forward pass and
+// backtrack fused, no workgroup barrier and no cross-wave anything.
+// Forward: lane = 4cq + rg holds rows [16rg, 16rg+16) of columns 4cq..4cq+3 of A (64
+// VGPRs, from the row-major table `a_rm`); delta_{t-1} is read from the wave's own LDS
+// row with four ds_read_b128 (4 distinct addresses, padded stride 20: conflict-free); per
+// pair one v_add_f32 and half a v_max3_f32; the 4 row-group partials of the 4 columns are
+// folded across the lane quad (xor1 keeps a column pair, xor2 one column: 3 DPP maxima +
+// 6 selects) so every lane ends with ONE column jw = 4cq + 2(rg&1) + (rg>>1) and stores it.
+// LDS instructions of one wave execute in order, so the next step's reads see this step's
+// writes without a barrier.  A workgroup holds 4 independent waves (sequences).
+// Backtrack (after an agent-scope acquire, so the delta rows this wave stored are read back
+// from L2): backtrack_v_f32's loop with VL = 1.  The f64 re-score runs afterwards
+// (rescore_f64_lanes).  Roofline: VALU issue, like the large-N kernels, without their
+// barrier and fold tail; the backtrack's dependent loads overlap other waves' forward work.
+template <bool FRC>
+__global__ __launch_bounds__(256) void trellis_wave64_f32(TrellisFwdArgs args, BacktrackArgs bargs) {
+  constexpr int NP = 64;
+  constexpr int LS = 20;  // padded LDS stride of a 16-row group
+  __shared__ __attribute__((aligned(16))) float lds_all[4][2][4 * LS];
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  const int rg = lane & 3, cq = lane >> 2;
+  const int p = rg & 1, q = rg >> 1;
+  const int jw = 4 * cq + 2 * p + q;  // this lane's column after the fold
+  const int64_t slot = args.seq_begin + 4 * (int64_t)blockIdx.x + wv;
+  if (slot >= bargs.seq_end) return;
+  int64_t seq, e0;
+  int T;
+  seq_range<false>(args, slot, seq, e0, T);
+  if (T <= 0) {
+    if (lane == 0) {
+      bargs.score[seq] = 0.0;
+      bargs.status[seq] = CVK_SEQ_EMPTY;
+    }
+    return;
+  }
+  float(*lds)[4 * LS] = lds_all[wv];
+  typedef const __attribute__((address_space(4))) int32_t* cobs_t;
+  const cobs_t obs = (cobs_t)(args.obs + e0);
+  const cobs_t frc = (cobs_t)(FRC ? args.forced + e0 : nullptr);
+  float* __restrict__ drow = args.delta + (e0 - args.delta_elem_base) * NP;
+  const unsigned V = (unsigned)args.nobs;
+  float a_reg[64];  // a_reg[4r + k] = A[16rg + r][4cq + k]
+  {
+    const float4* src = reinterpret_cast<const float4*>(args.a_img) + (size_t)(16 * rg) * (NP / 4) + cq;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float4 v = src[r * (NP / 4)];
+      a_reg[4 * r + 0] = v.x;
+      a_reg[4 * r + 1] = v.y;
+      a_reg[4 * r + 2] = v.z;
+      a_reg[4 * r + 3] = v.w;
+    }
+  }
+  unsigned bad = 0;
+  auto obs_s = [&](int t) -> unsigned {
+    const unsigned o = (unsigned)obs[t];
+    bad |= (o >= V);
+    return o < V ? o : 0u;
+  };
+  auto force = [&](float d, int f) -> float { return (FRC && f >= 0 && jw != f) ? ninf_f() : d; };
+  const int wofs = (jw >> 4) * LS + (jw & 15);  // where this lane's column lives in an LDS row
+  // ---- t = 0 ----
+  {
+    const float d0 = force(args.pi[jw] + args.et[(size_t)obs_s(0) * NP + jw], FRC ? frc[0] : -1);
+    lds[0][wofs] = d0;
+    drow[jw] = d0;
+  }
+  unsigned o_nx = obs_s(T > 1 ? 1 : 0);
+  float e_nx = args.et[(size_t)o_nx * NP + jw];
+  for (int t = 1; t < T; ++t) {
+    const float e_use = e_nx;
+    const int f_use = FRC ? frc[t] : -1;
+    o_nx = obs_s(t + 1 < T ? t + 1 : T - 1);
+    e_nx = args.et[(size_t)o_nx * NP + jw];  // one step ahead
+    const float* src = &lds[(t - 1) & 1][rg * LS];
+    float4 d[4];
+#pragma unroll
+    for (int b = 0; b < 4; ++b) d[b] = *reinterpret_cast<const float4*>(src + 4 * b);
+    float c[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      // s_i = d[i] + a[i,j]  (viterbi.rs:15), 16 rows of column 4cq + k
+      float m = fmaxf(d[0].x + a_reg[0 * 4 + k], d[0].y + a_reg[1 * 4 + k]);
+      m = fmaxf(fmaxf(m, d[0].z + a_reg[2 * 4 + k]), d[0].w + a_reg[3 * 4 + k]);
+#pragma unroll
+      for (int b = 1; b < 4; ++b) {
+        m = fmaxf(fmaxf(m, d[b].x + a_reg[(4 * b + 0) * 4 + k]), d[b].y + a_reg[(4 * b + 1) * 4 + k]);
+        m = fmaxf(fmaxf(m, d[b].z + a_reg[(4 * b + 2) * 4 + k]), d[b].w + a_reg[(4 * b + 3) * 4 + k]);
+      }
+      c[k] = m;
+    }
+    // fold the 4 row groups (lanes 4cq..4cq+3): xor1 keeps columns {2p, 2p+1}, xor2 keeps 2p+q
+    float k0 = p ? c[2] : c[0], k1 = p ? c[3] : c[1];
+    const float g0 = p ? c[0] : c[2], g1 = p ? c[1] : c[3];
+    k0 = dpp_max_xor1_other(k0, g0);
+    k1 = dpp_max_xor1_other(k1, g1);
+    float kk = q ? k1 : k0;
+    const float gg = q ? k0 : k1;
+    kk = dpp_max_xor2_other(kk, gg);
+    const float dn = force(kk + e_use, f_use);  // (d + a) + b -- viterbi.rs:15-17
+    lds[t & 1][wofs] = dn;
+    drow[(size_t)t * NP + jw] = dn;
+  }
+  // ---- backtrack (cp.rs:117-125) of this wave's own sequence: the delta rows were stored
+  // by other lanes of this wave -- make them visible (release to L2, then acquire) ----
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  backtrack_one<1, NP>(bargs, seq, e0, T, lane, drow + lane, bargs.at + lane, bad != 0);
 }
 
 // rescore_f64_lanes: the f64 re-score of rescore_path_f64, but one LANE per sequence, so the
@@ -1330,6 +1462,19 @@ hipError_t launch_trellis_fwd2(int np, const TrellisFwdArgs& fa, int64_t npairs,
 #define CVK_FWD2(NP) trellis_fwd2_np<NP>(fa, npairs, stream)
   CVK_NP_SWITCH(np, CVK_FWD2)
 #undef CVK_FWD2
+}
+
+hipError_t launch_trellis_wave64(const TrellisFwdArgs& fa, const BacktrackArgs& ba, int64_t nseq,
+                                 hipStream_t stream) {
+  if (nseq <= 0) return hipSuccess;
+  if (fa.ranges || fa.reverse || fa.last_row || fa.start || !fa.delta || fa.split || fa.slot_order)
+    return hipErrorInvalidValue;
+  const dim3 grid((unsigned)((nseq + 3) / 4));
+  if (fa.forced)
+    hipLaunchKernelGGL(trellis_wave64_f32<true>, grid, dim3(256), 0, stream, fa, ba);
+  else
+    hipLaunchKernelGGL(trellis_wave64_f32<false>, grid, dim3(256), 0, stream, fa, ba);
+  return hipGetLastError();
 }
 
 hipError_t launch_trellis_fwd(int np, const TrellisFwdArgs& fa, int64_t nseq, hipStream_t stream) {

@@ -22,6 +22,7 @@ ASSOC_VITERBI, ASSOC_CP, ASSOC_DP, ASSOC_DECODE = 0, 1, 2, 3
 KERNEL_AUTO, KERNEL_TRELLIS, KERNEL_GENERIC = 0, 1, 2
 FLAG_MFMA_TRELLIS = 0x1
 FLAG_NO_PAIR = 0x4
+FLAG_NO_WAVE = 0x8
 FLAG_SERIAL = 0x2
 
 

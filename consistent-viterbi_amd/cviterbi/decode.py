@@ -25,15 +25,18 @@ def _p(x):
 def make_opts(dtype="f32", assoc="viterbi", kernel="auto", rescore_f64=True, stream=None, workspace_bytes=0,
               variant=None, mfma_tiles=None, serial=False):
     """variant: None/"valu" (all-VALU trellis, two equal-length sequences per workgroup where
-    N % 64 == 0, default), "valu1" (one sequence per workgroup) or "mfma" (MFMA-assisted,
-    slower) -- all bit-identical;
+    N % 64 == 0, default; for N <= 64 one wave per sequence with the backtrack fused),
+    "nowave" (the workgroup kernels at N <= 64), "valu1" (one sequence per workgroup) or
+    "mfma" (MFMA-assisted, slower) -- all bit-identical;
     mfma_tiles: tuning override of the MFMA tiles per wave (bit-identical results);
     serial: no forward/backtrack stream overlap."""
     flags = L.FLAG_SERIAL if serial else 0
     if variant == "mfma":
         flags |= L.FLAG_MFMA_TRELLIS
     elif variant == "valu1":
-        flags |= L.FLAG_NO_PAIR
+        flags |= L.FLAG_NO_PAIR | L.FLAG_NO_WAVE
+    elif variant == "nowave":
+        flags |= L.FLAG_NO_WAVE
     if mfma_tiles is not None:
         flags |= L.FLAG_MFMA_TILES(mfma_tiles)
     return L.opts(_DT.get(dtype, dtype), _ASSOC.get(assoc, assoc), _KERNEL.get(kernel, kernel), rescore_f64, stream,

@@ -67,6 +67,8 @@ enum { CV_KERNEL_AUTO = 0, CV_KERNEL_TRELLIS = 1, CV_KERNEL_GENERIC = 2 };
 #define CV_FLAG_MFMA_TRELLIS 0x1u
 #define CV_FLAG_SERIAL 0x2u       /* one stream, fewest chunks: no forward/backtrack overlap */
 #define CV_FLAG_NO_PAIR 0x4u      /* one sequence per forward workgroup (A/B knob; bit-identical) */
+#define CV_FLAG_NO_WAVE 0x8u      /* N <= 64: the workgroup kernels instead of one wave per sequence
+                                     with the backtrack fused (A/B knob; bit-identical) */
 /* MFMA tiles per wave per step for the MFMA-assisted kernel (implies it; N in (224,256]:
  * 0, 4..8; default 6).  Results are bit-identical for every value. */
 #define CV_FLAG_MFMA_TILES(n) ((uint32_t)((n) + 1) << 8)

@@ -12,7 +12,7 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.mark.parametrize("n", [5, 45, 64, 200, 256])
-@pytest.mark.parametrize("variant", ["valu", "mfma"])
+@pytest.mark.parametrize("variant", ["valu", "nowave", "valu1", "mfma"])
 def test_forced_decode_bit_exact(gpu, n, variant):
     pi, a, b = synth.random_hmm(n, 19, seed=n)
     rng = np.random.default_rng(n)

@@ -91,6 +91,31 @@ def test_pair_kernel_equal_and_ragged(gpu, n, serial):
     _assert_same(cv.decode_batch(h, off2, obs2, rescore_f64=False, serial=serial), ref2, f"equal N={n}")
 
 
+@pytest.mark.parametrize("n", [33, 45, 64])
+@pytest.mark.parametrize("serial", [False, True])
+def test_wave_kernel_small_n(gpu, n, serial):
+    """N <= 64: one wave per sequence with the backtrack fused (trellis_wave64_f32): ragged
+    lengths incl. T = 0 and 1, -inf entries, a chunked workspace -- bit-identical to the
+    oracle and to the workgroup kernels."""
+    pi, a, b = synth.random_hmm(n, 17, seed=2000 + n, zero_frac=0.03)
+    rng = np.random.default_rng(n + 11)
+    off = synth.offsets_from_lengths(rng.choice([0, 1, 2, 7, 40, 129, 300], size=53))
+    obs = rng.integers(0, 17, size=int(off[-1])).astype(np.int32)
+    h = cv.HMM(pi, a, b)
+    ref = O.decode_batch(pi, a, b, off, obs, O.VITERBI, np.float32)
+    ws = 0 if serial else 64 * 4 * 700
+    got = cv.decode_batch(h, off, obs, rescore_f64=False, serial=serial, workspace_bytes=ws)
+    _assert_same(got, ref, f"wave N={n}")
+    other = cv.decode_batch(h, off, obs, rescore_f64=False, variant="nowave", serial=serial, workspace_bytes=ws)
+    _assert_same(got, other, f"wave vs workgroup N={n}")
+    # f64 re-score along the path
+    path, score, status = cv.decode_batch(h, off, obs, rescore_f64=True, serial=serial, workspace_bytes=ws)
+    for s in range(len(off) - 1):
+        if status[s] == 0:
+            lo, hi = off[s], off[s + 1]
+            assert score[s] == O.rescore_f64(pi, a, b, obs[lo:hi], path[lo:hi])
+
+
 @pytest.mark.parametrize("mt", [0, 4, 5, 6, 7, 8])
 def test_mfma_tile_counts_bit_exact(gpu, mt):
     pi, a, b, off, obs = _case(256, 31, seed=77, nseq=12, tmax=60, zero_frac=0.02)
