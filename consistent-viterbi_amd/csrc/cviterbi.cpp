@@ -26,6 +26,7 @@
 #include "../../include/cviterbi.h"
 #include "csp.hpp"
 #include "hmm_json.hpp"
+#include "kernels/fit.h"
 #include "kernels/trellis.h"
 
 namespace {
@@ -1532,5 +1533,216 @@ CV_API cv_status cv_solver_get_explored_nodes(const cv_solver* s, uint64_t* n) {
   return CV_OK;
 }
 CV_API void cv_solver_destroy(cv_solver* s) { delete s; }
+
+}  // extern "C"
+
+// ---- HMM fitting (hmm.rs:30-190) --------------------------------------
+namespace {
+
+// hmm.rs:192-205 `log()`: 0 -> -inf, else x.log(10.0), which Rust evaluates as ln(x) / ln(10)
+double ref_log(double x) { return x == 0.0 ? -INFINITY : std::log(x) / std::log(10.0); }
+
+cv_status fit_validate(int32_t N, int64_t V, int64_t nseq, const int64_t* offsets, const int32_t* obs,
+                       const int32_t* tags, bool all_tagged, double* pi, double* a, double* b) {
+  if (N <= 0 || V <= 0 || nseq <= 0) return set_err(CV_EINVAL, "nstates, nobs and nseq must be > 0");
+  if (!offsets || !obs || !tags || !pi || !a || !b) return set_err(CV_EINVAL, "null argument");
+  if (offsets[0] < 0) return set_err(CV_EINVAL, "offsets[0] < 0");
+  for (int64_t s = 0; s < nseq; ++s)
+    if (offsets[s + 1] <= offsets[s]) return set_err(CV_EINVAL, "sequence %lld is empty or offsets decrease", (long long)s);
+  const int64_t lo = offsets[0], hi = offsets[nseq];
+  int64_t k = first_bad(lo, hi, [&](int64_t i) { return obs[i] < 0 || obs[i] >= V; });
+  if (k >= 0) return set_err(CV_EINVAL, "obs[%lld] = %d out of range [0,%lld)", (long long)k, obs[k], (long long)V);
+  k = first_bad(lo, hi, [&](int64_t i) { return tags[i] < (all_tagged ? 0 : -1) || tags[i] >= N; });
+  if (k >= 0) return set_err(CV_EINVAL, "tags[%lld] = %d out of range [%d,%d)", (long long)k, tags[k], all_tagged ? 0 : -1, N);
+  return CV_OK;
+}
+
+struct FitDev {
+  DevBuf off, obs, tags, pi, a, at, et, alpha, beta, acc, cnt;
+};
+
+}  // namespace
+
+extern "C" {
+
+CV_API cv_status cv_hmm_fit_mle(int32_t nstates, int64_t nobs, int64_t nseq, const int64_t* offsets,
+                                const int32_t* obs, const int32_t* tags, int32_t device, double* pi, double* a,
+                                double* b) {
+  const int32_t N = nstates;
+  const int64_t V = nobs;
+  cv_status st = fit_validate(N, V, nseq, offsets, obs, tags, true, pi, a, b);
+  if (st != CV_OK) return st;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) {
+    (void)hipGetLastError();
+    return set_err(CV_EDEVICE, "device %d not available", device);
+  }
+  HIP_TRY(hipSetDevice(device));
+  const int64_t lo = offsets[0], total = offsets[nseq] - lo;
+  FitDev d;
+  std::vector<int64_t> off0((size_t)nseq + 1);
+  for (int64_t s = 0; s <= nseq; ++s) off0[s] = offsets[s] - lo;
+  const size_t ncnt = (size_t)N + (size_t)N * N + (size_t)N * V + 2 * (size_t)N;
+  if ((st = upload(d.off, off0.data(), off0.size() * 8)) != CV_OK) return st;
+  if ((st = upload(d.obs, obs + lo, (size_t)total * 4)) != CV_OK) return st;
+  if ((st = upload(d.tags, tags + lo, (size_t)total * 4)) != CV_OK) return st;
+  if ((st = d.cnt.ensure(ncnt * 8)) != CV_OK) return st;
+  HIP_TRY(hipMemset(d.cnt.p, 0, ncnt * 8));
+  cvf::MleArgs g{};
+  g.offsets = d.off.as<int64_t>();
+  g.obs = d.obs.as<int32_t>();
+  g.tags = d.tags.as<int32_t>();
+  g.nstates = N;
+  g.nobs = V;
+  uint64_t* c = d.cnt.as<uint64_t>();
+  g.pi_cnt = c;
+  g.a_cnt = c + N;
+  g.b_cnt = c + N + (size_t)N * N;
+  g.seen = g.b_cnt + (size_t)N * V;
+  g.end = g.seen + N;
+  hipError_t e = cvf::launch_mle_counts(g, nseq, nullptr);
+  if (e != hipSuccess) return set_err(CV_EDEVICE, "mle launch failed: %s", hipGetErrorString(e));
+  std::vector<uint64_t> cnt(ncnt);
+  HIP_TRY(hipMemcpy(cnt.data(), d.cnt.p, ncnt * 8, hipMemcpyDeviceToHost));
+  const uint64_t* pc = cnt.data();
+  const uint64_t* ac = pc + N;
+  const uint64_t* bc = ac + (size_t)N * N;
+  const uint64_t* seen = bc + (size_t)N * V;
+  const uint64_t* end = seen + N;
+  // The reference adds 1.0 per occurrence to the current probability (hmm.rs:39-48); all
+  // addends are 1.0, so the order is immaterial, but each add rounds: replay them.
+  auto add_ones = [](double x, uint64_t k) {
+    for (uint64_t i = 0; i < k; ++i) x += 1.0;
+    return x;
+  };
+  parallel_ranges((int64_t)N, [&](int, int64_t s0, int64_t s1) {
+    for (int64_t s = s0; s < s1; ++s) {
+      const double sn = add_ones(0.0, seen[s]), en = add_ones(0.0, end[s]);
+      for (int32_t j = 0; j < N; ++j) {
+        double& x = a[(size_t)s * N + j];
+        x = add_ones(x, ac[(size_t)s * N + j]);
+        x = sn != en ? x / (sn - en) : 0.0;  // hmm.rs:52-57
+      }
+      pi[s] = add_ones(pi[s], pc[s]) / (double)nseq;
+      for (int64_t o = 0; o < V; ++o) {
+        double& x = b[(size_t)s * V + o];
+        x = add_ones(x, bc[(size_t)s * V + o]) / sn;
+      }
+      pi[s] = ref_log(pi[s]);
+      for (int32_t j = 0; j < N; ++j) a[(size_t)s * N + j] = ref_log(a[(size_t)s * N + j]);
+      for (int64_t o = 0; o < V; ++o) b[(size_t)s * V + o] = ref_log(b[(size_t)s * V + o]);
+    }
+  }, 1);
+  return CV_OK;
+}
+
+CV_API cv_status cv_hmm_fit_train(int32_t nstates, int64_t nobs, int64_t nseq, const int64_t* offsets,
+                                  const int32_t* obs, const int32_t* tags, int32_t max_iter, double tol,
+                                  int32_t device, double* pi, double* a, double* b, int32_t* iters_out) {
+  const int32_t N = nstates;
+  const int64_t V = nobs;
+  cv_status st = fit_validate(N, V, nseq, offsets, obs, tags, false, pi, a, b);
+  if (st != CV_OK) return st;
+  if (N > cvf::kBwMaxStates) return set_err(CV_EUNSUPPORTED, "Baum-Welch covers N <= %d (N=%d)", cvf::kBwMaxStates, N);
+  if (max_iter < 0) return set_err(CV_EINVAL, "max_iter < 0");
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) {
+    (void)hipGetLastError();
+    return set_err(CV_EDEVICE, "device %d not available", device);
+  }
+  HIP_TRY(hipSetDevice(device));
+  const int64_t lo = offsets[0], total = offsets[nseq] - lo;
+  FitDev d;
+  std::vector<int64_t> off0((size_t)nseq + 1);
+  for (int64_t s = 0; s <= nseq; ++s) off0[s] = offsets[s] - lo;
+  if ((st = upload(d.off, off0.data(), off0.size() * 8)) != CV_OK) return st;
+  if ((st = upload(d.obs, obs + lo, (size_t)total * 4)) != CV_OK) return st;
+  if ((st = upload(d.tags, tags + lo, (size_t)total * 4)) != CV_OK) return st;
+  // alpha / beta rows for a chunk of sequences at a time (<= 2 GiB each)
+  const int64_t cap_elems = std::max<int64_t>((2ll << 30) / (8 * N), 1);
+  int64_t max_chunk = 0;
+  std::vector<std::pair<int64_t, int64_t>> chunks;
+  for (int64_t s0 = 0; s0 < nseq;) {
+    int64_t s1 = s0 + 1;
+    while (s1 < nseq && off0[s1 + 1] - off0[s0] <= cap_elems) ++s1;
+    chunks.emplace_back(s0, s1);
+    max_chunk = std::max(max_chunk, off0[s1] - off0[s0]);
+    s0 = s1;
+  }
+  if ((st = d.alpha.ensure((size_t)max_chunk * N * 8)) != CV_OK) return st;
+  if ((st = d.beta.ensure((size_t)max_chunk * N * 8)) != CV_OK) return st;
+  const size_t nacc = 3 * (size_t)N + (size_t)V * N + (size_t)N * N + 1;
+  if ((st = d.acc.ensure(nacc * 8)) != CV_OK) return st;
+  if ((st = d.pi.ensure((size_t)N * 8)) != CV_OK) return st;
+  if ((st = d.a.ensure((size_t)N * N * 8)) != CV_OK) return st;
+  if ((st = d.at.ensure((size_t)N * N * 8)) != CV_OK) return st;
+  if ((st = d.et.ensure((size_t)V * N * 8)) != CV_OK) return st;
+  std::vector<double> at((size_t)N * N), et((size_t)V * N), acc(nacc);
+  std::vector<double> npi(N), na((size_t)N * N), nb((size_t)N * V);
+  int32_t it = 0;
+  for (it = 1; it <= max_iter; ++it) {
+    for (int32_t i = 0; i < N; ++i)
+      for (int32_t j = 0; j < N; ++j) at[(size_t)j * N + i] = a[(size_t)i * N + j];
+    for (int32_t i = 0; i < N; ++i)
+      for (int64_t o = 0; o < V; ++o) et[(size_t)o * N + i] = b[(size_t)i * V + o];
+    HIP_TRY(hipMemcpy(d.pi.p, pi, (size_t)N * 8, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(d.a.p, a, (size_t)N * N * 8, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(d.at.p, at.data(), at.size() * 8, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(d.et.p, et.data(), et.size() * 8, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemset(d.acc.p, 0, nacc * 8));
+    double* A = d.acc.as<double>();
+    for (const auto& c : chunks) {
+      cvf::BwArgs g{};
+      g.offsets = d.off.as<int64_t>() + c.first;
+      g.obs = d.obs.as<int32_t>();
+      g.tags = d.tags.as<int32_t>();
+      g.elem_base = off0[c.first];
+      g.nstates = N;
+      g.pi = d.pi.as<double>();
+      g.a = d.a.as<double>();
+      g.at = d.at.as<double>();
+      g.et = d.et.as<double>();
+      g.alpha = d.alpha.as<double>();
+      g.beta = d.beta.as<double>();
+      g.pi_acc = A;
+      g.a_den = A + N;
+      g.b_den = A + 2 * N;
+      g.b_num = A + 3 * N;
+      g.xi_s = g.b_num + (size_t)V * N;
+      g.xi_zero = g.xi_s + (size_t)N * N;
+      const hipError_t e = cvf::launch_bw_estep(g, c.second - c.first, nullptr);
+      if (e != hipSuccess) return set_err(CV_EDEVICE, "Baum-Welch launch failed: %s", hipGetErrorString(e));
+    }
+    HIP_TRY(hipMemcpy(acc.data(), d.acc.p, nacc * 8, hipMemcpyDeviceToHost));
+    const double* pi_acc = acc.data();
+    const double* a_den = pi_acc + N;
+    const double* b_den = pi_acc + 2 * N;
+    const double* b_num = pi_acc + 3 * N;
+    const double* xs = b_num + (size_t)V * N;
+    const double z = xs[(size_t)N * N];
+    // M-step (hmm.rs:145-170): new_pi = sum gamma_0 / R; new_a = sum xi / a_den (row);
+    // new_b = sum gamma at o / b_den; sum_t xi_t = A o S + z / N^2 (see bw_stats)
+    const double zu = z / ((double)N * (double)N);
+    double dsum = 0.0;
+    for (int32_t i = 0; i < N; ++i) {
+      npi[i] = pi_acc[i] / (double)nseq;
+      for (int32_t j = 0; j < N; ++j)
+        na[(size_t)i * N + j] = (a[(size_t)i * N + j] * xs[(size_t)i * N + j] + zu) / a_den[i];
+      for (int64_t o = 0; o < V; ++o) nb[(size_t)i * V + o] = b_num[(size_t)o * N + i] / b_den[i];
+    }
+    for (int32_t i = 0; i < N; ++i) dsum += std::fabs(npi[i] - pi[i]);  // hmm.rs:172-175
+    for (size_t k = 0; k < na.size(); ++k) dsum += std::fabs(na[k] - a[k]);
+    for (size_t k = 0; k < nb.size(); ++k) dsum += std::fabs(nb[k] - b[k]);
+    std::copy(npi.begin(), npi.end(), pi);
+    std::copy(na.begin(), na.end(), a);
+    std::copy(nb.begin(), nb.end(), b);
+    if (dsum <= tol) break;
+  }
+  if (iters_out) *iters_out = std::min(it, max_iter);
+  for (int32_t i = 0; i < N; ++i) pi[i] = ref_log(pi[i]);
+  for (size_t k = 0; k < (size_t)N * N; ++k) a[k] = ref_log(a[k]);
+  for (size_t k = 0; k < (size_t)N * V; ++k) b[k] = ref_log(b[k]);
+  return CV_OK;
+}
 
 }  // extern "C"

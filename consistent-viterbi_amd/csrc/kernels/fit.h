@@ -1,0 +1,49 @@
+// fit.h -- argument blocks and launchers of the HMM-fitting kernels (fit.hip).
+// Internal to libcviterbi; the public boundary is include/cviterbi.h (cv_hmm_fit_*).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace cvf {
+
+constexpr int kBwMaxStates = 128;  // bw_stats keeps a sequence's N x N xi sum in LDS
+
+struct MleArgs {
+  const int64_t* offsets;
+  const int32_t* obs;   // [sum T] flattened observation index
+  const int32_t* tags;  // [sum T] state of every element (all >= 0)
+  int nstates;
+  int64_t nobs;
+  uint64_t* pi_cnt;     // [N]
+  uint64_t* a_cnt;      // [N][N]
+  uint64_t* b_cnt;      // [N][V]
+  uint64_t* seen;       // [N]
+  uint64_t* end;        // [N]
+};
+
+struct BwArgs {
+  const int64_t* offsets;
+  const int32_t* obs;
+  const int32_t* tags;  // -1 = untagged (None)
+  int64_t elem_base;    // element offset that maps to row 0 of alpha / beta
+  int nstates;
+  const double* pi;     // [N]
+  const double* a;      // [N][N] row-major (from, to)
+  const double* at;     // [N][N] transposed
+  const double* et;     // [V][N] emissions transposed
+  double* alpha;        // [elements][N] workspace
+  double* beta;         // [elements][N] workspace
+  // E-step sums (accumulated across sequences; zeroed by the host per iteration)
+  double* pi_acc;       // [N]  sum of gamma_0
+  double* a_den;        // [N]  sum of gamma_t, t < T-1
+  double* b_den;        // [N]  sum of gamma_t
+  double* b_num;        // [V][N] sum of gamma_t at o_t
+  double* xi_s;         // [N][N] sum of (alpha_t / c_t) (x) u_{t+1}
+  double* xi_zero;      // [1] number of steps with c_t == 0 (uniform xi)
+};
+
+hipError_t launch_mle_counts(const MleArgs& g, int64_t nseq, hipStream_t stream);
+// forward, backward and the E-step sums of sequences [0, nseq) of g.offsets
+hipError_t launch_bw_estep(const BwArgs& g, int64_t nseq, hipStream_t stream);
+
+}  // namespace cvf

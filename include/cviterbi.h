@@ -240,6 +240,24 @@ CV_API const char* cv_solver_get_name(const cv_solver* s);                      
 CV_API cv_status cv_solver_get_explored_nodes(const cv_solver* s, uint64_t* n);   /* CPSolver::get_explored_nodes cp.rs:128 */
 CV_API void cv_solver_destroy(cv_solver* s);
 
+/* ---- HMM fitting (hmm.rs:30-190) ------------------------------------
+ * pi[N], a[N*N] (from-major), b[N*V] (state-major, obs row-major over bdims): the CURRENT
+ * parameters in PROBABILITY space on entry (the reference starts from HMM::new's random
+ * draw, hmm.rs:22-28), the fitted parameters log-mapped on return (the reference's log():
+ * 0 -> -inf, else ln(x)/ln(10), hmm.rs:192-205) -- ready for cv_hmm_desc.  f64.
+ * tags[sum T]: the state of an element, -1 = unknown (None).  device: HIP device index. */
+/* maximum_likelihood_estimation (hmm.rs:30-62): exact integer counts on the GPU, ADDED to
+ * the current probabilities with the reference's sequential rounding; every tag >= 0. */
+CV_API cv_status cv_hmm_fit_mle(int32_t nstates, int64_t nobs, int64_t nseq, const int64_t* offsets,
+                                const int32_t* obs, const int32_t* tags, int32_t device, double* pi, double* a,
+                                double* b);
+/* train (hmm.rs:69-190): tag-clamped Baum-Welch, E-step on the GPU (N <= 128), M-step and
+ * the convergence test (sum |new - old| <= tol, checked after the update) on the host.
+ * *iters_out = iterations run. */
+CV_API cv_status cv_hmm_fit_train(int32_t nstates, int64_t nobs, int64_t nseq, const int64_t* offsets,
+                                  const int32_t* obs, const int32_t* tags, int32_t max_iter, double tol,
+                                  int32_t device, double* pi, double* a, double* b, int32_t* iters_out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,142 @@
+"""HMM fitting: cv_hmm_fit_mle / cv_hmm_fit_train against the numpy
+restatement of hmm.rs:30-62 / 69-190 (oracle/fit_oracle.py).
+
+CPU: the oracle against closed forms -- MLE by hand on a tiny corpus, and a fully tagged
+corpus, where one Baum-Welch iteration must reproduce the MLE counts (alpha, beta and
+gamma are one-hot, each xi_t is a single 1 at (tag_t, tag_t+1)).
+GPU: MLE to ~1 ulp (same host arithmetic; numpy's vectorised log may differ from glibc's by
+an ulp); Baum-Welch within 1e-9 (log10) after several iterations (f64 sums in another
+order -- the reference's own order is BLAS-internal, hmm.rs:94 `.dot`)."""
+import numpy as np
+import pytest
+
+import fit_oracle as FO
+
+
+def _corpus(n, v, nseq, tmax, tag_frac, seed):
+    rng = np.random.default_rng(seed)
+    lengths = rng.integers(1, tmax + 1, size=nseq)
+    off = np.zeros(nseq + 1, np.int64)
+    np.cumsum(lengths, out=off[1:])
+    obs = rng.integers(0, v, size=int(off[-1])).astype(np.int32)
+    tags = rng.integers(0, n, size=int(off[-1])).astype(np.int32)
+    if tag_frac < 1.0:
+        tags = np.where(rng.random(len(tags)) < tag_frac, tags, -1).astype(np.int32)
+    return off, obs, tags
+
+
+def _probs(n, v, seed):
+    rng = np.random.default_rng(seed + 100)
+    a = rng.random((n, n))
+    a /= a.sum(axis=1, keepdims=True)
+    b = rng.random((n, v))
+    b /= b.sum(axis=1, keepdims=True)
+    pi = rng.random(n)
+    pi /= pi.sum()
+    return pi, a, b
+
+
+def test_mle_oracle_by_hand():
+    # two sequences: states 0 1 1 / 1 0 ; obs 2 0 1 / 1 1 ; zero initial parameters
+    off = np.array([0, 3, 5])
+    obs = np.array([2, 0, 1, 1, 1])
+    tags = np.array([0, 1, 1, 1, 0])
+    pi, a, b = FO.mle(np.zeros(2), np.zeros((2, 2)), np.zeros((2, 3)), off, obs, tags)
+    # transitions 0->1, 1->1, 1->0; seen = [2, 3], end = [1, 1] -> rows divided by [1, 2]
+    np.testing.assert_array_equal(a, FO.log_map(np.array([[0.0, 1.0], [0.5, 0.5]])))
+    np.testing.assert_array_equal(pi, FO.log_map(np.array([0.5, 0.5])))
+    np.testing.assert_array_equal(b, FO.log_map(np.array([[0, 1, 1], [1, 2, 0]]) / np.array([[2.0], [3.0]])))
+    assert a[0, 0] == -np.inf and b[1, 2] == -np.inf
+
+
+def test_log_map_is_ln_over_ln10():
+    x = np.array([0.0, 1.0, 0.001, 0.3, 1e-300])
+    got = FO.log_map(x)
+    assert got[0] == -np.inf and got[1] == 0.0
+    for xi, gi in zip(x[2:], got[2:]):
+        assert gi == np.log(xi) / np.log(10.0)  # Rust f64::log(10.0), not log10
+
+
+def test_train_fully_tagged_equals_counts():
+    n, v = 4, 6
+    off, obs, tags = _corpus(n, v, 9, 12, 1.0, seed=5)
+    pi0, a0, b0 = _probs(n, v, seed=5)
+    pi1, a1, b1, _ = FO.train_step(pi0, a0, b0, off, obs, tags)
+    lp, la, lb = FO.mle(np.zeros(n), np.zeros((n, n)), np.zeros((n, v)), off, obs, tags)
+    seen_from = np.zeros(n)
+    for s in range(len(off) - 1):
+        for t in range(off[s], off[s + 1] - 1):
+            seen_from[tags[t]] += 1
+    ok = seen_from > 0  # rows of A with at least one outgoing transition
+    np.testing.assert_allclose(FO.log_map(a1[ok]), la[ok], rtol=1e-12)
+    np.testing.assert_allclose(FO.log_map(pi1), lp, rtol=1e-12)
+    np.testing.assert_allclose(FO.log_map(b1), lb, rtol=1e-12)
+
+
+def test_train_step_rows_are_distributions():
+    n, v = 5, 7
+    off, obs, tags = _corpus(n, v, 11, 15, 0.3, seed=9)
+    pi, a, b = _probs(n, v, seed=9)
+    for _ in range(3):
+        pi, a, b, d = FO.train_step(pi, a, b, off, obs, tags)
+        assert d >= 0
+    np.testing.assert_allclose(a.sum(axis=1), 1.0, rtol=1e-12)
+    np.testing.assert_allclose(b.sum(axis=1), 1.0, rtol=1e-12)
+    np.testing.assert_allclose(pi.sum(), 1.0, rtol=1e-12)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,v", [(2, 3), (12, 30), (45, 200)])
+def test_gpu_mle_matches_oracle(gpu, n, v):
+    import cviterbi as cv
+
+    off, obs, tags = _corpus(n, v, 40, 25, 1.0, seed=n)
+    pi0, a0, b0 = _probs(n, v, seed=n)
+    got = cv.fit_mle(pi0, a0, b0, off, obs, tags)
+    ref = FO.mle(pi0, a0, b0, off, obs, tags)
+    for g, r, what in zip(got, ref, ("pi", "a", "b")):
+        assert np.array_equal(np.isinf(g), np.isinf(r)), what
+        fin = np.isfinite(r)
+        np.testing.assert_allclose(g[fin], r[fin], rtol=1e-15, atol=0, err_msg=what)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,v,frac", [(3, 5, 0.0), (12, 30, 0.3), (45, 60, 0.2), (128, 40, 0.1)])
+def test_gpu_train_matches_oracle(gpu, n, v, frac):
+    import cviterbi as cv
+
+    off, obs, tags = _corpus(n, v, 24, 30, frac, seed=100 + n)
+    pi0, a0, b0 = _probs(n, v, seed=100 + n)
+    iters = 3
+    gp, ga, gb, it = cv.fit_train(pi0, a0, b0, off, obs, tags, max_iter=iters, tol=0.0)
+    assert it == iters
+    rp, ra, rb, rit = FO.train(pi0, a0, b0, off, obs, tags, iters, 0.0)
+    assert rit == iters
+    for g, r, what in zip((gp, ga, gb), (rp, ra, rb), ("pi", "a", "b")):
+        assert np.array_equal(np.isinf(g), np.isinf(r)), what
+        fin = np.isfinite(r)
+        np.testing.assert_allclose(g[fin], r[fin], rtol=0, atol=1e-9, err_msg=what)
+
+
+@pytest.mark.gpu
+def test_gpu_train_converges_like_oracle(gpu):
+    import cviterbi as cv
+
+    off, obs, tags = _corpus(6, 9, 30, 20, 0.5, seed=77)
+    pi0, a0, b0 = _probs(6, 9, seed=77)
+    gp, ga, gb, it = cv.fit_train(pi0, a0, b0, off, obs, tags, max_iter=200, tol=1e-6)
+    rp, ra, rb, rit = FO.train(pi0, a0, b0, off, obs, tags, 200, 1e-6)
+    assert it == rit < 200
+    np.testing.assert_allclose(ga, ra, rtol=0, atol=1e-8)
+
+
+@pytest.mark.gpu
+def test_gpu_fit_limits(gpu):
+    import cviterbi as cv
+
+    off, obs, tags = _corpus(129, 4, 3, 5, 0.5, seed=1)
+    pi0, a0, b0 = _probs(129, 4, seed=1)
+    with pytest.raises(cv.CVError):  # Baum-Welch covers N <= 128
+        cv.fit_train(pi0, a0, b0, off, obs, tags, max_iter=1)
+    with pytest.raises(cv.CVError):  # MLE needs every element tagged
+        cv.fit_mle(pi0, a0, b0, off, obs, tags)
