@@ -1558,7 +1558,7 @@ cv_status fit_validate(int32_t N, int64_t V, int64_t nseq, const int64_t* offset
 }
 
 struct FitDev {
-  DevBuf off, obs, tags, pi, a, at, et, alpha, beta, acc, cnt;
+  DevBuf off, obs, tags, pi, a, at, et, alpha, beta, acc, cnt, ord;
 };
 
 }  // namespace
@@ -1672,24 +1672,56 @@ CV_API cv_status cv_hmm_fit_train(int32_t nstates, int64_t nobs, int64_t nseq, c
   if ((st = d.alpha.ensure((size_t)max_chunk * N * 8)) != CV_OK) return st;
   if ((st = d.beta.ensure((size_t)max_chunk * N * 8)) != CV_OK) return st;
   const size_t nacc = 3 * (size_t)N + (size_t)V * N + (size_t)N * N + 1;
+  constexpr int kPartsB = 1024;  // blocks of the b M-step = partial convergence sums
   if ((st = d.acc.ensure(nacc * 8)) != CV_OK) return st;
   if ((st = d.pi.ensure((size_t)N * 8)) != CV_OK) return st;
   if ((st = d.a.ensure((size_t)N * N * 8)) != CV_OK) return st;
   if ((st = d.at.ensure((size_t)N * N * 8)) != CV_OK) return st;
   if ((st = d.et.ensure((size_t)V * N * 8)) != CV_OK) return st;
-  std::vector<double> at((size_t)N * N), et((size_t)V * N), acc(nacc);
-  std::vector<double> npi(N), na((size_t)N * N), nb((size_t)N * V);
-  int32_t it = 0;
-  for (it = 1; it <= max_iter; ++it) {
+  if ((st = d.cnt.ensure((1 + kPartsB) * 8)) != CV_OK) return st;
+  int cus = 0;
+  HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
+  const int64_t max_waves = (int64_t)std::max(cus, 1) * 8;  // backward waves resident at 2 per SIMD
+  {
+    // parameters go to the device once and stay there (M-step on the device)
+    std::vector<double> at((size_t)N * N), et((size_t)V * N);
     for (int32_t i = 0; i < N; ++i)
       for (int32_t j = 0; j < N; ++j) at[(size_t)j * N + i] = a[(size_t)i * N + j];
-    for (int32_t i = 0; i < N; ++i)
-      for (int64_t o = 0; o < V; ++o) et[(size_t)o * N + i] = b[(size_t)i * V + o];
+    parallel_ranges((int64_t)V, [&](int, int64_t o0, int64_t o1) {
+      for (int64_t o = o0; o < o1; ++o)
+        for (int32_t i = 0; i < N; ++i) et[(size_t)o * N + i] = b[(size_t)i * V + o];
+    }, 4096);
     HIP_TRY(hipMemcpy(d.pi.p, pi, (size_t)N * 8, hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(d.a.p, a, (size_t)N * N * 8, hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(d.at.p, at.data(), at.size() * 8, hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(d.et.p, et.data(), et.size() * 8, hipMemcpyHostToDevice));
-    HIP_TRY(hipMemset(d.acc.p, 0, nacc * 8));
+  }
+  cvf::MstepArgs m{};
+  m.acc = d.acc.as<double>();
+  m.nstates = N;
+  m.nobs = V;
+  m.nseq = nseq;
+  m.pi = d.pi.as<double>();
+  m.a = d.a.as<double>();
+  m.at = d.at.as<double>();
+  m.et = d.et.as<double>();
+  m.part = d.cnt.as<double>();
+  std::vector<double> part(1 + kPartsB);
+  {
+    // longest sequences first within each chunk (indices relative to the chunk)
+    std::vector<int64_t> ord((size_t)nseq);
+    for (const auto& c : chunks) {
+      int64_t* o = ord.data() + c.first;
+      for (int64_t k = 0; k < c.second - c.first; ++k) o[k] = k;
+      std::stable_sort(o, o + (c.second - c.first), [&](int64_t x, int64_t y) {
+        return off0[c.first + x + 1] - off0[c.first + x] > off0[c.first + y + 1] - off0[c.first + y];
+      });
+    }
+    if ((st = upload(d.ord, ord.data(), ord.size() * 8)) != CV_OK) return st;
+  }
+  int32_t it = 0;
+  for (it = 1; it <= max_iter; ++it) {
+    HIP_TRY(hipMemsetAsync(d.acc.p, 0, nacc * 8, nullptr));
     double* A = d.acc.as<double>();
     for (const auto& c : chunks) {
       cvf::BwArgs g{};
@@ -1697,6 +1729,7 @@ CV_API cv_status cv_hmm_fit_train(int32_t nstates, int64_t nobs, int64_t nseq, c
       g.obs = d.obs.as<int32_t>();
       g.tags = d.tags.as<int32_t>();
       g.elem_base = off0[c.first];
+      g.order = d.ord.as<int64_t>() + c.first;
       g.nstates = N;
       g.pi = d.pi.as<double>();
       g.a = d.a.as<double>();
@@ -1710,38 +1743,30 @@ CV_API cv_status cv_hmm_fit_train(int32_t nstates, int64_t nobs, int64_t nseq, c
       g.b_num = A + 3 * N;
       g.xi_s = g.b_num + (size_t)V * N;
       g.xi_zero = g.xi_s + (size_t)N * N;
-      const hipError_t e = cvf::launch_bw_estep(g, c.second - c.first, nullptr);
+      const hipError_t e = cvf::launch_bw_estep(g, c.second - c.first, max_waves, nullptr);
       if (e != hipSuccess) return set_err(CV_EDEVICE, "Baum-Welch launch failed: %s", hipGetErrorString(e));
     }
-    HIP_TRY(hipMemcpy(acc.data(), d.acc.p, nacc * 8, hipMemcpyDeviceToHost));
-    const double* pi_acc = acc.data();
-    const double* a_den = pi_acc + N;
-    const double* b_den = pi_acc + 2 * N;
-    const double* b_num = pi_acc + 3 * N;
-    const double* xs = b_num + (size_t)V * N;
-    const double z = xs[(size_t)N * N];
-    // M-step (hmm.rs:145-170): new_pi = sum gamma_0 / R; new_a = sum xi / a_den (row);
-    // new_b = sum gamma at o / b_den; sum_t xi_t = A o S + z / N^2 (see bw_stats)
-    const double zu = z / ((double)N * (double)N);
+    // M-step (hmm.rs:145-170) on the device: new_pi = sum gamma_0 / R; new_a = sum xi / a_den
+    // (row); new_b = sum gamma at o / b_den; sum_t xi_t = A o S + z / N^2 (see bw_stats);
+    // d = sum |new - old| (hmm.rs:172-175) as per-block parts added here in a fixed order
+    const hipError_t e = cvf::launch_bw_mstep(m, kPartsB, nullptr);
+    if (e != hipSuccess) return set_err(CV_EDEVICE, "M-step launch failed: %s", hipGetErrorString(e));
+    HIP_TRY(hipMemcpy(part.data(), d.cnt.p, part.size() * 8, hipMemcpyDeviceToHost));
     double dsum = 0.0;
-    for (int32_t i = 0; i < N; ++i) {
-      npi[i] = pi_acc[i] / (double)nseq;
-      for (int32_t j = 0; j < N; ++j)
-        na[(size_t)i * N + j] = (a[(size_t)i * N + j] * xs[(size_t)i * N + j] + zu) / a_den[i];
-      for (int64_t o = 0; o < V; ++o) nb[(size_t)i * V + o] = b_num[(size_t)o * N + i] / b_den[i];
-    }
-    for (int32_t i = 0; i < N; ++i) dsum += std::fabs(npi[i] - pi[i]);  // hmm.rs:172-175
-    for (size_t k = 0; k < na.size(); ++k) dsum += std::fabs(na[k] - a[k]);
-    for (size_t k = 0; k < nb.size(); ++k) dsum += std::fabs(nb[k] - b[k]);
-    std::copy(npi.begin(), npi.end(), pi);
-    std::copy(na.begin(), na.end(), a);
-    std::copy(nb.begin(), nb.end(), b);
+    for (double x : part) dsum += x;
     if (dsum <= tol) break;
   }
   if (iters_out) *iters_out = std::min(it, max_iter);
+  std::vector<double> et((size_t)V * N);
+  HIP_TRY(hipMemcpy(pi, d.pi.p, (size_t)N * 8, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(a, d.a.p, (size_t)N * N * 8, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(et.data(), d.et.p, et.size() * 8, hipMemcpyDeviceToHost));
   for (int32_t i = 0; i < N; ++i) pi[i] = ref_log(pi[i]);
   for (size_t k = 0; k < (size_t)N * N; ++k) a[k] = ref_log(a[k]);
-  for (size_t k = 0; k < (size_t)N * V; ++k) b[k] = ref_log(b[k]);
+  parallel_ranges((int64_t)N, [&](int, int64_t i0, int64_t i1) {
+    for (int64_t i = i0; i < i1; ++i)
+      for (int64_t o = 0; o < V; ++o) b[(size_t)i * V + o] = ref_log(et[(size_t)o * N + i]);
+  }, 1);
   return CV_OK;
 }
 

@@ -26,6 +26,7 @@ struct BwArgs {
   const int32_t* obs;
   const int32_t* tags;  // -1 = untagged (None)
   int64_t elem_base;    // element offset that maps to row 0 of alpha / beta
+  const int64_t* order; // N <= 64 kernels: processing order of the sequences (nullable)
   int nstates;
   const double* pi;     // [N]
   const double* a;      // [N][N] row-major (from, to)
@@ -42,8 +43,25 @@ struct BwArgs {
   double* xi_zero;      // [1] number of steps with c_t == 0 (uniform xi)
 };
 
+constexpr int kBwWaveStates = 64;  // N <= 64: one wave per sequence (bw_*_wave)
+
+// M-step: acc = [pi_acc N | a_den N | b_den N | b_num V*N | xi_s N*N | xi_zero 1]
+struct MstepArgs {
+  const double* acc;
+  int nstates;
+  int64_t nobs;
+  int64_t nseq;
+  double* pi;    // [N]     updated in place
+  double* a;     // [N][N]  updated in place
+  double* at;    // [N][N]  transposed copy, rewritten
+  double* et;    // [V][N]  b^T, updated in place
+  double* part;  // [1 + nparts_b] per-block sums of |new - old|
+};
+
 hipError_t launch_mle_counts(const MleArgs& g, int64_t nseq, hipStream_t stream);
-// forward, backward and the E-step sums of sequences [0, nseq) of g.offsets
-hipError_t launch_bw_estep(const BwArgs& g, int64_t nseq, hipStream_t stream);
+// forward, backward and the E-step sums of sequences [0, nseq) of g.offsets; the N <= 64
+// backward kernel runs at most max_waves waves (each walks several sequences)
+hipError_t launch_bw_estep(const BwArgs& g, int64_t nseq, int64_t max_waves, hipStream_t stream);
+hipError_t launch_bw_mstep(const MstepArgs& m, int nparts_b, hipStream_t stream);
 
 }  // namespace cvf

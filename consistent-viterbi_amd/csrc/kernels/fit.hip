@@ -8,9 +8,12 @@
 // sequence; thread i < N owns state i.  The transition matrix is read from L2 (row-major A
 // for the forward step, A^T for the backward and xi steps, so every read is coalesced
 // across the threads of a row).  bw_stats keeps the sequence's xi sum (N x N) in LDS, so
-// the trainer covers N <= 128 (the reference trains POS taggers: N = 12).
+// the trainer covers N <= 128 (the reference trains POS taggers: N = 12).  For N <= 64 the
+// one-wave-per-sequence kernels below (bw_fwd_wave, bw_bwd_stats_wave) replace all three.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+
+#include <algorithm>
 
 #include "fit.h"
 
@@ -183,15 +186,364 @@ __global__ __launch_bounds__(256) void bw_stats(BwArgs g) {
   if (i == 0 && z != 0.0) unsafeAtomicAdd(g.xi_zero, z);
 }
 
+// ---- N <= 64: one wave per sequence ---------------------------------------------------------
+// Lane i owns state i.  The transition matrix lives in VGPRs (forward: column i, backward:
+// row i), the vector being multiplied is broadcast through a per-wave LDS slot (ds_read_b128,
+// all lanes same address), and the three per-step sums are wave reductions (DPP inside a row
+// of 16, readlane across the 4 rows) -- no workgroup barrier anywhere.  LDS accesses of one
+// wave complete in order, so the slot is rewritten each step without a fence.  The observation
+// and tag of each step come from a 64-step block held one element per lane (readlane).
+
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)u, CTRL, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(u >> 32), CTRL, 0xf, 0xf, false);
+  return __builtin_bit_cast(double, ((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
+}
+
+__device__ __forceinline__ double readlane_f64(double v, int k) {
+  const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)u, k);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(u >> 32), k);
+  return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
+
+// sum over the 64 lanes, the identical value in every lane
+__device__ __forceinline__ double wave_sum(double v) {
+  v += dpp_f64<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp_f64<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp_f64<0x141>(v);  // row_half_mirror: quad q <-> 1-q within 8
+  v += dpp_f64<0x140>(v);  // row_mirror: half h <-> 1-h within 16
+  return (readlane_f64(v, 0) + readlane_f64(v, 16)) + (readlane_f64(v, 32) + readlane_f64(v, 48));
+}
+
+// two independent sums with their latencies overlapped
+__device__ __forceinline__ void wave_sum2(double& a, double& b) {
+  a += dpp_f64<0xB1>(a);
+  b += dpp_f64<0xB1>(b);
+  a += dpp_f64<0x4E>(a);
+  b += dpp_f64<0x4E>(b);
+  a += dpp_f64<0x141>(a);
+  b += dpp_f64<0x141>(b);
+  a += dpp_f64<0x140>(a);
+  b += dpp_f64<0x140>(b);
+  a = (readlane_f64(a, 0) + readlane_f64(a, 16)) + (readlane_f64(a, 32) + readlane_f64(a, 48));
+  b = (readlane_f64(b, 0) + readlane_f64(b, 16)) + (readlane_f64(b, 32) + readlane_f64(b, 48));
+}
+
+// 64-step blocks of observation indices and tags, one element per lane, double-buffered: the
+// next block is loaded when the current one is taken into use, 64 steps before it is needed.
+struct StepBlocks {
+  int base, ob, tg, ob_nx, tg_nx;
+  __device__ __forceinline__ void load(const int32_t* obs, const int32_t* tag, int b, int T, int lane, int& o, int& t) {
+    const bool in = b + lane >= 0 && b + lane < T;
+    o = in ? obs[b + lane] : 0;
+    t = in ? tag[b + lane] : -1;
+  }
+  __device__ __forceinline__ void init(const int32_t* obs, const int32_t* tag, int b, int step, int T, int lane) {
+    base = b;
+    load(obs, tag, b, T, lane, ob, tg);
+    load(obs, tag, b + step, T, lane, ob_nx, tg_nx);
+  }
+  __device__ __forceinline__ void advance(const int32_t* obs, const int32_t* tag, int step, int T, int lane) {
+    base += step;
+    ob = ob_nx;
+    tg = tg_nx;
+    load(obs, tag, base + step, T, lane, ob_nx, tg_nx);
+  }
+  __device__ __forceinline__ int obs_at(int s) const { return __builtin_amdgcn_readlane(ob, s - base); }
+  __device__ __forceinline__ int tag_at(int s) const { return __builtin_amdgcn_readlane(tg, s - base); }
+};
+
+// y = sum_j p[j] * m[j], p broadcast from LDS, 4 partial sums (fused multiply-add)
+template <int NP>
+__device__ __forceinline__ double dot_lds_fma(const double* p, const double (&m)[NP]) {
+  double y0 = 0.0, y1 = 0.0, y2 = 0.0, y3 = 0.0;
+#pragma unroll
+  for (int j = 0; j < NP; j += 4) {
+    const double2 u = *reinterpret_cast<const double2*>(p + j);
+    const double2 v = *reinterpret_cast<const double2*>(p + j + 2);
+    y0 = __builtin_fma(u.x, m[j], y0);
+    y1 = __builtin_fma(u.y, m[j + 1], y1);
+    y2 = __builtin_fma(v.x, m[j + 2], y2);
+    y3 = __builtin_fma(v.y, m[j + 3], y3);
+  }
+  return (y0 + y1) + (y2 + y3);
+}
+
+// Sequence order: ord[k] is the k-th sequence to start (longest first, see the host), so the
+// first resident waves take the long chains and short ones fill in behind them.
+template <int NP>
+__global__ __launch_bounds__(256) void bw_fwd_wave(BwArgs g, int64_t nseq) {
+  __shared__ __attribute__((aligned(16))) double slot[4][NP];
+  const int w = threadIdx.x >> 6, i = threadIdx.x & 63;
+  const int64_t k = (int64_t)blockIdx.x * 4 + w;
+  if (k >= nseq) return;  // wave-uniform
+  const int64_t seq = g.order ? g.order[k] : k;
+  const int N = g.nstates;
+  const bool act = i < N;
+  double* p = slot[w];
+  double acol[NP];
+#pragma unroll
+  for (int j = 0; j < NP; ++j) acol[j] = (act && j < N) ? g.a[(size_t)j * N + i] : 0.0;
+  const int64_t e0 = g.offsets[seq];
+  const int T = (int)(g.offsets[seq + 1] - e0);
+  if (T <= 0) return;
+  double* al = g.alpha + (e0 - g.elem_base) * N;
+  const int32_t* obs = g.obs + e0;
+  const int32_t* tag = g.tags + e0;
+  StepBlocks blk;
+  blk.init(obs, tag, 0, 64, T, i);
+  // t = 0 (hmm.rs:81-88)
+  double cur;
+  {
+    const int o = blk.obs_at(0), tg = blk.tag_at(0);
+    const double y = act ? g.pi[i] * g.et[(size_t)o * N + i] : 0.0;
+    const double s = wave_sum(y);
+    cur = tg >= 0 ? (i == tg ? 1.0 : 0.0) : (act ? normalized(y, s, N) : 0.0);
+    if (act) al[i] = cur;
+  }
+  double e_nx = (T > 1 && act) ? g.et[(size_t)blk.obs_at(1) * N + i] : 0.0;
+  int tg_nx = T > 1 ? blk.tag_at(1) : -1;
+  for (int t = 1; t < T; ++t) {
+    const double eo = e_nx;
+    const int tg = tg_nx;
+    if (t + 1 < T) {  // prefetch step t+1
+      if (t + 1 - blk.base >= 64) blk.advance(obs, tag, 64, T, i);
+      tg_nx = blk.tag_at(t + 1);
+      e_nx = act ? g.et[(size_t)blk.obs_at(t + 1) * N + i] : 0.0;
+    }
+    if (tg >= 0) {  // hmm.rs:91
+      cur = (i == tg) ? 1.0 : 0.0;
+    } else {        // (alpha[t-1] * b(o_t)) . A  -- hmm.rs:93-94
+      if (i < NP) p[i] = cur * eo;
+      __builtin_amdgcn_wave_barrier();
+      const double y = dot_lds_fma<NP>(p, acol);
+      __builtin_amdgcn_wave_barrier();
+      const double sy = wave_sum(y);
+      cur = act ? normalized(y, sy, N) : 0.0;
+    }
+    if (act) al[(size_t)t * N + i] = cur;
+  }
+}
+
+// Backward pass fused with the E-step sums: beta is never stored.  At step t the backward
+// product w = A u_{t+1} (u = b(o_{t+1}) o beta_{t+1}) is also xi's row sum, so
+// c_t = alpha_t . w, S += (alpha_t / c_t) (x) u_{t+1} and beta_t = normalize(w) (or one-hot).
+// u_{t+1} is the LDS row every lane reads for w anyway; r_t = alpha_t / c_t goes to a second
+// LDS row.  Every 4 steps the rank-4 update S += R^T U runs on the matrix cores
+// (v_mfma_f64_16x16x4_f64, K = the 4 steps), S being (NP/16)^2 accumulator tiles.
+// A wave walks sequences ord[w], ord[w + nwaves], ... keeping S and the gamma sums in
+// registers; one atomic flush at the end.
+template <int NP>
+__global__ __launch_bounds__(256) void bw_bwd_stats_wave(BwArgs g, int64_t nseq, int64_t nwaves) {
+  constexpr int NT = NP / 16;
+  __shared__ __attribute__((aligned(16))) double uu[4][4][NP];  // [wave][step mod 4][state]
+  __shared__ __attribute__((aligned(16))) double rr[4][4][NP];
+  const int w = threadIdx.x >> 6, i = threadIdx.x & 63;
+  const int64_t gw = (int64_t)blockIdx.x * 4 + w;
+  if (gw >= nwaves) return;
+  const int N = g.nstates;
+  const bool act = i < N;
+  double arow[NP];
+#pragma unroll
+  for (int j = 0; j < NP; ++j) arow[j] = (act && j < N) ? g.a[(size_t)i * N + j] : 0.0;
+  typedef double double4_t __attribute__((ext_vector_type(4)));
+  double4_t S[NT][NT];
+#pragma unroll
+  for (int m = 0; m < NT; ++m)
+#pragma unroll
+    for (int n = 0; n < NT; ++n) S[m][n] = double4_t{0.0, 0.0, 0.0, 0.0};
+  if (i < NP)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) uu[w][q][i] = rr[w][q][i] = 0.0;
+  // rank-4 update from the 4 staged steps: lane l supplies R[k = l>>4][m = 16 mt + (l&15)]
+  // as A and U[k][n = 16 nt + (l&15)] as B
+  auto mfma_update = [&]() {
+    __builtin_amdgcn_wave_barrier();
+    double av[NT], bv[NT];
+#pragma unroll
+    for (int m = 0; m < NT; ++m) {
+      av[m] = rr[w][i >> 4][16 * m + (i & 15)];
+      bv[m] = uu[w][i >> 4][16 * m + (i & 15)];
+    }
+#pragma unroll
+    for (int m = 0; m < NT; ++m)
+#pragma unroll
+      for (int n = 0; n < NT; ++n) S[m][n] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[m], bv[n], S[m][n], 0, 0, 0);
+    __builtin_amdgcn_wave_barrier();
+  };
+  double pi_acc = 0.0, a_den = 0.0, b_den = 0.0, z = 0.0;
+  for (int64_t kq = gw; kq < nseq; kq += nwaves) {
+    const int64_t seq = g.order ? g.order[kq] : kq;
+    const int64_t e0 = g.offsets[seq];
+    const int T = (int)(g.offsets[seq + 1] - e0);
+    if (T <= 0) continue;
+    const double* al = g.alpha + (e0 - g.elem_base) * N;
+    const int32_t* obs = g.obs + e0;
+    const int32_t* tag = g.tags + e0;
+    StepBlocks blk;  // blocks [T-64, T), [T-128, T-64), ... (lanes below 0 load nothing)
+    blk.init(obs, tag, T - 64, -64, T, i);
+    // t = T-1 (hmm.rs:105-108)
+    int o_t = blk.obs_at(T - 1);
+    int tg = blk.tag_at(T - 1);
+    double beta = tg >= 0 ? (i == tg ? 1.0 : 0.0) : (act ? 1.0 : 0.0);
+    double alt = act ? al[(size_t)(T - 1) * N + i] : 0.0;
+    double e_t = act ? g.et[(size_t)o_t * N + i] : 0.0;  // b(o_t), used as b(o_{t+1}) one step later
+    // step T-2 prefetched
+    int o_nx = T > 1 ? blk.obs_at(T - 2) : 0, tg_nx = T > 1 ? blk.tag_at(T - 2) : -1;
+    double e_nx = (T > 1 && act) ? g.et[(size_t)o_nx * N + i] : 0.0;
+    double a_nx = (T > 1 && act) ? al[(size_t)(T - 2) * N + i] : 0.0;
+    {
+      const double ab = alt * beta;
+      const double gm = normalized(ab, wave_sum(ab), N);
+      if (act) {
+        b_den += gm;
+        if (T == 1) pi_acc += gm;
+        unsafeAtomicAdd(&g.b_num[(size_t)o_t * N + i], gm);
+      }
+    }
+    int q = 0;  // staged steps
+    for (int t = T - 2; t >= 0; --t) {
+      const double e1 = e_t;
+      e_t = e_nx;
+      alt = a_nx;
+      o_t = o_nx;
+      tg = tg_nx;
+      if (t >= 1) {  // prefetch step t-1
+        if (t - 1 < blk.base) blk.advance(obs, tag, -64, T, i);
+        o_nx = blk.obs_at(t - 1);
+        tg_nx = blk.tag_at(t - 1);
+        e_nx = act ? g.et[(size_t)o_nx * N + i] : 0.0;
+        a_nx = act ? al[(size_t)(t - 1) * N + i] : 0.0;
+      }
+      // u_{t+1} = b(o_{t+1}) o beta_{t+1};  w_i = sum_j A[i][j] u_j  (hmm.rs:113-116, 135-141)
+      double* u = uu[w][q];
+      if (i < NP) u[i] = e1 * beta;
+      __builtin_amdgcn_wave_barrier();
+      const double wv = dot_lds_fma<NP>(u, arow);
+      double c = alt * wv, sw = wv;
+      wave_sum2(c, sw);
+      z += c == 0.0 ? 1.0 : 0.0;  // xi_t uniform (hmm.rs:306-317), counted separately
+      if (i < NP) rr[w][q][i] = c != 0.0 ? alt / c : 0.0;
+      if (++q == 4) {
+        mfma_update();
+        q = 0;
+      }
+      beta = tg >= 0 ? (i == tg ? 1.0 : 0.0) : (act ? normalized(wv, sw, N) : 0.0);
+      const double ab = alt * beta;
+      const double gm = normalized(ab, wave_sum(ab), N);  // hmm.rs:127-129
+      if (act) {
+        a_den += gm;
+        b_den += gm;
+        if (t == 0) pi_acc += gm;
+        unsafeAtomicAdd(&g.b_num[(size_t)o_t * N + i], gm);
+      }
+    }
+    if (q != 0) {  // flush a partial group: zero the unused staged steps
+      if (i < NP)
+        for (int k = q; k < 4; ++k) uu[w][k][i] = rr[w][k][i] = 0.0;
+      mfma_update();
+    }
+  }
+  if (act) {
+    unsafeAtomicAdd(&g.pi_acc[i], pi_acc);
+    unsafeAtomicAdd(&g.a_den[i], a_den);
+    unsafeAtomicAdd(&g.b_den[i], b_den);
+  }
+  // C/D layout of v_mfma_f64_16x16x4_f64: col = lane & 15, row = (lane >> 4) + 4 * reg
+#pragma unroll
+  for (int m = 0; m < NT; ++m)
+#pragma unroll
+    for (int n = 0; n < NT; ++n)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = 16 * m + (i >> 4) + 4 * r, col = 16 * n + (i & 15);
+        if (row < N && col < N) unsafeAtomicAdd(&g.xi_s[(size_t)row * N + col], S[m][n][r]);
+      }
+  if (i == 0 && z != 0.0) unsafeAtomicAdd(g.xi_zero, z);
+}
+
+// ---- M-step on the device (hmm.rs:145-175) ---------------------------------------------------
+// Parameters stay resident between iterations: pi, a (and its transpose at), et = b^T.  The
+// convergence sum d = sum |new - old| is reduced per block into part[]; the host adds the
+// parts in a fixed order.  Built with -ffp-contract=off: same roundings as the host M-step.
+
+__device__ __forceinline__ double block_sum_any(double v, double* red) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
+  const int w = threadIdx.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[w] = v;
+  __syncthreads();
+  return (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+__global__ __launch_bounds__(256) void bw_mstep_pa(MstepArgs m) {
+  __shared__ double red[4];
+  const int N = m.nstates;
+  const double* pi_acc = m.acc;
+  const double* a_den = m.acc + N;
+  const double* xs = m.acc + 3 * N + (size_t)m.nobs * N;
+  const double zu = xs[(size_t)N * N] / ((double)N * (double)N);
+  double d = 0.0;
+  for (int i = threadIdx.x; i < N; i += blockDim.x) {
+    const double np = pi_acc[i] / (double)m.nseq;
+    d += fabs(np - m.pi[i]);
+    m.pi[i] = np;
+  }
+  for (int k = threadIdx.x; k < N * N; k += blockDim.x) {
+    const int i = k / N, j = k - i * N;
+    const double na = (m.a[k] * xs[k] + zu) / a_den[i];
+    d += fabs(na - m.a[k]);
+    m.a[k] = na;
+    m.at[(size_t)j * N + i] = na;
+  }
+  d = block_sum_any(d, red);
+  if (threadIdx.x == 0) m.part[0] = d;
+}
+
+__global__ __launch_bounds__(256) void bw_mstep_b(MstepArgs m) {
+  __shared__ double red[4];
+  const int N = m.nstates;
+  const double* b_den = m.acc + 2 * N;
+  const double* b_num = m.acc + 3 * N;
+  const size_t n = (size_t)m.nobs * N;
+  double d = 0.0;
+  for (size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (size_t)gridDim.x * blockDim.x) {
+    const double nb = b_num[k] / b_den[k % N];
+    d += fabs(nb - m.et[k]);
+    m.et[k] = nb;
+  }
+  d = block_sum_any(d, red);
+  if (threadIdx.x == 0) m.part[1 + blockIdx.x] = d;
+}
+
 hipError_t launch_mle_counts(const MleArgs& g, int64_t nseq, hipStream_t stream) {
   if (nseq <= 0) return hipSuccess;
   hipLaunchKernelGGL(mle_counts, dim3((unsigned)nseq), dim3(256), 0, stream, g);
   return hipGetLastError();
 }
 
-hipError_t launch_bw_estep(const BwArgs& g, int64_t nseq, hipStream_t stream) {
+template <int NP>
+static void launch_wave_estep(const BwArgs& g, int64_t nseq, int64_t nwaves, hipStream_t stream) {
+  hipLaunchKernelGGL((bw_fwd_wave<NP>), dim3((unsigned)((nseq + 3) / 4)), dim3(256), 0, stream, g, nseq);
+  hipLaunchKernelGGL((bw_bwd_stats_wave<NP>), dim3((unsigned)((nwaves + 3) / 4)), dim3(256), 0, stream, g, nseq,
+                     nwaves);
+}
+
+hipError_t launch_bw_estep(const BwArgs& g, int64_t nseq, int64_t max_waves, hipStream_t stream) {
   if (nseq <= 0) return hipSuccess;
   if (g.nstates > kBwMaxStates) return hipErrorInvalidValue;
+  if (g.nstates <= kBwWaveStates) {
+    const int64_t nwaves = std::max<int64_t>(1, std::min<int64_t>(nseq, max_waves));
+    if (g.nstates <= 16) launch_wave_estep<16>(g, nseq, nwaves, stream);
+    else if (g.nstates <= 32) launch_wave_estep<32>(g, nseq, nwaves, stream);
+    else if (g.nstates <= 48) launch_wave_estep<48>(g, nseq, nwaves, stream);
+    else launch_wave_estep<64>(g, nseq, nwaves, stream);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(bw_forward, dim3((unsigned)nseq), dim3(256), 0, stream, g);
   hipLaunchKernelGGL(bw_backward, dim3((unsigned)nseq), dim3(256), 0, stream, g);
   const size_t lds = ((size_t)g.nstates * g.nstates + 256 + 4) * sizeof(double);
@@ -202,6 +554,12 @@ hipError_t launch_bw_estep(const BwArgs& g, int64_t nseq, hipStream_t stream) {
     attr = true;
   }
   hipLaunchKernelGGL(bw_stats, dim3((unsigned)nseq), dim3(256), lds, stream, g);
+  return hipGetLastError();
+}
+
+hipError_t launch_bw_mstep(const MstepArgs& m, int nparts_b, hipStream_t stream) {
+  hipLaunchKernelGGL(bw_mstep_pa, dim3(1), dim3(256), 0, stream, m);
+  hipLaunchKernelGGL(bw_mstep_b, dim3((unsigned)nparts_b), dim3(256), 0, stream, m);
   return hipGetLastError();
 }
 

@@ -101,11 +101,15 @@ def test_gpu_mle_matches_oracle(gpu, n, v):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n,v,frac", [(3, 5, 0.0), (12, 30, 0.3), (45, 60, 0.2), (128, 40, 0.1)])
-def test_gpu_train_matches_oracle(gpu, n, v, frac):
+# N <= 64 runs the one-wave kernels (padded to 16/32/48/64 states), N > 64 the workgroup
+# kernels; T > 64 crosses the 64-step observation blocks of the wave kernels
+@pytest.mark.parametrize("n,v,frac,tmax", [(3, 5, 0.0, 30), (12, 30, 0.3, 150), (20, 30, 0.5, 200),
+                                           (45, 60, 0.2, 130), (64, 40, 0.1, 70), (65, 40, 0.1, 40),
+                                           (128, 40, 0.1, 30)])
+def test_gpu_train_matches_oracle(gpu, n, v, frac, tmax):
     import cviterbi as cv
 
-    off, obs, tags = _corpus(n, v, 24, 30, frac, seed=100 + n)
+    off, obs, tags = _corpus(n, v, 24, tmax, frac, seed=100 + n)
     pi0, a0, b0 = _probs(n, v, seed=100 + n)
     iters = 3
     gp, ga, gb, it = cv.fit_train(pi0, a0, b0, off, obs, tags, max_iter=iters, tol=0.0)
