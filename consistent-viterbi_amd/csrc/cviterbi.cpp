@@ -909,6 +909,8 @@ CV_API cv_status cv_decode_batch(cv_hmm* h, int64_t nseq, const int64_t* offsets
 
 // ---- consistency-constrained decode --------------------------------------------------------
 // Spec: oracle/np_oracle.py constrained_decode; host search: csp.hpp.
+}  // extern "C"
+
 namespace {
 constexpr uint64_t kCspNodeLimit = 20000000;  // branch-and-bound nodes per call
 constexpr int64_t kSegmentSlots = 65536;      // segment-table rows per launch (64 MiB of rows)
@@ -1262,6 +1264,8 @@ bool pairs_sorted(const int32_t* pairs, int64_t npairs, int32_t ncomp) {
 }
 }  // namespace
 
+extern "C" {
+
 CV_API cv_status cv_constrained_pairs(int64_t nseq, const int64_t* offsets, const int32_t* component, int32_t ncomp,
                                       int32_t* pairs_out, int64_t cap_pairs, int64_t* npairs_out) {
   if (nseq < 0 || ncomp < 0 || !npairs_out || (nseq > 0 && (!offsets || !component)))
@@ -1558,7 +1562,7 @@ cv_status fit_validate(int32_t N, int64_t V, int64_t nseq, const int64_t* offset
 }
 
 struct FitDev {
-  DevBuf off, obs, tags, pi, a, at, et, alpha, beta, acc, cnt, ord;
+  DevBuf off, obs, tags, pi, a, at, et, alpha, beta, acc, cnt, ord, dump;
 };
 
 }  // namespace
@@ -1679,6 +1683,7 @@ CV_API cv_status cv_hmm_fit_train(int32_t nstates, int64_t nobs, int64_t nseq, c
   if ((st = d.at.ensure((size_t)N * N * 8)) != CV_OK) return st;
   if ((st = d.et.ensure((size_t)V * N * 8)) != CV_OK) return st;
   if ((st = d.cnt.ensure((1 + kPartsB) * 8)) != CV_OK) return st;
+  if ((st = d.dump.ensure((size_t)cvf::kBwDumpWaves * 64 * 8)) != CV_OK) return st;
   int cus = 0;
   HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
   const int64_t max_waves = (int64_t)std::max(cus, 1) * 8;  // backward waves resident at 2 per SIMD
@@ -1730,6 +1735,7 @@ CV_API cv_status cv_hmm_fit_train(int32_t nstates, int64_t nobs, int64_t nseq, c
       g.tags = d.tags.as<int32_t>();
       g.elem_base = off0[c.first];
       g.order = d.ord.as<int64_t>() + c.first;
+      g.dump = d.dump.as<double>();
       g.nstates = N;
       g.pi = d.pi.as<double>();
       g.a = d.a.as<double>();

@@ -34,6 +34,8 @@ struct BwArgs {
   const double* et;     // [V][N] emissions transposed
   double* alpha;        // [elements][N] workspace
   double* beta;         // [elements][N] workspace
+  double* dump;         // [kBwDumpWaves][64] N <= 64 kernels: target of the stores / atomic adds
+                        // of lanes without a state (one row per wave: no shared hot line)
   // E-step sums (accumulated across sequences; zeroed by the host per iteration)
   double* pi_acc;       // [N]  sum of gamma_0
   double* a_den;        // [N]  sum of gamma_t, t < T-1
@@ -44,6 +46,7 @@ struct BwArgs {
 };
 
 constexpr int kBwWaveStates = 64;  // N <= 64: one wave per sequence (bw_*_wave)
+constexpr int kBwDumpWaves = 4096;
 
 // M-step: acc = [pi_acc N | a_den N | b_den N | b_num V*N | xi_s N*N | xi_zero 1]
 struct MstepArgs {

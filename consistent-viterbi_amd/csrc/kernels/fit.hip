@@ -31,7 +31,11 @@ __device__ __forceinline__ double block_sum(double v, double* red) {
 }
 
 // normalize (hmm.rs:274-282): v / sum, or 1/len when the sum is 0
+#ifndef CVF_ABL_NODIV
 __device__ __forceinline__ double normalized(double v, double s, int n) { return s != 0.0 ? v / s : 1.0 / n; }
+#else
+__device__ __forceinline__ double normalized(double v, double s, int n) { return s != 0.0 ? v * s : 1.0 / n; }
+#endif
 
 __global__ __launch_bounds__(256) void mle_counts(MleArgs g) {
   const int64_t seq = blockIdx.x;
@@ -232,29 +236,38 @@ __device__ __forceinline__ void wave_sum2(double& a, double& b) {
   b = (readlane_f64(b, 0) + readlane_f64(b, 16)) + (readlane_f64(b, 32) + readlane_f64(b, 48));
 }
 
-// 64-step blocks of observation indices and tags, one element per lane, double-buffered: the
-// next block is loaded when the current one is taken into use, 64 steps before it is needed.
-struct StepBlocks {
-  int base, ob, tg, ob_nx, tg_nx;
-  __device__ __forceinline__ void load(const int32_t* obs, const int32_t* tag, int b, int T, int lane, int& o, int& t) {
-    const bool in = b + lane >= 0 && b + lane < T;
-    o = in ? obs[b + lane] : 0;
-    t = in ? tag[b + lane] : -1;
-  }
-  __device__ __forceinline__ void init(const int32_t* obs, const int32_t* tag, int b, int step, int T, int lane) {
-    base = b;
-    load(obs, tag, b, T, lane, ob, tg);
-    load(obs, tag, b + step, T, lane, ob_nx, tg_nx);
-  }
-  __device__ __forceinline__ void advance(const int32_t* obs, const int32_t* tag, int step, int T, int lane) {
-    base += step;
-    ob = ob_nx;
-    tg = tg_nx;
-    load(obs, tag, base + step, T, lane, ob_nx, tg_nx);
-  }
-  __device__ __forceinline__ int obs_at(int s) const { return __builtin_amdgcn_readlane(ob, s - base); }
-  __device__ __forceinline__ int tag_at(int s) const { return __builtin_amdgcn_readlane(tg, s - base); }
-};
+// Memory operations in the step loops are all unconditional (clamped indices; lanes without
+// a state store to / add into a per-lane dump slot): a load, store or atomic under a branch
+// makes the compiler's wait-count tracking give up and wait for every outstanding load
+// (vmcnt(0)) at the next use, which would expose the full HBM latency on every step.  The step
+// loops are unrolled with a static slot per step, so no loaded register is copied across the
+// loop edge either (a copy is a use, i.e. a wait for the load just issued).
+
+// a value loaded through a vector load but equal in all lanes, as a scalar (uniform control
+// flow and addresses downstream)
+__device__ __forceinline__ int64_t uniform64(int64_t v) {
+  const unsigned lo = (unsigned)__builtin_amdgcn_readfirstlane((int)v);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readfirstlane((int)(v >> 32));
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+
+// four independent sums with their latencies overlapped
+__device__ __forceinline__ void wave_sum4(double& a, double& b, double& c, double& d) {
+#define CVF_LVL(CTRL)          \
+  a += dpp_f64<CTRL>(a);       \
+  b += dpp_f64<CTRL>(b);       \
+  c += dpp_f64<CTRL>(c);       \
+  d += dpp_f64<CTRL>(d);
+  CVF_LVL(0xB1)
+  CVF_LVL(0x4E)
+  CVF_LVL(0x141)
+  CVF_LVL(0x140)
+#undef CVF_LVL
+  a = (readlane_f64(a, 0) + readlane_f64(a, 16)) + (readlane_f64(a, 32) + readlane_f64(a, 48));
+  b = (readlane_f64(b, 0) + readlane_f64(b, 16)) + (readlane_f64(b, 32) + readlane_f64(b, 48));
+  c = (readlane_f64(c, 0) + readlane_f64(c, 16)) + (readlane_f64(c, 32) + readlane_f64(c, 48));
+  d = (readlane_f64(d, 0) + readlane_f64(d, 16)) + (readlane_f64(d, 32) + readlane_f64(d, 48));
+}
 
 // y = sum_j p[j] * m[j], p broadcast from LDS, 4 partial sums (fused multiply-add)
 template <int NP>
@@ -278,77 +291,103 @@ template <int NP>
 __global__ __launch_bounds__(256) void bw_fwd_wave(BwArgs g, int64_t nseq) {
   __shared__ __attribute__((aligned(16))) double slot[4][NP];
   const int w = threadIdx.x >> 6, i = threadIdx.x & 63;
-  const int64_t k = (int64_t)blockIdx.x * 4 + w;
-  if (k >= nseq) return;  // wave-uniform
-  const int64_t seq = g.order ? g.order[k] : k;
+  const int64_t kq = (int64_t)blockIdx.x * 4 + w;
+  if (kq >= nseq) return;  // wave-uniform
+  const int64_t seq = uniform64(g.order ? g.order[kq] : kq);
   const int N = g.nstates;
   const bool act = i < N;
+  const int ic = act ? i : N - 1;  // state index inactive lanes load with (always in bounds)
   double* p = slot[w];
   double acol[NP];
 #pragma unroll
   for (int j = 0; j < NP; ++j) acol[j] = (act && j < N) ? g.a[(size_t)j * N + i] : 0.0;
-  const int64_t e0 = g.offsets[seq];
-  const int T = (int)(g.offsets[seq + 1] - e0);
+  const int64_t e0 = uniform64(g.offsets[seq]);
+  const int T = __builtin_amdgcn_readfirstlane((int)(g.offsets[seq + 1] - e0));
   if (T <= 0) return;
   double* al = g.alpha + (e0 - g.elem_base) * N;
+  double* const dump = g.dump + (size_t)(kq & (kBwDumpWaves - 1)) * 64 + i;
   const int32_t* obs = g.obs + e0;
   const int32_t* tag = g.tags + e0;
-  StepBlocks blk;
-  blk.init(obs, tag, 0, 64, T, i);
+  const double* et = g.et;
   // t = 0 (hmm.rs:81-88)
   double cur;
   {
-    const int o = blk.obs_at(0), tg = blk.tag_at(0);
-    const double y = act ? g.pi[i] * g.et[(size_t)o * N + i] : 0.0;
+    const int o = obs[0], tg = tag[0];
+    const double y = act ? g.pi[i] * et[(size_t)o * N + i] : 0.0;
     const double s = wave_sum(y);
     cur = tg >= 0 ? (i == tg ? 1.0 : 0.0) : (act ? normalized(y, s, N) : 0.0);
-    if (act) al[i] = cur;
+    *(act ? al + i : dump) = cur;
   }
-  double e_nx = (T > 1 && act) ? g.et[(size_t)blk.obs_at(1) * N + i] : 0.0;
-  int tg_nx = T > 1 ? blk.tag_at(1) : -1;
-  for (int t = 1; t < T; ++t) {
-    const double eo = e_nx;
-    const int tg = tg_nx;
-    if (t + 1 < T) {  // prefetch step t+1
-      if (t + 1 - blk.base >= 64) blk.advance(obs, tag, 64, T, i);
-      tg_nx = blk.tag_at(t + 1);
-      e_nx = act ? g.et[(size_t)blk.obs_at(t + 1) * N + i] : 0.0;
+  // observation index and tag of step s fetched 6 steps ahead (slot s mod 8), b(o_s) 3 steps
+  // ahead (slot s mod 4) from the index fetched 3 steps before that; all indices clamped.
+  int po[8], ptg[8];
+  double pe[4];
+  auto fetch_ot = [&](int s, int k8) {
+    const int sc = min(s, T - 1);
+    po[k8] = obs[sc];
+    ptg[k8] = tag[sc];
+  };
+#pragma unroll
+  for (int k = 0; k < 6; ++k) fetch_ot(1 + k, k);  // steps 1..6
+#pragma unroll
+  for (int k = 0; k < 3; ++k) pe[k] = et[(size_t)po[k] * N + ic];  // steps 1..3
+  for (int t0 = 1; t0 < T; t0 += 8) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int t = t0 + k;
+      if (t >= T) break;
+      fetch_ot(t + 6, (k + 6) & 7);
+      pe[(k + 3) & 3] = et[(size_t)po[(k + 3) & 7] * N + ic];
+      const int tg = __builtin_amdgcn_readfirstlane(ptg[k]);
+      if (tg >= 0) {  // hmm.rs:91
+        cur = (i == tg) ? 1.0 : 0.0;
+      } else {        // (alpha[t-1] * b(o_t)) . A  -- hmm.rs:93-94
+        if (i < NP) p[i] = act ? cur * pe[k & 3] : 0.0;
+        __builtin_amdgcn_wave_barrier();
+        const double y = dot_lds_fma<NP>(p, acol);
+        __builtin_amdgcn_wave_barrier();
+        const double sy = wave_sum(y);
+        cur = act ? normalized(y, sy, N) : 0.0;
+      }
+      *(act ? al + (size_t)t * N + i : dump) = cur;
     }
-    if (tg >= 0) {  // hmm.rs:91
-      cur = (i == tg) ? 1.0 : 0.0;
-    } else {        // (alpha[t-1] * b(o_t)) . A  -- hmm.rs:93-94
-      if (i < NP) p[i] = cur * eo;
-      __builtin_amdgcn_wave_barrier();
-      const double y = dot_lds_fma<NP>(p, acol);
-      __builtin_amdgcn_wave_barrier();
-      const double sy = wave_sum(y);
-      cur = act ? normalized(y, sy, N) : 0.0;
-    }
-    if (act) al[(size_t)t * N + i] = cur;
   }
 }
 
 // Backward pass fused with the E-step sums: beta is never stored.  At step t the backward
 // product w = A u_{t+1} (u = b(o_{t+1}) o beta_{t+1}) is also xi's row sum, so
 // c_t = alpha_t . w, S += (alpha_t / c_t) (x) u_{t+1} and beta_t = normalize(w) (or one-hot).
-// u_{t+1} is the LDS row every lane reads for w anyway; r_t = alpha_t / c_t goes to a second
-// LDS row.  Every 4 steps the rank-4 update S += R^T U runs on the matrix cores
-// (v_mfma_f64_16x16x4_f64, K = the 4 steps), S being (NP/16)^2 accumulator tiles.
-// A wave walks sequences ord[w], ord[w + nwaves], ... keeping S and the gamma sums in
+// Each wave runs TWO sequences side by side (consecutive in the longest-first order, so of
+// similar length, aligned at their last element): their chains are independent, which hides
+// the latency of the reductions and divisions, and one pass over lane i's row of A (in LDS)
+// serves both products.  u_{t+1} is the LDS row every lane reads for w anyway; r_t =
+// alpha_t / c_t goes to a second LDS row; every 2 steps the rank-4 update S += R^T U (2 steps
+// x 2 sequences) runs on the matrix cores (v_mfma_f64_16x16x4_f64), S being (NP/16)^2
+// accumulator tiles.  A wave walks pairs w, w + nwaves, ... keeping S and the gamma sums in
 // registers; one atomic flush at the end.
 template <int NP>
 __global__ __launch_bounds__(256) void bw_bwd_stats_wave(BwArgs g, int64_t nseq, int64_t nwaves) {
   constexpr int NT = NP / 16;
-  __shared__ __attribute__((aligned(16))) double uu[4][4][NP];  // [wave][step mod 4][state]
+  __shared__ __attribute__((aligned(16))) double uu[4][4][NP];  // [wave][2 * (step & 1) + seq][state]
   __shared__ __attribute__((aligned(16))) double rr[4][4][NP];
   const int w = threadIdx.x >> 6, i = threadIdx.x & 63;
   const int64_t gw = (int64_t)blockIdx.x * 4 + w;
-  if (gw >= nwaves) return;
   const int N = g.nstates;
   const bool act = i < N;
-  double arow[NP];
-#pragma unroll
-  for (int j = 0; j < NP; ++j) arow[j] = (act && j < N) ? g.a[(size_t)i * N + j] : 0.0;
+  const int ic = act ? i : N - 1;
+  double* const dump = g.dump + (size_t)(gw & (kBwDumpWaves - 1)) * 64 + i;
+  const double* et = g.et;
+  // A lives in LDS, row i read by lane i (row stride AS = 2 mod 32 doubles: the 16 lanes of a
+  // ds_read_b128 phase hit 16 distinct 4-bank groups); registers go to S and the fetch slots
+  constexpr int AS = (NP + 31) / 32 * 32 + 2;
+  __shared__ __attribute__((aligned(16))) double As[NP * AS];
+  for (int k = threadIdx.x; k < NP * AS; k += 256) {
+    const int r = k / AS, c = k - r * AS;
+    As[k] = (r < N && c < N) ? g.a[(size_t)r * N + c] : 0.0;
+  }
+  __syncthreads();  // every wave of the block loads its share of A before any leaves
+  if (gw >= nwaves) return;
+  const double* arow = As + (i < NP ? i : 0) * AS;
   typedef double double4_t __attribute__((ext_vector_type(4)));
   double4_t S[NT][NT];
 #pragma unroll
@@ -358,8 +397,8 @@ __global__ __launch_bounds__(256) void bw_bwd_stats_wave(BwArgs g, int64_t nseq,
   if (i < NP)
 #pragma unroll
     for (int q = 0; q < 4; ++q) uu[w][q][i] = rr[w][q][i] = 0.0;
-  // rank-4 update from the 4 staged steps: lane l supplies R[k = l>>4][m = 16 mt + (l&15)]
-  // as A and U[k][n = 16 nt + (l&15)] as B
+  // rank-4 update from the 4 staged rows: lane l supplies R[k = l>>4][m = 16 mt + (l&15)] as
+  // A and U[k][n = 16 nt + (l&15)] as B
   auto mfma_update = [&]() {
     __builtin_amdgcn_wave_barrier();
     double av[NT], bv[NT];
@@ -375,75 +414,147 @@ __global__ __launch_bounds__(256) void bw_bwd_stats_wave(BwArgs g, int64_t nseq,
     __builtin_amdgcn_wave_barrier();
   };
   double pi_acc = 0.0, a_den = 0.0, b_den = 0.0, z = 0.0;
-  for (int64_t kq = gw; kq < nseq; kq += nwaves) {
-    const int64_t seq = g.order ? g.order[kq] : kq;
-    const int64_t e0 = g.offsets[seq];
-    const int T = (int)(g.offsets[seq + 1] - e0);
-    if (T <= 0) continue;
-    const double* al = g.alpha + (e0 - g.elem_base) * N;
-    const int32_t* obs = g.obs + e0;
-    const int32_t* tag = g.tags + e0;
-    StepBlocks blk;  // blocks [T-64, T), [T-128, T-64), ... (lanes below 0 load nothing)
-    blk.init(obs, tag, T - 64, -64, T, i);
+  const int64_t npairs = (nseq + 1) / 2;
+  for (int64_t pq = gw; pq < npairs; pq += nwaves) {
+    // the two sequences; a missing second one (odd count) runs as T = 0 on the first's arrays
+    const double* al[2];
+    const int32_t* obs[2];
+    const int32_t* tag[2];
+    int T[2];
+#pragma unroll
+    for (int x = 0; x < 2; ++x) {
+      const int64_t kq = 2 * pq + x < nseq ? 2 * pq + x : 2 * pq;
+      const int64_t seq = uniform64(g.order ? g.order[kq] : kq);
+      const int64_t e0 = uniform64(g.offsets[seq]);
+      T[x] = 2 * pq + x < nseq ? __builtin_amdgcn_readfirstlane((int)(g.offsets[seq + 1] - e0)) : 0;
+      al[x] = g.alpha + (e0 - g.elem_base) * N;
+      obs[x] = g.obs + e0;
+      tag[x] = g.tags + e0;
+    }
     // t = T-1 (hmm.rs:105-108)
-    int o_t = blk.obs_at(T - 1);
-    int tg = blk.tag_at(T - 1);
-    double beta = tg >= 0 ? (i == tg ? 1.0 : 0.0) : (act ? 1.0 : 0.0);
-    double alt = act ? al[(size_t)(T - 1) * N + i] : 0.0;
-    double e_t = act ? g.et[(size_t)o_t * N + i] : 0.0;  // b(o_t), used as b(o_{t+1}) one step later
-    // step T-2 prefetched
-    int o_nx = T > 1 ? blk.obs_at(T - 2) : 0, tg_nx = T > 1 ? blk.tag_at(T - 2) : -1;
-    double e_nx = (T > 1 && act) ? g.et[(size_t)o_nx * N + i] : 0.0;
-    double a_nx = (T > 1 && act) ? al[(size_t)(T - 2) * N + i] : 0.0;
-    {
-      const double ab = alt * beta;
+    double beta[2], pe[2][4], pa[2][4];
+    int po[2][8], ptg[2][8];
+#pragma unroll
+    for (int x = 0; x < 2; ++x) {
+      const bool valid = T[x] > 0;
+      const int tl = valid ? T[x] - 1 : 0;
+      const int o = obs[x][tl], tg = tag[x][tl];
+      beta[x] = tg >= 0 ? (i == tg ? 1.0 : 0.0) : (act ? 1.0 : 0.0);
+      const double alt = (act && valid) ? al[x][(size_t)tl * N + i] : 0.0;
+      pe[x][3] = act ? et[(size_t)o * N + i] : 0.0;  // b(o_{T-1}), used by step T-2
+      const double ab = alt * beta[x];
       const double gm = normalized(ab, wave_sum(ab), N);
-      if (act) {
+      const bool on = act && valid;
+      if (on) {
         b_den += gm;
-        if (T == 1) pi_acc += gm;
-        unsafeAtomicAdd(&g.b_num[(size_t)o_t * N + i], gm);
+        if (T[x] == 1) pi_acc += gm;
+      }
+      unsafeAtomicAdd(on ? &g.b_num[(size_t)o * N + i] : dump, on ? gm : 0.0);
+    }
+    // observation index and tag of step s fetched 6 steps ahead (slot by step mod 8), b(o_s)
+    // and alpha_s 2 steps ahead (slot mod 4); all indices clamped into the sequence.
+    auto fetch_ot = [&](int x, int s, int k8) {
+      const int sc = min(max(s, 0), max(T[x] - 1, 0));
+#ifndef CVF_ABL_NOIDX
+      po[x][k8] = obs[x][sc];
+      ptg[x][k8] = tag[x][sc];
+#else
+      po[x][k8] = sc & 1023;
+      ptg[x][k8] = (sc % 5 == 0) ? 3 : -1;
+#endif
+    };
+    auto fetch_ea = [&](int x, int s, int k8, int k4) {
+      const int sc = min(max(s, 0), max(T[x] - 1, 0));
+#ifndef CVF_ABL_NOLOAD
+      pe[x][k4] = et[(size_t)po[x][k8] * N + ic];
+      pa[x][k4] = al[x][(size_t)sc * N + ic];
+#else
+      pe[x][k4] = 1e-3 * (double)(po[x][k8] + ic);
+      pa[x][k4] = 1e-2 * (double)(sc + ic);
+#endif
+    };
+#pragma unroll
+    for (int x = 0; x < 2; ++x) {
+#pragma unroll
+      for (int k = 0; k < 6; ++k) fetch_ot(x, T[x] - 2 - k, k);  // steps T-2 .. T-7
+      fetch_ea(x, T[x] - 2, 0, 0);
+      fetch_ea(x, T[x] - 3, 1, 1);
+    }
+    const int L = max(T[0], T[1]);
+    // step r of the pair is step t = T[x] - 2 - r of sequence x (inactive once t < 0)
+    for (int r0 = 0; r0 < L - 1; r0 += 8) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int r = r0 + k;
+        if (r >= L - 1) break;
+        double alt[2], wv[2];
+        bool valid[2];
+#pragma unroll
+        for (int x = 0; x < 2; ++x) {
+          const int t = T[x] - 2 - r;
+          valid[x] = t >= 0;
+          fetch_ot(x, t - 6, (k + 6) & 7);
+          fetch_ea(x, t - 2, (k + 2) & 7, (k + 2) & 3);
+          alt[x] = (act && valid[x]) ? pa[x][k & 3] : 0.0;
+          // u_{t+1} = b(o_{t+1}) o beta_{t+1}  (hmm.rs:113-116, 135-141)
+          if (i < NP) uu[w][2 * (k & 1) + x][i] = (act && valid[x]) ? pe[x][(k + 3) & 3] * beta[x] : 0.0;
+        }
+        __builtin_amdgcn_wave_barrier();
+        {  // w_x[i] = sum_j A[i][j] u_x[j], one pass over the row of A for both sequences
+          const double* u0 = uu[w][2 * (k & 1)];
+          const double* u1 = uu[w][2 * (k & 1) + 1];
+          double y0 = 0.0, y1 = 0.0, y2 = 0.0, y3 = 0.0;
+#pragma unroll
+          for (int j = 0; j < NP; j += 2) {
+            const double2 av = *reinterpret_cast<const double2*>(arow + j);
+            const double2 p0 = *reinterpret_cast<const double2*>(u0 + j);
+            const double2 p1 = *reinterpret_cast<const double2*>(u1 + j);
+            y0 = __builtin_fma(p0.x, av.x, y0);
+            y1 = __builtin_fma(p0.y, av.y, y1);
+            y2 = __builtin_fma(p1.x, av.x, y2);
+            y3 = __builtin_fma(p1.y, av.y, y3);
+          }
+          wv[0] = y0 + y1;
+          wv[1] = y2 + y3;
+        }
+        double c0 = alt[0] * wv[0], sw0 = wv[0], c1 = alt[1] * wv[1], sw1 = wv[1];
+        wave_sum4(c0, sw0, c1, sw1);
+        const double c[2] = {c0, c1}, sw[2] = {sw0, sw1};
+        double ab[2];
+#pragma unroll
+        for (int x = 0; x < 2; ++x) {
+          z += (valid[x] && c[x] == 0.0) ? 1.0 : 0.0;  // xi_t uniform (hmm.rs:306-317), counted separately
+          if (i < NP) rr[w][2 * (k & 1) + x][i] = c[x] != 0.0 ? alt[x] / c[x] : 0.0;
+          const int tg = ptg[x][k];
+          const double nb = tg >= 0 ? (i == tg ? 1.0 : 0.0) : (act ? normalized(wv[x], sw[x], N) : 0.0);
+          beta[x] = valid[x] ? nb : beta[x];
+          ab[x] = alt[x] * beta[x];
+        }
+#ifndef CVF_ABL_NOMFMA
+        if (k & 1) mfma_update();  // 2 steps x 2 sequences staged
+#endif
+        double s0 = ab[0], s1 = ab[1];
+        wave_sum2(s0, s1);  // hmm.rs:127-129
+        const double sab[2] = {s0, s1};
+#pragma unroll
+        for (int x = 0; x < 2; ++x) {
+          const double gm = normalized(ab[x], sab[x], N);
+          const bool on = act && valid[x];
+          if (on) {
+            a_den += gm;
+            b_den += gm;
+            if (T[x] - 2 - r == 0) pi_acc += gm;
+          }
+#ifndef CVF_ABL_NOATOMIC
+          unsafeAtomicAdd(on ? &g.b_num[(size_t)po[x][k] * N + i] : dump, on ? gm : 0.0);
+#else
+          b_den += on ? gm * (double)po[x][k] : 0.0;
+#endif
+        }
       }
     }
-    int q = 0;  // staged steps
-    for (int t = T - 2; t >= 0; --t) {
-      const double e1 = e_t;
-      e_t = e_nx;
-      alt = a_nx;
-      o_t = o_nx;
-      tg = tg_nx;
-      if (t >= 1) {  // prefetch step t-1
-        if (t - 1 < blk.base) blk.advance(obs, tag, -64, T, i);
-        o_nx = blk.obs_at(t - 1);
-        tg_nx = blk.tag_at(t - 1);
-        e_nx = act ? g.et[(size_t)o_nx * N + i] : 0.0;
-        a_nx = act ? al[(size_t)(t - 1) * N + i] : 0.0;
-      }
-      // u_{t+1} = b(o_{t+1}) o beta_{t+1};  w_i = sum_j A[i][j] u_j  (hmm.rs:113-116, 135-141)
-      double* u = uu[w][q];
-      if (i < NP) u[i] = e1 * beta;
-      __builtin_amdgcn_wave_barrier();
-      const double wv = dot_lds_fma<NP>(u, arow);
-      double c = alt * wv, sw = wv;
-      wave_sum2(c, sw);
-      z += c == 0.0 ? 1.0 : 0.0;  // xi_t uniform (hmm.rs:306-317), counted separately
-      if (i < NP) rr[w][q][i] = c != 0.0 ? alt / c : 0.0;
-      if (++q == 4) {
-        mfma_update();
-        q = 0;
-      }
-      beta = tg >= 0 ? (i == tg ? 1.0 : 0.0) : (act ? normalized(wv, sw, N) : 0.0);
-      const double ab = alt * beta;
-      const double gm = normalized(ab, wave_sum(ab), N);  // hmm.rs:127-129
-      if (act) {
-        a_den += gm;
-        b_den += gm;
-        if (t == 0) pi_acc += gm;
-        unsafeAtomicAdd(&g.b_num[(size_t)o_t * N + i], gm);
-      }
-    }
-    if (q != 0) {  // flush a partial group: zero the unused staged steps
-      if (i < NP)
-        for (int k = q; k < 4; ++k) uu[w][k][i] = rr[w][k][i] = 0.0;
+    if ((L - 1) & 1) {  // flush the odd last step: zero the rows of the missing one
+      if (i < NP) uu[w][2][i] = uu[w][3][i] = rr[w][2][i] = rr[w][3][i] = 0.0;
       mfma_update();
     }
   }
@@ -537,7 +648,7 @@ hipError_t launch_bw_estep(const BwArgs& g, int64_t nseq, int64_t max_waves, hip
   if (nseq <= 0) return hipSuccess;
   if (g.nstates > kBwMaxStates) return hipErrorInvalidValue;
   if (g.nstates <= kBwWaveStates) {
-    const int64_t nwaves = std::max<int64_t>(1, std::min<int64_t>(nseq, max_waves));
+    const int64_t nwaves = std::max<int64_t>(1, std::min<int64_t>((nseq + 1) / 2, max_waves));  // pairs
     if (g.nstates <= 16) launch_wave_estep<16>(g, nseq, nwaves, stream);
     else if (g.nstates <= 32) launch_wave_estep<32>(g, nseq, nwaves, stream);
     else if (g.nstates <= 48) launch_wave_estep<48>(g, nseq, nwaves, stream);

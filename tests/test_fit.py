@@ -109,7 +109,7 @@ def test_gpu_mle_matches_oracle(gpu, n, v):
 def test_gpu_train_matches_oracle(gpu, n, v, frac, tmax):
     import cviterbi as cv
 
-    off, obs, tags = _corpus(n, v, 24, tmax, frac, seed=100 + n)
+    off, obs, tags = _corpus(n, v, 27, tmax, frac, seed=100 + n)  # 27: a partly filled last block
     pi0, a0, b0 = _probs(n, v, seed=100 + n)
     iters = 3
     gp, ga, gb, it = cv.fit_train(pi0, a0, b0, off, obs, tags, max_iter=iters, tol=0.0)
