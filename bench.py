@@ -73,7 +73,7 @@ def cpu_baseline(pi, a, b, obs_rank, budget_s):
     km, dtm = sample(nth, budget_s / 2)
     return {"value": cells / dt, "unit": "trellis cells/s", "cores": 1, "kind": "port",
             "sample": f"first {k} sequences of config 4 (N=256, T=512), f64 CP association "
-                      f"(cp.rs:95-125), oracle/cv_oracle.c single thread, {dt:.1f} s",
+                      f"(cp.rs:63-93), oracle/cv_oracle.c single thread, {dt:.1f} s",
             "seconds": dt,
             "all_cores": {"value": km * T_LEN * N_STATES / dtm, "cores": nth, "sequences": km, "seconds": dtm,
                           "cpu": _cpu_model()}}

@@ -2,7 +2,7 @@
 //
 // Host side of the drop-in boundary: the HMM handle mirrors struct HMM<D> and its
 // log-prob lookups (src/hmm/hmm.rs:10-18, 407-445), the batch decode replaces the
-// dense forward + backtrack of viterbi_solver (cp.rs:95-125, viterbi.rs:5-32,
+// dense forward + backtrack of viterbi_solver (cp.rs:63-93, viterbi.rs:5-32,
 // dp.rs:94-209), and cv_solver_* mirrors `trait Solver` (viterbi_solver.rs:11-16).
 //
 // There is deliberately no CPU decode path here: every decode runs the HIP kernels
@@ -1515,7 +1515,7 @@ CV_API cv_status cv_solver_solve(cv_solver* s) {
     obj += s->scores[k];
   }
   s->objective = obj;
-  s->explored = 0;  // CPSolver explores no B&B node without constraints (cp.rs:169-174)
+  s->explored = 0;  // CPSolver explores no B&B node without constraints (cp.rs:137-142)
   return CV_OK;
 }
 

@@ -5,7 +5,7 @@
 //    "b": {"v":1,"dim":[N],"data":[{"v":1,"dim":[d0,...],"data":[...]}, ...]},
 //    "pi":{"v":1,"dim":[N],"data":[...]}}
 // serde_json writes non-finite floats as `null`; the reference maps null back to -inf
-// (parse_transmat / parse_bmat / parse_pi, hmm.rs:448-464).  Only -inf occurs in a
+// (parse_transmat / parse_bmat / parse_pi, hmm.rs:248-264).  Only -inf occurs in a
 // log10 model; NaN/+inf are rejected by cv_hmm_create.
 #include "hmm_json.hpp"
 
@@ -198,7 +198,7 @@ struct Parser {
 
 void put_num(std::ostream& os, double v) {
   if (!std::isfinite(v)) {
-    os << "null";  // serde_json: non-finite -> null (read back as -inf, hmm.rs:448-464)
+    os << "null";  // serde_json: non-finite -> null (read back as -inf, hmm.rs:248-264)
     return;
   }
   char buf[40];

@@ -1,11 +1,11 @@
 // trellis.hip -- MI355X (gfx950) Viterbi trellis kernels.
 //
 // Hot path of the reference's viterbi_solver forward pass:
-//   d0[j] = pi[j] + b[j,o0]                            (hmm/hmm.rs:415-418, cp.rs:98-100)
-//   s_i   = d[i] + a[i,j];  m = max_i s_i                (viterbi.rs:13-16, cp.rs:103-106)
+//   d0[j] = pi[j] + b[j,o0]                            (hmm/hmm.rs:215-218, cp.rs:66-68)
+//   s_i   = d[i] + a[i,j];  m = max_i s_i                (viterbi.rs:13-16, cp.rs:71-74)
 //   psi   = first i with s_i == m                       (ndarray-stats argmax)
 //   d'[j] = m + b[j,o]                                  (viterbi.rs:17)
-// followed by the backtrack of cp.rs:117-125 / viterbi.rs:24-31.
+// followed by the backtrack of cp.rs:85-93 / viterbi.rs:24-31.
 //
 // Kernels
 //   trellis_fwd_f32<NP>   one sequence per workgroup (NP/16 waves).  A is REGISTER
@@ -26,7 +26,7 @@
 //                         t = T-1..1 recompute s_i = delta_{t-1}[i] + a[i, path[t]] and
 //                         take the first argmax; optional f64 re-score along the path.
 //   generic_fwd<REAL>     any N, f32 or f64, every association mode of the reference
-//                         (VITERBI row A0, CP cp.rs:102-110, DP dp.rs:127-177, DECODE
+//                         (VITERBI row A0, CP cp.rs:70-78, DP dp.rs:127-177, DECODE
 //                         viterbi.rs:5-32) with inline first-argmax; writes u16 psi.
 //   generic_backtrack<REAL>
 #include <hip/hip_runtime.h>
@@ -229,7 +229,7 @@ __global__ __launch_bounds__(NP * 4) void trellis_fwd_f32(TrellisFwdArgs args) {
   auto force = [&](float d, int f) -> float { return (EXT && f >= 0 && jw != f) ? ninf_f() : d; };
 
   const int lds_w = (j0 / R) * S + (j0 % R) + (hi ? 1 : 0);
-  // ---- t = 0: d0 = pi + b[:,o0]  (hmm.rs:415-418, cp.rs:98-100) ----
+  // ---- t = 0: d0 = pi + b[:,o0]  (hmm.rs:215-218, cp.rs:66-68) ----
   {
     const float e = et_row(obs_s(0));
     float d0 = pi[jw] + e;
@@ -604,7 +604,7 @@ __global__ __launch_bounds__(NP * 2) void trellis_mfma_f32(TrellisFwdArgs args) 
 
   {
     const float e = et_row(obs_s(0));
-    float d0 = args.pi[j] + e;  // hmm.rs:415-418
+    float d0 = args.pi[j] + e;  // hmm.rs:215-218
     const int f0 = frc_s(0);
     if (EXT && f0 >= 0 && j != f0) d0 = ninf_f();
     if (lane < 32) {
@@ -814,7 +814,7 @@ __global__ __launch_bounds__(256) void backtrack_f32(BacktrackArgs args) {
 #pragma unroll
     for (int k = 0; k < KP; ++k) dst[k] = (r >= 0 && valid[k]) ? drow[(size_t)r * NP + lane + 64 * k] : ninf_f();
   };
-  // first argmax of the last row (cp.rs:117-118)
+  // first argmax of the last row (cp.rs:86)
   int cur;
   float bv;
   {
@@ -940,7 +940,7 @@ __device__ __forceinline__ void backtrack_one(const BacktrackArgs& args, int64_t
     for (int k = 1; k < VL; ++k) m = fmaxf(m, v[k]);
     return m;
   };
-  // first argmax of the last row (cp.rs:117-118)
+  // first argmax of the last row (cp.rs:86)
   int cur;
   float bv;
   {
@@ -1118,7 +1118,7 @@ __global__ __launch_bounds__(256) void trellis_wave64_f32(TrellisFwdArgs args, B
     lds[t & 1][wofs] = dn;
     drow[(size_t)t * NP + jw] = dn;
   }
-  // ---- backtrack (cp.rs:117-125) of this wave's own sequence: the delta rows were stored
+  // ---- backtrack (cp.rs:85-93) of this wave's own sequence: the delta rows were stored
   // by other lanes of this wave -- make them visible (release to L2, then acquire) ----
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
@@ -1140,7 +1140,7 @@ __global__ __launch_bounds__(64) void rescore_f64_lanes(RescoreArgs r) {
   const int32_t* __restrict__ obs = r.obs + e0;
   const int N = r.nstates;
   int pp = path[0];
-  double d = r.pi64[pp] + r.et64[(size_t)obs[0] * N + pp];  // init_prob: pi + b (hmm.rs:415-418)
+  double d = r.pi64[pp] + r.et64[(size_t)obs[0] * N + pp];  // init_prob: pi + b (hmm.rs:215-218)
   int t = 1;
   constexpr int U = 8;
   for (; t + U <= T; t += U) {

@@ -1,7 +1,7 @@
 """Batch Viterbi decode on MI355X (cv_decode_batch / cv_decode_batch_device).
 
 Replaces, per sequence, the dense forward + backtrack of the reference's solvers:
-CPSolver::init_viterbi + backtrack (viterbi_solver/cp.rs:95-125), viterbi::decode
+CPSolver::init_viterbi + backtrack (viterbi_solver/cp.rs:63-93), viterbi::decode
 (viterbi.rs:5-32) and DPSolver::solve (dp.rs:94-209); see include/cviterbi.h.
 """
 from __future__ import annotations

@@ -39,7 +39,7 @@ class HMM:
 
     @classmethod
     def from_json(cls, path, device=0):
-        """HMM::from_json (hmm.rs:442-445): the reference's serde layout, null = -inf."""
+        """HMM::from_json (hmm.rs:242-245): the reference's serde layout, null = -inf."""
         self = cls.__new__(cls)
         h = ctypes.c_void_p()
         L.check(L.lib().cv_hmm_from_json(str(path).encode(), int(device), ctypes.byref(h)))
@@ -48,7 +48,7 @@ class HMM:
         return self
 
     def write(self, path):
-        """HMM::write (hmm.rs:436-440)."""
+        """HMM::write (hmm.rs:236-240)."""
         L.check(L.lib().cv_hmm_write_json(self._h, str(path).encode()))
 
     def __del__(self):
@@ -66,7 +66,7 @@ class HMM:
 
     # ---- shape -----------------------------------------------------------------------
     def nstates(self) -> int:
-        """HMM::nstates (hmm.rs:407-409)."""
+        """HMM::nstates (hmm.rs:207-209)."""
         return L.lib().cv_hmm_nstates(self._h)
 
     def nobs(self) -> int:
@@ -87,7 +87,7 @@ class HMM:
         L.check(L.lib().cv_obs_flatten(self._h, _p(v), ctypes.byref(out)))
         return out.value
 
-    # ---- lookups (hmm.rs:411-434) -------------------------------------------------------
+    # ---- lookups (hmm.rs:211-234) -------------------------------------------------------
     def init_prob(self, state, obs) -> float:
         return L.lib().cv_hmm_init_prob(self._h, int(state), self.flat(obs))
 

@@ -7,7 +7,7 @@ corpora need the network), so these are synthetic by design:
   config 4  N=256, V=1,024 (bdims [32,32]), T=512, B=65,536, seed 20261015
   config 5  config 4 + one constrained position in half the sequences, K=7 components
 Rows of A, B and pi are Dirichlet(alpha) samples turned into log10 probabilities
-with exact zeros mapped to -inf (reference hmm/hmm.rs:392-405 `log`).
+with exact zeros mapped to -inf (reference hmm/hmm.rs:192-205 `log`).
 """
 from __future__ import annotations
 
@@ -15,7 +15,7 @@ import numpy as np
 
 
 def log10_probs(p: np.ndarray) -> np.ndarray:
-    """hmm.rs:392-405: x == 0 -> -inf else log10(x)."""
+    """hmm.rs:192-205: x == 0 -> -inf else log10(x)."""
     out = np.full(p.shape, -np.inf)
     nz = p != 0
     out[nz] = np.log10(p[nz])

@@ -8,14 +8,14 @@
  * sizes only; no torch or HIP types in the signatures (streams are opaque void*).
  *
  * Conventions
- *  - Probabilities are log10 doubles, -inf for zero (src/hmm/hmm.rs:392-405); JSON
- *    `null` reads as -inf (hmm.rs:448-464).
- *  - a[from*N + to] (hmm.rs:420-426), b[state*V + obs] with obs flattened row-major
- *    over bdims exactly as ndarray indexes `b[state][&obs[..]]` (hmm.rs:428-430).
+ *  - Probabilities are log10 doubles, -inf for zero (src/hmm/hmm.rs:192-205); JSON
+ *    `null` reads as -inf (hmm.rs:248-264).
+ *  - a[from*N + to] (hmm.rs:220-226), b[state*V + obs] with obs flattened row-major
+ *    over bdims exactly as ndarray indexes `b[state][&obs[..]]` (hmm.rs:228-230).
  *  - Sequences are CSR: offsets[nseq+1] (int64, element offsets), obs[offsets[nseq]]
  *    (int32 flattened observation indices).  Paths are int32 per element.
  *  - Functions return cv_status; cv_last_error() has a message for the calling thread.
- *    Nothing aborts (the reference panics: cp.rs:119, dp.rs:184-186, unwraps).
+ *    Nothing aborts (the reference panics: cp.rs:87, dp.rs:184-186, unwraps).
  */
 #ifndef CVITERBI_H
 #define CVITERBI_H
@@ -50,8 +50,8 @@ enum { CV_SEQ_OK = 0, CV_SEQ_INFEASIBLE = 1, CV_SEQ_EMPTY = 2, CV_SEQ_BADOBS = 3
 enum { CV_DTYPE_F32 = 0, CV_DTYPE_F64 = 1 };
 
 /* association of the recurrence:
- *  VITERBI  d' = max_i(d[i] + a[i,j]) + b[j,o]      viterbi.rs:13-18 order, pi init cp.rs:98-100
- *  CP       d' = d[psi] + (a[psi,j] + b[j,o])       CPSolver::init_viterbi cp.rs:95-115
+ *  VITERBI  d' = max_i(d[i] + a[i,j]) + b[j,o]      viterbi.rs:13-18 order, pi init cp.rs:66-68
+ *  CP       d' = d[psi] + (a[psi,j] + b[j,o])       CPSolver::init_viterbi cp.rs:63-83
  *  DP       d' = max_i((a[i,j] + b[j,o]) + d[i])    DPSolver::solve dp.rs:127-182 (first index)
  *  DECODE   VITERBI with row 0 = 0.0                viterbi::decode viterbi.rs:5-32 */
 enum { CV_ASSOC_VITERBI = 0, CV_ASSOC_CP = 1, CV_ASSOC_DP = 2, CV_ASSOC_DECODE = 3 };
@@ -113,7 +113,7 @@ typedef struct cv_timing {
 } cv_timing;
 
 typedef struct cv_superseq_desc {
-  /* The super-sequence of viterbi_solver/utils.rs:265-274 in element order: sequences
+  /* The super-sequence of viterbi_solver/utils.rs:49-58 in element order: sequences
    * concatenated (after reordering), each element carrying MetaElements fields. */
   int64_t nseq;
   const int64_t* offsets;    /* [nseq+1] */
@@ -133,35 +133,35 @@ CV_API void cv_opts_init(cv_opts* opts);
 /* ---- hmm::HMM (src/hmm/hmm.rs) ------------------------------------------------------- */
 /* HMM struct construction (hmm.rs:10-18). */
 CV_API cv_status cv_hmm_create(const cv_hmm_desc* desc, cv_hmm** out);
-/* HMM::from_json (hmm.rs:442-445 + null->-inf parsers 448-464). */
+/* HMM::from_json (hmm.rs:242-245 + null->-inf parsers 448-464). */
 CV_API cv_status cv_hmm_from_json(const char* path, int32_t device, cv_hmm** out);
-/* HMM::write (hmm.rs:436-440): serde_json layout, -inf written as null. */
+/* HMM::write (hmm.rs:236-240): serde_json layout, -inf written as null. */
 CV_API cv_status cv_hmm_write_json(const cv_hmm* h, const char* path);
 CV_API void cv_hmm_destroy(cv_hmm* h);
-/* HMM::nstates (hmm.rs:407-409). */
+/* HMM::nstates (hmm.rs:207-209). */
 CV_API int32_t cv_hmm_nstates(const cv_hmm* h);
 CV_API int64_t cv_hmm_nobs(const cv_hmm* h);                   /* V = prod(bdims) */
 CV_API int32_t cv_hmm_ndims(const cv_hmm* h);
 CV_API cv_status cv_hmm_bdims(const cv_hmm* h, int64_t* bdims_out /*[D]*/);
 /* flatten one D-dim observation value ([usize; D]) to the index used everywhere else. */
 CV_API cv_status cv_obs_flatten(const cv_hmm* h, const int64_t* value /*[D]*/, int64_t* flat_out);
-/* HMM::init_prob (hmm.rs:411-413) */
+/* HMM::init_prob (hmm.rs:211-213) */
 CV_API double cv_hmm_init_prob(const cv_hmm* h, int32_t state, int64_t obs);
-/* HMM::init_probs (hmm.rs:415-418) -> out[N] */
+/* HMM::init_probs (hmm.rs:215-218) -> out[N] */
 CV_API cv_status cv_hmm_init_probs(const cv_hmm* h, int64_t obs, double* out);
-/* HMM::transition_prob (hmm.rs:420-422) */
+/* HMM::transition_prob (hmm.rs:220-222) */
 CV_API double cv_hmm_transition_prob(const cv_hmm* h, int32_t from, int32_t to, int64_t obs);
-/* HMM::transitions_to (hmm.rs:424-426) -> out[N] = a[:, to] */
+/* HMM::transitions_to (hmm.rs:224-226) -> out[N] = a[:, to] */
 CV_API cv_status cv_hmm_transitions_to(const cv_hmm* h, int32_t to, double* out);
-/* HMM::emit_prob (hmm.rs:428-430) */
+/* HMM::emit_prob (hmm.rs:228-230) */
 CV_API double cv_hmm_emit_prob(const cv_hmm* h, int32_t state, int64_t obs);
-/* HMM::emit_probs (hmm.rs:432-434) -> out[N] */
+/* HMM::emit_probs (hmm.rs:232-234) -> out[N] */
 CV_API cv_status cv_hmm_emit_probs(const cv_hmm* h, int64_t obs, double* out);
 
 /* ---- batch decode: the trellis forward pass + backtrack -------------------------------
- * Replaces, per sequence, the dense forward of CPSolver::init_viterbi (cp.rs:95-115) /
+ * Replaces, per sequence, the dense forward of CPSolver::init_viterbi (cp.rs:63-83) /
  * viterbi::decode (viterbi.rs:9-23) / DPSolver::solve (dp.rs:127-182) plus the backtrack
- * (cp.rs:117-125, viterbi.rs:24-31, dp.rs:71-89).  Host pointers; synchronous. */
+ * (cp.rs:85-93, viterbi.rs:24-31, dp.rs:71-89).  Host pointers; synchronous. */
 CV_API cv_status cv_decode_batch(cv_hmm* h, int64_t nseq, const int64_t* offsets, const int32_t* obs,
                                  const cv_opts* opts, int32_t* path_out, double* score_out,
                                  uint8_t* status_out);

@@ -36,7 +36,7 @@
     REAL* cur = (REAL*)malloc(sizeof(REAL) * (size_t)N);                                        \
     int32_t* bt = (int32_t*)calloc((size_t)T * (size_t)N, sizeof(int32_t));                    \
     const REAL ninf = NEG_INF;                                                                  \
-    /* row 0: pi + b[:,o0] (hmm.rs:415-418, cp.rs:98-100); decode(): 0.0 (viterbi.rs:6,9) */    \
+    /* row 0: pi + b[:,o0] (hmm.rs:215-218, cp.rs:66-68); decode(): 0.0 (viterbi.rs:6,9) */    \
     {                                                                                           \
       const int64_t o = obs[0];                                                                 \
       for (int j = 0; j < N; ++j) {                                                             \
@@ -95,7 +95,7 @@
           }                                                                                     \
         }                                                                                       \
         bt_t[j] = arg;                                                                          \
-        if (assoc == CVO_ASSOC_CP) /* cp.rs:107-108: prev[psi] + (a[psi,j] + b[j,o]) */         \
+        if (assoc == CVO_ASSOC_CP) /* cp.rs:75-76: prev[psi] + (a[psi,j] + b[j,o]) */         \
           cur[j] = prev[arg] + (a[(int64_t)arg * N + j] + e);                                   \
         else /* viterbi.rs:15-17: (prev + a) + b */                                             \
           cur[j] = m + e;                                                                       \
@@ -107,7 +107,7 @@
       prev = cur;                                                                               \
       cur = tmp;                                                                                \
     }                                                                                           \
-    /* final: first argmax of last row (cp.rs:117-125; viterbi.rs:24) */                        \
+    /* final: first argmax of last row (cp.rs:85-93; viterbi.rs:24) */                        \
     int end = 0;                                                                                \
     REAL best = prev[0];                                                                        \
     for (int j = 1; j < N; ++j)                                                                 \
@@ -117,7 +117,7 @@
       }                                                                                         \
     int status = CVO_SEQ_OK;                                                                    \
     if (!(best > ninf)) {                                                                       \
-      /* infeasible: reference panics (cp.rs:119, dp.rs:184-186); we report it */              \
+      /* infeasible: reference panics (cp.rs:87, dp.rs:184-186); we report it */              \
       status = CVO_SEQ_INFEASIBLE;                                                              \
       for (int t = 0; t < T; ++t) path[t] = 0;                                                  \
       *score = ninf;                                                                            \
@@ -211,19 +211,19 @@ double cvo_cp_superseq_f64(int N, int V, const double* pi, const double* a, cons
   if (L <= 0) return 0.0;
   double* arr = (double*)malloc(sizeof(double) * (size_t)L * (size_t)N);
   int32_t* bt = (int32_t*)calloc((size_t)L * (size_t)N, sizeof(int32_t));
-  /* per-element "t == 0" flag: first element of each sequence (utils.rs:240-254) */
+  /* per-element "t == 0" flag: first element of each sequence (utils.rs:24-38) */
   unsigned char* first = (unsigned char*)calloc((size_t)L, 1);
   for (int64_t s = 0; s < nseq; ++s)
     if (offsets[s + 1] > offsets[s]) first[offsets[s] - offsets[0]] = 1;
   const int32_t* ob = obs + offsets[0];
-  /* element 0: init_probs (cp.rs:98-100) */
+  /* element 0: init_probs (cp.rs:66-68) */
   for (int j = 0; j < N; ++j) arr[j] = pi[j] + b[(int64_t)j * V + ob[0]];
   for (int64_t t = 1; t < L; ++t) {
     const double* prevr = arr + (t - 1) * N;
     double* row = arr + t * N;
     const int64_t o = ob[t];
     for (int j = 0; j < N; ++j) {
-      /* transitions(): constant pi[j] vector at t==0, else column a[:,j] (utils.rs:248-254) */
+      /* transitions(): constant pi[j] vector at t==0, else column a[:,j] (utils.rs:32-38) */
       double m, s;
       int arg = 0;
       if (first[t]) {
@@ -232,7 +232,7 @@ double cvo_cp_superseq_f64(int N, int V, const double* pi, const double* a, cons
           s = prevr[i] + pi[j];
           if (s > m) { m = s; arg = i; }
         }
-        /* arc_p at t==0 = init_prob (utils.rs:240-243, hmm.rs:411-413) */
+        /* arc_p at t==0 = init_prob (utils.rs:24-27, hmm.rs:211-213) */
         row[j] = prevr[arg] + (pi[j] + b[(int64_t)j * V + o]);
       } else {
         m = prevr[0] + a[j];

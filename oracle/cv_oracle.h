@@ -21,10 +21,10 @@
  * Association / semantics modes:
  *   CVO_ASSOC_VITERBI  row A0: d0 = pi + b[:,o0]; s_i = d[i] + a[i,j];
  *                      psi = first argmax s; d'[j] = max(s) + b[j,o]
- *                      (viterbi.rs:13-18 order, cp.rs:98-100 init)
- *   CVO_ASSOC_CP       CPSolver::init_viterbi (cp.rs:95-115):
+ *                      (viterbi.rs:13-18 order, cp.rs:66-68 init)
+ *   CVO_ASSOC_CP       CPSolver::init_viterbi (cp.rs:63-83):
  *                      psi = first argmax(d + a[:,j]); d'[j] = d[psi] + (a[psi,j] + b[j,o])
- *                      (arc_p utils.rs:240-246 -> transition_prob hmm.rs:420-422)
+ *                      (arc_p utils.rs:24-30 -> transition_prob hmm.rs:220-222)
  *   CVO_ASSOC_DP       DPSolver unconstrained branch (dp.rs:127-182): candidates
  *                      c_i = (a[i,j] + b[j,o]) + d[i] over finite d[i], finite arc;
  *                      keep strictly greater -> first index in ascending i (the
@@ -32,7 +32,7 @@
  *                      deterministic choice).
  *   CVO_ASSOC_DECODE   viterbi::decode (viterbi.rs:5-32): row 0 = 0.0 (no pi, no
  *                      first emission), otherwise as VITERBI.
- * Final state = first argmax of the last row (cp.rs:117-125, viterbi.rs:24);
+ * Final state = first argmax of the last row (cp.rs:85-93, viterbi.rs:24);
  * score = max of the last row.
  */
 #ifndef CV_ORACLE_H
@@ -80,7 +80,7 @@ int cvo_decode_batch_f32(int N, int V, const float* pi, const float* a, const fl
 double cvo_rescore_f64(int N, int V, const double* pi, const double* a, const double* b, int T,
                        const int32_t* obs, const int32_t* path);
 
-/* CPSolver over a whole super-sequence (cp.rs:95-115 + utils.rs:240-254):
+/* CPSolver over a whole super-sequence (cp.rs:63-83 + utils.rs:24-38):
  * sequences concatenated, t==0 elements use the constant pi[to] transition
  * vector.  Unconstrained only.  Returns objective; path[total] in element order. */
 double cvo_cp_superseq_f64(int N, int V, const double* pi, const double* a, const double* b,

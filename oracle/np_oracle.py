@@ -10,11 +10,11 @@ cannot be built or run here, with no tests or fixtures of its own; SURVEY.md §4
 known answers (tests/test_oracle_kat.py).
 
 Semantics follow SURVEY.md §8a (file:line into /root/reference/src):
-  VITERBI (row A0)  d0 = pi + b[:,o0] (hmm/hmm.rs:415-418, viterbi_solver/cp.rs:98-100);
+  VITERBI (row A0)  d0 = pi + b[:,o0] (hmm/hmm.rs:215-218, viterbi_solver/cp.rs:66-68);
                     s = d[:,None] + a; psi = first argmax; d' = max(s) + b[:,o]
                     (viterbi_solver/viterbi.rs:13-18).
   CP                psi as above; d'[j] = d[psi] + (a[psi,j] + b[j,o])
-                    (cp.rs:102-110 via utils.rs:240-246 -> hmm.rs:420-422).
+                    (cp.rs:70-78 via utils.rs:24-30 -> hmm.rs:220-222).
   DP                c = (a + b[None,:,o]) + d[:,None] over finite entries; first max
                     (dp.rs:127-177, ascending-index iteration instead of HashMap order).
   DECODE            viterbi.rs:5-32: row 0 = 0.0, -inf emission -> -inf, bt 0.

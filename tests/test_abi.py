@@ -60,15 +60,15 @@ def test_lookups_match_hmm_rs():
     assert h.nstates() == 6 and h.nobs() == 12 and h.bdims() == (3, 4)
     for s in range(6):
         for o in range(12):
-            assert h.emit_prob(s, o) == b[s, o]                                   # hmm.rs:428-430
-            assert h.init_prob(s, o) == pi[s] + b[s, o]                           # hmm.rs:411-413
+            assert h.emit_prob(s, o) == b[s, o]                                   # hmm.rs:228-230
+            assert h.init_prob(s, o) == pi[s] + b[s, o]                           # hmm.rs:211-213
             for f in range(6):
-                assert h.transition_prob(f, s, o) == a[f, s] + b[s, o]            # hmm.rs:420-422
+                assert h.transition_prob(f, s, o) == a[f, s] + b[s, o]            # hmm.rs:220-222
     for o in range(12):
-        np.testing.assert_array_equal(h.init_probs(o), pi + b[:, o])             # hmm.rs:415-418
-        np.testing.assert_array_equal(h.emit_probs(o), b[:, o])                  # hmm.rs:432-434
+        np.testing.assert_array_equal(h.init_probs(o), pi + b[:, o])             # hmm.rs:215-218
+        np.testing.assert_array_equal(h.emit_probs(o), b[:, o])                  # hmm.rs:232-234
     for t in range(6):
-        np.testing.assert_array_equal(h.transitions_to(t), a[:, t])              # hmm.rs:424-426
+        np.testing.assert_array_equal(h.transitions_to(t), a[:, t])              # hmm.rs:224-226
     # [usize; D] observations flatten row-major like ndarray's b[state][&obs[..]]
     assert h.flat((2, 3)) == 11 and h.flat((1, 0)) == 4
     assert h.emit_prob(2, h.flat((1, 2))) == b.reshape(6, 3, 4)[2, 1, 2]
