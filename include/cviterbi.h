@@ -251,8 +251,9 @@ CV_API void cv_solver_destroy(cv_solver* s);
 CV_API cv_status cv_hmm_fit_mle(int32_t nstates, int64_t nobs, int64_t nseq, const int64_t* offsets,
                                 const int32_t* obs, const int32_t* tags, int32_t device, double* pi, double* a,
                                 double* b);
-/* train (hmm.rs:69-190): tag-clamped Baum-Welch, E-step on the GPU (N <= 128), M-step and
- * the convergence test (sum |new - old| <= tol, checked after the update) on the host.
+/* train (hmm.rs:69-190): tag-clamped Baum-Welch, E- and M-step on the GPU (N <= 128) with
+ * the parameters resident between iterations; the convergence test (sum |new - old| <= tol,
+ * checked after the update, hmm.rs:172-177) adds per-block partial sums on the host.
  * *iters_out = iterations run. */
 CV_API cv_status cv_hmm_fit_train(int32_t nstates, int64_t nobs, int64_t nseq, const int64_t* offsets,
                                   const int32_t* obs, const int32_t* tags, int32_t max_iter, double tol,
