@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <charconv>
 #include <chrono>
 #include <cmath>
 #include <cstdarg>
@@ -26,6 +27,7 @@
 #include "../../include/cviterbi.h"
 #include "csp.hpp"
 #include "hmm_json.hpp"
+#include "kernels/cfn.h"
 #include "kernels/fit.h"
 #include "kernels/trellis.h"
 
@@ -1537,6 +1539,226 @@ CV_API cv_status cv_solver_get_explored_nodes(const cv_solver* s, uint64_t* n) {
   return CV_OK;
 }
 CV_API void cv_solver_destroy(cv_solver* s) { delete s; }
+
+}  // extern "C"
+
+namespace {
+
+// Rust's Display for f64 (what cfn.rs writes with format!("{}")): the shortest decimal that
+// reads back to the same double, in positional notation (never an exponent); inf / -inf / NaN.
+void append_rust_f64(std::string& out, double x) {
+  if (std::isnan(x)) {
+    out += "NaN";
+    return;
+  }
+  if (std::isinf(x)) {
+    out += x < 0 ? "-inf" : "inf";
+    return;
+  }
+  // shortest round-trip digits (scientific to_chars), then laid out positionally with zeros:
+  // Rust prints 2^60 as 1152921504606847000, not the exact 1152921504606846976
+  char buf[64];
+  const auto r = std::to_chars(buf, buf + sizeof(buf), x, std::chars_format::scientific);
+  const std::string sci(buf, r.ptr);
+  const size_t epos = sci.find('e');
+  std::string mant = sci.substr(0, epos);
+  const int exp10 = std::atoi(sci.c_str() + epos + 1);
+  const bool neg = mant[0] == '-';
+  if (neg) mant.erase(0, 1);
+  std::string digits;
+  for (char c : mant)
+    if (c != '.') digits += c;
+  // value = 0.d1d2...dn x 10^(exp10 + 1)
+  const int point = exp10 + 1;  // digits before the decimal point
+  std::string s;
+  if (point <= 0) {
+    s = "0." + std::string((size_t)(-point), '0') + digits;
+  } else if ((size_t)point >= digits.size()) {
+    s = digits + std::string((size_t)point - digits.size(), '0');
+  } else {
+    s = digits.substr(0, (size_t)point) + "." + digits.substr((size_t)point);
+  }
+  if (s.find('.') != std::string::npos) {  // "1.0" style trailing zeros never come from to_chars, but be safe
+    while (s.back() == '0') s.pop_back();
+    if (s.back() == '.') s.pop_back();
+  }
+  if (neg) out += '-';
+  out += s;
+}
+
+}  // namespace
+
+extern "C" {
+
+// write_cfn (viterbi_solver/cfn.rs:82-205) over the solver's super-sequence: constraint
+// boundaries where the active component changes, an N x N table per ordered component pair
+// of segment longest paths (accumulated over all boundaries between the two components, both
+// orientations), start/end unary costs, the lower bound, and the text file toulbar2 reads.
+// The segment rows run on the GPU (kernels/cfn.hip, bit-identical f64); the tables, bound and
+// formatting are the reference's host loops.
+CV_API cv_status cv_solver_write_cfn(cv_solver* s, const char* path, uint64_t* compile_ms) {
+  if (!s || !path) return set_err(CV_EINVAL, "null argument");
+  const auto t0 = std::chrono::steady_clock::now();
+  cv_hmm* h = s->hmm;
+  const int N = h->N;
+  const int64_t len = s->offsets.back();
+  if (len <= 0) return set_err(CV_EINVAL, "empty super-sequence");
+  // constraint boundaries (cfn.rs:88-110)
+  std::vector<std::pair<int64_t, int32_t>> bnd;
+  int32_t last = -1;
+  for (int64_t t = 0; t < len; ++t) {
+    const int32_t c = s->comp[(size_t)t];
+    if (c < 0) continue;
+    if (last < 0 || c != last) bnd.emplace_back(t, c);
+    last = c;
+  }
+  if (bnd.empty()) return set_err(CV_EINVAL, "no active constraint: cfn.rs:106 unwraps an empty boundary list");
+  // k = number of components with an active element (SuperSequence::number_constraints,
+  // utils.rs:200-202); the tables are indexed by component id (cfn.rs:115-118)
+  std::vector<uint8_t> seen((size_t)s->ncomp, 0);
+  int32_t k = 0;
+  for (int64_t t = 0; t < len; ++t)
+    if (s->comp[(size_t)t] >= 0 && !seen[(size_t)s->comp[(size_t)t]]) {
+      seen[(size_t)s->comp[(size_t)t]] = 1;
+      ++k;
+    }
+  if (s->ncomp > k)
+    return set_err(CV_EUNSUPPORTED, "component %d >= %d active components: cfn.rs:118 indexes out of bounds",
+                   s->ncomp - 1, k);
+  // jobs: every boundary pair x start state, the end cost per state, the start cost
+  std::vector<cvcfn::CfnJob> jobs;
+  const int64_t nb = (int64_t)bnd.size();
+  for (int64_t b = 0; b + 1 < nb; ++b)
+    for (int n1 = 0; n1 < N; ++n1) jobs.push_back({bnd[(size_t)b].first, bnd[(size_t)b + 1].first, n1, cvcfn::kCfnSegment});
+  const int64_t f_time = bnd.front().first, l_time = bnd.back().first;
+  const int32_t f_cid = bnd.front().second, l_cid = bnd.back().second;
+  const int64_t end_jobs = (int64_t)jobs.size();
+  if (l_time != len - 1)
+    for (int n = 0; n < N; ++n) jobs.push_back({l_time, len - 1, n, cvcfn::kCfnEnd});
+  const int64_t start_job = (int64_t)jobs.size();
+  jobs.push_back({0, f_time, 0, cvcfn::kCfnStart});
+  std::vector<double> rows(jobs.size() * (size_t)N);
+  {
+    std::lock_guard<std::mutex> lk(h->mu);
+    cv_status st = set_device(h);
+    if (st != CV_OK) return st;
+    if ((st = ensure_f64_tables(h)) != CV_OK) return st;
+    std::vector<uint8_t> first((size_t)len, 0);
+    for (int64_t q = 0; q < s->nseq; ++q)
+      if (s->offsets[(size_t)q] < len) first[(size_t)s->offsets[(size_t)q]] = 1;
+    DevBuf d_obs, d_comp, d_first, d_jobs, d_out;
+    if ((st = upload(d_obs, s->obs.data(), (size_t)len * 4)) != CV_OK) return st;
+    if ((st = upload(d_comp, s->comp.data(), (size_t)len * 4)) != CV_OK) return st;
+    if ((st = upload(d_first, first.data(), (size_t)len)) != CV_OK) return st;
+    // jobs in slices of <= 256 MiB of output rows
+    const int64_t per = std::max<int64_t>(1, (256ll << 20) / (8ll * N));
+    if ((st = d_out.ensure((size_t)std::min<int64_t>(per, (int64_t)jobs.size()) * N * 8)) != CV_OK) return st;
+    for (int64_t j0 = 0; j0 < (int64_t)jobs.size(); j0 += per) {
+      const int64_t nj = std::min<int64_t>(per, (int64_t)jobs.size() - j0);
+      if ((st = upload(d_jobs, jobs.data() + j0, (size_t)nj * sizeof(cvcfn::CfnJob))) != CV_OK) return st;
+      cvcfn::CfnArgs g{};
+      g.jobs = d_jobs.as<cvcfn::CfnJob>();
+      g.obs = d_obs.as<int32_t>();
+      g.comp = d_comp.as<int32_t>();
+      g.seq_start = d_first.as<uint8_t>();
+      g.a = h->d_a64.as<double>();
+      g.et = h->d_et64.as<double>();
+      g.pi = h->d_pi64.as<double>();
+      g.nstates = N;
+      g.out = d_out.as<double>();
+      const hipError_t e = cvcfn::launch_cfn_rows(g, nj, nullptr);
+      if (e != hipSuccess) return set_err(CV_EDEVICE, "cfn launch failed: %s", hipGetErrorString(e));
+      HIP_TRY(hipMemcpy(rows.data() + (size_t)j0 * N, d_out.p, (size_t)nj * N * 8, hipMemcpyDeviceToHost));
+    }
+  }
+  // cost tables (cfn.rs:117-140): [cid_from][cid_to][n1][n2], both orientations, -inf dropped
+  const size_t NN = (size_t)N * N;
+  std::vector<double> tab((size_t)k * k * NN, 0.0);
+  auto acc = [](double& x, double c) {
+    if (x == 0.0) x = c;
+    else x += c;
+  };
+  for (int64_t b = 0; b + 1 < nb; ++b) {
+    const int32_t cf = bnd[(size_t)b].second, ct = bnd[(size_t)b + 1].second;
+    double* tf = tab.data() + ((size_t)cf * k + ct) * NN;
+    double* tt = tab.data() + ((size_t)ct * k + cf) * NN;
+    for (int n1 = 0; n1 < N; ++n1) {
+      const double* row = rows.data() + ((size_t)b * N + n1) * N;
+      for (int n2 = 0; n2 < N; ++n2) {
+        // the row at t_to holds only n_to finite (the boundary element is constrained), so
+        // longest_path's final max is row[n2]
+        const double cost = row[n2];
+        if (cost == -INFINITY) continue;
+        acc(tf[(size_t)n1 * N + n2], cost);
+        acc(tt[(size_t)n2 * N + n1], cost);
+      }
+    }
+  }
+  // unary costs (cfn.rs:142-147)
+  std::vector<double> unary((size_t)k * N, 0.0);
+  for (int n = 0; n < N; ++n) unary[(size_t)f_cid * N + n] += rows[(size_t)start_job * N + n];
+  for (int n = 0; n < N; ++n) {
+    double e = 0.0;
+    if (l_time != len - 1) {
+      const double* row = rows.data() + ((size_t)end_jobs + n) * N;
+      e = -INFINITY;
+      for (int j = 0; j < N; ++j) e = row[j] > e ? row[j] : e;
+    }
+    unary[(size_t)l_cid * N + n] += e;
+  }
+  const uint64_t ms = (uint64_t)std::chrono::duration_cast<std::chrono::milliseconds>(
+                          std::chrono::steady_clock::now() - t0).count();
+  // lower bound (cfn.rs:151-158) and -inf unary entries (cfn.rs:160-166)
+  double lb = -1.0;
+  for (int32_t k1 = 0; k1 < k; ++k1)
+    for (int32_t k2 = k1 + 1; k2 < k; ++k2) {
+      const double* t = tab.data() + ((size_t)k1 * k + k2) * NN;
+      double m = t[0];
+      for (size_t q = 1; q < NN; ++q) m = t[q] < m ? t[q] : m;
+      lb += m;
+    }
+  for (auto& u : unary)
+    if (u == -INFINITY) u = lb;
+  // the file (cfn.rs:169-201)
+  std::string out;
+  out += "{\n\tproblem: { name: consistent_viterbi, mustbe: >";
+  append_rust_f64(out, lb);
+  out += "},\n\tvariables: {";
+  std::string dom = "[";
+  for (int i = 0; i < N; ++i) dom += "s" + std::to_string(i) + (i == N - 1 ? "]" : ",");
+  for (int32_t i = 0; i < k; ++i) out += "n" + std::to_string(i) + ": " + dom + (i != k - 1 ? "," : "},\n");
+  out += "\tfunctions: {\n";
+  auto vec_text = [&](const double* v, size_t n) {
+    out += "[";
+    for (size_t q = 0; q < n; ++q) {
+      append_rust_f64(out, v[q]);
+      out += q == n - 1 ? "] " : ", ";
+    }
+  };
+  for (int32_t i = 0; i < k; ++i) {
+    out += "\t\tf" + std::to_string(i) + ": { scope: [n" + std::to_string(i) + "], costs: ";
+    vec_text(unary.data() + (size_t)i * N, (size_t)N);
+    out += "}, \n";
+    for (int32_t j = i + 1; j < k; ++j) {
+      const double* t = tab.data() + ((size_t)i * k + j) * NN;
+      bool nonzero = false;
+      for (size_t q = 0; q < NN && !nonzero; ++q) nonzero = t[q] != 0.0;  // tcost.sum() != 0.0 (costs <= 0)
+      if (!nonzero) continue;
+      out += "\t\tf" + std::to_string(i) + "_" + std::to_string(j) + ": { scope: [n" + std::to_string(i) + ", n" +
+             std::to_string(j) + "], costs: ";
+      vec_text(t, NN);
+      out += "},\n";
+    }
+  }
+  out += "\t}\n}";
+  FILE* f = std::fopen(path, "wb");
+  if (!f) return set_err(CV_EIO, "cannot open %s for writing", path);
+  const size_t wr = std::fwrite(out.data(), 1, out.size(), f);
+  const int cl = std::fclose(f);
+  if (wr != out.size() || cl != 0) return set_err(CV_EIO, "short write to %s", path);
+  if (compile_ms) *compile_ms = ms;
+  return CV_OK;
+}
 
 }  // extern "C"
 

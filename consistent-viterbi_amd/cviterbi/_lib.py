@@ -39,7 +39,7 @@ EXPORTS = [
     "cv_constrained_pairs", "cv_constrained_partials", "cv_constrained_select", "cv_decode_forced_components", "cv_viterbi_decode",
     "cv_solver_create", "cv_solver_solve", "cv_solver_get_solution", "cv_solver_get_objective",
     "cv_solver_get_name", "cv_solver_get_explored_nodes", "cv_solver_destroy",
-    "cv_hmm_fit_mle", "cv_hmm_fit_train",
+    "cv_hmm_fit_mle", "cv_hmm_fit_train", "cv_solver_write_cfn",
 ]
 
 
@@ -127,6 +127,7 @@ def lib():
         "cv_solver_get_name": ([P], ctypes.c_char_p),
         "cv_solver_get_explored_nodes": ([P, P], S),
         "cv_solver_destroy": ([P], None),
+        "cv_solver_write_cfn": ([P, ctypes.c_char_p, P], S),
         "cv_hmm_fit_mle": ([I32, I64, I64, P, P, P, I32, P, P, P], S),
         "cv_hmm_fit_train": ([I32, I64, I64, P, P, P, I32, D, I32, P, P, P, P], S),
     }

@@ -277,6 +277,13 @@ class GpuSolver(Solver):
     def get_name(self) -> str:
         return L.lib().cv_solver_get_name(self._s).decode()
 
+    def write_cfn(self, path) -> int:
+        """write_cfn (cfn.rs:82-205) of this solver's super-sequence to `path`; returns the
+        table compilation time in ms (what main.rs:117 records)."""
+        ms = ctypes.c_uint64()
+        L.check(L.lib().cv_solver_write_cfn(self._s, str(path).encode(), ctypes.byref(ms)))
+        return ms.value
+
     def get_explored_nodes(self) -> int:
         v = ctypes.c_uint64()
         L.check(L.lib().cv_solver_get_explored_nodes(self._s, ctypes.byref(v)))

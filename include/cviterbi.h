@@ -239,6 +239,14 @@ CV_API cv_status cv_solver_get_objective(const cv_solver* s, double* obj);      
 CV_API const char* cv_solver_get_name(const cv_solver* s);                        /* get_name */
 CV_API cv_status cv_solver_get_explored_nodes(const cv_solver* s, uint64_t* n);   /* CPSolver::get_explored_nodes cp.rs:128 */
 CV_API void cv_solver_destroy(cv_solver* s);
+/* write_cfn (viterbi_solver/cfn.rs:82-205): the cost-function network of the solver's
+ * super-sequence for toulbar2 -- one variable per active component, unary start/end costs,
+ * N x N tables of segment longest paths between consecutive constraint boundaries (rows
+ * computed on the GPU in f64, bit-identical to the reference loops), the lower bound, in the
+ * reference's text layout and float formatting.  *compile_ms = table time (the value main.rs
+ * writes when run_cfn is set, main.rs:116-118).  Cost: (boundaries x N) segment passes of
+ * N^2 per element, as in the reference -- meant for the problem sizes toulbar2 takes. */
+CV_API cv_status cv_solver_write_cfn(cv_solver* s, const char* path, uint64_t* compile_ms);
 
 /* ---- HMM fitting (hmm.rs:30-190) ------------------------------------
  * pi[N], a[N*N] (from-major), b[N*V] (state-major, obs row-major over bdims): the CURRENT

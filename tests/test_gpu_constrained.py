@@ -173,3 +173,72 @@ def test_constrained_multi_position_sharded(gpu):
                                               pairs)
     got, _ = cv.constrained_select(h.nstates(), ncomp, part, pairs)
     assert np.array_equal(got, states)
+
+
+def _cli_input(tmp_path, seed=2, unknown=0.0):
+    rng = np.random.default_rng(seed)
+    seqs, tags, test_tags = [], [], []
+    for sid in range(8):
+        T = int(rng.integers(2, 9))
+        seqs += [f"{sid} {rng.integers(0, 4)} {rng.integers(0, 3)}" for _ in range(T)]
+        tags += [f"{sid} {-1 if rng.random() < unknown else rng.integers(0, 6)}" for _ in range(T)]
+        test_tags += [f"{sid} {rng.integers(0, 2) if t == 0 and sid % 2 == 0 else -1}" for t in range(T)]
+    (tmp_path / "sequences").write_text("\n".join(seqs) + "\n")
+    (tmp_path / "tags").write_text("\n".join(tags) + "\n")
+    (tmp_path / "test_tags").write_text("\n".join(test_tags) + "\n")
+    return len(seqs)
+
+
+@pytest.mark.parametrize("supervised", [True, False])
+def test_cli_train_then_decode(gpu, tmp_path, supervised):
+    """main.rs:89-98 with -t [-s]: the model is fitted on the GPU, written to INPUT/hmm.json,
+    and used for the decode; the written model equals a direct fit from the same start."""
+    from cviterbi import cli
+
+    # Baum-Welch on partly tagged data (a fully tagged corpus gives hard zero transitions,
+    # which can make the constrained decode infeasible)
+    n_el = _cli_input(tmp_path, unknown=0.0 if supervised else 0.5)
+    args = ["-i", str(tmp_path), "-o", str(tmp_path / "out"), "-n", "6", "-b", "4", "3", "-p", "1", "-t",
+            "--seed", "5"] + (["-s"] if supervised else [])
+    assert cli.main(args) == 0
+    lines = (tmp_path / "out" / "1_0").read_text().splitlines()
+    assert len(lines) == 2 + n_el
+    seqs = cv.load_sequences(tmp_path / "sequences", D=2)
+    tags = cv.load_tags(tmp_path / "tags")
+    pi0, a0, b0 = cli._random_start(6, (4, 3), np.random.default_rng(5))
+    off, obs, tg = cli._flatten(seqs, tags, (4, 3))
+    if supervised:
+        lp, la, lb = cv.fit_mle(pi0, a0, b0, off, obs, tg)
+    else:
+        lp, la, lb, _ = cv.fit_train(pi0, a0, b0, off, obs, tg, max_iter=1000, tol=0.001)
+    h = cv.HMM.from_json(tmp_path / "hmm.json")
+    # MLE is exact (integer counts); the Baum-Welch E-step sums with f64 atomics, so two runs
+    # may differ in the last bits
+    tol = 0 if supervised else 1e-12
+    for s in range(6):
+        assert h.init_prob(s, 0) == pytest.approx(lp[s] + lb[s, 0], rel=tol, abs=tol)
+        for o in range(12):
+            assert h.emit_prob(s, o) == pytest.approx(lb[s, o], rel=tol, abs=tol)
+
+
+def test_cli_cfn(gpu, tmp_path):
+    """main.rs:116-118 (run_cfn): OUTPUT/problem_{prop}_0.cfn and the compile time in {prop}_0;
+    the file equals the restatement of cfn.rs on the same super-sequence."""
+    import cfn_oracle as CO
+    from cviterbi import cli
+
+    pi, a, b = synth.random_hmm(6, 12, seed=2)
+    h = cv.HMM(pi, a, b.reshape(6, 4, 3))
+    h.write(tmp_path / "hmm.json")
+    _cli_input(tmp_path)
+    assert cli.main(["-i", str(tmp_path), "-o", str(tmp_path / "out"), "-n", "6", "-b", "4", "3", "-p", "1",
+                     "--cfn"]) == 0
+    assert int((tmp_path / "out" / "1_0").read_text().strip()) >= 0
+    seqs = cv.load_sequences(tmp_path / "sequences", D=2)
+    control = cv.load_tags(tmp_path / "test_tags")
+    ss = cv.SuperSequence(seqs, cv.Constraints.from_tags(control), h)
+    ss.recompute_constraints(1.0)
+    comp = np.where(ss.active == 1, ss.component, -1).tolist()
+    ref = CO.write_cfn_text(pi.tolist(), a.tolist(), b.tolist(), ss.value.tolist(), comp,
+                            (ss.t == 0).astype(int).tolist())
+    assert (tmp_path / "out" / "problem_1_0.cfn").read_text() == ref
