@@ -109,6 +109,9 @@ struct cv_hmm {
   // trellis kernel tables (f32, padded to NP)
   int np = 0;
   DevBuf t_aimg, t_aimg_mfma, t_pi, t_et, t_at, t_arm;  // t_arm: row-major A (one-wave kernel)
+  // one-wave kernel (N <= 64): tables padded to npw = 16 * ceil(N / 16) states
+  int npw = 0;
+  DevBuf w_arm, w_pi, w_et, w_at;
   DevBuf t_aimg_T, t_pi0;  // reversed (backward) pass: VALU image of a^T, pi = 0
   // f64 tables (generic f64 kernel + re-scoring): pi[N], a[N*N], et[V][N]
   bool f64_ready = false;
@@ -218,6 +221,20 @@ cv_status ensure_trellis_tables(cv_hmm* h) {
   if ((st = upload(h->t_at, at.data(), at.size() * 4)) != CV_OK) return st;
   if ((st = upload(h->t_arm, arm.data(), arm.size() * 4)) != CV_OK) return st;
   if ((st = upload(h->t_et, et.data(), et.size() * 4)) != CV_OK) return st;
+  h->npw = cvk::trellis_wave_states(N);
+  if (h->npw) {  // the one-wave kernel's tables: row-major A, A^T, pi, E^T at the npw stride
+    const int nw = h->npw;
+    std::vector<float> wpi(nw, NI), wat((size_t)nw * nw, NI), warm((size_t)nw * nw, NI), wet((size_t)V * nw, NI);
+    for (int j = 0; j < N; ++j) wpi[j] = f32(h->pi[j]);
+    for (int i = 0; i < N; ++i)
+      for (int j = 0; j < N; ++j) wat[(size_t)j * nw + i] = warm[(size_t)i * nw + j] = f32(h->a[(size_t)i * N + j]);
+    for (int j = 0; j < N; ++j)
+      for (int64_t o = 0; o < V; ++o) wet[(size_t)o * nw + j] = f32(h->b[(size_t)j * V + o]);
+    if ((st = upload(h->w_pi, wpi.data(), wpi.size() * 4)) != CV_OK) return st;
+    if ((st = upload(h->w_at, wat.data(), wat.size() * 4)) != CV_OK) return st;
+    if ((st = upload(h->w_arm, warm.data(), warm.size() * 4)) != CV_OK) return st;
+    if ((st = upload(h->w_et, wet.data(), wet.size() * 4)) != CV_OK) return st;
+  }
   h->np = np;
   return CV_OK;
 }
@@ -443,23 +460,24 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
   }
   h->last_launches = 0;
   h->last_kernel = use_trellis ? CV_KERNEL_TRELLIS : CV_KERNEL_GENERIC;
-  h->last_np = use_trellis ? h->np : 0;
+  // N <= 64: one wave per sequence, forward and backtrack fused (trellis_wave_f32) on tables
+  // padded to npw = 16 * ceil(N / 16); its chunks run back to back on one stream (nothing to
+  // overlap)
+  const bool wave = use_trellis && !use_mfma && h->npw > 0 && !(o.flags & CV_FLAG_NO_WAVE);
+  h->last_np = use_trellis ? (wave ? h->npw : h->np) : 0;
   h->last_mt = use_mfma ? mt : -1;
   if (nseq == 0) return CV_OK;
   HIP_TRY(hipMemsetAsync(status_dev, 0, (size_t)nseq, stream));
 
   // Per-element workspace bytes: trellis keeps f32 delta rows [NP]; generic keeps u16 psi [N].
   const uint64_t cap = o.workspace_bytes ? o.workspace_bytes : kDefaultWorkspace;
-  const uint64_t per_elem = use_trellis ? (uint64_t)h->np * 4 : (uint64_t)h->N * 2;
+  const uint64_t per_elem = use_trellis ? (uint64_t)(wave ? h->npw : h->np) * 4 : (uint64_t)h->N * 2;
   const int real_bytes = o.dtype == CV_DTYPE_F64 ? 8 : 4;
   const uint64_t total_elems = (uint64_t)(offsets_host[nseq] - offsets_host[0]);
   // Chunks (contiguous in the original order) are pipelined over two streams: the forward
   // pass of chunk k+1 runs while chunk k backtracks, out of a double-buffered workspace.
   // At least ~2,048 sequences per chunk (8 per CU), at most 8 chunks unless the
   // workspace cap forces more.
-  // N <= 64: one wave per sequence, forward and backtrack fused (trellis_wave64_f32); its
-  // chunks run back to back on one stream (nothing to overlap)
-  const bool wave = use_trellis && !use_mfma && h->np == 64 && !(o.flags & CV_FLAG_NO_WAVE);
   const bool serial = (o.flags & CV_FLAG_SERIAL) != 0 || wave;
   // Sequences per forward workgroup: 2 (trellis_fwd2_f32, equal-length pairs; default) or 1
   // (trellis_fwd_f32: leftovers, MFMA, N not a multiple of 64).
@@ -582,10 +600,13 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
       fa.nobs = (int)h->V;
       fa.forced = o.forced;
       if (wave) {
-        fa.a_img = h->t_arm.as<float>();
-        err = cvk::launch_trellis_wave64(fa, make_bt_args(h, wsb, offsets_host, offsets_dev, obs_dev, order_dev, c,
-                                                          path_dev, score_dev, status_dev),
-                                         n, stream);
+        fa.a_img = h->w_arm.as<float>();
+        fa.pi = h->w_pi.as<float>();
+        fa.et = h->w_et.as<float>();
+        cvk::BacktrackArgs ba =
+            make_bt_args(h, wsb, offsets_host, offsets_dev, obs_dev, order_dev, c, path_dev, score_dev, status_dev);
+        ba.at = h->w_at.as<float>();
+        err = cvk::launch_trellis_wave(h->npw, fa, ba, n, stream);
       } else if (use_mfma) {
         fa.a_img = h->t_aimg_mfma.as<float>();
         err = cvk::launch_trellis_mfma(h->np, mt, fa, n, stream);

@@ -130,10 +130,13 @@ hipError_t launch_trellis_fwd2(int np, const TrellisFwdArgs& fa, int64_t npairs,
 hipError_t launch_trellis_mfma(int np, int mt, const TrellisFwdArgs& fa, int64_t nseq, hipStream_t stream);
 int mfma_default_mt(int np);
 hipError_t launch_trellis_bt(int np, const BacktrackArgs& ba, int64_t nseq, hipStream_t stream, int lds_reserve = 0);
-// N <= 64 (NP = 64): one wave per sequence, forward + backtrack fused (trellis_wave64_f32).
-// fa.a_img = the ROW-MAJOR padded A table; fa.seq_begin .. ba.seq_end = the slots.
-hipError_t launch_trellis_wave64(const TrellisFwdArgs& fa, const BacktrackArgs& ba, int64_t nseq,
-                                 hipStream_t stream);
+// N <= 64: one wave per sequence, forward + backtrack fused (trellis_wave_f32), the tables
+// padded to npw = trellis_wave_states(N) (16, 32, 48 or 64; 0 = not covered).  fa.a_img = the
+// ROW-MAJOR padded A table, fa.pi / fa.et / ba.at and the delta rows use the npw stride;
+// fa.seq_begin .. ba.seq_end = the slots.
+int trellis_wave_states(int n);
+hipError_t launch_trellis_wave(int npw, const TrellisFwdArgs& fa, const BacktrackArgs& ba, int64_t nseq,
+                               hipStream_t stream);
 template <typename REAL>
 hipError_t launch_generic_fwd(const GenericFwdArgs<REAL>& fa, int64_t nseq, hipStream_t stream);
 template <typename REAL>

@@ -924,10 +924,12 @@ __device__ __forceinline__ void backtrack_one(const BacktrackArgs& args, int64_t
                                               const float* __restrict__ drow, const float* __restrict__ at,
                                               bool badobs) {
   constexpr int PF = 8;
+  // NP < 64 (one-wave kernels with 16/32/48 padded states): lanes >= NP hold no state
+  const bool own = NP >= 64 * VL || lane < NP;
   int32_t* __restrict__ path = args.path + e0;
   // padded states (>= N) hold -inf in delta and A^T, so they never win a feasible argmax
   auto load_row = [&](int r, float (&dst)[VL]) {
-    if (r >= 0) {
+    if (r >= 0 && own) {
       ld_vl<VL>(drow + (size_t)r * NP, dst);
     } else {
 #pragma unroll
@@ -971,7 +973,12 @@ __device__ __forceinline__ void backtrack_one(const BacktrackArgs& args, int64_t
       if (t >= 1) {
         // s_i = d_{t-1}[i] + a[i, cur]  -- the forward pass's exact f32 add
         float acol[VL], sv[VL];
-        ld_vl<VL>(at + (size_t)cur * NP, acol);
+        if (own) {
+          ld_vl<VL>(at + (size_t)cur * NP, acol);
+        } else {
+#pragma unroll
+          for (int k = 0; k < VL; ++k) acol[k] = ninf_f();
+        }
 #pragma unroll
         for (int k = 0; k < VL; ++k) sv[k] = ring[u][k] + acol[k];
         const float M = wave_max(lane_max(sv));
@@ -1014,30 +1021,42 @@ __global__ __launch_bounds__(256) void backtrack_v_f32(BacktrackArgs args) {
 }
 
 // ---------------------------------------------------------------------------------
-// trellis_wave64_f32<FRC>: small N (NP = 64) -- ONE WAVE per sequence, forward pass and
-// backtrack fused, no workgroup barrier and no cross-wave anything.
-// Forward: lane = 4cq + rg holds rows [16rg, 16rg+16) of columns 4cq..4cq+3 of A (64
-// VGPRs, from the row-major table `a_rm`); delta_{t-1} is read from the wave's own LDS
-// row with four ds_read_b128 (4 distinct addresses, padded stride 20: conflict-free); per
-// pair one v_add_f32 and half a v_max3_f32; the 4 row-group partials of the 4 columns are
-// folded across the lane quad (xor1 keeps a column pair, xor2 one column: 3 DPP maxima +
-// 6 selects) so every lane ends with ONE column jw = 4cq + 2(rg&1) + (rg>>1) and stores it.
-// LDS instructions of one wave execute in order, so the next step's reads see this step's
-// writes without a barrier.  A workgroup holds 4 independent waves (sequences).
+// trellis_wave_f32<NPW, FRC>: small N (NPW = 16, 32, 48 or 64 padded states) -- ONE WAVE per
+// sequence, forward pass and backtrack fused, no workgroup barrier and no cross-wave anything.
+// Forward: lane = 4cq + rg holds rows [R·rg, R·rg + R) (R = NPW/4) of the C = NPW/16 columns
+// C·cq .. C·cq + C-1 of A (R·C = NPW²/64 VGPRs, from the row-major table `a_rm`); delta_{t-1}
+// is read from the wave's own LDS row with R/4 ds_read_b128 (4 distinct addresses, padded
+// stride R+4: conflict-free); per pair one v_add_f32 and half a v_max3_f32; the 4 row-group
+// partials of the C columns are folded across the lane quad with DPP maxima (xor1 then xor2;
+// C = 4: xor1 keeps a column pair, xor2 one column; C = 3: xor1 keeps column p plus the shared
+// column 2, xor2 picks one; C ≤ 2: plain butterflies), so every lane ends with one column jw
+// (C < 4: some lanes hold the same column and store the same value).  Padding N to the next
+// multiple of 16 instead of 32 or 64 (N = 45: 48, not 64) cuts the per-step VALU work by
+// (48/64)² = 0.56.  LDS instructions of one wave execute in order, so the next step's reads
+// see this step's writes without a barrier.  A workgroup holds 4 independent waves.
 // Backtrack (after an agent-scope acquire, so the delta rows this wave stored are read back
-// from L2): backtrack_v_f32's loop with VL = 1.  The f64 re-score runs afterwards
-// (rescore_f64_lanes).  Roofline: VALU issue, like the large-N kernels, without their
-// barrier and fold tail; the backtrack's dependent loads overlap other waves' forward work.
-template <bool FRC>
-__global__ __launch_bounds__(256) void trellis_wave64_f32(TrellisFwdArgs args, BacktrackArgs bargs) {
-  constexpr int NP = 64;
-  constexpr int LS = 20;  // padded LDS stride of a 16-row group
+// from L2): backtrack_v_f32's loop with VL = 1 (lanes >= NPW idle), A^T read from LDS.  The f64 re-score runs
+// afterwards (rescore_f64_lanes).  Roofline: VALU issue / per-step latency (small batches).
+template <int NPW, bool FRC>
+__global__ __launch_bounds__(256) void trellis_wave_f32(TrellisFwdArgs args, BacktrackArgs bargs) {
+  constexpr int C = NPW / 16;  // columns per lane
+  constexpr int R = NPW / 4;   // rows per lane
+  constexpr int LS = R + 4;    // padded LDS stride of a row group
+  static_assert(NPW % 16 == 0 && NPW >= 16 && NPW <= 64, "NPW in {16, 32, 48, 64}");
   __shared__ __attribute__((aligned(16))) float lds_all[4][2][4 * LS];
+  // A^T for the backtrack's dependent per-step read (at[cur][.]): an LDS round trip instead
+  // of an L1/L2 one; filled by the whole workgroup before any wave starts
+  __shared__ __attribute__((aligned(16))) float at_lds[NPW * NPW];
+  for (int k = threadIdx.x; k < NPW * NPW; k += 256) at_lds[k] = bargs.at[k];
+  __syncthreads();
   const int lane = threadIdx.x & 63;
-  const int wv = threadIdx.x >> 6;
+  // wave-uniform in a scalar register, so the sequence bounds, the step loop and the
+  // observation reads are scalar (s_load) rather than per-lane
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int rg = lane & 3, cq = lane >> 2;
   const int p = rg & 1, q = rg >> 1;
-  const int jw = 4 * cq + 2 * p + q;  // this lane's column after the fold
+  // this lane's column after the fold
+  const int jw = C == 4 ? 4 * cq + 2 * p + q : C == 3 ? 3 * cq + (q ? 2 : p) : C == 2 ? 2 * cq + p : cq;
   const int64_t slot = args.seq_begin + 4 * (int64_t)blockIdx.x + wv;
   if (slot >= bargs.seq_end) return;
   int64_t seq, e0;
@@ -1054,19 +1073,25 @@ __global__ __launch_bounds__(256) void trellis_wave64_f32(TrellisFwdArgs args, B
   typedef const __attribute__((address_space(4))) int32_t* cobs_t;
   const cobs_t obs = (cobs_t)(args.obs + e0);
   const cobs_t frc = (cobs_t)(FRC ? args.forced + e0 : nullptr);
-  float* __restrict__ drow = args.delta + (e0 - args.delta_elem_base) * NP;
+  float* __restrict__ drow = args.delta + (e0 - args.delta_elem_base) * NPW;
   const unsigned V = (unsigned)args.nobs;
-  float a_reg[64];  // a_reg[4r + k] = A[16rg + r][4cq + k]
-  {
-    const float4* src = reinterpret_cast<const float4*>(args.a_img) + (size_t)(16 * rg) * (NP / 4) + cq;
+  float a_reg[R * C];  // a_reg[C·r + k] = A[R·rg + r][C·cq + k]
+  if constexpr (C == 4) {
+    const float4* src = reinterpret_cast<const float4*>(args.a_img) + (size_t)(R * rg) * (NPW / 4) + cq;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const float4 v = src[r * (NP / 4)];
+    for (int r = 0; r < R; ++r) {
+      const float4 v = src[r * (NPW / 4)];
       a_reg[4 * r + 0] = v.x;
       a_reg[4 * r + 1] = v.y;
       a_reg[4 * r + 2] = v.z;
       a_reg[4 * r + 3] = v.w;
     }
+  } else {
+    const float* src = args.a_img + (size_t)(R * rg) * NPW + C * cq;
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+      for (int k = 0; k < C; ++k) a_reg[C * r + k] = src[(size_t)r * NPW + k];
   }
   unsigned bad = 0;
   auto obs_s = [&](int t) -> unsigned {
@@ -1075,54 +1100,97 @@ __global__ __launch_bounds__(256) void trellis_wave64_f32(TrellisFwdArgs args, B
     return o < V ? o : 0u;
   };
   auto force = [&](float d, int f) -> float { return (FRC && f >= 0 && jw != f) ? ninf_f() : d; };
-  const int wofs = (jw >> 4) * LS + (jw & 15);  // where this lane's column lives in an LDS row
+  const int wofs = (jw / R) * LS + (jw % R);  // where this lane's column lives in an LDS row
   // ---- t = 0 ----
   {
-    const float d0 = force(args.pi[jw] + args.et[(size_t)obs_s(0) * NP + jw], FRC ? frc[0] : -1);
+    const float d0 = force(args.pi[jw] + args.et[(size_t)obs_s(0) * NPW + jw], FRC ? frc[0] : -1);
     lds[0][wofs] = d0;
     drow[jw] = d0;
   }
-  unsigned o_nx = obs_s(T > 1 ? 1 : 0);
-  float e_nx = args.et[(size_t)o_nx * NP + jw];
-  for (int t = 1; t < T; ++t) {
-    const float e_use = e_nx;
-    const int f_use = FRC ? frc[t] : -1;
-    o_nx = obs_s(t + 1 < T ? t + 1 : T - 1);
-    e_nx = args.et[(size_t)o_nx * NP + jw];  // one step ahead
-    const float* src = &lds[(t - 1) & 1][rg * LS];
-    float4 d[4];
+  // Steps unrolled by 4 with a static slot per step (k = (t-1) mod 4): the emission of step t
+  // is loaded 4 steps ahead (at the end of step t-4, from the observation read 4 steps before
+  // that by a scalar load), all indices clamped into the sequence so every load is issued
+  // unconditionally -- no loaded register is copied across the loop edge, so the wave never
+  // waits on the load it just issued (one-step-ahead prefetch exposed the full memory latency
+  // every step).
+  const int Tm1 = T - 1;
+  unsigned so[4];
+  float pe[4];
 #pragma unroll
-    for (int b = 0; b < 4; ++b) d[b] = *reinterpret_cast<const float4*>(src + 4 * b);
-    float c[4];
+  for (int k = 0; k < 4; ++k) {
+    pe[k] = args.et[(size_t)obs_s(min(1 + k, Tm1)) * NPW + jw];  // steps 1..4
+    so[k] = obs_s(min(5 + k, Tm1));                              // observations of steps 5..8
+  }
+  for (int t0 = 1; t0 < T; t0 += 4) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      // s_i = d[i] + a[i,j]  (viterbi.rs:15), 16 rows of column 4cq + k
-      float m = fmaxf(d[0].x + a_reg[0 * 4 + k], d[0].y + a_reg[1 * 4 + k]);
-      m = fmaxf(fmaxf(m, d[0].z + a_reg[2 * 4 + k]), d[0].w + a_reg[3 * 4 + k]);
+      const int t = t0 + k;
+      if (t >= T) break;
+      const int f_use = FRC ? frc[t] : -1;
+      const float* src = &lds[(t - 1) & 1][rg * LS];
+      float4 d[R / 4];
 #pragma unroll
-      for (int b = 1; b < 4; ++b) {
-        m = fmaxf(fmaxf(m, d[b].x + a_reg[(4 * b + 0) * 4 + k]), d[b].y + a_reg[(4 * b + 1) * 4 + k]);
-        m = fmaxf(fmaxf(m, d[b].z + a_reg[(4 * b + 2) * 4 + k]), d[b].w + a_reg[(4 * b + 3) * 4 + k]);
+      for (int b = 0; b < R / 4; ++b) d[b] = *reinterpret_cast<const float4*>(src + 4 * b);
+      float c[C];
+#pragma unroll
+      for (int kc = 0; kc < C; ++kc) {
+        // s_i = d[i] + a[i,j]  (viterbi.rs:15), R rows of column C·cq + kc
+        float m = fmaxf(d[0].x + a_reg[0 * C + kc], d[0].y + a_reg[1 * C + kc]);
+        m = fmaxf(fmaxf(m, d[0].z + a_reg[2 * C + kc]), d[0].w + a_reg[3 * C + kc]);
+#pragma unroll
+        for (int b = 1; b < R / 4; ++b) {
+          m = fmaxf(fmaxf(m, d[b].x + a_reg[(4 * b + 0) * C + kc]), d[b].y + a_reg[(4 * b + 1) * C + kc]);
+          m = fmaxf(fmaxf(m, d[b].z + a_reg[(4 * b + 2) * C + kc]), d[b].w + a_reg[(4 * b + 3) * C + kc]);
+        }
+        c[kc] = m;
       }
-      c[k] = m;
+      // fold the 4 row groups of the lane quad 4cq .. 4cq+3 into this lane's column jw
+      float kk;
+      if constexpr (C == 4) {  // xor1 keeps columns {2p, 2p+1}, xor2 keeps 2p+q
+        float k0 = p ? c[2] : c[0], k1 = p ? c[3] : c[1];
+        const float g0 = p ? c[0] : c[2], g1 = p ? c[1] : c[3];
+        k0 = dpp_max_xor1_other(k0, g0);
+        k1 = dpp_max_xor1_other(k1, g1);
+        kk = q ? k1 : k0;
+        const float gg = q ? k0 : k1;
+        kk = dpp_max_xor2_other(kk, gg);
+      } else if constexpr (C == 3) {  // xor1 keeps column p and the shared column 2, xor2 one
+        float k0 = p ? c[1] : c[0];
+        const float g0 = p ? c[0] : c[1];
+        k0 = dpp_max_xor1_other(k0, g0);
+        const float k2 = dpp_max_xor1(c[2]);
+        kk = q ? k2 : k0;
+        const float gg = q ? k0 : k2;
+        kk = dpp_max_xor2_other(kk, gg);
+      } else if constexpr (C == 2) {  // xor1 keeps column p, xor2 completes it
+        float k0 = p ? c[1] : c[0];
+        const float g0 = p ? c[0] : c[1];
+        k0 = dpp_max_xor1_other(k0, g0);
+        kk = dpp_max_xor2(k0);
+      } else {
+        kk = dpp_max_xor2(dpp_max_xor1(c[0]));
+      }
+#ifndef CVK_ABLATE_NOEMIT
+      const float e_use = pe[k];
+#else
+      const float e_use = -0.5f * (float)(t & 7);
+#endif
+      const float dn = force(kk + e_use, f_use);  // (d + a) + b -- viterbi.rs:15-17
+      lds[t & 1][wofs] = dn;
+      drow[(size_t)t * NPW + jw] = dn;
+#ifndef CVK_ABLATE_NOEMIT
+      pe[k] = args.et[(size_t)so[k] * NPW + jw];  // step t+4
+      so[k] = obs_s(min(t + 8, Tm1));            // observation of step t+8
+#endif
     }
-    // fold the 4 row groups (lanes 4cq..4cq+3): xor1 keeps columns {2p, 2p+1}, xor2 keeps 2p+q
-    float k0 = p ? c[2] : c[0], k1 = p ? c[3] : c[1];
-    const float g0 = p ? c[0] : c[2], g1 = p ? c[1] : c[3];
-    k0 = dpp_max_xor1_other(k0, g0);
-    k1 = dpp_max_xor1_other(k1, g1);
-    float kk = q ? k1 : k0;
-    const float gg = q ? k0 : k1;
-    kk = dpp_max_xor2_other(kk, gg);
-    const float dn = force(kk + e_use, f_use);  // (d + a) + b -- viterbi.rs:15-17
-    lds[t & 1][wofs] = dn;
-    drow[(size_t)t * NP + jw] = dn;
   }
   // ---- backtrack (cp.rs:85-93) of this wave's own sequence: the delta rows were stored
   // by other lanes of this wave -- make them visible (release to L2, then acquire) ----
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  backtrack_one<1, NP>(bargs, seq, e0, T, lane, drow + lane, bargs.at + lane, bad != 0);
+#ifndef CVK_ABLATE_NOBT
+  backtrack_one<1, NPW>(bargs, seq, e0, T, lane, drow + lane, at_lds + lane, bad != 0);
+#endif
 }
 
 // rescore_f64_lanes: the f64 re-score of rescore_path_f64, but one LANE per sequence, so the
@@ -1464,16 +1532,29 @@ hipError_t launch_trellis_fwd2(int np, const TrellisFwdArgs& fa, int64_t npairs,
 #undef CVK_FWD2
 }
 
-hipError_t launch_trellis_wave64(const TrellisFwdArgs& fa, const BacktrackArgs& ba, int64_t nseq,
-                                 hipStream_t stream) {
+int trellis_wave_states(int n) { return (n >= 1 && n <= 64) ? (n + 15) / 16 * 16 : 0; }
+
+hipError_t launch_trellis_wave(int npw, const TrellisFwdArgs& fa, const BacktrackArgs& ba, int64_t nseq,
+                               hipStream_t stream) {
   if (nseq <= 0) return hipSuccess;
   if (fa.ranges || fa.reverse || fa.last_row || fa.start || !fa.delta || fa.split || fa.slot_order)
     return hipErrorInvalidValue;
   const dim3 grid((unsigned)((nseq + 3) / 4));
-  if (fa.forced)
-    hipLaunchKernelGGL(trellis_wave64_f32<true>, grid, dim3(256), 0, stream, fa, ba);
-  else
-    hipLaunchKernelGGL(trellis_wave64_f32<false>, grid, dim3(256), 0, stream, fa, ba);
+#define CVK_WAVE(NPW)                                                                        \
+  do {                                                                                       \
+    if (fa.forced)                                                                           \
+      hipLaunchKernelGGL((trellis_wave_f32<NPW, true>), grid, dim3(256), 0, stream, fa, ba); \
+    else                                                                                     \
+      hipLaunchKernelGGL((trellis_wave_f32<NPW, false>), grid, dim3(256), 0, stream, fa, ba); \
+  } while (0)
+  switch (npw) {
+    case 16: CVK_WAVE(16); break;
+    case 32: CVK_WAVE(32); break;
+    case 48: CVK_WAVE(48); break;
+    case 64: CVK_WAVE(64); break;
+    default: return hipErrorInvalidValue;
+  }
+#undef CVK_WAVE
   return hipGetLastError();
 }
 

@@ -91,12 +91,12 @@ def test_pair_kernel_equal_and_ragged(gpu, n, serial):
     _assert_same(cv.decode_batch(h, off2, obs2, rescore_f64=False, serial=serial), ref2, f"equal N={n}")
 
 
-@pytest.mark.parametrize("n", [33, 45, 64])
+@pytest.mark.parametrize("n", [1, 5, 16, 17, 31, 32, 33, 45, 48, 49, 64])
 @pytest.mark.parametrize("serial", [False, True])
 def test_wave_kernel_small_n(gpu, n, serial):
-    """N <= 64: one wave per sequence with the backtrack fused (trellis_wave64_f32): ragged
-    lengths incl. T = 0 and 1, -inf entries, a chunked workspace -- bit-identical to the
-    oracle and to the workgroup kernels."""
+    """N <= 64: one wave per sequence with the backtrack fused (trellis_wave_f32, tables
+    padded to 16/32/48/64 states): ragged lengths incl. T = 0 and 1, -inf entries, a chunked
+    workspace -- bit-identical to the oracle and to the workgroup kernels."""
     pi, a, b = synth.random_hmm(n, 17, seed=2000 + n, zero_frac=0.03)
     rng = np.random.default_rng(n + 11)
     off = synth.offsets_from_lengths(rng.choice([0, 1, 2, 7, 40, 129, 300], size=53))
@@ -105,6 +105,7 @@ def test_wave_kernel_small_n(gpu, n, serial):
     ref = O.decode_batch(pi, a, b, off, obs, O.VITERBI, np.float32)
     ws = 0 if serial else 64 * 4 * 700
     got = cv.decode_batch(h, off, obs, rescore_f64=False, serial=serial, workspace_bytes=ws)
+    assert cv.last_timing(h)["padded_states"] == (n + 15) // 16 * 16
     _assert_same(got, ref, f"wave N={n}")
     other = cv.decode_batch(h, off, obs, rescore_f64=False, variant="nowave", serial=serial, workspace_bytes=ws)
     _assert_same(got, other, f"wave vs workgroup N={n}")
