@@ -658,12 +658,9 @@ hipError_t launch_bw_estep(const BwArgs& g, int64_t nseq, int64_t max_waves, hip
   hipLaunchKernelGGL(bw_forward, dim3((unsigned)nseq), dim3(256), 0, stream, g);
   hipLaunchKernelGGL(bw_backward, dim3((unsigned)nseq), dim3(256), 0, stream, g);
   const size_t lds = ((size_t)g.nstates * g.nstates + 256 + 4) * sizeof(double);
-  static bool attr = false;
-  if (!attr) {
+  if (lds > 64 * 1024)  // per device: set on every launch that needs it (cheap)
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&bw_stats), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024);
-    attr = true;
-  }
+                              (int)lds);
   hipLaunchKernelGGL(bw_stats, dim3((unsigned)nseq), dim3(256), lds, stream, g);
   return hipGetLastError();
 }
