@@ -279,3 +279,20 @@ def test_solver_api(gpu):
         assert s.get_objective() == pytest.approx(exp, rel=1e-12)
         per_seq = ss.parse_solution(sol)
         assert [len(x) for x in per_seq] == [len(x) for x in seqs]
+
+
+def test_long_sequence_large_alphabet(gpu):
+    """Maximum-size corner: N = 256, a 40,000-step sequence next to short ones, V = 200,000
+    observations (800 MB emission image) -- bit-exact vs the oracle, also with a workspace
+    cap below the long sequence's delta rows (a chunk never splits a sequence: it gets a
+    chunk of its own, the short ones others)."""
+    n, v = 256, 200_000
+    pi, a, b = synth.random_hmm(n, 64, seed=31)
+    rng = np.random.default_rng(31)
+    b = np.repeat(b, v // 64, axis=1)[:, :v] + rng.normal(0, 0.01, size=(n, v))  # log10, distinct values
+    off = synth.offsets_from_lengths(np.array([3, 40_000, 1, 17]))
+    obs = rng.integers(0, v, size=int(off[-1])).astype(np.int32)
+    h = cv.HMM(pi, a, b)
+    ref = O.decode_batch(pi, a, b, off, obs, O.VITERBI, np.float32, nthreads=4)
+    _assert_same(cv.decode_batch(h, off, obs, rescore_f64=False), ref, "long")
+    _assert_same(cv.decode_batch(h, off, obs, rescore_f64=False, workspace_bytes=256 * 4 * 9000), ref, "long, capped")
