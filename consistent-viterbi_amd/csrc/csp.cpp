@@ -1,5 +1,6 @@
 // Exact component-state search (see csp.hpp).  Pure host C++, no device code.
 #include "csp.hpp"
+#include "exact_fixed.h"
 
 #include <algorithm>
 #include <cmath>
@@ -13,32 +14,11 @@ void add_exact(int64_t* limbs4, int64_t* ninf_count, float x) {
     *ninf_count += 1;
     return;
   }
-  // v = nearbyint(x * 2^64) from the float's bits (integer ops only; the double -> __int128
-  // conversion this replaces is a slow library call): x = +-M * 2^(E-150), so x * 2^64 =
-  // +-M * 2^k, k = E - 86, rounded half-to-even (the default mode nearbyint uses).  |x| <
-  // 2^24 for any log10 probability sum we produce, so |v| < 2^88.  Checked bit-identical to
-  // the double form on 3.7e7 floats incl. every exponent (tools/debug notes in DESIGN.md).
-  uint32_t b;
-  std::memcpy(&b, &x, 4);
-  const int E = (int)((b >> 23) & 0xFF);
-  const uint64_t M = E ? ((b & 0x7FFFFFu) | 0x800000u) : (b & 0x7FFFFFu);
-  const int k = (E ? E : 1) - 86;
-  unsigned __int128 mag;
-  if (k >= 0) {
-    mag = (unsigned __int128)M << k;
-  } else if (-k >= 25) {
-    mag = 0;  // M * 2^k < 2^24 * 2^-25 = 1/2
-  } else {
-    const int s = -k;
-    const uint64_t q = M >> s, r = M & ((1ull << s) - 1), half = 1ull << (s - 1);
-    mag = q + ((r > half || (r == half && (q & 1))) ? 1 : 0);
-  }
-  const __int128 v = (b >> 31) ? -(__int128)mag : (__int128)mag;
-  const unsigned __int128 u = (unsigned __int128)v;
-  limbs4[0] += (int64_t)(uint32_t)u;
-  limbs4[1] += (int64_t)(uint32_t)(u >> 32);
-  limbs4[2] += (int64_t)(uint32_t)(u >> 64);
-  limbs4[3] += (int64_t)(v >> 96);
+  // the limbs of nearbyint(x * 2^64), shared with the device sums (exact_fixed.h); checked
+  // bit-identical to the double -> __int128 form on 3.7e7 floats incl. every exponent
+  int64_t l[4];
+  cvx::fixed64_limbs(x, l);
+  for (int k = 0; k < 4; ++k) limbs4[k] += l[k];
 }
 
 static inline __int128 limbs_value(const int64_t* l) {

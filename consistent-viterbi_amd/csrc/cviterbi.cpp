@@ -28,6 +28,7 @@
 #include "csp.hpp"
 #include "hmm_json.hpp"
 #include "kernels/cfn.h"
+#include "kernels/exact.h"
 #include "kernels/fit.h"
 #include "kernels/trellis.h"
 
@@ -123,6 +124,7 @@ struct cv_hmm {
   DevBuf ws_main, ws_last, ws_order;
   DevBuf st_off, st_obs, st_path, st_score, st_status, st_forced;
   DevBuf cs_ranges, cs_delta, cs_g, cs_mu, cs_start, cs_zero;  // constrained-decode scratch
+  DevBuf cs_comp, cs_words;  // device exact unary sums: per-sequence components, output words
   std::vector<int32_t> order_host;
   std::vector<float> host_dl, host_mu;  // constrained-decode term rows (kept: no per-call page faults)
   // timing events of the last call
@@ -1115,6 +1117,43 @@ cv_status constrained_partials_locked(cv_hmm* h, int64_t nseq, const int64_t* of
   }
   if (err != hipSuccess) return set_err(CV_EDEVICE, "max-marginal launch failed: %s", hipGetErrorString(err));
   trace_mark("term launches enqueued");
+  for (int64_t i = 0; i < nc; ++i)
+    for (int64_t e : order[i]->elems) part[(int64_t)component[e] * uw + 5 * N] += 1;
+  // CV_HOST_SUMS=1 takes the host loop (tests compare the two; same integers by construction)
+  const char* hs = getenv("CV_HOST_SUMS");
+  const bool host_sums = hs && *hs && *hs != '0';
+  if (!host_sums && ncomp <= cvx::kUnarySumMaxComp && N <= 256) {
+    // exact unary sums on the device (kernels/exact.hip): only the ncomp x uw words come back
+    std::vector<int32_t> cc((size_t)2 * nc);
+    for (int64_t i = 0; i < nc; ++i) {
+      cc[(size_t)i] = component[order[i]->elems.front()];
+      cc[(size_t)nc + i] = component[order[i]->elems.back()];
+    }
+    if ((st = h->cs_comp.ensure(cc.size() * 4)) != CV_OK) return st;
+    if ((st = h->cs_words.ensure((size_t)ncomp * uw * 8)) != CV_OK) return st;
+    HIP_TRY(hipMemcpyAsync(h->cs_comp.p, cc.data(), cc.size() * 4, hipMemcpyHostToDevice, stream));
+    HIP_TRY(hipMemsetAsync(h->cs_words.p, 0, (size_t)ncomp * uw * 8, stream));
+    cvx::UnarySumArgs us{};
+    us.mu = h->cs_mu.as<float>();
+    us.dl = h->cs_delta.as<float>();
+    us.c1 = h->cs_comp.as<int32_t>();
+    us.cm = h->cs_comp.as<int32_t>() + nc;
+    us.nc = nc;
+    us.n1 = n1;
+    us.np = np;
+    us.nstates = N;
+    us.ncomp = ncomp;
+    us.uw = uw;
+    us.part = h->cs_words.as<long long>();
+    const int nblocks = (int)std::max<int64_t>(1, std::min<int64_t>(2 * std::max(h->cus, 1), (nc + 31) / 32));
+    const hipError_t e = cvx::launch_unary_sums(us, nblocks, stream);
+    if (e != hipSuccess) return set_err(CV_EDEVICE, "unary sum launch failed: %s", hipGetErrorString(e));
+    std::vector<int64_t> words((size_t)ncomp * uw);
+    HIP_TRY(hipMemcpyAsync(words.data(), h->cs_words.p, words.size() * 8, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipStreamSynchronize(stream));  // `cc` and `words` are local buffers
+    trace_mark("terms + exact sums (device)");
+    for (size_t q = 0; q < words.size(); ++q) part[q] += words[q];
+  } else {
   std::vector<float>& dl = h->host_dl;
   std::vector<float>& mu = h->host_mu;
   if (dl.size() < (size_t)nc * np) dl.resize((size_t)nc * np);
@@ -1123,8 +1162,6 @@ cv_status constrained_partials_locked(cv_hmm* h, int64_t nseq, const int64_t* of
   HIP_TRY(hipMemcpyAsync(mu.data(), h->cs_mu.p, (size_t)nc * np * 4, hipMemcpyDeviceToHost, stream));
   HIP_TRY(hipStreamSynchronize(stream));
   trace_mark("terms device + D2H");
-  for (int64_t i = 0; i < nc; ++i)
-    for (int64_t e : order[i]->elems) part[(int64_t)component[e] * uw + 5 * N] += 1;
   // exact accumulation, parallel over states into worker-local words (the components'
   // word blocks are not cache-line aligned: writing `part` directly would false-share),
   // added into `part` at the end (integer sums: order-free)
@@ -1156,8 +1193,8 @@ cv_status constrained_partials_locked(cv_hmm* h, int64_t nseq, const int64_t* of
         u[4 * N + s] += cnt[q];
       }
   }, 1);
-
-  trace_mark("exact sums");
+  trace_mark("exact sums (host)");
+  }
   // ---- segment tables: one slot per (segment, start state), in batches ----
   struct Seg { int64_t e0, e1; int32_t c1, c2; int64_t p; };
   std::vector<Seg> segs;

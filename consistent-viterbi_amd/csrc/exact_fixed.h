@@ -1,0 +1,45 @@
+// exact_fixed.h -- the exact accumulation unit of the constrained decode's terms, shared by
+// the host (csp.cpp) and the device (kernels/exact.hip) so both add bit-identical integers.
+// A float x (a log10 path score, |x| < 2^24) becomes v = nearbyint(x * 2^64) (round half to
+// even), a signed integer below 2^88 in magnitude, added into 4 base-2^32 limbs held in int64
+// words (limb 3 signed); -inf is counted instead.  Integer sums are order-free, so partial
+// sums from any number of threads, blocks, shards or GPUs add up to the same words.
+#pragma once
+#include <stdint.h>
+#include <string.h>
+
+#if defined(__HIP__)
+#define CVX_HD __host__ __device__
+#else
+#define CVX_HD
+#endif
+
+namespace cvx {
+
+// The 4 limbs of v (x finite).  Integer ops only: x = +-M * 2^(E-150), so x * 2^64 =
+// +-M * 2^k with k = E - 86.
+CVX_HD inline void fixed64_limbs(float x, int64_t (&l)[4]) {
+  uint32_t b;
+  memcpy(&b, &x, 4);
+  const int E = (int)((b >> 23) & 0xFF);
+  const uint64_t M = E ? ((b & 0x7FFFFFu) | 0x800000u) : (b & 0x7FFFFFu);
+  const int k = (E ? E : 1) - 86;
+  unsigned __int128 mag;
+  if (k >= 0) {
+    mag = (unsigned __int128)M << k;
+  } else if (-k >= 25) {
+    mag = 0;  // M * 2^k < 2^24 * 2^-25 = 1/2
+  } else {
+    const int s = -k;
+    const uint64_t q = M >> s, r = M & ((1ull << s) - 1), half = 1ull << (s - 1);
+    mag = q + ((r > half || (r == half && (q & 1))) ? 1 : 0);
+  }
+  const __int128 v = (b >> 31) ? -(__int128)mag : (__int128)mag;
+  const unsigned __int128 u = (unsigned __int128)v;
+  l[0] = (int64_t)(uint32_t)u;
+  l[1] = (int64_t)(uint32_t)(u >> 32);
+  l[2] = (int64_t)(uint32_t)(u >> 64);
+  l[3] = (int64_t)(v >> 96);
+}
+
+}  // namespace cvx

@@ -242,3 +242,26 @@ def test_cli_cfn(gpu, tmp_path):
     ref = CO.write_cfn_text(pi.tolist(), a.tolist(), b.tolist(), ss.value.tolist(), comp,
                             (ss.t == 0).astype(int).tolist())
     assert (tmp_path / "out" / "problem_1_0.cfn").read_text() == ref
+
+
+@pytest.mark.parametrize("n,seed", [(7, 1), (64, 2), (256, 3)])
+def test_device_exact_sums_equal_host(gpu, monkeypatch, n, seed):
+    """The unary terms summed exactly on the device (kernels/exact.hip) give the same int64
+    words as the host loop (CV_HOST_SUMS=1): single- and multi-position sequences, -inf
+    terms, several components."""
+    pi, a, b = synth.random_hmm(n, 13, seed=seed, zero_frac=0.05)
+    rng = np.random.default_rng(seed)
+    off = synth.offsets_from_lengths(rng.integers(1, 50, size=300))
+    obs = rng.integers(0, 13, size=int(off[-1])).astype(np.int32)
+    comp = np.full(len(obs), -1, np.int32)
+    for s in range(len(off) - 1):  # 0, 1 or 3 constrained positions per sequence
+        k = int(rng.choice([0, 1, 1, 3]))
+        if k and off[s + 1] - off[s] >= k:
+            pos = rng.choice(np.arange(off[s], off[s + 1]), size=k, replace=False)
+            comp[pos] = rng.integers(0, 5, size=k)
+    h = cv.HMM(pi, a, b)
+    pairs = cv.constrained_pairs(off, comp, 5)
+    dev = cv.constrained_partials(h, off, obs, comp, 5, pairs)
+    monkeypatch.setenv("CV_HOST_SUMS", "1")
+    host = cv.constrained_partials(h, off, obs, comp, 5, pairs)
+    assert np.array_equal(dev, host)
