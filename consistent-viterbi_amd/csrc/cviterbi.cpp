@@ -1,7 +1,7 @@
 // cviterbi.cpp -- C ABI (include/cviterbi.h) over the MI355X trellis kernels.
 //
 // Host side of the drop-in boundary: the HMM handle mirrors struct HMM<D> and its
-// log-prob lookups (src/hmm/hmm.rs:10-18, 407-445), the batch decode replaces the
+// log-prob lookups (src/hmm/hmm.rs:10-18, 207-245), the batch decode replaces the
 // dense forward + backtrack of viterbi_solver (cp.rs:63-93, viterbi.rs:5-32,
 // dp.rs:94-209), and cv_solver_* mirrors `trait Solver` (viterbi_solver.rs:11-16).
 //

@@ -133,7 +133,7 @@ CV_API void cv_opts_init(cv_opts* opts);
 /* ---- hmm::HMM (src/hmm/hmm.rs) ------------------------------------------------------- */
 /* HMM struct construction (hmm.rs:10-18). */
 CV_API cv_status cv_hmm_create(const cv_hmm_desc* desc, cv_hmm** out);
-/* HMM::from_json (hmm.rs:242-245 + null->-inf parsers 448-464). */
+/* HMM::from_json (hmm.rs:242-245 + null->-inf parsers 248-264). */
 CV_API cv_status cv_hmm_from_json(const char* path, int32_t device, cv_hmm** out);
 /* HMM::write (hmm.rs:236-240): serde_json layout, -inf written as null. */
 CV_API cv_status cv_hmm_write_json(const cv_hmm* h, const char* path);
