@@ -2,13 +2,18 @@
 
 Workload (BASELINE.json configs[3]): synthetic HMM with N=256
 states, V=1,024 observations (bdims [32,32]), Dirichlet(1) rows in log10, iid uniform
-observations from splitmix64; T=512, B=65,536 sequences in total, f32 row-A0 trellis.
-The batch is sharded across ranks (strong scaling: total work fixed, B/N per GPU); one
-step = decode of the rank's shard (forward trellis kernel + backtrack + f64 re-score of
-every path) followed, for N>1, by ONE RCCL gather (torch.distributed "nccl") of the paths
-(u8 states), scores and statuses to rank 0 over xGMI.  Inputs are resident in HBM before the timed region.
+observations from splitmix64; T=512, B=65,536 sequences per batch, f32 row-A0 trellis.
+Sequences are independent, so the batch shards across ranks with no data-path collective:
+by default every rank decodes its own 65,536-sequence shard of a global batch of
+N x 65,536 (weak scaling); --scaling strong splits ONE 65,536-sequence batch
+B/N per GPU instead.  One step = decode of the rank's shard (forward trellis kernel +
+backtrack + f64 re-score of every path) and, for N>1, ONE RCCL gather (torch.distributed
+"nccl") of the paths (u8 states), scores and statuses to rank 0 over xGMI -- issued on a
+second stream so that step k's gather overlaps step k+1's decode (double-buffered outputs;
+the closing synchronize waits for the last one).  Inputs are resident in HBM before the
+timed region.
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--scaling weak|strong]
        (N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N)
 Rank 0 prints ONE JSON line.
 """
@@ -36,7 +41,9 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=2)
-    p.add_argument("--batch", type=int, default=B_TOTAL, help="total sequences (default 65,536)")
+    p.add_argument("--batch", type=int, default=B_TOTAL,
+                   help="sequences per rank (weak) or in total (strong); default 65,536")
+    p.add_argument("--scaling", choices=("weak", "strong"), default="weak")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
     p.add_argument("--no-cpu-baseline", action="store_true")
     return p.parse_args()
@@ -125,31 +132,54 @@ def main():
 
     from cviterbi import dist as cvd
 
-    B = args.batch
-    s0, s1, per = cvd.shard_range(B, world, rank)
+    if args.scaling == "weak":  # every rank: its own full batch of the global N x B
+        B = args.batch * world
+        s0, s1, per = rank * args.batch, (rank + 1) * args.batch, args.batch
+    else:
+        B = args.batch
+        s0, s1, per = cvd.shard_range(B, world, rank)
     nloc = s1 - s0
     pi, a, b = synth.random_hmm(N_STATES, V_OBS, seed=SEED)
     obs = synth.iid_obs(V_OBS, nloc * T_LEN, SEED, start=s0 * T_LEN)
     off = np.arange(nloc + 1, dtype=np.int64) * T_LEN
 
     h = cv.HMM(pi, a, b.reshape(N_STATES, 32, 32), device=local)
-    stream = torch.cuda.Stream(dev)  # non-default stream shared by the decode and the gathers
+    stream = torch.cuda.Stream(dev)  # the decode
+    comm = torch.cuda.Stream(dev)    # the gathers (RCCL waits on it), overlapping the next decode
     torch.cuda.set_stream(stream)
     off_d = torch.from_numpy(off).to(dev)
     obs_d = torch.from_numpy(obs).to(dev)
-    path_d = torch.empty(nloc * T_LEN, dtype=torch.int32, device=dev)
-    score_d = torch.empty(nloc, dtype=torch.float64, device=dev)
-    status_d = torch.empty(nloc, dtype=torch.uint8, device=dev)
+    nbuf = 2 if world > 1 else 1
+    outs = [(torch.empty(nloc * T_LEN, dtype=torch.int32, device=dev),
+             torch.empty(nloc, dtype=torch.float64, device=dev),
+             torch.empty(nloc, dtype=torch.uint8, device=dev)) for _ in range(nbuf)]
+    gathered = [None] * nbuf  # event: that buffer's gather has read it
+    k_step = [0]
+
     def step():
+        i = k_step[0] % nbuf
+        k_step[0] += 1
+        path_d, score_d, status_d = outs[i]
+        if gathered[i] is not None:
+            stream.wait_event(gathered[i])
         cv.decode_batch_device(h, off_d, obs_d, path_d, score_d, status_d, offsets_host=off,
                                stream=stream.cuda_stream, workspace_bytes=WORKSPACE)
         if world > 1:  # RCCL over xGMI: decoded paths (u8 states), scores, statuses to rank 0, one gather
-            cvd.gather_packed_to_root(path_d, score_d, status_d, N_STATES, per * T_LEN, per, dist)
+            done = torch.cuda.Event()
+            done.record(stream)
+            comm.wait_event(done)
+            with torch.cuda.stream(comm):
+                for t in outs[i]:
+                    t.record_stream(comm)
+                cvd.gather_packed_to_root(path_d, score_d, status_d, N_STATES, per * T_LEN, per, dist)
+                ev = torch.cuda.Event()
+                ev.record(comm)
+                gathered[i] = ev
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
-    bad = int((status_d != 0).sum().item())
+    bad = int(sum(int((o[2] != 0).sum().item()) for o in outs))
     if bad:
         raise SystemExit(f"rank {rank}: {bad} sequences did not decode cleanly")
 
@@ -195,12 +225,15 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": ms_step,
         "higher_is_better": True,
-        "scaling": "strong",
+        "scaling": args.scaling,
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic (Dirichlet(1) log10 HMM, splitmix64 iid observations; SURVEY.md §8d config 4)",
-        "config": {"workload": "config4: N=256 states, V=1024, T=512, batch=65536 sharded over ranks, f32 row-A0 "
-                               "trellis + backtrack + f64 re-score" + (", RCCL gather to rank 0" if world > 1 else ""),
+        "config": {"workload": "config4: N=256 states, V=1024, T=512, " +
+                               (f"batch=65536 per rank (global {B})" if args.scaling == "weak" else
+                                f"batch={B} sharded over {world} ranks") +
+                               ", f32 row-A0 trellis + backtrack + f64 re-score" +
+                               (", RCCL gather to rank 0 (overlapped with the next step)" if world > 1 else ""),
                    "global_batch": B, "seq_len": T_LEN, "states": N_STATES, "parallelism": f"batch-shard x{world}"},
         "seqs_per_s": B * args.steps / el,
         "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",

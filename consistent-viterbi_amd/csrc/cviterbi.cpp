@@ -1010,7 +1010,7 @@ cv_status constrained_validate(cv_hmm* h, int64_t nseq, const int64_t* offsets, 
 cv_status constrained_partials_locked(cv_hmm* h, int64_t nseq, const int64_t* offsets, const int32_t* obs,
                                       const int32_t* component, int32_t ncomp, const int32_t* pairs, int64_t npairs,
                                       cv_opts& o, int64_t* part, const std::vector<ConSeq>* pre = nullptr,
-                                      bool* obs_staged = nullptr) {
+                                      bool* obs_staged = nullptr, const int32_t* obs_dev = nullptr) {
   if (obs_staged) *obs_staged = false;
   std::vector<ConSeq> own;
   cv_status st = CV_OK;
@@ -1038,11 +1038,16 @@ cv_status constrained_partials_locked(cv_hmm* h, int64_t nseq, const int64_t* of
   const int np = h->np;
   hipStream_t stream = o.stream ? (hipStream_t)o.stream : h->stream;
   const int64_t base = offsets[0], total = offsets[nseq];
-  if ((st = h->st_obs.ensure((size_t)std::max<int64_t>(total, 1) * 4)) != CV_OK) return st;
-  HIP_TRY(hipMemcpyAsync(h->st_obs.as<int32_t>() + base, obs + base, (size_t)(total - base) * 4,
-                         hipMemcpyHostToDevice, stream));
-  if (obs_staged) *obs_staged = true;
-  trace_mark("obs H2D enqueued");
+  // observations on the device: the caller's (device API, validated) or staged here
+  const int32_t* dobs = obs_dev;
+  if (!dobs) {
+    if ((st = h->st_obs.ensure((size_t)std::max<int64_t>(total, 1) * 4)) != CV_OK) return st;
+    HIP_TRY(hipMemcpyAsync(h->st_obs.as<int32_t>() + base, obs + base, (size_t)(total - base) * 4,
+                           hipMemcpyHostToDevice, stream));
+    if (obs_staged) *obs_staged = true;
+    dobs = h->st_obs.as<int32_t>();
+    trace_mark("obs H2D enqueued");
+  }
 
   // ---- prefix / suffix passes for every constrained sequence (m == 1 ones first) ----
   std::vector<const ConSeq*> order;
@@ -1074,7 +1079,7 @@ cv_status constrained_partials_locked(cv_hmm* h, int64_t nseq, const int64_t* of
   fa.a_img = h->t_aimg.as<float>();
   fa.pi = h->t_pi.as<float>();
   fa.et = h->t_et.as<float>();
-  fa.obs = h->st_obs.as<int32_t>();
+  fa.obs = dobs;
   fa.status = h->st_status.as<uint8_t>();
   fa.nobs = (int)h->V;
   fa.ranges = h->cs_ranges.as<int64_t>();
@@ -1227,7 +1232,7 @@ cv_status constrained_partials_locked(cv_hmm* h, int64_t nseq, const int64_t* of
     sa.a_img = h->t_aimg.as<float>();
     sa.pi = h->t_pi.as<float>();
     sa.et = h->t_et.as<float>();
-    sa.obs = h->st_obs.as<int32_t>();
+    sa.obs = dobs;
     sa.status = h->st_status.as<uint8_t>();
     sa.nobs = (int)h->V;
     sa.ranges = h->cs_ranges.as<int64_t>();
@@ -1262,10 +1267,11 @@ cv_status constrained_partials_locked(cv_hmm* h, int64_t nseq, const int64_t* of
 // component has no feasible state are infeasible.  objective = sum of the f64 scores.  The
 // forced-state array is built on the device (fill -1, scatter the constrained elements of
 // `cs`); obs_staged: h->st_obs already holds the batch's observations.
-cv_status forced_decode_locked(cv_hmm* h, int64_t nseq, const int64_t* offsets, const int32_t* obs,
-                               const int32_t* component, const int32_t* comp_state, cv_opts o,
-                               const std::vector<ConSeq>& cs, bool obs_staged, int32_t* path_out,
-                               double* score_out, uint8_t* status_out, double* objective_out) {
+// The forced-state array of a batch on the device (h->st_forced, indexed like obs, -1 = free):
+// every constrained element of `cs` takes comp_state[component[e]] (0 when the component has
+// no state: such sequences are marked infeasible afterwards by mark_unassigned).
+cv_status stage_forced_locked(cv_hmm* h, const int64_t* offsets, int64_t nseq, const int32_t* component,
+                              const int32_t* comp_state, const std::vector<ConSeq>& cs, hipStream_t stream) {
   const int64_t base = offsets[0], total = offsets[nseq];
   std::vector<int64_t> el;
   std::vector<int32_t> sv;
@@ -1274,7 +1280,6 @@ cv_status forced_decode_locked(cv_hmm* h, int64_t nseq, const int64_t* offsets, 
       el.push_back(e);
       sv.push_back(comp_state[component[e]] >= 0 ? comp_state[component[e]] : 0);
     }
-  hipStream_t stream = o.stream ? (hipStream_t)o.stream : h->stream;
   cv_status st;
   if ((st = h->st_forced.ensure((size_t)std::max<int64_t>(total, 1) * 4)) != CV_OK) return st;
   if ((st = h->cs_ranges.ensure(std::max<size_t>(el.size(), 1) * 8)) != CV_OK) return st;
@@ -1286,20 +1291,43 @@ cv_status forced_decode_locked(cv_hmm* h, int64_t nseq, const int64_t* offsets, 
     const hipError_t err = cvk::launch_scatter_forced(h->cs_ranges.as<int64_t>(), h->cs_start.as<int32_t>(),
                                                       (int64_t)el.size(), h->st_forced.as<int32_t>(), stream);
     if (err != hipSuccess) return set_err(CV_EDEVICE, "forced-state scatter failed: %s", hipGetErrorString(err));
+    // the host vectors die at return: the copies must have read them
+    HIP_TRY(hipStreamSynchronize(stream));
   }
   trace_mark("forced array (device)");
+  return CV_OK;
+}
+
+// Host copies of the decode's scores/statuses: sequences with an element of a component
+// that got no state are infeasible; objective = the f64 sum in sequence order (that sum's
+// rounding is part of the spec).
+double mark_unassigned(int64_t nseq, const int32_t* component, const int32_t* comp_state,
+                       const std::vector<ConSeq>& cs, double* score, uint8_t* status) {
+  for (const auto& c : cs)
+    for (int64_t e : c.elems)
+      if (comp_state[component[e]] < 0) {
+        status[c.seq] = CV_SEQ_INFEASIBLE;
+        score[c.seq] = -INFINITY;
+      }
+  double obj = 0.0;
+  for (int64_t s = 0; s < nseq; ++s) obj += status[s] == CV_SEQ_INFEASIBLE ? -INFINITY : score[s];
+  return obj;
+}
+
+// Final decode with every constrained element forced (caller holds h->mu; `cs` as built by
+// `constrained_validate`); obs_staged: h->st_obs already holds the batch's observations.
+cv_status forced_decode_locked(cv_hmm* h, int64_t nseq, const int64_t* offsets, const int32_t* obs,
+                               const int32_t* component, const int32_t* comp_state, cv_opts o,
+                               const std::vector<ConSeq>& cs, bool obs_staged, int32_t* path_out,
+                               double* score_out, uint8_t* status_out, double* objective_out) {
+  hipStream_t stream = o.stream ? (hipStream_t)o.stream : h->stream;
+  cv_status st;
+  if ((st = stage_forced_locked(h, offsets, nseq, component, comp_state, cs, stream)) != CV_OK) return st;
   o.forced = h->st_forced.as<int32_t>();
   st = decode_host_locked(h, nseq, offsets, obs, o, path_out, score_out, status_out, obs_staged, true);
   if (st != CV_OK) return st;
   trace_mark("forced decode (sync)");
-  for (const auto& c : cs)
-    for (int64_t e : c.elems)
-      if (comp_state[component[e]] < 0) {
-        status_out[c.seq] = CV_SEQ_INFEASIBLE;
-        score_out[c.seq] = -INFINITY;
-      }
-  double obj = 0.0;  // sequential, in sequence order (the f64 sum's rounding is part of the spec)
-  for (int64_t s = 0; s < nseq; ++s) obj += status_out[s] == CV_SEQ_INFEASIBLE ? -INFINITY : score_out[s];
+  const double obj = mark_unassigned(nseq, component, comp_state, cs, score_out, status_out);
   if (objective_out) *objective_out = obj;
   return CV_OK;
 }
@@ -1438,6 +1466,86 @@ CV_API cv_status cv_decode_forced_components(cv_hmm* h, int64_t nseq, const int6
   build_conseq(nseq, offsets, component, cs);
   return forced_decode_locked(h, nseq, offsets, obs, component, comp_state, o, cs, false, path_out, score_out,
                               status_out, objective_out);
+}
+
+CV_API cv_status cv_decode_constrained_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host,
+                                              const int64_t* offsets_dev, const int32_t* obs_dev,
+                                              const int32_t* component, int32_t ncomp, const cv_opts* opts,
+                                              int32_t* path_dev, double* score_dev, uint8_t* status_dev,
+                                              int32_t* comp_state_out, double* objective_out) {
+  if (!h) return set_err(CV_EINVAL, "null handle");
+  if (nseq < 0 || ncomp < 0 || (nseq > 0 && (!offsets_host || !offsets_dev || !obs_dev || !component || !path_dev ||
+                                             !score_dev || !status_dev)) || (ncomp > 0 && !comp_state_out))
+    return set_err(CV_EINVAL, "null argument");
+  std::lock_guard<std::mutex> lk(h->mu);
+  cv_status st = set_device(h);
+  if (st != CV_OK) return st;
+  cv_opts o = opts ? *opts : default_opts();
+  for (int32_t c = 0; c < ncomp; ++c) comp_state_out[c] = -1;
+  if (objective_out) *objective_out = 0.0;
+  if (o.dtype != CV_DTYPE_F32 || o.assoc != CV_ASSOC_VITERBI || !cvk::trellis_padded_states(h->N))
+    return set_err(CV_EUNSUPPORTED, "constrained decode runs on the f32 VITERBI trellis path (N <= 256)");
+  if (o.forced) return set_err(CV_EINVAL, "opts->forced is set by the constrained decode itself");
+  if (nseq == 0) return CV_OK;
+  if ((st = check_batch(h, nseq, offsets_host)) != CV_OK) return st;
+  {
+    const int64_t k = first_bad(offsets_host[0], offsets_host[nseq],
+                                [&](int64_t i) { return component[i] < -1 || component[i] >= ncomp; });
+    if (k >= 0)
+      return set_err(CV_EINVAL, "component[%lld] = %d out of range [-1,%d)", (long long)k, component[k], ncomp);
+  }
+  hipStream_t stream = o.stream ? (hipStream_t)o.stream : h->stream;
+  // the host API rejects a bad observation before any term is computed: same here, on the device
+  if ((st = h->cs_zero.ensure(8)) != CV_OK) return st;
+  {
+    const hipError_t err = cvk::launch_obs_first_bad(obs_dev, offsets_host[0], offsets_host[nseq], h->V,
+                                                     h->cs_zero.as<unsigned long long>(), stream);
+    if (err != hipSuccess) return set_err(CV_EDEVICE, "observation check failed: %s", hipGetErrorString(err));
+    unsigned long long first = 0;
+    HIP_TRY(hipMemcpyAsync(&first, h->cs_zero.p, 8, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipStreamSynchronize(stream));
+    if (first != ~0ull) return set_err(CV_EINVAL, "obs[%llu] out of range [0,%lld)", first, (long long)h->V);
+  }
+  std::vector<ConSeq> cs;
+  build_conseq(nseq, offsets_host, component, cs);
+  trace_mark("device constrained: checks + constrained list");
+  const std::vector<int32_t> pairs = conseq_pairs(cs, component);
+  const int64_t npairs = (int64_t)pairs.size() / 2;
+  std::vector<int64_t> part((size_t)cvcsp::partial_words((int)h->N, ncomp, npairs), 0);
+  if ((st = constrained_partials_locked(h, nseq, offsets_host, nullptr, component, ncomp, pairs.data(), npairs, o,
+                                        part.data(), &cs, nullptr, obs_dev)) != CV_OK)
+    return st;
+  uint64_t explored = 0;
+  if ((st = select_locked((int32_t)h->N, ncomp, pairs.data(), npairs, part.data(), comp_state_out, &explored)) !=
+      CV_OK)
+    return st;
+  h->last_explored = explored;
+  trace_mark("select");
+  if ((st = stage_forced_locked(h, offsets_host, nseq, component, comp_state_out, cs, stream)) != CV_OK) return st;
+  o.forced = h->st_forced.as<int32_t>();
+  if ((st = decode_device(h, nseq, offsets_host, offsets_dev, obs_dev, o, path_dev, score_dev, status_dev, stream)) !=
+      CV_OK) {
+    (void)hipStreamSynchronize(stream);
+    return st;
+  }
+  // scores/statuses to the host for the objective (9 B per sequence), fixed up, and back
+  std::vector<double> sc((size_t)nseq);
+  std::vector<uint8_t> ss((size_t)nseq);
+  HIP_TRY(hipMemcpyAsync(sc.data(), score_dev, (size_t)nseq * 8, hipMemcpyDeviceToHost, stream));
+  HIP_TRY(hipMemcpyAsync(ss.data(), status_dev, (size_t)nseq, hipMemcpyDeviceToHost, stream));
+  HIP_TRY(hipStreamSynchronize(stream));
+  const double obj = mark_unassigned(nseq, component, comp_state_out, cs, sc.data(), ss.data());
+  if (objective_out) *objective_out = obj;
+  bool fixed = false;
+  for (const auto& c : cs)
+    for (int64_t e : c.elems) fixed |= comp_state_out[component[e]] < 0;
+  if (fixed) {
+    HIP_TRY(hipMemcpyAsync(score_dev, sc.data(), (size_t)nseq * 8, hipMemcpyHostToDevice, stream));
+    HIP_TRY(hipMemcpyAsync(status_dev, ss.data(), (size_t)nseq, hipMemcpyHostToDevice, stream));
+    HIP_TRY(hipStreamSynchronize(stream));
+  }
+  trace_mark("forced decode (device)");
+  return CV_OK;
 }
 
 CV_API cv_status cv_last_timing(cv_hmm* h, cv_timing* out) {

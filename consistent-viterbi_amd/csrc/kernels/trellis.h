@@ -120,6 +120,10 @@ hipError_t launch_max_marginal(int np, const MaxMarginalArgs& a, int64_t ncon, h
 hipError_t launch_scatter_forced(const int64_t* elems, const int32_t* states, int64_t n, int32_t* forced,
                                  hipStream_t stream);
 
+// *first = the first element index in [lo, hi) with obs outside [0, V), or ~0 (all valid).
+hipError_t launch_obs_first_bad(const int32_t* obs, int64_t lo, int64_t hi, int64_t V, unsigned long long* first,
+                                hipStream_t stream);
+
 int trellis_padded_states(int n);  // 0 if the trellis kernel does not cover n
 hipError_t launch_trellis_fwd(int np, const TrellisFwdArgs& fa, int64_t nseq, hipStream_t stream);
 // Two equal-length sequences per workgroup (slots seq_begin + 2k, +2k+1), plain decode only;

@@ -1491,6 +1491,30 @@ hipError_t launch_scatter_forced(const int64_t* elems, const int32_t* states, in
   return hipGetLastError();
 }
 
+// First out-of-range observation in [lo, hi) (device API of the constrained decode, which
+// must reject a bad batch before any term is computed, like the host API does): grid-stride
+// scan, one u64 atomicMin per wave that saw one; *first stays INT64_MAX when all are valid.
+__global__ void obs_first_bad(const int32_t* obs, int64_t lo, int64_t hi, uint32_t V,
+                              unsigned long long* first) {
+  unsigned long long mine = ~0ull;
+  for (int64_t i = lo + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < hi; i += (int64_t)gridDim.x * blockDim.x)
+    if ((uint32_t)obs[i] >= V && (unsigned long long)i < mine) mine = (unsigned long long)i;
+  for (int o = 32; o > 0; o >>= 1) {
+    const unsigned long long other = __shfl_xor(mine, o);
+    mine = other < mine ? other : mine;
+  }
+  if ((threadIdx.x & 63) == 0 && mine != ~0ull) atomicMin(first, mine);
+}
+
+hipError_t launch_obs_first_bad(const int32_t* obs, int64_t lo, int64_t hi, int64_t V, unsigned long long* first,
+                                hipStream_t stream) {
+  hipError_t e = hipMemsetAsync(first, 0xFF, sizeof(unsigned long long), stream);
+  if (e != hipSuccess || hi <= lo) return e;
+  const int64_t want = (hi - lo + 255) / 256, blocks = want < 4096 ? want : 4096;
+  hipLaunchKernelGGL(obs_first_bad, dim3((unsigned)blocks), dim3(256), 0, stream, obs, lo, hi, (uint32_t)V, first);
+  return hipGetLastError();
+}
+
 int trellis_padded_states(int n) {
   if (n <= 0 || n > 256) return 0;
   return ((n + 31) / 32) * 32;

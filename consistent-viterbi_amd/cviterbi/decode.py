@@ -172,6 +172,27 @@ def decode_batch_device(hmm: HMM, offsets_dev, obs_dev, path_dev, score_dev, sta
                                            ptr(status_dev)))
 
 
+def decode_constrained_device(hmm: HMM, offsets_host, offsets_dev, obs_dev, component, path_dev, score_dev, status_dev,
+                              ncomp=None, rescore_f64=True, stream=None, workspace_bytes=0):
+    """cv_decode_constrained_device: observations and outputs in HBM (ints or objects with
+    data_ptr()), offsets_host/component on the host.  Synchronous.  Returns
+    (comp_state[ncomp], objective)."""
+    def ptr(x):
+        return x.data_ptr() if hasattr(x, "data_ptr") else int(x)
+
+    oh = np.ascontiguousarray(offsets_host, np.int64)
+    component = np.ascontiguousarray(component, np.int32)
+    if ncomp is None:
+        ncomp = int(component.max()) + 1 if component.size else 0
+    states = np.full(max(ncomp, 1), -1, np.int32)
+    obj = ctypes.c_double()
+    o = make_opts("f32", "viterbi", "auto", rescore_f64, stream, workspace_bytes)
+    L.check(L.lib().cv_decode_constrained_device(hmm.handle, oh.shape[0] - 1, _p(oh), ptr(offsets_dev), ptr(obs_dev),
+                                                 _p(component), int(ncomp), ctypes.byref(o), ptr(path_dev),
+                                                 ptr(score_dev), ptr(status_dev), _p(states), ctypes.byref(obj)))
+    return states[:ncomp], obj.value
+
+
 def last_timing(hmm: HMM) -> dict:
     t = L.Timing()
     L.check(L.lib().cv_last_timing(hmm.handle, ctypes.byref(t)))

@@ -8,8 +8,8 @@ Mirrors (file:line into /root/reference/src):
   load_sequences / load_tags        utils.rs:7-60
   main's output file                main.rs:111-133
 Decoding goes through cv_solver_* (libcviterbi).  Active consistency constraints use
-cv_decode_constrained (exact when every sequence holds at most one active constrained
-element; more than one per sequence -> CV_EUNSUPPORTED).
+cv_decode_constrained (exact for any number of active constrained elements per
+sequence: unary + pairwise component terms and an exact search).
 """
 from __future__ import annotations
 

@@ -193,6 +193,16 @@ CV_API cv_status cv_decode_constrained(cv_hmm* h, int64_t nseq, const int64_t* o
                                        const int32_t* component, int32_t ncomp, const cv_opts* opts,
                                        int32_t* path_out, double* score_out, uint8_t* status_out,
                                        int32_t* comp_state_out, double* objective_out);
+/* The same on device-resident inputs/outputs (offsets_dev/obs_dev in HBM, path_dev/score_dev/
+ * status_dev written there; offsets_host and component stay on the host: the search's
+ * structure is host work).  Observation indices are range-checked on the device before any
+ * term is computed (CV_EINVAL, as the host API).  Enqueued on opts->stream (or the handle's
+ * stream); synchronous: returns after the decode has finished. */
+CV_API cv_status cv_decode_constrained_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host,
+                                              const int64_t* offsets_dev, const int32_t* obs_dev,
+                                              const int32_t* component, int32_t ncomp, const cv_opts* opts,
+                                              int32_t* path_dev, double* score_dev, uint8_t* status_dev,
+                                              int32_t* comp_state_out, double* objective_out);
 /* The same decode split at its one exchange step, for a batch sharded over processes/GPUs:
  * 0. cv_constrained_pairs (host only) on the FULL batch: the sorted component pairs (c1 < c2)
  *    that are consecutive constrained elements of some sequence -- the layout every rank

@@ -265,3 +265,44 @@ def test_device_exact_sums_equal_host(gpu, monkeypatch, n, seed):
     monkeypatch.setenv("CV_HOST_SUMS", "1")
     host = cv.constrained_partials(h, off, obs, comp, 5, pairs)
     assert np.array_equal(dev, host)
+
+
+@pytest.mark.parametrize("n,seed", [(5, 11), (64, 12), (256, 13)])
+def test_constrained_device_equals_host(gpu, n, seed):
+    """cv_decode_constrained_device (inputs/outputs in HBM) == cv_decode_constrained, incl.
+    several constrained positions per sequence and an unassignable component."""
+    import torch
+    pi, a, b = synth.random_hmm(n, 9, seed=seed)
+    rng = np.random.default_rng(seed)
+    off = synth.offsets_from_lengths(rng.integers(1, 48, size=40))
+    obs = rng.integers(0, 9, size=int(off[-1])).astype(np.int32)
+    comp = synth.constraint_components(off, seed=seed, ncomp=4, prob=0.7)
+    h = cv.HMM(pi, a, b)
+    ref = cv.decode_constrained(h, off, obs, comp, ncomp=5)  # component 4 has no element
+    dev = torch.device("cuda", 0)
+    path_d = torch.empty(int(off[-1]), dtype=torch.int32, device=dev)
+    score_d = torch.empty(len(off) - 1, dtype=torch.float64, device=dev)
+    status_d = torch.empty(len(off) - 1, dtype=torch.uint8, device=dev)
+    states, obj = cv.decode_constrained_device(h, off, torch.from_numpy(off).to(dev), torch.from_numpy(obs).to(dev),
+                                               comp, path_d, score_d, status_d, ncomp=5)
+    assert np.array_equal(states, ref[3])
+    assert np.array_equal(path_d.cpu().numpy(), ref[0])
+    assert np.array_equal(score_d.cpu().numpy(), ref[1])
+    assert np.array_equal(status_d.cpu().numpy(), ref[2])
+    assert obj == ref[4]
+
+
+def test_constrained_device_rejects_bad_obs(gpu):
+    import torch
+    pi, a, b = synth.random_hmm(8, 5, seed=1)
+    off = np.array([0, 10, 20], np.int64)
+    obs = np.zeros(20, np.int32)
+    obs[13] = 5
+    comp = np.full(20, -1, np.int32)
+    comp[3] = 0
+    dev = torch.device("cuda", 0)
+    h = cv.HMM(pi, a, b)
+    out = [torch.empty(20, dtype=torch.int32, device=dev), torch.empty(2, dtype=torch.float64, device=dev),
+           torch.empty(2, dtype=torch.uint8, device=dev)]
+    with pytest.raises(cv.CVError, match=r"obs\[13\]"):
+        cv.decode_constrained_device(h, off, torch.from_numpy(off).to(dev), torch.from_numpy(obs).to(dev), comp, *out)

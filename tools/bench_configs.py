@@ -2,9 +2,9 @@
 DESIGN.md; bench.py keeps config 4 as the headline):
   c2  N=45,  V=50,000, T~U[1,128], B=4,096          (plain decode, f32 + f64 re-score)
   c3  N=64,  V=256,    T~U[32,1024], B=16,384       (plain decode, length-sorted schedule)
-  c5  config 4 + one constrained position in half the sequences, K=7 (cv_decode_constrained)
-Inputs resident in HBM for c2/c3 (device API); c5 goes through the host API (its exact
-search runs on the host between the GPU passes), so its line includes PCIe transfers.
+  c5  config 4 + one constrained position in half the sequences, K=7
+      (cv_decode_constrained_device; "c5host": the host-pointer cv_decode_constrained)
+Inputs resident in HBM (device APIs) except c5host, whose line includes PCIe transfers.
 Prints one JSON line per config."""
 import json
 import os
@@ -27,7 +27,7 @@ stream = torch.cuda.Stream(dev)
 torch.cuda.set_stream(stream)
 
 for name in which:
-    c = synth.config(name)
+    c = synth.config("c5" if name == "c5host" else name)
     n = c["pi"].shape[0]
     off, obs = c["offsets"], c["obs"]
     B = len(off) - 1
@@ -41,11 +41,21 @@ for name in which:
 
         def run():
             cv.decode_batch_device(h, o_d, ob_d, p_d, s_d, st_d, offsets_host=off, stream=stream.cuda_stream)
-    else:
+    elif name == "c5host":
         comp = c["component"]
 
         def run():
             cv.decode_constrained(h, off, obs, comp, 7)
+    else:
+        comp = c["component"]
+        o_d, ob_d = torch.from_numpy(off).to(dev), torch.from_numpy(obs).to(dev)
+        p_d = torch.empty(len(obs), dtype=torch.int32, device=dev)
+        s_d = torch.empty(B, dtype=torch.float64, device=dev)
+        st_d = torch.empty(B, dtype=torch.uint8, device=dev)
+
+        def run():
+            cv.decode_constrained_device(h, off, o_d, ob_d, comp, p_d, s_d, st_d, ncomp=7,
+                                         stream=stream.cuda_stream)
     run()
     run()
     torch.cuda.synchronize()
