@@ -125,6 +125,10 @@ struct cv_hmm {
   DevBuf st_off, st_obs, st_path, st_score, st_status, st_forced;
   DevBuf cs_ranges, cs_delta, cs_g, cs_mu, cs_start, cs_zero;  // constrained-decode scratch
   DevBuf cs_comp, cs_words;  // device exact unary sums: per-sequence components, output words
+  DevBuf cs_seg;             // segment-table rows (cs_delta keeps the prefix rows t_1)
+  // resume flow of the constrained decode: stored prefix rows, forced row t_1 per constrained
+  // sequence, the compact suffix batch and its index arrays
+  DevBuf rs_rows, rs_rowbase, rs_resume, rs_start, rs_off2, rs_ridx, rs_slot, rs_obs2, rs_frc2, rs_path2;
   std::vector<int32_t> order_host;
   std::vector<float> host_dl, host_mu;  // constrained-decode term rows (kept: no per-call page faults)
   // timing events of the last call
@@ -414,7 +418,7 @@ cvk::BacktrackArgs make_bt_args(cv_hmm* h, unsigned char* wsb, const int64_t* of
 // Core device-side decode.  All pointers are device pointers except offsets_host.
 cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, const int64_t* offsets_dev,
                         const int32_t* obs_dev, const cv_opts& o, int32_t* path_dev, double* score_dev,
-                        uint8_t* status_dev, hipStream_t stream) {
+                        uint8_t* status_dev, hipStream_t stream, const float* resume_rows = nullptr) {
   if (o.dtype != CV_DTYPE_F32 && o.dtype != CV_DTYPE_F64) return set_err(CV_EINVAL, "bad dtype %d", o.dtype);
   if (o.assoc < CV_ASSOC_VITERBI || o.assoc > CV_ASSOC_DECODE) return set_err(CV_EINVAL, "bad assoc %d", o.assoc);
   const bool trellis_ok = o.dtype == CV_DTYPE_F32 && o.assoc == CV_ASSOC_VITERBI &&
@@ -601,6 +605,7 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
       fa.status = status_dev;
       fa.nobs = (int)h->V;
       fa.forced = o.forced;
+      fa.resume_rows = resume_rows;
       if (wave) {
         fa.a_img = h->w_arm.as<float>();
         fa.pi = h->w_pi.as<float>();
@@ -1007,10 +1012,28 @@ cv_status constrained_validate(cv_hmm* h, int64_t nseq, const int64_t* offsets, 
 //           pair (c_k, c_{k+1}) (or the diagonal into the unary when c_k == c_{k+1}).
 // `pre`: the caller's already validated constrained-sequence list (else validated here);
 // on return *obs_staged tells whether h->st_obs holds the batch's observations.
+// What the terms pass leaves on the device for the resume flow (forced_decode_resume): the
+// delta rows of every prefix [offsets[seq], t_1] (h->rs_rows, slot i from row row_base[i]) and
+// row t_1 itself (h->cs_delta row i).
+struct PrefixKeep {
+  bool kept = false;
+  std::vector<int64_t> seq, t1, row_base;  // per terms slot i
+};
+
+// The resume flow covers N > 64 with NP % 64 == 0 (pair kernel + backtrack_v); its stored rows
+// must fit 4x the workspace cap (32 GiB by default: config 5 needs 8.6 GB).
+bool resume_supported(const cv_hmm* h) {
+  const char* e = getenv("CV_NO_RESUME");
+  if (e && *e && *e != '0') return false;
+  return h->N > 64 && (h->np == 128 || h->np == 192 || h->np == 256);
+}
+
 cv_status constrained_partials_locked(cv_hmm* h, int64_t nseq, const int64_t* offsets, const int32_t* obs,
                                       const int32_t* component, int32_t ncomp, const int32_t* pairs, int64_t npairs,
                                       cv_opts& o, int64_t* part, const std::vector<ConSeq>* pre = nullptr,
-                                      bool* obs_staged = nullptr, const int32_t* obs_dev = nullptr) {
+                                      bool* obs_staged = nullptr, const int32_t* obs_dev = nullptr,
+                                      PrefixKeep* keep = nullptr) {
+  if (keep) *keep = PrefixKeep{};
   if (obs_staged) *obs_staged = false;
   std::vector<ConSeq> own;
   cv_status st = CV_OK;
@@ -1067,7 +1090,7 @@ cv_status constrained_partials_locked(cv_hmm* h, int64_t nseq, const int64_t* of
   }
   const int64_t nslot_max = std::max<int64_t>(nc, std::min<int64_t>(kSegmentSlots, (int64_t)seg_pair.size() * N));
   if ((st = h->cs_ranges.ensure(std::max(rg.size(), (size_t)nslot_max * 2) * 8)) != CV_OK) return st;
-  if ((st = h->cs_delta.ensure((size_t)nslot_max * np * 4)) != CV_OK) return st;
+  if ((st = h->cs_delta.ensure((size_t)nc * np * 4)) != CV_OK) return st;
   if ((st = h->cs_g.ensure((size_t)nc * np * 4)) != CV_OK) return st;
   if ((st = h->cs_mu.ensure((size_t)nc * np * 4)) != CV_OK) return st;
   if ((st = h->cs_zero.ensure((size_t)nc * np * 4)) != CV_OK) return st;
@@ -1091,6 +1114,27 @@ cv_status constrained_partials_locked(cv_hmm* h, int64_t nseq, const int64_t* of
   fa.a_img2 = h->t_aimg_T.as<float>();
   fa.pi2 = h->t_pi0.as<float>();
   fa.last_row2 = h->cs_g.as<float>();
+  if (keep && resume_supported(h)) {  // prefix rows stay on the device for the final decode
+    std::vector<int64_t> rb((size_t)nc);
+    int64_t rows = 0;
+    for (int64_t i = 0; i < nc; ++i) rb[(size_t)i] = rows, rows += rg[2 * i + 1] - rg[2 * i];
+    const uint64_t cap = 4 * (o.workspace_bytes ? o.workspace_bytes : kDefaultWorkspace);
+    if ((uint64_t)rows * np * 4 <= cap) {
+      if ((st = h->rs_rows.ensure((size_t)std::max<int64_t>(rows, 1) * np * 4)) != CV_OK) return st;
+      if ((st = h->rs_rowbase.ensure((size_t)nc * 8)) != CV_OK) return st;
+      HIP_TRY(hipMemcpyAsync(h->rs_rowbase.p, rb.data(), (size_t)nc * 8, hipMemcpyHostToDevice, stream));
+      fa.delta = h->rs_rows.as<float>();
+      fa.row_base = h->rs_rowbase.as<int64_t>();
+      keep->kept = true;
+      keep->row_base = std::move(rb);
+      keep->seq.resize((size_t)nc);
+      keep->t1.resize((size_t)nc);
+      for (int64_t i = 0; i < nc; ++i) {
+        keep->seq[(size_t)i] = order[i]->seq;
+        keep->t1[(size_t)i] = order[i]->elems.front();
+      }
+    }
+  }
   {
     std::vector<int32_t> so((size_t)2 * nc);
     std::iota(so.begin(), so.end(), 0);
@@ -1237,11 +1281,12 @@ cv_status constrained_partials_locked(cv_hmm* h, int64_t nseq, const int64_t* of
     sa.nobs = (int)h->V;
     sa.ranges = h->cs_ranges.as<int64_t>();
     sa.start = h->cs_start.as<int32_t>();
-    sa.last_row = h->cs_delta.as<float>();
+    if ((st = h->cs_seg.ensure((size_t)nb * np * 4)) != CV_OK) return st;
+    sa.last_row = h->cs_seg.as<float>();
     if ((err = cvk::launch_trellis_fwd(np, sa, nb, stream)) != hipSuccess)
       return set_err(CV_EDEVICE, "segment-table launch failed: %s", hipGetErrorString(err));
     rows.resize((size_t)nb * np);
-    HIP_TRY(hipMemcpyAsync(rows.data(), h->cs_delta.p, rows.size() * 4, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipMemcpyAsync(rows.data(), h->cs_seg.p, rows.size() * 4, hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipStreamSynchronize(stream));
     for (int64_t k = 0; k < nb; ++k) {
       const Seg& sg = segs[(b0 + k) / N];
@@ -1329,6 +1374,105 @@ cv_status forced_decode_locked(cv_hmm* h, int64_t nseq, const int64_t* offsets, 
   trace_mark("forced decode (sync)");
   const double obj = mark_unassigned(nseq, component, comp_state, cs, score_out, status_out);
   if (objective_out) *objective_out = obj;
+  return CV_OK;
+}
+
+// Final decode of the resume flow (see kernels/trellis.hip "resume flow"): the terms pass
+// stored every constrained sequence's prefix rows, so the decode runs [t_1, end) of those
+// sequences (from row t_1 with the chosen state forced) and whole unconstrained sequences as
+// one compact batch; then the suffix paths are scattered back, each prefix path is backtracked
+// from its forced state, and every path is re-scored in f64 over its whole sequence.
+// Bit-identical to forced_decode_locked's full forced decode.  Device pointers; synchronous.
+cv_status forced_decode_resume(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, const int64_t* offsets_dev,
+                               const int32_t* obs_dev, const int32_t* component, const int32_t* comp_state,
+                               const std::vector<ConSeq>& cs, const PrefixKeep& keep, cv_opts o, int32_t* path_dev,
+                               double* score_dev, uint8_t* status_dev, hipStream_t stream) {
+  cv_status st;
+  if ((st = stage_forced_locked(h, offsets_host, nseq, component, comp_state, cs, stream)) != CV_OK) return st;
+  const int64_t nc = (int64_t)keep.seq.size();
+  const int np = h->np;
+  std::vector<int64_t> start(offsets_host, offsets_host + nseq), off2((size_t)nseq + 1);
+  std::vector<int32_t> ridx((size_t)nseq, -1), state((size_t)nc);
+  for (int64_t i = 0; i < nc; ++i) {
+    start[(size_t)keep.seq[i]] = keep.t1[i];
+    ridx[(size_t)keep.seq[i]] = (int32_t)i;
+    const int32_t c = comp_state[component[keep.t1[i]]];
+    state[(size_t)i] = c >= 0 ? c : 0;  // no state: forced to 0 and marked infeasible (mark_unassigned)
+  }
+  off2[0] = 0;
+  for (int64_t s = 0; s < nseq; ++s) off2[(size_t)s + 1] = off2[(size_t)s] + offsets_host[s + 1] - start[(size_t)s];
+  const int64_t total2 = off2[(size_t)nseq];
+  // per-slot arrays: [seq | t1 | row_base] int64, then state int32
+  std::vector<int64_t> slot64((size_t)nc * 3);
+  std::copy(keep.seq.begin(), keep.seq.end(), slot64.begin());
+  std::copy(keep.t1.begin(), keep.t1.end(), slot64.begin() + nc);
+  std::copy(keep.row_base.begin(), keep.row_base.end(), slot64.begin() + 2 * nc);
+  if ((st = h->rs_start.ensure((size_t)nseq * 8)) != CV_OK) return st;
+  if ((st = h->rs_off2.ensure((size_t)(nseq + 1) * 8)) != CV_OK) return st;
+  if ((st = h->rs_ridx.ensure((size_t)nseq * 4)) != CV_OK) return st;
+  if ((st = h->rs_slot.ensure((size_t)std::max<int64_t>(nc, 1) * 28)) != CV_OK) return st;
+  if ((st = h->rs_resume.ensure((size_t)std::max<int64_t>(nc, 1) * np * 4)) != CV_OK) return st;
+  if ((st = h->rs_obs2.ensure((size_t)std::max<int64_t>(total2, 1) * 4)) != CV_OK) return st;
+  if ((st = h->rs_frc2.ensure((size_t)std::max<int64_t>(total2, 1) * 4)) != CV_OK) return st;
+  if ((st = h->rs_path2.ensure((size_t)std::max<int64_t>(total2, 1) * 4)) != CV_OK) return st;
+  int64_t* slot_d = h->rs_slot.as<int64_t>();
+  int32_t* state_d = reinterpret_cast<int32_t*>(slot_d + 3 * nc);
+  HIP_TRY(hipMemcpyAsync(h->rs_start.p, start.data(), (size_t)nseq * 8, hipMemcpyHostToDevice, stream));
+  HIP_TRY(hipMemcpyAsync(h->rs_off2.p, off2.data(), (size_t)(nseq + 1) * 8, hipMemcpyHostToDevice, stream));
+  HIP_TRY(hipMemcpyAsync(h->rs_ridx.p, ridx.data(), (size_t)nseq * 4, hipMemcpyHostToDevice, stream));
+  if (nc > 0) {
+    HIP_TRY(hipMemcpyAsync(slot_d, slot64.data(), (size_t)nc * 24, hipMemcpyHostToDevice, stream));
+    HIP_TRY(hipMemcpyAsync(state_d, state.data(), (size_t)nc * 4, hipMemcpyHostToDevice, stream));
+  }
+  hipError_t err = cvk::launch_resume_rows(h->cs_delta.as<float>(), state_d, nc, np, h->rs_resume.as<float>(), stream);
+  if (err == hipSuccess)
+    err = cvk::launch_compact_suffix(offsets_dev, h->rs_start.as<int64_t>(), h->rs_off2.as<int64_t>(), obs_dev,
+                                     h->st_forced.as<int32_t>(), h->rs_ridx.as<int32_t>(), h->rs_obs2.as<int32_t>(),
+                                     h->rs_frc2.as<int32_t>(), nseq, stream);
+  if (err != hipSuccess) return set_err(CV_EDEVICE, "resume staging failed: %s", hipGetErrorString(err));
+  trace_mark("resume: compact suffix batch");
+  cv_opts o2 = o;
+  o2.forced = h->rs_frc2.as<int32_t>();
+  o2.rescore_f64 = 0;  // re-scored below over the whole sequences
+  if ((st = decode_device(h, nseq, off2.data(), h->rs_off2.as<int64_t>(), h->rs_obs2.as<int32_t>(), o2,
+                          h->rs_path2.as<int32_t>(), score_dev, status_dev, stream, h->rs_resume.as<float>())) !=
+      CV_OK) {
+    (void)hipStreamSynchronize(stream);
+    return st;
+  }
+  err = cvk::launch_scatter_suffix_path(offsets_dev, h->rs_start.as<int64_t>(), h->rs_off2.as<int64_t>(),
+                                        h->rs_path2.as<int32_t>(), path_dev, nseq, stream);
+  if (err == hipSuccess) {
+    cvk::PrefixBtArgs pa{};
+    pa.rows = h->rs_rows.as<float>();
+    pa.seq = slot_d;
+    pa.t1 = slot_d + nc;
+    pa.row_base = slot_d + 2 * nc;
+    pa.state = state_d;
+    pa.offsets = offsets_dev;
+    pa.at = h->t_at.as<float>();
+    pa.status = status_dev;
+    pa.path = path_dev;
+    err = cvk::launch_prefix_backtrack(np, pa, nc, stream);
+  }
+  if (err == hipSuccess && o.rescore_f64) {
+    cvk::RescoreArgs ra{};
+    ra.path = path_dev;
+    ra.obs = obs_dev;
+    ra.offsets = offsets_dev;
+    ra.seq_begin = 0;
+    ra.seq_end = nseq;
+    ra.nstates = h->N;
+    ra.pi64 = h->d_pi64.as<double>();
+    ra.a64 = h->d_a64.as<double>();
+    ra.et64 = h->d_et64.as<double>();
+    ra.status = status_dev;
+    ra.score = score_dev;
+    err = cvk::launch_rescore_f64(ra, nseq, stream);
+  }
+  if (err != hipSuccess) return set_err(CV_EDEVICE, "resume finish failed: %s", hipGetErrorString(err));
+  HIP_TRY(hipStreamSynchronize(stream));  // host index vectors die at return
+  trace_mark("resume: decode + prefix backtrack + re-score");
   return CV_OK;
 }
 
@@ -1423,8 +1567,9 @@ CV_API cv_status cv_decode_constrained(cv_hmm* h, int64_t nseq, const int64_t* o
   const int64_t npairs = (int64_t)pairs.size() / 2;
   std::vector<int64_t> part((size_t)cvcsp::partial_words((int)h->N, ncomp, npairs), 0);
   bool obs_staged = false;
+  PrefixKeep keep;
   if ((st = constrained_partials_locked(h, nseq, offsets, obs, component, ncomp, pairs.data(), npairs, o,
-                                        part.data(), &cs, &obs_staged)) != CV_OK)
+                                        part.data(), &cs, &obs_staged, nullptr, &keep)) != CV_OK)
     return st;
   trace_mark("partials (device + exact sums)");
   uint64_t explored = 0;
@@ -1433,6 +1578,28 @@ CV_API cv_status cv_decode_constrained(cv_hmm* h, int64_t nseq, const int64_t* o
     return st;
   h->last_explored = explored;
   trace_mark("select");
+  if (keep.kept && obs_staged) {  // resume flow on the staged observations, results copied back
+    hipStream_t stream = o.stream ? (hipStream_t)o.stream : h->stream;
+    const int64_t base = offsets[0], total = offsets[nseq];
+    if ((st = h->st_off.ensure((size_t)(nseq + 1) * 8)) != CV_OK) return st;
+    if ((st = h->st_path.ensure((size_t)std::max<int64_t>(total, 1) * 4)) != CV_OK) return st;
+    if ((st = h->st_score.ensure((size_t)nseq * 8)) != CV_OK) return st;
+    if ((st = h->st_status.ensure((size_t)nseq)) != CV_OK) return st;
+    HIP_TRY(hipMemcpyAsync(h->st_off.p, offsets, (size_t)(nseq + 1) * 8, hipMemcpyHostToDevice, stream));
+    if ((st = forced_decode_resume(h, nseq, offsets, h->st_off.as<int64_t>(), h->st_obs.as<int32_t>(), component,
+                                   comp_state_out, cs, keep, o, h->st_path.as<int32_t>(), h->st_score.as<double>(),
+                                   h->st_status.as<uint8_t>(), stream)) != CV_OK)
+      return st;
+    if (total > base)
+      HIP_TRY(hipMemcpyAsync(path_out + base, h->st_path.as<int32_t>() + base, (size_t)(total - base) * 4,
+                             hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipMemcpyAsync(score_out, h->st_score.p, (size_t)nseq * 8, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipMemcpyAsync(status_out, h->st_status.p, (size_t)nseq, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipStreamSynchronize(stream));
+    const double obj = mark_unassigned(nseq, component, comp_state_out, cs, score_out, status_out);
+    if (objective_out) *objective_out = obj;
+    return CV_OK;
+  }
   return forced_decode_locked(h, nseq, offsets, obs, component, comp_state_out, o, cs, obs_staged, path_out,
                               score_out, status_out, objective_out);
 }
@@ -1512,8 +1679,9 @@ CV_API cv_status cv_decode_constrained_device(cv_hmm* h, int64_t nseq, const int
   const std::vector<int32_t> pairs = conseq_pairs(cs, component);
   const int64_t npairs = (int64_t)pairs.size() / 2;
   std::vector<int64_t> part((size_t)cvcsp::partial_words((int)h->N, ncomp, npairs), 0);
+  PrefixKeep keep;
   if ((st = constrained_partials_locked(h, nseq, offsets_host, nullptr, component, ncomp, pairs.data(), npairs, o,
-                                        part.data(), &cs, nullptr, obs_dev)) != CV_OK)
+                                        part.data(), &cs, nullptr, obs_dev, &keep)) != CV_OK)
     return st;
   uint64_t explored = 0;
   if ((st = select_locked((int32_t)h->N, ncomp, pairs.data(), npairs, part.data(), comp_state_out, &explored)) !=
@@ -1521,12 +1689,18 @@ CV_API cv_status cv_decode_constrained_device(cv_hmm* h, int64_t nseq, const int
     return st;
   h->last_explored = explored;
   trace_mark("select");
-  if ((st = stage_forced_locked(h, offsets_host, nseq, component, comp_state_out, cs, stream)) != CV_OK) return st;
-  o.forced = h->st_forced.as<int32_t>();
-  if ((st = decode_device(h, nseq, offsets_host, offsets_dev, obs_dev, o, path_dev, score_dev, status_dev, stream)) !=
-      CV_OK) {
-    (void)hipStreamSynchronize(stream);
-    return st;
+  if (keep.kept) {
+    if ((st = forced_decode_resume(h, nseq, offsets_host, offsets_dev, obs_dev, component, comp_state_out, cs, keep,
+                                   o, path_dev, score_dev, status_dev, stream)) != CV_OK)
+      return st;
+  } else {
+    if ((st = stage_forced_locked(h, offsets_host, nseq, component, comp_state_out, cs, stream)) != CV_OK) return st;
+    o.forced = h->st_forced.as<int32_t>();
+    if ((st = decode_device(h, nseq, offsets_host, offsets_dev, obs_dev, o, path_dev, score_dev, status_dev,
+                            stream)) != CV_OK) {
+      (void)hipStreamSynchronize(stream);
+      return st;
+    }
   }
   // scores/statuses to the host for the objective (9 B per sequence), fixed up, and back
   std::vector<double> sc((size_t)nseq);

@@ -37,6 +37,12 @@ struct TrellisFwdArgs {
   const float* pi2;
   float* last_row2;
   const int32_t* slot_order;
+  // constrained decode, resume flow (cviterbi.cpp forced_decode_resume):
+  const int64_t* row_base;   // EXT, ranged slots < split: delta row index of the range's first
+                             // element (instead of e0 - delta_elem_base); slots >= split then
+                             // write no delta rows
+  const float* resume_rows;  // forced[e0] = -2 - r (r >= 0): row 0 of the sequence is
+                             // resume_rows[r][:] (already forced), not pi + b
 };
 
 struct BacktrackArgs {
@@ -123,6 +129,32 @@ hipError_t launch_scatter_forced(const int64_t* elems, const int32_t* states, in
 // *first = the first element index in [lo, hi) with obs outside [0, V), or ~0 (all valid).
 hipError_t launch_obs_first_bad(const int32_t* obs, int64_t lo, int64_t hi, int64_t V, unsigned long long* first,
                                 hipStream_t stream);
+
+// Resume flow of the constrained decode (forced_decode_resume in cviterbi.cpp):
+// out[i][j] = j == state[i] ? last[i][j] : -inf  (row t_1 of sequence i, forced), np <= 256
+hipError_t launch_resume_rows(const float* last, const int32_t* state, int64_t n, int np, float* out,
+                              hipStream_t stream);
+// compact suffix batch: sequence s keeps elements [start[s], off[s+1]) at off2[s]; forced2 of
+// its first element = -2 - ridx[s] when ridx[s] >= 0 (resume row), else forced[start[s]]
+hipError_t launch_compact_suffix(const int64_t* off, const int64_t* start, const int64_t* off2, const int32_t* obs,
+                                 const int32_t* forced, const int32_t* ridx, int32_t* obs2, int32_t* forced2,
+                                 int64_t nseq, hipStream_t stream);
+// path[start[s] + k] = path2[off2[s] + k]
+hipError_t launch_scatter_suffix_path(const int64_t* off, const int64_t* start, const int64_t* off2,
+                                      const int32_t* path2, int32_t* path, int64_t nseq, hipStream_t stream);
+struct PrefixBtArgs {
+  const float* rows;        // compact prefix delta rows (the terms pass's first pass)
+  const int64_t* row_base;  // [n] first row of slot i
+  const int64_t* seq;       // [n] sequence id of slot i
+  const int64_t* t1;        // [n] element index of the first constrained element
+  const int32_t* state;     // [n] state forced there
+  const int64_t* offsets;   // original CSR offsets
+  const float* at;          // [NP][NP]
+  const uint8_t* status;    // final statuses (sequences not OK: prefix path zeroed)
+  int32_t* path;
+};
+// path[off[seq] .. t1] of every slot: backtrack from `state` at t1 through the stored prefix rows
+hipError_t launch_prefix_backtrack(int np, const PrefixBtArgs& a, int64_t n, hipStream_t stream);
 
 int trellis_padded_states(int n);  // 0 if the trellis kernel does not cover n
 hipError_t launch_trellis_fwd(int np, const TrellisFwdArgs& fa, int64_t nseq, hipStream_t stream);

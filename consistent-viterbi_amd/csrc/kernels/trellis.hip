@@ -188,7 +188,10 @@ __global__ __launch_bounds__(NP * 4) void trellis_fwd_f32(TrellisFwdArgs args) {
       (const __attribute__((address_space(4))) int32_t*)(args.obs + ob0);
   const __attribute__((address_space(4))) int32_t* frc =
       (const __attribute__((address_space(4))) int32_t*)((EXT && args.forced) ? args.forced + ob0 : nullptr);
-  float* __restrict__ drow = (!EXT || args.delta) ? args.delta + (e0 - args.delta_elem_base) * NP + jw : nullptr;
+  float* __restrict__ drow = !EXT ? args.delta + (e0 - args.delta_elem_base) * NP + jw
+                             : (args.delta && !second)
+                                 ? args.delta + (args.row_base ? args.row_base[slot] : e0 - args.delta_elem_base) * NP + jw
+                                 : nullptr;
   float* __restrict__ lrow = !EXT ? nullptr
                              : second ? args.last_row2 + (slot - args.split) * NP + jw
                              : args.last_row ? args.last_row + (slot - args.seq_begin) * NP + jw : nullptr;
@@ -237,7 +240,12 @@ __global__ __launch_bounds__(NP * 4) void trellis_fwd_f32(TrellisFwdArgs args) {
       const int s = args.start[slot - args.seq_begin];
       if (s >= 0) d0 = (jw == s) ? 0.0f : ninf_f();
     }
-    d0 = force(d0, frc_s(0));
+    int f0 = frc_s(0);
+    if (EXT && f0 <= -2) {  // resume: row t_1 of the prefix pass, already forced
+      d0 = args.resume_rows[(size_t)(-2 - f0) * NP + jw];
+      f0 = -1;
+    }
+    d0 = force(d0, f0);
     if (writer) {
       lds_delta[0][lds_w] = d0;
       if (!EXT || drow) *drow = d0;
@@ -407,7 +415,18 @@ __global__ __launch_bounds__(NP * 4) void trellis_fwd2_f32(TrellisFwdArgs args) 
   {
     const float ex = et_row(obs_x(0)), ey = et_row(obs_y(0));
     const float p = args.pi[jw];
-    const float dx = force(p + ex, FRC ? frcX[0] : -1), dy = force(p + ey, FRC ? frcY[0] : -1);
+    int fx = FRC ? frcX[0] : -1, fy = FRC ? frcY[0] : -1;
+    float dx = p + ex, dy = p + ey;
+    if (FRC && fx <= -2) {  // resume: row t_1 of the prefix pass, already forced
+      dx = args.resume_rows[(size_t)(-2 - fx) * NP + jw];
+      fx = -1;
+    }
+    if (FRC && fy <= -2) {
+      dy = args.resume_rows[(size_t)(-2 - fy) * NP + jw];
+      fy = -1;
+    }
+    dx = force(dx, fx);
+    dy = force(dy, fy);
     if (writer) {
       lds[0][0][lds_w] = dx;
       lds[1][0][lds_w] = dy;
@@ -922,7 +941,7 @@ __device__ __forceinline__ int first_argmax_vl(const float (&s)[VL], float M, in
 template <int VL, int NP>
 __device__ __forceinline__ void backtrack_one(const BacktrackArgs& args, int64_t seq, int64_t e0, int T, int lane,
                                               const float* __restrict__ drow, const float* __restrict__ at,
-                                              bool badobs) {
+                                              bool badobs, int fixed_last = -1, bool record = true) {
   constexpr int PF = 8;
   // NP < 64 (one-wave kernels with 16/32/48 padded states): lanes >= NP hold no state
   const bool own = NP >= 64 * VL || lane < NP;
@@ -945,7 +964,10 @@ __device__ __forceinline__ void backtrack_one(const BacktrackArgs& args, int64_t
   // first argmax of the last row (cp.rs:86)
   int cur;
   float bv;
-  {
+  if (fixed_last >= 0) {  // prefix of a resumed sequence: the forced state, known feasible
+    cur = fixed_last;
+    bv = 0.0f;
+  } else {
     float last[VL];
     load_row(T - 1, last);
     bv = wave_max(lane_max(last));
@@ -992,7 +1014,7 @@ __device__ __forceinline__ void backtrack_one(const BacktrackArgs& args, int64_t
 #pragma unroll
     for (int u = 0; u < PF; ++u) load_row(base - PF - 1 - u, ring[u]);
   }
-  if (lane == 0) {
+  if (record && lane == 0) {
     args.status[seq] = CVK_SEQ_OK;
     args.score[seq] = (double)score32;  // f64 re-score: rescore_f64_lanes (after this kernel)
     if (args.score32) args.score32[seq] = score32;
@@ -1512,6 +1534,92 @@ hipError_t launch_obs_first_bad(const int32_t* obs, int64_t lo, int64_t hi, int6
   if (e != hipSuccess || hi <= lo) return e;
   const int64_t want = (hi - lo + 255) / 256, blocks = want < 4096 ? want : 4096;
   hipLaunchKernelGGL(obs_first_bad, dim3((unsigned)blocks), dim3(256), 0, stream, obs, lo, hi, (uint32_t)V, first);
+  return hipGetLastError();
+}
+
+// ---- constrained decode, resume flow (cviterbi.cpp forced_decode_resume) ----------------
+// The forced decode of a constrained sequence repeats, up to its first constrained element
+// t_1, exactly the rows the terms pass's prefix computed (same adds, same max).  The terms
+// pass stores those rows; the final decode then runs only [t_1, end) of such a sequence,
+// starting from the stored row t_1 with the chosen state forced, and the prefix of the path
+// is backtracked through the stored rows from that state.  Bit-identical to the full forced
+// decode by construction (tests: CV_NO_RESUME A/B).
+__global__ void resume_rows_build(const float* last, const int32_t* state, int np, float* out) {
+  const int64_t i = blockIdx.x;
+  const int j = threadIdx.x;
+  if (j < np) out[i * np + j] = (j == state[i]) ? last[i * np + j] : ninf_f();
+}
+
+hipError_t launch_resume_rows(const float* last, const int32_t* state, int64_t n, int np, float* out,
+                              hipStream_t stream) {
+  if (n <= 0) return hipSuccess;
+  if (np <= 0 || np > 256) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(resume_rows_build, dim3((unsigned)n), dim3(256), 0, stream, last, state, np, out);
+  return hipGetLastError();
+}
+
+__global__ void compact_suffix(const int64_t* off, const int64_t* start, const int64_t* off2, const int32_t* obs,
+                               const int32_t* forced, const int32_t* ridx, int32_t* obs2, int32_t* forced2) {
+  const int64_t s = blockIdx.x;
+  const int64_t e0 = start[s], n = off[s + 1] - e0, o2 = off2[s];
+  const int r = ridx[s];
+  for (int64_t k = threadIdx.x; k < n; k += blockDim.x) {
+    obs2[o2 + k] = obs[e0 + k];
+    forced2[o2 + k] = (k == 0 && r >= 0) ? -2 - r : forced[e0 + k];
+  }
+}
+
+hipError_t launch_compact_suffix(const int64_t* off, const int64_t* start, const int64_t* off2, const int32_t* obs,
+                                 const int32_t* forced, const int32_t* ridx, int32_t* obs2, int32_t* forced2,
+                                 int64_t nseq, hipStream_t stream) {
+  if (nseq <= 0) return hipSuccess;
+  hipLaunchKernelGGL(compact_suffix, dim3((unsigned)nseq), dim3(256), 0, stream, off, start, off2, obs, forced, ridx,
+                     obs2, forced2);
+  return hipGetLastError();
+}
+
+__global__ void scatter_suffix_path(const int64_t* off, const int64_t* start, const int64_t* off2,
+                                    const int32_t* path2, int32_t* path) {
+  const int64_t s = blockIdx.x;
+  const int64_t e0 = start[s], n = off[s + 1] - e0, o2 = off2[s];
+  for (int64_t k = threadIdx.x; k < n; k += blockDim.x) path[e0 + k] = path2[o2 + k];
+}
+
+hipError_t launch_scatter_suffix_path(const int64_t* off, const int64_t* start, const int64_t* off2,
+                                      const int32_t* path2, int32_t* path, int64_t nseq, hipStream_t stream) {
+  if (nseq <= 0) return hipSuccess;
+  hipLaunchKernelGGL(scatter_suffix_path, dim3((unsigned)nseq), dim3(256), 0, stream, off, start, off2, path2, path);
+  return hipGetLastError();
+}
+
+template <int NP>
+__global__ __launch_bounds__(256) void prefix_backtrack(PrefixBtArgs a, int64_t n) {
+  constexpr int VL = NP / 64;
+  const int lane = threadIdx.x & 63;
+  const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= n) return;
+  const int64_t seq = a.seq[i];
+  const int64_t e0 = a.offsets[seq];
+  const int T = (int)(a.t1[i] - e0 + 1);
+  if (a.status[seq] != CVK_SEQ_OK) {  // infeasible: the whole path is 0 (backtrack_one's rule)
+    for (int t = lane; t < T - 1; t += 64) a.path[e0 + t] = 0;
+    return;
+  }
+  BacktrackArgs b{};
+  b.path = a.path;
+  backtrack_one<VL, NP>(b, seq, e0, T, lane, a.rows + a.row_base[i] * NP + VL * lane, a.at + VL * lane, false,
+                        a.state[i], false);
+}
+
+hipError_t launch_prefix_backtrack(int np, const PrefixBtArgs& a, int64_t n, hipStream_t stream) {
+  if (n <= 0) return hipSuccess;
+  const dim3 grid((unsigned)((n + 3) / 4));
+  switch (np) {
+    case 128: hipLaunchKernelGGL(prefix_backtrack<128>, grid, dim3(256), 0, stream, a, n); break;
+    case 192: hipLaunchKernelGGL(prefix_backtrack<192>, grid, dim3(256), 0, stream, a, n); break;
+    case 256: hipLaunchKernelGGL(prefix_backtrack<256>, grid, dim3(256), 0, stream, a, n); break;
+    default: return hipErrorInvalidValue;
+  }
   return hipGetLastError();
 }
 

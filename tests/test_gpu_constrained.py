@@ -306,3 +306,66 @@ def test_constrained_device_rejects_bad_obs(gpu):
            torch.empty(2, dtype=torch.uint8, device=dev)]
     with pytest.raises(cv.CVError, match=r"obs\[13\]"):
         cv.decode_constrained_device(h, off, torch.from_numpy(off).to(dev), torch.from_numpy(obs).to(dev), comp, *out)
+
+
+def _resume_case(n, seed, nseq=48, tmax=40, bad_obs=False):
+    pi, a, b = synth.random_hmm(n, 9, seed=seed)
+    if bad_obs:  # observation 8 is impossible in every state: sequences holding it are infeasible
+        b = b.copy()
+        b[:, 8] = -np.inf
+    rng = np.random.default_rng(seed)
+    lens = rng.integers(1, tmax, size=nseq)
+    lens[:3] = [1, 2, tmax]
+    off = synth.offsets_from_lengths(lens)
+    obs = rng.integers(0, 8, size=int(off[-1])).astype(np.int32)
+    if bad_obs:
+        obs[rng.integers(0, len(obs), size=3)] = 8
+    comp = np.full(len(obs), -1, np.int32)
+    for s in range(nseq):
+        if rng.random() < 0.7:
+            k = rng.integers(1, 4)
+            pos = rng.choice(lens[s], size=min(k, lens[s]), replace=False)
+            comp[off[s] + pos] = rng.integers(0, 4, size=len(pos))
+    comp[off[0]] = 0          # t_1 = first element (length-1 sequence)
+    comp[off[2] + lens[2] - 1] = 1  # t_1 = last element
+    return pi, a, b, off, obs, comp
+
+
+@pytest.mark.parametrize("n,seed,bad", [(128, 1, False), (192, 2, False), (256, 3, False), (256, 4, True),
+                                        (130, 5, True), (200, 6, False)])
+def test_constrained_resume_equals_full(gpu, monkeypatch, n, seed, bad):
+    """Resume flow (stored prefix rows, decode of [t_1, end), prefix backtrack from the forced
+    state) == the full forced decode (CV_NO_RESUME=1), host and device APIs, bit for bit;
+    N = 200 (NP 224) is outside the resume flow and runs the full decode both times."""
+    import torch
+    pi, a, b, off, obs, comp = _resume_case(n, seed, bad_obs=bad)
+    h = cv.HMM(pi, a, b)
+    for f64 in (False, True):  # f32 scores see the resumed row's value itself, not just the path
+        monkeypatch.setenv("CV_NO_RESUME", "1")
+        ref = cv.decode_constrained(h, off, obs, comp, ncomp=5, rescore_f64=f64)
+        monkeypatch.setenv("CV_NO_RESUME", "0")
+        got = cv.decode_constrained(h, off, obs, comp, ncomp=5, rescore_f64=f64)
+        for x, y, what in zip(got, ref, ("path", "score", "status", "states", "objective")):
+            assert np.array_equal(np.asarray(x), np.asarray(y)), (what, f64)
+    if bad:
+        assert (ref[2] == 1).any()
+    dev = torch.device("cuda", 0)
+    path_d = torch.full((int(off[-1]),), 7, dtype=torch.int32, device=dev)
+    score_d = torch.empty(len(off) - 1, dtype=torch.float64, device=dev)
+    status_d = torch.empty(len(off) - 1, dtype=torch.uint8, device=dev)
+    states, obj = cv.decode_constrained_device(h, off, torch.from_numpy(off).to(dev), torch.from_numpy(obs).to(dev),
+                                               comp, path_d, score_d, status_d, ncomp=5)
+    assert np.array_equal(states, ref[3])
+    assert np.array_equal(path_d.cpu().numpy(), ref[0])
+    assert np.array_equal(score_d.cpu().numpy(), ref[1])
+    assert np.array_equal(status_d.cpu().numpy(), ref[2])
+    assert obj == ref[4] or (np.isinf(obj) and np.isinf(ref[4]))
+
+
+def test_constrained_resume_oracle(gpu):
+    """Resume flow at N = 256 against the oracle spec directly."""
+    pi, a, b, off, obs, comp = _resume_case(256, 9, nseq=24, tmax=30)
+    for s in range(len(off) - 1):  # no component pairs (the oracle's search is brute force):
+        e = off[s] + np.nonzero(comp[off[s]:off[s + 1]] >= 0)[0]  # later positions repeat the first's
+        comp[e[1:]] = comp[e[0]] if len(e) else -1                # component (m >= 2, diagonal terms)
+    _check(cv.HMM(pi, a, b), pi, a, b, off, obs, comp)
