@@ -129,6 +129,7 @@ struct cv_hmm {
   // resume flow of the constrained decode: stored prefix rows, forced row t_1 per constrained
   // sequence, the compact suffix batch and its index arrays
   DevBuf rs_rows, rs_rowbase, rs_resume, rs_start, rs_off2, rs_ridx, rs_slot, rs_obs2, rs_frc2, rs_path2;
+  hipEvent_t rs_ev = nullptr;  // prefix backtrack done / staging done
   std::vector<int32_t> order_host;
   std::vector<float> host_dl, host_mu;  // constrained-decode term rows (kept: no per-call page faults)
   // timing events of the last call
@@ -141,6 +142,7 @@ struct cv_hmm {
 
   ~cv_hmm() {
     for (auto e : ev) (void)hipEventDestroy(e);
+    if (rs_ev) (void)hipEventDestroy(rs_ev);
     if (stream) (void)hipStreamDestroy(stream);
     if (bt_stream) (void)hipStreamDestroy(bt_stream);
   }
@@ -1136,11 +1138,15 @@ cv_status constrained_partials_locked(cv_hmm* h, int64_t nseq, const int64_t* of
     }
   }
   {
+    // longest first, stable: counting sort on the range lengths (a comparison sort of the
+    // 2nc slots cost ~4 ms of host time at config 5 with the GPU idle)
     std::vector<int32_t> so((size_t)2 * nc);
-    std::iota(so.begin(), so.end(), 0);
-    std::stable_sort(so.begin(), so.end(), [&](int32_t x, int32_t y) {
-      return rg[2 * x + 1] - rg[2 * x] > rg[2 * y + 1] - rg[2 * y];
-    });
+    int64_t maxlen = 0;
+    for (int64_t x = 0; x < 2 * nc; ++x) maxlen = std::max(maxlen, rg[2 * x + 1] - rg[2 * x]);
+    std::vector<int64_t> pos((size_t)maxlen + 2, 0);
+    for (int64_t x = 0; x < 2 * nc; ++x) ++pos[(size_t)(maxlen - (rg[2 * x + 1] - rg[2 * x])) + 1];
+    for (size_t k = 1; k < pos.size(); ++k) pos[k] += pos[k - 1];
+    for (int64_t x = 0; x < 2 * nc; ++x) so[(size_t)pos[(size_t)(maxlen - (rg[2 * x + 1] - rg[2 * x]))]++] = (int32_t)x;
     if ((st = h->ws_order.ensure(so.size() * 4)) != CV_OK) return st;
     HIP_TRY(hipMemcpyAsync(h->ws_order.p, so.data(), so.size() * 4, hipMemcpyHostToDevice, stream));
     fa.slot_order = h->ws_order.as<int32_t>();
@@ -1380,9 +1386,11 @@ cv_status forced_decode_locked(cv_hmm* h, int64_t nseq, const int64_t* offsets, 
 // Final decode of the resume flow (see kernels/trellis.hip "resume flow"): the terms pass
 // stored every constrained sequence's prefix rows, so the decode runs [t_1, end) of those
 // sequences (from row t_1 with the chosen state forced) and whole unconstrained sequences as
-// one compact batch; then the suffix paths are scattered back, each prefix path is backtracked
-// from its forced state, and every path is re-scored in f64 over its whole sequence.
-// Bit-identical to forced_decode_locked's full forced decode.  Device pointers; synchronous.
+// one compact batch, ordered longest first (contiguous chunks of near-equal lengths pair and
+// pack well); the prefix paths are backtracked from their forced states on the backtrack
+// stream beside that decode; then suffix paths, scores and statuses go back to the original
+// layout and every path is re-scored in f64 over its whole sequence.  Bit-identical to
+// forced_decode_locked's full forced decode.  Device pointers; synchronous.
 cv_status forced_decode_resume(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, const int64_t* offsets_dev,
                                const int32_t* obs_dev, const int32_t* component, const int32_t* comp_state,
                                const std::vector<ConSeq>& cs, const PrefixKeep& keep, cv_opts o, int32_t* path_dev,
@@ -1391,7 +1399,7 @@ cv_status forced_decode_resume(cv_hmm* h, int64_t nseq, const int64_t* offsets_h
   if ((st = stage_forced_locked(h, offsets_host, nseq, component, comp_state, cs, stream)) != CV_OK) return st;
   const int64_t nc = (int64_t)keep.seq.size();
   const int np = h->np;
-  std::vector<int64_t> start(offsets_host, offsets_host + nseq), off2((size_t)nseq + 1);
+  std::vector<int64_t> start(offsets_host, offsets_host + nseq);
   std::vector<int32_t> ridx((size_t)nseq, -1), state((size_t)nc);
   for (int64_t i = 0; i < nc; ++i) {
     start[(size_t)keep.seq[i]] = keep.t1[i];
@@ -1399,62 +1407,90 @@ cv_status forced_decode_resume(cv_hmm* h, int64_t nseq, const int64_t* offsets_h
     const int32_t c = comp_state[component[keep.t1[i]]];
     state[(size_t)i] = c >= 0 ? c : 0;  // no state: forced to 0 and marked infeasible (mark_unassigned)
   }
+  // compact order: longest first, stable (counting sort)
+  int64_t maxlen = 0;
+  for (int64_t s = 0; s < nseq; ++s) maxlen = std::max(maxlen, offsets_host[s + 1] - start[(size_t)s]);
+  std::vector<int64_t> pos((size_t)maxlen + 2, 0), perm((size_t)nseq);
+  for (int64_t s = 0; s < nseq; ++s) ++pos[(size_t)(maxlen - (offsets_host[s + 1] - start[(size_t)s])) + 1];
+  for (size_t k = 1; k < pos.size(); ++k) pos[k] += pos[k - 1];
+  for (int64_t s = 0; s < nseq; ++s) perm[(size_t)pos[(size_t)(maxlen - (offsets_host[s + 1] - start[(size_t)s]))]++] = s;
+  // per compact sequence: [cstart | perm | off2 (nseq+1)] int64, then ridx int32
+  std::vector<int64_t> c64((size_t)3 * nseq + 1);
+  std::vector<int32_t> cridx((size_t)nseq);
+  int64_t* cstart = c64.data();
+  int64_t* cperm = cstart + nseq;
+  int64_t* off2 = cperm + nseq;
   off2[0] = 0;
-  for (int64_t s = 0; s < nseq; ++s) off2[(size_t)s + 1] = off2[(size_t)s] + offsets_host[s + 1] - start[(size_t)s];
-  const int64_t total2 = off2[(size_t)nseq];
+  for (int64_t k = 0; k < nseq; ++k) {
+    const int64_t s = perm[(size_t)k];
+    cstart[k] = start[(size_t)s];
+    cperm[k] = s;
+    cridx[(size_t)k] = ridx[(size_t)s];
+    off2[k + 1] = off2[k] + offsets_host[s + 1] - start[(size_t)s];
+  }
+  const int64_t total2 = off2[nseq];
   // per-slot arrays: [seq | t1 | row_base] int64, then state int32
   std::vector<int64_t> slot64((size_t)nc * 3);
   std::copy(keep.seq.begin(), keep.seq.end(), slot64.begin());
   std::copy(keep.t1.begin(), keep.t1.end(), slot64.begin() + nc);
   std::copy(keep.row_base.begin(), keep.row_base.end(), slot64.begin() + 2 * nc);
-  if ((st = h->rs_start.ensure((size_t)nseq * 8)) != CV_OK) return st;
-  if ((st = h->rs_off2.ensure((size_t)(nseq + 1) * 8)) != CV_OK) return st;
+  if ((st = h->rs_start.ensure(c64.size() * 8)) != CV_OK) return st;
   if ((st = h->rs_ridx.ensure((size_t)nseq * 4)) != CV_OK) return st;
+  if ((st = h->rs_off2.ensure((size_t)nseq * 9)) != CV_OK) return st;  // score2 f64 + status2 u8
   if ((st = h->rs_slot.ensure((size_t)std::max<int64_t>(nc, 1) * 28)) != CV_OK) return st;
   if ((st = h->rs_resume.ensure((size_t)std::max<int64_t>(nc, 1) * np * 4)) != CV_OK) return st;
   if ((st = h->rs_obs2.ensure((size_t)std::max<int64_t>(total2, 1) * 4)) != CV_OK) return st;
   if ((st = h->rs_frc2.ensure((size_t)std::max<int64_t>(total2, 1) * 4)) != CV_OK) return st;
   if ((st = h->rs_path2.ensure((size_t)std::max<int64_t>(total2, 1) * 4)) != CV_OK) return st;
+  if (!h->rs_ev && hipEventCreateWithFlags(&h->rs_ev, hipEventDisableTiming) != hipSuccess)
+    return set_err(CV_EDEVICE, "hipEventCreate failed");
+  const int64_t* cstart_d = h->rs_start.as<int64_t>();
+  const int64_t* cperm_d = cstart_d + nseq;
+  const int64_t* off2_d = cperm_d + nseq;
+  double* score2 = h->rs_off2.as<double>();
+  uint8_t* status2 = reinterpret_cast<uint8_t*>(score2 + nseq);
   int64_t* slot_d = h->rs_slot.as<int64_t>();
   int32_t* state_d = reinterpret_cast<int32_t*>(slot_d + 3 * nc);
-  HIP_TRY(hipMemcpyAsync(h->rs_start.p, start.data(), (size_t)nseq * 8, hipMemcpyHostToDevice, stream));
-  HIP_TRY(hipMemcpyAsync(h->rs_off2.p, off2.data(), (size_t)(nseq + 1) * 8, hipMemcpyHostToDevice, stream));
-  HIP_TRY(hipMemcpyAsync(h->rs_ridx.p, ridx.data(), (size_t)nseq * 4, hipMemcpyHostToDevice, stream));
-  if (nc > 0) {
-    HIP_TRY(hipMemcpyAsync(slot_d, slot64.data(), (size_t)nc * 24, hipMemcpyHostToDevice, stream));
-    HIP_TRY(hipMemcpyAsync(state_d, state.data(), (size_t)nc * 4, hipMemcpyHostToDevice, stream));
-  }
+  HIP_TRY(hipMemcpyAsync(h->rs_start.p, c64.data(), c64.size() * 8, hipMemcpyHostToDevice, stream));
+  HIP_TRY(hipMemcpyAsync(h->rs_ridx.p, cridx.data(), (size_t)nseq * 4, hipMemcpyHostToDevice, stream));
+  HIP_TRY(hipMemcpyAsync(slot_d, slot64.data(), (size_t)nc * 24, hipMemcpyHostToDevice, stream));
+  HIP_TRY(hipMemcpyAsync(state_d, state.data(), (size_t)nc * 4, hipMemcpyHostToDevice, stream));
   hipError_t err = cvk::launch_resume_rows(h->cs_delta.as<float>(), state_d, nc, np, h->rs_resume.as<float>(), stream);
   if (err == hipSuccess)
-    err = cvk::launch_compact_suffix(offsets_dev, h->rs_start.as<int64_t>(), h->rs_off2.as<int64_t>(), obs_dev,
-                                     h->st_forced.as<int32_t>(), h->rs_ridx.as<int32_t>(), h->rs_obs2.as<int32_t>(),
-                                     h->rs_frc2.as<int32_t>(), nseq, stream);
+    err = cvk::launch_compact_suffix(cstart_d, off2_d, obs_dev, h->st_forced.as<int32_t>(), h->rs_ridx.as<int32_t>(),
+                                     h->rs_obs2.as<int32_t>(), h->rs_frc2.as<int32_t>(), nseq, stream);
   if (err != hipSuccess) return set_err(CV_EDEVICE, "resume staging failed: %s", hipGetErrorString(err));
+  // prefix paths on the backtrack stream, beside the suffix decode (one workgroup per CU at
+  // most: the 100 KiB LDS reservation, as the chunk pipeline's backtracks)
+  cvk::PrefixBtArgs pa{};
+  pa.rows = h->rs_rows.as<float>();
+  pa.seq = slot_d;
+  pa.t1 = slot_d + nc;
+  pa.row_base = slot_d + 2 * nc;
+  pa.state = state_d;
+  pa.offsets = offsets_dev;
+  pa.at = h->t_at.as<float>();
+  pa.status = status_dev;
+  pa.path = path_dev;
+  HIP_TRY(hipEventRecord(h->rs_ev, stream));
+  HIP_TRY(hipStreamWaitEvent(h->bt_stream, h->rs_ev, 0));
+  err = cvk::launch_prefix_backtrack(np, pa, nc, h->bt_stream, 100 * 1024);
+  if (err != hipSuccess) return set_err(CV_EDEVICE, "prefix backtrack failed: %s", hipGetErrorString(err));
+  HIP_TRY(hipEventRecord(h->rs_ev, h->bt_stream));
   trace_mark("resume: compact suffix batch");
   cv_opts o2 = o;
   o2.forced = h->rs_frc2.as<int32_t>();
   o2.rescore_f64 = 0;  // re-scored below over the whole sequences
-  if ((st = decode_device(h, nseq, off2.data(), h->rs_off2.as<int64_t>(), h->rs_obs2.as<int32_t>(), o2,
-                          h->rs_path2.as<int32_t>(), score_dev, status_dev, stream, h->rs_resume.as<float>())) !=
-      CV_OK) {
+  if ((st = decode_device(h, nseq, off2, off2_d, h->rs_obs2.as<int32_t>(), o2, h->rs_path2.as<int32_t>(), score2,
+                          status2, stream, h->rs_resume.as<float>())) != CV_OK) {
     (void)hipStreamSynchronize(stream);
+    (void)hipStreamSynchronize(h->bt_stream);
     return st;
   }
-  err = cvk::launch_scatter_suffix_path(offsets_dev, h->rs_start.as<int64_t>(), h->rs_off2.as<int64_t>(),
-                                        h->rs_path2.as<int32_t>(), path_dev, nseq, stream);
-  if (err == hipSuccess) {
-    cvk::PrefixBtArgs pa{};
-    pa.rows = h->rs_rows.as<float>();
-    pa.seq = slot_d;
-    pa.t1 = slot_d + nc;
-    pa.row_base = slot_d + 2 * nc;
-    pa.state = state_d;
-    pa.offsets = offsets_dev;
-    pa.at = h->t_at.as<float>();
-    pa.status = status_dev;
-    pa.path = path_dev;
-    err = cvk::launch_prefix_backtrack(np, pa, nc, stream);
-  }
+  HIP_TRY(hipStreamWaitEvent(stream, h->rs_ev, 0));  // prefix paths written
+  err = cvk::launch_scatter_suffix(cstart_d, off2_d, cperm_d, h->rs_path2.as<int32_t>(), score2, status2, path_dev,
+                                   score_dev, status_dev, nseq, stream);
+  if (err == hipSuccess) err = cvk::launch_zero_infeasible_prefix(pa, nc, stream);
   if (err == hipSuccess && o.rescore_f64) {
     cvk::RescoreArgs ra{};
     ra.path = path_dev;

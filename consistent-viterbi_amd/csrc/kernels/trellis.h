@@ -134,14 +134,16 @@ hipError_t launch_obs_first_bad(const int32_t* obs, int64_t lo, int64_t hi, int6
 // out[i][j] = j == state[i] ? last[i][j] : -inf  (row t_1 of sequence i, forced), np <= 256
 hipError_t launch_resume_rows(const float* last, const int32_t* state, int64_t n, int np, float* out,
                               hipStream_t stream);
-// compact suffix batch: sequence s keeps elements [start[s], off[s+1]) at off2[s]; forced2 of
-// its first element = -2 - ridx[s] when ridx[s] >= 0 (resume row), else forced[start[s]]
-hipError_t launch_compact_suffix(const int64_t* off, const int64_t* start, const int64_t* off2, const int32_t* obs,
-                                 const int32_t* forced, const int32_t* ridx, int32_t* obs2, int32_t* forced2,
-                                 int64_t nseq, hipStream_t stream);
-// path[start[s] + k] = path2[off2[s] + k]
-hipError_t launch_scatter_suffix_path(const int64_t* off, const int64_t* start, const int64_t* off2,
-                                      const int32_t* path2, int32_t* path, int64_t nseq, hipStream_t stream);
+// compact suffix batch (compact sequence k, any order): elements [cstart[k], cstart[k] +
+// off2[k+1] - off2[k]) of the original batch go to off2[k]; forced2 of the first element =
+// -2 - ridx[k] when ridx[k] >= 0 (resume row), else the original forced value
+hipError_t launch_compact_suffix(const int64_t* cstart, const int64_t* off2, const int32_t* obs, const int32_t* forced,
+                                 const int32_t* ridx, int32_t* obs2, int32_t* forced2, int64_t nseq,
+                                 hipStream_t stream);
+// back: path[cstart[k] + q] = path2[off2[k] + q]; score/status[perm[k]] = score2/status2[k]
+hipError_t launch_scatter_suffix(const int64_t* cstart, const int64_t* off2, const int64_t* perm,
+                                 const int32_t* path2, const double* score2, const uint8_t* status2, int32_t* path,
+                                 double* score, uint8_t* status, int64_t nseq, hipStream_t stream);
 struct PrefixBtArgs {
   const float* rows;        // compact prefix delta rows (the terms pass's first pass)
   const int64_t* row_base;  // [n] first row of slot i
@@ -150,11 +152,14 @@ struct PrefixBtArgs {
   const int32_t* state;     // [n] state forced there
   const int64_t* offsets;   // original CSR offsets
   const float* at;          // [NP][NP]
-  const uint8_t* status;    // final statuses (sequences not OK: prefix path zeroed)
+  const uint8_t* status;    // final statuses (zero_infeasible_prefix)
   int32_t* path;
 };
-// path[off[seq] .. t1] of every slot: backtrack from `state` at t1 through the stored prefix rows
-hipError_t launch_prefix_backtrack(int np, const PrefixBtArgs& a, int64_t n, hipStream_t stream);
+// path[off[seq] .. t1] of every slot: backtrack from `state` at t1 through the stored prefix
+// rows (statuses not read: may overlap the suffix decode; lds_reserve as launch_trellis_bt)
+hipError_t launch_prefix_backtrack(int np, const PrefixBtArgs& a, int64_t n, hipStream_t stream, int lds_reserve);
+// path[off[seq] .. t1) = 0 for every slot whose final status is not OK
+hipError_t launch_zero_infeasible_prefix(const PrefixBtArgs& a, int64_t n, hipStream_t stream);
 
 int trellis_padded_states(int n);  // 0 if the trellis kernel does not cover n
 hipError_t launch_trellis_fwd(int np, const TrellisFwdArgs& fa, int64_t nseq, hipStream_t stream);

@@ -1558,37 +1558,59 @@ hipError_t launch_resume_rows(const float* last, const int32_t* state, int64_t n
   return hipGetLastError();
 }
 
-__global__ void compact_suffix(const int64_t* off, const int64_t* start, const int64_t* off2, const int32_t* obs,
-                               const int32_t* forced, const int32_t* ridx, int32_t* obs2, int32_t* forced2) {
-  const int64_t s = blockIdx.x;
-  const int64_t e0 = start[s], n = off[s + 1] - e0, o2 = off2[s];
-  const int r = ridx[s];
-  for (int64_t k = threadIdx.x; k < n; k += blockDim.x) {
-    obs2[o2 + k] = obs[e0 + k];
-    forced2[o2 + k] = (k == 0 && r >= 0) ? -2 - r : forced[e0 + k];
+__global__ void compact_suffix(const int64_t* cstart, const int64_t* off2, const int32_t* obs, const int32_t* forced,
+                               const int32_t* ridx, int32_t* obs2, int32_t* forced2) {
+  const int64_t k = blockIdx.x;
+  const int64_t e0 = cstart[k], o2 = off2[k], n = off2[k + 1] - o2;
+  const int r = ridx[k];
+  for (int64_t q = threadIdx.x; q < n; q += blockDim.x) {
+    obs2[o2 + q] = obs[e0 + q];
+    forced2[o2 + q] = (q == 0 && r >= 0) ? -2 - r : forced[e0 + q];
   }
 }
 
-hipError_t launch_compact_suffix(const int64_t* off, const int64_t* start, const int64_t* off2, const int32_t* obs,
-                                 const int32_t* forced, const int32_t* ridx, int32_t* obs2, int32_t* forced2,
-                                 int64_t nseq, hipStream_t stream) {
+hipError_t launch_compact_suffix(const int64_t* cstart, const int64_t* off2, const int32_t* obs, const int32_t* forced,
+                                 const int32_t* ridx, int32_t* obs2, int32_t* forced2, int64_t nseq,
+                                 hipStream_t stream) {
   if (nseq <= 0) return hipSuccess;
-  hipLaunchKernelGGL(compact_suffix, dim3((unsigned)nseq), dim3(256), 0, stream, off, start, off2, obs, forced, ridx,
-                     obs2, forced2);
+  hipLaunchKernelGGL(compact_suffix, dim3((unsigned)nseq), dim3(256), 0, stream, cstart, off2, obs, forced, ridx, obs2,
+                     forced2);
   return hipGetLastError();
 }
 
-__global__ void scatter_suffix_path(const int64_t* off, const int64_t* start, const int64_t* off2,
-                                    const int32_t* path2, int32_t* path) {
-  const int64_t s = blockIdx.x;
-  const int64_t e0 = start[s], n = off[s + 1] - e0, o2 = off2[s];
-  for (int64_t k = threadIdx.x; k < n; k += blockDim.x) path[e0 + k] = path2[o2 + k];
+__global__ void scatter_suffix(const int64_t* cstart, const int64_t* off2, const int64_t* perm, const int32_t* path2,
+                               const double* score2, const uint8_t* status2, int32_t* path, double* score,
+                               uint8_t* status) {
+  const int64_t k = blockIdx.x;
+  const int64_t e0 = cstart[k], o2 = off2[k], n = off2[k + 1] - o2;
+  for (int64_t q = threadIdx.x; q < n; q += blockDim.x) path[e0 + q] = path2[o2 + q];
+  if (threadIdx.x == 0) {
+    score[perm[k]] = score2[k];
+    status[perm[k]] = status2[k];
+  }
 }
 
-hipError_t launch_scatter_suffix_path(const int64_t* off, const int64_t* start, const int64_t* off2,
-                                      const int32_t* path2, int32_t* path, int64_t nseq, hipStream_t stream) {
+hipError_t launch_scatter_suffix(const int64_t* cstart, const int64_t* off2, const int64_t* perm,
+                                 const int32_t* path2, const double* score2, const uint8_t* status2, int32_t* path,
+                                 double* score, uint8_t* status, int64_t nseq, hipStream_t stream) {
   if (nseq <= 0) return hipSuccess;
-  hipLaunchKernelGGL(scatter_suffix_path, dim3((unsigned)nseq), dim3(256), 0, stream, off, start, off2, path2, path);
+  hipLaunchKernelGGL(scatter_suffix, dim3((unsigned)nseq), dim3(256), 0, stream, cstart, off2, perm, path2, score2,
+                     status2, path, score, status);
+  return hipGetLastError();
+}
+
+// infeasible sequences: their whole path is 0 (backtrack_one's rule), prefix included
+__global__ void zero_infeasible_prefix(PrefixBtArgs a, int64_t n) {
+  const int64_t i = blockIdx.x;
+  const int64_t seq = a.seq[i];
+  if (a.status[seq] == CVK_SEQ_OK) return;
+  const int64_t e0 = a.offsets[seq], e1 = a.t1[i];
+  for (int64_t e = e0 + threadIdx.x; e < e1; e += blockDim.x) a.path[e] = 0;
+}
+
+hipError_t launch_zero_infeasible_prefix(const PrefixBtArgs& a, int64_t n, hipStream_t stream) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(zero_infeasible_prefix, dim3((unsigned)n), dim3(64), 0, stream, a, n);
   return hipGetLastError();
 }
 
@@ -1601,26 +1623,35 @@ __global__ __launch_bounds__(256) void prefix_backtrack(PrefixBtArgs a, int64_t 
   const int64_t seq = a.seq[i];
   const int64_t e0 = a.offsets[seq];
   const int T = (int)(a.t1[i] - e0 + 1);
-  if (a.status[seq] != CVK_SEQ_OK) {  // infeasible: the whole path is 0 (backtrack_one's rule)
-    for (int t = lane; t < T - 1; t += 64) a.path[e0 + t] = 0;
-    return;
-  }
+  // an infeasible forced row (-inf at the state) backtracks garbage: zero_infeasible_prefix
+  // overwrites it once the suffix decode has told which sequences are infeasible
   BacktrackArgs b{};
   b.path = a.path;
   backtrack_one<VL, NP>(b, seq, e0, T, lane, a.rows + a.row_base[i] * NP + VL * lane, a.at + VL * lane, false,
                         a.state[i], false);
 }
 
-hipError_t launch_prefix_backtrack(int np, const PrefixBtArgs& a, int64_t n, hipStream_t stream) {
+template <int NP>
+static hipError_t prefix_bt_np(const PrefixBtArgs& a, int64_t n, hipStream_t stream, int lds_reserve) {
+  static bool attr = false;  // allow the large dynamic-LDS reservation (see trellis_bt_np)
+  if (lds_reserve > 0 && !attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&prefix_backtrack<NP>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr = true;
+  }
+  hipLaunchKernelGGL(prefix_backtrack<NP>, dim3((unsigned)((n + 3) / 4)), dim3(256), (size_t)lds_reserve, stream, a,
+                     n);
+  return hipGetLastError();
+}
+
+hipError_t launch_prefix_backtrack(int np, const PrefixBtArgs& a, int64_t n, hipStream_t stream, int lds_reserve) {
   if (n <= 0) return hipSuccess;
-  const dim3 grid((unsigned)((n + 3) / 4));
   switch (np) {
-    case 128: hipLaunchKernelGGL(prefix_backtrack<128>, grid, dim3(256), 0, stream, a, n); break;
-    case 192: hipLaunchKernelGGL(prefix_backtrack<192>, grid, dim3(256), 0, stream, a, n); break;
-    case 256: hipLaunchKernelGGL(prefix_backtrack<256>, grid, dim3(256), 0, stream, a, n); break;
+    case 128: return prefix_bt_np<128>(a, n, stream, lds_reserve);
+    case 192: return prefix_bt_np<192>(a, n, stream, lds_reserve);
+    case 256: return prefix_bt_np<256>(a, n, stream, lds_reserve);
     default: return hipErrorInvalidValue;
   }
-  return hipGetLastError();
 }
 
 int trellis_padded_states(int n) {
