@@ -1512,6 +1512,39 @@ cv_status forced_decode_resume(cv_hmm* h, int64_t nseq, const int64_t* offsets_h
   return CV_OK;
 }
 
+// Host-API tail of the constrained decode: the resume flow on the staged observations
+// (h->st_obs) with results copied back, or the full forced decode.
+cv_status final_decode_host(cv_hmm* h, int64_t nseq, const int64_t* offsets, const int32_t* obs,
+                            const int32_t* component, const int32_t* comp_state, const cv_opts& o,
+                            const std::vector<ConSeq>& cs, const PrefixKeep& keep, bool obs_staged, int32_t* path_out,
+                            double* score_out, uint8_t* status_out, double* objective_out) {
+  cv_status st;
+  if (keep.kept && obs_staged) {
+    hipStream_t stream = o.stream ? (hipStream_t)o.stream : h->stream;
+    const int64_t base = offsets[0], total = offsets[nseq];
+    if ((st = h->st_off.ensure((size_t)(nseq + 1) * 8)) != CV_OK) return st;
+    if ((st = h->st_path.ensure((size_t)std::max<int64_t>(total, 1) * 4)) != CV_OK) return st;
+    if ((st = h->st_score.ensure((size_t)nseq * 8)) != CV_OK) return st;
+    if ((st = h->st_status.ensure((size_t)nseq)) != CV_OK) return st;
+    HIP_TRY(hipMemcpyAsync(h->st_off.p, offsets, (size_t)(nseq + 1) * 8, hipMemcpyHostToDevice, stream));
+    if ((st = forced_decode_resume(h, nseq, offsets, h->st_off.as<int64_t>(), h->st_obs.as<int32_t>(), component,
+                                   comp_state, cs, keep, o, h->st_path.as<int32_t>(), h->st_score.as<double>(),
+                                   h->st_status.as<uint8_t>(), stream)) != CV_OK)
+      return st;
+    if (total > base)
+      HIP_TRY(hipMemcpyAsync(path_out + base, h->st_path.as<int32_t>() + base, (size_t)(total - base) * 4,
+                             hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipMemcpyAsync(score_out, h->st_score.p, (size_t)nseq * 8, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipMemcpyAsync(status_out, h->st_status.p, (size_t)nseq, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipStreamSynchronize(stream));
+    const double obj = mark_unassigned(nseq, component, comp_state, cs, score_out, status_out);
+    if (objective_out) *objective_out = obj;
+    return CV_OK;
+  }
+  return forced_decode_locked(h, nseq, offsets, obs, component, comp_state, o, cs, obs_staged, path_out, score_out,
+                              status_out, objective_out);
+}
+
 cv_status select_locked(int32_t nstates, int32_t ncomp, const int32_t* pairs, int64_t npairs,
                         const int64_t* partials, int32_t* comp_state_out, uint64_t* explored_out) {
   const cvcsp::SolveResult r = cvcsp::solve(nstates, ncomp, pairs, npairs, partials, comp_state_out, kCspNodeLimit);
@@ -1614,30 +1647,8 @@ CV_API cv_status cv_decode_constrained(cv_hmm* h, int64_t nseq, const int64_t* o
     return st;
   h->last_explored = explored;
   trace_mark("select");
-  if (keep.kept && obs_staged) {  // resume flow on the staged observations, results copied back
-    hipStream_t stream = o.stream ? (hipStream_t)o.stream : h->stream;
-    const int64_t base = offsets[0], total = offsets[nseq];
-    if ((st = h->st_off.ensure((size_t)(nseq + 1) * 8)) != CV_OK) return st;
-    if ((st = h->st_path.ensure((size_t)std::max<int64_t>(total, 1) * 4)) != CV_OK) return st;
-    if ((st = h->st_score.ensure((size_t)nseq * 8)) != CV_OK) return st;
-    if ((st = h->st_status.ensure((size_t)nseq)) != CV_OK) return st;
-    HIP_TRY(hipMemcpyAsync(h->st_off.p, offsets, (size_t)(nseq + 1) * 8, hipMemcpyHostToDevice, stream));
-    if ((st = forced_decode_resume(h, nseq, offsets, h->st_off.as<int64_t>(), h->st_obs.as<int32_t>(), component,
-                                   comp_state_out, cs, keep, o, h->st_path.as<int32_t>(), h->st_score.as<double>(),
-                                   h->st_status.as<uint8_t>(), stream)) != CV_OK)
-      return st;
-    if (total > base)
-      HIP_TRY(hipMemcpyAsync(path_out + base, h->st_path.as<int32_t>() + base, (size_t)(total - base) * 4,
-                             hipMemcpyDeviceToHost, stream));
-    HIP_TRY(hipMemcpyAsync(score_out, h->st_score.p, (size_t)nseq * 8, hipMemcpyDeviceToHost, stream));
-    HIP_TRY(hipMemcpyAsync(status_out, h->st_status.p, (size_t)nseq, hipMemcpyDeviceToHost, stream));
-    HIP_TRY(hipStreamSynchronize(stream));
-    const double obj = mark_unassigned(nseq, component, comp_state_out, cs, score_out, status_out);
-    if (objective_out) *objective_out = obj;
-    return CV_OK;
-  }
-  return forced_decode_locked(h, nseq, offsets, obs, component, comp_state_out, o, cs, obs_staged, path_out,
-                              score_out, status_out, objective_out);
+  return final_decode_host(h, nseq, offsets, obs, component, comp_state_out, o, cs, keep, obs_staged, path_out,
+                           score_out, status_out, objective_out);
 }
 
 CV_API cv_status cv_decode_forced_components(cv_hmm* h, int64_t nseq, const int64_t* offsets, const int32_t* obs,
@@ -1756,6 +1767,47 @@ CV_API cv_status cv_decode_constrained_device(cv_hmm* h, int64_t nseq, const int
   }
   trace_mark("forced decode (device)");
   return CV_OK;
+}
+
+CV_API cv_status cv_decode_constrained_exchange(cv_hmm* h, int64_t nseq, const int64_t* offsets, const int32_t* obs,
+                                                const int32_t* component, int32_t ncomp, int64_t npairs,
+                                                const int32_t* pairs, cv_exchange_fn exchange, void* ctx,
+                                                const cv_opts* opts, int32_t* path_out, double* score_out,
+                                                uint8_t* status_out, int32_t* comp_state_out,
+                                                uint64_t* explored_out, double* objective_out) {
+  if (!h) return set_err(CV_EINVAL, "null handle");
+  if (nseq < 0 || ncomp < 0 || npairs < 0 ||
+      (nseq > 0 && (!offsets || !obs || !component || !path_out || !score_out || !status_out)) ||
+      (ncomp > 0 && !comp_state_out) || (npairs > 0 && !pairs))
+    return set_err(CV_EINVAL, "null argument");
+  if (!pairs_sorted(pairs, npairs, ncomp)) return set_err(CV_EINVAL, "pairs must be sorted (c1 < c2) and unique");
+  std::lock_guard<std::mutex> lk(h->mu);
+  cv_status st = set_device(h);
+  if (st != CV_OK) return st;
+  cv_opts o = opts ? *opts : default_opts();
+  for (int32_t c = 0; c < ncomp; ++c) comp_state_out[c] = -1;
+  if (objective_out) *objective_out = 0.0;
+  if (explored_out) *explored_out = 0;
+  std::vector<ConSeq> cs;
+  if (nseq > 0 && (st = constrained_validate(h, nseq, offsets, obs, component, ncomp, o, cs)) != CV_OK) return st;
+  std::vector<int64_t> part((size_t)std::max<int64_t>(cvcsp::partial_words((int)h->N, ncomp, npairs), 1), 0);
+  bool obs_staged = false;
+  PrefixKeep keep;
+  if (nseq > 0 && (st = constrained_partials_locked(h, nseq, offsets, obs, component, ncomp, pairs, npairs, o,
+                                                    part.data(), &cs, &obs_staged, nullptr, &keep)) != CV_OK)
+    return st;
+  trace_mark("exchange: shard partials");
+  if (exchange && exchange(part.data(), cvcsp::partial_words((int)h->N, ncomp, npairs), ctx) != 0)
+    return set_err(CV_EDEVICE, "exchange callback failed");
+  trace_mark("exchange: callback");
+  uint64_t explored = 0;
+  if ((st = select_locked((int32_t)h->N, ncomp, pairs, npairs, part.data(), comp_state_out, &explored)) != CV_OK)
+    return st;
+  h->last_explored = explored;
+  if (explored_out) *explored_out = explored;
+  if (nseq == 0) return CV_OK;
+  return final_decode_host(h, nseq, offsets, obs, component, comp_state_out, o, cs, keep, obs_staged, path_out,
+                           score_out, status_out, objective_out);
 }
 
 CV_API cv_status cv_last_timing(cv_hmm* h, cv_timing* out) {

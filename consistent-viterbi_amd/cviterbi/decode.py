@@ -172,6 +172,49 @@ def decode_batch_device(hmm: HMM, offsets_dev, obs_dev, path_dev, score_dev, sta
                                            ptr(status_dev)))
 
 
+EXCHANGE_FN = ctypes.CFUNCTYPE(ctypes.c_int32, ctypes.POINTER(ctypes.c_int64), ctypes.c_int64, ctypes.c_void_p)
+
+
+def decode_constrained_exchange(hmm: HMM, offsets, obs, component, ncomp, pairs, exchange=None, rescore_f64=True):
+    """cv_decode_constrained_exchange: one shard's constrained decode with the exchange step
+    made by `exchange(words)` -- a callable that returns the SUM over all shards of the int64
+    array `words` (e.g. cviterbi.dist.allreduce_partials); None = a single process.  `pairs`
+    = constrained_pairs of the FULL batch.  Returns (path, score, status, comp_state,
+    explored, objective) of this shard."""
+    offsets = np.ascontiguousarray(offsets, np.int64)
+    obs = np.ascontiguousarray(obs, np.int32)
+    component = np.ascontiguousarray(component, np.int32)
+    pairs = np.ascontiguousarray(pairs, np.int32).reshape(-1, 2)
+    nseq = offsets.shape[0] - 1
+    path = np.zeros(max(int(offsets[-1]), 1), np.int32)
+    score = np.zeros(max(nseq, 1), np.float64)
+    status = np.zeros(max(nseq, 1), np.uint8)
+    states = np.full(max(ncomp, 1), -1, np.int32)
+    explored, obj = ctypes.c_uint64(), ctypes.c_double()
+    err = []
+
+    def cb(words, n, _ctx):
+        try:
+            w = np.ctypeslib.as_array(words, shape=(n,))
+            w[:] = np.asarray(exchange(w.copy()), np.int64).reshape(-1)
+            return 0
+        except Exception as e:  # reported after the call returns
+            err.append(e)
+            return 1
+
+    fn = EXCHANGE_FN(cb) if exchange is not None else None  # kept alive for the call
+    o = make_opts("f32", "viterbi", "auto", rescore_f64)
+    st = L.lib().cv_decode_constrained_exchange(hmm.handle, nseq, _p(offsets), _p(obs), _p(component), int(ncomp),
+                                                len(pairs), _p(pairs) if len(pairs) else None,
+                                                ctypes.cast(fn, ctypes.c_void_p) if fn else None, None,
+                                                ctypes.byref(o), _p(path), _p(score), _p(status), _p(states),
+                                                ctypes.byref(explored), ctypes.byref(obj))
+    if err:
+        raise err[0]
+    L.check(st)
+    return (path[:int(offsets[-1])], score[:nseq], status[:nseq], states[:ncomp], explored.value, obj.value)
+
+
 def decode_constrained_device(hmm: HMM, offsets_host, offsets_dev, obs_dev, component, path_dev, score_dev, status_dev,
                               ncomp=None, rescore_f64=True, stream=None, workspace_bytes=0):
     """cv_decode_constrained_device: observations and outputs in HBM (ints or objects with

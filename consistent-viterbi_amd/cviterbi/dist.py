@@ -102,11 +102,11 @@ def allreduce_partials(partials, dist, device=None):
 
 def constrained_decode_sharded(hmm, offsets, obs, component, ncomp, dist, device=None):
     """Config 5 across ranks: shard sequences, exact partials, one all-reduce, select,
-    per-shard forced decode, gather to rank 0.  Returns (path, score, status, comp_state,
+    per-shard final decode (cv_decode_constrained_exchange), gather to rank 0.  Returns (path, score, status, comp_state,
     objective) on rank 0 and (None, None, None, comp_state, None) elsewhere."""
     import torch
 
-    from .decode import constrained_pairs, constrained_partials, constrained_select, decode_forced_components
+    from .decode import constrained_pairs, decode_constrained_exchange
 
     offsets = np.asarray(offsets, np.int64)
     world, rank = dist.get_world_size(), dist.get_rank()
@@ -117,10 +117,10 @@ def constrained_decode_sharded(hmm, offsets, obs, component, ncomp, dist, device
     ob = np.asarray(obs, np.int32)[lo:hi]
     cp = np.asarray(component, np.int32)[lo:hi]
     pairs = constrained_pairs(offsets, component, ncomp)  # full batch: the same layout on every rank
-    part = constrained_partials(hmm, off, ob, cp, ncomp, pairs)
-    part = allreduce_partials(part, dist, device)
-    states, _ = constrained_select(hmm.nstates(), ncomp, part, pairs)
-    path, score, status, _ = decode_forced_components(hmm, off, ob, cp, states)
+    # partials -> all-reduce SUM (the callback) -> search -> final decode, in one library call,
+    # so the shard's decode reuses its terms pass's prefix rows (the resume flow)
+    path, score, status, states, _, _ = decode_constrained_exchange(
+        hmm, off, ob, cp, ncomp, pairs, exchange=lambda w: allreduce_partials(w, dist, device))
     # gather: sequence counts and element counts differ per rank -> pad to capacities
     counts = torch.tensor([s1 - s0, hi - lo], dtype=torch.int64, device=device or "cpu")
     allc = [torch.zeros_like(counts) for _ in range(world)]

@@ -229,6 +229,21 @@ CV_API cv_status cv_decode_forced_components(cv_hmm* h, int64_t nseq, const int6
                                              const int32_t* component, int32_t ncomp, const int32_t* comp_state,
                                              const cv_opts* opts, int32_t* path_out, double* score_out,
                                              uint8_t* status_out, double* objective_out);
+/* Steps 1-3 in ONE call on a shard, the exchange made by the caller's callback: after this
+ * shard's partials are computed, exchange(words, nwords, ctx) must replace words[0, nwords)
+ * by their SUM over all shards (e.g. an all-reduce; return 0 on success) -- then the search
+ * and the shard's final decode run here, which lets the decode reuse the terms pass's prefix
+ * rows (the resume flow) like cv_decode_constrained.  pairs = cv_constrained_pairs of the
+ * FULL batch.  Every rank must reach the callback: it is called even for an empty shard.
+ * exchange == NULL: a single process (words already total).  Host pointers; synchronous.
+ * objective_out = the shard's sum of scores. */
+typedef int32_t (*cv_exchange_fn)(int64_t* words, int64_t nwords, void* ctx);
+CV_API cv_status cv_decode_constrained_exchange(cv_hmm* h, int64_t nseq, const int64_t* offsets, const int32_t* obs,
+                                                const int32_t* component, int32_t ncomp, int64_t npairs,
+                                                const int32_t* pairs, cv_exchange_fn exchange, void* ctx,
+                                                const cv_opts* opts, int32_t* path_out, double* score_out,
+                                                uint8_t* status_out, int32_t* comp_state_out,
+                                                uint64_t* explored_out, double* objective_out);
 /* viterbi::decode (viterbi.rs:5): one sequence, reference decode() semantics (row 0 = 0.0,
  * f64), path only. */
 CV_API cv_status cv_viterbi_decode(cv_hmm* h, int64_t T, const int32_t* obs, int32_t* path_out);

@@ -369,3 +369,68 @@ def test_constrained_resume_oracle(gpu):
         e = off[s] + np.nonzero(comp[off[s]:off[s + 1]] >= 0)[0]  # later positions repeat the first's
         comp[e[1:]] = comp[e[0]] if len(e) else -1                # component (m >= 2, diagonal terms)
     _check(cv.HMM(pi, a, b), pi, a, b, off, obs, comp)
+
+
+@pytest.mark.parametrize("nshards,resume", [(3, "0"), (3, "1"), (1, "0")])
+def test_constrained_exchange_shards(gpu, monkeypatch, nshards, resume):
+    """cv_decode_constrained_exchange per shard, the callback handing back the SUM of every
+    shard's partials (what the all-reduce returns), == cv_decode_constrained's slice of that
+    shard, with and without the resume flow; the callback sees exactly the shard's partials."""
+    from cviterbi import dist as cvdist
+
+    monkeypatch.setenv("CV_NO_RESUME", resume)
+    pi, a, b, off, obs, comp = _resume_case(256, 21, nseq=60)
+    h = cv.HMM(pi, a, b)
+    ncomp = 5
+    path, score, status, states, obj = cv.decode_constrained(h, off, obs, comp, ncomp)
+    B = len(off) - 1
+    pairs = cv.constrained_pairs(off, comp, ncomp)
+    shards = [cvdist.shard_range(B, nshards, r)[:2] for r in range(nshards)]
+    parts = [cv.constrained_partials(h, cvdist.shard_offsets(off, s0, s1), obs[off[s0]:off[s1]],
+                                     comp[off[s0]:off[s1]], ncomp, pairs) for s0, s1 in shards]
+    total = np.sum(parts, axis=0)
+    for (s0, s1), own in zip(shards, parts):
+        lo, hi = off[s0], off[s1]
+        seen = []
+
+        def exchange(w, own=own):
+            seen.append(np.array_equal(w, own))
+            return total
+
+        p, s, st, got_states, explored, _ = cv.decode_constrained_exchange(
+            h, cvdist.shard_offsets(off, s0, s1), obs[lo:hi], comp[lo:hi], ncomp, pairs, exchange)
+        assert seen == [True]
+        assert np.array_equal(got_states, states)
+        assert np.array_equal(p, path[lo:hi]) and np.array_equal(s, score[s0:s1]) and np.array_equal(st, status[s0:s1])
+
+
+def _sharded_worker(rank, world, port, q):
+    import os
+    import sys
+    from conftest import ROOT
+    sys.path.insert(0, os.path.join(ROOT, "consistent-viterbi_amd"))
+    import torch.distributed as dist
+    from cviterbi import dist as cvd
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        pi, a, b, off, obs, comp = _resume_case(256, 31, nseq=50)
+        h = cv.HMM(pi, a, b)
+        got = cvd.constrained_decode_sharded(h, off, obs, comp, 5, dist)
+        if rank == 0:
+            ref = cv.decode_constrained(h, off, obs, comp, 5)
+            q.put(all(np.array_equal(np.asarray(x), np.asarray(y)) for x, y in zip(got, ref)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_constrained_sharded_two_processes(gpu):
+    """cviterbi.dist.constrained_decode_sharded in 2 processes (gloo for the exchange and the
+    gather, both ranks on cuda:0) == the single-process decode on rank 0."""
+    import torch.multiprocessing as mp
+    from test_dist import _free_port
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    mp.start_processes(_sharded_worker, args=(2, _free_port(), q), nprocs=2, join=True, start_method="spawn")
+    assert q.get(timeout=5) is True
