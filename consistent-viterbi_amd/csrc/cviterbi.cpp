@@ -31,6 +31,7 @@
 #include "kernels/exact.h"
 #include "kernels/fit.h"
 #include "kernels/trellis.h"
+#include "kernels/trellis64.h"
 
 namespace {
 
@@ -117,6 +118,10 @@ struct cv_hmm {
   // f64 tables (generic f64 kernel + re-scoring): pi[N], a[N*N], et[V][N]
   bool f64_ready = false;
   DevBuf d_pi64, d_a64, d_et64;
+  // exact-f64 trellis tables (trellis_fwd_f64 / backtrack_f64), padded to np64 = 64*ceil(N/64)
+  int np64 = 0;
+  bool t64_ready = false;
+  DevBuf q_a, q_at, q_pi, q_et;
   // f32 generic tables
   bool g32_ready = false;
   DevBuf d_pi32, d_a32, d_et32;
@@ -259,6 +264,32 @@ cv_status ensure_f64_tables(cv_hmm* h) {
   if ((st = upload(h->d_a64, h->a.data(), (size_t)N * N * 8)) != CV_OK) return st;
   if ((st = upload(h->d_et64, et.data(), et.size() * 8)) != CV_OK) return st;
   h->f64_ready = true;
+  return CV_OK;
+}
+
+// Exact-f64 trellis tables: a [NP][NP] row-major, a^T, pi [NP], et [V][NP]; -inf padded.
+cv_status ensure_t64_tables(cv_hmm* h) {
+  if (h->t64_ready) return CV_OK;
+  const int N = h->N, NP = cvk::t64_padded_states(N);
+  const int64_t V = h->V;
+  const double ninf = -INFINITY;
+  std::vector<double> a((size_t)NP * NP, ninf), at((size_t)NP * NP, ninf), pi(NP, ninf), et((size_t)V * NP, ninf);
+  for (int i = 0; i < N; ++i) {
+    pi[i] = h->pi[i];
+    for (int j = 0; j < N; ++j) {
+      a[(size_t)i * NP + j] = h->a[(size_t)i * N + j];
+      at[(size_t)j * NP + i] = h->a[(size_t)i * N + j];
+    }
+  }
+  for (int j = 0; j < N; ++j)
+    for (int64_t o = 0; o < V; ++o) et[(size_t)o * NP + j] = h->b[(size_t)j * V + o];
+  cv_status st;
+  if ((st = upload(h->q_a, a.data(), a.size() * 8)) != CV_OK) return st;
+  if ((st = upload(h->q_at, at.data(), at.size() * 8)) != CV_OK) return st;
+  if ((st = upload(h->q_pi, pi.data(), pi.size() * 8)) != CV_OK) return st;
+  if ((st = upload(h->q_et, et.data(), et.size() * 8)) != CV_OK) return st;
+  h->np64 = NP;
+  h->t64_ready = true;
   return CV_OK;
 }
 
@@ -430,12 +461,20 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
     if (!trellis_ok)
       return set_err(CV_EUNSUPPORTED, "trellis kernel needs dtype f32, assoc VITERBI and N <= 256");
     use_trellis = true;
-  } else if (o.kernel == CV_KERNEL_GENERIC || o.kernel == CV_KERNEL_AUTO) {
+  } else if (o.kernel == CV_KERNEL_GENERIC || o.kernel == CV_KERNEL_AUTO || o.kernel == CV_KERNEL_TRELLIS_F64) {
     use_trellis = o.kernel == CV_KERNEL_AUTO && trellis_ok;
   } else {
     return set_err(CV_EINVAL, "bad kernel %d", o.kernel);
   }
-  if (!use_trellis && h->N > cvk::generic_max_states(o.dtype == CV_DTYPE_F64 ? 8 : 4))
+  // exact f64, row-A0 association, N <= 256, no forced states: trellis_fwd_f64 (one wave per
+  // S sequences) unless the generic kernel is asked for
+  const bool t64_ok = o.dtype == CV_DTYPE_F64 && o.assoc == CV_ASSOC_VITERBI && !o.forced && !resume_rows &&
+                      cvk::t64_padded_states(h->N) != 0;
+  if (o.kernel == CV_KERNEL_TRELLIS_F64 && !t64_ok)
+    return set_err(CV_EUNSUPPORTED, "f64 trellis kernel needs dtype f64, assoc VITERBI, N <= 256, no forced states");
+  const bool use_t64 = !use_trellis && t64_ok &&
+                       (o.kernel == CV_KERNEL_TRELLIS_F64 || (o.kernel == CV_KERNEL_AUTO && !(o.flags & CV_FLAG_NO_T64)));
+  if (!use_trellis && !use_t64 && h->N > cvk::generic_max_states(o.dtype == CV_DTYPE_F64 ? 8 : 4))
     return set_err(CV_EUNSUPPORTED, "N=%d exceeds the generic kernel's LDS capacity", h->N);
 
   std::vector<int64_t> off_copy;
@@ -452,6 +491,7 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
   if (use_trellis && (st = ensure_trellis_tables(h)) != CV_OK) return st;
   if (need_f64 && (st = ensure_f64_tables(h)) != CV_OK) return st;
   if (!use_trellis && o.dtype == CV_DTYPE_F32 && (st = ensure_g32_tables(h)) != CV_OK) return st;
+  if (use_t64 && (st = ensure_t64_tables(h)) != CV_OK) return st;
 
   // trellis variant: all-VALU unless the (slower, experimental) MFMA-assisted one is asked for
   const bool want_mfma = (o.flags & CV_FLAG_MFMA_TRELLIS) || ((o.flags >> 8) & 0xFF);
@@ -467,19 +507,21 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
     if (h->np != 256) mt = cvk::mfma_default_mt(h->np);
   }
   h->last_launches = 0;
-  h->last_kernel = use_trellis ? CV_KERNEL_TRELLIS : CV_KERNEL_GENERIC;
+  h->last_kernel = use_trellis ? CV_KERNEL_TRELLIS : use_t64 ? CV_KERNEL_TRELLIS_F64 : CV_KERNEL_GENERIC;
   // N <= 64: one wave per sequence, forward and backtrack fused (trellis_wave_f32) on tables
   // padded to npw = 16 * ceil(N / 16); its chunks run back to back on one stream (nothing to
   // overlap)
   const bool wave = use_trellis && !use_mfma && h->npw > 0 && !(o.flags & CV_FLAG_NO_WAVE);
-  h->last_np = use_trellis ? (wave ? h->npw : h->np) : 0;
+  h->last_np = use_trellis ? (wave ? h->npw : h->np) : use_t64 ? h->np64 : 0;
   h->last_mt = use_mfma ? mt : -1;
   if (nseq == 0) return CV_OK;
   HIP_TRY(hipMemsetAsync(status_dev, 0, (size_t)nseq, stream));
 
   // Per-element workspace bytes: trellis keeps f32 delta rows [NP]; generic keeps u16 psi [N].
   const uint64_t cap = o.workspace_bytes ? o.workspace_bytes : kDefaultWorkspace;
-  const uint64_t per_elem = use_trellis ? (uint64_t)(wave ? h->npw : h->np) * 4 : (uint64_t)h->N * 2;
+  const uint64_t per_elem = use_trellis ? (uint64_t)(wave ? h->npw : h->np) * 4
+                           : use_t64   ? (uint64_t)h->np64 * 8
+                                       : (uint64_t)h->N * 2;
   const int real_bytes = o.dtype == CV_DTYPE_F64 ? 8 : 4;
   const uint64_t total_elems = (uint64_t)(offsets_host[nseq] - offsets_host[0]);
   // Chunks (contiguous in the original order) are pipelined over two streams: the forward
@@ -493,7 +535,11 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
   const int group = (!plain || (o.flags & CV_FLAG_NO_PAIR)) ? 1 : 2;
   const uint64_t half_cap = std::max<uint64_t>(serial ? cap : cap / 2, per_elem);
   uint64_t nchunks = std::max<uint64_t>(1, (total_elems * per_elem + half_cap - 1) / half_cap);
-  if (!serial) nchunks = std::max<uint64_t>(nchunks, std::min<uint64_t>(8, (uint64_t)(nseq / 2048)));
+  // t64: chunks of >= 8 sequences x 2 waves x 4 SIMDs x CUs so every chunk runs S = 8
+  if (!serial)
+    nchunks = std::max<uint64_t>(
+        nchunks, use_t64 ? std::min<uint64_t>(4, (uint64_t)(nseq / (64 * (int64_t)std::max(h->cus, 1))))
+                         : std::min<uint64_t>(8, (uint64_t)(nseq / 2048)));
   const uint64_t target = std::max<uint64_t>(1, (total_elems + nchunks - 1) / nchunks);
   const uint64_t elem_cap = std::max<uint64_t>(half_cap / per_elem, 1);
   std::vector<std::pair<int64_t, int64_t>> chunks;
@@ -519,7 +565,7 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
     const int64_t T0c = offsets_host[1] - offsets_host[0];
     bool uniform = T0c > 0;
     for (int64_t s = 1; s < nseq && uniform; ++s) uniform = (offsets_host[s + 1] - offsets_host[s]) == T0c;
-    const int64_t unit = group * (int64_t)std::max(h->cus, 1);
+    const int64_t unit = (use_t64 ? 64 : group) * (int64_t)std::max(h->cus, 1);
     if (uniform && chunks.size() > 1) {
       const int64_t cap_seqs = std::max<int64_t>((int64_t)(elem_cap / (uint64_t)T0c), 1);
       int64_t per = (nseq + (int64_t)chunks.size() - 1) / (int64_t)chunks.size();
@@ -627,6 +673,23 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
           err = cvk::launch_trellis_fwd(h->np, fa, n - 2 * np2, stream);
         }
       }
+    } else if (use_t64) {
+      cvk::T64FwdArgs fa{};
+      fa.a = h->q_a.as<double>();
+      fa.pi = h->q_pi.as<double>();
+      fa.et = h->q_et.as<double>();
+      fa.offsets = offsets_dev;
+      fa.obs = obs_dev;
+      fa.order = order_dev;
+      fa.seq_begin = c.first;
+      fa.nslots = n;
+      fa.delta = reinterpret_cast<double*>(wsb);
+      fa.delta_elem_base = offsets_host[c.first];
+      fa.status = status_dev;
+      fa.nobs = (int)h->V;
+      const int spw = cvk::t64_seqs_per_wave(n, h->cus);
+      h->last_mt = spw;
+      err = cvk::launch_t64_fwd(h->np64, spw, fa, n, stream);
     } else if (o.dtype == CV_DTYPE_F64) {
       cvk::GenericFwdArgs<double> fa{};
       fa.a = h->d_a64.as<double>();
@@ -693,6 +756,20 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
         ra.score = score_dev;
         err = cvk::launch_rescore_f64(ra, n, bts, reserve);
       }
+    } else if (use_t64) {
+      cvk::T64BtArgs ba{};
+      ba.delta = reinterpret_cast<const double*>(wsb);
+      ba.delta_elem_base = offsets_host[c.first];
+      ba.at = h->q_at.as<double>();
+      ba.offsets = offsets_dev;
+      ba.order = order_dev;
+      ba.seq_begin = c.first;
+      ba.seq_end = c.second;
+      ba.nstates = h->N;
+      ba.path = path_dev;
+      ba.score = score_dev;  // the f64 delta is already the reference score: no re-score
+      ba.status = status_dev;
+      err = cvk::launch_t64_bt(h->np64, ba, n, bts);
     } else if (o.dtype == CV_DTYPE_F64) {
       cvk::GenericBtArgs<double> ba{};
       ba.psi = reinterpret_cast<const uint16_t*>(wsb);

@@ -1,0 +1,44 @@
+// trellis64.h -- exact-f64 trellis kernels for N <= 256 (trellis64.hip).
+// Internal to libcviterbi; the public boundary is include/cviterbi.h.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace cvk {
+
+struct T64FwdArgs {
+  const double* a;         // [NP][NP] row-major a[i][j], -inf padded
+  const double* pi;        // [NP], -inf padded
+  const double* et;        // [V][NP] emissions transposed, -inf padded
+  const int64_t* offsets;  // [nseq_total+1] element offsets
+  const int32_t* obs;      // [sum T]
+  const int32_t* order;    // optional schedule: slot -> sequence id
+  int64_t seq_begin;       // first schedule slot of this launch
+  int64_t nslots;          // slots in this launch
+  double* delta;           // [(elements of chunk)][NP] f64 delta rows for the backtrack
+  int64_t delta_elem_base; // element offset that maps to delta row 0
+  uint8_t* status;         // [nseq_total] (pre-zeroed); forward sets BADOBS
+  int nobs;                // V
+};
+
+struct T64BtArgs {
+  const double* delta;
+  int64_t delta_elem_base;
+  const double* at;        // [NP][NP]: at[j*NP + i] = a[i][j]
+  const int64_t* offsets;
+  const int32_t* order;
+  int64_t seq_begin, seq_end;
+  int nstates;             // real N
+  int32_t* path;           // [sum T]
+  double* score;           // [nseq_total]
+  uint8_t* status;
+};
+
+// NP = 64 * ceil(N / 64) for 1 <= N <= 256, else 0 (no f64 trellis kernel)
+int t64_padded_states(int n);
+// sequences per forward wave (2, 4 or 8) for a launch of nseq sequences on `cus` CUs
+int t64_seqs_per_wave(int64_t nseq, int cus);
+hipError_t launch_t64_fwd(int np, int s, const T64FwdArgs& fa, int64_t nseq, hipStream_t stream);
+hipError_t launch_t64_bt(int np, const T64BtArgs& ba, int64_t nseq, hipStream_t stream);
+
+}  // namespace cvk

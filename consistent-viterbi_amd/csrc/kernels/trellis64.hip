@@ -1,0 +1,320 @@
+// trellis64.hip -- exact-f64 Viterbi trellis for N <= 256 (gfx950).
+//
+// The reference solvers compute in f64 (hmm.rs:10-18 stores Array2<f64>; viterbi.rs:13-18,
+// cp.rs:70-79).  This is the row-A0 recurrence of SURVEY.md §8a in f64:
+//   d0[j] = pi[j] + b[j,o0]                 (hmm.rs:215-218, cp.rs:66-68)
+//   m     = max_i (d[i] + a[i,j])            (viterbi.rs:15-16)
+//   d'[j] = m + b[j,o]                       (viterbi.rs:17)
+// with the first-index argmax (ndarray-stats 0.5 argmax) recovered in the backtrack by the
+// same f64 adds, so paths and scores are bit-identical to the f64 oracle.
+//
+// trellis_fwd_f64<C, S>: ONE WAVE decodes S sequences in lock step.  Lane l owns the C
+// consecutive columns [C*l, C*l + C) of NP = 64*C padded states for all S sequences
+// (acc = C*S f64 accumulators).  A (NP*NP f64 = 512 KiB at N = 256) fits neither the
+// register file nor LDS, so each A row is streamed from L2 (2 KiB per row, coalesced, a
+// PF-deep register ring) and reused by the S sequences: 8/S bytes of L2 traffic per
+// (from,to) pair.  delta_{t-1} of the S sequences lives in the wave's own LDS slice as
+// [row][S] and is broadcast with ds_read_b128 (2 sequences per read, same address in every
+// lane).  Per pair: one v_add_f64 + one v_max_f64, both full rate on gfx950
+// (profiles/r01_f64_rates.txt: ~59 lane-ops/clk/CU at 4 waves/SIMD, ~53 at 2).  No barrier:
+// the wave is its own workgroup.  No argmax in the forward pass: each f64 delta row goes
+// to HBM (8*NP B per sequence step) for the backtrack.
+//
+// backtrack_f64<KP>: one wave per sequence, candidates i = lane + 64k; recomputes
+// s_i = d_{t-1}[i] + a[i, path[t]] in f64 and takes the first argmax (cp.rs:85-93).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "trellis.h"
+#include "trellis64.h"
+
+namespace cvk {
+
+namespace {
+
+__device__ __forceinline__ double ninf_d() { return -__builtin_inf(); }
+
+// C consecutive f64 of one A row (16-byte aligned for even C: dwordx4 loads)
+template <int C>
+__device__ __forceinline__ void load_a(const double* p, double (&a)[C]) {
+  if constexpr (C % 2 == 0) {
+    const double2* q = reinterpret_cast<const double2*>(p);
+#pragma unroll
+    for (int c = 0; c < C / 2; ++c) {
+      const double2 v = q[c];
+      a[2 * c] = v.x;
+      a[2 * c + 1] = v.y;
+    }
+  } else {
+#pragma unroll
+    for (int c = 0; c < C; ++c) a[c] = p[c];
+  }
+}
+
+template <int C, int S>
+__global__ __launch_bounds__(64) void trellis_fwd_f64(T64FwdArgs g) {
+  constexpr int NP = 64 * C;
+  constexpr int PF = 4;  // A rows in flight
+  static_assert(S % 2 == 0, "S sequences are read from LDS two at a time");
+  __shared__ __attribute__((aligned(16))) double dl[NP * S];  // delta_{t-1}: [row][S]
+  const int lane = threadIdx.x;
+  const int j0 = lane * C;
+  const int64_t slot0 = g.seq_begin + (int64_t)blockIdx.x * S;
+  const int64_t slot_end = g.seq_begin + g.nslots;
+  const double ninf = ninf_d();
+
+  int64_t seq[S], e0[S];
+  int T[S];
+  int Tmax = 0;
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    const int64_t slot = slot0 + s;
+    if (slot < slot_end) {
+      seq[s] = g.order ? (int64_t)g.order[slot] : slot;
+      e0[s] = g.offsets[seq[s]];
+      T[s] = (int)(g.offsets[seq[s] + 1] - e0[s]);
+    } else {
+      seq[s] = -1;
+      e0[s] = 0;
+      T[s] = 0;
+    }
+    Tmax = T[s] > Tmax ? T[s] : Tmax;
+  }
+  if (Tmax <= 0) return;
+  const unsigned V = (unsigned)g.nobs;
+  unsigned bad = 0;  // bit s: sequence s saw an out-of-range observation
+
+  // emission columns [j0, j0+C) of observation o (or -inf when o is out of range)
+  auto emis = [&](int s, int t, double (&e)[C]) {
+    int o = 0;
+    if (t < T[s]) o = g.obs[e0[s] + t];
+    const bool ok = (unsigned)o < V;
+    if (t < T[s] && !ok) bad |= 1u << s;
+    const double* row = g.et + (size_t)(ok ? o : 0) * NP + j0;
+#pragma unroll
+    for (int c = 0; c < C; ++c) e[c] = ok ? row[c] : ninf;
+  };
+  auto store_row = [&](int s, int t, const double (&v)[C]) {
+    if (t < T[s]) {
+      double* dst = g.delta + (e0[s] + t - g.delta_elem_base) * NP + j0;
+#pragma unroll
+      for (int c = 0; c < C; ++c) dst[c] = v[c];
+    }
+  };
+
+  // t = 0: d0 = pi + b[:, o0]
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    double e[C], v[C];
+    emis(s, 0, e);
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      v[c] = g.pi[j0 + c] + e[c];
+      dl[(j0 + c) * S + s] = v[c];
+    }
+    store_row(s, 0, v);
+  }
+  __syncthreads();
+
+  const double* __restrict__ arow = g.a + j0;
+  for (int t = 1; t < Tmax; ++t) {
+    double acc[C][S];
+#pragma unroll
+    for (int c = 0; c < C; ++c)
+#pragma unroll
+      for (int s = 0; s < S; ++s) acc[c][s] = ninf;
+    double ar[PF][C];
+#pragma unroll
+    for (int u = 0; u < PF; ++u) load_a(arow + (size_t)u * NP, ar[u]);
+#pragma nounroll
+    for (int i0 = 0; i0 < NP; i0 += PF) {
+#pragma unroll
+      for (int u = 0; u < PF; ++u) {
+        const int i = i0 + u;
+        double a[C];
+#pragma unroll
+        for (int c = 0; c < C; ++c) a[c] = ar[u][c];
+        // refill this ring slot with row i + PF (clamped: the last rows reload row NP-1)
+        const int nr = min(i + PF, NP - 1);
+        load_a(arow + (size_t)nr * NP, ar[u]);
+        const double2* drow = reinterpret_cast<const double2*>(dl + i * S);
+#pragma unroll
+        for (int s2 = 0; s2 < S / 2; ++s2) {
+          const double2 d = drow[s2];
+#pragma unroll
+          for (int c = 0; c < C; ++c) {
+            acc[c][2 * s2] = fmax(acc[c][2 * s2], d.x + a[c]);
+            acc[c][2 * s2 + 1] = fmax(acc[c][2 * s2 + 1], d.y + a[c]);
+          }
+        }
+      }
+    }
+    __syncthreads();  // every lane has read delta_{t-1} before it is overwritten
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      double e[C], v[C];
+      emis(s, t, e);
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        v[c] = acc[c][s] + e[c];
+        dl[(j0 + c) * S + s] = v[c];
+      }
+      store_row(s, t, v);
+    }
+    __syncthreads();
+  }
+  if (lane == 0) {
+#pragma unroll
+    for (int s = 0; s < S; ++s)
+      if (bad & (1u << s)) g.status[seq[s]] = CVK_SEQ_BADOBS;
+  }
+}
+
+__device__ __forceinline__ double wave_max_d(double v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v = fmax(v, __shfl_xor(v, off));
+  return v;
+}
+
+template <int KP>
+__global__ __launch_bounds__(256) void backtrack_f64(T64BtArgs g) {
+  constexpr int NP = 64 * KP;
+  constexpr int PF = 8;
+  const int lane = threadIdx.x & 63;
+  const int64_t slot = g.seq_begin + (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (slot >= g.seq_end) return;
+  const int64_t seq = g.order ? (int64_t)g.order[slot] : slot;
+  const int64_t e0 = g.offsets[seq];
+  const int T = (int)(g.offsets[seq + 1] - e0);
+  const int N = g.nstates;
+  if (T <= 0) {
+    if (lane == 0) {
+      g.score[seq] = 0.0;
+      g.status[seq] = CVK_SEQ_EMPTY;
+    }
+    return;
+  }
+  int32_t* __restrict__ path = g.path + e0;
+  const double* __restrict__ drow = g.delta + (e0 - g.delta_elem_base) * NP;
+  bool valid[KP];
+#pragma unroll
+  for (int k = 0; k < KP; ++k) valid[k] = (lane + 64 * k) < N;
+  auto load_row = [&](int r, double (&dst)[KP]) {
+#pragma unroll
+    for (int k = 0; k < KP; ++k) dst[k] = (r >= 0 && valid[k]) ? drow[(size_t)r * NP + lane + 64 * k] : ninf_d();
+  };
+  auto first_argmax = [&](const double (&s)[KP], double& M) {
+    double m = s[0];
+#pragma unroll
+    for (int k = 1; k < KP; ++k) m = fmax(m, s[k]);
+    M = wave_max_d(m);
+    int idx = 0;
+#pragma unroll
+    for (int k = KP - 1; k >= 0; --k) {
+      const unsigned long long mask = __ballot(valid[k] && s[k] == M);
+      if (mask) idx = 64 * k + __builtin_ctzll(mask);
+    }
+    return idx;
+  };
+  double bv;
+  int cur;
+  {
+    double last[KP];
+    load_row(T - 1, last);
+    cur = first_argmax(last, bv);  // cp.rs:86
+  }
+  const uint8_t prior = g.status[seq];
+  if (!(bv > ninf_d()) || prior == CVK_SEQ_BADOBS) {
+    for (int t = lane; t < T; t += 64) path[t] = 0;
+    if (lane == 0) {
+      g.score[seq] = ninf_d();
+      g.status[seq] = prior == CVK_SEQ_BADOBS ? CVK_SEQ_BADOBS : CVK_SEQ_INFEASIBLE;
+    }
+    return;
+  }
+  int pathreg = 0;
+  if (lane == ((T - 1) & 63)) pathreg = cur;
+  if (((T - 1) & 63) == 0 && lane == 0) path[T - 1] = cur;
+  double ring[PF][KP];
+#pragma unroll
+  for (int u = 0; u < PF; ++u) load_row(T - 2 - u, ring[u]);
+  for (int base = T - 1; base >= 1; base -= PF) {
+#pragma unroll
+    for (int u = 0; u < PF; ++u) {
+      const int t = base - u;
+      if (t >= 1) {
+        const double* acol = g.at + (size_t)cur * NP + lane;
+        double s[KP];
+#pragma unroll
+        for (int k = 0; k < KP; ++k) s[k] = valid[k] ? ring[u][k] + acol[64 * k] : ninf_d();
+        double M;
+        cur = first_argmax(s, M);
+        const int tp = t - 1;
+        if (lane == (tp & 63)) pathreg = cur;
+        if ((tp & 63) == 0 && tp + lane < T) path[tp + lane] = pathreg;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < PF; ++u) load_row(base - PF - 1 - u, ring[u]);
+  }
+  if (lane == 0) {
+    g.score[seq] = bv;
+    g.status[seq] = CVK_SEQ_OK;
+  }
+}
+
+template <int C, int S>
+hipError_t fwd_cs(const T64FwdArgs& fa, int64_t nseq, hipStream_t stream) {
+  const int64_t blocks = (nseq + S - 1) / S;
+  hipLaunchKernelGGL((trellis_fwd_f64<C, S>), dim3((unsigned)blocks), dim3(64), 0, stream, fa);
+  return hipGetLastError();
+}
+
+template <int C>
+hipError_t fwd_c(const T64FwdArgs& fa, int s, int64_t nseq, hipStream_t stream) {
+  switch (s) {
+    case 2: return fwd_cs<C, 2>(fa, nseq, stream);
+    case 4: return fwd_cs<C, 4>(fa, nseq, stream);
+    case 8: return fwd_cs<C, 8>(fa, nseq, stream);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+}  // namespace
+
+int t64_padded_states(int n) { return (n >= 1 && n <= 256) ? 64 * ((n + 63) / 64) : 0; }
+
+int t64_seqs_per_wave(int64_t nseq, int cus) {
+  // fill at least two waves per SIMD (4 SIMDs per CU), then prefer the larger S: each A row
+  // streamed from L2 serves S sequences
+  const int64_t simd_waves = 2 * 4 * (int64_t)(cus > 0 ? cus : 256);
+  if (nseq >= 8 * simd_waves) return 8;
+  if (nseq >= 4 * simd_waves) return 4;
+  return 2;
+}
+
+hipError_t launch_t64_fwd(int np, int s, const T64FwdArgs& fa, int64_t nseq, hipStream_t stream) {
+  if (nseq <= 0) return hipSuccess;
+  switch (np) {
+    case 64: return fwd_c<1>(fa, s, nseq, stream);
+    case 128: return fwd_c<2>(fa, s, nseq, stream);
+    case 192: return fwd_c<3>(fa, s, nseq, stream);
+    case 256: return fwd_c<4>(fa, s, nseq, stream);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+hipError_t launch_t64_bt(int np, const T64BtArgs& ba, int64_t nseq, hipStream_t stream) {
+  if (nseq <= 0) return hipSuccess;
+  const dim3 grid((unsigned)((nseq + 3) / 4)), block(256);
+  switch (np) {
+    case 64: hipLaunchKernelGGL(backtrack_f64<1>, grid, block, 0, stream, ba); break;
+    case 128: hipLaunchKernelGGL(backtrack_f64<2>, grid, block, 0, stream, ba); break;
+    case 192: hipLaunchKernelGGL(backtrack_f64<3>, grid, block, 0, stream, ba); break;
+    case 256: hipLaunchKernelGGL(backtrack_f64<4>, grid, block, 0, stream, ba); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+}  // namespace cvk

@@ -15,7 +15,8 @@ from .hmm import HMM
 
 _DT = {"f32": L.DTYPE_F32, "f64": L.DTYPE_F64, np.float32: L.DTYPE_F32, np.float64: L.DTYPE_F64}
 _ASSOC = {"viterbi": L.ASSOC_VITERBI, "cp": L.ASSOC_CP, "dp": L.ASSOC_DP, "decode": L.ASSOC_DECODE}
-_KERNEL = {"auto": L.KERNEL_AUTO, "trellis": L.KERNEL_TRELLIS, "generic": L.KERNEL_GENERIC}
+_KERNEL = {"auto": L.KERNEL_AUTO, "trellis": L.KERNEL_TRELLIS, "generic": L.KERNEL_GENERIC,
+           "trellis_f64": L.KERNEL_TRELLIS_F64}
 
 
 def _p(x):
@@ -240,7 +241,7 @@ def last_timing(hmm: HMM) -> dict:
     t = L.Timing()
     L.check(L.lib().cv_last_timing(hmm.handle, ctypes.byref(t)))
     return dict(fwd_ms=t.fwd_ms, bt_ms=t.bt_ms, total_ms=t.total_ms, launches=t.launches,
-                kernel={1: "trellis", 2: "generic"}.get(t.kernel, "none"), padded_states=t.padded_states,
+                kernel={1: "trellis", 2: "generic", 3: "trellis_f64"}.get(t.kernel, "none"), padded_states=t.padded_states,
                 mfma_tiles=t.mfma_tiles)
 
 

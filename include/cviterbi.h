@@ -57,8 +57,10 @@ enum { CV_DTYPE_F32 = 0, CV_DTYPE_F64 = 1 };
 enum { CV_ASSOC_VITERBI = 0, CV_ASSOC_CP = 1, CV_ASSOC_DP = 2, CV_ASSOC_DECODE = 3 };
 
 /* kernel choice: AUTO picks TRELLIS (register-resident A, f32, VITERBI, N <= 256) when it
- * applies, else GENERIC (inline argmax, f32/f64, any association, N <= 8192 f32 / 4096 f64). */
-enum { CV_KERNEL_AUTO = 0, CV_KERNEL_TRELLIS = 1, CV_KERNEL_GENERIC = 2 };
+ * applies, then TRELLIS_F64 (exact f64, VITERBI, N <= 256, no forced states: one wave per
+ * 2/4/8 sequences, A streamed from L2), else GENERIC (inline argmax, f32/f64, any
+ * association, N <= 8192 f32 / 4096 f64). */
+enum { CV_KERNEL_AUTO = 0, CV_KERNEL_TRELLIS = 1, CV_KERNEL_GENERIC = 2, CV_KERNEL_TRELLIS_F64 = 3 };
 
 /* cv_opts.flags */
 /* MFMA-assisted trellis (64 <= N <= 256) instead of the all-VALU one.  Bit-identical, but
@@ -69,6 +71,8 @@ enum { CV_KERNEL_AUTO = 0, CV_KERNEL_TRELLIS = 1, CV_KERNEL_GENERIC = 2 };
 #define CV_FLAG_NO_PAIR 0x4u      /* one sequence per forward workgroup (A/B knob; bit-identical) */
 #define CV_FLAG_NO_WAVE 0x8u      /* N <= 64: the workgroup kernels instead of one wave per sequence
                                      with the backtrack fused (A/B knob; bit-identical) */
+#define CV_FLAG_NO_T64 0x10u     /* f64: the generic kernel instead of TRELLIS_F64 (A/B knob;
+                                     bit-identical) */
 /* MFMA tiles per wave per step for the MFMA-assisted kernel (implies it; N in (224,256]:
  * 0, 4..8; default 6).  Results are bit-identical for every value. */
 #define CV_FLAG_MFMA_TILES(n) ((uint32_t)((n) + 1) << 8)
@@ -107,9 +111,10 @@ typedef struct cv_timing {
   double bt_ms;          /* backtrack (+ f64 re-score) kernel(s) */
   double total_ms;       /* first kernel start to last kernel end (device) */
   int64_t launches;      /* forward launches (chunks) */
-  int32_t kernel;        /* CV_KERNEL_TRELLIS or CV_KERNEL_GENERIC actually used */
+  int32_t kernel;        /* CV_KERNEL_TRELLIS, _TRELLIS_F64 or _GENERIC actually used */
   int32_t padded_states; /* NP of the trellis kernel (0 for generic) */
-  int32_t mfma_tiles;    /* MFMA tiles per wave of the trellis kernel, -1 = all-VALU kernel */
+  int32_t mfma_tiles;    /* MFMA tiles per wave of the trellis kernel, -1 = all-VALU kernel;
+                            TRELLIS_F64: sequences per forward wave (last chunk) */
 } cv_timing;
 
 typedef struct cv_superseq_desc {

@@ -1,0 +1,126 @@
+"""Exact-f64 trellis kernel (trellis_fwd_f64 + backtrack_f64) against the f64
+oracle: the reference's own precision (hmm.rs:10-18 stores f64; viterbi.rs:13-18 row A0).
+
+Bar (BASELINE.json north_star): paths bit-exact and scores bit-exact (tolerance 0 < 1e-6
+relative) against the f64 oracle, every status identical; and identical to the generic f64
+kernel (inline first-argmax) on batches too large for the oracle to finish in seconds.
+"""
+import numpy as np
+import pytest
+
+import c_oracle as O
+import cviterbi as cv
+from cviterbi import synth
+
+pytestmark = pytest.mark.gpu
+
+
+def _case(n, v, seed, nseq=12, tmax=70, zero_frac=0.0, tmin=1):
+    pi, a, b = synth.random_hmm(n, v, seed=seed, zero_frac=zero_frac)
+    rng = np.random.default_rng(seed + 100)
+    lengths = rng.integers(tmin, tmax + 1, size=nseq)
+    off = synth.offsets_from_lengths(lengths)
+    obs = rng.integers(0, v, size=int(off[-1])).astype(np.int32)
+    return pi, a, b, off, obs
+
+
+def _assert_same(got, ref, what):
+    gp, gs, gst = got
+    rp, rs, rst = ref
+    assert np.array_equal(gst, rst), f"{what}: status {gst} vs {rst}"
+    bad = np.nonzero(gs != rs)[0]
+    assert bad.size == 0, f"{what}: scores differ at seqs {bad[:8]}: {gs[bad[:4]]} vs {rs[bad[:4]]}"
+    assert np.array_equal(gp, rp), f"{what}: paths differ at {np.nonzero(gp != rp)[0][:8]}"
+
+
+@pytest.mark.parametrize("n", [1, 2, 5, 33, 45, 63, 64, 65, 100, 128, 129, 192, 200, 255, 256])
+def test_t64_bit_exact_vs_oracle(gpu, n):
+    pi, a, b, off, obs = _case(n, 41, seed=700 + n, zero_frac=0.05 if n % 2 else 0.0)
+    h = cv.HMM(pi, a, b)
+    got = cv.decode_batch(h, off, obs, dtype="f64", rescore_f64=False)
+    t = cv.last_timing(h)
+    assert t["kernel"] == "trellis_f64", t
+    assert t["padded_states"] == 64 * ((n + 63) // 64)
+    ref = O.decode_batch(pi, a, b, off, obs, O.VITERBI, np.float64)
+    _assert_same(got, ref, f"t64 N={n}")
+    # rescore_f64 changes nothing on the f64 path: the f64 delta already is the reference score
+    _assert_same(cv.decode_batch(h, off, obs, dtype="f64", rescore_f64=True), ref, f"t64 rescore N={n}")
+
+
+@pytest.mark.parametrize("n", [7, 64, 256])
+def test_t64_ties_and_infeasible(gpu, n):
+    """Quantised log-probs (many exact ties: first index must win), -inf transitions and
+    emissions (infeasible sequences), an out-of-range observation, empty and T=1 sequences."""
+    rng = np.random.default_rng(n)
+    v = 9
+    pi = np.round(rng.uniform(-2, 0, n) * 2) / 2
+    a = np.round(rng.uniform(-2, 0, (n, n)) * 2) / 2
+    b = np.round(rng.uniform(-2, 0, (n, v)) * 2) / 2
+    a[rng.random((n, n)) < 0.2] = -np.inf
+    b[:, 3] = -np.inf  # observation 3 is impossible in every state: infeasible sequences
+    lengths = np.array([0, 1, 2, 17, 40, 0, 5, 33, 1, 60, 12, 12])
+    off = synth.offsets_from_lengths(lengths)
+    obs = rng.integers(0, v, size=int(off[-1])).astype(np.int32)
+    obs[obs == 3] = 4
+    obs[off[3] + 5] = 3   # sequence 3 infeasible
+    obs[off[9] + 59] = 3  # sequence 9 infeasible at its last element
+    h = cv.HMM(pi, a, b)
+    ref = O.decode_batch(pi, a, b, off, obs, O.VITERBI, np.float64)
+    _assert_same(cv.decode_batch(h, off, obs, dtype="f64", rescore_f64=False), ref, f"ties N={n}")
+    assert cv.last_timing(h)["kernel"] == "trellis_f64"
+    # out-of-range observation index: rejected (CV_EINVAL) before any kernel runs
+    obs_bad = obs.copy()
+    obs_bad[off[4] + 2] = v + 5
+    for kernel in ("auto", "generic"):
+        with pytest.raises(cv.CVError, match="out of range"):
+            cv.decode_batch(h, off, obs_bad, dtype="f64", kernel=kernel, rescore_f64=False)
+
+
+@pytest.mark.parametrize("n", [45, 256])
+@pytest.mark.parametrize("serial", [False, True])
+def test_t64_matches_generic_f64_large(gpu, n, serial):
+    """Batches large enough for 8 sequences per wave and several chunks (workspace cap),
+    ragged lengths (longest-first schedule): identical to the generic f64 kernel, whose
+    inline first-argmax is itself bit-exact against the oracle (test_gpu_parity.py)."""
+    pi, a, b = synth.random_hmm(n, 200, seed=n + 9)
+    rng = np.random.default_rng(n + 9)
+    nseq = 20000
+    lengths = rng.integers(1, 24, size=nseq)
+    off = synth.offsets_from_lengths(lengths)
+    obs = rng.integers(0, 200, size=int(off[-1])).astype(np.int32)
+    h = cv.HMM(pi, a, b)
+    ws = int(off[-1]) * 64 * ((n + 63) // 64) * 8 // 3  # >= 3 chunks
+    got = cv.decode_batch(h, off, obs, dtype="f64", rescore_f64=False, workspace_bytes=ws, serial=serial)
+    t = cv.last_timing(h)
+    assert t["kernel"] == "trellis_f64" and t["launches"] >= 3, t
+    gen = cv.decode_batch(h, off, obs, dtype="f64", kernel="generic", rescore_f64=False)
+    _assert_same(got, gen, f"t64 vs generic N={n}")
+    # spot-check against the oracle
+    idx = rng.choice(nseq, 24, replace=False)
+    for k in idx:
+        lo, hi = off[k], off[k + 1]
+        rp, rs, rst = O.decode_batch(pi, a, b, np.array([0, hi - lo]), obs[lo:hi], O.VITERBI, np.float64)
+        assert rst[0] == got[2][k] and rs[0] == got[1][k] and np.array_equal(rp, got[0][lo:hi])
+
+
+def test_t64_config4_shape_sample(gpu):
+    """Config-4 shape (N=256, V=1,024, T=512) on 512 sequences (S=2 per wave): bit-exact vs
+    the f64 oracle on a sample, and the f32 trellis differs from the f64 reference on some
+    paths (why the exact kernel exists) while agreeing where both are exact."""
+    pi, a, b = synth.random_hmm(256, 1024, seed=20261015)
+    nseq, T = 512, 512
+    off = np.arange(nseq + 1, dtype=np.int64) * T
+    obs = synth.iid_obs(1024, nseq * T, 20261015)
+    h = cv.HMM(pi, a, b)
+    p64, s64, st64 = cv.decode_batch(h, off, obs, dtype="f64", rescore_f64=False)
+    assert cv.last_timing(h)["kernel"] == "trellis_f64"
+    sample = np.arange(0, nseq, 64)
+    for k in sample:
+        lo, hi = off[k], off[k + 1]
+        rp, rs, rst = O.decode_batch(pi, a, b, np.array([0, T]), obs[lo:hi], O.VITERBI, np.float64)
+        assert rst[0] == st64[k] and rs[0] == s64[k] and np.array_equal(rp, p64[lo:hi]), f"seq {k}"
+    p32, s32, _ = cv.decode_batch(h, off, obs, dtype="f32", rescore_f64=True)
+    same = np.array([np.array_equal(p32[off[k]:off[k + 1]], p64[off[k]:off[k + 1]]) for k in range(nseq)])
+    # where the f32 path equals the f64 one, the f64 re-score equals the f64 decode's score exactly
+    assert np.array_equal(s32[same], s64[same])
+    assert same.mean() > 0.5
