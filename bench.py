@@ -34,6 +34,8 @@ N_STATES, V_OBS, T_LEN, B_TOTAL, SEED = 256, 1024, 512, 65536, 20261015
 HBM_PEAK = 8.0e12            # B/s, MI355X_MICROARCH.md chip table (spec)
 VALU_PAIR_PEAK = 3.93e13     # (from,to) pairs/s: 256 CU x 4 SIMD x 32 lanes x 2.4 GHz / 2 VALU slots per pair
 WORKSPACE = 48 << 30         # delta workspace cap: one forward launch per step at N=1 (34.4 GB)
+WORKSPACE_F64 = 80 << 30     # f64: one launch per step too (68.7 GB of f64 delta rows)
+F64_PAIR_PEAK = 1.966e13     # f64 (from,to) pairs/s: 256 CU x 64 lanes x 2.4 GHz / (v_add_f64 + v_max_f64)
 
 
 def parse():
@@ -44,6 +46,9 @@ def parse():
     p.add_argument("--batch", type=int, default=B_TOTAL,
                    help="sequences per rank (weak) or in total (strong); default 65,536")
     p.add_argument("--scaling", choices=("weak", "strong"), default="weak")
+    p.add_argument("--dtype", choices=("f32", "f64"), default="f32",
+                   help="f32: BASELINE config 4 (f32 log-probs, f64 re-score); f64: the exact-f64 "
+                        "trellis (paths and scores bit-identical to the f64 reference recurrence)")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
     p.add_argument("--no-cpu-baseline", action="store_true")
     return p.parse_args()
@@ -139,6 +144,7 @@ def main():
         B = args.batch
         s0, s1, per = cvd.shard_range(B, world, rank)
     nloc = s1 - s0
+    f64 = args.dtype == "f64"
     pi, a, b = synth.random_hmm(N_STATES, V_OBS, seed=SEED)
     obs = synth.iid_obs(V_OBS, nloc * T_LEN, SEED, start=s0 * T_LEN)
     off = np.arange(nloc + 1, dtype=np.int64) * T_LEN
@@ -163,7 +169,8 @@ def main():
         if gathered[i] is not None:
             stream.wait_event(gathered[i])
         cv.decode_batch_device(h, off_d, obs_d, path_d, score_d, status_d, offsets_host=off,
-                               stream=stream.cuda_stream, workspace_bytes=WORKSPACE)
+                               stream=stream.cuda_stream, dtype=args.dtype,
+                               workspace_bytes=WORKSPACE_F64 if f64 else WORKSPACE)
         if world > 1:  # RCCL over xGMI: decoded paths (u8 states), scores, statuses to rank 0, one gather
             done = torch.cuda.Event()
             done.record(stream)
@@ -209,13 +216,18 @@ def main():
     ms_step = el * 1e3 / args.steps
     # roofline of the dominant kernel (forward trellis) on THIS rank, per launch
     steps_rank = nloc * T_LEN
-    alg_bytes = (9 * N_STATES + 8) * steps_rank + 8 * nloc
-    alg_read = (4 * N_STATES + 4) * steps_rank
+    if f64:  # read obs 4 B + f64 emission column 8N; write f64 delta column 8N + path 4 B
+        alg_bytes = (16 * N_STATES + 8) * steps_rank + 8 * nloc
+        alg_read = (8 * N_STATES + 4) * steps_rank
+    else:
+        alg_bytes = (9 * N_STATES + 8) * steps_rank + 8 * nloc
+        alg_read = (4 * N_STATES + 4) * steps_rank
     fwd_launch_s = fwd_ms / max(launches, 1) * 1e-3
     per_launch_bytes = alg_bytes / (launches / args.steps)
     achieved = per_launch_bytes / fwd_launch_s
     pairs_per_launch = N_STATES * N_STATES * (T_LEN - 1) * nloc / (launches / args.steps)
-    traffic = load_traffic()
+    traffic = None if f64 else load_traffic()
+    pair_peak = F64_PAIR_PEAK if f64 else VALU_PAIR_PEAK
     out = {
         "metric": "trellis cells/s (N*T*batch), N=256 T=512 batch=65536",
         "value": value,
@@ -227,23 +239,25 @@ def main():
         "higher_is_better": True,
         "scaling": args.scaling,
         "vs_baseline": None,
-        "dtype": "f32",
+        "dtype": args.dtype,
         "data": "synthetic (Dirichlet(1) log10 HMM, splitmix64 iid observations; SURVEY.md §8d config 4)",
         "config": {"workload": "config4: N=256 states, V=1024, T=512, " +
                                (f"batch=65536 per rank (global {B})" if args.scaling == "weak" else
                                 f"batch={B} sharded over {world} ranks") +
-                               ", f32 row-A0 trellis + backtrack + f64 re-score" +
+                               (", exact-f64 row-A0 trellis + backtrack" if f64 else
+                                ", f32 row-A0 trellis + backtrack + f64 re-score") +
                                (", RCCL gather to rank 0 (overlapped with the next step)" if world > 1 else ""),
                    "global_batch": B, "seq_len": T_LEN, "states": N_STATES, "parallelism": f"batch-shard x{world}"},
         "seqs_per_s": B * args.steps / el,
         "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK, "traffic": traffic,
-                     "kernel": "trellis_fwd2_f32<256>", "kernel_ms_per_launch": fwd_launch_s * 1e3,
+                     "kernel": "trellis_fwd_f64<C=4,S=8>" if f64 else "trellis_fwd2_f32<256>",
+                     "kernel_ms_per_launch": fwd_launch_s * 1e3,
                      "alg_bytes_per_launch": per_launch_bytes,
                      "read_only_frac": alg_read / (launches / args.steps) / fwd_launch_s / HBM_PEAK,
                      "binding": "valu",
-                     "valu": {"achieved_pairs_per_s": pairs_per_launch / fwd_launch_s, "peak_pairs_per_s": VALU_PAIR_PEAK,
-                              "frac": pairs_per_launch / fwd_launch_s / VALU_PAIR_PEAK}},
+                     "valu": {"achieved_pairs_per_s": pairs_per_launch / fwd_launch_s, "peak_pairs_per_s": pair_peak,
+                              "frac": pairs_per_launch / fwd_launch_s / pair_peak}},
         "kernel_ms_per_step": {"forward": fwd_ms / args.steps, "backtrack_rescore": bt_ms / args.steps},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -94,6 +94,7 @@ cv_status upload(DevBuf& buf, const void* src, size_t bytes) {
 }
 
 constexpr uint64_t kDefaultWorkspace = 8ull << 30;
+constexpr uint64_t kDefaultWorkspaceT64 = 40ull << 30;
 
 }  // namespace
 
@@ -518,7 +519,9 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
   HIP_TRY(hipMemsetAsync(status_dev, 0, (size_t)nseq, stream));
 
   // Per-element workspace bytes: trellis keeps f32 delta rows [NP]; generic keeps u16 psi [N].
-  const uint64_t cap = o.workspace_bytes ? o.workspace_bytes : kDefaultWorkspace;
+  // f64 trellis: 2 KiB of delta per element at N = 256 and >= 16,384 sequences per launch for
+  // 8 sequences per wave, so its default cap is larger (HBM3E: 288 GB per GPU)
+  const uint64_t cap = o.workspace_bytes ? o.workspace_bytes : use_t64 ? kDefaultWorkspaceT64 : kDefaultWorkspace;
   const uint64_t per_elem = use_trellis ? (uint64_t)(wave ? h->npw : h->np) * 4
                            : use_t64   ? (uint64_t)h->np64 * 8
                                        : (uint64_t)h->N * 2;
@@ -528,7 +531,10 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
   // pass of chunk k+1 runs while chunk k backtracks, out of a double-buffered workspace.
   // At least ~2,048 sequences per chunk (8 per CU), at most 8 chunks unless the
   // workspace cap forces more.
-  const bool serial = (o.flags & CV_FLAG_SERIAL) != 0 || wave;
+  // t64 runs serial: its 212-VGPR forward waves fill each SIMD exactly twice per launch, and a
+  // co-running backtrack cost more than it hid (config 4: 205.6 ms overlapped vs 191.9 ms
+  // serial, profiles/r01_t64_sweep.txt)
+  const bool serial = (o.flags & CV_FLAG_SERIAL) != 0 || wave || use_t64;
   // Sequences per forward workgroup: 2 (trellis_fwd2_f32, equal-length pairs; default) or 1
   // (trellis_fwd_f32: leftovers, MFMA, N not a multiple of 64).
   const bool plain = use_trellis && !use_mfma && !wave && cvk::trellis_pair_supported(h->np);

@@ -25,6 +25,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <cstdlib>
+
 #include "trellis.h"
 #include "trellis64.h"
 
@@ -51,10 +53,9 @@ __device__ __forceinline__ void load_a(const double* p, double (&a)[C]) {
   }
 }
 
-template <int C, int S>
+template <int C, int S, int PF>  // PF: A rows in flight
 __global__ __launch_bounds__(64) void trellis_fwd_f64(T64FwdArgs g) {
   constexpr int NP = 64 * C;
-  constexpr int PF = 4;  // A rows in flight
   static_assert(S % 2 == 0, "S sequences are read from LDS two at a time");
   __shared__ __attribute__((aligned(16))) double dl[NP * S];  // delta_{t-1}: [row][S]
   const int lane = threadIdx.x;
@@ -116,16 +117,30 @@ __global__ __launch_bounds__(64) void trellis_fwd_f64(T64FwdArgs g) {
   }
   __syncthreads();
 
+  // forward waves win issue arbitration over co-resident backtrack waves of the previous
+  // chunk (overlap mode), as in trellis_fwd2_f32
+  __builtin_amdgcn_s_setprio(3);
   const double* __restrict__ arow = g.a + j0;
+  double acc[C][S];  // after a step: delta_t of the S sequences (stored at the next step)
   for (int t = 1; t < Tmax; ++t) {
-    double acc[C][S];
+    double ar[PF][C];
+#pragma unroll
+    for (int u = 0; u < PF; ++u) load_a(arow + (size_t)u * NP, ar[u]);
+    // delta_{t-1} rows go to HBM only now: the ring loads above were issued first, so waiting
+    // for them (in-order vmcnt) does not wait for these stores
+    if (t > 1) {
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        double v[C];
+#pragma unroll
+        for (int c = 0; c < C; ++c) v[c] = acc[c][s];
+        store_row(s, t - 1, v);
+      }
+    }
 #pragma unroll
     for (int c = 0; c < C; ++c)
 #pragma unroll
       for (int s = 0; s < S; ++s) acc[c][s] = ninf;
-    double ar[PF][C];
-#pragma unroll
-    for (int u = 0; u < PF; ++u) load_a(arow + (size_t)u * NP, ar[u]);
 #pragma nounroll
     for (int i0 = 0; i0 < NP; i0 += PF) {
 #pragma unroll
@@ -157,11 +172,20 @@ __global__ __launch_bounds__(64) void trellis_fwd_f64(T64FwdArgs g) {
 #pragma unroll
       for (int c = 0; c < C; ++c) {
         v[c] = acc[c][s] + e[c];
+        acc[c][s] = v[c];
         dl[(j0 + c) * S + s] = v[c];
       }
-      store_row(s, t, v);
     }
     __syncthreads();
+  }
+  if (Tmax > 1) {
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      double v[C];
+#pragma unroll
+      for (int c = 0; c < C; ++c) v[c] = acc[c][s];
+      store_row(s, Tmax - 1, v);
+    }
   }
   if (lane == 0) {
 #pragma unroll
@@ -179,7 +203,9 @@ __device__ __forceinline__ double wave_max_d(double v) {
 template <int KP>
 __global__ __launch_bounds__(256) void backtrack_f64(T64BtArgs g) {
   constexpr int NP = 64 * KP;
-  constexpr int PF = 8;
+  // delta rows in flight; <= 88 VGPRs at KP = 4 so a backtrack wave fits beside the two
+  // 212-VGPR forward waves of a SIMD (overlap mode) instead of displacing the next chunk's
+  constexpr int PF = KP >= 3 ? 4 : 8;
   const int lane = threadIdx.x & 63;
   const int64_t slot = g.seq_begin + (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (slot >= g.seq_end) return;
@@ -266,7 +292,15 @@ __global__ __launch_bounds__(256) void backtrack_f64(T64BtArgs g) {
 template <int C, int S>
 hipError_t fwd_cs(const T64FwdArgs& fa, int64_t nseq, hipStream_t stream) {
   const int64_t blocks = (nseq + S - 1) / S;
-  hipLaunchKernelGGL((trellis_fwd_f64<C, S>), dim3((unsigned)blocks), dim3(64), 0, stream, fa);
+  static const int pf = [] {  // tuning knob (bit-identical): A rows in flight, 8 (default) or 4
+    const char* e = getenv("CV_T64_PF");
+    return e && atoi(e) == 4 ? 4 : 8;
+  }();
+  // PF = 8 measured 183 vs 208 ms (PF = 4) per config-4 forward (profiles/r01_t64_sweep.txt)
+  if (pf == 4)
+    hipLaunchKernelGGL((trellis_fwd_f64<C, S, 4>), dim3((unsigned)blocks), dim3(64), 0, stream, fa);
+  else
+    hipLaunchKernelGGL((trellis_fwd_f64<C, S, 8>), dim3((unsigned)blocks), dim3(64), 0, stream, fa);
   return hipGetLastError();
 }
 
@@ -287,6 +321,10 @@ int t64_padded_states(int n) { return (n >= 1 && n <= 256) ? 64 * ((n + 63) / 64
 int t64_seqs_per_wave(int64_t nseq, int cus) {
   // fill at least two waves per SIMD (4 SIMDs per CU), then prefer the larger S: each A row
   // streamed from L2 serves S sequences
+  if (const char* e = getenv("CV_T64_S")) {  // tuning knob (bit-identical for every value)
+    const int s = atoi(e);
+    if (s == 2 || s == 4 || s == 8) return s;
+  }
   const int64_t simd_waves = 2 * 4 * (int64_t)(cus > 0 ? cus : 256);
   if (nseq >= 8 * simd_waves) return 8;
   if (nseq >= 4 * simd_waves) return 4;
