@@ -534,7 +534,8 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
   // t64 runs serial: its 212-VGPR forward waves fill each SIMD exactly twice per launch, and a
   // co-running backtrack cost more than it hid (config 4: 205.6 ms overlapped vs 191.9 ms
   // serial, profiles/r01_t64_sweep.txt)
-  const bool serial = (o.flags & CV_FLAG_SERIAL) != 0 || wave || use_t64;
+  static const bool t64_overlap = getenv("CV_T64_OVERLAP") != nullptr;  // A/B knob (bit-identical)
+  const bool serial = (o.flags & CV_FLAG_SERIAL) != 0 || wave || (use_t64 && !t64_overlap);
   // Sequences per forward workgroup: 2 (trellis_fwd2_f32, equal-length pairs; default) or 1
   // (trellis_fwd_f32: leftovers, MFMA, N not a multiple of 64).
   const bool plain = use_trellis && !use_mfma && !wave && cvk::trellis_pair_supported(h->np);

@@ -57,6 +57,7 @@ template <int C, int S, int PF>  // PF: A rows in flight
 __global__ __launch_bounds__(64) void trellis_fwd_f64(T64FwdArgs g) {
   constexpr int NP = 64 * C;
   static_assert(S % 2 == 0, "S sequences are read from LDS two at a time");
+  static_assert(PF % 2 == 0, "the delta register double buffer alternates with the row parity");
   __shared__ __attribute__((aligned(16))) double dl[NP * S];  // delta_{t-1}: [row][S]
   const int lane = threadIdx.x;
   const int j0 = lane * C;
@@ -141,27 +142,35 @@ __global__ __launch_bounds__(64) void trellis_fwd_f64(T64FwdArgs g) {
     for (int c = 0; c < C; ++c)
 #pragma unroll
       for (int s = 0; s < S; ++s) acc[c][s] = ninf;
+    // delta rows double-buffered in registers (dv[u & 1] = row i): row i+1's broadcast reads
+    // are in flight while row i computes
+    double2 dv[2][S / 2];
+#pragma unroll
+    for (int s2 = 0; s2 < S / 2; ++s2) dv[0][s2] = reinterpret_cast<const double2*>(dl)[s2];
 #pragma nounroll
     for (int i0 = 0; i0 < NP; i0 += PF) {
 #pragma unroll
       for (int u = 0; u < PF; ++u) {
         const int i = i0 + u;
-        double a[C];
+        {
+          const double2* nrow = reinterpret_cast<const double2*>(dl + min(i + 1, NP - 1) * S);
 #pragma unroll
-        for (int c = 0; c < C; ++c) a[c] = ar[u][c];
-        // refill this ring slot with row i + PF (clamped: the last rows reload row NP-1)
-        const int nr = min(i + PF, NP - 1);
-        load_a(arow + (size_t)nr * NP, ar[u]);
-        const double2* drow = reinterpret_cast<const double2*>(dl + i * S);
+          for (int s2 = 0; s2 < S / 2; ++s2) dv[(u + 1) & 1][s2] = nrow[s2];
+        }
 #pragma unroll
         for (int s2 = 0; s2 < S / 2; ++s2) {
-          const double2 d = drow[s2];
+          const double2 d = dv[u & 1][s2];
 #pragma unroll
           for (int c = 0; c < C; ++c) {
-            acc[c][2 * s2] = fmax(acc[c][2 * s2], d.x + a[c]);
-            acc[c][2 * s2 + 1] = fmax(acc[c][2 * s2 + 1], d.y + a[c]);
+            acc[c][2 * s2] = fmax(acc[c][2 * s2], d.x + ar[u][c]);
+            acc[c][2 * s2 + 1] = fmax(acc[c][2 * s2 + 1], d.y + ar[u][c]);
           }
         }
+        // refill this ring slot with row i + PF (clamped: the last rows reload row NP-1) only
+        // after its last use, into the same registers: no copies, and the in-flight loads
+        // cross the loop back-edge without a vmcnt(0) drain
+        const int nr = min(i + PF, NP - 1);
+        load_a(arow + (size_t)nr * NP, ar[u]);
       }
     }
     __syncthreads();  // every lane has read delta_{t-1} before it is overwritten
