@@ -303,9 +303,10 @@ hipError_t fwd_cs(const T64FwdArgs& fa, int64_t nseq, hipStream_t stream) {
   const int64_t blocks = (nseq + S - 1) / S;
   static const int pf = [] {  // tuning knob (bit-identical): A rows in flight, 8 (default) or 4
     const char* e = getenv("CV_T64_PF");
-    return e && atoi(e) == 4 ? 4 : 8;
+    return e ? atoi(e) : 8;
   }();
-  // PF = 8 measured 183 vs 208 ms (PF = 4) per config-4 forward (profiles/r01_t64_sweep.txt)
+  // PF = 8 measured 183 vs 208 ms (PF = 4) per config-4 forward; S = 6 / PF = 6 lost too
+  // (176 / 170 vs 164 ms, profiles/r01_t64_sweep.txt)
   if (pf == 4)
     hipLaunchKernelGGL((trellis_fwd_f64<C, S, 4>), dim3((unsigned)blocks), dim3(64), 0, stream, fa);
   else
