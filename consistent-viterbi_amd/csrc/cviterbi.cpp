@@ -469,10 +469,14 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
   }
   // exact f64, row-A0 association, N <= 256, no forced states: trellis_fwd_f64 (one wave per
   // S sequences) unless the generic kernel is asked for
-  const bool t64_ok = o.dtype == CV_DTYPE_F64 && o.assoc == CV_ASSOC_VITERBI && !o.forced && !resume_rows &&
-                      cvk::t64_padded_states(h->N) != 0;
+  // VITERBI (row A0) and DECODE (row 0 = 0.0) share trellis_fwd_f64 + backtrack_f64; CP runs
+  // trellis_cp_f64 (argmax in the forward pass) + generic_backtrack<double>
+  const bool t64_ok = o.dtype == CV_DTYPE_F64 &&
+                      (o.assoc == CV_ASSOC_VITERBI || o.assoc == CV_ASSOC_DECODE || o.assoc == CV_ASSOC_CP) &&
+                      !o.forced && !resume_rows && cvk::t64_padded_states(h->N) != 0;
   if (o.kernel == CV_KERNEL_TRELLIS_F64 && !t64_ok)
-    return set_err(CV_EUNSUPPORTED, "f64 trellis kernel needs dtype f64, assoc VITERBI, N <= 256, no forced states");
+    return set_err(CV_EUNSUPPORTED,
+                   "f64 trellis kernel needs dtype f64, assoc VITERBI/DECODE/CP, N <= 256, no forced states");
   const bool use_t64 = !use_trellis && t64_ok &&
                        (o.kernel == CV_KERNEL_TRELLIS_F64 || (o.kernel == CV_KERNEL_AUTO && !(o.flags & CV_FLAG_NO_T64)));
   if (!use_trellis && !use_t64 && h->N > cvk::generic_max_states(o.dtype == CV_DTYPE_F64 ? 8 : 4))
@@ -493,6 +497,7 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
   if (need_f64 && (st = ensure_f64_tables(h)) != CV_OK) return st;
   if (!use_trellis && o.dtype == CV_DTYPE_F32 && (st = ensure_g32_tables(h)) != CV_OK) return st;
   if (use_t64 && (st = ensure_t64_tables(h)) != CV_OK) return st;
+  const bool t64cp = use_t64 && o.assoc == CV_ASSOC_CP;
 
   // trellis variant: all-VALU unless the (slower, experimental) MFMA-assisted one is asked for
   const bool want_mfma = (o.flags & CV_FLAG_MFMA_TRELLIS) || ((o.flags >> 8) & 0xFF);
@@ -523,7 +528,7 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
   // 8 sequences per wave, so its default cap is larger (HBM3E: 288 GB per GPU)
   const uint64_t cap = o.workspace_bytes ? o.workspace_bytes : use_t64 ? kDefaultWorkspaceT64 : kDefaultWorkspace;
   const uint64_t per_elem = use_trellis ? (uint64_t)(wave ? h->npw : h->np) * 4
-                           : use_t64   ? (uint64_t)h->np64 * 8
+                           : (use_t64 && !t64cp) ? (uint64_t)h->np64 * 8
                                        : (uint64_t)h->N * 2;
   const int real_bytes = o.dtype == CV_DTYPE_F64 ? 8 : 4;
   const uint64_t total_elems = (uint64_t)(offsets_host[nseq] - offsets_host[0]);
@@ -694,9 +699,17 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
       fa.delta_elem_base = offsets_host[c.first];
       fa.status = status_dev;
       fa.nobs = (int)h->V;
+      fa.zero_init = o.assoc == CV_ASSOC_DECODE ? 1 : 0;
       const int spw = cvk::t64_seqs_per_wave(n, h->cus);
-      h->last_mt = spw;
-      err = cvk::launch_t64_fwd(h->np64, spw, fa, n, stream);
+      h->last_mt = t64cp ? std::min(spw, 4) : spw;
+      if (t64cp) {
+        fa.nstates = h->N;
+        fa.psi = reinterpret_cast<uint16_t*>(wsb);
+        fa.last_row = reinterpret_cast<double*>(lrb);
+        err = cvk::launch_t64_cp_fwd(h->np64, spw, fa, n, stream);
+      } else {
+        err = cvk::launch_t64_fwd(h->np64, spw, fa, n, stream);
+      }
     } else if (o.dtype == CV_DTYPE_F64) {
       cvk::GenericFwdArgs<double> fa{};
       fa.a = h->d_a64.as<double>();
@@ -763,7 +776,7 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
         ra.score = score_dev;
         err = cvk::launch_rescore_f64(ra, n, bts, reserve);
       }
-    } else if (use_t64) {
+    } else if (use_t64 && !t64cp) {
       cvk::T64BtArgs ba{};
       ba.delta = reinterpret_cast<const double*>(wsb);
       ba.delta_elem_base = offsets_host[c.first];

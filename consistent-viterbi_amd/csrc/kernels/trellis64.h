@@ -19,6 +19,12 @@ struct T64FwdArgs {
   int64_t delta_elem_base; // element offset that maps to delta row 0
   uint8_t* status;         // [nseq_total] (pre-zeroed); forward sets BADOBS
   int nobs;                // V
+  int zero_init;           // 1: row 0 = 0.0 (viterbi::decode, viterbi.rs:6,9), else pi + b
+  // CP association (trellis_cp_f64 only): psi / last-row outputs in the generic kernel's
+  // layout so generic_backtrack<double> finishes the decode
+  int nstates;             // real N (psi row stride)
+  uint16_t* psi;           // [(elements of chunk)][N]
+  double* last_row;        // [(slots of launch)][N]
 };
 
 struct T64BtArgs {
@@ -39,6 +45,8 @@ int t64_padded_states(int n);
 // sequences per forward wave (2, 4 or 8) for a launch of nseq sequences on `cus` CUs
 int t64_seqs_per_wave(int64_t nseq, int cus);
 hipError_t launch_t64_fwd(int np, int s, const T64FwdArgs& fa, int64_t nseq, hipStream_t stream);
+// CP association (cp.rs:70-79): psi and the CP value d[psi] + (a[psi,j] + b[j,o]) in the forward
+hipError_t launch_t64_cp_fwd(int np, int s, const T64FwdArgs& fa, int64_t nseq, hipStream_t stream);
 hipError_t launch_t64_bt(int np, const T64BtArgs& ba, int64_t nseq, hipStream_t stream);
 
 }  // namespace cvk

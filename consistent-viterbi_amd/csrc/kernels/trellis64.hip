@@ -111,7 +111,7 @@ __global__ __launch_bounds__(64) void trellis_fwd_f64(T64FwdArgs g) {
     emis(s, 0, e);
 #pragma unroll
     for (int c = 0; c < C; ++c) {
-      v[c] = g.pi[j0 + c] + e[c];
+      v[c] = g.zero_init ? 0.0 : g.pi[j0 + c] + e[c];
       dl[(j0 + c) * S + s] = v[c];
     }
     store_row(s, 0, v);
@@ -195,6 +195,158 @@ __global__ __launch_bounds__(64) void trellis_fwd_f64(T64FwdArgs g) {
       for (int c = 0; c < C; ++c) v[c] = acc[c][s];
       store_row(s, Tmax - 1, v);
     }
+  }
+  if (lane == 0) {
+#pragma unroll
+    for (int s = 0; s < S; ++s)
+      if (bad & (1u << s)) g.status[seq[s]] = CVK_SEQ_BADOBS;
+  }
+}
+
+// CP association (CPSolver, cp.rs:70-79 via utils.rs:24-38, hmm.rs:220-222):
+//   psi = first argmax_i (d[i] + a[i,j]);  d'[j] = d[psi] + (a[psi,j] + b[j,o])
+// The value depends on psi, so the forward pass tracks the first argmax: per pair one add,
+// one compare, one max and one index select (4 VALU vs 2 for row A0), then per column one
+// LDS gather of d[psi] and one L2 gather of a[psi,j].  psi (u16) and the last row go out in
+// generic_fwd's layout; generic_backtrack<double> follows them (cp.rs:85-93).  Same wave
+// layout as trellis_fwd_f64 (S sequences per wave, A rows streamed through a register ring).
+template <int C, int S, int PF>
+__global__ __launch_bounds__(64) void trellis_cp_f64(T64FwdArgs g) {
+  constexpr int NP = 64 * C;
+  static_assert(S % 2 == 0 && PF % 2 == 0, "pairs of sequences / rows");
+  __shared__ __attribute__((aligned(16))) double dl[NP * S];  // delta_{t-1}: [row][S]
+  const int lane = threadIdx.x;
+  const int j0 = lane * C;
+  const int N = g.nstates;
+  const int64_t slot0 = g.seq_begin + (int64_t)blockIdx.x * S;
+  const int64_t slot_end = g.seq_begin + g.nslots;
+  const double ninf = ninf_d();
+
+  int64_t seq[S], e0[S];
+  int T[S];
+  int Tmax = 0;
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    const int64_t slot = slot0 + s;
+    if (slot < slot_end) {
+      seq[s] = g.order ? (int64_t)g.order[slot] : slot;
+      e0[s] = g.offsets[seq[s]];
+      T[s] = (int)(g.offsets[seq[s] + 1] - e0[s]);
+    } else {
+      seq[s] = -1;
+      e0[s] = 0;
+      T[s] = 0;
+    }
+    Tmax = T[s] > Tmax ? T[s] : Tmax;
+  }
+  if (Tmax <= 0) return;
+  const unsigned V = (unsigned)g.nobs;
+  unsigned bad = 0;
+  auto emis = [&](int s, int t, double (&e)[C]) {
+    int o = 0;
+    if (t < T[s]) o = g.obs[e0[s] + t];
+    const bool ok = (unsigned)o < V;
+    if (t < T[s] && !ok) bad |= 1u << s;
+    const double* row = g.et + (size_t)(ok ? o : 0) * NP + j0;
+#pragma unroll
+    for (int c = 0; c < C; ++c) e[c] = ok ? row[c] : ninf;
+  };
+  // row t of sequence s: psi (t >= 1) and, at t = T-1, the last row
+  auto emit = [&](int s, int t, const double (&v)[C], const int (&p)[C]) {
+    if (t >= T[s]) return;
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      if (j0 + c < N) {
+        if (t > 0) g.psi[(e0[s] + t - g.delta_elem_base) * (int64_t)N + j0 + c] = (uint16_t)p[c];
+        if (t == T[s] - 1) g.last_row[(slot0 + s - g.seq_begin) * (int64_t)N + j0 + c] = v[c];
+      }
+    }
+  };
+
+#pragma unroll
+  for (int s = 0; s < S; ++s) {  // t = 0: pi + b (cp.rs:66-68)
+    double e[C], v[C];
+    int p[C] = {};
+    emis(s, 0, e);
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      v[c] = g.pi[j0 + c] + e[c];
+      dl[(j0 + c) * S + s] = v[c];
+    }
+    emit(s, 0, v, p);
+  }
+  __syncthreads();
+
+  __builtin_amdgcn_s_setprio(3);
+  const double* __restrict__ arow = g.a + j0;
+  for (int t = 1; t < Tmax; ++t) {
+    double acc[C][S];
+    int idx[C][S];
+#pragma unroll
+    for (int c = 0; c < C; ++c)
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        acc[c][s] = ninf;
+        idx[c][s] = 0;
+      }
+    double ar[PF][C];
+#pragma unroll
+    for (int u = 0; u < PF; ++u) load_a(arow + (size_t)u * NP, ar[u]);
+    double2 dv[2][S / 2];
+#pragma unroll
+    for (int s2 = 0; s2 < S / 2; ++s2) dv[0][s2] = reinterpret_cast<const double2*>(dl)[s2];
+#pragma nounroll
+    for (int i0 = 0; i0 < NP; i0 += PF) {
+#pragma unroll
+      for (int u = 0; u < PF; ++u) {
+        const int i = i0 + u;
+        {
+          const double2* nrow = reinterpret_cast<const double2*>(dl + min(i + 1, NP - 1) * S);
+#pragma unroll
+          for (int s2 = 0; s2 < S / 2; ++s2) dv[(u + 1) & 1][s2] = nrow[s2];
+        }
+#pragma unroll
+        for (int s2 = 0; s2 < S / 2; ++s2) {
+          const double2 d = dv[u & 1][s2];
+#pragma unroll
+          for (int c = 0; c < C; ++c) {
+            // strict '>' from acc = -inf, idx = 0: the first maximal index, and 0 when every
+            // candidate is -inf (generic_fwd's "!any || s > best")
+            const double x0 = d.x + ar[u][c], x1 = d.y + ar[u][c];
+            idx[c][2 * s2] = x0 > acc[c][2 * s2] ? i : idx[c][2 * s2];
+            acc[c][2 * s2] = fmax(acc[c][2 * s2], x0);
+            idx[c][2 * s2 + 1] = x1 > acc[c][2 * s2 + 1] ? i : idx[c][2 * s2 + 1];
+            acc[c][2 * s2 + 1] = fmax(acc[c][2 * s2 + 1], x1);
+          }
+        }
+        const int nr = min(i + PF, NP - 1);
+        load_a(arow + (size_t)nr * NP, ar[u]);
+      }
+    }
+    // CP value d[psi] + (a[psi,j] + b[j,o]): gathers of d (this wave's LDS) and a (L2)
+    double v[S][C];
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      double e[C];
+      emis(s, t, e);
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        const int p = idx[c][s];
+        v[s][c] = dl[p * S + s] + (g.a[(size_t)p * NP + j0 + c] + e[c]);
+      }
+    }
+    __syncthreads();  // every lane has read delta_{t-1} before it is overwritten
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      int p[C];
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        dl[(j0 + c) * S + s] = v[s][c];
+        p[c] = idx[c][s];
+      }
+      emit(s, t, v[s], p);
+    }
+    __syncthreads();
   }
   if (lane == 0) {
 #pragma unroll
@@ -325,6 +477,29 @@ hipError_t fwd_c(const T64FwdArgs& fa, int s, int64_t nseq, hipStream_t stream) 
 }
 
 }  // namespace
+
+template <int C>
+hipError_t cp_c(const T64FwdArgs& fa, int s, int64_t nseq, hipStream_t stream) {
+  const dim3 block(64);
+  switch (s) {
+    case 2: hipLaunchKernelGGL((trellis_cp_f64<C, 2, 4>), dim3((unsigned)((nseq + 1) / 2)), block, 0, stream, fa); break;
+    case 4: hipLaunchKernelGGL((trellis_cp_f64<C, 4, 4>), dim3((unsigned)((nseq + 3) / 4)), block, 0, stream, fa); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_t64_cp_fwd(int np, int s, const T64FwdArgs& fa, int64_t nseq, hipStream_t stream) {
+  if (nseq <= 0) return hipSuccess;
+  s = s > 4 ? 4 : s;  // the argmax state (idx) costs registers: at most 4 sequences per wave
+  switch (np) {
+    case 64: return cp_c<1>(fa, s, nseq, stream);
+    case 128: return cp_c<2>(fa, s, nseq, stream);
+    case 192: return cp_c<3>(fa, s, nseq, stream);
+    case 256: return cp_c<4>(fa, s, nseq, stream);
+    default: return hipErrorInvalidValue;
+  }
+}
 
 int t64_padded_states(int n) { return (n >= 1 && n <= 256) ? 64 * ((n + 63) / 64) : 0; }
 

@@ -33,22 +33,30 @@ def _assert_same(got, ref, what):
     assert np.array_equal(gp, rp), f"{what}: paths differ at {np.nonzero(gp != rp)[0][:8]}"
 
 
+ASSOC = {"viterbi": O.VITERBI, "cp": O.CP, "decode": O.DECODE}
+
+
 @pytest.mark.parametrize("n", [1, 2, 5, 33, 45, 63, 64, 65, 100, 128, 129, 192, 200, 255, 256])
-def test_t64_bit_exact_vs_oracle(gpu, n):
+@pytest.mark.parametrize("assoc", ["viterbi", "cp", "decode"])
+def test_t64_bit_exact_vs_oracle(gpu, n, assoc):
+    """Row A0 (viterbi.rs:13-18), CPSolver's association (cp.rs:70-79: argmax tracked in the
+    forward pass, value d[psi] + (a + b)) and viterbi::decode (row 0 = 0.0)."""
     pi, a, b, off, obs = _case(n, 41, seed=700 + n, zero_frac=0.05 if n % 2 else 0.0)
     h = cv.HMM(pi, a, b)
-    got = cv.decode_batch(h, off, obs, dtype="f64", rescore_f64=False)
+    got = cv.decode_batch(h, off, obs, dtype="f64", assoc=assoc, rescore_f64=False)
     t = cv.last_timing(h)
     assert t["kernel"] == "trellis_f64", t
     assert t["padded_states"] == 64 * ((n + 63) // 64)
-    ref = O.decode_batch(pi, a, b, off, obs, O.VITERBI, np.float64)
-    _assert_same(got, ref, f"t64 N={n}")
-    # rescore_f64 changes nothing on the f64 path: the f64 delta already is the reference score
-    _assert_same(cv.decode_batch(h, off, obs, dtype="f64", rescore_f64=True), ref, f"t64 rescore N={n}")
+    ref = O.decode_batch(pi, a, b, off, obs, ASSOC[assoc], np.float64)
+    _assert_same(got, ref, f"t64 {assoc} N={n}")
+    if assoc == "viterbi":
+        # rescore_f64 changes nothing on the f64 path: the f64 delta already is the reference score
+        _assert_same(cv.decode_batch(h, off, obs, dtype="f64", rescore_f64=True), ref, f"t64 rescore N={n}")
 
 
 @pytest.mark.parametrize("n", [7, 64, 256])
-def test_t64_ties_and_infeasible(gpu, n):
+@pytest.mark.parametrize("assoc", ["viterbi", "cp", "decode"])
+def test_t64_ties_and_infeasible(gpu, n, assoc):
     """Quantised log-probs (many exact ties: first index must win), -inf transitions and
     emissions (infeasible sequences), an out-of-range observation, empty and T=1 sequences."""
     rng = np.random.default_rng(n)
@@ -65,8 +73,9 @@ def test_t64_ties_and_infeasible(gpu, n):
     obs[off[3] + 5] = 3   # sequence 3 infeasible
     obs[off[9] + 59] = 3  # sequence 9 infeasible at its last element
     h = cv.HMM(pi, a, b)
-    ref = O.decode_batch(pi, a, b, off, obs, O.VITERBI, np.float64)
-    _assert_same(cv.decode_batch(h, off, obs, dtype="f64", rescore_f64=False), ref, f"ties N={n}")
+    ref = O.decode_batch(pi, a, b, off, obs, ASSOC[assoc], np.float64)
+    _assert_same(cv.decode_batch(h, off, obs, dtype="f64", assoc=assoc, rescore_f64=False), ref,
+                 f"ties {assoc} N={n}")
     assert cv.last_timing(h)["kernel"] == "trellis_f64"
     # out-of-range observation index: rejected (CV_EINVAL) before any kernel runs
     obs_bad = obs.copy()
@@ -78,7 +87,8 @@ def test_t64_ties_and_infeasible(gpu, n):
 
 @pytest.mark.parametrize("n", [45, 256])
 @pytest.mark.parametrize("serial", [False, True])
-def test_t64_matches_generic_f64_large(gpu, n, serial):
+@pytest.mark.parametrize("assoc", ["viterbi", "cp"])
+def test_t64_matches_generic_f64_large(gpu, n, serial, assoc):
     """Batches large enough for 8 sequences per wave and several chunks (workspace cap),
     ragged lengths (longest-first schedule): identical to the generic f64 kernel, whose
     inline first-argmax is itself bit-exact against the oracle (test_gpu_parity.py)."""
@@ -89,17 +99,19 @@ def test_t64_matches_generic_f64_large(gpu, n, serial):
     off = synth.offsets_from_lengths(lengths)
     obs = rng.integers(0, 200, size=int(off[-1])).astype(np.int32)
     h = cv.HMM(pi, a, b)
-    ws = int(off[-1]) * 64 * ((n + 63) // 64) * 8 // 3  # >= 3 chunks
-    got = cv.decode_batch(h, off, obs, dtype="f64", rescore_f64=False, workspace_bytes=ws, serial=serial)
+    per_elem = 2 * n if assoc == "cp" else 8 * 64 * ((n + 63) // 64)  # u16 psi row / f64 delta row
+    ws = int(off[-1]) * per_elem // 3  # >= 3 chunks
+    got = cv.decode_batch(h, off, obs, dtype="f64", assoc=assoc, rescore_f64=False, workspace_bytes=ws,
+                          serial=serial)
     t = cv.last_timing(h)
     assert t["kernel"] == "trellis_f64" and t["launches"] >= 3, t
-    gen = cv.decode_batch(h, off, obs, dtype="f64", kernel="generic", rescore_f64=False)
-    _assert_same(got, gen, f"t64 vs generic N={n}")
+    gen = cv.decode_batch(h, off, obs, dtype="f64", assoc=assoc, kernel="generic", rescore_f64=False)
+    _assert_same(got, gen, f"t64 vs generic {assoc} N={n}")
     # spot-check against the oracle
     idx = rng.choice(nseq, 24, replace=False)
     for k in idx:
         lo, hi = off[k], off[k + 1]
-        rp, rs, rst = O.decode_batch(pi, a, b, np.array([0, hi - lo]), obs[lo:hi], O.VITERBI, np.float64)
+        rp, rs, rst = O.decode_batch(pi, a, b, np.array([0, hi - lo]), obs[lo:hi], ASSOC[assoc], np.float64)
         assert rst[0] == got[2][k] and rs[0] == got[1][k] and np.array_equal(rp, got[0][lo:hi])
 
 
