@@ -469,14 +469,16 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
   }
   // exact f64, row-A0 association, N <= 256, no forced states: trellis_fwd_f64 (one wave per
   // S sequences) unless the generic kernel is asked for
-  // VITERBI (row A0) and DECODE (row 0 = 0.0) share trellis_fwd_f64 + backtrack_f64; CP runs
+  // VITERBI (row A0), DECODE (row 0 = 0.0) and DP ((a + b) + d) share trellis_fwd_f64 +
+  // backtrack_f64; CP runs
   // trellis_cp_f64 (argmax in the forward pass) + generic_backtrack<double>
   const bool t64_ok = o.dtype == CV_DTYPE_F64 &&
-                      (o.assoc == CV_ASSOC_VITERBI || o.assoc == CV_ASSOC_DECODE || o.assoc == CV_ASSOC_CP) &&
+                      (o.assoc == CV_ASSOC_VITERBI || o.assoc == CV_ASSOC_DECODE || o.assoc == CV_ASSOC_CP ||
+                       o.assoc == CV_ASSOC_DP) &&
                       !o.forced && !resume_rows && cvk::t64_padded_states(h->N) != 0;
   if (o.kernel == CV_KERNEL_TRELLIS_F64 && !t64_ok)
     return set_err(CV_EUNSUPPORTED,
-                   "f64 trellis kernel needs dtype f64, assoc VITERBI/DECODE/CP, N <= 256, no forced states");
+                   "f64 trellis kernel needs dtype f64, N <= 256, no forced states");
   const bool use_t64 = !use_trellis && t64_ok &&
                        (o.kernel == CV_KERNEL_TRELLIS_F64 || (o.kernel == CV_KERNEL_AUTO && !(o.flags & CV_FLAG_NO_T64)));
   if (!use_trellis && !use_t64 && h->N > cvk::generic_max_states(o.dtype == CV_DTYPE_F64 ? 8 : 4))
@@ -700,8 +702,9 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
       fa.status = status_dev;
       fa.nobs = (int)h->V;
       fa.zero_init = o.assoc == CV_ASSOC_DECODE ? 1 : 0;
+      fa.dp_assoc = o.assoc == CV_ASSOC_DP ? 1 : 0;
       const int spw = cvk::t64_seqs_per_wave(n, h->cus);
-      h->last_mt = t64cp ? std::min(spw, 4) : spw;
+      h->last_mt = (t64cp || fa.dp_assoc) ? std::min(spw, 4) : spw;
       if (t64cp) {
         fa.nstates = h->N;
         fa.psi = reinterpret_cast<uint16_t*>(wsb);
@@ -789,6 +792,9 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
       ba.path = path_dev;
       ba.score = score_dev;  // the f64 delta is already the reference score: no re-score
       ba.status = status_dev;
+      ba.dp_assoc = o.assoc == CV_ASSOC_DP ? 1 : 0;
+      ba.obs = obs_dev;
+      ba.et = h->q_et.as<double>();
       err = cvk::launch_t64_bt(h->np64, ba, n, bts);
     } else if (o.dtype == CV_DTYPE_F64) {
       cvk::GenericBtArgs<double> ba{};

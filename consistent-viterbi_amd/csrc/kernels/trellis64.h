@@ -20,6 +20,7 @@ struct T64FwdArgs {
   uint8_t* status;         // [nseq_total] (pre-zeroed); forward sets BADOBS
   int nobs;                // V
   int zero_init;           // 1: row 0 = 0.0 (viterbi::decode, viterbi.rs:6,9), else pi + b
+  int dp_assoc;            // 1: DPSolver's (a + b) + d association (dp.rs:147-177)
   // CP association (trellis_cp_f64 only): psi / last-row outputs in the generic kernel's
   // layout so generic_backtrack<double> finishes the decode
   int nstates;             // real N (psi row stride)
@@ -38,6 +39,9 @@ struct T64BtArgs {
   int32_t* path;           // [sum T]
   double* score;           // [nseq_total]
   uint8_t* status;
+  int dp_assoc;            // 1: candidates (a[i,j] + b[j,o_t]) + d[i] (dp.rs:149)
+  const int32_t* obs;      // dp_assoc: observations, emissions [V][NP]
+  const double* et;
 };
 
 // NP = 64 * ceil(N / 64) for 1 <= N <= 256, else 0 (no f64 trellis kernel)

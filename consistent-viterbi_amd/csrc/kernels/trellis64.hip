@@ -53,7 +53,9 @@ __device__ __forceinline__ void load_a(const double* p, double (&a)[C]) {
   }
 }
 
-template <int C, int S, int PF>  // PF: A rows in flight
+// DPA: DPSolver's association (dp.rs:147-177): d'[j] = max_i ((a[i,j] + b[j,o]) + d[i]); the
+// emission enters every candidate, so it is loaded before the row loop (S <= 4: registers)
+template <int C, int S, int PF, bool DPA = false>  // PF: A rows in flight
 __global__ __launch_bounds__(64) void trellis_fwd_f64(T64FwdArgs g) {
   constexpr int NP = 64 * C;
   static_assert(S % 2 == 0, "S sequences are read from LDS two at a time");
@@ -142,6 +144,11 @@ __global__ __launch_bounds__(64) void trellis_fwd_f64(T64FwdArgs g) {
     for (int c = 0; c < C; ++c)
 #pragma unroll
       for (int s = 0; s < S; ++s) acc[c][s] = ninf;
+    double ecur[DPA ? S : 1][C];
+    if constexpr (DPA) {
+#pragma unroll
+      for (int s = 0; s < S; ++s) emis(s, t, ecur[s]);
+    }
     // delta rows double-buffered in registers (dv[u & 1] = row i): row i+1's broadcast reads
     // are in flight while row i computes
     double2 dv[2][S / 2];
@@ -162,8 +169,13 @@ __global__ __launch_bounds__(64) void trellis_fwd_f64(T64FwdArgs g) {
           const double2 d = dv[u & 1][s2];
 #pragma unroll
           for (int c = 0; c < C; ++c) {
-            acc[c][2 * s2] = fmax(acc[c][2 * s2], d.x + ar[u][c]);
-            acc[c][2 * s2 + 1] = fmax(acc[c][2 * s2 + 1], d.y + ar[u][c]);
+            if constexpr (DPA) {
+              acc[c][2 * s2] = fmax(acc[c][2 * s2], (ar[u][c] + ecur[2 * s2][c]) + d.x);
+              acc[c][2 * s2 + 1] = fmax(acc[c][2 * s2 + 1], (ar[u][c] + ecur[2 * s2 + 1][c]) + d.y);
+            } else {
+              acc[c][2 * s2] = fmax(acc[c][2 * s2], d.x + ar[u][c]);
+              acc[c][2 * s2 + 1] = fmax(acc[c][2 * s2 + 1], d.y + ar[u][c]);
+            }
           }
         }
         // refill this ring slot with row i + PF (clamped: the last rows reload row NP-1) only
@@ -177,10 +189,10 @@ __global__ __launch_bounds__(64) void trellis_fwd_f64(T64FwdArgs g) {
 #pragma unroll
     for (int s = 0; s < S; ++s) {
       double e[C], v[C];
-      emis(s, t, e);
+      if constexpr (!DPA) emis(s, t, e);
 #pragma unroll
       for (int c = 0; c < C; ++c) {
-        v[c] = acc[c][s] + e[c];
+        v[c] = DPA ? acc[c][s] : acc[c][s] + e[c];
         acc[c][s] = v[c];
         dl[(j0 + c) * S + s] = v[c];
       }
@@ -432,8 +444,14 @@ __global__ __launch_bounds__(256) void backtrack_f64(T64BtArgs g) {
       if (t >= 1) {
         const double* acol = g.at + (size_t)cur * NP + lane;
         double s[KP];
+        if (g.dp_assoc) {  // (a[i,cur] + b[cur,o_t]) + d_{t-1}[i]  (dp.rs:149 arc_p, then + cost)
+          const double e = g.et[(size_t)g.obs[e0 + t] * NP + cur];
 #pragma unroll
-        for (int k = 0; k < KP; ++k) s[k] = valid[k] ? ring[u][k] + acol[64 * k] : ninf_d();
+          for (int k = 0; k < KP; ++k) s[k] = valid[k] ? (acol[64 * k] + e) + ring[u][k] : ninf_d();
+        } else {
+#pragma unroll
+          for (int k = 0; k < KP; ++k) s[k] = valid[k] ? ring[u][k] + acol[64 * k] : ninf_d();
+        }
         double M;
         cur = first_argmax(s, M);
         const int tp = t - 1;
@@ -459,7 +477,12 @@ hipError_t fwd_cs(const T64FwdArgs& fa, int64_t nseq, hipStream_t stream) {
   }();
   // PF = 8 measured 183 vs 208 ms (PF = 4) per config-4 forward; S = 6 / PF = 6 lost too
   // (176 / 170 vs 164 ms, profiles/r01_t64_sweep.txt)
-  if (pf == 4)
+  if (fa.dp_assoc) {
+    if constexpr (S <= 4)
+      hipLaunchKernelGGL((trellis_fwd_f64<C, S, 8, true>), dim3((unsigned)blocks), dim3(64), 0, stream, fa);
+    else
+      return hipErrorInvalidValue;
+  } else if (pf == 4)
     hipLaunchKernelGGL((trellis_fwd_f64<C, S, 4>), dim3((unsigned)blocks), dim3(64), 0, stream, fa);
   else
     hipLaunchKernelGGL((trellis_fwd_f64<C, S, 8>), dim3((unsigned)blocks), dim3(64), 0, stream, fa);
@@ -518,6 +541,7 @@ int t64_seqs_per_wave(int64_t nseq, int cus) {
 
 hipError_t launch_t64_fwd(int np, int s, const T64FwdArgs& fa, int64_t nseq, hipStream_t stream) {
   if (nseq <= 0) return hipSuccess;
+  if (fa.dp_assoc && s > 4) s = 4;  // the emissions of every sequence stay in registers
   switch (np) {
     case 64: return fwd_c<1>(fa, s, nseq, stream);
     case 128: return fwd_c<2>(fa, s, nseq, stream);

@@ -33,11 +33,11 @@ def _assert_same(got, ref, what):
     assert np.array_equal(gp, rp), f"{what}: paths differ at {np.nonzero(gp != rp)[0][:8]}"
 
 
-ASSOC = {"viterbi": O.VITERBI, "cp": O.CP, "decode": O.DECODE}
+ASSOC = {"viterbi": O.VITERBI, "cp": O.CP, "dp": O.DP, "decode": O.DECODE}
 
 
 @pytest.mark.parametrize("n", [1, 2, 5, 33, 45, 63, 64, 65, 100, 128, 129, 192, 200, 255, 256])
-@pytest.mark.parametrize("assoc", ["viterbi", "cp", "decode"])
+@pytest.mark.parametrize("assoc", ["viterbi", "cp", "dp", "decode"])
 def test_t64_bit_exact_vs_oracle(gpu, n, assoc):
     """Row A0 (viterbi.rs:13-18), CPSolver's association (cp.rs:70-79: argmax tracked in the
     forward pass, value d[psi] + (a + b)) and viterbi::decode (row 0 = 0.0)."""
@@ -55,7 +55,7 @@ def test_t64_bit_exact_vs_oracle(gpu, n, assoc):
 
 
 @pytest.mark.parametrize("n", [7, 64, 256])
-@pytest.mark.parametrize("assoc", ["viterbi", "cp", "decode"])
+@pytest.mark.parametrize("assoc", ["viterbi", "cp", "dp", "decode"])
 def test_t64_ties_and_infeasible(gpu, n, assoc):
     """Quantised log-probs (many exact ties: first index must win), -inf transitions and
     emissions (infeasible sequences), an out-of-range observation, empty and T=1 sequences."""
@@ -87,7 +87,7 @@ def test_t64_ties_and_infeasible(gpu, n, assoc):
 
 @pytest.mark.parametrize("n", [45, 256])
 @pytest.mark.parametrize("serial", [False, True])
-@pytest.mark.parametrize("assoc", ["viterbi", "cp"])
+@pytest.mark.parametrize("assoc", ["viterbi", "cp", "dp"])
 def test_t64_matches_generic_f64_large(gpu, n, serial, assoc):
     """Batches large enough for 8 sequences per wave and several chunks (workspace cap),
     ragged lengths (longest-first schedule): identical to the generic f64 kernel, whose
