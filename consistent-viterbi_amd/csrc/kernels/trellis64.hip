@@ -373,12 +373,13 @@ __device__ __forceinline__ double wave_max_d(double v) {
   return v;
 }
 
-template <int KP>
+// PF: delta rows in flight per wave.  The backtrack streams 2 KiB f64 rows from HBM, and at
+// NP >= 192 occupancy hides the latency better than a deeper ring: config 4 (NP = 256, serial
+// schedule) 14.3 ms at PF = 2 (8 waves/SIMD) vs 15.3 (PF = 4, 74 VGPRs, 6 waves/SIMD),
+// 16.9 (PF = 8) and 21.9 (PF = 16) -- profiles/r01_t64_bt_pf.txt.
+template <int KP, int PF>
 __global__ __launch_bounds__(256) void backtrack_f64(T64BtArgs g) {
   constexpr int NP = 64 * KP;
-  // delta rows in flight; <= 88 VGPRs at KP = 4 so a backtrack wave fits beside the two
-  // 212-VGPR forward waves of a SIMD (overlap mode) instead of displacing the next chunk's
-  constexpr int PF = KP >= 3 ? 4 : 8;
   const int lane = threadIdx.x & 63;
   const int64_t slot = g.seq_begin + (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (slot >= g.seq_end) return;
@@ -551,17 +552,32 @@ hipError_t launch_t64_fwd(int np, int s, const T64FwdArgs& fa, int64_t nseq, hip
   }
 }
 
-hipError_t launch_t64_bt(int np, const T64BtArgs& ba, int64_t nseq, hipStream_t stream) {
-  if (nseq <= 0) return hipSuccess;
-  const dim3 grid((unsigned)((nseq + 3) / 4)), block(256);
+template <int PF>
+hipError_t bt_pf(int np, const T64BtArgs& ba, dim3 grid, dim3 block, hipStream_t stream) {
   switch (np) {
-    case 64: hipLaunchKernelGGL(backtrack_f64<1>, grid, block, 0, stream, ba); break;
-    case 128: hipLaunchKernelGGL(backtrack_f64<2>, grid, block, 0, stream, ba); break;
-    case 192: hipLaunchKernelGGL(backtrack_f64<3>, grid, block, 0, stream, ba); break;
-    case 256: hipLaunchKernelGGL(backtrack_f64<4>, grid, block, 0, stream, ba); break;
+    case 64: hipLaunchKernelGGL((backtrack_f64<1, PF>), grid, block, 0, stream, ba); break;
+    case 128: hipLaunchKernelGGL((backtrack_f64<2, PF>), grid, block, 0, stream, ba); break;
+    case 192: hipLaunchKernelGGL((backtrack_f64<3, PF>), grid, block, 0, stream, ba); break;
+    case 256: hipLaunchKernelGGL((backtrack_f64<4, PF>), grid, block, 0, stream, ba); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
+}
+
+hipError_t launch_t64_bt(int np, const T64BtArgs& ba, int64_t nseq, hipStream_t stream) {
+  if (nseq <= 0) return hipSuccess;
+  const dim3 grid((unsigned)((nseq + 3) / 4)), block(256);
+  static const int pf_env = [] {  // tuning knob (bit-identical): 2, 4, 8 or 16 rows in flight
+    const char* e = getenv("CV_T64_BT_PF");
+    return e ? atoi(e) : 0;
+  }();
+  const int pf = pf_env ? pf_env : np >= 192 ? 2 : 8;
+  switch (pf) {
+    case 2: return bt_pf<2>(np, ba, grid, block, stream);
+    case 4: return bt_pf<4>(np, ba, grid, block, stream);
+    case 16: return bt_pf<16>(np, ba, grid, block, stream);
+    default: return bt_pf<8>(np, ba, grid, block, stream);
+  }
 }
 
 }  // namespace cvk
