@@ -547,13 +547,18 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
   // (trellis_fwd_f32: leftovers, MFMA, N not a multiple of 64).
   const bool plain = use_trellis && !use_mfma && !wave && cvk::trellis_pair_supported(h->np);
   const int group = (!plain || (o.flags & CV_FLAG_NO_PAIR)) ? 1 : 2;
+  static const uint64_t max_chunks = [] {  // A/B knob (bit-identical): pipeline depth
+    const char* e = getenv("CV_MAX_CHUNKS");
+    const long v = e ? atol(e) : 8;
+    return (uint64_t)(v >= 1 && v <= 64 ? v : 8);
+  }();
   const uint64_t half_cap = std::max<uint64_t>(serial ? cap : cap / 2, per_elem);
   uint64_t nchunks = std::max<uint64_t>(1, (total_elems * per_elem + half_cap - 1) / half_cap);
   // t64: chunks of >= 8 sequences x 2 waves x 4 SIMDs x CUs so every chunk runs S = 8
   if (!serial)
     nchunks = std::max<uint64_t>(
         nchunks, use_t64 ? std::min<uint64_t>(4, (uint64_t)(nseq / (64 * (int64_t)std::max(h->cus, 1))))
-                         : std::min<uint64_t>(8, (uint64_t)(nseq / 2048)));
+                         : std::min<uint64_t>(max_chunks, (uint64_t)(nseq / 2048)));
   const uint64_t target = std::max<uint64_t>(1, (total_elems + nchunks - 1) / nchunks);
   const uint64_t elem_cap = std::max<uint64_t>(half_cap / per_elem, 1);
   std::vector<std::pair<int64_t, int64_t>> chunks;
