@@ -2,18 +2,22 @@
 
 Workload (BASELINE.json configs[3]): synthetic HMM with N=256
 states, V=1,024 observations (bdims [32,32]), Dirichlet(1) rows in log10, iid uniform
-observations from splitmix64; T=512, B=65,536 sequences per batch, f32 row-A0 trellis.
-Sequences are independent, so the batch shards across ranks with no data-path collective:
-by default every rank decodes its own 65,536-sequence shard of a global batch of
-N x 65,536 (weak scaling); --scaling strong splits ONE 65,536-sequence batch
-B/N per GPU instead.  One step = decode of the rank's shard (forward trellis kernel +
-backtrack + f64 re-score of every path) and, for N>1, ONE RCCL gather (torch.distributed
-"nccl") of the paths (u8 states), scores and statuses to rank 0 over xGMI -- issued on a
-second stream so that step k's gather overlaps step k+1's decode (double-buffered outputs;
-the closing synchronize waits for the last one).  Inputs are resident in HBM before the
-timed region.
+observations from splitmix64; T=512, B=65,536 sequences per batch.  The headline `value` is
+the EXACT-f64 decode (--dtype f64, the default): the reference's own arithmetic (hmm.rs:10-18
+stores f64; viterbi.rs:13-18 / cp.rs:70-79), so every path and score is bit-identical to the
+f64 recurrence -- the north star's "decoded state paths identical to CPU".  The f32 trellis
+(BASELINE's "f32 log-prob", paths differ from f64 on ~1-3% of sequences) is timed in the same
+run and reported as the extra key `f32_trellis`.
+Sequences are independent, so the batch shards across ranks with no data-path collective.
+For N>1 the default is strong scaling (--scaling strong: ONE 65,536-sequence batch, B/N per
+GPU, BASELINE config 4 read literally); --scaling weak gives every rank its own 65,536
+sequences.  One step = decode of the rank's shard (forward trellis kernel + backtrack) and,
+for N>1, ONE RCCL gather (torch.distributed "nccl") of the paths (u8 states), scores and
+statuses to rank 0 over xGMI -- issued on a second stream so that step k's gather overlaps
+step k+1's decode (double-buffered outputs; the closing synchronize waits for the last
+one).  Inputs are resident in HBM before the timed region.
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--scaling weak|strong]
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--scaling strong|weak] [--dtype f64|f32]
        (N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N)
 Rank 0 prints ONE JSON line.
 """
@@ -45,10 +49,11 @@ def parse():
     p.add_argument("--warmup", type=int, default=2)
     p.add_argument("--batch", type=int, default=B_TOTAL,
                    help="sequences per rank (weak) or in total (strong); default 65,536")
-    p.add_argument("--scaling", choices=("weak", "strong"), default="weak")
-    p.add_argument("--dtype", choices=("f32", "f64"), default="f32",
-                   help="f32: BASELINE config 4 (f32 log-probs, f64 re-score); f64: the exact-f64 "
-                        "trellis (paths and scores bit-identical to the f64 reference recurrence)")
+    p.add_argument("--scaling", choices=("weak", "strong"), default="strong")
+    p.add_argument("--dtype", choices=("f64", "f32"), default="f64",
+                   help="f64 (default): the exact-f64 trellis, paths and scores bit-identical to the "
+                        "f64 reference recurrence; f32: the f32 trellis + f64 re-score of each path")
+    p.add_argument("--no-f32-extra", action="store_true", help="skip the f32-trellis extra measurement")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
     p.add_argument("--no-cpu-baseline", action="store_true")
     return p.parse_args()
@@ -102,9 +107,9 @@ def _cpu_model():
     return None
 
 
-def load_traffic():
+def load_traffic(f64):
     """Per-launch HBM bytes of the forward kernel from the committed rocprofv3 PMC summary."""
-    p = os.path.join(ROOT, "profiles", "pmc_trellis_fwd_c4.json")
+    p = os.path.join(ROOT, "profiles", "pmc_trellis_fwd_f64_c4.json" if f64 else "pmc_trellis_fwd_c4.json")
     if not os.path.exists(p):
         return None
     try:
@@ -162,15 +167,15 @@ def main():
     gathered = [None] * nbuf  # event: that buffer's gather has read it
     k_step = [0]
 
-    def step():
+    def step(dtype):
         i = k_step[0] % nbuf
         k_step[0] += 1
         path_d, score_d, status_d = outs[i]
         if gathered[i] is not None:
             stream.wait_event(gathered[i])
         cv.decode_batch_device(h, off_d, obs_d, path_d, score_d, status_d, offsets_host=off,
-                               stream=stream.cuda_stream, dtype=args.dtype,
-                               workspace_bytes=WORKSPACE_F64 if f64 else WORKSPACE)
+                               stream=stream.cuda_stream, dtype=dtype,
+                               workspace_bytes=WORKSPACE_F64 if dtype == "f64" else WORKSPACE)
         if world > 1:  # RCCL over xGMI: decoded paths (u8 states), scores, statuses to rank 0, one gather
             done = torch.cuda.Event()
             done.record(stream)
@@ -183,33 +188,44 @@ def main():
                 ev.record(comm)
                 gathered[i] = ev
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize(dev)
-    bad = int(sum(int((o[2] != 0).sum().item()) for o in outs))
-    if bad:
-        raise SystemExit(f"rank {rank}: {bad} sequences did not decode cleanly")
+    def timed(dtype, steps, warmup):
+        for _ in range(warmup):
+            step(dtype)
+        torch.cuda.synchronize(dev)
+        bad = int(sum(int((o[2] != 0).sum().item()) for o in outs))
+        if bad:
+            raise SystemExit(f"rank {rank}: {bad} sequences did not decode cleanly")
+        # timed region: barrier + sync on both sides, exactly K steps
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        fwd_ms, bt_ms, launches = 0.0, 0.0, 0
+        for _ in range(steps):
+            step(dtype)
+            t = cv.last_timing(h)  # HIP events recorded around each kernel on `stream`
+            fwd_ms += t["fwd_ms"]
+            bt_ms += t["bt_ms"]
+            launches += t["launches"]
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        if world > 1:
+            tt = torch.tensor([el], dtype=torch.float64, device=dev)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            el = float(tt.item())
+        return el, fwd_ms, bt_ms, launches
 
-    # timed region: barrier + sync on both sides, exactly K steps
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    fwd_ms, bt_ms, launches = 0.0, 0.0, 0
-    for _ in range(args.steps):
-        step()
-        t = cv.last_timing(h)  # HIP events recorded around each kernel on `stream`
-        fwd_ms += t["fwd_ms"]
-        bt_ms += t["bt_ms"]
-        launches += t["launches"]
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    el = time.perf_counter() - t0
-    if world > 1:
-        tt = torch.tensor([el], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        el = float(tt.item())
+    el, fwd_ms, bt_ms, launches = timed(args.dtype, args.steps, args.warmup)
+    f32_extra = None
+    if f64 and not args.no_f32_extra:
+        el32, fwd32, bt32, l32 = timed("f32", args.steps, args.warmup)
+        f32_extra = {"value": B * T_LEN * N_STATES * args.steps / el32, "unit": "trellis cells/s",
+                     "ms_per_step": el32 * 1e3 / args.steps,
+                     "kernel": "trellis_fwd2_f32<256>", "kernel_ms_per_launch": fwd32 / max(l32, 1),
+                     "note": "f32 log-probs (BASELINE config 4 literally), f64 re-score of each path; "
+                             "paths differ from the f64 reference on ~1-3% of sequences"}
 
     cells_total = B * T_LEN * N_STATES * args.steps
     value = cells_total / el
@@ -226,7 +242,7 @@ def main():
     per_launch_bytes = alg_bytes / (launches / args.steps)
     achieved = per_launch_bytes / fwd_launch_s
     pairs_per_launch = N_STATES * N_STATES * (T_LEN - 1) * nloc / (launches / args.steps)
-    traffic = None if f64 else load_traffic()
+    traffic = load_traffic(f64)
     pair_peak = F64_PAIR_PEAK if f64 else VALU_PAIR_PEAK
     out = {
         "metric": "trellis cells/s (N*T*batch), N=256 T=512 batch=65536",
@@ -242,9 +258,10 @@ def main():
         "dtype": args.dtype,
         "data": "synthetic (Dirichlet(1) log10 HMM, splitmix64 iid observations; SURVEY.md §8d config 4)",
         "config": {"workload": "config4: N=256 states, V=1024, T=512, " +
-                               (f"batch=65536 per rank (global {B})" if args.scaling == "weak" else
-                                f"batch={B} sharded over {world} ranks") +
-                               (", exact-f64 row-A0 trellis + backtrack" if f64 else
+                               (f"batch={args.batch} per rank (weak scaling, global {B})" if args.scaling == "weak" else
+                                f"batch={B} sharded over {world} ranks (strong scaling)") +
+                               (", exact-f64 row-A0 trellis + backtrack (paths/scores bit-identical to the f64 "
+                                "reference recurrence)" if f64 else
                                 ", f32 row-A0 trellis + backtrack + f64 re-score") +
                                (", RCCL gather to rank 0 (overlapped with the next step)" if world > 1 else ""),
                    "global_batch": B, "seq_len": T_LEN, "states": N_STATES, "parallelism": f"batch-shard x{world}"},
@@ -260,6 +277,8 @@ def main():
                               "frac": pairs_per_launch / fwd_launch_s / pair_peak}},
         "kernel_ms_per_step": {"forward": fwd_ms / args.steps, "backtrack_rescore": bt_ms / args.steps},
     }
+    if f32_extra is not None:
+        out["f32_trellis"] = f32_extra
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(pi, a, b, obs, args.cpu_seconds)
         out["cpu_baseline"]["gpu_over_cpu"] = value / out["cpu_baseline"]["value"]

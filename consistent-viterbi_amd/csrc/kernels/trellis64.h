@@ -25,7 +25,15 @@ struct T64FwdArgs {
   // layout so generic_backtrack<double> finishes the decode
   int nstates;             // real N (psi row stride)
   uint16_t* psi;           // [(elements of chunk)][N]
-  double* last_row;        // [(slots of launch)][N]
+  double* last_row;        // [(slots of launch)][N] (CP); EXT: [(slots of launch)][NP] final rows
+  // EXT features of trellis_fwd_f64 (the constrained decode's passes; all null/0 otherwise)
+  const int32_t* forced;       // [sum T] -1 free, >= 0 forced state, <= -2: row 0 = resume_rows[-2 - f]
+  const int64_t* ranges;       // [slot][2] explicit element ranges (begin, end); sequence id = slot
+  int reverse;                 // 1: traverse each range from end-1 down to begin (suffix pass on a^T)
+  const int32_t* start;        // [slot - seq_begin] s >= 0: row 0 = 0 at state s, -inf elsewhere
+  const int64_t* row_base;     // [slot] delta row index of the range's first element
+  const double* resume_rows;   // [r][NP] already-forced rows (resume flow)
+  const int32_t* slot_order;   // [launch index] -> slot (longest first)
 };
 
 struct T64BtArgs {

@@ -53,166 +53,288 @@ __device__ __forceinline__ void load_a(const double* p, double (&a)[C]) {
   }
 }
 
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+typedef double f64x2 __attribute__((ext_vector_type(2)));
+// constant address space: wave-uniform loads through these become s_load (SMEM), off the
+// in-order vmcnt queue that the A-row ring lives in
+template <typename T>
+using sptr = const __attribute__((address_space(4))) T*;
+template <typename T>
+__device__ __forceinline__ sptr<T> scalar_view(const T* p) {
+  return (sptr<T>)p;
+}
+
+// The lane's C consecutive f64 of table row `row` through a buffer descriptor: the row offset
+// is a scalar (soffset), the lane offset a constant VGPR, so the ring refills cost no VALU
+// address arithmetic (64-bit flat addresses cost 2 VALU per load).
+template <int C>
+__device__ __forceinline__ void load_row_buf(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff, double (&a)[C]) {
+  if constexpr (C % 2 == 0) {
+#pragma unroll
+    for (int c = 0; c < C / 2; ++c) {
+      const f64x2 v = __builtin_bit_cast(f64x2, __builtin_amdgcn_raw_buffer_load_b128(r, voff + 16 * c, soff, 0));
+      a[2 * c] = v.x;
+      a[2 * c + 1] = v.y;
+    }
+  } else {
+#pragma unroll
+    for (int c = 0; c < C; ++c)
+      a[c] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, voff + 8 * c, soff, 0));
+  }
+}
+
+// trellis_fwd_f64<C, S, PF, DPA, EXT>: S sequences per wave in lock step (see the file
+// header).  The A-row ring is CONTINUOUS across time steps: the refill after row i loads row
+// (i + PF) mod NP, so the first PF rows of step t+1 are in flight during the last rows of
+// step t (A is the same matrix every step) and no step starts on an empty pipeline.
+// Observations (and forced states) are scalar loads issued one step ahead; the step's
+// emission rows are loaded together in the epilogue (one exposed L2 round trip per step).
+// Built with -fno-honor-nans (no NaN can occur: NaN / +inf inputs are rejected), so fmax is
+// a bare v_max_f64 (IEEE-mode maxnum would otherwise canonicalise loop-carried operands).
+//
 // DPA: DPSolver's association (dp.rs:147-177): d'[j] = max_i ((a[i,j] + b[j,o]) + d[i]); the
-// emission enters every candidate, so it is loaded before the row loop (S <= 4: registers)
-template <int C, int S, int PF, bool DPA = false>  // PF: A rows in flight
+// emission enters every candidate, so it is loaded before the row loop (S <= 4: registers).
+// EXT: the constrained decode's passes -- forced states, explicit element ranges (sequence id
+// = slot), reversed traversal (the suffix pass runs on a^T with pi = 0), final-row output,
+// per-slot start state (segment tables), compact delta rows (row_base), resume rows and a
+// longest-first slot order.
+template <int C, int S, int PF, bool DPA, bool EXT>
 __global__ __launch_bounds__(64) void trellis_fwd_f64(T64FwdArgs g) {
   constexpr int NP = 64 * C;
   static_assert(S % 2 == 0, "S sequences are read from LDS two at a time");
-  static_assert(PF % 2 == 0, "the delta register double buffer alternates with the row parity");
-  __shared__ __attribute__((aligned(16))) double dl[NP * S];  // delta_{t-1}: [row][S]
+  static_assert(NP % PF == 0, "the ring wraps around at row NP");
+  // delta_{t-1}: [row][S]; row NP is padding, read (and ignored) by the prefetch of row i+1
+  __shared__ __attribute__((aligned(16))) double dl[(NP + 1) * S];
   const int lane = threadIdx.x;
   const int j0 = lane * C;
-  const int64_t slot0 = g.seq_begin + (int64_t)blockIdx.x * S;
-  const int64_t slot_end = g.seq_begin + g.nslots;
   const double ninf = ninf_d();
 
-  int64_t seq[S], e0[S];
+  // Per-sequence bookkeeping lives in LANE s of a few VGPRs (lanes >= S idle) rather than in
+  // S-element scalar arrays (those exceed the 102 SGPRs at S = 8 and spill): each step lane s
+  // loads the observation (and forced state) of sequence s one step ahead, and the values a
+  // step needs uniformly are read back with v_readlane.
+  const int ls = lane < S ? lane : S - 1;
+  const int64_t my_k = (int64_t)blockIdx.x * S + ls;
+  int my_T = 0;
+  int64_t my_seq = -1, my_eb = 0, my_rb = 0;
+  if (my_k < g.nslots && lane < S) {
+    const int64_t sl = (EXT && g.slot_order) ? (int64_t)g.slot_order[my_k] : g.seq_begin + my_k;
+    int64_t e0;
+    if (EXT && g.ranges) {
+      my_seq = sl;
+      e0 = g.ranges[2 * sl];
+      my_T = (int)(g.ranges[2 * sl + 1] - e0);
+    } else {
+      my_seq = g.order ? (int64_t)g.order[sl] : sl;
+      e0 = g.offsets[my_seq];
+      my_T = (int)(g.offsets[my_seq + 1] - e0);
+    }
+    my_eb = (EXT && g.reverse) ? e0 + my_T - 1 : e0;
+    my_rb = (EXT && g.row_base) ? g.row_base[sl] : e0 - g.delta_elem_base;
+  }
+  const int64_t my_slot = (EXT && g.slot_order && my_k < g.nslots) ? (int64_t)g.slot_order[my_k] : g.seq_begin + my_k;
   int T[S];
   int Tmax = 0;
 #pragma unroll
   for (int s = 0; s < S; ++s) {
-    const int64_t slot = slot0 + s;
-    if (slot < slot_end) {
-      seq[s] = g.order ? (int64_t)g.order[slot] : slot;
-      e0[s] = g.offsets[seq[s]];
-      T[s] = (int)(g.offsets[seq[s] + 1] - e0[s]);
-    } else {
-      seq[s] = -1;
-      e0[s] = 0;
-      T[s] = 0;
-    }
+    T[s] = __builtin_amdgcn_readlane(my_T, s);
     Tmax = T[s] > Tmax ? T[s] : Tmax;
   }
   if (Tmax <= 0) return;
+  const int dir = (EXT && g.reverse) ? -1 : 1;
   const unsigned V = (unsigned)g.nobs;
-  unsigned bad = 0;  // bit s: sequence s saw an out-of-range observation
-
-  // emission columns [j0, j0+C) of observation o (or -inf when o is out of range)
-  auto emis = [&](int s, int t, double (&e)[C]) {
-    int o = 0;
-    if (t < T[s]) o = g.obs[e0[s] + t];
-    const bool ok = (unsigned)o < V;
-    if (t < T[s] && !ok) bad |= 1u << s;
-    const double* row = g.et + (size_t)(ok ? o : 0) * NP + j0;
-#pragma unroll
-    for (int c = 0; c < C; ++c) e[c] = ok ? row[c] : ninf;
+  // lanes without a sequence read the first element of some sequence of the wave, so every
+  // per-step load is unconditional (a load under an exec mask, waited for at once, would
+  // drain the A-row ring: vmcnt is in order)
+  {
+    const unsigned long long live = __ballot(my_T > 0);
+    const int l0 = __builtin_ctzll(live);  // Tmax > 0: some lane is live
+    const int64_t eb0 = (int64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)my_eb, l0) |
+                        ((int64_t)__builtin_amdgcn_readlane((int)(my_eb >> 32), l0) << 32);
+    if (my_T <= 0) my_eb = eb0;
+  }
+  const int my_Tc = my_T > 0 ? my_T : 1;
+  bool my_bad = false;  // lane s: sequence s saw an out-of-range observation
+  // lane s: raw observation of step t of sequence s (index clamped into the sequence); the
+  // range check happens when the value is used, one step later (obs_use)
+  auto obs_lane = [&](int t) -> unsigned {
+    return (unsigned)g.obs[my_eb + (int64_t)dir * (t < my_Tc ? t : my_Tc - 1)];
+  };
+  auto obs_use = [&](unsigned o, int t) -> unsigned {
+    my_bad = my_bad || (t < my_T && o >= V);
+    return o < V ? o : 0u;
+  };
+  const int32_t* fsrc = (EXT && g.forced) ? g.forced : g.obs;
+  auto frc_lane = [&](int t) -> int {
+    if constexpr (!EXT) return -1;
+    return fsrc[my_eb + (int64_t)dir * (t < my_Tc ? t : my_Tc - 1)];
+  };
+  auto frc_use = [&](int f) -> int { return (EXT && g.forced && my_T > 0) ? f : -1; };
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(g.a), 0, NP * NP * 8, 0x00020000);
+  const uint32_t voff = (uint32_t)lane * C * 8;
+  constexpr uint32_t RB = NP * 8;  // bytes per table row
+  // emission row of observation o (wave-uniform; the padded columns of the table are -inf)
+  auto emis = [&](unsigned o, double (&e)[C]) {
+    const double* row = g.et + (size_t)o * NP + j0;
+    load_a<C>(row, e);
   };
   auto store_row = [&](int s, int t, const double (&v)[C]) {
-    if (t < T[s]) {
-      double* dst = g.delta + (e0[s] + t - g.delta_elem_base) * NP + j0;
+    if (g.delta && t < T[s]) {
+      const int64_t r = (int64_t)__builtin_amdgcn_readlane((int)(uint32_t)my_rb, s) |
+                        ((int64_t)__builtin_amdgcn_readlane((int)(my_rb >> 32), s) << 32);
+      double* dst = g.delta + (r + t) * NP + j0;
+#pragma unroll
+      for (int c = 0; c < C; ++c) dst[c] = v[c];
+    }
+    if (EXT && g.last_row && t == T[s] - 1) {
+      const int64_t k = (int64_t)__builtin_amdgcn_readlane((int)(uint32_t)(my_slot - g.seq_begin), s);
+      double* dst = g.last_row + k * NP + j0;
 #pragma unroll
       for (int c = 0; c < C; ++c) dst[c] = v[c];
     }
   };
-
-  // t = 0: d0 = pi + b[:, o0]
+  // forced state f >= 0: every other state of that element is impossible
+  auto force = [&](double (&v)[C], int f) {
+    if (EXT && f >= 0) {
 #pragma unroll
-  for (int s = 0; s < S; ++s) {
-    double e[C], v[C];
-    emis(s, 0, e);
-#pragma unroll
-    for (int c = 0; c < C; ++c) {
-      v[c] = g.zero_init ? 0.0 : g.pi[j0 + c] + e[c];
-      dl[(j0 + c) * S + s] = v[c];
+      for (int c = 0; c < C; ++c) v[c] = (j0 + c == f) ? v[c] : ninf;
     }
-    store_row(s, 0, v);
+  };
+
+  // ---- t = 0: d0 = pi + b[:, o0] (hmm.rs:215-218, cp.rs:66-68) ----
+  unsigned onext_l;  // lane s: observation of the next step
+  int fnext_l;
+  {
+    const unsigned o0 = obs_use(obs_lane(0), 0);
+    const int f0l = frc_use(frc_lane(0));
+    const int st_l = (EXT && g.start && my_T > 0) ? g.start[my_slot - g.seq_begin] : -1;
+    double e[S][C];
+#pragma unroll
+    for (int s = 0; s < S; ++s) emis((unsigned)__builtin_amdgcn_readlane((int)o0, s), e[s]);
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      double v[C];
+#pragma unroll
+      for (int c = 0; c < C; ++c) v[c] = g.zero_init ? 0.0 : g.pi[j0 + c] + e[s][c];
+      if (EXT && g.start) {  // segment table: start in state st with score 0 (cfn.rs:11-34 pattern)
+        const int st = __builtin_amdgcn_readlane(st_l, s);
+        if (st >= 0) {
+#pragma unroll
+          for (int c = 0; c < C; ++c) v[c] = (j0 + c == st) ? 0.0 : ninf;
+        }
+      }
+      int f0 = __builtin_amdgcn_readlane(f0l, s);
+      if (EXT && f0 <= -2) {  // resume: row t_1 of the prefix pass, already forced
+        const double* rr = g.resume_rows + (size_t)(-2 - f0) * NP + j0;
+#pragma unroll
+        for (int c = 0; c < C; ++c) v[c] = rr[c];
+        f0 = -1;
+      }
+      force(v, f0);
+#pragma unroll
+      for (int c = 0; c < C; ++c) dl[(j0 + c) * S + s] = v[c];
+      store_row(s, 0, v);
+    }
+    onext_l = obs_lane(1);
+    fnext_l = frc_lane(1);
   }
-  __syncthreads();
 
   // forward waves win issue arbitration over co-resident backtrack waves of the previous
   // chunk (overlap mode), as in trellis_fwd2_f32
   __builtin_amdgcn_s_setprio(3);
-  const double* __restrict__ arow = g.a + j0;
-  double acc[C][S];  // after a step: delta_t of the S sequences (stored at the next step)
+  double ar[PF][C];  // the A-row ring: ar[u] holds row i0 + u
+#pragma unroll
+  for (int u = 0; u < PF; ++u) {
+    load_row_buf<C>(ra, voff, u * RB, ar[u]);
+    // keep the priming loads in ring order: the waitcnt pass then counts row u as 2(PF-u)-1
+    // loads old at the loop head (scheduled out of order it fell back to vmcnt(0) there)
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  double acc[C][S];
   for (int t = 1; t < Tmax; ++t) {
-    double ar[PF][C];
+    const unsigned ocur_l = obs_use(onext_l, t);
+    const int fcur_l = frc_use(fnext_l);
+    double ecur[DPA ? S : 1][C];
+    if constexpr (DPA) {
 #pragma unroll
-    for (int u = 0; u < PF; ++u) load_a(arow + (size_t)u * NP, ar[u]);
-    // delta_{t-1} rows go to HBM only now: the ring loads above were issued first, so waiting
-    // for them (in-order vmcnt) does not wait for these stores
-    if (t > 1) {
-#pragma unroll
-      for (int s = 0; s < S; ++s) {
-        double v[C];
-#pragma unroll
-        for (int c = 0; c < C; ++c) v[c] = acc[c][s];
-        store_row(s, t - 1, v);
-      }
+      for (int s = 0; s < S; ++s) emis((unsigned)__builtin_amdgcn_readlane((int)ocur_l, s), ecur[s]);
     }
 #pragma unroll
     for (int c = 0; c < C; ++c)
 #pragma unroll
       for (int s = 0; s < S; ++s) acc[c][s] = ninf;
-    double ecur[DPA ? S : 1][C];
-    if constexpr (DPA) {
-#pragma unroll
-      for (int s = 0; s < S; ++s) emis(s, t, ecur[s]);
-    }
     // delta rows double-buffered in registers (dv[u & 1] = row i): row i+1's broadcast reads
     // are in flight while row i computes
-    double2 dv[2][S / 2];
+    f64x2 dv[2][S / 2];
 #pragma unroll
-    for (int s2 = 0; s2 < S / 2; ++s2) dv[0][s2] = reinterpret_cast<const double2*>(dl)[s2];
+    for (int s2 = 0; s2 < S / 2; ++s2) dv[0][s2] = *reinterpret_cast<const f64x2*>(dl + 2 * s2);
 #pragma nounroll
     for (int i0 = 0; i0 < NP; i0 += PF) {
 #pragma unroll
       for (int u = 0; u < PF; ++u) {
         const int i = i0 + u;
         {
-          const double2* nrow = reinterpret_cast<const double2*>(dl + min(i + 1, NP - 1) * S);
+          const f64x2* nrow = reinterpret_cast<const f64x2*>(dl + (i + 1) * S);
 #pragma unroll
           for (int s2 = 0; s2 < S / 2; ++s2) dv[(u + 1) & 1][s2] = nrow[s2];
         }
 #pragma unroll
         for (int s2 = 0; s2 < S / 2; ++s2) {
-          const double2 d = dv[u & 1][s2];
+          const f64x2 d = dv[u & 1][s2];
 #pragma unroll
           for (int c = 0; c < C; ++c) {
             if constexpr (DPA) {
-              acc[c][2 * s2] = fmax(acc[c][2 * s2], (ar[u][c] + ecur[2 * s2][c]) + d.x);
-              acc[c][2 * s2 + 1] = fmax(acc[c][2 * s2 + 1], (ar[u][c] + ecur[2 * s2 + 1][c]) + d.y);
+              acc[c][2 * s2] = __builtin_fmax(acc[c][2 * s2], (ar[u][c] + ecur[2 * s2][c]) + d.x);
+              acc[c][2 * s2 + 1] = __builtin_fmax(acc[c][2 * s2 + 1], (ar[u][c] + ecur[2 * s2 + 1][c]) + d.y);
             } else {
-              acc[c][2 * s2] = fmax(acc[c][2 * s2], d.x + ar[u][c]);
-              acc[c][2 * s2 + 1] = fmax(acc[c][2 * s2 + 1], d.y + ar[u][c]);
+              acc[c][2 * s2] = __builtin_fmax(acc[c][2 * s2], d.x + ar[u][c]);
+              acc[c][2 * s2 + 1] = __builtin_fmax(acc[c][2 * s2 + 1], d.y + ar[u][c]);
             }
           }
         }
-        // refill this ring slot with row i + PF (clamped: the last rows reload row NP-1) only
-        // after its last use, into the same registers: no copies, and the in-flight loads
-        // cross the loop back-edge without a vmcnt(0) drain
-        const int nr = min(i + PF, NP - 1);
-        load_a(arow + (size_t)nr * NP, ar[u]);
+        // refill this ring slot with row (i + PF) mod NP -- the wrap-around rows are the next
+        // step's first rows -- only after its last use, into the same registers: no copies,
+        // and the in-flight loads cross the loop back-edge without a vmcnt(0) drain
+        const int nr = i + PF < NP ? i + PF : i + PF - NP;
+        load_row_buf<C>(ra, voff, (uint32_t)nr * RB, ar[u]);
       }
     }
-    __syncthreads();  // every lane has read delta_{t-1} before it is overwritten
+    // a single-wave workgroup: LDS operations of the wave execute in order, so the reads of
+    // delta_{t-1} above complete before the writes below; only the compiler must not reorder
+    asm volatile("" ::: "memory");
+    // epilogue: d_t = m + b[:, o_t] (viterbi.rs:17), emission rows of all S sequences in flight
+    // together; then the next step's observations (scalar loads)
+    double e[DPA ? 1 : S][C];
+    if constexpr (!DPA) {
 #pragma unroll
-    for (int s = 0; s < S; ++s) {
-      double e[C], v[C];
-      if constexpr (!DPA) emis(s, t, e);
+      for (int s = 0; s < S; ++s) emis((unsigned)__builtin_amdgcn_readlane((int)ocur_l, s), e[s]);
+    }
+    onext_l = obs_lane(t + 1);
+    fnext_l = frc_lane(t + 1);
+#pragma unroll
+    for (int s2 = 0; s2 < S / 2; ++s2) {
+      double v0[C], v1[C];
 #pragma unroll
       for (int c = 0; c < C; ++c) {
-        v[c] = DPA ? acc[c][s] : acc[c][s] + e[c];
-        acc[c][s] = v[c];
-        dl[(j0 + c) * S + s] = v[c];
+        v0[c] = DPA ? acc[c][2 * s2] : acc[c][2 * s2] + e[DPA ? 0 : 2 * s2][c];
+        v1[c] = DPA ? acc[c][2 * s2 + 1] : acc[c][2 * s2 + 1] + e[DPA ? 0 : 2 * s2 + 1][c];
       }
+      force(v0, __builtin_amdgcn_readlane(fcur_l, 2 * s2));
+      force(v1, __builtin_amdgcn_readlane(fcur_l, 2 * s2 + 1));
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        f64x2 w;
+        w.x = v0[c];
+        w.y = v1[c];
+        *reinterpret_cast<f64x2*>(dl + (j0 + c) * S + 2 * s2) = w;
+      }
+      store_row(2 * s2, t, v0);
+      store_row(2 * s2 + 1, t, v1);
     }
-    __syncthreads();
+    asm volatile("" ::: "memory");
   }
-  if (Tmax > 1) {
-#pragma unroll
-    for (int s = 0; s < S; ++s) {
-      double v[C];
-#pragma unroll
-      for (int c = 0; c < C; ++c) v[c] = acc[c][s];
-      store_row(s, Tmax - 1, v);
-    }
-  }
-  if (lane == 0) {
-#pragma unroll
-    for (int s = 0; s < S; ++s)
-      if (bad & (1u << s)) g.status[seq[s]] = CVK_SEQ_BADOBS;
-  }
+  if (lane < S && my_bad) g.status[my_seq] = CVK_SEQ_BADOBS;
 }
 
 // CP association (CPSolver, cp.rs:70-79 via utils.rs:24-38, hmm.rs:220-222):
@@ -476,17 +598,22 @@ hipError_t fwd_cs(const T64FwdArgs& fa, int64_t nseq, hipStream_t stream) {
     const char* e = getenv("CV_T64_PF");
     return e ? atoi(e) : 8;
   }();
-  // PF = 8 measured 183 vs 208 ms (PF = 4) per config-4 forward; S = 6 / PF = 6 lost too
-  // (176 / 170 vs 164 ms, profiles/r01_t64_sweep.txt)
+  const bool ext = fa.forced || fa.ranges || fa.reverse || fa.start || fa.row_base || fa.resume_rows ||
+                   fa.slot_order || fa.last_row;
+  const dim3 grid((unsigned)blocks), block(64);
   if (fa.dp_assoc) {
+    if (ext) return hipErrorInvalidValue;
     if constexpr (S <= 4)
-      hipLaunchKernelGGL((trellis_fwd_f64<C, S, 8, true>), dim3((unsigned)blocks), dim3(64), 0, stream, fa);
+      hipLaunchKernelGGL((trellis_fwd_f64<C, S, 8, true, false>), grid, block, 0, stream, fa);
     else
       return hipErrorInvalidValue;
-  } else if (pf == 4)
-    hipLaunchKernelGGL((trellis_fwd_f64<C, S, 4>), dim3((unsigned)blocks), dim3(64), 0, stream, fa);
-  else
-    hipLaunchKernelGGL((trellis_fwd_f64<C, S, 8>), dim3((unsigned)blocks), dim3(64), 0, stream, fa);
+  } else if (ext) {
+    hipLaunchKernelGGL((trellis_fwd_f64<C, S, 8, false, true>), grid, block, 0, stream, fa);
+  } else if (pf == 4) {
+    hipLaunchKernelGGL((trellis_fwd_f64<C, S, 4, false, false>), grid, block, 0, stream, fa);
+  } else {
+    hipLaunchKernelGGL((trellis_fwd_f64<C, S, 8, false, false>), grid, block, 0, stream, fa);
+  }
   return hipGetLastError();
 }
 

@@ -135,4 +135,35 @@ def test_t64_config4_shape_sample(gpu):
     same = np.array([np.array_equal(p32[off[k]:off[k + 1]], p64[off[k]:off[k + 1]]) for k in range(nseq)])
     # where the f32 path equals the f64 one, the f64 re-score equals the f64 decode's score exactly
     assert np.array_equal(s32[same], s64[same])
-    assert same.mean() > 0.5
+    # the f32 trellis is bit-exact against the f32 oracle (test_gpu_parity.py), so this count is a
+    # property of the inputs, not of the kernels: measured on MI355X and pinned here
+    ndiff = int((~same).sum())
+    print(f"f32/f64 path disagreement: {ndiff}/{nseq} sequences")
+    assert ndiff == F32_F64_DIFF_C4_512, ndiff
+    # where they differ, the f64 path scores at least as high in f64 (it is the f64 optimum)
+    assert np.all(s64[~same] >= s32[~same])
+
+
+F32_F64_DIFF_C4_512 = 19  # measured on MI355X (profiles/r02_pytest_f64.log): 3.7% of these paths
+
+
+def test_t64_config4_full_batch_vs_generic(gpu):
+    """The bench's headline mode on the FULL config-4 batch (65,536 sequences, N=256, T=512):
+    every path, score and status of the default f64 decode (trellis_fwd_f64 + backtrack_f64) is
+    identical to the generic f64 kernel (inline first-argmax, an independent implementation
+    that is itself bit-exact against the oracle), and a 16-sequence sample matches the f64
+    oracle (the reference recurrence, viterbi.rs:13-18 in f64)."""
+    c = synth.config("c4")
+    pi, a, b, off, obs = c["pi"], c["a"], c["b"], c["offsets"], c["obs"]
+    h = cv.HMM(pi, a, b.reshape(256, 32, 32))
+    p64, s64, st64 = cv.decode_batch(h, off, obs, dtype="f64", rescore_f64=False)
+    assert cv.last_timing(h)["kernel"] == "trellis_f64"
+    assert np.all(st64 == 0)
+    pg, sg, stg = cv.decode_batch(h, off, obs, dtype="f64", kernel="generic", rescore_f64=False)
+    assert cv.last_timing(h)["kernel"] == "generic"
+    _assert_same((p64, s64, st64), (pg, sg, stg), "config 4 full batch: t64 vs generic f64")
+    T = 512
+    for k in np.linspace(0, len(off) - 2, 16).astype(int):
+        lo, hi = off[k], off[k + 1]
+        rp, rs, rst = O.decode_batch(pi, a, b, np.array([0, T]), obs[lo:hi], O.VITERBI, np.float64)
+        assert rst[0] == st64[k] and rs[0] == s64[k] and np.array_equal(rp, p64[lo:hi]), f"seq {k}"
