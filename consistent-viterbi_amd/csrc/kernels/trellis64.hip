@@ -65,6 +65,42 @@ __device__ __forceinline__ sptr<T> scalar_view(const T* p) {
   return (sptr<T>)p;
 }
 
+// f64 -> its high / low 32-bit words (the hi word alone is the value with the mantissa
+// truncated to 20 bits: same sign and exponent, |d - hi| < |hi| * 2^-20)
+__device__ __forceinline__ uint32_t hi_word(double d) { return (uint32_t)(__builtin_bit_cast(uint64_t, d) >> 32); }
+__device__ __forceinline__ uint32_t lo_word(double d) { return (uint32_t)__builtin_bit_cast(uint64_t, d); }
+__device__ __forceinline__ double from_words(uint32_t hi, uint32_t lo) {
+  return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+
+// C f64 as two planes of C words each (dwordx4 / dwordx2 stores), non-temporal
+template <int C>
+__device__ __forceinline__ void store_split(uint32_t* hi, uint32_t* lo, const double (&v)[C]) {
+  if constexpr (C % 4 == 0) {
+#pragma unroll
+    for (int c = 0; c < C; c += 4) {
+      u32x4 h = {hi_word(v[c]), hi_word(v[c + 1]), hi_word(v[c + 2]), hi_word(v[c + 3])};
+      u32x4 l = {lo_word(v[c]), lo_word(v[c + 1]), lo_word(v[c + 2]), lo_word(v[c + 3])};
+      __builtin_nontemporal_store(h, reinterpret_cast<u32x4*>(hi + c));
+      __builtin_nontemporal_store(l, reinterpret_cast<u32x4*>(lo + c));
+    }
+  } else if constexpr (C % 2 == 0) {
+#pragma unroll
+    for (int c = 0; c < C; c += 2) {
+      u32x2 h = {hi_word(v[c]), hi_word(v[c + 1])};
+      u32x2 l = {lo_word(v[c]), lo_word(v[c + 1])};
+      __builtin_nontemporal_store(h, reinterpret_cast<u32x2*>(hi + c));
+      __builtin_nontemporal_store(l, reinterpret_cast<u32x2*>(lo + c));
+    }
+  } else {
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      __builtin_nontemporal_store(hi_word(v[c]), hi + c);
+      __builtin_nontemporal_store(lo_word(v[c]), lo + c);
+    }
+  }
+}
+
 // The lane's C consecutive f64 of table row `row` through a buffer descriptor: the row offset
 // is a scalar (soffset), the lane offset a constant VGPR, so the ring refills cost no VALU
 // address arithmetic (64-bit flat addresses cost 2 VALU per load).
@@ -181,11 +217,12 @@ __global__ __launch_bounds__(64) void trellis_fwd_f64(T64FwdArgs g) {
   };
   auto store_row = [&](int s, int t, const double (&v)[C]) {
     if (g.delta && t < T[s]) {
+      // split-plane row (see T64 row layout in trellis64.h): hi words [0, NP), lo words
+      // [NP, 2 NP); streaming stores (read once, by the backtrack)
       const int64_t r = (int64_t)__builtin_amdgcn_readlane((int)(uint32_t)my_rb, s) |
                         ((int64_t)__builtin_amdgcn_readlane((int)(my_rb >> 32), s) << 32);
-      double* dst = g.delta + (r + t) * NP + j0;
-#pragma unroll
-      for (int c = 0; c < C; ++c) dst[c] = v[c];
+      uint32_t* dst = reinterpret_cast<uint32_t*>(g.delta) + (r + t) * (2 * NP) + j0;
+      store_split<C>(dst, dst + NP, v);
     }
     if (EXT && g.last_row && t == T[s] - 1) {
       const int64_t k = (int64_t)__builtin_amdgcn_readlane((int)(uint32_t)(my_slot - g.seq_begin), s);
@@ -495,10 +532,17 @@ __device__ __forceinline__ double wave_max_d(double v) {
   return v;
 }
 
-// PF: delta rows in flight per wave.  The backtrack streams 2 KiB f64 rows from HBM, and at
-// NP >= 192 occupancy hides the latency better than a deeper ring: config 4 (NP = 256, serial
-// schedule) 14.3 ms at PF = 2 (8 waves/SIMD) vs 15.3 (PF = 4, 74 VGPRs, 6 waves/SIMD),
-// 16.9 (PF = 8) and 21.9 (PF = 16) -- profiles/r01_t64_bt_pf.txt.
+// PF: rows in flight per wave (hi planes, 1 KiB each at NP = 256); at NP >= 192 occupancy
+// hides the HBM latency better than a deeper ring (profiles/r01_t64_bt_pf.txt, 2-KiB rows).
+//
+// Rows come in the split-plane layout of the forward pass.  Each step first reads only the
+// HI words (the f64 with its mantissa truncated to 20 bits, error < |hi| * 2^-20): every
+// candidate s_i = d_{t-1}[i] + a[i, cur] gets an interval [L_i, U_i] around the f64 sum of
+// the truncated value (the truncation bound plus one rounding of the add, monotone f64
+// addition).  When exactly one candidate has U_i >= max_k L_k it is the unique -- hence
+// first -- argmax of the exact f64 sums; otherwise (near ties, ~1% of steps at config 4) the
+// LO words of that row are read too and the exact sums decide with the first-index rule.
+// Half the HBM bytes of a full-row backtrack, same path bit for bit.
 template <int KP, int PF>
 __global__ __launch_bounds__(256) void backtrack_f64(T64BtArgs g) {
   constexpr int NP = 64 * KP;
@@ -517,13 +561,20 @@ __global__ __launch_bounds__(256) void backtrack_f64(T64BtArgs g) {
     return;
   }
   int32_t* __restrict__ path = g.path + e0;
-  const double* __restrict__ drow = g.delta + (e0 - g.delta_elem_base) * NP;
+  const uint32_t* __restrict__ rows = reinterpret_cast<const uint32_t*>(g.delta) + (e0 - g.delta_elem_base) * (2 * NP);
+  constexpr uint32_t NINF_HI = 0xFFF00000u;  // hi word of -inf (lo word 0)
   bool valid[KP];
 #pragma unroll
   for (int k = 0; k < KP; ++k) valid[k] = (lane + 64 * k) < N;
-  auto load_row = [&](int r, double (&dst)[KP]) {
+  auto load_hi = [&](int r, uint32_t (&dst)[KP]) {
 #pragma unroll
-    for (int k = 0; k < KP; ++k) dst[k] = (r >= 0 && valid[k]) ? drow[(size_t)r * NP + lane + 64 * k] : ninf_d();
+    for (int k = 0; k < KP; ++k)
+      dst[k] = (r >= 0 && valid[k]) ? __builtin_nontemporal_load(rows + (size_t)r * (2 * NP) + lane + 64 * k) : NINF_HI;
+  };
+  auto load_lo = [&](int r, uint32_t (&dst)[KP]) {
+#pragma unroll
+    for (int k = 0; k < KP; ++k)
+      dst[k] = (r >= 0 && valid[k]) ? __builtin_nontemporal_load(rows + (size_t)r * (2 * NP) + NP + lane + 64 * k) : 0u;
   };
   auto first_argmax = [&](const double (&s)[KP], double& M) {
     double m = s[0];
@@ -541,8 +592,12 @@ __global__ __launch_bounds__(256) void backtrack_f64(T64BtArgs g) {
   double bv;
   int cur;
   {
+    uint32_t hw[KP], lw[KP];
+    load_hi(T - 1, hw);
+    load_lo(T - 1, lw);
     double last[KP];
-    load_row(T - 1, last);
+#pragma unroll
+    for (int k = 0; k < KP; ++k) last[k] = valid[k] ? from_words(hw[k], lw[k]) : ninf_d();
     cur = first_argmax(last, bv);  // cp.rs:86
   }
   const uint8_t prior = g.status[seq];
@@ -557,33 +612,64 @@ __global__ __launch_bounds__(256) void backtrack_f64(T64BtArgs g) {
   int pathreg = 0;
   if (lane == ((T - 1) & 63)) pathreg = cur;
   if (((T - 1) & 63) == 0 && lane == 0) path[T - 1] = cur;
-  double ring[PF][KP];
+  uint32_t ring[PF][KP];
 #pragma unroll
-  for (int u = 0; u < PF; ++u) load_row(T - 2 - u, ring[u]);
+  for (int u = 0; u < PF; ++u) load_hi(T - 2 - u, ring[u]);
   for (int base = T - 1; base >= 1; base -= PF) {
 #pragma unroll
     for (int u = 0; u < PF; ++u) {
       const int t = base - u;
       if (t >= 1) {
         const double* acol = g.at + (size_t)cur * NP + lane;
-        double s[KP];
-        if (g.dp_assoc) {  // (a[i,cur] + b[cur,o_t]) + d_{t-1}[i]  (dp.rs:149 arc_p, then + cost)
-          const double e = g.et[(size_t)g.obs[e0 + t] * NP + cur];
+        double e = 0.0;
+        if (g.dp_assoc) e = g.et[(size_t)g.obs[e0 + t] * NP + cur];
+        double av[KP];
 #pragma unroll
-          for (int k = 0; k < KP; ++k) s[k] = valid[k] ? (acol[64 * k] + e) + ring[u][k] : ninf_d();
-        } else {
+        for (int k = 0; k < KP; ++k) av[k] = g.dp_assoc ? acol[64 * k] + e : acol[64 * k];
+        // candidates from the truncated values: s~ = a + h (DPSolver: (a + b) + h)
+        double st[KP], up[KP];
+        double lmax = ninf_d();
 #pragma unroll
-          for (int k = 0; k < KP; ++k) s[k] = valid[k] ? ring[u][k] + acol[64 * k] : ninf_d();
+        for (int k = 0; k < KP; ++k) {
+          const double h = from_words(ring[u][k], 0u);
+          const double x = valid[k] ? (g.dp_assoc ? av[k] + h : h + av[k]) : ninf_d();
+          const bool fin = x > ninf_d();
+          // |d - h| < |h| 2^-20, plus one f64 rounding of the add (< |x| 2^-52; 2^-51 kept),
+          // plus an absolute floor for subnormal truncations
+          const double err = __builtin_fabs(h) * 0x1p-20 + __builtin_fabs(x) * 0x1p-51 + 0x1p-1000;
+          st[k] = x;
+          up[k] = fin ? x + err : ninf_d();
+          lmax = fmax(lmax, fin ? x - err : ninf_d());
         }
-        double M;
-        cur = first_argmax(s, M);
+        lmax = wave_max_d(lmax);
+        int cnt = 0, idx = 0;
+#pragma unroll
+        for (int k = KP - 1; k >= 0; --k) {
+          const unsigned long long mask = __ballot(valid[k] && st[k] > ninf_d() && up[k] >= lmax);
+          cnt += __builtin_popcountll(mask);
+          if (mask) idx = 64 * k + __builtin_ctzll(mask);
+        }
+        if (cnt == 1) {
+          cur = idx;
+        } else {  // near tie (or all -inf): the exact f64 sums of this row decide
+          uint32_t lw[KP];
+          load_lo(t - 1, lw);
+          double s[KP];
+#pragma unroll
+          for (int k = 0; k < KP; ++k) {
+            const double d = from_words(ring[u][k], lw[k]);
+            s[k] = valid[k] ? (g.dp_assoc ? av[k] + d : d + av[k]) : ninf_d();
+          }
+          double M;
+          cur = first_argmax(s, M);
+        }
         const int tp = t - 1;
         if (lane == (tp & 63)) pathreg = cur;
         if ((tp & 63) == 0 && tp + lane < T) path[tp + lane] = pathreg;
       }
     }
 #pragma unroll
-    for (int u = 0; u < PF; ++u) load_row(base - PF - 1 - u, ring[u]);
+    for (int u = 0; u < PF; ++u) load_hi(base - PF - 1 - u, ring[u]);
   }
   if (lane == 0) {
     g.score[seq] = bv;

@@ -1,0 +1,13 @@
+#!/bin/bash
+# A/B of bit-identical env knobs on the config-4 bench, interleaved on ONE box (clocks differ
+# between boxes by several %): AB="VAR=a VAR=b" ROUNDS=2 BENCH_ARGS=... tools/ab_env.sh
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$R/gpurun_out/${TAG:-ab}
+mkdir -p $OUT
+cd $R
+for r in $(seq 1 ${ROUNDS:-2}); do
+  for v in $AB; do
+    env $v timeout -k 10 ${T_BENCH:-240} python bench.py ${BENCH_ARGS:---steps 8 --warmup 2 --no-cpu-baseline --no-f32-extra} > $OUT/$v.$r.log 2>&1 || { echo "FAIL $v"; exit 1; }
+    python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[2], sys.argv[3], round(d['ms_per_step'],2), 'fwd', round(d['kernel_ms_per_step']['forward'],2), 'bt', round(d['kernel_ms_per_step']['backtrack_rescore'],2))" $OUT/$v.$r.log $v $r | tee -a $OUT/summary.txt
+  done
+done
