@@ -9,17 +9,23 @@
 
 namespace cvcsp {
 
-void add_exact(int64_t* limbs4, int64_t* ninf_count, float x) {
+template <typename REAL>
+static bool add_exact_t(int64_t* limbs4, int64_t* ninf_count, REAL x) {
   if (!(x > -INFINITY)) {
     *ninf_count += 1;
-    return;
+    return true;
   }
+  if (!cvx::term_in_range((double)x)) return false;  // |x| >= 2^32: outside the exact unit
   // the limbs of nearbyint(x * 2^64), shared with the device sums (exact_fixed.h); checked
   // bit-identical to the double -> __int128 form on 3.7e7 floats incl. every exponent
   int64_t l[4];
   cvx::fixed64_limbs(x, l);
   for (int k = 0; k < 4; ++k) limbs4[k] += l[k];
+  return true;
 }
+
+bool add_exact(int64_t* limbs4, int64_t* ninf_count, float x) { return add_exact_t(limbs4, ninf_count, x); }
+bool add_exact(int64_t* limbs4, int64_t* ninf_count, double x) { return add_exact_t(limbs4, ninf_count, x); }
 
 static inline __int128 limbs_value(const int64_t* l) {
   return (__int128)l[0] + ((__int128)l[1] << 32) + ((__int128)l[2] << 64) + ((__int128)l[3] << 96);

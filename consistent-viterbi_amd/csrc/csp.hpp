@@ -26,8 +26,10 @@ inline int64_t partial_words(int N, int ncomp, int64_t npairs) {
   return (int64_t)ncomp * unary_words(N) + npairs * pair_words(N);
 }
 
-// Adds the exact value of x (units of 2^-64) into 4 limbs, or counts it as -inf.
-void add_exact(int64_t* limbs4, int64_t* ninf_count, float x);
+// Adds the exact value of x (units of 2^-64) into 4 limbs, or counts it as -inf; false (and
+// nothing added) when |x| >= 2^32, outside the exact unit's range (exact_fixed.h).
+bool add_exact(int64_t* limbs4, int64_t* ninf_count, float x);
+bool add_exact(int64_t* limbs4, int64_t* ninf_count, double x);
 
 // Pairs (c1 < c2) of different components that are consecutive constrained elements of
 // some sequence, sorted and unique.

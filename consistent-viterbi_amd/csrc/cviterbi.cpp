@@ -123,6 +123,7 @@ struct cv_hmm {
   int np64 = 0;
   bool t64_ready = false;
   DevBuf q_a, q_at, q_pi, q_et;
+  DevBuf q_pi0;  // the reversed (suffix) pass: pi = 0 for the N states, -inf padding
   // f32 generic tables
   bool g32_ready = false;
   DevBuf d_pi32, d_a32, d_et32;
@@ -131,6 +132,7 @@ struct cv_hmm {
   DevBuf st_off, st_obs, st_path, st_score, st_status, st_forced;
   DevBuf cs_ranges, cs_delta, cs_g, cs_mu, cs_start, cs_zero;  // constrained-decode scratch
   DevBuf cs_comp, cs_words;  // device exact unary sums: per-sequence components, output words
+  DevBuf cs_flag;            // device exact sums: out-of-range term flag
   DevBuf cs_seg;             // segment-table rows (cs_delta keeps the prefix rows t_1)
   // resume flow of the constrained decode: stored prefix rows, forced row t_1 per constrained
   // sequence, the compact suffix batch and its index arrays
@@ -289,6 +291,9 @@ cv_status ensure_t64_tables(cv_hmm* h) {
   if ((st = upload(h->q_at, at.data(), at.size() * 8)) != CV_OK) return st;
   if ((st = upload(h->q_pi, pi.data(), pi.size() * 8)) != CV_OK) return st;
   if ((st = upload(h->q_et, et.data(), et.size() * 8)) != CV_OK) return st;
+  std::vector<double> pi0(NP, ninf);
+  for (int i = 0; i < N; ++i) pi0[i] = 0.0;
+  if ((st = upload(h->q_pi0, pi0.data(), pi0.size() * 8)) != CV_OK) return st;
   h->np64 = NP;
   h->t64_ready = true;
   return CV_OK;
@@ -452,7 +457,7 @@ cvk::BacktrackArgs make_bt_args(cv_hmm* h, unsigned char* wsb, const int64_t* of
 // Core device-side decode.  All pointers are device pointers except offsets_host.
 cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, const int64_t* offsets_dev,
                         const int32_t* obs_dev, const cv_opts& o, int32_t* path_dev, double* score_dev,
-                        uint8_t* status_dev, hipStream_t stream, const float* resume_rows = nullptr) {
+                        uint8_t* status_dev, hipStream_t stream, const void* resume_rows = nullptr) {
   if (o.dtype != CV_DTYPE_F32 && o.dtype != CV_DTYPE_F64) return set_err(CV_EINVAL, "bad dtype %d", o.dtype);
   if (o.assoc < CV_ASSOC_VITERBI || o.assoc > CV_ASSOC_DECODE) return set_err(CV_EINVAL, "bad assoc %d", o.assoc);
   const bool trellis_ok = o.dtype == CV_DTYPE_F32 && o.assoc == CV_ASSOC_VITERBI &&
@@ -472,13 +477,14 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
   // VITERBI (row A0), DECODE (row 0 = 0.0) and DP ((a + b) + d) share trellis_fwd_f64 +
   // backtrack_f64; CP runs
   // trellis_cp_f64 (argmax in the forward pass) + generic_backtrack<double>
+  // forced states / resume rows (the constrained decode): row A0 only (trellis_fwd_f64 EXT)
   const bool t64_ok = o.dtype == CV_DTYPE_F64 &&
                       (o.assoc == CV_ASSOC_VITERBI || o.assoc == CV_ASSOC_DECODE || o.assoc == CV_ASSOC_CP ||
                        o.assoc == CV_ASSOC_DP) &&
-                      !o.forced && !resume_rows && cvk::t64_padded_states(h->N) != 0;
+                      (!(o.forced || resume_rows) || o.assoc == CV_ASSOC_VITERBI) && cvk::t64_padded_states(h->N) != 0;
   if (o.kernel == CV_KERNEL_TRELLIS_F64 && !t64_ok)
     return set_err(CV_EUNSUPPORTED,
-                   "f64 trellis kernel needs dtype f64, N <= 256, no forced states");
+                   "f64 trellis kernel needs dtype f64, N <= 256, and forced states only with assoc VITERBI");
   const bool use_t64 = !use_trellis && t64_ok &&
                        (o.kernel == CV_KERNEL_TRELLIS_F64 || (o.kernel == CV_KERNEL_AUTO && !(o.flags & CV_FLAG_NO_T64)));
   if (!use_trellis && !use_t64 && h->N > cvk::generic_max_states(o.dtype == CV_DTYPE_F64 ? 8 : 4))
@@ -672,7 +678,7 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
       fa.status = status_dev;
       fa.nobs = (int)h->V;
       fa.forced = o.forced;
-      fa.resume_rows = resume_rows;
+      fa.resume_rows = static_cast<const float*>(resume_rows);
       if (wave) {
         fa.a_img = h->w_arm.as<float>();
         fa.pi = h->w_pi.as<float>();
@@ -708,6 +714,8 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
       fa.nobs = (int)h->V;
       fa.zero_init = o.assoc == CV_ASSOC_DECODE ? 1 : 0;
       fa.dp_assoc = o.assoc == CV_ASSOC_DP ? 1 : 0;
+      fa.forced = o.forced;
+      fa.resume_rows = static_cast<const double*>(resume_rows);
       const int spw = cvk::t64_seqs_per_wave(n, h->cus);
       h->last_mt = (t64cp || fa.dp_assoc) ? std::min(spw, 4) : spw;
       if (t64cp) {
@@ -875,7 +883,7 @@ CV_API int32_t cv_device_count(void) {
 CV_API void cv_opts_init(cv_opts* o) {
   if (!o) return;
   std::memset(o, 0, sizeof *o);
-  o->dtype = CV_DTYPE_F32;
+  o->dtype = CV_DTYPE_F64;  // the reference's arithmetic (hmm.rs:10-18)
   o->assoc = CV_ASSOC_VITERBI;
   o->kernel = CV_KERNEL_AUTO;
   o->rescore_f64 = 1;
@@ -1093,10 +1101,20 @@ std::vector<int32_t> conseq_pairs(const std::vector<ConSeq>& cs, const int32_t* 
   return out;
 }
 
+// The constrained decode's arithmetic: the row-A0 association (the terms of csp.hpp are
+// defined on it) in f64 -- the reference's precision, trellis_fwd_f64 -- or f32 (the f32
+// trellis), N <= 256 either way.
+cv_status constrained_dtype_check(const cv_hmm* h, const cv_opts& o) {
+  if (o.assoc != CV_ASSOC_VITERBI)
+    return set_err(CV_EUNSUPPORTED, "constrained decode runs the row-A0 (VITERBI) association");
+  if (o.dtype == CV_DTYPE_F64 && cvk::t64_padded_states(h->N)) return CV_OK;
+  if (o.dtype == CV_DTYPE_F32 && cvk::trellis_padded_states(h->N)) return CV_OK;
+  return set_err(CV_EUNSUPPORTED, "constrained decode needs dtype f32 or f64 and N <= 256 (N=%d)", h->N);
+}
+
 cv_status constrained_validate(cv_hmm* h, int64_t nseq, const int64_t* offsets, const int32_t* obs,
                                const int32_t* component, int32_t ncomp, const cv_opts& o, std::vector<ConSeq>& cs) {
-  if (o.dtype != CV_DTYPE_F32 || o.assoc != CV_ASSOC_VITERBI || !cvk::trellis_padded_states(h->N))
-    return set_err(CV_EUNSUPPORTED, "constrained decode runs on the f32 VITERBI trellis path (N <= 256)");
+  if ((cv_status)constrained_dtype_check(h, o) != CV_OK) return CV_EUNSUPPORTED;
   if (o.forced) return set_err(CV_EINVAL, "opts->forced is set by the constrained decode itself");
   cs.clear();
   if (nseq == 0) return CV_OK;
@@ -1130,11 +1148,13 @@ struct PrefixKeep {
   std::vector<int64_t> seq, t1, row_base;  // per terms slot i
 };
 
-// The resume flow covers N > 64 with NP % 64 == 0 (pair kernel + backtrack_v); its stored rows
-// must fit 4x the workspace cap (32 GiB by default: config 5 needs 8.6 GB).
-bool resume_supported(const cv_hmm* h) {
+// The resume flow covers f32 N > 64 with NP % 64 == 0 (pair kernel + backtrack_v) and every f64
+// N <= 256; its stored rows must fit 4x the workspace cap (32 GiB by default: config 5 needs
+// 8.6 GB of f32 rows; f64 rows are twice that, within the f64 trellis's 40 GiB cap x 4).
+bool resume_supported(const cv_hmm* h, bool f64) {
   const char* e = getenv("CV_NO_RESUME");
   if (e && *e && *e != '0') return false;
+  if (f64) return cvk::t64_padded_states(h->N) != 0;  // trellis_fwd_f64 EXT + prefix_backtrack_f64
   return h->N > 64 && (h->np == 128 || h->np == 192 || h->np == 256);
 }
 
@@ -1166,9 +1186,12 @@ cv_status constrained_partials_locked(cv_hmm* h, int64_t nseq, const int64_t* of
       if (p < 0) return set_err(CV_EINVAL, "component pair (%d,%d) missing from the pair list", c1, c2);
       seg_pair.push_back(p);
     }
-  if ((st = ensure_trellis_tables(h)) != CV_OK) return st;
+  const bool f64 = o.dtype == CV_DTYPE_F64;
+  if (!f64 && (st = ensure_trellis_tables(h)) != CV_OK) return st;
+  if (f64 && (st = ensure_t64_tables(h)) != CV_OK) return st;
   if ((st = ensure_f64_tables(h)) != CV_OK) return st;
-  const int np = h->np;
+  const int np = f64 ? h->np64 : h->np;
+  const size_t rb = f64 ? 8 : 4;  // bytes per term
   hipStream_t stream = o.stream ? (hipStream_t)o.stream : h->stream;
   const int64_t base = offsets[0], total = offsets[nseq];
   // observations on the device: the caller's (device API, validated) or staged here
@@ -1200,43 +1223,32 @@ cv_status constrained_partials_locked(cv_hmm* h, int64_t nseq, const int64_t* of
   }
   const int64_t nslot_max = std::max<int64_t>(nc, std::min<int64_t>(kSegmentSlots, (int64_t)seg_pair.size() * N));
   if ((st = h->cs_ranges.ensure(std::max(rg.size(), (size_t)nslot_max * 2) * 8)) != CV_OK) return st;
-  if ((st = h->cs_delta.ensure((size_t)nc * np * 4)) != CV_OK) return st;
-  if ((st = h->cs_g.ensure((size_t)nc * np * 4)) != CV_OK) return st;
-  if ((st = h->cs_mu.ensure((size_t)nc * np * 4)) != CV_OK) return st;
-  if ((st = h->cs_zero.ensure((size_t)nc * np * 4)) != CV_OK) return st;
+  if ((st = h->cs_delta.ensure((size_t)nc * np * rb)) != CV_OK) return st;
+  if ((st = h->cs_g.ensure((size_t)nc * np * rb)) != CV_OK) return st;
+  if ((st = h->cs_mu.ensure((size_t)nc * np * rb)) != CV_OK) return st;
+  if ((st = h->cs_zero.ensure((size_t)nc * np * rb)) != CV_OK) return st;
   if ((st = h->st_status.ensure((size_t)std::max<int64_t>(nseq, std::max<int64_t>(nslot_max, 2 * nc)))) != CV_OK)
     return st;
   HIP_TRY(hipMemcpyAsync(h->cs_ranges.p, rg.data(), rg.size() * 8, hipMemcpyHostToDevice, stream));
-  HIP_TRY(hipMemsetAsync(h->cs_zero.p, 0, (size_t)nc * np * 4, stream));
-  cvk::TrellisFwdArgs fa{};
-  fa.a_img = h->t_aimg.as<float>();
-  fa.pi = h->t_pi.as<float>();
-  fa.et = h->t_et.as<float>();
-  fa.obs = dobs;
-  fa.status = h->st_status.as<uint8_t>();
-  fa.nobs = (int)h->V;
-  fa.ranges = h->cs_ranges.as<int64_t>();
-  // one launch, longest range first: slots [0, nc) = prefixes, forward -> delta_{t_1};
-  // slots [nc, 2nc) = suffixes, the backward pass = same kernel on a^T with pi = 0,
-  // reversed -> g_{t_m+1}
-  fa.last_row = h->cs_delta.as<float>();
-  fa.split = nc;
-  fa.a_img2 = h->t_aimg_T.as<float>();
-  fa.pi2 = h->t_pi0.as<float>();
-  fa.last_row2 = h->cs_g.as<float>();
-  if (keep && resume_supported(h)) {  // prefix rows stay on the device for the final decode
-    std::vector<int64_t> rb((size_t)nc);
+  HIP_TRY(hipMemsetAsync(h->cs_zero.p, 0, (size_t)nc * np * rb, stream));
+  // prefix rows kept on the device for the resume flow's final decode
+  const uint64_t row_bytes = (uint64_t)np * rb;  // f64: split-plane rows of 2 NP words
+  const int64_t* row_base_d = nullptr;
+  void* rows_d = nullptr;
+  if (keep && resume_supported(h, f64)) {
+    std::vector<int64_t> rbv((size_t)nc);
     int64_t rows = 0;
-    for (int64_t i = 0; i < nc; ++i) rb[(size_t)i] = rows, rows += rg[2 * i + 1] - rg[2 * i];
-    const uint64_t cap = 4 * (o.workspace_bytes ? o.workspace_bytes : kDefaultWorkspace);
-    if ((uint64_t)rows * np * 4 <= cap) {
-      if ((st = h->rs_rows.ensure((size_t)std::max<int64_t>(rows, 1) * np * 4)) != CV_OK) return st;
+    for (int64_t i = 0; i < nc; ++i) rbv[(size_t)i] = rows, rows += rg[2 * i + 1] - rg[2 * i];
+    const uint64_t cap =
+        4 * (o.workspace_bytes ? o.workspace_bytes : f64 ? kDefaultWorkspaceT64 : kDefaultWorkspace);
+    if ((uint64_t)rows * row_bytes <= cap) {
+      if ((st = h->rs_rows.ensure((size_t)std::max<int64_t>(rows, 1) * row_bytes)) != CV_OK) return st;
       if ((st = h->rs_rowbase.ensure((size_t)nc * 8)) != CV_OK) return st;
-      HIP_TRY(hipMemcpyAsync(h->rs_rowbase.p, rb.data(), (size_t)nc * 8, hipMemcpyHostToDevice, stream));
-      fa.delta = h->rs_rows.as<float>();
-      fa.row_base = h->rs_rowbase.as<int64_t>();
+      HIP_TRY(hipMemcpyAsync(h->rs_rowbase.p, rbv.data(), (size_t)nc * 8, hipMemcpyHostToDevice, stream));
+      rows_d = h->rs_rows.p;
+      row_base_d = h->rs_rowbase.as<int64_t>();
       keep->kept = true;
-      keep->row_base = std::move(rb);
+      keep->row_base = std::move(rbv);
       keep->seq.resize((size_t)nc);
       keep->t1.resize((size_t)nc);
       for (int64_t i = 0; i < nc; ++i) {
@@ -1245,43 +1257,124 @@ cv_status constrained_partials_locked(cv_hmm* h, int64_t nseq, const int64_t* of
       }
     }
   }
+  hipError_t err = hipSuccess;
   {
     // longest first, stable: counting sort on the range lengths (a comparison sort of the
-    // 2nc slots cost ~4 ms of host time at config 5 with the GPU idle)
+    // 2nc slots cost ~4 ms of host time at config 5 with the GPU idle).  f32: the 2nc slots in
+    // one launch; f64: prefixes and suffixes in two launches (a wave's S sequences share one
+    // A table), each sorted on its own.
     std::vector<int32_t> so((size_t)2 * nc);
-    int64_t maxlen = 0;
-    for (int64_t x = 0; x < 2 * nc; ++x) maxlen = std::max(maxlen, rg[2 * x + 1] - rg[2 * x]);
-    std::vector<int64_t> pos((size_t)maxlen + 2, 0);
-    for (int64_t x = 0; x < 2 * nc; ++x) ++pos[(size_t)(maxlen - (rg[2 * x + 1] - rg[2 * x])) + 1];
-    for (size_t k = 1; k < pos.size(); ++k) pos[k] += pos[k - 1];
-    for (int64_t x = 0; x < 2 * nc; ++x) so[(size_t)pos[(size_t)(maxlen - (rg[2 * x + 1] - rg[2 * x]))]++] = (int32_t)x;
+    auto sort_slots = [&](int64_t x0, int64_t x1, int32_t* out, int32_t sub) {
+      int64_t maxlen = 0;
+      for (int64_t x = x0; x < x1; ++x) maxlen = std::max(maxlen, rg[2 * x + 1] - rg[2 * x]);
+      std::vector<int64_t> pos((size_t)maxlen + 2, 0);
+      for (int64_t x = x0; x < x1; ++x) ++pos[(size_t)(maxlen - (rg[2 * x + 1] - rg[2 * x])) + 1];
+      for (size_t k = 1; k < pos.size(); ++k) pos[k] += pos[k - 1];
+      for (int64_t x = x0; x < x1; ++x)
+        out[pos[(size_t)(maxlen - (rg[2 * x + 1] - rg[2 * x]))]++] = (int32_t)(x - sub);
+    };
+    if (f64) {
+      sort_slots(0, nc, so.data(), 0);
+      sort_slots(nc, 2 * nc, so.data() + nc, (int32_t)nc);
+    } else {
+      sort_slots(0, 2 * nc, so.data(), 0);
+    }
     if ((st = h->ws_order.ensure(so.size() * 4)) != CV_OK) return st;
     HIP_TRY(hipMemcpyAsync(h->ws_order.p, so.data(), so.size() * 4, hipMemcpyHostToDevice, stream));
-    fa.slot_order = h->ws_order.as<int32_t>();
     HIP_TRY(hipStreamSynchronize(stream));  // `so` is a local buffer
     trace_mark("obs H2D + slot order");
   }
-  hipError_t err = cvk::launch_trellis_fwd(np, fa, 2 * nc, stream);
-  cvk::MaxMarginalArgs ma{};
-  ma.g = h->cs_g.as<float>();
-  ma.ranges_suffix = h->cs_ranges.as<int64_t>() + 2 * nc;
-  ma.at = h->t_at.as<float>();
-  ma.mu = h->cs_mu.as<float>();
-  if (err == hipSuccess) {  // m == 1: mu = delta + beta
-    ma.delta = h->cs_delta.as<float>();
-    err = cvk::launch_max_marginal(np, ma, n1, stream);
+  if (!f64) {
+    cvk::TrellisFwdArgs fa{};
+    fa.a_img = h->t_aimg.as<float>();
+    fa.pi = h->t_pi.as<float>();
+    fa.et = h->t_et.as<float>();
+    fa.obs = dobs;
+    fa.status = h->st_status.as<uint8_t>();
+    fa.nobs = (int)h->V;
+    fa.ranges = h->cs_ranges.as<int64_t>();
+    // one launch, longest range first: slots [0, nc) = prefixes, forward -> delta_{t_1};
+    // slots [nc, 2nc) = suffixes, the backward pass = same kernel on a^T with pi = 0,
+    // reversed -> g_{t_m+1}
+    fa.last_row = h->cs_delta.as<float>();
+    fa.split = nc;
+    fa.a_img2 = h->t_aimg_T.as<float>();
+    fa.pi2 = h->t_pi0.as<float>();
+    fa.last_row2 = h->cs_g.as<float>();
+    fa.delta = static_cast<float*>(rows_d);
+    fa.row_base = row_base_d;
+    fa.slot_order = h->ws_order.as<int32_t>();
+    err = cvk::launch_trellis_fwd(np, fa, 2 * nc, stream);
+    cvk::MaxMarginalArgs ma{};
+    ma.g = h->cs_g.as<float>();
+    ma.ranges_suffix = h->cs_ranges.as<int64_t>() + 2 * nc;
+    ma.at = h->t_at.as<float>();
+    ma.mu = h->cs_mu.as<float>();
+    if (err == hipSuccess) {  // m == 1: mu = delta + beta
+      ma.delta = h->cs_delta.as<float>();
+      err = cvk::launch_max_marginal(np, ma, n1, stream);
+    }
+    if (err == hipSuccess && nc > n1) {  // m >= 2: beta alone (0 + beta is exact)
+      ma.delta = h->cs_zero.as<float>();
+      ma.g += n1 * np;
+      ma.ranges_suffix += 2 * n1;
+      ma.mu += n1 * np;
+      err = cvk::launch_max_marginal(np, ma, nc - n1, stream);
+    }
+  } else {
+    // prefixes: forward on a from each sequence start to t_1 (its last row = delta_{t_1})
+    cvk::T64FwdArgs fa{};
+    fa.a = h->q_a.as<double>();
+    fa.pi = h->q_pi.as<double>();
+    fa.et = h->q_et.as<double>();
+    fa.obs = dobs;
+    fa.status = h->st_status.as<uint8_t>();
+    fa.nobs = (int)h->V;
+    fa.ranges = h->cs_ranges.as<int64_t>();
+    fa.nslots = nc;
+    fa.last_row = h->cs_delta.as<double>();
+    fa.delta = static_cast<double*>(rows_d);
+    fa.row_base = row_base_d;
+    fa.slot_order = h->ws_order.as<int32_t>();
+    err = cvk::launch_t64_fwd(np, cvk::t64_seqs_per_wave(nc, h->cus), fa, nc, stream);
+    // suffixes: the same recurrence on a^T with pi = 0, reversed (its last row = g_{t_m+1})
+    if (err == hipSuccess) {
+      cvk::T64FwdArgs fb = fa;
+      fb.a = h->q_at.as<double>();
+      fb.pi = h->q_pi0.as<double>();
+      fb.ranges = h->cs_ranges.as<int64_t>() + 2 * nc;
+      fb.reverse = 1;
+      fb.last_row = h->cs_g.as<double>();
+      fb.delta = nullptr;
+      fb.row_base = nullptr;
+      fb.slot_order = h->ws_order.as<int32_t>() + nc;
+      err = cvk::launch_t64_fwd(np, cvk::t64_seqs_per_wave(nc, h->cus), fb, nc, stream);
+    }
+    cvk::MaxMarginal64Args ma{};
+    ma.g = h->cs_g.as<double>();
+    ma.ranges_suffix = h->cs_ranges.as<int64_t>() + 2 * nc;
+    ma.at = h->q_at.as<double>();
+    ma.mu = h->cs_mu.as<double>();
+    if (err == hipSuccess) {  // m == 1: mu = delta + beta
+      ma.delta = h->cs_delta.as<double>();
+      err = cvk::launch_t64_max_marginal(np, ma, n1, stream);
+    }
+    if (err == hipSuccess && nc > n1) {  // m >= 2: beta alone (0 + beta is exact)
+      ma.delta = h->cs_zero.as<double>();
+      ma.g += n1 * np;
+      ma.ranges_suffix += 2 * n1;
+      ma.mu += n1 * np;
+      err = cvk::launch_t64_max_marginal(np, ma, nc - n1, stream);
+    }
   }
-  if (err == hipSuccess && nc > n1) {  // m >= 2: beta alone (0 + beta is exact)
-    ma.delta = h->cs_zero.as<float>();
-    ma.g += n1 * np;
-    ma.ranges_suffix += 2 * n1;
-    ma.mu += n1 * np;
-    err = cvk::launch_max_marginal(np, ma, nc - n1, stream);
-  }
-  if (err != hipSuccess) return set_err(CV_EDEVICE, "max-marginal launch failed: %s", hipGetErrorString(err));
+  if (err != hipSuccess) return set_err(CV_EDEVICE, "term launches failed: %s", hipGetErrorString(err));
   trace_mark("term launches enqueued");
   for (int64_t i = 0; i < nc; ++i)
     for (int64_t e : order[i]->elems) part[(int64_t)component[e] * uw + 5 * N] += 1;
+  auto range_err = [] {
+    return set_err(CV_EINVAL, "a constrained-decode term is outside the exact unit's range (|score| >= 2^32): "
+                              "check the model's log-probabilities (null, not a huge negative, for impossible)");
+  };
   // CV_HOST_SUMS=1 takes the host loop (tests compare the two; same integers by construction)
   const char* hs = getenv("CV_HOST_SUMS");
   const bool host_sums = hs && *hs && *hs != '0';
@@ -1294,11 +1387,13 @@ cv_status constrained_partials_locked(cv_hmm* h, int64_t nseq, const int64_t* of
     }
     if ((st = h->cs_comp.ensure(cc.size() * 4)) != CV_OK) return st;
     if ((st = h->cs_words.ensure((size_t)ncomp * uw * 8)) != CV_OK) return st;
+    if ((st = h->cs_flag.ensure(16)) != CV_OK) return st;
     HIP_TRY(hipMemcpyAsync(h->cs_comp.p, cc.data(), cc.size() * 4, hipMemcpyHostToDevice, stream));
     HIP_TRY(hipMemsetAsync(h->cs_words.p, 0, (size_t)ncomp * uw * 8, stream));
+    HIP_TRY(hipMemsetAsync(h->cs_flag.p, 0, 4, stream));
     cvx::UnarySumArgs us{};
-    us.mu = h->cs_mu.as<float>();
-    us.dl = h->cs_delta.as<float>();
+    us.mu = h->cs_mu.p;
+    us.dl = h->cs_delta.p;
     us.c1 = h->cs_comp.as<int32_t>();
     us.cm = h->cs_comp.as<int32_t>() + nc;
     us.nc = nc;
@@ -1306,57 +1401,79 @@ cv_status constrained_partials_locked(cv_hmm* h, int64_t nseq, const int64_t* of
     us.np = np;
     us.nstates = N;
     us.ncomp = ncomp;
+    us.f64 = f64 ? 1 : 0;
     us.uw = uw;
     us.part = h->cs_words.as<long long>();
+    us.bad = h->cs_flag.as<unsigned>();
     const int nblocks = (int)std::max<int64_t>(1, std::min<int64_t>(2 * std::max(h->cus, 1), (nc + 31) / 32));
     const hipError_t e = cvx::launch_unary_sums(us, nblocks, stream);
     if (e != hipSuccess) return set_err(CV_EDEVICE, "unary sum launch failed: %s", hipGetErrorString(e));
     std::vector<int64_t> words((size_t)ncomp * uw);
+    unsigned bad = 0;
     HIP_TRY(hipMemcpyAsync(words.data(), h->cs_words.p, words.size() * 8, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipMemcpyAsync(&bad, h->cs_flag.p, 4, hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipStreamSynchronize(stream));  // `cc` and `words` are local buffers
     trace_mark("terms + exact sums (device)");
+    if (bad) return range_err();
     for (size_t q = 0; q < words.size(); ++q) part[q] += words[q];
   } else {
-  std::vector<float>& dl = h->host_dl;
-  std::vector<float>& mu = h->host_mu;
-  if (dl.size() < (size_t)nc * np) dl.resize((size_t)nc * np);
-  if (mu.size() < (size_t)nc * np) mu.resize((size_t)nc * np);
-  HIP_TRY(hipMemcpyAsync(dl.data(), h->cs_delta.p, (size_t)nc * np * 4, hipMemcpyDeviceToHost, stream));
-  HIP_TRY(hipMemcpyAsync(mu.data(), h->cs_mu.p, (size_t)nc * np * 4, hipMemcpyDeviceToHost, stream));
-  HIP_TRY(hipStreamSynchronize(stream));
-  trace_mark("terms device + D2H");
-  // exact accumulation, parallel over states into worker-local words (the components'
-  // word blocks are not cache-line aligned: writing `part` directly would false-share),
-  // added into `part` at the end (integer sums: order-free)
-  parallel_ranges(N, [&](int, int64_t s0, int64_t s1) {
-    const int64_t ns = s1 - s0;
-    std::vector<int64_t> loc((size_t)ncomp * ns * 5, 0);  // [comp][state][4 limbs], then [comp][state] -inf counts
-    int64_t* lim = loc.data();
-    int64_t* cnt = loc.data() + (size_t)ncomp * ns * 4;
-    for (int64_t i = 0; i < nc; ++i) {
-      const ConSeq& c = *order[i];
-      const int64_t c1 = component[c.elems.front()], cm = component[c.elems.back()];
-      const float* mr = &mu[(size_t)i * np];
-      const float* dr = &dl[(size_t)i * np];
-      for (int64_t s = s0; s < s1; ++s) {
-        const int64_t q1 = c1 * ns + (s - s0), qm = cm * ns + (s - s0);
-        if (i < n1) {
-          cvcsp::add_exact(lim + 4 * q1, cnt + q1, mr[s]);
-        } else {
-          cvcsp::add_exact(lim + 4 * q1, cnt + q1, dr[s]);
-          cvcsp::add_exact(lim + 4 * qm, cnt + qm, mr[s]);
-        }
-      }
+    std::vector<double> dl64, mu64;
+    std::vector<float>& dl = h->host_dl;
+    std::vector<float>& mu = h->host_mu;
+    if (f64) {
+      dl64.resize((size_t)nc * np);
+      mu64.resize((size_t)nc * np);
+    } else {
+      if (dl.size() < (size_t)nc * np) dl.resize((size_t)nc * np);
+      if (mu.size() < (size_t)nc * np) mu.resize((size_t)nc * np);
     }
-    for (int64_t c = 0; c < ncomp; ++c)
-      for (int64_t s = s0; s < s1; ++s) {
-        const int64_t q = c * ns + (s - s0);
-        int64_t* u = part + c * uw;
-        for (int k = 0; k < 4; ++k) u[4 * s + k] += lim[4 * q + k];
-        u[4 * N + s] += cnt[q];
-      }
-  }, 1);
-  trace_mark("exact sums (host)");
+    HIP_TRY(hipMemcpyAsync(f64 ? (void*)dl64.data() : (void*)dl.data(), h->cs_delta.p, (size_t)nc * np * rb,
+                           hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipMemcpyAsync(f64 ? (void*)mu64.data() : (void*)mu.data(), h->cs_mu.p, (size_t)nc * np * rb,
+                           hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipStreamSynchronize(stream));
+    trace_mark("terms device + D2H");
+    // exact accumulation, parallel over states into worker-local words (the components'
+    // word blocks are not cache-line aligned: writing `part` directly would false-share),
+    // added into `part` at the end (integer sums: order-free)
+    std::vector<uint8_t> badw((size_t)host_threads() + 1, 0);
+    parallel_ranges(N, [&](int t, int64_t s0, int64_t s1) {
+      const int64_t ns = s1 - s0;
+      std::vector<int64_t> loc((size_t)ncomp * ns * 5, 0);  // [comp][state][4 limbs], then [comp][state] -inf counts
+      int64_t* lim = loc.data();
+      int64_t* cnt = loc.data() + (size_t)ncomp * ns * 4;
+      bool ok = true;
+      auto run = [&](const auto* mrow, const auto* drow) {
+        for (int64_t i = 0; i < nc; ++i) {
+          const ConSeq& c = *order[i];
+          const int64_t c1 = component[c.elems.front()], cm = component[c.elems.back()];
+          const auto* mr = mrow + (size_t)i * np;
+          const auto* dr = drow + (size_t)i * np;
+          for (int64_t s = s0; s < s1; ++s) {
+            const int64_t q1 = c1 * ns + (s - s0), qm = cm * ns + (s - s0);
+            if (i < n1) {
+              ok &= cvcsp::add_exact(lim + 4 * q1, cnt + q1, mr[s]);
+            } else {
+              ok &= cvcsp::add_exact(lim + 4 * q1, cnt + q1, dr[s]);
+              ok &= cvcsp::add_exact(lim + 4 * qm, cnt + qm, mr[s]);
+            }
+          }
+        }
+      };
+      if (f64) run(mu64.data(), dl64.data());
+      else run(mu.data(), dl.data());
+      if (!ok) badw[(size_t)t] = 1;
+      for (int64_t c = 0; c < ncomp; ++c)
+        for (int64_t s = s0; s < s1; ++s) {
+          const int64_t q = c * ns + (s - s0);
+          int64_t* u = part + c * uw;
+          for (int k = 0; k < 4; ++k) u[4 * s + k] += lim[4 * q + k];
+          u[4 * N + s] += cnt[q];
+        }
+    }, 1);
+    trace_mark("exact sums (host)");
+    for (uint8_t b : badw)
+      if (b) return range_err();
   }
   // ---- segment tables: one slot per (segment, start state), in batches ----
   struct Seg { int64_t e0, e1; int32_t c1, c2; int64_t p; };
@@ -1373,6 +1490,8 @@ cv_status constrained_partials_locked(cv_hmm* h, int64_t nseq, const int64_t* of
   std::vector<int64_t> srg;
   std::vector<int32_t> sst;
   std::vector<float> rows;
+  std::vector<double> rows64;
+  bool ok = true;
   for (int64_t b0 = 0; b0 < nslots; b0 += kSegmentSlots) {
     const int64_t nb = std::min(kSegmentSlots, nslots - b0);
     srg.resize((size_t)nb * 2);
@@ -1386,39 +1505,62 @@ cv_status constrained_partials_locked(cv_hmm* h, int64_t nseq, const int64_t* of
     if ((st = h->cs_start.ensure((size_t)nb * 4)) != CV_OK) return st;
     HIP_TRY(hipMemcpyAsync(h->cs_ranges.p, srg.data(), srg.size() * 8, hipMemcpyHostToDevice, stream));
     HIP_TRY(hipMemcpyAsync(h->cs_start.p, sst.data(), sst.size() * 4, hipMemcpyHostToDevice, stream));
-    cvk::TrellisFwdArgs sa{};
-    sa.a_img = h->t_aimg.as<float>();
-    sa.pi = h->t_pi.as<float>();
-    sa.et = h->t_et.as<float>();
-    sa.obs = dobs;
-    sa.status = h->st_status.as<uint8_t>();
-    sa.nobs = (int)h->V;
-    sa.ranges = h->cs_ranges.as<int64_t>();
-    sa.start = h->cs_start.as<int32_t>();
-    if ((st = h->cs_seg.ensure((size_t)nb * np * 4)) != CV_OK) return st;
-    sa.last_row = h->cs_seg.as<float>();
-    if ((err = cvk::launch_trellis_fwd(np, sa, nb, stream)) != hipSuccess)
-      return set_err(CV_EDEVICE, "segment-table launch failed: %s", hipGetErrorString(err));
-    rows.resize((size_t)nb * np);
-    HIP_TRY(hipMemcpyAsync(rows.data(), h->cs_seg.p, rows.size() * 4, hipMemcpyDeviceToHost, stream));
-    HIP_TRY(hipStreamSynchronize(stream));
-    for (int64_t k = 0; k < nb; ++k) {
-      const Seg& sg = segs[(b0 + k) / N];
-      const int s = (int)((b0 + k) % N);
-      const float* r = &rows[(size_t)k * np];
-      if (sg.p < 0) {  // same component at both ends: only the diagonal is consistent
-        int64_t* u = part + (int64_t)sg.c1 * uw;
-        cvcsp::add_exact(u + 4 * s, u + 4 * N + s, r[s]);
-        continue;
-      }
-      int64_t* pp = pbase + sg.p * pw;
-      if (s == 0) pp[5 * (int64_t)N * N] += 1;
-      for (int s2 = 0; s2 < N; ++s2) {
-        const int64_t e = sg.c1 < sg.c2 ? (int64_t)s * N + s2 : (int64_t)s2 * N + s;
-        cvcsp::add_exact(pp + 4 * e, pp + 4 * (int64_t)N * N + e, r[s2]);
-      }
+    if ((st = h->cs_seg.ensure((size_t)nb * np * rb)) != CV_OK) return st;
+    if (!f64) {
+      cvk::TrellisFwdArgs sa{};
+      sa.a_img = h->t_aimg.as<float>();
+      sa.pi = h->t_pi.as<float>();
+      sa.et = h->t_et.as<float>();
+      sa.obs = dobs;
+      sa.status = h->st_status.as<uint8_t>();
+      sa.nobs = (int)h->V;
+      sa.ranges = h->cs_ranges.as<int64_t>();
+      sa.start = h->cs_start.as<int32_t>();
+      sa.last_row = h->cs_seg.as<float>();
+      err = cvk::launch_trellis_fwd(np, sa, nb, stream);
+    } else {
+      // the N slots of a segment share its range: a wave's S sequences run equal lengths
+      cvk::T64FwdArgs sa{};
+      sa.a = h->q_a.as<double>();
+      sa.pi = h->q_pi.as<double>();
+      sa.et = h->q_et.as<double>();
+      sa.obs = dobs;
+      sa.status = h->st_status.as<uint8_t>();
+      sa.nobs = (int)h->V;
+      sa.ranges = h->cs_ranges.as<int64_t>();
+      sa.nslots = nb;
+      sa.start = h->cs_start.as<int32_t>();
+      sa.last_row = h->cs_seg.as<double>();
+      err = cvk::launch_t64_fwd(np, cvk::t64_seqs_per_wave(nb, h->cus), sa, nb, stream);
     }
+    if (err != hipSuccess) return set_err(CV_EDEVICE, "segment-table launch failed: %s", hipGetErrorString(err));
+    if (f64) rows64.resize((size_t)nb * np);
+    else rows.resize((size_t)nb * np);
+    HIP_TRY(hipMemcpyAsync(f64 ? (void*)rows64.data() : (void*)rows.data(), h->cs_seg.p, (size_t)nb * np * rb,
+                           hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipStreamSynchronize(stream));
+    auto acc = [&](const auto* all) {
+      for (int64_t k = 0; k < nb; ++k) {
+        const Seg& sg = segs[(b0 + k) / N];
+        const int s = (int)((b0 + k) % N);
+        const auto* r = all + (size_t)k * np;
+        if (sg.p < 0) {  // same component at both ends: only the diagonal is consistent
+          int64_t* u = part + (int64_t)sg.c1 * uw;
+          ok &= cvcsp::add_exact(u + 4 * s, u + 4 * N + s, r[s]);
+          continue;
+        }
+        int64_t* pp = pbase + sg.p * pw;
+        if (s == 0) pp[5 * (int64_t)N * N] += 1;
+        for (int s2 = 0; s2 < N; ++s2) {
+          const int64_t e = sg.c1 < sg.c2 ? (int64_t)s * N + s2 : (int64_t)s2 * N + s;
+          ok &= cvcsp::add_exact(pp + 4 * e, pp + 4 * (int64_t)N * N + e, r[s2]);
+        }
+      }
+    };
+    if (f64) acc(rows64.data());
+    else acc(rows.data());
   }
+  if (!ok) return range_err();
   return CV_OK;
 }
 
@@ -1506,7 +1648,9 @@ cv_status forced_decode_resume(cv_hmm* h, int64_t nseq, const int64_t* offsets_h
   cv_status st;
   if ((st = stage_forced_locked(h, offsets_host, nseq, component, comp_state, cs, stream)) != CV_OK) return st;
   const int64_t nc = (int64_t)keep.seq.size();
-  const int np = h->np;
+  const bool f64 = o.dtype == CV_DTYPE_F64;
+  const int np = f64 ? h->np64 : h->np;
+  const size_t rb = f64 ? 8 : 4;
   std::vector<int64_t> start(offsets_host, offsets_host + nseq);
   std::vector<int32_t> ridx((size_t)nseq, -1), state((size_t)nc);
   for (int64_t i = 0; i < nc; ++i) {
@@ -1546,7 +1690,7 @@ cv_status forced_decode_resume(cv_hmm* h, int64_t nseq, const int64_t* offsets_h
   if ((st = h->rs_ridx.ensure((size_t)nseq * 4)) != CV_OK) return st;
   if ((st = h->rs_off2.ensure((size_t)nseq * 9)) != CV_OK) return st;  // score2 f64 + status2 u8
   if ((st = h->rs_slot.ensure((size_t)std::max<int64_t>(nc, 1) * 28)) != CV_OK) return st;
-  if ((st = h->rs_resume.ensure((size_t)std::max<int64_t>(nc, 1) * np * 4)) != CV_OK) return st;
+  if ((st = h->rs_resume.ensure((size_t)std::max<int64_t>(nc, 1) * np * rb)) != CV_OK) return st;
   if ((st = h->rs_obs2.ensure((size_t)std::max<int64_t>(total2, 1) * 4)) != CV_OK) return st;
   if ((st = h->rs_frc2.ensure((size_t)std::max<int64_t>(total2, 1) * 4)) != CV_OK) return st;
   if ((st = h->rs_path2.ensure((size_t)std::max<int64_t>(total2, 1) * 4)) != CV_OK) return st;
@@ -1563,7 +1707,10 @@ cv_status forced_decode_resume(cv_hmm* h, int64_t nseq, const int64_t* offsets_h
   HIP_TRY(hipMemcpyAsync(h->rs_ridx.p, cridx.data(), (size_t)nseq * 4, hipMemcpyHostToDevice, stream));
   HIP_TRY(hipMemcpyAsync(slot_d, slot64.data(), (size_t)nc * 24, hipMemcpyHostToDevice, stream));
   HIP_TRY(hipMemcpyAsync(state_d, state.data(), (size_t)nc * 4, hipMemcpyHostToDevice, stream));
-  hipError_t err = cvk::launch_resume_rows(h->cs_delta.as<float>(), state_d, nc, np, h->rs_resume.as<float>(), stream);
+  hipError_t err = f64 ? cvk::launch_t64_resume_rows(h->cs_delta.as<double>(), state_d, nc, np,
+                                                     h->rs_resume.as<double>(), stream)
+                       : cvk::launch_resume_rows(h->cs_delta.as<float>(), state_d, nc, np, h->rs_resume.as<float>(),
+                                                 stream);
   if (err == hipSuccess)
     err = cvk::launch_compact_suffix(cstart_d, off2_d, obs_dev, h->st_forced.as<int32_t>(), h->rs_ridx.as<int32_t>(),
                                      h->rs_obs2.as<int32_t>(), h->rs_frc2.as<int32_t>(), nseq, stream);
@@ -1580,26 +1727,45 @@ cv_status forced_decode_resume(cv_hmm* h, int64_t nseq, const int64_t* offsets_h
   pa.at = h->t_at.as<float>();
   pa.status = status_dev;
   pa.path = path_dev;
-  HIP_TRY(hipEventRecord(h->rs_ev, stream));
-  HIP_TRY(hipStreamWaitEvent(h->bt_stream, h->rs_ev, 0));
-  err = cvk::launch_prefix_backtrack(np, pa, nc, h->bt_stream, 100 * 1024);
-  if (err != hipSuccess) return set_err(CV_EDEVICE, "prefix backtrack failed: %s", hipGetErrorString(err));
-  HIP_TRY(hipEventRecord(h->rs_ev, h->bt_stream));
+  if (!f64) {
+    HIP_TRY(hipEventRecord(h->rs_ev, stream));
+    HIP_TRY(hipStreamWaitEvent(h->bt_stream, h->rs_ev, 0));
+    err = cvk::launch_prefix_backtrack(np, pa, nc, h->bt_stream, 100 * 1024);
+    if (err != hipSuccess) return set_err(CV_EDEVICE, "prefix backtrack failed: %s", hipGetErrorString(err));
+    HIP_TRY(hipEventRecord(h->rs_ev, h->bt_stream));
+  }
   trace_mark("resume: compact suffix batch");
   cv_opts o2 = o;
   o2.forced = h->rs_frc2.as<int32_t>();
-  o2.rescore_f64 = 0;  // re-scored below over the whole sequences
+  o2.rescore_f64 = 0;  // f32: re-scored below over the whole sequences; f64: the score is exact
   if ((st = decode_device(h, nseq, off2, off2_d, h->rs_obs2.as<int32_t>(), o2, h->rs_path2.as<int32_t>(), score2,
-                          status2, stream, h->rs_resume.as<float>())) != CV_OK) {
+                          status2, stream, h->rs_resume.p)) != CV_OK) {
     (void)hipStreamSynchronize(stream);
     (void)hipStreamSynchronize(h->bt_stream);
     return st;
   }
-  HIP_TRY(hipStreamWaitEvent(stream, h->rs_ev, 0));  // prefix paths written
+  if (f64) {
+    // f64: the prefix backtrack runs after the suffix decode on the same stream (a co-running
+    // backtrack slowed the 2-wave f64 forward more than it hid, profiles/r02_bench_c4_f64_overlap.log)
+    cvk::PrefixBt64Args p64{};
+    p64.rows = h->rs_rows.as<double>();
+    p64.seq = slot_d;
+    p64.t1 = slot_d + nc;
+    p64.row_base = slot_d + 2 * nc;
+    p64.state = state_d;
+    p64.offsets = offsets_dev;
+    p64.at = h->q_at.as<double>();
+    p64.nstates = h->N;
+    p64.path = path_dev;
+    err = cvk::launch_t64_prefix_bt(np, p64, nc, stream);
+    if (err != hipSuccess) return set_err(CV_EDEVICE, "prefix backtrack failed: %s", hipGetErrorString(err));
+  } else {
+    HIP_TRY(hipStreamWaitEvent(stream, h->rs_ev, 0));  // prefix paths written
+  }
   err = cvk::launch_scatter_suffix(cstart_d, off2_d, cperm_d, h->rs_path2.as<int32_t>(), score2, status2, path_dev,
                                    score_dev, status_dev, nseq, stream);
   if (err == hipSuccess) err = cvk::launch_zero_infeasible_prefix(pa, nc, stream);
-  if (err == hipSuccess && o.rescore_f64) {
+  if (err == hipSuccess && o.rescore_f64 && !f64) {
     cvk::RescoreArgs ra{};
     ra.path = path_dev;
     ra.obs = obs_dev;
@@ -1805,8 +1971,7 @@ CV_API cv_status cv_decode_constrained_device(cv_hmm* h, int64_t nseq, const int
   cv_opts o = opts ? *opts : default_opts();
   for (int32_t c = 0; c < ncomp; ++c) comp_state_out[c] = -1;
   if (objective_out) *objective_out = 0.0;
-  if (o.dtype != CV_DTYPE_F32 || o.assoc != CV_ASSOC_VITERBI || !cvk::trellis_padded_states(h->N))
-    return set_err(CV_EUNSUPPORTED, "constrained decode runs on the f32 VITERBI trellis path (N <= 256)");
+  if (constrained_dtype_check(h, o) != CV_OK) return CV_EUNSUPPORTED;
   if (o.forced) return set_err(CV_EINVAL, "opts->forced is set by the constrained decode itself");
   if (nseq == 0) return CV_OK;
   if ((st = check_batch(h, nseq, offsets_host)) != CV_OK) return st;
@@ -2019,8 +2184,12 @@ CV_API cv_status cv_solver_create(const char* kind, cv_hmm* h, const cv_superseq
 CV_API cv_status cv_solver_solve(cv_solver* s) {
   if (!s) return set_err(CV_EINVAL, "null solver");
   if (s->constrained) {
-    if (s->kind != "gpu")
-      return set_err(CV_EUNSUPPORTED, "constrained decode runs on the f32 trellis path (solver kind \"gpu\")");
+    // every kind: the consistency-constrained decode on the row-A0 association (the terms of
+    // csp.hpp are defined on it) at the kind's precision -- f64 for gpu-f64 / gpu-cp / gpu-dp
+    // (the reference's arithmetic, cp.rs:95-126 / dp.rs:147-166 in f64), f32 for "gpu"
+    cv_opts co = s->opts;
+    co.assoc = CV_ASSOC_VITERBI;
+    co.rescore_f64 = co.dtype == CV_DTYPE_F32 ? 1 : 0;
     const int64_t total = s->offsets.back();
     s->solution.assign((size_t)total, 0);
     s->scores.assign((size_t)s->nseq, 0.0);
@@ -2028,7 +2197,7 @@ CV_API cv_status cv_solver_solve(cv_solver* s) {
     std::vector<int32_t> states((size_t)s->ncomp, -1);
     double obj = 0;
     cv_status st = cv_decode_constrained(s->hmm, s->nseq, s->offsets.data(), s->obs.data(), s->comp.data(), s->ncomp,
-                                         &s->opts, s->solution.data(), s->scores.data(), s->status.data(),
+                                         &co, s->solution.data(), s->scores.data(), s->status.data(),
                                          states.data(), &obj);
     if (st != CV_OK) return st;
     s->objective = obj;

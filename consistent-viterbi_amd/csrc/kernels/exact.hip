@@ -6,7 +6,8 @@
 // in 4 limbs (exact_fixed.h), to its component's words: one thread per state accumulates a
 // block's share of the sequences in LDS (thread-private columns, no atomics), then adds its
 // words into the output with 64-bit atomics.  Integer sums: the result is the same words as
-// the host loop, in any order.
+// the host loop, in any order.  f32 (the f32 trellis) or f64 (the exact-f64 trellis) terms; a
+// term outside the exact unit's range (|x| >= 2^32) sets *bad instead of being added.
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
@@ -16,6 +17,7 @@
 
 namespace cvx {
 
+template <typename REAL>
 __global__ __launch_bounds__(256) void unary_sums(UnarySumArgs g) {
   extern __shared__ long long acc[];  // [ncomp][5][256]: 4 limbs + the -inf count, state-minor
   const int s = threadIdx.x;
@@ -23,10 +25,17 @@ __global__ __launch_bounds__(256) void unary_sums(UnarySumArgs g) {
   for (int q = 0; q < ncomp * 5; ++q) acc[q * 256 + s] = 0;
   const int64_t per = (g.nc + gridDim.x - 1) / gridDim.x;
   const int64_t i0 = (int64_t)blockIdx.x * per, i1 = min(g.nc, i0 + per);
-  auto add = [&](int c, float x) {
+  const REAL* mu = static_cast<const REAL*>(g.mu);
+  const REAL* dl = static_cast<const REAL*>(g.dl);
+  bool bad = false;
+  auto add = [&](int c, REAL x) {
     long long* a = acc + (size_t)c * 5 * 256 + s;
     if (!(x > -INFINITY)) {
       a[4 * 256] += 1;
+      return;
+    }
+    if (!term_in_range((double)x)) {  // outside the exact unit: the host reports CV_EINVAL
+      bad = true;
       return;
     }
     int64_t l[4];
@@ -36,11 +45,11 @@ __global__ __launch_bounds__(256) void unary_sums(UnarySumArgs g) {
   };
   if (s < g.nstates) {
     for (int64_t i = i0; i < i1; ++i) {
-      const float m = g.mu[(size_t)i * g.np + s];
+      const REAL m = mu[(size_t)i * g.np + s];
       if (i < g.n1) {
         add(g.c1[i], m);
       } else {
-        add(g.c1[i], g.dl[(size_t)i * g.np + s]);
+        add(g.c1[i], dl[(size_t)i * g.np + s]);
         add(g.cm[i], m);
       }
     }
@@ -53,16 +62,20 @@ __global__ __launch_bounds__(256) void unary_sums(UnarySumArgs g) {
       if (a[4 * 256]) atomicAdd(u + 4 * (size_t)g.nstates + s, (unsigned long long)a[4 * 256]);
     }
   }
+  if (bad) atomicOr(g.bad, 1u);
 }
 
 hipError_t launch_unary_sums(const UnarySumArgs& g, int nblocks, hipStream_t stream) {
   if (g.nc <= 0) return hipSuccess;
-  if (g.ncomp > kUnarySumMaxComp || g.nstates > 256) return hipErrorInvalidValue;
+  if (g.ncomp > kUnarySumMaxComp || g.nstates > 256 || !g.bad) return hipErrorInvalidValue;
   const size_t lds = (size_t)g.ncomp * 5 * 256 * sizeof(long long);
-  if (lds > 64 * 1024)
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&unary_sums), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)lds);
-  hipLaunchKernelGGL(unary_sums, dim3((unsigned)nblocks), dim3(256), lds, stream, g);
+  const void* fn = g.f64 ? reinterpret_cast<const void*>(&unary_sums<double>)
+                         : reinterpret_cast<const void*>(&unary_sums<float>);
+  if (lds > 64 * 1024) (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (g.f64)
+    hipLaunchKernelGGL(unary_sums<double>, dim3((unsigned)nblocks), dim3(256), lds, stream, g);
+  else
+    hipLaunchKernelGGL(unary_sums<float>, dim3((unsigned)nblocks), dim3(256), lds, stream, g);
   return hipGetLastError();
 }
 

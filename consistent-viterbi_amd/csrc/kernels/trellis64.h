@@ -52,6 +52,37 @@ struct T64BtArgs {
   const double* et;
 };
 
+// Delta rows of the f64 trellis (forward -> backtrack, resume-flow prefix rows) use a
+// SPLIT-PLANE layout: row r = 2*NP u32 words, [0, NP) the high words of the NP f64 values and
+// [NP, 2 NP) their low words (8*NP bytes per row, like a plain f64 row).  The backtrack reads
+// the high plane only (a 20-bit-mantissa truncation with a rigorous error bound) and the low
+// plane only on near ties.
+
+struct PrefixBt64Args {
+  const double* rows;       // compact split-plane prefix rows (the terms pass's prefix launch)
+  const int64_t* row_base;  // [n] first row of slot i
+  const int64_t* seq;       // [n] sequence id of slot i
+  const int64_t* t1;        // [n] element index of the first constrained element
+  const int32_t* state;     // [n] state forced there
+  const int64_t* offsets;   // original CSR offsets
+  const double* at;         // [NP][NP] a^T (t64 tables)
+  int nstates;
+  int32_t* path;
+};
+hipError_t launch_t64_prefix_bt(int np, const PrefixBt64Args& a, int64_t n, hipStream_t stream);
+
+struct MaxMarginal64Args {
+  const double* delta;          // [ncon][NP] forward row at the constrained position
+  const double* g;              // [ncon][NP] last row of the reversed suffix pass
+  const int64_t* ranges_suffix; // [ncon][2] suffix element range (empty -> beta = 0)
+  const double* at;             // [NP][NP] at[j*NP + i] = a[i][j]
+  double* mu;                   // [ncon][NP]
+};
+hipError_t launch_t64_max_marginal(int np, const MaxMarginal64Args& a, int64_t ncon, hipStream_t stream);
+// out[i][j] = j == state[i] ? last[i][j] : -inf (row t_1 of constrained sequence i, forced)
+hipError_t launch_t64_resume_rows(const double* last, const int32_t* state, int64_t n, int np, double* out,
+                                  hipStream_t stream);
+
 // NP = 64 * ceil(N / 64) for 1 <= N <= 256, else 0 (no f64 trellis kernel)
 int t64_padded_states(int n);
 // sequences per forward wave (2, 4 or 8) for a launch of nseq sequences on `cus` CUs

@@ -532,6 +532,22 @@ __device__ __forceinline__ double wave_max_d(double v) {
   return v;
 }
 
+// first index of the wave-wide maximum of s (candidate i = lane + 64k; invalid k excluded)
+template <int KP>
+__device__ __forceinline__ int first_argmax_d(const double (&s)[KP], const bool (&valid)[KP], double& M) {
+  double m = s[0];
+#pragma unroll
+  for (int k = 1; k < KP; ++k) m = fmax(m, s[k]);
+  M = wave_max_d(m);
+  int idx = 0;
+#pragma unroll
+  for (int k = KP - 1; k >= 0; --k) {
+    const unsigned long long mask = __ballot(valid[k] && s[k] == M);
+    if (mask) idx = 64 * k + __builtin_ctzll(mask);
+  }
+  return idx;
+}
+
 // PF: rows in flight per wave (hi planes, 1 KiB each at NP = 256); at NP >= 192 occupancy
 // hides the HBM latency better than a deeper ring (profiles/r01_t64_bt_pf.txt, 2-KiB rows).
 //
@@ -543,25 +559,14 @@ __device__ __forceinline__ double wave_max_d(double v) {
 // first -- argmax of the exact f64 sums; otherwise (near ties, ~1% of steps at config 4) the
 // LO words of that row are read too and the exact sums decide with the first-index rule.
 // Half the HBM bytes of a full-row backtrack, same path bit for bit.
+// One backtrack chain: path[T-1] = cur, then for t = T-1..1 the first argmax of
+// d_{t-1}[i] + a[i, path[t]] (DPSolver: (a[i, path[t]] + b[path[t], o_t]) + d_{t-1}[i])
+// through the split-plane rows rows[0 .. T-1] (row t = element t of the chain).
 template <int KP, int PF>
-__global__ __launch_bounds__(256) void backtrack_f64(T64BtArgs g) {
+__device__ __forceinline__ void bt_chain_f64(const uint32_t* __restrict__ rows, int T, int cur, int32_t* __restrict__ path,
+                                             const double* __restrict__ at, const double* __restrict__ et,
+                                             const int32_t* __restrict__ obs, int dp_assoc, int N, int lane) {
   constexpr int NP = 64 * KP;
-  const int lane = threadIdx.x & 63;
-  const int64_t slot = g.seq_begin + (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (slot >= g.seq_end) return;
-  const int64_t seq = g.order ? (int64_t)g.order[slot] : slot;
-  const int64_t e0 = g.offsets[seq];
-  const int T = (int)(g.offsets[seq + 1] - e0);
-  const int N = g.nstates;
-  if (T <= 0) {
-    if (lane == 0) {
-      g.score[seq] = 0.0;
-      g.status[seq] = CVK_SEQ_EMPTY;
-    }
-    return;
-  }
-  int32_t* __restrict__ path = g.path + e0;
-  const uint32_t* __restrict__ rows = reinterpret_cast<const uint32_t*>(g.delta) + (e0 - g.delta_elem_base) * (2 * NP);
   constexpr uint32_t NINF_HI = 0xFFF00000u;  // hi word of -inf (lo word 0)
   bool valid[KP];
 #pragma unroll
@@ -576,39 +581,6 @@ __global__ __launch_bounds__(256) void backtrack_f64(T64BtArgs g) {
     for (int k = 0; k < KP; ++k)
       dst[k] = (r >= 0 && valid[k]) ? __builtin_nontemporal_load(rows + (size_t)r * (2 * NP) + NP + lane + 64 * k) : 0u;
   };
-  auto first_argmax = [&](const double (&s)[KP], double& M) {
-    double m = s[0];
-#pragma unroll
-    for (int k = 1; k < KP; ++k) m = fmax(m, s[k]);
-    M = wave_max_d(m);
-    int idx = 0;
-#pragma unroll
-    for (int k = KP - 1; k >= 0; --k) {
-      const unsigned long long mask = __ballot(valid[k] && s[k] == M);
-      if (mask) idx = 64 * k + __builtin_ctzll(mask);
-    }
-    return idx;
-  };
-  double bv;
-  int cur;
-  {
-    uint32_t hw[KP], lw[KP];
-    load_hi(T - 1, hw);
-    load_lo(T - 1, lw);
-    double last[KP];
-#pragma unroll
-    for (int k = 0; k < KP; ++k) last[k] = valid[k] ? from_words(hw[k], lw[k]) : ninf_d();
-    cur = first_argmax(last, bv);  // cp.rs:86
-  }
-  const uint8_t prior = g.status[seq];
-  if (!(bv > ninf_d()) || prior == CVK_SEQ_BADOBS) {
-    for (int t = lane; t < T; t += 64) path[t] = 0;
-    if (lane == 0) {
-      g.score[seq] = ninf_d();
-      g.status[seq] = prior == CVK_SEQ_BADOBS ? CVK_SEQ_BADOBS : CVK_SEQ_INFEASIBLE;
-    }
-    return;
-  }
   int pathreg = 0;
   if (lane == ((T - 1) & 63)) pathreg = cur;
   if (((T - 1) & 63) == 0 && lane == 0) path[T - 1] = cur;
@@ -620,19 +592,19 @@ __global__ __launch_bounds__(256) void backtrack_f64(T64BtArgs g) {
     for (int u = 0; u < PF; ++u) {
       const int t = base - u;
       if (t >= 1) {
-        const double* acol = g.at + (size_t)cur * NP + lane;
+        const double* acol = at + (size_t)cur * NP + lane;
         double e = 0.0;
-        if (g.dp_assoc) e = g.et[(size_t)g.obs[e0 + t] * NP + cur];
+        if (dp_assoc) e = et[(size_t)obs[t] * NP + cur];
         double av[KP];
 #pragma unroll
-        for (int k = 0; k < KP; ++k) av[k] = g.dp_assoc ? acol[64 * k] + e : acol[64 * k];
-        // candidates from the truncated values: s~ = a + h (DPSolver: (a + b) + h)
+        for (int k = 0; k < KP; ++k) av[k] = dp_assoc ? acol[64 * k] + e : acol[64 * k];
+        // candidates from the truncated values: s~ = h + a (DPSolver: (a + b) + h)
         double st[KP], up[KP];
         double lmax = ninf_d();
 #pragma unroll
         for (int k = 0; k < KP; ++k) {
           const double h = from_words(ring[u][k], 0u);
-          const double x = valid[k] ? (g.dp_assoc ? av[k] + h : h + av[k]) : ninf_d();
+          const double x = valid[k] ? (dp_assoc ? av[k] + h : h + av[k]) : ninf_d();
           const bool fin = x > ninf_d();
           // |d - h| < |h| 2^-20, plus one f64 rounding of the add (< |x| 2^-52; 2^-51 kept),
           // plus an absolute floor for subnormal truncations
@@ -658,10 +630,10 @@ __global__ __launch_bounds__(256) void backtrack_f64(T64BtArgs g) {
 #pragma unroll
           for (int k = 0; k < KP; ++k) {
             const double d = from_words(ring[u][k], lw[k]);
-            s[k] = valid[k] ? (g.dp_assoc ? av[k] + d : d + av[k]) : ninf_d();
+            s[k] = valid[k] ? (dp_assoc ? av[k] + d : d + av[k]) : ninf_d();
           }
           double M;
-          cur = first_argmax(s, M);
+          cur = first_argmax_d<KP>(s, valid, M);
         }
         const int tp = t - 1;
         if (lane == (tp & 63)) pathreg = cur;
@@ -671,10 +643,99 @@ __global__ __launch_bounds__(256) void backtrack_f64(T64BtArgs g) {
 #pragma unroll
     for (int u = 0; u < PF; ++u) load_hi(base - PF - 1 - u, ring[u]);
   }
+}
+
+template <int KP, int PF>
+__global__ __launch_bounds__(256) void backtrack_f64(T64BtArgs g) {
+  constexpr int NP = 64 * KP;
+  const int lane = threadIdx.x & 63;
+  const int64_t slot = g.seq_begin + (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (slot >= g.seq_end) return;
+  const int64_t seq = g.order ? (int64_t)g.order[slot] : slot;
+  const int64_t e0 = g.offsets[seq];
+  const int T = (int)(g.offsets[seq + 1] - e0);
+  const int N = g.nstates;
+  if (T <= 0) {
+    if (lane == 0) {
+      g.score[seq] = 0.0;
+      g.status[seq] = CVK_SEQ_EMPTY;
+    }
+    return;
+  }
+  int32_t* __restrict__ path = g.path + e0;
+  const uint32_t* __restrict__ rows = reinterpret_cast<const uint32_t*>(g.delta) + (e0 - g.delta_elem_base) * (2 * NP);
+  bool valid[KP];
+#pragma unroll
+  for (int k = 0; k < KP; ++k) valid[k] = (lane + 64 * k) < N;
+  double bv;
+  int cur;
+  {
+    double last[KP];
+#pragma unroll
+    for (int k = 0; k < KP; ++k) {
+      const size_t q = (size_t)(T - 1) * (2 * NP) + lane + 64 * k;
+      last[k] = valid[k] ? from_words(__builtin_nontemporal_load(rows + q), __builtin_nontemporal_load(rows + q + NP))
+                         : ninf_d();
+    }
+    cur = first_argmax_d<KP>(last, valid, bv);  // cp.rs:86
+  }
+  const uint8_t prior = g.status[seq];
+  if (!(bv > ninf_d()) || prior == CVK_SEQ_BADOBS) {
+    for (int t = lane; t < T; t += 64) path[t] = 0;
+    if (lane == 0) {
+      g.score[seq] = ninf_d();
+      g.status[seq] = prior == CVK_SEQ_BADOBS ? CVK_SEQ_BADOBS : CVK_SEQ_INFEASIBLE;
+    }
+    return;
+  }
+  bt_chain_f64<KP, PF>(rows, T, cur, path, g.at, g.et, g.obs + e0, g.dp_assoc, N, lane);
   if (lane == 0) {
     g.score[seq] = bv;
     g.status[seq] = CVK_SEQ_OK;
   }
+}
+
+// Resume flow (f64): the prefix [offsets[seq], t1] of every constrained sequence backtracked
+// from its forced state through the rows the terms pass stored (split-plane, compact per slot).
+template <int KP>
+__global__ __launch_bounds__(256) void prefix_backtrack_f64(PrefixBt64Args a, int64_t n) {
+  const int lane = threadIdx.x & 63;
+  const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= n) return;
+  const int64_t seq = a.seq[i];
+  const int64_t e0 = a.offsets[seq];
+  const int T = (int)(a.t1[i] - e0 + 1);
+  constexpr int NP = 64 * KP;
+  // an infeasible forced row backtracks garbage: zero_infeasible_prefix overwrites it once the
+  // suffix decode has told which sequences are infeasible
+  bt_chain_f64<KP, 2>(reinterpret_cast<const uint32_t*>(a.rows) + a.row_base[i] * (2 * NP), T, a.state[i],
+                      a.path + e0, a.at, nullptr, nullptr, 0, a.nstates, lane);
+}
+
+// Max-marginal at one constrained position (f64; max_marginal_f32 in trellis.hip):
+//   beta[i] = max_j(g[j] + a[i,j])  (g = last row of the reversed pass; 0 if no suffix)
+//   mu[i]   = delta_tk[i] + beta[i]
+template <int NP>
+__global__ __launch_bounds__(NP) void max_marginal_f64(MaxMarginal64Args args) {
+  __shared__ double g[NP];
+  const int i = threadIdx.x;
+  const int64_t c = blockIdx.x;
+  const bool suffix = args.ranges_suffix[2 * c + 1] > args.ranges_suffix[2 * c];
+  g[i] = suffix ? args.g[c * NP + i] : 0.0;
+  __syncthreads();
+  double beta = 0.0;
+  if (suffix) {
+    beta = ninf_d();
+#pragma unroll 8
+    for (int j = 0; j < NP; ++j) beta = fmax(beta, g[j] + args.at[(size_t)j * NP + i]);
+  }
+  args.mu[c * NP + i] = args.delta[c * NP + i] + beta;
+}
+
+__global__ void resume_rows_f64(const double* last, const int32_t* state, int np, double* out) {
+  const int64_t i = blockIdx.x;
+  const int j = threadIdx.x;
+  if (j < np) out[i * np + j] = (j == state[i]) ? last[i * np + j] : ninf_d();
 }
 
 template <int C, int S>
@@ -791,6 +852,40 @@ hipError_t launch_t64_bt(int np, const T64BtArgs& ba, int64_t nseq, hipStream_t 
     case 16: return bt_pf<16>(np, ba, grid, block, stream);
     default: return bt_pf<8>(np, ba, grid, block, stream);
   }
+}
+
+hipError_t launch_t64_prefix_bt(int np, const PrefixBt64Args& a, int64_t n, hipStream_t stream) {
+  if (n <= 0) return hipSuccess;
+  const dim3 grid((unsigned)((n + 3) / 4)), block(256);
+  switch (np) {
+    case 64: hipLaunchKernelGGL((prefix_backtrack_f64<1>), grid, block, 0, stream, a, n); break;
+    case 128: hipLaunchKernelGGL((prefix_backtrack_f64<2>), grid, block, 0, stream, a, n); break;
+    case 192: hipLaunchKernelGGL((prefix_backtrack_f64<3>), grid, block, 0, stream, a, n); break;
+    case 256: hipLaunchKernelGGL((prefix_backtrack_f64<4>), grid, block, 0, stream, a, n); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_t64_max_marginal(int np, const MaxMarginal64Args& a, int64_t ncon, hipStream_t stream) {
+  if (ncon <= 0) return hipSuccess;
+  const dim3 grid((unsigned)ncon);
+  switch (np) {
+    case 64: hipLaunchKernelGGL(max_marginal_f64<64>, grid, dim3(64), 0, stream, a); break;
+    case 128: hipLaunchKernelGGL(max_marginal_f64<128>, grid, dim3(128), 0, stream, a); break;
+    case 192: hipLaunchKernelGGL(max_marginal_f64<192>, grid, dim3(192), 0, stream, a); break;
+    case 256: hipLaunchKernelGGL(max_marginal_f64<256>, grid, dim3(256), 0, stream, a); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_t64_resume_rows(const double* last, const int32_t* state, int64_t n, int np, double* out,
+                                  hipStream_t stream) {
+  if (n <= 0) return hipSuccess;
+  if (np <= 0 || np > 256) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(resume_rows_f64, dim3((unsigned)n), dim3(256), 0, stream, last, state, np, out);
+  return hipGetLastError();
 }
 
 }  // namespace cvk

@@ -3,6 +3,11 @@
 Replaces, per sequence, the dense forward + backtrack of the reference's solvers:
 CPSolver::init_viterbi + backtrack (viterbi_solver/cp.rs:63-93), viterbi::decode
 (viterbi.rs:5-32) and DPSolver::solve (dp.rs:94-209); see include/cviterbi.h.
+
+dtype defaults to "f64": the reference's own arithmetic (hmm.rs:10-18 stores f64), paths
+and scores bit-identical to the f64 recurrence.  dtype="f32" selects the f32 trellis (about
+twice as fast; paths differ from the f64 ones on a few % of long sequences, scores are the
+f64 re-score of the f32 path when rescore_f64 is set).
 """
 from __future__ import annotations
 
@@ -23,7 +28,7 @@ def _p(x):
     return x.ctypes.data_as(ctypes.c_void_p)
 
 
-def make_opts(dtype="f32", assoc="viterbi", kernel="auto", rescore_f64=True, stream=None, workspace_bytes=0,
+def make_opts(dtype="f64", assoc="viterbi", kernel="auto", rescore_f64=True, stream=None, workspace_bytes=0,
               variant=None, mfma_tiles=None, serial=False):
     """variant: None/"valu" (all-VALU trellis, two equal-length sequences per workgroup where
     N % 64 == 0, default; for N <= 64 one wave per sequence with the backtrack fused),
@@ -44,7 +49,7 @@ def make_opts(dtype="f32", assoc="viterbi", kernel="auto", rescore_f64=True, str
                   workspace_bytes, flags)
 
 
-def decode_batch(hmm: HMM, offsets, obs, dtype="f32", assoc="viterbi", kernel="auto", rescore_f64=True,
+def decode_batch(hmm: HMM, offsets, obs, dtype="f64", assoc="viterbi", kernel="auto", rescore_f64=True,
                  workspace_bytes=0, variant=None, mfma_tiles=None, serial=False, forced=None):
     """Decode CSR sequences (offsets[B+1], flat obs) -> (path int32[sum T], score f64[B], status u8[B]).
     forced[sum T] (optional): -1 free, s >= 0 forces state s at that element."""
@@ -64,9 +69,10 @@ def decode_batch(hmm: HMM, offsets, obs, dtype="f32", assoc="viterbi", kernel="a
     return path, score, status
 
 
-def decode_constrained(hmm: HMM, offsets, obs, component, ncomp=None, rescore_f64=True):
+def decode_constrained(hmm: HMM, offsets, obs, component, ncomp=None, rescore_f64=True, dtype="f64"):
     """Consistency-constrained decode (cv_decode_constrained): component[sum T] (-1 = free).
-    Returns (path, score, status, comp_state[ncomp], objective)."""
+    dtype "f64" (default, the reference's precision: cp.rs:95-126 / dp.rs:147-166 in f64) or
+    "f32".  Returns (path, score, status, comp_state[ncomp], objective)."""
     offsets = np.ascontiguousarray(offsets, np.int64)
     obs = np.ascontiguousarray(obs, np.int32)
     component = np.ascontiguousarray(component, np.int32)
@@ -78,7 +84,7 @@ def decode_constrained(hmm: HMM, offsets, obs, component, ncomp=None, rescore_f6
     status = np.zeros(nseq, np.uint8)
     states = np.full(max(ncomp, 1), -1, np.int32)
     obj = ctypes.c_double()
-    o = make_opts("f32", "viterbi", "auto", rescore_f64)
+    o = make_opts(dtype, "viterbi", "auto", rescore_f64)
     L.check(L.lib().cv_decode_constrained(hmm.handle, nseq, _p(offsets), _p(obs), _p(component), int(ncomp),
                                           ctypes.byref(o), _p(path), _p(score), _p(status), _p(states),
                                           ctypes.byref(obj)))
@@ -104,7 +110,7 @@ def constrained_pairs(offsets, component, ncomp):
     return pairs[:n.value]
 
 
-def constrained_partials(hmm: HMM, offsets, obs, component, ncomp, pairs=None):
+def constrained_partials(hmm: HMM, offsets, obs, component, ncomp, pairs=None, dtype="f64"):
     """cv_constrained_partials: this shard's exact unary + pairwise terms as int64 words
     (partial_words long); partials of disjoint shards add (one all-reduce SUM).  `pairs`
     must come from constrained_pairs on the full batch (default: this batch's own)."""
@@ -115,7 +121,7 @@ def constrained_partials(hmm: HMM, offsets, obs, component, ncomp, pairs=None):
         pairs = constrained_pairs(offsets, component, ncomp)
     pairs = np.ascontiguousarray(pairs, np.int32).reshape(-1, 2)
     part = np.zeros(max(partial_words(hmm.nstates(), ncomp, len(pairs)), 1), np.int64)
-    o = make_opts("f32", "viterbi", "auto", True)
+    o = make_opts(dtype, "viterbi", "auto", True)
     L.check(L.lib().cv_constrained_partials(hmm.handle, offsets.shape[0] - 1, _p(offsets), _p(obs), _p(component),
                                             int(ncomp), len(pairs), _p(pairs) if len(pairs) else None,
                                             ctypes.byref(o), _p(part)))
@@ -135,7 +141,7 @@ def constrained_select(nstates: int, ncomp: int, partials, pairs=None):
     return states[:ncomp], ex.value
 
 
-def decode_forced_components(hmm: HMM, offsets, obs, component, comp_state, rescore_f64=True):
+def decode_forced_components(hmm: HMM, offsets, obs, component, comp_state, rescore_f64=True, dtype="f64"):
     """cv_decode_forced_components: final decode of a shard given the component states.
     Returns (path, score, status, objective)."""
     offsets = np.ascontiguousarray(offsets, np.int64)
@@ -147,7 +153,7 @@ def decode_forced_components(hmm: HMM, offsets, obs, component, comp_state, resc
     score = np.zeros(nseq, np.float64)
     status = np.zeros(nseq, np.uint8)
     obj = ctypes.c_double()
-    o = make_opts("f32", "viterbi", "auto", rescore_f64)
+    o = make_opts(dtype, "viterbi", "auto", rescore_f64)
     L.check(L.lib().cv_decode_forced_components(hmm.handle, nseq, _p(offsets), _p(obs), _p(component), len(cs),
                                                 _p(cs) if len(cs) else None, ctypes.byref(o), _p(path), _p(score),
                                                 _p(status), ctypes.byref(obj)))
@@ -155,7 +161,7 @@ def decode_forced_components(hmm: HMM, offsets, obs, component, comp_state, resc
 
 
 def decode_batch_device(hmm: HMM, offsets_dev, obs_dev, path_dev, score_dev, status_dev, offsets_host=None,
-                        dtype="f32", assoc="viterbi", kernel="auto", rescore_f64=True, stream=None,
+                        dtype="f64", assoc="viterbi", kernel="auto", rescore_f64=True, stream=None,
                         workspace_bytes=0, variant=None, mfma_tiles=None, serial=False):
     """Device-pointer decode (ints or objects with data_ptr(), e.g. torch tensors); async on `stream`."""
     def ptr(x):
@@ -176,7 +182,8 @@ def decode_batch_device(hmm: HMM, offsets_dev, obs_dev, path_dev, score_dev, sta
 EXCHANGE_FN = ctypes.CFUNCTYPE(ctypes.c_int32, ctypes.POINTER(ctypes.c_int64), ctypes.c_int64, ctypes.c_void_p)
 
 
-def decode_constrained_exchange(hmm: HMM, offsets, obs, component, ncomp, pairs, exchange=None, rescore_f64=True):
+def decode_constrained_exchange(hmm: HMM, offsets, obs, component, ncomp, pairs, exchange=None, rescore_f64=True,
+                                dtype="f64"):
     """cv_decode_constrained_exchange: one shard's constrained decode with the exchange step
     made by `exchange(words)` -- a callable that returns the SUM over all shards of the int64
     array `words` (e.g. cviterbi.dist.allreduce_partials); None = a single process.  `pairs`
@@ -204,7 +211,7 @@ def decode_constrained_exchange(hmm: HMM, offsets, obs, component, ncomp, pairs,
             return 1
 
     fn = EXCHANGE_FN(cb) if exchange is not None else None  # kept alive for the call
-    o = make_opts("f32", "viterbi", "auto", rescore_f64)
+    o = make_opts(dtype, "viterbi", "auto", rescore_f64)
     st = L.lib().cv_decode_constrained_exchange(hmm.handle, nseq, _p(offsets), _p(obs), _p(component), int(ncomp),
                                                 len(pairs), _p(pairs) if len(pairs) else None,
                                                 ctypes.cast(fn, ctypes.c_void_p) if fn else None, None,
@@ -217,7 +224,7 @@ def decode_constrained_exchange(hmm: HMM, offsets, obs, component, ncomp, pairs,
 
 
 def decode_constrained_device(hmm: HMM, offsets_host, offsets_dev, obs_dev, component, path_dev, score_dev, status_dev,
-                              ncomp=None, rescore_f64=True, stream=None, workspace_bytes=0):
+                              ncomp=None, rescore_f64=True, stream=None, workspace_bytes=0, dtype="f64"):
     """cv_decode_constrained_device: observations and outputs in HBM (ints or objects with
     data_ptr()), offsets_host/component on the host.  Synchronous.  Returns
     (comp_state[ncomp], objective)."""
@@ -230,7 +237,7 @@ def decode_constrained_device(hmm: HMM, offsets_host, offsets_dev, obs_dev, comp
         ncomp = int(component.max()) + 1 if component.size else 0
     states = np.full(max(ncomp, 1), -1, np.int32)
     obj = ctypes.c_double()
-    o = make_opts("f32", "viterbi", "auto", rescore_f64, stream, workspace_bytes)
+    o = make_opts(dtype, "viterbi", "auto", rescore_f64, stream, workspace_bytes)
     L.check(L.lib().cv_decode_constrained_device(hmm.handle, oh.shape[0] - 1, _p(oh), ptr(offsets_dev), ptr(obs_dev),
                                                  _p(component), int(ncomp), ctypes.byref(o), ptr(path_dev),
                                                  ptr(score_dev), ptr(status_dev), _p(states), ctypes.byref(obj)))

@@ -100,7 +100,7 @@ def allreduce_partials(partials, dist, device=None):
     return t.cpu().numpy()
 
 
-def constrained_decode_sharded(hmm, offsets, obs, component, ncomp, dist, device=None):
+def constrained_decode_sharded(hmm, offsets, obs, component, ncomp, dist, device=None, dtype="f64"):
     """Config 5 across ranks: shard sequences, exact partials, one all-reduce, select,
     per-shard final decode (cv_decode_constrained_exchange), gather to rank 0.  Returns (path, score, status, comp_state,
     objective) on rank 0 and (None, None, None, comp_state, None) elsewhere."""
@@ -120,7 +120,7 @@ def constrained_decode_sharded(hmm, offsets, obs, component, ncomp, dist, device
     # partials -> all-reduce SUM (the callback) -> search -> final decode, in one library call,
     # so the shard's decode reuses its terms pass's prefix rows (the resume flow)
     path, score, status, states, _, _ = decode_constrained_exchange(
-        hmm, off, ob, cp, ncomp, pairs, exchange=lambda w: allreduce_partials(w, dist, device))
+        hmm, off, ob, cp, ncomp, pairs, exchange=lambda w: allreduce_partials(w, dist, device), dtype=dtype)
     # gather: sequence counts and element counts differ per rank -> pad to capacities
     counts = torch.tensor([s1 - s0, hi - lo], dtype=torch.int64, device=device or "cpu")
     allc = [torch.zeros_like(counts) for _ in range(world)]

@@ -57,9 +57,9 @@ enum { CV_DTYPE_F32 = 0, CV_DTYPE_F64 = 1 };
 enum { CV_ASSOC_VITERBI = 0, CV_ASSOC_CP = 1, CV_ASSOC_DP = 2, CV_ASSOC_DECODE = 3 };
 
 /* kernel choice: AUTO picks TRELLIS (register-resident A, f32, VITERBI, N <= 256) when it
- * applies, then TRELLIS_F64 (exact f64, VITERBI, N <= 256, no forced states: one wave per
- * 2/4/8 sequences, A streamed from L2), else GENERIC (inline argmax, f32/f64, any
- * association, N <= 8192 f32 / 4096 f64). */
+ * applies, then TRELLIS_F64 (exact f64, any association, N <= 256; forced states with VITERBI
+ * only: one wave per 2/4/8 sequences, A streamed from L2), else GENERIC (inline argmax,
+ * f32/f64, any association, N <= 8192 f32 / 4096 f64). */
 enum { CV_KERNEL_AUTO = 0, CV_KERNEL_TRELLIS = 1, CV_KERNEL_GENERIC = 2, CV_KERNEL_TRELLIS_F64 = 3 };
 
 /* cv_opts.flags */
@@ -93,7 +93,9 @@ typedef struct cv_hmm_desc {
 } cv_hmm_desc;
 
 typedef struct cv_opts {
-  int32_t dtype;         /* CV_DTYPE_F32 (default) */
+  int32_t dtype;         /* CV_DTYPE_F64 (default: the reference's arithmetic, hmm.rs:10-18;
+                            paths and scores bit-identical to the f64 recurrence) or
+                            CV_DTYPE_F32 (the f32 trellis, ~2x faster, paths may differ) */
   int32_t assoc;         /* CV_ASSOC_VITERBI (default) */
   int32_t kernel;        /* CV_KERNEL_AUTO (default) */
   int32_t rescore_f64;   /* 1 (default): score_out = f64 re-score of the decoded path with
@@ -190,10 +192,13 @@ CV_API cv_status cv_last_timing(cv_hmm* h, cv_timing* out);
  * sequences as exact integers (units of 2^-64: independent of order and sharding) this is
  * a weighted CSP with unary and pairwise terms, solved exactly per connected group of
  * components by branch and bound (ties: lexicographically smallest state vector in
- * component order); then a forced decode.  f32 trellis path (N <= 256).  comp_state_out[ncomp]
- * gets s_c (-1: no active element, or no feasible assignment of its group); objective_out =
- * sum of the per-sequence scores (f64 re-scored).  CV_ELIMIT if the search exceeds its node
- * limit.  Host pointers; synchronous. */
+ * component order); then a forced decode.  Row-A0 (VITERBI) association, N <= 256, every term,
+ * segment table and the final decode in opts->dtype: CV_DTYPE_F64 (default; the reference's
+ * precision, cp.rs:95-126 / dp.rs:147-166 compute in f64: trellis_fwd_f64) or CV_DTYPE_F32 (the
+ * f32 trellis, scores f64 re-scored).  A term outside the exact unit (|score| >= 2^32) is
+ * CV_EINVAL.  comp_state_out[ncomp] gets s_c (-1: no active element, or no feasible assignment
+ * of its group); objective_out = sum of the per-sequence scores.  CV_ELIMIT if the search
+ * exceeds its node limit.  Host pointers; synchronous. */
 CV_API cv_status cv_decode_constrained(cv_hmm* h, int64_t nseq, const int64_t* offsets, const int32_t* obs,
                                        const int32_t* component, int32_t ncomp, const cv_opts* opts,
                                        int32_t* path_out, double* score_out, uint8_t* status_out,
@@ -260,7 +265,8 @@ CV_API cv_status cv_viterbi_decode(cv_hmm* h, int64_t T, const int32_t* obs, int
  *       "gpu-dp"   f64, DP association = DPSolver (dp.rs), ascending-index ties
  * Unconstrained super-sequences decode per sequence: objective =
  * sum of per-sequence scores (sequence order), solution in element order.  Active
- * constraints go through cv_decode_constrained ("gpu" kind only); get_explored_nodes then
+ * constraints go through cv_decode_constrained on the row-A0 association at the kind's
+ * precision (f64 for gpu-f64 / gpu-cp / gpu-dp, f32 for gpu); get_explored_nodes then
  * reports the number of (component, state) candidates scored. */
 CV_API cv_status cv_solver_create(const char* kind, cv_hmm* h, const cv_superseq_desc* seq, cv_solver** out);
 CV_API cv_status cv_solver_solve(cv_solver* s);                                   /* Solver::solve */

@@ -46,7 +46,8 @@ def test_version_and_opts_defaults():
     assert b"gfx950" in lib.cv_version()
     o = L.Opts()
     lib.cv_opts_init(ctypes.byref(o))
-    assert (o.dtype, o.assoc, o.kernel, o.rescore_f64, o.workspace_bytes) == (0, 0, 0, 1, 0)
+    # default dtype = CV_DTYPE_F64: the reference's arithmetic (hmm.rs:10-18)
+    assert (o.dtype, o.assoc, o.kernel, o.rescore_f64, o.workspace_bytes) == (1, 0, 0, 1, 0)
 
 
 def _model():
@@ -146,7 +147,7 @@ def test_decode_without_device_fails_loudly():
     pi, a, b = _model()
     h = cv.HMM(pi, a, b)
     with pytest.raises(cv.CVError) as e:
-        cv.decode_batch(h, [0, 3], np.array([1, 2, 3], np.int32))
+        cv.decode_batch(h, [0, 3], np.array([1, 2, 3], np.int32), dtype="f32")
     assert e.value.status == L.CV_EDEVICE
 
 
@@ -154,10 +155,10 @@ def test_argument_errors():
     pi, a, b = _model()
     h = cv.HMM(pi, a, b)
     with pytest.raises(cv.CVError) as e:  # non-monotone offsets
-        cv.decode_batch(h, [0, 3, 2], np.array([1, 2, 3], np.int32))
+        cv.decode_batch(h, [0, 3, 2], np.array([1, 2, 3], np.int32), dtype="f32")
     assert e.value.status in (L.CV_EINVAL, L.CV_EDEVICE)
     with pytest.raises(cv.CVError) as e:  # obs out of range
-        cv.decode_batch(h, [0, 2], np.array([1, 99], np.int32))
+        cv.decode_batch(h, [0, 2], np.array([1, 99], np.int32), dtype="f32")
     assert e.value.status in (L.CV_EINVAL, L.CV_EDEVICE)
     with pytest.raises(cv.CVError) as e:
         cv.GpuSolver(h, cv.SuperSequence([[1, 2]], None, h), kind="nope")

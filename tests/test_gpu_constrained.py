@@ -1,6 +1,8 @@
 """GPU: forced-state decoding and the consistency-constrained decode (config 5) against
-the oracle spec (oracle/np_oracle.py constrained_decode, C-accelerated in c_oracle):
-component states identical, paths bit-exact (f32), scores = f64 re-score of the path."""
+the oracle spec (oracle/np_oracle.py constrained_decode, C-accelerated in c_oracle), in both
+precisions: f64 (the reference's, cp.rs:95-126 / dp.rs:147-166; the default) and f32.
+Component states identical, paths bit-exact in the same precision, scores = the f64 decode's
+own score (f64) or the f64 re-score of the path (f32)."""
 import numpy as np
 import pytest
 
@@ -20,20 +22,43 @@ def test_forced_decode_bit_exact(gpu, n, variant):
     obs = rng.integers(0, 19, size=int(off[-1])).astype(np.int32)
     forced = np.where(rng.random(len(obs)) < 0.05, rng.integers(0, n, size=len(obs)), -1).astype(np.int32)
     h = cv.HMM(pi, a, b)
-    got = cv.decode_batch(h, off, obs, rescore_f64=False, forced=forced, variant=variant)
+    got = cv.decode_batch(h, off, obs, rescore_f64=False, forced=forced, variant=variant, dtype="f32")
     ref = O.decode_batch(pi, a, b, off, obs, O.VITERBI, np.float32, forced=forced)
     for x, y, what in zip(got, ref, ("path", "score", "status")):
         assert np.array_equal(x, y), what
 
 
-def _check(h, pi, a, b, off, obs, comp):
-    path, score, status, states, obj = cv.decode_constrained(h, off, obs, comp)
-    ref_states, forced = O.constrained_forced(pi, a, b, off, obs, comp, np.float32)
+@pytest.mark.parametrize("n", [1, 5, 45, 64, 65, 200, 256])
+def test_forced_decode_f64_bit_exact(gpu, n):
+    """Forced states on the exact-f64 trellis (trellis_fwd_f64 EXT + backtrack_f64) against
+    the f64 oracle; incl. infeasible sequences (a forced state whose emission is -inf)."""
+    pi, a, b = synth.random_hmm(n, 19, seed=n + 300, zero_frac=0.1 if n > 1 else 0.0)
+    rng = np.random.default_rng(n + 300)
+    off = synth.offsets_from_lengths(rng.integers(1, 60, size=40))
+    obs = rng.integers(0, 19, size=int(off[-1])).astype(np.int32)
+    forced = np.where(rng.random(len(obs)) < 0.05, rng.integers(0, n, size=len(obs)), -1).astype(np.int32)
+    h = cv.HMM(pi, a, b)
+    got = cv.decode_batch(h, off, obs, rescore_f64=False, forced=forced, dtype="f64")
+    assert cv.last_timing(h)["kernel"] == "trellis_f64"
+    ref = O.decode_batch(pi, a, b, off, obs, O.VITERBI, np.float64, forced=forced)
+    for x, y, what in zip(got, ref, ("path", "score", "status")):
+        assert np.array_equal(x, y), what
+
+
+DTYPES = [("f64", np.float64), ("f32", np.float32)]
+
+
+def _check(h, pi, a, b, off, obs, comp, dtype="f64"):
+    dt = dict(DTYPES)[dtype]
+    path, score, status, states, obj = cv.decode_constrained(h, off, obs, comp, dtype=dtype)
+    ref_states, forced = O.constrained_forced(pi, a, b, off, obs, comp, dt)
     for c, s in ref_states.items():
         assert states[c] == s, (c, states[c], s)
-    rp, rs, rst = O.decode_batch(pi, a, b, off, obs, O.VITERBI, np.float32, forced=forced)
+    rp, rs, rst = O.decode_batch(pi, a, b, off, obs, O.VITERBI, dt, forced=forced)
     assert np.array_equal(status, rst)
     assert np.array_equal(path, rp)
+    if dtype == "f64":  # the f64 decode's own score: the reference's value, bit for bit
+        assert np.array_equal(score[status == 0], rs[status == 0])
     for k in range(len(off) - 1):
         if status[k] == 0:
             assert score[k] == O.rescore_f64(pi, a, b, obs[off[k]:off[k + 1]], path[off[k]:off[k + 1]])
@@ -42,22 +67,27 @@ def _check(h, pi, a, b, off, obs, comp):
         assert path[e] == states[comp[e]]
 
 
+@pytest.mark.parametrize("dtype", ["f64", "f32"])
 @pytest.mark.parametrize("n", [4, 33, 64, 256])
-def test_constrained_small(gpu, n):
+def test_constrained_small(gpu, n, dtype):
     pi, a, b = synth.random_hmm(n, 11, seed=50 + n)
     rng = np.random.default_rng(n)
     off = synth.offsets_from_lengths(rng.integers(1, 40, size=24))
     obs = rng.integers(0, 11, size=int(off[-1])).astype(np.int32)
     comp = synth.constraint_components(off, seed=n, ncomp=3, prob=0.6)
-    _check(cv.HMM(pi, a, b), pi, a, b, off, obs, comp)
+    _check(cv.HMM(pi, a, b), pi, a, b, off, obs, comp, dtype)
 
 
-def test_constrained_config5_subset(gpu):
+@pytest.mark.parametrize("dtype", ["f64", "f32"])
+def test_constrained_config5_subset(gpu, dtype):
     c = synth.config("c5", nseq=48)
-    _check(cv.HMM(c["pi"], c["a"], c["b"]), c["pi"], c["a"], c["b"], c["offsets"], c["obs"], c["component"])
+    _check(cv.HMM(c["pi"], c["a"], c["b"]), c["pi"], c["a"], c["b"], c["offsets"], c["obs"], c["component"], dtype)
 
 
-def test_constrained_solver_api(gpu):
+@pytest.mark.parametrize("kind,dtype", [("gpu", "f32"), ("gpu-f64", "f64"), ("gpu-cp", "f64"), ("gpu-dp", "f64")])
+def test_constrained_solver_api(gpu, kind, dtype):
+    """trait Solver with active constraints: every kind runs the constrained decode (row A0)
+    at its precision -- f64 for the reference-numerics kinds (what main.rs:120 runs)."""
     pi, a, b = synth.random_hmm(10, 8, seed=9)
     rng = np.random.default_rng(9)
     seqs = [[int(x) for x in rng.integers(0, 8, size=int(t))] for t in rng.integers(2, 20, size=12)]
@@ -66,7 +96,7 @@ def test_constrained_solver_api(gpu):
     h = cv.HMM(pi, a, b)
     ss = cv.SuperSequence(seqs, cv.Constraints.from_tags(tags), h)
     ss.recompute_constraints(1.0)
-    s = cv.GpuSolver(h, ss, "gpu")
+    s = cv.GpuSolver(h, ss, kind)
     s.solve()
     sol = s.get_solution()
     assert s.get_explored_nodes() == 10 * ss.number_constraints()
@@ -75,8 +105,8 @@ def test_constrained_solver_api(gpu):
         assert len(set(sol[(ss.component == c) & (ss.active == 1)].tolist())) == 1
     offsets, obs, _ = ss.sequence_blocks()
     comp = np.where(ss.active == 1, ss.component, -1).astype(np.int32)
-    _, _, _, _, obj = cv.decode_constrained(h, offsets, obs, comp)
-    assert s.get_objective() == pytest.approx(obj, rel=1e-12)
+    _, _, _, _, obj = cv.decode_constrained(h, offsets, obs, comp, dtype=dtype)
+    assert s.get_objective() == obj
 
 
 def test_cli_end_to_end(gpu, tmp_path):
@@ -103,8 +133,9 @@ def test_cli_end_to_end(gpu, tmp_path):
     assert len(lines) == 2 + len(seqs)
 
 
+@pytest.mark.parametrize("dtype", ["f64", "f32"])
 @pytest.mark.parametrize("nshards", [2, 5])
-def test_constrained_sharded_equals_single(gpu, nshards):
+def test_constrained_sharded_equals_single(gpu, nshards, dtype):
     """The multi-GPU split (cv_constrained_partials per shard, integer SUM, select, per-shard
     cv_decode_forced_components) reproduces cv_decode_constrained bit for bit, whatever the
     shard boundaries (the exchange step of cviterbi.dist.constrained_decode_sharded)."""
@@ -114,7 +145,7 @@ def test_constrained_sharded_equals_single(gpu, nshards):
     h = cv.HMM(c["pi"], c["a"], c["b"])
     off, obs, comp = c["offsets"], c["obs"], c["component"]
     ncomp = int(comp.max()) + 1
-    path, score, status, states, obj = cv.decode_constrained(h, off, obs, comp, ncomp)
+    path, score, status, states, obj = cv.decode_constrained(h, off, obs, comp, ncomp, dtype=dtype)
     B = len(off) - 1
     pairs = cv.constrained_pairs(off, comp, ncomp)
     part = 0
@@ -122,14 +153,14 @@ def test_constrained_sharded_equals_single(gpu, nshards):
     for s0, s1 in shards:
         lo, hi = off[s0], off[s1]
         part = part + cv.constrained_partials(h, cvdist.shard_offsets(off, s0, s1), obs[lo:hi], comp[lo:hi], ncomp,
-                                              pairs)
+                                              pairs, dtype=dtype)
     got_states, explored = cv.constrained_select(h.nstates(), ncomp, part, pairs)
     assert np.array_equal(got_states, states)
     assert explored == h.nstates() * len(set(comp[comp >= 0].tolist()))
     for s0, s1 in shards:
         lo, hi = off[s0], off[s1]
         p, s, st, _ = cv.decode_forced_components(h, cvdist.shard_offsets(off, s0, s1), obs[lo:hi], comp[lo:hi],
-                                                  got_states)
+                                                  got_states, dtype=dtype)
         assert np.array_equal(p, path[lo:hi]) and np.array_equal(s, score[s0:s1]) and np.array_equal(st, status[s0:s1])
 
 
@@ -147,13 +178,14 @@ def _multi_case(n, seed, nseq=16, tmax=24, ncomp=3, maxpos=3, v=7):
     return pi, a, b, off, obs, comp
 
 
+@pytest.mark.parametrize("dtype", ["f64", "f32"])
 @pytest.mark.parametrize("n,seed", [(3, 1), (5, 2), (8, 3), (13, 4), (16, 5), (32, 6)])
-def test_constrained_multi_position(gpu, n, seed):
+def test_constrained_multi_position(gpu, n, seed, dtype):
     """Several constrained positions per sequence: alpha / segment tables (the trellis
     kernel's `start` mode) / beta terms, pairwise component terms and the exact search;
     component states equal the spec's, paths bit-exact, scores the f64 re-score."""
     pi, a, b, off, obs, comp = _multi_case(n, seed, ncomp=3 if n <= 16 else 2)
-    _check(cv.HMM(pi, a, b), pi, a, b, off, obs, comp)
+    _check(cv.HMM(pi, a, b), pi, a, b, off, obs, comp, dtype)
 
 
 def test_constrained_multi_position_sharded(gpu):
@@ -244,8 +276,9 @@ def test_cli_cfn(gpu, tmp_path):
     assert (tmp_path / "out" / "problem_1_0.cfn").read_text() == ref
 
 
+@pytest.mark.parametrize("dtype", ["f64", "f32"])
 @pytest.mark.parametrize("n,seed", [(7, 1), (64, 2), (256, 3)])
-def test_device_exact_sums_equal_host(gpu, monkeypatch, n, seed):
+def test_device_exact_sums_equal_host(gpu, monkeypatch, n, seed, dtype):
     """The unary terms summed exactly on the device (kernels/exact.hip) give the same int64
     words as the host loop (CV_HOST_SUMS=1): single- and multi-position sequences, -inf
     terms, several components."""
@@ -261,14 +294,15 @@ def test_device_exact_sums_equal_host(gpu, monkeypatch, n, seed):
             comp[pos] = rng.integers(0, 5, size=k)
     h = cv.HMM(pi, a, b)
     pairs = cv.constrained_pairs(off, comp, 5)
-    dev = cv.constrained_partials(h, off, obs, comp, 5, pairs)
+    dev = cv.constrained_partials(h, off, obs, comp, 5, pairs, dtype=dtype)
     monkeypatch.setenv("CV_HOST_SUMS", "1")
-    host = cv.constrained_partials(h, off, obs, comp, 5, pairs)
+    host = cv.constrained_partials(h, off, obs, comp, 5, pairs, dtype=dtype)
     assert np.array_equal(dev, host)
 
 
+@pytest.mark.parametrize("dtype", ["f64", "f32"])
 @pytest.mark.parametrize("n,seed", [(5, 11), (64, 12), (256, 13)])
-def test_constrained_device_equals_host(gpu, n, seed):
+def test_constrained_device_equals_host(gpu, n, seed, dtype):
     """cv_decode_constrained_device (inputs/outputs in HBM) == cv_decode_constrained, incl.
     several constrained positions per sequence and an unassignable component."""
     import torch
@@ -278,13 +312,13 @@ def test_constrained_device_equals_host(gpu, n, seed):
     obs = rng.integers(0, 9, size=int(off[-1])).astype(np.int32)
     comp = synth.constraint_components(off, seed=seed, ncomp=4, prob=0.7)
     h = cv.HMM(pi, a, b)
-    ref = cv.decode_constrained(h, off, obs, comp, ncomp=5)  # component 4 has no element
+    ref = cv.decode_constrained(h, off, obs, comp, ncomp=5, dtype=dtype)  # component 4 has no element
     dev = torch.device("cuda", 0)
     path_d = torch.empty(int(off[-1]), dtype=torch.int32, device=dev)
     score_d = torch.empty(len(off) - 1, dtype=torch.float64, device=dev)
     status_d = torch.empty(len(off) - 1, dtype=torch.uint8, device=dev)
     states, obj = cv.decode_constrained_device(h, off, torch.from_numpy(off).to(dev), torch.from_numpy(obs).to(dev),
-                                               comp, path_d, score_d, status_d, ncomp=5)
+                                               comp, path_d, score_d, status_d, ncomp=5, dtype=dtype)
     assert np.array_equal(states, ref[3])
     assert np.array_equal(path_d.cpu().numpy(), ref[0])
     assert np.array_equal(score_d.cpu().numpy(), ref[1])
@@ -331,20 +365,22 @@ def _resume_case(n, seed, nseq=48, tmax=40, bad_obs=False):
     return pi, a, b, off, obs, comp
 
 
+@pytest.mark.parametrize("dtype", ["f64", "f32"])
 @pytest.mark.parametrize("n,seed,bad", [(128, 1, False), (192, 2, False), (256, 3, False), (256, 4, True),
-                                        (130, 5, True), (200, 6, False)])
-def test_constrained_resume_equals_full(gpu, monkeypatch, n, seed, bad):
+                                        (130, 5, True), (200, 6, False), (40, 7, True)])
+def test_constrained_resume_equals_full(gpu, monkeypatch, n, seed, bad, dtype):
     """Resume flow (stored prefix rows, decode of [t_1, end), prefix backtrack from the forced
     state) == the full forced decode (CV_NO_RESUME=1), host and device APIs, bit for bit;
-    N = 200 (NP 224) is outside the resume flow and runs the full decode both times."""
+    f32: N = 200 (NP 224) and N = 40 are outside the resume flow and run the full decode both
+    times; f64 resumes at every N <= 256."""
     import torch
     pi, a, b, off, obs, comp = _resume_case(n, seed, bad_obs=bad)
     h = cv.HMM(pi, a, b)
-    for f64 in (False, True):  # f32 scores see the resumed row's value itself, not just the path
+    for f64 in ((False, True) if dtype == "f32" else (False,)):  # f32 scores see the resumed row itself
         monkeypatch.setenv("CV_NO_RESUME", "1")
-        ref = cv.decode_constrained(h, off, obs, comp, ncomp=5, rescore_f64=f64)
+        ref = cv.decode_constrained(h, off, obs, comp, ncomp=5, rescore_f64=f64, dtype=dtype)
         monkeypatch.setenv("CV_NO_RESUME", "0")
-        got = cv.decode_constrained(h, off, obs, comp, ncomp=5, rescore_f64=f64)
+        got = cv.decode_constrained(h, off, obs, comp, ncomp=5, rescore_f64=f64, dtype=dtype)
         for x, y, what in zip(got, ref, ("path", "score", "status", "states", "objective")):
             assert np.array_equal(np.asarray(x), np.asarray(y)), (what, f64)
     if bad:
@@ -354,7 +390,7 @@ def test_constrained_resume_equals_full(gpu, monkeypatch, n, seed, bad):
     score_d = torch.empty(len(off) - 1, dtype=torch.float64, device=dev)
     status_d = torch.empty(len(off) - 1, dtype=torch.uint8, device=dev)
     states, obj = cv.decode_constrained_device(h, off, torch.from_numpy(off).to(dev), torch.from_numpy(obs).to(dev),
-                                               comp, path_d, score_d, status_d, ncomp=5)
+                                               comp, path_d, score_d, status_d, ncomp=5, dtype=dtype)
     assert np.array_equal(states, ref[3])
     assert np.array_equal(path_d.cpu().numpy(), ref[0])
     assert np.array_equal(score_d.cpu().numpy(), ref[1])
@@ -362,17 +398,19 @@ def test_constrained_resume_equals_full(gpu, monkeypatch, n, seed, bad):
     assert obj == ref[4] or (np.isinf(obj) and np.isinf(ref[4]))
 
 
-def test_constrained_resume_oracle(gpu):
+@pytest.mark.parametrize("dtype", ["f64", "f32"])
+def test_constrained_resume_oracle(gpu, dtype):
     """Resume flow at N = 256 against the oracle spec directly."""
     pi, a, b, off, obs, comp = _resume_case(256, 9, nseq=24, tmax=30)
     for s in range(len(off) - 1):  # no component pairs (the oracle's search is brute force):
         e = off[s] + np.nonzero(comp[off[s]:off[s + 1]] >= 0)[0]  # later positions repeat the first's
         comp[e[1:]] = comp[e[0]] if len(e) else -1                # component (m >= 2, diagonal terms)
-    _check(cv.HMM(pi, a, b), pi, a, b, off, obs, comp)
+    _check(cv.HMM(pi, a, b), pi, a, b, off, obs, comp, dtype)
 
 
+@pytest.mark.parametrize("dtype", ["f64", "f32"])
 @pytest.mark.parametrize("nshards,resume", [(3, "0"), (3, "1"), (1, "0")])
-def test_constrained_exchange_shards(gpu, monkeypatch, nshards, resume):
+def test_constrained_exchange_shards(gpu, monkeypatch, nshards, resume, dtype):
     """cv_decode_constrained_exchange per shard, the callback handing back the SUM of every
     shard's partials (what the all-reduce returns), == cv_decode_constrained's slice of that
     shard, with and without the resume flow; the callback sees exactly the shard's partials."""
@@ -382,12 +420,12 @@ def test_constrained_exchange_shards(gpu, monkeypatch, nshards, resume):
     pi, a, b, off, obs, comp = _resume_case(256, 21, nseq=60)
     h = cv.HMM(pi, a, b)
     ncomp = 5
-    path, score, status, states, obj = cv.decode_constrained(h, off, obs, comp, ncomp)
+    path, score, status, states, obj = cv.decode_constrained(h, off, obs, comp, ncomp, dtype=dtype)
     B = len(off) - 1
     pairs = cv.constrained_pairs(off, comp, ncomp)
     shards = [cvdist.shard_range(B, nshards, r)[:2] for r in range(nshards)]
     parts = [cv.constrained_partials(h, cvdist.shard_offsets(off, s0, s1), obs[off[s0]:off[s1]],
-                                     comp[off[s0]:off[s1]], ncomp, pairs) for s0, s1 in shards]
+                                     comp[off[s0]:off[s1]], ncomp, pairs, dtype=dtype) for s0, s1 in shards]
     total = np.sum(parts, axis=0)
     for (s0, s1), own in zip(shards, parts):
         lo, hi = off[s0], off[s1]
@@ -398,7 +436,7 @@ def test_constrained_exchange_shards(gpu, monkeypatch, nshards, resume):
             return total
 
         p, s, st, got_states, explored, _ = cv.decode_constrained_exchange(
-            h, cvdist.shard_offsets(off, s0, s1), obs[lo:hi], comp[lo:hi], ncomp, pairs, exchange)
+            h, cvdist.shard_offsets(off, s0, s1), obs[lo:hi], comp[lo:hi], ncomp, pairs, exchange, dtype=dtype)
         assert seen == [True]
         assert np.array_equal(got_states, states)
         assert np.array_equal(p, path[lo:hi]) and np.array_equal(s, score[s0:s1]) and np.array_equal(st, status[s0:s1])

@@ -62,7 +62,7 @@ def test_trellis_variants_bit_exact(gpu, n, variant, serial):
     h = cv.HMM(pi, a, b)
     ref = O.decode_batch(pi, a, b, off, obs, O.VITERBI, np.float32)
     got = cv.decode_batch(h, off, obs, rescore_f64=False, variant=variant, serial=serial,
-                          workspace_bytes=0 if serial else 256 * 4 * 300)
+                          workspace_bytes=0 if serial else 256 * 4 * 300, dtype="f32")
     t = cv.last_timing(h)
     assert (t["mfma_tiles"] >= 0) == (variant == "mfma" and t["padded_states"] >= 64)
     _assert_same(got, ref, f"{variant} N={n} serial={serial}")
@@ -82,13 +82,13 @@ def test_pair_kernel_equal_and_ragged(gpu, n, serial):
     ref = O.decode_batch(pi, a, b, off, obs, O.VITERBI, np.float32)
     ws = 0 if serial else n * 4 * 400
     for variant in ("valu", "valu1"):
-        got = cv.decode_batch(h, off, obs, rescore_f64=False, variant=variant, serial=serial, workspace_bytes=ws)
+        got = cv.decode_batch(h, off, obs, rescore_f64=False, variant=variant, serial=serial, workspace_bytes=ws, dtype="f32")
         _assert_same(got, ref, f"{variant} N={n} serial={serial}")
     # equal lengths, odd count: pairs (2k, 2k+1) straight from the CSR order, one single
     off2 = synth.offsets_from_lengths(np.full(9, 33))
     obs2 = rng.integers(0, 23, size=int(off2[-1])).astype(np.int32)
     ref2 = O.decode_batch(pi, a, b, off2, obs2, O.VITERBI, np.float32)
-    _assert_same(cv.decode_batch(h, off2, obs2, rescore_f64=False, serial=serial), ref2, f"equal N={n}")
+    _assert_same(cv.decode_batch(h, off2, obs2, rescore_f64=False, serial=serial, dtype="f32"), ref2, f"equal N={n}")
 
 
 @pytest.mark.parametrize("n", [1, 5, 16, 17, 31, 32, 33, 45, 48, 49, 64])
@@ -104,13 +104,13 @@ def test_wave_kernel_small_n(gpu, n, serial):
     h = cv.HMM(pi, a, b)
     ref = O.decode_batch(pi, a, b, off, obs, O.VITERBI, np.float32)
     ws = 0 if serial else 64 * 4 * 700
-    got = cv.decode_batch(h, off, obs, rescore_f64=False, serial=serial, workspace_bytes=ws)
+    got = cv.decode_batch(h, off, obs, rescore_f64=False, serial=serial, workspace_bytes=ws, dtype="f32")
     assert cv.last_timing(h)["padded_states"] == (n + 15) // 16 * 16
     _assert_same(got, ref, f"wave N={n}")
-    other = cv.decode_batch(h, off, obs, rescore_f64=False, variant="nowave", serial=serial, workspace_bytes=ws)
+    other = cv.decode_batch(h, off, obs, rescore_f64=False, variant="nowave", serial=serial, workspace_bytes=ws, dtype="f32")
     _assert_same(got, other, f"wave vs workgroup N={n}")
     # f64 re-score along the path
-    path, score, status = cv.decode_batch(h, off, obs, rescore_f64=True, serial=serial, workspace_bytes=ws)
+    path, score, status = cv.decode_batch(h, off, obs, rescore_f64=True, serial=serial, workspace_bytes=ws, dtype="f32")
     for s in range(len(off) - 1):
         if status[s] == 0:
             lo, hi = off[s], off[s + 1]
@@ -121,7 +121,7 @@ def test_wave_kernel_small_n(gpu, n, serial):
 def test_mfma_tile_counts_bit_exact(gpu, mt):
     pi, a, b, off, obs = _case(256, 31, seed=77, nseq=12, tmax=60, zero_frac=0.02)
     h = cv.HMM(pi, a, b)
-    got = cv.decode_batch(h, off, obs, rescore_f64=False, mfma_tiles=mt)
+    got = cv.decode_batch(h, off, obs, rescore_f64=False, mfma_tiles=mt, dtype="f32")
     assert cv.last_timing(h)["mfma_tiles"] == mt
     _assert_same(got, O.decode_batch(pi, a, b, off, obs, O.VITERBI, np.float32), f"mt={mt}")
 
@@ -179,8 +179,8 @@ def test_ties_first_index(gpu):
 def test_chunked_workspace(gpu):
     pi, a, b, off, obs = _case(64, 40, seed=5, nseq=40, tmax=90)
     h = cv.HMM(pi, a, b)
-    full = cv.decode_batch(h, off, obs, rescore_f64=False)
-    small = cv.decode_batch(h, off, obs, rescore_f64=False, workspace_bytes=64 * 4 * 200)
+    full = cv.decode_batch(h, off, obs, rescore_f64=False, dtype="f32")
+    small = cv.decode_batch(h, off, obs, rescore_f64=False, workspace_bytes=64 * 4 * 200, dtype="f32")
     assert cv.last_timing(h)["launches"] > 1
     for x, y in zip(full, small):
         assert np.array_equal(x, y)
@@ -201,21 +201,21 @@ def test_device_api_badobs(gpu, n):
     s_d = torch.zeros(len(off) - 1, dtype=torch.float64, device=dev)
     st_d = torch.zeros(len(off) - 1, dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream().cuda_stream
-    cv.decode_batch_device(h, o_d, ob_d, p_d, s_d, st_d, offsets_host=off, stream=stream)
+    cv.decode_batch_device(h, o_d, ob_d, p_d, s_d, st_d, offsets_host=off, stream=stream, dtype="f32")
     torch.cuda.synchronize()
     st = st_d.cpu().numpy()
     assert st[2] == cv._lib.SEQ_BADOBS
     assert (np.delete(st, 2) == 0).all()
     # host API rejects it up front
     with pytest.raises(cv.CVError):
-        cv.decode_batch(h, off, obs)
+        cv.decode_batch(h, off, obs, dtype="f32")
 
 
 @pytest.mark.parametrize("cfg,nseq", [("c2", 256), ("c3", 24), ("c4", 48)])
 def test_config_subsets_bit_exact(gpu, cfg, nseq):
     c = synth.config(cfg, nseq=nseq)
     h = cv.HMM(c["pi"], c["a"], c["b"])
-    got = cv.decode_batch(h, c["offsets"], c["obs"], rescore_f64=False)
+    got = cv.decode_batch(h, c["offsets"], c["obs"], rescore_f64=False, dtype="f32")
     ref = O.decode_batch(c["pi"], c["a"], c["b"], c["offsets"], c["obs"], O.VITERBI, np.float32, nthreads=8)
     _assert_same(got, ref, cfg)
 
@@ -229,7 +229,7 @@ def test_config4_full_properties(gpu):
     c = synth.config("c4")
     pi, a, b, off, obs = c["pi"], c["a"], c["b"], c["offsets"], c["obs"]
     h = cv.HMM(pi, a, b)
-    path, s32, st = cv.decode_batch(h, off, obs, rescore_f64=False)
+    path, s32, st = cv.decode_batch(h, off, obs, rescore_f64=False, dtype="f32")
     assert (st == 0).all()
     assert path.min() >= 0 and path.max() < 256
     B, T = len(off) - 1, 512
@@ -244,7 +244,7 @@ def test_config4_full_properties(gpu):
         if dt == np.float32:
             assert np.array_equal(d.astype(np.float64), ref_score)
         else:
-            _, s64, _ = cv.decode_batch(h, off, obs, rescore_f64=True)
+            _, s64, _ = cv.decode_batch(h, off, obs, rescore_f64=True, dtype="f32")
             assert np.array_equal(d, s64)
     rng = np.random.default_rng(1)
     pick = np.sort(rng.choice(B, size=16, replace=False))
@@ -294,5 +294,5 @@ def test_long_sequence_large_alphabet(gpu):
     obs = rng.integers(0, v, size=int(off[-1])).astype(np.int32)
     h = cv.HMM(pi, a, b)
     ref = O.decode_batch(pi, a, b, off, obs, O.VITERBI, np.float32, nthreads=4)
-    _assert_same(cv.decode_batch(h, off, obs, rescore_f64=False), ref, "long")
-    _assert_same(cv.decode_batch(h, off, obs, rescore_f64=False, workspace_bytes=256 * 4 * 9000), ref, "long, capped")
+    _assert_same(cv.decode_batch(h, off, obs, rescore_f64=False, dtype="f32"), ref, "long")
+    _assert_same(cv.decode_batch(h, off, obs, rescore_f64=False, workspace_bytes=256 * 4 * 9000, dtype="f32"), ref, "long, capped")
