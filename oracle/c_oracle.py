@@ -45,6 +45,8 @@ def lib():
             f.argtypes = [ctypes.c_int, ctypes.c_int, P, P, P, ctypes.c_int, P, P]
             f.restype = None
         L.cvo_rescore_f64.argtypes = [ctypes.c_int, ctypes.c_int, P, P, P, ctypes.c_int, P, P]
+        L.cvo_rescore_batch_f64.argtypes = [ctypes.c_int, ctypes.c_int, P, P, P, ctypes.c_int64, P, P, P, P]
+        L.cvo_rescore_batch_f64.restype = None
         L.cvo_rescore_f64.restype = ctypes.c_double
         L.cvo_cp_superseq_f64.argtypes = [ctypes.c_int, ctypes.c_int, P, P, P, ctypes.c_int64, P, P, P]
         L.cvo_cp_superseq_f64.restype = ctypes.c_double
@@ -123,6 +125,20 @@ def rescore_f64(pi, a, b, obs, path):
     obs = np.ascontiguousarray(obs, np.int32)
     path = np.ascontiguousarray(path, np.int32)
     return lib().cvo_rescore_f64(a.shape[0], b.shape[1], _p(pi), _p(a), _p(b), obs.shape[0], _p(obs), _p(path))
+
+
+def rescore_batch_f64(pi, a, b, offsets, obs, path):
+    """rescore_f64 of every sequence of a CSR batch (f64 row-A0 fold along each path)."""
+    pi = np.ascontiguousarray(pi, np.float64)
+    a = np.ascontiguousarray(a, np.float64)
+    b = np.ascontiguousarray(b, np.float64)
+    offsets = np.ascontiguousarray(offsets, np.int64)
+    obs = np.ascontiguousarray(obs, np.int32)
+    path = np.ascontiguousarray(path, np.int32)
+    out = np.zeros(offsets.shape[0] - 1, np.float64)
+    lib().cvo_rescore_batch_f64(a.shape[0], b.shape[1], _p(pi), _p(a), _p(b), offsets.shape[0] - 1, _p(offsets),
+                                _p(obs), _p(path), _p(out))
+    return out
 
 
 def cp_superseq_f64(pi, a, b, offsets, obs):

@@ -204,6 +204,13 @@ double cvo_rescore_f64(int N, int V, const double* pi, const double* a, const do
   return d;
 }
 
+/* cvo_rescore_f64 over a CSR batch (test infrastructure: full-size property checks). */
+void cvo_rescore_batch_f64(int N, int V, const double* pi, const double* a, const double* b, int64_t nseq,
+                           const int64_t* offsets, const int32_t* obs, const int32_t* path, double* out) {
+  for (int64_t s = 0; s < nseq; ++s)
+    out[s] = cvo_rescore_f64(N, V, pi, a, b, (int)(offsets[s + 1] - offsets[s]), obs + offsets[s], path + offsets[s]);
+}
+
 double cvo_cp_superseq_f64(int N, int V, const double* pi, const double* a, const double* b,
                            int64_t nseq, const int64_t* offsets, const int32_t* obs,
                            int32_t* path) {

@@ -79,6 +79,9 @@ int cvo_decode_batch_f32(int N, int V, const float* pi, const float* a, const fl
  * d = pi[p0] + b[p0,o0]; d = (d + a[p_{t-1},p_t]) + b[p_t,o_t]. */
 double cvo_rescore_f64(int N, int V, const double* pi, const double* a, const double* b, int T,
                        const int32_t* obs, const int32_t* path);
+/* cvo_rescore_f64 of every sequence of a CSR batch -> out[nseq] */
+void cvo_rescore_batch_f64(int N, int V, const double* pi, const double* a, const double* b, int64_t nseq,
+                           const int64_t* offsets, const int32_t* obs, const int32_t* path, double* out);
 
 /* CPSolver over a whole super-sequence (cp.rs:63-83 + utils.rs:24-38):
  * sequences concatenated, t==0 elements use the constant pi[to] transition

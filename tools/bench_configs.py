@@ -4,8 +4,9 @@ DESIGN.md; bench.py keeps config 4 as the headline):
   c3  N=64,  V=256,    T~U[32,1024], B=16,384       (plain decode, length-sorted schedule)
   c4f64, c2f64, c3f64  the same decodes in exact f64 (trellis_fwd_f64: paths and scores
       bit-identical to the f64 reference recurrence)
-  c5  config 4 + one constrained position in half the sequences, K=7
-      (cv_decode_constrained_device; "c5host": the host-pointer cv_decode_constrained)
+  c5  config 4 + one constrained position in half the sequences, K=7, exact f64 (the
+      reference's precision; cv_decode_constrained_device; "c5f32": the f32 trellis;
+      "c5host": the host-pointer cv_decode_constrained in f64)
 Inputs resident in HBM (device APIs) except c5host, whose line includes PCIe transfers.
 Prints one JSON line per config."""
 import json
@@ -30,7 +31,8 @@ torch.cuda.set_stream(stream)
 
 for name in which:
     f64 = name.endswith("f64")
-    c = synth.config("c5" if name == "c5host" else name[:-3] if f64 else name)
+    base = name.replace("f64", "").replace("f32", "").replace("host", "")
+    c = synth.config(base)
     n = c["pi"].shape[0]
     off, obs = c["offsets"], c["obs"]
     B = len(off) - 1
@@ -59,7 +61,7 @@ for name in which:
 
         def run():
             cv.decode_constrained_device(h, off, o_d, ob_d, comp, p_d, s_d, st_d, ncomp=7,
-                                         stream=stream.cuda_stream)
+                                         stream=stream.cuda_stream, dtype="f32" if name == "c5f32" else "f64")
     run()
     run()
     torch.cuda.synchronize()
