@@ -806,6 +806,7 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
       ba.score = score_dev;  // the f64 delta is already the reference score: no re-score
       ba.status = status_dev;
       ba.dp_assoc = o.assoc == CV_ASSOC_DP ? 1 : 0;
+      ba.decode_bt = o.assoc == CV_ASSOC_DECODE ? 1 : 0;
       ba.obs = obs_dev;
       ba.et = h->q_et.as<double>();
       err = cvk::launch_t64_bt(h->np64, ba, n, bts);
@@ -824,6 +825,7 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
       ba.status = status_dev;
       ba.obs = obs_dev;
       ba.rescore_f64 = 0;  // the f64 kernel's own score is already reference numerics
+      ba.decode_bt = o.assoc == CV_ASSOC_DECODE ? 1 : 0;
       ba.pi64 = h->d_pi64.as<double>();
       ba.a64 = h->d_a64.as<double>();
       ba.et64 = h->d_et64.as<double>();
@@ -843,6 +845,7 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
       ba.status = status_dev;
       ba.obs = obs_dev;
       ba.rescore_f64 = o.rescore_f64 ? 1 : 0;
+      ba.decode_bt = o.assoc == CV_ASSOC_DECODE ? 1 : 0;
       ba.pi64 = h->d_pi64.as<double>();
       ba.a64 = h->d_a64.as<double>();
       ba.et64 = h->d_et64.as<double>();
@@ -2122,6 +2125,59 @@ CV_API cv_status cv_viterbi_decode(cv_hmm* h, int64_t T, const int32_t* obs, int
   return cv_decode_batch(h, 1, off, obs, &o, path_out, &score, &status);
 }
 
+CV_API cv_status cv_decode_superseq_cp(cv_hmm* h, int64_t nseq, const int64_t* offsets, const int32_t* obs,
+                                       int32_t* path_out, double* objective_out) {
+  if (!h || nseq < 0 || (nseq > 0 && (!offsets || !obs || !path_out)) || !objective_out)
+    return set_err(CV_EINVAL, "bad argument");
+  *objective_out = 0.0;
+  if (nseq == 0) return CV_OK;
+  if (h->N > 1024) return set_err(CV_EUNSUPPORTED, "super-sequence chain covers N <= 1024 (N=%d)", h->N);
+  std::lock_guard<std::mutex> lk(h->mu);
+  cv_status st = set_device(h);
+  if (st != CV_OK) return st;
+  if ((st = check_batch(h, nseq, offsets)) != CV_OK) return st;
+  const int64_t base = offsets[0], L = offsets[nseq] - base;
+  if (L <= 0) return CV_OK;
+  {
+    const int64_t V = h->V;
+    const int64_t k = first_bad(base, offsets[nseq], [&](int64_t i) { return obs[i] < 0 || obs[i] >= V; });
+    if (k >= 0) return set_err(CV_EINVAL, "obs[%lld] = %d out of range [0,%lld)", (long long)k, obs[k], (long long)V);
+  }
+  if ((st = ensure_f64_tables(h)) != CV_OK) return st;
+  std::vector<uint8_t> first((size_t)L, 0);
+  for (int64_t q = 0; q < nseq; ++q)
+    if (offsets[q + 1] > offsets[q]) first[(size_t)(offsets[q] - base)] = 1;
+  hipStream_t stream = h->stream;
+  DevBuf d_obs, d_first, d_psi, d_path, d_obj;
+  if ((st = d_obs.ensure((size_t)L * 4)) != CV_OK) return st;
+  if ((st = d_first.ensure((size_t)L)) != CV_OK) return st;
+  if ((st = d_psi.ensure((size_t)L * h->N * 2)) != CV_OK) return st;
+  if ((st = d_path.ensure((size_t)L * 4)) != CV_OK) return st;
+  if ((st = d_obj.ensure(8)) != CV_OK) return st;
+  HIP_TRY(hipMemcpyAsync(d_obs.p, obs + base, (size_t)L * 4, hipMemcpyHostToDevice, stream));
+  HIP_TRY(hipMemcpyAsync(d_first.p, first.data(), (size_t)L, hipMemcpyHostToDevice, stream));
+  cvk::CpChainArgs g{};
+  g.pi = h->d_pi64.as<double>();
+  g.a = h->d_a64.as<double>();
+  g.et = h->d_et64.as<double>();
+  g.obs = d_obs.as<int32_t>();
+  g.first = d_first.as<uint8_t>();
+  g.len = L;
+  g.nstates = h->N;
+  g.nobs = (int)h->V;
+  g.psi = d_psi.as<uint16_t>();
+  g.path = d_path.as<int32_t>();
+  g.objective = d_obj.as<double>();
+  const hipError_t err = cvk::launch_cp_superseq_chain(g, stream);
+  if (err != hipSuccess) return set_err(CV_EDEVICE, "super-sequence chain launch failed: %s", hipGetErrorString(err));
+  HIP_TRY(hipMemcpyAsync(path_out, d_path.p, (size_t)L * 4, hipMemcpyDeviceToHost, stream));
+  HIP_TRY(hipMemcpyAsync(objective_out, d_obj.p, 8, hipMemcpyDeviceToHost, stream));
+  HIP_TRY(hipStreamSynchronize(stream));
+  if (!(*objective_out > -INFINITY))
+    return set_err(CV_EINFEASIBLE, "no finite-probability path through the super-sequence (cp.rs:87 asserts)");
+  return CV_OK;
+}
+
 // ---- trait Solver ------------------------------------------------------------------
 struct cv_solver {
   std::string kind;
@@ -2150,7 +2206,7 @@ CV_API cv_status cv_solver_create(const char* kind, cv_hmm* h, const cv_superseq
   if (s->kind == "gpu") {
   } else if (s->kind == "gpu-f64") {
     s->opts.dtype = CV_DTYPE_F64;
-  } else if (s->kind == "gpu-cp") {
+  } else if (s->kind == "gpu-cp" || s->kind == "gpu-cp-seq") {
     s->opts.dtype = CV_DTYPE_F64;
     s->opts.assoc = CV_ASSOC_CP;
     s->opts.rescore_f64 = 0;
@@ -2159,7 +2215,7 @@ CV_API cv_status cv_solver_create(const char* kind, cv_hmm* h, const cv_superseq
     s->opts.assoc = CV_ASSOC_DP;
     s->opts.rescore_f64 = 0;
   } else {
-    return set_err(CV_EINVAL, "unknown solver kind '%s' (gpu, gpu-f64, gpu-cp, gpu-dp)", kind);
+    return set_err(CV_EINVAL, "unknown solver kind '%s' (gpu, gpu-f64, gpu-cp, gpu-cp-seq, gpu-dp)", kind);
   }
   s->nseq = d->nseq;
   s->offsets.assign(d->offsets, d->offsets + d->nseq + 1);
@@ -2209,6 +2265,13 @@ CV_API cv_status cv_solver_solve(cv_solver* s) {
   s->solution.assign((size_t)total, 0);
   s->scores.assign((size_t)s->nseq, 0.0);
   s->status.assign((size_t)s->nseq, 0);
+  if (s->kind == "gpu-cp") {  // CPSolver::solve exactly: the chained super-sequence decode
+    double obj = -INFINITY;
+    cv_status st = cv_decode_superseq_cp(s->hmm, s->nseq, s->offsets.data(), s->obs.data(), s->solution.data(), &obj);
+    s->objective = st == CV_OK ? obj : -INFINITY;
+    s->explored = 0;  // no B&B node without constraints (cp.rs:137-142)
+    return st;
+  }
   cv_status st = cv_decode_batch(s->hmm, s->nseq, s->offsets.data(), s->obs.data(), &s->opts, s->solution.data(),
                                  s->scores.data(), s->status.data());
   if (st != CV_OK) return st;

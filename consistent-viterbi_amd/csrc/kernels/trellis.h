@@ -107,6 +107,8 @@ struct GenericBtArgs {
   uint8_t* status;
   const int32_t* obs;      // for the f64 re-score
   int rescore_f64;         // f32 kernels only: score = f64 VITERBI re-score of the path
+  int decode_bt;           // viterbi::decode: an infeasible sequence backtracks from argmax 0
+                           // through psi (viterbi.rs:24-30) instead of getting the 0 path
   const double* pi64;
   const double* a64;
   const double* et64;

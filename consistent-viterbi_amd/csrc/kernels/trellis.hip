@@ -1391,7 +1391,20 @@ __global__ __launch_bounds__(256) void generic_backtrack(GenericBtArgs<REAL> arg
   int32_t* path = args.path + e0;
   const uint8_t prior = args.status[seq];
   if (!(bv > (double)ninf) || prior == CVK_SEQ_BADOBS) {
-    for (int t = lane; t < T; t += 64) path[t] = 0;
+    if (args.decode_bt && prior != CVK_SEQ_BADOBS) {
+      // viterbi::decode backtracks an infeasible sequence too: from argmax 0 of the all -inf
+      // last row through bt (0 where the emission is -inf), viterbi.rs:19-21, 24-30
+      if (lane == 0) {
+        const uint16_t* psi = args.psi + (e0 - args.psi_elem_base) * (int64_t)N;
+        int cs = bi;
+        for (int t = T - 1; t >= 0; --t) {
+          path[t] = cs;
+          if (t > 0) cs = psi[(size_t)t * N + cs];
+        }
+      }
+    } else {
+      for (int t = lane; t < T; t += 64) path[t] = 0;
+    }
     if (lane == 0) {
       args.score[seq] = -__builtin_inf();
       args.status[seq] = prior == CVK_SEQ_BADOBS ? CVK_SEQ_BADOBS : CVK_SEQ_INFEASIBLE;

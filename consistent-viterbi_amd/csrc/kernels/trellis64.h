@@ -48,7 +48,9 @@ struct T64BtArgs {
   double* score;           // [nseq_total]
   uint8_t* status;
   int dp_assoc;            // 1: candidates (a[i,j] + b[j,o_t]) + d[i] (dp.rs:149)
-  const int32_t* obs;      // dp_assoc: observations, emissions [V][NP]
+  int decode_bt;           // viterbi::decode (zero_init): an infeasible sequence backtracks from
+                           // argmax 0, bt = 0 where the emission is -inf (viterbi.rs:19-30)
+  const int32_t* obs;      // dp_assoc / decode_bt: observations, emissions [V][NP]
   const double* et;
 };
 
@@ -82,6 +84,21 @@ hipError_t launch_t64_max_marginal(int np, const MaxMarginal64Args& a, int64_t n
 // out[i][j] = j == state[i] ? last[i][j] : -inf (row t_1 of constrained sequence i, forced)
 hipError_t launch_t64_resume_rows(const double* last, const int32_t* state, int64_t n, int np, double* out,
                                   hipStream_t stream);
+
+// CPSolver's super-sequence decode chained exactly over the whole batch (cp_superseq_chain).
+struct CpChainArgs {
+  const double* pi;      // [N]
+  const double* a;       // [N*N] from-major
+  const double* et;      // [V][N] emissions transposed
+  const int32_t* obs;    // [len] super-sequence observations
+  const uint8_t* first;  // [len] 1 at the first element of each sequence (MetaElements t == 0)
+  int64_t len;
+  int nstates, nobs;
+  uint16_t* psi;         // [len][N] workspace
+  int32_t* path;         // [len]
+  double* objective;     // [1]
+};
+hipError_t launch_cp_superseq_chain(const CpChainArgs& g, hipStream_t stream);
 
 // NP = 64 * ceil(N / 64) for 1 <= N <= 256, else 0 (no f64 trellis kernel)
 int t64_padded_states(int n);

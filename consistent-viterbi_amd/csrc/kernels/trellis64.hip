@@ -562,7 +562,10 @@ __device__ __forceinline__ int first_argmax_d(const double (&s)[KP], const bool 
 // One backtrack chain: path[T-1] = cur, then for t = T-1..1 the first argmax of
 // d_{t-1}[i] + a[i, path[t]] (DPSolver: (a[i, path[t]] + b[path[t], o_t]) + d_{t-1}[i])
 // through the split-plane rows rows[0 .. T-1] (row t = element t of the chain).
-template <int KP, int PF>
+// DEC (viterbi::decode, infeasible sequences only): bt = 0 where the emission of the current
+// state is -inf (viterbi.rs:19-21); on a feasible path every emission is finite, so the rule
+// never changes a feasible decode.
+template <int KP, int PF, bool DEC = false>
 __device__ __forceinline__ void bt_chain_f64(const uint32_t* __restrict__ rows, int T, int cur, int32_t* __restrict__ path,
                                              const double* __restrict__ at, const double* __restrict__ et,
                                              const int32_t* __restrict__ obs, int dp_assoc, int N, int lane) {
@@ -591,7 +594,12 @@ __device__ __forceinline__ void bt_chain_f64(const uint32_t* __restrict__ rows, 
 #pragma unroll
     for (int u = 0; u < PF; ++u) {
       const int t = base - u;
-      if (t >= 1) {
+      if (DEC && t >= 1 && !(et[(size_t)obs[t] * NP + cur] > ninf_d())) {
+        cur = 0;
+        const int tp = t - 1;
+        if (lane == (tp & 63)) pathreg = cur;
+        if ((tp & 63) == 0 && tp + lane < T) path[tp + lane] = pathreg;
+      } else if (t >= 1) {
         const double* acol = at + (size_t)cur * NP + lane;
         double e = 0.0;
         if (dp_assoc) e = et[(size_t)obs[t] * NP + cur];
@@ -681,7 +689,10 @@ __global__ __launch_bounds__(256) void backtrack_f64(T64BtArgs g) {
   }
   const uint8_t prior = g.status[seq];
   if (!(bv > ninf_d()) || prior == CVK_SEQ_BADOBS) {
-    for (int t = lane; t < T; t += 64) path[t] = 0;
+    if (g.decode_bt && prior != CVK_SEQ_BADOBS)  // viterbi.rs:24-30: from argmax 0 (= cur) through bt
+      bt_chain_f64<KP, PF, true>(rows, T, cur, path, g.at, g.et, g.obs + e0, 0, N, lane);
+    else
+      for (int t = lane; t < T; t += 64) path[t] = 0;
     if (lane == 0) {
       g.score[seq] = ninf_d();
       g.status[seq] = prior == CVK_SEQ_BADOBS ? CVK_SEQ_BADOBS : CVK_SEQ_INFEASIBLE;
@@ -885,6 +896,75 @@ hipError_t launch_t64_resume_rows(const double* last, const int32_t* state, int6
   if (n <= 0) return hipSuccess;
   if (np <= 0 || np > 256) return hipErrorInvalidValue;
   hipLaunchKernelGGL(resume_rows_f64, dim3((unsigned)n), dim3(256), 0, stream, last, state, np, out);
+  return hipGetLastError();
+}
+
+// ---- CPSolver's super-sequence decode, chained exactly (cp.rs:63-93 over utils.rs:62-103) ----
+// The reference decodes the whole batch as ONE super-sequence: at a sequence start the
+// predecessor term is the constant pi[j] (utils.rs:32-38), so every value of sequence k
+// carries the running total of sequences 0..k-1 and rounds accordingly.  A per-sequence
+// decode is the same up to those roundings; this kernel reproduces them: one workgroup walks
+// the elements in order, thread j = state j: first argmax over i of prev[i] + trans(i, j)
+// (strict '>' from i = 0), value prev[psi] + (trans(psi, j) + b[j, o]) (cp.rs:70-79), psi
+// stored as u16; then the first argmax of the last row and the backtrack (cp.rs:85-93).
+// Serial over elements (as the reference is): for the main.rs workflow, not the batch path.
+__global__ __launch_bounds__(1024) void cp_superseq_chain(CpChainArgs g) {
+  extern __shared__ double rowbuf[];  // [2][N]
+  const int j = threadIdx.x;
+  const int N = g.nstates;
+  const int64_t L = g.len;
+  double* prev = rowbuf;
+  double* cur = rowbuf + N;
+  if (j < N) prev[j] = g.pi[j] + g.et[(size_t)g.obs[0] * N + j];  // init_probs (cp.rs:66-68)
+  __syncthreads();
+  for (int64_t t = 1; t < L; ++t) {
+    if (j < N) {
+      const int o = g.obs[t];
+      const bool first = g.first[t] != 0;
+      const double pj = g.pi[j];
+      double m = prev[0] + (first ? pj : g.a[j]);
+      int arg = 0;
+      for (int i = 1; i < N; ++i) {
+        const double x = prev[i] + (first ? pj : g.a[(size_t)i * N + j]);
+        if (x > m) {
+          m = x;
+          arg = i;
+        }
+      }
+      const double tr = first ? pj : g.a[(size_t)arg * N + j];
+      cur[j] = prev[arg] + (tr + g.et[(size_t)o * N + j]);
+      g.psi[t * N + j] = (uint16_t)arg;
+    }
+    __syncthreads();
+    double* tmp = prev;
+    prev = cur;
+    cur = tmp;
+  }
+  if (j == 0) {
+    int cs = 0;
+    double obj = prev[0];
+    for (int i = 1; i < N; ++i)
+      if (prev[i] > obj) {
+        obj = prev[i];
+        cs = i;
+      }
+    *g.objective = obj;
+    for (int64_t t = L - 1; t >= 0; --t) {
+      g.path[t] = cs;
+      cs = g.psi[t * N + cs];
+    }
+  }
+}
+
+hipError_t launch_cp_superseq_chain(const CpChainArgs& g, hipStream_t stream) {
+  if (g.len <= 0) return hipSuccess;
+  if (g.nstates <= 0 || g.nstates > 1024) return hipErrorInvalidValue;
+  const int threads = ((g.nstates + 63) / 64) * 64;
+  const size_t lds = (size_t)2 * g.nstates * sizeof(double);
+  if (lds > 64 * 1024)
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&cp_superseq_chain), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds);
+  hipLaunchKernelGGL(cp_superseq_chain, dim3(1), dim3(threads), lds, stream, g);
   return hipGetLastError();
 }
 

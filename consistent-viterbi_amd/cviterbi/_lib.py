@@ -38,6 +38,7 @@ EXPORTS = [
     "cv_hmm_transition_prob", "cv_hmm_transitions_to", "cv_hmm_emit_prob", "cv_hmm_emit_probs",
     "cv_decode_batch", "cv_decode_batch_device", "cv_last_timing", "cv_decode_constrained", "cv_decode_constrained_device", "cv_decode_constrained_exchange",
     "cv_constrained_pairs", "cv_constrained_partials", "cv_constrained_select", "cv_decode_forced_components", "cv_viterbi_decode",
+    "cv_decode_superseq_cp",
     "cv_solver_create", "cv_solver_solve", "cv_solver_get_solution", "cv_solver_get_objective",
     "cv_solver_get_name", "cv_solver_get_explored_nodes", "cv_solver_destroy",
     "cv_hmm_fit_mle", "cv_hmm_fit_train", "cv_solver_write_cfn",
@@ -123,6 +124,7 @@ def lib():
         "cv_constrained_select": ([I32, I32, I64, P, P, P, P], S),
         "cv_decode_forced_components": ([P, I64, P, P, P, I32, P, P, P, P, P, P], S),
         "cv_viterbi_decode": ([P, I64, P, P], S),
+        "cv_decode_superseq_cp": ([P, I64, P, P, P, P], S),
         "cv_solver_create": ([ctypes.c_char_p, P, P, P], S),
         "cv_solver_solve": ([P], S),
         "cv_solver_get_solution": ([P, P, P], S),

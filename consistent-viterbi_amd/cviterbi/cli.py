@@ -1,7 +1,7 @@
 """Command line mirror of the reference's `main` (src/main.rs:25-136) on the GPU solver.
 
     python -m cviterbi.cli -i INPUT -o OUTPUT -n NSTATES -b NOBS [NOBS ...] -p PROP
-                           [-t [-s]] [--cfn] [--kind gpu] [--seed S]
+                           [-t [-s]] [--cfn] [--kind gpu-cp] [--seed S]
 
 Reads INPUT/sequences, INPUT/tags, INPUT/test_tags (main.rs:80-87) and either INPUT/hmm.json
 (main.rs:100-103) or, with -t, fits the HMM on the GPU from a random start (HMM::new,
@@ -13,6 +13,9 @@ main.rs:87; SuperSequence::from + recompute_constraints(prop), main.rs:106-115) 
 OUTPUT/{prop}_0 like main.rs:111-133: "{objective} {explored_nodes}\\n{elapsed_ms}\\n" then
 "{seq} {state}" per element.  --cfn takes the reference's run_cfn branch (main.rs:116-118):
 OUTPUT/problem_{prop}_0.cfn (cfn.rs:82-205) and the compile time in OUTPUT/{prop}_0.
+The solver defaults to what main.rs:120 runs, CPSolver: kind "gpu-cp" -- without active
+constraints the exact chained super-sequence decode in f64 (cv_decode_superseq_cp: the same
+path and objective bits as cp.rs), with them the consistency-constrained decode in f64.
 """
 from __future__ import annotations
 
@@ -81,7 +84,9 @@ def main(argv=None):
     p.add_argument("-s", "--supervised", action="store_true", help="with -t: supervised MLE")
     p.add_argument("--cfn", action="store_true", help="write the CFN instead of solving (main.rs run_cfn)")
     p.add_argument("--seed", type=int, default=None, help="random start of -t (reference: thread_rng)")
-    p.add_argument("--kind", default="gpu", help="solver kind (gpu, gpu-f64, gpu-cp, gpu-dp)")
+    p.add_argument("--kind", default="gpu-cp",
+                   help="solver kind: gpu-cp (default: CPSolver, main.rs:120, f64), gpu-cp-seq, gpu-f64, gpu-dp, "
+                        "gpu (f32 trellis)")
     p.add_argument("--device", type=int, default=0)
     a = p.parse_args(argv)
     print("Loading data")

@@ -244,6 +244,19 @@ def decode_constrained_device(hmm: HMM, offsets_host, offsets_dev, obs_dev, comp
     return states[:ncomp], obj.value
 
 
+def decode_superseq_cp(hmm: HMM, offsets, obs):
+    """cv_decode_superseq_cp: CPSolver::solve (cp.rs:133-143) exactly -- the sequences decoded
+    as ONE chained super-sequence in f64 (utils.rs:62-103), as main.rs:120 runs it.
+    Returns (path[sum T] in super-sequence order, objective)."""
+    offsets = np.ascontiguousarray(offsets, np.int64)
+    obs = np.ascontiguousarray(obs, np.int32)
+    path = np.zeros(max(int(offsets[-1] - offsets[0]), 1), np.int32)
+    obj = ctypes.c_double()
+    L.check(L.lib().cv_decode_superseq_cp(hmm.handle, offsets.shape[0] - 1, _p(offsets), _p(obs), _p(path),
+                                          ctypes.byref(obj)))
+    return path[:int(offsets[-1] - offsets[0])], obj.value
+
+
 def last_timing(hmm: HMM) -> dict:
     t = L.Timing()
     L.check(L.lib().cv_last_timing(hmm.handle, ctypes.byref(t)))

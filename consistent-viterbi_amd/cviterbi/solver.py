@@ -238,9 +238,10 @@ class Solver:
 
 
 class GpuSolver(Solver):
-    """Solver backed by cv_solver_* (kinds: gpu, gpu-f64, gpu-cp, gpu-dp; include/cviterbi.h)."""
+    """Solver backed by cv_solver_* (kinds: gpu-cp = CPSolver, the default, what main.rs:120
+    runs; gpu-cp-seq, gpu-f64, gpu-dp, gpu; include/cviterbi.h)."""
 
-    def __init__(self, hmm: HMM, sequence: SuperSequence, kind: str = "gpu"):
+    def __init__(self, hmm: HMM, sequence: SuperSequence, kind: str = "gpu-cp"):
         self.hmm = hmm
         self.sequence = sequence
         offsets, obs, seq_ids = sequence.sequence_blocks()

@@ -257,14 +257,29 @@ CV_API cv_status cv_decode_constrained_exchange(cv_hmm* h, int64_t nseq, const i
 /* viterbi::decode (viterbi.rs:5): one sequence, reference decode() semantics (row 0 = 0.0,
  * f64), path only. */
 CV_API cv_status cv_viterbi_decode(cv_hmm* h, int64_t T, const int32_t* obs, int32_t* path_out);
+/* CPSolver::solve without active constraints, exactly (cp.rs:133-143: init_viterbi cp.rs:63-83
+ * + backtrack cp.rs:85-93 over the super-sequence of utils.rs:62-103): the nseq sequences are
+ * decoded as ONE chain in order -- at a sequence start the predecessor term is pi[j]
+ * (utils.rs:24-38), so later sequences carry the running total and round exactly as the
+ * reference does (a per-sequence decode can differ from it at near ties).  f64, first-index
+ * argmax, CP association.  path_out[offsets[nseq] - offsets[0]] in super-sequence order;
+ * objective_out = the chain's final maximum (main.rs:129's first number).  Serial over
+ * elements on the GPU (one workgroup), as the reference is on the CPU: the main.rs drop-in,
+ * not the batch hot path.  N <= 1024.  CV_EINFEASIBLE when the maximum is -inf. */
+CV_API cv_status cv_decode_superseq_cp(cv_hmm* h, int64_t nseq, const int64_t* offsets, const int32_t* obs,
+                                       int32_t* path_out, double* objective_out);
 
 /* ---- trait Solver (viterbi_solver.rs:11-16) -------------------------------------------
  * kind: "gpu"      f32 trellis kernel, VITERBI association, f64 re-scored objective
  *       "gpu-f64"  f64, VITERBI association (reference numerics, row A0)
- *       "gpu-cp"   f64, CP association = CPSolver (cp.rs), what main.rs:120 runs
+ *       "gpu-cp"   CPSolver (cp.rs), what main.rs:120 runs: without constraints the exact
+ *                  chained super-sequence decode (cv_decode_superseq_cp, objective and path
+ *                  as the reference rounds them)
+ *       "gpu-cp-seq" f64, CP association, every sequence decoded on its own (parallel; equal
+ *                  to gpu-cp up to the chain's running-total roundings)
  *       "gpu-dp"   f64, DP association = DPSolver (dp.rs), ascending-index ties
- * Unconstrained super-sequences decode per sequence: objective =
- * sum of per-sequence scores (sequence order), solution in element order.  Active
+ * Unconstrained super-sequences decode per sequence (except "gpu-cp",
+ * chained): objective = sum of per-sequence scores (sequence order), solution in element order.  Active
  * constraints go through cv_decode_constrained on the row-A0 association at the kind's
  * precision (f64 for gpu-f64 / gpu-cp / gpu-dp, f32 for gpu); get_explored_nodes then
  * reports the number of (component, state) candidates scored. */

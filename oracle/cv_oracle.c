@@ -116,10 +116,20 @@
         end = j;                                                                                \
       }                                                                                         \
     int status = CVO_SEQ_OK;                                                                    \
-    if (!(best > ninf)) {                                                                       \
+    if (!(best > ninf) && assoc != CVO_ASSOC_DECODE) {                                          \
       /* infeasible: reference panics (cp.rs:87, dp.rs:184-186); we report it */              \
       status = CVO_SEQ_INFEASIBLE;                                                              \
       for (int t = 0; t < T; ++t) path[t] = 0;                                                  \
+      *score = ninf;                                                                            \
+    } else if (!(best > ninf)) {                                                                \
+      /* viterbi::decode: argmax 0 of the all -inf row, then bt (0 where the emission is      \
+       * -inf), viterbi.rs:19-21, 24-30 */                                                     \
+      status = CVO_SEQ_INFEASIBLE;                                                              \
+      int cs = end;                                                                             \
+      for (int t = T - 1; t >= 0; --t) {                                                        \
+        path[t] = cs;                                                                           \
+        cs = bt[(int64_t)t * N + cs];                                                           \
+      }                                                                                         \
       *score = ninf;                                                                            \
     } else {                                                                                    \
       int cs = end;                                                                             \

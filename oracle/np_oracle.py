@@ -17,7 +17,8 @@ Semantics follow SURVEY.md §8a (file:line into /root/reference/src):
                     (cp.rs:70-78 via utils.rs:24-30 -> hmm.rs:220-222).
   DP                c = (a + b[None,:,o]) + d[:,None] over finite entries; first max
                     (dp.rs:127-177, ascending-index iteration instead of HashMap order).
-  DECODE            viterbi.rs:5-32: row 0 = 0.0, -inf emission -> -inf, bt 0.
+  DECODE            viterbi.rs:5-32: row 0 = 0.0, -inf emission -> -inf, bt 0; an infeasible
+                    sequence still backtracks from argmax 0 (viterbi.rs:24-30).
 """
 from __future__ import annotations
 
@@ -76,12 +77,16 @@ def decode(pi, a, b, obs, assoc=VITERBI, dtype=np.float64):
     end = int(np.argmax(prev))
     best = prev[end]
     path = np.zeros(T, np.int32)
-    if not best > ninf:
+    if not best > ninf and assoc != DECODE:
         return path, ninf, SEQ_INFEASIBLE
+    # viterbi.rs:24-30 backtracks from argmax 0 of an all -inf last row too (bt left 0 where
+    # the emission is -inf); the other solvers panic there (cp.rs:87, dp.rs:184-186)
     cs = end
     for t in range(T - 1, -1, -1):
         path[t] = cs
         cs = bt[t, cs]
+    if not best > ninf:
+        return path, ninf, SEQ_INFEASIBLE
     return path, best, SEQ_OK
 
 

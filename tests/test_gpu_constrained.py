@@ -133,6 +133,78 @@ def test_cli_end_to_end(gpu, tmp_path):
     assert len(lines) == 2 + len(seqs)
 
 
+def _read_out(path):
+    lines = path.read_text().splitlines()
+    obj, nodes = lines[0].split()
+    return float(obj), int(nodes), [tuple(int(x) for x in ln.split()) for ln in lines[2:]]
+
+
+@pytest.mark.parametrize("seed", [2, 3])
+def test_cli_prop0_matches_cpsolver_superseq(gpu, tmp_path, seed):
+    """main.rs with prop = 0 on the default solver kind (gpu-cp = CPSolver, main.rs:120):
+    every "{seq} {state}" line of OUTPUT/0_0 equals the CP super-sequence restatement
+    (oracle cvo_cp_superseq_f64: cp.rs:63-93 over utils.rs:62-103, chained in f64) and the
+    objective is the same double."""
+    from cviterbi import cli
+
+    pi, a, b = synth.random_hmm(6, 12, seed=seed)
+    h = cv.HMM(pi, a, b.reshape(6, 4, 3))
+    h.write(tmp_path / "hmm.json")
+    _cli_input(tmp_path, seed=seed)
+    assert cli.main(["-i", str(tmp_path), "-o", str(tmp_path / "out"), "-n", "6", "-b", "4", "3", "-p", "0"]) == 0
+    obj, nodes, got = _read_out(tmp_path / "out" / "0_0")
+    seqs = cv.load_sequences(tmp_path / "sequences", D=2)
+    ss = cv.SuperSequence(seqs, cv.Constraints.from_tags(cv.load_tags(tmp_path / "test_tags")), h)
+    ss.recompute_constraints(0.0)
+    offsets, obs, _ = ss.sequence_blocks()
+    rp, robj = O.cp_superseq_f64(pi, a, b, offsets, obs)
+    assert got == [(int(ss.seq[k]), int(rp[k])) for k in range(len(rp))]
+    assert obj == robj and nodes == 0
+
+
+def test_cli_prop1_matches_constrained_spec_f64(gpu, tmp_path):
+    """main.rs with prop = 1 (every test tag active) on the default kind: the f64
+    consistency-constrained decode; every line equals the spec's forced decode in f64 given
+    the spec's component states (oracle/np_oracle.py constrained_decode, dtype f64)."""
+    from cviterbi import cli
+
+    pi, a, b = synth.random_hmm(6, 12, seed=4)
+    h = cv.HMM(pi, a, b.reshape(6, 4, 3))
+    h.write(tmp_path / "hmm.json")
+    _cli_input(tmp_path, seed=4)
+    assert cli.main(["-i", str(tmp_path), "-o", str(tmp_path / "out"), "-n", "6", "-b", "4", "3", "-p", "1"]) == 0
+    obj, nodes, got = _read_out(tmp_path / "out" / "1_0")
+    seqs = cv.load_sequences(tmp_path / "sequences", D=2)
+    ss = cv.SuperSequence(seqs, cv.Constraints.from_tags(cv.load_tags(tmp_path / "test_tags")), h)
+    ss.recompute_constraints(1.0)
+    offsets, obs, _ = ss.sequence_blocks()
+    comp = np.where(ss.active == 1, ss.component, -1).astype(np.int32)
+    _, forced = O.constrained_forced(pi, a, b, offsets, obs, comp, np.float64)
+    rp, rs, rst = O.decode_batch(pi, a, b, offsets, obs, O.VITERBI, np.float64, forced=forced)
+    assert np.all(rst == 0)
+    assert got == [(int(ss.seq[k]), int(rp[k])) for k in range(len(rp))]
+    assert obj == pytest.approx(float(np.sum(rs)), rel=1e-12) and nodes == 6 * ss.number_constraints()
+
+
+def test_superseq_cp_chain_rounding(gpu):
+    """The chained super-sequence rounds like the reference: a running total of -2^40 makes
+    two predecessors 2^-20 apart tie (ulp(2^40) = 2^-12), so the first index wins in the chain
+    while the per-sequence CP decode takes the strictly larger one."""
+    big = 2.0 ** 40
+    pi = np.array([-1.0, -1.0, -3.0])
+    a = np.array([[-1.0] * 3, [-1.0 + 2.0 ** -20] * 3, [-5.0] * 3])
+    b = np.array([[-0.5, -big], [-0.5, -big], [-0.5, -big]])
+    off = np.array([0, 1, 3], np.int64)
+    obs = np.array([1, 0, 0], np.int32)
+    h = cv.HMM(pi, a, b)
+    path, obj = cv.decode_superseq_cp(h, off, obs)
+    rp, robj = O.cp_superseq_f64(pi, a, b, off, obs)
+    assert np.array_equal(path, rp) and obj == robj
+    assert path[1] == 0  # the chain's tie -> first index
+    seq_path, _, _ = cv.decode_batch(h, off, obs, dtype="f64", assoc="cp", rescore_f64=False)
+    assert seq_path[1] == 1  # per sequence: the strictly larger predecessor
+
+
 @pytest.mark.parametrize("dtype", ["f64", "f32"])
 @pytest.mark.parametrize("nshards", [2, 5])
 def test_constrained_sharded_equals_single(gpu, nshards, dtype):

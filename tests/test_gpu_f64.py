@@ -85,6 +85,35 @@ def test_t64_ties_and_infeasible(gpu, n, assoc):
             cv.decode_batch(h, off, obs_bad, dtype="f64", kernel=kernel, rescore_f64=False)
 
 
+@pytest.mark.parametrize("kernel", ["auto", "generic"])
+@pytest.mark.parametrize("dtype", ["f64", "f32"])
+def test_decode_infeasible_backtrack(gpu, kernel, dtype):
+    """viterbi::decode (CV_ASSOC_DECODE) on infeasible sequences follows bt from argmax 0
+    (viterbi.rs:19-30), on the f64 trellis (backtrack_f64) and the generic kernel, f32 and f64:
+    the hand-worked case of test_oracle.py plus random ones, all equal to the oracle."""
+    if dtype == "f32" and kernel == "auto":
+        pytest.skip("f32 DECODE always runs the generic kernel")
+    pi = np.array([-0.3, -0.3])
+    a = np.array([[-1.0, -0.5], [-0.25, -2.0]])
+    b = np.array([[-0.5, -1.0, -np.inf], [-1.0, -0.5, -np.inf]])
+    h = cv.HMM(pi, a, b)
+    p, s, st = cv.decode_batch(h, [0, 3], np.array([0, 0, 2], np.int32), dtype=dtype, assoc="decode",
+                               kernel=kernel, rescore_f64=False)
+    assert st[0] == 1 and s[0] == -np.inf and p.tolist() == [1, 0, 0]
+    rng = np.random.default_rng(5)
+    for n in (3, 64, 130, 256):
+        pi, a, b = synth.random_hmm(n, 6, seed=n, zero_frac=0.3)
+        b[:, 5] = -np.inf  # observation 5: infeasible wherever it occurs
+        lengths = rng.integers(1, 40, size=30)
+        off = synth.offsets_from_lengths(lengths)
+        obs = rng.integers(0, 6, size=int(off[-1])).astype(np.int32)
+        h = cv.HMM(pi, a, b)
+        got = cv.decode_batch(h, off, obs, dtype=dtype, assoc="decode", kernel=kernel, rescore_f64=False)
+        ref = O.decode_batch(pi, a, b, off, obs, O.DECODE, np.float64 if dtype == "f64" else np.float32)
+        assert (ref[2] == 1).sum() > 5
+        _assert_same(got, ref, f"decode infeasible N={n} {kernel} {dtype}")
+
+
 @pytest.mark.parametrize("n", [45, 256])
 @pytest.mark.parametrize("serial", [False, True])
 @pytest.mark.parametrize("assoc", ["viterbi", "cp", "dp"])

@@ -263,12 +263,16 @@ def test_solver_api(gpu):
     ss = cv.SuperSequence(seqs, None, h)
     ss.recompute_constraints(0.0)  # main.rs:107 -> reorder (utils.rs:138-165)
     for kind, assoc, dt in (("gpu", O.VITERBI, np.float32), ("gpu-f64", O.VITERBI, np.float64),
-                            ("gpu-cp", O.CP, np.float64), ("gpu-dp", O.DP, np.float64)):
+                            ("gpu-cp-seq", O.CP, np.float64), ("gpu-dp", O.DP, np.float64), ("gpu-cp", None, None)):
         s = cv.GpuSolver(h, ss, kind)
         s.solve()
         sol = s.get_solution()
         assert s.get_name() == kind and s.get_explored_nodes() == 0
         offsets, obs, _ = ss.sequence_blocks()
+        if kind == "gpu-cp":  # CPSolver exactly: the chained super-sequence, path and objective bits
+            rp, robj = O.cp_superseq_f64(pi, a, b, offsets, obs)
+            assert np.array_equal(sol, rp) and s.get_objective() == robj
+            continue
         rp, rs, _ = O.decode_batch(pi, a, b, offsets, obs, assoc, dt)
         assert np.array_equal(sol, rp)
         if kind == "gpu":

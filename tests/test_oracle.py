@@ -84,6 +84,31 @@ def test_kat_infeasible():
         assert st[0] == 1 and s[0] == -np.inf and p.tolist() == [0, 0]
 
 
+def test_kat_decode_infeasible_backtracks_from_argmax0():
+    """viterbi::decode on an infeasible sequence (viterbi.rs:19-30): the last row is all -inf,
+    argmax gives 0 (first index), and the backtrack follows bt, which is 0 where the emission
+    is -inf but a real first argmax elsewhere.  Worked by hand (log10 values):
+      row 0 = [0, 0] (viterbi.rs:6, 9)
+      t1 (o=0): to 0: max(0 + -1, 0 + -0.25) -> psi 1, -0.25 + -0.5 = -0.75
+                to 1: max(0 + -0.5, 0 + -2) -> psi 0, -0.5 + -1 = -1.5
+      t2 (o=2): emission -inf in both states -> row -inf, bt 0
+      end = argmax([-inf, -inf]) = 0; path[1] = bt[2][0] = 0; path[0] = bt[1][0] = 1
+    so the reference returns [1, 0, 0] -- not the all-zero path of an infeasible CP/DP decode."""
+    pi = np.array([-0.3, -0.3])
+    a = np.array([[-1.0, -0.5], [-0.25, -2.0]])
+    b = np.array([[-0.5, -1.0, -np.inf], [-1.0, -0.5, -np.inf]])
+    obs = np.array([0, 0, 2], np.int32)
+    for dt in (np.float64, np.float32):
+        p, s, st = C.decode_batch(pi, a, b, [0, 3], obs, C.DECODE, dt)
+        assert st[0] == 1 and s[0] == -np.inf and p.tolist() == [1, 0, 0]
+        p2, s2, st2 = NO.decode(pi, a, b, obs, NO.DECODE, dt)
+        assert st2 == 1 and p2.tolist() == [1, 0, 0]
+    # an emission that is -inf mid-sequence resets bt to 0 there: obs [0, 2, 0] -> t1 row
+    # -inf with bt 0, t2 row -inf (all predecessors -inf: first argmax 0) -> [0, 0, 0]
+    p, _, st = C.decode_batch(pi, a, b, [0, 3], np.array([0, 2, 0], np.int32), C.DECODE, np.float64)
+    assert st[0] == 1 and p.tolist() == [0, 0, 0]
+
+
 @pytest.mark.parametrize("seed", range(40))
 def test_c_matches_numpy_restatement(seed):
     n = [1, 2, 3, 5, 8, 13][seed % 6]
