@@ -28,7 +28,10 @@ bool add_exact(int64_t* limbs4, int64_t* ninf_count, float x) { return add_exact
 bool add_exact(int64_t* limbs4, int64_t* ninf_count, double x) { return add_exact_t(limbs4, ninf_count, x); }
 
 static inline __int128 limbs_value(const int64_t* l) {
-  return (__int128)l[0] + ((__int128)l[1] << 32) + ((__int128)l[2] << 64) + ((__int128)l[3] << 96);
+  // multiplications, not shifts: limb 3 and carried limbs may be negative (a left shift of a
+  // negative value is undefined before C++20)
+  const __int128 B = (__int128)1 << 32;
+  return (__int128)l[0] + (__int128)l[1] * B + (__int128)l[2] * (B * B) + (__int128)l[3] * (B * B * B);
 }
 
 std::vector<int32_t> component_pairs(int64_t nseq, const int64_t* offsets, const int32_t* component) {

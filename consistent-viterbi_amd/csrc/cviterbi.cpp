@@ -111,7 +111,7 @@ struct cv_hmm {
 
   // trellis kernel tables (f32, padded to NP)
   int np = 0;
-  DevBuf t_aimg, t_aimg_mfma, t_pi, t_et, t_at, t_arm;  // t_arm: row-major A (one-wave kernel)
+  DevBuf t_aimg, t_pi, t_et, t_at, t_arm;  // t_arm: row-major A (one-wave kernel)
   // one-wave kernel (N <= 64): tables padded to npw = 16 * ceil(N / 16) states
   int npw = 0;
   DevBuf w_arm, w_pi, w_et, w_at;
@@ -196,16 +196,6 @@ cv_status ensure_trellis_tables(cv_hmm* h) {
         dst[2] = A(r0 + 1, j0);
         dst[3] = A(r0 + 1, j0 + 1);
       }
-  // MFMA-assisted kernel: [wave w][tile t][quad q][lane][4] in the 32x32 C/D layout:
-  // lane l, reg r = 4q + c -> row 32t + c + 8q + 4(l>>5), column 32w + (l&31).
-  std::vector<float> img2((size_t)np * np);
-  for (int w = 0; w < np / 32; ++w)
-    for (int t = 0; t < np / 32; ++t)
-      for (int q = 0; q < 4; ++q)
-        for (int lane = 0; lane < 64; ++lane)
-          for (int c = 0; c < 4; ++c)
-            img2[((((size_t)w * (np / 32) + t) * 4 + q) * 64 + lane) * 4 + c] =
-                A(32 * t + c + 8 * q + 4 * (lane >> 5), 32 * w + (lane & 31));
   std::vector<float> pi(np, NI), at((size_t)np * np, NI), arm((size_t)np * np, NI), et((size_t)V * np, NI);
   for (int j = 0; j < N; ++j) pi[j] = f32(h->pi[j]);
   for (int i = 0; i < N; ++i)
@@ -214,7 +204,6 @@ cv_status ensure_trellis_tables(cv_hmm* h) {
     for (int64_t o = 0; o < V; ++o) et[(size_t)o * np + j] = f32(h->b[(size_t)j * V + o]);
   cv_status st;
   if ((st = upload(h->t_aimg, img.data(), img.size() * 4)) != CV_OK) return st;
-  if ((st = upload(h->t_aimg_mfma, img2.data(), img2.size() * 4)) != CV_OK) return st;
   {  // the backward max-plus pass runs the same kernel on a^T with pi = 0
     auto AT = [&](int i, int j) -> float { return A(j, i); };
     std::vector<float> imgT((size_t)np * np);
@@ -507,27 +496,18 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
   if (use_t64 && (st = ensure_t64_tables(h)) != CV_OK) return st;
   const bool t64cp = use_t64 && o.assoc == CV_ASSOC_CP;
 
-  // trellis variant: all-VALU unless the (slower, experimental) MFMA-assisted one is asked for
-  const bool want_mfma = (o.flags & CV_FLAG_MFMA_TRELLIS) || ((o.flags >> 8) & 0xFF);
-  const bool use_mfma = use_trellis && want_mfma && h->np >= 64 && !o.forced;
-  int mt = -1;
-  if (use_mfma) {
-    const int req = (int)((o.flags >> 8) & 0xFF) - 1;
-    mt = req >= 0 ? req : cvk::mfma_default_mt(h->np);
-    if (h->np != 256 && req >= 0 && req != cvk::mfma_default_mt(h->np))
-      return set_err(CV_EUNSUPPORTED, "MFMA tile override is only built for N in (224,256]");
-    if (h->np == 256 && !(mt == 0 || (mt >= 4 && mt <= 8)))
-      return set_err(CV_EINVAL, "MFMA tiles per wave must be 0 or 4..8 (got %d)", mt);
-    if (h->np != 256) mt = cvk::mfma_default_mt(h->np);
-  }
+  // CV_FLAG_MFMA_TRELLIS (bit 0) and the MFMA tile bits 8-15 belonged to the retired
+  // MFMA-assisted f32 trellis (slower than the all-VALU one on gfx950: DESIGN.md §3)
+  if ((o.flags & 0x1u) || ((o.flags >> 8) & 0xFF))
+    return set_err(CV_EUNSUPPORTED, "the MFMA-assisted trellis was retired (flags 0x%x)", o.flags);
   h->last_launches = 0;
   h->last_kernel = use_trellis ? CV_KERNEL_TRELLIS : use_t64 ? CV_KERNEL_TRELLIS_F64 : CV_KERNEL_GENERIC;
   // N <= 64: one wave per sequence, forward and backtrack fused (trellis_wave_f32) on tables
   // padded to npw = 16 * ceil(N / 16); its chunks run back to back on one stream (nothing to
   // overlap)
-  const bool wave = use_trellis && !use_mfma && h->npw > 0 && !(o.flags & CV_FLAG_NO_WAVE);
+  const bool wave = use_trellis && h->npw > 0 && !(o.flags & CV_FLAG_NO_WAVE);
   h->last_np = use_trellis ? (wave ? h->npw : h->np) : use_t64 ? h->np64 : 0;
-  h->last_mt = use_mfma ? mt : -1;
+  h->last_mt = -1;
   if (nseq == 0) return CV_OK;
   HIP_TRY(hipMemsetAsync(status_dev, 0, (size_t)nseq, stream));
 
@@ -550,8 +530,8 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
   static const bool t64_overlap = getenv("CV_T64_OVERLAP") != nullptr;  // A/B knob (bit-identical)
   const bool serial = (o.flags & CV_FLAG_SERIAL) != 0 || wave || (use_t64 && !t64_overlap);
   // Sequences per forward workgroup: 2 (trellis_fwd2_f32, equal-length pairs; default) or 1
-  // (trellis_fwd_f32: leftovers, MFMA, N not a multiple of 64).
-  const bool plain = use_trellis && !use_mfma && !wave && cvk::trellis_pair_supported(h->np);
+  // (trellis_fwd_f32: leftovers, N not a multiple of 64).
+  const bool plain = use_trellis && !wave && cvk::trellis_pair_supported(h->np);
   const int group = (!plain || (o.flags & CV_FLAG_NO_PAIR)) ? 1 : 2;
   static const uint64_t max_chunks = [] {  // A/B knob (bit-identical): pipeline depth
     const char* e = getenv("CV_MAX_CHUNKS");
@@ -687,9 +667,6 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
             make_bt_args(h, wsb, offsets_host, offsets_dev, obs_dev, order_dev, c, path_dev, score_dev, status_dev);
         ba.at = h->w_at.as<float>();
         err = cvk::launch_trellis_wave(h->npw, fa, ba, n, stream);
-      } else if (use_mfma) {
-        fa.a_img = h->t_aimg_mfma.as<float>();
-        err = cvk::launch_trellis_mfma(h->np, mt, fa, n, stream);
       } else {
         const int64_t np2 = pairing ? (varlen ? npair[ci] : n / 2) : 0;
         err = cvk::launch_trellis_fwd2(h->np, fa, np2, stream);
@@ -771,7 +748,7 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
       const cvk::BacktrackArgs ba =
           make_bt_args(h, wsb, offsets_host, offsets_dev, obs_dev, order_dev, c, path_dev, score_dev, status_dev);
       // overlap mode: at most ONE backtrack workgroup (one 64-VGPR wave per SIMD) per CU, so
-      // the next forward workgroup (MFMA: 2 waves x 200 VGPRs per SIMD; VALU: 4 x 104) always
+      // the next forward workgroup (4 waves x 104 VGPRs per SIMD) always
       // finds its registers free: reserve 100 KiB of LDS (2 x 100 > 160 KiB)
       // the last chunk's backtrack has the device to itself: full occupancy
       const int reserve = (serial || ci + 1 == chunks.size()) ? 0 : 100 * 1024;

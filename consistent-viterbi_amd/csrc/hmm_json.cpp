@@ -20,6 +20,14 @@
 namespace cvh {
 namespace {
 
+// product of non-negative dimensions, or -1 when it overflows int64
+int64_t dim_product(const std::vector<int64_t>& dim) {
+  int64_t n = 1;
+  for (auto d : dim)
+    if (__builtin_mul_overflow(n, d, &n)) return -1;
+  return n;
+}
+
 struct Parser {
   const char* p;
   const char* end;
@@ -69,6 +77,9 @@ struct Parser {
       out = -INFINITY;
       return true;
     }
+    // JSON numbers only: strtod alone would also take nan/inf/hex forms serde_json never writes
+    if (p >= end || !(*p == '-' || (*p >= '0' && *p <= '9'))) return fail("expected number");
+    if (*p == '-' && (end - p < 2 || p[1] < '0' || p[1] > '9')) return fail("expected number");
     char* e = nullptr;
     out = strtod(p, &e);
     if (e == p) return fail("expected number");
@@ -113,6 +124,8 @@ struct Parser {
     for (;;) {
       double d;
       if (!number(d)) return false;
+      // a dimension: a non-negative integer (no cast of a huge, fractional or infinite value)
+      if (!(d >= 0 && d <= 2147483647.0) || d != (double)(int64_t)d) return fail("bad dimension");
       out.push_back((int64_t)d);
       if (peek(',')) { ++p; continue; }
       return expect(']');
@@ -152,9 +165,8 @@ struct Parser {
       break;
     }
     if (!have_dim || !have_data) return fail("ndarray missing dim/data");
-    int64_t n = 1;
-    for (auto d : dim) n *= d;
-    if ((int64_t)data.size() != n) return fail("ndarray data length != prod(dim)");
+    const int64_t n = dim_product(dim);
+    if (n < 0 || (int64_t)data.size() != n) return fail("ndarray data length != prod(dim)");
     return true;
   }
   // "b": {"v":1,"dim":[N],"data":[ndarray, ...]}
@@ -256,8 +268,7 @@ bool parse_hmm_json(const std::string& text, HmmJson& out, std::string& err) {
   if ((int64_t)b_data.size() != N) { err = "b must hold N emission arrays"; return false; }
   out.nstates = (int)N;
   out.bdims = N ? b_dims[0] : std::vector<int64_t>{};
-  int64_t V = 1;
-  for (auto d : out.bdims) V *= d;
+  const int64_t V = dim_product(out.bdims);  // == the first emission array's length (checked)
   out.b.assign((size_t)(N * V), 0.0);
   for (int64_t s = 0; s < N; ++s) {
     if (b_dims[s] != out.bdims) { err = "emission arrays differ in shape"; return false; }

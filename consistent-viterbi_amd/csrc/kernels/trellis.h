@@ -169,9 +169,6 @@ hipError_t launch_trellis_fwd(int np, const TrellisFwdArgs& fa, int64_t nseq, hi
 // NP in {64, 128, 192, 256}.
 bool trellis_pair_supported(int np);
 hipError_t launch_trellis_fwd2(int np, const TrellisFwdArgs& fa, int64_t npairs, hipStream_t stream);
-// MFMA-assisted forward (trellis_mfma_f32): A image in the 32x32 MFMA C/D layout; mt < 0 = default.
-hipError_t launch_trellis_mfma(int np, int mt, const TrellisFwdArgs& fa, int64_t nseq, hipStream_t stream);
-int mfma_default_mt(int np);
 hipError_t launch_trellis_bt(int np, const BacktrackArgs& ba, int64_t nseq, hipStream_t stream, int lds_reserve = 0);
 // N <= 64: one wave per sequence, forward + backtrack fused (trellis_wave_f32), the tables
 // padded to npw = trellis_wave_states(N) (16, 32, 48 or 64; 0 = not covered).  fa.a_img = the

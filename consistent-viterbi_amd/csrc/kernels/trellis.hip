@@ -540,202 +540,6 @@ __global__ __launch_bounds__(NP * 4) void trellis_fwd2_f32(TrellisFwdArgs args) 
 }
 
 // ---------------------------------------------------------------------------------
-// trellis_mfma_f32<NP, MT>: the same recurrence with part of the pair adds on the MFMA pipe.
-//
-// v_mfma_f32_32x32x2_f32 computes D = fma(a1,b1, fma(a0,b0, C)) with one rounding per fma
-// (cdna_hip_programming.md §3 "FP32-input MFMA").  With a0 = d[i] (lanes 0-31), b0 = 1,
-// a1 = b1 = 0 (lanes 32-63) and C = the 32x32 transition tile, D[i][j] = fma(d_i, 1, a_ij)
-// = round(d_i + a_ij): bit-identical to the VALU add (no NaN: 0*0 = 0, +inf rejected).
-// The VALU then only takes maxima of those tiles (2 slots/pair -> 1 slot/pair), and does
-// add+max for the remaining TPW-MT tiles, so the matrix and vector pipes run side by side.
-//
-// Layout: wave w owns the 32 columns [32w, 32w+32) for ALL rows, as TPW = NP/32 tiles of
-// 32x32 held in the MFMA C/D register layout (lane l, reg r -> row (r&3) + 8(r>>2) +
-// 4(l>>5) of the tile, column l&31): 16 VGPRs per tile, 128 at NP = 256.  Column maxima
-// need only an in-lane fold and one v_permlane32_swap (no cross-wave partials).
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-
-template <int NP>
-struct MfmaGeom {
-  static constexpr int WAVES = NP / 32;
-  static constexpr int TPW = NP / 32;                 // row tiles per wave
-  static constexpr int LDS_FLOATS = 2 * NP + NP;      // two delta buffers + a zero block
-  static_assert(NP % 32 == 0 && NP >= 64 && NP <= 256, "NP must be a multiple of 32 in [64,256]");
-};
-
-template <int NP, int MT, bool EXT>
-__global__ __launch_bounds__(NP * 2) void trellis_mfma_f32(TrellisFwdArgs args) {
-  using G = MfmaGeom<NP>;
-  constexpr int TPW = G::TPW;
-  static_assert(MT >= 0 && MT <= TPW, "MT tiles per wave on the MFMA pipe");
-  __shared__ __attribute__((aligned(16))) float lds[G::LDS_FLOATS];
-
-  const int lane = threadIdx.x & 63;
-  const int w = threadIdx.x >> 6;
-  const int h = lane >> 5;   // row half inside a tile
-  const int jl = lane & 31;  // column inside the wave's block
-  const int j = 32 * w + jl;
-
-  const int64_t slot = args.seq_begin + blockIdx.x;
-  int64_t seq, e0;
-  int T;
-  seq_range<EXT>(args, slot, seq, e0, T);
-  if (T <= 0) return;
-  const bool rev = EXT && args.reverse;
-  const int ob_step = rev ? -1 : 1;
-  const int64_t ob0 = rev ? e0 + T - 1 : e0;
-  const __attribute__((address_space(4))) int32_t* obs =
-      (const __attribute__((address_space(4))) int32_t*)(args.obs + ob0);
-  const __attribute__((address_space(4))) int32_t* frc =
-      (const __attribute__((address_space(4))) int32_t*)((EXT && args.forced) ? args.forced + ob0 : nullptr);
-  float* __restrict__ drow = (!EXT || args.delta) ? args.delta + (e0 - args.delta_elem_base) * NP + j : nullptr;
-  float* __restrict__ lrow = (EXT && args.last_row) ? args.last_row + (slot - args.seq_begin) * NP + j : nullptr;
-  const float* __restrict__ etj = args.et + j;
-  const unsigned V = (unsigned)args.nobs;
-
-  // transition tiles in the C/D layout: image [w][tile][reg/4][lane][4]
-  f32x16 at[TPW];
-  {
-    const float4* img = reinterpret_cast<const float4*>(args.a_img) + (size_t)w * TPW * 4 * 64 + lane;
-#pragma unroll
-    for (int t = 0; t < TPW; ++t)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const float4 v = img[(t * 4 + q) * 64];
-        at[t][4 * q + 0] = v.x;
-        at[t][4 * q + 1] = v.y;
-        at[t][4 * q + 2] = v.z;
-        at[t][4 * q + 3] = v.w;
-      }
-  }
-  // zero block read by lanes 32-63 as the a1 = 0 MFMA operand
-  for (int i = threadIdx.x; i < NP; i += blockDim.x) lds[2 * NP + i] = 0.f;
-  const float bone = lane < 32 ? 1.0f : 0.0f;  // b0 = 1 (k = 0), b1 = 0 (k = 1)
-
-  unsigned bad = 0;
-  auto obs_s = [&](int t) -> unsigned {
-    const unsigned o = (unsigned)obs[t * ob_step];
-    bad |= (o >= V);
-    return o < V ? o : 0u;
-  };
-  auto frc_s = [&](int t) -> int { return (EXT && frc) ? frc[t * ob_step] : -1; };
-  auto et_row = [&](unsigned o) -> float { return etj[(size_t)o * NP]; };
-
-  {
-    const float e = et_row(obs_s(0));
-    float d0 = args.pi[j] + e;  // hmm.rs:215-218
-    const int f0 = frc_s(0);
-    if (EXT && f0 >= 0 && j != f0) d0 = ninf_f();
-    if (lane < 32) {
-      lds[j] = d0;
-      if (!EXT || drow) drow[0] = d0;
-      if (EXT && lrow && T == 1) lrow[0] = d0;
-    }
-  }
-  int f_next = frc_s(T > 1 ? 1 : 0);
-  unsigned o_next = obs_s(T > 1 ? 1 : 0);
-  float eA = et_row(o_next);
-  o_next = obs_s(T > 2 ? 2 : T - 1);
-  float eB;
-  lds_barrier();
-
-  auto step = [&](int t, float e_use, float& e_pref) {
-    e_pref = et_row(o_next);
-    const int cur = (t - 1) & 1;
-    const float* dbuf = lds + cur * NP;
-    // MFMA a-operand source: d[rb*32 + lane] for lanes 0-31, the zero block for 32-63
-    const float* asrc = lane < 32 ? dbuf + lane : lds + 2 * NP;
-    const float* vsrc = dbuf + 4 * h;  // VALU tiles: rows 8q + 4h + {0..3}
-    float m0 = ninf_f(), m1 = ninf_f(), m2 = ninf_f(), m3 = ninf_f();
-    // Software pipeline: two MFMA results in flight; between an MFMA's issue and the
-    // max over its result the wave runs half a VALU tile (8 adds + 4 max3), so the
-    // matrix and vector pipes overlap.  sched_barrier pins the order (hipcc would
-    // otherwise pad each MFMA->VALU dependency with s_nop).
-    float amf[MT > 0 ? MT : 1];
-#pragma unroll
-    for (int k = 0; k < MT; ++k) amf[k] = asrc[32 * k];
-    constexpr int NV = TPW - MT;  // VALU tiles, processed as 2*NV half tiles
-    auto vhalf = [&](int vh) {    // half tile vh: tile MT + vh/2, quads 2*(vh&1), +1
-      const int t2 = MT + (vh >> 1);
-#pragma unroll
-      for (int qq = 0; qq < 2; ++qq) {
-        const int q = 2 * (vh & 1) + qq;
-        const float4 dv = *reinterpret_cast<const float4*>(vsrc + 32 * t2 + 8 * q);
-        const float s0 = dv.x + at[t2][4 * q + 0];  // viterbi.rs:15
-        const float s1 = dv.y + at[t2][4 * q + 1];
-        const float s2 = dv.z + at[t2][4 * q + 2];
-        const float s3 = dv.w + at[t2][4 * q + 3];
-        if (qq) {
-          m2 = fmaxf(fmaxf(m2, s0), s1);
-          m3 = fmaxf(fmaxf(m3, s2), s3);
-        } else {
-          m0 = fmaxf(fmaxf(m0, s0), s1);
-          m1 = fmaxf(fmaxf(m1, s2), s3);
-        }
-      }
-    };
-    auto dmax = [&](const f32x16& d) {
-      m0 = fmaxf(fmaxf(m0, d[0]), d[1]);
-      m1 = fmaxf(fmaxf(m1, d[2]), d[3]);
-      m2 = fmaxf(fmaxf(m2, d[4]), d[5]);
-      m3 = fmaxf(fmaxf(m3, d[6]), d[7]);
-      m0 = fmaxf(fmaxf(m0, d[8]), d[9]);
-      m1 = fmaxf(fmaxf(m1, d[10]), d[11]);
-      m2 = fmaxf(fmaxf(m2, d[12]), d[13]);
-      m3 = fmaxf(fmaxf(m3, d[14]), d[15]);
-    };
-    f32x16 dA, dB;
-    if constexpr (MT > 0) dA = __builtin_amdgcn_mfma_f32_32x32x2f32(amf[0], bone, at[0], 0, 0, 0);
-    if constexpr (MT > 1) dB = __builtin_amdgcn_mfma_f32_32x32x2f32(amf[1], bone, at[1], 0, 0, 0);
-    __builtin_amdgcn_sched_barrier(0);
-    int vh = 0;
-#pragma unroll
-    for (int k = 0; k < MT; ++k) {
-      if (vh < 2 * NV) {
-        vhalf(vh);
-        ++vh;
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      if (k & 1) {
-        dmax(dB);
-        if (k + 2 < MT) dB = __builtin_amdgcn_mfma_f32_32x32x2f32(amf[k + 2], bone, at[k + 2], 0, 0, 0);
-      } else {
-        dmax(dA);
-        if (k + 2 < MT) dA = __builtin_amdgcn_mfma_f32_32x32x2f32(amf[k + 2], bone, at[k + 2], 0, 0, 0);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    }
-#pragma unroll
-    for (; vh < 2 * NV; ++vh) vhalf(vh);
-    const int f_use = f_next;
-    o_next = obs_s(t + 2 < T ? t + 2 : T - 1);
-    f_next = frc_s(t + 1 < T ? t + 1 : T - 1);
-    float m = fmaxf(fmaxf(m0, m1), fmaxf(m2, m3));
-    m = swap_max(m, false);  // fold the two row halves (lanes l and l+32) of each column
-    float dn = m + e_use;    // (d + a) + b -- viterbi.rs:15-17 association
-    if (EXT && f_use >= 0 && j != f_use) dn = ninf_f();
-    if (lane < 32) {
-      lds[(cur ^ 1) * NP + j] = dn;
-      if (!EXT || drow) drow[(size_t)t * NP] = dn;
-      if (EXT && lrow && t == T - 1) lrow[0] = dn;
-    }
-    lds_barrier();
-  };
-
-  int t = 1;
-  if ((T - 1) & 1) {
-    step(t, eA, eB);
-    eA = eB;
-    ++t;
-  }
-  for (; t + 1 < T; t += 2) {
-    step(t, eA, eB);
-    step(t + 1, eB, eA);
-  }
-  if (bad && lane == 0 && w == 0) args.status[seq] = CVK_SEQ_BADOBS;
-}
-
-// ---------------------------------------------------------------------------------
 // Wave-level first-argmax: (v, i) pairs, larger v wins, ties -> smaller i.
 __device__ __forceinline__ void wave_argmax_first(float& v, int& i) {
 #pragma unroll
@@ -1739,43 +1543,6 @@ hipError_t launch_trellis_fwd(int np, const TrellisFwdArgs& fa, int64_t nseq, hi
 #define CVK_FWD(NP) trellis_fwd_np<NP>(fa, nseq, stream)
   CVK_NP_SWITCH(np, CVK_FWD)
 #undef CVK_FWD
-}
-
-// MFMA-assisted variant: default MFMA tiles per wave = 3/4 of the wave's row tiles
-// (pipe-balance model in DESIGN.md §3); NP = 32 has no MFMA variant.
-int mfma_default_mt(int np) { return (3 * (np / 32) + 2) / 4; }
-
-// The MFMA variant is built for the plain decode only (its EXT instantiation spills at
-// NP = 256); forced / ranged / reversed passes use the VALU kernel (launch_trellis_fwd).
-template <int NP, int MT>
-static hipError_t mfma_np(const TrellisFwdArgs& fa, int64_t nseq, hipStream_t stream) {
-  if (ext_args(fa)) return hipErrorInvalidValue;
-  hipLaunchKernelGGL((trellis_mfma_f32<NP, MT, false>), dim3((unsigned)nseq), dim3(NP * 2), 0, stream, fa);
-  return hipGetLastError();
-}
-
-hipError_t launch_trellis_mfma(int np, int mt, const TrellisFwdArgs& fa, int64_t nseq, hipStream_t stream) {
-  if (nseq <= 0) return hipSuccess;
-  if (mt < 0) mt = mfma_default_mt(np);
-  switch (np) {
-    case 64: return mfma_np<64, 2>(fa, nseq, stream);
-    case 96: return mfma_np<96, 2>(fa, nseq, stream);
-    case 128: return mfma_np<128, 3>(fa, nseq, stream);
-    case 160: return mfma_np<160, 4>(fa, nseq, stream);
-    case 192: return mfma_np<192, 5>(fa, nseq, stream);
-    case 224: return mfma_np<224, 5>(fa, nseq, stream);
-    case 256:
-      switch (mt) {
-        case 0: return mfma_np<256, 0>(fa, nseq, stream);
-        case 4: return mfma_np<256, 4>(fa, nseq, stream);
-        case 5: return mfma_np<256, 5>(fa, nseq, stream);
-        case 6: return mfma_np<256, 6>(fa, nseq, stream);
-        case 7: return mfma_np<256, 7>(fa, nseq, stream);
-        case 8: return mfma_np<256, 8>(fa, nseq, stream);
-        default: return hipErrorInvalidValue;
-      }
-    default: return hipErrorInvalidValue;
-  }
 }
 
 hipError_t launch_trellis_bt(int np, const BacktrackArgs& ba, int64_t nseq, hipStream_t stream, int lds_reserve) {

@@ -186,8 +186,8 @@ __global__ __launch_bounds__(64) void trellis_fwd_f64(T64FwdArgs g) {
   {
     const unsigned long long live = __ballot(my_T > 0);
     const int l0 = __builtin_ctzll(live);  // Tmax > 0: some lane is live
-    const int64_t eb0 = (int64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)my_eb, l0) |
-                        ((int64_t)__builtin_amdgcn_readlane((int)(my_eb >> 32), l0) << 32);
+    const int64_t eb0 = (int64_t)((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)my_eb, l0) |
+                                  ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(my_eb >> 32), l0) << 32));
     if (my_T <= 0) my_eb = eb0;
   }
   const int my_Tc = my_T > 0 ? my_T : 1;
@@ -219,8 +219,8 @@ __global__ __launch_bounds__(64) void trellis_fwd_f64(T64FwdArgs g) {
     if (g.delta && t < T[s]) {
       // split-plane row (see T64 row layout in trellis64.h): hi words [0, NP), lo words
       // [NP, 2 NP); streaming stores (read once, by the backtrack)
-      const int64_t r = (int64_t)__builtin_amdgcn_readlane((int)(uint32_t)my_rb, s) |
-                        ((int64_t)__builtin_amdgcn_readlane((int)(my_rb >> 32), s) << 32);
+      const int64_t r = (int64_t)((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)my_rb, s) |
+                                  ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(my_rb >> 32), s) << 32));
       uint32_t* dst = reinterpret_cast<uint32_t*>(g.delta) + (r + t) * (2 * NP) + j0;
       store_split<C>(dst, dst + NP, v);
     }

@@ -20,15 +20,11 @@ SEQ_OK, SEQ_INFEASIBLE, SEQ_EMPTY, SEQ_BADOBS = 0, 1, 2, 3
 DTYPE_F32, DTYPE_F64 = 0, 1
 ASSOC_VITERBI, ASSOC_CP, ASSOC_DP, ASSOC_DECODE = 0, 1, 2, 3
 KERNEL_AUTO, KERNEL_TRELLIS, KERNEL_GENERIC, KERNEL_TRELLIS_F64 = 0, 1, 2, 3
-FLAG_MFMA_TRELLIS = 0x1
 FLAG_NO_PAIR = 0x4
 FLAG_NO_WAVE = 0x8
 FLAG_NO_T64 = 0x10
 FLAG_SERIAL = 0x2
 
-
-def FLAG_MFMA_TILES(n):
-    return (n + 1) << 8
 
 # every symbol include/cviterbi.h declares (checked by tests/test_abi.py)
 EXPORTS = [

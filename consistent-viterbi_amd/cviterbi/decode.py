@@ -29,28 +29,24 @@ def _p(x):
 
 
 def make_opts(dtype="f64", assoc="viterbi", kernel="auto", rescore_f64=True, stream=None, workspace_bytes=0,
-              variant=None, mfma_tiles=None, serial=False):
-    """variant: None/"valu" (all-VALU trellis, two equal-length sequences per workgroup where
+              variant=None, serial=False):
+    """variant: None/"valu" (f32 trellis: two equal-length sequences per workgroup where
     N % 64 == 0, default; for N <= 64 one wave per sequence with the backtrack fused),
-    "nowave" (the workgroup kernels at N <= 64), "valu1" (one sequence per workgroup) or
-    "mfma" (MFMA-assisted, slower) -- all bit-identical;
-    mfma_tiles: tuning override of the MFMA tiles per wave (bit-identical results);
-    serial: no forward/backtrack stream overlap."""
+    "nowave" (the workgroup kernels at N <= 64) or "valu1" (one sequence per workgroup) --
+    all bit-identical; serial: no forward/backtrack stream overlap."""
     flags = L.FLAG_SERIAL if serial else 0
-    if variant == "mfma":
-        flags |= L.FLAG_MFMA_TRELLIS
-    elif variant == "valu1":
+    if variant == "valu1":
         flags |= L.FLAG_NO_PAIR | L.FLAG_NO_WAVE
     elif variant == "nowave":
         flags |= L.FLAG_NO_WAVE
-    if mfma_tiles is not None:
-        flags |= L.FLAG_MFMA_TILES(mfma_tiles)
+    elif variant not in (None, "valu"):
+        raise ValueError(f"unknown variant {variant!r}")
     return L.opts(_DT.get(dtype, dtype), _ASSOC.get(assoc, assoc), _KERNEL.get(kernel, kernel), rescore_f64, stream,
                   workspace_bytes, flags)
 
 
 def decode_batch(hmm: HMM, offsets, obs, dtype="f64", assoc="viterbi", kernel="auto", rescore_f64=True,
-                 workspace_bytes=0, variant=None, mfma_tiles=None, serial=False, forced=None):
+                 workspace_bytes=0, variant=None, serial=False, forced=None):
     """Decode CSR sequences (offsets[B+1], flat obs) -> (path int32[sum T], score f64[B], status u8[B]).
     forced[sum T] (optional): -1 free, s >= 0 forces state s at that element."""
     offsets = np.ascontiguousarray(offsets, np.int64)
@@ -60,7 +56,7 @@ def decode_batch(hmm: HMM, offsets, obs, dtype="f64", assoc="viterbi", kernel="a
     path = np.zeros(max(total, 0), np.int32)
     score = np.zeros(max(nseq, 0), np.float64)
     status = np.zeros(max(nseq, 0), np.uint8)
-    o = make_opts(dtype, assoc, kernel, rescore_f64, None, workspace_bytes, variant, mfma_tiles, serial)
+    o = make_opts(dtype, assoc, kernel, rescore_f64, None, workspace_bytes, variant, serial)
     if forced is not None:
         forced = np.ascontiguousarray(forced, np.int32)
         o.forced = forced.ctypes.data
@@ -162,7 +158,7 @@ def decode_forced_components(hmm: HMM, offsets, obs, component, comp_state, resc
 
 def decode_batch_device(hmm: HMM, offsets_dev, obs_dev, path_dev, score_dev, status_dev, offsets_host=None,
                         dtype="f64", assoc="viterbi", kernel="auto", rescore_f64=True, stream=None,
-                        workspace_bytes=0, variant=None, mfma_tiles=None, serial=False):
+                        workspace_bytes=0, variant=None, serial=False):
     """Device-pointer decode (ints or objects with data_ptr(), e.g. torch tensors); async on `stream`."""
     def ptr(x):
         if x is None:
@@ -173,7 +169,7 @@ def decode_batch_device(hmm: HMM, offsets_dev, obs_dev, path_dev, score_dev, sta
     oh = None
     if offsets_host is not None:
         oh = np.ascontiguousarray(offsets_host, np.int64)
-    o = make_opts(dtype, assoc, kernel, rescore_f64, stream, workspace_bytes, variant, mfma_tiles, serial)
+    o = make_opts(dtype, assoc, kernel, rescore_f64, stream, workspace_bytes, variant, serial)
     L.check(L.lib().cv_decode_batch_device(hmm.handle, nseq, _p(oh) if oh is not None else None, ptr(offsets_dev),
                                            ptr(obs_dev), ctypes.byref(o), ptr(path_dev), ptr(score_dev),
                                            ptr(status_dev)))
@@ -262,7 +258,7 @@ def last_timing(hmm: HMM) -> dict:
     L.check(L.lib().cv_last_timing(hmm.handle, ctypes.byref(t)))
     return dict(fwd_ms=t.fwd_ms, bt_ms=t.bt_ms, total_ms=t.total_ms, launches=t.launches,
                 kernel={1: "trellis", 2: "generic", 3: "trellis_f64"}.get(t.kernel, "none"), padded_states=t.padded_states,
-                mfma_tiles=t.mfma_tiles)
+                seqs_per_wave=t.mfma_tiles)
 
 
 def decode(sequence, hmm: HMM):

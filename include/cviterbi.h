@@ -63,19 +63,14 @@ enum { CV_ASSOC_VITERBI = 0, CV_ASSOC_CP = 1, CV_ASSOC_DP = 2, CV_ASSOC_DECODE =
 enum { CV_KERNEL_AUTO = 0, CV_KERNEL_TRELLIS = 1, CV_KERNEL_GENERIC = 2, CV_KERNEL_TRELLIS_F64 = 3 };
 
 /* cv_opts.flags */
-/* MFMA-assisted trellis (64 <= N <= 256) instead of the all-VALU one.  Bit-identical, but
- * SLOWER on gfx950: f32 MFMA does not co-execute with VALU work on a SIMD
- * (profiles/r01_mfma_overlap.txt), so it is kept as an experiment only. */
-#define CV_FLAG_MFMA_TRELLIS 0x1u
+/* bit 0 and bits 8-15 are reserved (they selected the retired MFMA-assisted f32 trellis,
+ * measured slower than the all-VALU one on gfx950; setting them is CV_EUNSUPPORTED) */
 #define CV_FLAG_SERIAL 0x2u       /* one stream, fewest chunks: no forward/backtrack overlap */
 #define CV_FLAG_NO_PAIR 0x4u      /* one sequence per forward workgroup (A/B knob; bit-identical) */
 #define CV_FLAG_NO_WAVE 0x8u      /* N <= 64: the workgroup kernels instead of one wave per sequence
                                      with the backtrack fused (A/B knob; bit-identical) */
 #define CV_FLAG_NO_T64 0x10u     /* f64: the generic kernel instead of TRELLIS_F64 (A/B knob;
                                      bit-identical) */
-/* MFMA tiles per wave per step for the MFMA-assisted kernel (implies it; N in (224,256]:
- * 0, 4..8; default 6).  Results are bit-identical for every value. */
-#define CV_FLAG_MFMA_TILES(n) ((uint32_t)((n) + 1) << 8)
 
 typedef struct cv_hmm cv_hmm;
 typedef struct cv_solver cv_solver;
@@ -115,8 +110,8 @@ typedef struct cv_timing {
   int64_t launches;      /* forward launches (chunks) */
   int32_t kernel;        /* CV_KERNEL_TRELLIS, _TRELLIS_F64 or _GENERIC actually used */
   int32_t padded_states; /* NP of the trellis kernel (0 for generic) */
-  int32_t mfma_tiles;    /* MFMA tiles per wave of the trellis kernel, -1 = all-VALU kernel;
-                            TRELLIS_F64: sequences per forward wave (last chunk) */
+  int32_t mfma_tiles;    /* TRELLIS_F64: sequences per forward wave (last chunk); -1 otherwise
+                            (the field name is kept for ABI stability) */
 } cv_timing;
 
 typedef struct cv_superseq_desc {

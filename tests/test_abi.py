@@ -111,7 +111,16 @@ def test_json_written_by_serde_style(tmp_path):
 
 @pytest.mark.parametrize("bad,code", [("{", L.CV_EPARSE), ('{"a":1}', L.CV_EPARSE),
                                       ('{"a":{"v":1,"dim":[2,2],"data":[1,2,3]},"b":{"dim":[0],"data":[]},'
-                                       '"pi":{"v":1,"dim":[2],"data":[0,0]}}', L.CV_EPARSE)])
+                                       '"pi":{"v":1,"dim":[2],"data":[0,0]}}', L.CV_EPARSE),
+                                      # dims: overflowing product, fractional, negative, huge
+                                      ('{"a":{"v":1,"dim":[99999999999,99999999999],"data":[]}}', L.CV_EPARSE),
+                                      ('{"a":{"v":1,"dim":[1.5,2],"data":[1,2,3]}}', L.CV_EPARSE),
+                                      ('{"a":{"v":1,"dim":[-1,2],"data":[]}}', L.CV_EPARSE),
+                                      ('{"a":{"v":1,"dim":[1e300],"data":[]}}', L.CV_EPARSE),
+                                      # non-JSON number forms strtod would accept
+                                      ('{"a":{"v":1,"dim":[1,1],"data":[nan]}}', L.CV_EPARSE),
+                                      ('{"a":{"v":1,"dim":[1,1],"data":[0x10]}}', L.CV_EPARSE),
+                                      ('{"a":{"v":1,"dim":[1,1],"data":[inf]}}', L.CV_EPARSE)])
 def test_json_errors(tmp_path, bad, code):
     p = tmp_path / "bad.json"
     p.write_text(bad)

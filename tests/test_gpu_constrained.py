@@ -14,7 +14,7 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.mark.parametrize("n", [5, 45, 64, 200, 256])
-@pytest.mark.parametrize("variant", ["valu", "nowave", "valu1", "mfma"])
+@pytest.mark.parametrize("variant", ["valu", "nowave", "valu1"])
 def test_forced_decode_bit_exact(gpu, n, variant):
     pi, a, b = synth.random_hmm(n, 19, seed=n)
     rng = np.random.default_rng(n)

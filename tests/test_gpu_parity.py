@@ -52,19 +52,17 @@ def test_trellis_f32_bit_exact(gpu, n):
 
 
 @pytest.mark.parametrize("n", [40, 64, 100, 128, 160, 200, 224, 256])
-@pytest.mark.parametrize("variant", ["valu", "valu1", "mfma"])
+@pytest.mark.parametrize("variant", ["valu", "valu1"])
 @pytest.mark.parametrize("serial", [False, True])
 def test_trellis_variants_bit_exact(gpu, n, variant, serial):
-    """All trellis variants (all-VALU with 2 or 1 sequences per workgroup; MFMA-assisted, whose MFMA tiles compute
-    fma(d, 1, a) = d + a exactly) and both schedules (pipelined chunks / serial) give the
-    oracle's f32 result bit for bit."""
+    """Both f32 trellis variants (2 or 1 sequences per workgroup) and both schedules
+    (pipelined chunks / serial) give the oracle's f32 result bit for bit."""
     pi, a, b, off, obs = _case(n, 29, seed=300 + n, nseq=30, tmax=50, zero_frac=0.03)
     h = cv.HMM(pi, a, b)
     ref = O.decode_batch(pi, a, b, off, obs, O.VITERBI, np.float32)
     got = cv.decode_batch(h, off, obs, rescore_f64=False, variant=variant, serial=serial,
                           workspace_bytes=0 if serial else 256 * 4 * 300, dtype="f32")
-    t = cv.last_timing(h)
-    assert (t["mfma_tiles"] >= 0) == (variant == "mfma" and t["padded_states"] >= 64)
+    assert cv.last_timing(h)["kernel"] == "trellis"
     _assert_same(got, ref, f"{variant} N={n} serial={serial}")
 
 
@@ -117,13 +115,23 @@ def test_wave_kernel_small_n(gpu, n, serial):
             assert score[s] == O.rescore_f64(pi, a, b, obs[lo:hi], path[lo:hi])
 
 
-@pytest.mark.parametrize("mt", [0, 4, 5, 6, 7, 8])
-def test_mfma_tile_counts_bit_exact(gpu, mt):
-    pi, a, b, off, obs = _case(256, 31, seed=77, nseq=12, tmax=60, zero_frac=0.02)
+def test_retired_mfma_flags_rejected(gpu):
+    """The MFMA-assisted f32 trellis was retired (slower than the all-VALU one, DESIGN.md
+    §3): its flag bits are reserved and rejected."""
+    import ctypes
+    from cviterbi import _lib as L
+    from cviterbi.decode import make_opts
+    pi, a, b, off, obs = _case(64, 9, seed=1, nseq=2, tmax=5)
     h = cv.HMM(pi, a, b)
-    got = cv.decode_batch(h, off, obs, rescore_f64=False, mfma_tiles=mt, dtype="f32")
-    assert cv.last_timing(h)["mfma_tiles"] == mt
-    _assert_same(got, O.decode_batch(pi, a, b, off, obs, O.VITERBI, np.float32), f"mt={mt}")
+    for flags in (0x1, 7 << 8):
+        o = make_opts("f32")
+        o.flags = flags
+        path, score, status = np.zeros(int(off[-1]), np.int32), np.zeros(2), np.zeros(2, np.uint8)
+        st = L.lib().cv_decode_batch(h.handle, 2, off.ctypes.data_as(ctypes.c_void_p),
+                                     np.ascontiguousarray(obs, np.int32).ctypes.data_as(ctypes.c_void_p),
+                                     ctypes.byref(o), path.ctypes.data_as(ctypes.c_void_p),
+                                     score.ctypes.data_as(ctypes.c_void_p), status.ctypes.data_as(ctypes.c_void_p))
+        assert st == L.CV_EUNSUPPORTED
 
 
 @pytest.mark.parametrize("dtype", ["f32", "f64"])

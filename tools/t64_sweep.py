@@ -39,4 +39,4 @@ for serial in (False, True):
     t = cv.last_timing(h)
     print(json.dumps({"S": os.environ.get("CV_T64_S", "auto"), "serial": serial, "nseq": B, "ms": dt * 1e3,
                       "fwd_ms": t["fwd_ms"], "bt_ms": t["bt_ms"], "launches": t["launches"],
-                      "spw": t["mfma_tiles"]}), flush=True)
+                      "spw": t["seqs_per_wave"]}), flush=True)

@@ -22,13 +22,6 @@ VARIANTS = [
     dict(name="valu1-overlap", variant="valu1", serial=False),
     dict(name="valu-serial", variant="valu", serial=True),
     dict(name="valu-overlap", variant="valu", serial=False),
-    dict(name="mfma0-serial", mfma_tiles=0, serial=True),
-    dict(name="mfma4-serial", mfma_tiles=4, serial=True),
-    dict(name="mfma5-serial", mfma_tiles=5, serial=True),
-    dict(name="mfma6-serial", mfma_tiles=6, serial=True),
-    dict(name="mfma7-serial", mfma_tiles=7, serial=True),
-    dict(name="mfma8-serial", mfma_tiles=8, serial=True),
-    dict(name="mfma6-overlap", mfma_tiles=6, serial=False),
 ]
 if os.environ.get("TUNE_ONLY"):
     keep = os.environ["TUNE_ONLY"].split(",")
@@ -67,12 +60,12 @@ for r in range(ROUNDS + 1):
             for x, y in zip(out, ref):
                 assert np.array_equal(x, y), f"variant {v['name']} differs"
         if r > 0:
-            res[v["name"]].append((wall, t["fwd_ms"], t["bt_ms"], t["launches"], t["mfma_tiles"], t["total_ms"]))
+            res[v["name"]].append((wall, t["fwd_ms"], t["bt_ms"], t["launches"], t["seqs_per_wave"], t["total_ms"]))
 summary = {}
 for name, rows in res.items():
     a = np.array(rows)
     summary[name] = dict(wall_ms=float(np.median(a[:, 0])), fwd_ms=float(np.median(a[:, 1])),
-                         bt_ms=float(np.median(a[:, 2])), total_ms=float(np.median(a[:, 5])), launches=int(a[0, 3]), mfma_tiles=int(a[0, 4]))
+                         bt_ms=float(np.median(a[:, 2])), total_ms=float(np.median(a[:, 5])), launches=int(a[0, 3]), seqs_per_wave=int(a[0, 4]))
     print(f"{name:16s} wall {summary[name]['wall_ms']:8.2f} ms  fwd {summary[name]['fwd_ms']:8.2f}  "
           f"bt {summary[name]['bt_ms']:7.2f}  gpu-total {summary[name]['total_ms']:7.2f}  launches {summary[name]['launches']}", flush=True)
 print(json.dumps(dict(B=B, rounds=ROUNDS, results=summary)))
