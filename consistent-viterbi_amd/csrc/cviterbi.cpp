@@ -123,6 +123,8 @@ struct cv_hmm {
   int np64 = 0;
   bool t64_ready = false;
   DevBuf q_a, q_at, q_pi, q_et;
+  DevBuf q_at32;            // f32(a^T), uploaded when t64_nonpos
+  bool t64_nonpos = false;  // every finite pi/a/b entry in [-2^80, 0] (NONPOS backtrack test)
   DevBuf q_pi0;  // the reversed (suffix) pass: pi = 0 for the N states, -inf padding
   // f32 generic tables
   bool g32_ready = false;
@@ -283,6 +285,23 @@ cv_status ensure_t64_tables(cv_hmm* h) {
   std::vector<double> pi0(NP, ninf);
   for (int i = 0; i < N; ++i) pi0[i] = 0.0;
   if ((st = upload(h->q_pi0, pi0.data(), pi0.size() * 8)) != CV_OK) return st;
+  // NONPOS backtrack test (trellis64.hip bt_chain_f64): log-probability models only; the
+  // CV_T64_NONPOS=0 knob forces the general f64 interval test (same paths, bit for bit)
+  static const bool nonpos_knob = [] {
+    const char* e = getenv("CV_T64_NONPOS");
+    return !(e && e[0] == '0');
+  }();
+  auto nonpos = [](const std::vector<double>& v) {
+    for (double x : v)
+      if (std::isfinite(x) && !(x <= 0.0 && x >= -0x1p80)) return false;
+    return true;
+  };
+  h->t64_nonpos = nonpos_knob && nonpos(h->pi) && nonpos(h->a) && nonpos(h->b);
+  if (h->t64_nonpos) {
+    std::vector<float> at32(at.size());
+    for (size_t k = 0; k < at.size(); ++k) at32[k] = (float)at[k];
+    if ((st = upload(h->q_at32, at32.data(), at32.size() * 4)) != CV_OK) return st;
+  }
   h->np64 = NP;
   h->t64_ready = true;
   return CV_OK;
@@ -786,6 +805,7 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
       ba.decode_bt = o.assoc == CV_ASSOC_DECODE ? 1 : 0;
       ba.obs = obs_dev;
       ba.et = h->q_et.as<double>();
+      ba.at32 = h->t64_nonpos ? h->q_at32.as<float>() : nullptr;
       err = cvk::launch_t64_bt(h->np64, ba, n, bts);
     } else if (o.dtype == CV_DTYPE_F64) {
       cvk::GenericBtArgs<double> ba{};

@@ -52,6 +52,8 @@ struct T64BtArgs {
                            // argmax 0, bt = 0 where the emission is -inf (viterbi.rs:19-30)
   const int32_t* obs;      // dp_assoc / decode_bt: observations, emissions [V][NP]
   const double* et;
+  const float* at32;       // f32(a^T) [NP][NP], set only for models whose finite entries are
+                           // all in [-2^80, 0]: the NONPOS interval test (null: f64 test)
 };
 
 // Delta rows of the f64 trellis (forward -> backtrack, resume-flow prefix rows) use a

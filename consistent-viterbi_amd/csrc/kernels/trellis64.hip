@@ -532,6 +532,24 @@ __device__ __forceinline__ double wave_max_d(double v) {
   return v;
 }
 
+// wave-wide f32 max through DPP (no LDS round trips): within each row of 16 lanes by quad
+// permutes and mirrors, then rows combined by the gfx9 row broadcasts; lane 63 holds the
+// maximum of all 64 lanes.  -fno-honor-nans: callers pass no NaN.
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ float max_dpp(float v) {
+  const int o = __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, v), __builtin_bit_cast(int, v), CTRL, ROWMASK, 0xF, false);
+  return __builtin_fmaxf(v, __builtin_bit_cast(float, o));
+}
+__device__ __forceinline__ float wave_max_f32(float v) {
+  v = max_dpp<0xB1, 0xF>(v);   // quad_perm [1,0,3,2]
+  v = max_dpp<0x4E, 0xF>(v);   // quad_perm [2,3,0,1]
+  v = max_dpp<0x141, 0xF>(v);  // row_half_mirror
+  v = max_dpp<0x140, 0xF>(v);  // row_mirror: every lane of a row holds the row max
+  v = max_dpp<0x142, 0xA>(v);  // row_bcast:15 -> rows 1, 3
+  v = max_dpp<0x143, 0xC>(v);  // row_bcast:31 -> rows 2, 3
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 63));
+}
+
 // first index of the wave-wide maximum of s (candidate i = lane + 64k; invalid k excluded)
 template <int KP>
 __device__ __forceinline__ int first_argmax_d(const double (&s)[KP], const bool (&valid)[KP], double& M) {
@@ -565,10 +583,25 @@ __device__ __forceinline__ int first_argmax_d(const double (&s)[KP], const bool 
 // DEC (viterbi::decode, infeasible sequences only): bt = 0 where the emission of the current
 // state is -inf (viterbi.rs:19-21); on a feasible path every emission is finite, so the rule
 // never changes a feasible decode.
-template <int KP, int PF, bool DEC = false>
+//
+// NONPOS (models whose finite log-probabilities are all in [-2^80, 0], the bench path; row-A0
+// association): every candidate is <= 0, so the error of its estimate is RELATIVE to the
+// estimate itself and the interval test collapses to one threshold on f32 estimates
+//   x_i = f32(hi_i) + at32[cur][i]      (f32 a^T table, round to nearest)
+//   |s_i - x_i| <= c |x_i|,  c = 1.25 * 2^-20:  hi truncation |h| 2^-20, the f32 roundings of
+//   h, a and their sum (2^-24 each), the f64 rounding of s (2^-53); |h|, |a| <= |x| as all
+//   three are <= 0; f32 flushes of subnormals stay below the 2^-100 floor
+//   survivors: x_i >= M (1 + 3 * 2^-20) - 2^-100, M = max_k x_k
+// since s_i* >= s_k >= M (1 + c) and s_i* <= x_i* (1 - c) give x_i* >= M (1 + c) / (1 - c),
+// with (1 + c) / (1 - c) < 1 + 2.6 * 2^-20 and the f32 rounding of the threshold (2^-24 |M|)
+// inside the remaining slack.  Half the L2 bytes of the f64 a^T column, a DPP wave max in
+// place of six ds_bpermute rounds, and no per-candidate bound arithmetic.  |x| < 2^112 for
+// T < 2^31, so no estimate overflows f32.
+template <int KP, int PF, bool DEC = false, bool NONPOS = false>
 __device__ __forceinline__ void bt_chain_f64(const uint32_t* __restrict__ rows, int T, int cur, int32_t* __restrict__ path,
                                              const double* __restrict__ at, const double* __restrict__ et,
-                                             const int32_t* __restrict__ obs, int dp_assoc, int N, int lane) {
+                                             const int32_t* __restrict__ obs, int dp_assoc, int N, int lane,
+                                             const float* __restrict__ at32 = nullptr) {
   constexpr int NP = 64 * KP;
   constexpr uint32_t NINF_HI = 0xFFF00000u;  // hi word of -inf (lo word 0)
   bool valid[KP];
@@ -596,6 +629,41 @@ __device__ __forceinline__ void bt_chain_f64(const uint32_t* __restrict__ rows, 
       const int t = base - u;
       if (DEC && t >= 1 && !(et[(size_t)obs[t] * NP + cur] > ninf_d())) {
         cur = 0;
+        const int tp = t - 1;
+        if (lane == (tp & 63)) pathreg = cur;
+        if ((tp & 63) == 0 && tp + lane < T) path[tp + lane] = pathreg;
+      } else if (NONPOS && t >= 1) {
+        const float* acol32 = at32 + (size_t)cur * NP + lane;
+        float x[KP];
+        float lm = -__builtin_inff();
+#pragma unroll
+        for (int k = 0; k < KP; ++k) {
+          // padded candidates: hi word -inf, at32 -inf
+          x[k] = (float)from_words(ring[u][k], 0u) + acol32[64 * k];
+          lm = __builtin_fmaxf(lm, x[k]);
+        }
+        const float M = wave_max_f32(lm);
+        const float thr = M * (1.0f + 0x3p-20f) - 0x1p-100f;
+        int cnt = 0, idx = 0;
+#pragma unroll
+        for (int k = KP - 1; k >= 0; --k) {
+          const unsigned long long mask = __ballot(x[k] >= thr);
+          cnt += __builtin_popcountll(mask);
+          if (mask) idx = 64 * k + __builtin_ctzll(mask);
+        }
+        if (cnt == 1) {
+          cur = idx;
+        } else {  // near tie: the exact f64 sums of this row decide (first index)
+          const double* acol = at + (size_t)cur * NP + lane;
+          uint32_t lw[KP];
+          load_lo(t - 1, lw);
+          double sx[KP];
+#pragma unroll
+          for (int k = 0; k < KP; ++k)
+            sx[k] = valid[k] ? from_words(ring[u][k], lw[k]) + acol[64 * k] : ninf_d();
+          double Md;
+          cur = first_argmax_d<KP>(sx, valid, Md);
+        }
         const int tp = t - 1;
         if (lane == (tp & 63)) pathreg = cur;
         if ((tp & 63) == 0 && tp + lane < T) path[tp + lane] = pathreg;
@@ -653,7 +721,10 @@ __device__ __forceinline__ void bt_chain_f64(const uint32_t* __restrict__ rows, 
   }
 }
 
-template <int KP, int PF>
+// NONPOS: the kernel holds only the NONPOS chain (fewer VGPRs, more waves per SIMD); the
+// host launches it for row-A0 decodes without the viterbi::decode infeasible rule when
+// g.at32 is set.
+template <int KP, int PF, bool NONPOS = false>
 __global__ __launch_bounds__(256) void backtrack_f64(T64BtArgs g) {
   constexpr int NP = 64 * KP;
   const int lane = threadIdx.x & 63;
@@ -689,7 +760,7 @@ __global__ __launch_bounds__(256) void backtrack_f64(T64BtArgs g) {
   }
   const uint8_t prior = g.status[seq];
   if (!(bv > ninf_d()) || prior == CVK_SEQ_BADOBS) {
-    if (g.decode_bt && prior != CVK_SEQ_BADOBS)  // viterbi.rs:24-30: from argmax 0 (= cur) through bt
+    if (!NONPOS && g.decode_bt && prior != CVK_SEQ_BADOBS)  // viterbi.rs:24-30: from argmax 0 (= cur) through bt
       bt_chain_f64<KP, PF, true>(rows, T, cur, path, g.at, g.et, g.obs + e0, 0, N, lane);
     else
       for (int t = lane; t < T; t += 64) path[t] = 0;
@@ -699,7 +770,10 @@ __global__ __launch_bounds__(256) void backtrack_f64(T64BtArgs g) {
     }
     return;
   }
-  bt_chain_f64<KP, PF>(rows, T, cur, path, g.at, g.et, g.obs + e0, g.dp_assoc, N, lane);
+  if constexpr (NONPOS)
+    bt_chain_f64<KP, PF, false, true>(rows, T, cur, path, g.at, g.et, g.obs + e0, 0, N, lane, g.at32);
+  else
+    bt_chain_f64<KP, PF>(rows, T, cur, path, g.at, g.et, g.obs + e0, g.dp_assoc, N, lane);
   if (lane == 0) {
     g.score[seq] = bv;
     g.status[seq] = CVK_SEQ_OK;
@@ -837,16 +911,22 @@ hipError_t launch_t64_fwd(int np, int s, const T64FwdArgs& fa, int64_t nseq, hip
   }
 }
 
-template <int PF>
-hipError_t bt_pf(int np, const T64BtArgs& ba, dim3 grid, dim3 block, hipStream_t stream) {
+template <int PF, bool NONPOS>
+hipError_t bt_pf_np(int np, const T64BtArgs& ba, dim3 grid, dim3 block, hipStream_t stream) {
   switch (np) {
-    case 64: hipLaunchKernelGGL((backtrack_f64<1, PF>), grid, block, 0, stream, ba); break;
-    case 128: hipLaunchKernelGGL((backtrack_f64<2, PF>), grid, block, 0, stream, ba); break;
-    case 192: hipLaunchKernelGGL((backtrack_f64<3, PF>), grid, block, 0, stream, ba); break;
-    case 256: hipLaunchKernelGGL((backtrack_f64<4, PF>), grid, block, 0, stream, ba); break;
+    case 64: hipLaunchKernelGGL((backtrack_f64<1, PF, NONPOS>), grid, block, 0, stream, ba); break;
+    case 128: hipLaunchKernelGGL((backtrack_f64<2, PF, NONPOS>), grid, block, 0, stream, ba); break;
+    case 192: hipLaunchKernelGGL((backtrack_f64<3, PF, NONPOS>), grid, block, 0, stream, ba); break;
+    case 256: hipLaunchKernelGGL((backtrack_f64<4, PF, NONPOS>), grid, block, 0, stream, ba); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
+}
+
+template <int PF>
+hipError_t bt_pf(int np, const T64BtArgs& ba, dim3 grid, dim3 block, hipStream_t stream) {
+  if (ba.at32 && !ba.dp_assoc && !ba.decode_bt) return bt_pf_np<PF, true>(np, ba, grid, block, stream);
+  return bt_pf_np<PF, false>(np, ba, grid, block, stream);
 }
 
 hipError_t launch_t64_bt(int np, const T64BtArgs& ba, int64_t nseq, hipStream_t stream) {

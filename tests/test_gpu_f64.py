@@ -85,6 +85,36 @@ def test_t64_ties_and_infeasible(gpu, n, assoc):
             cv.decode_batch(h, off, obs_bad, dtype="f64", kernel=kernel, rescore_f64=False)
 
 
+@pytest.mark.parametrize("n", [64, 200, 256])
+@pytest.mark.parametrize("kind", ["near_ties", "positive", "huge"])
+def test_t64_backtrack_interval_paths(gpu, n, kind):
+    """The backtrack's two interval tests (trellis64.hip bt_chain_f64).  near_ties: a log-prob
+    model whose transitions differ below f32 resolution (1e-12 perturbations of a quantised
+    matrix), so the NONPOS f32 test finds several survivors at most steps and the exact f64
+    fallback decides; positive / huge: a model with an entry > 0, or one below -2^80 -- the
+    NONPOS test does not apply and the general f64 interval test runs."""
+    rng = np.random.default_rng(900 + n)
+    v = 17
+    pi = np.round(rng.uniform(-2, 0, n) * 4) / 4
+    a = np.round(rng.uniform(-2, 0, (n, n)) * 4) / 4
+    b = np.round(rng.uniform(-2, 0, (n, v)) * 4) / 4
+    if kind == "near_ties":
+        a = a - rng.uniform(0, 1e-12, (n, n))
+        b = b - rng.uniform(0, 1e-12, (n, v))
+    elif kind == "positive":
+        a = a + 0.75  # some transitions > 0: scores, not log-probabilities
+    else:
+        a[rng.random((n, n)) < 0.02] = -1e30
+    lengths = np.array([1, 2, 17, 40, 5, 33, 60, 12, 64, 65, 128, 3])
+    off = synth.offsets_from_lengths(lengths)
+    obs = rng.integers(0, v, size=int(off[-1])).astype(np.int32)
+    h = cv.HMM(pi, a, b)
+    for assoc in ("viterbi", "decode"):
+        got = cv.decode_batch(h, off, obs, dtype="f64", assoc=assoc, rescore_f64=False)
+        assert cv.last_timing(h)["kernel"] == "trellis_f64"
+        _assert_same(got, O.decode_batch(pi, a, b, off, obs, ASSOC[assoc], np.float64), f"{kind} {assoc} N={n}")
+
+
 @pytest.mark.parametrize("kernel", ["auto", "generic"])
 @pytest.mark.parametrize("dtype", ["f64", "f32"])
 def test_decode_infeasible_backtrack(gpu, kernel, dtype):
