@@ -1,5 +1,5 @@
 #!/bin/bash
-# PMC passes over the exact-f64 forward kernel (trellis_fwd_f64) in the config-4 bench (one
+# PMC passes over an exact-f64 kernel (KRE, default trellis_fwd_f64; also backtrack_f64) in the config-4 bench (one
 # 65,536-sequence launch per step): HBM traffic (FETCH_SIZE, WRITE_SIZE: one pass each, the
 # gfx950 FETCH_SIZE x2 correction in tools/pmc_summary.py) and SQ issue/wait counters + the
 # clock (GRBM_GUI_ACTIVE).  One --pmc group per run, kernel trace only.
@@ -9,7 +9,7 @@ mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
 ARGS="--steps 1 --warmup 1 --no-cpu-baseline --no-f32-extra"
 for C in FETCH_SIZE WRITE_SIZE; do
-  timeout -k 10 ${T_PMC:-240} rocprofv3 --pmc $C --kernel-include-regex "trellis_fwd_f64" -d $OUT/$C -o p \
+  timeout -k 10 ${T_PMC:-240} rocprofv3 --pmc $C --kernel-include-regex "${KRE:-trellis_fwd_f64}" -d $OUT/$C -o p \
     --output-format csv -- python3 $R/bench.py $ARGS > $OUT/$C.log 2>&1 || exit $?
 done
 python3 $R/tools/pmc_summary.py $OUT > $OUT/traffic.json && cat $OUT/traffic.json | head -8
@@ -17,7 +17,7 @@ i=0
 for G in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_WAIT_ANY SQ_INSTS_LDS" \
          "SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_SALU GRBM_GUI_ACTIVE GRBM_COUNT"; do
   i=$((i + 1))
-  timeout -k 10 ${T_PMC:-240} rocprofv3 --pmc $G --kernel-include-regex "trellis_fwd_f64" -d $OUT/g$i -o p \
+  timeout -k 10 ${T_PMC:-240} rocprofv3 --pmc $G --kernel-include-regex "${KRE:-trellis_fwd_f64}" -d $OUT/g$i -o p \
     --output-format csv -- python3 $R/bench.py $ARGS > $OUT/g$i.log 2>&1 || exit $?
 done
 python3 - "$OUT" <<'PY' > $OUT/sq_summary.txt
