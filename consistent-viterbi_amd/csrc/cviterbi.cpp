@@ -543,10 +543,13 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
   // pass of chunk k+1 runs while chunk k backtracks, out of a double-buffered workspace.
   // At least ~2,048 sequences per chunk (8 per CU), at most 8 chunks unless the
   // workspace cap forces more.
-  // t64 runs serial: its 212-VGPR forward waves fill each SIMD exactly twice per launch, and a
-  // co-running backtrack cost more than it hid (config 4: 205.6 ms overlapped vs 191.9 ms
-  // serial, profiles/r01_t64_sweep.txt)
-  static const bool t64_overlap = getenv("CV_T64_OVERLAP") != nullptr;  // A/B knob (bit-identical)
+  // t64 runs serial: its 212-VGPR forward waves fill each SIMD exactly twice per launch and
+  // saturate the VALU; a co-running backtrack cost more than it hid (config 4: 159.8 ms with a
+  // persistent one-wave-per-SIMD backtrack vs 152.4 ms serial, profiles/r02_ab_t64_overlap.txt)
+  static const bool t64_overlap = [] {  // A/B knob (bit-identical): CV_T64_OVERLAP=0/1
+    const char* e = getenv("CV_T64_OVERLAP");
+    return e != nullptr && e[0] == '1';
+  }();
   const bool serial = (o.flags & CV_FLAG_SERIAL) != 0 || wave || (use_t64 && !t64_overlap);
   // Sequences per forward workgroup: 2 (trellis_fwd2_f32, equal-length pairs; default) or 1
   // (trellis_fwd_f32: leftovers, N not a multiple of 64).
@@ -806,7 +809,9 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
       ba.obs = obs_dev;
       ba.et = h->q_et.as<double>();
       ba.at32 = h->t64_nonpos ? h->q_at32.as<float>() : nullptr;
-      err = cvk::launch_t64_bt(h->np64, ba, n, bts);
+      // overlap mode: one persistent workgroup per CU while the next chunk's forward runs (one
+      // 60-VGPR wave per SIMD beside its two 212-VGPR waves); the last chunk at full occupancy
+      err = cvk::launch_t64_bt(h->np64, ba, n, bts, (serial || ci + 1 == chunks.size()) ? 0 : std::max(h->cus, 1));
     } else if (o.dtype == CV_DTYPE_F64) {
       cvk::GenericBtArgs<double> ba{};
       ba.psi = reinterpret_cast<const uint16_t*>(wsb);

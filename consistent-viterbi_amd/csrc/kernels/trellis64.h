@@ -109,6 +109,7 @@ int t64_seqs_per_wave(int64_t nseq, int cus);
 hipError_t launch_t64_fwd(int np, int s, const T64FwdArgs& fa, int64_t nseq, hipStream_t stream);
 // CP association (cp.rs:70-79): psi and the CP value d[psi] + (a[psi,j] + b[j,o]) in the forward
 hipError_t launch_t64_cp_fwd(int np, int s, const T64FwdArgs& fa, int64_t nseq, hipStream_t stream);
-hipError_t launch_t64_bt(int np, const T64BtArgs& ba, int64_t nseq, hipStream_t stream);
+// max_wgs > 0: at most that many 4-wave workgroups, each looping over the slots (persistent)
+hipError_t launch_t64_bt(int np, const T64BtArgs& ba, int64_t nseq, hipStream_t stream, int max_wgs = 0);
 
 }  // namespace cvk

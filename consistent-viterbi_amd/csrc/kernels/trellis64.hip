@@ -724,12 +724,9 @@ __device__ __forceinline__ void bt_chain_f64(const uint32_t* __restrict__ rows, 
 // NONPOS: the kernel holds only the NONPOS chain (fewer VGPRs, more waves per SIMD); the
 // host launches it for row-A0 decodes without the viterbi::decode infeasible rule when
 // g.at32 is set.
-template <int KP, int PF, bool NONPOS = false>
-__global__ __launch_bounds__(256) void backtrack_f64(T64BtArgs g) {
+template <int KP, int PF, bool NONPOS>
+__device__ __forceinline__ void backtrack_one_f64(const T64BtArgs& g, int64_t slot, int lane) {
   constexpr int NP = 64 * KP;
-  const int lane = threadIdx.x & 63;
-  const int64_t slot = g.seq_begin + (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (slot >= g.seq_end) return;
   const int64_t seq = g.order ? (int64_t)g.order[slot] : slot;
   const int64_t e0 = g.offsets[seq];
   const int T = (int)(g.offsets[seq + 1] - e0);
@@ -778,6 +775,17 @@ __global__ __launch_bounds__(256) void backtrack_f64(T64BtArgs g) {
     g.score[seq] = bv;
     g.status[seq] = CVK_SEQ_OK;
   }
+}
+
+// One wave per sequence; a grid smaller than the batch makes the kernel persistent (wave w of
+// workgroup b takes slots b*4 + w, then strides by the grid): the overlap schedule launches one
+// workgroup per CU (one wave per SIMD), which always fits beside two forward waves.
+template <int KP, int PF, bool NONPOS = false>
+__global__ __launch_bounds__(256) void backtrack_f64(T64BtArgs g) {
+  const int lane = threadIdx.x & 63;
+  const int64_t stride = (int64_t)gridDim.x * 4;
+  for (int64_t slot = g.seq_begin + (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); slot < g.seq_end; slot += stride)
+    backtrack_one_f64<KP, PF, NONPOS>(g, slot, lane);
 }
 
 // Resume flow (f64): the prefix [offsets[seq], t1] of every constrained sequence backtracked
@@ -929,9 +937,11 @@ hipError_t bt_pf(int np, const T64BtArgs& ba, dim3 grid, dim3 block, hipStream_t
   return bt_pf_np<PF, false>(np, ba, grid, block, stream);
 }
 
-hipError_t launch_t64_bt(int np, const T64BtArgs& ba, int64_t nseq, hipStream_t stream) {
+hipError_t launch_t64_bt(int np, const T64BtArgs& ba, int64_t nseq, hipStream_t stream, int max_wgs) {
   if (nseq <= 0) return hipSuccess;
-  const dim3 grid((unsigned)((nseq + 3) / 4)), block(256);
+  int64_t wgs = (nseq + 3) / 4;
+  if (max_wgs > 0 && wgs > max_wgs) wgs = max_wgs;
+  const dim3 grid((unsigned)wgs), block(256);
   static const int pf_env = [] {  // tuning knob (bit-identical): 2, 4, 8 or 16 rows in flight
     const char* e = getenv("CV_T64_BT_PF");
     return e ? atoi(e) : 0;
