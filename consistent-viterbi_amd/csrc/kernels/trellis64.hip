@@ -135,16 +135,37 @@ __device__ __forceinline__ void load_row_buf(__amdgpu_buffer_rsrc_t r, uint32_t 
 // = slot), reversed traversal (the suffix pass runs on a^T with pi = 0), final-row output,
 // per-slot start state (segment tables), compact delta rows (row_base), resume rows and a
 // longest-first slot order.
-template <int C, int S, int PF, bool DPA, bool EXT>
-__global__ __launch_bounds__(64) void trellis_fwd_f64(T64FwdArgs g) {
-  constexpr int NP = 64 * C;
+// W: waves per workgroup splitting the NP = 64*C*W columns.  W = 2 (C = 2 at N = 256) is the
+// small-batch layout: when S = 8 sequences per wave cannot give every SIMD two waves, S = 8
+// sequences per PAIR of waves keeps the wave count of S = 4 with twice its A-row reuse (8,192
+// sequences, 8-GPU strong scaling: profiles/r02_t64_small_batch.txt).  The W waves run the
+// same S sequences, share delta_{t-1} in LDS and meet at two barriers per step (before
+// overwriting delta_{t-1}, after writing delta_t).  At full batches W = 1 is faster (the VALU
+// is saturated either way and W = 2 runs at a lower clock, profiles/r02_ab_fwd_w2.txt).
+template <int C, int S, int PF, bool DPA, bool EXT, int W = 1, bool CAP2 = (W > 1)>
+__global__ __launch_bounds__(64 * W) void trellis_fwd_f64(T64FwdArgs g) {
+  constexpr int NP = 64 * C * W;
   static_assert(S % 2 == 0, "S sequences are read from LDS two at a time");
   static_assert(NP % PF == 0, "the ring wraps around at row NP");
-  // delta_{t-1}: [row][S]; row NP is padding, read (and ignored) by the prefetch of row i+1
-  __shared__ __attribute__((aligned(16))) double dl[(NP + 1) * S];
-  const int lane = threadIdx.x;
-  const int j0 = lane * C;
+  // delta rows in flight ahead of their use: 1 (W = 1: 212 VGPRs already) or 3 (W = 2, the
+  // small-batch layout: 32 VALU per row leave too little time for one LDS round trip)
+  constexpr int DV = W > 1 ? 4 : 2;
+  static_assert(PF % DV == 0, "the delta-row ring must wrap with the A-row ring");
+  // delta_{t-1}: [row][S]; rows NP .. NP+DV-2 are padding, read (and ignored) by the prefetch
+  __shared__ __attribute__((aligned(16))) double dl[(NP + DV - 1) * S];
+  const int lane = threadIdx.x & 63;
+  const int wv = W > 1 ? __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6) : 0;
+  const int j0 = (wv * 64 + lane) * C;
   const double ninf = ninf_d();
+  // workgroup rendezvous without the global-memory drain of __syncthreads (the A-row ring and
+  // the delta stores stay in flight): only this wave's LDS operations are waited for
+  auto wg_sync = [&]() {
+    if constexpr (W > 1) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  };
+  // W > 1 runs single-round small batches: reserve > 170 VGPRs so a SIMD holds at most two of
+  // these waves and every SIMD gets two (at ~150 VGPRs three fit, and a round that puts three
+  // on some SIMDs and one on others takes 1.5x as long)
+  if constexpr (CAP2) asm volatile("" ::: "v180");
 
   // Per-sequence bookkeeping lives in LANE s of a few VGPRs (lanes >= S idle) rather than in
   // S-element scalar arrays (those exceed the 102 SGPRs at S = 8 and spill): each step lane s
@@ -208,7 +229,7 @@ __global__ __launch_bounds__(64) void trellis_fwd_f64(T64FwdArgs g) {
   };
   auto frc_use = [&](int f) -> int { return (EXT && g.forced && my_T > 0) ? f : -1; };
   const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(g.a), 0, NP * NP * 8, 0x00020000);
-  const uint32_t voff = (uint32_t)lane * C * 8;
+  const uint32_t voff = (uint32_t)j0 * 8;
   constexpr uint32_t RB = NP * 8;  // bytes per table row
   // emission row of observation o (wave-uniform; the padded columns of the table are -inf)
   auto emis = [&](unsigned o, double (&e)[C]) {
@@ -276,6 +297,7 @@ __global__ __launch_bounds__(64) void trellis_fwd_f64(T64FwdArgs g) {
     onext_l = obs_lane(1);
     fnext_l = frc_lane(1);
   }
+  wg_sync();  // every wave's columns of delta_0 are in LDS
 
   // forward waves win issue arbitration over co-resident backtrack waves of the previous
   // chunk (overlap mode), as in trellis_fwd2_f32
@@ -301,24 +323,26 @@ __global__ __launch_bounds__(64) void trellis_fwd_f64(T64FwdArgs g) {
     for (int c = 0; c < C; ++c)
 #pragma unroll
       for (int s = 0; s < S; ++s) acc[c][s] = ninf;
-    // delta rows double-buffered in registers (dv[u & 1] = row i): row i+1's broadcast reads
-    // are in flight while row i computes
-    f64x2 dv[2][S / 2];
+    // delta rows in a DV-slot register ring (dv[u % DV] = row i): the broadcast reads of rows
+    // i+1 .. i+DV-1 are in flight while row i computes
+    f64x2 dv[DV][S / 2];
 #pragma unroll
-    for (int s2 = 0; s2 < S / 2; ++s2) dv[0][s2] = *reinterpret_cast<const f64x2*>(dl + 2 * s2);
+    for (int r = 0; r < DV - 1; ++r)
+#pragma unroll
+      for (int s2 = 0; s2 < S / 2; ++s2) dv[r][s2] = *reinterpret_cast<const f64x2*>(dl + r * S + 2 * s2);
 #pragma nounroll
     for (int i0 = 0; i0 < NP; i0 += PF) {
 #pragma unroll
       for (int u = 0; u < PF; ++u) {
         const int i = i0 + u;
         {
-          const f64x2* nrow = reinterpret_cast<const f64x2*>(dl + (i + 1) * S);
+          const f64x2* nrow = reinterpret_cast<const f64x2*>(dl + (i + DV - 1) * S);
 #pragma unroll
-          for (int s2 = 0; s2 < S / 2; ++s2) dv[(u + 1) & 1][s2] = nrow[s2];
+          for (int s2 = 0; s2 < S / 2; ++s2) dv[(u + DV - 1) % DV][s2] = nrow[s2];
         }
 #pragma unroll
         for (int s2 = 0; s2 < S / 2; ++s2) {
-          const f64x2 d = dv[u & 1][s2];
+          const f64x2 d = dv[u % DV][s2];
 #pragma unroll
           for (int c = 0; c < C; ++c) {
             if constexpr (DPA) {
@@ -337,9 +361,11 @@ __global__ __launch_bounds__(64) void trellis_fwd_f64(T64FwdArgs g) {
         load_row_buf<C>(ra, voff, (uint32_t)nr * RB, ar[u]);
       }
     }
-    // a single-wave workgroup: LDS operations of the wave execute in order, so the reads of
-    // delta_{t-1} above complete before the writes below; only the compiler must not reorder
+    // W = 1: LDS operations of the wave execute in order, so the reads of delta_{t-1} above
+    // complete before the writes below; only the compiler must not reorder.  W > 1: every
+    // wave has finished reading delta_{t-1} before any wave overwrites it
     asm volatile("" ::: "memory");
+    wg_sync();
     // epilogue: d_t = m + b[:, o_t] (viterbi.rs:17), emission rows of all S sequences in flight
     // together; then the next step's observations (scalar loads)
     double e[DPA ? 1 : S][C];
@@ -370,8 +396,9 @@ __global__ __launch_bounds__(64) void trellis_fwd_f64(T64FwdArgs g) {
       store_row(2 * s2 + 1, t, v1);
     }
     asm volatile("" ::: "memory");
+    wg_sync();  // delta_t complete in LDS before the next step reads it
   }
-  if (lane < S && my_bad) g.status[my_seq] = CVK_SEQ_BADOBS;
+  if (wv == 0 && lane < S && my_bad) g.status[my_seq] = CVK_SEQ_BADOBS;
 }
 
 // CP association (CPSolver, cp.rs:70-79 via utils.rs:24-38, hmm.rs:220-222):
@@ -831,6 +858,17 @@ __global__ void resume_rows_f64(const double* last, const int32_t* state, int np
   if (j < np) out[i * np + j] = (j == state[i]) ? last[i * np + j] : ninf_d();
 }
 
+// S sequences over a PAIR of waves (C = 2 each, N = 256): the small-batch layout
+template <int S>
+hipError_t fwd_w2(const T64FwdArgs& fa, int64_t nseq, bool ext, hipStream_t stream) {
+  const dim3 grid((unsigned)((nseq + S - 1) / S)), block(128);
+  if (ext)
+    hipLaunchKernelGGL((trellis_fwd_f64<2, S, 8, false, true, 2>), grid, block, 0, stream, fa);
+  else
+    hipLaunchKernelGGL((trellis_fwd_f64<2, S, 8, false, false, 2>), grid, block, 0, stream, fa);
+  return hipGetLastError();
+}
+
 template <int C, int S>
 hipError_t fwd_cs(const T64FwdArgs& fa, int64_t nseq, hipStream_t stream) {
   const int64_t blocks = (nseq + S - 1) / S;
@@ -838,8 +876,17 @@ hipError_t fwd_cs(const T64FwdArgs& fa, int64_t nseq, hipStream_t stream) {
     const char* e = getenv("CV_T64_PF");
     return e ? atoi(e) : 8;
   }();
+  static const bool w2 = [] {  // A/B knob (bit-identical): CV_T64_W2=0 keeps one wave per group
+    const char* e = getenv("CV_T64_W2");
+    return !(e && e[0] == '0');
+  }();
   const bool ext = fa.forced || fa.ranges || fa.reverse || fa.start || fa.row_base || fa.resume_rows ||
                    fa.slot_order || fa.last_row;
+  // N = 256 and fewer than 8 sequences per wave (small batch): 2S sequences over two waves --
+  // the same number of waves, twice the A-row reuse
+  if constexpr (C == 4 && S <= 4) {
+    if (w2 && !fa.dp_assoc) return fwd_w2<2 * S>(fa, nseq, ext, stream);
+  }
   const dim3 grid((unsigned)blocks), block(64);
   if (fa.dp_assoc) {
     if (ext) return hipErrorInvalidValue;
