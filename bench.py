@@ -108,14 +108,17 @@ def _cpu_model():
 
 
 def load_traffic(f64):
-    """Per-launch HBM bytes of the forward kernel from the committed rocprofv3 PMC summary."""
+    """HBM bytes per decoded ELEMENT of the forward kernel, from the committed rocprofv3 PMC
+    summary of the config-4 launch (f64: one 65,536-sequence launch; f32: one 8,192-sequence
+    launch); the traffic is the delta rows written, proportional to the elements a launch
+    decodes, so a rank's per-launch figure is this times its elements per launch."""
     p = os.path.join(ROOT, "profiles", "pmc_trellis_fwd_f64_c4.json" if f64 else "pmc_trellis_fwd_c4.json")
     if not os.path.exists(p):
         return None
     try:
         with open(p) as f:
             d = json.load(f)
-        return float(d["hbm_bytes_per_launch"])
+        return float(d["hbm_bytes_per_launch"]) / ((B_TOTAL if f64 else 8192) * T_LEN)
     except Exception:
         return None
 
@@ -242,7 +245,11 @@ def main():
     per_launch_bytes = alg_bytes / (launches / args.steps)
     achieved = per_launch_bytes / fwd_launch_s
     pairs_per_launch = N_STATES * N_STATES * (T_LEN - 1) * nloc / (launches / args.steps)
-    traffic = load_traffic(f64)
+    per_elem = load_traffic(f64)
+    traffic = per_elem * steps_rank / (launches / args.steps) if per_elem is not None else None
+    spw = cv.last_timing(h).get("seqs_per_wave", 8)
+    kname = ("trellis_fwd_f64<C=4,S=8>" if spw == 8 else "trellis_fwd_f64<C=2,S=%d,W=2>" % (2 * spw)) \
+        if f64 else "trellis_fwd2_f32<256>"
     pair_peak = F64_PAIR_PEAK if f64 else VALU_PAIR_PEAK
     out = {
         "metric": "trellis cells/s (N*T*batch), N=256 T=512 batch=65536",
@@ -268,7 +275,7 @@ def main():
         "seqs_per_s": B * args.steps / el,
         "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK, "traffic": traffic,
-                     "kernel": "trellis_fwd_f64<C=4,S=8>" if f64 else "trellis_fwd2_f32<256>",
+                     "kernel": kname,
                      "kernel_ms_per_launch": fwd_launch_s * 1e3,
                      "alg_bytes_per_launch": per_launch_bytes,
                      "read_only_frac": alg_read / (launches / args.steps) / fwd_launch_s / HBM_PEAK,

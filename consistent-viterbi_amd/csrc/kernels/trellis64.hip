@@ -1045,13 +1045,22 @@ hipError_t launch_t64_resume_rows(const double* last, const int32_t* state, int6
 // (strict '>' from i = 0), value prev[psi] + (trans(psi, j) + b[j, o]) (cp.rs:70-79), psi
 // stored as u16; then the first argmax of the last row and the backtrack (cp.rs:85-93).
 // Serial over elements (as the reference is): for the main.rs workflow, not the batch path.
+// A is staged in LDS when it fits (N <= 126: N^2 + 2N doubles <= 160 KiB), otherwise read
+// from L2 with the candidate loop unrolled so the loads overlap.
+template <bool LDS_A>
 __global__ __launch_bounds__(1024) void cp_superseq_chain(CpChainArgs g) {
-  extern __shared__ double rowbuf[];  // [2][N]
+  extern __shared__ double rowbuf[];  // [2][N] (+ [N][N] A when LDS_A)
   const int j = threadIdx.x;
   const int N = g.nstates;
   const int64_t L = g.len;
   double* prev = rowbuf;
   double* cur = rowbuf + N;
+  const double* A = g.a;
+  if constexpr (LDS_A) {
+    double* la = rowbuf + 2 * N;
+    for (int k = j; k < N * N; k += blockDim.x) la[k] = g.a[k];
+    A = la;
+  }
   if (j < N) prev[j] = g.pi[j] + g.et[(size_t)g.obs[0] * N + j];  // init_probs (cp.rs:66-68)
   __syncthreads();
   for (int64_t t = 1; t < L; ++t) {
@@ -1059,16 +1068,17 @@ __global__ __launch_bounds__(1024) void cp_superseq_chain(CpChainArgs g) {
       const int o = g.obs[t];
       const bool first = g.first[t] != 0;
       const double pj = g.pi[j];
-      double m = prev[0] + (first ? pj : g.a[j]);
+      double m = prev[0] + (first ? pj : A[j]);
       int arg = 0;
+#pragma unroll 8
       for (int i = 1; i < N; ++i) {
-        const double x = prev[i] + (first ? pj : g.a[(size_t)i * N + j]);
+        const double x = prev[i] + (first ? pj : A[(size_t)i * N + j]);
         if (x > m) {
           m = x;
           arg = i;
         }
       }
-      const double tr = first ? pj : g.a[(size_t)arg * N + j];
+      const double tr = first ? pj : A[(size_t)arg * N + j];
       cur[j] = prev[arg] + (tr + g.et[(size_t)o * N + j]);
       g.psi[t * N + j] = (uint16_t)arg;
     }
@@ -1097,11 +1107,20 @@ hipError_t launch_cp_superseq_chain(const CpChainArgs& g, hipStream_t stream) {
   if (g.len <= 0) return hipSuccess;
   if (g.nstates <= 0 || g.nstates > 1024) return hipErrorInvalidValue;
   const int threads = ((g.nstates + 63) / 64) * 64;
-  const size_t lds = (size_t)2 * g.nstates * sizeof(double);
-  if (lds > 64 * 1024)
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&cp_superseq_chain), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)lds);
-  hipLaunchKernelGGL(cp_superseq_chain, dim3(1), dim3(threads), lds, stream, g);
+  const size_t n = (size_t)g.nstates;
+  const size_t lds_a = (n * n + 2 * n) * sizeof(double);
+  if (lds_a <= 160 * 1024) {
+    if (lds_a > 64 * 1024)
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&cp_superseq_chain<true>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_a);
+    hipLaunchKernelGGL(cp_superseq_chain<true>, dim3(1), dim3(threads), lds_a, stream, g);
+  } else {
+    const size_t lds = 2 * n * sizeof(double);
+    if (lds > 64 * 1024)
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&cp_superseq_chain<false>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(cp_superseq_chain<false>, dim3(1), dim3(threads), lds, stream, g);
+  }
   return hipGetLastError();
 }
 

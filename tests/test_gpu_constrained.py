@@ -205,6 +205,26 @@ def test_superseq_cp_chain_rounding(gpu):
     assert seq_path[1] == 1  # per sequence: the strictly larger predecessor
 
 
+@pytest.mark.parametrize("n", [1, 7, 64, 126, 127, 200, 256])
+def test_superseq_cp_chain_sizes(gpu, n):
+    """cp_superseq_chain with A staged in LDS (N <= 126) and read from L2 (N >= 127), every
+    element against the chained restatement; quantised tables give exact ties (first index)."""
+    rng = np.random.default_rng(50 + n)
+    v = 13
+    pi = np.round(rng.uniform(-2, 0, n) * 4) / 4
+    a = np.round(rng.uniform(-2, 0, (n, n)) * 4) / 4
+    b = np.round(rng.uniform(-2, 0, (n, v)) * 4) / 4
+    if n > 1:  # keep one state feasible at N = 1
+        a[rng.random((n, n)) < 0.1] = -np.inf
+    lengths = rng.integers(1, 40, size=9)
+    off = synth.offsets_from_lengths(lengths)
+    obs = rng.integers(0, v, size=int(off[-1])).astype(np.int32)
+    h = cv.HMM(pi, a, b)
+    path, obj = cv.decode_superseq_cp(h, off, obs)
+    rp, robj = O.cp_superseq_f64(pi, a, b, off, obs)
+    assert np.array_equal(path, rp) and obj == robj
+
+
 @pytest.mark.parametrize("dtype", ["f64", "f32"])
 @pytest.mark.parametrize("nshards", [2, 5])
 def test_constrained_sharded_equals_single(gpu, nshards, dtype):
