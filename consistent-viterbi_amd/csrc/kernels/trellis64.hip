@@ -142,7 +142,7 @@ __device__ __forceinline__ void load_row_buf(__amdgpu_buffer_rsrc_t r, uint32_t 
 // same S sequences, share delta_{t-1} in LDS and meet at two barriers per step (before
 // overwriting delta_{t-1}, after writing delta_t).  At full batches W = 1 is faster (the VALU
 // is saturated either way and W = 2 runs at a lower clock, profiles/r02_ab_fwd_w2.txt).
-template <int C, int S, int PF, bool DPA, bool EXT, int W = 1, bool CAP2 = (W > 1)>
+template <int C, int S, int PF, bool DPA, bool EXT, int W = 1, bool CAP2 = (W > 1), int GRP = 2>
 __global__ __launch_bounds__(64 * W) void trellis_fwd_f64(T64FwdArgs g) {
   constexpr int NP = 64 * C * W;
   static_assert(S % 2 == 0, "S sequences are read from LDS two at a time");
@@ -340,19 +340,36 @@ __global__ __launch_bounds__(64 * W) void trellis_fwd_f64(T64FwdArgs g) {
 #pragma unroll
           for (int s2 = 0; s2 < S / 2; ++s2) dv[(u + DV - 1) % DV][s2] = nrow[s2];
         }
+        // the candidates of G sequence pairs are added before their maxima are taken, so each
+        // v_max_f64 issues ~2*C*G instructions after the v_add_f64 it reads (adjacent dependent
+        // f64 ops cost issue slots: profiles/r02_ab_fwd_group.txt)
+        constexpr int G = (S / 2) % GRP == 0 ? GRP : 1;
 #pragma unroll
-        for (int s2 = 0; s2 < S / 2; ++s2) {
-          const f64x2 d = dv[u % DV][s2];
+        for (int s0 = 0; s0 < S / 2; s0 += G) {
+          double x[G][2][C];
 #pragma unroll
-          for (int c = 0; c < C; ++c) {
-            if constexpr (DPA) {
-              acc[c][2 * s2] = __builtin_fmax(acc[c][2 * s2], (ar[u][c] + ecur[2 * s2][c]) + d.x);
-              acc[c][2 * s2 + 1] = __builtin_fmax(acc[c][2 * s2 + 1], (ar[u][c] + ecur[2 * s2 + 1][c]) + d.y);
-            } else {
-              acc[c][2 * s2] = __builtin_fmax(acc[c][2 * s2], d.x + ar[u][c]);
-              acc[c][2 * s2 + 1] = __builtin_fmax(acc[c][2 * s2 + 1], d.y + ar[u][c]);
+          for (int gg = 0; gg < G; ++gg) {
+            const f64x2 d = dv[u % DV][s0 + gg];
+#pragma unroll
+            for (int c = 0; c < C; ++c) {
+              if constexpr (DPA) {
+                x[gg][0][c] = (ar[u][c] + ecur[2 * (s0 + gg)][c]) + d.x;
+                x[gg][1][c] = (ar[u][c] + ecur[2 * (s0 + gg) + 1][c]) + d.y;
+              } else {
+                x[gg][0][c] = d.x + ar[u][c];
+                x[gg][1][c] = d.y + ar[u][c];
+              }
             }
           }
+          __builtin_amdgcn_sched_group_barrier(0x002, 2 * C * G, 0);
+          __builtin_amdgcn_sched_group_barrier(0x002, 2 * C * G, 0);
+#pragma unroll
+          for (int gg = 0; gg < G; ++gg)
+#pragma unroll
+            for (int c = 0; c < C; ++c) {
+              acc[c][2 * (s0 + gg)] = __builtin_fmax(acc[c][2 * (s0 + gg)], x[gg][0][c]);
+              acc[c][2 * (s0 + gg) + 1] = __builtin_fmax(acc[c][2 * (s0 + gg) + 1], x[gg][1][c]);
+            }
         }
         // refill this ring slot with row (i + PF) mod NP -- the wrap-around rows are the next
         // step's first rows -- only after its last use, into the same registers: no copies,
