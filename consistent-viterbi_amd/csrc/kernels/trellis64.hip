@@ -921,6 +921,133 @@ hipError_t fwd_cs(const T64FwdArgs& fa, int64_t nseq, hipStream_t stream) {
   return hipGetLastError();
 }
 
+
+// trellis_wave_f64<ZI>: N <= 64 (NP = 64) -- ONE WAVE per sequence, A register-resident.
+// The lock-step layouts (S sequences per wave) run one round of waves at configs 2/3, so the
+// waves holding the longest sequences set the makespan; one sequence per wave gives many
+// rounds that the longest-first order balances.  Lane = 4cq + rg holds rows [16 rg, 16 rg + 16)
+// of the columns 4cq .. 4cq+3 (64 doubles); delta_{t-1} comes from the wave's own LDS row
+// (8 ds_read_b128; row-group stride 18 doubles puts the 4 addresses of an instruction on
+// disjoint banks); per pair one v_add_f64 + one v_max_f64; the 4 row-group partials are folded
+// across the lane quad by DPP (xor1 keeps a column pair, xor2 one column: lane jw =
+// 4cq + 2p + q), then d_t[jw] = m + b (viterbi.rs:15-17).  Rows go to HBM split-plane for
+// backtrack_f64.  Emissions are loaded 4 steps ahead with clamped indices, observations by
+// scalar loads (as trellis_wave_f32).  ZI: viterbi::decode's row 0 = 0.0.
+__device__ __forceinline__ double dpp_f64(double v, int ctrl_is_xor2) {
+  const uint64_t b = __builtin_bit_cast(uint64_t, v);
+  int lo = (int)(uint32_t)b, hi = (int)(uint32_t)(b >> 32);
+  if (ctrl_is_xor2) {
+    lo = __builtin_amdgcn_mov_dpp(lo, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
+    hi = __builtin_amdgcn_mov_dpp(hi, 0x4E, 0xF, 0xF, false);
+  } else {
+    lo = __builtin_amdgcn_mov_dpp(lo, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+    hi = __builtin_amdgcn_mov_dpp(hi, 0xB1, 0xF, 0xF, false);
+  }
+  return from_words((uint32_t)hi, (uint32_t)lo);
+}
+
+template <bool ZI>
+__global__ __launch_bounds__(256) void trellis_wave_f64(T64FwdArgs g) {
+  constexpr int NPW = 64, C = 4, R = 16, LS = R + 2;
+  __shared__ __attribute__((aligned(16))) double lds_all[4][2][4 * LS];
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+  const int rg = lane & 3, cq = lane >> 2;
+  const int p = rg & 1, q = rg >> 1;
+  const int jw = 4 * cq + 2 * p + q;  // this lane's column after the fold
+  const int64_t slot = g.seq_begin + 4 * (int64_t)blockIdx.x + wv;
+  if (slot >= g.seq_begin + g.nslots) return;
+  const int64_t seq = g.order ? (int64_t)g.order[slot] : slot;
+  const int64_t e0 = g.offsets[seq];
+  const int T = (int)(g.offsets[seq + 1] - e0);
+  if (T <= 0) return;  // backtrack_f64 reports empty sequences
+  double(*lds)[4 * LS] = lds_all[wv];
+  const sptr<int32_t> obs = scalar_view(g.obs + e0);
+  uint32_t* __restrict__ rows = reinterpret_cast<uint32_t*>(g.delta) + (e0 - g.delta_elem_base) * (2 * NPW);
+  const unsigned V = (unsigned)g.nobs;
+  double a_reg[R * C];  // a_reg[C r + k] = A[R rg + r][C cq + k]
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const f64x2* src = reinterpret_cast<const f64x2*>(g.a + (size_t)(R * rg + r) * NPW + C * cq);
+    const f64x2 v0 = src[0], v1 = src[1];
+    a_reg[C * r + 0] = v0.x;
+    a_reg[C * r + 1] = v0.y;
+    a_reg[C * r + 2] = v1.x;
+    a_reg[C * r + 3] = v1.y;
+  }
+  unsigned bad = 0;
+  auto obs_s = [&](int t) -> unsigned {
+    const unsigned o = (unsigned)obs[t];
+    bad |= (o >= V);
+    return o < V ? o : 0u;
+  };
+  auto put = [&](int t, double v) {
+    uint32_t* r = rows + (size_t)t * (2 * NPW) + jw;
+    __builtin_nontemporal_store(hi_word(v), r);
+    __builtin_nontemporal_store(lo_word(v), r + NPW);
+  };
+  const int wofs = (jw / R) * LS + (jw % R);  // where this lane's column lives in an LDS row
+  {
+    const double d0 = ZI ? 0.0 : g.pi[jw] + g.et[(size_t)obs_s(0) * NPW + jw];  // cp.rs:66-68
+    lds[0][wofs] = d0;
+    put(0, d0);
+  }
+  const int Tm1 = T - 1;
+  unsigned so[4];
+  double pe[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    pe[k] = g.et[(size_t)obs_s(min(1 + k, Tm1)) * NPW + jw];  // steps 1..4
+    so[k] = obs_s(min(5 + k, Tm1));                           // observations of steps 5..8
+  }
+  for (int t0 = 1; t0 < T; t0 += 4) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int t = t0 + k;
+      if (t >= T) break;
+      const double* src = &lds[(t - 1) & 1][rg * LS];
+      f64x2 d[R / 2];
+#pragma unroll
+      for (int b = 0; b < R / 2; ++b) d[b] = *reinterpret_cast<const f64x2*>(src + 2 * b);
+      double c[C];
+#pragma unroll
+      for (int kc = 0; kc < C; ++kc) {
+        double m = d[0].x + a_reg[kc];  // s_i = d[i] + a[i,j]  (viterbi.rs:15)
+        m = __builtin_fmax(m, d[0].y + a_reg[C + kc]);
+#pragma unroll
+        for (int b = 1; b < R / 2; ++b) {
+          m = __builtin_fmax(m, d[b].x + a_reg[(2 * b) * C + kc]);
+          m = __builtin_fmax(m, d[b].y + a_reg[(2 * b + 1) * C + kc]);
+        }
+        c[kc] = m;
+      }
+      // fold the 4 row groups of the quad: xor1 keeps columns {2p, 2p+1}, xor2 keeps 2p+q
+      double k0 = p ? c[2] : c[0], k1 = p ? c[3] : c[1];
+      const double g0 = p ? c[0] : c[2], g1 = p ? c[1] : c[3];
+      k0 = __builtin_fmax(k0, dpp_f64(g0, 0));
+      k1 = __builtin_fmax(k1, dpp_f64(g1, 0));
+      double kk = q ? k1 : k0;
+      const double gg = q ? k0 : k1;
+      kk = __builtin_fmax(kk, dpp_f64(gg, 1));
+      const double dn = kk + pe[k];  // (d + a) + b -- viterbi.rs:15-17
+      lds[t & 1][wofs] = dn;
+      put(t, dn);
+      pe[k] = g.et[(size_t)so[k] * NPW + jw];  // step t+4
+      so[k] = obs_s(min(t + 8, Tm1));          // observation of step t+8
+    }
+  }
+  if (bad && lane == 0) g.status[seq] = CVK_SEQ_BADOBS;
+}
+
+hipError_t launch_t64_wave(const T64FwdArgs& fa, int64_t nseq, hipStream_t stream) {
+  const dim3 grid((unsigned)((nseq + 3) / 4)), block(256);
+  if (fa.zero_init)
+    hipLaunchKernelGGL(trellis_wave_f64<true>, grid, block, 0, stream, fa);
+  else
+    hipLaunchKernelGGL(trellis_wave_f64<false>, grid, block, 0, stream, fa);
+  return hipGetLastError();
+}
+
 template <int C>
 hipError_t fwd_c(const T64FwdArgs& fa, int s, int64_t nseq, hipStream_t stream) {
   switch (s) {
@@ -973,6 +1100,13 @@ int t64_seqs_per_wave(int64_t nseq, int cus) {
 
 hipError_t launch_t64_fwd(int np, int s, const T64FwdArgs& fa, int64_t nseq, hipStream_t stream) {
   if (nseq <= 0) return hipSuccess;
+  static const bool wave = [] {  // A/B knob (bit-identical): CV_T64_WAVE=0 keeps the lock-step layout
+    const char* e = getenv("CV_T64_WAVE");
+    return !(e && e[0] == '0');
+  }();
+  const bool ext = fa.forced || fa.ranges || fa.reverse || fa.start || fa.row_base || fa.resume_rows ||
+                   fa.slot_order || fa.last_row;
+  if (np == 64 && wave && !fa.dp_assoc && !ext) return launch_t64_wave(fa, nseq, stream);
   if (fa.dp_assoc && s > 4) s = 4;  // the emissions of every sequence stay in registers
   switch (np) {
     case 64: return fwd_c<1>(fa, s, nseq, stream);
