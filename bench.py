@@ -221,6 +221,7 @@ def main():
         return el, fwd_ms, bt_ms, launches
 
     el, fwd_ms, bt_ms, launches = timed(args.dtype, args.steps, args.warmup)
+    spw = cv.last_timing(h).get("seqs_per_wave", 8)  # the layout of the timed run (before the f32 extra)
     f32_extra = None
     if f64 and not args.no_f32_extra:
         el32, fwd32, bt32, l32 = timed("f32", args.steps, args.warmup)
@@ -247,7 +248,6 @@ def main():
     pairs_per_launch = N_STATES * N_STATES * (T_LEN - 1) * nloc / (launches / args.steps)
     per_elem = load_traffic(f64)
     traffic = per_elem * steps_rank / (launches / args.steps) if per_elem is not None else None
-    spw = cv.last_timing(h).get("seqs_per_wave", 8)
     kname = ("trellis_fwd_f64<C=4,S=8>" if spw == 8 else "trellis_fwd_f64<C=2,S=%d,W=2>" % (2 * spw)) \
         if f64 else "trellis_fwd2_f32<256>"
     pair_peak = F64_PAIR_PEAK if f64 else VALU_PAIR_PEAK
