@@ -824,8 +824,18 @@ __device__ __forceinline__ void backtrack_one_f64(const T64BtArgs& g, int64_t sl
 // One wave per sequence; a grid smaller than the batch makes the kernel persistent (wave w of
 // workgroup b takes slots b*4 + w, then strides by the grid): the overlap schedule launches one
 // workgroup per CU (one wave per SIMD), which always fits beside two forward waves.
+// NONPOS at NP = 64: the f32 a^T (16 KiB) is staged in LDS, so the one dependent read of each
+// chain step is an LDS round trip instead of an L2 one (the longest chains set the makespan
+// of ragged batches, config 3).
 template <int KP, int PF, bool NONPOS = false>
 __global__ __launch_bounds__(256) void backtrack_f64(T64BtArgs g) {
+  constexpr bool LDS_AT = NONPOS && KP == 1;
+  __shared__ float at_lds[LDS_AT ? 64 * 64 : 1];
+  if constexpr (LDS_AT) {
+    for (int k = threadIdx.x; k < 64 * 64; k += 256) at_lds[k] = g.at32[k];
+    __syncthreads();
+    g.at32 = at_lds;
+  }
   const int lane = threadIdx.x & 63;
   const int64_t stride = (int64_t)gridDim.x * 4;
   for (int64_t slot = g.seq_begin + (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); slot < g.seq_end; slot += stride)
