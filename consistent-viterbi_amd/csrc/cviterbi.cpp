@@ -1760,6 +1760,7 @@ cv_status forced_decode_resume(cv_hmm* h, int64_t nseq, const int64_t* offsets_h
     p64.state = state_d;
     p64.offsets = offsets_dev;
     p64.at = h->q_at.as<double>();
+    p64.at32 = h->t64_nonpos ? h->q_at32.as<float>() : nullptr;
     p64.nstates = h->N;
     p64.path = path_dev;
     err = cvk::launch_t64_prefix_bt(np, p64, nc, stream);

@@ -70,6 +70,7 @@ struct PrefixBt64Args {
   const int32_t* state;     // [n] state forced there
   const int64_t* offsets;   // original CSR offsets
   const double* at;         // [NP][NP] a^T (t64 tables)
+  const float* at32;        // f32(a^T) for the NONPOS interval test, or null (T64BtArgs::at32)
   int nstates;
   int32_t* path;
 };

@@ -844,7 +844,7 @@ __global__ __launch_bounds__(256) void backtrack_f64(T64BtArgs g) {
 
 // Resume flow (f64): the prefix [offsets[seq], t1] of every constrained sequence backtracked
 // from its forced state through the rows the terms pass stored (split-plane, compact per slot).
-template <int KP>
+template <int KP, bool NONPOS>
 __global__ __launch_bounds__(256) void prefix_backtrack_f64(PrefixBt64Args a, int64_t n) {
   const int lane = threadIdx.x & 63;
   const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -855,8 +855,8 @@ __global__ __launch_bounds__(256) void prefix_backtrack_f64(PrefixBt64Args a, in
   constexpr int NP = 64 * KP;
   // an infeasible forced row backtracks garbage: zero_infeasible_prefix overwrites it once the
   // suffix decode has told which sequences are infeasible
-  bt_chain_f64<KP, 2>(reinterpret_cast<const uint32_t*>(a.rows) + a.row_base[i] * (2 * NP), T, a.state[i],
-                      a.path + e0, a.at, nullptr, nullptr, 0, a.nstates, lane);
+  bt_chain_f64<KP, 2, false, NONPOS>(reinterpret_cast<const uint32_t*>(a.rows) + a.row_base[i] * (2 * NP), T,
+                                     a.state[i], a.path + e0, a.at, nullptr, nullptr, 0, a.nstates, lane, a.at32);
 }
 
 // Max-marginal at one constrained position (f64; max_marginal_f32 in trellis.hip):
@@ -1166,13 +1166,21 @@ hipError_t launch_t64_bt(int np, const T64BtArgs& ba, int64_t nseq, hipStream_t 
 hipError_t launch_t64_prefix_bt(int np, const PrefixBt64Args& a, int64_t n, hipStream_t stream) {
   if (n <= 0) return hipSuccess;
   const dim3 grid((unsigned)((n + 3) / 4)), block(256);
+#define CVK_PBT(KP)                                                                   \
+  do {                                                                                \
+    if (a.at32)                                                                       \
+      hipLaunchKernelGGL((prefix_backtrack_f64<KP, true>), grid, block, 0, stream, a, n); \
+    else                                                                              \
+      hipLaunchKernelGGL((prefix_backtrack_f64<KP, false>), grid, block, 0, stream, a, n); \
+  } while (0)
   switch (np) {
-    case 64: hipLaunchKernelGGL((prefix_backtrack_f64<1>), grid, block, 0, stream, a, n); break;
-    case 128: hipLaunchKernelGGL((prefix_backtrack_f64<2>), grid, block, 0, stream, a, n); break;
-    case 192: hipLaunchKernelGGL((prefix_backtrack_f64<3>), grid, block, 0, stream, a, n); break;
-    case 256: hipLaunchKernelGGL((prefix_backtrack_f64<4>), grid, block, 0, stream, a, n); break;
+    case 64: CVK_PBT(1); break;
+    case 128: CVK_PBT(2); break;
+    case 192: CVK_PBT(3); break;
+    case 256: CVK_PBT(4); break;
     default: return hipErrorInvalidValue;
   }
+#undef CVK_PBT
   return hipGetLastError();
 }
 
