@@ -85,6 +85,26 @@ def test_t64_ties_and_infeasible(gpu, n, assoc):
             cv.decode_batch(h, off, obs_bad, dtype="f64", kernel=kernel, rescore_f64=False)
 
 
+@pytest.mark.parametrize("nseq", [8192, 4096, 2048])
+def test_t64_small_batch_layouts_vs_generic(gpu, nseq):
+    """N = 256 batches too small for 8 sequences per wave (8,192 = one GPU of 8-GPU strong
+    scaling): 2S sequences over a pair of waves (trellis_fwd_f64<2, 2S, .., W=2>) -- the whole
+    batch equals the generic f64 kernel, scores are the f64 fold of each path, and the layout
+    reported is the small-batch one."""
+    pi, a, b = synth.random_hmm(256, 64, seed=77)
+    rng = np.random.default_rng(nseq)
+    lengths = rng.integers(40, 49, size=nseq)
+    off = synth.offsets_from_lengths(lengths)
+    obs = rng.integers(0, 64, size=int(off[-1])).astype(np.int32)
+    h = cv.HMM(pi, a, b)
+    got = cv.decode_batch(h, off, obs, dtype="f64", rescore_f64=False)
+    t = cv.last_timing(h)
+    assert t["kernel"] == "trellis_f64" and t["seqs_per_wave"] in (2, 4), t
+    _assert_same(got, cv.decode_batch(h, off, obs, dtype="f64", kernel="generic", rescore_f64=False), f"B={nseq}")
+    assert np.all(got[2] == 0)
+    np.testing.assert_array_equal(got[1], O.rescore_batch_f64(pi, a, b, off, obs, got[0]))
+
+
 @pytest.mark.parametrize("n", [64, 200, 256])
 @pytest.mark.parametrize("kind", ["near_ties", "positive", "huge"])
 def test_t64_backtrack_interval_paths(gpu, n, kind):
