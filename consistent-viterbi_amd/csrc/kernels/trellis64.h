@@ -54,6 +54,8 @@ struct T64BtArgs {
   const double* et;
   const float* at32;       // f32(a^T) [NP][NP], set only for models whose finite entries are
                            // all in [-2^80, 0]: the NONPOS interval test (null: f64 test)
+  int only_infeasible;     // set by launch_t64_bt: the general kernel's viterbi::decode pass over
+                           // the infeasible sequences the NONPOS kernel left (their DEC chain)
 };
 
 // Delta rows of the f64 trellis (forward -> backtrack, resume-flow prefix rows) use a

@@ -801,16 +801,20 @@ __device__ __forceinline__ void backtrack_one_f64(const T64BtArgs& g, int64_t sl
   }
   const uint8_t prior = g.status[seq];
   if (!(bv > ninf_d()) || prior == CVK_SEQ_BADOBS) {
-    if (!NONPOS && g.decode_bt && prior != CVK_SEQ_BADOBS)  // viterbi.rs:24-30: from argmax 0 (= cur) through bt
-      bt_chain_f64<KP, PF, true>(rows, T, cur, path, g.at, g.et, g.obs + e0, 0, N, lane);
-    else
+    if (g.decode_bt && prior != CVK_SEQ_BADOBS) {  // viterbi.rs:24-30: from argmax 0 (= cur) through bt
+      // the NONPOS kernel leaves the DEC chain (more VGPRs) to the general kernel's
+      // only_infeasible pass that launch_t64_bt queues after it
+      if constexpr (!NONPOS) bt_chain_f64<KP, PF, true>(rows, T, cur, path, g.at, g.et, g.obs + e0, 0, N, lane);
+    } else {
       for (int t = lane; t < T; t += 64) path[t] = 0;
+    }
     if (lane == 0) {
       g.score[seq] = ninf_d();
       g.status[seq] = prior == CVK_SEQ_BADOBS ? CVK_SEQ_BADOBS : CVK_SEQ_INFEASIBLE;
     }
     return;
   }
+  if (!NONPOS && g.only_infeasible) return;  // feasible: done by the NONPOS kernel
   if constexpr (NONPOS)
     bt_chain_f64<KP, PF, false, true>(rows, T, cur, path, g.at, g.et, g.obs + e0, 0, N, lane, g.at32);
   else
@@ -827,7 +831,7 @@ __device__ __forceinline__ void backtrack_one_f64(const T64BtArgs& g, int64_t sl
 // NONPOS at NP = 64: the f32 a^T (16 KiB) is staged in LDS, so the one dependent read of each
 // chain step is an LDS round trip instead of an L2 one (the longest chains set the makespan
 // of ragged batches, config 3).
-template <int KP, int PF, bool NONPOS = false>
+template <int KP, int PF, bool NONPOS = false, bool PERSIST = false>
 __global__ __launch_bounds__(256) void backtrack_f64(T64BtArgs g) {
   constexpr bool LDS_AT = NONPOS && KP == 1;
   __shared__ float at_lds[LDS_AT ? 64 * 64 : 1];
@@ -837,9 +841,13 @@ __global__ __launch_bounds__(256) void backtrack_f64(T64BtArgs g) {
     g.at32 = at_lds;
   }
   const int lane = threadIdx.x & 63;
-  const int64_t stride = (int64_t)gridDim.x * 4;
-  for (int64_t slot = g.seq_begin + (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); slot < g.seq_end; slot += stride)
-    backtrack_one_f64<KP, PF, NONPOS>(g, slot, lane);
+  const int64_t slot0 = g.seq_begin + (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if constexpr (PERSIST) {  // the loop costs VGPRs (60 -> 76 at NP = 256): overlap mode only
+    const int64_t stride = (int64_t)gridDim.x * 4;
+    for (int64_t slot = slot0; slot < g.seq_end; slot += stride) backtrack_one_f64<KP, PF, NONPOS>(g, slot, lane);
+  } else if (slot0 < g.seq_end) {
+    backtrack_one_f64<KP, PF, NONPOS>(g, slot0, lane);
+  }
 }
 
 // Resume flow (f64): the prefix [offsets[seq], t1] of every constrained sequence backtracked
@@ -1127,22 +1135,36 @@ hipError_t launch_t64_fwd(int np, int s, const T64FwdArgs& fa, int64_t nseq, hip
   }
 }
 
-template <int PF, bool NONPOS>
+template <int PF, bool NONPOS, bool PERSIST>
 hipError_t bt_pf_np(int np, const T64BtArgs& ba, dim3 grid, dim3 block, hipStream_t stream) {
   switch (np) {
-    case 64: hipLaunchKernelGGL((backtrack_f64<1, PF, NONPOS>), grid, block, 0, stream, ba); break;
-    case 128: hipLaunchKernelGGL((backtrack_f64<2, PF, NONPOS>), grid, block, 0, stream, ba); break;
-    case 192: hipLaunchKernelGGL((backtrack_f64<3, PF, NONPOS>), grid, block, 0, stream, ba); break;
-    case 256: hipLaunchKernelGGL((backtrack_f64<4, PF, NONPOS>), grid, block, 0, stream, ba); break;
+    case 64: hipLaunchKernelGGL((backtrack_f64<1, PF, NONPOS, PERSIST>), grid, block, 0, stream, ba); break;
+    case 128: hipLaunchKernelGGL((backtrack_f64<2, PF, NONPOS, PERSIST>), grid, block, 0, stream, ba); break;
+    case 192: hipLaunchKernelGGL((backtrack_f64<3, PF, NONPOS, PERSIST>), grid, block, 0, stream, ba); break;
+    case 256: hipLaunchKernelGGL((backtrack_f64<4, PF, NONPOS, PERSIST>), grid, block, 0, stream, ba); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
 }
 
+template <int PF, bool NONPOS>
+hipError_t bt_pf_np(int np, const T64BtArgs& ba, dim3 grid, dim3 block, hipStream_t stream, bool persist) {
+  return persist ? bt_pf_np<PF, NONPOS, true>(np, ba, grid, block, stream)
+                 : bt_pf_np<PF, NONPOS, false>(np, ba, grid, block, stream);
+}
+
 template <int PF>
-hipError_t bt_pf(int np, const T64BtArgs& ba, dim3 grid, dim3 block, hipStream_t stream) {
-  if (ba.at32 && !ba.dp_assoc && !ba.decode_bt) return bt_pf_np<PF, true>(np, ba, grid, block, stream);
-  return bt_pf_np<PF, false>(np, ba, grid, block, stream);
+hipError_t bt_pf(int np, const T64BtArgs& ba, dim3 grid, dim3 block, hipStream_t stream, bool persist) {
+  if (ba.at32 && !ba.dp_assoc) {
+    hipError_t e = bt_pf_np<PF, true>(np, ba, grid, block, stream, persist);
+    if (e == hipSuccess && ba.decode_bt) {  // viterbi::decode: the infeasible sequences' DEC chains
+      T64BtArgs b2 = ba;
+      b2.only_infeasible = 1;
+      e = bt_pf_np<PF, false>(np, b2, grid, block, stream, persist);
+    }
+    return e;
+  }
+  return bt_pf_np<PF, false>(np, ba, grid, block, stream, persist);
 }
 
 hipError_t launch_t64_bt(int np, const T64BtArgs& ba, int64_t nseq, hipStream_t stream, int max_wgs) {
@@ -1155,11 +1177,12 @@ hipError_t launch_t64_bt(int np, const T64BtArgs& ba, int64_t nseq, hipStream_t 
     return e ? atoi(e) : 0;
   }();
   const int pf = pf_env ? pf_env : np >= 192 ? 2 : 8;
+  const bool persist = max_wgs > 0 && (nseq + 3) / 4 > max_wgs;
   switch (pf) {
-    case 2: return bt_pf<2>(np, ba, grid, block, stream);
-    case 4: return bt_pf<4>(np, ba, grid, block, stream);
-    case 16: return bt_pf<16>(np, ba, grid, block, stream);
-    default: return bt_pf<8>(np, ba, grid, block, stream);
+    case 2: return bt_pf<2>(np, ba, grid, block, stream, persist);
+    case 4: return bt_pf<4>(np, ba, grid, block, stream, persist);
+    case 16: return bt_pf<16>(np, ba, grid, block, stream, persist);
+    default: return bt_pf<8>(np, ba, grid, block, stream, persist);
   }
 }
 
