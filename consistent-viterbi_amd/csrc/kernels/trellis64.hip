@@ -628,10 +628,12 @@ __device__ __forceinline__ int first_argmax_d(const double (&s)[KP], const bool 
 // state is -inf (viterbi.rs:19-21); on a feasible path every emission is finite, so the rule
 // never changes a feasible decode.
 //
-// NONPOS (models whose finite log-probabilities are all in [-2^80, 0], the bench path; row-A0
-// association): every candidate is <= 0, so the error of its estimate is RELATIVE to the
-// estimate itself and the interval test collapses to one threshold on f32 estimates
-//   x_i = f32(hi_i) + at32[cur][i]      (f32 a^T table, round to nearest)
+// NONPOS (models whose finite log-probabilities are all in [-2^80, 0], the bench path; row A0
+// and DPSolver's association): every candidate is <= 0, so the error of its estimate is
+// RELATIVE to the estimate itself and the interval test collapses to one threshold on f32
+// estimates
+//   x_i = f32(hi_i) + at32[cur][i]      (f32 a^T table, round to nearest; DPSolver: f32 of the
+//                                        f64 sum a[i,cur] + b[cur,o_t] the forward pass used)
 //   |s_i - x_i| <= c |x_i|,  c = 1.25 * 2^-20:  hi truncation |h| 2^-20, the f32 roundings of
 //   h, a and their sum (2^-24 each), the f64 rounding of s (2^-53); |h|, |a| <= |x| as all
 //   three are <= 0; f32 flushes of subnormals stay below the 2^-100 floor
@@ -677,13 +679,26 @@ __device__ __forceinline__ void bt_chain_f64(const uint32_t* __restrict__ rows, 
         if (lane == (tp & 63)) pathreg = cur;
         if ((tp & 63) == 0 && tp + lane < T) path[tp + lane] = pathreg;
       } else if (NONPOS && t >= 1) {
-        const float* acol32 = at32 + (size_t)cur * NP + lane;
+        // row A0: f32(a) from the f32 table; DPSolver (dp_assoc): f32 of the forward pass's own
+        // f64 sum a + b[cur, o_t] (all terms <= 0 either way: the same bound c)
+        float av32[KP];
+        double edp = 0.0;
+        if (dp_assoc) {
+          edp = et[(size_t)obs[t] * NP + cur];
+          const double* acol = at + (size_t)cur * NP + lane;
+#pragma unroll
+          for (int k = 0; k < KP; ++k) av32[k] = (float)(acol[64 * k] + edp);
+        } else {
+          const float* acol32 = at32 + (size_t)cur * NP + lane;
+#pragma unroll
+          for (int k = 0; k < KP; ++k) av32[k] = acol32[64 * k];
+        }
         float x[KP];
         float lm = -__builtin_inff();
 #pragma unroll
         for (int k = 0; k < KP; ++k) {
           // padded candidates: hi word -inf, at32 -inf
-          x[k] = (float)from_words(ring[u][k], 0u) + acol32[64 * k];
+          x[k] = (float)from_words(ring[u][k], 0u) + av32[k];
           lm = __builtin_fmaxf(lm, x[k]);
         }
         const float M = wave_max_f32(lm);
@@ -704,7 +719,9 @@ __device__ __forceinline__ void bt_chain_f64(const uint32_t* __restrict__ rows, 
           double sx[KP];
 #pragma unroll
           for (int k = 0; k < KP; ++k)
-            sx[k] = valid[k] ? from_words(ring[u][k], lw[k]) + acol[64 * k] : ninf_d();
+            sx[k] = valid[k] ? (dp_assoc ? (acol[64 * k] + edp) + from_words(ring[u][k], lw[k])
+                                         : from_words(ring[u][k], lw[k]) + acol[64 * k])
+                             : ninf_d();
           double Md;
           cur = first_argmax_d<KP>(sx, valid, Md);
         }
@@ -816,7 +833,7 @@ __device__ __forceinline__ void backtrack_one_f64(const T64BtArgs& g, int64_t sl
   }
   if (!NONPOS && g.only_infeasible) return;  // feasible: done by the NONPOS kernel
   if constexpr (NONPOS)
-    bt_chain_f64<KP, PF, false, true>(rows, T, cur, path, g.at, g.et, g.obs + e0, 0, N, lane, g.at32);
+    bt_chain_f64<KP, PF, false, true>(rows, T, cur, path, g.at, g.et, g.obs + e0, g.dp_assoc, N, lane, g.at32);
   else
     bt_chain_f64<KP, PF>(rows, T, cur, path, g.at, g.et, g.obs + e0, g.dp_assoc, N, lane);
   if (lane == 0) {
@@ -1155,7 +1172,7 @@ hipError_t bt_pf_np(int np, const T64BtArgs& ba, dim3 grid, dim3 block, hipStrea
 
 template <int PF>
 hipError_t bt_pf(int np, const T64BtArgs& ba, dim3 grid, dim3 block, hipStream_t stream, bool persist) {
-  if (ba.at32 && !ba.dp_assoc) {
+  if (ba.at32) {
     hipError_t e = bt_pf_np<PF, true>(np, ba, grid, block, stream, persist);
     if (e == hipSuccess && ba.decode_bt) {  // viterbi::decode: the infeasible sequences' DEC chains
       T64BtArgs b2 = ba;

@@ -129,7 +129,7 @@ def test_t64_backtrack_interval_paths(gpu, n, kind):
     off = synth.offsets_from_lengths(lengths)
     obs = rng.integers(0, v, size=int(off[-1])).astype(np.int32)
     h = cv.HMM(pi, a, b)
-    for assoc in ("viterbi", "decode"):
+    for assoc in ("viterbi", "decode", "dp"):
         got = cv.decode_batch(h, off, obs, dtype="f64", assoc=assoc, rescore_f64=False)
         assert cv.last_timing(h)["kernel"] == "trellis_f64"
         _assert_same(got, O.decode_batch(pi, a, b, off, obs, ASSOC[assoc], np.float64), f"{kind} {assoc} N={n}")
