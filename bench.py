@@ -56,6 +56,9 @@ def parse():
     p.add_argument("--no-f32-extra", action="store_true", help="skip the f32-trellis extra measurement")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--backend", choices=("nccl", "gloo"), default="nccl",
+                   help="collective backend for N>1 (nccl = RCCL over xGMI; gloo only to rehearse the "
+                        "multi-rank path with several ranks on one GPU)")
     return p.parse_args()
 
 
@@ -138,10 +141,14 @@ def main():
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     if not torch.cuda.is_available():
         raise SystemExit("bench.py needs a GPU (MI355X); none visible")
+    local = local % max(torch.cuda.device_count(), 1)  # == LOCAL_RANK on a node with one GPU per rank
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
 
     from cviterbi import dist as cvd
 
@@ -215,7 +222,7 @@ def main():
             dist.barrier()
         el = time.perf_counter() - t0
         if world > 1:
-            tt = torch.tensor([el], dtype=torch.float64, device=dev)
+            tt = torch.tensor([el], dtype=torch.float64, device="cpu" if args.backend == "gloo" else dev)
             dist.all_reduce(tt, op=dist.ReduceOp.MAX)
             el = float(tt.item())
         return el, fwd_ms, bt_ms, launches
@@ -270,7 +277,8 @@ def main():
                                (", exact-f64 row-A0 trellis + backtrack (paths/scores bit-identical to the f64 "
                                 "reference recurrence)" if f64 else
                                 ", f32 row-A0 trellis + backtrack + f64 re-score") +
-                               (", RCCL gather to rank 0 (overlapped with the next step)" if world > 1 else ""),
+                               ((", RCCL gather to rank 0 (overlapped with the next step)" if args.backend == "nccl" else
+                                 ", gloo gather to rank 0 (rehearsal: ranks may share a GPU)") if world > 1 else ""),
                    "global_batch": B, "seq_len": T_LEN, "states": N_STATES, "parallelism": f"batch-shard x{world}"},
         "seqs_per_s": B * args.steps / el,
         "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",

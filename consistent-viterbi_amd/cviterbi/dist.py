@@ -69,11 +69,16 @@ def gather_packed_to_root(path, score, status, nstates, elem_cap, seq_cap, dist)
     o += elem_cap * psz
     buf[o: o + status.numel()] = status.to(torch.uint8)
     rank = dist.get_rank()
-    lst = [torch.empty(nbytes, dtype=torch.uint8, device=dev) for _ in range(dist.get_world_size())] \
+    # gloo gathers host tensors only (CPU tests, the 1-GPU rehearsal of bench.py)
+    host = dist.get_backend() == "gloo" and buf.device.type != "cpu"
+    src = buf.cpu() if host else buf
+    lst = [torch.empty(nbytes, dtype=torch.uint8, device=src.device) for _ in range(dist.get_world_size())] \
         if rank == 0 else None
-    dist.gather(buf, lst, dst=0)
+    dist.gather(src, lst, dst=0)
     if rank != 0:
         return None
+    if host:
+        lst = [b.to(dev) for b in lst]
     out = []
     for b in lst:
         sc = b[: seq_cap * 8].view(torch.float64)

@@ -1,0 +1,30 @@
+"""GPU: bench.py's multi-rank path (strong-scaling shards, per-rank decode, barriers, the
+max-over-ranks timing, the packed gather to rank 0, the JSON line) rehearsed with 2 ranks on
+one GPU over gloo -- RCCL refuses two ranks on one device ("Duplicate GPU detected"), so the
+RCCL gather itself runs only on a multi-GPU node (the driver's scaling runs)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+from conftest import ROOT
+
+pytestmark = pytest.mark.gpu
+
+
+def test_bench_two_rank_rehearsal(gpu):
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", "29561", os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--steps", "2", "--warmup", "1", "--batch", "2048", "--backend", "gloo",
+           "--no-f32-extra"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]  # rank 0 prints ONE line
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["scaling"] == "strong" and d["dtype"] == "f64"
+    assert d["config"]["global_batch"] == 2048 and "sharded over 2 ranks" in d["config"]["workload"]
+    assert d["value"] > 0 and d["roofline"]["kernel"].startswith("trellis_fwd_f64")
