@@ -4,6 +4,7 @@ one GPU over gloo -- RCCL refuses two ranks on one device ("Duplicate GPU detect
 RCCL gather itself runs only on a multi-GPU node (the driver's scaling runs)."""
 import json
 import os
+import signal
 import subprocess
 import sys
 
@@ -20,10 +21,18 @@ def test_bench_two_rank_rehearsal(gpu):
            "--master-addr", "127.0.0.1", "--master-port", "29561", os.path.join(ROOT, "bench.py"),
            "--gpus", "2", "--steps", "2", "--warmup", "1", "--batch", "2048", "--backend", "gloo",
            "--no-f32-extra"]
-    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
-    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
-    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
-    assert len(lines) == 1, r.stdout[-2000:]  # rank 0 prints ONE line
+    # own session: on a timeout the launcher AND its ranks are killed (process group)
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env, cwd=ROOT,
+                         start_new_session=True)
+    try:
+        out, err = p.communicate(timeout=240)
+    except subprocess.TimeoutExpired:
+        os.killpg(p.pid, signal.SIGKILL)
+        p.communicate()
+        raise
+    assert p.returncode == 0, out[-3000:] + err[-3000:]
+    lines = [l for l in out.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out[-2000:]  # rank 0 prints ONE line
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["scaling"] == "strong" and d["dtype"] == "f64"
     assert d["config"]["global_batch"] == 2048 and "sharded over 2 ranks" in d["config"]["workload"]
