@@ -7,7 +7,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/${TAG:-pmc_f64}
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
-ARGS="--steps 1 --warmup 1 --no-cpu-baseline --no-f32-extra"
+ARGS="--steps 1 --warmup 1 --no-cpu-baseline --no-f32-extra ${PMC_ARGS:-}"
 for C in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 ${T_PMC:-240} rocprofv3 --pmc $C --kernel-include-regex "${KRE:-trellis_fwd_f64}" -d $OUT/$C -o p \
     --output-format csv -- python3 $R/bench.py $ARGS > $OUT/$C.log 2>&1 || exit $?
