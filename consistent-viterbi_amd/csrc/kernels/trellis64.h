@@ -34,6 +34,10 @@ struct T64FwdArgs {
   const int64_t* row_base;     // [slot] delta row index of the range's first element
   const double* resume_rows;   // [r][NP] already-forced rows (resume flow)
   const int32_t* slot_order;   // [launch index] -> slot (longest first)
+  // SIMD balancing (trellis_fwd_f64): every `balance` steps each wave publishes its remaining
+  // steps in a per-SIMD table and takes issue priority 3 if no other wave of its SIMD has more
+  // work left, else 1 (the arbiter runs the oldest wave first among equals); 0 = off
+  int balance;
 };
 
 struct T64BtArgs {

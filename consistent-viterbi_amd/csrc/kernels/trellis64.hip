@@ -142,8 +142,76 @@ __device__ __forceinline__ void load_row_buf(__amdgpu_buffer_rsrc_t r, uint32_t 
 // same S sequences, share delta_{t-1} in LDS and meet at two barriers per step (before
 // overwriting delta_{t-1}, after writing delta_t).  At full batches W = 1 is faster (the VALU
 // is saturated either way and W = 2 runs at a lower clock, profiles/r02_ab_fwd_w2.txt).
+// per-SIMD progress table of trellis_fwd_f64's balancing: [XCC][SE][SH][CU][SIMD][wave slot]
+// remaining steps (0 = empty); zero-initialised with the code object, every wave clears its slot
+__device__ int g_t64_simd[16 * 8 * 2 * 16 * 4 * 16];
+
+// SIMD balancing (T64FwdArgs::balance).  The arbiter issues the OLDEST of equal-priority waves
+// first, so of a SIMD's waves one finishes far ahead and the last one then runs alone at the
+// much lower one-wave issue rate (one round of 2,048 waves at 8,192 sequences: wave durations
+// 12.9 .. 20.9 ms; balanced 18.3 .. 19.5 ms, tools/debug/t64_probe.py).  Each wave publishes
+// its remaining steps in g_t64_simd[its SIMD][its wave slot] (HW_ID / XCC_ID) and runs at
+// priority 3 only while no other wave of its SIMD has more work left, else 1: the waves of a
+// SIMD finish together.  The words go through L2 (agent-scope relaxed atomics: vector memory
+// operations that bypass the CU's L1); a slot is 0 when empty, so a stale word only mis-sets a
+// priority, never a result.
+struct SimdBalance {
+  int* tab = nullptr;
+  int slot = 0;
+  __device__ void init(int enabled, int lane, int remaining) {
+    if (!enabled) return;
+    const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_REG_HW_ID
+    const unsigned xc = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // HW_REG_XCC_ID
+    const unsigned key = ((((xc & 15) * 8 + ((hw >> 13) & 7)) * 2 + ((hw >> 12) & 1)) * 16 + ((hw >> 8) & 15)) * 4 +
+                         ((hw >> 4) & 3);
+    tab = g_t64_simd + (size_t)key * 16;
+    slot = (int)(hw & 15);
+    publish(lane, remaining);
+  }
+  __device__ void publish(int lane, int remaining) const {
+    if (lane == 0) __hip_atomic_store(tab + slot, remaining, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  // lane k < 16: the remaining steps of wave slot k of this SIMD (0 for this wave's own slot)
+  __device__ int others(int lane) const {
+    return (lane < 16 && lane != slot) ? __hip_atomic_load(tab + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+  }
+  __device__ void decide(int other, int remaining) const {
+    int m = other;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) m = max(m, __builtin_amdgcn_readlane(other, k));
+    if (remaining >= m)
+      __builtin_amdgcn_s_setprio(3);
+    else
+      __builtin_amdgcn_s_setprio(1);
+  }
+  __device__ void finish(int lane) const {
+    if (tab) publish(lane, 0);
+  }
+};
+#ifdef CV_T64_PROBE
+// debug build only: per wave {real-time start, end, s_memtime start, end, HW_ID, XCC_ID}
+__device__ uint64_t g_t64_probe[1 << 17][6];
+#endif
 template <int C, int S, int PF, bool DPA, bool EXT, int W = 1, bool CAP2 = (W > 1), int GRP = 2>
 __global__ __launch_bounds__(64 * W) void trellis_fwd_f64(T64FwdArgs g) {
+#ifdef CV_T64_PROBE
+  const uint64_t pr_rt0 = __builtin_amdgcn_s_memrealtime(), pr_c0 = __builtin_amdgcn_s_memtime();
+  struct ProbeEnd {
+    uint64_t rt0, c0;
+    __device__ ~ProbeEnd() {
+      const unsigned idx = (blockIdx.x * W + (threadIdx.x >> 6)) & ((1u << 17) - 1);
+      if ((threadIdx.x & 63) == 0) {
+        uint64_t* p = g_t64_probe[idx];
+        p[0] = rt0;
+        p[1] = __builtin_amdgcn_s_memrealtime();
+        p[2] = c0;
+        p[3] = __builtin_amdgcn_s_memtime();
+        p[4] = (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);
+        p[5] = (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 20);
+      }
+    }
+  } pr_end{pr_rt0, pr_c0};
+#endif
   constexpr int NP = 64 * C * W;
   static_assert(S % 2 == 0, "S sequences are read from LDS two at a time");
   static_assert(NP % PF == 0, "the ring wraps around at row NP");
@@ -311,6 +379,10 @@ __global__ __launch_bounds__(64 * W) void trellis_fwd_f64(T64FwdArgs g) {
     __builtin_amdgcn_sched_barrier(0);
   }
   double acc[C][S];
+  // SIMD balancing (SimdBalance): every g.balance steps
+  const int bal = g.balance;
+  SimdBalance sb;
+  sb.init(bal > 0, lane, Tmax - 1);
   for (int t = 1; t < Tmax; ++t) {
     const unsigned ocur_l = obs_use(onext_l, t);
     const int fcur_l = frc_use(fnext_l);
@@ -385,6 +457,14 @@ __global__ __launch_bounds__(64 * W) void trellis_fwd_f64(T64FwdArgs g) {
     wg_sync();
     // epilogue: d_t = m + b[:, o_t] (viterbi.rs:17), emission rows of all S sequences in flight
     // together; then the next step's observations (scalar loads)
+    // balancing: publish this wave's remaining steps, read the other slots of its SIMD (the
+    // loads complete with the emission loads below, which the epilogue waits for anyway)
+    const bool bal_step = sb.tab && (t % bal == 0);
+    int other = 0;
+    if (bal_step) {
+      sb.publish(lane, Tmax - t);
+      other = sb.others(lane);
+    }
     double e[DPA ? 1 : S][C];
     if constexpr (!DPA) {
 #pragma unroll
@@ -414,7 +494,9 @@ __global__ __launch_bounds__(64 * W) void trellis_fwd_f64(T64FwdArgs g) {
     }
     asm volatile("" ::: "memory");
     wg_sync();  // delta_t complete in LDS before the next step reads it
+    if (bal_step) sb.decide(other, Tmax - t);
   }
+  sb.finish(lane);
   if (wv == 0 && lane < S && my_bad) g.status[my_seq] = CVK_SEQ_BADOBS;
 }
 
@@ -1118,6 +1200,13 @@ hipError_t launch_t64_cp_fwd(int np, int s, const T64FwdArgs& fa, int64_t nseq, 
   }
 }
 
+#ifdef CV_T64_PROBE
+extern "C" __attribute__((visibility("default"))) int cv_debug_t64_probe(uint64_t* out, int nwaves) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_t64_probe), sizeof(uint64_t) * 6 * (size_t)nwaves, 0,
+                                  hipMemcpyDeviceToHost);
+}
+#endif
+
 int t64_padded_states(int n) { return (n >= 1 && n <= 256) ? 64 * ((n + 63) / 64) : 0; }
 
 int t64_seqs_per_wave(int64_t nseq, int cus) {
@@ -1133,8 +1222,14 @@ int t64_seqs_per_wave(int64_t nseq, int cus) {
   return 2;
 }
 
-hipError_t launch_t64_fwd(int np, int s, const T64FwdArgs& fa, int64_t nseq, hipStream_t stream) {
+hipError_t launch_t64_fwd(int np, int s, const T64FwdArgs& fa_in, int64_t nseq, hipStream_t stream) {
   if (nseq <= 0) return hipSuccess;
+  static const int balance = [] {  // A/B knob (bit-identical): CV_T64_BAL = steps between SIMD balancing, 0 = off
+    const char* e = getenv("CV_T64_BAL");
+    return e ? atoi(e) : 8;
+  }();
+  T64FwdArgs fa = fa_in;
+  fa.balance = balance;
   static const bool wave = [] {  // A/B knob (bit-identical): CV_T64_WAVE=0 keeps the lock-step layout
     const char* e = getenv("CV_T64_WAVE");
     return !(e && e[0] == '0');
