@@ -1229,7 +1229,10 @@ hipError_t launch_t64_fwd(int np, int s, const T64FwdArgs& fa_in, int64_t nseq, 
     return e ? atoi(e) : 8;
   }();
   T64FwdArgs fa = fa_in;
-  fa.balance = balance;
+  // the batch decode only: the constrained decode's passes (EXT, 2 sequences per wave, two
+  // streams) ran ~2% slower balanced (profiles/r02_t64_simd_balance.txt)
+  fa.balance = (fa.forced || fa.ranges || fa.reverse || fa.start || fa.row_base || fa.resume_rows ||
+                fa.slot_order || fa.last_row) ? 0 : balance;
   static const bool wave = [] {  // A/B knob (bit-identical): CV_T64_WAVE=0 keeps the lock-step layout
     const char* e = getenv("CV_T64_WAVE");
     return !(e && e[0] == '0');
