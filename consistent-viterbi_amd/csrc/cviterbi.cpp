@@ -94,7 +94,7 @@ cv_status upload(DevBuf& buf, const void* src, size_t bytes) {
 }
 
 constexpr uint64_t kDefaultWorkspace = 8ull << 30;
-constexpr uint64_t kDefaultWorkspaceT64 = 40ull << 30;
+constexpr uint64_t kDefaultWorkspaceT64 = 64ull << 30;  // config 5 resume decode in one chunk: 3% faster than 40 GiB
 
 }  // namespace
 
@@ -1155,7 +1155,7 @@ struct PrefixKeep {
 
 // The resume flow covers f32 N > 64 with NP % 64 == 0 (pair kernel + backtrack_v) and every f64
 // N <= 256; its stored rows must fit 4x the workspace cap (32 GiB by default: config 5 needs
-// 8.6 GB of f32 rows; f64 rows are twice that, within the f64 trellis's 40 GiB cap x 4).
+// 8.6 GB of f32 rows; f64 rows are twice that, within the f64 trellis's 64 GiB cap x 4).
 bool resume_supported(const cv_hmm* h, bool f64) {
   const char* e = getenv("CV_NO_RESUME");
   if (e && *e && *e != '0') return false;

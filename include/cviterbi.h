@@ -97,7 +97,7 @@ typedef struct cv_opts {
                             the VITERBI association (what the f64 reference computes along
                             that path); 0: the kernel's own score (f32 widened for F32) */
   void* stream;          /* hipStream_t for the *_device entry points; NULL = handle stream */
-  uint64_t workspace_bytes; /* delta/psi workspace cap; 0 = default (8 GiB; 40 GiB for TRELLIS_F64) */
+  uint64_t workspace_bytes; /* delta/psi workspace cap; 0 = default (8 GiB; 64 GiB for TRELLIS_F64) */
   uint32_t flags;        /* CV_FLAG_* (0 = defaults) */
   const int32_t* forced; /* [sum T] nullable: -1 = free, s >= 0 = state s forced at that element
                             (host pointer for cv_decode_batch, device pointer for *_device) */

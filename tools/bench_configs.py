@@ -61,7 +61,8 @@ for name in which:
 
         def run():
             cv.decode_constrained_device(h, off, o_d, ob_d, comp, p_d, s_d, st_d, ncomp=7,
-                                         stream=stream.cuda_stream, dtype="f32" if name == "c5f32" else "f64")
+                                         stream=stream.cuda_stream, dtype="f32" if name == "c5f32" else "f64",
+                                         workspace_bytes=int(os.environ.get("WS_GB", "0")) << 30)
     run()
     run()
     torch.cuda.synchronize()
