@@ -5,6 +5,8 @@ Bar (BASELINE.json north_star): paths bit-exact and scores bit-exact (tolerance 
 relative) against the f64 oracle, every status identical; and identical to the generic f64
 kernel (inline first-argmax) on batches too large for the oracle to finish in seconds.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -13,6 +15,7 @@ import cviterbi as cv
 from cviterbi import synth
 
 pytestmark = pytest.mark.gpu
+PKG = os.path.dirname(os.path.dirname(os.path.abspath(cv.__file__)))
 
 
 def _case(n, v, seed, nseq=12, tmax=70, zero_frac=0.0, tmin=1):
@@ -103,6 +106,31 @@ def test_t64_small_batch_layouts_vs_generic(gpu, nseq):
     _assert_same(got, cv.decode_batch(h, off, obs, dtype="f64", kernel="generic", rescore_f64=False), f"B={nseq}")
     assert np.all(got[2] == 0)
     np.testing.assert_array_equal(got[1], O.rescore_batch_f64(pi, a, b, off, obs, got[0]))
+
+
+def test_t64_simd_balance_knob_bit_identical(gpu, tmp_path):
+    """SIMD balancing (issue priority by remaining work) and the small-batch pair layout are
+    scheduling only: a child process with CV_T64_BAL=0 (no balancing) and CV_T64_W2=0 (one wave
+    per group) decodes the same single-round batch to the same bits."""
+    import subprocess
+    import sys
+
+    pi, a, b = synth.random_hmm(256, 64, seed=79)
+    rng = np.random.default_rng(79)
+    off = synth.offsets_from_lengths(rng.integers(60, 97, size=8192))
+    obs = rng.integers(0, 64, size=int(off[-1])).astype(np.int32)
+    np.savez(tmp_path / "in.npz", pi=pi, a=a, b=b, off=off, obs=obs)
+    got = cv.decode_batch(cv.HMM(pi, a, b), off, obs, dtype="f64", rescore_f64=False)
+    code = (
+        "import sys, numpy as np; sys.path.insert(0, sys.argv[1]); import cviterbi as cv; "
+        "d = np.load(sys.argv[2]); h = cv.HMM(d['pi'], d['a'], d['b']); "
+        "p, s, st = cv.decode_batch(h, d['off'], d['obs'], dtype='f64', rescore_f64=False); "
+        "np.savez(sys.argv[3], p=p, s=s, st=st)")
+    env = dict(os.environ, CV_T64_BAL="0", CV_T64_W2="0")
+    subprocess.run([sys.executable, "-c", code, PKG, str(tmp_path / "in.npz"), str(tmp_path / "out.npz")],
+                   env=env, check=True, timeout=120)
+    ref = np.load(tmp_path / "out.npz")
+    _assert_same(got, (ref["p"], ref["s"], ref["st"]), "balance/W2 knobs")
 
 
 @pytest.mark.parametrize("n", [64, 200, 256])
