@@ -1287,16 +1287,20 @@ hipError_t launch_t64_bt(int np, const T64BtArgs& ba, int64_t nseq, hipStream_t 
   int64_t wgs = (nseq + 3) / 4;
   if (max_wgs > 0 && wgs > max_wgs) wgs = max_wgs;
   const dim3 grid((unsigned)wgs), block(256);
-  static const int pf_env = [] {  // tuning knob (bit-identical): 2, 4, 8 or 16 rows in flight
+  static const int pf_env = [] {  // tuning knob (bit-identical): 2, 4, 8, 16 or 32 rows in flight
     const char* e = getenv("CV_T64_BT_PF");
     return e ? atoi(e) : 0;
   }();
-  const int pf = pf_env ? pf_env : np >= 192 ? 2 : 8;
+  // NP = 64 (configs 2/3): the longest chains set the makespan and each step's hi row (256 B)
+  // comes from HBM: 32 rows in flight, config 3 backtrack 0.615 -> 0.51 ms (16: 0.54)
+  // (profiles/r02_ab_bt_pf_c3.txt); N = 256: occupancy matters more (2 rows, 8 waves/SIMD)
+  const int pf = pf_env ? pf_env : np >= 192 ? 2 : np == 64 ? 32 : 8;
   const bool persist = max_wgs > 0 && (nseq + 3) / 4 > max_wgs;
   switch (pf) {
     case 2: return bt_pf<2>(np, ba, grid, block, stream, persist);
     case 4: return bt_pf<4>(np, ba, grid, block, stream, persist);
     case 16: return bt_pf<16>(np, ba, grid, block, stream, persist);
+    case 32: return np == 64 ? bt_pf<32>(np, ba, grid, block, stream, persist) : hipErrorInvalidValue;
     default: return bt_pf<8>(np, ba, grid, block, stream, persist);
   }
 }
