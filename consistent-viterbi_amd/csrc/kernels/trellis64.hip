@@ -1252,12 +1252,17 @@ hipError_t launch_t64_fwd(int np, int s, const T64FwdArgs& fa_in, int64_t nseq, 
 
 template <int PF, bool NONPOS, bool PERSIST>
 hipError_t bt_pf_np(int np, const T64BtArgs& ba, dim3 grid, dim3 block, hipStream_t stream) {
-  switch (np) {
-    case 64: hipLaunchKernelGGL((backtrack_f64<1, PF, NONPOS, PERSIST>), grid, block, 0, stream, ba); break;
-    case 128: hipLaunchKernelGGL((backtrack_f64<2, PF, NONPOS, PERSIST>), grid, block, 0, stream, ba); break;
-    case 192: hipLaunchKernelGGL((backtrack_f64<3, PF, NONPOS, PERSIST>), grid, block, 0, stream, ba); break;
-    case 256: hipLaunchKernelGGL((backtrack_f64<4, PF, NONPOS, PERSIST>), grid, block, 0, stream, ba); break;
-    default: return hipErrorInvalidValue;
+  if constexpr (PF == 32) {  // NP = 64 only (launch_t64_bt)
+    if (np != 64) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((backtrack_f64<1, PF, NONPOS, PERSIST>), grid, block, 0, stream, ba);
+  } else {
+    switch (np) {
+      case 64: hipLaunchKernelGGL((backtrack_f64<1, PF, NONPOS, PERSIST>), grid, block, 0, stream, ba); break;
+      case 128: hipLaunchKernelGGL((backtrack_f64<2, PF, NONPOS, PERSIST>), grid, block, 0, stream, ba); break;
+      case 192: hipLaunchKernelGGL((backtrack_f64<3, PF, NONPOS, PERSIST>), grid, block, 0, stream, ba); break;
+      case 256: hipLaunchKernelGGL((backtrack_f64<4, PF, NONPOS, PERSIST>), grid, block, 0, stream, ba); break;
+      default: return hipErrorInvalidValue;
+    }
   }
   return hipGetLastError();
 }
