@@ -160,6 +160,26 @@ struct cv_hmm {
 
 namespace {
 
+// Device bytes free right now plus `held` (buffers the caller is about to re-size); 0 when the
+// runtime cannot tell.
+uint64_t free_device_bytes(uint64_t held) {
+  size_t fr = 0, tot = 0;
+  if (hipMemGetInfo(&fr, &tot) != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  return (uint64_t)fr + held;
+}
+
+// The default delta-workspace cap when the caller leaves opts.workspace_bytes at 0: `base`
+// (sized for 288 GB of HBM3E), clamped to 3/4 of what the device can still give this handle's
+// workspace, so a smaller or busier card chunks the batch instead of failing in hipMalloc.
+uint64_t default_workspace_cap(const cv_hmm* h, uint64_t base) {
+  const uint64_t avail = free_device_bytes(h->ws_main.bytes);
+  if (avail == 0) return base;
+  return std::max<uint64_t>(std::min<uint64_t>(base, avail / 4 * 3), 256ull << 20);
+}
+
 cv_status set_device(cv_hmm* h) {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) {
@@ -533,7 +553,8 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
   // Per-element workspace bytes: trellis keeps f32 delta rows [NP]; generic keeps u16 psi [N].
   // f64 trellis: 2 KiB of delta per element at N = 256 and >= 16,384 sequences per launch for
   // 8 sequences per wave, so its default cap is larger (HBM3E: 288 GB per GPU)
-  const uint64_t cap = o.workspace_bytes ? o.workspace_bytes : use_t64 ? kDefaultWorkspaceT64 : kDefaultWorkspace;
+  const uint64_t cap = o.workspace_bytes ? o.workspace_bytes
+                                         : default_workspace_cap(h, use_t64 ? kDefaultWorkspaceT64 : kDefaultWorkspace);
   const uint64_t per_elem = use_trellis ? (uint64_t)(wave ? h->npw : h->np) * 4
                            : (use_t64 && !t64cp) ? (uint64_t)h->np64 * 8
                                        : (uint64_t)h->N * 2;
@@ -1244,10 +1265,19 @@ cv_status constrained_partials_locked(cv_hmm* h, int64_t nseq, const int64_t* of
     std::vector<int64_t> rbv((size_t)nc);
     int64_t rows = 0;
     for (int64_t i = 0; i < nc; ++i) rbv[(size_t)i] = rows, rows += rg[2 * i + 1] - rg[2 * i];
-    const uint64_t cap =
-        4 * (o.workspace_bytes ? o.workspace_bytes : f64 ? kDefaultWorkspaceT64 : kDefaultWorkspace);
-    if ((uint64_t)rows * row_bytes <= cap) {
-      if ((st = h->rs_rows.ensure((size_t)std::max<int64_t>(rows, 1) * row_bytes)) != CV_OK) return st;
+    // kept rows live beside the final decode's delta workspace: at most 4x the workspace cap
+    // AND at most half of the device memory this handle can still get (the other half stays
+    // for that workspace); too large, or a failed allocation, means the final decode runs the
+    // full forced passes instead (bit-identical, DESIGN.md §3 resume flow)
+    const uint64_t cap = std::min<uint64_t>(
+        4 * (o.workspace_bytes ? o.workspace_bytes : f64 ? kDefaultWorkspaceT64 : kDefaultWorkspace),
+        free_device_bytes(h->rs_rows.bytes) / 2);
+    bool fits = (uint64_t)rows * row_bytes <= cap;
+    if (fits && h->rs_rows.ensure((size_t)std::max<int64_t>(rows, 1) * row_bytes) != CV_OK) {
+      fits = false;
+      g_err.clear();
+    }
+    if (fits) {
       if ((st = h->rs_rowbase.ensure((size_t)nc * 8)) != CV_OK) return st;
       HIP_TRY(hipMemcpyAsync(h->rs_rowbase.p, rbv.data(), (size_t)nc * 8, hipMemcpyHostToDevice, stream));
       rows_d = h->rs_rows.p;
@@ -2206,7 +2236,8 @@ CV_API cv_status cv_solver_create(const char* kind, cv_hmm* h, const cv_superseq
   s->kind = kind;
   s->hmm = h;
   cv_opts_init(&s->opts);
-  if (s->kind == "gpu") {
+  if (s->kind == "gpu") {  // the opt-in f32 trellis + f64 re-score (cviterbi.h)
+    s->opts.dtype = CV_DTYPE_F32;
   } else if (s->kind == "gpu-f64") {
     s->opts.dtype = CV_DTYPE_F64;
   } else if (s->kind == "gpu-cp" || s->kind == "gpu-cp-seq") {
