@@ -17,6 +17,14 @@ statuses to rank 0 over xGMI -- issued on a second stream so that step k's gathe
 step k+1's decode (double-buffered outputs; the closing synchronize waits for the last
 one).  Inputs are resident in HBM before the timed region.
 
+After the timed region (never inside it):
+* N>1: rank 0 assembles the LAST step's gathered result and compares it bit for bit (paths,
+  scores, statuses) with its own single-GPU decode of the same global batch -> "verified";
+* rank 0: the CPU baseline (the oracle, test infrastructure, timed on this host) whose leg
+  also checks the GPU's first sequences against the oracle's f64 row-A0 decode;
+* rank 0: configs 2, 3 and 5 (BASELINE.json configs[1], [2], [4]) on its GPU, inputs
+  resident, as the extra key `configs` (--no-configs skips them).
+
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--scaling strong|weak] [--dtype f64|f32]
        (N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N)
 Rank 0 prints ONE JSON line.
@@ -36,10 +44,13 @@ sys.path.insert(0, os.path.join(ROOT, "consistent-viterbi_amd"))
 
 N_STATES, V_OBS, T_LEN, B_TOTAL, SEED = 256, 1024, 512, 65536, 20261015
 HBM_PEAK = 8.0e12            # B/s, MI355X_MICROARCH.md chip table (spec)
-VALU_PAIR_PEAK = 3.93e13     # (from,to) pairs/s: 256 CU x 4 SIMD x 32 lanes x 2.4 GHz / 2 VALU slots per pair
+VALU_PAIR_PEAK = 3.93e13     # f32 (from,to) pairs/s: 256 CU x 4 SIMD x 32 lanes x 2.4 GHz / 2 VALU slots per pair
+F64_PAIR_PEAK = 1.966e13     # f64 (from,to) pairs/s: 256 CU x 64 lanes x 2.4 GHz / (v_add_f64 + v_max_f64)
+NOMINAL_GHZ = 2.4
 WORKSPACE = 48 << 30         # delta workspace cap: one forward launch per step at N=1 (34.4 GB)
 WORKSPACE_F64 = 80 << 30     # f64: one launch per step too (68.7 GB of f64 delta rows)
-F64_PAIR_PEAK = 1.966e13     # f64 (from,to) pairs/s: 256 CU x 64 lanes x 2.4 GHz / (v_add_f64 + v_max_f64)
+PMC_F64 = "profiles/pmc_trellis_fwd_f64_c4.json"   # committed rocprofv3 PMC summary (traffic, clock)
+PMC_F32 = "profiles/pmc_trellis_fwd_c4.json"
 
 
 def parse():
@@ -56,47 +67,63 @@ def parse():
     p.add_argument("--no-f32-extra", action="store_true", help="skip the f32-trellis extra measurement")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-configs", action="store_true", help="skip the configs 2/3/5 extra measurements")
+    p.add_argument("--no-verify", action="store_true", help="N>1: skip rank 0's re-decode of the global batch")
     p.add_argument("--backend", choices=("nccl", "gloo"), default="nccl",
                    help="collective backend for N>1 (nccl = RCCL over xGMI; gloo only to rehearse the "
                         "multi-rank path with several ranks on one GPU)")
     return p.parse_args()
 
 
-def cpu_baseline(pi, a, b, obs_rank, budget_s):
+def cpu_baseline(pi, a, b, obs_rank, budget_s, gpu_first):
     """Oracle (C restatement of the reference's CPSolver forward + backtrack, f64, CP
     association = what main.rs:120 runs) timed on this host on the first k sequences of this
     rank's shard; k grows until ~budget_s of CPU work.  `value` is the single-thread rate
     (the reference is single-threaded); `all_cores` repeats it with OpenMP across sequences
-    on this process's CPU share."""
+    on this process's CPU share.  As the checker, the leg also decodes the
+    first sequences of the shard with the oracle's f64 row-A0 recurrence (viterbi.rs:13-18)
+    and compares the GPU's result for them bit for bit (`gpu_first` = (path, score, status)
+    of those sequences)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import c_oracle
 
-    def run(k, threads):
-        off = np.arange(k + 1, dtype=np.int64) * T_LEN
-        t0 = time.perf_counter()
-        c_oracle.decode_batch(pi, a, b, off, obs_rank[: k * T_LEN], c_oracle.CP, np.float64, nthreads=threads)
-        return time.perf_counter() - t0
-
-    def sample(threads, budget):
-        k = 2 * threads
-        dt = run(k, threads)
-        k = max(2 * threads, min(int(budget / max(dt / k, 1e-6)), 4096 * threads))
-        return k, run(k, threads)
-
-    k, dt = sample(1, budget_s)
-    cells = k * T_LEN * N_STATES
     try:
         share = len(os.sched_getaffinity(0))
     except AttributeError:
         share = os.cpu_count() or 1
     nth = max(1, min(share, int(os.environ.get("OMP_NUM_THREADS", share)), 16))
+
+    def run(k, threads, assoc=c_oracle.CP):
+        off = np.arange(k + 1, dtype=np.int64) * T_LEN
+        t0 = time.perf_counter()
+        r = c_oracle.decode_batch(pi, a, b, off, obs_rank[: k * T_LEN], assoc, np.float64, nthreads=threads)
+        return time.perf_counter() - t0, r
+
+    def sample(threads, budget):
+        k = 2 * threads
+        dt, _ = run(k, threads)
+        k = max(2 * threads, min(int(budget / max(dt / k, 1e-6)), 4096 * threads))
+        return k, run(k, threads)[0]
+
+    k, dt = sample(1, budget_s)
+    cells = k * T_LEN * N_STATES
     km, dtm = sample(nth, budget_s / 2)
+    check = None
+    if gpu_first is not None:  # f64 decode: the oracle's f64 row-A0 result, bit for bit
+        kc = len(gpu_first[1])
+        _, (rp, rs, rst) = run(kc, nth, c_oracle.VITERBI)
+        gp, gs, gst = gpu_first
+        check = {"sequences": kc, "what": "GPU f64 decode vs oracle f64 row-A0 (viterbi.rs:13-18): paths, "
+                                          "scores (bits), statuses",
+                 "bit_exact": bool(np.array_equal(rp, gp) and np.array_equal(rs.view(np.int64), gs.view(np.int64))
+                                   and np.array_equal(rst, gst))}
     return {"value": cells / dt, "unit": "trellis cells/s", "cores": 1, "kind": "port",
             "sample": f"first {k} sequences of config 4 (N=256, T=512), f64 CP association "
                       f"(cp.rs:63-93), oracle/cv_oracle.c single thread, {dt:.1f} s",
             "seconds": dt,
             "all_cores": {"value": km * T_LEN * N_STATES / dtm, "cores": nth, "sequences": km, "seconds": dtm,
-                          "cpu": _cpu_model()}}
+                          "cpu": _cpu_model()},
+            "check": check}
 
 
 def _cpu_model():
@@ -110,20 +137,85 @@ def _cpu_model():
     return None
 
 
-def load_traffic(f64):
-    """HBM bytes per decoded ELEMENT of the forward kernel, from the committed rocprofv3 PMC
-    summary of the config-4 launch (f64: one 65,536-sequence launch; f32: one 8,192-sequence
-    launch); the traffic is the delta rows written, proportional to the elements a launch
-    decodes, so a rank's per-launch figure is this times its elements per launch."""
-    p = os.path.join(ROOT, "profiles", "pmc_trellis_fwd_f64_c4.json" if f64 else "pmc_trellis_fwd_c4.json")
+def load_pmc(f64):
+    """The committed rocprofv3 PMC summary of the forward kernel at config 4 (f64: one
+    65,536-sequence launch; f32: one 8,192-sequence launch): HBM bytes per decoded ELEMENT
+    (the traffic is the delta rows written, proportional to the elements a launch decodes)
+    and the effective clock (GRBM_GUI_ACTIVE over the kernel, when recorded)."""
+    rel = PMC_F64 if f64 else PMC_F32
+    p = os.path.join(ROOT, rel)
     if not os.path.exists(p):
         return None
     try:
         with open(p) as f:
             d = json.load(f)
-        return float(d["hbm_bytes_per_launch"]) / ((B_TOTAL if f64 else 8192) * T_LEN)
+        return {"per_elem": float(d["hbm_bytes_per_launch"]) / ((B_TOTAL if f64 else 8192) * T_LEN),
+                "clock_ghz": d.get("clock_ghz"), "source": rel + (" (" + d["source"] + ")" if "source" in d else "")}
     except Exception:
         return None
+
+
+def bench_configs(dev, stream):
+    """Configs 2, 3 (plain decode) and 5 (consistency-constrained decode, K=7) on this GPU in
+    the default mode (exact f64), inputs resident in HBM (device APIs), wall time per decode
+    after one warmup call.  Roofline fractions of the forward kernel: HBM on SURVEY.md §8(d)'s
+    (9N+8) B per step, f64 VALU on N^2 pairs per step."""
+    import torch
+
+    import cviterbi as cv
+    from cviterbi import synth
+
+    out = {}
+    for name, reps in (("c2", 20), ("c3", 10), ("c5", 3)):
+        c = synth.config(name)
+        n = c["pi"].shape[0]
+        off, obs = c["offsets"], c["obs"]
+        B = len(off) - 1
+        elems = int(off[-1])
+        h = cv.HMM(c["pi"], c["a"], c["b"], device=dev.index)
+        o_d, ob_d = torch.from_numpy(off).to(dev), torch.from_numpy(obs).to(dev)
+        p_d = torch.empty(elems, dtype=torch.int32, device=dev)
+        s_d = torch.empty(B, dtype=torch.float64, device=dev)
+        st_d = torch.empty(B, dtype=torch.uint8, device=dev)
+        if name == "c5":
+            comp = c["component"]
+
+            def run():
+                cv.decode_constrained_device(h, off, o_d, ob_d, comp, p_d, s_d, st_d, ncomp=7,
+                                             stream=stream.cuda_stream, dtype="f64")
+        else:
+            def run():
+                cv.decode_batch_device(h, o_d, ob_d, p_d, s_d, st_d, offsets_host=off, stream=stream.cuda_stream,
+                                       dtype="f64", workspace_bytes=WORKSPACE_F64)
+        run()
+        torch.cuda.synchronize(dev)
+        if int((st_d != 0).sum().item()):
+            raise SystemExit(f"{name}: sequences did not decode cleanly")
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            run()
+        torch.cuda.synchronize(dev)
+        dt = (time.perf_counter() - t0) / reps
+        t = cv.last_timing(h)
+        pairs = n * n * (elems - B)
+        d = {"workload": {"c2": "config2: N=45, V=50,000 Zipf emissions, 4,096 sequences, T in [1,128]",
+                          "c3": "config3: N=64, V=256, 16,384 sequences, T in [32,1024] (length-sorted schedule)",
+                          "c5": "config5: config 4 + one constrained position in half the sequences, K=7 "
+                                "components, exact f64 constrained decode"}[name],
+             "ms_per_decode": dt * 1e3, "cells_per_s": elems * n / dt, "seqs_per_s": B / dt, "reps": reps,
+             "valu_frac_end_to_end": pairs / dt / F64_PAIR_PEAK}
+        if name != "c5":
+            fwd = t["fwd_ms"] * 1e-3
+            d.update({"kernel": "trellis_wave_f64" if n <= 64 else "trellis_fwd_f64",
+                      "kernel_ms": t["fwd_ms"], "backtrack_ms": t["bt_ms"],
+                      "hbm_frac_8d": ((9 * n + 8) * elems + 8 * B) / fwd / HBM_PEAK,
+                      "valu_frac": pairs / fwd / F64_PAIR_PEAK})
+        else:
+            d["kernel"] = "trellis_fwd_f64 EXT (terms pass + resume decode) + backtracks + exact search"
+        out[name] = d
+        del h, o_d, ob_d, p_d, s_d, st_d
+        torch.cuda.empty_cache()
+    return out
 
 
 def main():
@@ -176,6 +268,7 @@ def main():
              torch.empty(nloc, dtype=torch.uint8, device=dev)) for _ in range(nbuf)]
     gathered = [None] * nbuf  # event: that buffer's gather has read it
     k_step = [0]
+    last = {}  # the last step's buffer index and, on rank 0, its gathered result
 
     def step(dtype):
         i = k_step[0] % nbuf
@@ -186,6 +279,7 @@ def main():
         cv.decode_batch_device(h, off_d, obs_d, path_d, score_d, status_d, offsets_host=off,
                                stream=stream.cuda_stream, dtype=dtype,
                                workspace_bytes=WORKSPACE_F64 if dtype == "f64" else WORKSPACE)
+        last["buf"] = i
         if world > 1:  # RCCL over xGMI: decoded paths (u8 states), scores, statuses to rank 0, one gather
             done = torch.cuda.Event()
             done.record(stream)
@@ -193,7 +287,8 @@ def main():
             with torch.cuda.stream(comm):
                 for t in outs[i]:
                     t.record_stream(comm)
-                cvd.gather_packed_to_root(path_d, score_d, status_d, N_STATES, per * T_LEN, per, dist)
+                last["gather"] = cvd.gather_packed_to_root(path_d, score_d, status_d, N_STATES, per * T_LEN, per,
+                                                           dist)
                 ev = torch.cuda.Event()
                 ev.record(comm)
                 gathered[i] = ev
@@ -205,36 +300,67 @@ def main():
         bad = int(sum(int((o[2] != 0).sum().item()) for o in outs))
         if bad:
             raise SystemExit(f"rank {rank}: {bad} sequences did not decode cleanly")
-        # timed region: barrier + sync on both sides, exactly K steps
+        # timed region: barrier + sync on both sides, exactly K steps; kernel times summed from
+        # HIP events recorded around each launch on the decode stream (read after the region)
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize(dev)
+        cv.timing_begin(h)
         t0 = time.perf_counter()
-        fwd_ms, bt_ms, launches = 0.0, 0.0, 0
         for _ in range(steps):
             step(dtype)
-            t = cv.last_timing(h)  # HIP events recorded around each kernel on `stream`
-            fwd_ms += t["fwd_ms"]
-            bt_ms += t["bt_ms"]
-            launches += t["launches"]
         torch.cuda.synchronize(dev)
         if world > 1:
             dist.barrier()
         el = time.perf_counter() - t0
+        kt = cv.timing_end(h)
         if world > 1:
             tt = torch.tensor([el], dtype=torch.float64, device="cpu" if args.backend == "gloo" else dev)
             dist.all_reduce(tt, op=dist.ReduceOp.MAX)
             el = float(tt.item())
-        return el, fwd_ms, bt_ms, launches
+        return el, kt
 
-    el, fwd_ms, bt_ms, launches = timed(args.dtype, args.steps, args.warmup)
-    spw = cv.last_timing(h).get("seqs_per_wave", 8)  # the layout of the timed run (before the f32 extra)
+    el, kt = timed(args.dtype, args.steps, args.warmup)
+    fwd_ms, bt_ms, launches = kt["fwd_ms"], kt["bt_ms"], kt["launches"]
+    spw = kt.get("seqs_per_wave", 8)  # the layout of the timed run (before the f32 extra)
+    # this rank's first sequences as the timed run decoded them (for the CPU baseline's check)
+    kc = min(64, nloc)
+    pb, sb, stb = outs[last["buf"]]
+    first = (pb[: kc * T_LEN].cpu().numpy(), sb[:kc].cpu().numpy(), stb[:kc].cpu().numpy()) if f64 else None
+
+    # ---- rank 0 re-decodes the global batch on its own GPU: the gathered last step must equal it
+    verify = None
+    if world > 1 and not args.no_verify:
+        ok = True
+        if rank == 0:
+            parts = last["gather"]
+            ns = [cvd.shard_range(B, world, r)[1] - cvd.shard_range(B, world, r)[0] if args.scaling == "strong"
+                  else args.batch for r in range(world)]
+            gp = cvd.assemble([x[0] for x in parts], [n * T_LEN for n in ns])
+            gs = cvd.assemble([x[1] for x in parts], ns)
+            gst = cvd.assemble([x[2] for x in parts], ns)
+            obs_g = torch.from_numpy(synth.iid_obs(V_OBS, B * T_LEN, SEED)).to(dev)
+            off_gh = np.arange(B + 1, dtype=np.int64) * T_LEN
+            rp = torch.empty(B * T_LEN, dtype=torch.int32, device=dev)
+            rs = torch.empty(B, dtype=torch.float64, device=dev)
+            rst = torch.empty(B, dtype=torch.uint8, device=dev)
+            cv.decode_batch_device(h, torch.from_numpy(off_gh).to(dev), obs_g, rp, rs, rst, offsets_host=off_gh,
+                                   stream=stream.cuda_stream, dtype=args.dtype,
+                                   workspace_bytes=WORKSPACE_F64 if f64 else WORKSPACE)
+            torch.cuda.synchronize(dev)
+            ok = bool(torch.equal(gp.to(dev), rp) and torch.equal(gs.to(dev).view(torch.int64), rs.view(torch.int64))
+                      and torch.equal(gst.to(dev), rst))
+            verify = {"what": "last step's gathered paths/scores/statuses (all ranks) == rank 0's single-GPU "
+                              "decode of the same global batch, bit for bit", "sequences": B, "equal": ok}
+            del obs_g, rp, rs, rst
+        dist.barrier()
+
     f32_extra = None
     if f64 and not args.no_f32_extra:
-        el32, fwd32, bt32, l32 = timed("f32", args.steps, args.warmup)
+        el32, kt32 = timed("f32", args.steps, args.warmup)
         f32_extra = {"value": B * T_LEN * N_STATES * args.steps / el32, "unit": "trellis cells/s",
                      "ms_per_step": el32 * 1e3 / args.steps,
-                     "kernel": "trellis_fwd2_f32<256>", "kernel_ms_per_launch": fwd32 / max(l32, 1),
+                     "kernel": "trellis_fwd2_f32<256>", "kernel_ms_per_launch": kt32["fwd_ms"] / max(kt32["launches"], 1),
                      "note": "f32 log-probs (BASELINE config 4 literally), f64 re-score of each path; "
                              "paths differ from the f64 reference on ~3.7% of config-4 sequences (19 of the first 512)"}
 
@@ -243,21 +369,27 @@ def main():
     ms_step = el * 1e3 / args.steps
     # roofline of the dominant kernel (forward trellis) on THIS rank, per launch
     steps_rank = nloc * T_LEN
-    if f64:  # read obs 4 B + f64 emission column 8N; write f64 delta column 8N + path 4 B
-        alg_bytes = (16 * N_STATES + 8) * steps_rank + 8 * nloc
-        alg_read = (8 * N_STATES + 4) * steps_rank
-    else:
-        alg_bytes = (9 * N_STATES + 8) * steps_rank + 8 * nloc
-        alg_read = (4 * N_STATES + 4) * steps_rank
+    lps = launches / args.steps  # forward launches per step
     fwd_launch_s = fwd_ms / max(launches, 1) * 1e-3
-    per_launch_bytes = alg_bytes / (launches / args.steps)
-    achieved = per_launch_bytes / fwd_launch_s
-    pairs_per_launch = N_STATES * N_STATES * (T_LEN - 1) * nloc / (launches / args.steps)
-    per_elem = load_traffic(f64)
-    traffic = per_elem * steps_rank / (launches / args.steps) if per_elem is not None else None
+    # read obs 4 B + emission column 4N, write delta column 4N + psi column N
+    # (u8) + path 4 B = (9N + 8) B per sequence step, + 8 B of score per sequence
+    alg_8d = ((9 * N_STATES + 8) * steps_rank + 8 * nloc) / lps
+    alg_read_8d = (4 * N_STATES + 4) * steps_rank / lps
+    # the f64 path's own bytes: f64 emission column 8N in, f64 delta column 8N out
+    alg_f64 = ((16 * N_STATES + 8) * steps_rank + 8 * nloc) / lps
+    achieved = alg_8d / fwd_launch_s
+    pairs_per_launch = N_STATES * N_STATES * (T_LEN - 1) * nloc / lps
+    pmc = load_pmc(f64)
+    traffic = pmc["per_elem"] * steps_rank / lps if pmc else None
     kname = ("trellis_fwd_f64<C=4,S=8>" if spw == 8 else "trellis_fwd_f64<C=2,S=%d,W=2>" % (2 * spw)) \
         if f64 else "trellis_fwd2_f32<256>"
     pair_peak = F64_PAIR_PEAK if f64 else VALU_PAIR_PEAK
+    valu_frac = pairs_per_launch / fwd_launch_s / pair_peak
+    valu = {"achieved_pairs_per_s": pairs_per_launch / fwd_launch_s, "peak_pairs_per_s": pair_peak,
+            "frac": valu_frac, "peak_basis": f"nominal {NOMINAL_GHZ} GHz"}
+    if pmc and pmc.get("clock_ghz"):
+        valu.update({"clock_ghz_pmc": pmc["clock_ghz"], "frac_at_pmc_clock": valu_frac * NOMINAL_GHZ / pmc["clock_ghz"],
+                     "clock_source": pmc["source"] + ": GRBM_GUI_ACTIVE / 8 XCDs over the kernel duration"})
     out = {
         "metric": "trellis cells/s (N*T*batch), N=256 T=512 batch=65536",
         "value": value,
@@ -281,27 +413,47 @@ def main():
                                  ", gloo gather to rank 0 (rehearsal: ranks may share a GPU)") if world > 1 else ""),
                    "global_batch": B, "seq_len": T_LEN, "states": N_STATES, "parallelism": f"batch-shard x{world}"},
         "seqs_per_s": B * args.steps / el,
-        "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK, "traffic": traffic,
+        "roofline": {"bound": "valu",
+                     "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": achieved / HBM_PEAK,
+                     "traffic": traffic,
+                     "traffic_source": (pmc["source"] + ": rocprofv3 FETCH_SIZE x2 (gfx950) + WRITE_SIZE, scaled "
+                                        "per decoded element") if pmc else None,
+                     "basis": "achieved/frac: HBM roof on SURVEY.md §8(d)'s algorithmic bytes ((9N+8) B per "
+                              "sequence step + 8 B per sequence) / the kernel's HIP-event time per launch; the "
+                              "binding roof is the f64 VALU one (roofs.valu)" if f64 else
+                              "achieved/frac: HBM roof on SURVEY.md §8(d)'s algorithmic bytes; binding roof: VALU",
                      "kernel": kname,
                      "kernel_ms_per_launch": fwd_launch_s * 1e3,
-                     "alg_bytes_per_launch": per_launch_bytes,
-                     "read_only_frac": alg_read / (launches / args.steps) / fwd_launch_s / HBM_PEAK,
-                     "binding": "valu",
-                     "valu": {"achieved_pairs_per_s": pairs_per_launch / fwd_launch_s, "peak_pairs_per_s": pair_peak,
-                              "frac": pairs_per_launch / fwd_launch_s / pair_peak}},
+                     "alg_bytes_per_launch": alg_8d,
+                     "read_only_frac": alg_read_8d / fwd_launch_s / HBM_PEAK,
+                     "frac_f64_bytes": alg_f64 / fwd_launch_s / HBM_PEAK if f64 else None,
+                     "roofs": {"hbm": {"achieved_GBps": achieved / 1e9, "peak_GBps": HBM_PEAK / 1e9,
+                                       "frac": achieved / HBM_PEAK},
+                               "valu": valu}},
         "kernel_ms_per_step": {"forward": fwd_ms / args.steps, "backtrack_rescore": bt_ms / args.steps},
     }
     if f32_extra is not None:
         out["f32_trellis"] = f32_extra
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(pi, a, b, obs, args.cpu_seconds)
+    if verify is not None:
+        out["multi_gpu_check"] = verify
+    if rank == 0 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(pi, a, b, obs, args.cpu_seconds, first)
         out["cpu_baseline"]["gpu_over_cpu"] = value / out["cpu_baseline"]["value"]
+    if rank == 0 and not args.no_configs:
+        out["configs"] = bench_configs(dev, stream)
+    checks = []
+    if verify is not None:
+        checks.append(verify["equal"])
+    if out.get("cpu_baseline", {}).get("check"):
+        checks.append(out["cpu_baseline"]["check"]["bit_exact"])
+    out["verified"] = bool(checks) and all(checks)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+    if rank == 0 and checks and not all(checks):
+        raise SystemExit("bench.py: the decoded result failed its check (see multi_gpu_check / cpu_baseline.check)")
 
 
 if __name__ == "__main__":

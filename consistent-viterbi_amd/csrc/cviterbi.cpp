@@ -94,7 +94,8 @@ cv_status upload(DevBuf& buf, const void* src, size_t bytes) {
 }
 
 constexpr uint64_t kDefaultWorkspace = 8ull << 30;
-constexpr uint64_t kDefaultWorkspaceT64 = 64ull << 30;  // config 5 resume decode in one chunk: 3% faster than 40 GiB
+constexpr uint64_t kDefaultWorkspaceT64 = 64ull << 30;
+constexpr size_t kMaxTimedEvents = 1 << 16;  // cv_timing_begin: at most 16,384 chunk launches timed  // config 5 resume decode in one chunk: 3% faster than 40 GiB
 
 }  // namespace
 
@@ -145,6 +146,10 @@ struct cv_hmm {
   // timing events of the last call
   std::vector<hipEvent_t> ev;  // 4 per chunk: fwd start/end (main stream), bt start/end
   int64_t last_launches = 0;
+  size_t last_ev_base = 0;  // first event of the last call in ev
+  // cv_timing_begin/end: every decode call's events kept (appended) until cv_timing_end
+  bool acc_on = false, acc_overflow = false;
+  size_t acc_used = 0;
   int32_t last_kernel = 0;
   int32_t last_np = 0;
   int32_t last_mt = -1;
@@ -675,16 +680,22 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
 
   hipStream_t bts = serial ? stream : h->bt_stream;
   const size_t nev = 4 * chunks.size();
+  // events of this call: from 0 (each call overwrites the last), or appended after the calls
+  // already timed since cv_timing_begin
+  if (h->acc_on && h->acc_used + nev > kMaxTimedEvents) h->acc_on = false, h->acc_overflow = true;
+  const size_t eb = h->acc_on ? h->acc_used : 0;
+  h->last_ev_base = eb;
   for (size_t i = 0; i < nev; ++i)
-    if (!get_event(h, i)) return set_err(CV_EDEVICE, "hipEventCreate failed");
+    if (!get_event(h, eb + i)) return set_err(CV_EDEVICE, "hipEventCreate failed");
   for (size_t ci = 0; ci < chunks.size(); ++ci) {
     const auto& c = chunks[ci];
     const int64_t n = c.second - c.first;
     const int buf = nbuf == 2 ? (int)(ci % 2) : 0;
     unsigned char* wsb = h->ws_main.as<unsigned char>() + buf * buf_bytes;
     unsigned char* lrb = h->ws_last.as<unsigned char>() + buf * last_bytes;
-    hipEvent_t f0 = h->ev[4 * ci], f1 = h->ev[4 * ci + 1], b0 = h->ev[4 * ci + 2], b1 = h->ev[4 * ci + 3];
-    if (!serial && ci >= 2) HIP_TRY(hipStreamWaitEvent(stream, h->ev[4 * (ci - 2) + 3], 0));  // buffer reuse
+    hipEvent_t f0 = h->ev[eb + 4 * ci], f1 = h->ev[eb + 4 * ci + 1], b0 = h->ev[eb + 4 * ci + 2],
+               b1 = h->ev[eb + 4 * ci + 3];
+    if (!serial && ci >= 2) HIP_TRY(hipStreamWaitEvent(stream, h->ev[eb + 4 * (ci - 2) + 3], 0));  // buffer reuse
     HIP_TRY(hipEventRecord(f0, stream));
     hipError_t err;
     if (use_trellis) {
@@ -879,7 +890,8 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
     ++h->last_launches;
   }
   // the caller's stream sees the whole decode complete
-  if (!serial) HIP_TRY(hipStreamWaitEvent(stream, h->ev[4 * (chunks.size() - 1) + 3], 0));
+  if (!serial) HIP_TRY(hipStreamWaitEvent(stream, h->ev[eb + 4 * (chunks.size() - 1) + 3], 0));
+  if (h->acc_on) h->acc_used += nev;
   return CV_OK;
 }
 
@@ -2119,6 +2131,27 @@ CV_API cv_status cv_decode_constrained_exchange(cv_hmm* h, int64_t nseq, const i
                            score_out, status_out, objective_out);
 }
 
+namespace {
+// Sums the forward / backtrack event pairs of `launches` chunks from event `eb` on.
+cv_status sum_timing(cv_hmm* h, size_t eb, int64_t launches, cv_timing* out) {
+  if (launches == 0) return CV_OK;
+  HIP_TRY(hipSetDevice(h->device));
+  const int64_t L = launches;
+  HIP_TRY(hipEventSynchronize(h->ev[eb + 4 * (L - 1) + 3]));
+  for (int64_t c = 0; c < L; ++c) {
+    float f = 0, b = 0;
+    HIP_TRY(hipEventElapsedTime(&f, h->ev[eb + 4 * c], h->ev[eb + 4 * c + 1]));
+    HIP_TRY(hipEventElapsedTime(&b, h->ev[eb + 4 * c + 2], h->ev[eb + 4 * c + 3]));
+    out->fwd_ms += f;
+    out->bt_ms += b;
+  }
+  float tot = 0;
+  HIP_TRY(hipEventElapsedTime(&tot, h->ev[eb], h->ev[eb + 4 * (L - 1) + 3]));
+  out->total_ms = tot;
+  return CV_OK;
+}
+}  // namespace
+
 CV_API cv_status cv_last_timing(cv_hmm* h, cv_timing* out) {
   if (!h || !out) return set_err(CV_EINVAL, "null argument");
   std::lock_guard<std::mutex> lk(h->mu);
@@ -2127,21 +2160,34 @@ CV_API cv_status cv_last_timing(cv_hmm* h, cv_timing* out) {
   out->kernel = h->last_kernel;
   out->padded_states = h->last_np;
   out->mfma_tiles = h->last_mt;
-  if (h->last_launches == 0) return CV_OK;
-  HIP_TRY(hipSetDevice(h->device));
-  const int64_t L = h->last_launches;
-  HIP_TRY(hipEventSynchronize(h->ev[4 * (L - 1) + 3]));
-  for (int64_t c = 0; c < L; ++c) {
-    float f = 0, b = 0;
-    HIP_TRY(hipEventElapsedTime(&f, h->ev[4 * c], h->ev[4 * c + 1]));
-    HIP_TRY(hipEventElapsedTime(&b, h->ev[4 * c + 2], h->ev[4 * c + 3]));
-    out->fwd_ms += f;
-    out->bt_ms += b;
-  }
-  float tot = 0;
-  HIP_TRY(hipEventElapsedTime(&tot, h->ev[0], h->ev[4 * (L - 1) + 3]));
-  out->total_ms = tot;
+  return sum_timing(h, h->last_ev_base, h->last_launches, out);
+}
+
+CV_API cv_status cv_timing_begin(cv_hmm* h) {
+  if (!h) return set_err(CV_EINVAL, "null argument");
+  std::lock_guard<std::mutex> lk(h->mu);
+  h->acc_on = true;
+  h->acc_overflow = false;
+  h->acc_used = 0;
   return CV_OK;
+}
+
+CV_API cv_status cv_timing_end(cv_hmm* h, cv_timing* out) {
+  if (!h || !out) return set_err(CV_EINVAL, "null argument");
+  std::lock_guard<std::mutex> lk(h->mu);
+  std::memset(out, 0, sizeof *out);
+  const bool was_on = h->acc_on, overflow = h->acc_overflow;
+  const size_t used = h->acc_used;
+  h->acc_on = false;
+  h->acc_overflow = false;
+  h->acc_used = 0;
+  if (!was_on && !overflow) return set_err(CV_EINVAL, "cv_timing_end without cv_timing_begin");
+  if (overflow) return set_err(CV_ELIMIT, "more than %zu chunk launches timed since cv_timing_begin", kMaxTimedEvents / 4);
+  out->launches = (int64_t)(used / 4);
+  out->kernel = h->last_kernel;
+  out->padded_states = h->last_np;
+  out->mfma_tiles = h->last_mt;
+  return sum_timing(h, 0, out->launches, out);
 }
 
 CV_API cv_status cv_viterbi_decode(cv_hmm* h, int64_t T, const int32_t* obs, int32_t* path_out) {

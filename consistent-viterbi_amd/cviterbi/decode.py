@@ -253,12 +253,29 @@ def decode_superseq_cp(hmm: HMM, offsets, obs):
     return path[:int(offsets[-1] - offsets[0])], obj.value
 
 
-def last_timing(hmm: HMM) -> dict:
-    t = L.Timing()
-    L.check(L.lib().cv_last_timing(hmm.handle, ctypes.byref(t)))
+def _timing_dict(t):
     return dict(fwd_ms=t.fwd_ms, bt_ms=t.bt_ms, total_ms=t.total_ms, launches=t.launches,
                 kernel={1: "trellis", 2: "generic", 3: "trellis_f64"}.get(t.kernel, "none"), padded_states=t.padded_states,
                 seqs_per_wave=t.mfma_tiles)
+
+
+def last_timing(hmm: HMM) -> dict:
+    """Device timings of the last decode call (synchronizes its events)."""
+    t = L.Timing()
+    L.check(L.lib().cv_last_timing(hmm.handle, ctypes.byref(t)))
+    return _timing_dict(t)
+
+
+def timing_begin(hmm: HMM):
+    """Start summing the device timings of every decode call on `hmm` (cv_timing_begin)."""
+    L.check(L.lib().cv_timing_begin(hmm.handle))
+
+
+def timing_end(hmm: HMM) -> dict:
+    """Sums since timing_begin (cv_timing_end; synchronizes the events)."""
+    t = L.Timing()
+    L.check(L.lib().cv_timing_end(hmm.handle, ctypes.byref(t)))
+    return _timing_dict(t)
 
 
 def decode(sequence, hmm: HMM):

@@ -132,15 +132,16 @@ def constrained_decode_sharded(hmm, offsets, obs, component, ncomp, dist, device
     dist.all_gather(allc, counts)
     ecap = max(int(c[1]) for c in allc)
     dev = device or "cpu"
-    g = gather_to_root([torch.from_numpy(path).to(dev), torch.from_numpy(score).to(dev),
-                        torch.from_numpy(status.astype(np.int32)).to(dev)], [ecap, per, per], dist)
+    # ONE packed collective (u8 states when N <= 256, raw f64 scores, u8 statuses), as bench.py
+    g = gather_packed_to_root(torch.from_numpy(path).to(dev), torch.from_numpy(score).to(dev),
+                              torch.from_numpy(status.astype(np.uint8)).to(dev), hmm.nstates(), ecap, per, dist)
     if rank != 0:
         return None, None, None, states, None
     ns = [int(c[0]) for c in allc]
     ne = [int(c[1]) for c in allc]
-    path = assemble(g[0], ne).cpu().numpy()
-    score = assemble(g[1], ns).cpu().numpy()
-    status = assemble(g[2], ns).cpu().numpy().astype(np.uint8)
+    path = assemble([x[0] for x in g], ne).cpu().numpy()
+    score = assemble([x[1] for x in g], ns).cpu().numpy()
+    status = assemble([x[2] for x in g], ns).cpu().numpy().astype(np.uint8)
     # sequential sum in sequence order, as cv_decode_constrained does (CV_SEQ_INFEASIBLE = 1)
     objective = float(np.cumsum(np.where(status == 1, -np.inf, score))[-1]) if B else 0.0
     return path, score, status, states, objective

@@ -177,6 +177,12 @@ CV_API cv_status cv_decode_batch_device(cv_hmm* h, int64_t nseq, const int64_t* 
                                         uint8_t* status_dev);
 /* Device timings of the last decode call on this handle (synchronizes its events). */
 CV_API cv_status cv_last_timing(cv_hmm* h, cv_timing* out);
+/* Device timings summed over EVERY decode call on this handle from cv_timing_begin to
+ * cv_timing_end (no synchronisation in between, so a timed loop can enqueue ahead; the end
+ * call synchronizes the events).  launches = chunk launches in all; total_ms = first kernel
+ * start to last kernel end.  CV_ELIMIT beyond 16,384 chunk launches. */
+CV_API cv_status cv_timing_begin(cv_hmm* h);
+CV_API cv_status cv_timing_end(cv_hmm* h, cv_timing* out);
 /* Consistency-constrained decode (the intended semantics of the reference's constrained
  * solvers, opti.rs:101-111 / dp.rs:157-164 / cp.rs:95-126): every element with
  * component[e] >= 0 takes the common state of its component, and the total log-likelihood

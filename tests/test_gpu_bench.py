@@ -20,7 +20,7 @@ def test_bench_two_rank_rehearsal(gpu):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", "29561", os.path.join(ROOT, "bench.py"),
            "--gpus", "2", "--steps", "2", "--warmup", "1", "--batch", "2048", "--backend", "gloo",
-           "--no-f32-extra"]
+           "--no-f32-extra", "--no-configs", "--cpu-seconds", "1"]
     # own session: on a timeout the launcher AND its ranks are killed (process group)
     p = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env, cwd=ROOT,
                          start_new_session=True)
@@ -37,3 +37,11 @@ def test_bench_two_rank_rehearsal(gpu):
     assert d["n_gpus"] == 2 and d["scaling"] == "strong" and d["dtype"] == "f64"
     assert d["config"]["global_batch"] == 2048 and "sharded over 2 ranks" in d["config"]["workload"]
     assert d["value"] > 0 and d["roofline"]["kernel"].startswith("trellis_fwd_f64")
+    # self-verification: rank 0 re-decoded the global batch and the gathered last step equals it
+    # bit for bit (main.rs:129-133's per-element output), and the CPU-baseline leg's oracle check
+    assert d["multi_gpu_check"]["equal"] is True and d["multi_gpu_check"]["sequences"] == 2048
+    assert d["cpu_baseline"]["check"]["bit_exact"] is True and d["cpu_baseline"]["check"]["sequences"] == 64
+    assert d["verified"] is True
+    r = d["roofline"]
+    assert r["bound"] == "valu" and 0 < r["frac"] < 1 and r["frac_f64_bytes"] > r["frac"]
+    assert r["roofs"]["valu"]["frac"] > 0

@@ -274,3 +274,64 @@ def test_t64_config4_full_batch_vs_generic(gpu):
         lo, hi = off[k], off[k + 1]
         rp, rs, rst = O.decode_batch(pi, a, b, np.array([0, T]), obs[lo:hi], O.VITERBI, np.float64)
         assert rst[0] == st64[k] and rs[0] == s64[k] and np.array_equal(rp, p64[lo:hi]), f"seq {k}"
+
+
+def test_t64_concurrent_handles_two_streams(gpu):
+    """Two handles decode different N = 256 batches on two streams at once (their forward
+    kernels co-run and share the process-global SIMD-balancing table, trellis64.hip
+    g_t64_simd): each result is bit-identical to the same decode run alone."""
+    import torch
+
+    dev = torch.device("cuda:0")
+    runs = []
+    for seed, nseq, T in ((81, 8192, 48), (82, 6144, 64)):
+        pi, a, b = synth.random_hmm(256, 64, seed=seed)
+        off = np.arange(nseq + 1, dtype=np.int64) * T
+        obs = np.random.default_rng(seed).integers(0, 64, size=nseq * T).astype(np.int32)
+        h = cv.HMM(pi, a, b)
+        bufs = (torch.from_numpy(off).to(dev), torch.from_numpy(obs).to(dev),
+                torch.empty(nseq * T, dtype=torch.int32, device=dev), torch.empty(nseq, dtype=torch.float64, device=dev),
+                torch.empty(nseq, dtype=torch.uint8, device=dev))
+        runs.append((h, off, bufs, torch.cuda.Stream(dev)))
+
+    def launch(r):
+        h, off, (o_d, ob_d, p_d, s_d, st_d), s = r
+        cv.decode_batch_device(h, o_d, ob_d, p_d, s_d, st_d, offsets_host=off, stream=s.cuda_stream, dtype="f64",
+                               rescore_f64=False)
+
+    def result(r):
+        return tuple(x.cpu().numpy().copy() for x in r[2][2:])
+
+    solo = []
+    for r in runs:
+        launch(r)
+        torch.cuda.synchronize()
+        assert cv.last_timing(r[0])["kernel"] == "trellis_f64"
+        solo.append(result(r))
+    for _ in range(3):
+        for r in runs:
+            r[2][2].fill_(-1)
+        for r in runs:  # both enqueued before either finishes
+            launch(r)
+        torch.cuda.synchronize()
+        for r, ref in zip(runs, solo):
+            _assert_same(result(r), ref, "concurrent decode")
+
+
+def test_timing_sums_every_call(gpu):
+    """cv_timing_begin / cv_timing_end: the device times of every decode call in between,
+    with no synchronisation per call (what bench.py's timed loop reads)."""
+    pi, a, b, off, obs = _case(64, 30, seed=5, nseq=200, tmax=60)
+    h = cv.HMM(pi, a, b)
+    cv.decode_batch(h, off, obs, rescore_f64=False)
+    one = cv.last_timing(h)
+    cv.timing_begin(h)
+    for _ in range(3):
+        cv.decode_batch(h, off, obs, rescore_f64=False)
+    t = cv.timing_end(h)
+    assert t["launches"] == 3 * one["launches"] and t["fwd_ms"] > 0 and t["bt_ms"] > 0
+    assert t["total_ms"] >= t["fwd_ms"] / 3
+    # last_timing still describes the last call alone
+    assert cv.last_timing(h)["launches"] == one["launches"]
+    with pytest.raises(cv.CVError):
+        cv.timing_end(h)  # no timing_begin pending

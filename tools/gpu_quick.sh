@@ -8,8 +8,9 @@ OUT=$R/gpurun_out
 mkdir -p $OUT
 cd $R
 TAG=${TAG:-quick}
-if [ -n "${PYSEL:-}" ]; then
-  timeout -k 10 ${T_TEST:-600} python -u -m pytest tests -x -v --timeout 300 --timeout-method thread -m gpu $PYSEL \
+if [ -n "${PYSEL:-}${PYK:-}" ]; then
+  timeout -k 10 ${T_TEST:-600} python -u -m pytest tests -x -v --timeout 300 --timeout-method thread -m gpu ${PYSEL:-} \
+    ${PYK:+-k "$PYK"} \
     > $OUT/${TAG}_pytest.log 2>&1; rc=$?
   echo "pytest rc=$rc"; tail -4 $OUT/${TAG}_pytest.log
   [ $rc -eq 0 ] || exit $rc
