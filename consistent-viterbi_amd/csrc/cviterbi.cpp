@@ -132,6 +132,17 @@ struct cv_hmm {
   DevBuf d_pi32, d_a32, d_et32;
   // workspace
   DevBuf ws_main, ws_last, ws_order;
+  // a second decode workspace + stream: the constrained decode's unconstrained sequences run
+  // on it beside the terms pass (constrained decode)
+  struct SideWs {
+    DevBuf main, last, order, idx, obs2, path2, res2;
+    std::vector<int32_t> order_host;
+    std::vector<int64_t> idx_host;
+    std::vector<hipEvent_t> ev;
+    hipStream_t stream = nullptr;  // lowest priority: fills what the constrained work leaves idle
+    hipStream_t hi = nullptr;      // highest priority: the constrained work itself
+    hipEvent_t start = nullptr, done = nullptr;
+  } side;
   DevBuf st_off, st_obs, st_path, st_score, st_status, st_forced;
   DevBuf cs_ranges, cs_delta, cs_g, cs_mu, cs_start, cs_zero;  // constrained-decode scratch
   DevBuf cs_comp, cs_words;  // device exact unary sums: per-sequence components, output words
@@ -157,6 +168,11 @@ struct cv_hmm {
 
   ~cv_hmm() {
     for (auto e : ev) (void)hipEventDestroy(e);
+    for (auto e : side.ev) (void)hipEventDestroy(e);
+    if (side.start) (void)hipEventDestroy(side.start);
+    if (side.done) (void)hipEventDestroy(side.done);
+    if (side.stream) (void)hipStreamDestroy(side.stream);
+    if (side.hi) (void)hipStreamDestroy(side.hi);
     if (rs_ev) (void)hipEventDestroy(rs_ev);
     if (stream) (void)hipStreamDestroy(stream);
     if (bt_stream) (void)hipStreamDestroy(bt_stream);
@@ -457,13 +473,13 @@ cv_status check_batch(const cv_hmm* h, int64_t nseq, const int64_t* offsets) {
   return CV_OK;
 }
 
-hipEvent_t get_event(cv_hmm* h, size_t i) {
-  while (h->ev.size() <= i) {
+hipEvent_t get_event(std::vector<hipEvent_t>& ev, size_t i) {
+  while (ev.size() <= i) {
     hipEvent_t e;
     if (hipEventCreate(&e) != hipSuccess) return nullptr;
-    h->ev.push_back(e);
+    ev.push_back(e);
   }
-  return h->ev[i];
+  return ev[i];
 }
 
 cvk::BacktrackArgs make_bt_args(cv_hmm* h, unsigned char* wsb, const int64_t* offsets_host,
@@ -490,7 +506,16 @@ cvk::BacktrackArgs make_bt_args(cv_hmm* h, unsigned char* wsb, const int64_t* of
 // Core device-side decode.  All pointers are device pointers except offsets_host.
 cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, const int64_t* offsets_dev,
                         const int32_t* obs_dev, const cv_opts& o, int32_t* path_dev, double* score_dev,
-                        uint8_t* status_dev, hipStream_t stream, const void* resume_rows = nullptr) {
+                        uint8_t* status_dev, hipStream_t stream, const void* resume_rows = nullptr,
+                        bool side_ws = false) {
+  // side_ws: the handle's second workspace (h->side), no timing / last-call bookkeeping -- a
+  // decode running beside another decode_device call of the same handle on another stream
+  DevBuf& w_main = side_ws ? h->side.main : h->ws_main;
+  DevBuf& w_last = side_ws ? h->side.last : h->ws_last;
+  DevBuf& w_order = side_ws ? h->side.order : h->ws_order;
+  std::vector<int32_t>& order_host = side_ws ? h->side.order_host : h->order_host;
+  std::vector<hipEvent_t>& evv = side_ws ? h->side.ev : h->ev;
+  int64_t launches_done = 0;
   if (o.dtype != CV_DTYPE_F32 && o.dtype != CV_DTYPE_F64) return set_err(CV_EINVAL, "bad dtype %d", o.dtype);
   if (o.assoc < CV_ASSOC_VITERBI || o.assoc > CV_ASSOC_DECODE) return set_err(CV_EINVAL, "bad assoc %d", o.assoc);
   const bool trellis_ok = o.dtype == CV_DTYPE_F32 && o.assoc == CV_ASSOC_VITERBI &&
@@ -544,14 +569,16 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
   // MFMA-assisted f32 trellis (slower than the all-VALU one on gfx950: DESIGN.md §3)
   if ((o.flags & 0x1u) || ((o.flags >> 8) & 0xFF))
     return set_err(CV_EUNSUPPORTED, "the MFMA-assisted trellis was retired (flags 0x%x)", o.flags);
-  h->last_launches = 0;
-  h->last_kernel = use_trellis ? CV_KERNEL_TRELLIS : use_t64 ? CV_KERNEL_TRELLIS_F64 : CV_KERNEL_GENERIC;
+  const bool wave = use_trellis && h->npw > 0 && !(o.flags & CV_FLAG_NO_WAVE);
+  if (!side_ws) {
+    h->last_launches = 0;
+    h->last_kernel = use_trellis ? CV_KERNEL_TRELLIS : use_t64 ? CV_KERNEL_TRELLIS_F64 : CV_KERNEL_GENERIC;
+    h->last_np = use_trellis ? (wave ? h->npw : h->np) : use_t64 ? h->np64 : 0;
+    h->last_mt = -1;
+  }
   // N <= 64: one wave per sequence, forward and backtrack fused (trellis_wave_f32) on tables
   // padded to npw = 16 * ceil(N / 16); its chunks run back to back on one stream (nothing to
   // overlap)
-  const bool wave = use_trellis && h->npw > 0 && !(o.flags & CV_FLAG_NO_WAVE);
-  h->last_np = use_trellis ? (wave ? h->npw : h->np) : use_t64 ? h->np64 : 0;
-  h->last_mt = -1;
   if (nseq == 0) return CV_OK;
   HIP_TRY(hipMemsetAsync(status_dev, 0, (size_t)nseq, stream));
 
@@ -576,7 +603,7 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
     const char* e = getenv("CV_T64_OVERLAP");
     return e != nullptr && e[0] == '1';
   }();
-  const bool serial = (o.flags & CV_FLAG_SERIAL) != 0 || wave || (use_t64 && !t64_overlap);
+  const bool serial = (o.flags & CV_FLAG_SERIAL) != 0 || wave || (use_t64 && !t64_overlap) || side_ws;
   // Sequences per forward workgroup: 2 (trellis_fwd2_f32, equal-length pairs; default) or 1
   // (trellis_fwd_f32: leftovers, N not a multiple of 64).
   const bool plain = use_trellis && !wave && cvk::trellis_pair_supported(h->np);
@@ -640,8 +667,8 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
   for (int64_t s = 1; s < nseq && !varlen; ++s) varlen = (offsets_host[s + 1] - offsets_host[s]) != T0;
   const size_t buf_bytes = ((std::max<uint64_t>(max_elems, 1) * per_elem + 255) / 256) * 256;
   const size_t last_bytes = ((size_t)max_seqs * h->N * real_bytes + 255) / 256 * 256;
-  if ((st = h->ws_main.ensure(buf_bytes * nbuf)) != CV_OK) return st;
-  if (!use_trellis && (st = h->ws_last.ensure(last_bytes * nbuf)) != CV_OK) return st;
+  if ((st = w_main.ensure(buf_bytes * nbuf)) != CV_OK) return st;
+  if (!use_trellis && (st = w_last.ensure(last_bytes * nbuf)) != CV_OK) return st;
   const int32_t* order_dev = nullptr;
   // group == 2: chunk slots [first, first + 2*npair) hold equal-length pairs, the rest run
   // one per workgroup.
@@ -650,11 +677,11 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
   if (varlen) {
     // longest-first schedule inside each chunk so the tail of the grid is short sequences;
     // with pairing, equal-length neighbours are paired first and leftovers go last
-    h->order_host.resize((size_t)nseq);
+    order_host.resize((size_t)nseq);
     std::vector<int32_t> tail;
     for (size_t ci = 0; ci < chunks.size(); ++ci) {
       const auto& c = chunks[ci];
-      auto b = h->order_host.begin() + c.first, e = h->order_host.begin() + c.second;
+      auto b = order_host.begin() + c.first, e = order_host.begin() + c.second;
       std::iota(b, e, (int32_t)c.first);
       auto len = [&](int32_t x) { return offsets_host[x + 1] - offsets_host[x]; };
       std::stable_sort(b, e, [&](int32_t x, int32_t y) { return len(x) > len(y); });
@@ -672,30 +699,29 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
       npair[ci] = (out - b) / 2;
       std::copy(tail.begin(), tail.end(), out);
     }
-    if ((st = h->ws_order.ensure((size_t)nseq * 4)) != CV_OK) return st;
-    HIP_TRY(hipMemcpyAsync(h->ws_order.p, h->order_host.data(), (size_t)nseq * 4, hipMemcpyHostToDevice, stream));
+    if ((st = w_order.ensure((size_t)nseq * 4)) != CV_OK) return st;
+    HIP_TRY(hipMemcpyAsync(w_order.p, order_host.data(), (size_t)nseq * 4, hipMemcpyHostToDevice, stream));
     HIP_TRY(hipStreamSynchronize(stream));  // order_host may be rewritten by the next call
-    order_dev = h->ws_order.as<int32_t>();
+    order_dev = w_order.as<int32_t>();
   }
 
   hipStream_t bts = serial ? stream : h->bt_stream;
   const size_t nev = 4 * chunks.size();
   // events of this call: from 0 (each call overwrites the last), or appended after the calls
   // already timed since cv_timing_begin
-  if (h->acc_on && h->acc_used + nev > kMaxTimedEvents) h->acc_on = false, h->acc_overflow = true;
-  const size_t eb = h->acc_on ? h->acc_used : 0;
-  h->last_ev_base = eb;
+  if (!side_ws && h->acc_on && h->acc_used + nev > kMaxTimedEvents) h->acc_on = false, h->acc_overflow = true;
+  const size_t eb = (!side_ws && h->acc_on) ? h->acc_used : 0;
+  if (!side_ws) h->last_ev_base = eb;
   for (size_t i = 0; i < nev; ++i)
-    if (!get_event(h, eb + i)) return set_err(CV_EDEVICE, "hipEventCreate failed");
+    if (!get_event(evv, eb + i)) return set_err(CV_EDEVICE, "hipEventCreate failed");
   for (size_t ci = 0; ci < chunks.size(); ++ci) {
     const auto& c = chunks[ci];
     const int64_t n = c.second - c.first;
     const int buf = nbuf == 2 ? (int)(ci % 2) : 0;
-    unsigned char* wsb = h->ws_main.as<unsigned char>() + buf * buf_bytes;
-    unsigned char* lrb = h->ws_last.as<unsigned char>() + buf * last_bytes;
-    hipEvent_t f0 = h->ev[eb + 4 * ci], f1 = h->ev[eb + 4 * ci + 1], b0 = h->ev[eb + 4 * ci + 2],
-               b1 = h->ev[eb + 4 * ci + 3];
-    if (!serial && ci >= 2) HIP_TRY(hipStreamWaitEvent(stream, h->ev[eb + 4 * (ci - 2) + 3], 0));  // buffer reuse
+    unsigned char* wsb = w_main.as<unsigned char>() + buf * buf_bytes;
+    unsigned char* lrb = w_last.as<unsigned char>() + buf * last_bytes;
+    hipEvent_t f0 = evv[eb + 4 * ci], f1 = evv[eb + 4 * ci + 1], b0 = evv[eb + 4 * ci + 2], b1 = evv[eb + 4 * ci + 3];
+    if (!serial && ci >= 2) HIP_TRY(hipStreamWaitEvent(stream, evv[eb + 4 * (ci - 2) + 3], 0));  // buffer reuse
     HIP_TRY(hipEventRecord(f0, stream));
     hipError_t err;
     if (use_trellis) {
@@ -748,7 +774,7 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
       fa.forced = o.forced;
       fa.resume_rows = static_cast<const double*>(resume_rows);
       const int spw = cvk::t64_seqs_per_wave(n, h->cus);
-      h->last_mt = (t64cp || fa.dp_assoc) ? std::min(spw, 4) : spw;
+      if (!side_ws) h->last_mt = (t64cp || fa.dp_assoc) ? std::min(spw, 4) : spw;
       if (t64cp) {
         fa.nstates = h->N;
         fa.psi = reinterpret_cast<uint16_t*>(wsb);
@@ -887,11 +913,12 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
     }
     if (err != hipSuccess) return set_err(CV_EDEVICE, "backtrack launch failed: %s", hipGetErrorString(err));
     HIP_TRY(hipEventRecord(b1, bts));
-    ++h->last_launches;
+    ++launches_done;
+    if (!side_ws) h->last_launches = launches_done;
   }
   // the caller's stream sees the whole decode complete
-  if (!serial) HIP_TRY(hipStreamWaitEvent(stream, h->ev[eb + 4 * (chunks.size() - 1) + 3], 0));
-  if (h->acc_on) h->acc_used += nev;
+  if (!serial) HIP_TRY(hipStreamWaitEvent(stream, evv[eb + 4 * (chunks.size() - 1) + 3], 0));
+  if (!side_ws && h->acc_on) h->acc_used += nev;
   return CV_OK;
 }
 
@@ -1688,10 +1715,108 @@ cv_status forced_decode_locked(cv_hmm* h, int64_t nseq, const int64_t* offsets, 
 // stream beside that decode; then suffix paths, scores and statuses go back to the original
 // layout and every path is re-scored in f64 over its whole sequence.  Bit-identical to
 // forced_decode_locked's full forced decode.  Device pointers; synchronous.
+// The constrained decode's UNCONSTRAINED sequences (no constrained element) do not depend on
+// the component states: they are decoded on the handle's side stream and workspace (h->side),
+// launched before the terms pass, so their waves fill the terms pass's tails and the host
+// phases (checks, search) that leave the GPU idle; the results are scattered into the caller's
+// outputs.  f64 only (the f32 resume flow re-scores every sequence at its end).  *launched:
+// h->side.done is recorded on the side stream; the caller waits for it (and synchronizes the
+// side stream on any error) before the outputs are read.
+cv_status side_decode_launch(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, const int32_t* obs_dev,
+                             const std::vector<ConSeq>& cs, const cv_opts& o, int32_t* path_dev, double* score_dev,
+                             uint8_t* status_dev, hipStream_t stream, bool* launched) {
+  *launched = false;
+  auto& sd = h->side;
+  std::vector<uint8_t> con((size_t)nseq, 0);
+  for (const auto& c : cs) con[(size_t)c.seq] = 1;
+  int64_t nu = 0;
+  for (int64_t q = 0; q < nseq; ++q) nu += con[(size_t)q] ? 0 : 1;
+  if (nu == 0) return CV_OK;
+  // [cstart | seq | off2 (nu + 1)] int64, in sequence order (decode_device orders by length)
+  sd.idx_host.assign((size_t)3 * nu + 1, 0);
+  int64_t* cstart = sd.idx_host.data();
+  int64_t* cseq = cstart + nu;
+  int64_t* off2 = cseq + nu;
+  for (int64_t q = 0, k = 0; q < nseq; ++q) {
+    if (con[(size_t)q]) continue;
+    cstart[k] = offsets_host[q];
+    cseq[k] = q;
+    off2[k + 1] = off2[k] + offsets_host[q + 1] - offsets_host[q];
+    ++k;
+  }
+  const int64_t total2 = off2[nu];
+  cv_status st;
+  if (!sd.done && hipEventCreateWithFlags(&sd.done, hipEventDisableTiming) != hipSuccess)
+    return set_err(CV_EDEVICE, "hipEventCreate failed");
+  if ((st = sd.idx.ensure(sd.idx_host.size() * 8)) != CV_OK) return st;
+  if ((st = sd.obs2.ensure((size_t)std::max<int64_t>(total2, 1) * 4)) != CV_OK) return st;
+  if ((st = sd.path2.ensure((size_t)std::max<int64_t>(total2, 1) * 4)) != CV_OK) return st;
+  if ((st = sd.res2.ensure((size_t)nu * 9)) != CV_OK) return st;
+  // the side stream starts behind everything the caller queued on its stream (inputs, outputs)
+  HIP_TRY(hipEventRecord(sd.start, stream));
+  HIP_TRY(hipStreamWaitEvent(sd.stream, sd.start, 0));
+  HIP_TRY(hipMemcpyAsync(sd.idx.p, sd.idx_host.data(), sd.idx_host.size() * 8, hipMemcpyHostToDevice, sd.stream));
+  const int64_t* cstart_d = sd.idx.as<int64_t>();
+  const int64_t* cseq_d = cstart_d + nu;
+  const int64_t* off2_d = cseq_d + nu;
+  double* score2 = sd.res2.as<double>();
+  uint8_t* status2 = reinterpret_cast<uint8_t*>(score2 + nu);
+  hipError_t err = cvk::launch_compact_suffix(cstart_d, off2_d, obs_dev, nullptr, nullptr, sd.obs2.as<int32_t>(),
+                                              nullptr, nu, sd.stream);
+  if (err != hipSuccess) return set_err(CV_EDEVICE, "side batch staging failed: %s", hipGetErrorString(err));
+  *launched = true;  // from here on the side stream holds work
+  cv_opts o2 = o;
+  o2.forced = nullptr;
+  o2.rescore_f64 = 0;  // f64: the decode's score is the reference's
+  if ((st = decode_device(h, nu, off2, off2_d, sd.obs2.as<int32_t>(), o2, sd.path2.as<int32_t>(), score2, status2,
+                          sd.stream, nullptr, /*side_ws=*/true)) != CV_OK)
+    return st;
+  err = cvk::launch_scatter_suffix(cstart_d, off2_d, cseq_d, sd.path2.as<int32_t>(), score2, status2, path_dev,
+                                   score_dev, status_dev, nu, sd.stream);
+  if (err != hipSuccess) return set_err(CV_EDEVICE, "side scatter failed: %s", hipGetErrorString(err));
+  HIP_TRY(hipEventRecord(sd.done, sd.stream));
+  trace_mark("side decode of the unconstrained sequences enqueued");
+  return CV_OK;
+}
+
+// Synchronizes the side stream at scope exit when a side decode was launched and not joined,
+// and the high-priority stream when the constrained work ran on it.
+struct SideJoin {
+  cv_hmm* h;
+  bool active = false, hi = false;
+  ~SideJoin() {
+    if (active) (void)hipStreamSynchronize(h->side.stream);
+    if (hi) (void)hipStreamSynchronize(h->side.hi);
+  }
+};
+
+// The side-decode streams (lowest / highest priority; equal priorities if CV_SIDE_PRIO=0).
+cv_status side_streams(cv_hmm* h) {
+  auto& sd = h->side;
+  if (!sd.stream) {
+    int least = 0, greatest = 0;
+    if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) {
+      (void)hipGetLastError();
+      least = greatest = 0;
+    }
+    const char* e = getenv("CV_SIDE_PRIO");
+    if (e && *e == '0') greatest = least;
+    if (hipStreamCreateWithPriority(&sd.stream, hipStreamNonBlocking, least) != hipSuccess ||
+        hipStreamCreateWithPriority(&sd.hi, hipStreamNonBlocking, greatest) != hipSuccess)
+      return set_err(CV_EDEVICE, "hipStreamCreateWithPriority failed");
+  }
+  if (!sd.start && hipEventCreateWithFlags(&sd.start, hipEventDisableTiming) != hipSuccess)
+    return set_err(CV_EDEVICE, "hipEventCreate failed");
+  return CV_OK;
+}
+
 cv_status forced_decode_resume(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, const int64_t* offsets_dev,
                                const int32_t* obs_dev, const int32_t* component, const int32_t* comp_state,
                                const std::vector<ConSeq>& cs, const PrefixKeep& keep, cv_opts o, int32_t* path_dev,
-                               double* score_dev, uint8_t* status_dev, hipStream_t stream) {
+                               double* score_dev, uint8_t* status_dev, hipStream_t stream,
+                               bool constrained_only = false) {
+  // constrained_only: the unconstrained sequences were decoded beside the terms pass
+  // (side_decode_launch); the compact batch holds the constrained sequences alone
   cv_status st;
   if ((st = stage_forced_locked(h, offsets_host, nseq, component, comp_state, cs, stream)) != CV_OK) return st;
   const int64_t nc = (int64_t)keep.seq.size();
@@ -1706,36 +1831,44 @@ cv_status forced_decode_resume(cv_hmm* h, int64_t nseq, const int64_t* offsets_h
     const int32_t c = comp_state[component[keep.t1[i]]];
     state[(size_t)i] = c >= 0 ? c : 0;  // no state: forced to 0 and marked infeasible (mark_unassigned)
   }
-  // compact order: longest first, stable (counting sort)
+  // compact order: longest first, stable (counting sort) over the member sequences
+  const int64_t nm = constrained_only ? nc : nseq;
+  std::vector<int64_t> mem((size_t)nm);
+  if (constrained_only) {  // keep.seq is in sequence order (terms-pass slot order)
+    for (int64_t i = 0; i < nc; ++i) mem[(size_t)i] = keep.seq[(size_t)i];
+    std::sort(mem.begin(), mem.end());
+  } else {
+    std::iota(mem.begin(), mem.end(), (int64_t)0);
+  }
   int64_t maxlen = 0;
-  for (int64_t s = 0; s < nseq; ++s) maxlen = std::max(maxlen, offsets_host[s + 1] - start[(size_t)s]);
-  std::vector<int64_t> pos((size_t)maxlen + 2, 0), perm((size_t)nseq);
-  for (int64_t s = 0; s < nseq; ++s) ++pos[(size_t)(maxlen - (offsets_host[s + 1] - start[(size_t)s])) + 1];
+  for (int64_t s : mem) maxlen = std::max(maxlen, offsets_host[s + 1] - start[(size_t)s]);
+  std::vector<int64_t> pos((size_t)maxlen + 2, 0), perm((size_t)nm);
+  for (int64_t s : mem) ++pos[(size_t)(maxlen - (offsets_host[s + 1] - start[(size_t)s])) + 1];
   for (size_t k = 1; k < pos.size(); ++k) pos[k] += pos[k - 1];
-  for (int64_t s = 0; s < nseq; ++s) perm[(size_t)pos[(size_t)(maxlen - (offsets_host[s + 1] - start[(size_t)s]))]++] = s;
-  // per compact sequence: [cstart | perm | off2 (nseq+1)] int64, then ridx int32
-  std::vector<int64_t> c64((size_t)3 * nseq + 1);
-  std::vector<int32_t> cridx((size_t)nseq);
+  for (int64_t s : mem) perm[(size_t)pos[(size_t)(maxlen - (offsets_host[s + 1] - start[(size_t)s]))]++] = s;
+  // per compact sequence: [cstart | perm | off2 (nm+1)] int64, then ridx int32
+  std::vector<int64_t> c64((size_t)3 * nm + 1);
+  std::vector<int32_t> cridx((size_t)nm);
   int64_t* cstart = c64.data();
-  int64_t* cperm = cstart + nseq;
-  int64_t* off2 = cperm + nseq;
+  int64_t* cperm = cstart + nm;
+  int64_t* off2 = cperm + nm;
   off2[0] = 0;
-  for (int64_t k = 0; k < nseq; ++k) {
+  for (int64_t k = 0; k < nm; ++k) {
     const int64_t s = perm[(size_t)k];
     cstart[k] = start[(size_t)s];
     cperm[k] = s;
     cridx[(size_t)k] = ridx[(size_t)s];
     off2[k + 1] = off2[k] + offsets_host[s + 1] - start[(size_t)s];
   }
-  const int64_t total2 = off2[nseq];
+  const int64_t total2 = off2[nm];
   // per-slot arrays: [seq | t1 | row_base] int64, then state int32
   std::vector<int64_t> slot64((size_t)nc * 3);
   std::copy(keep.seq.begin(), keep.seq.end(), slot64.begin());
   std::copy(keep.t1.begin(), keep.t1.end(), slot64.begin() + nc);
   std::copy(keep.row_base.begin(), keep.row_base.end(), slot64.begin() + 2 * nc);
   if ((st = h->rs_start.ensure(c64.size() * 8)) != CV_OK) return st;
-  if ((st = h->rs_ridx.ensure((size_t)nseq * 4)) != CV_OK) return st;
-  if ((st = h->rs_off2.ensure((size_t)nseq * 9)) != CV_OK) return st;  // score2 f64 + status2 u8
+  if ((st = h->rs_ridx.ensure((size_t)std::max<int64_t>(nm, 1) * 4)) != CV_OK) return st;
+  if ((st = h->rs_off2.ensure((size_t)std::max<int64_t>(nm, 1) * 9)) != CV_OK) return st;  // score2 f64 + status2 u8
   if ((st = h->rs_slot.ensure((size_t)std::max<int64_t>(nc, 1) * 28)) != CV_OK) return st;
   if ((st = h->rs_resume.ensure((size_t)std::max<int64_t>(nc, 1) * np * rb)) != CV_OK) return st;
   if ((st = h->rs_obs2.ensure((size_t)std::max<int64_t>(total2, 1) * 4)) != CV_OK) return st;
@@ -1744,14 +1877,14 @@ cv_status forced_decode_resume(cv_hmm* h, int64_t nseq, const int64_t* offsets_h
   if (!h->rs_ev && hipEventCreateWithFlags(&h->rs_ev, hipEventDisableTiming) != hipSuccess)
     return set_err(CV_EDEVICE, "hipEventCreate failed");
   const int64_t* cstart_d = h->rs_start.as<int64_t>();
-  const int64_t* cperm_d = cstart_d + nseq;
-  const int64_t* off2_d = cperm_d + nseq;
+  const int64_t* cperm_d = cstart_d + nm;
+  const int64_t* off2_d = cperm_d + nm;
   double* score2 = h->rs_off2.as<double>();
-  uint8_t* status2 = reinterpret_cast<uint8_t*>(score2 + nseq);
+  uint8_t* status2 = reinterpret_cast<uint8_t*>(score2 + nm);
   int64_t* slot_d = h->rs_slot.as<int64_t>();
   int32_t* state_d = reinterpret_cast<int32_t*>(slot_d + 3 * nc);
   HIP_TRY(hipMemcpyAsync(h->rs_start.p, c64.data(), c64.size() * 8, hipMemcpyHostToDevice, stream));
-  HIP_TRY(hipMemcpyAsync(h->rs_ridx.p, cridx.data(), (size_t)nseq * 4, hipMemcpyHostToDevice, stream));
+  HIP_TRY(hipMemcpyAsync(h->rs_ridx.p, cridx.data(), (size_t)nm * 4, hipMemcpyHostToDevice, stream));
   HIP_TRY(hipMemcpyAsync(slot_d, slot64.data(), (size_t)nc * 24, hipMemcpyHostToDevice, stream));
   HIP_TRY(hipMemcpyAsync(state_d, state.data(), (size_t)nc * 4, hipMemcpyHostToDevice, stream));
   hipError_t err = f64 ? cvk::launch_t64_resume_rows(h->cs_delta.as<double>(), state_d, nc, np,
@@ -1760,7 +1893,7 @@ cv_status forced_decode_resume(cv_hmm* h, int64_t nseq, const int64_t* offsets_h
                                                  stream);
   if (err == hipSuccess)
     err = cvk::launch_compact_suffix(cstart_d, off2_d, obs_dev, h->st_forced.as<int32_t>(), h->rs_ridx.as<int32_t>(),
-                                     h->rs_obs2.as<int32_t>(), h->rs_frc2.as<int32_t>(), nseq, stream);
+                                     h->rs_obs2.as<int32_t>(), h->rs_frc2.as<int32_t>(), nm, stream);
   if (err != hipSuccess) return set_err(CV_EDEVICE, "resume staging failed: %s", hipGetErrorString(err));
   // prefix paths on the backtrack stream, beside the suffix decode (one workgroup per CU at
   // most: the 100 KiB LDS reservation, as the chunk pipeline's backtracks)
@@ -1785,7 +1918,7 @@ cv_status forced_decode_resume(cv_hmm* h, int64_t nseq, const int64_t* offsets_h
   cv_opts o2 = o;
   o2.forced = h->rs_frc2.as<int32_t>();
   o2.rescore_f64 = 0;  // f32: re-scored below over the whole sequences; f64: the score is exact
-  if ((st = decode_device(h, nseq, off2, off2_d, h->rs_obs2.as<int32_t>(), o2, h->rs_path2.as<int32_t>(), score2,
+  if ((st = decode_device(h, nm, off2, off2_d, h->rs_obs2.as<int32_t>(), o2, h->rs_path2.as<int32_t>(), score2,
                           status2, stream, h->rs_resume.p)) != CV_OK) {
     (void)hipStreamSynchronize(stream);
     (void)hipStreamSynchronize(h->bt_stream);
@@ -1811,7 +1944,7 @@ cv_status forced_decode_resume(cv_hmm* h, int64_t nseq, const int64_t* offsets_h
     HIP_TRY(hipStreamWaitEvent(stream, h->rs_ev, 0));  // prefix paths written
   }
   err = cvk::launch_scatter_suffix(cstart_d, off2_d, cperm_d, h->rs_path2.as<int32_t>(), score2, status2, path_dev,
-                                   score_dev, status_dev, nseq, stream);
+                                   score_dev, status_dev, nm, stream);
   if (err == hipSuccess) err = cvk::launch_zero_infeasible_prefix(pa, nc, stream);
   if (err == hipSuccess && o.rescore_f64 && !f64) {
     cvk::RescoreArgs ra{};
@@ -2044,6 +2177,23 @@ CV_API cv_status cv_decode_constrained_device(cv_hmm* h, int64_t nseq, const int
   std::vector<ConSeq> cs;
   build_conseq(nseq, offsets_host, component, cs);
   trace_mark("device constrained: checks + constrained list");
+  // the unconstrained sequences beside the terms pass (A/B knob, bit-identical: CV_NO_SIDE=1)
+  SideJoin side{h};
+  const char* no_side = getenv("CV_NO_SIDE");
+  const bool side_off = no_side && *no_side && *no_side != '0';
+  if (!side_off && o.dtype == CV_DTYPE_F64 && resume_supported(h, true) && !cs.empty()) {
+    // the constrained work moves to a highest-priority stream (behind the caller's stream), the
+    // side decode gets the lowest: its waves take the slots the constrained work leaves free
+    if ((st = side_streams(h)) != CV_OK) return st;
+    HIP_TRY(hipEventRecord(h->side.start, stream));
+    HIP_TRY(hipStreamWaitEvent(h->side.hi, h->side.start, 0));
+    stream = h->side.hi;
+    o.stream = stream;
+    side.hi = true;
+    if ((st = side_decode_launch(h, nseq, offsets_host, obs_dev, cs, o, path_dev, score_dev, status_dev, stream,
+                                 &side.active)) != CV_OK)
+      return st;
+  }
   const std::vector<int32_t> pairs = conseq_pairs(cs, component);
   const int64_t npairs = (int64_t)pairs.size() / 2;
   std::vector<int64_t> part((size_t)cvcsp::partial_words((int)h->N, ncomp, npairs), 0);
@@ -2059,9 +2209,12 @@ CV_API cv_status cv_decode_constrained_device(cv_hmm* h, int64_t nseq, const int
   trace_mark("select");
   if (keep.kept) {
     if ((st = forced_decode_resume(h, nseq, offsets_host, offsets_dev, obs_dev, component, comp_state_out, cs, keep,
-                                   o, path_dev, score_dev, status_dev, stream)) != CV_OK)
+                                   o, path_dev, score_dev, status_dev, stream, side.active)) != CV_OK)
       return st;
   } else {
+    // the full forced decode covers every sequence: the side results land first, then are
+    // rewritten with the same values
+    if (side.active) HIP_TRY(hipStreamWaitEvent(stream, h->side.done, 0));
     if ((st = stage_forced_locked(h, offsets_host, nseq, component, comp_state_out, cs, stream)) != CV_OK) return st;
     o.forced = h->st_forced.as<int32_t>();
     if ((st = decode_device(h, nseq, offsets_host, offsets_dev, obs_dev, o, path_dev, score_dev, status_dev,
@@ -2069,6 +2222,10 @@ CV_API cv_status cv_decode_constrained_device(cv_hmm* h, int64_t nseq, const int
       (void)hipStreamSynchronize(stream);
       return st;
     }
+  }
+  if (side.active) {  // the unconstrained sequences' results are in the outputs
+    HIP_TRY(hipStreamWaitEvent(stream, h->side.done, 0));
+    side.active = false;
   }
   // scores/statuses to the host for the objective (9 B per sequence), fixed up, and back
   std::vector<double> sc((size_t)nseq);

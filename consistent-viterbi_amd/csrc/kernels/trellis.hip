@@ -1379,10 +1379,11 @@ __global__ void compact_suffix(const int64_t* cstart, const int64_t* off2, const
                                const int32_t* ridx, int32_t* obs2, int32_t* forced2) {
   const int64_t k = blockIdx.x;
   const int64_t e0 = cstart[k], o2 = off2[k], n = off2[k + 1] - o2;
-  const int r = ridx[k];
+  // forced2 == nullptr: observations only (the constrained decode's unconstrained sequences)
+  const int r = ridx ? ridx[k] : -1;
   for (int64_t q = threadIdx.x; q < n; q += blockDim.x) {
     obs2[o2 + q] = obs[e0 + q];
-    forced2[o2 + q] = (q == 0 && r >= 0) ? -2 - r : forced[e0 + q];
+    if (forced2) forced2[o2 + q] = (q == 0 && r >= 0) ? -2 - r : forced[e0 + q];
   }
 }
 

@@ -564,3 +564,52 @@ def test_constrained_sharded_two_processes(gpu):
     q = ctx.Queue()
     mp.start_processes(_sharded_worker, args=(2, _free_port(), q), nprocs=2, join=True, start_method="spawn")
     assert q.get(timeout=5) is True
+
+
+@pytest.mark.parametrize("nseq,T", [(4096, 64), (300, 33)])
+def test_constrained_device_side_decode_bit_identical(gpu, monkeypatch, nseq, T):
+    """The device API decodes the unconstrained sequences on a side stream beside the terms
+    pass: bit-identical to the same call with CV_NO_SIDE=1 and to the host API
+    (which does not use the side stream)."""
+    import torch
+
+    pi, a, b = synth.random_hmm(256, 40, seed=nseq)
+    off = np.arange(nseq + 1, dtype=np.int64) * T
+    rng = np.random.default_rng(nseq)
+    obs = rng.integers(0, 40, size=nseq * T).astype(np.int32)
+    comp = synth.constraint_components(off, seed=nseq, ncomp=5, prob=0.5)
+    h = cv.HMM(pi, a, b)
+    dev = torch.device("cuda", 0)
+    o_d, ob_d = torch.from_numpy(off).to(dev), torch.from_numpy(obs).to(dev)
+    res = []
+    for side in ("0", "1"):
+        monkeypatch.setenv("CV_NO_SIDE", side)
+        outs = (torch.full((nseq * T,), 9, dtype=torch.int32, device=dev),
+                torch.empty(nseq, dtype=torch.float64, device=dev), torch.empty(nseq, dtype=torch.uint8, device=dev))
+        states, obj = cv.decode_constrained_device(h, off, o_d, ob_d, comp, *outs, ncomp=5, dtype="f64")
+        res.append((outs[0].cpu().numpy(), outs[1].cpu().numpy(), outs[2].cpu().numpy(), states, obj))
+    ref = cv.decode_constrained(h, off, obs, comp, ncomp=5, dtype="f64")
+    for got in res:
+        for x, y, what in zip(got, ref, ("path", "score", "status", "states", "objective")):
+            assert np.array_equal(np.asarray(x), np.asarray(y)), what
+    assert np.all(ref[2] == 0)
+
+
+def test_full_config5_device_equals_host(gpu):
+    """Config 5 at full size through the device API (side-stream decode of the unconstrained
+    half, resume flow) == the host API, bit for bit."""
+    import torch
+
+    c = synth.config("c5")
+    pi, a, b, off, obs, comp = c["pi"], c["a"], c["b"], c["offsets"], c["obs"], c["component"]
+    h = cv.HMM(pi, a, b.reshape(256, 32, 32))
+    ref = cv.decode_constrained(h, off, obs, comp, 7, dtype="f64")
+    dev = torch.device("cuda", 0)
+    outs = (torch.empty(len(obs), dtype=torch.int32, device=dev), torch.empty(len(off) - 1, dtype=torch.float64,
+                                                                             device=dev),
+            torch.empty(len(off) - 1, dtype=torch.uint8, device=dev))
+    states, obj = cv.decode_constrained_device(h, off, torch.from_numpy(off).to(dev), torch.from_numpy(obs).to(dev),
+                                               comp, *outs, ncomp=7, dtype="f64")
+    got = (outs[0].cpu().numpy(), outs[1].cpu().numpy(), outs[2].cpu().numpy(), states, obj)
+    for x, y, what in zip(got, ref, ("path", "score", "status", "states", "objective")):
+        assert np.array_equal(np.asarray(x), np.asarray(y)), what
