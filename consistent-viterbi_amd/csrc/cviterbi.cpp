@@ -18,6 +18,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <memory>
+#include <functional>
 #include <mutex>
 #include <numeric>
 #include <string>
@@ -27,6 +28,7 @@
 #include "../../include/cviterbi.h"
 #include "csp.hpp"
 #include "hmm_json.hpp"
+#include "kernels/chain.h"
 #include "kernels/cfn.h"
 #include "kernels/exact.h"
 #include "kernels/fit.h"
@@ -1227,7 +1229,8 @@ cv_status constrained_partials_locked(cv_hmm* h, int64_t nseq, const int64_t* of
                                       const int32_t* component, int32_t ncomp, const int32_t* pairs, int64_t npairs,
                                       cv_opts& o, int64_t* part, const std::vector<ConSeq>* pre = nullptr,
                                       bool* obs_staged = nullptr, const int32_t* obs_dev = nullptr,
-                                      PrefixKeep* keep = nullptr) {
+                                      PrefixKeep* keep = nullptr,
+                                      const std::function<cv_status()>& after_terms = nullptr) {
   if (keep) *keep = PrefixKeep{};
   if (obs_staged) *obs_staged = false;
   std::vector<ConSeq> own;
@@ -1443,6 +1446,9 @@ cv_status constrained_partials_locked(cv_hmm* h, int64_t nseq, const int64_t* of
   }
   if (err != hipSuccess) return set_err(CV_EDEVICE, "term launches failed: %s", hipGetErrorString(err));
   trace_mark("term launches enqueued");
+  // work queued behind the term launches on another stream (the device API's side decode): it
+  // takes the slots the terms pass leaves free at its tails
+  if (after_terms && (st = after_terms()) != CV_OK) return st;
   for (int64_t i = 0; i < nc; ++i)
     for (int64_t e : order[i]->elems) part[(int64_t)component[e] * uw + 5 * N] += 1;
   auto range_err = [] {
@@ -1752,8 +1758,9 @@ cv_status side_decode_launch(cv_hmm* h, int64_t nseq, const int64_t* offsets_hos
   if ((st = sd.obs2.ensure((size_t)std::max<int64_t>(total2, 1) * 4)) != CV_OK) return st;
   if ((st = sd.path2.ensure((size_t)std::max<int64_t>(total2, 1) * 4)) != CV_OK) return st;
   if ((st = sd.res2.ensure((size_t)nu * 9)) != CV_OK) return st;
-  // the side stream starts behind everything the caller queued on its stream (inputs, outputs)
-  HIP_TRY(hipEventRecord(sd.start, stream));
+  // the side stream starts behind everything the caller had queued on its stream when the
+  // constrained decode began (h->side.start, recorded then), not behind the term launches
+  (void)stream;
   HIP_TRY(hipStreamWaitEvent(sd.stream, sd.start, 0));
   HIP_TRY(hipMemcpyAsync(sd.idx.p, sd.idx_host.data(), sd.idx_host.size() * 8, hipMemcpyHostToDevice, sd.stream));
   const int64_t* cstart_d = sd.idx.as<int64_t>();
@@ -2190,16 +2197,18 @@ CV_API cv_status cv_decode_constrained_device(cv_hmm* h, int64_t nseq, const int
     stream = h->side.hi;
     o.stream = stream;
     side.hi = true;
-    if ((st = side_decode_launch(h, nseq, offsets_host, obs_dev, cs, o, path_dev, score_dev, status_dev, stream,
-                                 &side.active)) != CV_OK)
-      return st;
   }
+  auto launch_side = [&]() -> cv_status {
+    return side.hi ? side_decode_launch(h, nseq, offsets_host, obs_dev, cs, o, path_dev, score_dev, status_dev, stream,
+                                        &side.active)
+                   : CV_OK;
+  };
   const std::vector<int32_t> pairs = conseq_pairs(cs, component);
   const int64_t npairs = (int64_t)pairs.size() / 2;
   std::vector<int64_t> part((size_t)cvcsp::partial_words((int)h->N, ncomp, npairs), 0);
   PrefixKeep keep;
   if ((st = constrained_partials_locked(h, nseq, offsets_host, nullptr, component, ncomp, pairs.data(), npairs, o,
-                                        part.data(), &cs, nullptr, obs_dev, &keep)) != CV_OK)
+                                        part.data(), &cs, nullptr, obs_dev, &keep, launch_side)) != CV_OK)
     return st;
   uint64_t explored = 0;
   if ((st = select_locked((int32_t)h->N, ncomp, pairs.data(), npairs, part.data(), comp_state_out, &explored)) !=
@@ -2361,6 +2370,91 @@ CV_API cv_status cv_viterbi_decode(cv_hmm* h, int64_t T, const int32_t* obs, int
   return cv_decode_batch(h, 1, off, obs, &o, path_out, &score, &status);
 }
 
+}  // extern "C"
+
+namespace {
+// cv_decode_superseq_cp for N <= 256: the chain forward (cp_chain_wg) writes psi [L][NP] u16
+// and the final state; the backtrack runs in segments: pass 1 maps every segment's last-state
+// to the state before it for all NP states (cp_chain_seg_map), the host follows the maps from
+// the final state, pass 2 writes each segment's path (cp_chain_seg_path).
+cv_status superseq_cp_wg(cv_hmm* h, int64_t L, const int32_t* obs, const std::vector<uint8_t>& first,
+                         int32_t* path_out, double* objective_out) {
+  cv_status st;
+  if ((st = ensure_t64_tables(h)) != CV_OK) return st;
+  const int NP = h->np64;
+  const uint64_t psi_bytes = (uint64_t)L * NP * 2;
+  const uint64_t avail = free_device_bytes(0);
+  if (avail && psi_bytes + (uint64_t)L * 9 > avail / 10 * 9)
+    return set_err(CV_ENOMEM,
+                   "super-sequence of %lld elements needs %.1f GB of back-pointers (%.1f GB of device memory "
+                   "free): decode it in parts or per sequence (solver kind gpu-cp-seq)",
+                   (long long)L, psi_bytes / 1e9, avail / 1e9);
+  hipStream_t stream = h->stream;
+  DevBuf d_obs, d_first, d_psi, d_path, d_out, d_map, d_end;
+  if ((st = d_obs.ensure((size_t)L * 4)) != CV_OK) return st;
+  if ((st = d_first.ensure((size_t)L)) != CV_OK) return st;
+  if ((st = d_psi.ensure((size_t)psi_bytes)) != CV_OK) return st;
+  if ((st = d_path.ensure((size_t)L * 4)) != CV_OK) return st;
+  if ((st = d_out.ensure(16)) != CV_OK) return st;
+  HIP_TRY(hipMemcpyAsync(d_obs.p, obs, (size_t)L * 4, hipMemcpyHostToDevice, stream));
+  HIP_TRY(hipMemcpyAsync(d_first.p, first.data(), (size_t)L, hipMemcpyHostToDevice, stream));
+  cvk::CpChainWgArgs g{};
+  g.pi = h->q_pi.as<double>();
+  g.a = h->q_a.as<double>();
+  g.et = h->q_et.as<double>();
+  g.obs = d_obs.as<int32_t>();
+  g.first = d_first.as<uint8_t>();
+  g.len = L;
+  g.nstates = h->N;
+  g.psi = d_psi.as<uint16_t>();
+  g.objective = d_out.as<double>();
+  g.final_state = reinterpret_cast<int32_t*>(d_out.as<double>() + 1);
+  hipError_t err = cvk::launch_cp_chain_wg(NP, g, stream);
+  if (err != hipSuccess) return set_err(CV_EDEVICE, "super-sequence chain launch failed: %s", hipGetErrorString(err));
+  double out[2];
+  HIP_TRY(hipMemcpyAsync(out, d_out.p, 16, hipMemcpyDeviceToHost, stream));
+  HIP_TRY(hipStreamSynchronize(stream));
+  *objective_out = out[0];
+  int32_t fs;
+  std::memcpy(&fs, &out[1], 4);
+  // segments: ~8,192 of them (>= 256 elements each) for the parallel passes
+  const int64_t seg = std::max<int64_t>(256, (L + 8191) / 8192);
+  const int64_t nseg = (L + seg - 1) / seg;
+  if ((st = d_map.ensure((size_t)nseg * NP * 2)) != CV_OK) return st;
+  if ((st = d_end.ensure((size_t)nseg * 4)) != CV_OK) return st;
+  cvk::CpChainBtArgs b{};
+  b.psi = d_psi.as<uint16_t>();
+  b.np = NP;
+  b.len = L;
+  b.seg = seg;
+  b.nseg = nseg;
+  b.map = d_map.as<uint16_t>();
+  b.end_state = d_end.as<int32_t>();
+  b.path = d_path.as<int32_t>();
+  err = cvk::launch_cp_chain_seg_map(b, stream);
+  if (err != hipSuccess) return set_err(CV_EDEVICE, "chain backtrack (maps) failed: %s", hipGetErrorString(err));
+  std::vector<uint16_t> map((size_t)nseg * NP);
+  HIP_TRY(hipMemcpyAsync(map.data(), d_map.p, map.size() * 2, hipMemcpyDeviceToHost, stream));
+  HIP_TRY(hipStreamSynchronize(stream));
+  std::vector<int32_t> end((size_t)nseg);
+  int32_t s = fs;
+  for (int64_t k = nseg - 1; k >= 0; --k) {
+    end[(size_t)k] = s;
+    if (k > 0) s = map[(size_t)k * NP + s];
+  }
+  HIP_TRY(hipMemcpyAsync(d_end.p, end.data(), (size_t)nseg * 4, hipMemcpyHostToDevice, stream));
+  err = cvk::launch_cp_chain_seg_path(b, stream);
+  if (err != hipSuccess) return set_err(CV_EDEVICE, "chain backtrack (paths) failed: %s", hipGetErrorString(err));
+  HIP_TRY(hipMemcpyAsync(path_out, d_path.p, (size_t)L * 4, hipMemcpyDeviceToHost, stream));
+  HIP_TRY(hipStreamSynchronize(stream));
+  if (!(*objective_out > -INFINITY))
+    return set_err(CV_EINFEASIBLE, "no finite-probability path through the super-sequence (cp.rs:87 asserts)");
+  return CV_OK;
+}
+}  // namespace
+
+extern "C" {
+
 CV_API cv_status cv_decode_superseq_cp(cv_hmm* h, int64_t nseq, const int64_t* offsets, const int32_t* obs,
                                        int32_t* path_out, double* objective_out) {
   if (!h || nseq < 0 || (nseq > 0 && (!offsets || !obs || !path_out)) || !objective_out)
@@ -2379,10 +2473,16 @@ CV_API cv_status cv_decode_superseq_cp(cv_hmm* h, int64_t nseq, const int64_t* o
     const int64_t k = first_bad(base, offsets[nseq], [&](int64_t i) { return obs[i] < 0 || obs[i] >= V; });
     if (k >= 0) return set_err(CV_EINVAL, "obs[%lld] = %d out of range [0,%lld)", (long long)k, obs[k], (long long)V);
   }
-  if ((st = ensure_f64_tables(h)) != CV_OK) return st;
   std::vector<uint8_t> first((size_t)L, 0);
   for (int64_t q = 0; q < nseq; ++q)
     if (offsets[q + 1] > offsets[q]) first[(size_t)(offsets[q] - base)] = 1;
+  // N <= 256: the one-workgroup chain with the candidates split over its waves and A on chip
+  // (kernels/chain.hip), then the parallel segmented backtrack; N > 256 (or CV_CHAIN_OLD=1, an
+  // A/B knob, bit-identical): one thread per state (cp_superseq_chain)
+  const char* old_env = getenv("CV_CHAIN_OLD");
+  if (cvk::t64_padded_states(h->N) && !(old_env && *old_env == '1'))
+    return superseq_cp_wg(h, L, obs + base, first, path_out, objective_out);
+  if ((st = ensure_f64_tables(h)) != CV_OK) return st;
   hipStream_t stream = h->stream;
   DevBuf d_obs, d_first, d_psi, d_path, d_obj;
   if ((st = d_obs.ensure((size_t)L * 4)) != CV_OK) return st;

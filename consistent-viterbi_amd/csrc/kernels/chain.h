@@ -1,0 +1,43 @@
+// chain.h -- CPSolver's super-sequence decode chained exactly (cp.rs:63-93 over
+// utils.rs:24-38), N <= 256: one workgroup walks the elements, candidates split across its
+// waves; then a parallel segmented backtrack over the stored psi rows.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace cvk {
+
+struct CpChainWgArgs {
+  const double* pi;      // [NP] -inf padded
+  const double* a;       // [NP][NP] from-major, -inf padded
+  const double* et;      // [V][NP] emissions transposed, -inf padded
+  const int32_t* obs;    // [len] super-sequence observations
+  const uint8_t* first;  // [len] 1 at the first element of each sequence (MetaElements t == 0)
+  int64_t len;
+  int nstates;
+  uint16_t* psi;         // [len][NP] first argmax per (element, state); row 0 unused
+  double* objective;     // [1] max of the last row (cp.rs:140)
+  int32_t* final_state;  // [1] its first argmax (cp.rs:86)
+};
+// forward of the whole chain on ONE workgroup; np = 64 * ceil(N / 64) <= 256
+hipError_t launch_cp_chain_wg(int np, const CpChainWgArgs& g, hipStream_t stream);
+// LDS bytes launch_cp_chain_wg asks for at this np (0: unsupported)
+size_t cp_chain_wg_lds(int np);
+
+struct CpChainBtArgs {
+  const uint16_t* psi;       // [len][np]
+  int np;
+  int64_t len;
+  int64_t seg;               // elements per segment
+  int64_t nseg;
+  uint16_t* map;             // [nseg][np]: segment k >= 1, state at its last element -> state at e0 - 1
+  const int32_t* end_state;  // [nseg] state at the last element of segment k
+  int32_t* path;             // [len]
+};
+// pass 1: every segment k >= 1 backtracks from ALL np end states at once -> map[k]
+hipError_t launch_cp_chain_seg_map(const CpChainBtArgs& g, hipStream_t stream);
+// pass 2 (after the host resolved end_state[] through the maps): each segment's path
+hipError_t launch_cp_chain_seg_path(const CpChainBtArgs& g, hipStream_t stream);
+
+}  // namespace cvk

@@ -225,6 +225,40 @@ def test_superseq_cp_chain_sizes(gpu, n):
     assert np.array_equal(path, rp) and obj == robj
 
 
+@pytest.mark.parametrize("n,quant", [(3, True), (64, False), (65, True), (128, False), (192, True), (256, False),
+                                     (256, True)])
+def test_superseq_cp_chain_segmented_backtrack(gpu, n, quant):
+    """The N <= 256 chain (one workgroup, candidates split over its waves, kernels/chain.hip)
+    over super-sequences long enough for a multi-segment parallel backtrack (256-element
+    segments), incl. empty and one-element sequences: every element and the objective equal the
+    chained restatement (cp.rs:63-93 over utils.rs:24-38)."""
+    rng = np.random.default_rng(900 + n)
+    v = 17
+    if quant:  # exact ties everywhere: the first index must win in every group and across groups
+        pi = np.round(rng.uniform(-2, 0, n) * 2) / 2
+        a = np.round(rng.uniform(-2, 0, (n, n)) * 2) / 2
+        b = np.round(rng.uniform(-2, 0, (n, v)) * 2) / 2
+        a[rng.random((n, n)) < 0.1] = -np.inf
+    else:
+        pi, a, b = synth.random_hmm(n, v, seed=n)
+    lengths = rng.integers(1, 200, size=24)
+    lengths[[3, 11]] = 0
+    lengths[5] = 1
+    off = synth.offsets_from_lengths(lengths)
+    obs = rng.integers(0, v, size=int(off[-1])).astype(np.int32)
+    assert off[-1] > 4 * 256
+    h = cv.HMM(pi, a, b)
+    path, obj = cv.decode_superseq_cp(h, off, obs)
+    rp, robj = O.cp_superseq_f64(pi, a, b, off, obs)
+    assert obj == robj
+    bad = np.nonzero(path != rp)[0]
+    assert bad.size == 0, f"elements {bad[:10]} of {len(rp)}"
+    # one element
+    p1, o1 = cv.decode_superseq_cp(h, off[:2] * 0 + np.array([0, 1]), obs[:1])
+    r1, ro1 = O.cp_superseq_f64(pi, a, b, np.array([0, 1]), obs[:1])
+    assert np.array_equal(p1, r1) and o1 == ro1
+
+
 @pytest.mark.parametrize("dtype", ["f64", "f32"])
 @pytest.mark.parametrize("nshards", [2, 5])
 def test_constrained_sharded_equals_single(gpu, nshards, dtype):
