@@ -1135,7 +1135,40 @@ struct ConSeq {
   std::vector<int64_t> elems;  // constrained elements, ascending
 };
 
-// Constrained sequences in sequence order (per-worker lists concatenated in order).
+// Constrained sequences in sequence order (per-worker lists concatenated in order), and the
+// range check of the components in the same pass: returns the first element with a component
+// outside [-1, ncomp), or -1.  A sequence whose components are all -1 (AND of the words = -1)
+// is skipped by one vectorised pass over it.
+int64_t build_conseq_checked(int64_t nseq, const int64_t* offsets, const int32_t* component, int32_t ncomp,
+                             std::vector<ConSeq>& cs) {
+  cs.clear();
+  std::vector<std::vector<ConSeq>> part((size_t)host_threads());
+  std::vector<int64_t> bad((size_t)host_threads(), -1);
+  parallel_ranges(nseq, [&](int t, int64_t lo, int64_t hi) {
+    for (int64_t s = lo; s < hi; ++s) {
+      const int32_t* c = component + offsets[s];
+      const int64_t n = offsets[s + 1] - offsets[s];
+      int32_t all = -1;
+      for (int64_t k = 0; k < n; ++k) all &= c[k];
+      if (all == -1) continue;  // every component is -1
+      ConSeq q{s, {}};
+      for (int64_t k = 0; k < n; ++k) {
+        if (c[k] < -1 || c[k] >= ncomp) {
+          bad[(size_t)t] = offsets[s] + k;
+          return;
+        }
+        if (c[k] >= 0) q.elems.push_back(offsets[s] + k);
+      }
+      part[(size_t)t].push_back(std::move(q));
+    }
+  }, 1024);
+  for (int64_t b : bad)
+    if (b >= 0) return b;  // workers hold ascending ranges
+  for (auto& p : part)
+    for (auto& c : p) cs.push_back(std::move(c));
+  return -1;
+}
+
 void build_conseq(int64_t nseq, const int64_t* offsets, const int32_t* component, std::vector<ConSeq>& cs) {
   cs.clear();
   std::vector<std::vector<ConSeq>> part((size_t)host_threads());
@@ -2163,9 +2196,10 @@ CV_API cv_status cv_decode_constrained_device(cv_hmm* h, int64_t nseq, const int
   if (o.forced) return set_err(CV_EINVAL, "opts->forced is set by the constrained decode itself");
   if (nseq == 0) return CV_OK;
   if ((st = check_batch(h, nseq, offsets_host)) != CV_OK) return st;
+  // components checked and the constrained list built in one host pass
+  std::vector<ConSeq> cs;
   {
-    const int64_t k = first_bad(offsets_host[0], offsets_host[nseq],
-                                [&](int64_t i) { return component[i] < -1 || component[i] >= ncomp; });
+    const int64_t k = build_conseq_checked(nseq, offsets_host, component, ncomp, cs);
     if (k >= 0)
       return set_err(CV_EINVAL, "component[%lld] = %d out of range [-1,%d)", (long long)k, component[k], ncomp);
   }
@@ -2181,8 +2215,6 @@ CV_API cv_status cv_decode_constrained_device(cv_hmm* h, int64_t nseq, const int
     HIP_TRY(hipStreamSynchronize(stream));
     if (first != ~0ull) return set_err(CV_EINVAL, "obs[%llu] out of range [0,%lld)", first, (long long)h->V);
   }
-  std::vector<ConSeq> cs;
-  build_conseq(nseq, offsets_host, component, cs);
   trace_mark("device constrained: checks + constrained list");
   // the unconstrained sequences beside the terms pass (A/B knob, bit-identical: CV_NO_SIDE=1)
   SideJoin side{h};

@@ -12,7 +12,8 @@
 // pairs are combined in row order (first index kept on ties: identical to the serial scan),
 // and d' goes back through LDS.  A (NP^2 f64 = 512 KiB at N = 256) is spread over the
 // workgroup's registers (RREG rows per thread), its LDS (RLDS rows) and L2 (RGLB rows, loaded
-// at the start of each element, consumed last).
+// at the start of each element, consumed last); at NP <= 128 all candidate rows sit in
+// registers and a full copy of A in LDS serves the value's a[psi][j].
 // The backtrack is parallel over segments: pass 1 maps each segment's last-element state to
 // the state before its first element for ALL NP states at once (one lane per state); the
 // host walks the segment maps from the final state; pass 2 writes every segment's path.
@@ -21,7 +22,9 @@
 namespace cvk {
 namespace {
 
-template <int NP, int G, int RREG, int RLDS, int RGLB>
+// AFULL: a full copy of A in LDS after the row slices (NP <= 128), so the value's a[psi][j]
+// is an LDS read instead of an L2 round trip on the element's critical path.
+template <int NP, int G, int RREG, int RLDS, int RGLB, bool AFULL>
 __global__ __launch_bounds__(NP * G) void cp_chain_wg(CpChainWgArgs g) {
   constexpr int R = NP / G;
   static_assert(RREG + RLDS + RGLB == R, "every candidate row has one home");
@@ -32,6 +35,7 @@ __global__ __launch_bounds__(NP * G) void cp_chain_wg(CpChainWgArgs g) {
   double* pm = sm + 2 * NP;             // [G][NP] partial maxima
   int* pa = reinterpret_cast<int*>(sm + 2 * NP + G * NP);  // [G][NP] their first indices
   double* al = sm + 2 * NP + G * NP + G * NP / 2;          // [G][RLDS][NP] LDS rows of A
+  double* afull = al + G * RLDS * NP;                      // [NP][NP] when AFULL
   const int tid = threadIdx.x;
   const int c = tid % NP;
   const int grp = __builtin_amdgcn_readfirstlane(tid / NP);  // wave-uniform (NP % 64 == 0)
@@ -41,6 +45,8 @@ __global__ __launch_bounds__(NP * G) void cp_chain_wg(CpChainWgArgs g) {
   for (int r = 0; r < RREG; ++r) areg[r] = g.a[(size_t)(i0 + r) * NP + c];
   for (int r = 0; r < RLDS; ++r) al[(grp * RLDS + r) * NP + c] = g.a[(size_t)(i0 + RREG + r) * NP + c];
   const double* aglb = g.a + (size_t)(i0 + RREG + RLDS) * NP + c;
+  if constexpr (AFULL)
+    for (int k = tid; k < NP * NP; k += NP * G) afull[k] = g.a[k];
   if (grp == 0) prev[c] = g.pi[c] + g.et[(size_t)g.obs[0] * NP + c];  // init_probs (cp.rs:66-68)
   __syncthreads();
   const int64_t L = g.len;
@@ -106,7 +112,7 @@ __global__ __launch_bounds__(NP * G) void cp_chain_wg(CpChainWgArgs g) {
           A = pa[q * NP + c];
         }
       }
-      const double tr = first ? g.pi[c] : g.a[(size_t)A * NP + c];
+      const double tr = first ? g.pi[c] : AFULL ? afull[A * NP + c] : g.a[(size_t)A * NP + c];
       cur[c] = prev[A] + (tr + g.et[(size_t)o * NP + c]);  // cp.rs:75-77
       g.psi[(size_t)t * NP + c] = (uint16_t)A;
     }
@@ -128,18 +134,18 @@ __global__ __launch_bounds__(NP * G) void cp_chain_wg(CpChainWgArgs g) {
   }
 }
 
-template <int NP, int G, int RREG, int RLDS, int RGLB>
+template <int NP, int G, int RREG, int RLDS, int RGLB, bool AFULL>
 size_t chain_lds() {
-  return (size_t)(2 * NP + G * NP + G * NP / 2 + G * RLDS * NP) * sizeof(double);
+  return (size_t)(2 * NP + G * NP + G * NP / 2 + G * RLDS * NP + (AFULL ? NP * NP : 0)) * sizeof(double);
 }
 
-template <int NP, int G, int RREG, int RLDS, int RGLB>
+template <int NP, int G, int RREG, int RLDS, int RGLB, bool AFULL>
 hipError_t chain_launch(const CpChainWgArgs& g, hipStream_t stream) {
-  const size_t lds = chain_lds<NP, G, RREG, RLDS, RGLB>();
+  const size_t lds = chain_lds<NP, G, RREG, RLDS, RGLB, AFULL>();
   if (lds > 64 * 1024)
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&cp_chain_wg<NP, G, RREG, RLDS, RGLB>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&cp_chain_wg<NP, G, RREG, RLDS, RGLB, AFULL>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL((cp_chain_wg<NP, G, RREG, RLDS, RGLB>), dim3(1), dim3(NP * G), lds, stream, g);
+  hipLaunchKernelGGL((cp_chain_wg<NP, G, RREG, RLDS, RGLB, AFULL>), dim3(1), dim3(NP * G), lds, stream, g);
   return hipGetLastError();
 }
 
@@ -197,10 +203,10 @@ __global__ __launch_bounds__(64) void cp_chain_seg_path(CpChainBtArgs g) {
 
 size_t cp_chain_wg_lds(int np) {
   switch (np) {
-    case 64: return chain_lds<64, 16, 4, 0, 0>();
-    case 128: return chain_lds<128, 8, 16, 0, 0>();
-    case 192: return chain_lds<192, 4, 32, 16, 0>();
-    case 256: return chain_lds<256, 4, 47, 17, 0>();
+    case 64: return chain_lds<64, 4, 16, 0, 0, true>();
+    case 128: return chain_lds<128, 4, 32, 0, 0, true>();
+    case 192: return chain_lds<192, 4, 32, 16, 0, false>();
+    case 256: return chain_lds<256, 4, 47, 17, 0, false>();
     default: return 0;
   }
 }
@@ -208,10 +214,10 @@ size_t cp_chain_wg_lds(int np) {
 hipError_t launch_cp_chain_wg(int np, const CpChainWgArgs& g, hipStream_t stream) {
   if (g.len <= 0) return hipSuccess;
   switch (np) {
-    case 64: return chain_launch<64, 16, 4, 0, 0>(g, stream);
-    case 128: return chain_launch<128, 8, 16, 0, 0>(g, stream);
-    case 192: return chain_launch<192, 4, 32, 16, 0>(g, stream);
-    case 256: return chain_launch<256, 4, 47, 17, 0>(g, stream);
+    case 64: return chain_launch<64, 4, 16, 0, 0, true>(g, stream);
+    case 128: return chain_launch<128, 4, 32, 0, 0, true>(g, stream);
+    case 192: return chain_launch<192, 4, 32, 16, 0, false>(g, stream);
+    case 256: return chain_launch<256, 4, 47, 17, 0, false>(g, stream);
     default: return hipErrorInvalidValue;
   }
 }

@@ -22,7 +22,7 @@ timeout -k 10 ${T_BENCH:-400} python -u bench.py ${BENCH_ARGS:---steps 10 --warm
 tail -c 2500 $OUT/bench.log
 step rocprof
 ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 ${T_PROF:-400} rocprofv3 --kernel-trace --stats -d $OUT/prof -o kt \
-    --output-format csv -- python3 $R/bench.py --steps 5 --warmup 1 --no-cpu-baseline > $OUT/prof.log 2>&1 ) \
+    --output-format csv -- python3 $R/bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-configs > $OUT/prof.log 2>&1 ) \
   || { echo "rocprof failed"; tail -20 $OUT/prof.log; exit 1; }
 f=$(find $OUT/prof -name "*kernel_stats.csv" | head -1)
 [ -n "$f" ] && cut -d, -f1-4 "$f" | head -8

@@ -23,7 +23,7 @@ fi
 if [ -z "${NO_PROF:-}" ]; then
   cd /tmp && export TMPDIR=/tmp
   timeout -k 10 ${T_PROF:-400} rocprofv3 --kernel-trace --stats -d $OUT/${TAG}_prof -o kt --output-format csv -- \
-    python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline > $OUT/${TAG}_prof.log 2>&1; rc=$?
+    python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-configs > $OUT/${TAG}_prof.log 2>&1; rc=$?
   echo "rocprof rc=$rc"
   f=$(find $OUT/${TAG}_prof -name "*kernel_stats.csv" | head -1)
   [ -n "$f" ] && cut -d, -f1-8 "$f" | head -12

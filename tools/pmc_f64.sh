@@ -7,7 +7,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/${TAG:-pmc_f64}
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
-ARGS="--steps 1 --warmup 1 --no-cpu-baseline --no-f32-extra ${PMC_ARGS:-}"
+ARGS="--steps 1 --warmup 1 --no-cpu-baseline --no-f32-extra --no-configs ${PMC_ARGS:-}"
 for C in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 ${T_PMC:-240} rocprofv3 --pmc $C --kernel-include-regex "${KRE:-trellis_fwd_f64}" -d $OUT/$C -o p \
     --output-format csv -- python3 $R/bench.py $ARGS > $OUT/$C.log 2>&1 || exit $?
@@ -49,3 +49,16 @@ if tot.get("GRBM_GUI_ACTIVE") and dur.get("GRBM_GUI_ACTIVE"):
           f"(kernel {dur['GRBM_GUI_ACTIVE'] * 1e-6:.2f} ms)")
 PY
 cat $OUT/sq_summary.txt
+# traffic + the effective clock in one summary (what bench.py reads from profiles/)
+python3 - "$OUT" "${TAG:-pmc_f64}" <<'PY'
+import json, re, sys, os
+out, tag = sys.argv[1], sys.argv[2]
+d = json.load(open(os.path.join(out, "traffic.json")))
+m = re.search(r"effective clock = ([0-9.]+) GHz \(kernel ([0-9.]+) ms\)", open(os.path.join(out, "sq_summary.txt")).read())
+if m:
+    d["clock_ghz"] = float(m.group(1))
+    d["kernel_ms_pmc"] = float(m.group(2))
+d["source"] = f"rocprofv3 --pmc passes, gpurun_out/{tag}"
+json.dump(d, open(os.path.join(out, "pmc_merged.json"), "w"), indent=1)
+print(json.dumps(d)[:300])
+PY
