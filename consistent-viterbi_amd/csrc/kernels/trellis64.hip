@@ -192,8 +192,9 @@ struct SimdBalance {
 // debug build only: per wave {real-time start, end, s_memtime start, end, HW_ID, XCC_ID}
 __device__ uint64_t g_t64_probe[1 << 17][6];
 #endif
-template <int C, int S, int PF, bool DPA, bool EXT, int W = 1, bool CAP2 = (W > 1), int GRP = 2>
-__global__ __launch_bounds__(64 * W) void trellis_fwd_f64(T64FwdArgs g) {
+// MINW: waves per SIMD the register allocation must allow (3: <= 168 VGPRs)
+template <int C, int S, int PF, bool DPA, bool EXT, int W = 1, bool CAP2 = (W > 1), int GRP = 2, int MINW = 1>
+__global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(MINW))) void trellis_fwd_f64(T64FwdArgs g) {
 #ifdef CV_T64_PROBE
   const uint64_t pr_rt0 = __builtin_amdgcn_s_memrealtime(), pr_c0 = __builtin_amdgcn_s_memtime();
   struct ProbeEnd {
@@ -1016,6 +1017,14 @@ hipError_t fwd_cs(const T64FwdArgs& fa, int64_t nseq, hipStream_t stream) {
   }();
   const bool ext = fa.forced || fa.ranges || fa.reverse || fa.start || fa.row_base || fa.resume_rows ||
                    fa.slot_order || fa.last_row;
+  // S = 6: three waves per SIMD (<= 168 VGPRs, 12.3 KiB of LDS each), batch decode only
+  if constexpr (S == 6) {
+    if (ext || fa.dp_assoc) return fwd_cs<C, 4>(fa, nseq, stream);
+    // 4 A rows in flight: 157 VGPRs (8 rows spill at 168)
+    hipLaunchKernelGGL((trellis_fwd_f64<C, 6, 4, false, false, 1, false, 2, 3>), dim3((unsigned)blocks), dim3(64), 0,
+                       stream, fa);
+    return hipGetLastError();
+  } else {
   // N = 256 and fewer than 8 sequences per wave (small batch): 2S sequences over two waves --
   // the same number of waves, twice the A-row reuse
   if constexpr (C == 4 && S <= 4) {
@@ -1036,6 +1045,7 @@ hipError_t fwd_cs(const T64FwdArgs& fa, int64_t nseq, hipStream_t stream) {
     hipLaunchKernelGGL((trellis_fwd_f64<C, S, 8, false, false>), grid, block, 0, stream, fa);
   }
   return hipGetLastError();
+  }
 }
 
 
@@ -1170,6 +1180,7 @@ hipError_t fwd_c(const T64FwdArgs& fa, int s, int64_t nseq, hipStream_t stream) 
   switch (s) {
     case 2: return fwd_cs<C, 2>(fa, nseq, stream);
     case 4: return fwd_cs<C, 4>(fa, nseq, stream);
+    case 6: return fwd_cs<C, 6>(fa, nseq, stream);
     case 8: return fwd_cs<C, 8>(fa, nseq, stream);
     default: return hipErrorInvalidValue;
   }
@@ -1214,7 +1225,7 @@ int t64_seqs_per_wave(int64_t nseq, int cus) {
   // streamed from L2 serves S sequences
   if (const char* e = getenv("CV_T64_S")) {  // tuning knob (bit-identical for every value)
     const int s = atoi(e);
-    if (s == 2 || s == 4 || s == 8) return s;
+    if (s == 2 || s == 4 || s == 6 || s == 8) return s;
   }
   const int64_t simd_waves = 2 * 4 * (int64_t)(cus > 0 ? cus : 256);
   if (nseq >= 8 * simd_waves) return 8;

@@ -135,6 +135,32 @@ def test_t64_simd_balance_knob_bit_identical(gpu, tmp_path):
 
 @pytest.mark.parametrize("n", [64, 200, 256])
 @pytest.mark.parametrize("kind", ["near_ties", "positive", "huge"])
+@pytest.mark.parametrize("n", [256, 200, 128])
+def test_t64_layout_knob_s6_bit_identical(gpu, tmp_path, n):
+    """The 3-waves-per-SIMD layout (6 sequences per wave, CV_T64_S=6) is scheduling only: a
+    child process decodes the same ragged batch to the same bits as the default layout."""
+    import subprocess
+    import sys
+
+    pi, a, b = synth.random_hmm(n, 64, seed=80 + n)
+    rng = np.random.default_rng(80 + n)
+    off = synth.offsets_from_lengths(rng.integers(1, 97, size=6000))
+    obs = rng.integers(0, 64, size=int(off[-1])).astype(np.int32)
+    np.savez(tmp_path / "in.npz", pi=pi, a=a, b=b, off=off, obs=obs)
+    got = cv.decode_batch(cv.HMM(pi, a, b), off, obs, dtype="f64", rescore_f64=False)
+    code = (
+        "import sys, numpy as np; sys.path.insert(0, sys.argv[1]); import cviterbi as cv; "
+        "d = np.load(sys.argv[2]); h = cv.HMM(d['pi'], d['a'], d['b']); "
+        "p, s, st = cv.decode_batch(h, d['off'], d['obs'], dtype='f64', rescore_f64=False); "
+        "assert cv.last_timing(h)['seqs_per_wave'] == 6; "
+        "np.savez(sys.argv[3], p=p, s=s, st=st)")
+    env = dict(os.environ, CV_T64_S="6")
+    subprocess.run([sys.executable, "-c", code, PKG, str(tmp_path / "in.npz"), str(tmp_path / "out.npz")],
+                   env=env, check=True, timeout=120)
+    ref = np.load(tmp_path / "out.npz")
+    _assert_same(got, (ref["p"], ref["s"], ref["st"]), f"S=6 layout N={n}")
+
+
 def test_t64_backtrack_interval_paths(gpu, n, kind):
     """The backtrack's two interval tests (trellis64.hip bt_chain_f64).  near_ties: a log-prob
     model whose transitions differ below f32 resolution (1e-12 perturbations of a quantised

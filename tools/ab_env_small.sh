@@ -14,7 +14,7 @@ fi
 for r in $(seq 1 ${ROUNDS:-2}); do
   for B in ${BATCHES:-8192 16384}; do
     for v in $AB; do
-      env $v timeout -k 10 ${T_BENCH:-200} python bench.py --batch $B --steps ${STEPS:-10} --warmup 2 --no-cpu-baseline --no-f32-extra > $OUT/$v.$B.$r.log 2>&1 || { echo "FAIL $v $B"; tail -5 $OUT/$v.$B.$r.log; exit 1; }
+      env $v timeout -k 10 ${T_BENCH:-200} python bench.py --batch $B --steps ${STEPS:-10} --warmup 2 --no-cpu-baseline --no-f32-extra --no-configs > $OUT/$v.$B.$r.log 2>&1 || { echo "FAIL $v $B"; tail -5 $OUT/$v.$B.$r.log; exit 1; }
       python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[2], sys.argv[3], sys.argv[4], round(d['ms_per_step'],3), 'fwd', round(d['kernel_ms_per_step']['forward'],3), 'bt', round(d['kernel_ms_per_step']['backtrack_rescore'],3))" $OUT/$v.$B.$r.log $B $v $r | tee -a $OUT/summary.txt
     done
   done
