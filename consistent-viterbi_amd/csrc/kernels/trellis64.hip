@@ -193,7 +193,8 @@ struct SimdBalance {
 __device__ uint64_t g_t64_probe[1 << 17][6];
 #endif
 // MINW: waves per SIMD the register allocation must allow (3: <= 168 VGPRs)
-template <int C, int S, int PF, bool DPA, bool EXT, int W = 1, bool CAP2 = (W > 1), int GRP = 2, int MINW = 1>
+template <int C, int S, int PF, bool DPA, bool EXT, int W = 1, bool CAP2 = (W > 1), int GRP = 2, int MINW = 1,
+          bool LDSFIRST = true>
 __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(MINW))) void trellis_fwd_f64(T64FwdArgs g) {
 #ifdef CV_T64_PROBE
   const uint64_t pr_rt0 = __builtin_amdgcn_s_memrealtime(), pr_c0 = __builtin_amdgcn_s_memtime();
@@ -306,7 +307,11 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(MINW))) 
     load_a<C>(row, e);
   };
   auto store_row = [&](int s, int t, const double (&v)[C]) {
+#ifdef CVK_ABL_NOSTORE  // ablation build (timing only): no delta-row stores
+    if (false) {
+#else
     if (g.delta && t < T[s]) {
+#endif
       // split-plane row (see T64 row layout in trellis64.h): hi words [0, NP), lo words
       // [NP, 2 NP); streaming stores (read once, by the backtrack)
       const int64_t r = (int64_t)((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)my_rb, s) |
@@ -410,9 +415,19 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(MINW))) 
         const int i = i0 + u;
         {
           const f64x2* nrow = reinterpret_cast<const f64x2*>(dl + (i + DV - 1) * S);
+#ifndef CVK_ABL_NOLDS  // ablation build (timing only): delta rows never re-read from LDS
 #pragma unroll
           for (int s2 = 0; s2 < S / 2; ++s2) dv[(u + DV - 1) % DV][s2] = nrow[s2];
+#else
+          (void)nrow;
+#pragma unroll
+          for (int s2 = 0; s2 < S / 2; ++s2) asm volatile("" : "+v"(dv[(u + DV - 1) % DV][s2].x), "+v"(dv[(u + DV - 1) % DV][s2].y));
+#endif
         }
+        // the broadcast reads of row i + DV - 1 issue BEFORE row i's adds (left alone, the
+        // scheduler sank them to just before their use: ~16 maxima of cover for an LDS round
+        // trip); nothing crosses this barrier
+        if constexpr (DV > 1 && LDSFIRST) __builtin_amdgcn_sched_barrier(0);
         // the candidates of G sequence pairs are added before their maxima are taken, so each
         // v_max_f64 issues ~2*C*G instructions after the v_add_f64 it reads (adjacent dependent
         // f64 ops cost issue slots: profiles/r02_ab_fwd_group.txt)
@@ -448,7 +463,13 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(MINW))) 
         // step's first rows -- only after its last use, into the same registers: no copies,
         // and the in-flight loads cross the loop back-edge without a vmcnt(0) drain
         const int nr = i + PF < NP ? i + PF : i + PF - NP;
+#ifndef CVK_ABL_NOLOAD  // ablation build (timing only): the A-row ring is never refilled
         load_row_buf<C>(ra, voff, (uint32_t)nr * RB, ar[u]);
+#else
+        (void)nr;
+#pragma unroll
+        for (int c = 0; c < C; ++c) asm volatile("" : "+v"(ar[u][c]));
+#endif
       }
     }
     // W = 1: LDS operations of the wave execute in order, so the reads of delta_{t-1} above
@@ -997,8 +1018,14 @@ __global__ void resume_rows_f64(const double* last, const int32_t* state, int np
 template <int S>
 hipError_t fwd_w2(const T64FwdArgs& fa, int64_t nseq, bool ext, hipStream_t stream) {
   const dim3 grid((unsigned)((nseq + S - 1) / S)), block(128);
+  static const bool ldsfirst = [] {  // A/B knob (bit-identical), as in fwd_cs
+    const char* e = getenv("CV_T64_LDSFIRST");
+    return !(e && e[0] == '0');
+  }();
   if (ext)
     hipLaunchKernelGGL((trellis_fwd_f64<2, S, 8, false, true, 2>), grid, block, 0, stream, fa);
+  else if (!ldsfirst)
+    hipLaunchKernelGGL((trellis_fwd_f64<2, S, 8, false, false, 2, true, 2, 1, false>), grid, block, 0, stream, fa);
   else
     hipLaunchKernelGGL((trellis_fwd_f64<2, S, 8, false, false, 2>), grid, block, 0, stream, fa);
   return hipGetLastError();
@@ -1010,6 +1037,10 @@ hipError_t fwd_cs(const T64FwdArgs& fa, int64_t nseq, hipStream_t stream) {
   static const int pf = [] {  // tuning knob (bit-identical): A rows in flight, 8 (default) or 4
     const char* e = getenv("CV_T64_PF");
     return e ? atoi(e) : 8;
+  }();
+  static const bool ldsfirst = [] {  // A/B knob (bit-identical): CV_T64_LDSFIRST=0, compiler-placed delta reads
+    const char* e = getenv("CV_T64_LDSFIRST");
+    return !(e && e[0] == '0');
   }();
   static const bool w2 = [] {  // A/B knob (bit-identical): CV_T64_W2=0 keeps one wave per group
     const char* e = getenv("CV_T64_W2");
@@ -1041,6 +1072,8 @@ hipError_t fwd_cs(const T64FwdArgs& fa, int64_t nseq, hipStream_t stream) {
     hipLaunchKernelGGL((trellis_fwd_f64<C, S, 8, false, true>), grid, block, 0, stream, fa);
   } else if (pf == 4) {
     hipLaunchKernelGGL((trellis_fwd_f64<C, S, 4, false, false>), grid, block, 0, stream, fa);
+  } else if (!ldsfirst) {
+    hipLaunchKernelGGL((trellis_fwd_f64<C, S, 8, false, false, 1, false, 2, 1, false>), grid, block, 0, stream, fa);
   } else {
     hipLaunchKernelGGL((trellis_fwd_f64<C, S, 8, false, false>), grid, block, 0, stream, fa);
   }
