@@ -133,8 +133,6 @@ def test_t64_simd_balance_knob_bit_identical(gpu, tmp_path):
     _assert_same(got, (ref["p"], ref["s"], ref["st"]), "balance/W2 knobs")
 
 
-@pytest.mark.parametrize("n", [64, 200, 256])
-@pytest.mark.parametrize("kind", ["near_ties", "positive", "huge"])
 @pytest.mark.parametrize("n", [256, 200, 128])
 def test_t64_layout_knob_s6_bit_identical(gpu, tmp_path, n):
     """The 3-waves-per-SIMD layout (6 sequences per wave, CV_T64_S=6) is scheduling only: a
@@ -161,6 +159,8 @@ def test_t64_layout_knob_s6_bit_identical(gpu, tmp_path, n):
     _assert_same(got, (ref["p"], ref["s"], ref["st"]), f"S=6 layout N={n}")
 
 
+@pytest.mark.parametrize("n", [64, 200, 256])
+@pytest.mark.parametrize("kind", ["near_ties", "positive", "huge"])
 def test_t64_backtrack_interval_paths(gpu, n, kind):
     """The backtrack's two interval tests (trellis64.hip bt_chain_f64).  near_ties: a log-prob
     model whose transitions differ below f32 resolution (1e-12 perturbations of a quantised
