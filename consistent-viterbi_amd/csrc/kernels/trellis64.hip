@@ -193,15 +193,22 @@ struct SimdBalance {
 __device__ uint64_t g_t64_probe[1 << 17][6];
 #endif
 // MINW: waves per SIMD the register allocation must allow (3: <= 168 VGPRs)
+// WG: independent units per workgroup, each of W waves with its own S sequences and LDS slice
+// (W * WG = 8: the CU's whole complement, two waves per SIMD).  SYNC bit 1: a workgroup barrier
+// per step; bit 2: the two waves of a SIMD (waves i and i ^ 4 of the workgroup) trade issue
+// priority every PF rows so that the one behind leads.  Together they keep the CU's waves on
+// the same A rows, so 8 waves share each row through the L1 (L1 -> L2 read requests per L1
+// access 0.44 -> 0.09 at config 4; profiles/r03_ab_wg.txt).  W > 1 units meet at workgroup
+// barriers anyway (their pair rendezvous), so they take bit 2 only.
 template <int C, int S, int PF, bool DPA, bool EXT, int W = 1, bool CAP2 = (W > 1), int GRP = 2, int MINW = 1,
-          bool LDSFIRST = true>
-__global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(MINW))) void trellis_fwd_f64(T64FwdArgs g) {
+          bool LDSFIRST = true, int WG = 1, int SYNC = 0>
+__global__ __launch_bounds__(64 * W * WG) __attribute__((amdgpu_waves_per_eu(MINW))) void trellis_fwd_f64(T64FwdArgs g) {
 #ifdef CV_T64_PROBE
   const uint64_t pr_rt0 = __builtin_amdgcn_s_memrealtime(), pr_c0 = __builtin_amdgcn_s_memtime();
   struct ProbeEnd {
     uint64_t rt0, c0;
     __device__ ~ProbeEnd() {
-      const unsigned idx = (blockIdx.x * W + (threadIdx.x >> 6)) & ((1u << 17) - 1);
+      const unsigned idx = (blockIdx.x * W * WG + (threadIdx.x >> 6)) & ((1u << 17) - 1);
       if ((threadIdx.x & 63) == 0) {
         uint64_t* p = g_t64_probe[idx];
         p[0] = rt0;
@@ -222,15 +229,24 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(MINW))) 
   constexpr int DV = W > 1 ? 4 : 2;
   static_assert(PF % DV == 0, "the delta-row ring must wrap with the A-row ring");
   // delta_{t-1}: [row][S]; rows NP .. NP+DV-2 are padding, read (and ignored) by the prefetch
-  __shared__ __attribute__((aligned(16))) double dl[(NP + DV - 1) * S];
+  static_assert(WG == 1 || W * WG == 8, "units per workgroup: the CU's eight waves");
+  __shared__ __attribute__((aligned(16))) double dl_all[WG][(NP + DV - 1) * S];
+  __shared__ int wg_prog[W * WG];  // each wave's Tmax, then its progress (step * NP + row block)
   const int lane = threadIdx.x & 63;
-  const int wv = W > 1 ? __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6) : 0;
+  const int wid = (W * WG > 1) ? __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6) : 0;
+  const int wv = W > 1 ? wid % W : 0;
+  const int wgi = WG > 1 ? wid / W : 0;
+  double* const dl = dl_all[wgi];
   const int j0 = (wv * 64 + lane) * C;
   const double ninf = ninf_d();
   // workgroup rendezvous without the global-memory drain of __syncthreads (the A-row ring and
   // the delta stores stay in flight): only this wave's LDS operations are waited for
   auto wg_sync = [&]() {
+#ifndef CVK_ABL_NOBAR  // ablation build (timing only): no pair rendezvous
     if constexpr (W > 1) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#else
+    if constexpr (W > 1) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#endif
   };
   // W > 1 runs single-round small batches: reserve > 170 VGPRs so a SIMD holds at most two of
   // these waves and every SIMD gets two (at ~150 VGPRs three fit, and a round that puts three
@@ -242,7 +258,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(MINW))) 
   // loads the observation (and forced state) of sequence s one step ahead, and the values a
   // step needs uniformly are read back with v_readlane.
   const int ls = lane < S ? lane : S - 1;
-  const int64_t my_k = (int64_t)blockIdx.x * S + ls;
+  const int64_t my_k = ((int64_t)blockIdx.x * WG + wgi) * S + ls;
   int my_T = 0;
   int64_t my_seq = -1, my_eb = 0, my_rb = 0;
   if (my_k < g.nslots && lane < S) {
@@ -268,7 +284,33 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(MINW))) 
     T[s] = __builtin_amdgcn_readlane(my_T, s);
     Tmax = T[s] > Tmax ? T[s] : Tmax;
   }
-  if (Tmax <= 0) return;
+  // Barriers are workgroup-wide once a workgroup holds several units: every wave then takes
+  // part in the workgroup's barriers up to the longest unit's last step (a wave with less work
+  // idles at them), so no barrier waits on a finished wave
+  constexpr bool kWgBar = WG > 1 && ((SYNC & 1) || W > 1);
+  // barriers per step: the pair rendezvous (W > 1: 2) or the step barrier (SYNC & 1)
+  constexpr int kStepBarriers = W > 1 ? 2 : ((SYNC & 1) ? 1 : 0);
+  int Twg = Tmax;
+  if constexpr (kWgBar) {
+    if (lane == 0) wg_prog[wid] = Tmax;
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < W * WG; ++k) Twg = max(Twg, wg_prog[k]);
+    __syncthreads();
+  }
+  if constexpr (WG > 1 && (SYNC & 2)) {
+    if (lane == 0) wg_prog[wid] = 0;
+  }
+  if (Tmax <= 0) {
+    if constexpr (kWgBar) {
+      if (Twg > 0) {
+        if constexpr (W > 1) asm volatile("s_barrier" ::: "memory");  // delta_0's rendezvous
+        for (int t = 1; t < Twg; ++t)
+          for (int k = 0; k < kStepBarriers; ++k) asm volatile("s_barrier" ::: "memory");
+      }
+    }
+    return;
+  }
   const int dir = (EXT && g.reverse) ? -1 : 1;
   const unsigned V = (unsigned)g.nobs;
   // lanes without a sequence read the first element of some sequence of the wave, so every
@@ -316,7 +358,11 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(MINW))) 
       // [NP, 2 NP); streaming stores (read once, by the backtrack)
       const int64_t r = (int64_t)((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)my_rb, s) |
                                   ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(my_rb >> 32), s) << 32));
+#ifndef CVK_ABL_STORE_L2
       uint32_t* dst = reinterpret_cast<uint32_t*>(g.delta) + (r + t) * (2 * NP) + j0;
+#else  // ablation build (timing only): every step of a sequence overwrites its first row (L2-resident)
+      uint32_t* dst = reinterpret_cast<uint32_t*>(g.delta) + r * (2 * NP) + j0;
+#endif
       store_split<C>(dst, dst + NP, v);
     }
     if (EXT && g.last_row && t == T[s] - 1) {
@@ -462,7 +508,11 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(MINW))) 
         // refill this ring slot with row (i + PF) mod NP -- the wrap-around rows are the next
         // step's first rows -- only after its last use, into the same registers: no copies,
         // and the in-flight loads cross the loop back-edge without a vmcnt(0) drain
+#ifndef CVK_ABL_LOADHOT
         const int nr = i + PF < NP ? i + PF : i + PF - NP;
+#else  // ablation build (timing only): the ring reloads rows 0 .. PF-1 only (L1/L2-hot, same addresses in every wave)
+        const int nr = u;
+#endif
 #ifndef CVK_ABL_NOLOAD  // ablation build (timing only): the A-row ring is never refilled
         load_row_buf<C>(ra, voff, (uint32_t)nr * RB, ar[u]);
 #else
@@ -470,6 +520,24 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(MINW))) 
 #pragma unroll
         for (int c = 0; c < C; ++c) asm volatile("" : "+v"(ar[u][c]));
 #endif
+      }
+      if constexpr (WG > 1 && (SYNC & 2)) {
+        // the wave behind its SIMD partner (or level with it) takes the higher priority; the
+        // partner's word is at most a block old (LDS, no barrier: a stale word only mis-sets a
+        // priority).  No C++ branch here (a divergent or scalar branch split the unrolled loop
+        // body and the ring registers spilled): every lane writes the same word, and the
+        // compare and branch are one asm block.
+        const int me = t * NP + i0;
+        wg_prog[wid] = me;
+        const int other = __builtin_amdgcn_readfirstlane(wg_prog[wid ^ 4]);
+        asm volatile(
+            "s_cmp_le_i32 %0, %1\n\t"
+            "s_cbranch_scc0 1f\n\t"
+            "s_setprio 3\n\t"
+            "s_branch 2f\n"
+            "1:\n\t"
+            "s_setprio 2\n"
+            "2:" ::"s"(me), "s"(other) : "scc");
       }
     }
     // W = 1: LDS operations of the wave execute in order, so the reads of delta_{t-1} above
@@ -517,7 +585,11 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(MINW))) 
     asm volatile("" ::: "memory");
     wg_sync();  // delta_t complete in LDS before the next step reads it
     if (bal_step) sb.decide(other, Tmax - t);
+    if constexpr (WG > 1 && W == 1 && (SYNC & 1)) asm volatile("s_barrier" ::: "memory");
   }
+  if constexpr (kWgBar)
+    for (int t = Tmax; t < Twg; ++t)
+      for (int k = 0; k < kStepBarriers; ++k) asm volatile("s_barrier" ::: "memory");
   sb.finish(lane);
   if (wv == 0 && lane < S && my_bad) g.status[my_seq] = CVK_SEQ_BADOBS;
 }
@@ -1022,9 +1094,19 @@ hipError_t fwd_w2(const T64FwdArgs& fa, int64_t nseq, bool ext, hipStream_t stre
     const char* e = getenv("CV_T64_LDSFIRST");
     return !(e && e[0] == '0');
   }();
+  static const int wg_mode = [] {  // A/B knob (bit-identical), as in fwd_cs: 0 = one pair per workgroup
+    const char* e = getenv("CV_T64_WG");
+    return e ? atoi(e) : 4;
+  }();
   if (ext)
     hipLaunchKernelGGL((trellis_fwd_f64<2, S, 8, false, true, 2>), grid, block, 0, stream, fa);
-  else if (!ldsfirst)
+  else if (wg_mode > 0) {
+    // four pairs per workgroup (the CU's eight waves), SIMD partners trade priority
+    T64FwdArgs f4 = fa;
+    f4.balance = 0;
+    hipLaunchKernelGGL((trellis_fwd_f64<2, S, 8, false, false, 2, true, 2, 1, true, 4, 2>),
+                       dim3((unsigned)((nseq + 4 * S - 1) / (4 * S))), dim3(512), 0, stream, f4);
+  } else if (!ldsfirst)
     hipLaunchKernelGGL((trellis_fwd_f64<2, S, 8, false, false, 2, true, 2, 1, false>), grid, block, 0, stream, fa);
   else
     hipLaunchKernelGGL((trellis_fwd_f64<2, S, 8, false, false, 2>), grid, block, 0, stream, fa);
@@ -1041,6 +1123,14 @@ hipError_t fwd_cs(const T64FwdArgs& fa, int64_t nseq, hipStream_t stream) {
   static const bool ldsfirst = [] {  // A/B knob (bit-identical): CV_T64_LDSFIRST=0, compiler-placed delta reads
     const char* e = getenv("CV_T64_LDSFIRST");
     return !(e && e[0] == '0');
+  }();
+  // A/B knob (bit-identical): CV_T64_WG = 1 + SYNC bits (1: barrier per step, 2: SIMD-pair
+  // priority trade) runs the batch decode as eight independent waves per workgroup; default 4
+  // (both), 0 = one wave per workgroup with the global SIMD balancing (round-2 layout).  Config
+  // 4 forward 136.4 -> 131.4 ms, 8,192 sequences 18.6 -> 17.7 ms (profiles/r03_ab_wg.txt)
+  static const int wg_mode = [] {
+    const char* e = getenv("CV_T64_WG");
+    return e ? atoi(e) : 4;
   }();
   static const bool w2 = [] {  // A/B knob (bit-identical): CV_T64_W2=0 keeps one wave per group
     const char* e = getenv("CV_T64_W2");
@@ -1062,6 +1152,31 @@ hipError_t fwd_cs(const T64FwdArgs& fa, int64_t nseq, hipStream_t stream) {
     if (w2 && !fa.dp_assoc) return fwd_w2<2 * S>(fa, nseq, ext, stream);
   }
   const dim3 grid((unsigned)blocks), block(64);
+  // C >= 3 only: at C <= 2 the one-wave workgroups fit three or more waves per SIMD, which beat
+  // two aligned ones (N = 128: 37.7 vs 38.1 ms; N = 192: 84.4 -> 81.1 ms; profiles/r03_ab_wg.txt)
+  if constexpr (S == 8 && C >= 3) {
+    static const bool wg_ext = [] {  // A/B knob (bit-identical): CV_T64_WG_EXT=1, the constrained passes too
+      const char* e = getenv("CV_T64_WG_EXT");
+      return e && e[0] == '1';
+    }();
+    if (wg_mode > 0 && !fa.dp_assoc && (!ext || wg_ext)) {
+      // eight independent waves per workgroup (two per SIMD), A-row reads kept together
+      const dim3 g8((unsigned)((nseq + 8 * S - 1) / (8 * S))), b8(512);
+      T64FwdArgs f8 = fa;
+      f8.balance = 0;
+      if (ext) {
+        hipLaunchKernelGGL((trellis_fwd_f64<C, S, 8, false, true, 1, false, 2, 1, true, 8, 3>), g8, b8, 0, stream, f8);
+        return hipGetLastError();
+      }
+      switch (wg_mode - 1) {
+        case 1: hipLaunchKernelGGL((trellis_fwd_f64<C, S, 8, false, false, 1, false, 2, 1, true, 8, 1>), g8, b8, 0, stream, f8); break;
+        case 2: hipLaunchKernelGGL((trellis_fwd_f64<C, S, 8, false, false, 1, false, 2, 1, true, 8, 2>), g8, b8, 0, stream, f8); break;
+        case 3: hipLaunchKernelGGL((trellis_fwd_f64<C, S, 8, false, false, 1, false, 2, 1, true, 8, 3>), g8, b8, 0, stream, f8); break;
+        default: hipLaunchKernelGGL((trellis_fwd_f64<C, S, 8, false, false, 1, false, 2, 1, true, 8, 0>), g8, b8, 0, stream, f8); break;
+      }
+      return hipGetLastError();
+    }
+  }
   if (fa.dp_assoc) {
     if (ext) return hipErrorInvalidValue;
     if constexpr (S <= 4)

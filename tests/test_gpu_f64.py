@@ -159,6 +159,40 @@ def test_t64_layout_knob_s6_bit_identical(gpu, tmp_path, n):
     _assert_same(got, (ref["p"], ref["s"], ref["st"]), f"S=6 layout N={n}")
 
 
+@pytest.mark.parametrize("n,s", [(256, 8), (200, 8), (192, 8), (256, 4)])
+def test_t64_workgroup_units_bit_identical(gpu, tmp_path, n, s):
+    """Eight waves per workgroup (S = 8: eight one-wave units, a barrier per step and the SIMD
+    pairs' priority trade; S = 4 at N = 256: four pairs of waves) are scheduling only.  Ragged
+    lengths 1..96 (units of one workgroup finish at different steps: the trailing barriers) and
+    a batch that leaves the last workgroup partly empty: child processes with CV_T64_WG=0 (one
+    unit per workgroup) and the default decode the same bits as this process's default
+    layout."""
+    import subprocess
+    import sys
+
+    pi, a, b = synth.random_hmm(n, 64, seed=90 + n)
+    rng = np.random.default_rng(90 + n + s)
+    lengths = rng.integers(1, 97, size=5000)
+    lengths[rng.integers(0, 5000, size=40)] = 0  # empty sequences inside workgroups
+    off = synth.offsets_from_lengths(lengths)
+    obs = rng.integers(0, 64, size=int(off[-1])).astype(np.int32)
+    np.savez(tmp_path / "in.npz", pi=pi, a=a, b=b, off=off, obs=obs)
+    got = cv.decode_batch(cv.HMM(pi, a, b), off, obs, dtype="f64", rescore_f64=False)
+    code = (
+        "import sys, numpy as np; sys.path.insert(0, sys.argv[1]); import cviterbi as cv; "
+        "d = np.load(sys.argv[2]); h = cv.HMM(d['pi'], d['a'], d['b']); "
+        "p, s, st = cv.decode_batch(h, d['off'], d['obs'], dtype='f64', rescore_f64=False); "
+        f"assert cv.last_timing(h)['seqs_per_wave'] == {s}; "
+        "np.savez(sys.argv[3], p=p, s=s, st=st)")
+    for wg in ("4", "0"):
+        env = dict(os.environ, CV_T64_S=str(s), CV_T64_WG=wg)
+        out = tmp_path / f"out{wg}.npz"
+        subprocess.run([sys.executable, "-c", code, PKG, str(tmp_path / "in.npz"), str(out)],
+                       env=env, check=True, timeout=120)
+        ref = np.load(out)
+        _assert_same(got, (ref["p"], ref["s"], ref["st"]), f"CV_T64_WG={wg} S={s} N={n}")
+
+
 @pytest.mark.parametrize("n", [64, 200, 256])
 @pytest.mark.parametrize("kind", ["near_ties", "positive", "huge"])
 def test_t64_backtrack_interval_paths(gpu, n, kind):

@@ -1,7 +1,8 @@
 """Config-4 shape decode time per reference-solver association in f64 (SURVEY.md §8a A0
 notes): viterbi (row A0: trellis_fwd_f64), cp (CPSolver cp.rs:70-79), dp (DPSolver
 dp.rs:127-177), decode (viterbi.rs:5-32).  NSEQ sequences of T=512 (default 8,192), device
-API, one JSON line per association."""
+API, one JSON line per association (sha16: digest of paths, scores and statuses: knobs
+that must be bit-identical print the same digest)."""
 import json
 import os
 import sys
@@ -16,6 +17,9 @@ from cviterbi import synth  # noqa: E402
 
 nseq = int(os.environ.get("NSEQ", "8192"))
 c = synth.config("c4", nseq)
+if os.environ.get("NSTATES"):  # config-4 shape with another state count (T = 512, V = 1,024)
+    ns = int(os.environ["NSTATES"])
+    c["pi"], c["a"], c["b"] = synth.random_hmm(ns, 1024, seed=20261015)
 off, obs = c["offsets"], c["obs"]
 B = len(off) - 1
 dev = torch.device("cuda:0")
@@ -37,5 +41,9 @@ for assoc in sys.argv[1:] or ["viterbi", "cp", "dp", "decode"]:
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     t = cv.last_timing(h)
-    print(json.dumps({"assoc": assoc, "nseq": B, "ms": dt * 1e3, "cells_per_s": B * 512 * 256 / dt,
-                      "kernel": t["kernel"], "fwd_ms": t["fwd_ms"], "bt_ms": t["bt_ms"]}), flush=True)
+    import hashlib
+    digest = hashlib.sha256(p_d.cpu().numpy().tobytes() + s_d.cpu().numpy().tobytes() +
+                            st_d.cpu().numpy().tobytes()).hexdigest()[:16]
+    print(json.dumps({"assoc": assoc, "nseq": B, "states": int(c["pi"].shape[0]), "ms": dt * 1e3,
+                      "cells_per_s": B * 512 * int(c["pi"].shape[0]) / dt,
+                      "kernel": t["kernel"], "fwd_ms": t["fwd_ms"], "bt_ms": t["bt_ms"], "sha16": digest}), flush=True)
