@@ -1319,7 +1319,9 @@ cv_status constrained_partials_locked(cv_hmm* h, int64_t nseq, const int64_t* of
     const ConSeq& c = *order[i];
     rg[2 * i] = offsets[c.seq];
     rg[2 * i + 1] = c.elems.front() + 1;
-    rg[2 * nc + 2 * i] = c.elems.back() + 1;
+    // f64: the suffix range starts AT t_m (one extra max-plus step without emission, the
+    // kernel's noemit_last): its last row is beta_{t_m} itself; f32: after t_m (max_marginal)
+    rg[2 * nc + 2 * i] = c.elems.back() + (o.dtype == CV_DTYPE_F64 ? 0 : 1);
     rg[2 * nc + 2 * i + 1] = offsets[c.seq + 1];
   }
   const int64_t nslot_max = std::max<int64_t>(nc, std::min<int64_t>(kSegmentSlots, (int64_t)seg_pair.size() * N));
@@ -1454,28 +1456,21 @@ cv_status constrained_partials_locked(cv_hmm* h, int64_t nseq, const int64_t* of
       fb.pi = h->q_pi0.as<double>();
       fb.ranges = h->cs_ranges.as<int64_t>() + 2 * nc;
       fb.reverse = 1;
-      fb.last_row = h->cs_g.as<double>();
+      fb.noemit_last = 1;
+      fb.last_row = h->cs_g.as<double>();  // beta_{t_m}
       fb.delta = nullptr;
       fb.row_base = nullptr;
       fb.slot_order = h->ws_order.as<int32_t>() + nc;
       err = cvk::launch_t64_fwd(np, cvk::t64_seqs_per_wave(nc, h->cus), fb, nc, stream);
     }
-    cvk::MaxMarginal64Args ma{};
-    ma.g = h->cs_g.as<double>();
-    ma.ranges_suffix = h->cs_ranges.as<int64_t>() + 2 * nc;
-    ma.at = h->q_at.as<double>();
-    ma.mu = h->cs_mu.as<double>();
-    if (err == hipSuccess) {  // m == 1: mu = delta + beta
-      ma.delta = h->cs_delta.as<double>();
-      err = cvk::launch_t64_max_marginal(np, ma, n1, stream);
-    }
-    if (err == hipSuccess && nc > n1) {  // m >= 2: beta alone (0 + beta is exact)
-      ma.delta = h->cs_zero.as<double>();
-      ma.g += n1 * np;
-      ma.ranges_suffix += 2 * n1;
-      ma.mu += n1 * np;
-      err = cvk::launch_t64_max_marginal(np, ma, nc - n1, stream);
-    }
+    // m == 1: mu = delta + beta (elementwise); m >= 2: the term is beta itself (0 + beta is
+    // exact), copied into place
+    if (err == hipSuccess)
+      err = cvk::launch_t64_mu_add(h->cs_delta.as<double>(), h->cs_g.as<double>(), h->cs_mu.as<double>(), n1, np,
+                                   stream);
+    if (err == hipSuccess && nc > n1)
+      err = hipMemcpyAsync(h->cs_mu.as<double>() + n1 * np, h->cs_g.as<double>() + n1 * np,
+                           (size_t)(nc - n1) * np * 8, hipMemcpyDeviceToDevice, stream);
   }
   if (err != hipSuccess) return set_err(CV_EDEVICE, "term launches failed: %s", hipGetErrorString(err));
   trace_mark("term launches enqueued");

@@ -6,7 +6,7 @@
 
 namespace cvx {
 
-constexpr int kUnarySumMaxComp = 15;  // LDS: ncomp x 5 x 256 x 8 B <= 150 KiB
+constexpr int kUnarySumMaxComp = 15;  // components summed on the device (one launch per kUnarySumGroup)
 
 struct UnarySumArgs {
   const void* mu;     // [nc][np] suffix max-marginal rows (float, or double when f64)
@@ -19,7 +19,9 @@ struct UnarySumArgs {
   int64_t uw;         // int64 words per component (5N + 1)
   long long* part;    // [ncomp][uw], accumulated into
   unsigned* bad;      // set to nonzero when a term is outside the exact unit's range
+  int cbase, cgroup;  // set by launch_unary_sums: one launch per kUnarySumGroup components
 };
+constexpr int kUnarySumGroup = 2;
 
 hipError_t launch_unary_sums(const UnarySumArgs& g, int nblocks, hipStream_t stream);
 

@@ -12,6 +12,8 @@
 #include <math.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "../exact_fixed.h"
 #include "exact.h"
 
@@ -19,9 +21,9 @@ namespace cvx {
 
 template <typename REAL>
 __global__ __launch_bounds__(256) void unary_sums(UnarySumArgs g) {
-  extern __shared__ long long acc[];  // [ncomp][5][256]: 4 limbs + the -inf count, state-minor
+  extern __shared__ long long acc[];  // [cgroup][5][256]: 4 limbs + the -inf count, state-minor
   const int s = threadIdx.x;
-  const int ncomp = g.ncomp;
+  const int ncomp = g.cgroup;  // this launch's components [cbase, cbase + cgroup)
   for (int q = 0; q < ncomp * 5; ++q) acc[q * 256 + s] = 0;
   const int64_t per = (g.nc + gridDim.x - 1) / gridDim.x;
   const int64_t i0 = (int64_t)blockIdx.x * per, i1 = min(g.nc, i0 + per);
@@ -29,6 +31,8 @@ __global__ __launch_bounds__(256) void unary_sums(UnarySumArgs g) {
   const REAL* dl = static_cast<const REAL*>(g.dl);
   bool bad = false;
   auto add = [&](int c, REAL x) {
+    c -= g.cbase;
+    if ((unsigned)c >= (unsigned)ncomp) return;  // another launch's component
     long long* a = acc + (size_t)c * 5 * 256 + s;
     if (!(x > -INFINITY)) {
       a[4 * 256] += 1;
@@ -55,7 +59,7 @@ __global__ __launch_bounds__(256) void unary_sums(UnarySumArgs g) {
     }
     for (int c = 0; c < ncomp; ++c) {
       const long long* a = acc + (size_t)c * 5 * 256 + s;
-      unsigned long long* u = reinterpret_cast<unsigned long long*>(g.part + (size_t)c * g.uw);
+      unsigned long long* u = reinterpret_cast<unsigned long long*>(g.part + (size_t)(g.cbase + c) * g.uw);
 #pragma unroll
       for (int k = 0; k < 4; ++k)
         if (a[k * 256]) atomicAdd(u + 4 * s + k, (unsigned long long)a[k * 256]);
@@ -68,15 +72,22 @@ __global__ __launch_bounds__(256) void unary_sums(UnarySumArgs g) {
 hipError_t launch_unary_sums(const UnarySumArgs& g, int nblocks, hipStream_t stream) {
   if (g.nc <= 0) return hipSuccess;
   if (g.ncomp > kUnarySumMaxComp || g.nstates > 256 || !g.bad) return hipErrorInvalidValue;
-  const size_t lds = (size_t)g.ncomp * 5 * 256 * sizeof(long long);
-  const void* fn = g.f64 ? reinterpret_cast<const void*>(&unary_sums<double>)
-                         : reinterpret_cast<const void*>(&unary_sums<float>);
-  if (lds > 64 * 1024) (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  if (g.f64)
-    hipLaunchKernelGGL(unary_sums<double>, dim3((unsigned)nblocks), dim3(256), lds, stream, g);
-  else
-    hipLaunchKernelGGL(unary_sums<float>, dim3((unsigned)nblocks), dim3(256), lds, stream, g);
-  return hipGetLastError();
+  // kUnarySumGroup components per launch: 20 KiB of LDS, so the launches co-reside with the
+  // workgroups of a long decode on the same CUs (eight-wave f64 forward: 128.5 KiB of the
+  // CU's 160) instead of waiting for whole CUs (config 5: 21 ms -> ...)
+  for (int cb = 0; cb < g.ncomp; cb += kUnarySumGroup) {
+    UnarySumArgs q = g;
+    q.cbase = cb;
+    q.cgroup = std::min(kUnarySumGroup, g.ncomp - cb);
+    const size_t lds = (size_t)q.cgroup * 5 * 256 * sizeof(long long);
+    if (g.f64)
+      hipLaunchKernelGGL(unary_sums<double>, dim3((unsigned)nblocks), dim3(256), lds, stream, q);
+    else
+      hipLaunchKernelGGL(unary_sums<float>, dim3((unsigned)nblocks), dim3(256), lds, stream, q);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
 }
 
 }  // namespace cvx

@@ -34,6 +34,9 @@ struct T64FwdArgs {
   const int64_t* row_base;     // [slot] delta row index of the range's first element
   const double* resume_rows;   // [r][NP] already-forced rows (resume flow)
   const int32_t* slot_order;   // [launch index] -> slot (longest first)
+  // 1: a range's LAST step adds no emission, so the suffix pass extended to the constrained
+  // element t_m ends on beta_{t_m}(s) = max_j (a[s][j] + g_{t_m+1}[j]) itself (its last row)
+  int noemit_last;
   // SIMD balancing (trellis_fwd_f64): every `balance` steps each wave publishes its remaining
   // steps in a per-SIMD table and takes issue priority 3 if no other wave of its SIMD has more
   // work left, else 1 (the arbiter runs the oldest wave first among equals); 0 = off
@@ -90,6 +93,12 @@ struct MaxMarginal64Args {
   double* mu;                   // [ncon][NP]
 };
 hipError_t launch_t64_max_marginal(int np, const MaxMarginal64Args& a, int64_t ncon, hipStream_t stream);
+// mu[i][j] = delta[i][j] + beta[i][j] for the first n1 rows (single-position sequences), the
+// rest left to the caller (their terms are delta and beta themselves): elementwise, so the
+// kernel co-resides with a long decode on the same CUs (max_marginal_f64's per-sequence
+// max-plus step is the suffix pass's extra step instead, noemit_last)
+hipError_t launch_t64_mu_add(const double* delta, const double* beta, double* mu, int64_t n1, int np,
+                             hipStream_t stream);
 // out[i][j] = j == state[i] ? last[i][j] : -inf (row t_1 of constrained sequence i, forced)
 hipError_t launch_t64_resume_rows(const double* last, const int32_t* state, int64_t n, int np, double* out,
                                   hipStream_t stream);

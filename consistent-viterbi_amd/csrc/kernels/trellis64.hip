@@ -394,7 +394,8 @@ __global__ __launch_bounds__(64 * W * WG) __attribute__((amdgpu_waves_per_eu(MIN
     for (int s = 0; s < S; ++s) {
       double v[C];
 #pragma unroll
-      for (int c = 0; c < C; ++c) v[c] = g.zero_init ? 0.0 : g.pi[j0 + c] + e[s][c];
+      for (int c = 0; c < C; ++c)
+        v[c] = g.zero_init ? 0.0 : (EXT && g.noemit_last && T[s] == 1) ? g.pi[j0 + c] : g.pi[j0 + c] + e[s][c];
       if (EXT && g.start) {  // segment table: start in state st with score 0 (cfn.rs:11-34 pattern)
         const int st = __builtin_amdgcn_readlane(st_l, s);
         if (st >= 0) {
@@ -569,6 +570,16 @@ __global__ __launch_bounds__(64 * W * WG) __attribute__((amdgpu_waves_per_eu(MIN
       for (int c = 0; c < C; ++c) {
         v0[c] = DPA ? acc[c][2 * s2] : acc[c][2 * s2] + e[DPA ? 0 : 2 * s2][c];
         v1[c] = DPA ? acc[c][2 * s2 + 1] : acc[c][2 * s2 + 1] + e[DPA ? 0 : 2 * s2 + 1][c];
+      }
+      if constexpr (EXT && !DPA) {  // noemit_last: the range's last step is the bare max-plus step
+        if (g.noemit_last) {
+          const bool l0 = t == T[2 * s2] - 1, l1 = t == T[2 * s2 + 1] - 1;
+#pragma unroll
+          for (int c = 0; c < C; ++c) {
+            v0[c] = l0 ? acc[c][2 * s2] : v0[c];
+            v1[c] = l1 ? acc[c][2 * s2 + 1] : v1[c];
+          }
+        }
       }
       force(v0, __builtin_amdgcn_readlane(fcur_l, 2 * s2));
       force(v1, __builtin_amdgcn_readlane(fcur_l, 2 * s2 + 1));
@@ -1080,6 +1091,11 @@ __global__ __launch_bounds__(NP) void max_marginal_f64(MaxMarginal64Args args) {
   args.mu[c * NP + i] = args.delta[c * NP + i] + beta;
 }
 
+__global__ void mu_add_f64(const double* delta, const double* beta, double* mu, int64_t n) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < n) mu[k] = delta[k] + beta[k];  // max_marginal_f64's delta + beta, the same f64 add
+}
+
 __global__ void resume_rows_f64(const double* last, const int32_t* state, int np, double* out) {
   const int64_t i = blockIdx.x;
   const int j = threadIdx.x;
@@ -1500,6 +1516,14 @@ hipError_t launch_t64_max_marginal(int np, const MaxMarginal64Args& a, int64_t n
     case 256: hipLaunchKernelGGL(max_marginal_f64<256>, grid, dim3(256), 0, stream, a); break;
     default: return hipErrorInvalidValue;
   }
+  return hipGetLastError();
+}
+
+hipError_t launch_t64_mu_add(const double* delta, const double* beta, double* mu, int64_t n1, int np,
+                             hipStream_t stream) {
+  const int64_t n = n1 * np;
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(mu_add_f64, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, delta, beta, mu, n);
   return hipGetLastError();
 }
 
