@@ -201,7 +201,7 @@ __device__ uint64_t g_t64_probe[1 << 17][6];
 // access 0.44 -> 0.09 at config 4; profiles/r03_ab_wg.txt).  W > 1 units meet at workgroup
 // barriers anyway (their pair rendezvous), so they take bit 2 only.
 template <int C, int S, int PF, bool DPA, bool EXT, int W = 1, bool CAP2 = (W > 1), int GRP = 2, int MINW = 1,
-          bool LDSFIRST = true, int WG = 1, int SYNC = 0>
+          bool LDSFIRST = true, int WG = 1, int SYNC = 0, bool DEFST = false>
 __global__ __launch_bounds__(64 * W * WG) __attribute__((amdgpu_waves_per_eu(MINW))) void trellis_fwd_f64(T64FwdArgs g) {
 #ifdef CV_T64_PROBE
   const uint64_t pr_rt0 = __builtin_amdgcn_s_memrealtime(), pr_c0 = __builtin_amdgcn_s_memtime();
@@ -230,13 +230,22 @@ __global__ __launch_bounds__(64 * W * WG) __attribute__((amdgpu_waves_per_eu(MIN
   static_assert(PF % DV == 0, "the delta-row ring must wrap with the A-row ring");
   // delta_{t-1}: [row][S]; rows NP .. NP+DV-2 are padding, read (and ignored) by the prefetch
   static_assert(WG == 1 || W * WG == 8, "units per workgroup: the CU's eight waves");
-  __shared__ __attribute__((aligned(16))) double dl_all[WG][(NP + DV - 1) * S];
+  // DEFST: delta row t-1 is stored during step t, one sequence pair per quarter of the row loop,
+  // read back from the LDS slice (spreads the 2S stores of a step over it)
+  static_assert(!DEFST || (W == 1 && !EXT), "deferred stores: batch decode, one-wave units");
+  // each lane's C rows are followed by 16 bytes of padding (C a power of two): the lane stride
+  // C*S*8 + 16 B puts the 16 lanes of an epilogue ds_write_b128 on distinct banks (without it
+  // every lane of the wave hit the same four banks); broadcast reads are unaffected
+  constexpr bool PADL = (C & (C - 1)) == 0;
+  constexpr int kPadGroups = PADL ? (NP + DV - 1 + C - 1) / C : 0;
+  __shared__ __attribute__((aligned(16))) double dl_all[WG][(NP + DV - 1) * S + 2 * kPadGroups];
   __shared__ int wg_prog[W * WG];  // each wave's Tmax, then its progress (step * NP + row block)
   const int lane = threadIdx.x & 63;
   const int wid = (W * WG > 1) ? __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6) : 0;
   const int wv = W > 1 ? wid % W : 0;
   const int wgi = WG > 1 ? wid / W : 0;
   double* const dl = dl_all[wgi];
+  auto rowp = [&](int i) -> double* { return dl + i * S + (PADL ? (i / C) * 2 : 0); };
   const int j0 = (wv * 64 + lane) * C;
   const double ninf = ninf_d();
   // workgroup rendezvous without the global-memory drain of __syncthreads (the A-row ring and
@@ -372,6 +381,18 @@ __global__ __launch_bounds__(64 * W * WG) __attribute__((amdgpu_waves_per_eu(MIN
       for (int c = 0; c < C; ++c) dst[c] = v[c];
     }
   };
+  // DEFST: rows r of sequences 2 s2, 2 s2 + 1 from the LDS slice (which holds delta_r)
+  auto deferred_store = [&](int s2, int r) {
+    double v0[C], v1[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      const f64x2 w = *reinterpret_cast<const f64x2*>(rowp(j0 + c) + 2 * s2);
+      v0[c] = w.x;
+      v1[c] = w.y;
+    }
+    store_row(2 * s2, r, v0);
+    store_row(2 * s2 + 1, r, v1);
+  };
   // forced state f >= 0: every other state of that element is impossible
   auto force = [&](double (&v)[C], int f) {
     if (EXT && f >= 0) {
@@ -412,8 +433,8 @@ __global__ __launch_bounds__(64 * W * WG) __attribute__((amdgpu_waves_per_eu(MIN
       }
       force(v, f0);
 #pragma unroll
-      for (int c = 0; c < C; ++c) dl[(j0 + c) * S + s] = v[c];
-      store_row(s, 0, v);
+      for (int c = 0; c < C; ++c) rowp(j0 + c)[s] = v[c];
+      if constexpr (!DEFST) store_row(s, 0, v);
     }
     onext_l = obs_lane(1);
     fnext_l = frc_lane(1);
@@ -454,14 +475,13 @@ __global__ __launch_bounds__(64 * W * WG) __attribute__((amdgpu_waves_per_eu(MIN
 #pragma unroll
     for (int r = 0; r < DV - 1; ++r)
 #pragma unroll
-      for (int s2 = 0; s2 < S / 2; ++s2) dv[r][s2] = *reinterpret_cast<const f64x2*>(dl + r * S + 2 * s2);
-#pragma nounroll
-    for (int i0 = 0; i0 < NP; i0 += PF) {
+      for (int s2 = 0; s2 < S / 2; ++s2) dv[r][s2] = *reinterpret_cast<const f64x2*>(rowp(r) + 2 * s2);
+    auto row_block = [&](const int i0) __attribute__((always_inline)) {
 #pragma unroll
       for (int u = 0; u < PF; ++u) {
         const int i = i0 + u;
         {
-          const f64x2* nrow = reinterpret_cast<const f64x2*>(dl + (i + DV - 1) * S);
+          const f64x2* nrow = reinterpret_cast<const f64x2*>(rowp(i + DV - 1));
 #ifndef CVK_ABL_NOLDS  // ablation build (timing only): delta rows never re-read from LDS
 #pragma unroll
           for (int s2 = 0; s2 < S / 2; ++s2) dv[(u + DV - 1) % DV][s2] = nrow[s2];
@@ -540,6 +560,17 @@ __global__ __launch_bounds__(64 * W * WG) __attribute__((amdgpu_waves_per_eu(MIN
             "s_setprio 2\n"
             "2:" ::"s"(me), "s"(other) : "scc");
       }
+        };
+    // the row loop in quarters (DEFST: one sequence pair's deferred stores before each; the
+    // same structure without them -- a single loop over row_block spilled ~113 VGPRs once the
+    // priority-trade asm block was in it)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if constexpr (DEFST) {
+        if (q < S / 2) deferred_store(q, t - 1);
+      }
+#pragma nounroll
+      for (int i0 = q * (NP / 4); i0 < (q + 1) * (NP / 4); i0 += PF) row_block(i0);
     }
     // W = 1: LDS operations of the wave execute in order, so the reads of delta_{t-1} above
     // complete before the writes below; only the compiler must not reorder.  W > 1: every
@@ -588,15 +619,21 @@ __global__ __launch_bounds__(64 * W * WG) __attribute__((amdgpu_waves_per_eu(MIN
         f64x2 w;
         w.x = v0[c];
         w.y = v1[c];
-        *reinterpret_cast<f64x2*>(dl + (j0 + c) * S + 2 * s2) = w;
+        *reinterpret_cast<f64x2*>(rowp(j0 + c) + 2 * s2) = w;
       }
-      store_row(2 * s2, t, v0);
-      store_row(2 * s2 + 1, t, v1);
+      if constexpr (!DEFST) {
+        store_row(2 * s2, t, v0);
+        store_row(2 * s2 + 1, t, v1);
+      }
     }
     asm volatile("" ::: "memory");
     wg_sync();  // delta_t complete in LDS before the next step reads it
     if (bal_step) sb.decide(other, Tmax - t);
     if constexpr (WG > 1 && W == 1 && (SYNC & 1)) asm volatile("s_barrier" ::: "memory");
+  }
+  if constexpr (DEFST) {  // the last row (the LDS slice holds delta_{Tmax-1})
+#pragma unroll
+    for (int s2 = 0; s2 < S / 2; ++s2) deferred_store(s2, Tmax - 1);
   }
   if constexpr (kWgBar)
     for (int t = Tmax; t < Twg; ++t)
@@ -1171,6 +1208,10 @@ hipError_t fwd_cs(const T64FwdArgs& fa, int64_t nseq, hipStream_t stream) {
   // C >= 3 only: at C <= 2 the one-wave workgroups fit three or more waves per SIMD, which beat
   // two aligned ones (N = 128: 37.7 vs 38.1 ms; N = 192: 84.4 -> 81.1 ms; profiles/r03_ab_wg.txt)
   if constexpr (S == 8 && C >= 3) {
+    static const bool defst = [] {  // A/B knob (bit-identical): CV_T64_DEFST=1, deferred delta stores
+      const char* e = getenv("CV_T64_DEFST");
+      return e && e[0] == '1';
+    }();
     static const bool wg_ext = [] {  // A/B knob (bit-identical): CV_T64_WG_EXT=1, the constrained passes too
       const char* e = getenv("CV_T64_WG_EXT");
       return e && e[0] == '1';
@@ -1187,7 +1228,12 @@ hipError_t fwd_cs(const T64FwdArgs& fa, int64_t nseq, hipStream_t stream) {
       switch (wg_mode - 1) {
         case 1: hipLaunchKernelGGL((trellis_fwd_f64<C, S, 8, false, false, 1, false, 2, 1, true, 8, 1>), g8, b8, 0, stream, f8); break;
         case 2: hipLaunchKernelGGL((trellis_fwd_f64<C, S, 8, false, false, 1, false, 2, 1, true, 8, 2>), g8, b8, 0, stream, f8); break;
-        case 3: hipLaunchKernelGGL((trellis_fwd_f64<C, S, 8, false, false, 1, false, 2, 1, true, 8, 3>), g8, b8, 0, stream, f8); break;
+        case 3:
+          if (defst)
+            hipLaunchKernelGGL((trellis_fwd_f64<C, S, 8, false, false, 1, false, 2, 1, true, 8, 3, true>), g8, b8, 0, stream, f8);
+          else
+            hipLaunchKernelGGL((trellis_fwd_f64<C, S, 8, false, false, 1, false, 2, 1, true, 8, 3>), g8, b8, 0, stream, f8);
+          break;
         default: hipLaunchKernelGGL((trellis_fwd_f64<C, S, 8, false, false, 1, false, 2, 1, true, 8, 0>), g8, b8, 0, stream, f8); break;
       }
       return hipGetLastError();
