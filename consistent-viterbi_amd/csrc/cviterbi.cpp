@@ -101,6 +101,52 @@ constexpr size_t kMaxTimedEvents = 1 << 16;  // cv_timing_begin: at most 16,384 
 
 }  // namespace
 
+// Pinned, double-buffered host staging of a decode call's longest-first order: the call
+// writes slot k only after that slot's previous copy has completed (its event), so the
+// copy is truly asynchronous and the host never waits for the stream's earlier work
+struct OrderStage {
+  int32_t* p[2] = {nullptr, nullptr};
+  size_t cap[2] = {0, 0};
+  hipEvent_t ev[2] = {nullptr, nullptr};
+  bool pending[2] = {false, false};
+  int slot = 0;
+  OrderStage() = default;
+  OrderStage(const OrderStage&) = delete;
+  OrderStage& operator=(const OrderStage&) = delete;
+  ~OrderStage() {
+    for (int k = 0; k < 2; ++k) {
+      if (pending[k]) (void)hipEventSynchronize(ev[k]);
+      if (p[k]) (void)hipHostFree(p[k]);
+      if (ev[k]) (void)hipEventDestroy(ev[k]);
+    }
+  }
+  // the current slot, at least n entries, free to write (nullptr: allocation failed)
+  int32_t* acquire(size_t n) {
+    const int k = slot;
+    if (pending[k]) {
+      if (hipEventSynchronize(ev[k]) != hipSuccess) return nullptr;
+      pending[k] = false;
+    }
+    if (!ev[k] && hipEventCreateWithFlags(&ev[k], hipEventDisableTiming) != hipSuccess) return nullptr;
+    if (cap[k] < n) {
+      if (p[k]) (void)hipHostFree(p[k]);
+      p[k] = nullptr;
+      cap[k] = 0;
+      const size_t want = std::max<size_t>(n, 4096);
+      if (hipHostMalloc((void**)&p[k], want * 4, hipHostMallocDefault) != hipSuccess) return nullptr;
+      cap[k] = want;
+    }
+    return p[k];
+  }
+  // after the copy out of the current slot is enqueued on `stream`
+  hipError_t release(hipStream_t stream) {
+    const hipError_t e = hipEventRecord(ev[slot], stream);
+    pending[slot] = e == hipSuccess;
+    slot ^= 1;
+    return e;
+  }
+};
+
 struct cv_hmm {
   int N = 0, D = 0;
   std::vector<int64_t> bdims;
@@ -139,6 +185,9 @@ struct cv_hmm {
   struct SideWs {
     DevBuf main, last, order, idx, obs2, path2, res2;
     std::vector<int32_t> order_host;
+    OrderStage order_pin;
+    hipEvent_t ws_done = nullptr;  // the last decode_device call on this workspace has finished
+    bool ws_rec = false;
     std::vector<int64_t> idx_host;
     std::vector<hipEvent_t> ev;
     hipStream_t stream = nullptr;  // lowest priority: fills what the constrained work leaves idle
@@ -155,7 +204,14 @@ struct cv_hmm {
   DevBuf rs_rows, rs_rowbase, rs_resume, rs_start, rs_off2, rs_ridx, rs_slot, rs_obs2, rs_frc2, rs_path2;
   hipEvent_t rs_ev = nullptr;  // prefix backtrack done / staging done
   std::vector<int32_t> order_host;
+  OrderStage order_pin;
+  // the last decode_device call on the main workspace has finished (recorded on its stream;
+  // the next call waits for it on ITS stream, so calls on different streams never share the
+  // workspace while it is in use)
+  hipEvent_t ws_done = nullptr;
+  bool ws_rec = false;
   std::vector<float> host_dl, host_mu;  // constrained-decode term rows (kept: no per-call page faults)
+  std::vector<int64_t> sort_pos;        // counting-sort buckets of the longest-first order
   // timing events of the last call
   std::vector<hipEvent_t> ev;  // 4 per chunk: fwd start/end (main stream), bt start/end
   int64_t last_launches = 0;
@@ -176,6 +232,8 @@ struct cv_hmm {
     if (side.stream) (void)hipStreamDestroy(side.stream);
     if (side.hi) (void)hipStreamDestroy(side.hi);
     if (rs_ev) (void)hipEventDestroy(rs_ev);
+    if (ws_done) (void)hipEventDestroy(ws_done);
+    if (side.ws_done) (void)hipEventDestroy(side.ws_done);
     if (stream) (void)hipStreamDestroy(stream);
     if (bt_stream) (void)hipStreamDestroy(bt_stream);
   }
@@ -516,6 +574,9 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
   DevBuf& w_last = side_ws ? h->side.last : h->ws_last;
   DevBuf& w_order = side_ws ? h->side.order : h->ws_order;
   std::vector<int32_t>& order_host = side_ws ? h->side.order_host : h->order_host;
+  OrderStage& order_pin = side_ws ? h->side.order_pin : h->order_pin;
+  hipEvent_t& ws_done = side_ws ? h->side.ws_done : h->ws_done;
+  bool& ws_rec = side_ws ? h->side.ws_rec : h->ws_rec;
   std::vector<hipEvent_t>& evv = side_ws ? h->side.ev : h->ev;
   int64_t launches_done = 0;
   if (o.dtype != CV_DTYPE_F32 && o.dtype != CV_DTYPE_F64) return set_err(CV_EINVAL, "bad dtype %d", o.dtype);
@@ -582,6 +643,8 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
   // padded to npw = 16 * ceil(N / 16); its chunks run back to back on one stream (nothing to
   // overlap)
   if (nseq == 0) return CV_OK;
+  // the workspace of the previous call on this handle may still be in use on another stream
+  if (ws_rec) HIP_TRY(hipStreamWaitEvent(stream, ws_done, 0));
   HIP_TRY(hipMemsetAsync(status_dev, 0, (size_t)nseq, stream));
 
   // Per-element workspace bytes: trellis keeps f32 delta rows [NP]; generic keeps u16 psi [N].
@@ -684,9 +747,21 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
     for (size_t ci = 0; ci < chunks.size(); ++ci) {
       const auto& c = chunks[ci];
       auto b = order_host.begin() + c.first, e = order_host.begin() + c.second;
-      std::iota(b, e, (int32_t)c.first);
       auto len = [&](int32_t x) { return offsets_host[x + 1] - offsets_host[x]; };
-      std::stable_sort(b, e, [&](int32_t x, int32_t y) { return len(x) > len(y); });
+      // stable longest-first: a counting sort on the lengths (a comparison sort of 16,384
+      // sequences cost ~1 ms of host time per call), a stable sort for very long lengths
+      int64_t maxlen = 0;
+      for (int64_t x = c.first; x < c.second; ++x) maxlen = std::max<int64_t>(maxlen, len((int32_t)x));
+      if (maxlen <= 4 * (c.second - c.first) + (1 << 16)) {
+        std::vector<int64_t>& pos = h->sort_pos;
+        pos.assign((size_t)maxlen + 2, 0);
+        for (int64_t x = c.first; x < c.second; ++x) ++pos[(size_t)(maxlen - len((int32_t)x)) + 1];
+        for (size_t k = 1; k < pos.size(); ++k) pos[k] += pos[k - 1];
+        for (int64_t x = c.first; x < c.second; ++x) b[pos[(size_t)(maxlen - len((int32_t)x))]++] = (int32_t)x;
+      } else {
+        std::iota(b, e, (int32_t)c.first);
+        std::stable_sort(b, e, [&](int32_t x, int32_t y) { return len(x) > len(y); });
+      }
       if (!pairing) continue;
       tail.clear();
       auto out = b;
@@ -702,8 +777,11 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
       std::copy(tail.begin(), tail.end(), out);
     }
     if ((st = w_order.ensure((size_t)nseq * 4)) != CV_OK) return st;
-    HIP_TRY(hipMemcpyAsync(w_order.p, order_host.data(), (size_t)nseq * 4, hipMemcpyHostToDevice, stream));
-    HIP_TRY(hipStreamSynchronize(stream));  // order_host may be rewritten by the next call
+    int32_t* pin = order_pin.acquire((size_t)nseq);
+    if (!pin) return set_err(CV_ENOMEM, "pinned staging of %lld order entries failed", (long long)nseq);
+    std::memcpy(pin, order_host.data(), (size_t)nseq * 4);
+    HIP_TRY(hipMemcpyAsync(w_order.p, pin, (size_t)nseq * 4, hipMemcpyHostToDevice, stream));
+    HIP_TRY(order_pin.release(stream));
     order_dev = w_order.as<int32_t>();
   }
 
@@ -921,6 +999,9 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
   // the caller's stream sees the whole decode complete
   if (!serial) HIP_TRY(hipStreamWaitEvent(stream, evv[eb + 4 * (chunks.size() - 1) + 3], 0));
   if (!side_ws && h->acc_on) h->acc_used += nev;
+  if (!ws_done) HIP_TRY(hipEventCreateWithFlags(&ws_done, hipEventDisableTiming));
+  HIP_TRY(hipEventRecord(ws_done, stream));
+  ws_rec = true;
   return CV_OK;
 }
 
