@@ -794,9 +794,31 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
   if (!side_ws) h->last_ev_base = eb;
   for (size_t i = 0; i < nev; ++i)
     if (!get_event(evv, eb + i)) return set_err(CV_EDEVICE, "hipEventCreate failed");
+  // the f64 trellis backtrack of one chunk (backtrack_f64, or fused into the N <= 64 forward)
+  auto t64_bt_args = [&](const std::pair<int64_t, int64_t>& c, unsigned char* wsb) {
+    cvk::T64BtArgs ba{};
+    ba.delta = reinterpret_cast<const double*>(wsb);
+    ba.delta_elem_base = offsets_host[c.first];
+    ba.at = h->q_at.as<double>();
+    ba.offsets = offsets_dev;
+    ba.order = order_dev;
+    ba.seq_begin = c.first;
+    ba.seq_end = c.second;
+    ba.nstates = h->N;
+    ba.path = path_dev;
+    ba.score = score_dev;  // the f64 delta is already the reference score: no re-score
+    ba.status = status_dev;
+    ba.dp_assoc = o.assoc == CV_ASSOC_DP ? 1 : 0;
+    ba.decode_bt = o.assoc == CV_ASSOC_DECODE ? 1 : 0;
+    ba.obs = obs_dev;
+    ba.et = h->q_et.as<double>();
+    ba.at32 = h->t64_nonpos ? h->q_at32.as<float>() : nullptr;
+    return ba;
+  };
   for (size_t ci = 0; ci < chunks.size(); ++ci) {
     const auto& c = chunks[ci];
     const int64_t n = c.second - c.first;
+    bool fused_chunk = false;  // the forward launch also backtracked the chunk
     const int buf = nbuf == 2 ? (int)(ci % 2) : 0;
     unsigned char* wsb = w_main.as<unsigned char>() + buf * buf_bytes;
     unsigned char* lrb = w_last.as<unsigned char>() + buf * last_bytes;
@@ -861,7 +883,10 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
         fa.last_row = reinterpret_cast<double*>(lrb);
         err = cvk::launch_t64_cp_fwd(h->np64, spw, fa, n, stream);
       } else {
-        err = cvk::launch_t64_fwd(h->np64, spw, fa, n, stream);
+        const cvk::T64BtArgs ba = t64_bt_args(c, wsb);
+        fused_chunk = cvk::t64_wave_fusable(h->np64, fa, ba);
+        err = fused_chunk ? cvk::launch_t64_wave_fused(fa, ba, n, stream)  // N <= 64: backtrack fused
+                          : cvk::launch_t64_fwd(h->np64, spw, fa, n, stream);
       }
     } else if (o.dtype == CV_DTYPE_F64) {
       cvk::GenericFwdArgs<double> fa{};
@@ -930,26 +955,11 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
         err = cvk::launch_rescore_f64(ra, n, bts, reserve);
       }
     } else if (use_t64 && !t64cp) {
-      cvk::T64BtArgs ba{};
-      ba.delta = reinterpret_cast<const double*>(wsb);
-      ba.delta_elem_base = offsets_host[c.first];
-      ba.at = h->q_at.as<double>();
-      ba.offsets = offsets_dev;
-      ba.order = order_dev;
-      ba.seq_begin = c.first;
-      ba.seq_end = c.second;
-      ba.nstates = h->N;
-      ba.path = path_dev;
-      ba.score = score_dev;  // the f64 delta is already the reference score: no re-score
-      ba.status = status_dev;
-      ba.dp_assoc = o.assoc == CV_ASSOC_DP ? 1 : 0;
-      ba.decode_bt = o.assoc == CV_ASSOC_DECODE ? 1 : 0;
-      ba.obs = obs_dev;
-      ba.et = h->q_et.as<double>();
-      ba.at32 = h->t64_nonpos ? h->q_at32.as<float>() : nullptr;
       // overlap mode: one persistent workgroup per CU while the next chunk's forward runs (one
       // 60-VGPR wave per SIMD beside its two 212-VGPR waves); the last chunk at full occupancy
-      err = cvk::launch_t64_bt(h->np64, ba, n, bts, (serial || ci + 1 == chunks.size()) ? 0 : std::max(h->cus, 1));
+      err = fused_chunk ? hipSuccess
+                        : cvk::launch_t64_bt(h->np64, t64_bt_args(c, wsb), n, bts,
+                                             (serial || ci + 1 == chunks.size()) ? 0 : std::max(h->cus, 1));
     } else if (o.dtype == CV_DTYPE_F64) {
       cvk::GenericBtArgs<double> ba{};
       ba.psi = reinterpret_cast<const uint16_t*>(wsb);

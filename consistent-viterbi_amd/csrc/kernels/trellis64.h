@@ -123,6 +123,10 @@ int t64_padded_states(int n);
 // sequences per forward wave (2, 4 or 8) for a launch of nseq sequences on `cus` CUs
 int t64_seqs_per_wave(int64_t nseq, int cus);
 hipError_t launch_t64_fwd(int np, int s, const T64FwdArgs& fa, int64_t nseq, hipStream_t stream);
+// N <= 64 row-A0 decodes of NONPOS models: forward and backtrack in one launch (each wave
+// backtracks its own sequence after its forward pass); t64_wave_fusable says when it applies
+bool t64_wave_fusable(int np, const T64FwdArgs& fa, const T64BtArgs& ba);
+hipError_t launch_t64_wave_fused(const T64FwdArgs& fa, const T64BtArgs& ba, int64_t nseq, hipStream_t stream);
 // CP association (cp.rs:70-79): psi and the CP value d[psi] + (a[psi,j] + b[j,o]) in the forward
 hipError_t launch_t64_cp_fwd(int np, int s, const T64FwdArgs& fa, int64_t nseq, hipStream_t stream);
 // max_wgs > 0: at most that many 4-wave workgroups, each looping over the slots (persistent)

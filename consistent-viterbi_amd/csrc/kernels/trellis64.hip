@@ -1009,8 +1009,10 @@ __device__ __forceinline__ void bt_chain_f64(const uint32_t* __restrict__ rows, 
 // NONPOS: the kernel holds only the NONPOS chain (fewer VGPRs, more waves per SIMD); the
 // host launches it for row-A0 decodes without the viterbi::decode infeasible rule when
 // g.at32 is set.
+// prior_in >= 0: the sequence's status as its forward pass left it, passed in registers (the
+// fused N <= 64 kernel: a uniform load of g.status could come from a stale scalar-cache line)
 template <int KP, int PF, bool NONPOS>
-__device__ __forceinline__ void backtrack_one_f64(const T64BtArgs& g, int64_t slot, int lane) {
+__device__ __forceinline__ void backtrack_one_f64(const T64BtArgs& g, int64_t slot, int lane, int prior_in = -1) {
   constexpr int NP = 64 * KP;
   const int64_t seq = g.order ? (int64_t)g.order[slot] : slot;
   const int64_t e0 = g.offsets[seq];
@@ -1040,7 +1042,7 @@ __device__ __forceinline__ void backtrack_one_f64(const T64BtArgs& g, int64_t sl
     }
     cur = first_argmax_d<KP>(last, valid, bv);  // cp.rs:86
   }
-  const uint8_t prior = g.status[seq];
+  const uint8_t prior = prior_in >= 0 ? (uint8_t)prior_in : g.status[seq];
   if (!(bv > ninf_d()) || prior == CVK_SEQ_BADOBS) {
     if (g.decode_bt && prior != CVK_SEQ_BADOBS) {  // viterbi.rs:24-30: from argmax 0 (= cur) through bt
       // the NONPOS kernel leaves the DEC chain (more VGPRs) to the general kernel's
@@ -1283,10 +1285,22 @@ __device__ __forceinline__ double dpp_f64(double v, int ctrl_is_xor2) {
   return from_words((uint32_t)hi, (uint32_t)lo);
 }
 
-template <bool ZI>
-__global__ __launch_bounds__(256) void trellis_wave_f64(T64FwdArgs g) {
+// FUSE (knob CV_T64_FUSE=1, off: slower, see t64_wave_fusable): the wave backtracks its own
+// sequence right after its forward pass (backtrack_one_f64,
+// NONPOS test, a^T in f32 staged in LDS as backtrack_f64 does at NP = 64): the chains of the
+// long sequences, scheduled first, run while other waves still compute forward passes instead
+// of after the whole grid (config 3: their 1,024-step chains set the separate backtrack's
+// makespan).  Row-A0 decodes of NONPOS models only (the host checks).
+template <bool ZI, bool FUSE = false>
+__global__ __launch_bounds__(256) void trellis_wave_f64(T64FwdArgs g, T64BtArgs bt) {
   constexpr int NPW = 64, C = 4, R = 16, LS = R + 2;
   __shared__ __attribute__((aligned(16))) double lds_all[4][2][4 * LS];
+  __shared__ float at_lds[FUSE ? 64 * 64 : 1];
+  if constexpr (FUSE) {  // before any wave leaves: every wave takes part in the barrier
+    for (int k = threadIdx.x; k < 64 * 64; k += 256) at_lds[k] = bt.at32[k];
+    __syncthreads();
+    bt.at32 = at_lds;
+  }
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
   const int rg = lane & 3, cq = lane >> 2;
@@ -1297,7 +1311,10 @@ __global__ __launch_bounds__(256) void trellis_wave_f64(T64FwdArgs g) {
   const int64_t seq = g.order ? (int64_t)g.order[slot] : slot;
   const int64_t e0 = g.offsets[seq];
   const int T = (int)(g.offsets[seq + 1] - e0);
-  if (T <= 0) return;  // backtrack_f64 reports empty sequences
+  if (T <= 0) {  // the backtrack reports empty sequences
+    if constexpr (FUSE) backtrack_one_f64<1, 32, true>(bt, slot, lane, 0);
+    return;
+  }
   double(*lds)[4 * LS] = lds_all[wv];
   const sptr<int32_t> obs = scalar_view(g.obs + e0);
   uint32_t* __restrict__ rows = reinterpret_cast<uint32_t*>(g.delta) + (e0 - g.delta_elem_base) * (2 * NPW);
@@ -1373,15 +1390,23 @@ __global__ __launch_bounds__(256) void trellis_wave_f64(T64FwdArgs g) {
       so[k] = obs_s(min(t + 8, Tm1));          // observation of step t+8
     }
   }
-  if (bad && lane == 0) g.status[seq] = CVK_SEQ_BADOBS;
+  if constexpr (FUSE) {
+    // this wave's rows are in L2 before it reads them back (no other wave touches them, so no
+    // L1 line of them can be stale); the status stays in registers
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    backtrack_one_f64<1, 32, true>(bt, slot, lane, bad ? (int)CVK_SEQ_BADOBS : 0);
+  } else {
+    if (bad && lane == 0) g.status[seq] = CVK_SEQ_BADOBS;
+  }
 }
 
 hipError_t launch_t64_wave(const T64FwdArgs& fa, int64_t nseq, hipStream_t stream) {
   const dim3 grid((unsigned)((nseq + 3) / 4)), block(256);
+  const T64BtArgs none{};
   if (fa.zero_init)
-    hipLaunchKernelGGL(trellis_wave_f64<true>, grid, block, 0, stream, fa);
+    hipLaunchKernelGGL(trellis_wave_f64<true>, grid, block, 0, stream, fa, none);
   else
-    hipLaunchKernelGGL(trellis_wave_f64<false>, grid, block, 0, stream, fa);
+    hipLaunchKernelGGL(trellis_wave_f64<false>, grid, block, 0, stream, fa, none);
   return hipGetLastError();
 }
 
@@ -1427,6 +1452,31 @@ extern "C" __attribute__((visibility("default"))) int cv_debug_t64_probe(uint64_
                                   hipMemcpyDeviceToHost);
 }
 #endif
+
+bool t64_wave_fusable(int np, const T64FwdArgs& fa, const T64BtArgs& ba) {
+  // A/B knob (bit-identical): CV_T64_FUSE=1.  Off by default: measured slower (config 3 3.46
+  // vs 3.22 ms, config 2 0.189 vs 0.179 ms; profiles/r03_ab_fuse.txt) -- the chains run at the
+  // forward's two waves per SIMD (184 VGPRs held) instead of the separate kernel's eight, so
+  // their HBM latency is exposed
+  static const bool fuse = [] {
+    const char* e = getenv("CV_T64_FUSE");
+    return e && e[0] == '1';
+  }();
+  static const bool wave = [] {  // as launch_t64_fwd's CV_T64_WAVE
+    const char* e = getenv("CV_T64_WAVE");
+    return !(e && e[0] == '0');
+  }();
+  const bool ext = fa.forced || fa.ranges || fa.reverse || fa.start || fa.row_base || fa.resume_rows ||
+                   fa.slot_order || fa.last_row;
+  return fuse && wave && np == 64 && !ext && !fa.dp_assoc && !fa.zero_init && !ba.dp_assoc && !ba.decode_bt &&
+         ba.at32 != nullptr;
+}
+
+hipError_t launch_t64_wave_fused(const T64FwdArgs& fa, const T64BtArgs& ba, int64_t nseq, hipStream_t stream) {
+  if (nseq <= 0) return hipSuccess;
+  hipLaunchKernelGGL((trellis_wave_f64<false, true>), dim3((unsigned)((nseq + 3) / 4)), dim3(256), 0, stream, fa, ba);
+  return hipGetLastError();
+}
 
 int t64_padded_states(int n) { return (n >= 1 && n <= 256) ? 64 * ((n + 63) / 64) : 0; }
 
