@@ -168,8 +168,10 @@ CV_API cv_status cv_decode_batch(cv_hmm* h, int64_t nseq, const int64_t* offsets
                                  const cv_opts* opts, int32_t* path_out, double* score_out,
                                  uint8_t* status_out);
 /* Same on device-resident buffers, enqueued on opts->stream (or the handle's stream);
- * returns after enqueueing.  offsets_host (nullable) is a host copy of offsets used for
- * chunking; without it the offsets are copied back once.  Observation indices are
+ * returns after enqueueing (no host synchronisation, so consecutive calls queue ahead).
+ * Consecutive calls on one handle may use different streams: each waits, on its own stream,
+ * for the previous call's workspace.  offsets_host (nullable) is a host copy of offsets used
+ * for chunking; without it the offsets are copied back once.  Observation indices are
  * range-checked on the device: a bad one sets status CV_SEQ_BADOBS. */
 CV_API cv_status cv_decode_batch_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host,
                                         const int64_t* offsets_dev, const int32_t* obs_dev,
