@@ -37,6 +37,10 @@ struct T64FwdArgs {
   // 1: a range's LAST step adds no emission, so the suffix pass extended to the constrained
   // element t_m ends on beta_{t_m}(s) = max_j (a[s][j] + g_{t_m+1}[j]) itself (its last row)
   int noemit_last;
+  // set by the host: the batch suits eight-wave workgroups (equal lengths, or >= 4 rounds of
+  // them); a single round of longest-first workgroups puts all the longest sequences on a few
+  // CUs (ragged 16,384 sequences: 65.5 vs 56 ms), the one-wave layout spreads them
+  int wg_ok;
   // SIMD balancing (trellis_fwd_f64): every `balance` steps each wave publishes its remaining
   // steps in a per-SIMD table and takes issue priority 3 if no other wave of its SIMD has more
   // work left, else 1 (the arbiter runs the oldest wave first among equals); 0 = off

@@ -1141,6 +1141,15 @@ __global__ void resume_rows_f64(const double* last, const int32_t* state, int np
   if (j < np) out[i * np + j] = (j == state[i]) ? last[i * np + j] : ninf_d();
 }
 
+// test knob: CV_T64_WG_FORCE=1 takes the eight-wave layout whatever the batch (T64FwdArgs::wg_ok)
+bool wg_force() {
+  static const bool f = [] {
+    const char* e = getenv("CV_T64_WG_FORCE");
+    return e && e[0] == '1';
+  }();
+  return f;
+}
+
 // S sequences over a PAIR of waves (C = 2 each, N = 256): the small-batch layout
 template <int S>
 hipError_t fwd_w2(const T64FwdArgs& fa, int64_t nseq, bool ext, hipStream_t stream) {
@@ -1155,7 +1164,7 @@ hipError_t fwd_w2(const T64FwdArgs& fa, int64_t nseq, bool ext, hipStream_t stre
   }();
   if (ext)
     hipLaunchKernelGGL((trellis_fwd_f64<2, S, 8, false, true, 2>), grid, block, 0, stream, fa);
-  else if (wg_mode > 0) {
+  else if (wg_mode > 0 && (fa.wg_ok || wg_force())) {
     // four pairs per workgroup (the CU's eight waves), SIMD partners trade priority
     T64FwdArgs f4 = fa;
     f4.balance = 0;
@@ -1218,7 +1227,7 @@ hipError_t fwd_cs(const T64FwdArgs& fa, int64_t nseq, hipStream_t stream) {
       const char* e = getenv("CV_T64_WG_EXT");
       return e && e[0] == '1';
     }();
-    if (wg_mode > 0 && !fa.dp_assoc && (!ext || wg_ext)) {
+    if (wg_mode > 0 && !fa.dp_assoc && (ext ? wg_ext : (fa.wg_ok != 0 || wg_force()))) {
       // eight independent waves per workgroup (two per SIMD), A-row reads kept together
       const dim3 g8((unsigned)((nseq + 8 * S - 1) / (8 * S))), b8(512);
       T64FwdArgs f8 = fa;

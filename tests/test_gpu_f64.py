@@ -216,8 +216,8 @@ def test_t64_workgroup_units_bit_identical(gpu, tmp_path, n, s):
         "p, s, st = cv.decode_batch(h, d['off'], d['obs'], dtype='f64', rescore_f64=False); "
         f"assert cv.last_timing(h)['seqs_per_wave'] == {s}; "
         "np.savez(sys.argv[3], p=p, s=s, st=st)")
-    for wg in ("4", "0"):
-        env = dict(os.environ, CV_T64_S=str(s), CV_T64_WG=wg)
+    for wg in ("4", "0"):  # ragged and < 4 rounds: the default takes one-wave units, so force
+        env = dict(os.environ, CV_T64_S=str(s), CV_T64_WG=wg, CV_T64_WG_FORCE="1")
         out = tmp_path / f"out{wg}.npz"
         subprocess.run([sys.executable, "-c", code, PKG, str(tmp_path / "in.npz"), str(out)],
                        env=env, check=True, timeout=120)

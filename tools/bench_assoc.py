@@ -20,6 +20,12 @@ c = synth.config("c4", nseq)
 if os.environ.get("NSTATES"):  # config-4 shape with another state count (T = 512, V = 1,024)
     ns = int(os.environ["NSTATES"])
     c["pi"], c["a"], c["b"] = synth.random_hmm(ns, 1024, seed=20261015)
+if os.environ.get("TRANGE"):  # ragged lengths: T ~ U[lo, hi] (seeded), iid observations
+    import numpy as np
+    lo, hi = (int(x) for x in os.environ["TRANGE"].split(","))
+    lengths = np.random.default_rng(5).integers(lo, hi + 1, size=nseq)
+    c["offsets"] = synth.offsets_from_lengths(lengths)
+    c["obs"] = synth.iid_obs(1024, int(c["offsets"][-1]), 20261015)
 off, obs = c["offsets"], c["obs"]
 B = len(off) - 1
 dev = torch.device("cuda:0")
