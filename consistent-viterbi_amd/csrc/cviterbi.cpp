@@ -877,14 +877,16 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
       fa.resume_rows = static_cast<const double*>(resume_rows);
       const int spw = cvk::t64_seqs_per_wave(n, h->cus);
       if (!side_ws) h->last_mt = (t64cp || fa.dp_assoc) ? std::min(spw, 4) : spw;
-      {  // eight-wave workgroups: equal lengths (within 1/8), or >= 4 rounds of 64 x CUs
+      {  // eight-wave workgroups: equal lengths (within 1/8), or >= 2 rounds of 64 x CUs
+         // (ragged T in [32, 1024], chunks of 32,768: 158 vs 168 ms; one round, 16,384: 65.5
+         // vs 56 ms -- profiles/r03_ab_wg.txt)
         int64_t tmin = INT64_MAX, tmax = 0;
         for (int64_t sq = c.first; sq < c.second; ++sq) {
           const int64_t T = offsets_host[sq + 1] - offsets_host[sq];
           tmin = std::min(tmin, T);
           tmax = std::max(tmax, T);
         }
-        fa.wg_ok = (8 * tmin >= 7 * tmax || n >= 4 * 64 * (int64_t)std::max(h->cus, 1)) ? 1 : 0;
+        fa.wg_ok = (8 * tmin >= 7 * tmax || n >= 2 * 64 * (int64_t)std::max(h->cus, 1)) ? 1 : 0;
       }
       if (t64cp) {
         fa.nstates = h->N;

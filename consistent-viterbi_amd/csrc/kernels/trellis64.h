@@ -37,7 +37,7 @@ struct T64FwdArgs {
   // 1: a range's LAST step adds no emission, so the suffix pass extended to the constrained
   // element t_m ends on beta_{t_m}(s) = max_j (a[s][j] + g_{t_m+1}[j]) itself (its last row)
   int noemit_last;
-  // set by the host: the batch suits eight-wave workgroups (equal lengths, or >= 4 rounds of
+  // set by the host: the batch suits eight-wave workgroups (equal lengths, or >= 2 rounds of
   // them); a single round of longest-first workgroups puts all the longest sequences on a few
   // CUs (ragged 16,384 sequences: 65.5 vs 56 ms), the one-wave layout spreads them
   int wg_ok;
