@@ -1360,6 +1360,17 @@ bool resume_supported(const cv_hmm* h, bool f64) {
   return h->N > 64 && (h->np == 128 || h->np == 192 || h->np == 256);
 }
 
+// A/B knob (bit-identical): CV_T64_WG_TERMS=1 runs the terms pass in eight-wave workgroups
+// from two rounds on; off: neutral at config 5 (185.2 vs 185.9 ms, profiles/r03_ab_c5_terms.txt
+// -- the faster prefix/suffix passes leave the side decode less room)
+bool terms_wg() {
+  static const bool on = [] {
+    const char* e = getenv("CV_T64_WG_TERMS");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+
 cv_status constrained_partials_locked(cv_hmm* h, int64_t nseq, const int64_t* offsets, const int32_t* obs,
                                       const int32_t* component, int32_t ncomp, const int32_t* pairs, int64_t npairs,
                                       cv_opts& o, int64_t* part, const std::vector<ConSeq>* pre = nullptr,
@@ -1550,6 +1561,9 @@ cv_status constrained_partials_locked(cv_hmm* h, int64_t nseq, const int64_t* of
     fa.delta = static_cast<double*>(rows_d);
     fa.row_base = row_base_d;
     fa.slot_order = h->ws_order.as<int32_t>();
+    // prefix / suffix passes: longest-first ranges; with CV_T64_WG_TERMS=1 and at least two
+    // rounds of eight-wave workgroups, that layout
+    fa.wg_ok = (terms_wg() && nc >= 2 * 64 * (int64_t)std::max(h->cus, 1)) ? 1 : 0;
     err = cvk::launch_t64_fwd(np, cvk::t64_seqs_per_wave(nc, h->cus), fa, nc, stream);
     // suffixes: the same recurrence on a^T with pi = 0, reversed (its last row = g_{t_m+1})
     if (err == hipSuccess) {

@@ -1227,7 +1227,7 @@ hipError_t fwd_cs(const T64FwdArgs& fa, int64_t nseq, hipStream_t stream) {
       const char* e = getenv("CV_T64_WG_EXT");
       return e && e[0] == '1';
     }();
-    if (wg_mode > 0 && !fa.dp_assoc && (ext ? wg_ext : (fa.wg_ok != 0 || wg_force()))) {
+    if (wg_mode > 0 && !fa.dp_assoc && (ext ? (wg_ext || fa.wg_ok != 0) : (fa.wg_ok != 0 || wg_force()))) {
       // eight independent waves per workgroup (two per SIMD), A-row reads kept together
       const dim3 g8((unsigned)((nseq + 8 * S - 1) / (8 * S))), b8(512);
       T64FwdArgs f8 = fa;

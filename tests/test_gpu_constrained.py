@@ -647,3 +647,36 @@ def test_full_config5_device_equals_host(gpu):
     got = (outs[0].cpu().numpy(), outs[1].cpu().numpy(), outs[2].cpu().numpy(), states, obj)
     for x, y, what in zip(got, ref, ("path", "score", "status", "states", "objective")):
         assert np.array_equal(np.asarray(x), np.asarray(y)), what
+
+
+@pytest.mark.parametrize("n", [256, 192])
+def test_constrained_ext_workgroup_units_bit_identical(gpu, tmp_path, n):
+    """The constrained passes in eight-wave workgroups (the terms pass takes them from two
+    rounds on; CV_T64_WG_EXT=1 forces them for every EXT launch: prefix, suffix, segment
+    tables, resume decode) decode the same bits as one-wave workgroups: ragged lengths, multi-
+    position sequences (segment tables), empty sequences."""
+    import os
+    import subprocess
+    import sys
+
+    pkg = os.path.dirname(os.path.dirname(os.path.abspath(cv.__file__)))
+    pi, a, b = synth.random_hmm(n, 30, seed=300 + n)
+    rng = np.random.default_rng(300 + n)
+    lengths = rng.integers(0, 90, size=1500)
+    off = synth.offsets_from_lengths(lengths)
+    obs = rng.integers(0, 30, size=int(off[-1])).astype(np.int32)
+    comp = synth.constraint_components(off, seed=300 + n, ncomp=4, prob=0.4)
+    np.savez(tmp_path / "in.npz", pi=pi, a=a, b=b, off=off, obs=obs, comp=comp)
+    h = cv.HMM(pi, a, b)
+    ref = cv.decode_constrained(h, off, obs, comp, ncomp=4, dtype="f64")
+    code = (
+        "import sys, numpy as np; sys.path.insert(0, sys.argv[1]); import cviterbi as cv; "
+        "d = np.load(sys.argv[2]); h = cv.HMM(d['pi'], d['a'], d['b']); "
+        "p, s, st, states, obj = cv.decode_constrained(h, d['off'], d['obs'], d['comp'], ncomp=4, dtype='f64'); "
+        "np.savez(sys.argv[3], p=p, s=s, st=st, states=np.asarray(states), obj=np.asarray(obj))")
+    env = dict(os.environ, CV_T64_WG_EXT="1", CV_T64_S="8")
+    subprocess.run([sys.executable, "-c", code, pkg, str(tmp_path / "in.npz"), str(tmp_path / "out.npz")],
+                   env=env, check=True, timeout=180)
+    got = np.load(tmp_path / "out.npz")
+    for key, x in zip(("p", "s", "st", "states", "obj"), ref):
+        assert np.array_equal(np.asarray(x), got[key]), key
