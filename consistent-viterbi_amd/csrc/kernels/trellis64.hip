@@ -642,6 +642,244 @@ __global__ __launch_bounds__(64 * W * WG) __attribute__((amdgpu_waves_per_eu(MIN
   if (wv == 0 && lane < S && my_bad) g.status[my_seq] = CVK_SEQ_BADOBS;
 }
 
+// trellis_fwd_f64_rs<PF> -- the small-batch layout with a ROW split (round 3, N = 256): a PAIR
+// of waves decodes S = 8 sequences, both waves over all NP = 256 columns (C = 4 per lane), wave
+// wv over the candidate rows [wv*NP/2, wv*NP/2 + NP/2).  Per row each wave keeps the full-batch
+// kernel's ratios -- 2 A-row loads and 4 delta broadcasts per 64 VALU; the column split
+// (trellis_fwd_f64<2, 8, .., W = 2>) needs twice the broadcasts per VALU, which cost 6.7% at
+// 8,192 sequences (timing-only build without them, profiles/r03_ablate_fwd_f64.txt).  At the
+// step's end each wave writes its partial maxima of the partner's 4 sequences to LDS and, after
+// the rendezvous, finalises its own 4: the max of the two partials (max is exact in any order)
+// plus the emission -- the same f64 value as the one-wave kernel -- into the delta slice and
+// HBM (split planes).  Four pairs per workgroup (the CU's eight waves, two per SIMD); the SIMD
+// partners (waves i and i ^ 4: the same row half) trade issue priority as in trellis_fwd_f64.
+// Row-A0 batch decode only (no EXT, no DPSolver association).
+template <int PF>
+__global__ __launch_bounds__(512) void trellis_fwd_f64_rs(T64FwdArgs g) {
+  constexpr int C = 4, S = 8, NP = 256, H = NP / 2, HS = S / 2, NPAIR = 4, DV = 2;
+  static_assert(H % PF == 0 && (H / 2) % PF == 0, "the ring wraps inside the row half");
+  constexpr int kPadGroups = (NP + DV - 1 + C - 1) / C;
+  __shared__ __attribute__((aligned(16))) double dl_all[NPAIR][(NP + DV - 1) * S + 2 * kPadGroups];
+  // partial maxima of the partner's sequences: [pair][writer wave][chunk k = 2c + pair][lane]
+  __shared__ __attribute__((aligned(16))) f64x2 xb_all[NPAIR][2][8][64];
+  __shared__ int wg_prog[8];
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+  const int wv = wid & 1, pr = wid >> 1;
+  double* const dl = dl_all[pr];
+  // 16 bytes of padding after each lane's C rows: conflict-free epilogue writes (as trellis_fwd_f64)
+  auto rowp = [&](int i) -> double* { return dl + i * S + (i / C) * 2; };
+  const int j0 = lane * C;
+  const int rbase = wv * H;      // this wave's candidate rows
+  const int sown = wv * HS;      // this wave's sequences [sown, sown + HS)
+  const double ninf = ninf_d();
+  auto rendezvous = [&]() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
+
+  // per-sequence bookkeeping in lane s (s < 8), as trellis_fwd_f64 (both waves of the pair)
+  const int ls = lane < S ? lane : S - 1;
+  const int64_t my_k = ((int64_t)blockIdx.x * NPAIR + pr) * S + ls;
+  int my_T = 0;
+  int64_t my_seq = -1, my_eb = 0, my_rb = 0;
+  if (my_k < g.nslots && lane < S) {
+    const int64_t sl = g.seq_begin + my_k;
+    my_seq = g.order ? (int64_t)g.order[sl] : sl;
+    my_eb = g.offsets[my_seq];
+    my_T = (int)(g.offsets[my_seq + 1] - my_eb);
+    my_rb = my_eb - g.delta_elem_base;
+  }
+  int Tmax = 0;
+#pragma unroll
+  for (int s = 0; s < S; ++s) Tmax = max(Tmax, __builtin_amdgcn_readlane(my_T, s));
+  // workgroup-wide barriers (1 after row 0, 2 per step): every wave takes part up to the
+  // longest pair's last step
+  int Twg = Tmax;
+  if (lane == 0) wg_prog[wid] = Tmax;
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 8; ++k) Twg = max(Twg, wg_prog[k]);
+  __syncthreads();
+  if (lane == 0) wg_prog[wid] = 0;
+  if (Tmax <= 0) {
+    if (Twg > 0) {
+      asm volatile("s_barrier" ::: "memory");
+      for (int t = 1; t < Twg; ++t) {
+        asm volatile("s_barrier" ::: "memory");
+        asm volatile("s_barrier" ::: "memory");
+      }
+    }
+    return;
+  }
+  const unsigned V = (unsigned)g.nobs;
+  {
+    const unsigned long long live = __ballot(my_T > 0);
+    const int l0 = __builtin_ctzll(live);
+    const int64_t eb0 = (int64_t)((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)my_eb, l0) |
+                                  ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(my_eb >> 32), l0) << 32));
+    if (my_T <= 0) my_eb = eb0;
+  }
+  const int my_Tc = my_T > 0 ? my_T : 1;
+  bool my_bad = false;
+  auto obs_lane = [&](int t) -> unsigned { return (unsigned)g.obs[my_eb + (t < my_Tc ? t : my_Tc - 1)]; };
+  auto obs_use = [&](unsigned o, int t) -> unsigned {
+    my_bad = my_bad || (t < my_T && o >= V);
+    return o < V ? o : 0u;
+  };
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(g.a), 0, NP * NP * 8, 0x00020000);
+  const uint32_t voff = (uint32_t)j0 * 8;
+  constexpr uint32_t RB = NP * 8;
+  auto emis = [&](unsigned o, double (&e)[C]) { load_a<C>(g.et + (size_t)o * NP + j0, e); };
+  // own sequence sown + q (q < HS): length, delta row base (uniform, from its lane)
+  auto seq_T = [&](int q) { return __builtin_amdgcn_readlane(my_T, sown + q); };
+  auto store_row = [&](int q, int t, const double (&v)[C]) {
+    if (g.delta && t < seq_T(q)) {
+      const int64_t r = (int64_t)((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)my_rb, sown + q) |
+                                  ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(my_rb >> 32), sown + q) << 32));
+      uint32_t* dst = reinterpret_cast<uint32_t*>(g.delta) + (r + t) * (2 * NP) + j0;
+      store_split<C>(dst, dst + NP, v);
+    }
+  };
+  // acc of own (partner = false) or partner sequence q of this wave (selects: no runtime
+  // register indexing)
+  double acc[C][S];
+  auto acc_of = [&](int c, int q, bool partner) -> double {
+    return ((wv == 0) != partner) ? acc[c][q] : acc[c][q + HS];
+  };
+
+  // ---- t = 0: d0 = pi + b[:, o0] for the own sequences ----
+  unsigned onext_l;
+  {
+    const unsigned o0 = obs_use(obs_lane(0), 0);
+#pragma unroll
+    for (int q = 0; q < HS; ++q) {
+      double e[C], v[C];
+      emis((unsigned)__builtin_amdgcn_readlane((int)o0, sown + q), e);
+#pragma unroll
+      for (int c = 0; c < C; ++c) v[c] = g.zero_init ? 0.0 : g.pi[j0 + c] + e[c];
+#pragma unroll
+      for (int c = 0; c < C; ++c) rowp(j0 + c)[sown + q] = v[c];
+      store_row(q, 0, v);
+    }
+    onext_l = obs_lane(1);
+  }
+  rendezvous();  // delta_0 of all 8 sequences in the slice
+
+  __builtin_amdgcn_s_setprio(3);
+  double ar[PF][C];
+#pragma unroll
+  for (int u = 0; u < PF; ++u) {
+    load_row_buf<C>(ra, voff, (uint32_t)(rbase + u) * RB, ar[u]);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  for (int t = 1; t < Tmax; ++t) {
+    const unsigned ocur_l = obs_use(onext_l, t);
+#pragma unroll
+    for (int c = 0; c < C; ++c)
+#pragma unroll
+      for (int s = 0; s < S; ++s) acc[c][s] = ninf;
+    f64x2 dv[DV][S / 2];
+#pragma unroll
+    for (int s2 = 0; s2 < S / 2; ++s2) dv[0][s2] = *reinterpret_cast<const f64x2*>(rowp(rbase) + 2 * s2);
+    auto row_block = [&](const int i0) __attribute__((always_inline)) {  // rows rbase + i0 .. + PF - 1
+#pragma unroll
+      for (int u = 0; u < PF; ++u) {
+        const int i = rbase + i0 + u;
+        {
+          const f64x2* nrow = reinterpret_cast<const f64x2*>(rowp(i + 1));
+#pragma unroll
+          for (int s2 = 0; s2 < S / 2; ++s2) dv[(u + 1) % DV][s2] = nrow[s2];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int s0 = 0; s0 < S / 2; s0 += 2) {
+          double x[2][2][C];
+#pragma unroll
+          for (int gg = 0; gg < 2; ++gg) {
+            const f64x2 d = dv[u % DV][s0 + gg];
+#pragma unroll
+            for (int c = 0; c < C; ++c) {
+              x[gg][0][c] = d.x + ar[u][c];
+              x[gg][1][c] = d.y + ar[u][c];
+            }
+          }
+          __builtin_amdgcn_sched_group_barrier(0x002, 4 * C, 0);
+          __builtin_amdgcn_sched_group_barrier(0x002, 4 * C, 0);
+#pragma unroll
+          for (int gg = 0; gg < 2; ++gg)
+#pragma unroll
+            for (int c = 0; c < C; ++c) {
+              acc[c][2 * (s0 + gg)] = __builtin_fmax(acc[c][2 * (s0 + gg)], x[gg][0][c]);
+              acc[c][2 * (s0 + gg) + 1] = __builtin_fmax(acc[c][2 * (s0 + gg) + 1], x[gg][1][c]);
+            }
+        }
+        // refill with the half's row (i0 + u + PF) mod H: the next step's first rows wrap in
+        const int rel = i0 + u + PF;
+        load_row_buf<C>(ra, voff, (uint32_t)(rbase + (rel < H ? rel : rel - H)) * RB, ar[u]);
+      }
+      {  // SIMD partners (same row half) trade priority, as trellis_fwd_f64 (one asm block)
+        const int me = t * H + i0;
+        wg_prog[wid] = me;
+        const int other = __builtin_amdgcn_readfirstlane(wg_prog[wid ^ 4]);
+        asm volatile(
+            "s_cmp_le_i32 %0, %1\n\t"
+            "s_cbranch_scc0 1f\n\t"
+            "s_setprio 3\n\t"
+            "s_branch 2f\n"
+            "1:\n\t"
+            "s_setprio 2\n"
+            "2:" ::"s"(me), "s"(other) : "scc");
+      }
+    };
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+#pragma nounroll
+      for (int i0 = q * (H / 2); i0 < (q + 1) * (H / 2); i0 += PF) row_block(i0);
+    }
+    asm volatile("" ::: "memory");
+    // epilogue: own emissions in flight, partials of the partner's sequences to LDS
+    double e[HS][C];
+#pragma unroll
+    for (int q = 0; q < HS; ++q) emis((unsigned)__builtin_amdgcn_readlane((int)ocur_l, sown + q), e[q]);
+    onext_l = obs_lane(t + 1);
+    f64x2(*xw)[64] = xb_all[pr][wv];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int c = k >> 1, q = 2 * (k & 1);
+      f64x2 w;
+      w.x = acc_of(c, q, true);
+      w.y = acc_of(c, q + 1, true);
+      xw[k][lane] = w;
+    }
+    rendezvous();  // partials written; every wave is done reading delta_{t-1}
+    const f64x2(*xr)[64] = xb_all[pr][wv ^ 1];
+#pragma unroll
+    for (int qp = 0; qp < HS / 2; ++qp) {
+      double v0[C], v1[C];
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        const f64x2 p = xr[2 * c + qp][lane];
+        v0[c] = __builtin_fmax(acc_of(c, 2 * qp, false), p.x) + e[2 * qp][c];       // viterbi.rs:15-17
+        v1[c] = __builtin_fmax(acc_of(c, 2 * qp + 1, false), p.y) + e[2 * qp + 1][c];
+      }
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        f64x2 w;
+        w.x = v0[c];
+        w.y = v1[c];
+        *reinterpret_cast<f64x2*>(rowp(j0 + c) + sown + 2 * qp) = w;
+      }
+      store_row(2 * qp, t, v0);
+      store_row(2 * qp + 1, t, v1);
+    }
+    asm volatile("" ::: "memory");
+    rendezvous();  // delta_t of all 8 sequences in the slice
+  }
+  for (int t = Tmax; t < Twg; ++t) {
+    asm volatile("s_barrier" ::: "memory");
+    asm volatile("s_barrier" ::: "memory");
+  }
+  if (lane >= sown && lane < sown + HS && my_bad) g.status[my_seq] = CVK_SEQ_BADOBS;
+}
+
 // CP association (CPSolver, cp.rs:70-79 via utils.rs:24-38, hmm.rs:220-222):
 //   psi = first argmax_i (d[i] + a[i,j]);  d'[j] = d[psi] + (a[psi,j] + b[j,o])
 // The value depends on psi, so the forward pass tracks the first argmax: per pair one add,
@@ -1158,13 +1396,28 @@ hipError_t fwd_w2(const T64FwdArgs& fa, int64_t nseq, bool ext, hipStream_t stre
     const char* e = getenv("CV_T64_LDSFIRST");
     return !(e && e[0] == '0');
   }();
+  static const bool rs_mode = [] {  // A/B knob (bit-identical): CV_T64_RS=0 keeps the column split
+    const char* e = getenv("CV_T64_RS");
+    return !(e && e[0] == '0');
+  }();
   static const int wg_mode = [] {  // A/B knob (bit-identical), as in fwd_cs: 0 = one pair per workgroup
     const char* e = getenv("CV_T64_WG");
     return e ? atoi(e) : 4;
   }();
-  if (ext)
+  if (ext) {
     hipLaunchKernelGGL((trellis_fwd_f64<2, S, 8, false, true, 2>), grid, block, 0, stream, fa);
-  else if (wg_mode > 0 && (fa.wg_ok || wg_force())) {
+    return hipGetLastError();
+  }
+  if constexpr (S == 8) {
+    if (rs_mode && !fa.dp_assoc && (fa.wg_ok || wg_force())) {  // the row split (trellis_fwd_f64_rs)
+      T64FwdArgs f4 = fa;
+      f4.balance = 0;
+      hipLaunchKernelGGL((trellis_fwd_f64_rs<8>), dim3((unsigned)((nseq + 4 * S - 1) / (4 * S))), dim3(512), 0,
+                         stream, f4);
+      return hipGetLastError();
+    }
+  }
+  if (wg_mode > 0 && (fa.wg_ok || wg_force())) {
     // four pairs per workgroup (the CU's eight waves), SIMD partners trade priority
     T64FwdArgs f4 = fa;
     f4.balance = 0;

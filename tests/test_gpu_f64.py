@@ -88,15 +88,16 @@ def test_t64_ties_and_infeasible(gpu, n, assoc):
             cv.decode_batch(h, off, obs_bad, dtype="f64", kernel=kernel, rescore_f64=False)
 
 
-@pytest.mark.parametrize("nseq", [8192, 4096, 2048])
-def test_t64_small_batch_layouts_vs_generic(gpu, nseq):
+@pytest.mark.parametrize("nseq,uniform", [(8192, False), (8192, True), (12000, True), (4096, False), (2048, False)])
+def test_t64_small_batch_layouts_vs_generic(gpu, nseq, uniform):
     """N = 256 batches too small for 8 sequences per wave (8,192 = one GPU of 8-GPU strong
-    scaling): 2S sequences over a pair of waves (trellis_fwd_f64<2, 2S, .., W=2>) -- the whole
-    batch equals the generic f64 kernel, scores are the f64 fold of each path, and the layout
-    reported is the small-batch one."""
+    scaling): 2S sequences over a pair of waves -- the row split (trellis_fwd_f64_rs, four pairs
+    per workgroup) for equal lengths, the column split (trellis_fwd_f64<2, 2S, .., W=2>) for
+    ragged ones -- the whole batch equals the generic f64 kernel, scores are the f64 fold of
+    each path, and the layout reported is the small-batch one."""
     pi, a, b = synth.random_hmm(256, 64, seed=77)
     rng = np.random.default_rng(nseq)
-    lengths = rng.integers(40, 49, size=nseq)
+    lengths = np.full(nseq, 44) if uniform else rng.integers(40, 49, size=nseq)
     off = synth.offsets_from_lengths(lengths)
     obs = rng.integers(0, 64, size=int(off[-1])).astype(np.int32)
     h = cv.HMM(pi, a, b)
