@@ -202,6 +202,8 @@ struct cv_hmm {
   // resume flow of the constrained decode: stored prefix rows, forced row t_1 per constrained
   // sequence, the compact suffix batch and its index arrays
   DevBuf rs_rows, rs_rowbase, rs_resume, rs_start, rs_off2, rs_ridx, rs_slot, rs_obs2, rs_frc2, rs_path2;
+  // certified suffix trace (f64): the suffix pass's rows, their per-slot bases, the slot flags
+  DevBuf rs_srows, rs_srowbase, rs_cert;
   hipEvent_t rs_ev = nullptr;  // prefix backtrack done / staging done
   std::vector<int32_t> order_host;
   OrderStage order_pin;
@@ -223,6 +225,7 @@ struct cv_hmm {
   int32_t last_np = 0;
   int32_t last_mt = -1;
   uint64_t last_explored = 0;
+  int64_t last_traced = 0;  // constrained sequences the last resume flow certified (suffix trace)
 
   ~cv_hmm() {
     for (auto e : ev) (void)hipEventDestroy(e);
@@ -1348,7 +1351,19 @@ cv_status constrained_validate(cv_hmm* h, int64_t nseq, const int64_t* offsets, 
 struct PrefixKeep {
   bool kept = false;
   std::vector<int64_t> seq, t1, row_base;  // per terms slot i
+  // f64: the suffix pass's rows of slots [0, n1) (one constrained element each) are kept too
+  // (h->rs_srows, slot i from row srow_base[i]) for the certified suffix trace
+  bool suffix_kept = false;
+  int64_t n1 = 0;
 };
+
+// The certified suffix trace (suffix_trace_f64) replaces the resume flow's second forward pass
+// for one-position sequences: f64, models whose finite entries are all in [-2^80, 0].  A/B knob
+// (bit-identical): CV_NO_TRACE=1.
+bool trace_supported(const cv_hmm* h) {
+  const char* e = getenv("CV_NO_TRACE");  // read per call: tests flip it within one process
+  return !(e && *e && *e != '0') && h->t64_nonpos;
+}
 
 // The resume flow covers f32 N > 64 with NP % 64 == 0 (pair kernel + backtrack_v) and every f64
 // N <= 256; its stored rows must fit 4x the workspace cap (32 GiB by default: config 5 needs
@@ -1378,6 +1393,7 @@ cv_status constrained_partials_locked(cv_hmm* h, int64_t nseq, const int64_t* of
                                       PrefixKeep* keep = nullptr,
                                       const std::function<cv_status()>& after_terms = nullptr) {
   if (keep) *keep = PrefixKeep{};
+  h->last_traced = 0;
   if (obs_staged) *obs_staged = false;
   std::vector<ConSeq> own;
   cv_status st = CV_OK;
@@ -1451,6 +1467,9 @@ cv_status constrained_partials_locked(cv_hmm* h, int64_t nseq, const int64_t* of
   const uint64_t row_bytes = (uint64_t)np * rb;  // f64: split-plane rows of 2 NP words
   const int64_t* row_base_d = nullptr;
   void* rows_d = nullptr;
+  const int64_t* srow_base_d = nullptr;  // the suffix pass's rows (certified suffix trace)
+  void* srows_d = nullptr;
+  std::vector<int64_t> sbv;  // read by an async copy: lives until the slot-order sync below
   if (keep && resume_supported(h, f64)) {
     std::vector<int64_t> rbv((size_t)nc);
     int64_t rows = 0;
@@ -1479,6 +1498,26 @@ cv_status constrained_partials_locked(cv_hmm* h, int64_t nseq, const int64_t* of
       for (int64_t i = 0; i < nc; ++i) {
         keep->seq[(size_t)i] = order[i]->seq;
         keep->t1[(size_t)i] = order[i]->elems.front();
+      }
+      // f64, one-position slots present: keep the suffix pass's rows as well, within half of
+      // what the device can still give (else the resume decode covers those slots)
+      if (f64 && n1 > 0 && trace_supported(h)) {
+        sbv.resize((size_t)nc);
+        int64_t srows = 0;
+        for (int64_t i = 0; i < nc; ++i) sbv[(size_t)i] = srows, srows += rg[2 * nc + 2 * i + 1] - rg[2 * nc + 2 * i];
+        bool sfits = (uint64_t)srows * row_bytes <= free_device_bytes(h->rs_srows.bytes) / 2;
+        if (sfits && h->rs_srows.ensure((size_t)std::max<int64_t>(srows, 1) * row_bytes) != CV_OK) {
+          sfits = false;
+          g_err.clear();
+        }
+        if (sfits) {
+          if ((st = h->rs_srowbase.ensure((size_t)nc * 8)) != CV_OK) return st;
+          HIP_TRY(hipMemcpyAsync(h->rs_srowbase.p, sbv.data(), (size_t)nc * 8, hipMemcpyHostToDevice, stream));
+          srows_d = h->rs_srows.p;
+          srow_base_d = h->rs_srowbase.as<int64_t>();
+          keep->suffix_kept = true;
+          keep->n1 = n1;
+        }
       }
     }
   }
@@ -1574,8 +1613,8 @@ cv_status constrained_partials_locked(cv_hmm* h, int64_t nseq, const int64_t* of
       fb.reverse = 1;
       fb.noemit_last = 1;
       fb.last_row = h->cs_g.as<double>();  // beta_{t_m}
-      fb.delta = nullptr;
-      fb.row_base = nullptr;
+      fb.delta = static_cast<double*>(srows_d);  // kept for the certified suffix trace, or none
+      fb.row_base = srow_base_d;
       fb.slot_order = h->ws_order.as<int32_t>() + nc;
       err = cvk::launch_t64_fwd(np, cvk::t64_seqs_per_wave(nc, h->cus), fb, nc, stream);
     }
@@ -1982,14 +2021,65 @@ cv_status forced_decode_resume(cv_hmm* h, int64_t nseq, const int64_t* offsets_h
     const int32_t c = comp_state[component[keep.t1[i]]];
     state[(size_t)i] = c >= 0 ? c : 0;  // no state: forced to 0 and marked infeasible (mark_unassigned)
   }
+  // per-slot arrays: [seq | t1 | row_base] int64, then state int32
+  std::vector<int64_t> slot64((size_t)nc * 3);
+  std::copy(keep.seq.begin(), keep.seq.end(), slot64.begin());
+  std::copy(keep.t1.begin(), keep.t1.end(), slot64.begin() + nc);
+  std::copy(keep.row_base.begin(), keep.row_base.end(), slot64.begin() + 2 * nc);
+  if ((st = h->rs_slot.ensure((size_t)std::max<int64_t>(nc, 1) * 28)) != CV_OK) return st;
+  int64_t* slot_d = h->rs_slot.as<int64_t>();
+  int32_t* state_d = reinterpret_cast<int32_t*>(slot_d + 3 * nc);
+  HIP_TRY(hipMemcpyAsync(slot_d, slot64.data(), (size_t)nc * 24, hipMemcpyHostToDevice, stream));
+  HIP_TRY(hipMemcpyAsync(state_d, state.data(), (size_t)nc * 4, hipMemcpyHostToDevice, stream));
+  // certified suffix trace (f64, suffix rows kept): the one-position slots whose forced path
+  // after t1 reads off the suffix pass's rows (suffix_trace_f64) need no second forward pass;
+  // only the others join the compact forced decode below
+  std::vector<uint8_t> cert((size_t)nc, 0);
+  if (f64 && keep.suffix_kept && keep.n1 > 0) {
+    const int64_t n1 = keep.n1;
+    std::vector<int32_t> tstate((size_t)n1);
+    for (int64_t i = 0; i < n1; ++i) tstate[(size_t)i] = comp_state[component[keep.t1[i]]] >= 0 ? state[(size_t)i] : -1;
+    const size_t cert_bytes = (size_t)((n1 + 3) / 4) * 4;  // then the states, 4-byte aligned
+    if ((st = h->rs_cert.ensure(cert_bytes + (size_t)n1 * 4)) != CV_OK) return st;
+    uint8_t* cert_d = h->rs_cert.as<uint8_t>();
+    int32_t* tstate_d = reinterpret_cast<int32_t*>(cert_d + cert_bytes);
+    HIP_TRY(hipMemcpyAsync(tstate_d, tstate.data(), (size_t)n1 * 4, hipMemcpyHostToDevice, stream));
+    cvk::SuffixTrace64Args ta{};
+    ta.rows = h->rs_srows.as<double>();
+    ta.srow_base = h->rs_srowbase.as<int64_t>();
+    ta.seq = slot_d;
+    ta.t1 = slot_d + nc;
+    ta.state = tstate_d;
+    ta.dlast = h->cs_delta.as<double>();
+    ta.offsets = offsets_dev;
+    ta.obs = obs_dev;
+    ta.a = h->q_a.as<double>();
+    ta.et = h->q_et.as<double>();
+    ta.nstates = h->N;
+    ta.path = path_dev;
+    ta.score = score_dev;
+    ta.status = status_dev;
+    ta.cert = cert_d;
+    const hipError_t e = cvk::launch_t64_suffix_trace(np, ta, n1, stream);
+    if (e != hipSuccess) return set_err(CV_EDEVICE, "suffix trace failed: %s", hipGetErrorString(e));
+    HIP_TRY(hipMemcpyAsync(cert.data(), cert_d, (size_t)n1, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipStreamSynchronize(stream));
+    trace_mark("resume: certified suffix trace");
+  }
+  int64_t ncert = 0;
+  for (uint8_t c : cert) ncert += c;
+  h->last_traced = ncert;
   // compact order: longest first, stable (counting sort) over the member sequences
-  const int64_t nm = constrained_only ? nc : nseq;
-  std::vector<int64_t> mem((size_t)nm);
+  const int64_t nm = (constrained_only ? nc : nseq) - ncert;
+  std::vector<int64_t> mem;
+  mem.reserve((size_t)nm);
   if (constrained_only) {  // keep.seq is in sequence order (terms-pass slot order)
-    for (int64_t i = 0; i < nc; ++i) mem[(size_t)i] = keep.seq[(size_t)i];
+    for (int64_t i = 0; i < nc; ++i)
+      if (!cert[(size_t)i]) mem.push_back(keep.seq[(size_t)i]);
     std::sort(mem.begin(), mem.end());
   } else {
-    std::iota(mem.begin(), mem.end(), (int64_t)0);
+    for (int64_t s = 0; s < nseq; ++s)
+      if (ridx[(size_t)s] < 0 || !cert[(size_t)ridx[(size_t)s]]) mem.push_back(s);
   }
   int64_t maxlen = 0;
   for (int64_t s : mem) maxlen = std::max(maxlen, offsets_host[s + 1] - start[(size_t)s]);
@@ -2012,15 +2102,9 @@ cv_status forced_decode_resume(cv_hmm* h, int64_t nseq, const int64_t* offsets_h
     off2[k + 1] = off2[k] + offsets_host[s + 1] - start[(size_t)s];
   }
   const int64_t total2 = off2[nm];
-  // per-slot arrays: [seq | t1 | row_base] int64, then state int32
-  std::vector<int64_t> slot64((size_t)nc * 3);
-  std::copy(keep.seq.begin(), keep.seq.end(), slot64.begin());
-  std::copy(keep.t1.begin(), keep.t1.end(), slot64.begin() + nc);
-  std::copy(keep.row_base.begin(), keep.row_base.end(), slot64.begin() + 2 * nc);
   if ((st = h->rs_start.ensure(c64.size() * 8)) != CV_OK) return st;
   if ((st = h->rs_ridx.ensure((size_t)std::max<int64_t>(nm, 1) * 4)) != CV_OK) return st;
   if ((st = h->rs_off2.ensure((size_t)std::max<int64_t>(nm, 1) * 9)) != CV_OK) return st;  // score2 f64 + status2 u8
-  if ((st = h->rs_slot.ensure((size_t)std::max<int64_t>(nc, 1) * 28)) != CV_OK) return st;
   if ((st = h->rs_resume.ensure((size_t)std::max<int64_t>(nc, 1) * np * rb)) != CV_OK) return st;
   if ((st = h->rs_obs2.ensure((size_t)std::max<int64_t>(total2, 1) * 4)) != CV_OK) return st;
   if ((st = h->rs_frc2.ensure((size_t)std::max<int64_t>(total2, 1) * 4)) != CV_OK) return st;
@@ -2032,12 +2116,8 @@ cv_status forced_decode_resume(cv_hmm* h, int64_t nseq, const int64_t* offsets_h
   const int64_t* off2_d = cperm_d + nm;
   double* score2 = h->rs_off2.as<double>();
   uint8_t* status2 = reinterpret_cast<uint8_t*>(score2 + nm);
-  int64_t* slot_d = h->rs_slot.as<int64_t>();
-  int32_t* state_d = reinterpret_cast<int32_t*>(slot_d + 3 * nc);
   HIP_TRY(hipMemcpyAsync(h->rs_start.p, c64.data(), c64.size() * 8, hipMemcpyHostToDevice, stream));
-  HIP_TRY(hipMemcpyAsync(h->rs_ridx.p, cridx.data(), (size_t)nm * 4, hipMemcpyHostToDevice, stream));
-  HIP_TRY(hipMemcpyAsync(slot_d, slot64.data(), (size_t)nc * 24, hipMemcpyHostToDevice, stream));
-  HIP_TRY(hipMemcpyAsync(state_d, state.data(), (size_t)nc * 4, hipMemcpyHostToDevice, stream));
+  if (nm > 0) HIP_TRY(hipMemcpyAsync(h->rs_ridx.p, cridx.data(), (size_t)nm * 4, hipMemcpyHostToDevice, stream));
   hipError_t err = f64 ? cvk::launch_t64_resume_rows(h->cs_delta.as<double>(), state_d, nc, np,
                                                      h->rs_resume.as<double>(), stream)
                        : cvk::launch_resume_rows(h->cs_delta.as<float>(), state_d, nc, np, h->rs_resume.as<float>(),
@@ -2460,6 +2540,12 @@ cv_status sum_timing(cv_hmm* h, size_t eb, int64_t launches, cv_timing* out) {
   return CV_OK;
 }
 }  // namespace
+
+CV_API cv_status cv_last_suffix_traced(const cv_hmm* h, int64_t* out) {
+  if (!h || !out) return set_err(CV_EINVAL, "null argument");
+  *out = h->last_traced;
+  return CV_OK;
+}
 
 CV_API cv_status cv_last_timing(cv_hmm* h, cv_timing* out) {
   if (!h || !out) return set_err(CV_EINVAL, "null argument");

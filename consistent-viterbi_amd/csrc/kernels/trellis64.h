@@ -89,6 +89,32 @@ struct PrefixBt64Args {
 };
 hipError_t launch_t64_prefix_bt(int np, const PrefixBt64Args& a, int64_t n, hipStream_t stream);
 
+// Certified suffix trace (resume flow, f64, one constrained element t1, NONPOS models): the
+// forced decode's path after t1 read off the suffix pass's stored rows instead of a second
+// forward pass.  Slot i certifies when every step's first argmax beats the runner-up by more
+// than the bound on the rounding of both passes (suffix_trace_f64 in trellis64.hip); then the
+// path [t1 + 1, end), the score (the forward fold (d + a) + b from delta_{t1}(state)) and
+// status OK are written and cert[i] = 1.  cert[i] = 0: nothing but path garbage in
+// [t1 + 1, end), which the fallback forced decode overwrites.
+struct SuffixTrace64Args {
+  const double* rows;        // compact split-plane rows of the reversed suffix pass
+  const int64_t* srow_base;  // [n] first row of slot i (row k = element end - 1 - k)
+  const int64_t* seq;        // [n] sequence id of slot i
+  const int64_t* t1;         // [n] the constrained element
+  const int32_t* state;      // [n] state forced there (-1: no state, not traced)
+  const double* dlast;       // [n][NP] the prefix pass's row t1 (delta_{t1}, unforced)
+  const int64_t* offsets;    // original CSR offsets
+  const int32_t* obs;        // observations (element-indexed)
+  const double* a;           // [NP][NP] a (from-major, t64 tables)
+  const double* et;          // [V][NP]
+  int nstates;
+  int32_t* path;
+  double* score;
+  uint8_t* status;
+  uint8_t* cert;             // [n]
+};
+hipError_t launch_t64_suffix_trace(int np, const SuffixTrace64Args& a, int64_t n, hipStream_t stream);
+
 struct MaxMarginal64Args {
   const double* delta;          // [ncon][NP] forward row at the constrained position
   const double* g;              // [ncon][NP] last row of the reversed suffix pass

@@ -1348,6 +1348,114 @@ __global__ __launch_bounds__(256) void prefix_backtrack_f64(PrefixBt64Args a, in
                                      a.state[i], a.path + e0, a.at, nullptr, nullptr, 0, a.nstates, lane, a.at32);
 }
 
+// Resume flow, certified suffix trace (f64; one constrained element t1; models whose finite
+// entries all lie in [-2^80, 0]).  The forced decode from state s* at t1 maximises, over the
+// paths P of [t1, end), the forward fold F(P) = ((D + a) + b) + ... from D = delta_{t1}(s*)
+// (viterbi.rs:15-17 order).  The reversed suffix pass stored r_x(j) = b_j(o_x) + beta_x(j) for
+// every element x > t1, so the path can be read FORWARD: from cur = P_x the candidates are
+// w_j = r_{x+1}(j) + a[cur][j] and P_{x+1} = their first argmax.  That path is the forced
+// decode's exactly when no other path's fold can reach it.  All terms are <= 0, so an fp sum
+// of k terms is within ~k 2^-53 relative of its real value; a path Q leaving P at x+1 for j
+// scores at most C + W_j (real) against P's C + W_P, C the common real prefix
+// (|C| <= |d_x|(1 + rho), d_x = P's fold so far).  With rho = (4L + 8) 2^-52 (L = end-1-t1
+// steps: 2L roundings forward, 2L + 1 in r and w, doubled for slack) the test
+//     w2 (1 - rho) + 2 rho |d_x|  <  w_P (1 + rho)      (w2 = best candidate other than P_{x+1})
+// at every step gives F(Q) < F(P) for every Q != P: the forced forward decode then ends in
+// P's last state (unique maximum), every backtrack step's first argmax is P's predecessor (a
+// tie or a larger value there would make some Q reach F(P)), and its score is F(P), the fold
+// computed here in the forward order -- bit-identical.  A failed step (near tie, -inf, no
+// state) leaves the slot to the fallback forced decode: cert = 0.
+template <int KP>
+__global__ __launch_bounds__(256) void suffix_trace_f64(SuffixTrace64Args g, int64_t n) {
+  constexpr int NP = 64 * KP;
+  constexpr uint32_t NINF_HI = 0xFFF00000u;
+  const int lane = threadIdx.x & 63;
+  const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= n) return;
+  const int64_t seq = g.seq[i];
+  const int64_t x0 = g.t1[i];
+  const int64_t end = g.offsets[seq + 1];
+  const int L = (int)(end - 1 - x0);
+  int cur = g.state[i];
+  double d = cur >= 0 ? g.dlast[(size_t)i * NP + cur] : ninf_d();
+  bool ok = d > ninf_d();
+  bool valid[KP];
+#pragma unroll
+  for (int k = 0; k < KP; ++k) valid[k] = (lane + 64 * k) < g.nstates;
+  const double rho = (double)(4 * L + 8) * 0x1p-52;
+  const uint32_t* rows = reinterpret_cast<const uint32_t*>(g.rows) + g.srow_base[i] * (2 * NP);
+  auto readlane_d = [](double v, int l) {
+    const uint64_t u = __builtin_bit_cast(uint64_t, v);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, l);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), l);
+    return from_words(hi, lo);
+  };
+  // the next step's operands, loaded a step ahead: its row (both planes) and emission row
+  uint32_t nh[KP], nl[KP];
+  double ne[KP];
+  auto prefetch = [&](int s) {  // step s: element x0 + s + 1 = row L - 1 - s
+    const uint32_t* r = rows + (size_t)(L - 1 - s) * (2 * NP) + lane;
+    const double* e = g.et + (size_t)g.obs[x0 + s + 1] * NP + lane;
+#pragma unroll
+    for (int k = 0; k < KP; ++k) {
+      nh[k] = valid[k] ? __builtin_nontemporal_load(r + 64 * k) : NINF_HI;
+      nl[k] = valid[k] ? __builtin_nontemporal_load(r + NP + 64 * k) : 0u;
+      ne[k] = e[64 * k];
+    }
+  };
+  if (ok && L > 0) prefetch(0);
+  int pathreg = 0;
+  for (int s = 0; ok && s < L; ++s) {
+    uint32_t ch[KP], cl[KP];
+    double ce[KP];
+#pragma unroll
+    for (int k = 0; k < KP; ++k) ch[k] = nh[k], cl[k] = nl[k], ce[k] = ne[k];
+    if (s + 1 < L) prefetch(s + 1);
+    const double* arow = g.a + (size_t)cur * NP + lane;
+    double av[KP], w[KP];
+    double m = ninf_d();
+#pragma unroll
+    for (int k = 0; k < KP; ++k) {
+      av[k] = arow[64 * k];
+      w[k] = valid[k] ? from_words(ch[k], cl[k]) + av[k] : ninf_d();
+      m = fmax(m, w[k]);
+    }
+    const double M = wave_max_d(m);
+    int idx = 0;
+#pragma unroll
+    for (int k = KP - 1; k >= 0; --k) {
+      const unsigned long long mask = __ballot(valid[k] && w[k] == M);
+      if (mask) idx = 64 * k + __builtin_ctzll(mask);
+    }
+    double m2 = ninf_d();
+#pragma unroll
+    for (int k = 0; k < KP; ++k) m2 = fmax(m2, (64 * k + lane == idx) ? ninf_d() : w[k]);
+    const double M2 = wave_max_d(m2);
+    ok = M > ninf_d() && M2 * (1.0 - rho) + 2.0 * rho * __builtin_fabs(d) < M * (1.0 + rho);
+    if (!ok) break;  // wave-uniform
+    // the fold's a[cur][idx] and b_idx(o): lane idx & 63 holds them in slot idx >> 6
+    double asel = av[0], esel = ce[0];
+#pragma unroll
+    for (int k = 1; k < KP; ++k)
+      if ((idx >> 6) == k) asel = av[k], esel = ce[k];
+    d = (d + readlane_d(asel, idx & 63)) + readlane_d(esel, idx & 63);
+    cur = idx;
+    const int64_t p = x0 + s + 1;
+    if (lane == (int)(p & 63)) pathreg = cur;
+    if ((p & 63) == 63 || p == end - 1) {
+      const int64_t q = (p & ~(int64_t)63) + lane;
+      if (q > x0 && q <= p) g.path[q] = pathreg;
+    }
+  }
+  if (lane == 0) {
+    g.cert[i] = ok ? 1 : 0;
+    if (ok) {
+      g.score[seq] = d;
+      g.status[seq] = CVK_SEQ_OK;
+    }
+  }
+}
+
 // Max-marginal at one constrained position (f64; max_marginal_f32 in trellis.hip):
 //   beta[i] = max_j(g[j] + a[i,j])  (g = last row of the reversed pass; 0 if no suffix)
 //   mu[i]   = delta_tk[i] + beta[i]
@@ -1890,6 +1998,19 @@ hipError_t launch_t64_resume_rows(const double* last, const int32_t* state, int6
   if (n <= 0) return hipSuccess;
   if (np <= 0 || np > 256) return hipErrorInvalidValue;
   hipLaunchKernelGGL(resume_rows_f64, dim3((unsigned)n), dim3(256), 0, stream, last, state, np, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_t64_suffix_trace(int np, const SuffixTrace64Args& a, int64_t n, hipStream_t stream) {
+  if (n <= 0) return hipSuccess;
+  const dim3 grid((unsigned)((n + 3) / 4)), block(256);
+  switch (np) {
+    case 64: hipLaunchKernelGGL(suffix_trace_f64<1>, grid, block, 0, stream, a, n); break;
+    case 128: hipLaunchKernelGGL(suffix_trace_f64<2>, grid, block, 0, stream, a, n); break;
+    case 192: hipLaunchKernelGGL(suffix_trace_f64<3>, grid, block, 0, stream, a, n); break;
+    case 256: hipLaunchKernelGGL(suffix_trace_f64<4>, grid, block, 0, stream, a, n); break;
+    default: return hipErrorInvalidValue;
+  }
   return hipGetLastError();
 }
 

@@ -33,7 +33,7 @@ EXPORTS = [
     "cv_hmm_ndims", "cv_hmm_bdims", "cv_obs_flatten", "cv_hmm_init_prob", "cv_hmm_init_probs",
     "cv_hmm_transition_prob", "cv_hmm_transitions_to", "cv_hmm_emit_prob", "cv_hmm_emit_probs",
     "cv_decode_batch", "cv_decode_batch_device", "cv_last_timing", "cv_timing_begin", "cv_timing_end",
-    "cv_decode_constrained", "cv_decode_constrained_device", "cv_decode_constrained_exchange",
+    "cv_decode_constrained", "cv_decode_constrained_device", "cv_last_suffix_traced", "cv_decode_constrained_exchange",
     "cv_constrained_pairs", "cv_constrained_partials", "cv_constrained_select", "cv_decode_forced_components", "cv_viterbi_decode",
     "cv_decode_superseq_cp",
     "cv_solver_create", "cv_solver_solve", "cv_solver_get_solution", "cv_solver_get_objective",
@@ -115,6 +115,7 @@ def lib():
         "cv_last_timing": ([P, P], S),
         "cv_timing_begin": ([P], S),
         "cv_timing_end": ([P, P], S),
+        "cv_last_suffix_traced": ([P, P], S),
         "cv_decode_constrained": ([P, I64, P, P, P, I32, P, P, P, P, P, P], S),
         "cv_decode_constrained_device": ([P, I64, P, P, P, P, I32, P, P, P, P, P, P], S),
         "cv_decode_constrained_exchange": ([P, I64, P, P, P, I32, I64, P, P, P, P, P, P, P, P, P, P], S),

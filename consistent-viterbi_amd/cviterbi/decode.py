@@ -259,6 +259,14 @@ def _timing_dict(t):
                 seqs_per_wave=t.mfma_tiles)
 
 
+def last_suffix_traced(hmm: HMM) -> int:
+    """Constrained sequences of the last constrained decode whose forced path came from the
+    certified suffix trace (cv_last_suffix_traced) rather than a second forward pass."""
+    n = ctypes.c_int64()
+    L.check(L.lib().cv_last_suffix_traced(hmm.handle, ctypes.byref(n)))
+    return n.value
+
+
 def last_timing(hmm: HMM) -> dict:
     """Device timings of the last decode call (synchronizes its events)."""
     t = L.Timing()

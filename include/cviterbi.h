@@ -216,6 +216,12 @@ CV_API cv_status cv_decode_constrained_device(cv_hmm* h, int64_t nseq, const int
                                               const int32_t* component, int32_t ncomp, const cv_opts* opts,
                                               int32_t* path_dev, double* score_dev, uint8_t* status_dev,
                                               int32_t* comp_state_out, double* objective_out);
+/* Constrained sequences whose final forced path the last constrained decode on this handle
+ * took from the certified suffix trace (f64, one constrained element, log-probability models:
+ * the path after t1 read off the terms pass's suffix rows, with a rounding-error margin that
+ * proves it is the forced decode's own path) instead of a second forward pass; 0 when the
+ * trace was off (CV_NO_TRACE=1, f32, no kept rows). */
+CV_API cv_status cv_last_suffix_traced(const cv_hmm* h, int64_t* out);
 /* The same decode split at its one exchange step, for a batch sharded over processes/GPUs:
  * 0. cv_constrained_pairs (host only) on the FULL batch: the sorted component pairs (c1 < c2)
  *    that are consecutive constrained elements of some sequence -- the layout every rank
