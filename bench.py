@@ -211,7 +211,9 @@ def bench_configs(dev, stream):
                       "hbm_frac_8d": ((9 * n + 8) * elems + 8 * B) / fwd / HBM_PEAK,
                       "valu_frac": pairs / fwd / F64_PAIR_PEAK})
         else:
-            d["kernel"] = "trellis_fwd_f64 EXT (terms pass + resume decode) + backtracks + exact search"
+            d["kernel"] = ("trellis_fwd_f64 EXT (prefix + suffix passes, suffix rows kept) + exact search + "
+                           "certified suffix trace (suffix_trace_f64) + backtracks")
+            d["suffix_traced"] = cv.last_suffix_traced(h)  # constrained sequences needing no 2nd forward pass
         out[name] = d
         del h, o_d, ob_d, p_d, s_d, st_d
         torch.cuda.empty_cache()
