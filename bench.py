@@ -69,6 +69,8 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-configs", action="store_true", help="skip the configs 2/3/5 extra measurements")
     p.add_argument("--no-verify", action="store_true", help="N>1: skip rank 0's re-decode of the global batch")
+    p.add_argument("--c5-batch", type=int, default=B_TOTAL, help="N>1: sequences of the sharded config-5 leg")
+    p.add_argument("--no-c5-sharded", action="store_true", help="N>1: skip the sharded config-5 leg")
     p.add_argument("--backend", choices=("nccl", "gloo"), default="nccl",
                    help="collective backend for N>1 (nccl = RCCL over xGMI; gloo only to rehearse the "
                         "multi-rank path with several ranks on one GPU)")
@@ -217,6 +219,52 @@ def bench_configs(dev, stream):
         out[name] = d
         del h, o_d, ob_d, p_d, s_d, st_d
         torch.cuda.empty_cache()
+    return out
+
+
+def c5_sharded(dev, world, rank, dist, backend, nseq, reps):
+    """BASELINE config 5 (consistency-constrained decode, "8x MI355X") across the ranks:
+    cviterbi.dist.constrained_decode_sharded -- each rank's contiguous shard through
+    cv_decode_constrained_exchange (terms pass, ONE all-reduce of exact integer partials, the
+    search, the certified-trace resume decode), then the packed gather of paths/scores/statuses
+    to rank 0.  Host arrays in and out (PCIe and the host's pair scan included): end-to-end wall
+    time per call, max over ranks -- not the device-API figure of configs.c5.  Rank 0 checks the
+    gathered result bit for bit against its own single-process cv_decode_constrained of the
+    global batch (cp.rs:95-126 semantics, main.rs:129-133 output)."""
+    import torch
+
+    import cviterbi as cv
+    from cviterbi import dist as cvd
+    from cviterbi import synth
+
+    c = synth.config("c5", nseq)
+    h = cv.HMM(c["pi"], c["a"], c["b"].reshape(N_STATES, 32, 32), device=dev.index)
+    device = dev if backend == "nccl" else None
+    call = (h, c["offsets"], c["obs"], c["component"], 7, dist)
+    got = cvd.constrained_decode_sharded(*call, device=device)  # warmup
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        got = cvd.constrained_decode_sharded(*call, device=device)
+    dist.barrier()
+    el = (time.perf_counter() - t0) / reps
+    tt = torch.tensor([el], dtype=torch.float64, device="cpu" if backend == "gloo" else dev)
+    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    el = float(tt.item())
+    out = None
+    if rank == 0:
+        ref = cv.decode_constrained(h, c["offsets"], c["obs"], c["component"], 7, dtype="f64")
+        equal = all(np.array_equal(np.asarray(x), np.asarray(y)) for x, y in zip(got, ref))
+        B = len(c["offsets"]) - 1
+        out = {"workload": f"config5: N=256, T=512, batch={B} sharded over {world} ranks, one constrained "
+                           "position in half the sequences, K=7, exact f64; host arrays (PCIe included)",
+               "ms_per_decode": el * 1e3, "cells_per_s": B * T_LEN * N_STATES / el, "seqs_per_s": B / el,
+               "reps": reps, "suffix_traced_rank0": cv.last_suffix_traced(h),
+               "check": {"what": "gathered paths/scores/statuses, component states and objective == rank 0's "
+                                 "single-process cv_decode_constrained of the global batch, bit for bit",
+                         "equal": bool(equal)}}
+    dist.barrier()
+    del h
     return out
 
 
@@ -375,6 +423,10 @@ def main():
                              "paths_differ_frac = share of this rank's sequences whose f32 path differs from the "
                              "f64 (reference-exact) path of the same batch"}
 
+    c5s = None
+    if world > 1 and not args.no_c5_sharded:
+        c5s = c5_sharded(dev, world, rank, dist, args.backend, args.c5_batch, 2)
+
     cells_total = B * T_LEN * N_STATES * args.steps
     value = cells_total / el
     ms_step = el * 1e3 / args.steps
@@ -447,6 +499,8 @@ def main():
         out["f32_trellis"] = f32_extra
     if verify is not None:
         out["multi_gpu_check"] = verify
+    if c5s is not None:
+        out["c5_sharded"] = c5s
     if rank == 0 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(pi, a, b, obs, args.cpu_seconds, first)
         out["cpu_baseline"]["gpu_over_cpu"] = value / out["cpu_baseline"]["value"]
@@ -455,6 +509,8 @@ def main():
     checks = []
     if verify is not None:
         checks.append(verify["equal"])
+    if c5s is not None:
+        checks.append(c5s["check"]["equal"])
     if out.get("cpu_baseline", {}).get("check"):
         checks.append(out["cpu_baseline"]["check"]["bit_exact"])
     out["verified"] = bool(checks) and all(checks)

@@ -2387,25 +2387,26 @@ CV_API cv_status cv_decode_constrained_device(cv_hmm* h, int64_t nseq, const int
   if (o.forced) return set_err(CV_EINVAL, "opts->forced is set by the constrained decode itself");
   if (nseq == 0) return CV_OK;
   if ((st = check_batch(h, nseq, offsets_host)) != CV_OK) return st;
-  // components checked and the constrained list built in one host pass
-  std::vector<ConSeq> cs;
-  {
-    const int64_t k = build_conseq_checked(nseq, offsets_host, component, ncomp, cs);
-    if (k >= 0)
-      return set_err(CV_EINVAL, "component[%lld] = %d out of range [-1,%d)", (long long)k, component[k], ncomp);
-  }
   hipStream_t stream = o.stream ? (hipStream_t)o.stream : h->stream;
-  // the host API rejects a bad observation before any term is computed: same here, on the device
+  // the host API rejects a bad observation before any term is computed: same here, on the
+  // device, checked while the host builds the constrained list
   if ((st = h->cs_zero.ensure(8)) != CV_OK) return st;
+  unsigned long long first_bad_obs = 0;
   {
     const hipError_t err = cvk::launch_obs_first_bad(obs_dev, offsets_host[0], offsets_host[nseq], h->V,
                                                      h->cs_zero.as<unsigned long long>(), stream);
     if (err != hipSuccess) return set_err(CV_EDEVICE, "observation check failed: %s", hipGetErrorString(err));
-    unsigned long long first = 0;
-    HIP_TRY(hipMemcpyAsync(&first, h->cs_zero.p, 8, hipMemcpyDeviceToHost, stream));
-    HIP_TRY(hipStreamSynchronize(stream));
-    if (first != ~0ull) return set_err(CV_EINVAL, "obs[%llu] out of range [0,%lld)", first, (long long)h->V);
+    HIP_TRY(hipMemcpyAsync(&first_bad_obs, h->cs_zero.p, 8, hipMemcpyDeviceToHost, stream));
   }
+  // components checked and the constrained list built in one host pass
+  std::vector<ConSeq> cs;
+  const int64_t bad_comp = build_conseq_checked(nseq, offsets_host, component, ncomp, cs);
+  HIP_TRY(hipStreamSynchronize(stream));  // first_bad_obs is a local the copy writes
+  if (bad_comp >= 0)
+    return set_err(CV_EINVAL, "component[%lld] = %d out of range [-1,%d)", (long long)bad_comp, component[bad_comp],
+                   ncomp);
+  if (first_bad_obs != ~0ull)
+    return set_err(CV_EINVAL, "obs[%llu] out of range [0,%lld)", first_bad_obs, (long long)h->V);
   trace_mark("device constrained: checks + constrained list");
   // the unconstrained sequences beside the terms pass (A/B knob, bit-identical: CV_NO_SIDE=1)
   SideJoin side{h};

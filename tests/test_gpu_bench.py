@@ -20,7 +20,7 @@ def test_bench_two_rank_rehearsal(gpu):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", "29561", os.path.join(ROOT, "bench.py"),
            "--gpus", "2", "--steps", "2", "--warmup", "1", "--batch", "2048", "--backend", "gloo",
-           "--no-f32-extra", "--no-configs", "--cpu-seconds", "1"]
+           "--no-f32-extra", "--no-configs", "--cpu-seconds", "1", "--c5-batch", "2048"]
     # own session: on a timeout the launcher AND its ranks are killed (process group)
     p = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env, cwd=ROOT,
                          start_new_session=True)
@@ -42,6 +42,9 @@ def test_bench_two_rank_rehearsal(gpu):
     assert d["multi_gpu_check"]["equal"] is True and d["multi_gpu_check"]["sequences"] == 2048
     assert d["cpu_baseline"]["check"]["bit_exact"] is True and d["cpu_baseline"]["check"]["sequences"] == 64
     assert d["verified"] is True
+    # config 5 sharded over the 2 ranks (exchange + gather) == rank 0's single-process decode
+    c5 = d["c5_sharded"]
+    assert c5["check"]["equal"] is True and c5["ms_per_decode"] > 0 and "sharded over 2 ranks" in c5["workload"]
     r = d["roofline"]
     assert r["bound"] == "valu" and 0 < r["frac"] < 1 and r["frac_f64_bytes"] > r["frac"]
     assert r["roofs"]["valu"]["frac"] > 0
