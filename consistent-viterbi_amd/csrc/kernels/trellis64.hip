@@ -1056,6 +1056,28 @@ __device__ __forceinline__ float wave_max_f32(float v) {
   return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 63));
 }
 
+// The same DPP pattern for f64 (both 32-bit halves move with one control, so a lane always
+// pairs the words of one source lane); the result is uniform (lane 63's, read back).
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ double max_dpp_d(double v) {
+  const uint64_t u = __builtin_bit_cast(uint64_t, v);
+  const int lo = (int)(uint32_t)u, hi = (int)(uint32_t)(u >> 32);
+  const int olo = __builtin_amdgcn_update_dpp(lo, lo, CTRL, ROWMASK, 0xF, false);
+  const int ohi = __builtin_amdgcn_update_dpp(hi, hi, CTRL, ROWMASK, 0xF, false);
+  return fmax(v, from_words((uint32_t)ohi, (uint32_t)olo));
+}
+__device__ __forceinline__ double wave_max_d_dpp(double v) {
+  v = max_dpp_d<0xB1, 0xF>(v);   // quad_perm [1,0,3,2]
+  v = max_dpp_d<0x4E, 0xF>(v);   // quad_perm [2,3,0,1]
+  v = max_dpp_d<0x141, 0xF>(v);  // row_half_mirror
+  v = max_dpp_d<0x140, 0xF>(v);  // row_mirror
+  v = max_dpp_d<0x142, 0xA>(v);  // row_bcast:15 -> rows 1, 3
+  v = max_dpp_d<0x143, 0xC>(v);  // row_bcast:31 -> rows 2, 3
+  const uint64_t u = __builtin_bit_cast(uint64_t, v);
+  return from_words((uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), 63),
+                    (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, 63));
+}
+
 // first index of the wave-wide maximum of s (candidate i = lane + 64k; invalid k excluded)
 template <int KP>
 __device__ __forceinline__ int first_argmax_d(const double (&s)[KP], const bool (&valid)[KP], double& M) {
@@ -1420,7 +1442,7 @@ __global__ __launch_bounds__(256) void suffix_trace_f64(SuffixTrace64Args g, int
       w[k] = valid[k] ? from_words(ch[k], cl[k]) + av[k] : ninf_d();
       m = fmax(m, w[k]);
     }
-    const double M = wave_max_d(m);
+    const double M = wave_max_d_dpp(m);  // DPP: no LDS round trips on the chain
     int idx = 0;
 #pragma unroll
     for (int k = KP - 1; k >= 0; --k) {
@@ -1430,7 +1452,7 @@ __global__ __launch_bounds__(256) void suffix_trace_f64(SuffixTrace64Args g, int
     double m2 = ninf_d();
 #pragma unroll
     for (int k = 0; k < KP; ++k) m2 = fmax(m2, (64 * k + lane == idx) ? ninf_d() : w[k]);
-    const double M2 = wave_max_d(m2);
+    const double M2 = wave_max_d_dpp(m2);
     ok = M > ninf_d() && M2 * (1.0 - rho) + 2.0 * rho * __builtin_fabs(d) < M * (1.0 + rho);
     if (!ok) break;  // wave-uniform
     // the fold's a[cur][idx] and b_idx(o): lane idx & 63 holds them in slot idx >> 6
