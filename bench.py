@@ -248,6 +248,7 @@ def c5_sharded(dev, world, rank, dist, backend, nseq, reps):
         got = cvd.constrained_decode_sharded(*call, device=device)
     dist.barrier()
     el = (time.perf_counter() - t0) / reps
+    traced = cv.last_suffix_traced(h)  # this rank's shard, before rank 0's reference decode below
     tt = torch.tensor([el], dtype=torch.float64, device="cpu" if backend == "gloo" else dev)
     dist.all_reduce(tt, op=dist.ReduceOp.MAX)
     el = float(tt.item())
@@ -259,7 +260,7 @@ def c5_sharded(dev, world, rank, dist, backend, nseq, reps):
         out = {"workload": f"config5: N=256, T=512, batch={B} sharded over {world} ranks, one constrained "
                            "position in half the sequences, K=7, exact f64; host arrays (PCIe included)",
                "ms_per_decode": el * 1e3, "cells_per_s": B * T_LEN * N_STATES / el, "seqs_per_s": B / el,
-               "reps": reps, "suffix_traced_rank0": cv.last_suffix_traced(h),
+               "reps": reps, "suffix_traced_rank0": traced,
                "check": {"what": "gathered paths/scores/statuses, component states and objective == rank 0's "
                                  "single-process cv_decode_constrained of the global batch, bit for bit",
                          "equal": bool(equal)}}

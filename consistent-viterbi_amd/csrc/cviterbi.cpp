@@ -96,8 +96,8 @@ cv_status upload(DevBuf& buf, const void* src, size_t bytes) {
 }
 
 constexpr uint64_t kDefaultWorkspace = 8ull << 30;
-constexpr uint64_t kDefaultWorkspaceT64 = 64ull << 30;
-constexpr size_t kMaxTimedEvents = 1 << 16;  // cv_timing_begin: at most 16,384 chunk launches timed  // config 5 resume decode in one chunk: 3% faster than 40 GiB
+constexpr uint64_t kDefaultWorkspaceT64 = 64ull << 30;  // config 5 resume decode in one chunk: 3% faster than 40 GiB
+constexpr size_t kMaxTimedEvents = 1 << 16;  // cv_timing_begin: at most 16,384 chunk launches timed
 
 }  // namespace
 
@@ -256,10 +256,11 @@ uint64_t free_device_bytes(uint64_t held) {
 }
 
 // The default delta-workspace cap when the caller leaves opts.workspace_bytes at 0: `base`
-// (sized for 288 GB of HBM3E), clamped to 3/4 of what the device can still give this handle's
-// workspace, so a smaller or busier card chunks the batch instead of failing in hipMalloc.
-uint64_t default_workspace_cap(const cv_hmm* h, uint64_t base) {
-  const uint64_t avail = free_device_bytes(h->ws_main.bytes);
+// (sized for 288 GB of HBM3E), clamped to 3/4 of what the device can still give the workspace
+// being sized (`held` = its current bytes, reclaimable), so a smaller or busier card chunks the
+// batch instead of failing in hipMalloc.
+uint64_t default_workspace_cap(uint64_t held, uint64_t base) {
+  const uint64_t avail = free_device_bytes(held);
   if (avail == 0) return base;
   return std::max<uint64_t>(std::min<uint64_t>(base, avail / 4 * 3), 256ull << 20);
 }
@@ -654,7 +655,7 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
   // f64 trellis: 2 KiB of delta per element at N = 256 and >= 16,384 sequences per launch for
   // 8 sequences per wave, so its default cap is larger (HBM3E: 288 GB per GPU)
   const uint64_t cap = o.workspace_bytes ? o.workspace_bytes
-                                         : default_workspace_cap(h, use_t64 ? kDefaultWorkspaceT64 : kDefaultWorkspace);
+                                         : default_workspace_cap(w_main.bytes, use_t64 ? kDefaultWorkspaceT64 : kDefaultWorkspace);
   const uint64_t per_elem = use_trellis ? (uint64_t)(wave ? h->npw : h->np) * 4
                            : (use_t64 && !t64cp) ? (uint64_t)h->np64 * 8
                                        : (uint64_t)h->N * 2;
@@ -1351,8 +1352,10 @@ cv_status constrained_validate(cv_hmm* h, int64_t nseq, const int64_t* offsets, 
 struct PrefixKeep {
   bool kept = false;
   std::vector<int64_t> seq, t1, row_base;  // per terms slot i
-  // f64: the suffix pass's rows of slots [0, n1) (one constrained element each) are kept too
-  // (h->rs_srows, slot i from row srow_base[i]) for the certified suffix trace
+  // f64: the suffix pass's rows are kept too (h->rs_srows, slot i from row srow_base[i]) for
+  // the certified suffix trace, which reads the one-element slots [0, n1) only; the pass writes
+  // every slot's rows, so the multi-element slots' rows are stored (and counted in the
+  // free-memory check) as well -- few at config 5, where every sequence has one element
   bool suffix_kept = false;
   int64_t n1 = 0;
 };
@@ -1423,6 +1426,9 @@ cv_status constrained_partials_locked(cv_hmm* h, int64_t nseq, const int64_t* of
   const int np = f64 ? h->np64 : h->np;
   const size_t rb = f64 ? 8 : 4;  // bytes per term
   hipStream_t stream = o.stream ? (hipStream_t)o.stream : h->stream;
+  // h->ws_order below is the main workspace's: a cv_decode_batch_device call still running on
+  // another stream reads it (cviterbi.h promises cross-stream workspace ordering)
+  if (h->ws_rec) HIP_TRY(hipStreamWaitEvent(stream, h->ws_done, 0));
   const int64_t base = offsets[0], total = offsets[nseq];
   // observations on the device: the caller's (device API, validated) or staged here
   const int32_t* dobs = obs_dev;
@@ -1937,10 +1943,15 @@ cv_status side_decode_launch(cv_hmm* h, int64_t nseq, const int64_t* offsets_hos
   cv_status st;
   if (!sd.done && hipEventCreateWithFlags(&sd.done, hipEventDisableTiming) != hipSuccess)
     return set_err(CV_EDEVICE, "hipEventCreate failed");
-  if ((st = sd.idx.ensure(sd.idx_host.size() * 8)) != CV_OK) return st;
-  if ((st = sd.obs2.ensure((size_t)std::max<int64_t>(total2, 1) * 4)) != CV_OK) return st;
-  if ((st = sd.path2.ensure((size_t)std::max<int64_t>(total2, 1) * 4)) != CV_OK) return st;
-  if ((st = sd.res2.ensure((size_t)nu * 9)) != CV_OK) return st;
+  // no room for the side buffers: the final forced decode covers these sequences as well
+  // (launched stays false; same results)
+  if ((st = sd.idx.ensure(sd.idx_host.size() * 8)) != CV_OK || (st = sd.obs2.ensure((size_t)std::max<int64_t>(total2, 1) * 4)) != CV_OK ||
+      (st = sd.path2.ensure((size_t)std::max<int64_t>(total2, 1) * 4)) != CV_OK ||
+      (st = sd.res2.ensure((size_t)nu * 9)) != CV_OK) {
+    if (st != CV_ENOMEM) return st;
+    g_err.clear();
+    return CV_OK;
+  }
   // the side stream starts behind everything the caller had queued on its stream when the
   // constrained decode began (h->side.start, recorded then), not behind the term launches
   (void)stream;
@@ -1959,8 +1970,16 @@ cv_status side_decode_launch(cv_hmm* h, int64_t nseq, const int64_t* offsets_hos
   o2.forced = nullptr;
   o2.rescore_f64 = 0;  // f64: the decode's score is the reference's
   if ((st = decode_device(h, nu, off2, off2_d, sd.obs2.as<int32_t>(), o2, sd.path2.as<int32_t>(), score2, status2,
-                          sd.stream, nullptr, /*side_ws=*/true)) != CV_OK)
-    return st;
+                          sd.stream, nullptr, /*side_ws=*/true)) != CV_OK) {
+    if (st != CV_ENOMEM) return st;
+    // the side workspace did not fit beside the terms pass's buffers: drop the side decode (its
+    // staging kernel wrote only side buffers) and let the final forced decode cover these
+    // sequences -- the same results, no CV_ENOMEM for the caller
+    HIP_TRY(hipStreamSynchronize(sd.stream));
+    *launched = false;
+    g_err.clear();
+    return CV_OK;
+  }
   err = cvk::launch_scatter_suffix(cstart_d, off2_d, cseq_d, sd.path2.as<int32_t>(), score2, status2, path_dev,
                                    score_dev, status_dev, nu, sd.stream);
   if (err != hipSuccess) return set_err(CV_EDEVICE, "side scatter failed: %s", hipGetErrorString(err));
@@ -2388,6 +2407,9 @@ CV_API cv_status cv_decode_constrained_device(cv_hmm* h, int64_t nseq, const int
   if (nseq == 0) return CV_OK;
   if ((st = check_batch(h, nseq, offsets_host)) != CV_OK) return st;
   hipStream_t stream = o.stream ? (hipStream_t)o.stream : h->stream;
+  // the handle's shared buffers (ws_order, cs_zero, st_status) may still be in use by a
+  // cv_decode_batch_device call on another stream: wait for it on this one
+  if (h->ws_rec) HIP_TRY(hipStreamWaitEvent(stream, h->ws_done, 0));
   // the host API rejects a bad observation before any term is computed: same here, on the
   // device, checked while the host builds the constrained list
   if ((st = h->cs_zero.ensure(8)) != CV_OK) return st;
