@@ -226,6 +226,9 @@ struct cv_hmm {
   int32_t last_mt = -1;
   uint64_t last_explored = 0;
   int64_t last_traced = 0;  // constrained sequences the last resume flow certified (suffix trace)
+  // the last cv_decode_superseq_cp: parallel chain ran (1/0), sequences certified, sequences in
+  // serial-chain runs, runs, certified folds done by the quantised sum
+  int64_t last_chain[5] = {0, 0, 0, 0, 0};
 
   ~cv_hmm() {
     for (auto e : ev) (void)hipEventDestroy(e);
@@ -571,7 +574,9 @@ cvk::BacktrackArgs make_bt_args(cv_hmm* h, unsigned char* wsb, const int64_t* of
 cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, const int64_t* offsets_dev,
                         const int32_t* obs_dev, const cv_opts& o, int32_t* path_dev, double* score_dev,
                         uint8_t* status_dev, hipStream_t stream, const void* resume_rows = nullptr,
-                        bool side_ws = false) {
+                        bool side_ws = false, double* cp_cert = nullptr) {
+  // cp_cert (the parallel CPSolver chain, row-A0 f64 trellis only): after each chunk's
+  // backtrack, cp_cert_f64 reads the chunk's rows and paths -> [nseq][2] certificates
   // side_ws: the handle's second workspace (h->side), no timing / last-call bookkeeping -- a
   // decode running beside another decode_device call of the same handle on another stream
   DevBuf& w_main = side_ws ? h->side.main : h->ws_main;
@@ -899,7 +904,7 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
         err = cvk::launch_t64_cp_fwd(h->np64, spw, fa, n, stream);
       } else {
         const cvk::T64BtArgs ba = t64_bt_args(c, wsb);
-        fused_chunk = cvk::t64_wave_fusable(h->np64, fa, ba);
+        fused_chunk = !cp_cert && cvk::t64_wave_fusable(h->np64, fa, ba);
         err = fused_chunk ? cvk::launch_t64_wave_fused(fa, ba, n, stream)  // N <= 64: backtrack fused
                           : cvk::launch_t64_fwd(h->np64, spw, fa, n, stream);
       }
@@ -975,6 +980,21 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
       err = fused_chunk ? hipSuccess
                         : cvk::launch_t64_bt(h->np64, t64_bt_args(c, wsb), n, bts,
                                              (serial || ci + 1 == chunks.size()) ? 0 : std::max(h->cus, 1));
+      if (err == hipSuccess && cp_cert) {
+        cvk::CpCert64Args ca{};
+        ca.delta = reinterpret_cast<const double*>(wsb);
+        ca.delta_elem_base = offsets_host[c.first];
+        ca.at = h->q_at.as<double>();
+        ca.offsets = offsets_dev;
+        ca.order = order_dev;
+        ca.seq_begin = c.first;
+        ca.seq_end = c.second;
+        ca.nstates = h->N;
+        ca.path = path_dev;
+        ca.status = status_dev;
+        ca.out = cp_cert;
+        err = cvk::launch_cp_cert(h->np64, ca, bts);
+      }
     } else if (o.dtype == CV_DTYPE_F64) {
       cvk::GenericBtArgs<double> ba{};
       ba.psi = reinterpret_cast<const uint16_t*>(wsb);
@@ -2564,6 +2584,12 @@ cv_status sum_timing(cv_hmm* h, size_t eb, int64_t launches, cv_timing* out) {
 }
 }  // namespace
 
+CV_API cv_status cv_last_superseq_stats(const cv_hmm* h, int64_t* out) {
+  if (!h || !out) return set_err(CV_EINVAL, "null argument");
+  for (int q = 0; q < 5; ++q) out[q] = h->last_chain[q];
+  return CV_OK;
+}
+
 CV_API cv_status cv_last_suffix_traced(const cv_hmm* h, int64_t* out) {
   if (!h || !out) return set_err(CV_EINVAL, "null argument");
   *out = h->last_traced;
@@ -2625,10 +2651,51 @@ CV_API cv_status cv_viterbi_decode(cv_hmm* h, int64_t T, const int32_t* obs, int
 }  // extern "C"
 
 namespace {
+// The chain's segmented backtrack (kernels/chain.hip) over psi [L][NP] from `end_state` at the
+// last element: pass 1 maps every segment's last-element state to the state before it for all
+// NP states (cp_chain_seg_map), the host follows the maps from the end state, pass 2 writes
+// each segment's path into path_dev[0, L).
+cv_status chain_backtrack(cv_hmm* h, const uint16_t* psi, int64_t L, int32_t end_state, int32_t* path_dev,
+                          hipStream_t stream) {
+  const int NP = h->np64;
+  // segments: ~8,192 of them (>= 256 elements each) for the parallel passes
+  const int64_t seg = std::max<int64_t>(256, (L + 8191) / 8192);
+  const int64_t nseg = (L + seg - 1) / seg;
+  DevBuf d_map, d_end;
+  cv_status st;
+  if ((st = d_map.ensure((size_t)nseg * NP * 2)) != CV_OK) return st;
+  if ((st = d_end.ensure((size_t)nseg * 4)) != CV_OK) return st;
+  cvk::CpChainBtArgs b{};
+  b.psi = psi;
+  b.np = NP;
+  b.len = L;
+  b.seg = seg;
+  b.nseg = nseg;
+  b.map = d_map.as<uint16_t>();
+  b.end_state = d_end.as<int32_t>();
+  b.path = path_dev;
+  hipError_t err = cvk::launch_cp_chain_seg_map(b, stream);
+  if (err != hipSuccess) return set_err(CV_EDEVICE, "chain backtrack (maps) failed: %s", hipGetErrorString(err));
+  std::vector<uint16_t> map((size_t)nseg * NP);
+  if (nseg > 1) {
+    HIP_TRY(hipMemcpyAsync(map.data(), d_map.p, map.size() * 2, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipStreamSynchronize(stream));
+  }
+  std::vector<int32_t> end((size_t)nseg);
+  int32_t s = end_state;
+  for (int64_t k = nseg - 1; k >= 0; --k) {
+    end[(size_t)k] = s;
+    if (k > 0) s = map[(size_t)k * NP + s];
+  }
+  HIP_TRY(hipMemcpyAsync(d_end.p, end.data(), (size_t)nseg * 4, hipMemcpyHostToDevice, stream));
+  err = cvk::launch_cp_chain_seg_path(b, stream);
+  if (err != hipSuccess) return set_err(CV_EDEVICE, "chain backtrack (paths) failed: %s", hipGetErrorString(err));
+  HIP_TRY(hipStreamSynchronize(stream));  // `end` is a local buffer
+  return CV_OK;
+}
+
 // cv_decode_superseq_cp for N <= 256: the chain forward (cp_chain_wg) writes psi [L][NP] u16
-// and the final state; the backtrack runs in segments: pass 1 maps every segment's last-state
-// to the state before it for all NP states (cp_chain_seg_map), the host follows the maps from
-// the final state, pass 2 writes each segment's path (cp_chain_seg_path).
+// and the final state, then the segmented backtrack (chain_backtrack).
 cv_status superseq_cp_wg(cv_hmm* h, int64_t L, const int32_t* obs, const std::vector<uint8_t>& first,
                          int32_t* path_out, double* objective_out) {
   cv_status st;
@@ -2642,7 +2709,7 @@ cv_status superseq_cp_wg(cv_hmm* h, int64_t L, const int32_t* obs, const std::ve
                    "free): decode it in parts or per sequence (solver kind gpu-cp-seq)",
                    (long long)L, psi_bytes / 1e9, avail / 1e9);
   hipStream_t stream = h->stream;
-  DevBuf d_obs, d_first, d_psi, d_path, d_out, d_map, d_end;
+  DevBuf d_obs, d_first, d_psi, d_path, d_out;
   if ((st = d_obs.ensure((size_t)L * 4)) != CV_OK) return st;
   if ((st = d_first.ensure((size_t)L)) != CV_OK) return st;
   if ((st = d_psi.ensure((size_t)psi_bytes)) != CV_OK) return st;
@@ -2669,37 +2736,284 @@ cv_status superseq_cp_wg(cv_hmm* h, int64_t L, const int32_t* obs, const std::ve
   *objective_out = out[0];
   int32_t fs;
   std::memcpy(&fs, &out[1], 4);
-  // segments: ~8,192 of them (>= 256 elements each) for the parallel passes
-  const int64_t seg = std::max<int64_t>(256, (L + 8191) / 8192);
-  const int64_t nseg = (L + seg - 1) / seg;
-  if ((st = d_map.ensure((size_t)nseg * NP * 2)) != CV_OK) return st;
-  if ((st = d_end.ensure((size_t)nseg * 4)) != CV_OK) return st;
-  cvk::CpChainBtArgs b{};
-  b.psi = d_psi.as<uint16_t>();
-  b.np = NP;
-  b.len = L;
-  b.seg = seg;
-  b.nseg = nseg;
-  b.map = d_map.as<uint16_t>();
-  b.end_state = d_end.as<int32_t>();
-  b.path = d_path.as<int32_t>();
-  err = cvk::launch_cp_chain_seg_map(b, stream);
-  if (err != hipSuccess) return set_err(CV_EDEVICE, "chain backtrack (maps) failed: %s", hipGetErrorString(err));
-  std::vector<uint16_t> map((size_t)nseg * NP);
-  HIP_TRY(hipMemcpyAsync(map.data(), d_map.p, map.size() * 2, hipMemcpyDeviceToHost, stream));
-  HIP_TRY(hipStreamSynchronize(stream));
-  std::vector<int32_t> end((size_t)nseg);
-  int32_t s = fs;
-  for (int64_t k = nseg - 1; k >= 0; --k) {
-    end[(size_t)k] = s;
-    if (k > 0) s = map[(size_t)k * NP + s];
-  }
-  HIP_TRY(hipMemcpyAsync(d_end.p, end.data(), (size_t)nseg * 4, hipMemcpyHostToDevice, stream));
-  err = cvk::launch_cp_chain_seg_path(b, stream);
-  if (err != hipSuccess) return set_err(CV_EDEVICE, "chain backtrack (paths) failed: %s", hipGetErrorString(err));
+  if ((st = chain_backtrack(h, d_psi.as<uint16_t>(), L, fs, d_path.as<int32_t>(), stream)) != CV_OK) return st;
   HIP_TRY(hipMemcpyAsync(path_out, d_path.p, (size_t)L * 4, hipMemcpyDeviceToHost, stream));
   HIP_TRY(hipStreamSynchronize(stream));
   if (!(*objective_out > -INFINITY))
+    return set_err(CV_EINFEASIBLE, "no finite-probability path through the super-sequence (cp.rs:87 asserts)");
+  return CV_OK;
+}
+
+// ---- the parallel chain (DESIGN.md §3 "parallel CPSolver chain") -------------------------
+// The chain couples sequence k to sequences 0..k-1 only through M, the running maximum its
+// start values carry (fl(M + fl(pi + b)) when the previous row's maximum is clean).  So:
+//  1. every sequence is decoded ON ITS OWN by the row-A0 f64 trellis (the batch hot path, all
+//     sequences in parallel) and cp_cert_f64 reduces its path's gaps to a certificate rho
+//     (trellis64.h: the row-A0 path is the chain's path in sequence k at offset M whenever
+//     rho > U = 2^-52 (|M| + |S_k| + 16));
+//  2. the host walks the sequences in order: a certified sequence's maximum is the CP fold of
+//     its path from M -- M + q 2^(e-52) with cp_quant_f64's quantised arc sum q when M and the
+//     sequence's values share the binade 2^e predicted from the per-sequence optima, else
+//     element by element -- and its end state is its path's; the boundary into the next
+//     sequence must be clean (gF);
+//  3. an uncertified sequence (near ties at the chain's magnitude, rho <= U) runs through the
+//     serial chain kernel itself (cp_chain_wg) from the exact previous row -- a synthetic one
+//     (M at the previous end state, -inf elsewhere: what a clean boundary sees) or the previous
+//     run's last row -- and consecutive such sequences form one run, backtracked from the state
+//     the next sequence's boundary picks.
+// Bit-identical to the serial chain by construction (tests: the serial chain, CV_CHAIN_PAR=0,
+// and the C oracle cvo_cp_superseq_f64).  Models with entries outside [-2^80, 0], infeasible
+// sequences or N > 256: *applied = false (the caller runs the serial chain).
+// Knobs (bit-identical): CV_CHAIN_PAR=0 (serial chain), CV_CHAIN_PAR_FORCE=m (every m-th
+// non-empty sequence taken as uncertified: exercises the runs).
+cv_status superseq_cp_par(cv_hmm* h, int64_t nseq, const int64_t* offsets, const int32_t* obs, int32_t* path_out,
+                          double* objective_out, bool* applied) {
+  *applied = false;
+  cv_status st;
+  if ((st = ensure_t64_tables(h)) != CV_OK) return st;
+  if (!h->t64_nonpos || !cvk::t64_padded_states(h->N)) return CV_OK;
+  const int N = h->N, NP = h->np64;
+  const int64_t V = h->V;
+  const int64_t base = offsets[0], L = offsets[nseq] - base;
+  hipStream_t stream = h->stream;
+  trace_mark("chain: start");
+  std::vector<int64_t> off((size_t)nseq + 1);
+  int64_t maxT = 0;
+  for (int64_t k = 0; k <= nseq; ++k) off[(size_t)k] = offsets[k] - base;
+  for (int64_t k = 0; k < nseq; ++k) maxT = std::max(maxT, off[(size_t)k + 1] - off[(size_t)k]);
+  // 1. the per-sequence row-A0 decode with certificates
+  DevBuf d_off, d_obs, d_path, d_res, d_cert;
+  if ((st = d_off.ensure((size_t)(nseq + 1) * 8)) != CV_OK) return st;
+  if ((st = d_obs.ensure((size_t)L * 4)) != CV_OK) return st;
+  if ((st = d_path.ensure((size_t)L * 4)) != CV_OK) return st;
+  if ((st = d_res.ensure((size_t)nseq * 9)) != CV_OK) return st;
+  if ((st = d_cert.ensure((size_t)nseq * 16)) != CV_OK) return st;
+  HIP_TRY(hipMemcpyAsync(d_off.p, off.data(), off.size() * 8, hipMemcpyHostToDevice, stream));
+  HIP_TRY(hipMemcpyAsync(d_obs.p, obs + base, (size_t)L * 4, hipMemcpyHostToDevice, stream));
+  double* d_score = d_res.as<double>();
+  uint8_t* d_status = reinterpret_cast<uint8_t*>(d_score + nseq);
+  cv_opts o = default_opts();
+  o.dtype = CV_DTYPE_F64;
+  o.assoc = CV_ASSOC_VITERBI;
+  o.kernel = CV_KERNEL_TRELLIS_F64;
+  o.rescore_f64 = 0;
+  o.stream = stream;
+  if ((st = decode_device(h, nseq, off.data(), d_off.as<int64_t>(), d_obs.as<int32_t>(), o, d_path.as<int32_t>(),
+                          d_score, d_status, stream, nullptr, false, d_cert.as<double>())) != CV_OK)
+    return st;
+  std::vector<double> score((size_t)nseq), cert((size_t)nseq * 2);
+  std::vector<uint8_t> status((size_t)nseq);
+  HIP_TRY(hipMemcpyAsync(path_out, d_path.p, (size_t)L * 4, hipMemcpyDeviceToHost, stream));
+  HIP_TRY(hipMemcpyAsync(score.data(), d_score, (size_t)nseq * 8, hipMemcpyDeviceToHost, stream));
+  HIP_TRY(hipMemcpyAsync(status.data(), d_status, (size_t)nseq, hipMemcpyDeviceToHost, stream));
+  HIP_TRY(hipMemcpyAsync(cert.data(), d_cert.p, (size_t)nseq * 16, hipMemcpyDeviceToHost, stream));
+  HIP_TRY(hipStreamSynchronize(stream));
+  trace_mark("chain: row-A0 decode + certificates");
+  for (int64_t k = 0; k < nseq; ++k)
+    if (status[(size_t)k] != CV_SEQ_OK && status[(size_t)k] != CV_SEQ_EMPTY) return CV_OK;  // serial chain
+  // 2a. predicted binades and the quantised folds of every path
+  std::vector<int32_t> ebin((size_t)nseq, cvk::CVK_NO_BINADE);
+  {
+    double mp = 0.0;
+    for (int64_t k = 0; k < nseq; ++k) {
+      if (off[(size_t)k + 1] == off[(size_t)k]) continue;
+      const double em = std::fabs(mp), sk = std::fabs(score[(size_t)k]);
+      if (em >= 0x1p12) {
+        const int e = std::ilogb(em);
+        // the prediction is off by far less than 2^-20 relative: both ends of the sequence's
+        // value range stay in the binade with that margin
+        if (std::ilogb(em * (1.0 - 0x1p-20)) == e && std::ilogb((em + sk + 16.0) * (1.0 + 0x1p-20)) == e)
+          ebin[(size_t)k] = e;
+      }
+      mp -= sk;
+    }
+  }
+  DevBuf d_ebin, d_q;
+  if ((st = d_ebin.ensure((size_t)nseq * 4)) != CV_OK) return st;
+  if ((st = d_q.ensure((size_t)nseq * 9)) != CV_OK) return st;
+  HIP_TRY(hipMemcpyAsync(d_ebin.p, ebin.data(), (size_t)nseq * 4, hipMemcpyHostToDevice, stream));
+  {
+    cvk::CpQuant64Args qa{};
+    qa.a = h->q_a.as<double>();
+    qa.pi = h->q_pi.as<double>();
+    qa.et = h->q_et.as<double>();
+    qa.np = NP;
+    qa.offsets = d_off.as<int64_t>();
+    qa.obs = d_obs.as<int32_t>();
+    qa.path = d_path.as<int32_t>();
+    qa.ebin = d_ebin.as<int32_t>();
+    qa.nseq = nseq;
+    qa.q = d_q.as<long long>();
+    qa.tie = reinterpret_cast<uint8_t*>(d_q.as<long long>() + nseq);
+    const hipError_t err = cvk::launch_cp_quant(qa, stream);
+    if (err != hipSuccess) return set_err(CV_EDEVICE, "chain quantised folds failed: %s", hipGetErrorString(err));
+  }
+  std::vector<long long> qv((size_t)nseq);
+  std::vector<uint8_t> tie((size_t)nseq);
+  HIP_TRY(hipMemcpyAsync(qv.data(), d_q.p, (size_t)nseq * 8, hipMemcpyDeviceToHost, stream));
+  HIP_TRY(hipMemcpyAsync(tie.data(), d_q.as<long long>() + nseq, (size_t)nseq, hipMemcpyDeviceToHost, stream));
+  HIP_TRY(hipStreamSynchronize(stream));
+  trace_mark("chain: quantised folds");
+  // 2b/3. the walk
+  double pimax = 0.0;
+  for (double x : h->pi)
+    if (std::isfinite(x)) pimax = std::max(pimax, std::fabs(x));
+  const int force_m = [] {
+    const char* e = getenv("CV_CHAIN_PAR_FORCE");
+    return e ? std::max(0, atoi(e)) : 0;
+  }();
+  const int32_t* P = path_out;  // the row-A0 paths (element index relative to base)
+  const int32_t* ob = obs + base;
+  auto fold_elems = [&](int64_t k, double M) {  // the CP fold of sequence k's path from M
+    const int64_t e0 = off[(size_t)k], T = off[(size_t)k + 1] - e0;
+    int32_t p = P[e0];
+    double d = M + (h->pi[(size_t)p] + h->b[(size_t)p * V + ob[e0]]);
+    for (int64_t t = 1; t < T; ++t) {
+      const int32_t c = P[e0 + t];
+      d = d + (h->a[(size_t)p * N + c] + h->b[(size_t)c * V + ob[e0 + t]]);
+      p = c;
+    }
+    return d;
+  };
+  // run state: the chain kernel over consecutive uncertified sequences
+  DevBuf d_first, d_rpsi, d_rows, d_small, d_rpath;
+  if ((st = d_first.ensure((size_t)std::max<int64_t>(maxT, 1))) != CV_OK) return st;
+  HIP_TRY(hipMemsetAsync(d_first.p, 0, (size_t)std::max<int64_t>(maxT, 1), stream));
+  HIP_TRY(hipMemsetAsync(d_first.p, 1, 1, stream));  // one sequence per launch: its element 0 starts it
+  if ((st = d_rows.ensure((size_t)NP * 8 * 3)) != CV_OK) return st;
+  if ((st = d_small.ensure(16)) != CV_OK) return st;
+  double* row_in = d_rows.as<double>();  // synthetic start row
+  double* row_a = row_in + NP;           // the run's last rows (ping-pong)
+  double* row_b = row_a + NP;
+  std::vector<double> row_host((size_t)NP), syn((size_t)NP);
+  bool in_run = false;
+  int64_t run_e0 = 0, run_len = 0, runs = 0, run_seqs = 0, ncert = 0, nquant = 0;
+  int64_t psi_cap = 0;
+  int32_t run_arg = 0;  // first argmax of the run's last row
+  enum { NONE, CERT, RUN } prev = NONE;
+  int32_t prev_end = 0;
+  double M = 0.0;
+  auto end_run = [&](int32_t end_state) -> cv_status {
+    if ((st = d_rpath.ensure((size_t)run_len * 4)) != CV_OK) return st;
+    if ((st = chain_backtrack(h, d_rpsi.as<uint16_t>(), run_len, end_state, d_rpath.as<int32_t>(), stream)) != CV_OK)
+      return st;
+    HIP_TRY(hipMemcpyAsync(path_out + run_e0, d_rpath.p, (size_t)run_len * 4, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipStreamSynchronize(stream));
+    in_run = false;
+    return CV_OK;
+  };
+  auto run_step = [&](int64_t k) -> cv_status {  // sequence k through the serial chain kernel
+    const int64_t e0 = off[(size_t)k], T = off[(size_t)k + 1] - e0;
+    const double* init = nullptr;
+    if (!in_run) {
+      in_run = true;
+      run_e0 = e0;
+      run_len = 0;
+      ++runs;
+      if (prev == CERT) {  // what a clean boundary after a certified sequence sees
+        std::fill(syn.begin(), syn.end(), -INFINITY);
+        syn[(size_t)prev_end] = M;
+        HIP_TRY(hipMemcpyAsync(row_in, syn.data(), (size_t)NP * 8, hipMemcpyHostToDevice, stream));
+        init = row_in;
+      }
+    } else {
+      init = row_a;
+    }
+    if (run_len + T > psi_cap) {  // grow the run's psi rows (rare: long runs)
+      const int64_t cap = std::max<int64_t>(2 * psi_cap, std::max<int64_t>(run_len + T, 4 * maxT));
+      DevBuf nb;
+      if ((st = nb.ensure((size_t)cap * NP * 2)) != CV_OK) return st;
+      if (run_len > 0)
+        HIP_TRY(hipMemcpyAsync(nb.p, d_rpsi.p, (size_t)run_len * NP * 2, hipMemcpyDeviceToDevice, stream));
+      HIP_TRY(hipStreamSynchronize(stream));
+      std::swap(nb.p, d_rpsi.p);
+      std::swap(nb.bytes, d_rpsi.bytes);
+      psi_cap = cap;
+    }
+    if (!init) HIP_TRY(hipMemsetAsync(d_rpsi.as<uint16_t>() + run_len * NP, 0, (size_t)NP * 2, stream));
+    cvk::CpChainWgArgs g{};
+    g.pi = h->q_pi.as<double>();
+    g.a = h->q_a.as<double>();
+    g.et = h->q_et.as<double>();
+    g.obs = d_obs.as<int32_t>() + e0;
+    g.first = d_first.as<uint8_t>();
+    g.len = T;
+    g.nstates = N;
+    g.psi = d_rpsi.as<uint16_t>() + run_len * NP;
+    g.objective = d_small.as<double>();
+    g.final_state = reinterpret_cast<int32_t*>(d_small.as<double>() + 1);
+    g.init_row = init;
+    g.final_row = row_b;
+    const hipError_t err = cvk::launch_cp_chain_wg(NP, g, stream);
+    if (err != hipSuccess) return set_err(CV_EDEVICE, "chain run launch failed: %s", hipGetErrorString(err));
+    double out[2];
+    HIP_TRY(hipMemcpyAsync(out, d_small.p, 16, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipMemcpyAsync(row_host.data(), row_b, (size_t)NP * 8, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipStreamSynchronize(stream));
+    std::swap(row_a, row_b);
+    M = out[0];
+    std::memcpy(&run_arg, &out[1], 4);
+    run_len += T;
+    ++run_seqs;
+    prev = RUN;
+    return CV_OK;
+  };
+  // the last row of a run is clean for a start whose values reach magnitude `mag`: no earlier
+  // state's value can round onto the maximum when pi[j] is added (utils.rs:32-35)
+  auto run_clean = [&](double mag) {
+    const double gap = 0x1p-51 * (std::fabs(M) + mag);
+    for (int32_t i = 0; i < run_arg; ++i)
+      if (!(M - row_host[(size_t)i] > gap)) return false;
+    return true;
+  };
+  std::vector<int64_t> ks;
+  for (int64_t k = 0; k < nseq; ++k)
+    if (off[(size_t)k + 1] > off[(size_t)k]) ks.push_back(k);
+  for (size_t x = 0; x < ks.size(); ++x) {
+    const int64_t k = ks[x];
+    const int64_t T = off[(size_t)k + 1] - off[(size_t)k];
+    const double S = std::fabs(score[(size_t)k]);
+    const double snext = x + 1 < ks.size() ? std::fabs(score[(size_t)ks[x + 1]]) : 0.0;
+    const double rho = cert[(size_t)k * 2], gF = cert[(size_t)k * 2 + 1];
+    const double U = 0x1p-52 * (std::fabs(M) + S + 16.0);
+    bool ok = rho > U && !(force_m > 0 && (int64_t)(x % (size_t)force_m) == force_m - 1);
+    if (ok && prev == RUN && !run_clean(S + pimax + 16.0)) ok = false;
+    if (ok) {
+      double Mn;
+      const int e = ebin[(size_t)k];
+      if (e != cvk::CVK_NO_BINADE && !tie[(size_t)k] && M != 0.0 && std::ilogb(std::fabs(M)) == e &&
+          std::fabs((double)qv[(size_t)k]) < 0x1p53) {
+        Mn = M + std::ldexp((double)qv[(size_t)k], e - 52);
+        if (std::ilogb(std::fabs(Mn)) != e) Mn = fold_elems(k, M);  // left the binade
+        else ++nquant;
+      } else {
+        Mn = fold_elems(k, M);
+      }
+      // the boundary into the next sequence: its start values must not merge with this
+      // sequence's maximum (the exact final gap, less the chain's error, beats 2 ulps there)
+      const double U1 = 0x1p-52 * (std::fabs(Mn) + snext + pimax + 16.0);
+      if (x + 1 < ks.size() && !(gF - 3.0 * (double)T * U > 2.0 * U1)) ok = false;
+      if (ok) {
+        if (in_run && (st = end_run(run_arg)) != CV_OK) return st;
+        M = Mn;
+        prev = CERT;
+        prev_end = P[off[(size_t)k + 1] - 1];
+        ++ncert;
+        continue;
+      }
+    }
+    if ((st = run_step(k)) != CV_OK) return st;
+  }
+  if (in_run && (st = end_run(run_arg)) != CV_OK) return st;  // cp.rs:86: first argmax of the last row
+  trace_mark("chain: walk + runs");
+  h->last_chain[0] = 1;
+  h->last_chain[1] = ncert;
+  h->last_chain[2] = run_seqs;
+  h->last_chain[3] = runs;
+  h->last_chain[4] = nquant;
+  *objective_out = M;
+  *applied = true;
+  if (!(M > -INFINITY))
     return set_err(CV_EINFEASIBLE, "no finite-probability path through the super-sequence (cp.rs:87 asserts)");
   return CV_OK;
 }
@@ -2732,6 +3046,14 @@ CV_API cv_status cv_decode_superseq_cp(cv_hmm* h, int64_t nseq, const int64_t* o
   // (kernels/chain.hip), then the parallel segmented backtrack; N > 256 (or CV_CHAIN_OLD=1, an
   // A/B knob, bit-identical): one thread per state (cp_superseq_chain)
   const char* old_env = getenv("CV_CHAIN_OLD");
+  const char* par_env = getenv("CV_CHAIN_PAR");  // read per call: tests flip it within one process
+  h->last_chain[0] = 0;
+  for (int q = 1; q < 5; ++q) h->last_chain[q] = 0;
+  if (cvk::t64_padded_states(h->N) && !(old_env && *old_env == '1') && !(par_env && *par_env == '0')) {
+    bool applied = false;
+    st = superseq_cp_par(h, nseq, offsets, obs, path_out, objective_out, &applied);
+    if (st != CV_OK || applied) return st;
+  }
   if (cvk::t64_padded_states(h->N) && !(old_env && *old_env == '1'))
     return superseq_cp_wg(h, L, obs + base, first, path_out, objective_out);
   if ((st = ensure_f64_tables(h)) != CV_OK) return st;

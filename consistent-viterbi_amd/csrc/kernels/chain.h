@@ -17,8 +17,14 @@ struct CpChainWgArgs {
   int64_t len;
   int nstates;
   uint16_t* psi;         // [len][NP] first argmax per (element, state); row 0 unused
+                         // unless init_row is set
   double* objective;     // [1] max of the last row (cp.rs:140)
   int32_t* final_state;  // [1] its first argmax (cp.rs:86)
+  // a PART of the chain (the parallel chain's fallback runs): init_row [NP] = the chain's row
+  // before element 0 (element 0 then runs like any element, psi row 0 included); final_row
+  // [NP] receives the last row.  Both null: the whole chain (row 0 = init_probs, cp.rs:66-68).
+  const double* init_row;
+  double* final_row;
 };
 // forward of the whole chain on ONE workgroup; np = 64 * ceil(N / 64) <= 256
 hipError_t launch_cp_chain_wg(int np, const CpChainWgArgs& g, hipStream_t stream);

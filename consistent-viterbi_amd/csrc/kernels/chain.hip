@@ -18,6 +18,9 @@
 // the state before its first element for ALL NP states at once (one lane per state); the
 // host walks the segment maps from the final state; pass 2 writes every segment's path.
 #include "chain.h"
+#include "trellis.h"
+#include "trellis64.h"
+#include "wave64.h"
 
 namespace cvk {
 namespace {
@@ -47,10 +50,11 @@ __global__ __launch_bounds__(NP * G) void cp_chain_wg(CpChainWgArgs g) {
   const double* aglb = g.a + (size_t)(i0 + RREG + RLDS) * NP + c;
   if constexpr (AFULL)
     for (int k = tid; k < NP * NP; k += NP * G) afull[k] = g.a[k];
-  if (grp == 0) prev[c] = g.pi[c] + g.et[(size_t)g.obs[0] * NP + c];  // init_probs (cp.rs:66-68)
+  if (grp == 0)  // init_probs (cp.rs:66-68), or the row before this part of the chain
+    prev[c] = g.init_row ? g.init_row[c] : g.pi[c] + g.et[(size_t)g.obs[0] * NP + c];
   __syncthreads();
   const int64_t L = g.len;
-  for (int64_t t = 1; t < L; ++t) {
+  for (int64_t t = g.init_row ? 0 : 1; t < L; ++t) {
     const bool first = g.first[t] != 0;
     const int o = g.obs[t];
     double m;
@@ -121,6 +125,7 @@ __global__ __launch_bounds__(NP * G) void cp_chain_wg(CpChainWgArgs g) {
     prev = cur;
     cur = tmp;
   }
+  if (g.final_row && grp == 0) g.final_row[c] = prev[c];
   if (tid == 0) {  // cp.rs:86 / 140: first argmax and max of the last row
     int cs = 0;
     double obj = prev[0];
@@ -199,6 +204,143 @@ __global__ __launch_bounds__(64) void cp_chain_seg_path(CpChainBtArgs g) {
   }
 }
 
+// ---- the parallel CPSolver chain (cv_decode_superseq_cp; DESIGN.md §3 "parallel chain") ----
+// The chain's sequence k starts from the running maximum M of sequences 0..k-1 (utils.rs:24-38:
+// at t == 0 the candidates are prev[i] + pi[j], so every start value is fl(M + fl(pi + b)) when
+// the previous row's maximum is clean), and every later value carries M.  With all finite model
+// entries in [-2^80, 0], every value the chain computes for sequence k that can still reach its
+// optimum lies in [M + S_k - 1, M] (S_k = the sequence's own optimum), so each of its roundings
+// is at most half of U = 2^-52 (|M| + |S_k| + 16): the chain's values stay within 1.5 (t + 1) U
+// of the exact ones on the CP arcs w = fl(a + b) after t steps (one rounding for the value add,
+// one for each candidate of the argmax), and its argmax at step t keeps the exact one whenever
+// the exact gap exceeds (3t + 1) U.  The row-A0 decode at offset 0 (trellis_fwd_f64) gives
+// those gaps up to its own error, (4t + 1) u0 with u0 = 2^-51 (|S_k| + 16).  cp_cert_f64 turns
+// the path's gaps into ONE number per sequence,
+//   rho = min( min_t (gap_t - (4t + 1) u0) / (3t + 1),  (gapF - 4T u0) / (3T + 2) )
+// (gap_t = on-path candidate minus the best other candidate of step t, gapF = top-2 gap of the
+// last row), so the host certifies sequence k at any offset M by rho > U: then the chain's path
+// in sequence k IS the row-A0 path, its end state is the unique first argmax of its last row,
+// and its maximum is the CP fold along that path from M (computed exactly on the host, or as
+// M + the quantised sum of cp_quant_f64).  gF = gapF - 4T u0 bounds the exact final gap for
+// the next sequence's boundary test.  rho = -1: some step is a tie (or the status is not OK) --
+// the host runs the chain itself over that sequence.
+template <int KP>
+__global__ __launch_bounds__(256) void cp_cert_f64(CpCert64Args g) {
+  constexpr int NP = 64 * KP;
+  constexpr uint32_t NINF_HI = 0xFFF00000u;
+  const int lane = threadIdx.x & 63;
+  const int64_t slot = g.seq_begin + (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (slot >= g.seq_end) return;
+  const int64_t seq = g.order ? (int64_t)g.order[slot] : slot;
+  const int64_t e0 = g.offsets[seq];
+  const int T = (int)(g.offsets[seq + 1] - e0);
+  if (T <= 0 || g.status[seq] != CVK_SEQ_OK) {
+    if (lane == 0) g.out[2 * seq] = -1.0, g.out[2 * seq + 1] = -1.0;
+    return;
+  }
+  const uint32_t* __restrict__ rows = reinterpret_cast<const uint32_t*>(g.delta) + (e0 - g.delta_elem_base) * (2 * NP);
+  const int32_t* __restrict__ path = g.path + e0;
+  bool valid[KP];
+#pragma unroll
+  for (int k = 0; k < KP; ++k) valid[k] = (lane + 64 * k) < g.nstates;
+  auto load_row = [&](int r, uint32_t (&h)[KP], uint32_t (&l)[KP]) {
+#pragma unroll
+    for (int k = 0; k < KP; ++k) {
+      h[k] = valid[k] ? __builtin_nontemporal_load(rows + (size_t)r * (2 * NP) + lane + 64 * k) : NINF_HI;
+      l[k] = valid[k] ? __builtin_nontemporal_load(rows + (size_t)r * (2 * NP) + NP + lane + 64 * k) : 0u;
+    }
+  };
+  // top, first argmax and the best OTHER value of x (candidate i = lane + 64k)
+  auto top2 = [&](const double (&x)[KP], int& arg, double& m1, double& m2) {
+    double m = (-__builtin_inf());
+#pragma unroll
+    for (int k = 0; k < KP; ++k) m = fmax(m, x[k]);
+    m1 = wave_max_d_dpp(m);
+    arg = -1;
+#pragma unroll
+    for (int k = KP - 1; k >= 0; --k) {
+      const unsigned long long mask = __ballot(valid[k] && x[k] == m1);
+      if (mask) arg = 64 * k + __builtin_ctzll(mask);
+    }
+    double o = (-__builtin_inf());
+#pragma unroll
+    for (int k = 0; k < KP; ++k) o = fmax(o, (64 * k + lane == arg) ? (-__builtin_inf()) : x[k]);
+    m2 = wave_max_d_dpp(o);
+  };
+  uint32_t ch[KP], cl[KP];
+  load_row(T - 1, ch, cl);
+  double x[KP];
+#pragma unroll
+  for (int k = 0; k < KP; ++k) x[k] = valid[k] ? from_words(ch[k], cl[k]) : (-__builtin_inf());
+  int arg;
+  double m1, m2;
+  top2(x, arg, m1, m2);
+  const double u0 = (__builtin_fabs(m1) + 16.0) * 0x1p-51;
+  bool ok = m1 > (-__builtin_inf()) && arg == path[T - 1];
+  const double gF = m1 - m2 - 4.0 * (double)T * u0;  // +inf when the row has one finite entry
+  double rho = gF / (double)(3 * T + 2);
+  if (ok && T > 1) load_row(T - 2, ch, cl);
+  for (int t = T - 1; ok && t >= 1; --t) {
+    uint32_t nh[KP], nl[KP];
+    if (t >= 2) load_row(t - 2, nh, nl);  // the next step's row, a step ahead
+    const int j = path[t], p = path[t - 1];
+    const double* __restrict__ acol = g.at + (size_t)j * NP + lane;
+#pragma unroll
+    for (int k = 0; k < KP; ++k) x[k] = valid[k] ? from_words(ch[k], cl[k]) + acol[64 * k] : (-__builtin_inf());
+    top2(x, arg, m1, m2);
+    ok = arg == p && m1 > (-__builtin_inf());  // the path's predecessor is the strict first argmax
+    rho = fmin(rho, (m1 - m2 - (double)(4 * t + 1) * u0) / (double)(3 * t + 1));
+#pragma unroll
+    for (int k = 0; k < KP; ++k) ch[k] = nh[k], cl[k] = nl[k];
+  }
+  if (lane == 0) {
+    // the divisions and subtractions above round: a relative 2^-50 covers them
+    const bool pass = ok && rho > 0.0;
+    g.out[2 * seq] = pass ? rho * (1.0 - 0x1p-50) : -1.0;
+    g.out[2 * seq + 1] = pass ? gF * (1.0 - 0x1p-50) : -1.0;
+  }
+}
+
+// Quantised CP fold of a certified path at a predicted binade e (cp_cert_f64 above): while
+// every value of the chain's sequence lies in [2^e, 2^(e+1)) in magnitude, each value is a
+// multiple of g = 2^(e-52) and fl(d + w) = d + rint(w / g) g unless w / g has fractional part
+// exactly 1/2 (a tie, where round-to-even depends on d).  So the fold from M is
+// M + q g with q = sum_t rint(w_t / g) over the arcs w_0 = fl(pi + b), w_t = fl(a + b) of the
+// path -- exact, one add per sequence on the host.  tie = 1: some w_t is a tie or out of range
+// (the host folds that sequence element by element).
+__global__ __launch_bounds__(256) void cp_quant_f64(CpQuant64Args g) {
+  const int lane = threadIdx.x & 63;
+  const int64_t seq = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (seq >= g.nseq) return;
+  const int e = g.ebin[seq];
+  if (e == CVK_NO_BINADE) return;
+  const int64_t e0 = g.offsets[seq];
+  const int T = (int)(g.offsets[seq + 1] - e0);
+  const double scale = __builtin_ldexp(1.0, 52 - e);
+  const int NP = g.np;
+  long long q = 0;
+  bool tie = false;
+  for (int t = lane; t < T; t += 64) {
+    const int P = g.path[e0 + t];
+    const double b = g.et[(size_t)g.obs[e0 + t] * NP + P];
+    const double w = t == 0 ? g.pi[P] + b : g.a[(size_t)g.path[e0 + t - 1] * NP + P] + b;
+    const double xs = w * scale;  // exact: a power-of-two scale of a normal f64
+    if (!(__builtin_fabs(xs) < 0x1p61)) {
+      tie = true;
+      continue;
+    }
+    tie |= xs - __builtin_floor(xs) == 0.5;
+    q += (long long)__builtin_rint(xs);
+  }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) q += __shfl_xor(q, off);
+  const bool anytie = __ballot(tie) != 0;
+  if (lane == 0) {
+    g.q[seq] = q;
+    g.tie[seq] = anytie ? 1 : 0;
+  }
+}
+
 }  // namespace
 
 size_t cp_chain_wg_lds(int np) {
@@ -245,6 +387,26 @@ hipError_t launch_cp_chain_seg_path(const CpChainBtArgs& g, hipStream_t stream) 
     case 256: hipLaunchKernelGGL(cp_chain_seg_path<256>, grid, dim3(64), 0, stream, g); break;
     default: return hipErrorInvalidValue;
   }
+  return hipGetLastError();
+}
+
+hipError_t launch_cp_cert(int np, const CpCert64Args& a, hipStream_t stream) {
+  const int64_t n = a.seq_end - a.seq_begin;
+  if (n <= 0) return hipSuccess;
+  const dim3 grid((unsigned)((n + 3) / 4)), block(256);
+  switch (np) {
+    case 64: hipLaunchKernelGGL(cp_cert_f64<1>, grid, block, 0, stream, a); break;
+    case 128: hipLaunchKernelGGL(cp_cert_f64<2>, grid, block, 0, stream, a); break;
+    case 192: hipLaunchKernelGGL(cp_cert_f64<3>, grid, block, 0, stream, a); break;
+    case 256: hipLaunchKernelGGL(cp_cert_f64<4>, grid, block, 0, stream, a); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_cp_quant(const CpQuant64Args& a, hipStream_t stream) {
+  if (a.nseq <= 0) return hipSuccess;
+  hipLaunchKernelGGL(cp_quant_f64, dim3((unsigned)((a.nseq + 3) / 4)), dim3(256), 0, stream, a);
   return hipGetLastError();
 }
 

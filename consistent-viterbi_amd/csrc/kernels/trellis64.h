@@ -133,6 +133,38 @@ hipError_t launch_t64_mu_add(const double* delta, const double* beta, double* mu
 hipError_t launch_t64_resume_rows(const double* last, const int32_t* state, int64_t n, int np, double* out,
                                   hipStream_t stream);
 
+// Parallel CPSolver chain (cv_decode_superseq_cp, N <= 256, log-probability models): the
+// certificate of each sequence's row-A0 path at offset 0 (cp_cert_f64) and the quantised CP
+// fold of a certified path at a predicted binade (cp_quant_f64).  See trellis64.hip.
+struct CpCert64Args {
+  const double* delta;     // split-plane rows of the row-A0 forward (decode_device's workspace)
+  int64_t delta_elem_base;
+  const double* at;        // [NP][NP] a^T
+  const int64_t* offsets;
+  const int32_t* order;
+  int64_t seq_begin, seq_end;
+  int nstates;
+  const int32_t* path;     // the row-A0 backtrack's paths
+  const uint8_t* status;
+  double* out;             // [nseq_total][2]: rho, gF (-1: not certifiable)
+};
+hipError_t launch_cp_cert(int np, const CpCert64Args& a, hipStream_t stream);
+constexpr int CVK_NO_BINADE = -0x7fffffff;
+struct CpQuant64Args {
+  const double* a;         // [NP][NP] (t64 tables)
+  const double* pi;        // [NP]
+  const double* et;        // [V][NP]
+  int np;
+  const int64_t* offsets;
+  const int32_t* obs;
+  const int32_t* path;
+  const int32_t* ebin;     // [nseq] predicted binade exponent of |M| (CVK_NO_BINADE: skip)
+  int64_t nseq;
+  long long* q;            // [nseq] quantised arc sum in units of 2^(e-52)
+  uint8_t* tie;            // [nseq] 1: a tie or out-of-range arc (fold element by element)
+};
+hipError_t launch_cp_quant(const CpQuant64Args& a, hipStream_t stream);
+
 // CPSolver's super-sequence decode chained exactly over the whole batch (cp_superseq_chain).
 struct CpChainArgs {
   const double* pi;      // [N]

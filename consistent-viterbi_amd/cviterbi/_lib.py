@@ -35,7 +35,7 @@ EXPORTS = [
     "cv_decode_batch", "cv_decode_batch_device", "cv_last_timing", "cv_timing_begin", "cv_timing_end",
     "cv_decode_constrained", "cv_decode_constrained_device", "cv_last_suffix_traced", "cv_decode_constrained_exchange",
     "cv_constrained_pairs", "cv_constrained_partials", "cv_constrained_select", "cv_decode_forced_components", "cv_viterbi_decode",
-    "cv_decode_superseq_cp",
+    "cv_decode_superseq_cp", "cv_last_superseq_stats",
     "cv_solver_create", "cv_solver_solve", "cv_solver_get_solution", "cv_solver_get_objective",
     "cv_solver_get_name", "cv_solver_get_explored_nodes", "cv_solver_destroy",
     "cv_hmm_fit_mle", "cv_hmm_fit_train", "cv_solver_write_cfn",
@@ -125,6 +125,7 @@ def lib():
         "cv_decode_forced_components": ([P, I64, P, P, P, I32, P, P, P, P, P, P], S),
         "cv_viterbi_decode": ([P, I64, P, P], S),
         "cv_decode_superseq_cp": ([P, I64, P, P, P, P], S),
+        "cv_last_superseq_stats": ([P, P], S),
         "cv_solver_create": ([ctypes.c_char_p, P, P, P], S),
         "cv_solver_solve": ([P], S),
         "cv_solver_get_solution": ([P, P, P], S),

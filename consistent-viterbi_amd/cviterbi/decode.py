@@ -253,6 +253,15 @@ def decode_superseq_cp(hmm: HMM, offsets, obs):
     return path[:int(offsets[-1] - offsets[0])], obj.value
 
 
+def last_superseq_stats(hmm: HMM) -> dict:
+    """How the last decode_superseq_cp ran (cv_last_superseq_stats): parallel (the certified
+    per-sequence decode + host fold) or the serial chain, and how many sequences certified /
+    re-ran through the serial chain kernel."""
+    out = (ctypes.c_int64 * 5)()
+    L.check(L.lib().cv_last_superseq_stats(hmm.handle, out))
+    return dict(parallel=bool(out[0]), certified=out[1], rerun=out[2], runs=out[3], quantised=out[4])
+
+
 def _timing_dict(t):
     return dict(fwd_ms=t.fwd_ms, bt_ms=t.bt_ms, total_ms=t.total_ms, launches=t.launches,
                 kernel={1: "trellis", 2: "generic", 3: "trellis_f64"}.get(t.kernel, "none"), padded_states=t.padded_states,

@@ -272,11 +272,23 @@ CV_API cv_status cv_viterbi_decode(cv_hmm* h, int64_t T, const int32_t* obs, int
  * (utils.rs:24-38), so later sequences carry the running total and round exactly as the
  * reference does (a per-sequence decode can differ from it at near ties).  f64, first-index
  * argmax, CP association.  path_out[offsets[nseq] - offsets[0]] in super-sequence order;
- * objective_out = the chain's final maximum (main.rs:129's first number).  Serial over
- * elements on the GPU (one workgroup), as the reference is on the CPU: the main.rs drop-in,
- * not the batch hot path.  N <= 1024.  CV_EINFEASIBLE when the maximum is -inf. */
+ * objective_out = the chain's final maximum (main.rs:129's first number).  N <= 256 with
+ * log-probability models (finite entries in [-2^80, 0]): every sequence is decoded on its own
+ * by the f64 trellis in parallel and certified to be the chain's path at the chain's running
+ * total (a rounding-error margin), the running total folded on the host, and only the
+ * uncertified sequences (near ties at that magnitude) re-run through the serial chain kernel
+ * -- bit-identical to the serial chain (cv_last_superseq_stats).  Otherwise serial over
+ * elements on the GPU (one workgroup), as the reference is on the CPU.  N <= 1024.
+ * CV_EINFEASIBLE when the maximum is -inf. */
 CV_API cv_status cv_decode_superseq_cp(cv_hmm* h, int64_t nseq, const int64_t* offsets, const int32_t* obs,
                                        int32_t* path_out, double* objective_out);
+/* How the last cv_decode_superseq_cp on this handle ran (out[5]): out[0] = 1 when the PARALLEL
+ * chain ran (N <= 256, every finite entry of the model in [-2^80, 0], every sequence feasible:
+ * each sequence decoded on its own by the f64 trellis and certified to be the chain's own path
+ * at the chain's running total), 0 for the serial chain; out[1] = sequences
+ * certified, out[2] = sequences the serial chain kernel re-ran (near ties at the chain's
+ * magnitude), out[3] = such runs, out[4] = certified sequences folded by one quantised add. */
+CV_API cv_status cv_last_superseq_stats(const cv_hmm* h, int64_t* out);
 
 /* ---- trait Solver (viterbi_solver.rs:11-16) -------------------------------------------
  * kind: "gpu"      f32 trellis kernel, VITERBI association, f64 re-scored objective

@@ -1,0 +1,172 @@
+"""GPU: the parallel CPSolver chain (cv_decode_superseq_cp, main.rs:120 / cp.rs:63-93 over the
+super-sequence of utils.rs:62-103).  Every sequence is decoded on its own by the f64 trellis,
+certified to be the chain's own path at the chain's running total, and folded on the host;
+uncertified sequences re-run through the serial chain kernel.  The result must equal the serial
+chain (CV_CHAIN_PAR=0) and the C oracle's chained restatement (cvo_cp_superseq_f64) bit for bit:
+every element of the path and the objective."""
+import os
+
+import numpy as np
+import pytest
+
+import c_oracle as O
+import cviterbi as cv
+from cviterbi import synth
+
+pytestmark = pytest.mark.gpu
+
+
+def _serial(h, off, obs):
+    old = os.environ.get("CV_CHAIN_PAR")
+    os.environ["CV_CHAIN_PAR"] = "0"
+    try:
+        out = cv.decode_superseq_cp(h, off, obs)
+        assert not cv.last_superseq_stats(h)["parallel"]
+        return out
+    finally:
+        if old is None:
+            del os.environ["CV_CHAIN_PAR"]
+        else:
+            os.environ["CV_CHAIN_PAR"] = old
+
+
+def _par(h, off, obs, force=None):
+    old = os.environ.get("CV_CHAIN_PAR_FORCE")
+    if force is not None:
+        os.environ["CV_CHAIN_PAR_FORCE"] = str(force)
+    try:
+        out = cv.decode_superseq_cp(h, off, obs)
+        return out, cv.last_superseq_stats(h)
+    finally:
+        if force is not None:
+            if old is None:
+                del os.environ["CV_CHAIN_PAR_FORCE"]
+            else:
+                os.environ["CV_CHAIN_PAR_FORCE"] = old
+
+
+def _case(n, v, nseq, tlo, thi, seed, scale=1.0, zeros=(), ones=()):
+    pi, a, b = synth.random_hmm(n, v, seed=seed)
+    pi, a, b = pi * scale, a * scale, b * scale
+    rng = np.random.default_rng(seed + 1)
+    lengths = rng.integers(tlo, thi + 1, size=nseq)
+    for k in zeros:
+        lengths[k] = 0
+    for k in ones:
+        lengths[k] = 1
+    off = synth.offsets_from_lengths(lengths)
+    obs = rng.integers(0, v, size=int(off[-1])).astype(np.int32)
+    return pi, a, b, off, obs
+
+
+@pytest.mark.parametrize("n", [1, 5, 64, 100, 128, 192, 256])
+def test_chain_par_equals_oracle(gpu, n):
+    """Random log10 models at every padded width, ragged lengths incl. empty and one-element
+    sequences: the parallel chain equals the oracle's chained restatement element by element."""
+    pi, a, b, off, obs = _case(n, 23, 60, 1, 90, seed=4000 + n, zeros=(3, 17), ones=(5, 40))
+    h = cv.HMM(pi, a, b)
+    (path, obj), st = _par(h, off, obs)
+    assert st["parallel"], st
+    rp, robj = O.cp_superseq_f64(pi, a, b, off, obs)
+    assert obj == robj
+    bad = np.nonzero(path != rp)[0]
+    assert bad.size == 0, f"elements {bad[:10]} of {len(rp)}; {st}"
+
+
+@pytest.mark.parametrize("n,force", [(64, 1), (64, 2), (64, 3), (256, 2), (256, 5), (7, 4)])
+def test_chain_par_forced_runs(gpu, n, force):
+    """CV_CHAIN_PAR_FORCE=m takes every m-th sequence as uncertified, so the serial chain kernel
+    re-runs it from a synthetic start row (after a certified sequence) or from the previous run's
+    last row (consecutive runs, m = 1: the whole chain in one run): still the oracle's chain."""
+    pi, a, b, off, obs = _case(n, 19, 40, 1, 70, seed=4100 + n + force, zeros=(2,), ones=(7,))
+    h = cv.HMM(pi, a, b)
+    (path, obj), st = _par(h, off, obs, force=force)
+    assert st["parallel"] and st["rerun"] >= 1, st
+    rp, robj = O.cp_superseq_f64(pi, a, b, off, obs)
+    assert obj == robj and np.array_equal(path, rp), st
+
+
+def test_chain_par_rounding_case(gpu):
+    """The chain-rounding case of test_superseq_cp_chain_rounding with more sequences around it:
+    at a running total of -2^40 two predecessors 2^-20 apart tie in the chain -- no certificate
+    can hold there, so the serial chain kernel decides (first index), exactly as the reference."""
+    big = 2.0 ** 40
+    pi = np.array([-1.0, -1.0, -3.0])
+    a = np.array([[-1.0] * 3, [-1.0 + 2.0 ** -20] * 3, [-5.0] * 3])
+    b = np.array([[-0.5, -big], [-0.5, -big], [-0.5, -big]])
+    lengths = np.array([1, 2, 3, 1, 2, 5, 2])
+    off = synth.offsets_from_lengths(lengths)
+    obs = np.zeros(int(off[-1]), np.int32)
+    obs[0] = 1
+    h = cv.HMM(pi, a, b)
+    (path, obj), st = _par(h, off, obs)
+    rp, robj = O.cp_superseq_f64(pi, a, b, off, obs)
+    assert np.array_equal(path, rp) and obj == robj, st
+    assert st["parallel"] and st["rerun"] >= 1, st
+
+
+@pytest.mark.parametrize("scale", [1.0, 1e3, 1e6])
+def test_chain_par_large_totals(gpu, scale):
+    """Scaled models (still log-probability-like: every entry <= 0) push the running total to
+    1e7..1e13, where the chain's ulp reaches the path margins: certificates fail for some
+    sequences, quantised folds take the rest, and the result is still the serial chain's."""
+    pi, a, b, off, obs = _case(64, 31, 400, 50, 300, seed=4200, scale=scale)
+    h = cv.HMM(pi, a, b)
+    (path, obj), st = _par(h, off, obs)
+    sp, sobj = _serial(h, off, obs)
+    assert st["parallel"], st
+    assert obj == sobj, (obj, sobj, st)
+    bad = np.nonzero(path != sp)[0]
+    assert bad.size == 0, f"elements {bad[:10]} of {len(sp)}; {st}"
+    if scale == 1.0:
+        assert st["rerun"] == 0 and st["quantised"] > 300, st
+
+
+def test_chain_par_1m_elements_vs_serial(gpu):
+    """>= 1 M elements at N = 256 (config-4 model, 2,048 sequences of 512): the parallel chain
+    equals the serial chain kernel bit for bit (every element and the objective), with nearly
+    every sequence certified and folded by one quantised add."""
+    c = synth.config("c4", 2048)
+    h = cv.HMM(c["pi"], c["a"], c["b"])
+    (path, obj), st = _par(h, c["offsets"], c["obs"])
+    assert int(c["offsets"][-1]) >= 1 << 20
+    sp, sobj = _serial(h, c["offsets"], c["obs"])
+    assert st["parallel"] and st["certified"] + st["rerun"] == 2048, st
+    assert st["certified"] >= 2000 and st["quantised"] >= 1900, st
+    assert obj == sobj
+    bad = np.nonzero(path != sp)[0]
+    assert bad.size == 0, f"elements {bad[:10]}; {st}"
+
+
+def test_chain_par_quantised_ties(gpu):
+    """Dyadic (quantised) tables: exact ties at every step defeat every certificate, so every
+    sequence re-runs through the serial chain kernel in one run -- equal to the oracle."""
+    rng = np.random.default_rng(4300)
+    n, v = 65, 9
+    pi = np.round(rng.uniform(-2, 0, n) * 2) / 2
+    a = np.round(rng.uniform(-2, 0, (n, n)) * 2) / 2
+    b = np.round(rng.uniform(-2, 0, (n, v)) * 2) / 2
+    off = synth.offsets_from_lengths(rng.integers(0, 50, size=30))
+    obs = rng.integers(0, v, size=int(off[-1])).astype(np.int32)
+    h = cv.HMM(pi, a, b)
+    (path, obj), st = _par(h, off, obs)
+    rp, robj = O.cp_superseq_f64(pi, a, b, off, obs)
+    assert obj == robj and np.array_equal(path, rp), st
+
+
+def test_chain_par_not_applicable(gpu):
+    """A positive entry (outside the certificate's [-2^80, 0] models) or an infeasible sequence:
+    the serial chain runs (stats: parallel = False) with the same results / CV_EINFEASIBLE."""
+    pi, a, b, off, obs = _case(16, 7, 12, 1, 30, seed=4400)
+    a2 = a.copy()
+    a2[0, 0] = 0.25
+    h = cv.HMM(pi, a2, b)
+    (path, obj), st = _par(h, off, obs)
+    rp, robj = O.cp_superseq_f64(pi, a2, b, off, obs)
+    assert not st["parallel"] and obj == robj and np.array_equal(path, rp)
+    b3 = b.copy()
+    b3[:, int(obs[off[4]])] = -np.inf  # sequence 4 cannot start
+    h3 = cv.HMM(pi, a, b3)
+    with pytest.raises(cv.CVError, match="INFEASIBLE"):
+        cv.decode_superseq_cp(h3, off, obs)
+    assert not cv.last_superseq_stats(h3)["parallel"]

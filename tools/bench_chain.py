@@ -1,6 +1,11 @@
-"""CPSolver chained super-sequence decode (cv_decode_superseq_cp, kind gpu-cp, what main.rs:120
-runs): wall time per element at several N.  CV_CHAIN_OLD=1 selects the one-thread-per-state
-kernel for comparison (N <= 256 otherwise runs kernels/chain.hip)."""
+"""CPSolver chained super-sequence decode (cv_decode_superseq_cp = solver kind gpu-cp, what
+main.rs:120 runs): wall time of the PARALLEL chain (per-sequence f64 trellis + certificates +
+host fold + serial re-runs of the uncertified sequences) on config-4-shaped inputs, with the
+serial chain kernel (CV_CHAIN_PAR=0) on a smaller slice for comparison; every parallel result
+is checked against the serial chain where both run.
+
+  python tools/bench_chain.py [nseq_full=65536] [nseq_cmp=2048]
+"""
 import os
 import sys
 import time
@@ -11,17 +16,44 @@ import numpy as np  # noqa: E402
 import cviterbi as cv  # noqa: E402
 from cviterbi import synth  # noqa: E402
 
-sizes = [(12, 200000), (64, 200000), (126, 100000), (256, 100000)]
-if os.environ.get("CV_CHAIN_OLD") == "1":
-    sizes = [(12, 200000), (64, 50000), (126, 20000), (256, 5000)]
-for n, L in sizes:
-    pi, a, b = synth.random_hmm(n, 50, seed=1)
-    lengths = np.full(L // 25, 25)
-    off = synth.offsets_from_lengths(lengths)
-    obs = np.random.default_rng(0).integers(0, 50, size=int(off[-1])).astype(np.int32)
-    h = cv.HMM(pi, a, b)
-    cv.decode_superseq_cp(h, off[:3], obs[:off[2]])
-    t0 = time.perf_counter()
-    cv.decode_superseq_cp(h, off, obs)
-    el = time.perf_counter() - t0
-    print(f"N={n} elements={off[-1]} {el*1e3:.1f} ms  {el/off[-1]*1e6:.3f} us/element", flush=True)
+
+def run(h, off, obs, serial=False):
+    if serial:
+        os.environ["CV_CHAIN_PAR"] = "0"
+    try:
+        t0 = time.perf_counter()
+        path, obj = cv.decode_superseq_cp(h, off, obs)
+        el = time.perf_counter() - t0
+    finally:
+        os.environ.pop("CV_CHAIN_PAR", None)
+    return path, obj, el, cv.last_superseq_stats(h)
+
+
+def main():
+    nfull = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
+    ncmp = int(sys.argv[2]) if len(sys.argv) > 2 else 2048
+    c = synth.config("c4", nfull)
+    h = cv.HMM(c["pi"], c["a"], c["b"])
+    off, obs = c["offsets"], c["obs"]
+    run(h, off[:3], obs[:off[2]])  # tables, first-call setup
+    # comparison slice: parallel vs serial, bit for bit
+    oc, bc = off[:ncmp + 1], obs[:off[ncmp]]
+    p1, o1, t1, s1 = run(h, oc, bc)
+    p0, o0, t0, _ = run(h, oc, bc, serial=True)
+    same = bool(np.array_equal(p1, p0) and o1 == o0)
+    L = int(oc[-1])
+    print(f"N=256 {ncmp} seqs x 512 = {L} elements: parallel {t1*1e3:.1f} ms ({t1/L*1e9:.1f} ns/element), "
+          f"serial chain {t0*1e3:.1f} ms ({t0/L*1e6:.3f} us/element), equal={same}, stats {s1}", flush=True)
+    if not same:
+        raise SystemExit("parallel chain differs from the serial chain")
+    for rep in range(2):
+        p, o, t, s = run(h, off, obs)
+        L = int(off[-1])
+        print(f"N=256 {nfull} seqs x 512 = {L} elements (config-4-sized gpu-cp solve): {t*1e3:.1f} ms "
+              f"({t/L*1e9:.1f} ns/element), objective {o!r}, stats {s}", flush=True)
+    # the full chain's prefix slice must agree with the comparison run's serial chain
+    assert np.array_equal(p[:int(oc[-1])][:-512], p0[:-512]), "prefix of the full chain differs"
+
+
+if __name__ == "__main__":
+    main()
