@@ -365,13 +365,19 @@ def main():
             dist.barrier()
         el = time.perf_counter() - t0
         kt = cv.timing_end(h)
-        if world > 1:
-            tt = torch.tensor([el], dtype=torch.float64, device="cpu" if args.backend == "gloo" else dev)
-            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-            el = float(tt.item())
-        return el, kt
+        per_rank = [el]
+        if world > 1:  # every rank's time (the SCALE record shows imbalance); the max is the job's
+            per_rank = [r[0] for r in all_gather_floats([el])]
+            el = max(per_rank)
+        return el, kt, per_rank
 
-    el, kt = timed(args.dtype, args.steps, args.warmup)
+    def all_gather_floats(vals):
+        t = torch.tensor(vals, dtype=torch.float64, device="cpu" if args.backend == "gloo" else dev)
+        parts = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(parts, t)
+        return [p.cpu().tolist() for p in parts]
+
+    el, kt, per_rank_s = timed(args.dtype, args.steps, args.warmup)
     fwd_ms, bt_ms, launches = kt["fwd_ms"], kt["bt_ms"], kt["launches"]
     spw = kt.get("seqs_per_wave", 8)  # the layout of the timed run (before the f32 extra)
     # this rank's first sequences as the timed run decoded them (for the CPU baseline's check)
@@ -409,7 +415,7 @@ def main():
     f32_extra = None
     if f64 and not args.no_f32_extra:
         p64 = outs[last["buf"]][0].clone()  # the f64 (reference-exact) paths of this rank's shard
-        el32, kt32 = timed("f32", args.steps, args.warmup)
+        el32, kt32, _ = timed("f32", args.steps, args.warmup)
         # measured, not quoted: the share of this rank's sequences whose f32 path differs from
         # the f64 one (the f32 mode's cost in parity; the f64 headline is the reference's)
         p32 = outs[last["buf"]][0]
@@ -427,6 +433,10 @@ def main():
     c5s = None
     if world > 1 and not args.no_c5_sharded:
         c5s = c5_sharded(dev, world, rank, dist, args.backend, args.c5_batch, 2)
+
+    # per-rank peak device memory: torch's tensors + the library's tables and workspaces
+    mem = [torch.cuda.max_memory_allocated(dev) / 1e9, cv.device_memory()["peak"] / 1e9]
+    mem_ranks = all_gather_floats(mem) if world > 1 else [mem]
 
     cells_total = B * T_LEN * N_STATES * args.steps
     value = cells_total / el
@@ -495,6 +505,12 @@ def main():
                                        "frac": achieved / HBM_PEAK},
                                "valu": valu}},
         "kernel_ms_per_step": {"forward": fwd_ms / args.steps, "backtrack_rescore": bt_ms / args.steps},
+        "per_rank": {"ms_per_step": [x * 1e3 / args.steps for x in per_rank_s],
+                     "min_ms_per_step": min(per_rank_s) * 1e3 / args.steps,
+                     "max_ms_per_step": max(per_rank_s) * 1e3 / args.steps,
+                     "peak_device_gb": [{"torch": m[0], "library": m[1]} for m in mem_ranks],
+                     "note": "timed region of the headline dtype; peak device memory over the whole run so far "
+                             "(decode workspaces, rank 0's verify decode, the sharded config-5 leg)"},
     }
     if f32_extra is not None:
         out["f32_trellis"] = f32_extra

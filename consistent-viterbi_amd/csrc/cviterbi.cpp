@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <charconv>
 #include <chrono>
 #include <cmath>
@@ -57,6 +58,9 @@ cv_status set_err(cv_status st, const char* fmt, ...) {
                      __LINE__);                                                                \
   } while (0)
 
+// device bytes this process's library holds now / at most (cv_device_memory)
+std::atomic<int64_t> g_dev_cur{0}, g_dev_peak{0};
+
 struct DevBuf {
   void* p = nullptr;
   size_t bytes = 0;
@@ -65,7 +69,10 @@ struct DevBuf {
   DevBuf& operator=(const DevBuf&) = delete;
   ~DevBuf() { release(); }
   void release() {
-    if (p) (void)hipFree(p);
+    if (p) {
+      (void)hipFree(p);
+      g_dev_cur -= (int64_t)bytes;
+    }
     p = nullptr;
     bytes = 0;
   }
@@ -80,6 +87,10 @@ struct DevBuf {
       return set_err(CV_ENOMEM, "hipMalloc(%zu) failed: %s", n, hipGetErrorString(e));
     }
     bytes = n;
+    const int64_t cur = g_dev_cur += (int64_t)n;
+    int64_t pk = g_dev_peak.load();
+    while (cur > pk && !g_dev_peak.compare_exchange_weak(pk, cur)) {
+    }
     return CV_OK;
   }
   template <typename T>
@@ -1064,6 +1075,11 @@ extern "C" {
 CV_API const char* cv_last_error(void) { return g_err.c_str(); }
 CV_API const char* cv_version(void) { return "cviterbi 0.1.0 (gfx950)"; }
 CV_API int32_t cv_abi_version(void) { return CV_ABI_VERSION; }
+CV_API cv_status cv_device_memory(int64_t* current_bytes, int64_t* peak_bytes) {
+  if (current_bytes) *current_bytes = g_dev_cur.load();
+  if (peak_bytes) *peak_bytes = g_dev_peak.load();
+  return CV_OK;
+}
 CV_API int32_t cv_device_count(void) {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess) {

@@ -6,7 +6,7 @@ in include/cviterbi.h (libcviterbi.so: hand-written gfx950 HIP kernels).
 from ._lib import CVError, EXPORTS, LIB_PATH  # noqa: F401
 from .hmm import HMM  # noqa: F401
 from .decode import (constrained_pairs, constrained_partials, constrained_select, decode, decode_batch, decode_batch_device, decode_constrained_device, decode_constrained_exchange,  # noqa: F401
-                     decode_constrained, decode_forced_components, decode_superseq_cp, last_suffix_traced, last_superseq_stats, last_timing, timing_begin,
+                     decode_constrained, decode_forced_components, decode_superseq_cp, device_memory, last_suffix_traced, last_superseq_stats, last_timing, timing_begin,
                      timing_end)
 from .fit import fit_mle, fit_train  # noqa: F401
 from .solver import (Constraints, GpuSolver, Solver, SuperSequence, load_sequences, load_tags,  # noqa: F401

@@ -28,7 +28,7 @@ FLAG_SERIAL = 0x2
 
 # every symbol include/cviterbi.h declares (checked by tests/test_abi.py)
 EXPORTS = [
-    "cv_last_error", "cv_version", "cv_abi_version", "cv_device_count", "cv_opts_init",
+    "cv_last_error", "cv_version", "cv_abi_version", "cv_device_count", "cv_device_memory", "cv_opts_init",
     "cv_hmm_create", "cv_hmm_from_json", "cv_hmm_write_json", "cv_hmm_destroy", "cv_hmm_nstates", "cv_hmm_nobs",
     "cv_hmm_ndims", "cv_hmm_bdims", "cv_obs_flatten", "cv_hmm_init_prob", "cv_hmm_init_probs",
     "cv_hmm_transition_prob", "cv_hmm_transitions_to", "cv_hmm_emit_prob", "cv_hmm_emit_probs",
@@ -126,6 +126,7 @@ def lib():
         "cv_viterbi_decode": ([P, I64, P, P], S),
         "cv_decode_superseq_cp": ([P, I64, P, P, P, P], S),
         "cv_last_superseq_stats": ([P, P], S),
+        "cv_device_memory": ([P, P], S),
         "cv_solver_create": ([ctypes.c_char_p, P, P, P], S),
         "cv_solver_solve": ([P], S),
         "cv_solver_get_solution": ([P, P, P], S),

@@ -262,6 +262,13 @@ def last_superseq_stats(hmm: HMM) -> dict:
     return dict(parallel=bool(out[0]), certified=out[1], rerun=out[2], runs=out[3], quantised=out[4])
 
 
+def device_memory() -> dict:
+    """Device bytes this process's library holds now and at most (cv_device_memory)."""
+    cur, peak = ctypes.c_int64(), ctypes.c_int64()
+    L.check(L.lib().cv_device_memory(ctypes.byref(cur), ctypes.byref(peak)))
+    return dict(current=cur.value, peak=peak.value)
+
+
 def _timing_dict(t):
     return dict(fwd_ms=t.fwd_ms, bt_ms=t.bt_ms, total_ms=t.total_ms, launches=t.launches,
                 kernel={1: "trellis", 2: "generic", 3: "trellis_f64"}.get(t.kernel, "none"), padded_states=t.padded_states,

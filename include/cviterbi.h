@@ -130,6 +130,9 @@ CV_API const char* cv_last_error(void);
 CV_API const char* cv_version(void);
 CV_API int32_t cv_abi_version(void);
 CV_API int32_t cv_device_count(void);
+/* Device memory this process's library holds (handles' tables and workspaces, call buffers):
+ * now and at most since load (either pointer may be NULL). */
+CV_API cv_status cv_device_memory(int64_t* current_bytes, int64_t* peak_bytes);
 CV_API void cv_opts_init(cv_opts* opts);
 
 /* ---- hmm::HMM (src/hmm/hmm.rs) ------------------------------------------------------- */
