@@ -3667,7 +3667,8 @@ CV_API cv_status cv_hmm_fit_train(int32_t nstates, int64_t nobs, int64_t nseq, c
       g.b_num = A + 3 * N;
       g.xi_s = g.b_num + (size_t)V * N;
       g.xi_zero = g.xi_s + (size_t)N * N;
-      const hipError_t e = cvf::launch_bw_estep(g, c.second - c.first, max_waves, nullptr);
+      const hipError_t e =
+          cvf::launch_bw_estep(g, c.second - c.first, max_waves, nullptr, off0[c.second] - off0[c.first]);
       if (e != hipSuccess) return set_err(CV_EDEVICE, "Baum-Welch launch failed: %s", hipGetErrorString(e));
     }
     // M-step (hmm.rs:145-170) on the device: new_pi = sum gamma_0 / R; new_a = sum xi / a_den

@@ -6,7 +6,9 @@
 
 namespace cvf {
 
-constexpr int kBwMaxStates = 128;  // bw_stats keeps a sequence's N x N xi sum in LDS
+constexpr int kBwLdsStates = 128;  // bw_stats keeps a sequence's N x N xi sum in LDS up to here
+constexpr int kBwMaxStates = 256;  // one thread per state (256-thread workgroups); beyond
+                                   // kBwLdsStates the xi sum is a GEMM over stored rows
 
 struct MleArgs {
   const int64_t* offsets;
@@ -64,7 +66,8 @@ struct MstepArgs {
 hipError_t launch_mle_counts(const MleArgs& g, int64_t nseq, hipStream_t stream);
 // forward, backward and the E-step sums of sequences [0, nseq) of g.offsets; the N <= 64
 // backward kernel runs at most max_waves waves (each walks several sequences)
-hipError_t launch_bw_estep(const BwArgs& g, int64_t nseq, int64_t max_waves, hipStream_t stream);
+// nrows: the chunk's elements (alpha / beta rows from elem_base), for the GEMM path (N > 128)
+hipError_t launch_bw_estep(const BwArgs& g, int64_t nseq, int64_t max_waves, hipStream_t stream, int64_t nrows);
 hipError_t launch_bw_mstep(const MstepArgs& m, int nparts_b, hipStream_t stream);
 
 }  // namespace cvf

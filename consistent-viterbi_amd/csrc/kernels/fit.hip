@@ -7,8 +7,8 @@
 // f64 throughout, probability space, like the reference.  One workgroup (256 threads) per
 // sequence; thread i < N owns state i.  The transition matrix is read from L2 (row-major A
 // for the forward step, A^T for the backward and xi steps, so every read is coalesced
-// across the threads of a row).  bw_stats keeps the sequence's xi sum (N x N) in LDS, so
-// the trainer covers N <= 128 (the reference trains POS taggers: N = 12).  For N <= 64 the
+// across the threads of a row).  bw_stats keeps the sequence's xi sum (N x N) in LDS up to
+// N = 128 (the reference trains POS taggers: N = 12; it has no limit on N).  For N <= 64 the
 // one-wave-per-sequence kernels below (bw_fwd_wave, bw_bwd_stats_wave) replace all three.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -188,6 +188,113 @@ __global__ __launch_bounds__(256) void bw_stats(BwArgs g) {
   }
   for (int k = i; k < N * N; k += blockDim.x) unsafeAtomicAdd(&g.xi_s[k], S[k]);
   if (i == 0 && z != 0.0) unsafeAtomicAdd(g.xi_zero, z);
+}
+
+// ---- 128 < N <= 256: the xi sum as a GEMM ---------------------------------------------------
+// S (N x N, 512 KiB at N = 256) no longer fits LDS.  bw_stats_rows computes the same per-step
+// quantities as bw_stats but, instead of the rank-1 update S += r_t (x) u_{t+1}, writes
+// r_t = alpha_t / c_t (0 when c_t == 0) over alpha's row t and u_{t+1} over beta's row t (both
+// rows are dead by then: alpha_t and beta_t were last read for gamma_t and xi_t; beta_{t+1} is
+// read in this step, rewritten in the next), and zeros at the last step of each sequence.  Then
+// sum_t S_t = R^T U over all rows of the chunk: bw_xi_gemm, on the matrix cores.
+__global__ __launch_bounds__(256) void bw_stats_rows(BwArgs g) {
+  __shared__ double p[256];
+  __shared__ double red[4];
+  const int64_t seq = blockIdx.x;
+  const int64_t e0 = g.offsets[seq];
+  const int T = (int)(g.offsets[seq + 1] - e0);
+  const int N = g.nstates;
+  const int i = threadIdx.x;
+  if (T <= 0) return;
+  double* al = g.alpha + (e0 - g.elem_base) * N;
+  double* be = g.beta + (e0 - g.elem_base) * N;
+  const int32_t* obs = g.obs + e0;
+  double pi_acc = 0.0, a_den = 0.0, b_den = 0.0, z = 0.0;
+  for (int t = 0; t < T; ++t) {
+    // gamma_t = normalize(alpha_t * beta_t)  (hmm.rs:127-129)
+    const double ai = (i < N) ? al[(size_t)t * N + i] : 0.0;
+    const double ab = (i < N) ? ai * be[(size_t)t * N + i] : 0.0;
+    const double s = block_sum(ab, red);
+    if (i < N) {
+      const double gm = normalized(ab, s, N);
+      if (t == 0) pi_acc += gm;
+      if (t < T - 1) a_den += gm;
+      b_den += gm;
+      unsafeAtomicAdd(&g.b_num[(size_t)obs[t] * N + i], gm);  // hmm.rs:155-163
+    }
+    double r = 0.0, u = 0.0;
+    if (t + 1 < T) {
+      // u_j = b(o_{t+1})[j] * beta_{t+1}[j];  w_i = sum_j A[i][j] u_j;  c = alpha_t . w
+      __syncthreads();
+      if (i < N) p[i] = g.et[(size_t)obs[t + 1] * N + i] * be[(size_t)(t + 1) * N + i];
+      __syncthreads();
+      double w = 0.0;
+      if (i < N)
+        for (int k = 0; k < N; ++k) w += g.at[(size_t)k * N + i] * p[k];
+      const double c = block_sum(ai * w, red);
+      u = (i < N) ? p[i] : 0.0;
+      if (c != 0.0) r = ai / c;
+      else z += 1.0;  // xi_t uniform (hmm.rs:306-317), counted separately
+    }
+    if (i < N) {
+      al[(size_t)t * N + i] = r;
+      be[(size_t)t * N + i] = u;
+    }
+  }
+  if (i < N) {
+    unsafeAtomicAdd(&g.pi_acc[i], pi_acc);
+    unsafeAtomicAdd(&g.a_den[i], a_den);
+    unsafeAtomicAdd(&g.b_den[i], b_den);
+  }
+  if (i == 0 && z != 0.0) unsafeAtomicAdd(g.xi_zero, z);
+}
+
+// xi_s[m][n] += sum_r R[r][m] U[r][n] over rows [0, nrows) (R = alpha rows, U = beta rows of
+// bw_stats_rows).  One wave per 32 x 32 output tile and row range: per 4 rows, lane l feeds
+// R[r + l/16][m0 + 16 mt + l%16] and U[...][n0 + 16 nt + l%16] into four
+// v_mfma_f64_16x16x4_f64 (2 x 2 tiles); one atomic flush of the tile at the end.
+__global__ __launch_bounds__(64) void bw_xi_gemm(BwArgs g, int64_t nrows, int64_t rows_per_wave) {
+  const int N = g.nstates;
+  const int nt32 = (N + 31) / 32;
+  const int tile = blockIdx.x % (nt32 * nt32);
+  const int64_t part = blockIdx.x / (nt32 * nt32);
+  const int m0 = 32 * (tile / nt32), n0 = 32 * (tile % nt32);
+  const int l = threadIdx.x, kk = l >> 4, cl = l & 15;
+  const int64_t r0 = part * rows_per_wave, r1 = r0 + rows_per_wave < nrows ? r0 + rows_per_wave : nrows;
+  typedef double double4_t __attribute__((ext_vector_type(4)));
+  double4_t acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) acc[a][b] = double4_t{0.0, 0.0, 0.0, 0.0};
+  const int cm[2] = {m0 + cl, m0 + 16 + cl}, cn[2] = {n0 + cl, n0 + 16 + cl};
+  const bool vm[2] = {cm[0] < N, cm[1] < N}, vn[2] = {cn[0] < N, cn[1] < N};
+  for (int64_t r = r0; r < r1; r += 4) {
+    const int64_t row = r + kk;
+    const bool vr = row < r1;
+    const double* R = g.alpha + (size_t)(vr ? row : r0) * N;
+    const double* U = g.beta + (size_t)(vr ? row : r0) * N;
+    double av[2], bv[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      av[q] = (vr && vm[q]) ? R[cm[q]] : 0.0;
+      bv[q] = (vr && vn[q]) ? U[cn[q]] : 0.0;
+    }
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[a], bv[b], acc[a][b], 0, 0, 0);
+  }
+  // C/D layout of v_mfma_f64_16x16x4_f64: col = lane & 15, row = (lane >> 4) + 4 * reg
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int row = m0 + 16 * a + (l >> 4) + 4 * q, col = n0 + 16 * b + (l & 15);
+        if (row < N && col < N && acc[a][b][q] != 0.0) unsafeAtomicAdd(&g.xi_s[(size_t)row * N + col], acc[a][b][q]);
+      }
 }
 
 // ---- N <= 64: one wave per sequence ---------------------------------------------------------
@@ -644,9 +751,21 @@ static void launch_wave_estep(const BwArgs& g, int64_t nseq, int64_t nwaves, hip
                      nwaves);
 }
 
-hipError_t launch_bw_estep(const BwArgs& g, int64_t nseq, int64_t max_waves, hipStream_t stream) {
+hipError_t launch_bw_estep(const BwArgs& g, int64_t nseq, int64_t max_waves, hipStream_t stream, int64_t nrows) {
   if (nseq <= 0) return hipSuccess;
   if (g.nstates > kBwMaxStates) return hipErrorInvalidValue;
+  if (g.nstates > kBwLdsStates) {  // the xi sum as R^T U on the matrix cores
+    hipLaunchKernelGGL(bw_forward, dim3((unsigned)nseq), dim3(256), 0, stream, g);
+    hipLaunchKernelGGL(bw_backward, dim3((unsigned)nseq), dim3(256), 0, stream, g);
+    hipLaunchKernelGGL(bw_stats_rows, dim3((unsigned)nseq), dim3(256), 0, stream, g);
+    const int nt32 = (g.nstates + 31) / 32;
+    // ~4,096 waves: row ranges of a multiple of 4 rows per output tile
+    const int64_t parts = std::max<int64_t>(1, std::min<int64_t>(4096 / (nt32 * nt32), (nrows + 255) / 256));
+    const int64_t per = ((nrows + parts - 1) / parts + 3) / 4 * 4;
+    const int64_t np = (nrows + per - 1) / per;
+    hipLaunchKernelGGL(bw_xi_gemm, dim3((unsigned)(np * nt32 * nt32)), dim3(64), 0, stream, g, nrows, per);
+    return hipGetLastError();
+  }
   if (g.nstates <= kBwWaveStates) {
     const int64_t nwaves = std::max<int64_t>(1, std::min<int64_t>((nseq + 1) / 2, max_waves));  // pairs
     if (g.nstates <= 16) launch_wave_estep<16>(g, nseq, nwaves, stream);

@@ -105,7 +105,8 @@ def test_gpu_mle_matches_oracle(gpu, n, v):
 # kernels; T > 64 crosses the 64-step observation blocks of the wave kernels
 @pytest.mark.parametrize("n,v,frac,tmax", [(3, 5, 0.0, 30), (12, 30, 0.3, 150), (20, 30, 0.5, 200),
                                            (45, 60, 0.2, 130), (64, 40, 0.1, 70), (65, 40, 0.1, 40),
-                                           (128, 40, 0.1, 30)])
+                                           (128, 40, 0.1, 30), (129, 40, 0.1, 30), (200, 50, 0.2, 40),
+                                           (256, 40, 0.1, 24)])
 def test_gpu_train_matches_oracle(gpu, n, v, frac, tmax):
     import cviterbi as cv
 
@@ -138,9 +139,9 @@ def test_gpu_train_converges_like_oracle(gpu):
 def test_gpu_fit_limits(gpu):
     import cviterbi as cv
 
-    off, obs, tags = _corpus(129, 4, 3, 5, 0.5, seed=1)
-    pi0, a0, b0 = _probs(129, 4, seed=1)
-    with pytest.raises(cv.CVError):  # Baum-Welch covers N <= 128
+    off, obs, tags = _corpus(257, 4, 3, 5, 0.5, seed=1)
+    pi0, a0, b0 = _probs(257, 4, seed=1)
+    with pytest.raises(cv.CVError):  # Baum-Welch covers N <= 256 (one thread per state)
         cv.fit_train(pi0, a0, b0, off, obs, tags, max_iter=1)
     with pytest.raises(cv.CVError):  # MLE needs every element tagged
         cv.fit_mle(pi0, a0, b0, off, obs, tags)

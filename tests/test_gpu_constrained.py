@@ -379,6 +379,38 @@ def test_cli_train_then_decode(gpu, tmp_path, supervised):
             assert h.emit_prob(s, o) == pytest.approx(lb[s, o], rel=tol, abs=tol)
 
 
+def test_cli_train_config4_states(gpu, tmp_path):
+    """main.rs:89-98 with -t at config 4's N = 256 and bdims [32, 32]: Baum-Welch beyond N = 128
+    (the xi sums as a matrix-core GEMM, fit.hip bw_xi_gemm), the fitted model written and used
+    by the decode; it equals a direct fit from the same start."""
+    from cviterbi import cli
+
+    rng = np.random.default_rng(11)
+    seqs, tags, test_tags = [], [], []
+    for sid in range(12):
+        T = int(rng.integers(3, 12))
+        seqs += [f"{sid} {rng.integers(0, 32)} {rng.integers(0, 32)}" for _ in range(T)]
+        tags += [f"{sid} {-1 if rng.random() < 0.5 else rng.integers(0, 256)}" for _ in range(T)]
+        test_tags += [f"{sid} -1" for _ in range(T)]
+    (tmp_path / "sequences").write_text("\n".join(seqs) + "\n")
+    (tmp_path / "tags").write_text("\n".join(tags) + "\n")
+    (tmp_path / "test_tags").write_text("\n".join(test_tags) + "\n")
+    args = ["-i", str(tmp_path), "-o", str(tmp_path / "out"), "-n", "256", "-b", "32", "32", "-p", "0", "-t",
+            "--seed", "3"]
+    assert cli.main(args) == 0
+    assert len((tmp_path / "out" / "0_0").read_text().splitlines()) == 2 + len(seqs)
+    h = cv.HMM.from_json(tmp_path / "hmm.json")
+    assert h.nstates() == 256
+    s2 = cv.load_sequences(tmp_path / "sequences", D=2)
+    t2 = cv.load_tags(tmp_path / "tags")
+    pi0, a0, b0 = cli._random_start(256, (32, 32), np.random.default_rng(3))
+    off, obs, tg = cli._flatten(s2, t2, (32, 32))
+    lp, la, lb, it = cv.fit_train(pi0, a0, b0, off, obs, tg, max_iter=1000, tol=0.001)
+    assert it >= 1
+    for s in (0, 17, 255):
+        assert h.transition_prob(s, 3, int(obs[0])) == pytest.approx(la[s, 3] + lb[3, obs[0]], rel=1e-12, abs=1e-12)
+
+
 def test_cli_cfn(gpu, tmp_path):
     """main.rs:116-118 (run_cfn): OUTPUT/problem_{prop}_0.cfn and the compile time in {prop}_0;
     the file equals the restatement of cfn.rs on the same super-sequence."""
