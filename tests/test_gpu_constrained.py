@@ -387,11 +387,20 @@ def test_cli_train_config4_states(gpu, tmp_path):
 
     rng = np.random.default_rng(11)
     seqs, tags, test_tags = [], [], []
-    for sid in range(12):
-        T = int(rng.integers(3, 12))
+    nxt = 0
+    for sid in range(64):
+        T = int(rng.integers(6, 14))
         seqs += [f"{sid} {rng.integers(0, 32)} {rng.integers(0, 32)}" for _ in range(T)]
-        tags += [f"{sid} {-1 if rng.random() < 0.5 else rng.integers(0, 256)}" for _ in range(T)]
+        for t in range(T):
+            # every state tagged at some non-final element (it keeps its a / b denominators
+            # away from 0 -- hmm.rs:165-170 divides by them), 40% of the elements untagged
+            if t < T - 1 and rng.random() < 0.6:
+                tags.append(f"{sid} {nxt % 256}")
+                nxt += 1
+            else:
+                tags.append(f"{sid} -1")
         test_tags += [f"{sid} -1" for _ in range(T)]
+    assert nxt >= 256
     (tmp_path / "sequences").write_text("\n".join(seqs) + "\n")
     (tmp_path / "tags").write_text("\n".join(tags) + "\n")
     (tmp_path / "test_tags").write_text("\n".join(test_tags) + "\n")

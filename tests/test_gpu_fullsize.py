@@ -91,3 +91,57 @@ def test_full_config5_properties(gpu, dtype):
         assert rst[0] == status[k] and np.array_equal(rp, path[lo:hi]), f"seq {k}"
         if dtype == "f64":
             assert rs[0] == score[k]
+
+
+def test_full_config5_state_terms_sample(gpu):
+    """The component STATES of full config 5 rest on the exact unary sums U_c(s) of ~32,768
+    constrained sequences' max-marginals (csp.hpp).  This checks those terms independently: the
+    GPU's exact partials of the full batch select the decode's states, and for a sample of 192
+    constrained sequences (every component) the GPU's partial words equal the oracle's own
+    max-marginals (oracle/c_oracle.py max_marginal, f64: forward row to t1 + reversed suffix
+    pass, dp.rs:153-165 semantics) turned into exact integers (units of 2^-64), state by state."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    c = synth.config("c5")
+    pi, a, b, off, obs, comp = c["pi"], c["a"], c["b"], c["offsets"], c["obs"], c["component"]
+    n, K = 256, 7
+    h = cv.HMM(pi, a, b.reshape(n, 32, 32))
+    _, _, status, states, _ = cv.decode_constrained(h, off, obs, comp, K, dtype="f64")
+    assert np.all(status == 0) and np.all(states >= 0)
+    full = cv.constrained_partials(h, off, obs, comp, K)
+    sel, _ = cv.constrained_select(n, K, full)
+    assert np.array_equal(sel, states), "the full partials select other states than the decode"
+    # sample: constrained sequences spread over the batch
+    e = np.nonzero(comp >= 0)[0]
+    seqs = np.searchsorted(off, e, side="right") - 1
+    pick = np.linspace(0, len(e) - 1, 192).astype(int)
+    ks, ts = seqs[pick], e[pick]
+    lens = off[ks + 1] - off[ks]
+    so = synth.offsets_from_lengths(lens)
+    sobs = np.concatenate([obs[off[k]:off[k + 1]] for k in ks]).astype(np.int32)
+    scomp = np.concatenate([comp[off[k]:off[k + 1]] for k in ks]).astype(np.int32)
+    gw = cv.constrained_partials(h, so, sobs, scomp, K)
+    # oracle max-marginals of the sample (C restatement, threads: ctypes releases the GIL)
+    with ThreadPoolExecutor(8) as ex:
+        mus = list(ex.map(lambda q: O.max_marginal(pi, a, b, obs[off[ks[q]]:off[ks[q] + 1]],
+                                                   int(ts[q] - off[ks[q]]), np.float64), range(len(ks))))
+    words = 5 * n + 1
+    for cc in range(K):
+        mine = [q for q in range(len(ks)) if comp[ts[q]] == cc]
+        assert mine, f"component {cc} not sampled"
+        blk = gw[cc * words:(cc + 1) * words].astype(object)
+        got = [int(blk[4 * s]) + (int(blk[4 * s + 1]) << 32) + (int(blk[4 * s + 2]) << 64) + (int(blk[4 * s + 3]) << 96)
+               for s in range(n)]
+        ninf = [int(x) for x in blk[4 * n:5 * n]]
+        want, want_inf = [0] * n, [0] * n
+        for q in mine:
+            for s in range(n):
+                x = float(mus[q][s])
+                if x == -np.inf:
+                    want_inf[s] += 1
+                else:
+                    want[s] += int(np.rint(x * 2.0 ** 64))
+        assert int(blk[5 * n]) == len(mine)
+        assert ninf == want_inf, f"component {cc}: -inf counts"
+        bad = [s for s in range(n) if got[s] != want[s]]
+        assert not bad, f"component {cc}: exact sums differ at states {bad[:8]}"
