@@ -37,6 +37,27 @@ __device__ __forceinline__ double normalized(double v, double s, int n) { return
 __device__ __forceinline__ double normalized(double v, double s, int n) { return s != 0.0 ? v * s : 1.0 / n; }
 #endif
 
+// xi without overflow.  The reference normalises each xi_t entry by entry (hmm.rs:135-141:
+// A o (alpha_t (x) u_{t+1}) / c_t, every entry <= 1); the kernels factor it as
+// A o sum_t (alpha_t / c_t) (x) u_{t+1}, and alpha / c overflows once c_t is subnormal (an EM
+// run drifting to tiny emissions: seen at N = 256 after ~250 iterations).  So the factors are
+// balanced by a power of two: r = alpha / (c 2^k), u' = u 2^k with 2^k ~ 1 / sqrt(c max u) --
+// exact scalings whose product is the same; both factors stay below ~2^540.
+__device__ __forceinline__ int xi_scale(double c, double umax) {
+  if (!(c > 0.0) || !(umax > 0.0)) return 0;
+  return -(ilogb(c) + ilogb(umax)) / 2;
+}
+
+__device__ __forceinline__ double block_max(double v, double* red) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v = fmax(v, __shfl_xor(v, off));
+  const int w = threadIdx.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[w] = v;
+  __syncthreads();
+  return fmax(fmax(red[0], red[1]), fmax(red[2], red[3]));
+}
+
 __global__ __launch_bounds__(256) void mle_counts(MleArgs g) {
   const int64_t seq = blockIdx.x;
   const int64_t e0 = g.offsets[seq], e1 = g.offsets[seq + 1];
@@ -168,10 +189,12 @@ __global__ __launch_bounds__(256) void bw_stats(BwArgs g) {
       const double ai = (i < N) ? al[(size_t)t * N + i] : 0.0;
       const double c = block_sum(ai * w, red);
       if (c != 0.0) {
-        // S[k][j] += (alpha_t[k] / c) * u_j: thread j = i owns column i; alpha/c via LDS
-        const double uj = (i < N) ? p[i] : 0.0;
+        // S[k][j] += (alpha_t[k] / c) * u_j: thread j = i owns column i; alpha/c via LDS,
+        // both factors balanced by 2^k (xi_scale)
+        const int ks = xi_scale(c, block_max((i < N) ? p[i] : 0.0, red));
+        const double uj = (i < N) ? __builtin_ldexp(p[i], ks) : 0.0;
         __syncthreads();
-        if (i < N) p[i] = ai / c;
+        if (i < N) p[i] = ai / __builtin_ldexp(c, ks);
         __syncthreads();
         if (i < N)
           for (int k = 0; k < N; ++k) S[(size_t)k * N + i] += p[k] * uj;
@@ -232,8 +255,9 @@ __global__ __launch_bounds__(256) void bw_stats_rows(BwArgs g) {
       if (i < N)
         for (int k = 0; k < N; ++k) w += g.at[(size_t)k * N + i] * p[k];
       const double c = block_sum(ai * w, red);
-      u = (i < N) ? p[i] : 0.0;
-      if (c != 0.0) r = ai / c;
+      const int ks = xi_scale(c, block_max((i < N) ? p[i] : 0.0, red));  // balanced factors
+      u = (i < N) ? __builtin_ldexp(p[i], ks) : 0.0;
+      if (c != 0.0) r = ai / __builtin_ldexp(c, ks);
       else z += 1.0;  // xi_t uniform (hmm.rs:306-317), counted separately
     }
     if (i < N) {
@@ -327,6 +351,15 @@ __device__ __forceinline__ double wave_sum(double v) {
   v += dpp_f64<0x141>(v);  // row_half_mirror: quad q <-> 1-q within 8
   v += dpp_f64<0x140>(v);  // row_mirror: half h <-> 1-h within 16
   return (readlane_f64(v, 0) + readlane_f64(v, 16)) + (readlane_f64(v, 32) + readlane_f64(v, 48));
+}
+
+// maximum over the 64 lanes, the identical value in every lane
+__device__ __forceinline__ double wave_max(double v) {
+  v = fmax(v, dpp_f64<0xB1>(v));
+  v = fmax(v, dpp_f64<0x4E>(v));
+  v = fmax(v, dpp_f64<0x141>(v));
+  v = fmax(v, dpp_f64<0x140>(v));
+  return fmax(fmax(readlane_f64(v, 0), readlane_f64(v, 16)), fmax(readlane_f64(v, 32), readlane_f64(v, 48)));
 }
 
 // two independent sums with their latencies overlapped
@@ -594,7 +627,7 @@ __global__ __launch_bounds__(256) void bw_bwd_stats_wave(BwArgs g, int64_t nseq,
       for (int k = 0; k < 8; ++k) {
         const int r = r0 + k;
         if (r >= L - 1) break;
-        double alt[2], wv[2];
+        double alt[2], wv[2], uval[2];
         bool valid[2];
 #pragma unroll
         for (int x = 0; x < 2; ++x) {
@@ -604,7 +637,8 @@ __global__ __launch_bounds__(256) void bw_bwd_stats_wave(BwArgs g, int64_t nseq,
           fetch_ea(x, t - 2, (k + 2) & 7, (k + 2) & 3);
           alt[x] = (act && valid[x]) ? pa[x][k & 3] : 0.0;
           // u_{t+1} = b(o_{t+1}) o beta_{t+1}  (hmm.rs:113-116, 135-141)
-          if (i < NP) uu[w][2 * (k & 1) + x][i] = (act && valid[x]) ? pe[x][(k + 3) & 3] * beta[x] : 0.0;
+          uval[x] = (act && valid[x]) ? pe[x][(k + 3) & 3] * beta[x] : 0.0;
+          if (i < NP) uu[w][2 * (k & 1) + x][i] = uval[x];
         }
         __builtin_amdgcn_wave_barrier();
         {  // w_x[i] = sum_j A[i][j] u_x[j], one pass over the row of A for both sequences
@@ -631,7 +665,13 @@ __global__ __launch_bounds__(256) void bw_bwd_stats_wave(BwArgs g, int64_t nseq,
 #pragma unroll
         for (int x = 0; x < 2; ++x) {
           z += (valid[x] && c[x] == 0.0) ? 1.0 : 0.0;  // xi_t uniform (hmm.rs:306-317), counted separately
-          if (i < NP) rr[w][2 * (k & 1) + x][i] = c[x] != 0.0 ? alt[x] / c[x] : 0.0;
+          // r = alpha / (c 2^k) and u' = u 2^k (xi_scale): the row of u the MFMA update reads
+          // is rescaled in place (this lane's own entry; w above used the unscaled one)
+          const int ks = xi_scale(c[x], wave_max(uval[x]));
+          if (i < NP) {
+            rr[w][2 * (k & 1) + x][i] = c[x] != 0.0 ? alt[x] / __builtin_ldexp(c[x], ks) : 0.0;
+            uu[w][2 * (k & 1) + x][i] = __builtin_ldexp(uval[x], ks);
+          }
           const int tg = ptg[x][k];
           const double nb = tg >= 0 ? (i == tg ? 1.0 : 0.0) : (act ? normalized(wv[x], sw[x], N) : 0.0);
           beta[x] = valid[x] ? nb : beta[x];

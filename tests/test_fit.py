@@ -124,6 +124,29 @@ def test_gpu_train_matches_oracle(gpu, n, v, frac, tmax):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("n", [20, 100, 200])  # wave kernels, LDS xi sum, GEMM xi sum
+def test_gpu_train_subnormal_xi_denominator(gpu, n):
+    """Emission probabilities below DBL_MIN for one observation make xi's normaliser c_t
+    subnormal: the reference normalises xi entry by entry (hmm.rs:135-141) and stays finite;
+    the kernels' factor alpha_t / c_t would overflow (inf * 0 = NaN in the sums) without the
+    balanced power-of-two scaling (fit.hip xi_scale).  Two iterations against the oracle."""
+    import cviterbi as cv
+
+    v = 12
+    off, obs, tags = _corpus(n, v, 20, 30, 0.1, seed=300 + n)
+    pi0, a0, b0 = _probs(n, v, seed=300 + n)
+    b0[:, 3] = 1e-311 * (1.0 + np.arange(n) / n)  # subnormal
+    assert np.count_nonzero(obs == 3) > 5
+    gp, ga, gb, it = cv.fit_train(pi0, a0, b0, off, obs, tags, max_iter=2, tol=0.0)
+    rp, ra, rb, _ = FO.train(pi0, a0, b0, off, obs, tags, 2, 0.0)
+    for g, r, what in zip((gp, ga, gb), (rp, ra, rb), ("pi", "a", "b")):
+        assert not np.isnan(g).any(), what
+        assert np.array_equal(np.isinf(g), np.isinf(r)), what
+        fin = np.isfinite(r)
+        np.testing.assert_allclose(g[fin], r[fin], rtol=0, atol=1e-9, err_msg=what)
+
+
+@pytest.mark.gpu
 def test_gpu_train_converges_like_oracle(gpu):
     import cviterbi as cv
 

@@ -410,14 +410,13 @@ def test_cli_train_config4_states(gpu, tmp_path):
     assert len((tmp_path / "out" / "0_0").read_text().splitlines()) == 2 + len(seqs)
     h = cv.HMM.from_json(tmp_path / "hmm.json")
     assert h.nstates() == 256
-    s2 = cv.load_sequences(tmp_path / "sequences", D=2)
-    t2 = cv.load_tags(tmp_path / "tags")
-    pi0, a0, b0 = cli._random_start(256, (32, 32), np.random.default_rng(3))
-    off, obs, tg = cli._flatten(s2, t2, (32, 32))
-    lp, la, lb, it = cv.fit_train(pi0, a0, b0, off, obs, tg, max_iter=1000, tol=0.001)
-    assert it >= 1
-    for s in (0, 17, 255):
-        assert h.transition_prob(s, 3, int(obs[0])) == pytest.approx(la[s, 3] + lb[3, obs[0]], rel=1e-12, abs=1e-12)
+    # this EM does not settle (sum |new - old| oscillates: the 1,000 iterations all run), so
+    # two GPU runs, whose f64 atomics add in different orders, drift apart: check the written
+    # model is a proper log10 HMM (rows sum to 1, nothing NaN; the tiny-c_t steps it meets are
+    # test_gpu_train_subnormal_xi_denominator's) -- parity vs the oracle is test_fit.py's
+    a = np.stack([h.transitions_to(j) for j in range(256)], axis=1)  # a[i, j], log10
+    assert not np.isnan(a).any()
+    assert np.allclose((10.0 ** a).sum(axis=1), 1.0, rtol=1e-9)
 
 
 def test_cli_cfn(gpu, tmp_path):
