@@ -203,7 +203,7 @@ struct cv_hmm {
     std::vector<hipEvent_t> ev;
     hipStream_t stream = nullptr;  // lowest priority: fills what the constrained work leaves idle
     hipStream_t hi = nullptr;      // highest priority: the constrained work itself
-    hipEvent_t start = nullptr, done = nullptr;
+    hipEvent_t start = nullptr, done = nullptr, after = nullptr;
   } side;
   DevBuf st_off, st_obs, st_path, st_score, st_status, st_forced;
   DevBuf cs_ranges, cs_delta, cs_g, cs_mu, cs_start, cs_zero;  // constrained-decode scratch
@@ -246,6 +246,7 @@ struct cv_hmm {
     for (auto e : side.ev) (void)hipEventDestroy(e);
     if (side.start) (void)hipEventDestroy(side.start);
     if (side.done) (void)hipEventDestroy(side.done);
+    if (side.after) (void)hipEventDestroy(side.after);
     if (side.stream) (void)hipStreamDestroy(side.stream);
     if (side.hi) (void)hipStreamDestroy(side.hi);
     if (rs_ev) (void)hipEventDestroy(rs_ev);
@@ -1989,9 +1990,18 @@ cv_status side_decode_launch(cv_hmm* h, int64_t nseq, const int64_t* offsets_hos
     return CV_OK;
   }
   // the side stream starts behind everything the caller had queued on its stream when the
-  // constrained decode began (h->side.start, recorded then), not behind the term launches
-  (void)stream;
-  HIP_TRY(hipStreamWaitEvent(sd.stream, sd.start, 0));
+  // constrained decode began (h->side.start, recorded then), not behind the term launches;
+  // A/B knob CV_SIDE_AFTER=1: behind the term launches (the terms pass alone on the device,
+  // then the side decode beside the search and the suffix trace)
+  const char* after_env = getenv("CV_SIDE_AFTER");
+  if (after_env && *after_env == '1') {
+    if (!sd.after && hipEventCreateWithFlags(&sd.after, hipEventDisableTiming) != hipSuccess)
+      return set_err(CV_EDEVICE, "hipEventCreate failed");
+    HIP_TRY(hipEventRecord(sd.after, stream));
+    HIP_TRY(hipStreamWaitEvent(sd.stream, sd.after, 0));
+  } else {
+    HIP_TRY(hipStreamWaitEvent(sd.stream, sd.start, 0));
+  }
   HIP_TRY(hipMemcpyAsync(sd.idx.p, sd.idx_host.data(), sd.idx_host.size() * 8, hipMemcpyHostToDevice, sd.stream));
   const int64_t* cstart_d = sd.idx.as<int64_t>();
   const int64_t* cseq_d = cstart_d + nu;
