@@ -401,10 +401,13 @@ def main():
             rp = torch.empty(B * T_LEN, dtype=torch.int32, device=dev)
             rs = torch.empty(B, dtype=torch.float64, device=dev)
             rst = torch.empty(B, dtype=torch.uint8, device=dev)
-            cv.decode_batch_device(h, torch.from_numpy(off_gh).to(dev), obs_g, rp, rs, rst, offsets_host=off_gh,
+            # its own handle: the global batch's workspace (68.7 GB of f64 rows) is freed with it
+            hv = cv.HMM(pi, a, b.reshape(N_STATES, 32, 32), device=local)
+            cv.decode_batch_device(hv, torch.from_numpy(off_gh).to(dev), obs_g, rp, rs, rst, offsets_host=off_gh,
                                    stream=stream.cuda_stream, dtype=args.dtype,
                                    workspace_bytes=WORKSPACE_F64 if f64 else WORKSPACE)
             torch.cuda.synchronize(dev)
+            del hv
             ok = bool(torch.equal(gp.to(dev), rp) and torch.equal(gs.to(dev).view(torch.int64), rs.view(torch.int64))
                       and torch.equal(gst.to(dev), rst))
             verify = {"what": "last step's gathered paths/scores/statuses (all ranks) == rank 0's single-GPU "
