@@ -2015,6 +2015,13 @@ cv_status side_decode_launch(cv_hmm* h, int64_t nseq, const int64_t* offsets_hos
   cv_opts o2 = o;
   o2.forced = nullptr;
   o2.rescore_f64 = 0;  // f64: the decode's score is the reference's
+  {  // A/B knob CV_SIDE_CHUNKS=k: the side decode in k chunks (each chunk's backtrack runs
+     // beside the next chunk's forward and the constrained work; the last one is shorter)
+    const char* e = getenv("CV_SIDE_CHUNKS");
+    const int k = e ? atoi(e) : 1;
+    if (k > 1 && cvk::t64_padded_states(h->N))
+      o2.workspace_bytes = ((uint64_t)total2 * h->np64 * 8 + (uint64_t)k - 1) / (uint64_t)k + 4096;
+  }
   if ((st = decode_device(h, nu, off2, off2_d, sd.obs2.as<int32_t>(), o2, sd.path2.as<int32_t>(), score2, status2,
                           sd.stream, nullptr, /*side_ws=*/true)) != CV_OK) {
     if (st != CV_ENOMEM) return st;
