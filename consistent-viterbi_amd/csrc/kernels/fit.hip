@@ -753,7 +753,10 @@ __global__ __launch_bounds__(256) void bw_mstep_pa(MstepArgs m) {
   }
   for (int k = threadIdx.x; k < N * N; k += blockDim.x) {
     const int i = k / N, j = k - i * N;
-    const double na = (m.a[k] * xs[k] + zu) / a_den[i];
+    // a == 0: every xi_t entry at (i, j) is 0 in the reference (A o ..., hmm.rs:135-141), so
+    // the term is 0 whatever the factored sum S holds there (it may overflow to inf when
+    // alpha_t u_t+1 / c_t grows where A is 0: 0 * inf would be NaN)
+    const double na = ((m.a[k] != 0.0 ? m.a[k] * xs[k] : 0.0) + zu) / a_den[i];
     d += fabs(na - m.a[k]);
     m.a[k] = na;
     m.at[(size_t)j * N + i] = na;
