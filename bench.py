@@ -219,7 +219,36 @@ def bench_configs(dev, stream):
         out[name] = d
         del h, o_d, ob_d, p_d, s_d, st_d
         torch.cuda.empty_cache()
+    out["c4_superseq_cp"] = bench_superseq_cp(dev)
     return out
+
+
+def bench_superseq_cp(dev):
+    """What main.rs:120 runs on config 4's data: CPSolver over the WHOLE batch as one chained
+    super-sequence (cv_decode_superseq_cp = solver kind gpu-cp, the CLI default; 33.5 M
+    elements, N = 256): the parallel chain (per-sequence f64 trellis decode certified to be the
+    chain's own path at the running total, host fold, serial-chain re-runs of the uncertified
+    sequences), bit-identical to the serial chain.  Host arrays in and out (the host API)."""
+    import cviterbi as cv
+    from cviterbi import synth
+
+    c = synth.config("c4")
+    h = cv.HMM(c["pi"], c["a"], c["b"].reshape(N_STATES, 32, 32), device=dev.index)
+    cv.decode_superseq_cp(h, c["offsets"][:3], c["obs"][:2 * T_LEN])  # tables
+    times = []
+    for _ in range(2):
+        t0 = time.perf_counter()
+        _, obj = cv.decode_superseq_cp(h, c["offsets"], c["obs"])
+        times.append(time.perf_counter() - t0)
+    st = cv.last_superseq_stats(h)
+    L = int(c["offsets"][-1])
+    del h
+    return {"workload": "config4's 65,536 x 512 elements as ONE CPSolver super-sequence (main.rs:120, "
+                        "cp.rs:63-93 over utils.rs:62-103), N=256, exact f64; host arrays (PCIe included)",
+            "ms_per_solve": min(times) * 1e3, "elements_per_s": L / min(times), "objective": obj,
+            "stats": st, "serial_chain_us_per_element": 3.48,
+            "note": "serial chain kernel: 3.48 us/element at N=256 (profiles/r03_cp_chain.txt), i.e. ~117 s "
+                    "for this input"}
 
 
 def c5_sharded(dev, world, rank, dist, backend, nseq, reps):
