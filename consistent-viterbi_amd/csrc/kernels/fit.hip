@@ -753,10 +753,13 @@ __global__ __launch_bounds__(256) void bw_mstep_pa(MstepArgs m) {
   }
   for (int k = threadIdx.x; k < N * N; k += blockDim.x) {
     const int i = k / N, j = k - i * N;
-    // a == 0: every xi_t entry at (i, j) is 0 in the reference (A o ..., hmm.rs:135-141), so
-    // the term is 0 whatever the factored sum S holds there (it may overflow to inf when
-    // alpha_t u_t+1 / c_t grows where A is 0: 0 * inf would be NaN)
-    const double na = ((m.a[k] != 0.0 ? m.a[k] * xs[k] : 0.0) + zu) / a_den[i];
+    // The factored sum S = sum_t alpha_t u_t+1 / c_t can exceed DBL_MAX exactly where A is 0
+    // or subnormal (each xi_t entry A alpha u / c is <= 1, hmm.rs:135-141, so alpha u / c <=
+    // 1 / A): a == 0 takes no term (the reference's entries are 0 there; 0 * inf would be NaN),
+    // and S is clamped to DBL_MAX (finite for a subnormal a; never reached for a normal one
+    // unless ~1/a summed over steps overflows)
+    const double na =
+        ((m.a[k] != 0.0 ? m.a[k] * fmin(xs[k], 1.7976931348623157e308) : 0.0) + zu) / a_den[i];
     d += fabs(na - m.a[k]);
     m.a[k] = na;
     m.at[(size_t)j * N + i] = na;

