@@ -238,8 +238,9 @@ struct cv_hmm {
   uint64_t last_explored = 0;
   int64_t last_traced = 0;  // constrained sequences the last resume flow certified (suffix trace)
   // the last cv_decode_superseq_cp: parallel chain ran (1/0), sequences certified, sequences in
-  // serial-chain runs, runs, certified folds done by the quantised sum
-  int64_t last_chain[5] = {0, 0, 0, 0, 0};
+  // serial-chain runs, runs, certified folds done by the quantised sum, sequences taken from
+  // speculative parallel re-decodes, such batches
+  int64_t last_chain[7] = {0, 0, 0, 0, 0, 0, 0};
 
   ~cv_hmm() {
     for (auto e : ev) (void)hipEventDestroy(e);
@@ -586,7 +587,8 @@ cvk::BacktrackArgs make_bt_args(cv_hmm* h, unsigned char* wsb, const int64_t* of
 cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, const int64_t* offsets_dev,
                         const int32_t* obs_dev, const cv_opts& o, int32_t* path_dev, double* score_dev,
                         uint8_t* status_dev, hipStream_t stream, const void* resume_rows = nullptr,
-                        bool side_ws = false, double* cp_cert = nullptr) {
+                        bool side_ws = false, double* cp_cert = nullptr, const double* cp_init = nullptr,
+                        double* cp_last = nullptr) {
   // cp_cert (the parallel CPSolver chain, row-A0 f64 trellis only): after each chunk's
   // backtrack, cp_cert_f64 reads the chunk's rows and paths -> [nseq][2] certificates
   // side_ws: the handle's second workspace (h->side), no timing / last-call bookkeeping -- a
@@ -913,6 +915,8 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
         fa.nstates = h->N;
         fa.psi = reinterpret_cast<uint16_t*>(wsb);
         fa.last_row = reinterpret_cast<double*>(lrb);
+        fa.cp_init = cp_init;  // the parallel chain's speculative re-decodes (start offsets)
+        fa.cp_last = cp_last;
         err = cvk::launch_t64_cp_fwd(h->np64, spw, fa, n, stream);
       } else {
         const cvk::T64BtArgs ba = t64_bt_args(c, wsb);
@@ -2619,7 +2623,7 @@ cv_status sum_timing(cv_hmm* h, size_t eb, int64_t launches, cv_timing* out) {
 
 CV_API cv_status cv_last_superseq_stats(const cv_hmm* h, int64_t* out) {
   if (!h || !out) return set_err(CV_EINVAL, "null argument");
-  for (int q = 0; q < 5; ++q) out[q] = h->last_chain[q];
+  for (int q = 0; q < 7; ++q) out[q] = h->last_chain[q];
   return CV_OK;
 }
 
@@ -2789,16 +2793,21 @@ cv_status superseq_cp_wg(cv_hmm* h, int64_t L, const int32_t* obs, const std::ve
 //     sequence's values share the binade 2^e predicted from the per-sequence optima, else
 //     element by element -- and its end state is its path's; the boundary into the next
 //     sequence must be clean (gF);
-//  3. an uncertified sequence (near ties at the chain's magnitude, rho <= U) runs through the
-//     serial chain kernel itself (cp_chain_wg) from the exact previous row -- a synthetic one
-//     (M at the previous end state, -inf elsewhere: what a clean boundary sees) or the previous
-//     run's last row -- and consecutive such sequences form one run, backtracked from the state
-//     the next sequence's boundary picks.
+//  3. the uncertified sequences (near ties at the chain's magnitude, rho <= U) are re-decoded
+//     IN PARALLEL by the per-sequence CP kernel from the offsets a fold along the row-A0 paths
+//     predicts (speculation); a result is the chain's own when its offset was the chain's exact
+//     maximum and its start and end boundaries are clean;
+//  4. what speculation cannot settle runs through the serial chain kernel itself (cp_chain_wg)
+//     from the exact previous row -- a synthetic one (M at the previous end state, -inf
+//     elsewhere: what a clean boundary sees) or the previous sequence's exact last row -- and
+//     consecutive such sequences form one run, backtracked from the state the next sequence's
+//     boundary picks.
 // Bit-identical to the serial chain by construction (tests: the serial chain, CV_CHAIN_PAR=0,
 // and the C oracle cvo_cp_superseq_f64).  Models with entries outside [-2^80, 0], infeasible
 // sequences or N > 256: *applied = false (the caller runs the serial chain).
 // Knobs (bit-identical): CV_CHAIN_PAR=0 (serial chain), CV_CHAIN_PAR_FORCE=m (every m-th
-// non-empty sequence taken as uncertified: exercises the runs).
+// non-empty sequence taken as uncertified: exercises speculation and the runs), CV_CHAIN_SPEC=0
+// (no speculation: every uncertified sequence through the serial chain kernel).
 cv_status superseq_cp_par(cv_hmm* h, int64_t nseq, const int64_t* offsets, const int32_t* obs, int32_t* path_out,
                           double* objective_out, bool* applied) {
   *applied = false;
@@ -2895,6 +2904,10 @@ cv_status superseq_cp_par(cv_hmm* h, int64_t nseq, const int64_t* offsets, const
     const char* e = getenv("CV_CHAIN_PAR_FORCE");
     return e ? std::max(0, atoi(e)) : 0;
   }();
+  const bool spec_env = [] {  // A/B knob: CV_CHAIN_SPEC=0 re-runs every uncertified sequence serially
+    const char* e = getenv("CV_CHAIN_SPEC");
+    return !(e && *e == '0');
+  }();
   const int32_t* P = path_out;  // the row-A0 paths (element index relative to base)
   const int32_t* ob = obs + base;
   auto fold_elems = [&](int64_t k, double M) {  // the CP fold of sequence k's path from M
@@ -2908,24 +2921,72 @@ cv_status superseq_cp_par(cv_hmm* h, int64_t nseq, const int64_t* offsets, const
     }
     return d;
   };
-  // run state: the chain kernel over consecutive uncertified sequences
+  // the fold of a certified path: M + q 2^(e-52) when M and the sequence's values share the
+  // predicted binade 2^e (cp_quant_f64), else element by element
+  auto fold = [&](int64_t k, double M, bool* quant) {
+    *quant = false;
+    const int e = ebin[(size_t)k];
+    if (e != cvk::CVK_NO_BINADE && !tie[(size_t)k] && M != 0.0 && std::ilogb(std::fabs(M)) == e &&
+        std::fabs((double)qv[(size_t)k]) < 0x1p53) {
+      const double Mn = M + std::ldexp((double)qv[(size_t)k], e - 52);
+      if (std::ilogb(std::fabs(Mn)) == e) {
+        *quant = true;
+        return Mn;
+      }
+    }
+    return fold_elems(k, M);
+  };
+  std::vector<int64_t> ks;
+  for (int64_t k = 0; k < nseq; ++k)
+    if (off[(size_t)k + 1] > off[(size_t)k]) ks.push_back(k);
+  auto score_of = [&](size_t x) { return x < ks.size() ? std::fabs(score[(size_t)ks[x]]) : 0.0; };
+
+  // The state of the chain before the sequence at hand: NONE (first sequence), CERT (a certified
+  // sequence ended in prev_end with maximum M, a clean boundary), ROW (the exact last row is
+  // known: row_host, NP wide, -inf padded; on the device at row_dev when non-null).
+  enum Kind { NONE, CERT, ROW };
+  Kind prev = NONE;
+  int32_t prev_end = 0, row_arg = 0;
+  double M = 0.0;
+  std::vector<double> row_host((size_t)NP, -INFINITY), syn((size_t)NP);
+  const double* row_dev = nullptr;
+  // the last row is clean for a start whose values reach magnitude `mag`: no earlier state's
+  // value can round onto its maximum when pi[j] is added (utils.rs:32-35)
+  auto row_clean = [&](const double* row, int32_t arg, double m1, double mag) {
+    const double gap = 0x1p-51 * (std::fabs(m1) + mag);
+    for (int32_t i = 0; i < arg; ++i)
+      if (!(m1 - row[i] > gap)) return false;
+    return true;
+  };
+  // sequence ks[x] certified at running maximum Mc after a predecessor of kind pk (the row test
+  // against row_host when pk == ROW); *Mn = its fold
+  auto certify = [&](size_t x, double Mc, Kind pk, double* Mn, bool* quant) {
+    const int64_t k = ks[x];
+    const int64_t T = off[(size_t)k + 1] - off[(size_t)k];
+    const double S = score_of(x), rho = cert[(size_t)k * 2], gF = cert[(size_t)k * 2 + 1];
+    const double U = 0x1p-52 * (std::fabs(Mc) + S + 16.0);
+    if (!(rho > U) || (force_m > 0 && (int64_t)(x % (size_t)force_m) == force_m - 1)) return false;
+    if (pk == ROW && !row_clean(row_host.data(), row_arg, Mc, S + pimax + 16.0)) return false;
+    *Mn = fold(k, Mc, quant);
+    // the boundary into the next sequence: its start values must not merge with this
+    // sequence's maximum (the exact final gap, less the chain's drift, beats 2 ulps there)
+    const double U1 = 0x1p-52 * (std::fabs(*Mn) + score_of(x + 1) + pimax + 16.0);
+    return x + 1 >= ks.size() || gF - 3.0 * (double)T * U > 2.0 * U1;
+  };
+
+  // ---- runs: the serial chain kernel over consecutive uncertified sequences ----
   DevBuf d_first, d_rpsi, d_rows, d_small, d_rpath;
   if ((st = d_first.ensure((size_t)std::max<int64_t>(maxT, 1))) != CV_OK) return st;
   HIP_TRY(hipMemsetAsync(d_first.p, 0, (size_t)std::max<int64_t>(maxT, 1), stream));
   HIP_TRY(hipMemsetAsync(d_first.p, 1, 1, stream));  // one sequence per launch: its element 0 starts it
   if ((st = d_rows.ensure((size_t)NP * 8 * 3)) != CV_OK) return st;
   if ((st = d_small.ensure(16)) != CV_OK) return st;
-  double* row_in = d_rows.as<double>();  // synthetic start row
+  double* row_in = d_rows.as<double>();  // start row uploaded from the host
   double* row_a = row_in + NP;           // the run's last rows (ping-pong)
   double* row_b = row_a + NP;
-  std::vector<double> row_host((size_t)NP), syn((size_t)NP);
   bool in_run = false;
-  int64_t run_e0 = 0, run_len = 0, runs = 0, run_seqs = 0, ncert = 0, nquant = 0;
+  int64_t run_e0 = 0, run_len = 0, runs = 0, run_seqs = 0, ncert = 0, nquant = 0, spec_acc = 0, spec_batches = 0;
   int64_t psi_cap = 0;
-  int32_t run_arg = 0;  // first argmax of the run's last row
-  enum { NONE, CERT, RUN } prev = NONE;
-  int32_t prev_end = 0;
-  double M = 0.0;
   auto end_run = [&](int32_t end_state) -> cv_status {
     if ((st = d_rpath.ensure((size_t)run_len * 4)) != CV_OK) return st;
     if ((st = chain_backtrack(h, d_rpsi.as<uint16_t>(), run_len, end_state, d_rpath.as<int32_t>(), stream)) != CV_OK)
@@ -2938,19 +2999,23 @@ cv_status superseq_cp_par(cv_hmm* h, int64_t nseq, const int64_t* offsets, const
   auto run_step = [&](int64_t k) -> cv_status {  // sequence k through the serial chain kernel
     const int64_t e0 = off[(size_t)k], T = off[(size_t)k + 1] - e0;
     const double* init = nullptr;
+    if (prev == CERT) {  // what a clean boundary after a certified sequence sees
+      std::fill(syn.begin(), syn.end(), -INFINITY);
+      syn[(size_t)prev_end] = M;
+      HIP_TRY(hipMemcpyAsync(row_in, syn.data(), (size_t)NP * 8, hipMemcpyHostToDevice, stream));
+      init = row_in;
+    } else if (prev == ROW) {
+      if (!row_dev) {  // a speculative decode's last row: the exact row, uploaded
+        HIP_TRY(hipMemcpyAsync(row_in, row_host.data(), (size_t)NP * 8, hipMemcpyHostToDevice, stream));
+        row_dev = row_in;
+      }
+      init = row_dev;
+    }
     if (!in_run) {
       in_run = true;
       run_e0 = e0;
       run_len = 0;
       ++runs;
-      if (prev == CERT) {  // what a clean boundary after a certified sequence sees
-        std::fill(syn.begin(), syn.end(), -INFINITY);
-        syn[(size_t)prev_end] = M;
-        HIP_TRY(hipMemcpyAsync(row_in, syn.data(), (size_t)NP * 8, hipMemcpyHostToDevice, stream));
-        init = row_in;
-      }
-    } else {
-      init = row_a;
     }
     if (run_len + T > psi_cap) {  // grow the run's psi rows (rare: long runs)
       const int64_t cap = std::max<int64_t>(2 * psi_cap, std::max<int64_t>(run_len + T, 4 * maxT));
@@ -2976,74 +3041,162 @@ cv_status superseq_cp_par(cv_hmm* h, int64_t nseq, const int64_t* offsets, const
     g.objective = d_small.as<double>();
     g.final_state = reinterpret_cast<int32_t*>(d_small.as<double>() + 1);
     g.init_row = init;
-    g.final_row = row_b;
+    double* out_row = init == row_a ? row_b : row_a;
+    g.final_row = out_row;
     const hipError_t err = cvk::launch_cp_chain_wg(NP, g, stream);
     if (err != hipSuccess) return set_err(CV_EDEVICE, "chain run launch failed: %s", hipGetErrorString(err));
     double out[2];
     HIP_TRY(hipMemcpyAsync(out, d_small.p, 16, hipMemcpyDeviceToHost, stream));
-    HIP_TRY(hipMemcpyAsync(row_host.data(), row_b, (size_t)NP * 8, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipMemcpyAsync(row_host.data(), out_row, (size_t)NP * 8, hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipStreamSynchronize(stream));
-    std::swap(row_a, row_b);
+    row_dev = out_row;
     M = out[0];
-    std::memcpy(&run_arg, &out[1], 4);
+    std::memcpy(&row_arg, &out[1], 4);
     run_len += T;
     ++run_seqs;
-    prev = RUN;
+    prev = ROW;
     return CV_OK;
   };
-  // the last row of a run is clean for a start whose values reach magnitude `mag`: no earlier
-  // state's value can round onto the maximum when pi[j] is added (utils.rs:32-35)
-  auto run_clean = [&](double mag) {
-    const double gap = 0x1p-51 * (std::fabs(M) + mag);
-    for (int32_t i = 0; i < run_arg; ++i)
-      if (!(M - row_host[(size_t)i] > gap)) return false;
-    return true;
-  };
-  std::vector<int64_t> ks;
-  for (int64_t k = 0; k < nseq; ++k)
-    if (off[(size_t)k + 1] > off[(size_t)k]) ks.push_back(k);
-  for (size_t x = 0; x < ks.size(); ++x) {
-    const int64_t k = ks[x];
-    const int64_t T = off[(size_t)k + 1] - off[(size_t)k];
-    const double S = std::fabs(score[(size_t)k]);
-    const double snext = x + 1 < ks.size() ? std::fabs(score[(size_t)ks[x + 1]]) : 0.0;
-    const double rho = cert[(size_t)k * 2], gF = cert[(size_t)k * 2 + 1];
-    const double U = 0x1p-52 * (std::fabs(M) + S + 16.0);
-    bool ok = rho > U && !(force_m > 0 && (int64_t)(x % (size_t)force_m) == force_m - 1);
-    if (ok && prev == RUN && !run_clean(S + pimax + 16.0)) ok = false;
-    if (ok) {
+
+  // ---- speculation: the uncertified sequences re-decoded IN PARALLEL by the per-sequence CP
+  // kernel (trellis_cp_f64) from the offsets a fold along the row-A0 paths predicts.  A
+  // sequence's result is the chain's own exactly when its offset was the chain's exact running
+  // maximum and its start clean; a prediction goes wrong only after an earlier uncertified
+  // sequence's path changed, so one batch resolves the fallbacks up to there, and the next
+  // batch (from the exact maximum) the ones after.  Batches that resolve little (tie-heavy
+  // models) switch speculation off: the serial runs take over.
+  std::vector<int64_t> spec_idx((size_t)nseq, -1);
+  std::vector<double> spec_guess, spec_last;
+  std::vector<int64_t> spec_off;
+  std::vector<int32_t> spec_path;
+  bool spec_on = spec_env;
+  int64_t batch_acc = 0, batch_size = 0;
+  size_t spec_from = SIZE_MAX;  // position a batch was last launched from
+  constexpr int64_t kSpecMax = 16384;
+  DevBuf d_soff, d_sobs, d_spath, d_sres, d_sinit, d_slast;
+  auto speculate = [&](size_t x0) -> cv_status {
+    std::vector<int64_t> F;
+    std::vector<double> G;
+    double Ms = M;
+    Kind pk = prev;
+    for (size_t y = x0; y < ks.size() && (int64_t)F.size() < kSpecMax; ++y) {
       double Mn;
-      const int e = ebin[(size_t)k];
-      if (e != cvk::CVK_NO_BINADE && !tie[(size_t)k] && M != 0.0 && std::ilogb(std::fabs(M)) == e &&
-          std::fabs((double)qv[(size_t)k]) < 0x1p53) {
-        Mn = M + std::ldexp((double)qv[(size_t)k], e - 52);
-        if (std::ilogb(std::fabs(Mn)) != e) Mn = fold_elems(k, M);  // left the binade
-        else ++nquant;
-      } else {
-        Mn = fold_elems(k, M);
-      }
-      // the boundary into the next sequence: its start values must not merge with this
-      // sequence's maximum (the exact final gap, less the chain's error, beats 2 ulps there)
-      const double U1 = 0x1p-52 * (std::fabs(Mn) + snext + pimax + 16.0);
-      if (x + 1 < ks.size() && !(gF - 3.0 * (double)T * U > 2.0 * U1)) ok = false;
-      if (ok) {
-        if (in_run && (st = end_run(run_arg)) != CV_OK) return st;
-        M = Mn;
-        prev = CERT;
-        prev_end = P[off[(size_t)k + 1] - 1];
-        ++ncert;
+      bool qd;
+      if (certify(y, Ms, y == x0 ? pk : CERT, &Mn, &qd)) {
+        Ms = Mn;
         continue;
+      }
+      if (y == x0 && pk == ROW && !row_clean(row_host.data(), row_arg, Ms, score_of(y) + pimax + 16.0)) break;
+      F.push_back(ks[y]);
+      G.push_back(Ms);
+      Ms = fold_elems(ks[y], Ms);  // predicted: the chain keeps the row-A0 path
+    }
+    std::fill(spec_idx.begin(), spec_idx.end(), -1);
+    spec_guess.clear();
+    if (F.empty()) return CV_OK;
+    const int64_t nf = (int64_t)F.size();
+    std::vector<int64_t> so((size_t)nf + 1, 0);
+    for (int64_t i = 0; i < nf; ++i) so[(size_t)i + 1] = so[(size_t)i] + (off[(size_t)F[i] + 1] - off[(size_t)F[i]]);
+    const int64_t Ls = so[(size_t)nf];
+    std::vector<int32_t> sob((size_t)Ls);
+    for (int64_t i = 0; i < nf; ++i)
+      std::memcpy(sob.data() + so[(size_t)i], ob + off[(size_t)F[i]], (size_t)(so[(size_t)i + 1] - so[(size_t)i]) * 4);
+    if ((st = d_soff.ensure((size_t)(nf + 1) * 8)) != CV_OK) return st;
+    if ((st = d_sobs.ensure((size_t)Ls * 4)) != CV_OK) return st;
+    if ((st = d_spath.ensure((size_t)Ls * 4)) != CV_OK) return st;
+    if ((st = d_sres.ensure((size_t)nf * 9)) != CV_OK) return st;
+    if ((st = d_sinit.ensure((size_t)nf * 8)) != CV_OK) return st;
+    if ((st = d_slast.ensure((size_t)nf * N * 8)) != CV_OK) return st;
+    HIP_TRY(hipMemcpyAsync(d_soff.p, so.data(), so.size() * 8, hipMemcpyHostToDevice, stream));
+    HIP_TRY(hipMemcpyAsync(d_sobs.p, sob.data(), sob.size() * 4, hipMemcpyHostToDevice, stream));
+    HIP_TRY(hipMemcpyAsync(d_sinit.p, G.data(), (size_t)nf * 8, hipMemcpyHostToDevice, stream));
+    cv_opts oc = default_opts();
+    oc.dtype = CV_DTYPE_F64;
+    oc.assoc = CV_ASSOC_CP;
+    oc.kernel = CV_KERNEL_TRELLIS_F64;
+    oc.rescore_f64 = 0;
+    oc.stream = stream;
+    double* sc = d_sres.as<double>();
+    if ((st = decode_device(h, nf, so.data(), d_soff.as<int64_t>(), d_sobs.as<int32_t>(), oc, d_spath.as<int32_t>(), sc,
+                            reinterpret_cast<uint8_t*>(sc + nf), stream, nullptr, false, nullptr,
+                            d_sinit.as<double>(), d_slast.as<double>())) != CV_OK)
+      return st;
+    spec_path.resize((size_t)Ls);
+    spec_last.resize((size_t)nf * N);
+    HIP_TRY(hipMemcpyAsync(spec_path.data(), d_spath.p, (size_t)Ls * 4, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipMemcpyAsync(spec_last.data(), d_slast.p, (size_t)nf * N * 8, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipStreamSynchronize(stream));
+    spec_off = std::move(so);
+    spec_guess = std::move(G);
+    for (int64_t i = 0; i < nf; ++i) spec_idx[(size_t)F[i]] = i;
+    ++spec_batches;
+    batch_acc = 0;
+    batch_size = nf;
+    return CV_OK;
+  };
+
+  for (size_t x = 0; x < ks.size();) {
+    const int64_t k = ks[x];
+    const int64_t e0 = off[(size_t)k], T = off[(size_t)k + 1] - e0;
+    double Mn;
+    bool qd;
+    if (certify(x, M, prev, &Mn, &qd)) {
+      if (in_run && (st = end_run(row_arg)) != CV_OK) return st;  // clean: the run ends in its argmax
+      M = Mn;
+      prev = CERT;
+      prev_end = P[e0 + T - 1];
+      ++ncert;
+      nquant += qd ? 1 : 0;
+      ++x;
+      continue;
+    }
+    const double S = score_of(x);
+    const bool start_clean = prev != ROW || row_clean(row_host.data(), row_arg, M, S + pimax + 16.0);
+    const int64_t si = spec_idx[(size_t)k];
+    if (si >= 0 && start_clean && spec_guess[(size_t)si] == M && std::signbit(spec_guess[(size_t)si]) == std::signbit(M)) {
+      // the speculative decode started from the chain's exact state: it IS the chain there
+      const double* lr = spec_last.data() + (size_t)si * N;
+      int32_t arg = 0;
+      for (int32_t i = 1; i < N; ++i)
+        if (lr[i] > lr[arg]) arg = i;
+      const double m1 = lr[arg];
+      if (m1 > -INFINITY && (x + 1 >= ks.size() || row_clean(lr, arg, m1, score_of(x + 1) + pimax + 16.0))) {
+        if (in_run && (st = end_run(row_arg)) != CV_OK) return st;
+        std::memcpy(path_out + e0, spec_path.data() + spec_off[(size_t)si], (size_t)T * 4);
+        std::copy(lr, lr + N, row_host.begin());
+        std::fill(row_host.begin() + N, row_host.end(), -INFINITY);
+        row_dev = nullptr;
+        row_arg = arg;
+        M = m1;
+        prev = ROW;
+        ++spec_acc;
+        ++batch_acc;
+        ++x;
+        continue;
+      }
+      // its end state could differ from its argmax (an unclean boundary): the serial chain
+    } else if (spec_on && start_clean && spec_from != x) {
+      // no valid speculation for this sequence (none yet, or an earlier path changed): a new
+      // batch from the exact state here, unless the last one resolved too little
+      if (spec_batches > 0 && batch_acc < 4 && batch_acc * 4 < batch_size) spec_on = false;
+      if (spec_on) {
+        spec_from = x;
+        if ((st = speculate(x)) != CV_OK) return st;
+        continue;  // retry x with the new batch
       }
     }
     if ((st = run_step(k)) != CV_OK) return st;
+    ++x;
   }
-  if (in_run && (st = end_run(run_arg)) != CV_OK) return st;  // cp.rs:86: first argmax of the last row
+  if (in_run && (st = end_run(row_arg)) != CV_OK) return st;  // cp.rs:86: first argmax of the last row
   trace_mark("chain: walk + runs");
   h->last_chain[0] = 1;
   h->last_chain[1] = ncert;
   h->last_chain[2] = run_seqs;
   h->last_chain[3] = runs;
   h->last_chain[4] = nquant;
+  h->last_chain[5] = spec_acc;
+  h->last_chain[6] = spec_batches;
   *objective_out = M;
   *applied = true;
   if (!(M > -INFINITY))
@@ -3081,7 +3234,7 @@ CV_API cv_status cv_decode_superseq_cp(cv_hmm* h, int64_t nseq, const int64_t* o
   const char* old_env = getenv("CV_CHAIN_OLD");
   const char* par_env = getenv("CV_CHAIN_PAR");  // read per call: tests flip it within one process
   h->last_chain[0] = 0;
-  for (int q = 1; q < 5; ++q) h->last_chain[q] = 0;
+  for (int q = 1; q < 7; ++q) h->last_chain[q] = 0;
   if (cvk::t64_padded_states(h->N) && !(old_env && *old_env == '1') && !(par_env && *par_env == '0')) {
     bool applied = false;
     st = superseq_cp_par(h, nseq, offsets, obs, path_out, objective_out, &applied);

@@ -26,6 +26,11 @@ struct T64FwdArgs {
   int nstates;             // real N (psi row stride)
   uint16_t* psi;           // [(elements of chunk)][N]
   double* last_row;        // [(slots of launch)][N] (CP); EXT: [(slots of launch)][NP] final rows
+  // CP only (the parallel chain): cp_init [nseq] = offset M of each sequence (row 0 =
+  // fl(M + fl(pi + b)), a chain entered with running maximum M), null = 0; cp_last
+  // [nseq][N] = each sequence's last row, indexed by sequence id (null = not written)
+  const double* cp_init;
+  double* cp_last;
   // EXT features of trellis_fwd_f64 (the constrained decode's passes; all null/0 otherwise)
   const int32_t* forced;       // [sum T] -1 free, >= 0 forced state, <= -2: row 0 = resume_rows[-2 - f]
   const int64_t* ranges;       // [slot][2] explicit element ranges (begin, end); sequence id = slot

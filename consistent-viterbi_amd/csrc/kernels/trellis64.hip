@@ -929,7 +929,10 @@ __global__ __launch_bounds__(64) void trellis_cp_f64(T64FwdArgs g) {
     for (int c = 0; c < C; ++c) {
       if (j0 + c < N) {
         if (t > 0) g.psi[(e0[s] + t - g.delta_elem_base) * (int64_t)N + j0 + c] = (uint16_t)p[c];
-        if (t == T[s] - 1) g.last_row[(slot0 + s - g.seq_begin) * (int64_t)N + j0 + c] = v[c];
+        if (t == T[s] - 1) {
+          g.last_row[(slot0 + s - g.seq_begin) * (int64_t)N + j0 + c] = v[c];
+          if (g.cp_last) g.cp_last[seq[s] * (int64_t)N + j0 + c] = v[c];
+        }
       }
     }
   };
@@ -941,7 +944,9 @@ __global__ __launch_bounds__(64) void trellis_cp_f64(T64FwdArgs g) {
     emis(s, 0, e);
 #pragma unroll
     for (int c = 0; c < C; ++c) {
-      v[c] = g.pi[j0 + c] + e[c];
+      // cp_init (the parallel chain's speculative re-runs): the chain's start value
+      // fl(M + fl(pi + b)) of a sequence entered with running maximum M (utils.rs:32-38)
+      v[c] = g.cp_init ? g.cp_init[seq[s] >= 0 ? seq[s] : 0] + (g.pi[j0 + c] + e[c]) : g.pi[j0 + c] + e[c];
       dl[(j0 + c) * S + s] = v[c];
     }
     emit(s, 0, v, p);

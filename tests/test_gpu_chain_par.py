@@ -30,19 +30,21 @@ def _serial(h, off, obs):
             os.environ["CV_CHAIN_PAR"] = old
 
 
-def _par(h, off, obs, force=None):
-    old = os.environ.get("CV_CHAIN_PAR_FORCE")
-    if force is not None:
-        os.environ["CV_CHAIN_PAR_FORCE"] = str(force)
+def _par(h, off, obs, force=None, spec=True):
+    env = {"CV_CHAIN_PAR_FORCE": None if force is None else str(force), "CV_CHAIN_SPEC": None if spec else "0"}
+    old = {k: os.environ.get(k) for k in env}
+    for k, v in env.items():
+        if v is not None:
+            os.environ[k] = v
     try:
         out = cv.decode_superseq_cp(h, off, obs)
         return out, cv.last_superseq_stats(h)
     finally:
-        if force is not None:
-            if old is None:
-                del os.environ["CV_CHAIN_PAR_FORCE"]
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
             else:
-                os.environ["CV_CHAIN_PAR_FORCE"] = old
+                os.environ[k] = v
 
 
 def _case(n, v, nseq, tlo, thi, seed, scale=1.0, zeros=(), ones=()):
@@ -73,15 +75,22 @@ def test_chain_par_equals_oracle(gpu, n):
     assert bad.size == 0, f"elements {bad[:10]} of {len(rp)}; {st}"
 
 
+@pytest.mark.parametrize("spec", [True, False])
 @pytest.mark.parametrize("n,force", [(64, 1), (64, 2), (64, 3), (256, 2), (256, 5), (7, 4)])
-def test_chain_par_forced_runs(gpu, n, force):
-    """CV_CHAIN_PAR_FORCE=m takes every m-th sequence as uncertified, so the serial chain kernel
-    re-runs it from a synthetic start row (after a certified sequence) or from the previous run's
-    last row (consecutive runs, m = 1: the whole chain in one run): still the oracle's chain."""
+def test_chain_par_forced_runs(gpu, n, force, spec):
+    """CV_CHAIN_PAR_FORCE=m takes every m-th sequence as uncertified.  With speculation they are
+    re-decoded in parallel from their predicted offsets and taken where the offset was exact;
+    without it (CV_CHAIN_SPEC=0) the serial chain kernel re-runs each from a synthetic start row
+    (after a certified sequence) or from the previous sequence's last row (consecutive runs,
+    m = 1: the whole chain in one run).  Either way: the oracle's chain."""
     pi, a, b, off, obs = _case(n, 19, 40, 1, 70, seed=4100 + n + force, zeros=(2,), ones=(7,))
     h = cv.HMM(pi, a, b)
-    (path, obj), st = _par(h, off, obs, force=force)
-    assert st["parallel"] and st["rerun"] >= 1, st
+    (path, obj), st = _par(h, off, obs, force=force, spec=spec)
+    assert st["parallel"] and st["rerun"] + st["speculated"] >= 1, st
+    if spec:
+        assert st["spec_batches"] >= 1 and st["speculated"] >= 1, st
+    else:
+        assert st["speculated"] == 0 and st["rerun"] >= 1, st
     rp, robj = O.cp_superseq_f64(pi, a, b, off, obs)
     assert obj == robj and np.array_equal(path, rp), st
 
@@ -99,10 +108,11 @@ def test_chain_par_rounding_case(gpu):
     obs = np.zeros(int(off[-1]), np.int32)
     obs[0] = 1
     h = cv.HMM(pi, a, b)
-    (path, obj), st = _par(h, off, obs)
-    rp, robj = O.cp_superseq_f64(pi, a, b, off, obs)
-    assert np.array_equal(path, rp) and obj == robj, st
-    assert st["parallel"] and st["rerun"] >= 1, st
+    for spec in (True, False):
+        (path, obj), st = _par(h, off, obs, spec=spec)
+        rp, robj = O.cp_superseq_f64(pi, a, b, off, obs)
+        assert np.array_equal(path, rp) and obj == robj, st
+        assert st["parallel"] and st["rerun"] + st["speculated"] >= 1, st
 
 
 @pytest.mark.parametrize("scale", [1.0, 1e3, 1e6])
@@ -116,6 +126,8 @@ def test_chain_par_large_totals(gpu, scale):
     sp, sobj = _serial(h, off, obs)
     assert st["parallel"], st
     assert obj == sobj, (obj, sobj, st)
+    (p2, o2), st2 = _par(h, off, obs, spec=False)
+    assert o2 == sobj and np.array_equal(p2, sp), st2
     bad = np.nonzero(path != sp)[0]
     assert bad.size == 0, f"elements {bad[:10]} of {len(sp)}; {st}"
     if scale == 1.0:
@@ -149,9 +161,10 @@ def test_chain_par_quantised_ties(gpu):
     off = synth.offsets_from_lengths(rng.integers(0, 50, size=30))
     obs = rng.integers(0, v, size=int(off[-1])).astype(np.int32)
     h = cv.HMM(pi, a, b)
-    (path, obj), st = _par(h, off, obs)
-    rp, robj = O.cp_superseq_f64(pi, a, b, off, obs)
-    assert obj == robj and np.array_equal(path, rp), st
+    for spec in (True, False):
+        (path, obj), st = _par(h, off, obs, spec=spec)
+        rp, robj = O.cp_superseq_f64(pi, a, b, off, obs)
+        assert obj == robj and np.array_equal(path, rp), st
 
 
 def test_chain_par_not_applicable(gpu):
