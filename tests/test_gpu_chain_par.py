@@ -143,7 +143,7 @@ def test_chain_par_1m_elements_vs_serial(gpu):
     (path, obj), st = _par(h, c["offsets"], c["obs"])
     assert int(c["offsets"][-1]) >= 1 << 20
     sp, sobj = _serial(h, c["offsets"], c["obs"])
-    assert st["parallel"] and st["certified"] + st["rerun"] == 2048, st
+    assert st["parallel"] and st["certified"] + st["rerun"] + st["speculated"] == 2048, st
     assert st["certified"] >= 2000 and st["quantised"] >= 1900, st
     assert obj == sobj
     bad = np.nonzero(path != sp)[0]
