@@ -53,6 +53,13 @@ def main():
               f"({t/L*1e9:.1f} ns/element), objective {o!r}, stats {s}", flush=True)
     # the full chain's prefix slice must agree with the comparison run's serial chain
     assert np.array_equal(p[:int(oc[-1])][:-512], p0[:-512]), "prefix of the full chain differs"
+    if os.environ.get("FULL_SERIAL") == "1":  # the whole input through the serial chain (~2 min)
+        ps, os_, ts, _ = run(h, off, obs, serial=True)
+        same = bool(np.array_equal(ps, p) and os_ == o)
+        print(f"serial chain over all {int(off[-1])} elements: {ts:.1f} s, objective {os_!r}, "
+              f"parallel == serial: {same}", flush=True)
+        if not same:
+            raise SystemExit("parallel chain differs from the serial chain at full size")
 
 
 if __name__ == "__main__":
