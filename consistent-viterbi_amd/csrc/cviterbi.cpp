@@ -910,6 +910,10 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
           tmax = std::max(tmax, T);
         }
         fa.wg_ok = (8 * tmin >= 7 * tmax || n >= 2 * 64 * (int64_t)std::max(h->cus, 1)) ? 1 : 0;
+        if (side_ws) {  // A/B knob CV_SIDE_WG=0: the config-5 side decode in one-wave workgroups
+          const char* e = getenv("CV_SIDE_WG");
+          if (e && *e == '0') fa.wg_ok = 0;
+        }
       }
       if (t64cp) {
         fa.nstates = h->N;
