@@ -51,6 +51,7 @@ WORKSPACE = 48 << 30         # delta workspace cap: one forward launch per step 
 WORKSPACE_F64 = 80 << 30     # f64: one launch per step too (68.7 GB of f64 delta rows)
 PMC_F64 = "profiles/pmc_trellis_fwd_f64_c4.json"   # committed rocprofv3 PMC summary (traffic, clock)
 PMC_F32 = "profiles/pmc_trellis_fwd_c4.json"
+PMC_F64_RS = "profiles/pmc_trellis_fwd_f64_rs_8192.json"  # the 8,192-sequence shard's kernel (N = 8, strong)
 
 
 def parse():
@@ -139,19 +140,21 @@ def _cpu_model():
     return None
 
 
-def load_pmc(f64):
-    """The committed rocprofv3 PMC summary of the forward kernel at config 4 (f64: one
-    65,536-sequence launch; f32: one 8,192-sequence launch): HBM bytes per decoded ELEMENT
-    (the traffic is the delta rows written, proportional to the elements a launch decodes)
-    and the effective clock (GRBM_GUI_ACTIVE over the kernel, when recorded)."""
-    rel = PMC_F64 if f64 else PMC_F32
+def load_pmc(f64, row_split=False):
+    """The committed rocprofv3 PMC summary of the forward kernel that ran (f64: one
+    65,536-sequence launch of trellis_fwd_f64, or with row_split one 8,192-sequence launch of
+    trellis_fwd_f64_rs, the strong-scaling shard's kernel; f32: one 8,192-sequence launch):
+    HBM bytes per decoded ELEMENT (the traffic is the delta rows written, proportional to the
+    elements a launch decodes) and the effective clock (GRBM_GUI_ACTIVE over the kernel)."""
+    rel = (PMC_F64_RS if row_split else PMC_F64) if f64 else PMC_F32
     p = os.path.join(ROOT, rel)
     if not os.path.exists(p):
         return None
     try:
         with open(p) as f:
             d = json.load(f)
-        return {"per_elem": float(d["hbm_bytes_per_launch"]) / ((B_TOTAL if f64 else 8192) * T_LEN),
+        seqs = d.get("sequences_per_launch", B_TOTAL if f64 else 8192)
+        return {"per_elem": float(d["hbm_bytes_per_launch"]) / (seqs * T_LEN),
                 "clock_ghz": d.get("clock_ghz"), "source": rel + (" (" + d["source"] + ")" if "source" in d else "")}
     except Exception:
         return None
@@ -485,10 +488,13 @@ def main():
     alg_f64 = ((16 * N_STATES + 8) * steps_rank + 8 * nloc) / lps
     achieved = alg_8d / fwd_launch_s
     pairs_per_launch = N_STATES * N_STATES * (T_LEN - 1) * nloc / lps
-    pmc = load_pmc(f64)
+    # spw 4 = the pair-of-waves small-batch layout with S = 8, run as the row split
+    # (trellis_fwd_f64_rs, four pairs per workgroup) on equal-length batches like this one
+    row_split = f64 and spw == 4
+    pmc = load_pmc(f64, row_split)
     traffic = pmc["per_elem"] * steps_rank / lps if pmc else None
-    kname = ("trellis_fwd_f64<C=4,S=8>" if spw == 8 else "trellis_fwd_f64<C=2,S=%d,W=2>" % (2 * spw)) \
-        if f64 else "trellis_fwd2_f32<256>"
+    kname = ("trellis_fwd_f64<C=4,S=8>" if spw == 8 else "trellis_fwd_f64_rs<8> (row-split pairs, S=8)" if row_split
+             else "trellis_fwd_f64<C=2,S=%d,W=2>" % (2 * spw)) if f64 else "trellis_fwd2_f32<256>"
     pair_peak = F64_PAIR_PEAK if f64 else VALU_PAIR_PEAK
     valu_frac = pairs_per_launch / fwd_launch_s / pair_peak
     valu = {"achieved_pairs_per_s": pairs_per_launch / fwd_launch_s, "peak_pairs_per_s": pair_peak,
