@@ -3753,8 +3753,17 @@ CV_API cv_status cv_hmm_fit_train(int32_t nstates, int64_t nobs, int64_t nseq, c
   if ((st = upload(d.off, off0.data(), off0.size() * 8)) != CV_OK) return st;
   if ((st = upload(d.obs, obs + lo, (size_t)total * 4)) != CV_OK) return st;
   if ((st = upload(d.tags, tags + lo, (size_t)total * 4)) != CV_OK) return st;
-  // alpha / beta rows for a chunk of sequences at a time (<= 2 GiB each)
-  const int64_t cap_elems = std::max<int64_t>((2ll << 30) / (8 * N), 1);
+  // alpha / beta rows for a chunk of sequences at a time: at least 2 GiB each, and up to half
+  // of the free device memory for both (N > 64: a launch of 64-sequence workgroups fills the
+  // chip only with >= 16,384 sequences; config 4's corpus is one 137 GB chunk)
+  size_t free_b = 0, total_b = 0;
+  if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) {
+    (void)hipGetLastError();
+    free_b = 0;
+  }
+  const int64_t cap_elems = std::max<int64_t>(
+      std::max<int64_t>((2ll << 30) / (8 * N), 1),
+      N > cvf::kBwWaveStates ? (int64_t)(free_b / 2 / (16 * (size_t)N)) : 0);
   int64_t max_chunk = 0;
   std::vector<std::pair<int64_t, int64_t>> chunks;
   for (int64_t s0 = 0; s0 < nseq;) {

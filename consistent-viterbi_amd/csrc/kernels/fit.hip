@@ -12,12 +12,15 @@
 // one-wave-per-sequence kernels below (bw_fwd_wave, bw_bwd_stats_wave) replace all three.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include <algorithm>
 
 #include "fit.h"
 
 namespace cvf {
+
+typedef double f64x4_t __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ double block_sum(double v, double* red) {
   // 256 threads = 4 waves: wave shuffle-reduce, then across the 4 waves through LDS
@@ -274,46 +277,88 @@ __global__ __launch_bounds__(256) void bw_stats_rows(BwArgs g) {
 }
 
 // xi_s[m][n] += sum_r R[r][m] U[r][n] over rows [0, nrows) (R = alpha rows, U = beta rows of
-// bw_stats_rows).  One wave per 32 x 32 output tile and row range: per 4 rows, lane l feeds
-// R[r + l/16][m0 + 16 mt + l%16] and U[...][n0 + 16 nt + l%16] into four
-// v_mfma_f64_16x16x4_f64 (2 x 2 tiles); one atomic flush of the tile at the end.
-__global__ __launch_bounds__(64) void bw_xi_gemm(BwArgs g, int64_t nrows, int64_t rows_per_wave) {
+// bw_stats_rows / bw_bwd_mm).  One wave per (16 TM)^2 output tile and row range: per 4 rows,
+// lane l feeds R[r + l/16][m0 + 16 mt + l%16] and U[...][n0 + 16 nt + l%16] into TM^2
+// v_mfma_f64_16x16x4_f64 (TM = 4: 16 MFMAs per 8 loads, each row of R and U read by N/64
+// waves); one atomic flush of the tile at the end.
+template <int TM, int ST>
+__global__ __launch_bounds__(64, 2) void bw_xi_gemm(BwArgs g, int64_t nrows, int64_t rows_per_wave) {
+  constexpr int TS = 16 * TM;
   const int N = g.nstates;
-  const int nt32 = (N + 31) / 32;
-  const int tile = blockIdx.x % (nt32 * nt32);
-  const int64_t part = blockIdx.x / (nt32 * nt32);
-  const int m0 = 32 * (tile / nt32), n0 = 32 * (tile % nt32);
+  const int ntt = (N + TS - 1) / TS;
+  // XCD-aware: workgroup b runs on XCD b % 8 (round-robin dispatch), so the ntt^2 tiles of one
+  // row range are the blocks b = 8 (part / 8 * ntt^2 + tile) + part % 8 -- one XCD, dispatched
+  // together: the range's rows come from HBM once into that XCD's L2 and serve every tile
+#ifndef CVF_GEMM_NOXCD
+  const int64_t b = blockIdx.x, j = b / 8;
+  const int tile = (int)(j % (ntt * ntt));
+  const int64_t part = (j / (ntt * ntt)) * 8 + b % 8;
+#else
+  const int tile = blockIdx.x % (ntt * ntt);
+  const int64_t part = blockIdx.x / (ntt * ntt);
+#endif
+  const int m0 = TS * (tile / ntt), n0 = TS * (tile % ntt);
   const int l = threadIdx.x, kk = l >> 4, cl = l & 15;
   const int64_t r0 = part * rows_per_wave, r1 = r0 + rows_per_wave < nrows ? r0 + rows_per_wave : nrows;
-  typedef double double4_t __attribute__((ext_vector_type(4)));
-  double4_t acc[2][2];
+  if (r0 >= nrows) return;  // padding blocks of the XCD mapping (wave-uniform)
+  f64x4_t acc[TM][TM];
 #pragma unroll
-  for (int a = 0; a < 2; ++a)
+  for (int a = 0; a < TM; ++a)
 #pragma unroll
-    for (int b = 0; b < 2; ++b) acc[a][b] = double4_t{0.0, 0.0, 0.0, 0.0};
-  const int cm[2] = {m0 + cl, m0 + 16 + cl}, cn[2] = {n0 + cl, n0 + 16 + cl};
-  const bool vm[2] = {cm[0] < N, cm[1] < N}, vn[2] = {cn[0] < N, cn[1] < N};
-  for (int64_t r = r0; r < r1; r += 4) {
-    const int64_t row = r + kk;
-    const bool vr = row < r1;
-    const double* R = g.alpha + (size_t)(vr ? row : r0) * N;
-    const double* U = g.beta + (size_t)(vr ? row : r0) * N;
-    double av[2], bv[2];
+    for (int b = 0; b < TM; ++b) acc[a][b] = f64x4_t{0.0, 0.0, 0.0, 0.0};
+  int cm[TM], cn[TM];
+  bool vm[TM], vn[TM];
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      av[q] = (vr && vm[q]) ? R[cm[q]] : 0.0;
-      bv[q] = (vr && vn[q]) ? U[cn[q]] : 0.0;
-    }
-#pragma unroll
-    for (int a = 0; a < 2; ++a)
-#pragma unroll
-      for (int b = 0; b < 2; ++b) acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[a], bv[b], acc[a][b], 0, 0, 0);
+  for (int q = 0; q < TM; ++q) {
+    cm[q] = m0 + 16 * q + cl;
+    cn[q] = n0 + 16 * q + cl;
+    vm[q] = cm[q] < N;
+    vn[q] = cn[q] < N;
+    cm[q] = min(cm[q], N - 1);
+    cn[q] = min(cn[q], N - 1);
   }
+  // per 4 rows: TM loads of R and of U (lane l: row r + l/16, column l%16 of each 16-wide
+  // tile), masked loads (a select on a loaded value cost ~30% here); ST = 2 issues the next 4
+  // rows' loads before the current rows' MFMAs
+  auto mma = [&](const double (&av)[TM], const double (&bv)[TM]) {
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+      for (int b = 0; b < TM; ++b) acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[a], bv[b], acc[a][b], 0, 0, 0);
+  };
+#define CVF_GEMM_LOAD(RR, AV, BV)                                            \
+  {                                                                          \
+    const int64_t row_ = (RR) + kk;                                          \
+    const bool vr_ = row_ < r1;                                              \
+    const double* R_ = g.alpha + (size_t)(vr_ ? row_ : r0) * N;              \
+    const double* U_ = g.beta + (size_t)(vr_ ? row_ : r0) * N;               \
+    _Pragma("unroll") for (int q = 0; q < TM; ++q) {                         \
+      AV[q] = (vr_ && vm[q]) ? R_[cm[q]] : 0.0;                              \
+      BV[q] = (vr_ && vn[q]) ? U_[cn[q]] : 0.0;                              \
+    }                                                                        \
+  }
+  if constexpr (ST == 2) {
+    double a0[TM], b0[TM], a1[TM], b1[TM];
+    CVF_GEMM_LOAD(r0, a0, b0)
+    for (int64_t r = r0; r < r1; r += 8) {
+      CVF_GEMM_LOAD(r + 4, a1, b1)
+      mma(a0, b0);
+      CVF_GEMM_LOAD(r + 8, a0, b0)
+      mma(a1, b1);
+    }
+  } else {
+    for (int64_t r = r0; r < r1; r += 4) {
+      double av[TM], bv[TM];
+      CVF_GEMM_LOAD(r, av, bv)
+      mma(av, bv);
+    }
+  }
+#undef CVF_GEMM_LOAD
   // C/D layout of v_mfma_f64_16x16x4_f64: col = lane & 15, row = (lane >> 4) + 4 * reg
 #pragma unroll
-  for (int a = 0; a < 2; ++a)
+  for (int a = 0; a < TM; ++a)
 #pragma unroll
-    for (int b = 0; b < 2; ++b)
+    for (int b = 0; b < TM; ++b)
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int row = m0 + 16 * a + (l >> 4) + 4 * q, col = n0 + 16 * b + (l & 15);
@@ -723,6 +768,400 @@ __global__ __launch_bounds__(256) void bw_bwd_stats_wave(BwArgs g, int64_t nseq,
   if (i == 0 && z != 0.0) unsafeAtomicAdd(g.xi_zero, z);
 }
 
+// ---- 64 < N <= 256: 64 sequences per workgroup, each step's products on the matrix cores ----
+// The workgroup kernels above give every sequence its own workgroup, so every sequence step
+// streams all of A (512 KiB at N = 256) through L1/L2 for N^2 FMAs: ~5 TFLOP/s.  Here a
+// workgroup advances 64 sequences (consecutive in the longest-first order) in lock step and
+// one step is the product X (64 x NP) . A (NP x NP) on v_mfma_f64_16x16x4_f64: each A value
+// read serves 64 sequences.  Wave w owns the output columns [64 w, 64 w + 64) (CT = NP / 64
+// tiles of 16) for all 64 sequences (4 tiles of 16): 16 CT independent accumulators, lane l
+// holding Y[g = 16 m + (l >> 4) + 4 r][i = 16 (w CT + n) + (l & 15)] (f64 C/D layout).  The
+// next step's operand X goes through LDS transposed, X^T[k][g] (xt_at: swizzled against bank
+// conflicts on both the writes and the operand reads).  Row sums (normalisation, c_t, gamma) reduce in registers over the wave's tiles,
+// by DPP over the 16 lanes of a row, then over the 4 waves through LDS -- one order, so runs
+// repeat bit for bit.  A's indices are clamped into [0, N): rows k >= N meet X entries that
+// are 0, columns >= N are dropped.
+
+__device__ __forceinline__ double row16_sum(double v) {  // sum over the 16 lanes of a DPP row
+  v += dpp_f64<0xB1>(v);
+  v += dpp_f64<0x4E>(v);
+  v += dpp_f64<0x141>(v);
+  v += dpp_f64<0x140>(v);
+  return v;
+}
+__device__ __forceinline__ double row16_max(double v) {
+  v = fmax(v, dpp_f64<0xB1>(v));
+  v = fmax(v, dpp_f64<0x4E>(v));
+  v = fmax(v, dpp_f64<0x141>(v));
+  v = fmax(v, dpp_f64<0x140>(v));
+  return v;
+}
+// normalize by a reciprocal taken once per sequence step: v / s to within an ulp (the sums run
+// in another order than the reference's anyway).  Both scaled by 2^64, so a subnormal s (tiny
+// emissions) still has a finite reciprocal; every v here is one of s's non-negative terms.
+__device__ __forceinline__ double recip64(double s) { return 1.0 / (s * 0x1p64); }
+__device__ __forceinline__ double normalized_r(double v, double s, double inv, int n) {
+  return s != 0.0 ? (v * 0x1p64) * inv : 1.0 / n;
+}
+
+// X^T[k][g] swizzled: g ^ (k & 15) spreads the 16 consecutive k of one ds_write_b64 (16 lanes,
+// one g) over 16 bank pairs; ^ 16 on odd k puts the two 16-lane halves of an operand read (k,
+// k + 1; 16 consecutive g) on opposite bank halves.  Needs G >= 32.
+template <int G>
+__device__ __forceinline__ int xt_at(int k, int g) { return k * G + (g ^ (k & 15) ^ ((k & 1) << 4)); }
+
+// Y = X . M over the LDS operand X^T (xt) and the row-major N x N matrix M (A or A^T)
+template <int NP, int MT>
+__device__ __forceinline__ void mm_step(const double* __restrict__ xt, const double* __restrict__ M, int N, int w,
+                                        int l, f64x4_t (&acc)[MT][NP / 64]) {
+  constexpr int CT = NP / 64, NK = NP / 4, PF = 4, G = 16 * MT;
+  const int cl = l & 15, kq = l >> 4;
+  int col[CT];
+#pragma unroll
+  for (int n = 0; n < CT; ++n) col[n] = min(16 * (w * CT + n) + cl, N - 1);
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int n = 0; n < CT; ++n) acc[m][n] = f64x4_t{0.0, 0.0, 0.0, 0.0};
+  double ring[PF][CT];
+  auto load = [&](int kk, double (&dst)[CT]) {
+    const int k = min(4 * kk + kq, N - 1);
+#pragma unroll
+    for (int n = 0; n < CT; ++n) dst[n] = M[(size_t)k * N + col[n]];
+  };
+#pragma unroll
+  for (int p = 0; p < PF; ++p) load(p, ring[p]);
+#pragma unroll 1
+  for (int kk0 = 0; kk0 < NK; kk0 += PF) {
+#pragma unroll
+    for (int p = 0; p < PF; ++p) {
+      const int kk = kk0 + p, k = 4 * kk + kq;
+      double bv[CT];
+#pragma unroll
+      for (int n = 0; n < CT; ++n) bv[n] = ring[p][n];
+      load(min(kk + PF, NK - 1), ring[p]);
+      double av[MT];
+#pragma unroll
+      for (int m = 0; m < MT; ++m) av[m] = xt[xt_at<G>(k, 16 * m + cl)];
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int n = 0; n < CT; ++n) acc[m][n] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[m], bv[n], acc[m][n], 0, 0, 0);
+    }
+  }
+}
+
+// the group's sequences: element offset, length, and the longest length
+template <int G>
+__device__ __forceinline__ void mm_setup(const BwArgs& g, int64_t nseq, int64_t* s_e0, int* s_T, int* s_tmax) {
+  const int tid = threadIdx.x;
+  if (tid < G) {
+    const int64_t k = (int64_t)blockIdx.x * G + tid;
+    int64_t e0 = 0;
+    int T = 0;
+    if (k < nseq) {
+      const int64_t s = g.order ? g.order[k] : k;
+      e0 = g.offsets[s];
+      T = (int)(g.offsets[s + 1] - e0);
+    }
+    s_e0[tid] = e0 - g.elem_base;
+    s_T[tid] = T;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    int tm = 0;
+    for (int k = 0; k < G; ++k) tm = max(tm, s_T[k]);
+    *s_tmax = tm;
+  }
+  __syncthreads();
+}
+
+// forward (hmm.rs:78-100) of 64 sequences: alpha rows to g.alpha
+template <int NP, int MT>
+__global__ __launch_bounds__(256, MT == 4 ? 1 : 2) void bw_fwd_mm(BwArgs g, int64_t nseq) {
+  constexpr int CT = NP / 64, G = 16 * MT;
+  __shared__ __attribute__((aligned(16))) double xt[NP * G];
+  __shared__ double red[4][G];
+  __shared__ int64_t s_e0[G];
+  __shared__ int s_T[G], s_ob[2][G], s_tg[2][G];
+  __shared__ int s_tmax;
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, cl = l & 15;
+  const int N = g.nstates;
+  mm_setup<G>(g, nseq, s_e0, s_T, &s_tmax);
+  const int tmax = s_tmax;
+  if (tmax <= 0) return;  // workgroup-uniform
+  auto fetch = [&](int t) {  // observation and tag of step t into slot t & 1
+    if (tid < G) {
+      const bool v = t < s_T[tid];
+      const int64_t e = (int64_t)s_e0[tid] + g.elem_base + (v ? t : 0);
+      s_ob[t & 1][tid] = v ? g.obs[e] : 0;
+      s_tg[t & 1][tid] = v ? g.tags[e] : -1;
+    }
+  };
+  fetch(0);
+  fetch(1);
+  __syncthreads();
+  int col[CT];
+#pragma unroll
+  for (int n = 0; n < CT; ++n) col[n] = 16 * (w * CT + n) + cl;
+  f64x4_t acc[MT][CT];
+  // t = 0 (hmm.rs:81-88): y = pi * b(o_0)
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int gi = 16 * m + (l >> 4) + 4 * r;
+      const int o = s_ob[0][gi];
+#pragma unroll
+      for (int n = 0; n < CT; ++n) {
+        const int c = min(col[n], N - 1);
+        acc[m][n][r] = g.pi[c] * g.et[(size_t)o * N + c];
+      }
+    }
+  for (int t = 0;; ++t) {
+    if (t > 0) {
+      fetch(t + 1);  // slot (t + 1) & 1 was last read in phase t - 1, before its closing barrier
+      mm_step<NP, MT>(xt, g.a, N, w, l, acc);  // (alpha_{t-1} o b(o_t)) . A  (hmm.rs:93-94)
+    }
+    // row sums of y over the N states
+    double s[MT][4];
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        double v = 0.0;
+#pragma unroll
+        for (int n = 0; n < CT; ++n) v += col[n] < N ? acc[m][n][r] : 0.0;
+        s[m][r] = row16_sum(v);
+        if (cl == 0) red[w][16 * m + (l >> 4) + 4 * r] = s[m][r];
+      }
+    __syncthreads();
+    const bool more = t + 1 < tmax;
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int gi = 16 * m + (l >> 4) + 4 * r;
+        const double sum = (red[0][gi] + red[1][gi]) + (red[2][gi] + red[3][gi]);
+        const double inv = recip64(sum);
+        const int tg = s_tg[t & 1][gi];
+        const bool on = t < s_T[gi];
+        const int o1 = s_ob[(t + 1) & 1][gi];
+        const bool on1 = t + 1 < s_T[gi];
+        double* arow = g.alpha + (size_t)(s_e0[gi] + t) * N;
+#pragma unroll
+        for (int n = 0; n < CT; ++n) {
+          const int c = col[n];
+          const double a = tg >= 0 ? (c == tg ? 1.0 : 0.0) : normalized_r(acc[m][n][r], sum, inv, N);
+          if (on && c < N) arow[c] = a;
+          if (more) xt[xt_at<G>(c, gi)] = (on1 && c < N) ? a * g.et[(size_t)o1 * N + min(c, N - 1)] : 0.0;
+        }
+      }
+    __syncthreads();  // xt complete; red and the step-t slot free
+    if (!more) break;
+  }
+}
+
+// backward (hmm.rs:102-121) fused with gamma / xi of hmm.rs:124-143 for 64 sequences, aligned
+// at their last elements: step r is t = T_g - 1 - r of sequence g.  W_t = A u_{t+1} (u_{t+1} =
+// b(o_{t+1}) o beta_{t+1}, in xt) gives c_t = alpha_t . W_t and beta_t = normalize(W_t); gamma_t =
+// normalize(alpha_t o beta_t) goes into the sums, and r_t = alpha_t / (c_t 2^k) and
+// u'_{t+1} = u_{t+1} 2^k overwrite alpha's and beta's row t for bw_xi_gemm (zeros at t = T - 1),
+// as bw_stats_rows writes them.
+template <int NP, int MT>
+__global__ __launch_bounds__(256, MT == 4 ? 1 : 2) void bw_bwd_mm(BwArgs g, int64_t nseq) {
+  constexpr int CT = NP / 64, G = 16 * MT;
+  __shared__ __attribute__((aligned(16))) double xt[NP * G];
+  __shared__ double red1[3][4][G], red2[4][G];  // the two reduction rounds
+  __shared__ int64_t s_e0[G];
+  __shared__ int s_T[G], s_ob[2][G], s_tg[2][G];
+  __shared__ int s_tmax;
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, cl = l & 15;
+  const int N = g.nstates;
+  mm_setup<G>(g, nseq, s_e0, s_T, &s_tmax);
+  const int tmax = s_tmax;
+  if (tmax <= 0) return;
+  auto fetch = [&](int r) {  // observation and tag of step r (t = T - 1 - r) into slot r & 1
+    if (tid < G) {
+      const int t = s_T[tid] - 1 - r;
+      const int64_t e = (int64_t)s_e0[tid] + g.elem_base + (t >= 0 ? t : 0);
+      s_ob[r & 1][tid] = t >= 0 ? g.obs[e] : 0;
+      s_tg[r & 1][tid] = t >= 0 ? g.tags[e] : -1;
+    }
+  };
+  fetch(0);
+  __syncthreads();
+  int col[CT];
+#pragma unroll
+  for (int n = 0; n < CT; ++n) col[n] = 16 * (w * CT + n) + cl;
+  f64x4_t acc[MT][CT];
+  double pi_acc[CT], a_den[CT], b_den[CT], z = 0.0;
+#pragma unroll
+  for (int n = 0; n < CT; ++n) pi_acc[n] = a_den[n] = b_den[n] = 0.0;
+  double* const dump = g.dump + (size_t)((blockIdx.x * 4 + w) & (kBwDumpWaves - 1)) * 64 + l;
+  for (int r = 0; r < tmax; ++r) {
+    if (r > 0) {
+      fetch(r);
+      mm_step<NP, MT>(xt, g.at, N, w, l, acc);  // W_t[i] = sum_j A[i][j] u_{t+1}[j]  (hmm.rs:113-116)
+    }
+    // alpha_t, and (r > 0) the first round: c_t = alpha_t . W_t, sum W_t, max u_{t+1}
+    double al[MT][CT][4];
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int gi = 16 * m + (l >> 4) + 4 * q;
+        const int t = s_T[gi] - 1 - r;
+        const double* arow = g.alpha + (size_t)(s_e0[gi] + max(t, 0)) * N;
+#pragma unroll
+        for (int n = 0; n < CT; ++n)
+#ifndef CVF_ABL_NOALPHA
+          al[m][n][q] = (t >= 0 && col[n] < N) ? arow[min(col[n], N - 1)] : 0.0;
+#else
+          al[m][n][q] = (t >= 0 && col[n] < N) ? 1e-3 * (double)(t + col[n]) : 0.0;
+#endif
+      }
+    // beta_t replaces W_t in the accumulators (registers: alpha_t and beta_t stay live)
+    if (r > 0) {
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int gi = 16 * m + (l >> 4) + 4 * q;
+          double c = 0.0, sw = 0.0, um = 0.0;
+#pragma unroll
+          for (int n = 0; n < CT; ++n) {
+            const double wv = col[n] < N ? acc[m][n][q] : 0.0;
+            c += al[m][n][q] * wv;
+            sw += wv;
+            um = fmax(um, xt[xt_at<G>(col[n], gi)]);  // u_{t+1} (0 beyond N)
+          }
+          c = row16_sum(c);
+          sw = row16_sum(sw);
+          um = row16_max(um);
+          if (cl == 0) {
+            red1[0][w][gi] = c;
+            red1[1][w][gi] = sw;
+            red1[2][w][gi] = um;
+          }
+        }
+      __syncthreads();
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int gi = 16 * m + (l >> 4) + 4 * q;
+          const double c = (red1[0][0][gi] + red1[0][1][gi]) + (red1[0][2][gi] + red1[0][3][gi]);
+          const double sw = (red1[1][0][gi] + red1[1][1][gi]) + (red1[1][2][gi] + red1[1][3][gi]);
+          const double isw = recip64(sw);
+          const int t = s_T[gi] - 1 - r;
+          const bool on = t >= 0;
+          const double umax = fmax(fmax(red1[2][0][gi], red1[2][1][gi]), fmax(red1[2][2][gi], red1[2][3][gi]));
+          const int ks = xi_scale(c, umax);  // balanced factors (xi_scale)
+          const double ics = recip64(__builtin_ldexp(c, ks));  // r = alpha / (c 2^k), by one reciprocal
+          const int tg = s_tg[r & 1][gi];
+          double* rrow = g.alpha + (size_t)(s_e0[gi] + max(t, 0)) * N;
+          double* urow = g.beta + (size_t)(s_e0[gi] + max(t, 0)) * N;
+#pragma unroll
+          for (int n = 0; n < CT; ++n) {
+            const int cc = col[n];
+            const double u = xt[xt_at<G>(cc, gi)];  // u_{t+1}, unscaled
+            if (on && cc < N) {
+              rrow[cc] = c != 0.0 ? (al[m][n][q] * 0x1p64) * ics : 0.0;
+              urow[cc] = __builtin_ldexp(u, ks);
+            }
+            const double wv = acc[m][n][q];
+            acc[m][n][q] = tg >= 0 ? (cc == tg ? 1.0 : 0.0) : (cc < N ? normalized_r(wv, sw, isw, N) : 0.0);
+          }
+          // xi_t uniform (hmm.rs:306-317), counted separately: once per sequence step (lanes
+          // 0, 16, 32, 48 of wave 0 between them see every g)
+          if (on && c == 0.0 && cl == 0 && w == 0) z += 1.0;
+        }
+    } else {
+      // t = T - 1 (hmm.rs:105-108): tagged -> one-hot, else ones; no xi term (zero rows)
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int gi = 16 * m + (l >> 4) + 4 * q;
+          const int t = s_T[gi] - 1;
+          const int tg = s_tg[0][gi];
+          double* rrow = g.alpha + (size_t)(s_e0[gi] + max(t, 0)) * N;
+          double* urow = g.beta + (size_t)(s_e0[gi] + max(t, 0)) * N;
+#pragma unroll
+          for (int n = 0; n < CT; ++n) {
+            const int cc = col[n];
+            if (t >= 0 && cc < N) rrow[cc] = urow[cc] = 0.0;
+            acc[m][n][q] = tg >= 0 ? (cc == tg ? 1.0 : 0.0) : (cc < N ? 1.0 : 0.0);
+          }
+        }
+    }
+    // second round: gamma_t's sum
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int gi = 16 * m + (l >> 4) + 4 * q;
+        double sab = 0.0;
+#pragma unroll
+        for (int n = 0; n < CT; ++n) sab += al[m][n][q] * acc[m][n][q];
+        sab = row16_sum(sab);
+        if (cl == 0) red2[w][gi] = sab;
+      }
+    __syncthreads();  // every wave is past its reads of xt (u_{t+1})
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int gi = 16 * m + (l >> 4) + 4 * q;
+        const double sab = (red2[0][gi] + red2[1][gi]) + (red2[2][gi] + red2[3][gi]);
+        const double isab = recip64(sab);
+        const int t = s_T[gi] - 1 - r;
+        const int o = s_ob[r & 1][gi];
+#pragma unroll
+        for (int n = 0; n < CT; ++n) {
+          const int cc = col[n];
+          const bool on = t >= 0 && cc < N;
+          const double gm = normalized_r(al[m][n][q] * acc[m][n][q], sab, isab, N);  // hmm.rs:127-129
+          if (on) {
+            b_den[n] += gm;
+            if (r > 0) a_den[n] += gm;
+            if (t == 0) pi_acc[n] += gm;
+          }
+#ifndef CVF_ABL_NOBNUM
+          unsafeAtomicAdd(on ? &g.b_num[(size_t)o * N + cc] : dump, on ? gm : 0.0);  // hmm.rs:155-163
+#else
+          b_den[n] += on ? gm * (double)o : 0.0;
+#endif
+          // u_t = b(o_t) o beta_t, the next step's operand
+          xt[xt_at<G>(cc, gi)] = (t >= 1 && cc < N) ? g.et[(size_t)o * N + min(cc, N - 1)] * acc[m][n][q] : 0.0;
+        }
+      }
+    __syncthreads();  // xt = u_t complete; red and the step-r slot free
+  }
+  // the gamma sums of this wave's states over the 4 lane rows; one atomic per state
+#pragma unroll
+  for (int n = 0; n < CT; ++n) {
+    double p = pi_acc[n], a = a_den[n], b = b_den[n];
+    p += __shfl_xor(p, 16);
+    a += __shfl_xor(a, 16);
+    b += __shfl_xor(b, 16);
+    p += __shfl_xor(p, 32);
+    a += __shfl_xor(a, 32);
+    b += __shfl_xor(b, 32);
+    if ((l >> 4) == 0 && col[n] < N) {
+      unsafeAtomicAdd(&g.pi_acc[col[n]], p);
+      unsafeAtomicAdd(&g.a_den[col[n]], a);
+      unsafeAtomicAdd(&g.b_den[col[n]], b);
+    }
+  }
+  if (w == 0) {
+    z += __shfl_xor(z, 16);
+    z += __shfl_xor(z, 32);
+    if (l == 0 && z != 0.0) unsafeAtomicAdd(g.xi_zero, z);
+  }
+}
+
 // ---- M-step on the device (hmm.rs:145-175) ---------------------------------------------------
 // Parameters stay resident between iterations: pi, a (and its transpose at), et = b^T.  The
 // convergence sum d = sum |new - old| is reduced per block into part[]; the host adds the
@@ -797,19 +1236,83 @@ static void launch_wave_estep(const BwArgs& g, int64_t nseq, int64_t nwaves, hip
                      nwaves);
 }
 
+// sequences per workgroup of the 64 < N <= 256 kernels: 16 MT; MT = 2 (default) runs two
+// workgroups per CU, so one's reductions and barriers overlap the other's matrix products;
+// CV_BW_MT=4: one workgroup of 64 per CU
+static int bw_mt() {
+  static const int v = [] {
+    const char* e = getenv("CV_BW_MT");
+    return (e && e[0] == '4') ? 4 : 2;
+  }();
+  return v;
+}
+
+template <int NP, int MT>
+static void launch_mm(const BwArgs& g, int64_t nseq, hipStream_t stream) {
+  const dim3 grid((unsigned)((nseq + 16 * MT - 1) / (16 * MT))), block(256);
+  hipLaunchKernelGGL((bw_fwd_mm<NP, MT>), grid, block, 0, stream, g, nseq);
+  hipLaunchKernelGGL((bw_bwd_mm<NP, MT>), grid, block, 0, stream, g, nseq);
+}
+
+static bool gemm_st2() {  // A/B knob: CV_BW_GEMM_ST2=1 double-buffers the GEMM's loads
+  static const bool v = [] {
+    const char* e = getenv("CV_BW_GEMM_ST2");
+#ifdef CVF_GEMM_ST2_DEFAULT
+    return !(e && e[0] == '0');
+#else
+    return e && e[0] == '1';
+#endif
+  }();
+  return v;
+}
+
+static bool gemm32() {  // A/B knob: CV_BW_GEMM32=1 keeps 32 x 32 tiles at every N
+  static const bool v = [] {
+    const char* e = getenv("CV_BW_GEMM32");
+    return e && e[0] == '1';
+  }();
+  return v;
+}
+
 hipError_t launch_bw_estep(const BwArgs& g, int64_t nseq, int64_t max_waves, hipStream_t stream, int64_t nrows) {
   if (nseq <= 0) return hipSuccess;
   if (g.nstates > kBwMaxStates) return hipErrorInvalidValue;
-  if (g.nstates > kBwLdsStates) {  // the xi sum as R^T U on the matrix cores
-    hipLaunchKernelGGL(bw_forward, dim3((unsigned)nseq), dim3(256), 0, stream, g);
-    hipLaunchKernelGGL(bw_backward, dim3((unsigned)nseq), dim3(256), 0, stream, g);
-    hipLaunchKernelGGL(bw_stats_rows, dim3((unsigned)nseq), dim3(256), 0, stream, g);
-    const int nt32 = (g.nstates + 31) / 32;
-    // ~4,096 waves: row ranges of a multiple of 4 rows per output tile
-    const int64_t parts = std::max<int64_t>(1, std::min<int64_t>(4096 / (nt32 * nt32), (nrows + 255) / 256));
+  static const bool per_seq = [] {  // A/B knob: CV_BW_PERSEQ=1 keeps one workgroup per sequence
+    const char* e = getenv("CV_BW_PERSEQ");
+    return e && e[0] == '1';
+  }();
+  const bool mm = g.nstates > kBwWaveStates && !per_seq;
+  if (g.nstates > kBwLdsStates || mm) {  // the xi sum as R^T U on the matrix cores
+    if (mm) {  // 16 MT sequences per workgroup, the step products on the matrix cores
+      if (bw_mt() == 4) {
+        if (g.nstates <= 128) launch_mm<128, 4>(g, nseq, stream);
+        else if (g.nstates <= 192) launch_mm<192, 4>(g, nseq, stream);
+        else launch_mm<256, 4>(g, nseq, stream);
+      } else {
+        if (g.nstates <= 128) launch_mm<128, 2>(g, nseq, stream);
+        else if (g.nstates <= 192) launch_mm<192, 2>(g, nseq, stream);
+        else launch_mm<256, 2>(g, nseq, stream);
+      }
+    } else {
+      hipLaunchKernelGGL(bw_forward, dim3((unsigned)nseq), dim3(256), 0, stream, g);
+      hipLaunchKernelGGL(bw_backward, dim3((unsigned)nseq), dim3(256), 0, stream, g);
+      hipLaunchKernelGGL(bw_stats_rows, dim3((unsigned)nseq), dim3(256), 0, stream, g);
+    }
+    // 64 x 64 tiles per wave above 128 states (32 x 32 below); ~4,096 waves: row ranges of a
+    // multiple of 4 rows per output tile
+    const bool t64 = g.nstates > 128 && !gemm32();
+    const int ts = t64 ? 64 : 32, ntt = (g.nstates + ts - 1) / ts;
+    const int64_t parts = std::max<int64_t>(1, std::min<int64_t>(4096 / (ntt * ntt), (nrows + 255) / 256));
     const int64_t per = ((nrows + parts - 1) / parts + 3) / 4 * 4;
     const int64_t np = (nrows + per - 1) / per;
-    hipLaunchKernelGGL(bw_xi_gemm, dim3((unsigned)(np * nt32 * nt32)), dim3(64), 0, stream, g, nrows, per);
+    // a multiple of 8 row ranges (empty ones exit): the XCD-aware block mapping of bw_xi_gemm
+    const dim3 grid((unsigned)((np + 7) / 8 * 8 * ntt * ntt)), block(64);
+    if (t64 && gemm_st2())
+      hipLaunchKernelGGL((bw_xi_gemm<4, 2>), grid, block, 0, stream, g, nrows, per);
+    else if (t64)
+      hipLaunchKernelGGL((bw_xi_gemm<4, 1>), grid, block, 0, stream, g, nrows, per);
+    else
+      hipLaunchKernelGGL((bw_xi_gemm<2, 1>), grid, block, 0, stream, g, nrows, per);
     return hipGetLastError();
   }
   if (g.nstates <= kBwWaveStates) {

@@ -124,6 +124,37 @@ def test_gpu_train_matches_oracle(gpu, n, v, frac, tmax):
 
 
 @pytest.mark.gpu
+# 64 < N <= 256 runs 64 sequences per workgroup (bw_fwd_mm / bw_bwd_mm): several workgroups,
+# ragged lengths inside each (longest first), one-element sequences, tagged first/last
+# elements, fully tagged sequences and a padded state count per kernel width (128/192/256)
+@pytest.mark.parametrize("n,nseq,tmax,frac", [(65, 150, 40, 0.2), (100, 200, 60, 0.3), (128, 130, 33, 0.0),
+                                              (150, 97, 50, 0.5), (192, 70, 45, 0.1), (255, 140, 30, 0.2),
+                                              (256, 260, 40, 0.15)])
+def test_gpu_train_groups_match_oracle(gpu, n, nseq, tmax, frac):
+    import cviterbi as cv
+
+    v = 37
+    off, obs, tags = _corpus(n, v, nseq, tmax, frac, seed=500 + n)
+    lengths = np.diff(off)
+    # a fully tagged sequence and one with only its ends tagged
+    k = int(np.argmax(lengths))
+    tags[off[k]:off[k + 1]] = np.arange(lengths[k]) % n
+    k2 = (k + 1) % nseq
+    tags[off[k2]:off[k2 + 1]] = -1
+    tags[off[k2]] = 3
+    tags[off[k2 + 1] - 1] = n - 1
+    pi0, a0, b0 = _probs(n, v, seed=500 + n)
+    iters = 2
+    gp, ga, gb, it = cv.fit_train(pi0, a0, b0, off, obs, tags, max_iter=iters, tol=0.0)
+    assert it == iters
+    rp, ra, rb, _ = FO.train(pi0, a0, b0, off, obs, tags, iters, 0.0)
+    for g, r, what in zip((gp, ga, gb), (rp, ra, rb), ("pi", "a", "b")):
+        assert np.array_equal(np.isinf(g), np.isinf(r)), what
+        fin = np.isfinite(r)
+        np.testing.assert_allclose(g[fin], r[fin], rtol=0, atol=1e-9, err_msg=what)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("n", [20, 100, 200])  # wave kernels, LDS xi sum, GEMM xi sum
 def test_gpu_train_subnormal_xi_denominator(gpu, n):
     """Emission probabilities below DBL_MIN for one observation make xi's normaliser c_t

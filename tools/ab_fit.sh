@@ -1,0 +1,26 @@
+#!/bin/bash
+# A/B of libcviterbi.so builds (tools/_ab/lib_<v>.so) on the Baum-Welch E-step kernels at
+# config-4 shape: kernel times from a rocprofv3 kernel trace, interleaved on ONE box.
+# Usage: VARIANTS="a b" ROUNDS=2 TAG=... tools/ab_fit.sh
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$R/gpurun_out/${TAG:-abfit}
+mkdir -p $OUT
+LIB=$R/consistent-viterbi_amd/cviterbi/libcviterbi.so
+cp $LIB $OUT/lib_orig.so
+for r in $(seq 1 ${ROUNDS:-2}); do
+  for v in ${VARIANTS:-a b}; do
+    cp $R/tools/_ab/lib_$v.so $LIB
+    (cd /tmp && TMPDIR=/tmp SHAPE=c4 ITERS=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
+      -d $OUT/$v.$r -o kt -- python3 $R/tools/bench_fit.py > $OUT/$v.$r.log 2>&1) || { cp $OUT/lib_orig.so $LIB; echo "FAIL $v"; exit 1; }
+    python3 - $OUT/$v.$r/kt_kernel_stats.csv $v $r <<'PY' | tee -a $OUT/summary.txt
+import csv, sys
+row = [f"{sys.argv[2]} {sys.argv[3]}"]
+for r in csv.DictReader(open(sys.argv[1])):
+    if "bw_" in r["Name"] and "mstep" not in r["Name"]:
+        row.append(f'{r["Name"].split("(")[0].replace("void cvf::", "")} {float(r["AverageNs"]) / 1e6:.2f}')
+print("  ".join(row))
+PY
+  done
+done
+cp $OUT/lib_orig.so $LIB
