@@ -366,6 +366,88 @@ __global__ __launch_bounds__(64, 2) void bw_xi_gemm(BwArgs g, int64_t nrows, int
       }
 }
 
+// The same sum with 128 x 128 output tiles per workgroup (four waves of 64 x 64): 16 rows of R
+// and U at a time go through LDS (double-buffered, 64 KiB), so each row segment comes from L2
+// once per workgroup instead of once per wave -- half the L2 traffic of bw_xi_gemm<4> at 256
+// states.  Row ranges and the XCD-aware block map as above.
+constexpr int kGemmKB = 16;  // rows per LDS stage
+__global__ __launch_bounds__(256, 2) void bw_xi_gemm_lds(BwArgs g, int64_t nrows, int64_t rows_per_wg) {
+  constexpr int TS = 128, KB = kGemmKB, LS = TS + 2;  // LS: row stride (doubles) of a stage
+  __shared__ __attribute__((aligned(16))) double rs[2][KB * LS], us[2][KB * LS];
+  const int N = g.nstates;
+  const int ntt = (N + TS - 1) / TS;
+  const int64_t b = blockIdx.x, j = b / 8;
+  const int tile = (int)(j % (ntt * ntt));
+  const int64_t part = (j / (ntt * ntt)) * 8 + b % 8;
+  const int m0 = TS * (tile / ntt), n0 = TS * (tile % ntt);
+  const int64_t r0 = part * rows_per_wg;
+  if (r0 >= nrows) return;  // workgroup-uniform (padding blocks)
+  const int64_t r1 = r0 + rows_per_wg < nrows ? r0 + rows_per_wg : nrows;
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, kk = l >> 4, cl = l & 15;
+  const int wm = w >> 1, wn = w & 1;
+  // staging: thread tid copies rows (tid >> 4) of R and U, 8 doubles from column 8 (tid & 15)
+  const int srow = tid >> 4, scol = 8 * (tid & 15);
+  auto stage_load = [&](int64_t rb, double (&ra)[8], double (&ua)[8]) {
+    const int64_t row = rb + srow;
+    const bool vr = row < r1;
+    const double* R = g.alpha + (size_t)(vr ? row : r0) * N;
+    const double* U = g.beta + (size_t)(vr ? row : r0) * N;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int cm = m0 + scol + q, cn = n0 + scol + q;
+      ra[q] = (vr && cm < N) ? R[cm] : 0.0;
+      ua[q] = (vr && cn < N) ? U[cn] : 0.0;
+    }
+  };
+  auto stage_store = [&](int buf, const double (&ra)[8], const double (&ua)[8]) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      rs[buf][srow * LS + scol + q] = ra[q];
+      us[buf][srow * LS + scol + q] = ua[q];
+    }
+  };
+  f64x4_t acc[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) acc[a][c] = f64x4_t{0.0, 0.0, 0.0, 0.0};
+  double ra[8], ua[8];
+  stage_load(r0, ra, ua);
+  stage_store(0, ra, ua);
+  __syncthreads();
+  int buf = 0;
+  for (int64_t rb = r0; rb < r1; rb += KB) {
+    const bool next = rb + KB < r1;  // workgroup-uniform
+    if (next) stage_load(rb + KB, ra, ua);  // in flight during this stage's products
+#pragma unroll
+    for (int ks = 0; ks < KB / 4; ++ks) {
+      const int row = 4 * ks + kk;
+      double av[4], bv[4];
+#pragma unroll
+      for (int a = 0; a < 4; ++a) av[a] = rs[buf][row * LS + 64 * wm + 16 * a + cl];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) bv[c] = us[buf][row * LS + 64 * wn + 16 * c + cl];
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) acc[a][c] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[a], bv[c], acc[a][c], 0, 0, 0);
+    }
+    if (next) stage_store(buf ^ 1, ra, ua);
+    __syncthreads();  // the next stage complete; this one free
+    buf ^= 1;
+  }
+  // C/D layout of v_mfma_f64_16x16x4_f64: col = lane & 15, row = (lane >> 4) + 4 * reg
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int row = m0 + 64 * wm + 16 * a + (l >> 4) + 4 * q, col = n0 + 64 * wn + 16 * c + (l & 15);
+        if (row < N && col < N && acc[a][c][q] != 0.0) unsafeAtomicAdd(&g.xi_s[(size_t)row * N + col], acc[a][c][q]);
+      }
+}
+
 // ---- N <= 64: one wave per sequence ---------------------------------------------------------
 // Lane i owns state i.  The transition matrix lives in VGPRs (forward: column i, backward:
 // row i), the vector being multiplied is broadcast through a per-wave LDS slot (ds_read_b128,
@@ -776,8 +858,7 @@ __global__ __launch_bounds__(256) void bw_bwd_stats_wave(BwArgs g, int64_t nseq,
 // read serves 64 sequences.  Wave w owns the output columns [64 w, 64 w + 64) (CT = NP / 64
 // tiles of 16) for all 64 sequences (4 tiles of 16): 16 CT independent accumulators, lane l
 // holding Y[g = 16 m + (l >> 4) + 4 r][i = 16 (w CT + n) + (l & 15)] (f64 C/D layout).  The
-// next step's operand X goes through LDS transposed, X^T[k][g] (xt_at: swizzled against bank
-// conflicts on both the writes and the operand reads).  Row sums (normalisation, c_t, gamma) reduce in registers over the wave's tiles,
+// next step's operand X goes through LDS transposed, X^T[k][g] (xt_at: a padded row stride).  Row sums (normalisation, c_t, gamma) reduce in registers over the wave's tiles,
 // by DPP over the 16 lanes of a row, then over the 4 waves through LDS -- one order, so runs
 // repeat bit for bit.  A's indices are clamped into [0, N): rows k >= N meet X entries that
 // are 0, columns >= N are dropped.
@@ -800,21 +881,44 @@ __device__ __forceinline__ double row16_max(double v) {
 // in another order than the reference's anyway).  Both scaled by 2^64, so a subnormal s (tiny
 // emissions) still has a finite reciprocal; every v here is one of s's non-negative terms.
 __device__ __forceinline__ double recip64(double s) { return 1.0 / (s * 0x1p64); }
-__device__ __forceinline__ double normalized_r(double v, double s, double inv, int n) {
-  return s != 0.0 ? (v * 0x1p64) * inv : 1.0 / n;
+// a select of two computed values: without the empty asm the compiler turns a per-lane `?:`
+// with arithmetic on one side into an exec-masked branch, and a branch here waits for every
+// outstanding load (vmcnt(0))
+__device__ __forceinline__ double sel(bool c, double a, double b) {
+  asm("" : "+v"(a));
+  asm("" : "+v"(b));
+  return c ? a : b;
+}
+// s != 0: v / s (to an ulp, by the reciprocal); s == 0: 1 / n (hmm.rs:274-282)
+__device__ __forceinline__ double normalized_r(double v, double s, double inv, double inv_n) {
+  return sel(s != 0.0, (v * 0x1p64) * inv, inv_n);
 }
 
-// X^T[k][g] swizzled: g ^ (k & 15) spreads the 16 consecutive k of one ds_write_b64 (16 lanes,
-// one g) over 16 bank pairs; ^ 16 on odd k puts the two 16-lane halves of an operand read (k,
-// k + 1; 16 consecutive g) on opposite bank halves.  Needs G >= 32.
+// X^T[k][g] with a row stride of G + 1 doubles: one ds_write_b64 (16 lanes: 16 consecutive k,
+// one g) spreads over 16 bank pairs; an operand read (16 consecutive g at k and k + 1) is a
+// 2-way conflict.  Additive, so every (tile, register) offset is a compile-time constant the
+// LDS instructions carry (an XOR swizzle kept 16-32 per-lane addresses live and spilled).
 template <int G>
-__device__ __forceinline__ int xt_at(int k, int g) { return k * G + (g ^ (k & 15) ^ ((k & 1) << 4)); }
+__device__ __forceinline__ int xt_at(int k, int g) { return k * (G + 1) + g; }
 
-// Y = X . M over the LDS operand X^T (xt) and the row-major N x N matrix M (A or A^T)
-template <int NP, int MT>
+// the WV waves' partials of sequence gi (red[w * G + gi]) added in one fixed (pairwise) order
+template <int WV>
+__device__ __forceinline__ double wsum(const double* red, int G, int gi) {
+  if constexpr (WV == 4) return (red[gi] + red[G + gi]) + (red[2 * G + gi] + red[3 * G + gi]);
+  else return wsum<WV / 2>(red, G, gi) + wsum<WV / 2>(red + (WV / 2) * G, G, gi);
+}
+template <int WV>
+__device__ __forceinline__ double wmax(const double* red, int G, int gi) {
+  double v = red[gi];
+#pragma unroll
+  for (int w = 1; w < WV; ++w) v = fmax(v, red[w * G + gi]);
+  return v;
+}
+
+template <int NP, int MT, int WV, class Pre>
 __device__ __forceinline__ void mm_step(const double* __restrict__ xt, const double* __restrict__ M, int N, int w,
-                                        int l, f64x4_t (&acc)[MT][NP / 64]) {
-  constexpr int CT = NP / 64, NK = NP / 4, PF = 4, G = 16 * MT;
+                                        int l, f64x4_t (&acc)[MT][NP / (16 * WV)], Pre&& pre) {
+  constexpr int CT = NP / (16 * WV), NK = NP / 4, PF = 4, G = 16 * MT;
   const int cl = l & 15, kq = l >> 4;
   int col[CT];
 #pragma unroll
@@ -823,32 +927,42 @@ __device__ __forceinline__ void mm_step(const double* __restrict__ xt, const dou
   for (int m = 0; m < MT; ++m)
 #pragma unroll
     for (int n = 0; n < CT; ++n) acc[m][n] = f64x4_t{0.0, 0.0, 0.0, 0.0};
+  // A rows PF k-blocks ahead (L2), the LDS operand one k-block ahead
   double ring[PF][CT];
-  auto load = [&](int kk, double (&dst)[CT]) {
-    const int k = min(4 * kk + kq, N - 1);
+#define CVF_MM_LOAD(KK, DST)                                                  \
+  {                                                                           \
+    const int k_ = min(4 * (KK) + kq, N - 1);                                 \
+    _Pragma("unroll") for (int n = 0; n < CT; ++n) DST[n] = M[(size_t)k_ * N + col[n]]; \
+  }
 #pragma unroll
-    for (int n = 0; n < CT; ++n) dst[n] = M[(size_t)k * N + col[n]];
-  };
+  for (int p = 0; p < PF; ++p) CVF_MM_LOAD(p, ring[p])
+  // loads the caller wants in flight during the products: issued after the ring's first
+  // blocks, so the in-order wait for those does not wait for them
+  pre();
+  double av[MT];
 #pragma unroll
-  for (int p = 0; p < PF; ++p) load(p, ring[p]);
+  for (int m = 0; m < MT; ++m) av[m] = xt[xt_at<G>(kq, 16 * m + cl)];
 #pragma unroll 1
   for (int kk0 = 0; kk0 < NK; kk0 += PF) {
 #pragma unroll
     for (int p = 0; p < PF; ++p) {
-      const int kk = kk0 + p, k = 4 * kk + kq;
-      double bv[CT];
+      const int kk = kk0 + p;
+      double bv[CT], an[MT];
 #pragma unroll
       for (int n = 0; n < CT; ++n) bv[n] = ring[p][n];
-      load(min(kk + PF, NK - 1), ring[p]);
-      double av[MT];
+      CVF_MM_LOAD(min(kk + PF, NK - 1), ring[p])
+      const int kn = 4 * min(kk + 1, NK - 1) + kq;
 #pragma unroll
-      for (int m = 0; m < MT; ++m) av[m] = xt[xt_at<G>(k, 16 * m + cl)];
+      for (int m = 0; m < MT; ++m) an[m] = xt[xt_at<G>(kn, 16 * m + cl)];
 #pragma unroll
       for (int m = 0; m < MT; ++m)
 #pragma unroll
         for (int n = 0; n < CT; ++n) acc[m][n] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[m], bv[n], acc[m][n], 0, 0, 0);
+#pragma unroll
+      for (int m = 0; m < MT; ++m) av[m] = an[m];
     }
   }
+#undef CVF_MM_LOAD
 }
 
 // the group's sequences: element offset, length, and the longest length
@@ -876,55 +990,58 @@ __device__ __forceinline__ void mm_setup(const BwArgs& g, int64_t nseq, int64_t*
   __syncthreads();
 }
 
-// forward (hmm.rs:78-100) of 64 sequences: alpha rows to g.alpha
-template <int NP, int MT>
-__global__ __launch_bounds__(256, MT == 4 ? 1 : 2) void bw_fwd_mm(BwArgs g, int64_t nseq) {
-  constexpr int CT = NP / 64, G = 16 * MT;
-  __shared__ __attribute__((aligned(16))) double xt[NP * G];
-  __shared__ double red[4][G];
+// forward (hmm.rs:78-100) of 16 MT sequences: alpha rows to g.alpha (observation slots two
+// steps ahead: slot t & 3 holds step t, written at step t - 2 behind two barriers).
+template <int NP, int MT, int WV>
+__global__ __launch_bounds__(64 * WV, (MT == 4 ? 1 : 2) * WV / 4) void bw_fwd_mm(BwArgs g, int64_t nseq) {
+  constexpr int CT = NP / (16 * WV), G = 16 * MT;
+  __shared__ __attribute__((aligned(16))) double xt[NP * (G + 1)];
+  __shared__ double red[WV][G];
   __shared__ int64_t s_e0[G];
-  __shared__ int s_T[G], s_ob[2][G], s_tg[2][G];
+  __shared__ int s_T[G], s_ob[4][G], s_tg[4][G];
   __shared__ int s_tmax;
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, cl = l & 15;
   const int N = g.nstates;
+  const double inv_n = 1.0 / N;
+  double* const dump = g.dump + (size_t)((blockIdx.x * WV + (tid >> 6)) & (kBwDumpWaves - 1)) * 64 + (tid & 63);
   mm_setup<G>(g, nseq, s_e0, s_T, &s_tmax);
   const int tmax = s_tmax;
   if (tmax <= 0) return;  // workgroup-uniform
-  auto fetch = [&](int t) {  // observation and tag of step t into slot t & 1
+  auto fetch = [&](int t) {  // observation and tag of step t into slot t & 3
     if (tid < G) {
       const bool v = t < s_T[tid];
       const int64_t e = (int64_t)s_e0[tid] + g.elem_base + (v ? t : 0);
-      s_ob[t & 1][tid] = v ? g.obs[e] : 0;
-      s_tg[t & 1][tid] = v ? g.tags[e] : -1;
+      s_ob[t & 3][tid] = v ? g.obs[e] : 0;
+      s_tg[t & 3][tid] = v ? g.tags[e] : -1;
     }
   };
   fetch(0);
   fetch(1);
+  fetch(2);
   __syncthreads();
-  int col[CT];
+  int col[CT], cc[CT];
 #pragma unroll
-  for (int n = 0; n < CT; ++n) col[n] = 16 * (w * CT + n) + cl;
+  for (int n = 0; n < CT; ++n) {
+    col[n] = 16 * (w * CT + n) + cl;
+    cc[n] = min(col[n], N - 1);
+  }
   f64x4_t acc[MT][CT];
   // t = 0 (hmm.rs:81-88): y = pi * b(o_0)
 #pragma unroll
   for (int m = 0; m < MT; ++m)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int gi = 16 * m + (l >> 4) + 4 * r;
-      const int o = s_ob[0][gi];
+      const int o = s_ob[0][16 * m + (l >> 4) + 4 * r];
 #pragma unroll
-      for (int n = 0; n < CT; ++n) {
-        const int c = min(col[n], N - 1);
-        acc[m][n][r] = g.pi[c] * g.et[(size_t)o * N + c];
-      }
+      for (int n = 0; n < CT; ++n) acc[m][n][r] = g.pi[cc[n]] * g.et[(size_t)o * N + cc[n]];
     }
   for (int t = 0;; ++t) {
     if (t > 0) {
-      fetch(t + 1);  // slot (t + 1) & 1 was last read in phase t - 1, before its closing barrier
-      mm_step<NP, MT>(xt, g.a, N, w, l, acc);  // (alpha_{t-1} o b(o_t)) . A  (hmm.rs:93-94)
+      fetch(t + 2);  // slot (t + 2) & 3 held step t - 2, last read before step t - 1's closing barrier
+      // (alpha_{t-1} o b(o_t)) . A  (hmm.rs:93-94)
+      mm_step<NP, MT, WV>(xt, g.a, N, w, l, acc, [] {});
     }
     // row sums of y over the N states
-    double s[MT][4];
 #pragma unroll
     for (int m = 0; m < MT; ++m)
 #pragma unroll
@@ -932,8 +1049,8 @@ __global__ __launch_bounds__(256, MT == 4 ? 1 : 2) void bw_fwd_mm(BwArgs g, int6
         double v = 0.0;
 #pragma unroll
         for (int n = 0; n < CT; ++n) v += col[n] < N ? acc[m][n][r] : 0.0;
-        s[m][r] = row16_sum(v);
-        if (cl == 0) red[w][16 * m + (l >> 4) + 4 * r] = s[m][r];
+        v = row16_sum(v);
+        if (cl == 0) red[w][16 * m + (l >> 4) + 4 * r] = v;
       }
     __syncthreads();
     const bool more = t + 1 < tmax;
@@ -942,42 +1059,59 @@ __global__ __launch_bounds__(256, MT == 4 ? 1 : 2) void bw_fwd_mm(BwArgs g, int6
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int gi = 16 * m + (l >> 4) + 4 * r;
-        const double sum = (red[0][gi] + red[1][gi]) + (red[2][gi] + red[3][gi]);
+        const double sum = wsum<WV>(&red[0][0], G, gi);
         const double inv = recip64(sum);
-        const int tg = s_tg[t & 1][gi];
+        const int tg = s_tg[t & 3][gi];
         const bool on = t < s_T[gi];
-        const int o1 = s_ob[(t + 1) & 1][gi];
         const bool on1 = t + 1 < s_T[gi];
         double* arow = g.alpha + (size_t)(s_e0[gi] + t) * N;
 #pragma unroll
         for (int n = 0; n < CT; ++n) {
           const int c = col[n];
-          const double a = tg >= 0 ? (c == tg ? 1.0 : 0.0) : normalized_r(acc[m][n][r], sum, inv, N);
-          if (on && c < N) arow[c] = a;
-          if (more) xt[xt_at<G>(c, gi)] = (on1 && c < N) ? a * g.et[(size_t)o1 * N + min(c, N - 1)] : 0.0;
+          const double a = sel(tg >= 0, c == tg ? 1.0 : 0.0, normalized_r(acc[m][n][r], sum, inv, inv_n));
+          *((on && c < N) ? arow + c : dump) = a;  // branch-free: dead lanes store to their dump slot
+          acc[m][n][r] = sel(on1 && c < N, a, 0.0);
         }
       }
-    __syncthreads();  // xt complete; red and the step-t slot free
+    // the next operand alpha_t o b(o_{t+1}): all emission loads (L2 hits) issued together
+    if (more) {
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int gi = 16 * m + (l >> 4) + 4 * r;
+          const double* er = g.et + (size_t)s_ob[(t + 1) & 3][gi] * N;  // b(o_{t+1})
+#pragma unroll
+          for (int n = 0; n < CT; ++n) xt[xt_at<G>(col[n], gi)] = acc[m][n][r] * er[cc[n]];
+        }
+    }
+    __syncthreads();  // xt complete; red free
     if (!more) break;
   }
 }
 
-// backward (hmm.rs:102-121) fused with gamma / xi of hmm.rs:124-143 for 64 sequences, aligned
-// at their last elements: step r is t = T_g - 1 - r of sequence g.  W_t = A u_{t+1} (u_{t+1} =
-// b(o_{t+1}) o beta_{t+1}, in xt) gives c_t = alpha_t . W_t and beta_t = normalize(W_t); gamma_t =
-// normalize(alpha_t o beta_t) goes into the sums, and r_t = alpha_t / (c_t 2^k) and
-// u'_{t+1} = u_{t+1} 2^k overwrite alpha's and beta's row t for bw_xi_gemm (zeros at t = T - 1),
-// as bw_stats_rows writes them.
-template <int NP, int MT>
-__global__ __launch_bounds__(256, MT == 4 ? 1 : 2) void bw_bwd_mm(BwArgs g, int64_t nseq) {
-  constexpr int CT = NP / 64, G = 16 * MT;
-  __shared__ __attribute__((aligned(16))) double xt[NP * G];
-  __shared__ double red1[3][4][G], red2[4][G];  // the two reduction rounds
+// backward (hmm.rs:102-121) fused with gamma / xi of hmm.rs:124-143 for 16 MT sequences,
+// aligned at their last elements: step r is t = T_g - 1 - r of sequence g.  W_t = A u_{t+1}
+// (u_{t+1} = b(o_{t+1}) o beta_{t+1}, in xt) gives c_t = alpha_t . W_t and beta_t =
+// normalize(W_t); r_t = alpha_t / (c_t 2^k) and u'_{t+1} = u_{t+1} 2^k overwrite alpha's and
+// beta's row t for bw_xi_gemm (zeros at t = T - 1), as bw_stats_rows writes them.  One
+// reduction round per step: gamma_t = normalize(alpha_t o beta_t) needs sum_i alpha_i beta_i,
+// which is c_t / sum W_t for an untagged step (beta = W / sum W), 1 at a tagged one (alpha_t and
+// beta_t both one-hot at the tag: the forward wrote alpha_t so), and sum alpha_t at t = T - 1
+// (beta = 1) or where sum W_t = 0 (beta uniform, / N).  alpha_t's loads are in flight during
+// the step's products with -DCVF_BWD_PREFETCH (its registers spill at N = 256).
+template <int NP, int MT, int WV>
+__global__ __launch_bounds__(64 * WV, (MT == 4 ? 1 : 2) * WV / 4) void bw_bwd_mm(BwArgs g, int64_t nseq) {
+  constexpr int CT = NP / (16 * WV), G = 16 * MT;
+  __shared__ __attribute__((aligned(16))) double xt[NP * (G + 1)];
+  __shared__ double red[4][WV][G];  // c, sum W, max u_{t+1}, sum alpha -- per wave
+  __shared__ double s_den[3][NP];   // the workgroup's pi_acc, a_den, b_den (LDS atomics)
   __shared__ int64_t s_e0[G];
   __shared__ int s_T[G], s_ob[2][G], s_tg[2][G];
   __shared__ int s_tmax;
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, cl = l & 15;
   const int N = g.nstates;
+  const double inv_n = 1.0 / N;
   mm_setup<G>(g, nseq, s_e0, s_T, &s_tmax);
   const int tmax = s_tmax;
   if (tmax <= 0) return;
@@ -990,22 +1124,17 @@ __global__ __launch_bounds__(256, MT == 4 ? 1 : 2) void bw_bwd_mm(BwArgs g, int6
     }
   };
   fetch(0);
+  for (int i = tid; i < 3 * NP; i += 64 * WV) (&s_den[0][0])[i] = 0.0;
   __syncthreads();
-  int col[CT];
+  int col[CT], cc[CT];
 #pragma unroll
-  for (int n = 0; n < CT; ++n) col[n] = 16 * (w * CT + n) + cl;
+  for (int n = 0; n < CT; ++n) {
+    col[n] = 16 * (w * CT + n) + cl;
+    cc[n] = min(col[n], N - 1);
+  }
   f64x4_t acc[MT][CT];
-  double pi_acc[CT], a_den[CT], b_den[CT], z = 0.0;
-#pragma unroll
-  for (int n = 0; n < CT; ++n) pi_acc[n] = a_den[n] = b_den[n] = 0.0;
-  double* const dump = g.dump + (size_t)((blockIdx.x * 4 + w) & (kBwDumpWaves - 1)) * 64 + l;
-  for (int r = 0; r < tmax; ++r) {
-    if (r > 0) {
-      fetch(r);
-      mm_step<NP, MT>(xt, g.at, N, w, l, acc);  // W_t[i] = sum_j A[i][j] u_{t+1}[j]  (hmm.rs:113-116)
-    }
-    // alpha_t, and (r > 0) the first round: c_t = alpha_t . W_t, sum W_t, max u_{t+1}
-    double al[MT][CT][4];
+  double al[MT][CT][4];
+  auto load_alpha = [&](int r) {
 #pragma unroll
     for (int m = 0; m < MT; ++m)
 #pragma unroll
@@ -1014,146 +1143,141 @@ __global__ __launch_bounds__(256, MT == 4 ? 1 : 2) void bw_bwd_mm(BwArgs g, int6
         const int t = s_T[gi] - 1 - r;
         const double* arow = g.alpha + (size_t)(s_e0[gi] + max(t, 0)) * N;
 #pragma unroll
-        for (int n = 0; n < CT; ++n)
-#ifndef CVF_ABL_NOALPHA
-          al[m][n][q] = (t >= 0 && col[n] < N) ? arow[min(col[n], N - 1)] : 0.0;
-#else
-          al[m][n][q] = (t >= 0 && col[n] < N) ? 1e-3 * (double)(t + col[n]) : 0.0;
-#endif
+        for (int n = 0; n < CT; ++n) {
+          // unconditional (clamped row): a load under a per-lane branch is waited for at once
+          al[m][n][q] = sel(t >= 0 && col[n] < N, arow[cc[n]], 0.0);
+        }
       }
-    // beta_t replaces W_t in the accumulators (registers: alpha_t and beta_t stay live)
+  };
+  double z = 0.0;
+  double* const dump = g.dump + (size_t)((blockIdx.x * WV + w) & (kBwDumpWaves - 1)) * 64 + l;
+  for (int r = 0; r < tmax; ++r) {
     if (r > 0) {
-#pragma unroll
-      for (int m = 0; m < MT; ++m)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int gi = 16 * m + (l >> 4) + 4 * q;
-          double c = 0.0, sw = 0.0, um = 0.0;
-#pragma unroll
-          for (int n = 0; n < CT; ++n) {
-            const double wv = col[n] < N ? acc[m][n][q] : 0.0;
-            c += al[m][n][q] * wv;
-            sw += wv;
-            um = fmax(um, xt[xt_at<G>(col[n], gi)]);  // u_{t+1} (0 beyond N)
-          }
-          c = row16_sum(c);
-          sw = row16_sum(sw);
-          um = row16_max(um);
-          if (cl == 0) {
-            red1[0][w][gi] = c;
-            red1[1][w][gi] = sw;
-            red1[2][w][gi] = um;
-          }
-        }
-      __syncthreads();
-#pragma unroll
-      for (int m = 0; m < MT; ++m)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int gi = 16 * m + (l >> 4) + 4 * q;
-          const double c = (red1[0][0][gi] + red1[0][1][gi]) + (red1[0][2][gi] + red1[0][3][gi]);
-          const double sw = (red1[1][0][gi] + red1[1][1][gi]) + (red1[1][2][gi] + red1[1][3][gi]);
-          const double isw = recip64(sw);
-          const int t = s_T[gi] - 1 - r;
-          const bool on = t >= 0;
-          const double umax = fmax(fmax(red1[2][0][gi], red1[2][1][gi]), fmax(red1[2][2][gi], red1[2][3][gi]));
-          const int ks = xi_scale(c, umax);  // balanced factors (xi_scale)
-          const double ics = recip64(__builtin_ldexp(c, ks));  // r = alpha / (c 2^k), by one reciprocal
-          const int tg = s_tg[r & 1][gi];
-          double* rrow = g.alpha + (size_t)(s_e0[gi] + max(t, 0)) * N;
-          double* urow = g.beta + (size_t)(s_e0[gi] + max(t, 0)) * N;
-#pragma unroll
-          for (int n = 0; n < CT; ++n) {
-            const int cc = col[n];
-            const double u = xt[xt_at<G>(cc, gi)];  // u_{t+1}, unscaled
-            if (on && cc < N) {
-              rrow[cc] = c != 0.0 ? (al[m][n][q] * 0x1p64) * ics : 0.0;
-              urow[cc] = __builtin_ldexp(u, ks);
-            }
-            const double wv = acc[m][n][q];
-            acc[m][n][q] = tg >= 0 ? (cc == tg ? 1.0 : 0.0) : (cc < N ? normalized_r(wv, sw, isw, N) : 0.0);
-          }
-          // xi_t uniform (hmm.rs:306-317), counted separately: once per sequence step (lanes
-          // 0, 16, 32, 48 of wave 0 between them see every g)
-          if (on && c == 0.0 && cl == 0 && w == 0) z += 1.0;
-        }
+      fetch(r);  // slot r & 1 held step r - 2, read before step r - 1's closing barrier
+      // W_t[i] = sum_j A[i][j] u_{t+1}[j]  (hmm.rs:113-116)
+#ifdef CVF_BWD_PREFETCH
+      mm_step<NP, MT, WV>(xt, g.at, N, w, l, acc, [&] { load_alpha(r); });
+#else
+      mm_step<NP, MT, WV>(xt, g.at, N, w, l, acc, [] {});
+      load_alpha(r);
+#endif
     } else {
-      // t = T - 1 (hmm.rs:105-108): tagged -> one-hot, else ones; no xi term (zero rows)
+      load_alpha(0);
 #pragma unroll
       for (int m = 0; m < MT; ++m)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int gi = 16 * m + (l >> 4) + 4 * q;
-          const int t = s_T[gi] - 1;
-          const int tg = s_tg[0][gi];
-          double* rrow = g.alpha + (size_t)(s_e0[gi] + max(t, 0)) * N;
-          double* urow = g.beta + (size_t)(s_e0[gi] + max(t, 0)) * N;
-#pragma unroll
-          for (int n = 0; n < CT; ++n) {
-            const int cc = col[n];
-            if (t >= 0 && cc < N) rrow[cc] = urow[cc] = 0.0;
-            acc[m][n][q] = tg >= 0 ? (cc == tg ? 1.0 : 0.0) : (cc < N ? 1.0 : 0.0);
-          }
-        }
+        for (int n = 0; n < CT; ++n) acc[m][n] = f64x4_t{0.0, 0.0, 0.0, 0.0};
     }
-    // second round: gamma_t's sum
+    // the reduction round: c_t, sum W_t, max u_{t+1} (r > 0), sum alpha_t
 #pragma unroll
     for (int m = 0; m < MT; ++m)
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int gi = 16 * m + (l >> 4) + 4 * q;
-        double sab = 0.0;
-#pragma unroll
-        for (int n = 0; n < CT; ++n) sab += al[m][n][q] * acc[m][n][q];
-        sab = row16_sum(sab);
-        if (cl == 0) red2[w][gi] = sab;
-      }
-    __syncthreads();  // every wave is past its reads of xt (u_{t+1})
-#pragma unroll
-    for (int m = 0; m < MT; ++m)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int gi = 16 * m + (l >> 4) + 4 * q;
-        const double sab = (red2[0][gi] + red2[1][gi]) + (red2[2][gi] + red2[3][gi]);
-        const double isab = recip64(sab);
-        const int t = s_T[gi] - 1 - r;
-        const int o = s_ob[r & 1][gi];
+        double c = 0.0, sw = 0.0, um = 0.0, sa = 0.0;
 #pragma unroll
         for (int n = 0; n < CT; ++n) {
-          const int cc = col[n];
-          const bool on = t >= 0 && cc < N;
-          const double gm = normalized_r(al[m][n][q] * acc[m][n][q], sab, isab, N);  // hmm.rs:127-129
-          if (on) {
-            b_den[n] += gm;
-            if (r > 0) a_den[n] += gm;
-            if (t == 0) pi_acc[n] += gm;
-          }
-#ifndef CVF_ABL_NOBNUM
-          unsafeAtomicAdd(on ? &g.b_num[(size_t)o * N + cc] : dump, on ? gm : 0.0);  // hmm.rs:155-163
-#else
-          b_den[n] += on ? gm * (double)o : 0.0;
-#endif
-          // u_t = b(o_t) o beta_t, the next step's operand
-          xt[xt_at<G>(cc, gi)] = (t >= 1 && cc < N) ? g.et[(size_t)o * N + min(cc, N - 1)] * acc[m][n][q] : 0.0;
+          const double wv = col[n] < N ? acc[m][n][q] : 0.0;
+          c += al[m][n][q] * wv;
+          sw += wv;
+          sa += al[m][n][q];
+          if (r > 0) um = fmax(um, xt[xt_at<G>(col[n], gi)]);  // u_{t+1} (0 beyond N)
         }
+        c = row16_sum(c);
+        sw = row16_sum(sw);
+        um = row16_max(um);
+        sa = row16_sum(sa);
+        if (cl == 0) {
+          red[0][w][gi] = c;
+          red[1][w][gi] = sw;
+          red[2][w][gi] = um;
+          red[3][w][gi] = sa;
+        }
+      }
+    __syncthreads();
+    double gb[CT], gp[CT];  // this step's gamma sums over the lane's sequences (all; t == 0)
+#pragma unroll
+    for (int n = 0; n < CT; ++n) gb[n] = gp[n] = 0.0;
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      // b(o_t) for u_t, this tile's loads (L2 hits) issued before its stores and atomics; one
+      // M-tile at a time (sched_barrier): both at once spill at 256 states
+      __builtin_amdgcn_sched_barrier(0);
+      double ev[CT][4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const double* er = g.et + (size_t)s_ob[r & 1][16 * m + (l >> 4) + 4 * q] * N;
+#pragma unroll
+        for (int n = 0; n < CT; ++n) ev[n][q] = er[cc[n]];
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int gi = 16 * m + (l >> 4) + 4 * q;
+        const double c = wsum<WV>(&red[0][0][0], G, gi);
+        const double sw = wsum<WV>(&red[1][0][0], G, gi);
+        const double umax = wmax<WV>(&red[2][0][0], G, gi);
+        const double sa = wsum<WV>(&red[3][0][0], G, gi);
+        const int t = s_T[gi] - 1 - r;
+        const bool on = t >= 0;
+        const int tg = s_tg[r & 1][gi];
+        const int o = s_ob[r & 1][gi];
+        const double isw = recip64(sw);
+        const int ks = xi_scale(c, umax);  // balanced factors (xi_scale)
+        const double ics = recip64(__builtin_ldexp(c, ks));  // r = alpha / (c 2^k), by one reciprocal
+        // sum_i alpha_i beta_i (see above); tagged steps take gamma = one-hot directly
+        const double sab = r == 0 ? sa : sel(sw != 0.0, (c * 0x1p64) * isw, sa * inv_n);
+        const double isab = recip64(sab);
+        double* rrow = g.alpha + (size_t)(s_e0[gi] + max(t, 0)) * N;
+        double* urow = g.beta + (size_t)(s_e0[gi] + max(t, 0)) * N;
+        if (r > 0 && on && c == 0.0 && cl == 0 && w == 0) z += 1.0;  // xi_t uniform (hmm.rs:306-317)
+#pragma unroll
+        for (int n = 0; n < CT; ++n) {
+          const int k = col[n];
+          const bool onk = on && k < N;
+          double beta;
+          // rows for bw_xi_gemm; t = T - 1 (r = 0): zero rows (branch-free: dead lanes store
+          // to their dump slot)
+          double rv = 0.0, uv = 0.0;
+          if (r > 0) {  // workgroup-uniform
+            rv = sel(c != 0.0, (al[m][n][q] * 0x1p64) * ics, 0.0);
+            uv = __builtin_ldexp(xt[xt_at<G>(k, gi)], ks);  // u_{t+1} 2^k
+            beta = sel(tg >= 0, k == tg ? 1.0 : 0.0, sel(k < N, normalized_r(acc[m][n][q], sw, isw, inv_n), 0.0));
+          } else {  // t = T - 1 (hmm.rs:105-108): tagged -> one-hot, else ones
+            beta = tg >= 0 ? (k == tg ? 1.0 : 0.0) : (k < N ? 1.0 : 0.0);
+          }
+          *(onk ? rrow + k : dump) = rv;
+          *(onk ? urow + k : dump) = uv;
+          // gamma_t (hmm.rs:127-129)
+          const double gm = sel(tg >= 0, k == tg ? 1.0 : 0.0, normalized_r(al[m][n][q] * beta, sab, isab, inv_n));
+          const double gon = onk ? gm : 0.0;
+          gb[n] += gon;
+          gp[n] += t == 0 ? gon : 0.0;
+#ifndef CVF_ABL_NOBNUM
+          unsafeAtomicAdd(onk ? &g.b_num[(size_t)o * N + k] : dump, onk ? gm : 0.0);  // hmm.rs:155-163
+#else
+          gb[n] += onk ? gm * (double)o : 0.0;
+#endif
+          // u_t = b(o_t) o beta_t, the next step's operand (this lane read u_{t+1} there above)
+          xt[xt_at<G>(k, gi)] = sel(t >= 1 && k < N, ev[n][q] * beta, 0.0);
+        }
+      }
+    }
+    // the sums of gamma (hmm.rs:145-170): b_den over every step, a_den over t < T - 1 (r > 0),
+    // pi over t == 0 -- into the workgroup's LDS sums (no loop-carried registers)
+#pragma unroll
+    for (int n = 0; n < CT; ++n)
+      if (col[n] < N) {
+        atomicAdd(&s_den[2][col[n]], gb[n]);
+        if (r > 0) atomicAdd(&s_den[1][col[n]], gb[n]);
+        atomicAdd(&s_den[0][col[n]], gp[n]);
       }
     __syncthreads();  // xt = u_t complete; red and the step-r slot free
   }
-  // the gamma sums of this wave's states over the 4 lane rows; one atomic per state
-#pragma unroll
-  for (int n = 0; n < CT; ++n) {
-    double p = pi_acc[n], a = a_den[n], b = b_den[n];
-    p += __shfl_xor(p, 16);
-    a += __shfl_xor(a, 16);
-    b += __shfl_xor(b, 16);
-    p += __shfl_xor(p, 32);
-    a += __shfl_xor(a, 32);
-    b += __shfl_xor(b, 32);
-    if ((l >> 4) == 0 && col[n] < N) {
-      unsafeAtomicAdd(&g.pi_acc[col[n]], p);
-      unsafeAtomicAdd(&g.a_den[col[n]], a);
-      unsafeAtomicAdd(&g.b_den[col[n]], b);
-    }
+  // the workgroup's gamma sums: one atomic per state
+  for (int i = tid; i < N; i += 64 * WV) {
+    unsafeAtomicAdd(&g.pi_acc[i], s_den[0][i]);
+    unsafeAtomicAdd(&g.a_den[i], s_den[1][i]);
+    unsafeAtomicAdd(&g.b_den[i], s_den[2][i]);
   }
   if (w == 0) {
     z += __shfl_xor(z, 16);
@@ -1247,11 +1371,29 @@ static int bw_mt() {
   return v;
 }
 
-template <int NP, int MT>
+template <int NP, int MT, int WVF, int WVB>
 static void launch_mm(const BwArgs& g, int64_t nseq, hipStream_t stream) {
-  const dim3 grid((unsigned)((nseq + 16 * MT - 1) / (16 * MT))), block(256);
-  hipLaunchKernelGGL((bw_fwd_mm<NP, MT>), grid, block, 0, stream, g, nseq);
-  hipLaunchKernelGGL((bw_bwd_mm<NP, MT>), grid, block, 0, stream, g, nseq);
+  const dim3 grid((unsigned)((nseq + 16 * MT - 1) / (16 * MT)));
+  hipLaunchKernelGGL((bw_fwd_mm<NP, MT, WVF>), grid, dim3(64 * WVF), 0, stream, g, nseq);
+  hipLaunchKernelGGL((bw_bwd_mm<NP, MT, WVB>), grid, dim3(64 * WVB), 0, stream, g, nseq);
+}
+
+// waves per workgroup of the 64 < N <= 256 forward: 4, or with CV_BW_WV=8 eight (two 16-column
+// tiles per wave at 256 states, four waves per SIMD: 82.4 vs 79.2 ms at config 4)
+static int bw_wv() {
+  static const int v = [] {
+    const char* e = getenv("CV_BW_WV");
+    return (e && e[0] == '8') ? 8 : 4;
+  }();
+  return v;
+}
+
+static bool gemm_wave() {  // A/B knob: CV_BW_GEMM_WAVE=1 keeps one wave per 64 x 64 tile
+  static const bool v = [] {
+    const char* e = getenv("CV_BW_GEMM_WAVE");
+    return e && e[0] == '1';
+  }();
+  return v;
 }
 
 static bool gemm_st2() {  // A/B knob: CV_BW_GEMM_ST2=1 double-buffers the GEMM's loads
@@ -1284,14 +1426,20 @@ hipError_t launch_bw_estep(const BwArgs& g, int64_t nseq, int64_t max_waves, hip
   const bool mm = g.nstates > kBwWaveStates && !per_seq;
   if (g.nstates > kBwLdsStates || mm) {  // the xi sum as R^T U on the matrix cores
     if (mm) {  // 16 MT sequences per workgroup, the step products on the matrix cores
+      // waves per workgroup: forward / backward (the backward's per-step state needs the
+      // registers of four waves at 256 states)
       if (bw_mt() == 4) {
-        if (g.nstates <= 128) launch_mm<128, 4>(g, nseq, stream);
-        else if (g.nstates <= 192) launch_mm<192, 4>(g, nseq, stream);
-        else launch_mm<256, 4>(g, nseq, stream);
+        if (g.nstates <= 128) launch_mm<128, 4, 4, 4>(g, nseq, stream);
+        else if (g.nstates <= 192) launch_mm<192, 4, 4, 4>(g, nseq, stream);
+        else launch_mm<256, 4, 4, 4>(g, nseq, stream);
+      } else if (bw_wv() == 4) {
+        if (g.nstates <= 128) launch_mm<128, 2, 4, 4>(g, nseq, stream);
+        else if (g.nstates <= 192) launch_mm<192, 2, 4, 4>(g, nseq, stream);
+        else launch_mm<256, 2, 4, 4>(g, nseq, stream);
       } else {
-        if (g.nstates <= 128) launch_mm<128, 2>(g, nseq, stream);
-        else if (g.nstates <= 192) launch_mm<192, 2>(g, nseq, stream);
-        else launch_mm<256, 2>(g, nseq, stream);
+        if (g.nstates <= 128) launch_mm<128, 2, 8, 4>(g, nseq, stream);
+        else if (g.nstates <= 192) launch_mm<192, 2, 4, 4>(g, nseq, stream);  // 12 tiles: four waves
+        else launch_mm<256, 2, 8, 4>(g, nseq, stream);
       }
     } else {
       hipLaunchKernelGGL(bw_forward, dim3((unsigned)nseq), dim3(256), 0, stream, g);
@@ -1307,7 +1455,15 @@ hipError_t launch_bw_estep(const BwArgs& g, int64_t nseq, int64_t max_waves, hip
     const int64_t np = (nrows + per - 1) / per;
     // a multiple of 8 row ranges (empty ones exit): the XCD-aware block mapping of bw_xi_gemm
     const dim3 grid((unsigned)((np + 7) / 8 * 8 * ntt * ntt)), block(64);
-    if (t64 && gemm_st2())
+    if (t64 && !gemm_wave()) {
+      // 128 x 128 per workgroup: ~2 workgroups per CU over 256 CUs
+      const int nt = (g.nstates + 127) / 128;
+      const int64_t parts2 = std::max<int64_t>(1, std::min<int64_t>(512 / (nt * nt), (nrows + 255) / 256));
+      const int64_t per2 = ((nrows + parts2 - 1) / parts2 + kGemmKB - 1) / kGemmKB * kGemmKB;
+      const int64_t np2 = (nrows + per2 - 1) / per2;
+      hipLaunchKernelGGL(bw_xi_gemm_lds, dim3((unsigned)((np2 + 7) / 8 * 8 * nt * nt)), dim3(256), 0, stream, g, nrows,
+                         per2);
+    } else if (t64 && gemm_st2())
       hipLaunchKernelGGL((bw_xi_gemm<4, 2>), grid, block, 0, stream, g, nrows, per);
     else if (t64)
       hipLaunchKernelGGL((bw_xi_gemm<4, 1>), grid, block, 0, stream, g, nrows, per);
