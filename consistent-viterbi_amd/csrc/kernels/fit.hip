@@ -51,6 +51,15 @@ __device__ __forceinline__ int xi_scale(double c, double umax) {
   return -(ilogb(c) + ilogb(umax)) / 2;
 }
 
+// a select of two computed values: without the empty asm the compiler turns a per-lane `?:`
+// with arithmetic on one side into an exec-masked branch, and a branch here waits for every
+// outstanding load (vmcnt(0))
+__device__ __forceinline__ double sel(bool c, double a, double b) {
+  asm("" : "+v"(a));
+  asm("" : "+v"(b));
+  return c ? a : b;
+}
+
 __device__ __forceinline__ double block_max(double v, double* red) {
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) v = fmax(v, __shfl_xor(v, off));
@@ -385,7 +394,9 @@ __global__ __launch_bounds__(256, 2) void bw_xi_gemm_lds(BwArgs g, int64_t nrows
   const int64_t r1 = r0 + rows_per_wg < nrows ? r0 + rows_per_wg : nrows;
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, kk = l >> 4, cl = l & 15;
   const int wm = w >> 1, wn = w & 1;
-  // staging: thread tid copies rows (tid >> 4) of R and U, 8 doubles from column 8 (tid & 15)
+  // staging: thread tid copies row (tid >> 4) of R and U, 8 doubles from column 8 (tid & 15);
+  // A/B: 16-byte loads of strided column pairs with forced selects (2-way LDS write conflicts)
+  // 98 vs 79 ms, 8-byte strided loads 109 ms
   const int srow = tid >> 4, scol = 8 * (tid & 15);
   auto stage_load = [&](int64_t rb, double (&ra)[8], double (&ua)[8]) {
     const int64_t row = rb + srow;
@@ -881,14 +892,6 @@ __device__ __forceinline__ double row16_max(double v) {
 // in another order than the reference's anyway).  Both scaled by 2^64, so a subnormal s (tiny
 // emissions) still has a finite reciprocal; every v here is one of s's non-negative terms.
 __device__ __forceinline__ double recip64(double s) { return 1.0 / (s * 0x1p64); }
-// a select of two computed values: without the empty asm the compiler turns a per-lane `?:`
-// with arithmetic on one side into an exec-masked branch, and a branch here waits for every
-// outstanding load (vmcnt(0))
-__device__ __forceinline__ double sel(bool c, double a, double b) {
-  asm("" : "+v"(a));
-  asm("" : "+v"(b));
-  return c ? a : b;
-}
 // s != 0: v / s (to an ulp, by the reciprocal); s == 0: 1 / n (hmm.rs:274-282)
 __device__ __forceinline__ double normalized_r(double v, double s, double inv, double inv_n) {
   return sel(s != 0.0, (v * 0x1p64) * inv, inv_n);
