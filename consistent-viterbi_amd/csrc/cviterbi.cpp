@@ -1553,9 +1553,10 @@ cv_status constrained_partials_locked(cv_hmm* h, int64_t nseq, const int64_t* of
       // f64, one-position slots present: keep the suffix pass's rows as well, within half of
       // what the device can still give (else the resume decode covers those slots)
       if (f64 && n1 > 0 && trace_supported(h)) {
-        sbv.resize((size_t)nc);
+        // rows only for the one-position slots [0, n1) the trace reads (row base -1: none kept)
+        sbv.assign((size_t)nc, -1);
         int64_t srows = 0;
-        for (int64_t i = 0; i < nc; ++i) sbv[(size_t)i] = srows, srows += rg[2 * nc + 2 * i + 1] - rg[2 * nc + 2 * i];
+        for (int64_t i = 0; i < n1; ++i) sbv[(size_t)i] = srows, srows += rg[2 * nc + 2 * i + 1] - rg[2 * nc + 2 * i];
         bool sfits = (uint64_t)srows * row_bytes <= free_device_bytes(h->rs_srows.bytes) / 2;
         if (sfits && h->rs_srows.ensure((size_t)std::max<int64_t>(srows, 1) * row_bytes) != CV_OK) {
           sfits = false;
@@ -2140,6 +2141,13 @@ cv_status forced_decode_resume(cv_hmm* h, int64_t nseq, const int64_t* offsets_h
     ta.score = score_dev;
     ta.status = status_dev;
     ta.cert = cert_d;
+    // A/B knob CV_TRACE_AFTER_SIDE=1: the trace waits for the side decode (it then runs alone on
+    // the chip instead of beside the side decode's tail)
+    static const bool after_side = [] {
+      const char* e = getenv("CV_TRACE_AFTER_SIDE");
+      return e && *e == '1';
+    }();
+    if (after_side && constrained_only) HIP_TRY(hipStreamWaitEvent(stream, h->side.done, 0));
     const hipError_t e = cvk::launch_t64_suffix_trace(np, ta, n1, stream);
     if (e != hipSuccess) return set_err(CV_EDEVICE, "suffix trace failed: %s", hipGetErrorString(e));
     HIP_TRY(hipMemcpyAsync(cert.data(), cert_d, (size_t)n1, hipMemcpyDeviceToHost, stream));

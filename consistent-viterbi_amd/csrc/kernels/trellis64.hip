@@ -352,15 +352,16 @@ __global__ __launch_bounds__(64 * W * WG) __attribute__((amdgpu_waves_per_eu(MIN
     load_a<C>(row, e);
   };
   auto store_row = [&](int s, int t, const double (&v)[C]) {
+    const int64_t r = (int64_t)((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)my_rb, s) |
+                                ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(my_rb >> 32), s) << 32));
 #ifdef CVK_ABL_NOSTORE  // ablation build (timing only): no delta-row stores
     if (false) {
 #else
-    if (g.delta && t < T[s]) {
+    // EXT: a negative row base keeps no rows for that slot (wave-uniform)
+    if (g.delta && t < T[s] && (!EXT || r >= 0)) {
 #endif
       // split-plane row (see T64 row layout in trellis64.h): hi words [0, NP), lo words
       // [NP, 2 NP); streaming stores (read once, by the backtrack)
-      const int64_t r = (int64_t)((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)my_rb, s) |
-                                  ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(my_rb >> 32), s) << 32));
 #ifndef CVK_ABL_STORE_L2
       uint32_t* dst = reinterpret_cast<uint32_t*>(g.delta) + (r + t) * (2 * NP) + j0;
 #else  // ablation build (timing only): every step of a sequence overwrites its first row (L2-resident)

@@ -720,3 +720,56 @@ def test_constrained_ext_workgroup_units_bit_identical(gpu, tmp_path, n):
     got = np.load(tmp_path / "out.npz")
     for key, x in zip(("p", "s", "st", "states", "obj"), ref):
         assert np.array_equal(np.asarray(x), got[key]), key
+
+
+def test_one_handle_batch_and_constrained_on_two_streams(gpu):
+    """one handle, cv_decode_batch_device enqueued on stream A and, with no
+    synchronisation, cv_decode_constrained_device on stream B.  Both share the handle's
+    workspace buffers (longest-first order, zero rows, statuses); the constrained call waits on
+    its own stream for the batch call's workspace (ws_done) before writing them.  Each result
+    equals the same call run alone, bit for bit (several interleavings)."""
+    import torch
+
+    dev = torch.device("cuda", 0)
+    n = 256
+    pi, a, b = synth.random_hmm(n, 40, seed=91)
+    rng = np.random.default_rng(91)
+    # batch A: 8,192 ragged sequences (a long forward pass: the constrained call starts while it runs)
+    offa = synth.offsets_from_lengths(rng.integers(16, 96, size=8192))
+    obsa = rng.integers(0, 40, size=int(offa[-1])).astype(np.int32)
+    # constrained B: 600 sequences, 5 components
+    offb = synth.offsets_from_lengths(rng.integers(1, 60, size=600))
+    obsb = rng.integers(0, 40, size=int(offb[-1])).astype(np.int32)
+    comp = synth.constraint_components(offb, seed=92, ncomp=5, prob=0.6)
+    h = cv.HMM(pi, a, b)
+    da = [torch.from_numpy(offa).to(dev), torch.from_numpy(obsa).to(dev)]
+    db = [torch.from_numpy(offb).to(dev), torch.from_numpy(obsb).to(dev)]
+
+    def outs(off):
+        return (torch.full((int(off[-1]),), -1, dtype=torch.int32, device=dev),
+                torch.full((len(off) - 1,), 7.0, dtype=torch.float64, device=dev),
+                torch.full((len(off) - 1,), 9, dtype=torch.uint8, device=dev))
+
+    def host(t):
+        return tuple(x.cpu().numpy().copy() for x in t)
+
+    sa, sb = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    oa = outs(offa)
+    cv.decode_batch_device(h, da[0], da[1], *oa, offsets_host=offa, stream=sa.cuda_stream, dtype="f64")
+    torch.cuda.synchronize()
+    ref_a = host(oa)
+    ob = outs(offb)
+    ref_b = cv.decode_constrained_device(h, offb, db[0], db[1], comp, *ob, ncomp=5, stream=sb.cuda_stream)
+    torch.cuda.synchronize()
+    ref_bo = host(ob)
+    for rep in range(3):
+        oa, ob = outs(offa), outs(offb)
+        torch.cuda.synchronize()
+        cv.decode_batch_device(h, da[0], da[1], *oa, offsets_host=offa, stream=sa.cuda_stream, dtype="f64")
+        got_b = cv.decode_constrained_device(h, offb, db[0], db[1], comp, *ob, ncomp=5, stream=sb.cuda_stream)
+        torch.cuda.synchronize()
+        for x, y, what in zip(host(oa), ref_a, ("path", "score", "status")):
+            assert np.array_equal(x, y), (rep, "batch", what)
+        for x, y, what in zip(host(ob), ref_bo, ("path", "score", "status")):
+            assert np.array_equal(x, y), (rep, "constrained", what)
+        assert np.array_equal(got_b[0], ref_b[0]) and got_b[1] == ref_b[1], rep
