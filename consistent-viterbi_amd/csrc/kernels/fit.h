@@ -7,8 +7,9 @@
 namespace cvf {
 
 constexpr int kBwLdsStates = 128;  // bw_stats keeps a sequence's N x N xi sum in LDS up to here
-constexpr int kBwMaxStates = 256;  // one thread per state (256-thread workgroups); beyond
-                                   // kBwLdsStates the xi sum is a GEMM over stored rows
+constexpr int kBwMmStates = 256;   // up to here: the matrix-core step kernels (bw_*_mm)
+constexpr int kBwMaxStates = 4096; // beyond kBwMmStates: states strided over 256 threads, the
+                                   // step's vector and 3 gamma sums in LDS (4 N doubles)
 
 struct MleArgs {
   const int64_t* offsets;

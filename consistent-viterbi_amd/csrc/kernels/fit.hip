@@ -159,6 +159,150 @@ __global__ __launch_bounds__(256) void bw_backward(BwArgs g) {
   }
 }
 
+// ---- N > 256 (up to kBwMaxStates): the per-sequence kernels with the states strided over the
+// 256 threads (thread i owns states i, i + 256, ...), the vector operand and (stats) the owned
+// states' gamma sums in dynamic LDS; the xi sum is the GEMM over the rows, as for N <= 256.
+// One workgroup per sequence and all of A per step: a correctness path for large models (the
+// reference trains any N, hmm.rs:69-190), not a tuned one.
+__global__ __launch_bounds__(256) void bw_forward_g(BwArgs g) {
+  extern __shared__ double xs[];  // [N]
+  __shared__ double red[4];
+  const int64_t e0 = g.offsets[blockIdx.x];
+  const int T = (int)(g.offsets[blockIdx.x + 1] - e0);
+  const int N = g.nstates, tid = threadIdx.x;
+  if (T <= 0) return;
+  double* al = g.alpha + (e0 - g.elem_base) * N;
+  const int32_t* obs = g.obs + e0;
+  const int32_t* tag = g.tags + e0;
+  {  // t = 0 (hmm.rs:81-88)
+    const int tg = tag[0];
+    double part = 0.0;
+    for (int i = tid; i < N; i += 256) {
+      const double y = g.pi[i] * g.et[(size_t)obs[0] * N + i];
+      al[i] = y;
+      part += y;
+    }
+    const double s = block_sum(part, red);
+    for (int i = tid; i < N; i += 256) al[i] = tg >= 0 ? (i == tg ? 1.0 : 0.0) : normalized(al[i], s, N);
+  }
+  for (int t = 1; t < T; ++t) {
+    const int tg = tag[t];  // uniform
+    double* row = al + (size_t)t * N;
+    if (tg >= 0) {  // hmm.rs:91
+      for (int i = tid; i < N; i += 256) row[i] = (i == tg) ? 1.0 : 0.0;
+      continue;
+    }
+    __syncthreads();  // xs free
+    for (int i = tid; i < N; i += 256) xs[i] = row[i - N] * g.et[(size_t)obs[t] * N + i];
+    __syncthreads();
+    double part = 0.0;
+    for (int i = tid; i < N; i += 256) {  // (alpha[t-1] * b(o_t)) . A  -- hmm.rs:93-94
+      double y = 0.0;
+      for (int k = 0; k < N; ++k) y += xs[k] * g.a[(size_t)k * N + i];
+      row[i] = y;
+      part += y;
+    }
+    const double s = block_sum(part, red);
+    for (int i = tid; i < N; i += 256) row[i] = normalized(row[i], s, N);
+  }
+}
+
+__global__ __launch_bounds__(256) void bw_backward_g(BwArgs g) {
+  extern __shared__ double xs[];  // [N]
+  __shared__ double red[4];
+  const int64_t e0 = g.offsets[blockIdx.x];
+  const int T = (int)(g.offsets[blockIdx.x + 1] - e0);
+  const int N = g.nstates, tid = threadIdx.x;
+  if (T <= 0) return;
+  double* be = g.beta + (e0 - g.elem_base) * N;
+  const int32_t* obs = g.obs + e0;
+  const int32_t* tag = g.tags + e0;
+  {  // t = T-1 (hmm.rs:105-108)
+    const int tg = tag[T - 1];
+    for (int i = tid; i < N; i += 256) be[(size_t)(T - 1) * N + i] = tg >= 0 ? (i == tg ? 1.0 : 0.0) : 1.0;
+  }
+  for (int t = T - 2; t >= 0; --t) {
+    const int tg = tag[t];
+    double* row = be + (size_t)t * N;
+    if (tg >= 0) {
+      for (int i = tid; i < N; i += 256) row[i] = (i == tg) ? 1.0 : 0.0;
+      continue;
+    }
+    __syncthreads();
+    for (int i = tid; i < N; i += 256) xs[i] = row[i + N] * g.et[(size_t)obs[t + 1] * N + i];
+    __syncthreads();
+    double part = 0.0;
+    for (int i = tid; i < N; i += 256) {  // (beta[t+1] * b(o_{t+1})) . A^T  -- hmm.rs:113-116
+      double y = 0.0;
+      for (int k = 0; k < N; ++k) y += xs[k] * g.at[(size_t)k * N + i];
+      row[i] = y;
+      part += y;
+    }
+    const double s = block_sum(part, red);
+    for (int i = tid; i < N; i += 256) row[i] = normalized(row[i], s, N);
+  }
+}
+
+// gamma and xi of one sequence (as bw_stats_rows): r_t over alpha's row t, u_{t+1} 2^k over
+// beta's row t, zeros at the last step; the gamma sums of the owned states in LDS
+__global__ __launch_bounds__(256) void bw_stats_rows_g(BwArgs g) {
+  extern __shared__ double sm[];  // ps[N] | pi_acc[N] | a_den[N] | b_den[N]
+  __shared__ double red[4];
+  const int64_t e0 = g.offsets[blockIdx.x];
+  const int T = (int)(g.offsets[blockIdx.x + 1] - e0);
+  const int N = g.nstates, tid = threadIdx.x;
+  if (T <= 0) return;
+  double *ps = sm, *sp = sm + N, *sa = sm + 2 * N, *sb = sm + 3 * N;
+  for (int i = tid; i < N; i += 256) sp[i] = sa[i] = sb[i] = 0.0;
+  double* al = g.alpha + (e0 - g.elem_base) * N;
+  double* be = g.beta + (e0 - g.elem_base) * N;
+  const int32_t* obs = g.obs + e0;
+  double z = 0.0;
+  for (int t = 0; t < T; ++t) {
+    double* ar = al + (size_t)t * N;
+    double* br = be + (size_t)t * N;
+    double part = 0.0;
+    for (int i = tid; i < N; i += 256) part += ar[i] * br[i];
+    const double s = block_sum(part, red);
+    for (int i = tid; i < N; i += 256) {  // gamma_t (hmm.rs:127-129) into the sums
+      const double gm = normalized(ar[i] * br[i], s, N);
+      if (t == 0) sp[i] += gm;
+      if (t < T - 1) sa[i] += gm;
+      sb[i] += gm;
+      unsafeAtomicAdd(&g.b_num[(size_t)obs[t] * N + i], gm);  // hmm.rs:155-163
+    }
+    if (t + 1 < T) {
+      __syncthreads();  // ps free
+      for (int i = tid; i < N; i += 256) ps[i] = g.et[(size_t)obs[t + 1] * N + i] * br[i + N];
+      __syncthreads();
+      double pc = 0.0, pu = 0.0;
+      for (int i = tid; i < N; i += 256) {  // w_i = sum_j A[i][j] u_j; c = alpha_t . w
+        double w = 0.0;
+        for (int j = 0; j < N; ++j) w += g.at[(size_t)j * N + i] * ps[j];
+        pc += ar[i] * w;
+        pu = fmax(pu, ps[i]);
+      }
+      const double c = block_sum(pc, red);
+      const int ks = xi_scale(c, block_max(pu, red));  // balanced factors
+      for (int i = tid; i < N; i += 256) {
+        const double r = c != 0.0 ? ar[i] / __builtin_ldexp(c, ks) : 0.0;
+        const double u = __builtin_ldexp(ps[i], ks);
+        ar[i] = r;
+        br[i] = u;
+      }
+      if (tid == 0 && c == 0.0) z += 1.0;  // xi_t uniform (hmm.rs:306-317)
+    } else {
+      for (int i = tid; i < N; i += 256) ar[i] = br[i] = 0.0;
+    }
+  }
+  for (int i = tid; i < N; i += 256) {
+    unsafeAtomicAdd(&g.pi_acc[i], sp[i]);
+    unsafeAtomicAdd(&g.a_den[i], sa[i]);
+    unsafeAtomicAdd(&g.b_den[i], sb[i]);
+  }
+  if (tid == 0 && z != 0.0) unsafeAtomicAdd(g.xi_zero, z);
+}
+
 // E-step sums of one sequence.  xi_t = normalize(A o (alpha_t (x) u_{t+1})), u = b(o_{t+1}) o
 // beta_{t+1} (hmm.rs:135-141); its sum c_t = alpha_t . (A u_{t+1}), so sum_t xi_t =
 // A o S + z / N^2 with S = sum over c_t != 0 of (alpha_t / c_t) (x) u_{t+1} and z = #{c_t == 0}
@@ -1430,6 +1574,24 @@ static bool gemm32() {  // A/B knob: CV_BW_GEMM32=1 keeps 32 x 32 tiles at every
 hipError_t launch_bw_estep(const BwArgs& g, int64_t nseq, int64_t max_waves, hipStream_t stream, int64_t nrows) {
   if (nseq <= 0) return hipSuccess;
   if (g.nstates > kBwMaxStates) return hipErrorInvalidValue;
+  if (g.nstates > kBwMmStates) {  // 256 < N <= kBwMaxStates: the strided per-sequence kernels
+    const size_t l1 = (size_t)g.nstates * 8, l4 = 4 * l1;
+    for (const void* k : {reinterpret_cast<const void*>(&bw_forward_g), reinterpret_cast<const void*>(&bw_backward_g)})
+      if (l1 > 64 * 1024) (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)l1);
+    if (l4 > 64 * 1024)
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&bw_stats_rows_g), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)l4);
+    hipLaunchKernelGGL(bw_forward_g, dim3((unsigned)nseq), dim3(256), l1, stream, g);
+    hipLaunchKernelGGL(bw_backward_g, dim3((unsigned)nseq), dim3(256), l1, stream, g);
+    hipLaunchKernelGGL(bw_stats_rows_g, dim3((unsigned)nseq), dim3(256), l4, stream, g);
+    const int nt = (g.nstates + 127) / 128;
+    const int64_t parts2 = std::max<int64_t>(1, std::min<int64_t>(512 / (nt * nt), (nrows + 255) / 256));
+    const int64_t per2 = ((nrows + parts2 - 1) / parts2 + kGemmKB - 1) / kGemmKB * kGemmKB;
+    const int64_t np2 = (nrows + per2 - 1) / per2;
+    hipLaunchKernelGGL(bw_xi_gemm_lds, dim3((unsigned)((np2 + 7) / 8 * 8 * nt * nt)), dim3(256), 0, stream, g, nrows,
+                       per2);
+    return hipGetLastError();
+  }
   static const bool per_seq = [] {  // A/B knob: CV_BW_PERSEQ=1 keeps one workgroup per sequence
     const char* e = getenv("CV_BW_PERSEQ");
     return e && e[0] == '1';

@@ -124,12 +124,14 @@ def test_gpu_train_matches_oracle(gpu, n, v, frac, tmax):
 
 
 @pytest.mark.gpu
-# 64 < N <= 256 runs 64 sequences per workgroup (bw_fwd_mm / bw_bwd_mm): several workgroups,
+# 64 < N <= 256 runs 32 sequences per workgroup (bw_fwd_mm / bw_bwd_mm): several workgroups,
 # ragged lengths inside each (longest first), one-element sequences, tagged first/last
-# elements, fully tagged sequences and a padded state count per kernel width (128/192/256)
+# elements, fully tagged sequences and a padded state count per kernel width (128/192/256);
+# N > 256: the strided per-sequence kernels (2 and 3 states per thread)
 @pytest.mark.parametrize("n,nseq,tmax,frac", [(65, 150, 40, 0.2), (100, 200, 60, 0.3), (128, 130, 33, 0.0),
                                               (150, 97, 50, 0.5), (192, 70, 45, 0.1), (255, 140, 30, 0.2),
-                                              (256, 260, 40, 0.15)])
+                                              (256, 260, 40, 0.15), (257, 40, 20, 0.2), (300, 50, 25, 0.1),
+                                              (520, 24, 16, 0.3)])
 def test_gpu_train_groups_match_oracle(gpu, n, nseq, tmax, frac):
     import cviterbi as cv
 
@@ -155,7 +157,7 @@ def test_gpu_train_groups_match_oracle(gpu, n, nseq, tmax, frac):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n", [20, 100, 200])  # wave kernels, LDS xi sum, GEMM xi sum
+@pytest.mark.parametrize("n", [20, 100, 200, 300])  # wave, matrix-core and strided kernels
 def test_gpu_train_subnormal_xi_denominator(gpu, n):
     """Emission probabilities below DBL_MIN for one observation make xi's normaliser c_t
     subnormal: the reference normalises xi entry by entry (hmm.rs:135-141) and stays finite;
@@ -195,9 +197,9 @@ def test_gpu_train_converges_like_oracle(gpu):
 def test_gpu_fit_limits(gpu):
     import cviterbi as cv
 
-    off, obs, tags = _corpus(257, 4, 3, 5, 0.5, seed=1)
-    pi0, a0, b0 = _probs(257, 4, seed=1)
-    with pytest.raises(cv.CVError):  # Baum-Welch covers N <= 256 (one thread per state)
+    off, obs, tags = _corpus(4097, 4, 3, 5, 0.5, seed=1)
+    pi0, a0, b0 = _probs(4097, 4, seed=1)
+    with pytest.raises(cv.CVError):  # Baum-Welch covers N <= 4096 (4 N doubles of LDS per sequence)
         cv.fit_train(pi0, a0, b0, off, obs, tags, max_iter=1)
     with pytest.raises(cv.CVError):  # MLE needs every element tagged
         cv.fit_mle(pi0, a0, b0, off, obs, tags)
