@@ -1065,7 +1065,12 @@ __device__ __forceinline__ double wmax(const double* red, int G, int gi) {
 template <int NP, int MT, int WV, class Pre>
 __device__ __forceinline__ void mm_step(const double* __restrict__ xt, const double* __restrict__ M, int N, int w,
                                         int l, f64x4_t (&acc)[MT][NP / (16 * WV)], Pre&& pre) {
-  constexpr int CT = NP / (16 * WV), NK = NP / 4, PF = 4, G = 16 * MT;
+#ifndef CVF_MM_PF
+  constexpr int PF = 4;
+#else
+  constexpr int PF = CVF_MM_PF;
+#endif
+  constexpr int CT = NP / (16 * WV), NK = NP / 4, G = 16 * MT;
   const int cl = l & 15, kq = l >> 4;
   int col[CT];
 #pragma unroll
@@ -1075,6 +1080,11 @@ __device__ __forceinline__ void mm_step(const double* __restrict__ xt, const dou
 #pragma unroll
     for (int n = 0; n < CT; ++n) acc[m][n] = f64x4_t{0.0, 0.0, 0.0, 0.0};
   // A rows PF k-blocks ahead (L2), the LDS operand one k-block ahead
+  // the products at a higher issue priority than the other workgroup's phase-E VALU work on
+  // the SIMD (A/B: forward 77.8 vs 79.1 ms, backward 110.0 vs 110.8 ms at config-4 shape)
+#ifndef CVF_MM_NOPRIO
+  __builtin_amdgcn_s_setprio(2);
+#endif
   double ring[PF][CT];
 #define CVF_MM_LOAD(KK, DST)                                                  \
   {                                                                           \
@@ -1109,6 +1119,9 @@ __device__ __forceinline__ void mm_step(const double* __restrict__ xt, const dou
       for (int m = 0; m < MT; ++m) av[m] = an[m];
     }
   }
+#ifndef CVF_MM_NOPRIO
+  __builtin_amdgcn_s_setprio(0);
+#endif
 #undef CVF_MM_LOAD
 }
 
