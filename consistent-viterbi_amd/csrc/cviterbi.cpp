@@ -2061,7 +2061,8 @@ struct SideJoin {
   }
 };
 
-// The side-decode streams (lowest / highest priority; equal priorities if CV_SIDE_PRIO=0).
+// The side-decode streams (lowest / highest priority; equal priorities if CV_SIDE_PRIO=0,
+// swapped if CV_SIDE_PRIO=2).
 cv_status side_streams(cv_hmm* h) {
   auto& sd = h->side;
   if (!sd.stream) {
@@ -2072,6 +2073,7 @@ cv_status side_streams(cv_hmm* h) {
     }
     const char* e = getenv("CV_SIDE_PRIO");
     if (e && *e == '0') greatest = least;
+    if (e && *e == '2') std::swap(least, greatest);  // A/B: the side decode first, the terms pass in its gaps
     if (hipStreamCreateWithPriority(&sd.stream, hipStreamNonBlocking, least) != hipSuccess ||
         hipStreamCreateWithPriority(&sd.hi, hipStreamNonBlocking, greatest) != hipSuccess)
       return set_err(CV_EDEVICE, "hipStreamCreateWithPriority failed");
