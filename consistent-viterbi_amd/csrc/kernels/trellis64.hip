@@ -1365,8 +1365,13 @@ __global__ __launch_bounds__(256) void prefix_backtrack_f64(PrefixBt64Args a, in
 // tie or a larger value there would make some Q reach F(P)), and its score is F(P), the fold
 // computed here in the forward order -- bit-identical.  A failed step (near tie, -inf, no
 // state) leaves the slot to the fallback forced decode: cert = 0.
+// CVK_TRACE_WAVES: minimum waves per SIMD the register budget must allow (A/B: 8 = at most 64
+// VGPRs, so a trace wave fits beside the two 224-VGPR waves of a forward workgroup)
+#ifndef CVK_TRACE_WAVES
+#define CVK_TRACE_WAVES 1
+#endif
 template <int KP>
-__global__ __launch_bounds__(256) void suffix_trace_f64(SuffixTrace64Args g, int64_t n) {
+__global__ __launch_bounds__(256, CVK_TRACE_WAVES) void suffix_trace_f64(SuffixTrace64Args g, int64_t n) {
   constexpr int NP = 64 * KP;
   constexpr uint32_t NINF_HI = 0xFFF00000u;
   const int lane = threadIdx.x & 63;
