@@ -3663,7 +3663,7 @@ cv_status fit_validate(int32_t N, int64_t V, int64_t nseq, const int64_t* offset
 }
 
 struct FitDev {
-  DevBuf off, obs, tags, pi, a, at, et, alpha, beta, acc, cnt, ord, dump;
+  DevBuf off, obs, tags, pi, a, at, et, alpha, beta, rscale, acc, cnt, ord, dump;
 };
 
 }  // namespace
@@ -3786,6 +3786,8 @@ CV_API cv_status cv_hmm_fit_train(int32_t nstates, int64_t nobs, int64_t nseq, c
   if ((st = d.alpha.ensure((size_t)max_chunk * N * 8)) != CV_OK) return st;
   // beta rows only for the workgroup kernels (N > 64); the one-wave backward never stores beta
   if (N > cvf::kBwWaveStates && (st = d.beta.ensure((size_t)max_chunk * N * 8)) != CV_OK) return st;
+  if (N > cvf::kBwWaveStates && N <= cvf::kBwMmStates && (st = d.rscale.ensure((size_t)max_chunk * 8)) != CV_OK)
+    return st;
   const size_t nacc = 3 * (size_t)N + (size_t)V * N + (size_t)N * N + 1;
   constexpr int kPartsB = 1024;  // blocks of the b M-step = partial convergence sums
   if ((st = d.acc.ensure(nacc * 8)) != CV_OK) return st;
@@ -3854,6 +3856,7 @@ CV_API cv_status cv_hmm_fit_train(int32_t nstates, int64_t nobs, int64_t nseq, c
       g.et = d.et.as<double>();
       g.alpha = d.alpha.as<double>();
       g.beta = d.beta.as<double>();
+      g.rscale = d.rscale.p ? d.rscale.as<double>() : nullptr;  // null: R stored over alpha
       g.pi_acc = A;
       g.a_den = A + N;
       g.b_den = A + 2 * N;

@@ -37,6 +37,8 @@ struct BwArgs {
   const double* et;     // [V][N] emissions transposed
   double* alpha;        // [elements][N] workspace
   double* beta;         // [elements][N] workspace
+  double* rscale;       // [elements] N > 64 matrix-core path: row t of R = alpha_t * rscale[t]
+                        // (1 / (c_t 2^k), 0 where c_t = 0 or t = T - 1); null: R is stored over alpha
   double* dump;         // [kBwDumpWaves][64] N <= 64 kernels: target of the stores / atomic adds
                         // of lanes without a state (one row per wave: no shared hot line)
   // E-step sums (accumulated across sequences; zeroed by the host per iteration)

@@ -485,8 +485,9 @@ __global__ __launch_bounds__(64, 2) void bw_xi_gemm(BwArgs g, int64_t nrows, int
     const bool vr_ = row_ < r1;                                              \
     const double* R_ = g.alpha + (size_t)(vr_ ? row_ : r0) * N;              \
     const double* U_ = g.beta + (size_t)(vr_ ? row_ : r0) * N;               \
+    const double rs_ = g.rscale ? g.rscale[vr_ ? row_ : r0] : 1.0;           \
     _Pragma("unroll") for (int q = 0; q < TM; ++q) {                         \
-      AV[q] = (vr_ && vm[q]) ? R_[cm[q]] : 0.0;                              \
+      AV[q] = (vr_ && vm[q]) ? R_[cm[q]] * rs_ : 0.0;                        \
       BV[q] = (vr_ && vn[q]) ? U_[cn[q]] : 0.0;                              \
     }                                                                        \
   }
@@ -542,11 +543,13 @@ __global__ __launch_bounds__(256, 2) void bw_xi_gemm_lds(BwArgs g, int64_t nrows
   // A/B: 16-byte loads of strided column pairs with forced selects (2-way LDS write conflicts)
   // 98 vs 79 ms, 8-byte strided loads 109 ms
   const int srow = tid >> 4, scol = 8 * (tid & 15);
+  double rsc = 1.0;  // the staged row's R scale
   auto stage_load = [&](int64_t rb, double (&ra)[8], double (&ua)[8]) {
     const int64_t row = rb + srow;
     const bool vr = row < r1;
     const double* R = g.alpha + (size_t)(vr ? row : r0) * N;
     const double* U = g.beta + (size_t)(vr ? row : r0) * N;
+    rsc = g.rscale ? g.rscale[vr ? row : r0] : 1.0;  // R = alpha rscale (bw_bwd_mm), applied at the LDS write
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
       const int cm = m0 + scol + q, cn = n0 + scol + q;
@@ -557,7 +560,7 @@ __global__ __launch_bounds__(256, 2) void bw_xi_gemm_lds(BwArgs g, int64_t nrows
   auto stage_store = [&](int buf, const double (&ra)[8], const double (&ua)[8]) {
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
-      rs[buf][srow * LS + scol + q] = ra[q];
+      rs[buf][srow * LS + scol + q] = ra[q] * rsc;
       us[buf][srow * LS + scol + q] = ua[q];
     }
   };
@@ -1391,9 +1394,11 @@ __global__ __launch_bounds__(64 * WV, (MT == 4 ? 1 : 2) * WV / 4) void bw_bwd_mm
         // sum_i alpha_i beta_i (see above); tagged steps take gamma = one-hot directly
         const double sab = r == 0 ? sa : sel(sw != 0.0, (c * 0x1p64) * isw, sa * inv_n);
         const double isab = recip64(sab);
-        double* rrow = g.alpha + (size_t)(s_e0[gi] + max(t, 0)) * N;
         double* urow = g.beta + (size_t)(s_e0[gi] + max(t, 0)) * N;
         if (r > 0 && on && c == 0.0 && cl == 0 && w == 0) z += 1.0;  // xi_t uniform (hmm.rs:306-317)
+        // R's row t is alpha_t (left in place) times this scalar: 2^64 ics = 1 / (c 2^k), 0 where
+        // c = 0 or at t = T - 1 -- the same product (alpha 2^64) ics the GEMM used to read
+        if (on && cl == 0 && w == 0) g.rscale[s_e0[gi] + t] = (r > 0 && c != 0.0) ? ics * 0x1p64 : 0.0;
 #pragma unroll
         for (int n = 0; n < CT; ++n) {
           const int k = col[n];
@@ -1401,19 +1406,17 @@ __global__ __launch_bounds__(64 * WV, (MT == 4 ? 1 : 2) * WV / 4) void bw_bwd_mm
           double beta;
           // rows for bw_xi_gemm; t = T - 1 (r = 0): zero rows (branch-free: dead lanes store
           // to their dump slot)
-          double rv = 0.0, uv = 0.0;
+          double uv = 0.0;
           if (r > 0) {  // workgroup-uniform
-            rv = sel(c != 0.0, (al[m][n][q] * 0x1p64) * ics, 0.0);
             uv = __builtin_ldexp(xt[xt_at<G>(k, gi)], ks);  // u_{t+1} 2^k
             beta = sel(tg >= 0, k == tg ? 1.0 : 0.0, sel(k < N, normalized_r(acc[m][n][q], sw, isw, inv_n), 0.0));
           } else {  // t = T - 1 (hmm.rs:105-108): tagged -> one-hot, else ones
             beta = tg >= 0 ? (k == tg ? 1.0 : 0.0) : (k < N ? 1.0 : 0.0);
           }
 #ifndef CVF_ABL_NOROWS
-          *(onk ? rrow + k : dump) = rv;
           *(onk ? urow + k : dump) = uv;
 #else
-          gb[n] += rv * 1e-300 + uv * 1e-300;
+          gb[n] += uv * 1e-300;
 #endif
           // gamma_t (hmm.rs:127-129)
           const double gm = sel(tg >= 0, k == tg ? 1.0 : 0.0, normalized_r(al[m][n][q] * beta, sab, isab, inv_n));
@@ -1611,6 +1614,8 @@ hipError_t launch_bw_estep(const BwArgs& g, int64_t nseq, int64_t max_waves, hip
   }();
   const bool mm = g.nstates > kBwWaveStates && !per_seq;
   if (g.nstates > kBwLdsStates || mm) {  // the xi sum as R^T U on the matrix cores
+    BwArgs gg = g;
+    if (!mm) gg.rscale = nullptr;  // the per-sequence kernels store R over alpha
     if (mm) {  // 16 MT sequences per workgroup, the step products on the matrix cores
       // waves per workgroup: forward / backward (the backward's per-step state needs the
       // registers of four waves at 256 states)
@@ -1647,14 +1652,14 @@ hipError_t launch_bw_estep(const BwArgs& g, int64_t nseq, int64_t max_waves, hip
       const int64_t parts2 = std::max<int64_t>(1, std::min<int64_t>(512 / (nt * nt), (nrows + 255) / 256));
       const int64_t per2 = ((nrows + parts2 - 1) / parts2 + kGemmKB - 1) / kGemmKB * kGemmKB;
       const int64_t np2 = (nrows + per2 - 1) / per2;
-      hipLaunchKernelGGL(bw_xi_gemm_lds, dim3((unsigned)((np2 + 7) / 8 * 8 * nt * nt)), dim3(256), 0, stream, g, nrows,
+      hipLaunchKernelGGL(bw_xi_gemm_lds, dim3((unsigned)((np2 + 7) / 8 * 8 * nt * nt)), dim3(256), 0, stream, gg, nrows,
                          per2);
     } else if (t64 && gemm_st2())
-      hipLaunchKernelGGL((bw_xi_gemm<4, 2>), grid, block, 0, stream, g, nrows, per);
+      hipLaunchKernelGGL((bw_xi_gemm<4, 2>), grid, block, 0, stream, gg, nrows, per);
     else if (t64)
-      hipLaunchKernelGGL((bw_xi_gemm<4, 1>), grid, block, 0, stream, g, nrows, per);
+      hipLaunchKernelGGL((bw_xi_gemm<4, 1>), grid, block, 0, stream, gg, nrows, per);
     else
-      hipLaunchKernelGGL((bw_xi_gemm<2, 1>), grid, block, 0, stream, g, nrows, per);
+      hipLaunchKernelGGL((bw_xi_gemm<2, 1>), grid, block, 0, stream, gg, nrows, per);
     return hipGetLastError();
   }
   if (g.nstates <= kBwWaveStates) {
