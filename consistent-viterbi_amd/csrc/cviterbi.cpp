@@ -206,7 +206,7 @@ struct cv_hmm {
     hipEvent_t start = nullptr, done = nullptr, after = nullptr;
   } side;
   DevBuf st_off, st_obs, st_path, st_score, st_status, st_forced;
-  DevBuf cs_ranges, cs_delta, cs_g, cs_mu, cs_start, cs_zero;  // constrained-decode scratch
+  DevBuf cs_ranges, cs_delta, cs_g, cs_mu, cs_start, cs_zero, cs_queue;  // constrained-decode scratch
   DevBuf cs_comp, cs_words;  // device exact unary sums: per-sequence components, output words
   DevBuf cs_flag;            // device exact sums: out-of-range term flag
   DevBuf cs_seg;             // segment-table rows (cs_delta keeps the prefix rows t_1)
@@ -1652,6 +1652,10 @@ cv_status constrained_partials_locked(cv_hmm* h, int64_t nseq, const int64_t* of
     fa.delta = static_cast<double*>(rows_d);
     fa.row_base = row_base_d;
     fa.slot_order = h->ws_order.as<int32_t>();
+    // the ragged passes take their units from a work queue (one counter, reset before each
+    // launch on this stream)
+    if ((st = h->cs_queue.ensure(16)) != CV_OK) return st;
+    fa.queue = h->cs_queue.as<int>();
     // prefix / suffix passes: longest-first ranges; with CV_T64_WG_TERMS=1 and at least two
     // rounds of eight-wave workgroups, that layout
     fa.wg_ok = (terms_wg() && nc >= 2 * 64 * (int64_t)std::max(h->cus, 1)) ? 1 : 0;
@@ -2074,8 +2078,18 @@ cv_status side_streams(cv_hmm* h) {
     const char* e = getenv("CV_SIDE_PRIO");
     if (e && *e == '0') greatest = least;
     if (e && *e == '2') std::swap(least, greatest);  // A/B: the side decode first, the terms pass in its gaps
-    if (hipStreamCreateWithPriority(&sd.stream, hipStreamNonBlocking, least) != hipSuccess ||
-        hipStreamCreateWithPriority(&sd.hi, hipStreamNonBlocking, greatest) != hipSuccess)
+    // A/B knob CV_SIDE_CUMASK=p (1..7): the side stream on the CUs i with i % 8 < p, the
+    // constrained stream on the others (disjoint halves instead of shared CUs)
+    const char* cm = getenv("CV_SIDE_CUMASK");
+    const int p = cm ? atoi(cm) : 0;
+    if (p >= 1 && p <= 7 && h->cus > 0) {
+      std::vector<uint32_t> ms((size_t)(h->cus + 31) / 32, 0u), mh(ms.size(), 0u);
+      for (int i = 0; i < h->cus; ++i) ((i % 8) < p ? ms : mh)[(size_t)i / 32] |= 1u << (i % 32);
+      if (hipExtStreamCreateWithCUMask(&sd.stream, (uint32_t)ms.size(), ms.data()) != hipSuccess ||
+          hipExtStreamCreateWithCUMask(&sd.hi, (uint32_t)mh.size(), mh.data()) != hipSuccess)
+        return set_err(CV_EDEVICE, "hipExtStreamCreateWithCUMask failed");
+    } else if (hipStreamCreateWithPriority(&sd.stream, hipStreamNonBlocking, least) != hipSuccess ||
+               hipStreamCreateWithPriority(&sd.hi, hipStreamNonBlocking, greatest) != hipSuccess)
       return set_err(CV_EDEVICE, "hipStreamCreateWithPriority failed");
   }
   if (!sd.start && hipEventCreateWithFlags(&sd.start, hipEventDisableTiming) != hipSuccess)

@@ -37,6 +37,7 @@ struct T64FwdArgs {
   int reverse;                 // 1: traverse each range from end-1 down to begin (suffix pass on a^T)
   const int32_t* start;        // [slot - seq_begin] s >= 0: row 0 = 0 at state s, -inf elsewhere
   const int64_t* row_base;     // [slot] delta row index of the range's first element (< 0: no rows kept)
+  int* queue;                  // EXT one-wave passes: work-queue counter (null: one workgroup per unit)
   const double* resume_rows;   // [r][NP] already-forced rows (resume flow)
   const int32_t* slot_order;   // [launch index] -> slot (longest first)
   // 1: a range's LAST step adds no emission, so the suffix pass extended to the constrained

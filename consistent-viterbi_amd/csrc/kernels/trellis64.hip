@@ -25,6 +25,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
 #include <cstdlib>
 
 #include "trellis.h"
@@ -195,7 +196,7 @@ __device__ uint64_t g_t64_probe[1 << 17][6];
 // access 0.44 -> 0.09 at config 4; profiles/r03_ab_wg.txt).  W > 1 units meet at workgroup
 // barriers anyway (their pair rendezvous), so they take bit 2 only.
 template <int C, int S, int PF, bool DPA, bool EXT, int W = 1, bool CAP2 = (W > 1), int GRP = 2, int MINW = 1,
-          bool LDSFIRST = true, int WG = 1, int SYNC = 0, bool DEFST = false>
+          bool LDSFIRST = true, int WG = 1, int SYNC = 0, bool DEFST = false, bool PERSIST = false>
 __global__ __launch_bounds__(64 * W * WG) __attribute__((amdgpu_waves_per_eu(MINW))) void trellis_fwd_f64(T64FwdArgs g) {
 #ifdef CV_T64_PROBE
   const uint64_t pr_rt0 = __builtin_amdgcn_s_memrealtime(), pr_c0 = __builtin_amdgcn_s_memtime();
@@ -256,12 +257,15 @@ __global__ __launch_bounds__(64 * W * WG) __attribute__((amdgpu_waves_per_eu(MIN
   // on some SIMDs and one on others takes 1.5x as long)
   if constexpr (CAP2) asm volatile("" ::: "v180");
 
+  static_assert(!PERSIST || (W == 1 && WG == 1 && EXT), "work queue: one-wave EXT units");
+  // one unit = S consecutive slots; PERSIST: the wave runs units taken from a queue (below)
+  auto run_unit = [&](const int64_t unit) {
   // Per-sequence bookkeeping lives in LANE s of a few VGPRs (lanes >= S idle) rather than in
   // S-element scalar arrays (those exceed the 102 SGPRs at S = 8 and spill): each step lane s
   // loads the observation (and forced state) of sequence s one step ahead, and the values a
   // step needs uniformly are read back with v_readlane.
   const int ls = lane < S ? lane : S - 1;
-  const int64_t my_k = ((int64_t)blockIdx.x * WG + wgi) * S + ls;
+  const int64_t my_k = (unit * WG + wgi) * S + ls;
   int my_T = 0;
   int64_t my_seq = -1, my_eb = 0, my_rb = 0;
   if (my_k < g.nslots && lane < S) {
@@ -635,6 +639,22 @@ __global__ __launch_bounds__(64 * W * WG) __attribute__((amdgpu_waves_per_eu(MIN
       for (int k = 0; k < kStepBarriers; ++k) asm volatile("s_barrier" ::: "memory");
   sb.finish(lane);
   if (wv == 0 && lane < S && my_bad) g.status[my_seq] = CVK_SEQ_BADOBS;
+  };
+  if constexpr (PERSIST) {
+    // work queue over the longest-first units: a wave takes the next unit when it finishes one,
+    // so the ragged passes end together instead of on the dispatch order's starved waves
+    // (oldest-first issue lets the first wave of a SIMD run ahead of its partner).  One
+    // lane's vector atomic, read back uniform; every wave exits once the units are taken.
+    for (;;) {
+      int u = 0;
+      if (lane == 0) u = atomicAdd(g.queue, 1);
+      u = __builtin_amdgcn_readfirstlane(u);
+      if ((int64_t)u * S >= g.nslots) break;
+      run_unit(u);
+    }
+  } else {
+    run_unit((int64_t)blockIdx.x);
+  }
 }
 
 // trellis_fwd_f64_rs<PF> -- the small-batch layout with a ROW split (round 3, N = 256): a PAIR
@@ -1543,6 +1563,30 @@ hipError_t fwd_w2(const T64FwdArgs& fa, int64_t nseq, bool ext, hipStream_t stre
   return hipGetLastError();
 }
 
+// A/B knob CV_T64_PERSIST=1: the constrained passes from a work queue (persistent waves) instead
+// of one workgroup per unit.  Rejected: config 5 160.5 vs 154.9 ms (profiles/r04_ab_c5_persist.txt)
+// -- 4,096 units over 2,048 waves is two units a wave, so the queue cannot even out the ragged tail
+bool persist_ext() {
+  static const bool on = [] {
+    const char* e = getenv("CV_T64_PERSIST");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+
+// compute units of the current device (queried once)
+int device_cus() {
+  static const int n = [] {
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) {
+      (void)hipGetLastError();
+      cus = 256;
+    }
+    return cus > 0 ? cus : 256;
+  }();
+  return n;
+}
+
 template <int C, int S>
 hipError_t fwd_cs(const T64FwdArgs& fa, int64_t nseq, hipStream_t stream) {
   const int64_t blocks = (nseq + S - 1) / S;
@@ -1622,6 +1666,14 @@ hipError_t fwd_cs(const T64FwdArgs& fa, int64_t nseq, hipStream_t stream) {
       hipLaunchKernelGGL((trellis_fwd_f64<C, S, 8, true, false>), grid, block, 0, stream, fa);
     else
       return hipErrorInvalidValue;
+  } else if (ext && fa.queue && persist_ext()) {
+    // the ragged constrained passes from a work queue: two waves per SIMD, each taking units
+    const int64_t units = (nseq + S - 1) / S;
+    const int64_t waves = std::min<int64_t>(units, 2 * 4 * (int64_t)device_cus());
+    hipError_t e = hipMemsetAsync(fa.queue, 0, sizeof(int), stream);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((trellis_fwd_f64<C, S, 8, false, true, 1, false, 2, 1, true, 1, 0, false, true>),
+                       dim3((unsigned)waves), block, 0, stream, fa);
   } else if (ext) {
     hipLaunchKernelGGL((trellis_fwd_f64<C, S, 8, false, true>), grid, block, 0, stream, fa);
   } else if (pf == 4) {
@@ -1877,8 +1929,12 @@ hipError_t launch_t64_fwd(int np, int s, const T64FwdArgs& fa_in, int64_t nseq, 
   T64FwdArgs fa = fa_in;
   // the batch decode only: the constrained decode's passes (EXT, 2 sequences per wave, two
   // streams) ran ~2% slower balanced (profiles/r02_t64_simd_balance.txt)
-  fa.balance = (fa.forced || fa.ranges || fa.reverse || fa.start || fa.row_base || fa.resume_rows ||
-                fa.slot_order || fa.last_row) ? 0 : balance;
+  static const bool bal_ext = [] {  // A/B knob (bit-identical): CV_T64_BAL_EXT=1 balances the EXT passes too
+    const char* e = getenv("CV_T64_BAL_EXT");
+    return e && e[0] == '1';
+  }();
+  fa.balance = ((fa.forced || fa.ranges || fa.reverse || fa.start || fa.row_base || fa.resume_rows ||
+                 fa.slot_order || fa.last_row) && !bal_ext) ? 0 : balance;
   static const bool wave = [] {  // A/B knob (bit-identical): CV_T64_WAVE=0 keeps the lock-step layout
     const char* e = getenv("CV_T64_WAVE");
     return !(e && e[0] == '0');
