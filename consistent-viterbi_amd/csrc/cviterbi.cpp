@@ -179,6 +179,8 @@ struct cv_hmm {
   // f64 tables (generic f64 kernel + re-scoring): pi[N], a[N*N], et[V][N]
   bool f64_ready = false;
   DevBuf d_pi64, d_a64, d_et64;
+  DevBuf d_at64;  // [N][N] a^T, f64: the constrained decode's suffix pass for N > 256
+
   // exact-f64 trellis tables (trellis_fwd_f64 / backtrack_f64), padded to np64 = 64*ceil(N/64)
   int np64 = 0;
   bool t64_ready = false;
@@ -380,6 +382,16 @@ cv_status ensure_f64_tables(cv_hmm* h) {
   if ((st = upload(h->d_et64, et.data(), et.size() * 8)) != CV_OK) return st;
   h->f64_ready = true;
   return CV_OK;
+}
+
+// a^T [N][N] f64 (generic_ext's suffix pass), uploaded on first use
+cv_status ensure_at64(cv_hmm* h) {
+  if (h->d_at64.p) return CV_OK;
+  const int N = h->N;
+  std::vector<double> at((size_t)N * N);
+  for (int i = 0; i < N; ++i)
+    for (int j = 0; j < N; ++j) at[(size_t)j * N + i] = h->a[(size_t)i * N + j];
+  return upload(h->d_at64, at.data(), at.size() * 8);
 }
 
 // Exact-f64 trellis tables: a [NP][NP] row-major, a^T, pi [NP], et [V][NP]; -inf padded.
@@ -1353,14 +1365,20 @@ std::vector<int32_t> conseq_pairs(const std::vector<ConSeq>& cs, const int32_t* 
 }
 
 // The constrained decode's arithmetic: the row-A0 association (the terms of csp.hpp are
-// defined on it) in f64 -- the reference's precision, trellis_fwd_f64 -- or f32 (the f32
-// trellis), N <= 256 either way.
+// defined on it) in f64 -- the reference's precision: trellis_fwd_f64 for N <= 256, the
+// generic kernels above (generic_ext + generic_fwd, N <= generic_max_states) -- or f32 (the
+// f32 trellis, N <= 256).
+bool constrained_generic(const cv_hmm* h, const cv_opts& o) {
+  return o.dtype == CV_DTYPE_F64 && !cvk::t64_padded_states(h->N);
+}
+
 cv_status constrained_dtype_check(const cv_hmm* h, const cv_opts& o) {
   if (o.assoc != CV_ASSOC_VITERBI)
     return set_err(CV_EUNSUPPORTED, "constrained decode runs the row-A0 (VITERBI) association");
-  if (o.dtype == CV_DTYPE_F64 && cvk::t64_padded_states(h->N)) return CV_OK;
+  if (o.dtype == CV_DTYPE_F64 && (cvk::t64_padded_states(h->N) || h->N <= cvk::generic_max_states(8))) return CV_OK;
   if (o.dtype == CV_DTYPE_F32 && cvk::trellis_padded_states(h->N)) return CV_OK;
-  return set_err(CV_EUNSUPPORTED, "constrained decode needs dtype f32 or f64 and N <= 256 (N=%d)", h->N);
+  return set_err(CV_EUNSUPPORTED, "constrained decode needs f64 with N <= %d, or f32 with N <= 256 (N=%d)",
+                 cvk::generic_max_states(8), h->N);
 }
 
 cv_status constrained_validate(cv_hmm* h, int64_t nseq, const int64_t* offsets, const int32_t* obs,
@@ -1465,10 +1483,12 @@ cv_status constrained_partials_locked(cv_hmm* h, int64_t nseq, const int64_t* of
       seg_pair.push_back(p);
     }
   const bool f64 = o.dtype == CV_DTYPE_F64;
+  const bool gen = constrained_generic(h, o);  // f64, N > 256: generic_ext passes, rows of N
   if (!f64 && (st = ensure_trellis_tables(h)) != CV_OK) return st;
-  if (f64 && (st = ensure_t64_tables(h)) != CV_OK) return st;
+  if (f64 && !gen && (st = ensure_t64_tables(h)) != CV_OK) return st;
   if ((st = ensure_f64_tables(h)) != CV_OK) return st;
-  const int np = f64 ? h->np64 : h->np;
+  if (gen && (st = ensure_at64(h)) != CV_OK) return st;
+  const int np = gen ? N : f64 ? h->np64 : h->np;
   const size_t rb = f64 ? 8 : 4;  // bytes per term
   hipStream_t stream = o.stream ? (hipStream_t)o.stream : h->stream;
   // h->ws_order below is the main workspace's: a cv_decode_batch_device call still running on
@@ -1637,6 +1657,33 @@ cv_status constrained_partials_locked(cv_hmm* h, int64_t nseq, const int64_t* of
       ma.mu += n1 * np;
       err = cvk::launch_max_marginal(np, ma, nc - n1, stream);
     }
+  } else if (gen) {
+    // N > 256: the same passes, one workgroup per slot (generic_ext); no rows kept (the final
+    // decode runs the full forced passes)
+    cvk::GenericExtArgs ga{};
+    ga.tab = h->d_a64.as<double>();
+    ga.pi = h->d_pi64.as<double>();
+    ga.et = h->d_et64.as<double>();
+    ga.obs = dobs;
+    ga.ranges = h->cs_ranges.as<int64_t>();
+    ga.nstates = N;
+    ga.last_row = h->cs_delta.as<double>();
+    err = cvk::launch_generic_ext(ga, nc, stream);
+    if (err == hipSuccess) {
+      ga.tab = h->d_at64.as<double>();
+      ga.pi = h->cs_zero.as<double>();  // zeroed above: pi = 0 for the reversed pass
+      ga.ranges = h->cs_ranges.as<int64_t>() + 2 * nc;
+      ga.reverse = 1;
+      ga.noemit_last = 1;
+      ga.last_row = h->cs_g.as<double>();
+      err = cvk::launch_generic_ext(ga, nc, stream);
+    }
+    if (err == hipSuccess)
+      err = cvk::launch_t64_mu_add(h->cs_delta.as<double>(), h->cs_g.as<double>(), h->cs_mu.as<double>(), n1, np,
+                                   stream);
+    if (err == hipSuccess && nc > n1)
+      err = hipMemcpyAsync(h->cs_mu.as<double>() + n1 * np, h->cs_g.as<double>() + n1 * np,
+                           (size_t)(nc - n1) * np * 8, hipMemcpyDeviceToDevice, stream);
   } else {
     // prefixes: forward on a from each sequence start to t_1 (its last row = delta_{t_1})
     cvk::T64FwdArgs fa{};
@@ -1825,7 +1872,18 @@ cv_status constrained_partials_locked(cv_hmm* h, int64_t nseq, const int64_t* of
     HIP_TRY(hipMemcpyAsync(h->cs_ranges.p, srg.data(), srg.size() * 8, hipMemcpyHostToDevice, stream));
     HIP_TRY(hipMemcpyAsync(h->cs_start.p, sst.data(), sst.size() * 4, hipMemcpyHostToDevice, stream));
     if ((st = h->cs_seg.ensure((size_t)nb * np * rb)) != CV_OK) return st;
-    if (!f64) {
+    if (gen) {
+      cvk::GenericExtArgs sa{};
+      sa.tab = h->d_a64.as<double>();
+      sa.pi = h->d_pi64.as<double>();
+      sa.et = h->d_et64.as<double>();
+      sa.obs = dobs;
+      sa.ranges = h->cs_ranges.as<int64_t>();
+      sa.start = h->cs_start.as<int32_t>();
+      sa.nstates = N;
+      sa.last_row = h->cs_seg.as<double>();
+      err = cvk::launch_generic_ext(sa, nb, stream);
+    } else if (!f64) {
       cvk::TrellisFwdArgs sa{};
       sa.a_img = h->t_aimg.as<float>();
       sa.pi = h->t_pi.as<float>();
@@ -3241,7 +3299,8 @@ CV_API cv_status cv_decode_superseq_cp(cv_hmm* h, int64_t nseq, const int64_t* o
     return set_err(CV_EINVAL, "bad argument");
   *objective_out = 0.0;
   if (nseq == 0) return CV_OK;
-  if (h->N > 1024) return set_err(CV_EUNSUPPORTED, "super-sequence chain covers N <= 1024 (N=%d)", h->N);
+  if (h->N > cvk::kChainMaxStates)
+    return set_err(CV_EUNSUPPORTED, "super-sequence chain covers N <= %d (N=%d)", cvk::kChainMaxStates, h->N);
   std::lock_guard<std::mutex> lk(h->mu);
   cv_status st = set_device(h);
   if (st != CV_OK) return st;

@@ -183,4 +183,25 @@ template <typename REAL>
 hipError_t launch_generic_bt(const GenericBtArgs<REAL>& ba, int64_t nseq, hipStream_t stream);
 int generic_max_states(int real_bytes);
 
+// The constrained decode's f64 passes for N > 256 (the padded EXT kernels' range): one
+// workgroup per slot over an explicit element range, row-A0 association
+//   row 0 = start >= 0 ? (0 at `start`, -inf elsewhere) : pi + b(o_first)   (pi alone when
+//   noemit_last and the range has one element);  row t = max_i (row_{t-1}[i] + tab[i][j]) +
+//   b_j(o_t), the last step without the emission when noemit_last;
+// only the range's last row is written.  reverse: the range runs from end-1 down to begin (the
+// suffix pass: tab = a^T, pi = 0).  Same values as trellis_fwd_f64's EXT passes, bit for bit
+// (a max is exact whatever its order).
+struct GenericExtArgs {
+  const double* tab;       // [N][N] tab[i][j]: predecessor i -> state j (a, or a^T for the suffix)
+  const double* pi;        // [N]
+  const double* et;        // [V][N]
+  const int32_t* obs;      // [sum T], validated by the caller
+  const int64_t* ranges;   // [slot][2] element range [begin, end)
+  const int32_t* start;    // [slot] nullable: start state (segment tables)
+  int reverse, noemit_last;
+  int nstates;
+  double* last_row;        // [slot][N]
+};
+hipError_t launch_generic_ext(const GenericExtArgs& g, int64_t nslots, hipStream_t stream);
+
 }  // namespace cvk

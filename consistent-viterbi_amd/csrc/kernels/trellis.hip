@@ -1557,6 +1557,9 @@ template <typename REAL>
 hipError_t launch_generic_fwd(const GenericFwdArgs<REAL>& fa, int64_t nseq, hipStream_t stream) {
   if (nseq <= 0) return hipSuccess;
   const size_t lds = sizeof(REAL) * 2 * (size_t)fa.nstates;
+  if (lds > 64 * 1024)  // N > 4096 (f64) / 8192 (f32): the two rows in up to 160 KiB of LDS
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&generic_fwd<REAL>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipLaunchKernelGGL(generic_fwd<REAL>, dim3((unsigned)nseq), dim3(256), lds, stream, fa);
   return hipGetLastError();
 }
@@ -1572,6 +1575,60 @@ template hipError_t launch_generic_bt<float>(const GenericBtArgs<float>&, int64_
 template hipError_t launch_generic_bt<double>(const GenericBtArgs<double>&, int64_t, hipStream_t);
 
 // Generic kernel keeps 2*N REAL delta values in LDS.
-int generic_max_states(int real_bytes) { return (int)(65536 / (2 * real_bytes)); }
+// generic_ext (trellis.h): one workgroup per slot, the two rows in LDS, states strided over
+// the 256 threads; an empty range writes nothing (the host never builds one).
+__global__ __launch_bounds__(256) void generic_ext(GenericExtArgs g) {
+  extern __shared__ __attribute__((aligned(16))) double rows[];  // [2][N]
+  const int N = g.nstates;
+  const int64_t slot = blockIdx.x;
+  const int64_t b0 = g.ranges[2 * slot];
+  const int T = (int)(g.ranges[2 * slot + 1] - b0);
+  if (T <= 0) return;
+  const double ninf = -__builtin_inf();
+  auto elem = [&](int t) -> int64_t { return g.reverse ? b0 + T - 1 - t : b0 + t; };
+  {
+    const double* e = g.et + (size_t)g.obs[elem(0)] * N;
+    const int st = g.start ? g.start[slot] : -1;
+    const bool emit = !(g.noemit_last && T == 1);
+    for (int j = threadIdx.x; j < N; j += blockDim.x)
+      rows[j] = st >= 0 ? (j == st ? 0.0 : ninf) : emit ? g.pi[j] + e[j] : g.pi[j];
+  }
+  __syncthreads();
+  for (int t = 1; t < T; ++t) {
+    const double* prev = rows + ((t - 1) & 1) * N;
+    double* cur = rows + (t & 1) * N;
+    const double* e = g.et + (size_t)g.obs[elem(t)] * N;
+    const bool emit = !(g.noemit_last && t == T - 1);
+    for (int j = threadIdx.x; j < N; j += blockDim.x) {
+      const double* col = g.tab + j;
+      double m0 = ninf, m1 = ninf;
+      int i = 0;
+      for (; i + 1 < N; i += 2) {
+        m0 = fmax(m0, prev[i] + col[(size_t)i * N]);
+        m1 = fmax(m1, prev[i + 1] + col[(size_t)(i + 1) * N]);
+      }
+      if (i < N) m0 = fmax(m0, prev[i] + col[(size_t)i * N]);
+      const double m = fmax(m0, m1);
+      cur[j] = emit ? m + e[j] : m;
+    }
+    __syncthreads();
+  }
+  const double* last = rows + ((T - 1) & 1) * N;
+  double* out = g.last_row + slot * (int64_t)N;
+  for (int j = threadIdx.x; j < N; j += blockDim.x) out[j] = last[j];
+}
+
+hipError_t launch_generic_ext(const GenericExtArgs& g, int64_t nslots, hipStream_t stream) {
+  if (nslots <= 0) return hipSuccess;
+  if (g.nstates <= 0 || g.nstates > generic_max_states(8)) return hipErrorInvalidValue;
+  const size_t lds = 2 * (size_t)g.nstates * sizeof(double);
+  if (lds > 64 * 1024)
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&generic_ext), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds);
+  hipLaunchKernelGGL(generic_ext, dim3((unsigned)nslots), dim3(256), lds, stream, g);
+  return hipGetLastError();
+}
+
+int generic_max_states(int real_bytes) { return (int)(160 * 1024 / (2 * real_bytes)); }
 
 }  // namespace cvk

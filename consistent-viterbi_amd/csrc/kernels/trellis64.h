@@ -184,6 +184,8 @@ struct CpChainArgs {
   int32_t* path;         // [len]
   double* objective;     // [1]
 };
+// the chain's two rows in LDS (2 N doubles <= 160 KiB); psi is u16
+constexpr int kChainMaxStates = 10240;
 hipError_t launch_cp_superseq_chain(const CpChainArgs& g, hipStream_t stream);
 
 // NP = 64 * ceil(N / 64) for 1 <= N <= 256, else 0 (no f64 trellis kernel)

@@ -2080,7 +2080,7 @@ hipError_t launch_t64_suffix_trace(int np, const SuffixTrace64Args& a, int64_t n
 // predecessor term is the constant pi[j] (utils.rs:32-38), so every value of sequence k
 // carries the running total of sequences 0..k-1 and rounds accordingly.  A per-sequence
 // decode is the same up to those roundings; this kernel reproduces them: one workgroup walks
-// the elements in order, thread j = state j: first argmax over i of prev[i] + trans(i, j)
+// the elements in order, thread j = state j (states strided over 1,024 threads above that): first argmax over i of prev[i] + trans(i, j)
 // (strict '>' from i = 0), value prev[psi] + (trans(psi, j) + b[j, o]) (cp.rs:70-79), psi
 // stored as u16; then the first argmax of the last row and the backtrack (cp.rs:85-93).
 // Serial over elements (as the reference is): for the main.rs workflow, not the batch path.
@@ -2089,7 +2089,6 @@ hipError_t launch_t64_suffix_trace(int np, const SuffixTrace64Args& a, int64_t n
 template <bool LDS_A>
 __global__ __launch_bounds__(1024) void cp_superseq_chain(CpChainArgs g) {
   extern __shared__ double rowbuf[];  // [2][N] (+ [N][N] A when LDS_A)
-  const int j = threadIdx.x;
   const int N = g.nstates;
   const int64_t L = g.len;
   double* prev = rowbuf;
@@ -2097,15 +2096,16 @@ __global__ __launch_bounds__(1024) void cp_superseq_chain(CpChainArgs g) {
   const double* A = g.a;
   if constexpr (LDS_A) {
     double* la = rowbuf + 2 * N;
-    for (int k = j; k < N * N; k += blockDim.x) la[k] = g.a[k];
+    for (int k = threadIdx.x; k < N * N; k += blockDim.x) la[k] = g.a[k];
     A = la;
   }
-  if (j < N) prev[j] = g.pi[j] + g.et[(size_t)g.obs[0] * N + j];  // init_probs (cp.rs:66-68)
+  // N > 1024: thread j owns states j, j + 1024, ... (each state's candidate loop is its own)
+  for (int j = threadIdx.x; j < N; j += blockDim.x) prev[j] = g.pi[j] + g.et[(size_t)g.obs[0] * N + j];  // cp.rs:66-68
   __syncthreads();
   for (int64_t t = 1; t < L; ++t) {
-    if (j < N) {
-      const int o = g.obs[t];
-      const bool first = g.first[t] != 0;
+    const int o = g.obs[t];
+    const bool first = g.first[t] != 0;
+    for (int j = threadIdx.x; j < N; j += blockDim.x) {
       const double pj = g.pi[j];
       double m = prev[0] + (first ? pj : A[j]);
       int arg = 0;
@@ -2126,7 +2126,7 @@ __global__ __launch_bounds__(1024) void cp_superseq_chain(CpChainArgs g) {
     prev = cur;
     cur = tmp;
   }
-  if (j == 0) {
+  if (threadIdx.x == 0) {
     int cs = 0;
     double obj = prev[0];
     for (int i = 1; i < N; ++i)
@@ -2144,8 +2144,8 @@ __global__ __launch_bounds__(1024) void cp_superseq_chain(CpChainArgs g) {
 
 hipError_t launch_cp_superseq_chain(const CpChainArgs& g, hipStream_t stream) {
   if (g.len <= 0) return hipSuccess;
-  if (g.nstates <= 0 || g.nstates > 1024) return hipErrorInvalidValue;
-  const int threads = ((g.nstates + 63) / 64) * 64;
+  if (g.nstates <= 0 || g.nstates > kChainMaxStates) return hipErrorInvalidValue;
+  const int threads = std::min(1024, ((g.nstates + 63) / 64) * 64);
   const size_t n = (size_t)g.nstates;
   const size_t lds_a = (n * n + 2 * n) * sizeof(double);
   if (lds_a <= 160 * 1024) {

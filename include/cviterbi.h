@@ -59,7 +59,7 @@ enum { CV_ASSOC_VITERBI = 0, CV_ASSOC_CP = 1, CV_ASSOC_DP = 2, CV_ASSOC_DECODE =
 /* kernel choice: AUTO picks TRELLIS (register-resident A, f32, VITERBI, N <= 256) when it
  * applies, then TRELLIS_F64 (exact f64, any association, N <= 256; forced states with VITERBI
  * only: one wave per 2/4/8 sequences, A streamed from L2), else GENERIC (inline argmax,
- * f32/f64, any association, N <= 8192 f32 / 4096 f64). */
+ * f32/f64, any association, N <= 20480 f32 / 10240 f64: two rows of N in <= 160 KiB of LDS). */
 enum { CV_KERNEL_AUTO = 0, CV_KERNEL_TRELLIS = 1, CV_KERNEL_GENERIC = 2, CV_KERNEL_TRELLIS_F64 = 3 };
 
 /* cv_opts.flags */
@@ -198,10 +198,11 @@ CV_API cv_status cv_timing_end(cv_hmm* h, cv_timing* out);
  * sequences as exact integers (units of 2^-64: independent of order and sharding) this is
  * a weighted CSP with unary and pairwise terms, solved exactly per connected group of
  * components by branch and bound (ties: lexicographically smallest state vector in
- * component order); then a forced decode.  Row-A0 (VITERBI) association, N <= 256, every term,
+ * component order); then a forced decode.  Row-A0 (VITERBI) association, every term,
  * segment table and the final decode in opts->dtype: CV_DTYPE_F64 (default; the reference's
- * precision, cp.rs:95-126 / dp.rs:147-166 compute in f64: trellis_fwd_f64) or CV_DTYPE_F32 (the
- * f32 trellis, scores f64 re-scored).  A term outside the exact unit (|score| >= 2^32) is
+ * precision, cp.rs:95-126 / dp.rs:147-166 compute in f64: trellis_fwd_f64 for N <= 256, the
+ * generic kernels up to N = 10240) or CV_DTYPE_F32 (the f32 trellis, N <= 256, scores f64
+ * re-scored).  A term outside the exact unit (|score| >= 2^32) is
  * CV_EINVAL.  comp_state_out[ncomp] gets s_c (-1: no active element, or no feasible assignment
  * of its group); objective_out = sum of the per-sequence scores.  CV_ELIMIT if the search
  * exceeds its node limit.  Host pointers; synchronous. */
@@ -281,7 +282,7 @@ CV_API cv_status cv_viterbi_decode(cv_hmm* h, int64_t T, const int32_t* obs, int
  * total (a rounding-error margin), the running total folded on the host, and only the
  * uncertified sequences (near ties at that magnitude) re-run through the serial chain kernel
  * -- bit-identical to the serial chain (cv_last_superseq_stats).  Otherwise serial over
- * elements on the GPU (one workgroup), as the reference is on the CPU.  N <= 1024.
+ * elements on the GPU (one workgroup), as the reference is on the CPU.  N <= 10240.
  * CV_EINFEASIBLE when the maximum is -inf. */
 CV_API cv_status cv_decode_superseq_cp(cv_hmm* h, int64_t nseq, const int64_t* offsets, const int32_t* obs,
                                        int32_t* path_out, double* objective_out);

@@ -1,0 +1,137 @@
+"""GPU: models beyond the padded kernels' N <= 256, up to the LDS-bound limits of the generic
+decode (two rows of N in <= 160 KiB: N <= 10,240 in f64, 20,480 in f32) and of the serial
+super-sequence chain (N <= 10,240).  The reference has no state limit (hmm.rs:10-18 stores any
+N; viterbi.rs:5-32, cp.rs:63-93 loop over it); every case is checked against the C oracle bit
+for bit, and one state past each limit is refused with CV_EUNSUPPORTED.
+"""
+import numpy as np
+import pytest
+
+import c_oracle as O
+import cviterbi as cv
+from cviterbi import synth
+
+pytestmark = pytest.mark.gpu
+
+
+def _case(n, v, seed, lengths):
+    rng = np.random.default_rng(seed)
+    pi = np.log10(rng.dirichlet(np.ones(n)))
+    a = rng.uniform(-4.0, 0.0, (n, n))
+    b = rng.uniform(-3.0, 0.0, (n, v))
+    a[rng.random((n, n)) < 0.05] = -np.inf
+    off = synth.offsets_from_lengths(np.asarray(lengths))
+    obs = rng.integers(0, v, size=int(off[-1])).astype(np.int32)
+    return pi, a, b, off, obs
+
+
+@pytest.mark.parametrize("dtype,n", [("f64", 4200), ("f64", 10240), ("f32", 8300)])
+def test_generic_decode_beyond_64k_lds(gpu, dtype, n):
+    """The generic kernel's two rows above 64 KiB of LDS (the launch raises the limit)."""
+    pi, a, b, off, obs = _case(n, 5, seed=n, lengths=[3, 0, 4] if n > 5000 else [5, 1, 6])
+    h = cv.HMM(pi, a, b)
+    got = cv.decode_batch(h, off, obs, dtype=dtype, assoc="viterbi", rescore_f64=False)
+    ref = O.decode_batch(pi, a, b, off, obs, O.VITERBI, np.float32 if dtype == "f32" else np.float64)
+    assert np.array_equal(got[2], ref[2])
+    assert np.array_equal(got[1], ref[1])
+    assert np.array_equal(got[0], ref[0])
+
+
+def test_generic_decode_state_limit(gpu):
+    pi, a, b, off, obs = _case(10241, 3, seed=7, lengths=[2])
+    h = cv.HMM(pi, a, b)
+    with pytest.raises(cv.CVError) as e:
+        cv.decode_batch(h, off, obs, dtype="f64", assoc="viterbi", rescore_f64=False)
+    assert "LDS" in str(e.value)
+
+
+@pytest.mark.parametrize("n", [300, 1100, 2500])
+def test_superseq_chain_strided_states(gpu, n):
+    """cp_superseq_chain with N > 256 (and > 1,024: states strided over the workgroup's 1,024
+    threads), every element and the objective against the chained restatement."""
+    rng = np.random.default_rng(70 + n)
+    v = 7
+    # quantised tables: exact ties, the first index must win in every strided slice
+    pi = np.round(rng.uniform(-2, 0, n) * 4) / 4
+    a = np.round(rng.uniform(-2, 0, (n, n)) * 4) / 4
+    b = np.round(rng.uniform(-2, 0, (n, v)) * 4) / 4
+    a[rng.random((n, n)) < 0.1] = -np.inf
+    lengths = [3, 0, 1, 5, 2] if n > 1024 else [6, 0, 1, 9, 4, 3]
+    off = synth.offsets_from_lengths(np.asarray(lengths))
+    obs = rng.integers(0, v, size=int(off[-1])).astype(np.int32)
+    h = cv.HMM(pi, a, b)
+    path, obj = cv.decode_superseq_cp(h, off, obs)
+    rp, robj = O.cp_superseq_f64(pi, a, b, off, obs)
+    assert obj == robj
+    assert np.array_equal(path, rp)
+
+
+def _constrained_case(n, seed, nseq=10, tmax=14, multi=True):
+    """One- and several-position constrained sequences over N states: components 0..3 when
+    every sequence has one position; 0..1 with several (the oracle's exhaustive search runs
+    over N^(components coupled by pairs))."""
+    pi, a, b = synth.random_hmm(n, 9, seed=seed, zero_frac=0.05)
+    rng = np.random.default_rng(seed)
+    lens = rng.integers(1, tmax, size=nseq)
+    lens[:3] = [1, 2, tmax]
+    off = synth.offsets_from_lengths(lens)
+    obs = rng.integers(0, 9, size=int(off[-1])).astype(np.int32)
+    comp = np.full(len(obs), -1, np.int32)
+    for s in range(nseq):
+        if rng.random() < 0.8:
+            k = int(rng.integers(1, 4)) if multi else 1
+            pos = rng.choice(lens[s], size=min(k, lens[s]), replace=False)
+            comp[off[s] + pos] = rng.integers(0, 2 if multi else 4, size=len(pos))
+    comp[off[2]:off[3]] = -1
+    comp[off[0]] = 0                 # t_1 = first element (length-1 sequence)
+    comp[off[2] + lens[2] - 1] = 1   # t_1 = last element
+    return pi, a, b, off, obs, comp
+
+
+@pytest.mark.parametrize("n,multi", [(257, True), (300, False), (400, True), (520, False)])
+def test_constrained_f64_beyond_256(gpu, n, multi):
+    """The constrained decode at N > 256 (generic_ext terms passes + segment tables, host exact
+    sums, generic forced decode) against the oracle spec (np_oracle.constrained_decode): the
+    component states, paths and f64 scores bit for bit, every active element on its state."""
+    pi, a, b, off, obs, comp = _constrained_case(n, seed=n, multi=multi)
+    h = cv.HMM(pi, a, b)
+    path, score, status, states, obj = cv.decode_constrained(h, off, obs, comp, dtype="f64")
+    ref_states, forced = O.constrained_forced(pi, a, b, off, obs, comp, np.float64)
+    for c, s in ref_states.items():
+        assert states[c] == s, (c, states[c], s)
+    rp, rs, rst = O.decode_batch(pi, a, b, off, obs, O.VITERBI, np.float64, forced=forced)
+    assert np.array_equal(status, rst)
+    assert np.array_equal(path, rp)
+    assert np.array_equal(score[status == 0], rs[status == 0])
+    for e in np.nonzero(comp >= 0)[0]:
+        assert path[e] == states[comp[e]]
+    assert obj == pytest.approx(float(np.sum(score)), rel=1e-12)
+
+
+def test_constrained_device_and_sharded_beyond_256(gpu):
+    """The device API and the sharded partials (integer SUM over shards) at N = 300 equal the
+    host API's result."""
+    import torch
+    pi, a, b, off, obs, comp = _constrained_case(300, seed=31)
+    h = cv.HMM(pi, a, b)
+    ref = cv.decode_constrained(h, off, obs, comp, ncomp=4, dtype="f64")
+    dev = torch.device("cuda", 0)
+    path_d = torch.empty(int(off[-1]), dtype=torch.int32, device=dev)
+    score_d = torch.empty(len(off) - 1, dtype=torch.float64, device=dev)
+    status_d = torch.empty(len(off) - 1, dtype=torch.uint8, device=dev)
+    states, obj = cv.decode_constrained_device(h, off, torch.from_numpy(off).to(dev), torch.from_numpy(obs).to(dev),
+                                               comp, path_d, score_d, status_d, ncomp=4, dtype="f64")
+    assert np.array_equal(states, ref[3])
+    assert np.array_equal(path_d.cpu().numpy(), ref[0])
+    assert np.array_equal(score_d.cpu().numpy(), ref[1])
+    assert np.array_equal(status_d.cpu().numpy(), ref[2])
+    assert obj == ref[4]
+    from cviterbi import dist as cvdist
+    pairs = cv.constrained_pairs(off, comp, 4)
+    part = 0
+    for s0, s1 in ((0, 4), (4, len(off) - 1)):
+        lo, hi = off[s0], off[s1]
+        part = part + cv.constrained_partials(h, cvdist.shard_offsets(off, s0, s1), obs[lo:hi], comp[lo:hi], 4, pairs,
+                                              dtype="f64")
+    got_states, _ = cv.constrained_select(300, 4, part, pairs)
+    assert np.array_equal(got_states, ref[3])
