@@ -191,6 +191,7 @@ struct cv_hmm {
   // f32 generic tables
   bool g32_ready = false;
   DevBuf d_pi32, d_a32, d_et32;
+  DevBuf d_at32;  // [N][N] a^T f32 (generic_bt_rows)
   // workspace
   DevBuf ws_main, ws_last, ws_order;
   // a second decode workspace + stream: the constrained decode's unconstrained sequences run
@@ -384,7 +385,7 @@ cv_status ensure_f64_tables(cv_hmm* h) {
   return CV_OK;
 }
 
-// a^T [N][N] f64 (generic_ext's suffix pass), uploaded on first use
+// a^T [N][N] f64 (generic_ext's suffix pass, generic_bt_rows), uploaded on first use
 cv_status ensure_at64(cv_hmm* h) {
   if (h->d_at64.p) return CV_OK;
   const int N = h->N;
@@ -392,6 +393,16 @@ cv_status ensure_at64(cv_hmm* h) {
   for (int i = 0; i < N; ++i)
     for (int j = 0; j < N; ++j) at[(size_t)j * N + i] = h->a[(size_t)i * N + j];
   return upload(h->d_at64, at.data(), at.size() * 8);
+}
+
+// a^T [N][N] f32 (generic_bt_rows), uploaded on first use
+cv_status ensure_at32(cv_hmm* h) {
+  if (h->d_at32.p) return CV_OK;
+  const int N = h->N;
+  std::vector<float> at((size_t)N * N);
+  for (int i = 0; i < N; ++i)
+    for (int j = 0; j < N; ++j) at[(size_t)j * N + i] = f32(h->a[(size_t)i * N + j]);
+  return upload(h->d_at32, at.data(), at.size() * 4);
 }
 
 // Exact-f64 trellis tables: a [NP][NP] row-major, a^T, pi [NP], et [V][NP]; -inf padded.
@@ -687,8 +698,15 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
   // 8 sequences per wave, so its default cap is larger (HBM3E: 288 GB per GPU)
   const uint64_t cap = o.workspace_bytes ? o.workspace_bytes
                                          : default_workspace_cap(w_main.bytes, use_t64 ? kDefaultWorkspaceT64 : kDefaultWorkspace);
+  // generic kernels: rows mode (the delta rows, argmax recomputed along the path) for every
+  // association but CP (whose values need the argmax in the forward pass); knob
+  // CV_GENERIC_ROWS=1 (bit-identical to psi mode), read per call
+  const char* gr_env = getenv("CV_GENERIC_ROWS");
+  const bool gen_rows = !use_trellis && !use_t64 && o.assoc != CV_ASSOC_CP && gr_env && *gr_env == '1';
+  if (gen_rows && (st = o.dtype == CV_DTYPE_F64 ? ensure_at64(h) : ensure_at32(h)) != CV_OK) return st;
   const uint64_t per_elem = use_trellis ? (uint64_t)(wave ? h->npw : h->np) * 4
                            : (use_t64 && !t64cp) ? (uint64_t)h->np64 * 8
+                           : gen_rows ? (uint64_t)h->N * (o.dtype == CV_DTYPE_F64 ? 8 : 4)
                                        : (uint64_t)h->N * 2;
   const int real_bytes = o.dtype == CV_DTYPE_F64 ? 8 : 4;
   const uint64_t total_elems = (uint64_t)(offsets_host[nseq] - offsets_host[0]);
@@ -957,6 +975,7 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
       fa.last_row = reinterpret_cast<double*>(lrb);
       fa.status = status_dev;
       fa.forced = o.forced;
+      if (gen_rows) fa.rows = reinterpret_cast<double*>(wsb);
       err = cvk::launch_generic_fwd<double>(fa, n, stream);
     } else {
       cvk::GenericFwdArgs<float> fa{};
@@ -975,6 +994,7 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
       fa.last_row = reinterpret_cast<float*>(lrb);
       fa.status = status_dev;
       fa.forced = o.forced;
+      if (gen_rows) fa.rows = reinterpret_cast<float*>(wsb);
       err = cvk::launch_generic_fwd<float>(fa, n, stream);
     }
     if (err != hipSuccess) return set_err(CV_EDEVICE, "forward launch failed: %s", hipGetErrorString(err));
@@ -1046,7 +1066,14 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
       ba.pi64 = h->d_pi64.as<double>();
       ba.a64 = h->d_a64.as<double>();
       ba.et64 = h->d_et64.as<double>();
-      err = cvk::launch_generic_bt<double>(ba, n, bts);
+      if (gen_rows) {
+        ba.rows = reinterpret_cast<const double*>(wsb);
+        ba.at = h->d_at64.as<double>();
+        ba.et = h->d_et64.as<double>();
+        ba.assoc = o.assoc;
+        ba.nobs = (int)h->V;
+      }
+      err = gen_rows ? cvk::launch_generic_bt_rows<double>(ba, n, bts) : cvk::launch_generic_bt<double>(ba, n, bts);
     } else {
       cvk::GenericBtArgs<float> ba{};
       ba.psi = reinterpret_cast<const uint16_t*>(wsb);
@@ -1066,7 +1093,14 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
       ba.pi64 = h->d_pi64.as<double>();
       ba.a64 = h->d_a64.as<double>();
       ba.et64 = h->d_et64.as<double>();
-      err = cvk::launch_generic_bt<float>(ba, n, bts);
+      if (gen_rows) {
+        ba.rows = reinterpret_cast<const float*>(wsb);
+        ba.at = h->d_at32.as<float>();
+        ba.et = h->d_et32.as<float>();
+        ba.assoc = o.assoc;
+        ba.nobs = (int)h->V;
+      }
+      err = gen_rows ? cvk::launch_generic_bt_rows<float>(ba, n, bts) : cvk::launch_generic_bt<float>(ba, n, bts);
     }
     if (err != hipSuccess) return set_err(CV_EDEVICE, "backtrack launch failed: %s", hipGetErrorString(err));
     HIP_TRY(hipEventRecord(b1, bts));

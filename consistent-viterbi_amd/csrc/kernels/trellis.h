@@ -91,6 +91,11 @@ struct GenericFwdArgs {
   int64_t psi_elem_base;
   REAL* last_row;          // [(seqs of chunk)][N]
   uint8_t* status;
+  // rows mode (VITERBI / DECODE / DP, generic_fwd_ms<.., ROWS>): the delta rows themselves
+  // [(elements of chunk)][N] (from psi_elem_base) instead of psi -- the forward pass keeps
+  // only the maximum (2 VALU per pair instead of 4), generic_bt_rows recomputes the argmax
+  // along the path
+  REAL* rows;
 };
 
 template <typename REAL>
@@ -112,6 +117,11 @@ struct GenericBtArgs {
   const double* pi64;
   const double* a64;
   const double* et64;
+  // rows mode (generic_bt_rows): the forward's delta rows, a^T and b^T in REAL, the association
+  const REAL* rows;
+  const REAL* at;          // [N][N] at[j][i] = a[i][j]
+  const REAL* et;          // [V][N]
+  int assoc, nobs;
 };
 
 struct MaxMarginalArgs {
@@ -181,6 +191,9 @@ template <typename REAL>
 hipError_t launch_generic_fwd(const GenericFwdArgs<REAL>& fa, int64_t nseq, hipStream_t stream);
 template <typename REAL>
 hipError_t launch_generic_bt(const GenericBtArgs<REAL>& ba, int64_t nseq, hipStream_t stream);
+// rows mode: forward (fa.rows set, assoc != CP) and its backtrack
+template <typename REAL>
+hipError_t launch_generic_bt_rows(const GenericBtArgs<REAL>& ba, int64_t nseq, hipStream_t stream);
 int generic_max_states(int real_bytes);
 
 // The constrained decode's f64 passes for N > 256 (the padded EXT kernels' range): one

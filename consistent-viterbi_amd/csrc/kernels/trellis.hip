@@ -31,6 +31,9 @@
 //   generic_backtrack<REAL>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
+
+#include <algorithm>
 
 #include "trellis.h"
 
@@ -1164,6 +1167,171 @@ __global__ __launch_bounds__(256) void generic_fwd(GenericFwdArgs<REAL> args) {
   if (bad && threadIdx.x == 0) args.status[seq] = CVK_SEQ_BADOBS;
 }
 
+// generic_fwd_ms<REAL, S, ROWS>: S sequences per workgroup (consecutive slots of the
+// longest-first schedule, so near-equal lengths), every A element loaded once for all S -- the
+// one-sequence kernel above streams A from L2 once per sequence step and is bound by that
+// stream -- and 64 * ceil(N / 64) threads (<= 1,024), one state each where N <= 1,024.
+//   ROWS = false: argmax inline, u16 psi: same values, arguments and statuses as generic_fwd,
+//                 bit for bit (the same candidates in the same order per sequence);
+//   ROWS = true (VITERBI, DECODE, DP): the maximum only (add + max per candidate: a max is exact
+//                 in any order) and every delta row stored; generic_bt_rows recomputes the
+//                 first argmax along the path from those rows, so the paths equal generic_fwd's.
+// A finished sequence's rows stay untouched.
+template <typename REAL, int S, bool ROWS>
+__global__ __launch_bounds__(1024) void generic_fwd_ms(GenericFwdArgs<REAL> args, int64_t nslots) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  REAL* dbuf = reinterpret_cast<REAL*>(smem_raw);  // [2][S][N]
+  const int N = args.nstates;
+  const int V = args.nobs;
+  const int assoc = args.assoc;
+  const REAL ninf = -__builtin_inf();
+  int64_t e0[S], slot[S], seq[S];
+  int T[S];
+  int Tmax = 0;
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    const int64_t k = (int64_t)blockIdx.x * S + s;
+    slot[s] = args.seq_begin + k;
+    seq[s] = -1;
+    T[s] = 0;
+    e0[s] = 0;
+    if (k < nslots) {
+      seq[s] = args.order ? (int64_t)args.order[slot[s]] : slot[s];
+      e0[s] = args.offsets[seq[s]];
+      T[s] = (int)(args.offsets[seq[s] + 1] - e0[s]);
+    }
+    Tmax = T[s] > Tmax ? T[s] : Tmax;
+  }
+  if (Tmax <= 0) return;
+  auto row = [&](int buf, int s) -> REAL* { return dbuf + ((size_t)buf * S + s) * N; };
+  auto grow = [&](int s, int t) -> REAL* { return args.rows + (e0[s] + t - args.psi_elem_base) * (int64_t)N; };
+  int bad = 0;  // bit s: sequence s saw an observation outside [0, V)
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    if (T[s] <= 0) continue;
+    const int o = args.obs[e0[s]];
+    const bool ok = (unsigned)o < (unsigned)V;
+    bad |= ok ? 0 : 1 << s;
+    const int fs = args.forced ? args.forced[e0[s]] : -1;
+    REAL* d0 = row(0, s);
+    for (int j = threadIdx.x; j < N; j += blockDim.x) {
+      const REAL e = ok ? args.et[(size_t)o * N + j] : ninf;
+      REAL d;
+      if (assoc == CVK_ASSOC_DECODE)
+        d = (REAL)0;
+      else if (assoc == CVK_ASSOC_DP)
+        d = (e > ninf) ? (REAL)(args.pi[j] + e) : ninf;
+      else
+        d = args.pi[j] + e;
+      if (fs >= 0 && j != fs) d = ninf;
+      d0[j] = d;
+      if constexpr (ROWS) grow(s, 0)[j] = d;
+    }
+  }
+  __syncthreads();
+  for (int t = 1; t < Tmax; ++t) {
+    int o[S], fs[S];
+    bool act[S], ok[S];
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      act[s] = t < T[s];
+      o[s] = act[s] ? args.obs[e0[s] + t] : 0;
+      ok[s] = (unsigned)o[s] < (unsigned)V;
+      if (act[s] && !ok[s]) bad |= 1 << s;
+      fs[s] = (act[s] && args.forced) ? args.forced[e0[s] + t] : -1;
+    }
+    const int pb = (t - 1) & 1, cb = t & 1;
+    for (int j = threadIdx.x; j < N; j += blockDim.x) {
+      REAL e[S], best[S];
+      int arg[S];
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        e[s] = ok[s] ? args.et[(size_t)o[s] * N + j] : ninf;
+        best[s] = ninf;
+        arg[s] = 0;
+      }
+      const REAL* col = args.a + j;
+      if (assoc == CVK_ASSOC_DP) {
+        bool live[S];  // a -inf emission leaves the column at -inf (dp.rs:147-177)
+#pragma unroll
+        for (int s = 0; s < S; ++s) live[s] = act[s] && e[s] > ninf;
+        for (int i = 0; i < N; ++i) {
+          const REAL aij = col[(size_t)i * N];
+#pragma unroll
+          for (int s = 0; s < S; ++s) {
+            const REAL c = (aij + e[s]) + row(pb, s)[i];
+            if constexpr (ROWS) {
+              best[s] = fmax(best[s], c);
+            } else if (live[s] && c > best[s]) {
+              best[s] = c;
+              arg[s] = i;
+            }
+          }
+        }
+#pragma unroll
+        for (int s = 0; s < S; ++s)
+          if (act[s]) {
+            REAL v = live[s] ? best[s] : ninf;
+            if (fs[s] >= 0 && j != fs[s]) v = ninf;
+            row(cb, s)[j] = v;
+            if constexpr (ROWS)
+              grow(s, t)[j] = v;
+            else
+              args.psi[(e0[s] + t - args.psi_elem_base) * (int64_t)N + j] = (uint16_t)arg[s];
+          }
+      } else {
+        {  // i = 0 seeds the maximum (generic_fwd's `!any` case)
+          const REAL a0 = col[0];
+#pragma unroll
+          for (int s = 0; s < S; ++s) best[s] = row(pb, s)[0] + a0;
+        }
+        for (int i = 1; i < N; ++i) {
+          const REAL aij = col[(size_t)i * N];
+#pragma unroll
+          for (int s = 0; s < S; ++s) {
+            const REAL x = row(pb, s)[i] + aij;
+            if constexpr (ROWS) {
+              best[s] = fmax(best[s], x);
+            } else if (x > best[s]) {
+              best[s] = x;
+              arg[s] = i;
+            }
+          }
+        }
+#pragma unroll
+        for (int s = 0; s < S; ++s)
+          if (act[s]) {
+            REAL v;
+            int ag = arg[s];
+            if (!ROWS && assoc == CVK_ASSOC_CP)
+              v = row(pb, s)[ag] + (col[(size_t)ag * N] + e[s]);
+            else
+              v = best[s] + e[s];
+            if (assoc == CVK_ASSOC_DECODE && !(e[s] > ninf)) {
+              v = ninf;
+              ag = 0;
+            }
+            if (fs[s] >= 0 && j != fs[s]) v = ninf;
+            row(cb, s)[j] = v;
+            if constexpr (ROWS)
+              grow(s, t)[j] = v;
+            else
+              args.psi[(e0[s] + t - args.psi_elem_base) * (int64_t)N + j] = (uint16_t)ag;
+          }
+      }
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    if (T[s] <= 0) continue;
+    const REAL* last = row((T[s] - 1) & 1, s);
+    REAL* lastout = args.last_row + (slot[s] - args.seq_begin) * (int64_t)N;
+    for (int j = threadIdx.x; j < N; j += blockDim.x) lastout[j] = last[j];
+    if ((bad >> s) & 1 && threadIdx.x == 0) args.status[seq[s]] = CVK_SEQ_BADOBS;
+  }
+}
+
 template <typename REAL>
 __global__ __launch_bounds__(256) void generic_backtrack(GenericBtArgs<REAL> args) {
   const int lane = threadIdx.x & 63;
@@ -1222,6 +1390,104 @@ __global__ __launch_bounds__(256) void generic_backtrack(GenericBtArgs<REAL> arg
       path[t] = cs;
       if (t > 0) cs = psi[(size_t)t * N + cs];
     }
+    args.status[seq] = CVK_SEQ_OK;
+    if (!args.rescore_f64) args.score[seq] = bv;
+  }
+  if (args.rescore_f64) {
+    const double d = rescore_path_f64(path, args.obs + e0, T, args.pi64, args.a64, args.et64, N, lane);
+    if (lane == 0) args.score[seq] = d;
+  }
+}
+
+// generic_bt_rows<REAL>: the backtrack of generic_fwd_ms<.., ROWS = true>, one wave per
+// sequence.  At step t the predecessor of state s is the FIRST argmax over i of the forward's
+// own candidate values, recomputed from the stored row t-1 and a^T[s][.] (coalesced):
+// VITERBI / DECODE prev[i] + a[i][s] (index 0 when every candidate is -inf, and for DECODE
+// when b_s(o_t) is -inf), DP (a[i][s] + b_s(o_t)) + prev[i] over the candidates above -inf
+// (index 0 when none) -- exactly generic_fwd's psi.  Statuses, scores and the infeasible /
+// bad-observation paths as generic_backtrack.
+template <typename REAL>
+__global__ __launch_bounds__(256) void generic_bt_rows(GenericBtArgs<REAL> args) {
+  const int lane = threadIdx.x & 63;
+  const int64_t slot = args.seq_begin + (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (slot >= args.seq_end) return;
+  const int64_t seq = args.order ? (int64_t)args.order[slot] : slot;
+  const int64_t e0 = args.offsets[seq];
+  const int T = (int)(args.offsets[seq + 1] - e0);
+  const int N = args.nstates;
+  if (T <= 0) {
+    if (lane == 0) {
+      args.score[seq] = 0.0;
+      args.status[seq] = CVK_SEQ_EMPTY;
+    }
+    return;
+  }
+  const REAL ninf = -__builtin_inf();
+  const REAL* last = args.last_row + (slot - args.seq_begin) * (int64_t)N;
+  double bv = (double)ninf;
+  int bi = 0x7fffffff;
+  for (int i = lane; i < N; i += 64) {
+    const double v = (double)last[i];
+    if (bi == 0x7fffffff || v > bv) {
+      bv = v;
+      bi = i;
+    }
+  }
+  wave_argmax_first_d(bv, bi);
+  int32_t* path = args.path + e0;
+  const uint8_t prior = args.status[seq];
+  const bool feasible = bv > (double)ninf && prior != CVK_SEQ_BADOBS;
+  if (!feasible && !(args.decode_bt && prior != CVK_SEQ_BADOBS)) {
+    for (int t = lane; t < T; t += 64) path[t] = 0;
+    if (lane == 0) {
+      args.score[seq] = -__builtin_inf();
+      args.status[seq] = prior == CVK_SEQ_BADOBS ? CVK_SEQ_BADOBS : CVK_SEQ_INFEASIBLE;
+    }
+    return;
+  }
+  const REAL* rows = args.rows + (e0 - args.psi_elem_base) * (int64_t)N;
+  const int32_t* obs = args.obs + e0;
+  const bool dp = args.assoc == CVK_ASSOC_DP, dec = args.assoc == CVK_ASSOC_DECODE;
+  int cs = bi;
+  for (int t = T - 1; t >= 0; --t) {
+    if (lane == 0) path[t] = cs;
+    if (t == 0) break;
+    const REAL* prev = rows + (int64_t)(t - 1) * N;
+    const REAL* ac = args.at + (size_t)cs * N;
+    const int o = obs[t];
+    const REAL e = (unsigned)o < (unsigned)args.nobs ? args.et[(size_t)o * N + cs] : ninf;
+    double v = (double)ninf;
+    int a = 0x7fffffff;
+    if (dp) {
+      if (e > ninf)
+        for (int i = lane; i < N; i += 64) {
+          const double c = (double)((ac[i] + e) + prev[i]);
+          if (c > v) {
+            v = c;
+            a = i;
+          }
+        }
+    } else {
+      for (int i = lane; i < N; i += 64) {
+        const double x = (double)(prev[i] + ac[i]);
+        if (a == 0x7fffffff || x > v) {
+          v = x;
+          a = i;
+        }
+      }
+    }
+    wave_argmax_first_d(v, a);
+    if (a == 0x7fffffff || (dec && !(e > ninf))) a = 0;
+    cs = a;
+  }
+  if (!feasible) {  // viterbi::decode's infeasible walk (viterbi.rs:19-21, 24-30)
+    if (lane == 0) {
+      args.score[seq] = -__builtin_inf();
+      args.status[seq] = CVK_SEQ_INFEASIBLE;
+    }
+    return;
+  }
+  if (lane == 0) {
     args.status[seq] = CVK_SEQ_OK;
     if (!args.rescore_f64) args.score[seq] = bv;
   }
@@ -1553,9 +1819,50 @@ hipError_t launch_trellis_bt(int np, const BacktrackArgs& ba, int64_t nseq, hipS
 #undef CVK_BT
 }
 
+// sequences per workgroup of generic_fwd_ms: 4 while their rows fit the LDS and the launch
+// keeps >= 2 workgroups per CU (256 CUs), else fewer; 1 = generic_fwd.  CV_GENERIC_S=k sets it
+// (1, 2 or 4 where the rows fit; read per launch: A/B knob and tests, bit-identical)
+template <typename REAL>
+int generic_seqs_per_wg(int n, int64_t nseq) {
+  auto fits = [&](int s) { return 2 * (size_t)s * n * sizeof(REAL) <= 160 * 1024; };
+  if (const char* e = getenv("CV_GENERIC_S")) {
+    int s = atoi(e) >= 4 ? 4 : atoi(e) >= 2 ? 2 : 1;
+    while (s > 1 && !fits(s)) s /= 2;
+    return s;
+  }
+  int s = 4;
+  while (s > 1 && (!fits(s) || nseq < (int64_t)s * 512)) s /= 2;
+  return s;
+}
+
+template <typename REAL, int S, bool ROWS>
+hipError_t launch_generic_ms(const GenericFwdArgs<REAL>& fa, int64_t nseq, hipStream_t stream) {
+  const size_t lds = sizeof(REAL) * 2 * S * (size_t)fa.nstates;
+  if (lds > 64 * 1024)
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&generic_fwd_ms<REAL, S, ROWS>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  const unsigned threads = (unsigned)std::min(1024, (fa.nstates + 63) / 64 * 64);
+  hipLaunchKernelGGL((generic_fwd_ms<REAL, S, ROWS>), dim3((unsigned)((nseq + S - 1) / S)), dim3(threads), lds,
+                     stream, fa, nseq);
+  return hipGetLastError();
+}
+
 template <typename REAL>
 hipError_t launch_generic_fwd(const GenericFwdArgs<REAL>& fa, int64_t nseq, hipStream_t stream) {
   if (nseq <= 0) return hipSuccess;
+  if (fa.rows) {  // rows mode: the maximum only (VITERBI / DECODE / DP)
+    if (fa.assoc == CVK_ASSOC_CP) return hipErrorInvalidValue;
+    switch (generic_seqs_per_wg<REAL>(fa.nstates, nseq)) {
+      case 4: return launch_generic_ms<REAL, 4, true>(fa, nseq, stream);
+      case 2: return launch_generic_ms<REAL, 2, true>(fa, nseq, stream);
+      default: return launch_generic_ms<REAL, 1, true>(fa, nseq, stream);
+    }
+  }
+  switch (generic_seqs_per_wg<REAL>(fa.nstates, nseq)) {
+    case 4: return launch_generic_ms<REAL, 4, false>(fa, nseq, stream);
+    case 2: return launch_generic_ms<REAL, 2, false>(fa, nseq, stream);
+    default: break;
+  }
   const size_t lds = sizeof(REAL) * 2 * (size_t)fa.nstates;
   if (lds > 64 * 1024)  // N > 4096 (f64) / 8192 (f32): the two rows in up to 160 KiB of LDS
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&generic_fwd<REAL>),
@@ -1569,6 +1876,14 @@ hipError_t launch_generic_bt(const GenericBtArgs<REAL>& ba, int64_t nseq, hipStr
   hipLaunchKernelGGL(generic_backtrack<REAL>, dim3((unsigned)((nseq + 3) / 4)), dim3(256), 0, stream, ba);
   return hipGetLastError();
 }
+template <typename REAL>
+hipError_t launch_generic_bt_rows(const GenericBtArgs<REAL>& ba, int64_t nseq, hipStream_t stream) {
+  if (nseq <= 0) return hipSuccess;
+  hipLaunchKernelGGL(generic_bt_rows<REAL>, dim3((unsigned)((nseq + 3) / 4)), dim3(256), 0, stream, ba);
+  return hipGetLastError();
+}
+template hipError_t launch_generic_bt_rows<float>(const GenericBtArgs<float>&, int64_t, hipStream_t);
+template hipError_t launch_generic_bt_rows<double>(const GenericBtArgs<double>&, int64_t, hipStream_t);
 template hipError_t launch_generic_fwd<float>(const GenericFwdArgs<float>&, int64_t, hipStream_t);
 template hipError_t launch_generic_fwd<double>(const GenericFwdArgs<double>&, int64_t, hipStream_t);
 template hipError_t launch_generic_bt<float>(const GenericBtArgs<float>&, int64_t, hipStream_t);

@@ -135,3 +135,57 @@ def test_constrained_device_and_sharded_beyond_256(gpu):
                                               dtype="f64")
     got_states, _ = cv.constrained_select(300, 4, part, pairs)
     assert np.array_equal(got_states, ref[3])
+
+
+@pytest.mark.parametrize("rows", ["1", "0"])
+@pytest.mark.parametrize("S", ["1", "2", "4"])
+@pytest.mark.parametrize("assoc", ["viterbi", "cp", "dp", "decode"])
+@pytest.mark.parametrize("dtype,n", [("f64", 300), ("f32", 300), ("f64", 700), ("f64", 1100)])
+def test_generic_multi_sequence_workgroups(gpu, monkeypatch, rows, S, assoc, dtype, n):
+    """generic_fwd_ms (S sequences per workgroup, CV_GENERIC_S) in rows mode (the maximum
+    only, argmax recomputed by generic_bt_rows; CV_GENERIC_ROWS=1, CP always psi) and psi
+    mode against the oracle in every association: ragged and empty sequences in one
+    workgroup, forced states, -inf transitions and emissions, N above 1,024 threads."""
+    monkeypatch.setenv("CV_GENERIC_S", S)
+    monkeypatch.setenv("CV_GENERIC_ROWS", rows)
+    pi, a, b = synth.random_hmm(n, 11, seed=n + 5, zero_frac=0.1)
+    rng = np.random.default_rng(n + int(S))
+    lens = rng.integers(1, 24, size=23)
+    lens[[4, 9]] = 0
+    lens[6] = 1
+    off = synth.offsets_from_lengths(lens)
+    obs = rng.integers(0, 11, size=int(off[-1])).astype(np.int32)
+    forced = np.where(rng.random(len(obs)) < 0.05, rng.integers(0, n, size=len(obs)), -1).astype(np.int32)
+    dt = np.float32 if dtype == "f32" else np.float64
+    ASSOC = {"viterbi": O.VITERBI, "cp": O.CP, "dp": O.DP, "decode": O.DECODE}
+    h = cv.HMM(pi, a, b)
+    fr = forced if assoc == "viterbi" else None
+    got = cv.decode_batch(h, off, obs, dtype=dtype, assoc=assoc, kernel="generic", rescore_f64=False, forced=fr)
+    ref = O.decode_batch(pi, a, b, off, obs, ASSOC[assoc], dt, forced=fr)
+    assert np.array_equal(got[2], ref[2])
+    ok = got[2] == 0
+    assert np.array_equal(got[1][ok], ref[1][ok])
+    assert np.array_equal(got[0], ref[0])
+
+
+@pytest.mark.parametrize("rows", ["1", "0"])
+@pytest.mark.parametrize("name", ["golden_ties.npz", "golden_inf.npz", "golden_small.npz"])
+def test_generic_rows_golden(gpu, monkeypatch, rows, name):
+    """The golden fixtures (exact ties everywhere, -inf entries and infeasible sequences incl.
+    viterbi::decode's infeasible walk) through the generic kernels in both modes."""
+    from conftest import load_golden
+    monkeypatch.setenv("CV_GENERIC_ROWS", rows)
+    g = load_golden(name)
+    h = cv.HMM(g["pi"], g["a"], g["b"])
+    seen = 0
+    for dt in ("f32", "f64"):
+        for assoc in ("viterbi", "cp", "dp", "decode"):
+            k = f"{dt}_{assoc}"
+            if k + "_path" not in g:
+                continue
+            got = cv.decode_batch(h, g["offsets"], g["obs"], dtype=dt, assoc=assoc, kernel="generic",
+                                  rescore_f64=False)
+            for x, y, what in zip(got, (g[k + "_path"], g[k + "_score"], g[k + "_status"]), ("path", "score", "status")):
+                assert np.array_equal(x, y), (k, what)
+            seen += 1
+    assert seen > 0
