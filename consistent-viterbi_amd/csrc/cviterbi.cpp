@@ -699,10 +699,12 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
   const uint64_t cap = o.workspace_bytes ? o.workspace_bytes
                                          : default_workspace_cap(w_main.bytes, use_t64 ? kDefaultWorkspaceT64 : kDefaultWorkspace);
   // generic kernels: rows mode (the delta rows, argmax recomputed along the path) for every
-  // association but CP (whose values need the argmax in the forward pass); knob
-  // CV_GENERIC_ROWS=1 (bit-identical to psi mode), read per call
+  // association but CP (whose values need the argmax in the forward pass); A/B knob
+  // CV_GENERIC_ROWS=0 (psi mode, bit-identical), read per call.  4,096 x 128 sequences:
+  // N = 300 14.9 -> 11.5 ms, N = 512 28.7 -> 21.5 ms, N = 1,024 163 -> 139 ms
+  // (profiles/r04_large_n.txt)
   const char* gr_env = getenv("CV_GENERIC_ROWS");
-  const bool gen_rows = !use_trellis && !use_t64 && o.assoc != CV_ASSOC_CP && gr_env && *gr_env == '1';
+  const bool gen_rows = !use_trellis && !use_t64 && o.assoc != CV_ASSOC_CP && !(gr_env && *gr_env == '0');
   if (gen_rows && (st = o.dtype == CV_DTYPE_F64 ? ensure_at64(h) : ensure_at32(h)) != CV_OK) return st;
   const uint64_t per_elem = use_trellis ? (uint64_t)(wave ? h->npw : h->np) * 4
                            : (use_t64 && !t64cp) ? (uint64_t)h->np64 * 8
