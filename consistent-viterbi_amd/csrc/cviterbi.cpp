@@ -408,7 +408,8 @@ cv_status ensure_at32(cv_hmm* h) {
 // Exact-f64 trellis tables: a [NP][NP] row-major, a^T, pi [NP], et [V][NP]; -inf padded.
 cv_status ensure_t64_tables(cv_hmm* h) {
   if (h->t64_ready) return CV_OK;
-  const int N = h->N, NP = cvk::t64_padded_states(N);
+  const int N = h->N, NP = cvk::t64_batch_states(N);
+  if (NP == 0) return set_err(CV_EUNSUPPORTED, "f64 trellis tables need N <= 512 (N=%d)", N);
   const int64_t V = h->V;
   const double ninf = -INFINITY;
   std::vector<double> a((size_t)NP * NP, ninf), at((size_t)NP * NP, ninf), pi(NP, ninf), et((size_t)V * NP, ninf);
@@ -645,10 +646,13 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
   // backtrack_f64; CP runs
   // trellis_cp_f64 (argmax in the forward pass) + generic_backtrack<double>
   // forced states / resume rows (the constrained decode): row A0 only (trellis_fwd_f64 EXT)
+  // 256 < N <= 512 (cvk::t64_batch_states): VITERBI / DECODE without forced states only
   const bool t64_ok = o.dtype == CV_DTYPE_F64 &&
-                      (o.assoc == CV_ASSOC_VITERBI || o.assoc == CV_ASSOC_DECODE || o.assoc == CV_ASSOC_CP ||
-                       o.assoc == CV_ASSOC_DP) &&
-                      (!(o.forced || resume_rows) || o.assoc == CV_ASSOC_VITERBI) && cvk::t64_padded_states(h->N) != 0;
+                      (((o.assoc == CV_ASSOC_VITERBI || o.assoc == CV_ASSOC_DECODE || o.assoc == CV_ASSOC_CP ||
+                         o.assoc == CV_ASSOC_DP) &&
+                        (!(o.forced || resume_rows) || o.assoc == CV_ASSOC_VITERBI) && cvk::t64_padded_states(h->N) != 0) ||
+                       (cvk::t64_batch_states(h->N) == 512 && (o.assoc == CV_ASSOC_VITERBI || o.assoc == CV_ASSOC_DECODE) &&
+                        !o.forced && !resume_rows && !cp_cert && !cp_init && !cp_last));
   if (o.kernel == CV_KERNEL_TRELLIS_F64 && !t64_ok)
     return set_err(CV_EUNSUPPORTED,
                    "f64 trellis kernel needs dtype f64, N <= 256, and forced states only with assoc VITERBI");

@@ -190,6 +190,9 @@ hipError_t launch_cp_superseq_chain(const CpChainArgs& g, hipStream_t stream);
 
 // NP = 64 * ceil(N / 64) for 1 <= N <= 256, else 0 (no f64 trellis kernel)
 int t64_padded_states(int n);
+// the batch decode's NP (VITERBI / DECODE, no forced states): t64_padded_states, or 512 for
+// 256 < N <= 512 (column-split pairs of waves); 0 = the generic kernels
+int t64_batch_states(int n);
 // sequences per forward wave (2, 4 or 8) for a launch of nseq sequences on `cus` CUs
 int t64_seqs_per_wave(int64_t nseq, int cus);
 hipError_t launch_t64_fwd(int np, int s, const T64FwdArgs& fa, int64_t nseq, hipStream_t stream);

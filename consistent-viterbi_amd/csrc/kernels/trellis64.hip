@@ -1907,6 +1907,30 @@ hipError_t launch_t64_wave_fused(const T64FwdArgs& fa, const T64BtArgs& ba, int6
 
 int t64_padded_states(int n) { return (n >= 1 && n <= 256) ? 64 * ((n + 63) / 64) : 0; }
 
+// The batch decode's f64 trellis (VITERBI / DECODE rows, no forced states) also covers
+// 256 < N <= 512: NP = 512 as PAIRS of C = 4 waves splitting the columns (the W = 2 layout of
+// the small-batch kernel with the full batch's C), four pairs per workgroup, and backtrack_f64
+// at KP = 8.  Knob CV_T64_512=1 (read per call; 0 / unset: the generic kernels, bit-identical).
+int t64_batch_states(int n) {
+  if (n <= 256) return t64_padded_states(n);
+  const char* e = getenv("CV_T64_512");
+  return (e && e[0] == '1' && n <= 512) ? 512 : 0;
+}
+
+template <int S>
+hipError_t fwd_512(const T64FwdArgs& fa, int64_t nseq, hipStream_t stream) {
+  if (fa.wg_ok || wg_force()) {  // four pairs per workgroup, SIMD partners trade priority
+    T64FwdArgs f4 = fa;
+    f4.balance = 0;
+    hipLaunchKernelGGL((trellis_fwd_f64<4, S, 8, false, false, 2, true, 2, 1, true, 4, 2>),
+                       dim3((unsigned)((nseq + 4 * S - 1) / (4 * S))), dim3(512), 0, stream, f4);
+  } else {
+    hipLaunchKernelGGL((trellis_fwd_f64<4, S, 8, false, false, 2>), dim3((unsigned)((nseq + S - 1) / S)), dim3(128), 0,
+                       stream, fa);
+  }
+  return hipGetLastError();
+}
+
 int t64_seqs_per_wave(int64_t nseq, int cus) {
   // fill at least two waves per SIMD (4 SIMDs per CU), then prefer the larger S: each A row
   // streamed from L2 serves S sequences
@@ -1942,6 +1966,14 @@ hipError_t launch_t64_fwd(int np, int s, const T64FwdArgs& fa_in, int64_t nseq, 
   const bool ext = fa.forced || fa.ranges || fa.reverse || fa.start || fa.row_base || fa.resume_rows ||
                    fa.slot_order || fa.last_row;
   if (np == 64 && wave && !fa.dp_assoc && !ext) return launch_t64_wave(fa, nseq, stream);
+  if (np == 512) {  // batch decode only (t64_batch_states)
+    if (ext || fa.dp_assoc) return hipErrorInvalidValue;
+    switch (s) {
+      case 8: return fwd_512<8>(fa, nseq, stream);
+      case 4: return fwd_512<4>(fa, nseq, stream);
+      default: return fwd_512<2>(fa, nseq, stream);
+    }
+  }
   if (fa.dp_assoc && s > 4) s = 4;  // the emissions of every sequence stay in registers
   switch (np) {
     case 64: return fwd_c<1>(fa, s, nseq, stream);
@@ -1963,6 +1995,12 @@ hipError_t bt_pf_np(int np, const T64BtArgs& ba, dim3 grid, dim3 block, hipStrea
       case 128: hipLaunchKernelGGL((backtrack_f64<2, PF, NONPOS, PERSIST>), grid, block, 0, stream, ba); break;
       case 192: hipLaunchKernelGGL((backtrack_f64<3, PF, NONPOS, PERSIST>), grid, block, 0, stream, ba); break;
       case 256: hipLaunchKernelGGL((backtrack_f64<4, PF, NONPOS, PERSIST>), grid, block, 0, stream, ba); break;
+      case 512:
+        if constexpr (PF <= 8) {
+          hipLaunchKernelGGL((backtrack_f64<8, PF, NONPOS, PERSIST>), grid, block, 0, stream, ba);
+          break;
+        }
+        return hipErrorInvalidValue;
       default: return hipErrorInvalidValue;
     }
   }

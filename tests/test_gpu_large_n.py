@@ -189,3 +189,50 @@ def test_generic_rows_golden(gpu, monkeypatch, rows, name):
                 assert np.array_equal(x, y), (k, what)
             seen += 1
     assert seen > 0
+
+
+@pytest.mark.parametrize("S", ["2", "4", "8"])
+@pytest.mark.parametrize("assoc", ["viterbi", "decode"])
+@pytest.mark.parametrize("n", [300, 512])
+def test_t64_512_vs_oracle(gpu, monkeypatch, S, assoc, n):
+    """256 < N <= 512 on the f64 trellis (NP = 512: column-split pairs of C = 4 waves,
+    backtrack_f64 at KP = 8), S sequences per pair (CV_T64_S), one pair per workgroup (ragged
+    batch): paths, scores and statuses bit for bit against the oracle, incl. empty sequences
+    and infeasible ones (viterbi::decode's infeasible walk for `decode`)."""
+    monkeypatch.setenv("CV_T64_S", S)
+    monkeypatch.setenv("CV_T64_512", "1")
+    pi, a, b = synth.random_hmm(n, 13, seed=n + 17, zero_frac=0.05)
+    b = b.copy()
+    b[:, 12] = -np.inf  # observation 12: no state emits it
+    rng = np.random.default_rng(n + int(S))
+    lens = rng.integers(1, 30, size=40)
+    lens[[3, 17]] = 0
+    off = synth.offsets_from_lengths(lens)
+    obs = rng.integers(0, 12, size=int(off[-1])).astype(np.int32)
+    obs[int(off[5]) + lens[5] // 2] = 12  # sequence 5 infeasible
+    h = cv.HMM(pi, a, b)
+    got = cv.decode_batch(h, off, obs, dtype="f64", assoc=assoc, rescore_f64=False)
+    t = cv.last_timing(h)
+    assert t["kernel"] == "trellis_f64" and t["padded_states"] == 512
+    ref = O.decode_batch(pi, a, b, off, obs, {"viterbi": O.VITERBI, "decode": O.DECODE}[assoc], np.float64)
+    assert np.array_equal(got[2], ref[2])
+    assert np.array_equal(got[1], ref[1])
+    assert np.array_equal(got[0], ref[0])
+
+
+def test_t64_512_eight_wave_batch_vs_generic(gpu, monkeypatch):
+    """The four-pairs-per-workgroup layout (equal lengths, S = 8 at 16,384 sequences) against
+    the generic kernel (itself oracle-checked above) over the whole batch."""
+    monkeypatch.setenv("CV_T64_512", "1")
+    n = 449
+    pi, a, b = synth.random_hmm(n, 64, seed=449)
+    off = synth.offsets_from_lengths(np.full(16384, 24))
+    obs = synth.iid_obs(64, int(off[-1]), 449)
+    h = cv.HMM(pi, a, b)
+    got = cv.decode_batch(h, off, obs, dtype="f64", rescore_f64=False)
+    t = cv.last_timing(h)
+    assert t["kernel"] == "trellis_f64" and t["padded_states"] == 512 and t["seqs_per_wave"] == 8
+    ref = cv.decode_batch(h, off, obs, dtype="f64", kernel="generic", rescore_f64=False)
+    assert cv.last_timing(h)["kernel"] == "generic"
+    for x, y, what in zip(got, ref, ("path", "score", "status")):
+        assert np.array_equal(x, y), what
