@@ -646,12 +646,18 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
   // backtrack_f64; CP runs
   // trellis_cp_f64 (argmax in the forward pass) + generic_backtrack<double>
   // forced states / resume rows (the constrained decode): row A0 only (trellis_fwd_f64 EXT)
-  // 256 < N <= 512 (cvk::t64_batch_states): VITERBI / DECODE without forced states only
+  // 256 < N <= 512 (cvk::t64_batch_states): VITERBI / DECODE without forced states only, where
+  // the padded NP = 512 trellis beats the generic kernels: N >= 384 or >= 8,192 sequences
+  // (4,096 x 128: N = 384 15.3 vs 15.8 ms, N = 320 15.4 vs 12.3; 16,384 x 128: N = 320 34.1
+  // vs 46.7 ms, N = 512 35.8 vs 84.0 -- profiles/r04_large_n.txt); CV_T64_512=1 forces it
+  const char* t512_env = getenv("CV_T64_512");
+  const bool t512_pick = (t512_env && t512_env[0] == '1') || h->N >= 384 || nseq >= 8192;
   const bool t64_ok = o.dtype == CV_DTYPE_F64 &&
                       (((o.assoc == CV_ASSOC_VITERBI || o.assoc == CV_ASSOC_DECODE || o.assoc == CV_ASSOC_CP ||
                          o.assoc == CV_ASSOC_DP) &&
                         (!(o.forced || resume_rows) || o.assoc == CV_ASSOC_VITERBI) && cvk::t64_padded_states(h->N) != 0) ||
-                       (cvk::t64_batch_states(h->N) == 512 && (o.assoc == CV_ASSOC_VITERBI || o.assoc == CV_ASSOC_DECODE) &&
+                       (cvk::t64_batch_states(h->N) == 512 && t512_pick &&
+                        (o.assoc == CV_ASSOC_VITERBI || o.assoc == CV_ASSOC_DECODE) &&
                         !o.forced && !resume_rows && !cp_cert && !cp_init && !cp_last));
   if (o.kernel == CV_KERNEL_TRELLIS_F64 && !t64_ok)
     return set_err(CV_EUNSUPPORTED,

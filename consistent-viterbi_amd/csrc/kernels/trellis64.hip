@@ -1910,11 +1910,11 @@ int t64_padded_states(int n) { return (n >= 1 && n <= 256) ? 64 * ((n + 63) / 64
 // The batch decode's f64 trellis (VITERBI / DECODE rows, no forced states) also covers
 // 256 < N <= 512: NP = 512 as PAIRS of C = 4 waves splitting the columns (the W = 2 layout of
 // the small-batch kernel with the full batch's C), four pairs per workgroup, and backtrack_f64
-// at KP = 8.  Knob CV_T64_512=1 (read per call; 0 / unset: the generic kernels, bit-identical).
+// at KP = 8.  A/B knob CV_T64_512=0 (read per call): the generic kernels (bit-identical).
 int t64_batch_states(int n) {
   if (n <= 256) return t64_padded_states(n);
   const char* e = getenv("CV_T64_512");
-  return (e && e[0] == '1' && n <= 512) ? 512 : 0;
+  return (!(e && e[0] == '0') && n <= 512) ? 512 : 0;
 }
 
 template <int S>

@@ -27,5 +27,7 @@ def run(n, nseq, T, reps=3):
 
 
 if __name__ == "__main__":
+    import os
+    nseq = int(os.environ.get("NSEQ", "4096"))
     for n in [int(x) for x in sys.argv[1:]] or [256, 300, 512, 1024]:
-        run(n, 4096, 128)
+        run(n, nseq, 128)
