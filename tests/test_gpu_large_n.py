@@ -236,3 +236,24 @@ def test_t64_512_eight_wave_batch_vs_generic(gpu, monkeypatch):
     assert cv.last_timing(h)["kernel"] == "generic"
     for x, y, what in zip(got, ref, ("path", "score", "status")):
         assert np.array_equal(x, y), what
+
+
+@pytest.mark.parametrize("S", ["2", "4", "8"])
+@pytest.mark.parametrize("n", [300, 449])
+def test_t64_512_forced_vs_oracle(gpu, monkeypatch, S, n):
+    """Forced states on the NP = 512 f64 trellis (EXT pairs; S = 8 runs at 4): paths, scores and
+    statuses bit for bit against the oracle, incl. infeasible forced states."""
+    monkeypatch.setenv("CV_T64_S", S)
+    monkeypatch.setenv("CV_T64_512", "1")
+    pi, a, b = synth.random_hmm(n, 19, seed=n + 300, zero_frac=0.1)
+    rng = np.random.default_rng(n + 300)
+    off = synth.offsets_from_lengths(rng.integers(1, 40, size=40))
+    obs = rng.integers(0, 19, size=int(off[-1])).astype(np.int32)
+    forced = np.where(rng.random(len(obs)) < 0.05, rng.integers(0, n, size=len(obs)), -1).astype(np.int32)
+    h = cv.HMM(pi, a, b)
+    got = cv.decode_batch(h, off, obs, rescore_f64=False, forced=forced, dtype="f64")
+    t = cv.last_timing(h)
+    assert t["kernel"] == "trellis_f64" and t["padded_states"] == 512
+    ref = O.decode_batch(pi, a, b, off, obs, O.VITERBI, np.float64, forced=forced)
+    for x, y, what in zip(got, ref, ("path", "score", "status")):
+        assert np.array_equal(x, y), what
