@@ -646,7 +646,7 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
   // backtrack_f64; CP runs
   // trellis_cp_f64 (argmax in the forward pass) + generic_backtrack<double>
   // forced states / resume rows (the constrained decode): row A0 only (trellis_fwd_f64 EXT)
-  // 256 < N <= 512 (cvk::t64_batch_states): VITERBI (forced states too) / DECODE only, where
+  // 256 < N <= 512 (cvk::t64_batch_states): VITERBI (forced states too) / DECODE / DP, where
   // the padded NP = 512 trellis beats the generic kernels: N >= 384 or >= 8,192 sequences
   // (4,096 x 128: N = 384 15.3 vs 15.8 ms, N = 320 15.4 vs 12.3; 16,384 x 128: N = 320 34.1
   // vs 46.7 ms, N = 512 35.8 vs 84.0 -- profiles/r04_large_n.txt); CV_T64_512=1 forces it
@@ -657,7 +657,7 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
                          o.assoc == CV_ASSOC_DP) &&
                         (!(o.forced || resume_rows) || o.assoc == CV_ASSOC_VITERBI) && cvk::t64_padded_states(h->N) != 0) ||
                        (cvk::t64_batch_states(h->N) == 512 && t512_pick &&
-                        (o.assoc == CV_ASSOC_VITERBI || (o.assoc == CV_ASSOC_DECODE && !o.forced)) &&
+                        (o.assoc == CV_ASSOC_VITERBI || ((o.assoc == CV_ASSOC_DECODE || o.assoc == CV_ASSOC_DP) && !o.forced)) &&
                         !resume_rows && !cp_cert && !cp_init && !cp_last));
   if (o.kernel == CV_KERNEL_TRELLIS_F64 && !t64_ok)
     return set_err(CV_EUNSUPPORTED,

@@ -1924,6 +1924,14 @@ hipError_t fwd_512(const T64FwdArgs& fa, int64_t nseq, hipStream_t stream) {
                        stream, fa);
     return hipGetLastError();
   }
+  if (fa.dp_assoc) {  // DPSolver's (a + b) + d, one pair per workgroup (S <= 4: the emissions in registers)
+    if constexpr (S <= 4) {
+      hipLaunchKernelGGL((trellis_fwd_f64<4, S, 8, true, false, 2>), dim3((unsigned)((nseq + S - 1) / S)), dim3(128), 0,
+                         stream, fa);
+      return hipGetLastError();
+    }
+    return hipErrorInvalidValue;
+  }
   if (fa.wg_ok || wg_force()) {  // four pairs per workgroup, SIMD partners trade priority
     T64FwdArgs f4 = fa;
     f4.balance = 0;
@@ -1972,10 +1980,10 @@ hipError_t launch_t64_fwd(int np, int s, const T64FwdArgs& fa_in, int64_t nseq, 
                    fa.slot_order || fa.last_row;
   if (np == 64 && wave && !fa.dp_assoc && !ext) return launch_t64_wave(fa, nseq, stream);
   if (np == 512) {  // batch decode only (t64_batch_states), forced states allowed
-    if (fa.dp_assoc || fa.ranges || fa.reverse || fa.start || fa.row_base || fa.resume_rows || fa.slot_order ||
-        fa.last_row)
+    if (fa.ranges || fa.reverse || fa.start || fa.row_base || fa.resume_rows || fa.slot_order || fa.last_row ||
+        (fa.dp_assoc && fa.forced))
       return hipErrorInvalidValue;
-    if (fa.forced && s > 4) s = 4;  // EXT at S = 8: 275 VGPRs + 19 AGPRs, one wave per SIMD
+    if ((fa.forced || fa.dp_assoc) && s > 4) s = 4;  // EXT at S = 8: 275 VGPRs + 19 AGPRs, one wave per SIMD
     switch (s) {
       case 8: return fwd_512<8>(fa, nseq, stream);
       case 4: return fwd_512<4>(fa, nseq, stream);

@@ -192,7 +192,7 @@ def test_generic_rows_golden(gpu, monkeypatch, rows, name):
 
 
 @pytest.mark.parametrize("S", ["2", "4", "8"])
-@pytest.mark.parametrize("assoc", ["viterbi", "decode"])
+@pytest.mark.parametrize("assoc", ["viterbi", "decode", "dp"])
 @pytest.mark.parametrize("n", [300, 512])
 def test_t64_512_vs_oracle(gpu, monkeypatch, S, assoc, n):
     """256 < N <= 512 on the f64 trellis (NP = 512: column-split pairs of C = 4 waves,
@@ -214,7 +214,7 @@ def test_t64_512_vs_oracle(gpu, monkeypatch, S, assoc, n):
     got = cv.decode_batch(h, off, obs, dtype="f64", assoc=assoc, rescore_f64=False)
     t = cv.last_timing(h)
     assert t["kernel"] == "trellis_f64" and t["padded_states"] == 512
-    ref = O.decode_batch(pi, a, b, off, obs, {"viterbi": O.VITERBI, "decode": O.DECODE}[assoc], np.float64)
+    ref = O.decode_batch(pi, a, b, off, obs, {"viterbi": O.VITERBI, "decode": O.DECODE, "dp": O.DP}[assoc], np.float64)
     assert np.array_equal(got[2], ref[2])
     assert np.array_equal(got[1], ref[1])
     assert np.array_equal(got[0], ref[0])
