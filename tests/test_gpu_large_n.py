@@ -257,3 +257,20 @@ def test_t64_512_forced_vs_oracle(gpu, monkeypatch, S, n):
     ref = O.decode_batch(pi, a, b, off, obs, O.VITERBI, np.float64, forced=forced)
     for x, y, what in zip(got, ref, ("path", "score", "status")):
         assert np.array_equal(x, y), what
+
+
+def test_generic_rows_f32_rescore(gpu):
+    """f32 generic decode at N > 256 (rows mode) with the default f64 re-score: each score is
+    the oracle's f64 fold along the decoded path, the paths are the f32 oracle's."""
+    n = 333
+    pi, a, b = synth.random_hmm(n, 9, seed=333)
+    rng = np.random.default_rng(333)
+    off = synth.offsets_from_lengths(rng.integers(0, 30, size=24))
+    obs = rng.integers(0, 9, size=int(off[-1])).astype(np.int32)
+    h = cv.HMM(pi, a, b)
+    path, score, status = cv.decode_batch(h, off, obs, dtype="f32")
+    rp, _, rst = O.decode_batch(pi, a, b, off, obs, O.VITERBI, np.float32)
+    assert np.array_equal(path, rp) and np.array_equal(status, rst)
+    for k in range(len(off) - 1):
+        if status[k] == 0:
+            assert score[k] == O.rescore_f64(pi, a, b, obs[off[k]:off[k + 1]], path[off[k]:off[k + 1]])
