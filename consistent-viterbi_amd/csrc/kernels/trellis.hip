@@ -1890,58 +1890,98 @@ template hipError_t launch_generic_bt<float>(const GenericBtArgs<float>&, int64_
 template hipError_t launch_generic_bt<double>(const GenericBtArgs<double>&, int64_t, hipStream_t);
 
 // Generic kernel keeps 2*N REAL delta values in LDS.
-// generic_ext (trellis.h): one workgroup per slot, the two rows in LDS, states strided over
-// the 256 threads; an empty range writes nothing (the host never builds one).
-__global__ __launch_bounds__(256) void generic_ext(GenericExtArgs g) {
-  extern __shared__ __attribute__((aligned(16))) double rows[];  // [2][N]
+// generic_ext<S> (trellis.h): S consecutive slots per workgroup (a segment table's N slots
+// share one range; the terms passes' slots are ragged and finish at their own lengths), each A
+// element loaded once for the S slots, 64 * ceil(N / 64) threads (<= 1,024), the rows in LDS;
+// an empty range writes nothing (the host never builds one).
+template <int S>
+__global__ __launch_bounds__(1024) void generic_ext(GenericExtArgs g, int64_t nslots) {
+  extern __shared__ __attribute__((aligned(16))) double rows[];  // [2][S][N]
   const int N = g.nstates;
-  const int64_t slot = blockIdx.x;
-  const int64_t b0 = g.ranges[2 * slot];
-  const int T = (int)(g.ranges[2 * slot + 1] - b0);
-  if (T <= 0) return;
   const double ninf = -__builtin_inf();
-  auto elem = [&](int t) -> int64_t { return g.reverse ? b0 + T - 1 - t : b0 + t; };
-  {
-    const double* e = g.et + (size_t)g.obs[elem(0)] * N;
-    const int st = g.start ? g.start[slot] : -1;
-    const bool emit = !(g.noemit_last && T == 1);
+  int64_t b0[S];
+  int T[S];
+  int Tmax = 0;
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    const int64_t slot = (int64_t)blockIdx.x * S + s;
+    b0[s] = 0;
+    T[s] = 0;
+    if (slot < nslots) {
+      b0[s] = g.ranges[2 * slot];
+      T[s] = (int)(g.ranges[2 * slot + 1] - b0[s]);
+    }
+    Tmax = T[s] > Tmax ? T[s] : Tmax;
+  }
+  if (Tmax <= 0) return;
+  auto row = [&](int buf, int s) -> double* { return rows + ((size_t)buf * S + s) * N; };
+  auto elem = [&](int s, int t) -> int64_t { return g.reverse ? b0[s] + T[s] - 1 - t : b0[s] + t; };
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    if (T[s] <= 0) continue;
+    const double* e = g.et + (size_t)g.obs[elem(s, 0)] * N;
+    const int st = g.start ? g.start[(int64_t)blockIdx.x * S + s] : -1;
+    const bool emit = !(g.noemit_last && T[s] == 1);
     for (int j = threadIdx.x; j < N; j += blockDim.x)
-      rows[j] = st >= 0 ? (j == st ? 0.0 : ninf) : emit ? g.pi[j] + e[j] : g.pi[j];
+      row(0, s)[j] = st >= 0 ? (j == st ? 0.0 : ninf) : emit ? g.pi[j] + e[j] : g.pi[j];
   }
   __syncthreads();
-  for (int t = 1; t < T; ++t) {
-    const double* prev = rows + ((t - 1) & 1) * N;
-    double* cur = rows + (t & 1) * N;
-    const double* e = g.et + (size_t)g.obs[elem(t)] * N;
-    const bool emit = !(g.noemit_last && t == T - 1);
+  for (int t = 1; t < Tmax; ++t) {
+    const int pb = (t - 1) & 1, cb = t & 1;
+    const double* e[S];
+    bool act[S], emit[S];
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      act[s] = t < T[s];
+      e[s] = act[s] ? g.et + (size_t)g.obs[elem(s, t)] * N : g.et;
+      emit[s] = !(g.noemit_last && t == T[s] - 1);
+    }
     for (int j = threadIdx.x; j < N; j += blockDim.x) {
       const double* col = g.tab + j;
-      double m0 = ninf, m1 = ninf;
-      int i = 0;
-      for (; i + 1 < N; i += 2) {
-        m0 = fmax(m0, prev[i] + col[(size_t)i * N]);
-        m1 = fmax(m1, prev[i + 1] + col[(size_t)(i + 1) * N]);
+      double m[S];
+#pragma unroll
+      for (int s = 0; s < S; ++s) m[s] = ninf;
+      for (int i = 0; i < N; ++i) {
+        const double aij = col[(size_t)i * N];
+#pragma unroll
+        for (int s = 0; s < S; ++s) m[s] = fmax(m[s], row(pb, s)[i] + aij);
       }
-      if (i < N) m0 = fmax(m0, prev[i] + col[(size_t)i * N]);
-      const double m = fmax(m0, m1);
-      cur[j] = emit ? m + e[j] : m;
+#pragma unroll
+      for (int s = 0; s < S; ++s)
+        if (act[s]) row(cb, s)[j] = emit[s] ? m[s] + e[s][j] : m[s];
     }
     __syncthreads();
   }
-  const double* last = rows + ((T - 1) & 1) * N;
-  double* out = g.last_row + slot * (int64_t)N;
-  for (int j = threadIdx.x; j < N; j += blockDim.x) out[j] = last[j];
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    if (T[s] <= 0) continue;
+    const double* last = row((T[s] - 1) & 1, s);
+    double* out = g.last_row + ((int64_t)blockIdx.x * S + s) * N;
+    for (int j = threadIdx.x; j < N; j += blockDim.x) out[j] = last[j];
+  }
+}
+
+template <int S>
+hipError_t launch_generic_ext_s(const GenericExtArgs& g, int64_t nslots, hipStream_t stream) {
+  const size_t lds = 2 * (size_t)S * g.nstates * sizeof(double);
+  if (lds > 64 * 1024)
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&generic_ext<S>), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds);
+  const unsigned threads = (unsigned)std::min(1024, (g.nstates + 63) / 64 * 64);
+  hipLaunchKernelGGL((generic_ext<S>), dim3((unsigned)((nslots + S - 1) / S)), dim3(threads), lds, stream, g, nslots);
+  return hipGetLastError();
 }
 
 hipError_t launch_generic_ext(const GenericExtArgs& g, int64_t nslots, hipStream_t stream) {
   if (nslots <= 0) return hipSuccess;
   if (g.nstates <= 0 || g.nstates > generic_max_states(8)) return hipErrorInvalidValue;
-  const size_t lds = 2 * (size_t)g.nstates * sizeof(double);
-  if (lds > 64 * 1024)
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&generic_ext), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)lds);
-  hipLaunchKernelGGL(generic_ext, dim3((unsigned)nslots), dim3(256), lds, stream, g);
-  return hipGetLastError();
+  // as generic_fwd_ms: 4 slots while their rows fit and the launch keeps >= 2 workgroups per
+  // CU, CV_GENERIC_S=k sets it
+  switch (generic_seqs_per_wg<double>(g.nstates, nslots)) {
+    case 4: return launch_generic_ext_s<4>(g, nslots, stream);
+    case 2: return launch_generic_ext_s<2>(g, nslots, stream);
+    default: return launch_generic_ext_s<1>(g, nslots, stream);
+  }
 }
 
 int generic_max_states(int real_bytes) { return (int)(160 * 1024 / (2 * real_bytes)); }

@@ -88,11 +88,14 @@ def _constrained_case(n, seed, nseq=10, tmax=14, multi=True):
     return pi, a, b, off, obs, comp
 
 
+@pytest.mark.parametrize("S", ["1", "4"])
 @pytest.mark.parametrize("n,multi", [(257, True), (300, False), (400, True), (520, False)])
-def test_constrained_f64_beyond_256(gpu, n, multi):
-    """The constrained decode at N > 256 (generic_ext terms passes + segment tables, host exact
-    sums, generic forced decode) against the oracle spec (np_oracle.constrained_decode): the
-    component states, paths and f64 scores bit for bit, every active element on its state."""
+def test_constrained_f64_beyond_256(gpu, monkeypatch, S, n, multi):
+    """The constrained decode at N > 256 (generic_ext terms passes + segment tables with S
+    slots per workgroup, CV_GENERIC_S; host exact sums; the forced decode) against the oracle
+    spec (np_oracle.constrained_decode): the component states, paths and f64 scores bit for
+    bit, every active element on its state."""
+    monkeypatch.setenv("CV_GENERIC_S", S)
     pi, a, b, off, obs, comp = _constrained_case(n, seed=n, multi=multi)
     h = cv.HMM(pi, a, b)
     path, score, status, states, obj = cv.decode_constrained(h, off, obs, comp, dtype="f64")
