@@ -656,7 +656,7 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
                       (((o.assoc == CV_ASSOC_VITERBI || o.assoc == CV_ASSOC_DECODE || o.assoc == CV_ASSOC_CP ||
                          o.assoc == CV_ASSOC_DP) &&
                         (!(o.forced || resume_rows) || o.assoc == CV_ASSOC_VITERBI) && cvk::t64_padded_states(h->N) != 0) ||
-                       (cvk::t64_batch_states(h->N) == 512 && t512_pick &&
+                       (cvk::t64_batch_states(h->N) >= 512 && (t512_pick || h->N > 512) &&
                         (o.assoc == CV_ASSOC_VITERBI || ((o.assoc == CV_ASSOC_DECODE || o.assoc == CV_ASSOC_DP) && !o.forced)) &&
                         !resume_rows && !cp_cert && !cp_init && !cp_last));
   if (o.kernel == CV_KERNEL_TRELLIS_F64 && !t64_ok)

@@ -1914,7 +1914,30 @@ int t64_padded_states(int n) { return (n >= 1 && n <= 256) ? 64 * ((n + 63) / 64
 int t64_batch_states(int n) {
   if (n <= 256) return t64_padded_states(n);
   const char* e = getenv("CV_T64_512");
-  return (!(e && e[0] == '0') && n <= 512) ? 512 : 0;
+  if (n <= 512) return !(e && e[0] == '0') ? 512 : 0;
+  // 512 < N <= 1,024: QUADS of C = 4 waves, where A (N^2 f64) outgrows an XCD's 4 MiB L2
+  // (N > 724) and the generic kernels turn HBM-bound: 16,384 x 128 at N = 800 188 vs 455 ms,
+  // N = 1,024 191 vs 552 ms; at N = 600 the padding loses (179 vs 139 ms;
+  // profiles/r04_large_n.txt).  A/B knob CV_T64_1024=0 / =1 (read per call): never / always
+  if (n > 1024) return 0;
+  const char* q = getenv("CV_T64_1024");
+  if (q && (q[0] == '0' || q[0] == '1')) return q[0] == '1' ? 1024 : 0;
+  return n > 724 ? 1024 : 0;
+}
+
+template <int S>
+hipError_t fwd_1024(const T64FwdArgs& fa, int64_t nseq, hipStream_t stream) {
+  const dim3 grid((unsigned)((nseq + S - 1) / S)), block(256);
+  if (fa.forced)
+    hipLaunchKernelGGL((trellis_fwd_f64<4, S, 8, false, true, 4>), grid, block, 0, stream, fa);
+  else if (fa.dp_assoc) {
+    if constexpr (S <= 4)
+      hipLaunchKernelGGL((trellis_fwd_f64<4, S, 8, true, false, 4>), grid, block, 0, stream, fa);
+    else
+      return hipErrorInvalidValue;
+  } else
+    hipLaunchKernelGGL((trellis_fwd_f64<4, S, 8, false, false, 4>), grid, block, 0, stream, fa);
+  return hipGetLastError();
 }
 
 template <int S>
@@ -1979,11 +2002,15 @@ hipError_t launch_t64_fwd(int np, int s, const T64FwdArgs& fa_in, int64_t nseq, 
   const bool ext = fa.forced || fa.ranges || fa.reverse || fa.start || fa.row_base || fa.resume_rows ||
                    fa.slot_order || fa.last_row;
   if (np == 64 && wave && !fa.dp_assoc && !ext) return launch_t64_wave(fa, nseq, stream);
-  if (np == 512) {  // batch decode only (t64_batch_states), forced states allowed
+  if (np == 512 || np == 1024) {  // batch decode only (t64_batch_states), forced states allowed
     if (fa.ranges || fa.reverse || fa.start || fa.row_base || fa.resume_rows || fa.slot_order || fa.last_row ||
         (fa.dp_assoc && fa.forced))
       return hipErrorInvalidValue;
     if ((fa.forced || fa.dp_assoc) && s > 4) s = 4;  // EXT at S = 8: 275 VGPRs + 19 AGPRs, one wave per SIMD
+    if (np == 1024) {
+      if (s > 4) s = 4;  // the quad's LDS slice: (NP + 3) x S doubles
+      return s == 4 ? fwd_1024<4>(fa, nseq, stream) : fwd_1024<2>(fa, nseq, stream);
+    }
     switch (s) {
       case 8: return fwd_512<8>(fa, nseq, stream);
       case 4: return fwd_512<4>(fa, nseq, stream);
@@ -2014,6 +2041,12 @@ hipError_t bt_pf_np(int np, const T64BtArgs& ba, dim3 grid, dim3 block, hipStrea
       case 512:
         if constexpr (PF <= 8) {
           hipLaunchKernelGGL((backtrack_f64<8, PF, NONPOS, PERSIST>), grid, block, 0, stream, ba);
+          break;
+        }
+        return hipErrorInvalidValue;
+      case 1024:
+        if constexpr (PF <= 4) {
+          hipLaunchKernelGGL((backtrack_f64<16, PF, NONPOS, PERSIST>), grid, block, 0, stream, ba);
           break;
         }
         return hipErrorInvalidValue;

@@ -277,3 +277,36 @@ def test_generic_rows_f32_rescore(gpu):
     for k in range(len(off) - 1):
         if status[k] == 0:
             assert score[k] == O.rescore_f64(pi, a, b, obs[off[k]:off[k + 1]], path[off[k]:off[k + 1]])
+
+
+@pytest.mark.parametrize("S", ["2", "4"])
+@pytest.mark.parametrize("assoc", ["viterbi", "decode", "dp", "forced"])
+@pytest.mark.parametrize("n", [600, 1024])
+def test_t64_1024_vs_oracle(gpu, monkeypatch, S, assoc, n):
+    """512 < N <= 1,024 on the f64 trellis (NP = 1,024: quads of C = 4 waves, backtrack_f64 at
+    KP = 16; CV_T64_1024=1): paths, scores and statuses bit for bit against the oracle, incl.
+    empty and infeasible sequences and forced states."""
+    monkeypatch.setenv("CV_T64_S", S)
+    monkeypatch.setenv("CV_T64_1024", "1")
+    pi, a, b = synth.random_hmm(n, 13, seed=n + 71, zero_frac=0.05)
+    b = b.copy()
+    b[:, 12] = -np.inf
+    rng = np.random.default_rng(n + int(S))
+    lens = rng.integers(1, 16, size=24)
+    lens[[3, 17]] = 0
+    off = synth.offsets_from_lengths(lens)
+    obs = rng.integers(0, 12, size=int(off[-1])).astype(np.int32)
+    obs[int(off[5]) + lens[5] // 2] = 12
+    forced = None
+    if assoc == "forced":
+        forced = np.where(rng.random(len(obs)) < 0.08, rng.integers(0, n, size=len(obs)), -1).astype(np.int32)
+    ak = "viterbi" if assoc == "forced" else assoc
+    h = cv.HMM(pi, a, b)
+    got = cv.decode_batch(h, off, obs, dtype="f64", assoc=ak, rescore_f64=False, forced=forced)
+    t = cv.last_timing(h)
+    assert t["kernel"] == "trellis_f64" and t["padded_states"] == 1024
+    ref = O.decode_batch(pi, a, b, off, obs, {"viterbi": O.VITERBI, "decode": O.DECODE, "dp": O.DP}[ak], np.float64,
+                         forced=forced)
+    assert np.array_equal(got[2], ref[2])
+    assert np.array_equal(got[1], ref[1])
+    assert np.array_equal(got[0], ref[0])
