@@ -327,6 +327,13 @@ def main():
 
     from cviterbi import dist as cvd
 
+    if world > 1:  # RCCL first-run readiness: one known-value gather + one int64 all-reduce
+        ok, msg = cvd.preflight(dist, dev if args.backend == "nccl" else None, N_STATES)
+        if not ok:
+            print(f"bench.py rank {rank}: collective pre-flight failed ({args.backend}): {msg}", file=sys.stderr, flush=True)
+            dist.destroy_process_group()
+            raise SystemExit(3)
+
     if args.scaling == "weak":  # every rank: its own full batch of the global N x B
         B = args.batch * world
         s0, s1, per = rank * args.batch, (rank + 1) * args.batch, args.batch
@@ -411,6 +418,10 @@ def main():
 
     el, kt, per_rank_s = timed(args.dtype, args.steps, args.warmup)
     fwd_ms, bt_ms, launches = kt["fwd_ms"], kt["bt_ms"], kt["launches"]
+    # every rank's shard kernel times (HIP events on its decode stream): a SCALE line's gap to
+    # linear shows up here as forward / backtrack vs host and gather time
+    kms = [fwd_ms / args.steps, bt_ms / args.steps]
+    kms_ranks = all_gather_floats(kms) if world > 1 else [kms]
     spw = kt.get("seqs_per_wave", 8)  # the layout of the timed run (before the f32 extra)
     # this rank's first sequences as the timed run decoded them (for the CPU baseline's check)
     kc = min(64, nloc)
@@ -546,6 +557,8 @@ def main():
         "per_rank": {"ms_per_step": [x * 1e3 / args.steps for x in per_rank_s],
                      "min_ms_per_step": min(per_rank_s) * 1e3 / args.steps,
                      "max_ms_per_step": max(per_rank_s) * 1e3 / args.steps,
+                     "kernel_ms_per_step": [{"forward": k[0], "backtrack": k[1]} for k in kms_ranks],
+                     "preflight": "gather_packed_to_root + int64 all_reduce checked" if world > 1 else None,
                      "peak_device_gb": [{"torch": m[0], "library": m[1]} for m in mem_ranks],
                      "note": "timed region of the headline dtype; peak device memory over the whole run so far "
                              "(decode workspaces, rank 0's verify decode, the sharded config-5 leg)"},

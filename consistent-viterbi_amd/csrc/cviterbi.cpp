@@ -187,6 +187,7 @@ struct cv_hmm {
   DevBuf q_a, q_at, q_pi, q_et;
   DevBuf q_at32;            // f32(a^T), uploaded when t64_nonpos
   bool t64_nonpos = false;  // every finite pi/a/b entry in [-2^80, 0] (NONPOS backtrack test)
+  int nonpos_cache = -1;    // model_nonpos(): the same predicate without the t64 tables (any N)
   DevBuf q_pi0;  // the reversed (suffix) pass: pi = 0 for the N states, -inf padding
   // f32 generic tables
   bool g32_ready = false;
@@ -405,11 +406,30 @@ cv_status ensure_at32(cv_hmm* h) {
   return upload(h->d_at32, at.data(), at.size() * 4);
 }
 
-// Exact-f64 trellis tables: a [NP][NP] row-major, a^T, pi [NP], et [V][NP]; -inf padded.
+// Every finite pi/a/b entry in [-2^80, 0] (log-probabilities): the NONPOS backtrack test and the
+// parallel chain's certificates hold for such models.  The CV_T64_NONPOS=0 knob forces the
+// general f64 interval test (same paths, bit for bit) and turns the parallel chain off.
+bool model_nonpos(cv_hmm* h) {
+  if (h->nonpos_cache >= 0) return h->nonpos_cache != 0;
+  static const bool nonpos_knob = [] {
+    const char* e = getenv("CV_T64_NONPOS");
+    return !(e && e[0] == '0');
+  }();
+  auto nonpos = [](const std::vector<double>& v) {
+    for (double x : v)
+      if (std::isfinite(x) && !(x <= 0.0 && x >= -0x1p80)) return false;
+    return true;
+  };
+  h->nonpos_cache = nonpos_knob && nonpos(h->pi) && nonpos(h->a) && nonpos(h->b) ? 1 : 0;
+  return h->nonpos_cache != 0;
+}
+
+// Exact-f64 trellis tables: a [NP][NP] row-major, a^T, pi [NP], et [V][NP]; -inf padded to the
+// NP every f64 trellis kernel supports at this N (cvk::t64_support_states: 512 / 1,024 above 256).
 cv_status ensure_t64_tables(cv_hmm* h) {
   if (h->t64_ready) return CV_OK;
-  const int N = h->N, NP = cvk::t64_batch_states(N);
-  if (NP == 0) return set_err(CV_EUNSUPPORTED, "f64 trellis tables need N <= 512 (N=%d)", N);
+  const int N = h->N, NP = cvk::t64_support_states(N);
+  if (NP == 0) return set_err(CV_EUNSUPPORTED, "f64 trellis tables need N <= 1024 (N=%d)", N);
   const int64_t V = h->V;
   const double ninf = -INFINITY;
   std::vector<double> a((size_t)NP * NP, ninf), at((size_t)NP * NP, ninf), pi(NP, ninf), et((size_t)V * NP, ninf);
@@ -430,18 +450,8 @@ cv_status ensure_t64_tables(cv_hmm* h) {
   std::vector<double> pi0(NP, ninf);
   for (int i = 0; i < N; ++i) pi0[i] = 0.0;
   if ((st = upload(h->q_pi0, pi0.data(), pi0.size() * 8)) != CV_OK) return st;
-  // NONPOS backtrack test (trellis64.hip bt_chain_f64): log-probability models only; the
-  // CV_T64_NONPOS=0 knob forces the general f64 interval test (same paths, bit for bit)
-  static const bool nonpos_knob = [] {
-    const char* e = getenv("CV_T64_NONPOS");
-    return !(e && e[0] == '0');
-  }();
-  auto nonpos = [](const std::vector<double>& v) {
-    for (double x : v)
-      if (std::isfinite(x) && !(x <= 0.0 && x >= -0x1p80)) return false;
-    return true;
-  };
-  h->t64_nonpos = nonpos_knob && nonpos(h->pi) && nonpos(h->a) && nonpos(h->b);
+  // NONPOS backtrack test (trellis64.hip bt_chain_f64): log-probability models only
+  h->t64_nonpos = model_nonpos(h);
   if (h->t64_nonpos) {
     std::vector<float> at32(at.size());
     for (size_t k = 0; k < at.size(); ++k) at32[k] = (float)at[k];
@@ -650,20 +660,27 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
   // the padded NP = 512 trellis beats the generic kernels: N >= 384 or >= 8,192 sequences
   // (4,096 x 128: N = 384 15.3 vs 15.8 ms, N = 320 15.4 vs 12.3; 16,384 x 128: N = 320 34.1
   // vs 46.7 ms, N = 512 35.8 vs 84.0 -- profiles/r04_large_n.txt); CV_T64_512=1 forces it
+  // What the f64 trellis SUPPORTS (an explicit CV_KERNEL_TRELLIS_F64 request gets it) is wider
+  // than what AUTO picks: 256 < N <= 512 only for N >= 384 or >= 8,192 sequences, 512 < N <=
+  // 1,024 only above N = 724 (cvk::t64_batch_states; the generic kernels win below)
   const char* t512_env = getenv("CV_T64_512");
   const bool t512_pick = (t512_env && t512_env[0] == '1') || h->N >= 384 || nseq >= 8192;
-  const bool t64_ok = o.dtype == CV_DTYPE_F64 &&
-                      (((o.assoc == CV_ASSOC_VITERBI || o.assoc == CV_ASSOC_DECODE || o.assoc == CV_ASSOC_CP ||
+  const bool small_ok = (o.assoc == CV_ASSOC_VITERBI || o.assoc == CV_ASSOC_DECODE || o.assoc == CV_ASSOC_CP ||
                          o.assoc == CV_ASSOC_DP) &&
-                        (!(o.forced || resume_rows) || o.assoc == CV_ASSOC_VITERBI) && cvk::t64_padded_states(h->N) != 0) ||
-                       (cvk::t64_batch_states(h->N) >= 512 && (t512_pick || h->N > 512) &&
-                        (o.assoc == CV_ASSOC_VITERBI || ((o.assoc == CV_ASSOC_DECODE || o.assoc == CV_ASSOC_DP) && !o.forced)) &&
-                        !resume_rows && !cp_cert && !cp_init && !cp_last));
+                        (!(o.forced || resume_rows) || o.assoc == CV_ASSOC_VITERBI) && cvk::t64_padded_states(h->N) != 0;
+  const bool big_ok = cvk::t64_support_states(h->N) >= 512 &&
+                      (o.assoc == CV_ASSOC_VITERBI || ((o.assoc == CV_ASSOC_DECODE || o.assoc == CV_ASSOC_DP) && !o.forced)) &&
+                      !resume_rows && !cp_init && !cp_last;
+  const bool big_pick = cvk::t64_batch_states(h->N) >= 512 && (t512_pick || h->N > 512);
+  const bool t64_ok = o.dtype == CV_DTYPE_F64 && (small_ok || big_ok);
   if (o.kernel == CV_KERNEL_TRELLIS_F64 && !t64_ok)
     return set_err(CV_EUNSUPPORTED,
-                   "f64 trellis kernel needs dtype f64, N <= 256, and forced states only with assoc VITERBI");
+                   "f64 trellis kernel needs dtype f64 and N <= 1024; above N = 256 only the VITERBI, DECODE and DP "
+                   "associations, forced states only with VITERBI (N=%d, assoc %d)",
+                   h->N, o.assoc);
   const bool use_t64 = !use_trellis && t64_ok &&
-                       (o.kernel == CV_KERNEL_TRELLIS_F64 || (o.kernel == CV_KERNEL_AUTO && !(o.flags & CV_FLAG_NO_T64)));
+                       (o.kernel == CV_KERNEL_TRELLIS_F64 ||
+                        (o.kernel == CV_KERNEL_AUTO && !(o.flags & CV_FLAG_NO_T64) && (small_ok || big_pick)));
   if (!use_trellis && !use_t64 && h->N > cvk::generic_max_states(o.dtype == CV_DTYPE_F64 ? 8 : 4))
     return set_err(CV_EUNSUPPORTED, "N=%d exceeds the generic kernel's LDS capacity", h->N);
 
@@ -715,6 +732,8 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
   // (profiles/r04_large_n.txt)
   const char* gr_env = getenv("CV_GENERIC_ROWS");
   const bool gen_rows = !use_trellis && !use_t64 && o.assoc != CV_ASSOC_CP && !(gr_env && *gr_env == '0');
+  if (cp_cert && !use_t64 && !(gen_rows && o.dtype == CV_DTYPE_F64))
+    return set_err(CV_EUNSUPPORTED, "chain certificates need the f64 trellis or the generic kernels' rows mode");
   if (gen_rows && (st = o.dtype == CV_DTYPE_F64 ? ensure_at64(h) : ensure_at32(h)) != CV_OK) return st;
   const uint64_t per_elem = use_trellis ? (uint64_t)(wave ? h->npw : h->np) * 4
                            : (use_t64 && !t64cp) ? (uint64_t)h->np64 * 8
@@ -941,7 +960,9 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
       fa.forced = o.forced;
       fa.resume_rows = static_cast<const double*>(resume_rows);
       const int spw = cvk::t64_seqs_per_wave(n, h->cus);
-      if (!side_ws) h->last_mt = (t64cp || fa.dp_assoc) ? std::min(spw, 4) : spw;
+      // the S actually launched: CP / DP, NP = 1,024 and forced NP = 512 run S <= 4 (launch_t64_fwd)
+      if (!side_ws)
+        h->last_mt = (t64cp || fa.dp_assoc || h->np64 == 1024 || (h->np64 == 512 && o.forced)) ? std::min(spw, 4) : spw;
       {  // eight-wave workgroups: equal lengths (within 1/8), or >= 2 rounds of 64 x CUs
          // (ragged T in [32, 1024], chunks of 32,768: 158 vs 168 ms; one round, 16,384: 65.5
          // vs 56 ms -- profiles/r03_ab_wg.txt)
@@ -987,6 +1008,8 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
       fa.last_row = reinterpret_cast<double*>(lrb);
       fa.status = status_dev;
       fa.forced = o.forced;
+      fa.cp_init = cp_init;  // the parallel chain's speculative re-decodes (N > 256)
+      fa.cp_last = cp_last;
       if (gen_rows) fa.rows = reinterpret_cast<double*>(wsb);
       err = cvk::launch_generic_fwd<double>(fa, n, stream);
     } else {
@@ -1086,6 +1109,21 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
         ba.nobs = (int)h->V;
       }
       err = gen_rows ? cvk::launch_generic_bt_rows<double>(ba, n, bts) : cvk::launch_generic_bt<double>(ba, n, bts);
+      if (err == hipSuccess && cp_cert) {  // the parallel chain (N > 256): certificates over the plain rows
+        cvk::CpCert64Args ca{};
+        ca.delta = reinterpret_cast<const double*>(wsb);
+        ca.delta_elem_base = offsets_host[c.first];
+        ca.at = h->d_at64.as<double>();
+        ca.offsets = offsets_dev;
+        ca.order = order_dev;
+        ca.seq_begin = c.first;
+        ca.seq_end = c.second;
+        ca.nstates = h->N;
+        ca.path = path_dev;
+        ca.status = status_dev;
+        ca.out = cp_cert;
+        err = cvk::launch_cp_cert_plain(ca, bts);
+      }
     } else {
       cvk::GenericBtArgs<float> ba{};
       ba.psi = reinterpret_cast<const uint16_t*>(wsb);
@@ -2824,9 +2862,8 @@ namespace {
 // last element: pass 1 maps every segment's last-element state to the state before it for all
 // NP states (cp_chain_seg_map), the host follows the maps from the end state, pass 2 writes
 // each segment's path into path_dev[0, L).
-cv_status chain_backtrack(cv_hmm* h, const uint16_t* psi, int64_t L, int32_t end_state, int32_t* path_dev,
+cv_status chain_backtrack(int NP, const uint16_t* psi, int64_t L, int32_t end_state, int32_t* path_dev,
                           hipStream_t stream) {
-  const int NP = h->np64;
   // segments: ~8,192 of them (>= 256 elements each) for the parallel passes
   const int64_t seg = std::max<int64_t>(256, (L + 8191) / 8192);
   const int64_t nseg = (L + seg - 1) / seg;
@@ -2905,7 +2942,7 @@ cv_status superseq_cp_wg(cv_hmm* h, int64_t L, const int32_t* obs, const std::ve
   *objective_out = out[0];
   int32_t fs;
   std::memcpy(&fs, &out[1], 4);
-  if ((st = chain_backtrack(h, d_psi.as<uint16_t>(), L, fs, d_path.as<int32_t>(), stream)) != CV_OK) return st;
+  if ((st = chain_backtrack(NP, d_psi.as<uint16_t>(), L, fs, d_path.as<int32_t>(), stream)) != CV_OK) return st;
   HIP_TRY(hipMemcpyAsync(path_out, d_path.p, (size_t)L * 4, hipMemcpyDeviceToHost, stream));
   HIP_TRY(hipStreamSynchronize(stream));
   if (!(*objective_out > -INFINITY))
@@ -2935,8 +2972,12 @@ cv_status superseq_cp_wg(cv_hmm* h, int64_t L, const int32_t* obs, const std::ve
 //     consecutive such sequences form one run, backtracked from the state the next sequence's
 //     boundary picks.
 // Bit-identical to the serial chain by construction (tests: the serial chain, CV_CHAIN_PAR=0,
-// and the C oracle cvo_cp_superseq_f64).  Models with entries outside [-2^80, 0], infeasible
-// sequences or N > 256: *applied = false (the caller runs the serial chain).
+// and the C oracle cvo_cp_superseq_f64).  Models with entries outside [-2^80, 0] or infeasible
+// sequences: *applied = false (the caller runs the serial chain).
+// Any N (round 5): N <= 256 on the padded f64 trellis + trellis_cp_f64 + cp_chain_wg; above
+// that, step 1 runs whatever row-A0 f64 decode the batch path picks (the NP = 512 / 1,024
+// trellis or the generic kernels' rows mode, both with certificates), speculation the generic
+// CP kernel, and the runs cp_superseq_chain (one thread per state) with the segmented backtrack.
 // Knobs (bit-identical): CV_CHAIN_PAR=0 (serial chain), CV_CHAIN_PAR_FORCE=m (every m-th
 // non-empty sequence taken as uncertified: exercises speculation and the runs), CV_CHAIN_SPEC=0
 // (no speculation: every uncertified sequence through the serial chain kernel).
@@ -2944,9 +2985,12 @@ cv_status superseq_cp_par(cv_hmm* h, int64_t nseq, const int64_t* offsets, const
                           double* objective_out, bool* applied) {
   *applied = false;
   cv_status st;
-  if ((st = ensure_t64_tables(h)) != CV_OK) return st;
-  if (!h->t64_nonpos || !cvk::t64_padded_states(h->N)) return CV_OK;
-  const int N = h->N, NP = h->np64;
+  const int N = h->N;
+  const bool small = cvk::t64_padded_states(N) != 0;  // N <= 256: padded tables, cp_chain_wg runs
+  if (small && (st = ensure_t64_tables(h)) != CV_OK) return st;
+  if ((st = ensure_f64_tables(h)) != CV_OK) return st;
+  if (!model_nonpos(h)) return CV_OK;
+  const int W = small ? h->np64 : N;  // row width of the runs (psi rows, start / last rows)
   const int64_t V = h->V;
   const int64_t base = offsets[0], L = offsets[nseq] - base;
   hipStream_t stream = h->stream;
@@ -2969,12 +3013,13 @@ cv_status superseq_cp_par(cv_hmm* h, int64_t nseq, const int64_t* offsets, const
   cv_opts o = default_opts();
   o.dtype = CV_DTYPE_F64;
   o.assoc = CV_ASSOC_VITERBI;
-  o.kernel = CV_KERNEL_TRELLIS_F64;
+  o.kernel = small ? CV_KERNEL_TRELLIS_F64 : CV_KERNEL_AUTO;  // N > 256: the batch path's own pick
   o.rescore_f64 = 0;
   o.stream = stream;
-  if ((st = decode_device(h, nseq, off.data(), d_off.as<int64_t>(), d_obs.as<int32_t>(), o, d_path.as<int32_t>(),
-                          d_score, d_status, stream, nullptr, false, d_cert.as<double>())) != CV_OK)
-    return st;
+  st = decode_device(h, nseq, off.data(), d_off.as<int64_t>(), d_obs.as<int32_t>(), o, d_path.as<int32_t>(), d_score,
+                     d_status, stream, nullptr, false, d_cert.as<double>());
+  if (st == CV_EUNSUPPORTED && !small) return CV_OK;  // no rows to certify (CV_GENERIC_ROWS=0): serial chain
+  if (st != CV_OK) return st;
   std::vector<double> score((size_t)nseq), cert((size_t)nseq * 2);
   std::vector<uint8_t> status((size_t)nseq);
   HIP_TRY(hipMemcpyAsync(path_out, d_path.p, (size_t)L * 4, hipMemcpyDeviceToHost, stream));
@@ -3008,10 +3053,10 @@ cv_status superseq_cp_par(cv_hmm* h, int64_t nseq, const int64_t* offsets, const
   HIP_TRY(hipMemcpyAsync(d_ebin.p, ebin.data(), (size_t)nseq * 4, hipMemcpyHostToDevice, stream));
   {
     cvk::CpQuant64Args qa{};
-    qa.a = h->q_a.as<double>();
-    qa.pi = h->q_pi.as<double>();
-    qa.et = h->q_et.as<double>();
-    qa.np = NP;
+    qa.a = small ? h->q_a.as<double>() : h->d_a64.as<double>();
+    qa.pi = small ? h->q_pi.as<double>() : h->d_pi64.as<double>();
+    qa.et = small ? h->q_et.as<double>() : h->d_et64.as<double>();
+    qa.np = W;
     qa.offsets = d_off.as<int64_t>();
     qa.obs = d_obs.as<int32_t>();
     qa.path = d_path.as<int32_t>();
@@ -3075,12 +3120,12 @@ cv_status superseq_cp_par(cv_hmm* h, int64_t nseq, const int64_t* offsets, const
 
   // The state of the chain before the sequence at hand: NONE (first sequence), CERT (a certified
   // sequence ended in prev_end with maximum M, a clean boundary), ROW (the exact last row is
-  // known: row_host, NP wide, -inf padded; on the device at row_dev when non-null).
+  // known: row_host, W wide, -inf padded; on the device at row_dev when non-null).
   enum Kind { NONE, CERT, ROW };
   Kind prev = NONE;
   int32_t prev_end = 0, row_arg = 0;
   double M = 0.0;
-  std::vector<double> row_host((size_t)NP, -INFINITY), syn((size_t)NP);
+  std::vector<double> row_host((size_t)W, -INFINITY), syn((size_t)W);
   const double* row_dev = nullptr;
   // the last row is clean for a start whose values reach magnitude `mag`: no earlier state's
   // value can round onto its maximum when pi[j] is added (utils.rs:32-35)
@@ -3111,17 +3156,17 @@ cv_status superseq_cp_par(cv_hmm* h, int64_t nseq, const int64_t* offsets, const
   if ((st = d_first.ensure((size_t)std::max<int64_t>(maxT, 1))) != CV_OK) return st;
   HIP_TRY(hipMemsetAsync(d_first.p, 0, (size_t)std::max<int64_t>(maxT, 1), stream));
   HIP_TRY(hipMemsetAsync(d_first.p, 1, 1, stream));  // one sequence per launch: its element 0 starts it
-  if ((st = d_rows.ensure((size_t)NP * 8 * 3)) != CV_OK) return st;
+  if ((st = d_rows.ensure((size_t)W * 8 * 3)) != CV_OK) return st;
   if ((st = d_small.ensure(16)) != CV_OK) return st;
   double* row_in = d_rows.as<double>();  // start row uploaded from the host
-  double* row_a = row_in + NP;           // the run's last rows (ping-pong)
-  double* row_b = row_a + NP;
+  double* row_a = row_in + W;            // the run's last rows (ping-pong)
+  double* row_b = row_a + W;
   bool in_run = false;
   int64_t run_e0 = 0, run_len = 0, runs = 0, run_seqs = 0, ncert = 0, nquant = 0, spec_acc = 0, spec_batches = 0;
   int64_t psi_cap = 0;
   auto end_run = [&](int32_t end_state) -> cv_status {
     if ((st = d_rpath.ensure((size_t)run_len * 4)) != CV_OK) return st;
-    if ((st = chain_backtrack(h, d_rpsi.as<uint16_t>(), run_len, end_state, d_rpath.as<int32_t>(), stream)) != CV_OK)
+    if ((st = chain_backtrack(W, d_rpsi.as<uint16_t>(), run_len, end_state, d_rpath.as<int32_t>(), stream)) != CV_OK)
       return st;
     HIP_TRY(hipMemcpyAsync(path_out + run_e0, d_rpath.p, (size_t)run_len * 4, hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipStreamSynchronize(stream));
@@ -3134,11 +3179,11 @@ cv_status superseq_cp_par(cv_hmm* h, int64_t nseq, const int64_t* offsets, const
     if (prev == CERT) {  // what a clean boundary after a certified sequence sees
       std::fill(syn.begin(), syn.end(), -INFINITY);
       syn[(size_t)prev_end] = M;
-      HIP_TRY(hipMemcpyAsync(row_in, syn.data(), (size_t)NP * 8, hipMemcpyHostToDevice, stream));
+      HIP_TRY(hipMemcpyAsync(row_in, syn.data(), (size_t)W * 8, hipMemcpyHostToDevice, stream));
       init = row_in;
     } else if (prev == ROW) {
       if (!row_dev) {  // a speculative decode's last row: the exact row, uploaded
-        HIP_TRY(hipMemcpyAsync(row_in, row_host.data(), (size_t)NP * 8, hipMemcpyHostToDevice, stream));
+        HIP_TRY(hipMemcpyAsync(row_in, row_host.data(), (size_t)W * 8, hipMemcpyHostToDevice, stream));
         row_dev = row_in;
       }
       init = row_dev;
@@ -3152,34 +3197,54 @@ cv_status superseq_cp_par(cv_hmm* h, int64_t nseq, const int64_t* offsets, const
     if (run_len + T > psi_cap) {  // grow the run's psi rows (rare: long runs)
       const int64_t cap = std::max<int64_t>(2 * psi_cap, std::max<int64_t>(run_len + T, 4 * maxT));
       DevBuf nb;
-      if ((st = nb.ensure((size_t)cap * NP * 2)) != CV_OK) return st;
+      if ((st = nb.ensure((size_t)cap * W * 2)) != CV_OK) return st;
       if (run_len > 0)
-        HIP_TRY(hipMemcpyAsync(nb.p, d_rpsi.p, (size_t)run_len * NP * 2, hipMemcpyDeviceToDevice, stream));
+        HIP_TRY(hipMemcpyAsync(nb.p, d_rpsi.p, (size_t)run_len * W * 2, hipMemcpyDeviceToDevice, stream));
       HIP_TRY(hipStreamSynchronize(stream));
       std::swap(nb.p, d_rpsi.p);
       std::swap(nb.bytes, d_rpsi.bytes);
       psi_cap = cap;
     }
-    if (!init) HIP_TRY(hipMemsetAsync(d_rpsi.as<uint16_t>() + run_len * NP, 0, (size_t)NP * 2, stream));
-    cvk::CpChainWgArgs g{};
-    g.pi = h->q_pi.as<double>();
-    g.a = h->q_a.as<double>();
-    g.et = h->q_et.as<double>();
-    g.obs = d_obs.as<int32_t>() + e0;
-    g.first = d_first.as<uint8_t>();
-    g.len = T;
-    g.nstates = N;
-    g.psi = d_rpsi.as<uint16_t>() + run_len * NP;
-    g.objective = d_small.as<double>();
-    g.final_state = reinterpret_cast<int32_t*>(d_small.as<double>() + 1);
-    g.init_row = init;
+    if (!init) HIP_TRY(hipMemsetAsync(d_rpsi.as<uint16_t>() + run_len * W, 0, (size_t)W * 2, stream));
     double* out_row = init == row_a ? row_b : row_a;
-    g.final_row = out_row;
-    const hipError_t err = cvk::launch_cp_chain_wg(NP, g, stream);
+    hipError_t err;
+    if (small) {
+      cvk::CpChainWgArgs g{};
+      g.pi = h->q_pi.as<double>();
+      g.a = h->q_a.as<double>();
+      g.et = h->q_et.as<double>();
+      g.obs = d_obs.as<int32_t>() + e0;
+      g.first = d_first.as<uint8_t>();
+      g.len = T;
+      g.nstates = N;
+      g.psi = d_rpsi.as<uint16_t>() + run_len * W;
+      g.objective = d_small.as<double>();
+      g.final_state = reinterpret_cast<int32_t*>(d_small.as<double>() + 1);
+      g.init_row = init;
+      g.final_row = out_row;
+      err = cvk::launch_cp_chain_wg(W, g, stream);
+    } else {  // N > 256: one thread per state (cp_superseq_chain), the unpadded f64 tables
+      cvk::CpChainArgs g{};
+      g.pi = h->d_pi64.as<double>();
+      g.a = h->d_a64.as<double>();
+      g.et = h->d_et64.as<double>();
+      g.obs = d_obs.as<int32_t>() + e0;
+      g.first = d_first.as<uint8_t>();
+      g.len = T;
+      g.nstates = N;
+      g.nobs = (int)V;
+      g.psi = d_rpsi.as<uint16_t>() + run_len * W;
+      g.path = nullptr;
+      g.objective = d_small.as<double>();
+      g.final_state = reinterpret_cast<int32_t*>(d_small.as<double>() + 1);
+      g.init_row = init;
+      g.final_row = out_row;
+      err = cvk::launch_cp_superseq_chain(g, stream);
+    }
     if (err != hipSuccess) return set_err(CV_EDEVICE, "chain run launch failed: %s", hipGetErrorString(err));
     double out[2];
     HIP_TRY(hipMemcpyAsync(out, d_small.p, 16, hipMemcpyDeviceToHost, stream));
-    HIP_TRY(hipMemcpyAsync(row_host.data(), out_row, (size_t)NP * 8, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipMemcpyAsync(row_host.data(), out_row, (size_t)W * 8, hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipStreamSynchronize(stream));
     row_dev = out_row;
     M = out[0];
@@ -3245,7 +3310,7 @@ cv_status superseq_cp_par(cv_hmm* h, int64_t nseq, const int64_t* offsets, const
     cv_opts oc = default_opts();
     oc.dtype = CV_DTYPE_F64;
     oc.assoc = CV_ASSOC_CP;
-    oc.kernel = CV_KERNEL_TRELLIS_F64;
+    oc.kernel = small ? CV_KERNEL_TRELLIS_F64 : CV_KERNEL_GENERIC;  // trellis_cp_f64 / generic_fwd_ms (psi)
     oc.rescore_f64 = 0;
     oc.stream = stream;
     double* sc = d_sres.as<double>();
@@ -3361,14 +3426,15 @@ CV_API cv_status cv_decode_superseq_cp(cv_hmm* h, int64_t nseq, const int64_t* o
   std::vector<uint8_t> first((size_t)L, 0);
   for (int64_t q = 0; q < nseq; ++q)
     if (offsets[q + 1] > offsets[q]) first[(size_t)(offsets[q] - base)] = 1;
-  // N <= 256: the one-workgroup chain with the candidates split over its waves and A on chip
-  // (kernels/chain.hip), then the parallel segmented backtrack; N > 256 (or CV_CHAIN_OLD=1, an
-  // A/B knob, bit-identical): one thread per state (cp_superseq_chain)
+  // The parallel chain (any N, log-probability models); else serially: N <= 256 the
+  // one-workgroup chain with the candidates split over its waves and A on chip
+  // (kernels/chain.hip), N > 256 (or CV_CHAIN_OLD=1, an A/B knob, bit-identical) one thread per
+  // state (cp_superseq_chain); both then the parallel segmented backtrack
   const char* old_env = getenv("CV_CHAIN_OLD");
   const char* par_env = getenv("CV_CHAIN_PAR");  // read per call: tests flip it within one process
   h->last_chain[0] = 0;
   for (int q = 1; q < 7; ++q) h->last_chain[q] = 0;
-  if (cvk::t64_padded_states(h->N) && !(old_env && *old_env == '1') && !(par_env && *par_env == '0')) {
+  if (!(old_env && *old_env == '1') && !(par_env && *par_env == '0')) {
     bool applied = false;
     st = superseq_cp_par(h, nseq, offsets, obs, path_out, objective_out, &applied);
     if (st != CV_OK || applied) return st;
@@ -3382,7 +3448,7 @@ CV_API cv_status cv_decode_superseq_cp(cv_hmm* h, int64_t nseq, const int64_t* o
   if ((st = d_first.ensure((size_t)L)) != CV_OK) return st;
   if ((st = d_psi.ensure((size_t)L * h->N * 2)) != CV_OK) return st;
   if ((st = d_path.ensure((size_t)L * 4)) != CV_OK) return st;
-  if ((st = d_obj.ensure(8)) != CV_OK) return st;
+  if ((st = d_obj.ensure(16)) != CV_OK) return st;
   HIP_TRY(hipMemcpyAsync(d_obs.p, obs + base, (size_t)L * 4, hipMemcpyHostToDevice, stream));
   HIP_TRY(hipMemcpyAsync(d_first.p, first.data(), (size_t)L, hipMemcpyHostToDevice, stream));
   cvk::CpChainArgs g{};
@@ -3395,12 +3461,19 @@ CV_API cv_status cv_decode_superseq_cp(cv_hmm* h, int64_t nseq, const int64_t* o
   g.nstates = h->N;
   g.nobs = (int)h->V;
   g.psi = d_psi.as<uint16_t>();
-  g.path = d_path.as<int32_t>();
+  g.path = nullptr;  // the segmented backtrack below (a single-thread walk was one dependent load per element)
   g.objective = d_obj.as<double>();
+  g.final_state = reinterpret_cast<int32_t*>(d_obj.as<double>() + 1);
   const hipError_t err = cvk::launch_cp_superseq_chain(g, stream);
   if (err != hipSuccess) return set_err(CV_EDEVICE, "super-sequence chain launch failed: %s", hipGetErrorString(err));
+  double out[2];
+  HIP_TRY(hipMemcpyAsync(out, d_obj.p, 16, hipMemcpyDeviceToHost, stream));
+  HIP_TRY(hipStreamSynchronize(stream));
+  *objective_out = out[0];
+  int32_t fs;
+  std::memcpy(&fs, &out[1], 4);
+  if ((st = chain_backtrack(h->N, d_psi.as<uint16_t>(), L, fs, d_path.as<int32_t>(), stream)) != CV_OK) return st;
   HIP_TRY(hipMemcpyAsync(path_out, d_path.p, (size_t)L * 4, hipMemcpyDeviceToHost, stream));
-  HIP_TRY(hipMemcpyAsync(objective_out, d_obj.p, 8, hipMemcpyDeviceToHost, stream));
   HIP_TRY(hipStreamSynchronize(stream));
   if (!(*objective_out > -INFINITY))
     return set_err(CV_EINFEASIBLE, "no finite-probability path through the super-sequence (cp.rs:87 asserts)");

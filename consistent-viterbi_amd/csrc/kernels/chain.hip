@@ -18,6 +18,8 @@
 // the state before its first element for ALL NP states at once (one lane per state); the
 // host walks the segment maps from the final state; pass 2 writes every segment's path.
 #include "chain.h"
+
+#include <algorithm>
 #include "trellis.h"
 #include "trellis64.h"
 #include "wave64.h"
@@ -341,6 +343,118 @@ __global__ __launch_bounds__(256) void cp_quant_f64(CpQuant64Args g) {
   }
 }
 
+// N > 256 (the serial chain's runs, cp_superseq_chain): the two backtrack passes above with a
+// runtime row width and psi read straight from global memory (no LDS staging: a row of u16 at
+// N = 10,240 is 20 KiB).  pass 1: thread j walks segment k's state j down to e0.
+__global__ __launch_bounds__(1024) void cp_chain_seg_map_g(CpChainBtArgs g) {
+  const int64_t k = (int64_t)blockIdx.x + 1;
+  const int64_t e0 = k * g.seg, e1 = e0 + g.seg < g.len ? e0 + g.seg : g.len;
+  const int np = g.np;
+  for (int j = threadIdx.x; j < np; j += blockDim.x) {
+    int cs = j;
+    for (int64_t t = e1 - 1; t >= e0; --t) cs = g.psi[t * np + cs];
+    g.map[k * np + j] = (uint16_t)cs;
+  }
+}
+
+// pass 2: one thread per segment follows psi from its resolved end state (cp.rs:88-92)
+__global__ __launch_bounds__(64) void cp_chain_seg_path_g(CpChainBtArgs g) {
+  const int64_t k = (int64_t)blockIdx.x * 64 + threadIdx.x;
+  if (k >= g.nseg) return;
+  const int64_t e0 = k * g.seg, e1 = e0 + g.seg < g.len ? e0 + g.seg : g.len;
+  int cs = g.end_state[k];
+  for (int64_t t = e1 - 1; t >= e0; --t) {
+    g.path[t] = cs;
+    cs = g.psi[t * g.np + cs];
+  }
+}
+
+// cp_cert_f64 for N > 256: the same certificate (rho, gF) over the rows of any row-A0 decode --
+// SPLIT: the f64 trellis's split-plane rows (NP = 512 / 1,024, width W = NP, a^T [NP][NP]);
+// otherwise the generic kernels' plain f64 rows (width W = N, a^T [N][N]).  Each lane keeps the
+// top two of its candidates i = lane + 64 k (first index on ties: a later equal candidate
+// becomes the runner-up, gap 0); the wave's maximum, its lane and the best OTHER value follow
+// (a tie across lanes leaves the runner-up equal to the maximum: gap 0, no certificate -- the
+// only case where the arg below is not the first index, and then the result fails anyway).
+template <bool SPLIT>
+__global__ __launch_bounds__(256) void cp_cert_rows(CpCert64Args g, int W) {
+  const int lane = threadIdx.x & 63;
+  const int64_t slot = g.seq_begin + (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (slot >= g.seq_end) return;
+  const int64_t seq = g.order ? (int64_t)g.order[slot] : slot;
+  const int64_t e0 = g.offsets[seq];
+  const int T = (int)(g.offsets[seq + 1] - e0);
+  if (T <= 0 || g.status[seq] != CVK_SEQ_OK) {
+    if (lane == 0) g.out[2 * seq] = -1.0, g.out[2 * seq + 1] = -1.0;
+    return;
+  }
+  const int N = g.nstates;
+  const int64_t r0 = e0 - g.delta_elem_base;
+  auto rowval = [&](int r, int i) -> double {
+    if constexpr (SPLIT) {
+      const uint32_t* row = reinterpret_cast<const uint32_t*>(g.delta) + (r0 + r) * (int64_t)(2 * W);
+      return from_words(__builtin_nontemporal_load(row + i), __builtin_nontemporal_load(row + W + i));
+    } else {
+      return __builtin_nontemporal_load(g.delta + (r0 + r) * (int64_t)W + i);
+    }
+  };
+  auto finish = [&](double m1l, int a1l, double m2l, int& arg, double& m1, double& m2) {
+    m1 = wave_max_d_dpp(m1l);
+    const unsigned long long mask = __ballot(a1l >= 0 && m1l == m1);
+    const int wl = mask ? __builtin_ctzll(mask) : 0;
+    arg = mask ? __shfl(a1l, wl) : -1;
+    m2 = wave_max_d_dpp((mask && lane == wl) ? m2l : m1l);
+  };
+  int arg;
+  double m1, m2;
+  {
+    double a = -__builtin_inf(), b = -__builtin_inf();
+    int ia = -1;
+#pragma unroll 4
+    for (int i = lane; i < N; i += 64) {
+      const double x = rowval(T - 1, i);
+      if (x > a) {
+        b = a;
+        a = x;
+        ia = i;
+      } else {
+        b = fmax(b, x);
+      }
+    }
+    finish(a, ia, b, arg, m1, m2);
+  }
+  const int32_t* __restrict__ path = g.path + e0;
+  const double u0 = (__builtin_fabs(m1) + 16.0) * 0x1p-51;
+  bool ok = m1 > (-__builtin_inf()) && arg == path[T - 1];
+  const double gF = m1 - m2 - 4.0 * (double)T * u0;  // +inf when the row has one finite entry
+  double rho = gF / (double)(3 * T + 2);
+  for (int t = T - 1; ok && t >= 1; --t) {
+    const int j = path[t], p = path[t - 1];
+    const double* __restrict__ acol = g.at + (size_t)j * W;
+    double a = -__builtin_inf(), b = -__builtin_inf();
+    int ia = -1;
+#pragma unroll 4
+    for (int i = lane; i < N; i += 64) {
+      const double x = rowval(t - 1, i) + acol[i];
+      if (x > a) {
+        b = a;
+        a = x;
+        ia = i;
+      } else {
+        b = fmax(b, x);
+      }
+    }
+    finish(a, ia, b, arg, m1, m2);
+    ok = arg == p && m1 > (-__builtin_inf());  // the path's predecessor is the strict first argmax
+    rho = fmin(rho, (m1 - m2 - (double)(4 * t + 1) * u0) / (double)(3 * t + 1));
+  }
+  if (lane == 0) {
+    const bool pass = ok && rho > 0.0;
+    g.out[2 * seq] = pass ? rho * (1.0 - 0x1p-50) : -1.0;
+    g.out[2 * seq + 1] = pass ? gF * (1.0 - 0x1p-50) : -1.0;
+  }
+}
+
 }  // namespace
 
 size_t cp_chain_wg_lds(int np) {
@@ -372,7 +486,9 @@ hipError_t launch_cp_chain_seg_map(const CpChainBtArgs& g, hipStream_t stream) {
     case 128: hipLaunchKernelGGL(cp_chain_seg_map<128>, grid, dim3(128), 0, stream, g); break;
     case 192: hipLaunchKernelGGL(cp_chain_seg_map<192>, grid, dim3(192), 0, stream, g); break;
     case 256: hipLaunchKernelGGL(cp_chain_seg_map<256>, grid, dim3(256), 0, stream, g); break;
-    default: return hipErrorInvalidValue;
+    default:
+      if (g.np <= 0 || g.np > kChainMaxStates) return hipErrorInvalidValue;
+      hipLaunchKernelGGL(cp_chain_seg_map_g, grid, dim3((unsigned)std::min(1024, (g.np + 63) / 64 * 64)), 0, stream, g);
   }
   return hipGetLastError();
 }
@@ -385,7 +501,9 @@ hipError_t launch_cp_chain_seg_path(const CpChainBtArgs& g, hipStream_t stream) 
     case 128: hipLaunchKernelGGL(cp_chain_seg_path<128>, grid, dim3(64), 0, stream, g); break;
     case 192: hipLaunchKernelGGL(cp_chain_seg_path<192>, grid, dim3(64), 0, stream, g); break;
     case 256: hipLaunchKernelGGL(cp_chain_seg_path<256>, grid, dim3(64), 0, stream, g); break;
-    default: return hipErrorInvalidValue;
+    default:
+      if (g.np <= 0 || g.np > kChainMaxStates) return hipErrorInvalidValue;
+      hipLaunchKernelGGL(cp_chain_seg_path_g, dim3((unsigned)((g.nseg + 63) / 64)), dim3(64), 0, stream, g);
   }
   return hipGetLastError();
 }
@@ -399,8 +517,17 @@ hipError_t launch_cp_cert(int np, const CpCert64Args& a, hipStream_t stream) {
     case 128: hipLaunchKernelGGL(cp_cert_f64<2>, grid, block, 0, stream, a); break;
     case 192: hipLaunchKernelGGL(cp_cert_f64<3>, grid, block, 0, stream, a); break;
     case 256: hipLaunchKernelGGL(cp_cert_f64<4>, grid, block, 0, stream, a); break;
+    case 512:
+    case 1024: hipLaunchKernelGGL(cp_cert_rows<true>, grid, block, 0, stream, a, np); break;
     default: return hipErrorInvalidValue;
   }
+  return hipGetLastError();
+}
+
+hipError_t launch_cp_cert_plain(const CpCert64Args& a, hipStream_t stream) {
+  const int64_t n = a.seq_end - a.seq_begin;
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(cp_cert_rows<false>, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, stream, a, a.nstates);
   return hipGetLastError();
 }
 

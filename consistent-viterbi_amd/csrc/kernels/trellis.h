@@ -96,6 +96,11 @@ struct GenericFwdArgs {
   // only the maximum (2 VALU per pair instead of 4), generic_bt_rows recomputes the argmax
   // along the path
   REAL* rows;
+  // CP only (the parallel chain's speculative re-decodes, N > 256): cp_init [nseq] = offset M
+  // of each sequence (row 0 = fl(M + fl(pi + b)): a chain entered with running maximum M),
+  // cp_last [nseq][N] = each sequence's last row, by sequence id (null: not used / written)
+  const REAL* cp_init;
+  REAL* cp_last;
 };
 
 template <typename REAL>

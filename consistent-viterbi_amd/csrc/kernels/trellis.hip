@@ -1110,7 +1110,7 @@ __global__ __launch_bounds__(256) void generic_fwd(GenericFwdArgs<REAL> args) {
       else if (assoc == CVK_ASSOC_DP)
         d = (e > ninf) ? (REAL)(args.pi[j] + e) : ninf;
       else
-        d = args.pi[j] + e;
+        d = args.cp_init ? args.cp_init[seq] + (args.pi[j] + e) : args.pi[j] + e;
       if (args.forced && args.forced[e0] >= 0 && j != args.forced[e0]) d = ninf;
       dbuf[j] = d;
     }
@@ -1164,6 +1164,8 @@ __global__ __launch_bounds__(256) void generic_fwd(GenericFwdArgs<REAL> args) {
   const REAL* last = dbuf + ((T - 1) & 1) * N;
   REAL* lastout = args.last_row + (slot - args.seq_begin) * (int64_t)N;
   for (int j = threadIdx.x; j < N; j += blockDim.x) lastout[j] = last[j];
+  if (args.cp_last)
+    for (int j = threadIdx.x; j < N; j += blockDim.x) args.cp_last[seq * N + j] = last[j];
   if (bad && threadIdx.x == 0) args.status[seq] = CVK_SEQ_BADOBS;
 }
 
@@ -1222,7 +1224,7 @@ __global__ __launch_bounds__(1024) void generic_fwd_ms(GenericFwdArgs<REAL> args
       else if (assoc == CVK_ASSOC_DP)
         d = (e > ninf) ? (REAL)(args.pi[j] + e) : ninf;
       else
-        d = args.pi[j] + e;
+        d = args.cp_init ? args.cp_init[seq[s]] + (args.pi[j] + e) : args.pi[j] + e;
       if (fs >= 0 && j != fs) d = ninf;
       d0[j] = d;
       if constexpr (ROWS) grow(s, 0)[j] = d;
@@ -1328,6 +1330,8 @@ __global__ __launch_bounds__(1024) void generic_fwd_ms(GenericFwdArgs<REAL> args
     const REAL* last = row((T[s] - 1) & 1, s);
     REAL* lastout = args.last_row + (slot[s] - args.seq_begin) * (int64_t)N;
     for (int j = threadIdx.x; j < N; j += blockDim.x) lastout[j] = last[j];
+    if (args.cp_last)
+      for (int j = threadIdx.x; j < N; j += blockDim.x) args.cp_last[seq[s] * N + j] = last[j];
     if ((bad >> s) & 1 && threadIdx.x == 0) args.status[seq[s]] = CVK_SEQ_BADOBS;
   }
 }

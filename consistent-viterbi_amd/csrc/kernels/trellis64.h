@@ -1,4 +1,4 @@
-// trellis64.h -- exact-f64 trellis kernels for N <= 256 (trellis64.hip).
+// trellis64.h -- exact-f64 trellis kernels for N <= 1,024 (trellis64.hip).
 // Internal to libcviterbi; the public boundary is include/cviterbi.h.
 #pragma once
 #include <hip/hip_runtime.h>
@@ -139,7 +139,7 @@ hipError_t launch_t64_mu_add(const double* delta, const double* beta, double* mu
 hipError_t launch_t64_resume_rows(const double* last, const int32_t* state, int64_t n, int np, double* out,
                                   hipStream_t stream);
 
-// Parallel CPSolver chain (cv_decode_superseq_cp, N <= 256, log-probability models): the
+// Parallel CPSolver chain (cv_decode_superseq_cp, log-probability models): the
 // certificate of each sequence's row-A0 path at offset 0 (cp_cert_f64) and the quantised CP
 // fold of a certified path at a predicted binade (cp_quant_f64).  See trellis64.hip.
 struct CpCert64Args {
@@ -154,7 +154,11 @@ struct CpCert64Args {
   const uint8_t* status;
   double* out;             // [nseq_total][2]: rho, gF (-1: not certifiable)
 };
+// np: the f64 trellis's NP (64..256 in registers; 512 / 1,024: the split-plane rows of the
+// column-split pairs / quads of waves)
 hipError_t launch_cp_cert(int np, const CpCert64Args& a, hipStream_t stream);
+// the same certificate over the generic kernels' plain f64 rows [elem][N] (a.at = a^T [N][N])
+hipError_t launch_cp_cert_plain(const CpCert64Args& a, hipStream_t stream);
 constexpr int CVK_NO_BINADE = -0x7fffffff;
 struct CpQuant64Args {
   const double* a;         // [NP][NP] (t64 tables)
@@ -181,8 +185,14 @@ struct CpChainArgs {
   int64_t len;
   int nstates, nobs;
   uint16_t* psi;         // [len][N] workspace
-  int32_t* path;         // [len]
+  int32_t* path;         // [len]; null: no in-kernel backtrack (the caller runs chain_backtrack)
   double* objective;     // [1]
+  // a PART of the chain (the parallel chain's fallback runs, N > 256): init_row [N] = the
+  // chain's row before element 0 (element 0 then runs like any element, psi row 0 included);
+  // final_row [N] receives the last row, final_state [1] its first argmax.  All optional.
+  const double* init_row;
+  double* final_row;
+  int32_t* final_state;
 };
 // the chain's two rows in LDS (2 N doubles <= 160 KiB); psi is u16
 constexpr int kChainMaxStates = 10240;
@@ -190,9 +200,13 @@ hipError_t launch_cp_superseq_chain(const CpChainArgs& g, hipStream_t stream);
 
 // NP = 64 * ceil(N / 64) for 1 <= N <= 256, else 0 (no f64 trellis kernel)
 int t64_padded_states(int n);
-// the batch decode's NP (VITERBI / DECODE, no forced states): t64_padded_states, or 512 for
-// 256 < N <= 512 (column-split pairs of waves); 0 = the generic kernels
+// the batch decode's NP under CV_KERNEL_AUTO: t64_padded_states, 512 for 256 < N <= 512
+// (column-split pairs of waves), 1,024 for 724 < N <= 1,024 (quads; CV_T64_512 / CV_T64_1024
+// knobs); 0 = the generic kernels
 int t64_batch_states(int n);
+// every NP the kernels support at this N (64..256 padded, 512, 1,024; 0 above): what an
+// explicit CV_KERNEL_TRELLIS_F64 request gets and what the handle's t64 tables are padded to
+int t64_support_states(int n);
 // sequences per forward wave (2, 4 or 8) for a launch of nseq sequences on `cus` CUs
 int t64_seqs_per_wave(int64_t nseq, int cus);
 hipError_t launch_t64_fwd(int np, int s, const T64FwdArgs& fa, int64_t nseq, hipStream_t stream);

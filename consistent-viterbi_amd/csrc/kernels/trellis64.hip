@@ -1925,6 +1925,13 @@ int t64_batch_states(int n) {
   return n > 724 ? 1024 : 0;
 }
 
+// every NP the f64 trellis kernels support at this N (an explicit CV_KERNEL_TRELLIS_F64
+// request, and the handle's padded tables): 64 * ceil(N / 64) up to 256, then 512 and 1,024
+int t64_support_states(int n) {
+  if (n <= 256) return t64_padded_states(n);
+  return n <= 512 ? 512 : n <= 1024 ? 1024 : 0;
+}
+
 template <int S>
 hipError_t fwd_1024(const T64FwdArgs& fa, int64_t nseq, hipStream_t stream) {
   const dim3 grid((unsigned)((nseq + S - 1) / S)), block(256);
@@ -2187,9 +2194,10 @@ __global__ __launch_bounds__(1024) void cp_superseq_chain(CpChainArgs g) {
     A = la;
   }
   // N > 1024: thread j owns states j, j + 1024, ... (each state's candidate loop is its own)
-  for (int j = threadIdx.x; j < N; j += blockDim.x) prev[j] = g.pi[j] + g.et[(size_t)g.obs[0] * N + j];  // cp.rs:66-68
+  for (int j = threadIdx.x; j < N; j += blockDim.x)  // cp.rs:66-68, or the row before this part
+    prev[j] = g.init_row ? g.init_row[j] : g.pi[j] + g.et[(size_t)g.obs[0] * N + j];
   __syncthreads();
-  for (int64_t t = 1; t < L; ++t) {
+  for (int64_t t = g.init_row ? 0 : 1; t < L; ++t) {
     const int o = g.obs[t];
     const bool first = g.first[t] != 0;
     for (int j = threadIdx.x; j < N; j += blockDim.x) {
@@ -2213,6 +2221,8 @@ __global__ __launch_bounds__(1024) void cp_superseq_chain(CpChainArgs g) {
     prev = cur;
     cur = tmp;
   }
+  if (g.final_row)
+    for (int j = threadIdx.x; j < N; j += blockDim.x) g.final_row[j] = prev[j];
   if (threadIdx.x == 0) {
     int cs = 0;
     double obj = prev[0];
@@ -2222,10 +2232,12 @@ __global__ __launch_bounds__(1024) void cp_superseq_chain(CpChainArgs g) {
         cs = i;
       }
     *g.objective = obj;
-    for (int64_t t = L - 1; t >= 0; --t) {
-      g.path[t] = cs;
-      cs = g.psi[t * N + cs];
-    }
+    if (g.final_state) *g.final_state = cs;
+    if (g.path)
+      for (int64_t t = L - 1; t >= 0; --t) {
+        g.path[t] = cs;
+        cs = g.psi[t * N + cs];
+      }
   }
 }
 

@@ -145,3 +145,52 @@ def constrained_decode_sharded(hmm, offsets, obs, component, ncomp, dist, device
     # sequential sum in sequence order, as cv_decode_constrained does (CV_SEQ_INFEASIBLE = 1)
     objective = float(np.cumsum(np.where(status == 1, -np.inf, score))[-1]) if B else 0.0
     return path, score, status, states, objective
+
+
+def preflight(dist, device=None, nstates=256, corrupt=None):
+    """First-run check of the two collectives bench.py relies on, right after
+    init_process_group: ONE packed gather (gather_packed_to_root, the decode's result path) of
+    known per-rank values, and ONE int64 all-reduce SUM (allreduce_partials, the config-5
+    exchange) of known words incl. values above 2^53.  Every rank learns the outcome (an
+    all-reduce MIN of the per-rank verdicts), so all ranks fail together.  Returns
+    (True, "") or (False, message naming the collective and the rank that saw it fail).
+    corrupt: test hook ("gather" / "allreduce") that perturbs rank 1's contribution.
+    Contract: main.rs:129-133 writes one output line per element; a gather that silently
+    dropped or reordered a rank would break it, so the bench exits before timing anything."""
+    import torch
+
+    world, rank = dist.get_world_size(), dist.get_rank()
+    dev = device or "cpu"
+    seq_cap, elem_cap = 3, 7
+    n_el = elem_cap - (rank % 2)  # ragged: odd ranks one element short (padded by the gather)
+    path = torch.tensor([(rank * 13 + k) % nstates for k in range(n_el)], dtype=torch.int32, device=dev)
+    score = torch.tensor([-(rank + 0.25) * 10.0 ** k for k in range(seq_cap)], dtype=torch.float64, device=dev)
+    status = torch.tensor([(rank + k) % 4 for k in range(seq_cap)], dtype=torch.uint8, device=dev)
+    if corrupt == "gather" and rank == 1:
+        path = path.clone()
+        path[0] += 1
+    problems = []
+    g = gather_packed_to_root(path, score, status, nstates, elem_cap, seq_cap, dist)
+    if rank == 0:
+        for r, (p, sc, st) in enumerate(g):
+            ne = elem_cap - (r % 2)
+            want_p = torch.tensor([(r * 13 + k) % nstates for k in range(ne)], dtype=torch.int32)
+            want_s = torch.tensor([-(r + 0.25) * 10.0 ** k for k in range(seq_cap)], dtype=torch.float64)
+            want_st = torch.tensor([(r + k) % 4 for k in range(seq_cap)], dtype=torch.uint8)
+            if not (torch.equal(p[:ne].cpu(), want_p) and torch.equal(sc.cpu().view(torch.int64), want_s.view(torch.int64))
+                    and torch.equal(st.cpu(), want_st)):
+                problems.append(f"gather_packed_to_root: rank {r}'s part arrived wrong at rank 0")
+    words = np.array([rank + 1, (1 << 60) + rank, -(1 << 55) * (rank + 1), 7 * rank - 3], np.int64)
+    if corrupt == "allreduce" and rank == 1:
+        words[1] += 1
+    got = allreduce_partials(words, dist, dev if dev != "cpu" else None)
+    rs = np.arange(world, dtype=np.int64)
+    want = np.array([(rs + 1).sum(), (1 << 60) * world + rs.sum(), -(1 << 55) * (rs + 1).sum(), (7 * rs - 3).sum()],
+                    np.int64)
+    if not np.array_equal(got, want):
+        problems.append(f"all_reduce(int64 SUM): rank {rank} got {got.tolist()}, expected {want.tolist()}")
+    ok = torch.tensor([0 if problems else 1], dtype=torch.int64, device=dev)
+    dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    if int(ok.item()) == 1:
+        return True, ""
+    return False, "; ".join(problems) if problems else f"rank {rank}: another rank's collective check failed"

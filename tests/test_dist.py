@@ -226,3 +226,39 @@ def test_constrained_select_limb_carries():
         best = max(cand, key=lambda s: (exact[c, s], -s))
         assert states[c] == best
     assert ex == n * ncomp
+
+
+def _preflight_worker(rank, world, port, corrupt, q):
+    sys.path.insert(0, os.path.join(ROOT, "consistent-viterbi_amd"))
+    import torch.distributed as dist
+
+    from cviterbi import dist as cvd
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    ok, msg = cvd.preflight(dist, None, 256, corrupt=corrupt)
+    q.put((rank, ok, msg))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,corrupt", [(2, None), (3, None), (2, "gather"), (3, "allreduce")])
+def test_collective_preflight(world, corrupt):
+    """bench.py's RCCL first-run check (cviterbi.dist.preflight) over gloo: known values through
+    the packed gather and an int64 all-reduce (incl. words above 2^53); a perturbed contribution
+    on rank 1 makes EVERY rank report failure, the message naming the collective."""
+    ctx = mp.get_context("spawn")
+    q = ctx.SimpleQueue()
+    port = _free_port()
+    procs = [ctx.Process(target=_preflight_worker, args=(r, world, port, corrupt, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get() for _ in range(world))
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    assert all(ok == (corrupt is None) for _, ok, _ in res), res
+    if corrupt == "gather":
+        assert "gather_packed_to_root: rank 1" in res[0][2], res
+    if corrupt == "allreduce":
+        assert all("all_reduce" in m or "another rank" in m for _, _, m in res), res

@@ -183,3 +183,67 @@ def test_chain_par_not_applicable(gpu):
     with pytest.raises(cv.CVError, match="INFEASIBLE"):
         cv.decode_superseq_cp(h3, off, obs)
     assert not cv.last_superseq_stats(h3)["parallel"]
+
+
+# ---- N > 256 (round 5): the parallel chain on the batch path's own row-A0 decode ----------
+# N = 300 / 600 (small batches) run the generic kernels' rows mode, N = 512 the NP = 512 f64
+# trellis (split-plane rows), N = 1,024 the NP = 1,024 quads; speculation runs the generic CP
+# kernel (cp_init / cp_last), the runs cp_superseq_chain with the segmented backtrack.
+
+@pytest.mark.parametrize("n", [300, 512, 600, 1024])
+def test_chain_par_large_n_equals_oracle(gpu, n):
+    """Ragged lengths incl. empty and one-element sequences: the oracle's chain element by
+    element and the objective, with the row-A0 kernel the batch path picks at this N."""
+    pi, a, b, off, obs = _case(n, 17, 30, 1, 40, seed=4500 + n, zeros=(3, 17), ones=(5, 21))
+    h = cv.HMM(pi, a, b)
+    (path, obj), st = _par(h, off, obs)
+    assert st["parallel"] and st["certified"] >= 20, st
+    rp, robj = O.cp_superseq_f64(pi, a, b, off, obs)
+    assert obj == robj
+    bad = np.nonzero(path != rp)[0]
+    assert bad.size == 0, f"elements {bad[:10]} of {len(rp)}; {st}"
+
+
+@pytest.mark.parametrize("spec", [True, False])
+@pytest.mark.parametrize("n,force", [(300, 2), (512, 3), (600, 1), (1024, 2)])
+def test_chain_par_large_n_forced_runs(gpu, n, force, spec):
+    """CV_CHAIN_PAR_FORCE=m above N = 256: speculation through the generic CP kernel (start
+    offsets, last rows by sequence), or the serial runs of cp_superseq_chain from a synthetic or
+    exact start row (m = 1: the whole chain in one run) -- the oracle's chain either way."""
+    pi, a, b, off, obs = _case(n, 11, 16, 1, 30, seed=4600 + n + force, zeros=(2,), ones=(7,))
+    h = cv.HMM(pi, a, b)
+    (path, obj), st = _par(h, off, obs, force=force, spec=spec)
+    assert st["parallel"] and st["rerun"] + st["speculated"] >= 1, st
+    if spec:
+        assert st["spec_batches"] >= 1 and st["speculated"] >= 1, st
+    else:
+        assert st["speculated"] == 0 and st["rerun"] >= 1, st
+    rp, robj = O.cp_superseq_f64(pi, a, b, off, obs)
+    assert obj == robj and np.array_equal(path, rp), st
+
+
+@pytest.mark.parametrize("n", [512, 1024])
+def test_chain_par_large_n_vs_serial(gpu, n):
+    """1,024 sequences of 96 at N = 512 / 1,024 (a config-4-like model): the parallel chain equals
+    the serial chain kernel (cp_superseq_chain) bit for bit, nearly every sequence certified."""
+    pi, a, b = synth.random_hmm(n, 64, seed=4700 + n)
+    off = synth.offsets_from_lengths(np.full(1024, 96))
+    obs = synth.iid_obs(64, int(off[-1]), 4700 + n)
+    h = cv.HMM(pi, a, b)
+    (path, obj), st = _par(h, off, obs)
+    sp, sobj = _serial(h, off, obs)
+    assert st["parallel"] and st["certified"] + st["rerun"] + st["speculated"] == 1024, st
+    assert st["certified"] >= 950, st
+    assert obj == sobj
+    bad = np.nonzero(path != sp)[0]
+    assert bad.size == 0, f"elements {bad[:10]}; {st}"
+
+
+def test_chain_serial_large_n_segmented_backtrack(gpu):
+    """The serial chain above N = 256 now backtracks through the segmented passes (runtime row
+    width, psi from global memory): > 256 elements per segment, several segments -- the oracle."""
+    pi, a, b, off, obs = _case(300, 9, 12, 200, 400, seed=4800)
+    h = cv.HMM(pi, a, b)
+    sp, sobj = _serial(h, off, obs)
+    rp, robj = O.cp_superseq_f64(pi, a, b, off, obs)
+    assert sobj == robj and np.array_equal(sp, rp)

@@ -310,3 +310,41 @@ def test_t64_1024_vs_oracle(gpu, monkeypatch, S, assoc, n):
     assert np.array_equal(got[2], ref[2])
     assert np.array_equal(got[1], ref[1])
     assert np.array_equal(got[0], ref[0])
+
+
+@pytest.mark.parametrize("n", [300, 600])
+def test_t64_explicit_request_below_auto_pick(gpu, n):
+    """An explicit kernel='trellis_f64' gets the f64 trellis wherever it exists (N <= 1,024),
+    not only where AUTO picks it: N = 300 with 100 sequences (AUTO: generic) and N = 600 (AUTO:
+    generic, NP = 1,024 on request) -- bit for bit the generic kernel's results."""
+    pi, a, b = synth.random_hmm(n, 21, seed=n + 900, zero_frac=0.05)
+    rng = np.random.default_rng(n + 900)
+    off = synth.offsets_from_lengths(rng.integers(0, 20, size=100))
+    obs = rng.integers(0, 21, size=int(off[-1])).astype(np.int32)
+    h = cv.HMM(pi, a, b)
+    got = cv.decode_batch(h, off, obs, dtype="f64", kernel="trellis_f64", rescore_f64=False)
+    t = cv.last_timing(h)
+    assert t["kernel"] == "trellis_f64" and t["padded_states"] == (512 if n <= 512 else 1024)
+    auto = cv.decode_batch(h, off, obs, dtype="f64", rescore_f64=False)
+    assert cv.last_timing(h)["kernel"] == "generic"
+    for x, y, what in zip(got, auto, ("path", "score", "status")):
+        assert np.array_equal(x, y), what
+
+
+def test_t64_1024_equal_batch_chunks_vs_generic(gpu, monkeypatch):
+    """NP = 1,024 quads on a large equal-length batch (S = 8 clamped to 4, many workgroups) with a
+    small workspace forcing several chunks (8 KiB of rows per element): the generic kernel's
+    results bit for bit, and last_timing reports the S actually launched."""
+    n = 900
+    pi, a, b = synth.random_hmm(n, 32, seed=901)
+    off = synth.offsets_from_lengths(np.full(32768, 12))
+    obs = synth.iid_obs(32, int(off[-1]), 901)
+    h = cv.HMM(pi, a, b)
+    # two chunks of 16,384 sequences (8 KiB of split-plane rows per element): S = 8 picked, 4 run
+    got = cv.decode_batch(h, off, obs, dtype="f64", rescore_f64=False, workspace_bytes=16384 * 12 * 8192)
+    t = cv.last_timing(h)
+    assert t["kernel"] == "trellis_f64" and t["padded_states"] == 1024 and t["seqs_per_wave"] == 4
+    assert t["launches"] >= 2, t
+    ref = cv.decode_batch(h, off, obs, dtype="f64", kernel="generic", rescore_f64=False)
+    for x, y, what in zip(got, ref, ("path", "score", "status")):
+        assert np.array_equal(x, y), what

@@ -205,7 +205,7 @@ int main() {
     std::vector<double> hs((size_t)ntile * 256), hc((size_t)ntile * 256);
     (void)hipMemcpy(hs.data(), ds, hs.size() * 8, hipMemcpyDeviceToHost);
     (void)hipMemcpy(hc.data(), dc, hc.size() * 8, hipMemcpyDeviceToHost);
-    long bad_s = 0, bad_c = 0, ninf = 0, sub = 0;
+    long bad_s = 0, bad_c = 0, ninf = 0, sub = 0, zsign_s = 0, zsign_c = 0;
     for (int t = 0; t < ntile; ++t)
       for (int i = 0; i < 16; ++i)
         for (int j = 0; j < 16; ++j) {
@@ -214,17 +214,27 @@ int main() {
           const double gs = hs[(size_t)t * 256 + i * 16 + j], gc = hc[(size_t)t * 256 + i * 16 + j];
           ninf += std::isinf(ref);
           sub += ref != 0.0 && std::fabs(ref) < 2.2250738585072014e-308;
+          // -0 + -0 = -0 in IEEE; the MFMA adds its zero products / zero C (+0) too: +0.  The
+          // model tables are canonicalised to +0 (cv_hmm_create), so the trellis never sees it
           if (std::memcmp(&gs, &ref, 8) != 0) {
-            if (bad_s < 5) printf("  sum form: x=%a y=%a ref=%a mfma=%a\n", (double)xi, (double)yj, ref, gs);
-            ++bad_s;
+            if (ref == 0.0 && gs == 0.0) {
+              ++zsign_s;
+            } else {
+              if (bad_s < 5) printf("  sum form: x=%a y=%a ref=%a mfma=%a\n", (double)xi, (double)yj, ref, gs);
+              ++bad_s;
+            }
           }
           if (std::memcmp(&gc, &ref, 8) != 0) {
-            if (bad_c < 5) printf("  C form:   x=%a y=%a ref=%a mfma=%a\n", (double)xi, (double)yj, ref, gc);
-            ++bad_c;
+            if (ref == 0.0 && gc == 0.0) {
+              ++zsign_c;
+            } else {
+              if (bad_c < 5) printf("  C form:   x=%a y=%a ref=%a mfma=%a\n", (double)xi, (double)yj, ref, gc);
+              ++bad_c;
+            }
           }
         }
-    printf("exactness over %d sums (%ld -inf, %ld subnormal): sum form %ld differ, C form %ld differ\n", ntile * 256,
-           ninf, sub, bad_s, bad_c);
+    printf("exactness over %d sums (%ld -inf, %ld subnormal): sum form %ld differ (+%ld -0 vs +0), C form %ld differ "
+           "(+%ld -0 vs +0)\n", ntile * 256, ninf, sub, bad_s, zsign_s, bad_c, zsign_c);
   }
 
   // ---- 2. rates, alone
