@@ -959,7 +959,7 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
       fa.dp_assoc = o.assoc == CV_ASSOC_DP ? 1 : 0;
       fa.forced = o.forced;
       fa.resume_rows = static_cast<const double*>(resume_rows);
-      const int spw = cvk::t64_seqs_per_wave(n, h->cus);
+      const int spw = cvk::t64_seqs_per_wave(n, h->cus, h->np64);
       // the S actually launched: CP / DP, NP = 1,024 and forced NP = 512 run S <= 4 (launch_t64_fwd)
       if (!side_ws)
         h->last_mt = (t64cp || fa.dp_assoc || h->np64 == 1024 || (h->np64 == 512 && o.forced)) ? std::min(spw, 4) : spw;

@@ -208,7 +208,7 @@ int t64_batch_states(int n);
 // explicit CV_KERNEL_TRELLIS_F64 request gets and what the handle's t64 tables are padded to
 int t64_support_states(int n);
 // sequences per forward wave (2, 4 or 8) for a launch of nseq sequences on `cus` CUs
-int t64_seqs_per_wave(int64_t nseq, int cus);
+int t64_seqs_per_wave(int64_t nseq, int cus, int np = 0);
 hipError_t launch_t64_fwd(int np, int s, const T64FwdArgs& fa, int64_t nseq, hipStream_t stream);
 // N <= 64 row-A0 decodes of NONPOS models: forward and backtrack in one launch (each wave
 // backtracks its own sequence after its forward pass); t64_wave_fusable says when it applies

@@ -1974,16 +1974,20 @@ hipError_t fwd_512(const T64FwdArgs& fa, int64_t nseq, hipStream_t stream) {
   return hipGetLastError();
 }
 
-int t64_seqs_per_wave(int64_t nseq, int cus) {
+int t64_seqs_per_wave(int64_t nseq, int cus, int np) {
   // fill at least two waves per SIMD (4 SIMDs per CU), then prefer the larger S: each A row
-  // streamed from L2 serves S sequences
+  // streamed from L2 serves S sequences.  NP = 512 / 1,024 units are pairs / quads of waves
+  // over the same S sequences (W = NP / 256 waves each), so W times fewer sequences fill the
+  // chip: at NP = 1,024, where A (8 MiB) streams from beyond an XCD's L2 every step, S = 2
+  // doubled that stream (4,096 x 512 at N = 1,024: ~0.8 s forward at S = 2)
   if (const char* e = getenv("CV_T64_S")) {  // tuning knob (bit-identical for every value)
     const int s = atoi(e);
     if (s == 2 || s == 4 || s == 6 || s == 8) return s;
   }
+  const int64_t w = np >= 512 ? np / 256 : 1;
   const int64_t simd_waves = 2 * 4 * (int64_t)(cus > 0 ? cus : 256);
-  if (nseq >= 8 * simd_waves) return 8;
-  if (nseq >= 4 * simd_waves) return 4;
+  if (nseq * w >= 8 * simd_waves) return 8;
+  if (nseq * w >= 4 * simd_waves) return 4;
   return 2;
 }
 

@@ -180,12 +180,13 @@ def preflight(dist, device=None, nstates=256, corrupt=None):
             if not (torch.equal(p[:ne].cpu(), want_p) and torch.equal(sc.cpu().view(torch.int64), want_s.view(torch.int64))
                     and torch.equal(st.cpu(), want_st)):
                 problems.append(f"gather_packed_to_root: rank {r}'s part arrived wrong at rank 0")
-    words = np.array([rank + 1, (1 << 60) + rank, -(1 << 55) * (rank + 1), 7 * rank - 3], np.int64)
+    # above 2^53 (not representable in f64) but summing within int64 for up to 32 ranks
+    words = np.array([rank + 1, (1 << 57) + rank, -(1 << 55) - rank, 7 * rank - 3], np.int64)
     if corrupt == "allreduce" and rank == 1:
         words[1] += 1
     got = allreduce_partials(words, dist, dev if dev != "cpu" else None)
     rs = np.arange(world, dtype=np.int64)
-    want = np.array([(rs + 1).sum(), (1 << 60) * world + rs.sum(), -(1 << 55) * (rs + 1).sum(), (7 * rs - 3).sum()],
+    want = np.array([(rs + 1).sum(), (1 << 57) * world + rs.sum(), -(1 << 55) * world - rs.sum(), (7 * rs - 3).sum()],
                     np.int64)
     if not np.array_equal(got, want):
         problems.append(f"all_reduce(int64 SUM): rank {rank} got {got.tolist()}, expected {want.tolist()}")

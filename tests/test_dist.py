@@ -242,11 +242,12 @@ def _preflight_worker(rank, world, port, corrupt, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,corrupt", [(2, None), (3, None), (2, "gather"), (3, "allreduce")])
+@pytest.mark.parametrize("world,corrupt", [(2, None), (3, None), (8, None), (2, "gather"), (3, "allreduce")])
 def test_collective_preflight(world, corrupt):
     """bench.py's RCCL first-run check (cviterbi.dist.preflight) over gloo: known values through
     the packed gather and an int64 all-reduce (incl. words above 2^53); a perturbed contribution
-    on rank 1 makes EVERY rank report failure, the message naming the collective."""
+    on rank 1 makes EVERY rank report failure, the message naming the collective.  World 8 is
+    the driver's SCALE node (round 5: a 2^60-based word overflowed int64 there)."""
     ctx = mp.get_context("spawn")
     q = ctx.SimpleQueue()
     port = _free_port()

@@ -5,7 +5,8 @@ serial chain kernel (cp_superseq_chain, CV_CHAIN_PAR=0) on config-4-shaped input
 
   python tools/bench_chain_large_n.py N [nseq=4096] [nseq_par_only=0]
 
-nseq_par_only > 0 adds a parallel-only run over that many sequences (config-4 size: 65,536).
+nseq_par_only > 0 adds a parallel-only run over that many sequences (config-4 size: 65,536);
+SERIAL=0 skips the serial comparison (and that run).
 """
 import os
 import sys
@@ -60,6 +61,9 @@ def main():
           f"objective {o1!r}, stats {s1}", flush=True)
     p2, o2, t2, _ = run(h, off, obs)
     print(f"  again: {t2*1e3:.1f} ms, same result {bool(np.array_equal(p1, p2) and o1 == o2)}", flush=True)
+    if os.environ.get("SERIAL", "1") == "0":
+        print("  (serial comparison skipped: SERIAL=0)", flush=True)
+        return
     print(f"  serial chain (cp_superseq_chain, one thread per state) over the same {L} elements ...", flush=True)
     p0, o0, t0, s0 = run(h, off, obs, serial=True)
     same = bool(np.array_equal(p1, p0) and o1 == o0)
