@@ -344,7 +344,11 @@ __global__ __launch_bounds__(NP * 4) void trellis_fwd_f32(TrellisFwdArgs args) {
 // forced states (FRC: the consistency-constrained final decode) -- no other EXT features;
 // the host pairs equal-length sequences and runs leftovers through trellis_fwd_f32.
 // NP % 64 == 0 so that the delta blocks are whole float4s.
-template <int NP, bool FRC>
+// ONEBAR (round 5): one workgroup barrier per STEP instead of per half-step.  Each sequence
+// keeps its own double-buffered delta, so X(t) only needs X(t-1) complete (the barrier closing
+// step t-1) and Y(t) only Y(t-1) (same barrier); the price is that Y(t) can no longer prefetch
+// X's delta_t (not complete until the barrier), so that block is read right after it.
+template <int NP, bool FRC, bool ONEBAR = false>
 __global__ __launch_bounds__(NP * 4) void trellis_fwd2_f32(TrellisFwdArgs args) {
   using G = TrellisGeom<NP>;
   constexpr int R = G::R;
@@ -471,6 +475,7 @@ __global__ __launch_bounds__(NP * 4) void trellis_fwd2_f32(TrellisFwdArgs args) 
   // half-step's (row o_load); then o_load <- obs(t_obs) of the sequence `is_y`.
   auto half = [&](const float* dsrc, const float* nsrc, float* ldst, float* drow, int t, const float& e_use,
                   float& e_load, unsigned& o_load, bool is_y, int t_obs) {
+    const bool sync = !ONEBAR || is_y;  // ONEBAR: the barrier closes the step (after Y)
     const int f_use = f_nx;
     e_load = et_row(o_load);
     if (KB > 1) ld8(dsrc + 8, Q);
@@ -501,7 +506,7 @@ __global__ __launch_bounds__(NP * 4) void trellis_fwd2_f32(TrellisFwdArgs args) 
       __builtin_amdgcn_sched_barrier(0);
       if (k + 2 < KB)
         ld8(dsrc + 8 * (k + 2), B);
-      else if (!(k & 1) && (k + 2 == KB || k + 1 == KB))
+      else if (!(k & 1) && (k + 2 == KB || k + 1 == KB) && !(ONEBAR && is_y))
         ld8(nsrc, P);  // next half-step's block 0 (KB odd: no adds left to hide it)
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -521,7 +526,8 @@ __global__ __launch_bounds__(NP * 4) void trellis_fwd2_f32(TrellisFwdArgs args) 
       float* row = drow + (size_t)t * NP;  // uniform
       row[jw] = dn;
     }
-    lds_barrier();
+    if (sync) lds_barrier();
+    if (ONEBAR && is_y) ld8(nsrc, P);  // X's delta_t, complete since the barrier
   };
   // step t: X(t) prefetches Y's delta_{t-1} and loads e_Y(t); Y(t) prefetches X's delta_t and
   // loads e_X(t+1)
@@ -1760,16 +1766,26 @@ int trellis_padded_states(int n) {
     default: return hipErrorInvalidValue; \
   }
 
+constexpr bool kF32OneBarDefault = false;
+
 template <int NP>
 static hipError_t trellis_fwd2_np(const TrellisFwdArgs& fa, int64_t npairs, hipStream_t stream) {
   if constexpr (NP % 64 != 0) {
     return hipErrorInvalidValue;
   } else {
     if (fa.ranges || fa.reverse || fa.last_row || fa.start || !fa.delta) return hipErrorInvalidValue;
-    if (fa.forced)
-      hipLaunchKernelGGL((trellis_fwd2_f32<NP, true>), dim3((unsigned)npairs), dim3(NP * 4), 0, stream, fa);
+    // A/B knob CV_F32_ONEBAR=0/1 (bit-identical; read per launch)
+    const char* e = getenv("CV_F32_ONEBAR");
+    const bool onebar = e ? e[0] == '1' : kF32OneBarDefault;
+    const dim3 grid((unsigned)npairs), block(NP * 4);
+    if (fa.forced && onebar)
+      hipLaunchKernelGGL((trellis_fwd2_f32<NP, true, true>), grid, block, 0, stream, fa);
+    else if (fa.forced)
+      hipLaunchKernelGGL((trellis_fwd2_f32<NP, true, false>), grid, block, 0, stream, fa);
+    else if (onebar)
+      hipLaunchKernelGGL((trellis_fwd2_f32<NP, false, true>), grid, block, 0, stream, fa);
     else
-      hipLaunchKernelGGL((trellis_fwd2_f32<NP, false>), dim3((unsigned)npairs), dim3(NP * 4), 0, stream, fa);
+      hipLaunchKernelGGL((trellis_fwd2_f32<NP, false, false>), grid, block, 0, stream, fa);
     return hipGetLastError();
   }
 }

@@ -10,7 +10,9 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libcviterbi.so")
+# CV_LIB_PATH: an A/B variant build (tools/ab_*.sh) loaded instead of the in-tree library, so
+# the scripts never overwrite the product .so (a killed A/B run used to leave a variant behind)
+LIB_PATH = os.environ.get("CV_LIB_PATH") or os.path.join(_HERE, "libcviterbi.so")
 
 (CV_OK, CV_EINVAL, CV_EDEVICE, CV_ENOMEM, CV_EINFEASIBLE, CV_EIO, CV_EPARSE, CV_EUNSUPPORTED, CV_EINTERNAL,
  CV_ELIMIT) = range(10)

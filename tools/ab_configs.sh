@@ -6,13 +6,12 @@ OUT=$R/gpurun_out/${TAG:-abcfg}
 mkdir -p $OUT
 cd $R
 LIB=consistent-viterbi_amd/cviterbi/libcviterbi.so
-cp $LIB $OUT/lib_intree.so
 for r in $(seq 1 ${ROUNDS:-2}); do
   for v in ${VARIANTS:-intree}; do
-    [ "$v" = intree ] && cp $OUT/lib_intree.so $LIB || cp tools/_ab/lib_$v.so $LIB
+    if [ "$v" = intree ]; then unset CV_LIB_PATH; else export CV_LIB_PATH=$(pwd)/tools/_ab/lib_$v.so; fi
     for e in ${ENVS:-NONE=0}; do
       env $e REPS=${REPS:-10} timeout -k 10 ${T_CFG:-300} python tools/bench_configs.py ${CONFIGS:-c2f64 c3f64} > $OUT/$v.$e.$r.log 2>/dev/null \
-        || { echo "FAIL $v $e"; cp $OUT/lib_intree.so $LIB; exit 1; }
+        || { echo "FAIL $v $e"; exit 1; }
       python3 -c "
 import json,sys
 for l in open(sys.argv[1]):
@@ -23,4 +22,3 @@ for l in open(sys.argv[1]):
     done
   done
 done
-cp $OUT/lib_intree.so $LIB

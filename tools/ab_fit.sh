@@ -7,13 +7,12 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/${TAG:-abfit}
 mkdir -p $OUT
 LIB=$R/consistent-viterbi_amd/cviterbi/libcviterbi.so
-cp $LIB $OUT/lib_orig.so
 for r in $(seq 1 ${ROUNDS:-2}); do
   for vv in ${VARIANTS:-a b}; do
     v=${vv%%@*}; ENVS=""; [ "$vv" != "$v" ] && ENVS=$(echo "${vv#*@}" | tr ',' ' ')
-    cp $R/tools/_ab/lib_$v.so $LIB
+    export CV_LIB_PATH=$R/tools/_ab/lib_$v.so  # the variant, never copied over the in-tree .so
     (cd /tmp && env $ENVS TMPDIR=/tmp SHAPE=c4 ITERS=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
-      -d $OUT/$vv.$r -o kt -- python3 $R/tools/bench_fit.py > $OUT/$vv.$r.log 2>&1) || { cp $OUT/lib_orig.so $LIB; echo "FAIL $vv"; exit 1; }
+      -d $OUT/$vv.$r -o kt -- python3 $R/tools/bench_fit.py > $OUT/$vv.$r.log 2>&1) || { echo "FAIL $vv"; exit 1; }
     python3 - $OUT/$vv.$r/kt_kernel_stats.csv $vv $r <<'PY' | tee -a $OUT/summary.txt
 import csv, sys
 row = [f"{sys.argv[2]} {sys.argv[3]}"]
@@ -24,4 +23,3 @@ print("  ".join(row))
 PY
   done
 done
-cp $OUT/lib_orig.so $LIB

@@ -5,17 +5,14 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/${TAG:-pmc_l1}
 mkdir -p $OUT
 LIB=$R/consistent-viterbi_amd/cviterbi/libcviterbi.so
-cp $LIB $OUT/lib_orig.so
 cd /tmp && export TMPDIR=/tmp
 export NSEQ=${NSEQ:-16384}
 for v in ${VARIANTS:-base}; do
-  cp $R/tools/_ab/lib_$v.so $LIB
+  export CV_LIB_PATH=$R/tools/_ab/lib_$v.so
   timeout -s KILL 120 rocprofv3 --pmc ${COUNTERS:-TCP_TCC_READ_REQ_sum TCP_TOTAL_CACHE_ACCESSES_sum TCC_HIT_sum TCC_MISS_sum} \
     --kernel-include-regex "trellis_fwd_f64" -d $OUT/$v -o p --output-format csv -- python3 $R/tools/t64_sweep.py \
-    > $OUT/$v.log 2>&1 || { cp $OUT/lib_orig.so $LIB; exit 1; }
+    > $OUT/$v.log 2>&1 || exit 1
 done
-cp $OUT/lib_orig.so $LIB
-rm -f $OUT/lib_orig.so
 python3 - "$OUT" ${VARIANTS:-base} <<'PY' | tee $OUT/summary.txt
 import csv, glob, os, sys, collections
 out = sys.argv[1]

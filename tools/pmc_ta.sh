@@ -10,7 +10,7 @@ for G in "TA_TA_BUSY TA_ADDR_STALLED_BY_TC_CYCLES GRBM_GUI_ACTIVE" "TA_DATA_STAL
          "TCP_PENDING_STALL_CYCLES TCP_READ_TAGCONFLICT_STALL_CYCLES TCP_RFIFO_STALL_CYCLES TCP_LFIFO_STALL_CYCLES"; do
   i=$((i + 1))
   for v in ${VARIANTS:-base NOSTORE}; do
-    cp $R/tools/_ab/lib_$v.so $R/consistent-viterbi_amd/cviterbi/libcviterbi.so
+    export CV_LIB_PATH=$R/tools/_ab/lib_$v.so
     NSEQ=65536 timeout -s KILL 120 rocprofv3 --pmc $G --kernel-include-regex trellis_fwd_f64 -d $OUT/$v.g$i -o p \
       --output-format csv -- python3 $R/tools/bench_assoc.py viterbi > $OUT/$v.g$i.log 2>&1 || exit $?
   done
