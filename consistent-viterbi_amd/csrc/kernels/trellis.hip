@@ -398,6 +398,12 @@ __global__ __launch_bounds__(NP * 4) void trellis_fwd2_f32(TrellisFwdArgs args) 
       a_reg[4 * q + 3] = v.w;
     }
   }
+#ifndef CVK_F32_NO_AWAIT
+  // the A image is resident before the step loop: without this wait the compiler's waitcnt
+  // pass, merging the loop's back edge with the preheader, kept in-loop vmcnt waits for these
+  // loads, and those in-order waits also drained this wave's delta-row stores every half-step
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // gfx9 encoding: vmcnt(0), expcnt/lgkmcnt unconstrained
+#endif
   unsigned bad = 0;  // bit 0: X, bit 1: Y
   auto obs_x = [&](int t) -> unsigned {
     const unsigned o = (unsigned)obsX[t];
@@ -521,11 +527,21 @@ __global__ __launch_bounds__(NP * 4) void trellis_fwd2_f32(TrellisFwdArgs args) 
     o_load = is_y ? obs_y(t_obs) : obs_x(t_obs);
     // X(t) is followed by Y(t), Y(t) by X(t+1)
     if (FRC) f_nx = is_y ? frcY[clampT(t)] : frcX[clampT(t + 1)];
+    // every lane stores (the 4 lanes of a column half hold the same value, so the duplicate
+    // stores coalesce): under the old `if (writer)` the compiler could not count the store
+    // in the in-order vmcnt queue, so the next half-step's wait for its emission row
+    // (vmcnt(1) instead of vmcnt(2)) also drained this store
+#ifndef CVK_F32_WRITER_STORES
+    ldst[lds_w] = dn;
+    float* row = drow + (size_t)t * NP;  // uniform
+    row[jw] = dn;
+#else  // A/B: the round-4 form
     if (writer) {
       ldst[lds_w] = dn;
       float* row = drow + (size_t)t * NP;  // uniform
       row[jw] = dn;
     }
+#endif
     if (sync) lds_barrier();
     if (ONEBAR && is_y) ld8(nsrc, P);  // X's delta_t, complete since the barrier
   };

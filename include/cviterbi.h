@@ -57,9 +57,13 @@ enum { CV_DTYPE_F32 = 0, CV_DTYPE_F64 = 1 };
 enum { CV_ASSOC_VITERBI = 0, CV_ASSOC_CP = 1, CV_ASSOC_DP = 2, CV_ASSOC_DECODE = 3 };
 
 /* kernel choice: AUTO picks TRELLIS (register-resident A, f32, VITERBI, N <= 256) when it
- * applies, then TRELLIS_F64 (exact f64, any association, N <= 256; forced states with VITERBI
- * only: one wave per 2/4/8 sequences, A streamed from L2), else GENERIC (inline argmax,
- * f32/f64, any association, N <= 20480 f32 / 10240 f64: two rows of N in <= 160 KiB of LDS). */
+ * applies, then TRELLIS_F64 (exact f64: any association for N <= 256, forced states with
+ * VITERBI only; one wave per 2/4/8 sequences, A streamed from L2.  Above 256, VITERBI /
+ * DECODE / DP without forced states (VITERBI with them) as pairs of waves at NP = 512 or quads
+ * at NP = 1,024; AUTO takes NP = 512 for N >= 384 or >= 8,192 sequences and NP = 1,024 for
+ * N > 724, knobs CV_T64_512 / CV_T64_1024; an explicit TRELLIS_F64 gets it for any N <= 1,024),
+ * else GENERIC (f32/f64, any association, N <= 20480 f32 / 10240 f64: two rows of N in
+ * <= 160 KiB of LDS). */
 enum { CV_KERNEL_AUTO = 0, CV_KERNEL_TRELLIS = 1, CV_KERNEL_GENERIC = 2, CV_KERNEL_TRELLIS_F64 = 3 };
 
 /* cv_opts.flags */
@@ -276,18 +280,19 @@ CV_API cv_status cv_viterbi_decode(cv_hmm* h, int64_t T, const int32_t* obs, int
  * (utils.rs:24-38), so later sequences carry the running total and round exactly as the
  * reference does (a per-sequence decode can differ from it at near ties).  f64, first-index
  * argmax, CP association.  path_out[offsets[nseq] - offsets[0]] in super-sequence order;
- * objective_out = the chain's final maximum (main.rs:129's first number).  N <= 256 with
- * log-probability models (finite entries in [-2^80, 0]): every sequence is decoded on its own
- * by the f64 trellis in parallel and certified to be the chain's path at the chain's running
+ * objective_out = the chain's final maximum (main.rs:129's first number).  Log-probability
+ * models (finite entries in [-2^80, 0]), any N: every sequence is decoded on its own by the
+ * batch path's f64 row-A0 decode in parallel and certified to be the chain's path at the chain's running
  * total (a rounding-error margin), the running total folded on the host, and only the
- * uncertified sequences (near ties at that magnitude) re-run through the serial chain kernel
- * -- bit-identical to the serial chain (cv_last_superseq_stats).  Otherwise serial over
+ * uncertified sequences (near ties at that magnitude) re-decoded from their predicted offsets
+ * or re-run through the serial chain kernel -- bit-identical to the serial chain
+ * (cv_last_superseq_stats).  Otherwise serial over
  * elements on the GPU (one workgroup), as the reference is on the CPU.  N <= 10240.
  * CV_EINFEASIBLE when the maximum is -inf. */
 CV_API cv_status cv_decode_superseq_cp(cv_hmm* h, int64_t nseq, const int64_t* offsets, const int32_t* obs,
                                        int32_t* path_out, double* objective_out);
 /* How the last cv_decode_superseq_cp on this handle ran (out[7]): out[0] = 1 when the PARALLEL
- * chain ran (N <= 256, every finite entry of the model in [-2^80, 0], every sequence feasible:
+ * chain ran (every finite entry of the model in [-2^80, 0], every sequence feasible:
  * each sequence decoded on its own by the f64 trellis and certified to be the chain's own path
  * at the chain's running total), 0 for the serial chain; out[1] = sequences
  * certified, out[2] = sequences the serial chain kernel re-ran, out[3] = such runs, out[4] =
