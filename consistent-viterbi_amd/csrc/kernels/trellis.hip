@@ -1103,6 +1103,16 @@ hipError_t launch_rescore_f64(const RescoreArgs& r, int64_t nseq, hipStream_t st
 }
 
 // ---------------------------------------------------------------------------------
+// Candidate loops of the generic kernels unrolled (round 5): with one load of A per candidate
+// and the compare / select after it, the rolled loop waited for every load in turn -- a few
+// sequences (the parallel chain's speculative re-decodes above N = 256) then ran at one L2
+// round trip per candidate.  Only generic_fwd_ms<S = 1> in psi mode (a handful of sequences;
+// large batches run S = 2 / 4 at full occupancy, and the unrolled rows mode, 84 vs 40 VGPRs,
+// lost 37% at N = 600: profiles/r05_ab_generic_unroll.txt).  A/B: -DCVK_GEN_UNROLL=1.
+#ifndef CVK_GEN_UNROLL
+#define CVK_GEN_UNROLL 8
+#endif
+
 // Generic kernel: one workgroup (256 threads) per sequence, any N, f32/f64, all modes.
 template <typename REAL>
 __global__ __launch_bounds__(256) void generic_fwd(GenericFwdArgs<REAL> args) {
@@ -1209,6 +1219,8 @@ __global__ __launch_bounds__(1024) void generic_fwd_ms(GenericFwdArgs<REAL> args
   const int V = args.nobs;
   const int assoc = args.assoc;
   const REAL ninf = -__builtin_inf();
+  // candidate loops unrolled for one-sequence workgroups in psi mode only (see CVK_GEN_UNROLL)
+  constexpr int kCandUnroll = (S == 1 && !ROWS) ? CVK_GEN_UNROLL : 1;
   int64_t e0[S], slot[S], seq[S];
   int T[S];
   int Tmax = 0;
@@ -1279,6 +1291,7 @@ __global__ __launch_bounds__(1024) void generic_fwd_ms(GenericFwdArgs<REAL> args
         bool live[S];  // a -inf emission leaves the column at -inf (dp.rs:147-177)
 #pragma unroll
         for (int s = 0; s < S; ++s) live[s] = act[s] && e[s] > ninf;
+        #pragma unroll kCandUnroll
         for (int i = 0; i < N; ++i) {
           const REAL aij = col[(size_t)i * N];
 #pragma unroll
@@ -1309,6 +1322,7 @@ __global__ __launch_bounds__(1024) void generic_fwd_ms(GenericFwdArgs<REAL> args
 #pragma unroll
           for (int s = 0; s < S; ++s) best[s] = row(pb, s)[0] + a0;
         }
+        #pragma unroll kCandUnroll
         for (int i = 1; i < N; ++i) {
           const REAL aij = col[(size_t)i * N];
 #pragma unroll
@@ -1782,7 +1796,9 @@ int trellis_padded_states(int n) {
     default: return hipErrorInvalidValue; \
   }
 
-constexpr bool kF32OneBarDefault = false;
+// one barrier per step: 79.5-80.8 vs 81.8-82.4 ms forward at config 4 f32, three interleaved
+// rounds on one box (profiles/r05_ab_f32_onebar.txt)
+constexpr bool kF32OneBarDefault = true;
 
 template <int NP>
 static hipError_t trellis_fwd2_np(const TrellisFwdArgs& fa, int64_t npairs, hipStream_t stream) {
@@ -1899,6 +1915,10 @@ hipError_t launch_generic_fwd(const GenericFwdArgs<REAL>& fa, int64_t nseq, hipS
     case 2: return launch_generic_ms<REAL, 2, false>(fa, nseq, stream);
     default: break;
   }
+  // one sequence per workgroup: one thread per state up to N = 1,024 (64 ceil(N / 64) threads;
+  // generic_fwd's 256 threads walk 4 states each at N = 1,024 -- a handful of sequences, e.g.
+  // the parallel chain's speculative re-decodes, then ran latency-bound on a few CUs)
+  if (fa.nstates <= 1024) return launch_generic_ms<REAL, 1, false>(fa, nseq, stream);
   const size_t lds = sizeof(REAL) * 2 * (size_t)fa.nstates;
   if (lds > 64 * 1024)  // N > 4096 (f64) / 8192 (f32): the two rows in up to 160 KiB of LDS
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&generic_fwd<REAL>),
