@@ -405,17 +405,28 @@ __global__ __launch_bounds__(NP * 4) void trellis_fwd2_f32(TrellisFwdArgs args) 
   __builtin_amdgcn_s_waitcnt(0x0F70);  // gfx9 encoding: vmcnt(0), expcnt/lgkmcnt unconstrained
 #endif
   unsigned bad = 0;  // bit 0: X, bit 1: Y
+  // CVK_F32_ABL_*: timing-only ablations (results wrong; tools/build_variant_f32.sh):
+  // OBS = observations from arithmetic instead of scalar loads, NOE = no emission loads
   auto obs_x = [&](int t) -> unsigned {
+#ifdef CVK_F32_ABL_OBS
+    return ((unsigned)t * 7u + (unsigned)e0[0]) % V;
+#endif
     const unsigned o = (unsigned)obsX[t];
     bad |= (o >= V) ? 1u : 0u;
     return o < V ? o : 0u;
   };
   auto obs_y = [&](int t) -> unsigned {
+#ifdef CVK_F32_ABL_OBS
+    return ((unsigned)t * 5u + (unsigned)e0[1]) % V;
+#endif
     const unsigned o = (unsigned)obsY[t];
     bad |= (o >= V) ? 2u : 0u;
     return o < V ? o : 0u;
   };
   auto et_row = [&](unsigned o) -> float {
+#ifdef CVK_F32_ABL_NOE
+    return -1.0f * (float)(o & 3u);
+#endif
     const float* row = args.et + (size_t)o * NP;  // uniform
     return row[jw];
   };
@@ -469,10 +480,24 @@ __global__ __launch_bounds__(NP * 4) void trellis_fwd2_f32(TrellisFwdArgs args) 
   // delta instead of 32: 4 waves x <=112 VGPRs leave a backtrack wave room on every SIMD.
   constexpr int KB = R / 8;  // 8-row blocks per lane
   static_assert(R % 8 == 0, "pair kernel needs NP % 64 == 0");
+#ifndef CVK_F32_ABL_NOLDS
   auto ld8 = [&](const float* src, float4 (&dst)[2]) {
     dst[0] = *reinterpret_cast<const float4*>(src);
     dst[1] = *reinterpret_cast<const float4*>(src + 4);
   };
+#else  // timing only: no LDS reads in the loop -- the block registers are declared changed by
+       // an empty asm (no instructions), so the adds stay in the loop (results wrong)
+  bool abl_first = true;
+  auto ld8 = [&](const float* src, float4 (&dst)[2]) {
+    if (abl_first) {
+      dst[0] = *reinterpret_cast<const float4*>(src);
+      dst[1] = *reinterpret_cast<const float4*>(src + 4);
+      abl_first = false;
+    }
+    asm volatile("" : "+v"(dst[0].x), "+v"(dst[0].y), "+v"(dst[0].z), "+v"(dst[0].w), "+v"(dst[1].x), "+v"(dst[1].y),
+                 "+v"(dst[1].z), "+v"(dst[1].w));
+  };
+#endif
   float4 P[2], Q[2];
   ld8(&lds[0][0][rg * S], P);
 
@@ -534,7 +559,11 @@ __global__ __launch_bounds__(NP * 4) void trellis_fwd2_f32(TrellisFwdArgs args) 
 #ifndef CVK_F32_WRITER_STORES
     ldst[lds_w] = dn;
     float* row = drow + (size_t)t * NP;  // uniform
+#ifndef CVK_F32_ABL_NOSTORE
     row[jw] = dn;
+#else
+    if (dn == 12345.0f) row[jw] = dn;  // timing only: no delta-row stores
+#endif
 #else  // A/B: the round-4 form
     if (writer) {
       ldst[lds_w] = dn;

@@ -15,6 +15,14 @@
 #include <cstdio>
 
 #define ITERS 4096
+#define CLOB ::: "v0","v1","v2","v3","v4","v5","v6","v7","v8","v9","v10","v11","v12","v13","v14","v15", \
+          "v16","v17","v18","v19","v20","v21","v22","v23","v24","v25","v26","v27","v28","v29","v30","v31", \
+          "v32","v33","v34","v35","v36","v37","v38","v39","v40","v41","v42","v43","v44","v45","v46","v47", \
+          "v48","v49","v50","v51","v52","v53","v54","v55","v56","v57","v58","v59","v60","v61","v62","v63", \
+          "v64","v65","v66","v67","v68","v69","v70","v71","v72","v73","v74","v75","v76","v77","v78","v79", \
+          "v80","v81","v82","v83","v84","v85","v86","v87","v88","v89","v90","v91","v92","v93","v94","v95", \
+          "v96","v97","v98","v99","v100","v101","v102","v103","v104","v105","v106","v107","v108","v109","v110","v111", \
+          "v112","v113","v114","v115","v116","v117","v118","v119","v120","v121","v122","v123","v124","v125","v126","v127"
 
 // 8 independent groups per block; group g uses registers v[16 g + ...]
 template <int KIND>
@@ -115,6 +123,25 @@ __global__ __launch_bounds__(1024) void k(unsigned long long* cyc, float seed) {
           "v80","v81","v82","v83","v84","v85","v86","v87","v88","v89","v90","v91","v92","v93","v94","v95",
           "v96","v97","v98","v99","v100","v101","v102","v103","v104","v105","v106","v107","v108","v109","v110","v111",
           "v112","v113","v114","v115","v116","v117","v118","v119","v120","v121","v122","v123","v124","v125","v126","v127");
+    } else if constexpr (KIND == 7) {  // ADD_S: x(bank0) = d(bank0) + a(bank0); 16 adds
+      asm volatile(
+          ".irp g, 0,1,2,3,4,5,6,7\n"
+          "v_add_f32 v[\\g*16+8], v[\\g*16+0], v[\\g*16+4]\n"
+          "v_add_f32 v[\\g*16+12], v[\\g*16+0], v[\\g*16+4]\n"
+          ".endr" CLOB);
+    } else if constexpr (KIND == 8) {  // MIX_SS: the adds' sources in one bank (d = g+1, a0 = g+5, a1 = g+9)
+      asm volatile(
+          ".irp g, 0,1,2,3,4,5,6,7\n"
+          "v_add_f32 v[\\g*16+4], v[\\g*16+1], v[\\g*16+5]\n"
+          "v_add_f32 v[\\g*16+6], v[\\g*16+1], v[\\g*16+9]\n"
+          "v_max3_f32 v[\\g*16+7], v[\\g*16+7], v[\\g*16+4], v[\\g*16+6]\n"
+          ".endr" CLOB);
+    } else if constexpr (KIND == 9) {  // DPP: v_max_f32_dpp (quad_perm), 16 independent
+      asm volatile(
+          ".irp g, 0,1,2,3,4,5,6,7\n"
+          "v_max_f32_dpp v[\\g*16+3], v[\\g*16+0], v[\\g*16+3] quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n"
+          "v_max_f32_dpp v[\\g*16+7], v[\\g*16+4], v[\\g*16+7] quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n"
+          ".endr" CLOB);
     }
   }
   const unsigned long long t1 = __builtin_amdgcn_s_memtime();
@@ -123,8 +150,8 @@ __global__ __launch_bounds__(1024) void k(unsigned long long* cyc, float seed) {
 }
 
 // instructions per iteration and the (from, to) pairs they cover per lane
-constexpr int kInsts[] = {16, 16, 16, 16, 24, 24, 16};
-constexpr int kPairs[] = {0, 0, 0, 0, 16, 16, 16};
+constexpr int kInsts[] = {16, 16, 16, 16, 24, 24, 16, 16, 24, 16};
+constexpr int kPairs[] = {0, 0, 0, 0, 16, 16, 16, 0, 16, 0};
 
 template <int KIND>
 void run(const char* name, int cus) {
@@ -160,5 +187,8 @@ int main() {
   run<4>("MIX_D", cus);
   run<5>("MIX_S", cus);
   run<6>("PK", cus);
+  run<7>("ADD_S", cus);
+  run<8>("MIX_SS", cus);
+  run<9>("DPP", cus);
   return 0;
 }
