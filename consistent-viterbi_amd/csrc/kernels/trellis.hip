@@ -541,6 +541,7 @@ __global__ __launch_bounds__(NP * 4) void trellis_fwd2_f32(TrellisFwdArgs args) 
         ld8(nsrc, P);  // next half-step's block 0 (KB odd: no adds left to hide it)
       __builtin_amdgcn_sched_barrier(0);
     }
+
     const float m0 = fmaxf(m0a, m0b);
     const float m1 = fmaxf(m1a, m1b);
     // fold the 8 row groups; column j0 + hi ends in this lane

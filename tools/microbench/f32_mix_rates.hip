@@ -142,6 +142,29 @@ __global__ __launch_bounds__(1024) void k(unsigned long long* cyc, float seed) {
           "v_max_f32_dpp v[\\g*16+3], v[\\g*16+0], v[\\g*16+3] quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n"
           "v_max_f32_dpp v[\\g*16+7], v[\\g*16+4], v[\\g*16+7] quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n"
           ".endr" CLOB);
+    } else if constexpr (KIND == 10) {  // ADD_S2: both sources in bank 0, no register reused by the next add
+      asm volatile(
+          ".irp g, 0,1,2,3,4,5,6,7\n"
+          "v_add_f32 v[\\g*16+2], v[\\g*16+0], v[\\g*16+4]\n"
+          "v_add_f32 v[\\g*16+6], v[\\g*16+8], v[\\g*16+12]\n"
+          ".endr" CLOB);
+    } else if constexpr (KIND == 11) {  // ADD_D2: sources in banks 0 / 1, no register reused by the next add
+      asm volatile(
+          ".irp g, 0,1,2,3,4,5,6,7\n"
+          "v_add_f32 v[\\g*16+2], v[\\g*16+0], v[\\g*16+5]\n"
+          "v_add_f32 v[\\g*16+6], v[\\g*16+8], v[\\g*16+13]\n"
+          ".endr" CLOB);
+    } else if constexpr (KIND == 12) {  // MIX_K: the kernel's rows4 shape -- one d (bank 0) into 2 adds with
+                                        // distinct a's (banks 1, 2), two rows, then max3 of 2 sums per column
+      asm volatile(
+          ".irp g, 0,1,2,3,4,5,6,7\n"
+          "v_add_f32 v[\\g*16+3], v[\\g*16+0], v[\\g*16+1]\n"
+          "v_add_f32 v[\\g*16+7], v[\\g*16+0], v[\\g*16+2]\n"
+          "v_add_f32 v[\\g*16+11], v[\\g*16+4], v[\\g*16+5]\n"
+          "v_add_f32 v[\\g*16+15], v[\\g*16+4], v[\\g*16+6]\n"
+          "v_max3_f32 v[\\g*16+8], v[\\g*16+8], v[\\g*16+3], v[\\g*16+11]\n"
+          "v_max3_f32 v[\\g*16+9], v[\\g*16+9], v[\\g*16+7], v[\\g*16+15]\n"
+          ".endr" CLOB);
     }
   }
   const unsigned long long t1 = __builtin_amdgcn_s_memtime();
@@ -150,8 +173,8 @@ __global__ __launch_bounds__(1024) void k(unsigned long long* cyc, float seed) {
 }
 
 // instructions per iteration and the (from, to) pairs they cover per lane
-constexpr int kInsts[] = {16, 16, 16, 16, 24, 24, 16, 16, 24, 16};
-constexpr int kPairs[] = {0, 0, 0, 0, 16, 16, 16, 0, 16, 0};
+constexpr int kInsts[] = {16, 16, 16, 16, 24, 24, 16, 16, 24, 16, 16, 16, 48};
+constexpr int kPairs[] = {0, 0, 0, 0, 16, 16, 16, 0, 16, 0, 0, 0, 32};
 
 template <int KIND>
 void run(const char* name, int cus) {
@@ -190,5 +213,8 @@ int main() {
   run<7>("ADD_S", cus);
   run<8>("MIX_SS", cus);
   run<9>("DPP", cus);
+  run<10>("ADD_S2", cus);
+  run<11>("ADD_D2", cus);
+  run<12>("MIX_K", cus);
   return 0;
 }

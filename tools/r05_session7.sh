@@ -3,7 +3,7 @@
 # (tools/build_variant_f32.sh: CVK_F32_ABL_OBS / NOE / NOSTORE) interleaved on one box.
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-O=$R/gpurun_out/r05_s7
+O=$R/gpurun_out/${ABTAG:-r05_s7}
 mkdir -p $O
 cd $R
 for r in 1 2; do
