@@ -247,3 +247,20 @@ def test_chain_serial_large_n_segmented_backtrack(gpu):
     sp, sobj = _serial(h, off, obs)
     rp, robj = O.cp_superseq_f64(pi, a, b, off, obs)
     assert sobj == robj and np.array_equal(sp, rp)
+
+
+@pytest.mark.parametrize("n", [1100, 2500])
+def test_chain_par_beyond_1024_equals_oracle(gpu, n):
+    """N > 1,024: the row-A0 decode is the generic kernels' rows mode (states strided over the
+    workgroup), the certificates read its plain rows, speculation / runs the generic CP kernel
+    and cp_superseq_chain with states strided -- the oracle's chain element by element."""
+    pi, a, b, off, obs = _case(n, 7, 10, 1, 12, seed=4900 + n, zeros=(1,), ones=(4,))
+    h = cv.HMM(pi, a, b)
+    (path, obj), st = _par(h, off, obs)
+    assert st["parallel"], st
+    rp, robj = O.cp_superseq_f64(pi, a, b, off, obs)
+    assert obj == robj and np.array_equal(path, rp), st
+    (p2, o2), st2 = _par(h, off, obs, force=1, spec=False)  # the whole chain as one serial run
+    assert st2["rerun"] >= 1 and o2 == robj and np.array_equal(p2, rp), st2
+    (p3, o3), st3 = _par(h, off, obs, force=2)  # speculation through the generic CP kernel
+    assert st3["speculated"] >= 1 and o3 == robj and np.array_equal(p3, rp), st3
