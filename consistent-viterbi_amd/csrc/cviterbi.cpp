@@ -3423,9 +3423,6 @@ CV_API cv_status cv_decode_superseq_cp(cv_hmm* h, int64_t nseq, const int64_t* o
     const int64_t k = first_bad(base, offsets[nseq], [&](int64_t i) { return obs[i] < 0 || obs[i] >= V; });
     if (k >= 0) return set_err(CV_EINVAL, "obs[%lld] = %d out of range [0,%lld)", (long long)k, obs[k], (long long)V);
   }
-  std::vector<uint8_t> first((size_t)L, 0);
-  for (int64_t q = 0; q < nseq; ++q)
-    if (offsets[q + 1] > offsets[q]) first[(size_t)(offsets[q] - base)] = 1;
   // The parallel chain (any N, log-probability models); else serially: N <= 256 the
   // one-workgroup chain with the candidates split over its waves and A on chip
   // (kernels/chain.hip), N > 256 (or CV_CHAIN_OLD=1, an A/B knob, bit-identical) one thread per
@@ -3439,6 +3436,11 @@ CV_API cv_status cv_decode_superseq_cp(cv_hmm* h, int64_t nseq, const int64_t* o
     st = superseq_cp_par(h, nseq, offsets, obs, path_out, objective_out, &applied);
     if (st != CV_OK || applied) return st;
   }
+  // the serial chain's sequence-start flags (MetaElements t == 0), built only when it runs (the
+  // parallel chain never reads them: 33.5 MB zeroed and walked at config-4 size)
+  std::vector<uint8_t> first((size_t)L, 0);
+  for (int64_t q = 0; q < nseq; ++q)
+    if (offsets[q + 1] > offsets[q]) first[(size_t)(offsets[q] - base)] = 1;
   if (cvk::t64_padded_states(h->N) && !(old_env && *old_env == '1'))
     return superseq_cp_wg(h, L, obs + base, first, path_out, objective_out);
   if ((st = ensure_f64_tables(h)) != CV_OK) return st;
