@@ -245,6 +245,11 @@ struct cv_hmm {
   // serial-chain runs, runs, certified folds done by the quantised sum, sequences taken from
   // speculative parallel re-decodes, such batches
   int64_t last_chain[7] = {0, 0, 0, 0, 0, 0, 0};
+  // the parallel chain's per-call device arrays, kept between calls (grow-only): a
+  // config-4-sized call allocated and freed ~0.4 GB of them each time (hipFree synchronises)
+  struct ChainBufs {
+    DevBuf off, obs, path, res, cert, ebin, q;
+  } chainb;
 
   ~cv_hmm() {
     for (auto e : ev) (void)hipEventDestroy(e);
@@ -521,12 +526,15 @@ cv_status make_hmm(int N, const std::vector<int64_t>& bdims, const double* pi, c
 }
 
 // CV_TRACE=1: host-side phase timestamps of the constrained decode on stderr (profiling aid).
-void trace_mark(const char* what) {
+bool trace_on() {
   static const bool on = [] {
     const char* e = getenv("CV_TRACE");
     return e && *e && *e != '0';
   }();
-  if (!on) return;
+  return on;
+}
+void trace_mark(const char* what) {
+  if (!trace_on()) return;
   static thread_local auto last = std::chrono::steady_clock::now();
   const auto now = std::chrono::steady_clock::now();
   fprintf(stderr, "[cv] %-28s +%8.3f ms\n", what, std::chrono::duration<double, std::milli>(now - last).count());
@@ -3000,7 +3008,8 @@ cv_status superseq_cp_par(cv_hmm* h, int64_t nseq, const int64_t* offsets, const
   for (int64_t k = 0; k <= nseq; ++k) off[(size_t)k] = offsets[k] - base;
   for (int64_t k = 0; k < nseq; ++k) maxT = std::max(maxT, off[(size_t)k + 1] - off[(size_t)k]);
   // 1. the per-sequence row-A0 decode with certificates
-  DevBuf d_off, d_obs, d_path, d_res, d_cert;
+  DevBuf &d_off = h->chainb.off, &d_obs = h->chainb.obs, &d_path = h->chainb.path, &d_res = h->chainb.res,
+         &d_cert = h->chainb.cert;
   if ((st = d_off.ensure((size_t)(nseq + 1) * 8)) != CV_OK) return st;
   if ((st = d_obs.ensure((size_t)L * 4)) != CV_OK) return st;
   if ((st = d_path.ensure((size_t)L * 4)) != CV_OK) return st;
@@ -3008,6 +3017,10 @@ cv_status superseq_cp_par(cv_hmm* h, int64_t nseq, const int64_t* offsets, const
   if ((st = d_cert.ensure((size_t)nseq * 16)) != CV_OK) return st;
   HIP_TRY(hipMemcpyAsync(d_off.p, off.data(), off.size() * 8, hipMemcpyHostToDevice, stream));
   HIP_TRY(hipMemcpyAsync(d_obs.p, obs + base, (size_t)L * 4, hipMemcpyHostToDevice, stream));
+  if (trace_on()) {  // phase split (CV_TRACE only: the syncs cost overlap)
+    HIP_TRY(hipStreamSynchronize(stream));
+    trace_mark("chain: obs H2D");
+  }
   double* d_score = d_res.as<double>();
   uint8_t* d_status = reinterpret_cast<uint8_t*>(d_score + nseq);
   cv_opts o = default_opts();
@@ -3022,12 +3035,16 @@ cv_status superseq_cp_par(cv_hmm* h, int64_t nseq, const int64_t* offsets, const
   if (st != CV_OK) return st;
   std::vector<double> score((size_t)nseq), cert((size_t)nseq * 2);
   std::vector<uint8_t> status((size_t)nseq);
+  if (trace_on()) {
+    HIP_TRY(hipStreamSynchronize(stream));
+    trace_mark("chain: row-A0 decode + certificates (device)");
+  }
   HIP_TRY(hipMemcpyAsync(path_out, d_path.p, (size_t)L * 4, hipMemcpyDeviceToHost, stream));
   HIP_TRY(hipMemcpyAsync(score.data(), d_score, (size_t)nseq * 8, hipMemcpyDeviceToHost, stream));
   HIP_TRY(hipMemcpyAsync(status.data(), d_status, (size_t)nseq, hipMemcpyDeviceToHost, stream));
   HIP_TRY(hipMemcpyAsync(cert.data(), d_cert.p, (size_t)nseq * 16, hipMemcpyDeviceToHost, stream));
   HIP_TRY(hipStreamSynchronize(stream));
-  trace_mark("chain: row-A0 decode + certificates");
+  trace_mark("chain: paths, scores, certificates D2H");
   for (int64_t k = 0; k < nseq; ++k)
     if (status[(size_t)k] != CV_SEQ_OK && status[(size_t)k] != CV_SEQ_EMPTY) return CV_OK;  // serial chain
   // 2a. predicted binades and the quantised folds of every path
@@ -3047,7 +3064,7 @@ cv_status superseq_cp_par(cv_hmm* h, int64_t nseq, const int64_t* offsets, const
       mp -= sk;
     }
   }
-  DevBuf d_ebin, d_q;
+  DevBuf &d_ebin = h->chainb.ebin, &d_q = h->chainb.q;
   if ((st = d_ebin.ensure((size_t)nseq * 4)) != CV_OK) return st;
   if ((st = d_q.ensure((size_t)nseq * 9)) != CV_OK) return st;
   HIP_TRY(hipMemcpyAsync(d_ebin.p, ebin.data(), (size_t)nseq * 4, hipMemcpyHostToDevice, stream));
