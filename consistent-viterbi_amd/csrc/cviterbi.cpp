@@ -689,8 +689,16 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
   const bool use_t64 = !use_trellis && t64_ok &&
                        (o.kernel == CV_KERNEL_TRELLIS_F64 ||
                         (o.kernel == CV_KERNEL_AUTO && !(o.flags & CV_FLAG_NO_T64) && (small_ok || big_pick)));
-  if (!use_trellis && !use_t64 && h->N > cvk::generic_max_states(o.dtype == CV_DTYPE_F64 ? 8 : 4))
-    return set_err(CV_EUNSUPPORTED, "N=%d exceeds the generic kernel's LDS capacity", h->N);
+  // above generic_max_states (10,240 f64 / 20,480 f32) the generic decode runs wide (two rows
+  // per sequence in global memory, states over many workgroups, psi mode); psi is u16
+  if (!use_trellis && !use_t64 && h->N > cvk::kGenericGlobalMaxStates)
+    return set_err(CV_EUNSUPPORTED, "N=%d exceeds the generic kernel's u16 back-pointer range (N <= %d)", h->N,
+                   cvk::kGenericGlobalMaxStates);
+  // (the chain's certificates read the rows mode's rows: no wide decode for them below the limit)
+  const bool gen_global =
+      !use_trellis && !use_t64 &&
+      (h->N > cvk::generic_max_states(o.dtype == CV_DTYPE_F64 ? 8 : 4) ||
+       (!cp_cert && cvk::generic_wide(h->N, o.dtype == CV_DTYPE_F64 ? 8 : 4, nseq, o.assoc == CV_ASSOC_CP)));
 
   std::vector<int64_t> off_copy;
   if (!offsets_host) {
@@ -718,7 +726,7 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
     h->last_launches = 0;
     h->last_kernel = use_trellis ? CV_KERNEL_TRELLIS : use_t64 ? CV_KERNEL_TRELLIS_F64 : CV_KERNEL_GENERIC;
     h->last_np = use_trellis ? (wave ? h->npw : h->np) : use_t64 ? h->np64 : 0;
-    h->last_mt = -1;
+    h->last_mt = gen_global ? 0 : -1;  // GENERIC: 0 = wide (states over workgroups)
   }
   // N <= 64: one wave per sequence, forward and backtrack fused (trellis_wave_f32) on tables
   // padded to npw = 16 * ceil(N / 16); its chunks run back to back on one stream (nothing to
@@ -739,7 +747,8 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
   // N = 300 14.9 -> 11.5 ms, N = 512 28.7 -> 21.5 ms, N = 1,024 163 -> 139 ms
   // (profiles/r04_large_n.txt)
   const char* gr_env = getenv("CV_GENERIC_ROWS");
-  const bool gen_rows = !use_trellis && !use_t64 && o.assoc != CV_ASSOC_CP && !(gr_env && *gr_env == '0');
+  const bool gen_rows =
+      !use_trellis && !use_t64 && !gen_global && o.assoc != CV_ASSOC_CP && !(gr_env && *gr_env == '0');
   if (cp_cert && !use_t64 && !(gen_rows && o.dtype == CV_DTYPE_F64))
     return set_err(CV_EUNSUPPORTED, "chain certificates need the f64 trellis or the generic kernels' rows mode");
   if (gen_rows && (st = o.dtype == CV_DTYPE_F64 ? ensure_at64(h) : ensure_at32(h)) != CV_OK) return st;
@@ -823,7 +832,8 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
   const int64_t T0 = offsets_host[1] - offsets_host[0];
   for (int64_t s = 1; s < nseq && !varlen; ++s) varlen = (offsets_host[s + 1] - offsets_host[s]) != T0;
   const size_t buf_bytes = ((std::max<uint64_t>(max_elems, 1) * per_elem + 255) / 256) * 256;
-  const size_t last_bytes = ((size_t)max_seqs * h->N * real_bytes + 255) / 256 * 256;
+  // gen_global: each sequence's two rows follow the chunk's last rows ([max_seqs][2][N])
+  const size_t last_bytes = ((size_t)max_seqs * h->N * real_bytes * (gen_global ? 3 : 1) + 255) / 256 * 256;
   if ((st = w_main.ensure(buf_bytes * nbuf)) != CV_OK) return st;
   if (!use_trellis && (st = w_last.ensure(last_bytes * nbuf)) != CV_OK) return st;
   const int32_t* order_dev = nullptr;
@@ -1019,6 +1029,11 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
       fa.cp_init = cp_init;  // the parallel chain's speculative re-decodes (N > 256)
       fa.cp_last = cp_last;
       if (gen_rows) fa.rows = reinterpret_cast<double*>(wsb);
+      if (gen_global) {  // wide: the chunk's rows after its last rows, one launch per step
+        fa.grows = reinterpret_cast<double*>(lrb) + (size_t)max_seqs * h->N;
+        for (int64_t sq = c.first; sq < c.second; ++sq)
+          fa.wide_steps = std::max<int64_t>(fa.wide_steps, offsets_host[sq + 1] - offsets_host[sq]);
+      }
       err = cvk::launch_generic_fwd<double>(fa, n, stream);
     } else {
       cvk::GenericFwdArgs<float> fa{};
@@ -1038,6 +1053,11 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
       fa.status = status_dev;
       fa.forced = o.forced;
       if (gen_rows) fa.rows = reinterpret_cast<float*>(wsb);
+      if (gen_global) {  // wide: the chunk's rows after its last rows, one launch per step
+        fa.grows = reinterpret_cast<float*>(lrb) + (size_t)max_seqs * h->N;
+        for (int64_t sq = c.first; sq < c.second; ++sq)
+          fa.wide_steps = std::max<int64_t>(fa.wide_steps, offsets_host[sq + 1] - offsets_host[sq]);
+      }
       err = cvk::launch_generic_fwd<float>(fa, n, stream);
     }
     if (err != hipSuccess) return set_err(CV_EDEVICE, "forward launch failed: %s", hipGetErrorString(err));
@@ -2995,6 +3015,9 @@ cv_status superseq_cp_par(cv_hmm* h, int64_t nseq, const int64_t* offsets, const
   cv_status st;
   const int N = h->N;
   const bool small = cvk::t64_padded_states(N) != 0;  // N <= 256: padded tables, cp_chain_wg runs
+  // the certificates need the generic kernels' rows mode, which keeps its rows in LDS
+  // (N <= 10,240): above it the serial chain runs
+  if (N > cvk::generic_max_states(8)) return CV_OK;
   if (small && (st = ensure_t64_tables(h)) != CV_OK) return st;
   if ((st = ensure_f64_tables(h)) != CV_OK) return st;
   if (!model_nonpos(h)) return CV_OK;
@@ -3174,7 +3197,8 @@ cv_status superseq_cp_par(cv_hmm* h, int64_t nseq, const int64_t* offsets, const
   HIP_TRY(hipMemsetAsync(d_first.p, 0, (size_t)std::max<int64_t>(maxT, 1), stream));
   HIP_TRY(hipMemsetAsync(d_first.p, 1, 1, stream));  // one sequence per launch: its element 0 starts it
   if ((st = d_rows.ensure((size_t)W * 8 * 3)) != CV_OK) return st;
-  if ((st = d_small.ensure(16)) != CV_OK) return st;
+  // objective, final state (+ the wide chain's two rows, CV_CHAIN_WIDE_MIN)
+  if ((st = d_small.ensure(16 + (!small && cvk::cp_chain_wide(N) ? (size_t)N * 16 : 0))) != CV_OK) return st;
   double* row_in = d_rows.as<double>();  // start row uploaded from the host
   double* row_a = row_in + W;            // the run's last rows (ping-pong)
   double* row_b = row_a + W;
@@ -3256,6 +3280,7 @@ cv_status superseq_cp_par(cv_hmm* h, int64_t nseq, const int64_t* offsets, const
       g.final_state = reinterpret_cast<int32_t*>(d_small.as<double>() + 1);
       g.init_row = init;
       g.final_row = out_row;
+      if (cvk::cp_chain_wide(N)) g.grows = d_small.as<double>() + 2;
       err = cvk::launch_cp_superseq_chain(g, stream);
     }
     if (err != hipSuccess) return set_err(CV_EDEVICE, "chain run launch failed: %s", hipGetErrorString(err));
@@ -3467,7 +3492,9 @@ CV_API cv_status cv_decode_superseq_cp(cv_hmm* h, int64_t nseq, const int64_t* o
   if ((st = d_first.ensure((size_t)L)) != CV_OK) return st;
   if ((st = d_psi.ensure((size_t)L * h->N * 2)) != CV_OK) return st;
   if ((st = d_path.ensure((size_t)L * 4)) != CV_OK) return st;
-  if ((st = d_obj.ensure(16)) != CV_OK) return st;
+  // the wide chain (N > 10,240): its two rows in global memory after the objective / final state
+  const bool grows = cvk::cp_chain_wide(h->N);
+  if ((st = d_obj.ensure(16 + (grows ? (size_t)h->N * 16 : 0))) != CV_OK) return st;
   HIP_TRY(hipMemcpyAsync(d_obs.p, obs + base, (size_t)L * 4, hipMemcpyHostToDevice, stream));
   HIP_TRY(hipMemcpyAsync(d_first.p, first.data(), (size_t)L, hipMemcpyHostToDevice, stream));
   cvk::CpChainArgs g{};
@@ -3483,6 +3510,7 @@ CV_API cv_status cv_decode_superseq_cp(cv_hmm* h, int64_t nseq, const int64_t* o
   g.path = nullptr;  // the segmented backtrack below (a single-thread walk was one dependent load per element)
   g.objective = d_obj.as<double>();
   g.final_state = reinterpret_cast<int32_t*>(d_obj.as<double>() + 1);
+  if (grows) g.grows = d_obj.as<double>() + 2;
   const hipError_t err = cvk::launch_cp_superseq_chain(g, stream);
   if (err != hipSuccess) return set_err(CV_EDEVICE, "super-sequence chain launch failed: %s", hipGetErrorString(err));
   double out[2];

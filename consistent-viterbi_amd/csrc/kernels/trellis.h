@@ -101,6 +101,11 @@ struct GenericFwdArgs {
   // cp_last [nseq][N] = each sequence's last row, by sequence id (null: not used / written)
   const REAL* cp_init;
   REAL* cp_last;
+  // wide mode (psi only; N > generic_max_states, where the two rows no longer fit in LDS):
+  // grows = [(seqs of launch)][2][N] global rows, wide_steps = the launch's longest sequence;
+  // one launch per step, each sequence's states spread over ceil(N / 256) workgroups
+  REAL* grows;
+  int64_t wide_steps;
 };
 
 template <typename REAL>
@@ -200,6 +205,14 @@ hipError_t launch_generic_bt(const GenericBtArgs<REAL>& ba, int64_t nseq, hipStr
 template <typename REAL>
 hipError_t launch_generic_bt_rows(const GenericBtArgs<REAL>& ba, int64_t nseq, hipStream_t stream);
 int generic_max_states(int real_bytes);
+// The generic decode runs wide (GenericFwdArgs::grows, up to the u16 psi's range): always above
+// generic_max_states; above N = 1,024 (one thread per state no longer fits one workgroup) also
+// for CP (psi mode in one workgroup: 4x the rows mode's time), batches below 4,096 sequences or
+// N > 3,072 -- everywhere the one-workgroup kernels lost (profiles/r05_wide_crossover.txt).
+// Read per call (A/B knobs and tests, bit-identical): CV_GENERIC_WIDE=0 only above the LDS
+// limit, CV_GENERIC_WIDE_MIN=n from n states whatever the batch.
+constexpr int kGenericGlobalMaxStates = 65535;
+bool generic_wide(int n, int real_bytes, int64_t nseq, bool cp);
 
 // The constrained decode's f64 passes for N > 256 (the padded EXT kernels' range): one
 // workgroup per slot over an explicit element range, row-A0 association

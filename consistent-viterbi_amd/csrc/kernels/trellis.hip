@@ -1231,6 +1231,168 @@ __global__ __launch_bounds__(256) void generic_fwd(GenericFwdArgs<REAL> args) {
   if (bad && threadIdx.x == 0) args.status[seq] = CVK_SEQ_BADOBS;
 }
 
+// generic_wide_step<REAL, S>: step t of the generic decode with each sequence's states spread
+// over ceil(N / 256) workgroups, S consecutive slots per workgroup (each table element loaded
+// once for the S), the rows in global memory (args.grows) -- where one workgroup per sequence
+// would stream the N x N table (>= 134 MB at N = 4,096 f64) through a single CU every step.
+// XCD-aware: blocks b and b + 8 share an XCD (MI355X_MICROARCH.md: dealt round-robin), so block
+// b takes column block jb = b % 8 + 8 k: each XCD's L2 serves a fixed eighth of the table's
+// columns to every slot group (the column blocks are padded to a multiple of 8; a padding
+// block exits at once).  The same candidates in the same order per state as generic_fwd
+// (viterbi.rs:5-32, cp.rs:70-79, dp.rs, decode), so the same values, back-pointers and statuses
+// bit for bit.  t = 0 seeds row 0; the step at t = T - 1 also writes the sequence's last row.
+template <typename REAL, int S>
+__global__ __launch_bounds__(256) void generic_wide_step(GenericFwdArgs<REAL> args, int t, int nblk8, int64_t nslots) {
+  const int N = args.nstates;
+  const int64_t k = (int64_t)(blockIdx.x >> 3);
+  const int jb = (int)(blockIdx.x & 7) + 8 * (int)(k % nblk8);
+  const int64_t g0 = (k / nblk8) * S;  // first local slot of the group
+  const int j = jb * 256 + (int)threadIdx.x;
+  if (j >= N) return;
+  const REAL ninf = -__builtin_inf();
+  const int assoc = args.assoc;
+  int64_t seq[S], e0[S];
+  int T[S];
+  bool act[S], ok[S];
+  REAL e[S];
+  const REAL* prev[S];
+  bool any = false;
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    const int64_t ls = g0 + s;
+    act[s] = false;
+    seq[s] = 0;
+    e0[s] = 0;
+    T[s] = 0;
+    ok[s] = true;
+    e[s] = ninf;
+    prev[s] = args.grows;
+    if (ls < nslots) {
+      const int64_t slot = args.seq_begin + ls;
+      seq[s] = args.order ? (int64_t)args.order[slot] : slot;
+      e0[s] = args.offsets[seq[s]];
+      T[s] = (int)(args.offsets[seq[s] + 1] - e0[s]);
+      act[s] = t < T[s];
+    }
+    if (act[s]) {
+      const int o = args.obs[e0[s] + t];
+      ok[s] = (unsigned)o < (unsigned)args.nobs;
+      e[s] = ok[s] ? args.et[(size_t)o * N + j] : ninf;
+      prev[s] = args.grows + ls * 2 * N + ((t & 1) ^ 1) * N;
+    }
+    any |= act[s];
+  }
+  if (!any) return;
+  const REAL* __restrict__ col = args.a + j;
+  REAL d[S];
+  int arg[S];
+#pragma unroll
+  for (int s = 0; s < S; ++s) arg[s] = 0;
+  if (t == 0) {
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      if (assoc == CVK_ASSOC_DECODE)
+        d[s] = (REAL)0;
+      else if (assoc == CVK_ASSOC_DP)
+        d[s] = (e[s] > ninf) ? (REAL)(args.pi[j] + e[s]) : ninf;
+      else
+        d[s] = args.cp_init ? args.cp_init[seq[s]] + (args.pi[j] + e[s]) : args.pi[j] + e[s];
+    }
+  } else if (assoc == CVK_ASSOC_DP) {
+    // e = -inf: every candidate is -inf, the maximum stays -inf at index 0 (generic_fwd skips it)
+#pragma unroll
+    for (int s = 0; s < S; ++s) d[s] = ninf;
+#pragma unroll 8
+    for (int i = 0; i < N; ++i) {
+      const REAL aij = col[(size_t)i * N];
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        const REAL c = (aij + e[s]) + prev[s][i];
+        if (c > d[s]) {
+          d[s] = c;
+          arg[s] = i;
+        }
+      }
+    }
+  } else {
+    REAL best[S];
+#pragma unroll
+    for (int s = 0; s < S; ++s) best[s] = prev[s][0] + col[0];  // i = 0 seeds the maximum (generic_fwd's `!any`)
+#pragma unroll 8
+    for (int i = 1; i < N; ++i) {
+      const REAL aij = col[(size_t)i * N];
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        const REAL x = prev[s][i] + aij;
+        if (x > best[s]) {
+          best[s] = x;
+          arg[s] = i;
+        }
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      d[s] = assoc == CVK_ASSOC_CP ? prev[s][arg[s]] + (col[(size_t)arg[s] * N] + e[s]) : best[s] + e[s];
+      if (assoc == CVK_ASSOC_DECODE && !(e[s] > ninf)) {
+        d[s] = ninf;
+        arg[s] = 0;
+      }
+    }
+  }
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    if (!act[s]) continue;
+    const int64_t ls = g0 + s;
+    if (args.forced && args.forced[e0[s] + t] >= 0 && j != args.forced[e0[s] + t]) d[s] = ninf;
+    args.grows[ls * 2 * N + (t & 1) * N + j] = d[s];
+    if (t > 0) args.psi[(e0[s] - args.psi_elem_base + t) * (int64_t)N + j] = (uint16_t)arg[s];
+    if (t == T[s] - 1) {
+      args.last_row[ls * N + j] = d[s];
+      if (args.cp_last) args.cp_last[seq[s] * N + j] = d[s];
+    }
+    if (!ok[s] && j == 0) args.status[seq[s]] = CVK_SEQ_BADOBS;
+  }
+}
+
+// slots per wide workgroup: 4 once that still gives >= one workgroup per CU (256 CUs), else 1
+// (S = 2 was never the fastest: profiles/r05_wide_crossover.txt); CV_WIDE_S=k sets it (1, 2 or
+// 4; read per launch: A/B knob and tests, bit-identical)
+inline int generic_wide_seqs(int n, int64_t nseq) {
+  if (const char* e = getenv("CV_WIDE_S")) return atoi(e) >= 4 ? 4 : atoi(e) >= 2 ? 2 : 1;
+  return (nseq + 3) / 4 * ((n + 255) / 256) >= 256 ? 4 : 1;
+}
+
+template <typename REAL, int S>
+hipError_t launch_generic_wide_s(const GenericFwdArgs<REAL>& fa, int64_t nseq, hipStream_t stream) {
+  const int nblk8 = ((fa.nstates + 255) / 256 + 7) / 8;
+  const int64_t grid = (nseq + S - 1) / S * nblk8 * 8;
+  if (grid > (int64_t)INT32_MAX) return hipErrorInvalidValue;
+  for (int64_t t = 0; t < fa.wide_steps; ++t) {
+    hipLaunchKernelGGL((generic_wide_step<REAL, S>), dim3((unsigned)grid), dim3(256), 0, stream, fa, (int)t, nblk8,
+                       nseq);
+    const hipError_t err = hipGetLastError();
+    if (err != hipSuccess) return err;
+  }
+  return hipSuccess;
+}
+
+template <typename REAL>
+hipError_t launch_generic_wide(const GenericFwdArgs<REAL>& fa, int64_t nseq, hipStream_t stream) {
+  if (fa.rows || !fa.grows || fa.nstates > kGenericGlobalMaxStates) return hipErrorInvalidValue;
+  switch (generic_wide_seqs(fa.nstates, nseq)) {
+    case 4: return launch_generic_wide_s<REAL, 4>(fa, nseq, stream);
+    case 2: return launch_generic_wide_s<REAL, 2>(fa, nseq, stream);
+    default: return launch_generic_wide_s<REAL, 1>(fa, nseq, stream);
+  }
+}
+
+bool generic_wide(int n, int real_bytes, int64_t nseq, bool cp) {
+  if (n > generic_max_states(real_bytes)) return true;
+  if (const char* e = getenv("CV_GENERIC_WIDE_MIN"); e && *e) return n >= atoi(e);
+  if (const char* e = getenv("CV_GENERIC_WIDE"); e && *e == '0') return false;
+  return n > 1024 && (cp || nseq < 4096 || n > 3072);
+}
+
 // generic_fwd_ms<REAL, S, ROWS>: S sequences per workgroup (consecutive slots of the
 // longest-first schedule, so near-equal lengths), every A element loaded once for all S -- the
 // one-sequence kernel above streams A from L2 once per sequence step and is bound by that
@@ -1932,8 +2094,9 @@ hipError_t launch_generic_ms(const GenericFwdArgs<REAL>& fa, int64_t nseq, hipSt
 template <typename REAL>
 hipError_t launch_generic_fwd(const GenericFwdArgs<REAL>& fa, int64_t nseq, hipStream_t stream) {
   if (nseq <= 0) return hipSuccess;
+  if (fa.grows) return launch_generic_wide<REAL>(fa, nseq, stream);
   if (fa.rows) {  // rows mode: the maximum only (VITERBI / DECODE / DP)
-    if (fa.assoc == CVK_ASSOC_CP) return hipErrorInvalidValue;
+    if (fa.assoc == CVK_ASSOC_CP || fa.nstates > generic_max_states((int)sizeof(REAL))) return hipErrorInvalidValue;
     switch (generic_seqs_per_wg<REAL>(fa.nstates, nseq)) {
       case 4: return launch_generic_ms<REAL, 4, true>(fa, nseq, stream);
       case 2: return launch_generic_ms<REAL, 2, true>(fa, nseq, stream);

@@ -193,9 +193,18 @@ struct CpChainArgs {
   const double* init_row;
   double* final_row;
   int32_t* final_state;
+  // the wide chain (cp_chain_wide(N)): [2][N] global rows
+  double* grows;
 };
-// the chain's two rows in LDS (2 N doubles <= 160 KiB); psi is u16
-constexpr int kChainMaxStates = 10240;
+// the chain's two rows in LDS up to N = 10,240 (2 N doubles <= 160 KiB); above, the wide chain
+// (one launch per element, states over workgroups, rows in CpChainArgs::grows); psi is u16
+constexpr int kChainMaxStates = 65535;
+constexpr int kChainLdsMaxStates = 10240;
+// the wide chain runs above N = 1,024 (one workgroup then strides its states: 0.18 vs 0.08 ms
+// per element at N = 1,100, 17 vs 1.1 ms at 10,240 -- profiles/r05_wide_crossover.txt); read
+// per call (A/B knobs and tests, bit-identical): CV_CHAIN_WIDE=0 only above N = 10,240,
+// CV_CHAIN_WIDE_MIN=n from n states
+bool cp_chain_wide(int n);
 hipError_t launch_cp_superseq_chain(const CpChainArgs& g, hipStream_t stream);
 
 // NP = 64 * ceil(N / 64) for 1 <= N <= 256, else 0 (no f64 trellis kernel)

@@ -2183,7 +2183,8 @@ hipError_t launch_t64_suffix_trace(int np, const SuffixTrace64Args& a, int64_t n
 // stored as u16; then the first argmax of the last row and the backtrack (cp.rs:85-93).
 // Serial over elements (as the reference is): for the main.rs workflow, not the batch path.
 // A is staged in LDS when it fits (N <= 126: N^2 + 2N doubles <= 160 KiB), otherwise read
-// from L2 with the candidate loop unrolled so the loads overlap.
+// from L2 with the candidate loop unrolled so the loads overlap.  Above N = 1,024 (states
+// strided over the workgroup's threads) the wide kernels below run instead (cp_chain_wide).
 template <bool LDS_A>
 __global__ __launch_bounds__(1024) void cp_superseq_chain(CpChainArgs g) {
   extern __shared__ double rowbuf[];  // [2][N] (+ [N][N] A when LDS_A)
@@ -2245,11 +2246,91 @@ __global__ __launch_bounds__(1024) void cp_superseq_chain(CpChainArgs g) {
   }
 }
 
+// The chain wide: element t's states over ceil(N / 256) workgroups, one launch per element, the
+// two rows in g.grows ([2][N], row t & 1 is element t's) -- one workgroup would stream the
+// N x N table (>= 800 MB above N = 10,240) through a single CU per element.  Same candidates,
+// order and roundings as cp_superseq_chain (cp.rs:70-79 over utils.rs:24-38).  Element 0
+// without init_row seeds pi + b (cp.rs:66-68); with it, the host has put init_row in row 1.
+__global__ __launch_bounds__(256) void cp_chain_wide_step(CpChainArgs g, int64_t t) {
+  const int N = g.nstates;
+  const int j = (int)blockIdx.x * 256 + (int)threadIdx.x;
+  if (j >= N) return;
+  double* cur = g.grows + (t & 1) * N;
+  const double* prev = g.grows + ((t & 1) ^ 1) * N;
+  const int o = g.obs[t];
+  if (t == 0 && !g.init_row) {
+    cur[j] = g.pi[j] + g.et[(size_t)o * N + j];
+    return;
+  }
+  const bool first = g.first[t] != 0;
+  const double pj = g.pi[j];
+  const double* __restrict__ col = g.a + j;
+  double m = prev[0] + (first ? pj : col[0]);
+  int arg = 0;
+#pragma unroll 8
+  for (int i = 1; i < N; ++i) {
+    const double x = prev[i] + (first ? pj : col[(size_t)i * N]);
+    if (x > m) {
+      m = x;
+      arg = i;
+    }
+  }
+  const double tr = first ? pj : col[(size_t)arg * N];
+  cur[j] = prev[arg] + (tr + g.et[(size_t)o * N + j]);
+  g.psi[t * N + j] = (uint16_t)arg;
+}
+
+// the last row's first argmax (cp.rs:85-87), final_row, and the single-thread backtrack when
+// g.path is set (cp.rs:88-93)
+__global__ __launch_bounds__(1024) void cp_chain_wide_finish(CpChainArgs g) {
+  const int N = g.nstates;
+  const double* last = g.grows + ((g.len - 1) & 1) * N;
+  if (g.final_row)
+    for (int j = threadIdx.x; j < N; j += blockDim.x) g.final_row[j] = last[j];
+  if (threadIdx.x != 0) return;
+  int cs = 0;
+  double obj = last[0];
+  for (int i = 1; i < N; ++i)
+    if (last[i] > obj) {
+      obj = last[i];
+      cs = i;
+    }
+  *g.objective = obj;
+  if (g.final_state) *g.final_state = cs;
+  if (g.path)
+    for (int64_t t = g.len - 1; t >= 0; --t) {
+      g.path[t] = cs;
+      cs = g.psi[t * N + cs];
+    }
+}
+
+bool cp_chain_wide(int n) {
+  if (n > kChainLdsMaxStates) return true;
+  if (const char* e = getenv("CV_CHAIN_WIDE_MIN"); e && *e) return n >= atoi(e);
+  if (const char* e = getenv("CV_CHAIN_WIDE"); e && *e == '0') return false;
+  return n > 1024;
+}
+
 hipError_t launch_cp_superseq_chain(const CpChainArgs& g, hipStream_t stream) {
   if (g.len <= 0) return hipSuccess;
   if (g.nstates <= 0 || g.nstates > kChainMaxStates) return hipErrorInvalidValue;
-  const int threads = std::min(1024, ((g.nstates + 63) / 64) * 64);
   const size_t n = (size_t)g.nstates;
+  if (cp_chain_wide(g.nstates)) {
+    if (!g.grows) return hipErrorInvalidValue;
+    if (g.init_row) {
+      const hipError_t err = hipMemcpyAsync(g.grows + n, g.init_row, n * 8, hipMemcpyDeviceToDevice, stream);
+      if (err != hipSuccess) return err;
+    }
+    const unsigned nblk = (unsigned)((n + 255) / 256);
+    for (int64_t t = 0; t < g.len; ++t) {
+      hipLaunchKernelGGL(cp_chain_wide_step, dim3(nblk), dim3(256), 0, stream, g, t);
+      const hipError_t err = hipGetLastError();
+      if (err != hipSuccess) return err;
+    }
+    hipLaunchKernelGGL(cp_chain_wide_finish, dim3(1), dim3(1024), 0, stream, g);
+    return hipGetLastError();
+  }
+  const int threads = std::min(1024, ((g.nstates + 63) / 64) * 64);
   const size_t lds_a = (n * n + 2 * n) * sizeof(double);
   if (lds_a <= 160 * 1024) {
     if (lds_a > 64 * 1024)

@@ -62,8 +62,9 @@ enum { CV_ASSOC_VITERBI = 0, CV_ASSOC_CP = 1, CV_ASSOC_DP = 2, CV_ASSOC_DECODE =
  * DECODE / DP without forced states (VITERBI with them) as pairs of waves at NP = 512 or quads
  * at NP = 1,024; AUTO takes NP = 512 for N >= 384 or >= 8,192 sequences and NP = 1,024 for
  * N > 724, knobs CV_T64_512 / CV_T64_1024; an explicit TRELLIS_F64 gets it for any N <= 1,024),
- * else GENERIC (f32/f64, any association, N <= 20480 f32 / 10240 f64: two rows of N in
- * <= 160 KiB of LDS). */
+ * else GENERIC (f32/f64, any association, N <= 65535: one workgroup per sequence with two rows
+ * of N in LDS, or above N = 1024 -- always above 20480 f32 / 10240 f64 -- wide: one launch per
+ * step, each sequence's states over ceil(N / 256) workgroups, rows in global memory). */
 enum { CV_KERNEL_AUTO = 0, CV_KERNEL_TRELLIS = 1, CV_KERNEL_GENERIC = 2, CV_KERNEL_TRELLIS_F64 = 3 };
 
 /* cv_opts.flags */
@@ -114,8 +115,9 @@ typedef struct cv_timing {
   int64_t launches;      /* forward launches (chunks) */
   int32_t kernel;        /* CV_KERNEL_TRELLIS, _TRELLIS_F64 or _GENERIC actually used */
   int32_t padded_states; /* NP of the trellis kernel (0 for generic) */
-  int32_t mfma_tiles;    /* TRELLIS_F64: sequences per forward wave (last chunk); -1 otherwise
-                            (the field name is kept for ABI stability) */
+  int32_t mfma_tiles;    /* TRELLIS_F64: sequences per forward wave (last chunk); GENERIC: 0 wide
+                            (each step over many workgroups, N > 10240 f64 / 20480 f32), else -1;
+                            -1 otherwise (the field name is kept for ABI stability) */
 } cv_timing;
 
 typedef struct cv_superseq_desc {
@@ -287,7 +289,8 @@ CV_API cv_status cv_viterbi_decode(cv_hmm* h, int64_t T, const int32_t* obs, int
  * uncertified sequences (near ties at that magnitude) re-decoded from their predicted offsets
  * or re-run through the serial chain kernel -- bit-identical to the serial chain
  * (cv_last_superseq_stats).  Otherwise serial over
- * elements on the GPU (one workgroup), as the reference is on the CPU.  N <= 10240.
+ * elements on the GPU (one workgroup; above N = 1024 one launch per element with the states
+ * over workgroups), as the reference is on the CPU.  N <= 65535.
  * CV_EINFEASIBLE when the maximum is -inf. */
 CV_API cv_status cv_decode_superseq_cp(cv_hmm* h, int64_t nseq, const int64_t* offsets, const int32_t* obs,
                                        int32_t* path_out, double* objective_out);

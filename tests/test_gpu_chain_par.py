@@ -264,3 +264,34 @@ def test_chain_par_beyond_1024_equals_oracle(gpu, n):
     assert st2["rerun"] >= 1 and o2 == robj and np.array_equal(p2, rp), st2
     (p3, o3), st3 = _par(h, off, obs, force=2)  # speculation through the generic CP kernel
     assert st3["speculated"] >= 1 and o3 == robj and np.array_equal(p3, rp), st3
+
+
+@pytest.mark.parametrize("n,force", [(300, 2), (600, 1), (1100, 3)])
+def test_chain_par_wide_runs(gpu, monkeypatch, n, force):
+    """The wide chain (cp_chain_wide_step: one launch per element, the states over workgroups,
+    the rows in global memory; what runs above N = 10,240) as the parallel chain's serial runs
+    from a start row (CV_CHAIN_WIDE_MIN=1 brings it down to these N), and the whole serial chain
+    with the segmented backtrack: the oracle's chain either way."""
+    monkeypatch.setenv("CV_CHAIN_WIDE_MIN", "1")
+    pi, a, b, off, obs = _case(n, 11, 16, 1, 30, seed=5000 + n + force, zeros=(2,), ones=(7,))
+    h = cv.HMM(pi, a, b)
+    rp, robj = O.cp_superseq_f64(pi, a, b, off, obs)
+    (path, obj), st = _par(h, off, obs, force=force, spec=False)
+    assert st["parallel"] and st["rerun"] >= 1, st
+    assert obj == robj and np.array_equal(path, rp), st
+    sp, sobj = _serial(h, off, obs)
+    assert sobj == robj and np.array_equal(sp, rp)
+
+
+@pytest.mark.parametrize("n", [300, 1100])
+def test_chain_par_wide_speculation(gpu, monkeypatch, n):
+    """Speculative re-decodes through the wide generic CP kernel (start offsets cp_init, last
+    rows cp_last by sequence id; CV_GENERIC_WIDE_MIN=1 -- the certificates keep the rows mode):
+    the oracle's chain."""
+    monkeypatch.setenv("CV_GENERIC_WIDE_MIN", "1")
+    pi, a, b, off, obs = _case(n, 11, 16, 1, 30, seed=5100 + n, zeros=(2,), ones=(7,))
+    h = cv.HMM(pi, a, b)
+    (path, obj), st = _par(h, off, obs, force=2)
+    assert st["parallel"] and st["speculated"] >= 1, st
+    rp, robj = O.cp_superseq_f64(pi, a, b, off, obs)
+    assert obj == robj and np.array_equal(path, rp), st

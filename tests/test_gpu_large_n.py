@@ -1,8 +1,9 @@
-"""GPU: models beyond the padded kernels' N <= 256, up to the LDS-bound limits of the generic
-decode (two rows of N in <= 160 KiB: N <= 10,240 in f64, 20,480 in f32) and of the serial
-super-sequence chain (N <= 10,240).  The reference has no state limit (hmm.rs:10-18 stores any
-N; viterbi.rs:5-32, cp.rs:63-93 loop over it); every case is checked against the C oracle bit
-for bit, and one state past each limit is refused with CV_EUNSUPPORTED.
+"""GPU: models beyond the padded kernels' N <= 256: the generic decode with its rows in LDS
+(two rows of N in <= 160 KiB: N <= 10,240 in f64, 20,480 in f32) and wide above that (each step
+over many workgroups, the rows in global memory, up to the u16 back-pointers' N <= 65,535), the
+same for the serial super-sequence chain.  The reference has no state limit (hmm.rs:10-18 stores
+any N; viterbi.rs:5-32, cp.rs:63-93 loop over it); every case is checked against the C oracle
+bit for bit.
 """
 import numpy as np
 import pytest
@@ -26,8 +27,10 @@ def _case(n, v, seed, lengths):
 
 
 @pytest.mark.parametrize("dtype,n", [("f64", 4200), ("f64", 10240), ("f32", 8300)])
-def test_generic_decode_beyond_64k_lds(gpu, dtype, n):
-    """The generic kernel's two rows above 64 KiB of LDS (the launch raises the limit)."""
+def test_generic_decode_beyond_64k_lds(gpu, monkeypatch, dtype, n):
+    """The generic kernel's two rows above 64 KiB of LDS (the launch raises the limit; the wide
+    decode, the default at these N, off: CV_GENERIC_WIDE=0)."""
+    monkeypatch.setenv("CV_GENERIC_WIDE", "0")
     pi, a, b, off, obs = _case(n, 5, seed=n, lengths=[3, 0, 4] if n > 5000 else [5, 1, 6])
     h = cv.HMM(pi, a, b)
     got = cv.decode_batch(h, off, obs, dtype=dtype, assoc="viterbi", rescore_f64=False)
@@ -37,18 +40,91 @@ def test_generic_decode_beyond_64k_lds(gpu, dtype, n):
     assert np.array_equal(got[0], ref[0])
 
 
-def test_generic_decode_state_limit(gpu):
-    pi, a, b, off, obs = _case(10241, 3, seed=7, lengths=[2])
+@pytest.mark.parametrize("dtype,n,assocs", [("f64", 10241, ("viterbi", "cp", "dp", "decode", "forced")),
+                                            ("f32", 20481, ("viterbi", "cp"))])
+def test_generic_decode_beyond_lds(gpu, dtype, n, assocs):
+    """One state past the LDS-resident rows (2 N REAL > 160 KiB): the wide generic decode (each
+    step one launch, the states over workgroups, the rows in global memory) against the oracle,
+    incl. an empty sequence, a one-element sequence and forced states."""
+    pi, a, b, off, obs = _case(n, 4, seed=n, lengths=[3, 0, 2, 1])
     h = cv.HMM(pi, a, b)
-    with pytest.raises(cv.CVError) as e:
-        cv.decode_batch(h, off, obs, dtype="f64", assoc="viterbi", rescore_f64=False)
-    assert "LDS" in str(e.value)
+    dt = np.float32 if dtype == "f32" else np.float64
+    ASSOC = {"viterbi": O.VITERBI, "cp": O.CP, "dp": O.DP, "decode": O.DECODE, "forced": O.VITERBI}
+    for assoc in assocs:
+        fr = np.array([-1, n - 1, -1, 5, -1, -1], np.int32) if assoc == "forced" else None
+        got = cv.decode_batch(h, off, obs, dtype=dtype, assoc="viterbi" if fr is not None else assoc,
+                              rescore_f64=False, forced=fr)
+        t = cv.last_timing(h)
+        assert t["kernel"] == "generic" and t["seqs_per_wave"] == 0, t
+        ref = O.decode_batch(pi, a, b, off, obs, ASSOC[assoc], dt, forced=fr)
+        assert np.array_equal(got[2], ref[2]), assoc
+        ok = got[2] == 0
+        assert np.array_equal(got[1][ok], ref[1][ok]), assoc
+        assert np.array_equal(got[0], ref[0]), assoc
 
 
+@pytest.mark.parametrize("S", ["1", "2", "4"])
+@pytest.mark.parametrize("assoc", ["viterbi", "cp", "dp", "decode", "forced"])
+@pytest.mark.parametrize("dtype,n", [("f64", 300), ("f32", 300), ("f64", 1100)])
+def test_generic_wide_vs_oracle(gpu, monkeypatch, S, assoc, dtype, n):
+    """The wide generic decode at small N (CV_GENERIC_WIDE_MIN=1), S slots per workgroup
+    (CV_WIDE_S; ragged groups with finished and empty slots): ragged and empty sequences, -inf
+    transitions and emissions, forced states, every association -- the oracle bit for bit."""
+    monkeypatch.setenv("CV_GENERIC_WIDE_MIN", "1")
+    monkeypatch.setenv("CV_WIDE_S", S)
+    pi, a, b = synth.random_hmm(n, 11, seed=n + 55, zero_frac=0.1)
+    rng = np.random.default_rng(n + 55)
+    lens = rng.integers(1, 20, size=19)
+    lens[[4, 9]] = 0
+    lens[6] = 1
+    off = synth.offsets_from_lengths(lens)
+    obs = rng.integers(0, 11, size=int(off[-1])).astype(np.int32)
+    fr = None
+    if assoc == "forced":
+        fr = np.where(rng.random(len(obs)) < 0.08, rng.integers(0, n, size=len(obs)), -1).astype(np.int32)
+    ak = "viterbi" if assoc == "forced" else assoc
+    dt = np.float32 if dtype == "f32" else np.float64
+    h = cv.HMM(pi, a, b)
+    got = cv.decode_batch(h, off, obs, dtype=dtype, assoc=ak, kernel="generic", rescore_f64=False, forced=fr)
+    t = cv.last_timing(h)
+    assert t["kernel"] == "generic" and t["seqs_per_wave"] == 0, t
+    ref = O.decode_batch(pi, a, b, off, obs, {"viterbi": O.VITERBI, "cp": O.CP, "dp": O.DP, "decode": O.DECODE}[ak],
+                         dt, forced=fr)
+    assert np.array_equal(got[2], ref[2])
+    ok = got[2] == 0
+    assert np.array_equal(got[1][ok], ref[1][ok])
+    assert np.array_equal(got[0], ref[0])
+
+
+def test_superseq_chain_wide_beyond_lds(gpu):
+    """The serial super-sequence chain one state past its LDS-resident rows (N = 10,241: the
+    wide chain, then the segmented backtrack) against the chained restatement."""
+    n, v = 10241, 3
+    rng = np.random.default_rng(10241)
+    pi = np.round(rng.uniform(-2, 0, n) * 4) / 4
+    a = np.round(rng.uniform(-2, 0, (n, n)) * 4) / 4
+    b = np.round(rng.uniform(-2, 0, (n, v)) * 4) / 4
+    off = synth.offsets_from_lengths(np.asarray([2, 0, 1, 2]))
+    obs = rng.integers(0, v, size=int(off[-1])).astype(np.int32)
+    h = cv.HMM(pi, a, b)
+    path, obj = cv.decode_superseq_cp(h, off, obs)
+    assert not cv.last_superseq_stats(h)["parallel"]
+    rp, robj = O.cp_superseq_f64(pi, a, b, off, obs)
+    assert obj == robj
+    assert np.array_equal(path, rp)
+
+
+@pytest.mark.parametrize("wide", ["0", "1"])
 @pytest.mark.parametrize("n", [300, 1100, 2500])
-def test_superseq_chain_strided_states(gpu, n):
+def test_superseq_chain_strided_states(gpu, monkeypatch, n, wide):
     """cp_superseq_chain with N > 256 (and > 1,024: states strided over the workgroup's 1,024
-    threads), every element and the objective against the chained restatement."""
+    threads), every element and the objective against the chained restatement; wide = "1": the
+    serial chain as the wide kernels (CV_CHAIN_WIDE_MIN=1, CV_CHAIN_PAR=0)."""
+    if wide == "1":
+        monkeypatch.setenv("CV_CHAIN_WIDE_MIN", "1")
+        monkeypatch.setenv("CV_CHAIN_PAR", "0")
+    else:  # the one-workgroup chain (states strided above 1,024 threads; wide is the default there)
+        monkeypatch.setenv("CV_CHAIN_WIDE", "0")
     rng = np.random.default_rng(70 + n)
     v = 7
     # quantised tables: exact ties, the first index must win in every strided slice
@@ -151,6 +227,7 @@ def test_generic_multi_sequence_workgroups(gpu, monkeypatch, rows, S, assoc, dty
     workgroup, forced states, -inf transitions and emissions, N above 1,024 threads."""
     monkeypatch.setenv("CV_GENERIC_S", S)
     monkeypatch.setenv("CV_GENERIC_ROWS", rows)
+    monkeypatch.setenv("CV_GENERIC_WIDE", "0")  # N = 1,100: the one-workgroup kernels, not wide
     pi, a, b = synth.random_hmm(n, 11, seed=n + 5, zero_frac=0.1)
     rng = np.random.default_rng(n + int(S))
     lens = rng.integers(1, 24, size=23)
