@@ -3352,7 +3352,11 @@ cv_status superseq_cp_par(cv_hmm* h, int64_t nseq, const int64_t* offsets, const
     cv_opts oc = default_opts();
     oc.dtype = CV_DTYPE_F64;
     oc.assoc = CV_ASSOC_CP;
-    oc.kernel = small ? CV_KERNEL_TRELLIS_F64 : CV_KERNEL_GENERIC;  // trellis_cp_f64 / generic_fwd_ms (psi)
+    // trellis_cp_f64 / generic_fwd_ms (psi); CV_CHAIN_SPEC_KERNEL=generic|trellis (read per call:
+    // A/B knob, bit-identical) picks for N <= 256
+    const char* sk = getenv("CV_CHAIN_SPEC_KERNEL");
+    const bool spec_generic = !small || (sk && *sk == 'g');
+    oc.kernel = spec_generic ? CV_KERNEL_GENERIC : CV_KERNEL_TRELLIS_F64;
     oc.rescore_f64 = 0;
     oc.stream = stream;
     double* sc = d_sres.as<double>();
@@ -3365,6 +3369,7 @@ cv_status superseq_cp_par(cv_hmm* h, int64_t nseq, const int64_t* offsets, const
     HIP_TRY(hipMemcpyAsync(spec_path.data(), d_spath.p, (size_t)Ls * 4, hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipMemcpyAsync(spec_last.data(), d_slast.p, (size_t)nf * N * 8, hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipStreamSynchronize(stream));
+    trace_mark("chain: speculative batch (pack, decode, D2H)");
     spec_off = std::move(so);
     spec_guess = std::move(G);
     for (int64_t i = 0; i < nf; ++i) spec_idx[(size_t)F[i]] = i;
