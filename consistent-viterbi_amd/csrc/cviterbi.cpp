@@ -3352,10 +3352,11 @@ cv_status superseq_cp_par(cv_hmm* h, int64_t nseq, const int64_t* offsets, const
     cv_opts oc = default_opts();
     oc.dtype = CV_DTYPE_F64;
     oc.assoc = CV_ASSOC_CP;
-    // trellis_cp_f64 / generic_fwd_ms (psi); CV_CHAIN_SPEC_KERNEL=generic|trellis (read per call:
-    // A/B knob, bit-identical) picks for N <= 256
+    // generic_fwd_ms (psi, one state per thread, one sequence per workgroup) or, N <= 256,
+    // trellis_cp_f64 by CV_CHAIN_SPEC_KERNEL=trellis (read per call: A/B knob, bit-identical):
+    // config-4 size, 620 sequences, the batch 15-17 vs 17-17.7 ms (profiles/r05_spec_ab.txt)
     const char* sk = getenv("CV_CHAIN_SPEC_KERNEL");
-    const bool spec_generic = !small || (sk && *sk == 'g');
+    const bool spec_generic = !small || !(sk && *sk == 't');
     oc.kernel = spec_generic ? CV_KERNEL_GENERIC : CV_KERNEL_TRELLIS_F64;
     oc.rescore_f64 = 0;
     oc.stream = stream;

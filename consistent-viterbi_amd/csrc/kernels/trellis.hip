@@ -1235,18 +1235,30 @@ __global__ __launch_bounds__(256) void generic_fwd(GenericFwdArgs<REAL> args) {
 // over ceil(N / 256) workgroups, S consecutive slots per workgroup (each table element loaded
 // once for the S), the rows in global memory (args.grows) -- where one workgroup per sequence
 // would stream the N x N table (>= 134 MB at N = 4,096 f64) through a single CU every step.
-// XCD-aware: blocks b and b + 8 share an XCD (MI355X_MICROARCH.md: dealt round-robin), so block
-// b takes column block jb = b % 8 + 8 k: each XCD's L2 serves a fixed eighth of the table's
-// columns to every slot group (the column blocks are padded to a multiple of 8; a padding
-// block exits at once).  The same candidates in the same order per state as generic_fwd
+// XCD-aware when the column blocks come in eights (xcd = 1): blocks b and b + 8 share an XCD
+// (MI355X_MICROARCH.md: dealt round-robin), so block b takes column block jb = b % 8 + 8 k and
+// each XCD's L2 serves a fixed eighth of the table's columns to every slot group; otherwise
+// (xcd = 0) jb = b % nblk (padding to eights put every block of N <= 256 on one XCD: 165 us
+// per step at 620 sequences).  The candidate loop keeps the previous rows on the scalar path and
+// no barriers (the pipelined LDS-tile loop of wide.h, tried here: slower at few sequences,
+// 6.7 vs 5.6 ms at N = 10,240 x 4).  The same candidates in the same order per state as generic_fwd
 // (viterbi.rs:5-32, cp.rs:70-79, dp.rs, decode), so the same values, back-pointers and statuses
 // bit for bit.  t = 0 seeds row 0; the step at t = T - 1 also writes the sequence's last row.
 template <typename REAL, int S>
-__global__ __launch_bounds__(256) void generic_wide_step(GenericFwdArgs<REAL> args, int t, int nblk8, int64_t nslots) {
+__global__ __launch_bounds__(256) void generic_wide_step(GenericFwdArgs<REAL> args, int t, int nblk, int xcd,
+                                                        int64_t nslots) {
   const int N = args.nstates;
-  const int64_t k = (int64_t)(blockIdx.x >> 3);
-  const int jb = (int)(blockIdx.x & 7) + 8 * (int)(k % nblk8);
-  const int64_t g0 = (k / nblk8) * S;  // first local slot of the group
+  int jb;
+  int64_t grp;
+  if (xcd) {
+    const int64_t k = (int64_t)(blockIdx.x >> 3);
+    jb = (int)(blockIdx.x & 7) + 8 * (int)(k % (nblk >> 3));
+    grp = k / (nblk >> 3);
+  } else {
+    jb = (int)(blockIdx.x % (unsigned)nblk);
+    grp = (int64_t)(blockIdx.x / (unsigned)nblk);
+  }
+  const int64_t g0 = grp * S;  // first local slot of the group
   const int j = jb * 256 + (int)threadIdx.x;
   if (j >= N) return;
   const REAL ninf = -__builtin_inf();
@@ -1364,11 +1376,15 @@ inline int generic_wide_seqs(int n, int64_t nseq) {
 
 template <typename REAL, int S>
 hipError_t launch_generic_wide_s(const GenericFwdArgs<REAL>& fa, int64_t nseq, hipStream_t stream) {
-  const int nblk8 = ((fa.nstates + 255) / 256 + 7) / 8;
-  const int64_t grid = (nseq + S - 1) / S * nblk8 * 8;
+  const int nblk = (fa.nstates + 255) / 256;
+  // XCD-aware column blocks when they come in eights (CV_WIDE_XCD=0: never; A/B knob, read per
+  // launch, bit-identical)
+  const char* xe = getenv("CV_WIDE_XCD");
+  const int xcd = (nblk % 8 == 0 && !(xe && *xe == '0')) ? 1 : 0;
+  const int64_t grid = (nseq + S - 1) / S * nblk;
   if (grid > (int64_t)INT32_MAX) return hipErrorInvalidValue;
   for (int64_t t = 0; t < fa.wide_steps; ++t) {
-    hipLaunchKernelGGL((generic_wide_step<REAL, S>), dim3((unsigned)grid), dim3(256), 0, stream, fa, (int)t, nblk8,
+    hipLaunchKernelGGL((generic_wide_step<REAL, S>), dim3((unsigned)grid), dim3(256), 0, stream, fa, (int)t, nblk, xcd,
                        nseq);
     const hipError_t err = hipGetLastError();
     if (err != hipSuccess) return err;

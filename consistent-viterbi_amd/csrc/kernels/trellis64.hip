@@ -31,6 +31,7 @@
 #include "trellis.h"
 #include "trellis64.h"
 #include "wave64.h"
+#include "wide.h"
 
 namespace cvk {
 
@@ -2252,32 +2253,31 @@ __global__ __launch_bounds__(1024) void cp_superseq_chain(CpChainArgs g) {
 // order and roundings as cp_superseq_chain (cp.rs:70-79 over utils.rs:24-38).  Element 0
 // without init_row seeds pi + b (cp.rs:66-68); with it, the host has put init_row in row 1.
 __global__ __launch_bounds__(256) void cp_chain_wide_step(CpChainArgs g, int64_t t) {
+  __shared__ double tile[256];
   const int N = g.nstates;
   const int j = (int)blockIdx.x * 256 + (int)threadIdx.x;
-  if (j >= N) return;
+  const bool jv = j < N;  // threads past N stay for the tile barriers
+  const int jc = jv ? j : N - 1;
   double* cur = g.grows + (t & 1) * N;
-  const double* prev = g.grows + ((t & 1) ^ 1) * N;
+  const double* prev[1] = {g.grows + ((t & 1) ^ 1) * N};
   const int o = g.obs[t];
-  if (t == 0 && !g.init_row) {
-    cur[j] = g.pi[j] + g.et[(size_t)o * N + j];
+  if (t == 0 && !g.init_row) {  // workgroup-uniform
+    if (jv) cur[j] = g.pi[j] + g.et[(size_t)o * N + j];
     return;
   }
   const bool first = g.first[t] != 0;
-  const double pj = g.pi[j];
-  const double* __restrict__ col = g.a + j;
-  double m = prev[0] + (first ? pj : col[0]);
-  int arg = 0;
-#pragma unroll 8
-  for (int i = 1; i < N; ++i) {
-    const double x = prev[i] + (first ? pj : col[(size_t)i * N]);
-    if (x > m) {
-      m = x;
-      arg = i;
-    }
-  }
-  const double tr = first ? pj : col[(size_t)arg * N];
-  cur[j] = prev[arg] + (tr + g.et[(size_t)o * N + j]);
-  g.psi[t * N + j] = (uint16_t)arg;
+  const double pj = g.pi[jc];
+  const double* __restrict__ col = g.a + jc;
+  const double e[1] = {0.0};
+  double m[1];
+  int arg[1];
+  // the first index of the maximum of prev[i] + (first ? pi[j] : a[i][j]) (strict '>' from -inf:
+  // i = 0 seeds it whenever it is above -inf, as cp_superseq_chain's m = prev[0] + ...)
+  wide_candidates<double, 1, false>(first ? nullptr : col, N, prev, e, m, arg, tile, pj);
+  if (!jv) return;
+  const double tr = first ? pj : col[(size_t)arg[0] * N];
+  cur[j] = prev[0][arg[0]] + (tr + g.et[(size_t)o * N + j]);
+  g.psi[t * N + j] = (uint16_t)arg[0];
 }
 
 // the last row's first argmax (cp.rs:85-87), final_row, and the single-thread backtrack when

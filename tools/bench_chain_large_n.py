@@ -63,15 +63,15 @@ def main():
     print(f"  again: {t2*1e3:.1f} ms, same result {bool(np.array_equal(p1, p2) and o1 == o2)}", flush=True)
     if os.environ.get("SERIAL", "1") == "0":
         print("  (serial comparison skipped: SERIAL=0)", flush=True)
-        return
-    print(f"  serial chain (cp_superseq_chain, one thread per state) over the same {L} elements ...", flush=True)
-    p0, o0, t0, s0 = run(h, off, obs, serial=True)
-    same = bool(np.array_equal(p1, p0) and o1 == o0)
-    print(f"  serial chain {t0:.2f} s ({t0/L*1e6:.2f} us/element), objective {o0!r}, parallel == serial: {same}, "
-          f"speedup {t0/t1:.1f}x", flush=True)
-    if not same:
-        bad = np.nonzero(p1 != p0)[0]
-        raise SystemExit(f"parallel chain differs from the serial chain: {bad.size} elements, first {bad[:5]}")
+    else:
+        print(f"  serial chain (cp_superseq_chain, one thread per state) over the same {L} elements ...", flush=True)
+        p0, o0, t0, s0 = run(h, off, obs, serial=True)
+        same = bool(np.array_equal(p1, p0) and o1 == o0)
+        print(f"  serial chain {t0:.2f} s ({t0/L*1e6:.2f} us/element), objective {o0!r}, parallel == serial: {same}, "
+              f"speedup {t0/t1:.1f}x", flush=True)
+        if not same:
+            bad = np.nonzero(p1 != p0)[0]
+            raise SystemExit(f"parallel chain differs from the serial chain: {bad.size} elements, first {bad[:5]}")
     if nbig > 0:
         ob, bb = off_all[:nbig + 1], obs_all[:off_all[nbig]]
         Lb = int(ob[-1])

@@ -1,25 +1,27 @@
-"""Timeline of one rocprofv3 --kernel-trace CSV: per-kernel spans (in dispatch order) and the
-device-idle gaps between them, for the last `--last` ms of the trace (the final timed call).
-Usage: python tools/trace_gaps.py <kernel_trace.csv> [--window-ms W]"""
+"""Per-kernel durations and the gaps between consecutive dispatches from a rocprofv3
+--kernel-trace CSV (kernel_trace.csv): python tools/trace_gaps.py <dir> [kernel regex]"""
 import csv
+import glob
+import os
+import re
 import sys
 
-path = sys.argv[1]
-win = float(sys.argv[sys.argv.index("--window-ms") + 1]) if "--window-ms" in sys.argv else 400.0
+d = sys.argv[1]
+rx = re.compile(sys.argv[2] if len(sys.argv) > 2 else ".")
 rows = []
-for r in csv.DictReader(open(path)):
-    rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"][:70], r.get("Queue_Id", "")))
+for f in glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True):
+    for r in csv.DictReader(open(f)):
+        rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
 rows.sort()
-t_end = max(e for _, e, _, _ in rows)
-rows = [r for r in rows if r[1] >= t_end - win * 1e6]
-t0 = rows[0][0]
-busy_until = t0
-idle = 0.0
-for s, e, n, q in rows:
-    gap = (s - busy_until) / 1e6
-    if gap > 0.05:
-        print(f"   idle {gap:8.3f} ms")
-        idle += gap
-    print(f"{(s - t0) / 1e6:9.3f} -> {(e - t0) / 1e6:9.3f} ms ({(e - s) / 1e6:8.3f}) q{q} {n}")
-    busy_until = max(busy_until, e)
-print(f"span {(busy_until - t0) / 1e6:.3f} ms, device idle {idle:.3f} ms")
+sel = [(s, e, k) for s, e, k in rows if rx.search(k)]
+if not sel:
+    sys.exit("no kernels matched")
+dur = [e - s for s, e, _ in sel]
+gaps = [sel[i + 1][0] - sel[i][1] for i in range(len(sel) - 1)]
+gaps.sort()
+print(f"{len(sel)} dispatches of /{rx.pattern}/: mean duration {sum(dur) / len(dur) / 1e3:.2f} us, "
+      f"median gap {gaps[len(gaps) // 2] / 1e3 if gaps else 0:.2f} us, p90 gap {gaps[int(len(gaps) * 0.9)] / 1e3 if gaps else 0:.2f} us")
+names = sorted({k for _, _, k in sel})
+for n in names[:6]:
+    dd = [e - s for s, e, k in sel if k == n]
+    print(f"  {len(dd):6d} x {sum(dd) / len(dd) / 1e3:9.2f} us  {n[:110]}")
