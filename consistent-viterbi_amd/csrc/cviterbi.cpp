@@ -211,6 +211,7 @@ struct cv_hmm {
   } side;
   DevBuf st_off, st_obs, st_path, st_score, st_status, st_forced;
   DevBuf cs_ranges, cs_delta, cs_g, cs_mu, cs_start, cs_zero, cs_queue;  // constrained-decode scratch
+  DevBuf cs_wrows;  // the wide generic_ext's rows ([slot][2][N], N > 10,240)
   DevBuf cs_comp, cs_words;  // device exact unary sums: per-sequence components, output words
   DevBuf cs_flag;            // device exact sums: out-of-range term flag
   DevBuf cs_seg;             // segment-table rows (cs_delta keeps the prefix rows t_1)
@@ -1478,8 +1479,8 @@ std::vector<int32_t> conseq_pairs(const std::vector<ConSeq>& cs, const int32_t* 
 
 // The constrained decode's arithmetic: the row-A0 association (the terms of csp.hpp are
 // defined on it) in f64 -- the reference's precision: trellis_fwd_f64 for N <= 256, the
-// generic kernels above (generic_ext + generic_fwd, N <= generic_max_states) -- or f32 (the
-// f32 trellis, N <= 256).
+// generic kernels above (generic_ext + generic_fwd, wide above N = 10,240, N <= 65,535) -- or
+// f32 (the f32 trellis, N <= 256).
 bool constrained_generic(const cv_hmm* h, const cv_opts& o) {
   return o.dtype == CV_DTYPE_F64 && !cvk::t64_padded_states(h->N);
 }
@@ -1487,10 +1488,10 @@ bool constrained_generic(const cv_hmm* h, const cv_opts& o) {
 cv_status constrained_dtype_check(const cv_hmm* h, const cv_opts& o) {
   if (o.assoc != CV_ASSOC_VITERBI)
     return set_err(CV_EUNSUPPORTED, "constrained decode runs the row-A0 (VITERBI) association");
-  if (o.dtype == CV_DTYPE_F64 && (cvk::t64_padded_states(h->N) || h->N <= cvk::generic_max_states(8))) return CV_OK;
+  if (o.dtype == CV_DTYPE_F64 && (cvk::t64_padded_states(h->N) || h->N <= cvk::kGenericGlobalMaxStates)) return CV_OK;
   if (o.dtype == CV_DTYPE_F32 && cvk::trellis_padded_states(h->N)) return CV_OK;
   return set_err(CV_EUNSUPPORTED, "constrained decode needs f64 with N <= %d, or f32 with N <= 256 (N=%d)",
-                 cvk::generic_max_states(8), h->N);
+                 cvk::kGenericGlobalMaxStates, h->N);
 }
 
 cv_status constrained_validate(cv_hmm* h, int64_t nseq, const int64_t* offsets, const int32_t* obs,
@@ -1780,6 +1781,12 @@ cv_status constrained_partials_locked(cv_hmm* h, int64_t nseq, const int64_t* of
     ga.ranges = h->cs_ranges.as<int64_t>();
     ga.nstates = N;
     ga.last_row = h->cs_delta.as<double>();
+    if (cvk::generic_ext_wide(N)) {  // the rows in global memory, one launch per step
+      // sized once for the segment tables' batches too (no reallocation under running launches)
+      if ((st = h->cs_wrows.ensure((size_t)nslot_max * 2 * N * 8)) != CV_OK) return st;
+      ga.grows = h->cs_wrows.as<double>();
+      for (int64_t i = 0; i < 2 * nc; ++i) ga.wide_steps = std::max<int64_t>(ga.wide_steps, rg[2 * i + 1] - rg[2 * i]);
+    }
     err = cvk::launch_generic_ext(ga, nc, stream);
     if (err == hipSuccess) {
       ga.tab = h->d_at64.as<double>();
@@ -1994,6 +2001,11 @@ cv_status constrained_partials_locked(cv_hmm* h, int64_t nseq, const int64_t* of
       sa.start = h->cs_start.as<int32_t>();
       sa.nstates = N;
       sa.last_row = h->cs_seg.as<double>();
+      if (cvk::generic_ext_wide(N)) {
+        if ((st = h->cs_wrows.ensure((size_t)nb * 2 * N * 8)) != CV_OK) return st;
+        sa.grows = h->cs_wrows.as<double>();
+        for (int64_t k = 0; k < nb; ++k) sa.wide_steps = std::max<int64_t>(sa.wide_steps, srg[2 * k + 1] - srg[2 * k]);
+      }
       err = cvk::launch_generic_ext(sa, nb, stream);
     } else if (!f64) {
       cvk::TrellisFwdArgs sa{};

@@ -232,7 +232,13 @@ struct GenericExtArgs {
   int reverse, noemit_last;
   int nstates;
   double* last_row;        // [slot][N]
+  // wide (N > generic_max_states(8), or from CV_EXT_WIDE_MIN states: read per call, tests):
+  // grows = [slot][2][N] global rows, wide_steps = the longest range; one launch per step,
+  // each slot's states over ceil(N / 256) workgroups
+  double* grows;
+  int64_t wide_steps;
 };
 hipError_t launch_generic_ext(const GenericExtArgs& g, int64_t nslots, hipStream_t stream);
+bool generic_ext_wide(int n);
 
 }  // namespace cvk

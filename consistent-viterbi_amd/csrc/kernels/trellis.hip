@@ -2237,8 +2237,59 @@ hipError_t launch_generic_ext_s(const GenericExtArgs& g, int64_t nslots, hipStre
   return hipGetLastError();
 }
 
+// generic_ext wide: step t of every slot, the slot's states over nblk workgroups (block = slot
+// x nblk + column block), its two rows in g.grows -- the constrained decode's terms passes and
+// segment tables above N = 10,240.  Values only (an order-free maximum): generic_ext's rows bit
+// for bit.
+__global__ __launch_bounds__(256) void generic_ext_wide_step(GenericExtArgs g, int t, int nblk, int64_t nslots) {
+  const int N = g.nstates;
+  const int64_t slot = (int64_t)(blockIdx.x / (unsigned)nblk);
+  const int j = (int)(blockIdx.x % (unsigned)nblk) * 256 + (int)threadIdx.x;
+  if (slot >= nslots || j >= N) return;
+  const int64_t b0 = g.ranges[2 * slot];
+  const int T = (int)(g.ranges[2 * slot + 1] - b0);
+  if (t >= T) return;
+  const double ninf = -__builtin_inf();
+  const int64_t el = g.reverse ? b0 + T - 1 - t : b0 + t;
+  const double e = g.et[(size_t)g.obs[el] * N + j];
+  const bool emit = !(g.noemit_last && t == T - 1);
+  double* cur = g.grows + slot * 2 * N + (t & 1) * N;
+  double v;
+  if (t == 0) {
+    const int st = g.start ? g.start[slot] : -1;
+    v = st >= 0 ? (j == st ? 0.0 : ninf) : emit ? g.pi[j] + e : g.pi[j];
+  } else {
+    const double* prev = g.grows + slot * 2 * N + ((t & 1) ^ 1) * N;
+    const double* col = g.tab + j;
+    double m = ninf;
+#pragma unroll 8
+    for (int i = 0; i < N; ++i) m = fmax(m, prev[i] + col[(size_t)i * N]);
+    v = emit ? m + e : m;
+  }
+  cur[j] = v;
+  if (t == T - 1) g.last_row[slot * N + j] = v;
+}
+
+bool generic_ext_wide(int n) {
+  if (n > generic_max_states(8)) return true;
+  const char* e = getenv("CV_EXT_WIDE_MIN");
+  return e && *e && n >= atoi(e);
+}
+
 hipError_t launch_generic_ext(const GenericExtArgs& g, int64_t nslots, hipStream_t stream) {
   if (nslots <= 0) return hipSuccess;
+  if (g.grows) {
+    if (g.nstates <= 0 || g.nstates > kGenericGlobalMaxStates) return hipErrorInvalidValue;
+    const int nblk = (g.nstates + 255) / 256;
+    if (nslots * nblk > (int64_t)INT32_MAX) return hipErrorInvalidValue;
+    for (int64_t t = 0; t < g.wide_steps; ++t) {
+      hipLaunchKernelGGL(generic_ext_wide_step, dim3((unsigned)(nslots * nblk)), dim3(256), 0, stream, g, (int)t, nblk,
+                         nslots);
+      const hipError_t err = hipGetLastError();
+      if (err != hipSuccess) return err;
+    }
+    return hipSuccess;
+  }
   if (g.nstates <= 0 || g.nstates > generic_max_states(8)) return hipErrorInvalidValue;
   // as generic_fwd_ms: 4 slots while their rows fit and the launch keeps >= 2 workgroups per
   // CU, CV_GENERIC_S=k sets it

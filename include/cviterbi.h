@@ -207,7 +207,7 @@ CV_API cv_status cv_timing_end(cv_hmm* h, cv_timing* out);
  * component order); then a forced decode.  Row-A0 (VITERBI) association, every term,
  * segment table and the final decode in opts->dtype: CV_DTYPE_F64 (default; the reference's
  * precision, cp.rs:95-126 / dp.rs:147-166 compute in f64: trellis_fwd_f64 for N <= 256, the
- * generic kernels up to N = 10240) or CV_DTYPE_F32 (the f32 trellis, N <= 256, scores f64
+ * generic kernels up to N = 65535, wide above 10240) or CV_DTYPE_F32 (the f32 trellis, N <= 256, scores f64
  * re-scored).  A term outside the exact unit (|score| >= 2^32) is
  * CV_EINVAL.  comp_state_out[ncomp] gets s_c (-1: no active element, or no feasible assignment
  * of its group); objective_out = sum of the per-sequence scores.  CV_ELIMIT if the search

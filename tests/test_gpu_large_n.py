@@ -187,6 +187,50 @@ def test_constrained_f64_beyond_256(gpu, monkeypatch, S, n, multi):
     assert obj == pytest.approx(float(np.sum(score)), rel=1e-12)
 
 
+@pytest.mark.parametrize("n,multi", [(257, True), (400, True), (520, False)])
+def test_constrained_f64_wide(gpu, monkeypatch, n, multi):
+    """The constrained decode with the wide kernels (what runs above N = 10,240): the terms
+    passes and segment tables through generic_ext's wide step (CV_EXT_WIDE_MIN=1), the final
+    forced decode through the wide generic decode (CV_GENERIC_WIDE_MIN=1) -- the oracle spec."""
+    monkeypatch.setenv("CV_EXT_WIDE_MIN", "1")
+    monkeypatch.setenv("CV_GENERIC_WIDE_MIN", "1")
+    pi, a, b, off, obs, comp = _constrained_case(n, seed=n + 7, multi=multi)
+    h = cv.HMM(pi, a, b)
+    path, score, status, states, obj = cv.decode_constrained(h, off, obs, comp, dtype="f64")
+    ref_states, forced = O.constrained_forced(pi, a, b, off, obs, comp, np.float64)
+    for c, s in ref_states.items():
+        assert states[c] == s, (c, states[c], s)
+    rp, rs, rst = O.decode_batch(pi, a, b, off, obs, O.VITERBI, np.float64, forced=forced)
+    assert np.array_equal(status, rst)
+    assert np.array_equal(path, rp)
+    assert np.array_equal(score[status == 0], rs[status == 0])
+
+
+def test_constrained_f64_beyond_lds(gpu):
+    """One state past the LDS-resident rows (N = 10,241): the constrained decode's terms passes
+    wide, one-position sequences (the oracle's C max-marginal), the oracle spec bit for bit."""
+    n = 10241
+    rng = np.random.default_rng(n)
+    pi = np.log10(rng.dirichlet(np.ones(n)))
+    a = rng.uniform(-4.0, 0.0, (n, n))
+    b = rng.uniform(-3.0, 0.0, (n, 5))
+    a[rng.random((n, n)) < 0.05] = -np.inf
+    lens = np.array([3, 1, 4, 2])
+    off = synth.offsets_from_lengths(lens)
+    obs = rng.integers(0, 5, size=int(off[-1])).astype(np.int32)
+    comp = np.full(len(obs), -1, np.int32)
+    comp[[0, 3, 6, 8]] = [0, 1, 0, 1]  # one position each: t = 0, the one-element sequence, t = 2, t = 0
+    h = cv.HMM(pi, a, b)
+    path, score, status, states, obj = cv.decode_constrained(h, off, obs, comp, dtype="f64")
+    ref_states, forced = O.constrained_forced(pi, a, b, off, obs, comp, np.float64)
+    for c, s in ref_states.items():
+        assert states[c] == s, (c, states[c], s)
+    rp, rs, rst = O.decode_batch(pi, a, b, off, obs, O.VITERBI, np.float64, forced=forced)
+    assert np.array_equal(status, rst)
+    assert np.array_equal(path, rp)
+    assert np.array_equal(score[status == 0], rs[status == 0])
+
+
 def test_constrained_device_and_sharded_beyond_256(gpu):
     """The device API and the sharded partials (integer SUM over shards) at N = 300 equal the
     host API's result."""
