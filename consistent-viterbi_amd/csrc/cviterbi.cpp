@@ -3920,7 +3920,7 @@ cv_status fit_validate(int32_t N, int64_t V, int64_t nseq, const int64_t* offset
 }
 
 struct FitDev {
-  DevBuf off, obs, tags, pi, a, at, et, alpha, beta, rscale, acc, cnt, ord, dump;
+  DevBuf off, obs, tags, pi, a, at, et, alpha, beta, rscale, acc, cnt, ord, dump, gscratch;
 };
 
 }  // namespace
@@ -4006,6 +4006,12 @@ CV_API cv_status cv_hmm_fit_train(int32_t nstates, int64_t nobs, int64_t nseq, c
   cv_status st = fit_validate(N, V, nseq, offsets, obs, tags, false, pi, a, b);
   if (st != CV_OK) return st;
   if (N > cvf::kBwMaxStates) return set_err(CV_EUNSUPPORTED, "Baum-Welch covers N <= %d (N=%d)", cvf::kBwMaxStates, N);
+  // the strided kernels' vectors in global scratch: above kBwLdsMaxStates, or from N = 257
+  // with CV_BW_GLOBAL=1 (A/B knob and tests)
+  const bool bw_global = N > cvf::kBwLdsMaxStates || (N > cvf::kBwMmStates && [] {
+                           const char* e = getenv("CV_BW_GLOBAL");
+                           return e && *e == '1';
+                         }());
   if (max_iter < 0) return set_err(CV_EINVAL, "max_iter < 0");
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) {
@@ -4047,12 +4053,14 @@ CV_API cv_status cv_hmm_fit_train(int32_t nstates, int64_t nobs, int64_t nseq, c
     return st;
   const size_t nacc = 3 * (size_t)N + (size_t)V * N + (size_t)N * N + 1;
   constexpr int kPartsB = 1024;  // blocks of the b M-step = partial convergence sums
+  const int parts_a = N > cvf::kBwLdsMaxStates ? 1024 : 1;  // blocks of the pi / a M-step
   if ((st = d.acc.ensure(nacc * 8)) != CV_OK) return st;
   if ((st = d.pi.ensure((size_t)N * 8)) != CV_OK) return st;
   if ((st = d.a.ensure((size_t)N * N * 8)) != CV_OK) return st;
   if ((st = d.at.ensure((size_t)N * N * 8)) != CV_OK) return st;
   if ((st = d.et.ensure((size_t)V * N * 8)) != CV_OK) return st;
-  if ((st = d.cnt.ensure((1 + kPartsB) * 8)) != CV_OK) return st;
+  if ((st = d.cnt.ensure((size_t)(parts_a + kPartsB) * 8)) != CV_OK) return st;
+  if (bw_global && (st = d.gscratch.ensure((size_t)cvf::kBwScratchSeqs * 4 * N * 8)) != CV_OK) return st;
   if ((st = d.dump.ensure((size_t)cvf::kBwDumpWaves * 64 * 8)) != CV_OK) return st;
   int cus = 0;
   HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
@@ -4081,7 +4089,8 @@ CV_API cv_status cv_hmm_fit_train(int32_t nstates, int64_t nobs, int64_t nseq, c
   m.at = d.at.as<double>();
   m.et = d.et.as<double>();
   m.part = d.cnt.as<double>();
-  std::vector<double> part(1 + kPartsB);
+  m.parts_a = parts_a;
+  std::vector<double> part((size_t)(parts_a + kPartsB));
   {
     // longest sequences first within each chunk (indices relative to the chunk)
     std::vector<int64_t> ord((size_t)nseq);
@@ -4106,6 +4115,7 @@ CV_API cv_status cv_hmm_fit_train(int32_t nstates, int64_t nobs, int64_t nseq, c
       g.elem_base = off0[c.first];
       g.order = d.ord.as<int64_t>() + c.first;
       g.dump = d.dump.as<double>();
+      g.gscratch = bw_global ? d.gscratch.as<double>() : nullptr;
       g.nstates = N;
       g.pi = d.pi.as<double>();
       g.a = d.a.as<double>();

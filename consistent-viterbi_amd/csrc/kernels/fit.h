@@ -8,8 +8,11 @@ namespace cvf {
 
 constexpr int kBwLdsStates = 128;  // bw_stats keeps a sequence's N x N xi sum in LDS up to here
 constexpr int kBwMmStates = 256;   // up to here: the matrix-core step kernels (bw_*_mm)
-constexpr int kBwMaxStates = 4096; // beyond kBwMmStates: states strided over 256 threads, the
-                                   // step's vector and 3 gamma sums in LDS (4 N doubles)
+constexpr int kBwLdsMaxStates = 4096;  // beyond kBwMmStates: states strided over 256 threads, the
+                                       // step's vector and 3 gamma sums in LDS (4 N doubles)
+constexpr int kBwMaxStates = 65535;    // beyond kBwLdsMaxStates: the same vectors in global
+                                       // scratch (BwArgs::gscratch), kBwScratchSeqs per launch
+constexpr int kBwScratchSeqs = 2048;
 
 struct MleArgs {
   const int64_t* offsets;
@@ -39,6 +42,8 @@ struct BwArgs {
   double* beta;         // [elements][N] workspace
   double* rscale;       // [elements] N > 64 matrix-core path: row t of R = alpha_t * rscale[t]
                         // (1 / (c_t 2^k), 0 where c_t = 0 or t = T - 1); null: R is stored over alpha
+  double* gscratch;     // [kBwScratchSeqs][4 N] N > kBwLdsMaxStates (or CV_BW_GLOBAL=1 above 256):
+                        // the strided kernels' per-sequence vectors in global memory
   double* dump;         // [kBwDumpWaves][64] N <= 64 kernels: target of the stores / atomic adds
                         // of lanes without a state (one row per wave: no shared hot line)
   // E-step sums (accumulated across sequences; zeroed by the host per iteration)
@@ -63,7 +68,8 @@ struct MstepArgs {
   double* a;     // [N][N]  updated in place
   double* at;    // [N][N]  transposed copy, rewritten
   double* et;    // [V][N]  b^T, updated in place
-  double* part;  // [1 + nparts_b] per-block sums of |new - old|
+  double* part;  // [parts_a + nparts_b] per-block sums of |new - old|
+  int parts_a;   // blocks of the pi / a M-step (1; 1,024 above kBwLdsMaxStates: N^2 entries)
 };
 
 hipError_t launch_mle_counts(const MleArgs& g, int64_t nseq, hipStream_t stream);

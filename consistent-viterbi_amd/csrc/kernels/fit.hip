@@ -163,9 +163,12 @@ __global__ __launch_bounds__(256) void bw_backward(BwArgs g) {
 // 256 threads (thread i owns states i, i + 256, ...), the vector operand and (stats) the owned
 // states' gamma sums in dynamic LDS; the xi sum is the GEMM over the rows, as for N <= 256.
 // One workgroup per sequence and all of A per step: a correctness path for large models (the
-// reference trains any N, hmm.rs:69-190), not a tuned one.
+// reference trains any N, hmm.rs:69-190), not a tuned one.  GS: the vectors in global scratch
+// (g.gscratch, 4 N doubles per workgroup: N > kBwLdsMaxStates), the same values.
+template <bool GS>
 __global__ __launch_bounds__(256) void bw_forward_g(BwArgs g) {
-  extern __shared__ double xs[];  // [N]
+  extern __shared__ double xs_lds[];
+  double* xs = GS ? g.gscratch + (size_t)blockIdx.x * 4 * g.nstates : xs_lds;  // [N]
   __shared__ double red[4];
   const int64_t e0 = g.offsets[blockIdx.x];
   const int T = (int)(g.offsets[blockIdx.x + 1] - e0);
@@ -207,8 +210,10 @@ __global__ __launch_bounds__(256) void bw_forward_g(BwArgs g) {
   }
 }
 
+template <bool GS>
 __global__ __launch_bounds__(256) void bw_backward_g(BwArgs g) {
-  extern __shared__ double xs[];  // [N]
+  extern __shared__ double xs_lds[];
+  double* xs = GS ? g.gscratch + (size_t)blockIdx.x * 4 * g.nstates : xs_lds;  // [N]
   __shared__ double red[4];
   const int64_t e0 = g.offsets[blockIdx.x];
   const int T = (int)(g.offsets[blockIdx.x + 1] - e0);
@@ -245,8 +250,10 @@ __global__ __launch_bounds__(256) void bw_backward_g(BwArgs g) {
 
 // gamma and xi of one sequence (as bw_stats_rows): r_t over alpha's row t, u_{t+1} 2^k over
 // beta's row t, zeros at the last step; the gamma sums of the owned states in LDS
+template <bool GS>
 __global__ __launch_bounds__(256) void bw_stats_rows_g(BwArgs g) {
-  extern __shared__ double sm[];  // ps[N] | pi_acc[N] | a_den[N] | b_den[N]
+  extern __shared__ double sm_lds[];
+  double* sm = GS ? g.gscratch + (size_t)blockIdx.x * 4 * g.nstates : sm_lds;  // ps[N] | pi_acc[N] | a_den[N] | b_den[N]
   __shared__ double red[4];
   const int64_t e0 = g.offsets[blockIdx.x];
   const int T = (int)(g.offsets[blockIdx.x + 1] - e0);
@@ -1472,6 +1479,8 @@ __device__ __forceinline__ double block_sum_any(double v, double* red) {
   return (red[0] + red[1]) + (red[2] + red[3]);
 }
 
+// m.parts_a blocks (1 up to kBwLdsMaxStates: the parts add in the same order as ever); block 0
+// also updates pi
 __global__ __launch_bounds__(256) void bw_mstep_pa(MstepArgs m) {
   __shared__ double red[4];
   const int N = m.nstates;
@@ -1480,13 +1489,15 @@ __global__ __launch_bounds__(256) void bw_mstep_pa(MstepArgs m) {
   const double* xs = m.acc + 3 * N + (size_t)m.nobs * N;
   const double zu = xs[(size_t)N * N] / ((double)N * (double)N);
   double d = 0.0;
-  for (int i = threadIdx.x; i < N; i += blockDim.x) {
-    const double np = pi_acc[i] / (double)m.nseq;
-    d += fabs(np - m.pi[i]);
-    m.pi[i] = np;
-  }
-  for (int k = threadIdx.x; k < N * N; k += blockDim.x) {
-    const int i = k / N, j = k - i * N;
+  if (blockIdx.x == 0)
+    for (int i = threadIdx.x; i < N; i += blockDim.x) {
+      const double np = pi_acc[i] / (double)m.nseq;
+      d += fabs(np - m.pi[i]);
+      m.pi[i] = np;
+    }
+  const int64_t nn = (int64_t)N * N;
+  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < nn; k += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = k / N, j = k - i * N;
     // The factored sum S = sum_t alpha_t u_t+1 / c_t can exceed DBL_MAX exactly where A is 0
     // or subnormal (each xi_t entry A alpha u / c is <= 1, hmm.rs:135-141, so alpha u / c <=
     // 1 / A): a == 0 takes no term (the reference's entries are 0 there; 0 * inf would be NaN),
@@ -1499,7 +1510,7 @@ __global__ __launch_bounds__(256) void bw_mstep_pa(MstepArgs m) {
     m.at[(size_t)j * N + i] = na;
   }
   d = block_sum_any(d, red);
-  if (threadIdx.x == 0) m.part[0] = d;
+  if (threadIdx.x == 0) m.part[blockIdx.x] = d;
 }
 
 __global__ __launch_bounds__(256) void bw_mstep_b(MstepArgs m) {
@@ -1515,7 +1526,7 @@ __global__ __launch_bounds__(256) void bw_mstep_b(MstepArgs m) {
     m.et[k] = nb;
   }
   d = block_sum_any(d, red);
-  if (threadIdx.x == 0) m.part[1 + blockIdx.x] = d;
+  if (threadIdx.x == 0) m.part[m.parts_a + blockIdx.x] = d;
 }
 
 hipError_t launch_mle_counts(const MleArgs& g, int64_t nseq, hipStream_t stream) {
@@ -1590,16 +1601,29 @@ static bool gemm32() {  // A/B knob: CV_BW_GEMM32=1 keeps 32 x 32 tiles at every
 hipError_t launch_bw_estep(const BwArgs& g, int64_t nseq, int64_t max_waves, hipStream_t stream, int64_t nrows) {
   if (nseq <= 0) return hipSuccess;
   if (g.nstates > kBwMaxStates) return hipErrorInvalidValue;
-  if (g.nstates > kBwMmStates) {  // 256 < N <= kBwMaxStates: the strided per-sequence kernels
-    const size_t l1 = (size_t)g.nstates * 8, l4 = 4 * l1;
-    for (const void* k : {reinterpret_cast<const void*>(&bw_forward_g), reinterpret_cast<const void*>(&bw_backward_g)})
-      if (l1 > 64 * 1024) (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)l1);
-    if (l4 > 64 * 1024)
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&bw_stats_rows_g), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)l4);
-    hipLaunchKernelGGL(bw_forward_g, dim3((unsigned)nseq), dim3(256), l1, stream, g);
-    hipLaunchKernelGGL(bw_backward_g, dim3((unsigned)nseq), dim3(256), l1, stream, g);
-    hipLaunchKernelGGL(bw_stats_rows_g, dim3((unsigned)nseq), dim3(256), l4, stream, g);
+  if (g.nstates > kBwMmStates) {  // N > 256: the strided per-sequence kernels, then the xi GEMM
+    if (g.gscratch) {  // their vectors in global scratch, kBwScratchSeqs sequences per launch
+      for (int64_t s0 = 0; s0 < nseq; s0 += kBwScratchSeqs) {
+        BwArgs gb = g;
+        gb.offsets = g.offsets + s0;  // rows stay at (element - elem_base)
+        const unsigned n = (unsigned)std::min<int64_t>(kBwScratchSeqs, nseq - s0);
+        hipLaunchKernelGGL(bw_forward_g<true>, dim3(n), dim3(256), 0, stream, gb);
+        hipLaunchKernelGGL(bw_backward_g<true>, dim3(n), dim3(256), 0, stream, gb);
+        hipLaunchKernelGGL(bw_stats_rows_g<true>, dim3(n), dim3(256), 0, stream, gb);
+      }
+    } else {  // in LDS (N <= kBwLdsMaxStates)
+      if (g.nstates > kBwLdsMaxStates) return hipErrorInvalidValue;
+      const size_t l1 = (size_t)g.nstates * 8, l4 = 4 * l1;
+      for (const void* k :
+           {reinterpret_cast<const void*>(&bw_forward_g<false>), reinterpret_cast<const void*>(&bw_backward_g<false>)})
+        if (l1 > 64 * 1024) (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)l1);
+      if (l4 > 64 * 1024)
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&bw_stats_rows_g<false>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)l4);
+      hipLaunchKernelGGL(bw_forward_g<false>, dim3((unsigned)nseq), dim3(256), l1, stream, g);
+      hipLaunchKernelGGL(bw_backward_g<false>, dim3((unsigned)nseq), dim3(256), l1, stream, g);
+      hipLaunchKernelGGL(bw_stats_rows_g<false>, dim3((unsigned)nseq), dim3(256), l4, stream, g);
+    }
     const int nt = (g.nstates + 127) / 128;
     const int64_t parts2 = std::max<int64_t>(1, std::min<int64_t>(512 / (nt * nt), (nrows + 255) / 256));
     const int64_t per2 = ((nrows + parts2 - 1) / parts2 + kGemmKB - 1) / kGemmKB * kGemmKB;
@@ -1681,7 +1705,7 @@ hipError_t launch_bw_estep(const BwArgs& g, int64_t nseq, int64_t max_waves, hip
 }
 
 hipError_t launch_bw_mstep(const MstepArgs& m, int nparts_b, hipStream_t stream) {
-  hipLaunchKernelGGL(bw_mstep_pa, dim3(1), dim3(256), 0, stream, m);
+  hipLaunchKernelGGL(bw_mstep_pa, dim3((unsigned)std::max(m.parts_a, 1)), dim3(256), 0, stream, m);
   hipLaunchKernelGGL(bw_mstep_b, dim3((unsigned)nparts_b), dim3(256), 0, stream, m);
   return hipGetLastError();
 }

@@ -344,9 +344,10 @@ CV_API cv_status cv_solver_write_cfn(cv_solver* s, const char* path, uint64_t* c
 CV_API cv_status cv_hmm_fit_mle(int32_t nstates, int64_t nobs, int64_t nseq, const int64_t* offsets,
                                 const int32_t* obs, const int32_t* tags, int32_t device, double* pi, double* a,
                                 double* b);
-/* train (hmm.rs:69-190): tag-clamped Baum-Welch, E- and M-step on the GPU (N <= 4096: one wave
+/* train (hmm.rs:69-190): tag-clamped Baum-Welch, E- and M-step on the GPU (N <= 65535: one wave
  * per sequence up to 64 states, 32 sequences per workgroup on the f64 matrix cores up to 256,
- * strided per-sequence kernels above; over 64 states the xi sums run as one f64 matrix-core
+ * strided per-sequence kernels above (their vectors in LDS to N = 4096, in global memory
+ * beyond); over 64 states the xi sums run as one f64 matrix-core
  * GEMM over stored rows per chunk) with
  * the parameters resident between iterations; the convergence test (sum |new - old| <= tol,
  * checked after the update, hmm.rs:172-177) adds per-block partial sums on the host.

@@ -197,9 +197,30 @@ def test_gpu_train_converges_like_oracle(gpu):
 def test_gpu_fit_limits(gpu):
     import cviterbi as cv
 
-    off, obs, tags = _corpus(4097, 4, 3, 5, 0.5, seed=1)
-    pi0, a0, b0 = _probs(4097, 4, seed=1)
-    with pytest.raises(cv.CVError):  # Baum-Welch covers N <= 4096 (4 N doubles of LDS per sequence)
-        cv.fit_train(pi0, a0, b0, off, obs, tags, max_iter=1)
+    off, obs, tags = _corpus(300, 4, 3, 5, 0.5, seed=1)
+    pi0, a0, b0 = _probs(300, 4, seed=1)
     with pytest.raises(cv.CVError):  # MLE needs every element tagged
         cv.fit_mle(pi0, a0, b0, off, obs, tags)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,nseq,tmax,forced", [(300, 50, 25, True), (520, 2100, 6, True), (4097, 5, 4, False)])
+def test_gpu_train_global_scratch_match_oracle(gpu, monkeypatch, n, nseq, tmax, forced):
+    """Baum-Welch beyond the LDS-resident vectors (N > 4,096: the strided kernels' step vector and
+    gamma sums in global scratch, kBwScratchSeqs sequences per launch, the pi / a M-step over
+    1,024 blocks) -- at N = 4,097 itself, and at N = 300 / 520 with CV_BW_GLOBAL=1 (2,100
+    sequences: two scratch batches) -- two EM iterations against the oracle (hmm.rs:69-190)."""
+    import cviterbi as cv
+
+    if forced:
+        monkeypatch.setenv("CV_BW_GLOBAL", "1")
+    v = 11
+    off, obs, tags = _corpus(n, v, nseq, tmax, 0.25, seed=700 + n)
+    pi0, a0, b0 = _probs(n, v, seed=700 + n)
+    gp, ga, gb, it = cv.fit_train(pi0, a0, b0, off, obs, tags, max_iter=2, tol=0.0)
+    assert it == 2
+    rp, ra, rb, _ = FO.train(pi0, a0, b0, off, obs, tags, 2, 0.0)
+    for g, r, what in zip((gp, ga, gb), (rp, ra, rb), ("pi", "a", "b")):
+        assert np.array_equal(np.isinf(g), np.isinf(r)), what
+        fin = np.isfinite(r)
+        np.testing.assert_allclose(g[fin], r[fin], rtol=0, atol=1e-9, err_msg=what)
