@@ -28,6 +28,7 @@
 
 #include "../../include/cviterbi.h"
 #include "csp.hpp"
+#include "hostscan.hpp"
 #include "hmm_json.hpp"
 #include "kernels/chain.h"
 #include "kernels/cfn.h"
@@ -1413,8 +1414,8 @@ struct ConSeq {
 
 // Constrained sequences in sequence order (per-worker lists concatenated in order), and the
 // range check of the components in the same pass: returns the first element with a component
-// outside [-1, ncomp), or -1.  A sequence whose components are all -1 (AND of the words = -1)
-// is skipped by one vectorised pass over it.
+// outside [-1, ncomp), or -1.  One vectorised min / max / AND pass per sequence
+// (hostscan.cpp); the positions only for sequences with a component >= 0.
 int64_t build_conseq_checked(int64_t nseq, const int64_t* offsets, const int32_t* component, int32_t ncomp,
                              std::vector<ConSeq>& cs) {
   cs.clear();
@@ -1422,19 +1423,15 @@ int64_t build_conseq_checked(int64_t nseq, const int64_t* offsets, const int32_t
   std::vector<int64_t> bad((size_t)host_threads(), -1);
   parallel_ranges(nseq, [&](int t, int64_t lo, int64_t hi) {
     for (int64_t s = lo; s < hi; ++s) {
-      const int32_t* c = component + offsets[s];
       const int64_t n = offsets[s + 1] - offsets[s];
-      int32_t all = -1;
-      for (int64_t k = 0; k < n; ++k) all &= c[k];
-      if (all == -1) continue;  // every component is -1
-      ConSeq q{s, {}};
-      for (int64_t k = 0; k < n; ++k) {
-        if (c[k] < -1 || c[k] >= ncomp) {
-          bad[(size_t)t] = offsets[s] + k;
-          return;
-        }
-        if (c[k] >= 0) q.elems.push_back(offsets[s] + k);
+      const cvscan::SeqScan r = cvscan::scan_sequence(component + offsets[s], n, ncomp);
+      if (r.bad >= 0) {
+        bad[(size_t)t] = offsets[s] + r.bad;
+        return;
       }
+      if (!r.constrained) continue;  // every component is -1
+      ConSeq q{s, {}};
+      cvscan::constrained_positions(component + offsets[s], n, offsets[s], q.elems);
       part[(size_t)t].push_back(std::move(q));
     }
   }, 1024);
@@ -1445,14 +1442,14 @@ int64_t build_conseq_checked(int64_t nseq, const int64_t* offsets, const int32_t
   return -1;
 }
 
+// The same list for components already range-checked.
 void build_conseq(int64_t nseq, const int64_t* offsets, const int32_t* component, std::vector<ConSeq>& cs) {
   cs.clear();
   std::vector<std::vector<ConSeq>> part((size_t)host_threads());
   parallel_ranges(nseq, [&](int t, int64_t lo, int64_t hi) {
     for (int64_t s = lo; s < hi; ++s) {
       ConSeq c{s, {}};
-      for (int64_t e = offsets[s]; e < offsets[s + 1]; ++e)
-        if (component[e] >= 0) c.elems.push_back(e);
+      cvscan::constrained_positions(component + offsets[s], offsets[s + 1] - offsets[s], offsets[s], c.elems);
       if (!c.elems.empty()) part[t].push_back(std::move(c));
     }
   }, 1024);

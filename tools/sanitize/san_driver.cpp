@@ -2,6 +2,7 @@
 // host units that parse untrusted input or do wide integer arithmetic:
 //   hmm_json.cpp  the hmm.json reader/writer (malformed files, nulls, round trips)
 //   csp.cpp       exact term accumulation (add_exact), pair lists, the component search
+//   hostscan.cpp  the constrained decode's component scan vs a scalar loop (both builds)
 //   exact_fixed.h nearbyint(x * 2^64) limbs for f32 and f64 vs an __int128 reference
 // Built with g++ -fsanitize=address,undefined (tools/sanitize/Makefile); runs in the
 // container, never on the GPU box.  Exit status 0 = every check passed with no sanitizer
@@ -17,6 +18,7 @@
 #include "../../consistent-viterbi_amd/csrc/csp.hpp"
 #include "../../consistent-viterbi_amd/csrc/exact_fixed.h"
 #include "../../consistent-viterbi_amd/csrc/hmm_json.hpp"
+#include "../../consistent-viterbi_amd/csrc/hostscan.hpp"
 
 static int g_fail = 0;
 static int g_csp_feasible = 0;  // CSP trials with a feasible optimum (compared)
@@ -173,6 +175,40 @@ static void check_csp() {
   }
 }
 
+// cvscan::scan_sequence / constrained_positions vs the scalar definition: random lengths
+// (incl. 0 and non-multiples of 16), sparse / dense constrained elements, out-of-range values
+static void check_hostscan() {
+  std::mt19937_64 rng(7);
+  for (int trial = 0; trial < 20000; ++trial) {
+    const int64_t n = (int64_t)(rng() % 300);
+    const int32_t ncomp = 1 + (int32_t)(rng() % 9);
+    std::vector<int32_t> c((size_t)n, -1);
+    const int mode = (int)(rng() % 4);
+    for (int64_t k = 0; k < n; ++k) {
+      const uint64_t x = rng() % 1000;
+      if (mode >= 1 && x < (mode == 1 ? 5u : mode == 2 ? 300u : 1000u)) c[(size_t)k] = (int32_t)(rng() % ncomp);
+    }
+    if (n > 0 && rng() % 8 == 0)  // an out-of-range value somewhere
+      c[(size_t)(rng() % n)] = (rng() % 2) ? ncomp + (int32_t)(rng() % 3) : -2 - (int32_t)(rng() % 3);
+    int64_t bad = -1;
+    bool any = false;
+    std::vector<int64_t> pos;
+    for (int64_t k = 0; k < n; ++k) {
+      if (bad < 0 && (c[(size_t)k] < -1 || c[(size_t)k] >= ncomp)) bad = k;
+      if (c[(size_t)k] >= 0) any = true;
+    }
+    const cvscan::SeqScan r = cvscan::scan_sequence(c.data(), n, ncomp);
+    CHECK(r.bad == bad);
+    if (bad >= 0) continue;
+    CHECK(r.constrained == any);
+    for (int64_t k = 0; k < n; ++k)
+      if (c[(size_t)k] >= 0) pos.push_back(1000 + k);
+    std::vector<int64_t> got;
+    cvscan::constrained_positions(c.data(), n, 1000, got);
+    CHECK(got == pos);
+  }
+}
+
 static void check_json() {
   const std::string good =
       "{\"a\":{\"v\":1,\"dim\":[2,2],\"data\":[-0.1549019599857432,-0.5228787452803376,null,0.0]},"
@@ -213,6 +249,7 @@ static void check_json() {
 }
 
 int main() {
+  check_hostscan();
   check_exact_fixed();
   check_add_exact();
   check_csp();
