@@ -4088,23 +4088,79 @@ CV_API cv_status cv_hmm_fit_train(int32_t nstates, int64_t nobs, int64_t nseq, c
   m.part = d.cnt.as<double>();
   m.parts_a = parts_a;
   std::vector<double> part((size_t)(parts_a + kPartsB));
-  {
-    // longest sequences first within each chunk (indices relative to the chunk)
-    std::vector<int64_t> ord((size_t)nseq);
-    for (const auto& c : chunks) {
-      int64_t* o = ord.data() + c.first;
-      for (int64_t k = 0; k < c.second - c.first; ++k) o[k] = k;
-      std::stable_sort(o, o + (c.second - c.first), [&](int64_t x, int64_t y) {
-        return off0[c.first + x + 1] - off0[c.first + x] > off0[c.first + y + 1] - off0[c.first + y];
-      });
+  // The E-step pipeline (64 < N <= 256): each chunk's sequences in P contiguous parts on their
+  // own streams, part p's forward behind part p - 1's, so one part's backward and xi GEMM run
+  // beside the next part's forward (the kernels' per-step phases without matrix products
+  // leave the matrix cores to the other kernel's workgroups on the CU).  CV_BW_PIPE=P (1..4;
+  // 1: one launch of each kernel per chunk).  Same sums up to the atomics' order.
+  const int pipe = [&] {
+    if (!cvf::bw_estep_mm(N)) return 1;
+    const char* e = getenv("CV_BW_PIPE");
+    const int v = e ? atoi(e) : 1;
+    return std::max(1, std::min(v, 4));
+  }();
+  // parts: contiguous sequence ranges of a chunk with about equal element counts
+  std::vector<std::vector<std::pair<int64_t, int64_t>>> parts(chunks.size());
+  for (size_t ci = 0; ci < chunks.size(); ++ci) {
+    const int64_t s0 = chunks[ci].first, s1 = chunks[ci].second, E = off0[s1] - off0[s0];
+    int64_t a = s0;
+    for (int p = 1; p <= pipe && a < s1; ++p) {
+      int64_t b = a + 1;
+      while (b < s1 && (p == pipe || off0[b] - off0[s0] < E * p / pipe)) ++b;
+      parts[ci].emplace_back(a, b);
+      a = b;
     }
+  }
+  {
+    // longest sequences first within each part (indices relative to the part)
+    std::vector<int64_t> ord((size_t)nseq);
+    for (const auto& pc : parts)
+      for (const auto& c : pc) {
+        int64_t* o = ord.data() + c.first;
+        for (int64_t k = 0; k < c.second - c.first; ++k) o[k] = k;
+        std::stable_sort(o, o + (c.second - c.first), [&](int64_t x, int64_t y) {
+          return off0[c.first + x + 1] - off0[c.first + x] > off0[c.first + y + 1] - off0[c.first + y];
+        });
+      }
     if ((st = upload(d.ord, ord.data(), ord.size() * 8)) != CV_OK) return st;
+  }
+  struct PipeStreams {
+    hipStream_t s[4] = {};
+    hipEvent_t ev[5] = {};  // [0..3] forward done per part, [4] the accumulators zeroed
+    ~PipeStreams() {
+      for (auto x : s)
+        if (x) (void)hipStreamDestroy(x);
+      for (auto x : ev)
+        if (x) (void)hipEventDestroy(x);
+    }
+  } ps;
+  if (pipe > 1) {
+    for (int p = 0; p < pipe; ++p)
+      if (hipStreamCreateWithFlags(&ps.s[p], hipStreamNonBlocking) != hipSuccess)
+        return set_err(CV_EDEVICE, "hipStreamCreate failed");
+    for (auto& x : ps.ev)
+      if (hipEventCreateWithFlags(&x, hipEventDisableTiming) != hipSuccess) return set_err(CV_EDEVICE, "hipEventCreate failed");
   }
   int32_t it = 0;
   for (it = 1; it <= max_iter; ++it) {
     HIP_TRY(hipMemsetAsync(d.acc.p, 0, nacc * 8, nullptr));
     double* A = d.acc.as<double>();
-    for (const auto& c : chunks) {
+    for (size_t ci = 0; ci < chunks.size(); ++ci)
+      for (size_t pi_ = 0; pi_ < parts[ci].size(); ++pi_) {
+      const auto& c = parts[ci][pi_];
+      // the part's rows from its first element on (a part of a chunk: rows after the chunk's
+      // earlier parts, so the parts' rows never overlap)
+      const int64_t row0 = off0[c.first] - off0[chunks[ci].first];
+      hipStream_t ss = nullptr;
+      if (pipe > 1) {
+        ss = ps.s[pi_];
+        if (pi_ == 0) {  // behind the zeroed accumulators and the previous chunk (null stream)
+          HIP_TRY(hipEventRecord(ps.ev[4], nullptr));
+          for (int p = 0; p < pipe; ++p) HIP_TRY(hipStreamWaitEvent(ps.s[p], ps.ev[4], 0));
+        } else {
+          HIP_TRY(hipStreamWaitEvent(ss, ps.ev[pi_ - 1], 0));
+        }
+      }
       cvf::BwArgs g{};
       g.offsets = d.off.as<int64_t>() + c.first;
       g.obs = d.obs.as<int32_t>();
@@ -4118,18 +4174,23 @@ CV_API cv_status cv_hmm_fit_train(int32_t nstates, int64_t nobs, int64_t nseq, c
       g.a = d.a.as<double>();
       g.at = d.at.as<double>();
       g.et = d.et.as<double>();
-      g.alpha = d.alpha.as<double>();
-      g.beta = d.beta.as<double>();
-      g.rscale = d.rscale.p ? d.rscale.as<double>() : nullptr;  // null: R stored over alpha
+      g.alpha = d.alpha.as<double>() + (size_t)row0 * N;
+      g.beta = d.beta.p ? d.beta.as<double>() + (size_t)row0 * N : nullptr;
+      g.rscale = d.rscale.p ? d.rscale.as<double>() + row0 : nullptr;  // null: R stored over alpha
       g.pi_acc = A;
       g.a_den = A + N;
       g.b_den = A + 2 * N;
       g.b_num = A + 3 * N;
       g.xi_s = g.b_num + (size_t)V * N;
       g.xi_zero = g.xi_s + (size_t)N * N;
-      const hipError_t e =
-          cvf::launch_bw_estep(g, c.second - c.first, max_waves, nullptr, off0[c.second] - off0[c.first]);
+      const hipError_t e = cvf::launch_bw_estep(g, c.second - c.first, max_waves, ss, off0[c.second] - off0[c.first],
+                                                pipe > 1 ? ps.ev[pi_] : nullptr);
       if (e != hipSuccess) return set_err(CV_EDEVICE, "Baum-Welch launch failed: %s", hipGetErrorString(e));
+      if (pipe > 1 && pi_ + 1 == parts[ci].size())  // the chunk's parts joined on the null stream
+        for (size_t p = 0; p < parts[ci].size(); ++p) {
+          HIP_TRY(hipEventRecord(ps.ev[p], ps.s[p]));
+          HIP_TRY(hipStreamWaitEvent(nullptr, ps.ev[p], 0));
+        }
     }
     // M-step (hmm.rs:145-170) on the device: new_pi = sum gamma_0 / R; new_a = sum xi / a_den
     // (row); new_b = sum gamma at o / b_den; sum_t xi_t = A o S + z / N^2 (see bw_stats);

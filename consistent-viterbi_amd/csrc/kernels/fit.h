@@ -76,7 +76,12 @@ hipError_t launch_mle_counts(const MleArgs& g, int64_t nseq, hipStream_t stream)
 // forward, backward and the E-step sums of sequences [0, nseq) of g.offsets; the N <= 64
 // backward kernel runs at most max_waves waves (each walks several sequences)
 // nrows: the chunk's elements (alpha / beta rows from elem_base), for the GEMM path (N > 128)
-hipError_t launch_bw_estep(const BwArgs& g, int64_t nseq, int64_t max_waves, hipStream_t stream, int64_t nrows);
+// fwd_done (64 < N <= 256, the matrix-core kernels): recorded on `stream` right after the
+// forward launch (the E-step pipeline of cv_hmm_fit_train staggers its parts on it)
+hipError_t launch_bw_estep(const BwArgs& g, int64_t nseq, int64_t max_waves, hipStream_t stream, int64_t nrows,
+                           hipEvent_t fwd_done = nullptr);
+// the E-step sequences per pipeline part have the matrix-core kernels (64 < N <= 256)
+bool bw_estep_mm(int nstates);
 hipError_t launch_bw_mstep(const MstepArgs& m, int nparts_b, hipStream_t stream);
 
 }  // namespace cvf

@@ -1554,9 +1554,10 @@ static int bw_mt() {
 }
 
 template <int NP, int MT, int WVF, int WVB>
-static void launch_mm(const BwArgs& g, int64_t nseq, hipStream_t stream) {
+static void launch_mm(const BwArgs& g, int64_t nseq, hipStream_t stream, hipEvent_t fwd_done) {
   const dim3 grid((unsigned)((nseq + 16 * MT - 1) / (16 * MT)));
   hipLaunchKernelGGL((bw_fwd_mm<NP, MT, WVF>), grid, dim3(64 * WVF), 0, stream, g, nseq);
+  if (fwd_done) (void)hipEventRecord(fwd_done, stream);
   hipLaunchKernelGGL((bw_bwd_mm<NP, MT, WVB>), grid, dim3(64 * WVB), 0, stream, g, nseq);
 }
 
@@ -1598,7 +1599,18 @@ static bool gemm32() {  // A/B knob: CV_BW_GEMM32=1 keeps 32 x 32 tiles at every
   return v;
 }
 
-hipError_t launch_bw_estep(const BwArgs& g, int64_t nseq, int64_t max_waves, hipStream_t stream, int64_t nrows) {
+static bool bw_per_seq() {  // A/B knob: CV_BW_PERSEQ=1 keeps one workgroup per sequence
+  static const bool v = [] {
+    const char* e = getenv("CV_BW_PERSEQ");
+    return e && e[0] == '1';
+  }();
+  return v;
+}
+
+bool bw_estep_mm(int nstates) { return nstates > kBwWaveStates && nstates <= kBwMmStates && !bw_per_seq(); }
+
+hipError_t launch_bw_estep(const BwArgs& g, int64_t nseq, int64_t max_waves, hipStream_t stream, int64_t nrows,
+                           hipEvent_t fwd_done) {
   if (nseq <= 0) return hipSuccess;
   if (g.nstates > kBwMaxStates) return hipErrorInvalidValue;
   if (g.nstates > kBwMmStates) {  // N > 256: the strided per-sequence kernels, then the xi GEMM
@@ -1632,11 +1644,7 @@ hipError_t launch_bw_estep(const BwArgs& g, int64_t nseq, int64_t max_waves, hip
                        per2);
     return hipGetLastError();
   }
-  static const bool per_seq = [] {  // A/B knob: CV_BW_PERSEQ=1 keeps one workgroup per sequence
-    const char* e = getenv("CV_BW_PERSEQ");
-    return e && e[0] == '1';
-  }();
-  const bool mm = g.nstates > kBwWaveStates && !per_seq;
+  const bool mm = bw_estep_mm(g.nstates);
   if (g.nstates > kBwLdsStates || mm) {  // the xi sum as R^T U on the matrix cores
     BwArgs gg = g;
     if (!mm) gg.rscale = nullptr;  // the per-sequence kernels store R over alpha
@@ -1644,17 +1652,17 @@ hipError_t launch_bw_estep(const BwArgs& g, int64_t nseq, int64_t max_waves, hip
       // waves per workgroup: forward / backward (the backward's per-step state needs the
       // registers of four waves at 256 states)
       if (bw_mt() == 4) {
-        if (g.nstates <= 128) launch_mm<128, 4, 4, 4>(g, nseq, stream);
-        else if (g.nstates <= 192) launch_mm<192, 4, 4, 4>(g, nseq, stream);
-        else launch_mm<256, 4, 4, 4>(g, nseq, stream);
+        if (g.nstates <= 128) launch_mm<128, 4, 4, 4>(g, nseq, stream, fwd_done);
+        else if (g.nstates <= 192) launch_mm<192, 4, 4, 4>(g, nseq, stream, fwd_done);
+        else launch_mm<256, 4, 4, 4>(g, nseq, stream, fwd_done);
       } else if (bw_wv() == 4) {
-        if (g.nstates <= 128) launch_mm<128, 2, 4, 4>(g, nseq, stream);
-        else if (g.nstates <= 192) launch_mm<192, 2, 4, 4>(g, nseq, stream);
-        else launch_mm<256, 2, 4, 4>(g, nseq, stream);
+        if (g.nstates <= 128) launch_mm<128, 2, 4, 4>(g, nseq, stream, fwd_done);
+        else if (g.nstates <= 192) launch_mm<192, 2, 4, 4>(g, nseq, stream, fwd_done);
+        else launch_mm<256, 2, 4, 4>(g, nseq, stream, fwd_done);
       } else {
-        if (g.nstates <= 128) launch_mm<128, 2, 8, 4>(g, nseq, stream);
-        else if (g.nstates <= 192) launch_mm<192, 2, 4, 4>(g, nseq, stream);  // 12 tiles: four waves
-        else launch_mm<256, 2, 8, 4>(g, nseq, stream);
+        if (g.nstates <= 128) launch_mm<128, 2, 8, 4>(g, nseq, stream, fwd_done);
+        else if (g.nstates <= 192) launch_mm<192, 2, 4, 4>(g, nseq, stream, fwd_done);  // 12 tiles: four waves
+        else launch_mm<256, 2, 8, 4>(g, nseq, stream, fwd_done);
       }
     } else {
       hipLaunchKernelGGL(bw_forward, dim3((unsigned)nseq), dim3(256), 0, stream, g);

@@ -224,3 +224,28 @@ def test_gpu_train_global_scratch_match_oracle(gpu, monkeypatch, n, nseq, tmax, 
         assert np.array_equal(np.isinf(g), np.isinf(r)), what
         fin = np.isfinite(r)
         np.testing.assert_allclose(g[fin], r[fin], rtol=0, atol=1e-9, err_msg=what)
+
+
+@pytest.mark.gpu
+# the E-step pipeline (CV_BW_PIPE = P parts per chunk on their own streams, 64 < N <= 256):
+# contiguous parts with their own longest-first order and rows; against the oracle and against
+# one part (the same sums up to the atomics' order)
+@pytest.mark.parametrize("n,pipe", [(100, 2), (200, 3), (256, 4), (256, 3)])
+def test_gpu_train_pipeline_parts_match_oracle(gpu, monkeypatch, n, pipe):
+    import cviterbi as cv
+
+    v = 29
+    off, obs, tags = _corpus(n, v, 230, 45, 0.2, seed=900 + n)
+    pi0, a0, b0 = _probs(n, v, seed=900 + n)
+    iters = 2
+    monkeypatch.setenv("CV_BW_PIPE", str(pipe))
+    gp, ga, gb, it = cv.fit_train(pi0, a0, b0, off, obs, tags, max_iter=iters, tol=0.0)
+    assert it == iters
+    monkeypatch.setenv("CV_BW_PIPE", "1")
+    one = cv.fit_train(pi0, a0, b0, off, obs, tags, max_iter=iters, tol=0.0)
+    rp, ra, rb, _ = FO.train(pi0, a0, b0, off, obs, tags, iters, 0.0)
+    for g, o, r, what in zip((gp, ga, gb), one[:3], (rp, ra, rb), ("pi", "a", "b")):
+        assert np.array_equal(np.isinf(g), np.isinf(r)), what
+        fin = np.isfinite(r)
+        np.testing.assert_allclose(g[fin], r[fin], rtol=0, atol=1e-9, err_msg=what)
+        np.testing.assert_allclose(g[fin], o[fin], rtol=0, atol=1e-12, err_msg=what)

@@ -14,4 +14,6 @@ step() {
 }
 step pytest 900 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu tests &&
 step smoke 200 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" &&
-step bench 400 python -u bench.py
+step bench 400 python -u bench.py &&
+step c5_configs 300 python -u tools/bench_configs.py c5 &&
+step c5_trace 300 env CV_TRACE=1 REPS=3 python -u tools/bench_configs.py c5
