@@ -252,6 +252,10 @@ struct cv_hmm {
   struct ChainBufs {
     DevBuf off, obs, path, res, cert, ebin, q;
   } chainb;
+  // the parallel chain's path copy: on its own stream, behind the last backtrack (paths_ev),
+  // beside the certificate pass
+  hipStream_t copy_stream = nullptr;
+  hipEvent_t paths_ev = nullptr;
 
   ~cv_hmm() {
     for (auto e : ev) (void)hipEventDestroy(e);
@@ -266,6 +270,8 @@ struct cv_hmm {
     if (side.ws_done) (void)hipEventDestroy(side.ws_done);
     if (stream) (void)hipStreamDestroy(stream);
     if (bt_stream) (void)hipStreamDestroy(bt_stream);
+    if (copy_stream) (void)hipStreamDestroy(copy_stream);
+    if (paths_ev) (void)hipEventDestroy(paths_ev);
   }
 };
 
@@ -632,9 +638,11 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
                         const int32_t* obs_dev, const cv_opts& o, int32_t* path_dev, double* score_dev,
                         uint8_t* status_dev, hipStream_t stream, const void* resume_rows = nullptr,
                         bool side_ws = false, double* cp_cert = nullptr, const double* cp_init = nullptr,
-                        double* cp_last = nullptr) {
+                        double* cp_last = nullptr, bool* paths_ev_rec = nullptr) {
   // cp_cert (the parallel CPSolver chain, row-A0 f64 trellis only): after each chunk's
-  // backtrack, cp_cert_f64 reads the chunk's rows and paths -> [nseq][2] certificates
+  // backtrack, cp_cert_f64 reads the chunk's rows and paths -> [nseq][2] certificates;
+  // paths_ev_rec: h->paths_ev is recorded after the last chunk's backtrack (every path written),
+  // before its certificate pass, and *paths_ev_rec set
   // side_ws: the handle's second workspace (h->side), no timing / last-call bookkeeping -- a
   // decode running beside another decode_device call of the same handle on another stream
   DevBuf& w_main = side_ws ? h->side.main : h->ws_main;
@@ -1097,6 +1105,11 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
       err = fused_chunk ? hipSuccess
                         : cvk::launch_t64_bt(h->np64, t64_bt_args(c, wsb), n, bts,
                                              (serial || ci + 1 == chunks.size()) ? 0 : std::max(h->cus, 1));
+      if (err == hipSuccess && cp_cert && paths_ev_rec && ci + 1 == chunks.size()) {
+        if (!h->paths_ev) HIP_TRY(hipEventCreateWithFlags(&h->paths_ev, hipEventDisableTiming));
+        HIP_TRY(hipEventRecord(h->paths_ev, bts));
+        *paths_ev_rec = true;
+      }
       if (err == hipSuccess && cp_cert) {
         cvk::CpCert64Args ca{};
         ca.delta = reinterpret_cast<const double*>(wsb);
@@ -1139,6 +1152,11 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
         ba.nobs = (int)h->V;
       }
       err = gen_rows ? cvk::launch_generic_bt_rows<double>(ba, n, bts) : cvk::launch_generic_bt<double>(ba, n, bts);
+      if (err == hipSuccess && cp_cert && paths_ev_rec && ci + 1 == chunks.size()) {
+        if (!h->paths_ev) HIP_TRY(hipEventCreateWithFlags(&h->paths_ev, hipEventDisableTiming));
+        HIP_TRY(hipEventRecord(h->paths_ev, bts));
+        *paths_ev_rec = true;
+      }
       if (err == hipSuccess && cp_cert) {  // the parallel chain (N > 256): certificates over the plain rows
         cvk::CpCert64Args ca{};
         ca.delta = reinterpret_cast<const double*>(wsb);
@@ -3061,21 +3079,37 @@ cv_status superseq_cp_par(cv_hmm* h, int64_t nseq, const int64_t* offsets, const
   o.kernel = small ? CV_KERNEL_TRELLIS_F64 : CV_KERNEL_AUTO;  // N > 256: the batch path's own pick
   o.rescore_f64 = 0;
   o.stream = stream;
+  // the paths' copy to the host (4 B per element) runs on its own stream beside the
+  // certificate pass, which reads every row (A/B knob: CV_CHAIN_COPY_OVERLAP=0)
+  const char* cov = getenv("CV_CHAIN_COPY_OVERLAP");
+  bool paths_rec = false;
+  const bool overlap_copy = !(cov && *cov == '0') && !trace_on();
+  if (overlap_copy && !h->copy_stream) HIP_TRY(hipStreamCreateWithFlags(&h->copy_stream, hipStreamNonBlocking));
   st = decode_device(h, nseq, off.data(), d_off.as<int64_t>(), d_obs.as<int32_t>(), o, d_path.as<int32_t>(), d_score,
-                     d_status, stream, nullptr, false, d_cert.as<double>());
+                     d_status, stream, nullptr, false, d_cert.as<double>(), nullptr, nullptr,
+                     overlap_copy ? &paths_rec : nullptr);
   if (st == CV_EUNSUPPORTED && !small) return CV_OK;  // no rows to certify (CV_GENERIC_ROWS=0): serial chain
-  if (st != CV_OK) return st;
+  if (st != CV_OK) {
+    if (paths_rec) (void)hipStreamSynchronize(h->copy_stream);
+    return st;
+  }
   std::vector<double> score((size_t)nseq), cert((size_t)nseq * 2);
   std::vector<uint8_t> status((size_t)nseq);
   if (trace_on()) {
     HIP_TRY(hipStreamSynchronize(stream));
     trace_mark("chain: row-A0 decode + certificates (device)");
   }
-  HIP_TRY(hipMemcpyAsync(path_out, d_path.p, (size_t)L * 4, hipMemcpyDeviceToHost, stream));
+  if (paths_rec) {
+    HIP_TRY(hipStreamWaitEvent(h->copy_stream, h->paths_ev, 0));
+    HIP_TRY(hipMemcpyAsync(path_out, d_path.p, (size_t)L * 4, hipMemcpyDeviceToHost, h->copy_stream));
+  } else {
+    HIP_TRY(hipMemcpyAsync(path_out, d_path.p, (size_t)L * 4, hipMemcpyDeviceToHost, stream));
+  }
   HIP_TRY(hipMemcpyAsync(score.data(), d_score, (size_t)nseq * 8, hipMemcpyDeviceToHost, stream));
   HIP_TRY(hipMemcpyAsync(status.data(), d_status, (size_t)nseq, hipMemcpyDeviceToHost, stream));
   HIP_TRY(hipMemcpyAsync(cert.data(), d_cert.p, (size_t)nseq * 16, hipMemcpyDeviceToHost, stream));
   HIP_TRY(hipStreamSynchronize(stream));
+  if (paths_rec) HIP_TRY(hipStreamSynchronize(h->copy_stream));
   trace_mark("chain: paths, scores, certificates D2H");
   for (int64_t k = 0; k < nseq; ++k)
     if (status[(size_t)k] != CV_SEQ_OK && status[(size_t)k] != CV_SEQ_EMPTY) return CV_OK;  // serial chain

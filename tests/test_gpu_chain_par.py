@@ -295,3 +295,26 @@ def test_chain_par_wide_speculation(gpu, monkeypatch, n):
     assert st["parallel"] and st["speculated"] >= 1, st
     rp, robj = O.cp_superseq_f64(pi, a, b, off, obs)
     assert obj == robj and np.array_equal(path, rp), st
+
+
+@pytest.mark.parametrize("n,nseq", [(256, 2048), (300, 120)])
+def test_chain_par_copy_overlap_knob(gpu, monkeypatch, n, nseq):
+    """The paths' host copy runs on its own stream behind the last backtrack, beside the
+    certificate pass (default); CV_CHAIN_COPY_OVERLAP=0 copies after the certificates on the
+    decode's stream.  Both return the same paths and objective (f64 trellis at N = 256, the
+    generic rows mode's plain-row certificates at N = 300)."""
+    if n == 256:
+        c = synth.config("c4", nseq)
+        pi, a, b, off, obs = c["pi"], c["a"], c["b"], c["offsets"], c["obs"]
+    else:
+        pi, a, b, off, obs = _case(n, 17, nseq, 1, 60, seed=4700)
+    h = cv.HMM(pi, a, b)
+    (path, obj), st = _par(h, off, obs)
+    assert st["parallel"], st
+    monkeypatch.setenv("CV_CHAIN_COPY_OVERLAP", "0")
+    (p0, o0), st0 = _par(h, off, obs)
+    assert st0["parallel"], st0
+    assert obj == o0 and np.array_equal(path, p0)
+    if n == 300:
+        rp, robj = O.cp_superseq_f64(pi, a, b, off, obs)
+        assert obj == robj and np.array_equal(path, rp)
