@@ -1580,6 +1580,132 @@ __global__ __launch_bounds__(1024) void generic_fwd_ms(GenericFwdArgs<REAL> args
   }
 }
 
+// generic_fwd_split<REAL, K>: generic_fwd_ms<REAL, 1, false> (one sequence per workgroup,
+// u16 psi) with K threads per state.  A few sequences (the parallel chain's speculative
+// re-decodes: ~600 at config-4 size) leave most of the chip idle, and each step is one thread's
+// latency-bound walk over all N candidates; here thread (q, j) walks candidates
+// [q C, (q + 1) C) of state j (C = ceil(N / K)) and thread (0, j) merges the K partial
+// maxima in range order, taking a later range's only when strictly greater -- the first index
+// of the maximum, as the sequential walk finds it -- so the values, arguments and statuses are
+// generic_fwd_ms's bit for bit.  64 ceil(N / 64) K <= 1,024 threads.
+template <typename REAL, int K>
+__global__ __launch_bounds__(1024) void generic_fwd_split(GenericFwdArgs<REAL> args, int64_t nslots) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  const int N = args.nstates;
+  const int NT = (int)blockDim.x / K;  // threads per range: 64 ceil(N / 64)
+  REAL* dbuf = reinterpret_cast<REAL*>(smem_raw);  // [2][N]
+  REAL* pbest = dbuf + 2 * (size_t)N;               // [K - 1][NT] partial maxima of ranges 1..K-1
+  int* parg = reinterpret_cast<int*>(pbest + (size_t)(K - 1) * NT);  // [K - 1][NT] their arguments
+  const int V = args.nobs;
+  const int assoc = args.assoc;
+  const REAL ninf = -__builtin_inf();
+  const int64_t k = blockIdx.x;
+  if (k >= nslots) return;
+  const int64_t slot = args.seq_begin + k;
+  const int64_t seq = args.order ? (int64_t)args.order[slot] : slot;
+  const int64_t e0 = args.offsets[seq];
+  const int T = (int)(args.offsets[seq + 1] - e0);
+  if (T <= 0) return;  // workgroup-uniform
+  const int q = (int)threadIdx.x / NT, j = (int)threadIdx.x - q * NT;
+  const int C = (N + K - 1) / K, i0 = q * C, i1 = min(N, i0 + C);
+  int bad = 0;
+  {
+    const int o = args.obs[e0];
+    const bool ok = (unsigned)o < (unsigned)V;
+    bad = ok ? 0 : 1;
+    const int fs = args.forced ? args.forced[e0] : -1;
+    if (q == 0 && j < N) {
+      const REAL e = ok ? args.et[(size_t)o * N + j] : ninf;
+      REAL d;
+      if (assoc == CVK_ASSOC_DECODE)
+        d = (REAL)0;
+      else if (assoc == CVK_ASSOC_DP)
+        d = (e > ninf) ? (REAL)(args.pi[j] + e) : ninf;
+      else
+        d = args.cp_init ? args.cp_init[seq] + (args.pi[j] + e) : args.pi[j] + e;
+      if (fs >= 0 && j != fs) d = ninf;
+      dbuf[j] = d;
+    }
+  }
+  __syncthreads();
+  for (int t = 1; t < T; ++t) {
+    const int o = args.obs[e0 + t];
+    const bool ok = (unsigned)o < (unsigned)V;
+    if (!ok) bad = 1;
+    const int fs = args.forced ? args.forced[e0 + t] : -1;
+    const REAL* prow = dbuf + (size_t)((t - 1) & 1) * N;
+    REAL* crow = dbuf + (size_t)(t & 1) * N;
+    REAL e = ninf, best = ninf;
+    int arg = 0;
+    const REAL* col = args.a + (j < N ? j : 0);
+    if (j < N) {
+      e = ok ? args.et[(size_t)o * N + j] : ninf;
+      if (assoc == CVK_ASSOC_DP) {
+        const bool live = e > ninf;  // a -inf emission leaves the column at -inf (dp.rs:147-177)
+        #pragma unroll 8
+        for (int i = i0; i < i1; ++i) {
+          const REAL c = (col[(size_t)i * N] + e) + prow[i];
+          if (live && c > best) {
+            best = c;
+            arg = i;
+          }
+        }
+      } else {
+        int ib = i0;
+        if (q == 0) {  // i = 0 seeds the maximum (generic_fwd's `!any` case)
+          best = prow[0] + col[0];
+          ib = 1;
+        }
+        #pragma unroll 8
+        for (int i = ib; i < i1; ++i) {
+          const REAL x = prow[i] + col[(size_t)i * N];
+          if (x > best) {
+            best = x;
+            arg = i;
+          }
+        }
+      }
+      if (q > 0) {
+        pbest[(size_t)(q - 1) * NT + j] = best;
+        parg[(size_t)(q - 1) * NT + j] = arg;
+      }
+    }
+    __syncthreads();
+    if (q == 0 && j < N) {
+#pragma unroll
+      for (int r = 0; r < K - 1; ++r) {
+        const REAL pb = pbest[(size_t)r * NT + j];
+        if (pb > best) {
+          best = pb;
+          arg = parg[(size_t)r * NT + j];
+        }
+      }
+      REAL v;
+      int ag = arg;
+      if (assoc == CVK_ASSOC_DP)
+        v = (e > ninf) ? best : ninf;
+      else if (assoc == CVK_ASSOC_CP)
+        v = prow[ag] + (col[(size_t)ag * N] + e);
+      else
+        v = best + e;
+      if (assoc == CVK_ASSOC_DECODE && !(e > ninf)) {
+        v = ninf;
+        ag = 0;
+      }
+      if (fs >= 0 && j != fs) v = ninf;
+      crow[j] = v;
+      args.psi[(e0 + t - args.psi_elem_base) * (int64_t)N + j] = (uint16_t)ag;
+    }
+    __syncthreads();
+  }
+  if (q == 0 && j < N) {
+    const REAL* last = dbuf + (size_t)((T - 1) & 1) * N;
+    args.last_row[(slot - args.seq_begin) * (int64_t)N + j] = last[j];
+    if (args.cp_last) args.cp_last[seq * N + j] = last[j];
+  }
+  if (bad && threadIdx.x == 0) args.status[seq] = CVK_SEQ_BADOBS;
+}
+
 template <typename REAL>
 __global__ __launch_bounds__(256) void generic_backtrack(GenericBtArgs<REAL> args) {
   const int lane = threadIdx.x & 63;
@@ -2126,7 +2252,29 @@ hipError_t launch_generic_fwd(const GenericFwdArgs<REAL>& fa, int64_t nseq, hipS
   }
   // one sequence per workgroup: one thread per state up to N = 1,024 (64 ceil(N / 64) threads;
   // generic_fwd's 256 threads walk 4 states each at N = 1,024 -- a handful of sequences, e.g.
-  // the parallel chain's speculative re-decodes, then ran latency-bound on a few CUs)
+  // the parallel chain's speculative re-decodes, then ran latency-bound on a few CUs); below
+  // N = 512 and under 2,048 sequences K = 1,024 / 64 ceil(N / 64) threads per state split each
+  // state's candidates (generic_fwd_split; CV_GENERIC_SPLIT=0: never, =1: at any batch size --
+  // read per launch, A/B knob and tests, bit-identical)
+  {
+    const int nt = (fa.nstates + 63) / 64 * 64;
+    const char* se = getenv("CV_GENERIC_SPLIT");
+    const bool split = se && *se ? *se != '0' : nseq < 2048;
+    const int K = std::min(8, 1024 / nt);
+    if (split && K >= 2 && fa.nstates <= 512) {
+      const size_t lds = sizeof(REAL) * 2 * (size_t)fa.nstates + (sizeof(REAL) + 4) * (size_t)(K - 1) * nt;
+      auto go = [&](auto kern) {
+        if (lds > 64 * 1024)
+          (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)lds);
+        hipLaunchKernelGGL(kern, dim3((unsigned)nseq), dim3((unsigned)(nt * K)), lds, stream, fa, nseq);
+        return hipGetLastError();
+      };
+      if (K >= 8) return go(generic_fwd_split<REAL, 8>);
+      if (K >= 4) return go(generic_fwd_split<REAL, 4>);
+      return go(generic_fwd_split<REAL, 2>);
+    }
+  }
   if (fa.nstates <= 1024) return launch_generic_ms<REAL, 1, false>(fa, nseq, stream);
   const size_t lds = sizeof(REAL) * 2 * (size_t)fa.nstates;
   if (lds > 64 * 1024)  // N > 4096 (f64) / 8192 (f32): the two rows in up to 160 KiB of LDS

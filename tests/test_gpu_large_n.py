@@ -469,3 +469,63 @@ def test_t64_1024_equal_batch_chunks_vs_generic(gpu, monkeypatch):
     ref = cv.decode_batch(h, off, obs, dtype="f64", kernel="generic", rescore_f64=False)
     for x, y, what in zip(got, ref, ("path", "score", "status")):
         assert np.array_equal(x, y), what
+
+
+@pytest.mark.parametrize("split", ["1", "0"])
+@pytest.mark.parametrize("assoc", ["viterbi", "cp", "dp", "decode"])
+@pytest.mark.parametrize("dtype,n", [("f64", 5), ("f64", 64), ("f64", 100), ("f32", 200), ("f64", 256), ("f64", 300),
+                                     ("f64", 512)])
+def test_generic_split_candidates(gpu, monkeypatch, split, assoc, dtype, n):
+    """generic_fwd_split (one sequence per workgroup, K = 2..8 threads per state walking
+    ranges of the candidates, merged in range order; the small-batch psi-mode default below
+    N = 512, CV_GENERIC_SPLIT) and the one-thread-per-state kernel against the oracle in every
+    association: ragged and empty sequences, forced states, -inf transitions and emissions, an
+    observation no state emits."""
+    monkeypatch.setenv("CV_GENERIC_SPLIT", split)
+    monkeypatch.setenv("CV_GENERIC_S", "1")
+    monkeypatch.setenv("CV_GENERIC_ROWS", "0")
+    pi, a, b = synth.random_hmm(n, 11, seed=n + 31, zero_frac=0.1)
+    b = b.copy()
+    b[:, 10] = -np.inf
+    rng = np.random.default_rng(n + 77)
+    lens = rng.integers(1, 30, size=19)
+    lens[[3, 11]] = 0
+    lens[5] = 1
+    off = synth.offsets_from_lengths(lens)
+    obs = rng.integers(0, 11, size=int(off[-1])).astype(np.int32)
+    forced = np.where(rng.random(len(obs)) < 0.05, rng.integers(0, n, size=len(obs)), -1).astype(np.int32)
+    dt = np.float32 if dtype == "f32" else np.float64
+    ASSOC = {"viterbi": O.VITERBI, "cp": O.CP, "dp": O.DP, "decode": O.DECODE}
+    h = cv.HMM(pi, a, b)
+    fr = forced if assoc == "viterbi" else None
+    got = cv.decode_batch(h, off, obs, dtype=dtype, assoc=assoc, kernel="generic", rescore_f64=False, forced=fr)
+    ref = O.decode_batch(pi, a, b, off, obs, ASSOC[assoc], dt, forced=fr)
+    assert np.array_equal(got[2], ref[2])
+    ok = got[2] == 0
+    assert np.array_equal(got[1][ok], ref[1][ok])
+    assert np.array_equal(got[0], ref[0])
+
+
+@pytest.mark.parametrize("split", ["1", "0"])
+@pytest.mark.parametrize("name", ["golden_ties.npz", "golden_inf.npz", "golden_small.npz"])
+def test_generic_split_golden(gpu, monkeypatch, split, name):
+    """The golden fixtures (exact ties everywhere: the range merge must keep the first index)
+    through the one-sequence psi-mode kernels with and without the candidate split."""
+    from conftest import load_golden
+    monkeypatch.setenv("CV_GENERIC_SPLIT", split)
+    monkeypatch.setenv("CV_GENERIC_S", "1")
+    monkeypatch.setenv("CV_GENERIC_ROWS", "0")
+    g = load_golden(name)
+    h = cv.HMM(g["pi"], g["a"], g["b"])
+    seen = 0
+    for dt in ("f32", "f64"):
+        for assoc in ("viterbi", "cp", "dp", "decode"):
+            k = f"{dt}_{assoc}"
+            if k + "_path" not in g:
+                continue
+            got = cv.decode_batch(h, g["offsets"], g["obs"], dtype=dt, assoc=assoc, kernel="generic",
+                                  rescore_f64=False)
+            for x, y, what in zip(got, (g[k + "_path"], g[k + "_score"], g[k + "_status"]), ("path", "score", "status")):
+                assert np.array_equal(x, y), (k, what)
+            seen += 1
+    assert seen > 0
