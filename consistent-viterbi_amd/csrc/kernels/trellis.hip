@@ -1642,7 +1642,7 @@ __global__ __launch_bounds__(1024) void generic_fwd_split(GenericFwdArgs<REAL> a
       e = ok ? args.et[(size_t)o * N + j] : ninf;
       if (assoc == CVK_ASSOC_DP) {
         const bool live = e > ninf;  // a -inf emission leaves the column at -inf (dp.rs:147-177)
-        #pragma unroll 8
+        #pragma unroll 16
         for (int i = i0; i < i1; ++i) {
           const REAL c = (col[(size_t)i * N] + e) + prow[i];
           if (live && c > best) {
@@ -1656,7 +1656,7 @@ __global__ __launch_bounds__(1024) void generic_fwd_split(GenericFwdArgs<REAL> a
           best = prow[0] + col[0];
           ib = 1;
         }
-        #pragma unroll 8
+        #pragma unroll 16
         for (int i = ib; i < i1; ++i) {
           const REAL x = prow[i] + col[(size_t)i * N];
           if (x > best) {
@@ -2260,7 +2260,13 @@ hipError_t launch_generic_fwd(const GenericFwdArgs<REAL>& fa, int64_t nseq, hipS
     const int nt = (fa.nstates + 63) / 64 * 64;
     const char* se = getenv("CV_GENERIC_SPLIT");
     const bool split = se && *se ? *se != '0' : nseq < 2048;
-    const int K = std::min(8, 1024 / nt);
+    // K: at most 512 threads per workgroup, so four workgroups fit a CU and a batch of ~1,000
+    // sequences runs in one round (1,024-thread workgroups: two per CU, a second round at 620
+    // sequences); CV_GENERIC_SPLIT_K=2/4/8 sets it (A/B knob)
+    const char* ke = getenv("CV_GENERIC_SPLIT_K");
+    int K = ke && *ke ? atoi(ke) : 512 / nt;
+    K = K >= 8 ? 8 : K >= 4 ? 4 : K >= 2 ? 2 : 1;
+    while (K > 1 && nt * K > 1024) K /= 2;
     if (split && K >= 2 && fa.nstates <= 512) {
       const size_t lds = sizeof(REAL) * 2 * (size_t)fa.nstates + (sizeof(REAL) + 4) * (size_t)(K - 1) * nt;
       auto go = [&](auto kern) {

@@ -471,17 +471,19 @@ def test_t64_1024_equal_batch_chunks_vs_generic(gpu, monkeypatch):
         assert np.array_equal(x, y), what
 
 
-@pytest.mark.parametrize("split", ["1", "0"])
+@pytest.mark.parametrize("split", ["1:", "1:8", "0:"])
 @pytest.mark.parametrize("assoc", ["viterbi", "cp", "dp", "decode"])
 @pytest.mark.parametrize("dtype,n", [("f64", 5), ("f64", 64), ("f64", 100), ("f32", 200), ("f64", 256), ("f64", 300),
                                      ("f64", 512)])
 def test_generic_split_candidates(gpu, monkeypatch, split, assoc, dtype, n):
     """generic_fwd_split (one sequence per workgroup, K = 2..8 threads per state walking
-    ranges of the candidates, merged in range order; the small-batch psi-mode default below
-    N = 512, CV_GENERIC_SPLIT) and the one-thread-per-state kernel against the oracle in every
+    ranges of the candidates, merged in range order; CV_GENERIC_SPLIT, K from the state count
+    or CV_GENERIC_SPLIT_K) and the one-thread-per-state kernel against the oracle in every
     association: ragged and empty sequences, forced states, -inf transitions and emissions, an
     observation no state emits."""
+    split, k = split.split(":")
     monkeypatch.setenv("CV_GENERIC_SPLIT", split)
+    monkeypatch.setenv("CV_GENERIC_SPLIT_K", k)
     monkeypatch.setenv("CV_GENERIC_S", "1")
     monkeypatch.setenv("CV_GENERIC_ROWS", "0")
     pi, a, b = synth.random_hmm(n, 11, seed=n + 31, zero_frac=0.1)
