@@ -116,6 +116,35 @@ constexpr size_t kMaxTimedEvents = 1 << 16;  // cv_timing_begin: at most 16,384 
 // Pinned, double-buffered host staging of a decode call's longest-first order: the call
 // writes slot k only after that slot's previous copy has completed (its event), so the
 // copy is truly asynchronous and the host never waits for the stream's earlier work
+// A grow-only pinned host buffer (hipHostMalloc) for small device-to-host results read right
+// after a synchronize: a pageable destination goes through the runtime's staging copies (the
+// parallel chain's scores / statuses / certificates: ~2 ms per 1 MB array that way).
+struct PinnedHost {
+  void* p = nullptr;
+  size_t cap = 0;
+  PinnedHost() = default;
+  PinnedHost(const PinnedHost&) = delete;
+  PinnedHost& operator=(const PinnedHost&) = delete;
+  ~PinnedHost() {
+    if (p) (void)hipHostFree(p);
+  }
+  bool ensure(size_t bytes) {
+    if (cap >= bytes && p) return true;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+    const size_t want = std::max<size_t>(bytes, 4096);
+    if (hipHostMalloc(&p, want, hipHostMallocDefault) != hipSuccess) {
+      (void)hipGetLastError();
+      return false;
+    }
+    cap = want;
+    return true;
+  }
+  template <typename T>
+  T* as() const { return static_cast<T*>(p); }
+};
+
 struct OrderStage {
   int32_t* p[2] = {nullptr, nullptr};
   size_t cap[2] = {0, 0};
@@ -256,6 +285,7 @@ struct cv_hmm {
   // beside the certificate pass
   hipStream_t copy_stream = nullptr;
   hipEvent_t paths_ev = nullptr;
+  PinnedHost chain_pin;  // the chain's scores, statuses and certificates on their way to the host
 
   ~cv_hmm() {
     for (auto e : ev) (void)hipEventDestroy(e);
@@ -3105,10 +3135,22 @@ cv_status superseq_cp_par(cv_hmm* h, int64_t nseq, const int64_t* offsets, const
   } else {
     HIP_TRY(hipMemcpyAsync(path_out, d_path.p, (size_t)L * 4, hipMemcpyDeviceToHost, stream));
   }
-  HIP_TRY(hipMemcpyAsync(score.data(), d_score, (size_t)nseq * 8, hipMemcpyDeviceToHost, stream));
-  HIP_TRY(hipMemcpyAsync(status.data(), d_status, (size_t)nseq, hipMemcpyDeviceToHost, stream));
-  HIP_TRY(hipMemcpyAsync(cert.data(), d_cert.p, (size_t)nseq * 16, hipMemcpyDeviceToHost, stream));
-  HIP_TRY(hipStreamSynchronize(stream));
+  // scores, certificates and statuses through one pinned buffer (d_res holds scores then
+  // statuses contiguously)
+  if (h->chain_pin.ensure((size_t)nseq * 25)) {
+    unsigned char* pin = h->chain_pin.as<unsigned char>();
+    HIP_TRY(hipMemcpyAsync(pin, d_res.p, (size_t)nseq * 9, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipMemcpyAsync(pin + (size_t)nseq * 9, d_cert.p, (size_t)nseq * 16, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipStreamSynchronize(stream));
+    std::memcpy(score.data(), pin, (size_t)nseq * 8);
+    std::memcpy(status.data(), pin + (size_t)nseq * 8, (size_t)nseq);
+    std::memcpy(cert.data(), pin + (size_t)nseq * 9, (size_t)nseq * 16);
+  } else {
+    HIP_TRY(hipMemcpyAsync(score.data(), d_score, (size_t)nseq * 8, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipMemcpyAsync(status.data(), d_status, (size_t)nseq, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipMemcpyAsync(cert.data(), d_cert.p, (size_t)nseq * 16, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipStreamSynchronize(stream));
+  }
   if (paths_rec) HIP_TRY(hipStreamSynchronize(h->copy_stream));
   trace_mark("chain: paths, scores, certificates D2H");
   for (int64_t k = 0; k < nseq; ++k)
