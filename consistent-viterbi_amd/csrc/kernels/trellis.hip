@@ -2252,14 +2252,14 @@ hipError_t launch_generic_fwd(const GenericFwdArgs<REAL>& fa, int64_t nseq, hipS
   }
   // one sequence per workgroup: one thread per state up to N = 1,024 (64 ceil(N / 64) threads;
   // generic_fwd's 256 threads walk 4 states each at N = 1,024 -- a handful of sequences, e.g.
-  // the parallel chain's speculative re-decodes, then ran latency-bound on a few CUs); below
-  // N = 512 and under 2,048 sequences K = 1,024 / 64 ceil(N / 64) threads per state split each
-  // state's candidates (generic_fwd_split; CV_GENERIC_SPLIT=0: never, =1: at any batch size --
-  // read per launch, A/B knob and tests, bit-identical)
+  // the parallel chain's speculative re-decodes, then ran latency-bound on a few CUs).
+  // CV_GENERIC_SPLIT=1 (A/B knob, read per launch, bit-identical): K threads per state split
+  // each state's candidates (generic_fwd_split) -- measured neutral on the chain's speculative
+  // batch (12.4 vs 12.2 ms, profiles/r05_ab_spec_s.txt), so off by default
   {
     const int nt = (fa.nstates + 63) / 64 * 64;
     const char* se = getenv("CV_GENERIC_SPLIT");
-    const bool split = se && *se ? *se != '0' : nseq < 2048;
+    const bool split = se && *se == '1';
     // K: at most 512 threads per workgroup, so four workgroups fit a CU and a batch of ~1,000
     // sequences runs in one round (1,024-thread workgroups: two per CU, a second round at 620
     // sequences); CV_GENERIC_SPLIT_K=2/4/8 sets it (A/B knob)
