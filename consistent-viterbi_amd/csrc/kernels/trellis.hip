@@ -1595,8 +1595,7 @@ __global__ __launch_bounds__(1024) void generic_fwd_split(GenericFwdArgs<REAL> a
   const int NT = (int)blockDim.x / K;  // threads per range: 64 ceil(N / 64)
   REAL* dbuf = reinterpret_cast<REAL*>(smem_raw);  // [2][N]
   REAL* pbest = dbuf + 2 * (size_t)N;               // [K - 1][NT] partial maxima of ranges 1..K-1
-  REAL* pa = pbest + (size_t)(K - 1) * NT;          // [K - 1][NT] a[arg][j] of those maxima
-  int* parg = reinterpret_cast<int*>(pa + (size_t)(K - 1) * NT);  // [K - 1][NT] their arguments
+  int* parg = reinterpret_cast<int*>(pbest + (size_t)(K - 1) * NT);  // [K - 1][NT] their arguments
   const int V = args.nobs;
   const int assoc = args.assoc;
   const REAL ninf = -__builtin_inf();
@@ -1629,29 +1628,18 @@ __global__ __launch_bounds__(1024) void generic_fwd_split(GenericFwdArgs<REAL> a
     }
   }
   __syncthreads();
-  // the next step's observation, forced state and emission are loaded a step ahead (they do
-  // not depend on the recurrence), and the candidate walk carries a[arg][j] for the CP value,
-  // so no step waits on a dependent global load outside its candidate walk
-  const REAL* col = args.a + (j < N ? j : 0);
-  auto fetch = [&](int t, int& o, int& fs, REAL& e) {
-    o = args.obs[e0 + t];
-    fs = args.forced ? args.forced[e0 + t] : -1;
-    e = (j < N && (unsigned)o < (unsigned)V) ? args.et[(size_t)o * N + j] : ninf;
-  };
-  int o_n = 0, fs_n = -1;
-  REAL e_n = ninf;
-  if (T > 1) fetch(1, o_n, fs_n, e_n);
   for (int t = 1; t < T; ++t) {
-    const int o = o_n, fs = fs_n;
-    const REAL e = e_n;
+    const int o = args.obs[e0 + t];
     const bool ok = (unsigned)o < (unsigned)V;
     if (!ok) bad = 1;
-    if (t + 1 < T) fetch(t + 1, o_n, fs_n, e_n);
+    const int fs = args.forced ? args.forced[e0 + t] : -1;
     const REAL* prow = dbuf + (size_t)((t - 1) & 1) * N;
     REAL* crow = dbuf + (size_t)(t & 1) * N;
-    REAL best = ninf, besta = (REAL)0;
+    REAL e = ninf, best = ninf;
     int arg = 0;
+    const REAL* col = args.a + (j < N ? j : 0);
     if (j < N) {
+      e = ok ? args.et[(size_t)o * N + j] : ninf;
       if (assoc == CVK_ASSOC_DP) {
         const bool live = e > ninf;  // a -inf emission leaves the column at -inf (dp.rs:147-177)
         #pragma unroll 16
@@ -1665,24 +1653,20 @@ __global__ __launch_bounds__(1024) void generic_fwd_split(GenericFwdArgs<REAL> a
       } else {
         int ib = i0;
         if (q == 0) {  // i = 0 seeds the maximum (generic_fwd's `!any` case)
-          besta = col[0];
-          best = prow[0] + besta;
+          best = prow[0] + col[0];
           ib = 1;
         }
         #pragma unroll 16
         for (int i = ib; i < i1; ++i) {
-          const REAL aij = col[(size_t)i * N];
-          const REAL x = prow[i] + aij;
+          const REAL x = prow[i] + col[(size_t)i * N];
           if (x > best) {
             best = x;
             arg = i;
-            besta = aij;
           }
         }
       }
       if (q > 0) {
         pbest[(size_t)(q - 1) * NT + j] = best;
-        pa[(size_t)(q - 1) * NT + j] = besta;
         parg[(size_t)(q - 1) * NT + j] = arg;
       }
     }
@@ -1694,7 +1678,6 @@ __global__ __launch_bounds__(1024) void generic_fwd_split(GenericFwdArgs<REAL> a
         if (pb > best) {
           best = pb;
           arg = parg[(size_t)r * NT + j];
-          besta = pa[(size_t)r * NT + j];
         }
       }
       REAL v;
@@ -1702,7 +1685,7 @@ __global__ __launch_bounds__(1024) void generic_fwd_split(GenericFwdArgs<REAL> a
       if (assoc == CVK_ASSOC_DP)
         v = (e > ninf) ? best : ninf;
       else if (assoc == CVK_ASSOC_CP)
-        v = prow[ag] + (besta + e);  // besta = a[ag][j]
+        v = prow[ag] + (col[(size_t)ag * N] + e);
       else
         v = best + e;
       if (assoc == CVK_ASSOC_DECODE && !(e > ninf)) {
@@ -2285,7 +2268,7 @@ hipError_t launch_generic_fwd(const GenericFwdArgs<REAL>& fa, int64_t nseq, hipS
     K = K >= 8 ? 8 : K >= 4 ? 4 : K >= 2 ? 2 : 1;
     while (K > 1 && nt * K > 1024) K /= 2;
     if (split && K >= 2 && fa.nstates <= 512) {
-      const size_t lds = sizeof(REAL) * 2 * (size_t)fa.nstates + (2 * sizeof(REAL) + 4) * (size_t)(K - 1) * nt;
+      const size_t lds = sizeof(REAL) * 2 * (size_t)fa.nstates + (sizeof(REAL) + 4) * (size_t)(K - 1) * nt;
       auto go = [&](auto kern) {
         if (lds > 64 * 1024)
           (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
