@@ -224,6 +224,8 @@ hipError_t launch_t64_fwd(int np, int s, const T64FwdArgs& fa, int64_t nseq, hip
 bool t64_wave_fusable(int np, const T64FwdArgs& fa, const T64BtArgs& ba);
 hipError_t launch_t64_wave_fused(const T64FwdArgs& fa, const T64BtArgs& ba, int64_t nseq, hipStream_t stream);
 // CP association (cp.rs:70-79): psi and the CP value d[psi] + (a[psi,j] + b[j,o]) in the forward
+// sequences per wave the CP forward launches for a requested s and batch size
+int t64_cp_seqs_per_wave(int s, int64_t nseq);
 hipError_t launch_t64_cp_fwd(int np, int s, const T64FwdArgs& fa, int64_t nseq, hipStream_t stream);
 // max_wgs > 0: at most that many 4-wave workgroups, each looping over the slots (persistent)
 hipError_t launch_t64_bt(int np, const T64BtArgs& ba, int64_t nseq, hipStream_t stream, int max_wgs = 0);

@@ -903,10 +903,12 @@ __global__ __launch_bounds__(512) void trellis_fwd_f64_rs(T64FwdArgs g) {
 // LDS gather of d[psi] and one L2 gather of a[psi,j].  psi (u16) and the last row go out in
 // generic_fwd's layout; generic_backtrack<double> follows them (cp.rs:85-93).  Same wave
 // layout as trellis_fwd_f64 (S sequences per wave, A rows streamed through a register ring).
+// S = 1 (round 5): one sequence per wave for small batches (the parallel chain's speculative
+// re-decodes, ~620 sequences at config-4 size), so every sequence has a SIMD of its own.
 template <int C, int S, int PF>
 __global__ __launch_bounds__(64) void trellis_cp_f64(T64FwdArgs g) {
   constexpr int NP = 64 * C;
-  static_assert(S % 2 == 0 && PF % 2 == 0, "pairs of sequences / rows");
+  static_assert((S == 1 || S % 2 == 0) && PF % 2 == 0, "one sequence or pairs of sequences / rows");
   __shared__ __attribute__((aligned(16))) double dl[NP * S];  // delta_{t-1}: [row][S]
   const int lane = threadIdx.x;
   const int j0 = lane * C;
@@ -990,14 +992,33 @@ __global__ __launch_bounds__(64) void trellis_cp_f64(T64FwdArgs g) {
     double ar[PF][C];
 #pragma unroll
     for (int u = 0; u < PF; ++u) load_a(arow + (size_t)u * NP, ar[u]);
-    double2 dv[2][S / 2];
+    constexpr int S2 = S / 2 > 0 ? S / 2 : 1;
+    double2 dv[2][S2];
+    double d1[2];  // S = 1: delta_{t-1}[i] and the next row's
+    if constexpr (S == 1) {
+      d1[0] = dl[0];
+    } else {
 #pragma unroll
-    for (int s2 = 0; s2 < S / 2; ++s2) dv[0][s2] = reinterpret_cast<const double2*>(dl)[s2];
+      for (int s2 = 0; s2 < S / 2; ++s2) dv[0][s2] = reinterpret_cast<const double2*>(dl)[s2];
+    }
 #pragma nounroll
     for (int i0 = 0; i0 < NP; i0 += PF) {
 #pragma unroll
       for (int u = 0; u < PF; ++u) {
         const int i = i0 + u;
+        if constexpr (S == 1) {
+          d1[(u + 1) & 1] = dl[min(i + 1, NP - 1)];
+          const double d = d1[u & 1];
+#pragma unroll
+          for (int c = 0; c < C; ++c) {
+            const double x = d + ar[u][c];
+            idx[c][0] = x > acc[c][0] ? i : idx[c][0];
+            acc[c][0] = fmax(acc[c][0], x);
+          }
+          const int nr = min(i + PF, NP - 1);
+          load_a(arow + (size_t)nr * NP, ar[u]);
+          continue;
+        }
         {
           const double2* nrow = reinterpret_cast<const double2*>(dl + min(i + 1, NP - 1) * S);
 #pragma unroll
@@ -1855,6 +1876,7 @@ template <int C>
 hipError_t cp_c(const T64FwdArgs& fa, int s, int64_t nseq, hipStream_t stream) {
   const dim3 block(64);
   switch (s) {
+    case 1: hipLaunchKernelGGL((trellis_cp_f64<C, 1, 4>), dim3((unsigned)nseq), block, 0, stream, fa); break;
     case 2: hipLaunchKernelGGL((trellis_cp_f64<C, 2, 4>), dim3((unsigned)((nseq + 1) / 2)), block, 0, stream, fa); break;
     case 4: hipLaunchKernelGGL((trellis_cp_f64<C, 4, 4>), dim3((unsigned)((nseq + 3) / 4)), block, 0, stream, fa); break;
     default: return hipErrorInvalidValue;
@@ -1862,9 +1884,17 @@ hipError_t cp_c(const T64FwdArgs& fa, int s, int64_t nseq, hipStream_t stream) {
   return hipGetLastError();
 }
 
+int t64_cp_seqs_per_wave(int s, int64_t nseq) {
+  s = s > 4 ? 4 : s;  // the argmax state (idx) costs registers: at most 4 sequences per wave
+  // a batch that leaves SIMDs idle at two sequences per wave: one per wave (the sequences are
+  // independent, so the results are the same); CV_T64_CP_S=1/2/4 sets it (A/B knob, per launch)
+  if (const char* e = getenv("CV_T64_CP_S"); e && *e) return atoi(e) >= 4 ? 4 : atoi(e) >= 2 ? 2 : 1;
+  return nseq <= 1024 ? 1 : s;
+}
+
 hipError_t launch_t64_cp_fwd(int np, int s, const T64FwdArgs& fa, int64_t nseq, hipStream_t stream) {
   if (nseq <= 0) return hipSuccess;
-  s = s > 4 ? 4 : s;  // the argmax state (idx) costs registers: at most 4 sequences per wave
+  s = t64_cp_seqs_per_wave(s, nseq);
   switch (np) {
     case 64: return cp_c<1>(fa, s, nseq, stream);
     case 128: return cp_c<2>(fa, s, nseq, stream);

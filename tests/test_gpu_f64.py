@@ -428,3 +428,32 @@ def test_timing_sums_every_call(gpu):
     assert cv.last_timing(h)["launches"] == one["launches"]
     with pytest.raises(cv.CVError):
         cv.timing_end(h)  # no timing_begin pending
+
+
+@pytest.mark.parametrize("s", ["1", "2", "4"])
+@pytest.mark.parametrize("n", [7, 100, 256])
+def test_t64_cp_seqs_per_wave(gpu, monkeypatch, s, n):
+    """trellis_cp_f64 at S = 1 (one sequence per wave: the default up to 1,024 sequences, the
+    parallel chain's speculative batches), 2 and 4 (CV_T64_CP_S): CPSolver's association against
+    the oracle on quantised ties (first index), -inf entries and ragged / empty sequences; the
+    reported seqs_per_wave is the S launched."""
+    monkeypatch.setenv("CV_T64_CP_S", s)
+    rng = np.random.default_rng(n + 5)
+    v = 9
+    pi = np.round(rng.uniform(-2, 0, n) * 2) / 2
+    a = np.round(rng.uniform(-2, 0, (n, n)) * 2) / 2
+    b = np.round(rng.uniform(-2, 0, (n, v)) * 2) / 2
+    a[rng.random((n, n)) < 0.2] = -np.inf
+    b[:, 3] = -np.inf
+    lengths = rng.integers(0, 70, size=37)
+    off = synth.offsets_from_lengths(lengths)
+    obs = rng.integers(0, v, size=int(off[-1])).astype(np.int32)
+    h = cv.HMM(pi, a, b)
+    got = cv.decode_batch(h, off, obs, dtype="f64", assoc="cp", rescore_f64=False)
+    t = cv.last_timing(h)
+    assert t["kernel"] == "trellis_f64" and t["seqs_per_wave"] == int(s), t
+    _assert_same(got, O.decode_batch(pi, a, b, off, obs, O.CP, np.float64), f"cp S={s} N={n}")
+    pi2, a2, b2, off2, obs2 = _case(n, 41, seed=900 + n)
+    h2 = cv.HMM(pi2, a2, b2)
+    _assert_same(cv.decode_batch(h2, off2, obs2, dtype="f64", assoc="cp", rescore_f64=False),
+                 O.decode_batch(pi2, a2, b2, off2, obs2, O.CP, np.float64), f"cp random S={s} N={n}")
