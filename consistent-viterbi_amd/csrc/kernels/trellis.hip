@@ -1427,8 +1427,9 @@ __global__ __launch_bounds__(1024) void generic_fwd_ms(GenericFwdArgs<REAL> args
   const int V = args.nobs;
   const int assoc = args.assoc;
   const REAL ninf = -__builtin_inf();
-  // candidate loops unrolled for one-sequence workgroups in psi mode only (see CVK_GEN_UNROLL)
-  constexpr int kCandUnroll = (S == 1 && !ROWS) ? CVK_GEN_UNROLL : 1;
+  // candidate loops unrolled for one- and two-sequence workgroups in psi mode only (see
+  // CVK_GEN_UNROLL): a rolled walk waits out one L2 latency per candidate
+  constexpr int kCandUnroll = (S <= 2 && !ROWS) ? CVK_GEN_UNROLL : 1;
   int64_t e0[S], slot[S], seq[S];
   int T[S];
   int Tmax = 0;
