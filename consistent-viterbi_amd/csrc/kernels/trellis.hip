@@ -2246,7 +2246,12 @@ hipError_t launch_generic_fwd(const GenericFwdArgs<REAL>& fa, int64_t nseq, hipS
       default: return launch_generic_ms<REAL, 1, true>(fa, nseq, stream);
     }
   }
-  switch (generic_seqs_per_wg<REAL>(fa.nstates, nseq)) {
+  int s = generic_seqs_per_wg<REAL>(fa.nstates, nseq);
+  // psi mode from 256 sequences on: two per workgroup (each A load serves both, the walk
+  // unrolled) -- the chain's speculative batch (~620 sequences at N = 256) 11.9 -> 8.5 ms
+  // (profiles/r05_ab_spec_s2.txt); below, one per workgroup keeps more of them in flight
+  if (s == 1 && nseq >= 256 && !getenv("CV_GENERIC_S") && 4 * (size_t)fa.nstates * sizeof(REAL) <= 160 * 1024) s = 2;
+  switch (s) {
     case 4: return launch_generic_ms<REAL, 4, false>(fa, nseq, stream);
     case 2: return launch_generic_ms<REAL, 2, false>(fa, nseq, stream);
     default: break;

@@ -531,3 +531,29 @@ def test_generic_split_golden(gpu, monkeypatch, split, name):
                 assert np.array_equal(x, y), (k, what)
             seen += 1
     assert seen > 0
+
+
+@pytest.mark.parametrize("assoc", ["cp", "viterbi"])
+@pytest.mark.parametrize("n", [100, 300])
+def test_generic_psi_two_per_workgroup_default(gpu, monkeypatch, assoc, n):
+    """psi mode from 256 sequences on runs two sequences per workgroup by default (the walk
+    unrolled): 300 ragged sequences against the oracle and against one per workgroup
+    (CV_GENERIC_S=1), bit for bit."""
+    monkeypatch.setenv("CV_GENERIC_ROWS", "0")
+    monkeypatch.delenv("CV_GENERIC_S", raising=False)
+    pi, a, b = synth.random_hmm(n, 13, seed=n + 404, zero_frac=0.05)
+    rng = np.random.default_rng(n + 405)
+    lens = rng.integers(0, 20, size=300)
+    off = synth.offsets_from_lengths(lens)
+    obs = rng.integers(0, 13, size=int(off[-1])).astype(np.int32)
+    h = cv.HMM(pi, a, b)
+    got = cv.decode_batch(h, off, obs, dtype="f64", assoc=assoc, kernel="generic", rescore_f64=False)
+    ref = O.decode_batch(pi, a, b, off, obs, O.CP if assoc == "cp" else O.VITERBI, np.float64)
+    assert np.array_equal(got[2], ref[2])
+    ok = got[2] == 0
+    assert np.array_equal(got[1][ok], ref[1][ok])
+    assert np.array_equal(got[0], ref[0])
+    monkeypatch.setenv("CV_GENERIC_S", "1")
+    one = cv.decode_batch(h, off, obs, dtype="f64", assoc=assoc, kernel="generic", rescore_f64=False)
+    for x, y in zip(got, one):
+        assert np.array_equal(x, y)
