@@ -53,7 +53,17 @@ struct BwArgs {
   double* b_num;        // [V][N] sum of gamma_t at o_t
   double* xi_s;         // [N][N] sum of (alpha_t / c_t) (x) u_{t+1}
   double* xi_zero;      // [1] number of steps with c_t == 0 (uniform xi)
+  // rows of A with an entry below kBwTinyArc (bw_rowscale): rowscale[i] = a power of two <= the
+  // row's smallest nonzero entry (0 for the other rows); non-null: the E-step runs the xi GEMM
+  // path at every N and a second GEMM pass accumulates sum_t (rowscale[i] r_t[i]) u_{t+1}[j]
+  // into xi_s2, which stays inside the f64 range where xi_s overflows
+  const double* rowscale;
+  double* xi_s2;        // [N][N]
 };
+
+// an arc below this (2^-960) can make the factored xi sum of its entry overflow once its
+// per-step counts (each <= 1) summed over the corpus pass ~2^63 * a (never for a larger arc)
+constexpr double kBwTinyArc = 0x1p-960;
 
 constexpr int kBwWaveStates = 64;  // N <= 64: one wave per sequence (bw_*_wave)
 constexpr int kBwDumpWaves = 4096;
@@ -70,6 +80,8 @@ struct MstepArgs {
   double* et;    // [V][N]  b^T, updated in place
   double* part;  // [parts_a + nparts_b] per-block sums of |new - old|
   int parts_a;   // blocks of the pi / a M-step (1; 1,024 above kBwLdsMaxStates: N^2 entries)
+  const double* rowscale;  // BwArgs::rowscale of the E-step just run, or null
+  const double* xs2;       // BwArgs::xi_s2 of that E-step (with rowscale)
 };
 
 hipError_t launch_mle_counts(const MleArgs& g, int64_t nseq, hipStream_t stream);
@@ -82,6 +94,8 @@ hipError_t launch_bw_estep(const BwArgs& g, int64_t nseq, int64_t max_waves, hip
                            hipEvent_t fwd_done = nullptr);
 // the E-step sequences per pipeline part have the matrix-core kernels (64 < N <= 256)
 bool bw_estep_mm(int nstates);
+// rowscale[i] for A's rows (BwArgs::rowscale); *flag |= 1 when some row has a tiny arc
+hipError_t launch_bw_rowscale(const double* a, int nstates, double* rowscale, unsigned* flag, hipStream_t stream);
 hipError_t launch_bw_mstep(const MstepArgs& m, int nparts_b, hipStream_t stream);
 
 }  // namespace cvf

@@ -477,6 +477,17 @@ __global__ __launch_bounds__(64, 2) void bw_xi_gemm(BwArgs g, int64_t nrows, int
     cm[q] = min(cm[q], N - 1);
     cn[q] = min(cn[q], N - 1);
   }
+  // the row-scaled second pass (g.rowscale): R's column m times rowscale[m]; tiles without a
+  // scaled row have nothing to add (wave-uniform exit)
+  double csc[TM];
+#pragma unroll
+  for (int q = 0; q < TM; ++q) csc[q] = g.rowscale ? g.rowscale[cm[q]] : 1.0;
+  if (g.rowscale) {
+    bool any = false;
+#pragma unroll
+    for (int q = 0; q < TM; ++q) any |= vm[q] && csc[q] != 0.0;
+    if (__ballot(any) == 0) return;
+  }
   // per 4 rows: TM loads of R and of U (lane l: row r + l/16, column l%16 of each 16-wide
   // tile), masked loads (a select on a loaded value cost ~30% here); ST = 2 issues the next 4
   // rows' loads before the current rows' MFMAs
@@ -494,7 +505,7 @@ __global__ __launch_bounds__(64, 2) void bw_xi_gemm(BwArgs g, int64_t nrows, int
     const double* U_ = g.beta + (size_t)(vr_ ? row_ : r0) * N;               \
     const double rs_ = g.rscale ? g.rscale[vr_ ? row_ : r0] : 1.0;           \
     _Pragma("unroll") for (int q = 0; q < TM; ++q) {                         \
-      AV[q] = (vr_ && vm[q]) ? R_[cm[q]] * rs_ : 0.0;                        \
+      AV[q] = (vr_ && vm[q]) ? (R_[cm[q]] * rs_) * csc[q] : 0.0;             \
       BV[q] = (vr_ && vn[q]) ? U_[cn[q]] : 0.0;                              \
     }                                                                        \
   }
@@ -546,11 +557,17 @@ __global__ __launch_bounds__(256, 2) void bw_xi_gemm_lds(BwArgs g, int64_t nrows
   const int64_t r1 = r0 + rows_per_wg < nrows ? r0 + rows_per_wg : nrows;
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, kk = l >> 4, cl = l & 15;
   const int wm = w >> 1, wn = w & 1;
+  // the row-scaled second pass (g.rowscale): R's column m times rowscale[m]; a tile without a
+  // scaled row has nothing to add (workgroup-uniform exit, before any other barrier)
+  if (g.rowscale && !__syncthreads_or(tid < TS && m0 + tid < N && g.rowscale[m0 + tid] != 0.0)) return;
   // staging: thread tid copies row (tid >> 4) of R and U, 8 doubles from column 8 (tid & 15);
   // A/B: 16-byte loads of strided column pairs with forced selects (2-way LDS write conflicts)
   // 98 vs 79 ms, 8-byte strided loads 109 ms
   const int srow = tid >> 4, scol = 8 * (tid & 15);
   double rsc = 1.0;  // the staged row's R scale
+  double csc[8];     // the staged columns' row scales (second pass), else 1
+#pragma unroll
+  for (int q = 0; q < 8; ++q) csc[q] = g.rowscale ? g.rowscale[min(m0 + scol + q, N - 1)] : 1.0;
   auto stage_load = [&](int64_t rb, double (&ra)[8], double (&ua)[8]) {
     const int64_t row = rb + srow;
     const bool vr = row < r1;
@@ -567,7 +584,7 @@ __global__ __launch_bounds__(256, 2) void bw_xi_gemm_lds(BwArgs g, int64_t nrows
   auto stage_store = [&](int buf, const double (&ra)[8], const double (&ua)[8]) {
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
-      rs[buf][srow * LS + scol + q] = ra[q] * rsc;
+      rs[buf][srow * LS + scol + q] = (ra[q] * rsc) * csc[q];
       us[buf][srow * LS + scol + q] = ua[q];
     }
   };
@@ -1464,6 +1481,38 @@ __global__ __launch_bounds__(64 * WV, (MT == 4 ? 1 : 2) * WV / 4) void bw_bwd_mm
   }
 }
 
+// ---- rows of A with a tiny arc (BwArgs::rowscale) ----------------------------------------------
+// rowscale[i] = 2^ilogb(min nonzero a[i][j]) when that minimum is below kBwTinyArc (an exact
+// power of two <= every nonzero entry of the row, subnormal allowed), else 0.
+__global__ __launch_bounds__(256) void bw_rowscale(const double* __restrict__ a, int N, double* rowscale,
+                                                   unsigned* flag) {
+  __shared__ double red[4];
+  const int64_t i = blockIdx.x;
+  double mn = __builtin_inf();
+  for (int j = threadIdx.x; j < N; j += 256) {
+    const double v = a[i * N + j];
+    mn = v > 0.0 ? fmin(mn, v) : mn;
+  }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) mn = fmin(mn, __shfl_xor(mn, off));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mn;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const double m = fmin(fmin(red[0], red[1]), fmin(red[2], red[3]));
+    double sc = 0.0;
+    if (m < kBwTinyArc) {
+      sc = ldexp(1.0, ilogb(m));
+      atomicOr(flag, 1u);
+    }
+    rowscale[i] = sc;
+  }
+}
+
+hipError_t launch_bw_rowscale(const double* a, int nstates, double* rowscale, unsigned* flag, hipStream_t stream) {
+  hipLaunchKernelGGL(bw_rowscale, dim3((unsigned)nstates), dim3(256), 0, stream, a, nstates, rowscale, flag);
+  return hipGetLastError();
+}
+
 // ---- M-step on the device (hmm.rs:145-175) ---------------------------------------------------
 // Parameters stay resident between iterations: pi, a (and its transpose at), et = b^T.  The
 // convergence sum d = sum |new - old| is reduced per block into part[]; the host adds the
@@ -1503,8 +1552,13 @@ __global__ __launch_bounds__(256) void bw_mstep_pa(MstepArgs m) {
     // 1 / A): a == 0 takes no term (the reference's entries are 0 there; 0 * inf would be NaN),
     // and S is clamped to DBL_MAX (finite for a subnormal a; never reached for a normal one
     // unless ~1/a summed over steps overflows)
-    const double na =
-        ((m.a[k] != 0.0 ? m.a[k] * fmin(xs[k], 1.7976931348623157e308) : 0.0) + zu) / a_den[i];
+    // ... unless the row was rescaled (m.rowscale): a tiny arc's count then comes from the
+    // second pass's sum S' = rowscale[i] S, which stays in range: (a / rowscale[i]) S'
+    const double rsc = m.rowscale ? m.rowscale[i] : 0.0;
+    const double cnt = (m.xs2 && rsc > 0.0 && m.a[k] != 0.0 && m.a[k] < kBwTinyArc)
+                           ? (m.a[k] / rsc) * m.xs2[k]
+                           : (m.a[k] != 0.0 ? m.a[k] * fmin(xs[k], 1.7976931348623157e308) : 0.0);
+    const double na = (cnt + zu) / a_den[i];
     d += fabs(na - m.a[k]);
     m.a[k] = na;
     m.at[(size_t)j * N + i] = na;
@@ -1640,12 +1694,21 @@ hipError_t launch_bw_estep(const BwArgs& g, int64_t nseq, int64_t max_waves, hip
     const int64_t parts2 = std::max<int64_t>(1, std::min<int64_t>(512 / (nt * nt), (nrows + 255) / 256));
     const int64_t per2 = ((nrows + parts2 - 1) / parts2 + kGemmKB - 1) / kGemmKB * kGemmKB;
     const int64_t np2 = (nrows + per2 - 1) / per2;
-    hipLaunchKernelGGL(bw_xi_gemm_lds, dim3((unsigned)((np2 + 7) / 8 * 8 * nt * nt)), dim3(256), 0, stream, g, nrows,
+    BwArgs g0 = g;
+    g0.rowscale = nullptr;  // the plain sum first
+    hipLaunchKernelGGL(bw_xi_gemm_lds, dim3((unsigned)((np2 + 7) / 8 * 8 * nt * nt)), dim3(256), 0, stream, g0, nrows,
                        per2);
+    if (g.rowscale) {  // the row-scaled second pass (tiny arcs) into xi_s2
+      BwArgs gs = g;
+      gs.xi_s = g.xi_s2;
+      hipLaunchKernelGGL(bw_xi_gemm_lds, dim3((unsigned)((np2 + 7) / 8 * 8 * nt * nt)), dim3(256), 0, stream, gs,
+                         nrows, per2);
+    }
     return hipGetLastError();
   }
   const bool mm = bw_estep_mm(g.nstates);
-  if (g.nstates > kBwLdsStates || mm) {  // the xi sum as R^T U on the matrix cores
+  // tiny arcs (g.rowscale): the GEMM path at any N, so the row-scaled second pass has rows to read
+  if (g.nstates > kBwLdsStates || mm || g.rowscale) {  // the xi sum as R^T U on the matrix cores
     BwArgs gg = g;
     if (!mm) gg.rscale = nullptr;  // the per-sequence kernels store R over alpha
     if (mm) {  // 16 MT sequences per workgroup, the step products on the matrix cores
@@ -1669,6 +1732,11 @@ hipError_t launch_bw_estep(const BwArgs& g, int64_t nseq, int64_t max_waves, hip
       hipLaunchKernelGGL(bw_backward, dim3((unsigned)nseq), dim3(256), 0, stream, g);
       hipLaunchKernelGGL(bw_stats_rows, dim3((unsigned)nseq), dim3(256), 0, stream, g);
     }
+    // the GEMM, then (tiny arcs) its row-scaled second pass into xi_s2
+    for (int pass = 0; pass < (g.rowscale ? 2 : 1); ++pass) {
+    if (pass == 1) gg.xi_s = g.xi_s2;
+    else gg.rowscale = nullptr;
+    if (pass == 1) gg.rowscale = g.rowscale;
     // 64 x 64 tiles per wave above 128 states (32 x 32 below); ~4,096 waves: row ranges of a
     // multiple of 4 rows per output tile
     const bool t64 = g.nstates > 128 && !gemm32();
@@ -1692,6 +1760,7 @@ hipError_t launch_bw_estep(const BwArgs& g, int64_t nseq, int64_t max_waves, hip
       hipLaunchKernelGGL((bw_xi_gemm<4, 1>), grid, block, 0, stream, gg, nrows, per);
     else
       hipLaunchKernelGGL((bw_xi_gemm<2, 1>), grid, block, 0, stream, gg, nrows, per);
+    }
     return hipGetLastError();
   }
   if (g.nstates <= kBwWaveStates) {

@@ -249,3 +249,41 @@ def test_gpu_train_pipeline_parts_match_oracle(gpu, monkeypatch, n, pipe):
         fin = np.isfinite(r)
         np.testing.assert_allclose(g[fin], r[fin], rtol=0, atol=1e-9, err_msg=what)
         np.testing.assert_allclose(g[fin], o[fin], rtol=0, atol=1e-12, err_msg=what)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [20, 100, 300])  # one-wave sizes (routed to the GEMM path), matrix-core, strided
+def test_gpu_train_tiny_arcs_forced(gpu, n):
+    """Arcs far below DBL_MIN's square root that tags force through: a 1e-306 arc
+    p -> q and a subnormal 5e-320 arc p2 -> q2, each taken ~1,200 times by fully tagged
+    sequences, so every step's xi is one-hot there and the factored sum sum_t r_t u_{t+1}
+    (~1 / a per step) leaves the f64 range.  The row-scaled second xi pass keeps those counts
+    exact: two EM iterations against the oracle (per-entry xi, hmm.rs:133-143)."""
+    import cviterbi as cv
+
+    v = 23
+    rng = np.random.default_rng(7000 + n)
+    pi0, a0, b0 = _probs(n, v, seed=7000 + n)
+    p, q, p2, q2 = 1, 3, 5, 2
+    a0[p, q] = 1e-306
+    a0[p2, q2] = 5e-320
+    a0 /= a0.sum(axis=1, keepdims=True)
+    assert 0 < a0[p2, q2] < 2.3e-308  # still subnormal after the renormalisation
+    tagged = [np.tile([p, q], 30), np.tile([p2, q2], 30)] * 20  # 1,200 forced steps per arc
+    free = [rng.integers(0, n, size=int(rng.integers(5, 40))) for _ in range(30)]
+    seqs = tagged + free
+    lengths = np.array([len(x) for x in seqs])
+    off = np.zeros(len(seqs) + 1, np.int64)
+    np.cumsum(lengths, out=off[1:])
+    obs = rng.integers(0, v, size=int(off[-1])).astype(np.int32)
+    tags = np.full(int(off[-1]), -1, np.int32)
+    for k in range(len(tagged)):
+        tags[off[k]:off[k + 1]] = tagged[k]
+    iters = 2
+    gp, ga, gb, it = cv.fit_train(pi0, a0, b0, off, obs, tags, max_iter=iters, tol=0.0)
+    assert it == iters
+    rp, ra, rb, _ = FO.train(pi0, a0, b0, off, obs, tags, iters, 0.0)
+    for g, r, what in zip((gp, ga, gb), (rp, ra, rb), ("pi", "a", "b")):
+        assert np.array_equal(np.isinf(g), np.isinf(r)), what
+        fin = np.isfinite(r)
+        np.testing.assert_allclose(g[fin], r[fin], rtol=0, atol=1e-9, err_msg=what)
