@@ -12,6 +12,7 @@ step() {
   echo "== $name" ; timeout -k 10 $t "$@" > $O/$name.log 2>&1; local rc=$?
   tail -3 $O/$name.log | cut -c1-300; echo "== $name rc=$rc"; return $rc
 }
+step fit 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu tests/test_fit.py &&
 step pytest 900 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu tests &&
 step smoke 200 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" &&
 step bench 400 python -u bench.py
