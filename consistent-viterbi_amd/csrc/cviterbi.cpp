@@ -3130,9 +3130,18 @@ cv_status superseq_cp_par(cv_hmm* h, int64_t nseq, const int64_t* offsets, const
     HIP_TRY(hipStreamSynchronize(stream));
     trace_mark("chain: row-A0 decode + certificates (device)");
   }
+  // an early return below must not leave the copy writing into the caller's buffer
+  struct CopyJoin {
+    hipStream_t s;
+    bool on;
+    ~CopyJoin() {
+      if (on) (void)hipStreamSynchronize(s);
+    }
+  } copy_join{h->copy_stream, false};
   if (paths_rec) {
     HIP_TRY(hipStreamWaitEvent(h->copy_stream, h->paths_ev, 0));
     HIP_TRY(hipMemcpyAsync(path_out, d_path.p, (size_t)L * 4, hipMemcpyDeviceToHost, h->copy_stream));
+    copy_join.on = true;
   } else {
     HIP_TRY(hipMemcpyAsync(path_out, d_path.p, (size_t)L * 4, hipMemcpyDeviceToHost, stream));
   }
@@ -3152,7 +3161,10 @@ cv_status superseq_cp_par(cv_hmm* h, int64_t nseq, const int64_t* offsets, const
     HIP_TRY(hipMemcpyAsync(cert.data(), d_cert.p, (size_t)nseq * 16, hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipStreamSynchronize(stream));
   }
-  if (paths_rec) HIP_TRY(hipStreamSynchronize(h->copy_stream));
+  if (paths_rec) {
+    copy_join.on = false;
+    HIP_TRY(hipStreamSynchronize(h->copy_stream));
+  }
   trace_mark("chain: paths, scores, certificates D2H");
   for (int64_t k = 0; k < nseq; ++k)
     if (status[(size_t)k] != CV_SEQ_OK && status[(size_t)k] != CV_SEQ_EMPTY) return CV_OK;  // serial chain
