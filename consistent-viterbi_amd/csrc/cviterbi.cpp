@@ -4134,8 +4134,10 @@ CV_API cv_status cv_hmm_fit_train(int32_t nstates, int64_t nobs, int64_t nseq, c
     s0 = s1;
   }
   if ((st = d.alpha.ensure((size_t)max_chunk * N * 8)) != CV_OK) return st;
-  // beta rows only for the workgroup kernels (N > 64); the one-wave backward never stores beta
-  if (N > cvf::kBwWaveStates && (st = d.beta.ensure((size_t)max_chunk * N * 8)) != CV_OK) return st;
+  // beta rows only for the workgroup kernels (N > 64, or CV_BW_GEMM_PATH=1); the one-wave
+  // backward never stores beta
+  if ((N > cvf::kBwWaveStates || cvf::bw_gemm_path()) && (st = d.beta.ensure((size_t)max_chunk * N * 8)) != CV_OK)
+    return st;
   if (N > cvf::kBwWaveStates && N <= cvf::kBwMmStates && (st = d.rscale.ensure((size_t)max_chunk * 8)) != CV_OK)
     return st;
   const size_t nacc = 3 * (size_t)N + (size_t)V * N + (size_t)N * N + 1;

@@ -94,6 +94,8 @@ hipError_t launch_bw_estep(const BwArgs& g, int64_t nseq, int64_t max_waves, hip
                            hipEvent_t fwd_done = nullptr);
 // the E-step sequences per pipeline part have the matrix-core kernels (64 < N <= 256)
 bool bw_estep_mm(int nstates);
+// CV_BW_GEMM_PATH=1: the per-sequence kernels + xi GEMM at every N (what tiny arcs select)
+bool bw_gemm_path();
 // rowscale[i] for A's rows (BwArgs::rowscale); *flag |= 1 when some row has a tiny arc
 hipError_t launch_bw_rowscale(const double* a, int nstates, double* rowscale, unsigned* flag, hipStream_t stream);
 hipError_t launch_bw_mstep(const MstepArgs& m, int nparts_b, hipStream_t stream);

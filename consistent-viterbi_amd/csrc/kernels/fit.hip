@@ -1663,6 +1663,11 @@ static bool bw_per_seq() {  // A/B knob: CV_BW_PERSEQ=1 keeps one workgroup per 
 
 bool bw_estep_mm(int nstates) { return nstates > kBwWaveStates && nstates <= kBwMmStates && !bw_per_seq(); }
 
+bool bw_gemm_path() {  // A/B knob and tests: CV_BW_GEMM_PATH=1 takes the xi GEMM path at every N
+  const char* e = getenv("CV_BW_GEMM_PATH");  // read per call
+  return e && e[0] == '1';
+}
+
 hipError_t launch_bw_estep(const BwArgs& g, int64_t nseq, int64_t max_waves, hipStream_t stream, int64_t nrows,
                            hipEvent_t fwd_done) {
   if (nseq <= 0) return hipSuccess;
@@ -1708,7 +1713,7 @@ hipError_t launch_bw_estep(const BwArgs& g, int64_t nseq, int64_t max_waves, hip
   }
   const bool mm = bw_estep_mm(g.nstates);
   // tiny arcs (g.rowscale): the GEMM path at any N, so the row-scaled second pass has rows to read
-  if (g.nstates > kBwLdsStates || mm || g.rowscale) {  // the xi sum as R^T U on the matrix cores
+  if (g.nstates > kBwLdsStates || mm || g.rowscale || bw_gemm_path()) {  // the xi sum as R^T U on the matrix cores
     BwArgs gg = g;
     if (!mm) gg.rscale = nullptr;  // the per-sequence kernels store R over alpha
     if (mm) {  // 16 MT sequences per workgroup, the step products on the matrix cores
