@@ -28,11 +28,13 @@ def case(n, arcs, iters):
     pi0, a0, b0 = _probs(n, v, seed=7000 + n)
     p, q, p2, q2 = 1, 3, 5, 2
     tagged = []
-    if "normal" in arcs:
-        a0[p, q] = 1e-306
+    if "normal" in arcs or "tags" in arcs:
+        if "normal" in arcs:
+            a0[p, q] = 1e-306
         tagged += [np.tile([p, q], 30)] * 20
-    if "sub" in arcs:
-        a0[p2, q2] = 5e-320
+    if "sub" in arcs or "tags" in arcs:
+        if "sub" in arcs:
+            a0[p2, q2] = 5e-320
         tagged += [np.tile([p2, q2], 30)] * 20
     a0 /= a0.sum(axis=1, keepdims=True)
     free = [rng.integers(0, n, size=int(rng.integers(5, 40))) for _ in range(30)]
@@ -55,6 +57,8 @@ for n in (20, 100, 300):
         print(f"N={n} iters={iters} tiny normal:     {case(n, ('normal',), iters)}", flush=True)
         print(f"N={n} iters={iters} tiny sub:        {case(n, ('sub',), iters)}", flush=True)
         print(f"N={n} iters={iters} none:            {case(n, (), iters)}", flush=True)
+        print(f"N={n} iters={iters} tags, no tiny:   {case(n, ('tags',), iters)}", flush=True)
         os.environ["CV_BW_GEMM_PATH"] = "1"
         print(f"N={n} iters={iters} none, GEMM path: {case(n, (), iters)}", flush=True)
+        print(f"N={n} iters={iters} tags, GEMM path: {case(n, ('tags',), iters)}", flush=True)
         del os.environ["CV_BW_GEMM_PATH"]
