@@ -4007,7 +4007,7 @@ cv_status fit_validate(int32_t N, int64_t V, int64_t nseq, const int64_t* offset
 
 struct FitDev {
   DevBuf off, obs, tags, pi, a, at, et, alpha, beta, rscale, acc, cnt, ord, dump, gscratch;
-  DevBuf rowsc, xs2, flag;  // tiny arcs: per-row scales, the row-scaled xi sum, the any-row flag
+  DevBuf amin, a2, at2;  // tiny arcs: A's smallest positive entry, A 2^K and A^T 2^K
 };
 
 }  // namespace
@@ -4233,28 +4233,37 @@ CV_API cv_status cv_hmm_fit_train(int32_t nstates, int64_t nobs, int64_t nseq, c
     for (auto& x : ps.ev)
       if (hipEventCreateWithFlags(&x, hipEventDisableTiming) != hipSuccess) return set_err(CV_EDEVICE, "hipEventCreate failed");
   }
-  // Rows of A with an arc below cvf::kBwTinyArc (checked on the device before every E-step):
-  // their factored xi sums can overflow, so the E-step then also accumulates a row-scaled copy
-  // (BwArgs::rowscale / xi_s2) and the M-step takes those arcs' counts from it
-  if ((st = d.rowsc.ensure((size_t)N * 8)) != CV_OK) return st;
-  if ((st = d.flag.ensure(8)) != CV_OK) return st;
-  unsigned tiny = 0;
+  // Arcs below cvf::kBwTinyArc (A's smallest positive entry, checked on the device before every
+  // E-step): the E-step then runs on A 2^K and A^T 2^K, K the least that lifts every arc to
+  // kBwTinyArc -- its factored xi sums stay in range and no step normaliser c_t is subnormal;
+  // every normalised vector is the same (the scaling is exact), and the M-step multiplies the
+  // counts back by a 2^K (MstepArgs::ascale).  A model without such arcs runs unscaled.
+  if ((st = d.amin.ensure(8)) != CV_OK) return st;
+  static const unsigned long long kInfBits = 0x7FF0000000000000ull;
+  double ascale = 0.0;
   auto scan_tiny = [&]() -> cv_status {
-    HIP_TRY(hipMemsetAsync(d.flag.p, 0, 4, nullptr));
-    const hipError_t e = cvf::launch_bw_rowscale(d.a.as<double>(), N, d.rowsc.as<double>(), d.flag.as<unsigned>(), nullptr);
-    if (e != hipSuccess) return set_err(CV_EDEVICE, "row-scale launch failed: %s", hipGetErrorString(e));
+    HIP_TRY(hipMemcpyAsync(d.amin.p, &kInfBits, 8, hipMemcpyHostToDevice, nullptr));
+    const hipError_t e = cvf::launch_bw_amin(d.a.as<double>(), (int64_t)N * N, d.amin.as<unsigned long long>(), nullptr);
+    if (e != hipSuccess) return set_err(CV_EDEVICE, "arc scan launch failed: %s", hipGetErrorString(e));
     return CV_OK;
   };
-  if ((st = scan_tiny()) != CV_OK) return st;
-  HIP_TRY(hipMemcpy(&tiny, d.flag.p, 4, hipMemcpyDeviceToHost));
+  auto read_tiny = [&]() -> cv_status {
+    double amin = 0.0;
+    HIP_TRY(hipMemcpy(&amin, d.amin.p, 8, hipMemcpyDeviceToHost));
+    ascale = 0.0;
+    if (amin < cvf::kBwTinyArc) ascale = std::ldexp(1.0, std::ilogb(cvf::kBwTinyArc) - std::ilogb(amin));
+    return CV_OK;
+  };
+  if ((st = scan_tiny()) != CV_OK || (st = read_tiny()) != CV_OK) return st;
   int32_t it = 0;
   for (it = 1; it <= max_iter; ++it) {
     HIP_TRY(hipMemsetAsync(d.acc.p, 0, nacc * 8, nullptr));
-    if (tiny) {
-      // the GEMM path at any N: beta rows (U) for the one-wave sizes too, and the scaled sum
-      if (!d.beta.p && (st = d.beta.ensure((size_t)max_chunk * N * 8)) != CV_OK) return st;
-      if ((st = d.xs2.ensure((size_t)N * N * 8)) != CV_OK) return st;
-      HIP_TRY(hipMemsetAsync(d.xs2.p, 0, (size_t)N * N * 8, nullptr));
+    if (ascale != 0.0) {  // this E-step's A 2^K and A^T 2^K
+      if ((st = d.a2.ensure((size_t)N * N * 8)) != CV_OK || (st = d.at2.ensure((size_t)N * N * 8)) != CV_OK) return st;
+      hipError_t e = cvf::launch_bw_scale(d.a.as<double>(), d.a2.as<double>(), (int64_t)N * N, ascale, nullptr);
+      if (e == hipSuccess)
+        e = cvf::launch_bw_scale(d.at.as<double>(), d.at2.as<double>(), (int64_t)N * N, ascale, nullptr);
+      if (e != hipSuccess) return set_err(CV_EDEVICE, "arc scaling launch failed: %s", hipGetErrorString(e));
     }
     double* A = d.acc.as<double>();
     for (size_t ci = 0; ci < chunks.size(); ++ci)
@@ -4283,8 +4292,8 @@ CV_API cv_status cv_hmm_fit_train(int32_t nstates, int64_t nobs, int64_t nseq, c
       g.gscratch = bw_global ? d.gscratch.as<double>() : nullptr;
       g.nstates = N;
       g.pi = d.pi.as<double>();
-      g.a = d.a.as<double>();
-      g.at = d.at.as<double>();
+      g.a = ascale != 0.0 ? d.a2.as<double>() : d.a.as<double>();
+      g.at = ascale != 0.0 ? d.at2.as<double>() : d.at.as<double>();
       g.et = d.et.as<double>();
       g.alpha = d.alpha.as<double>() + (size_t)row0 * N;
       g.beta = d.beta.p ? d.beta.as<double>() + (size_t)row0 * N : nullptr;
@@ -4295,8 +4304,6 @@ CV_API cv_status cv_hmm_fit_train(int32_t nstates, int64_t nobs, int64_t nseq, c
       g.b_num = A + 3 * N;
       g.xi_s = g.b_num + (size_t)V * N;
       g.xi_zero = g.xi_s + (size_t)N * N;
-      g.rowscale = tiny ? d.rowsc.as<double>() : nullptr;
-      g.xi_s2 = tiny ? d.xs2.as<double>() : nullptr;
       const hipError_t e = cvf::launch_bw_estep(g, c.second - c.first, max_waves, ss, off0[c.second] - off0[c.first],
                                                 pipe > 1 ? ps.ev[pi_] : nullptr);
       if (e != hipSuccess) return set_err(CV_EDEVICE, "Baum-Welch launch failed: %s", hipGetErrorString(e));
@@ -4309,13 +4316,12 @@ CV_API cv_status cv_hmm_fit_train(int32_t nstates, int64_t nobs, int64_t nseq, c
     // M-step (hmm.rs:145-170) on the device: new_pi = sum gamma_0 / R; new_a = sum xi / a_den
     // (row); new_b = sum gamma at o / b_den; sum_t xi_t = A o S + z / N^2 (see bw_stats);
     // d = sum |new - old| (hmm.rs:172-175) as per-block parts added here in a fixed order
-    m.rowscale = tiny ? d.rowsc.as<double>() : nullptr;
-    m.xs2 = tiny ? d.xs2.as<double>() : nullptr;
+    m.ascale = ascale;
     const hipError_t e = cvf::launch_bw_mstep(m, kPartsB, nullptr);
     if (e != hipSuccess) return set_err(CV_EDEVICE, "M-step launch failed: %s", hipGetErrorString(e));
-    if ((st = scan_tiny()) != CV_OK) return st;  // the new A's rows, for the next E-step
+    if ((st = scan_tiny()) != CV_OK) return st;  // the new A, for the next E-step
     HIP_TRY(hipMemcpy(part.data(), d.cnt.p, part.size() * 8, hipMemcpyDeviceToHost));
-    HIP_TRY(hipMemcpy(&tiny, d.flag.p, 4, hipMemcpyDeviceToHost));
+    if ((st = read_tiny()) != CV_OK) return st;
     double dsum = 0.0;
     for (double x : part) dsum += x;
     if (dsum <= tol) break;

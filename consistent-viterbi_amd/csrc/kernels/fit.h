@@ -53,16 +53,11 @@ struct BwArgs {
   double* b_num;        // [V][N] sum of gamma_t at o_t
   double* xi_s;         // [N][N] sum of (alpha_t / c_t) (x) u_{t+1}
   double* xi_zero;      // [1] number of steps with c_t == 0 (uniform xi)
-  // rows of A with an entry below kBwTinyArc (bw_rowscale): rowscale[i] = a power of two <= the
-  // row's smallest nonzero entry (0 for the other rows); non-null: the E-step runs the xi GEMM
-  // path at every N and a second GEMM pass accumulates sum_t (rowscale[i] r_t[i]) u_{t+1}[j]
-  // into xi_s2, which stays inside the f64 range where xi_s overflows
-  const double* rowscale;
-  double* xi_s2;        // [N][N]
 };
 
-// an arc below this (2^-960) can make the factored xi sum of its entry overflow once its
-// per-step counts (each <= 1) summed over the corpus pass ~2^63 * a (never for a larger arc)
+// An arc below this (2^-960) can make the factored xi sum of its entry overflow (its per-step
+// terms are ~xi / a) and, when subnormal, leaves the step normaliser c_t = fl(a u) with a few
+// significant bits; cv_hmm_fit_train then runs the E-step on A 2^K (MstepArgs::ascale)
 constexpr double kBwTinyArc = 0x1p-960;
 
 constexpr int kBwWaveStates = 64;  // N <= 64: one wave per sequence (bw_*_wave)
@@ -80,8 +75,7 @@ struct MstepArgs {
   double* et;    // [V][N]  b^T, updated in place
   double* part;  // [parts_a + nparts_b] per-block sums of |new - old|
   int parts_a;   // blocks of the pi / a M-step (1; 1,024 above kBwLdsMaxStates: N^2 entries)
-  const double* rowscale;  // BwArgs::rowscale of the E-step just run, or null
-  const double* xs2;       // BwArgs::xi_s2 of that E-step (with rowscale)
+  double ascale;  // the E-step ran on A 2^K (tiny arcs): count = (a ascale) S; 0: unscaled
 };
 
 hipError_t launch_mle_counts(const MleArgs& g, int64_t nseq, hipStream_t stream);
@@ -96,8 +90,10 @@ hipError_t launch_bw_estep(const BwArgs& g, int64_t nseq, int64_t max_waves, hip
 bool bw_estep_mm(int nstates);
 // CV_BW_GEMM_PATH=1: the per-sequence kernels + xi GEMM at every N (what tiny arcs select)
 bool bw_gemm_path();
-// rowscale[i] for A's rows (BwArgs::rowscale); *flag |= 1 when some row has a tiny arc
-hipError_t launch_bw_rowscale(const double* a, int nstates, double* rowscale, unsigned* flag, hipStream_t stream);
+// *out = the bits of the smallest positive a[k], k < n (*out preset to +inf's bits by the caller)
+hipError_t launch_bw_amin(const double* a, int64_t n, unsigned long long* out, hipStream_t stream);
+// dst[k] = src[k] * scale (a power of two: exact), k < n
+hipError_t launch_bw_scale(const double* src, double* dst, int64_t n, double scale, hipStream_t stream);
 hipError_t launch_bw_mstep(const MstepArgs& m, int nparts_b, hipStream_t stream);
 
 }  // namespace cvf

@@ -477,17 +477,6 @@ __global__ __launch_bounds__(64, 2) void bw_xi_gemm(BwArgs g, int64_t nrows, int
     cm[q] = min(cm[q], N - 1);
     cn[q] = min(cn[q], N - 1);
   }
-  // the row-scaled second pass (g.rowscale): R's column m times rowscale[m]; tiles without a
-  // scaled row have nothing to add (wave-uniform exit)
-  double csc[TM];
-#pragma unroll
-  for (int q = 0; q < TM; ++q) csc[q] = g.rowscale ? g.rowscale[cm[q]] : 1.0;
-  if (g.rowscale) {
-    bool any = false;
-#pragma unroll
-    for (int q = 0; q < TM; ++q) any |= vm[q] && csc[q] != 0.0;
-    if (__ballot(any) == 0) return;
-  }
   // per 4 rows: TM loads of R and of U (lane l: row r + l/16, column l%16 of each 16-wide
   // tile), masked loads (a select on a loaded value cost ~30% here); ST = 2 issues the next 4
   // rows' loads before the current rows' MFMAs
@@ -505,7 +494,7 @@ __global__ __launch_bounds__(64, 2) void bw_xi_gemm(BwArgs g, int64_t nrows, int
     const double* U_ = g.beta + (size_t)(vr_ ? row_ : r0) * N;               \
     const double rs_ = g.rscale ? g.rscale[vr_ ? row_ : r0] : 1.0;           \
     _Pragma("unroll") for (int q = 0; q < TM; ++q) {                         \
-      AV[q] = (vr_ && vm[q]) ? (R_[cm[q]] * rs_) * csc[q] : 0.0;             \
+      AV[q] = (vr_ && vm[q]) ? R_[cm[q]] * rs_ : 0.0;                        \
       BV[q] = (vr_ && vn[q]) ? U_[cn[q]] : 0.0;                              \
     }                                                                        \
   }
@@ -557,17 +546,11 @@ __global__ __launch_bounds__(256, 2) void bw_xi_gemm_lds(BwArgs g, int64_t nrows
   const int64_t r1 = r0 + rows_per_wg < nrows ? r0 + rows_per_wg : nrows;
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, kk = l >> 4, cl = l & 15;
   const int wm = w >> 1, wn = w & 1;
-  // the row-scaled second pass (g.rowscale): R's column m times rowscale[m]; a tile without a
-  // scaled row has nothing to add (workgroup-uniform exit, before any other barrier)
-  if (g.rowscale && !__syncthreads_or(tid < TS && m0 + tid < N && g.rowscale[m0 + tid] != 0.0)) return;
   // staging: thread tid copies row (tid >> 4) of R and U, 8 doubles from column 8 (tid & 15);
   // A/B: 16-byte loads of strided column pairs with forced selects (2-way LDS write conflicts)
   // 98 vs 79 ms, 8-byte strided loads 109 ms
   const int srow = tid >> 4, scol = 8 * (tid & 15);
   double rsc = 1.0;  // the staged row's R scale
-  double csc[8];     // the staged columns' row scales (second pass), else 1
-#pragma unroll
-  for (int q = 0; q < 8; ++q) csc[q] = g.rowscale ? g.rowscale[min(m0 + scol + q, N - 1)] : 1.0;
   auto stage_load = [&](int64_t rb, double (&ra)[8], double (&ua)[8]) {
     const int64_t row = rb + srow;
     const bool vr = row < r1;
@@ -584,7 +567,7 @@ __global__ __launch_bounds__(256, 2) void bw_xi_gemm_lds(BwArgs g, int64_t nrows
   auto stage_store = [&](int buf, const double (&ra)[8], const double (&ua)[8]) {
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
-      rs[buf][srow * LS + scol + q] = (ra[q] * rsc) * csc[q];
+      rs[buf][srow * LS + scol + q] = ra[q] * rsc;
       us[buf][srow * LS + scol + q] = ua[q];
     }
   };
@@ -1481,35 +1464,33 @@ __global__ __launch_bounds__(64 * WV, (MT == 4 ? 1 : 2) * WV / 4) void bw_bwd_mm
   }
 }
 
-// ---- rows of A with a tiny arc (BwArgs::rowscale) ----------------------------------------------
-// rowscale[i] = 2^ilogb(min nonzero a[i][j]) when that minimum is below kBwTinyArc (an exact
-// power of two <= every nonzero entry of the row, subnormal allowed), else 0.
-__global__ __launch_bounds__(256) void bw_rowscale(const double* __restrict__ a, int N, double* rowscale,
-                                                   unsigned* flag) {
-  __shared__ double red[4];
-  const int64_t i = blockIdx.x;
+// ---- tiny arcs (cv_hmm_fit_train runs the E-step on A 2^K while A has one) --------------------
+// the bits of the smallest positive entry (positive doubles order like their bit patterns)
+__global__ __launch_bounds__(256) void bw_amin(const double* __restrict__ a, int64_t n, unsigned long long* out) {
   double mn = __builtin_inf();
-  for (int j = threadIdx.x; j < N; j += 256) {
-    const double v = a[i * N + j];
+  for (int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x; k < n; k += (int64_t)gridDim.x * 256) {
+    const double v = a[k];
     mn = v > 0.0 ? fmin(mn, v) : mn;
   }
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) mn = fmin(mn, __shfl_xor(mn, off));
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mn;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const double m = fmin(fmin(red[0], red[1]), fmin(red[2], red[3]));
-    double sc = 0.0;
-    if (m < kBwTinyArc) {
-      sc = ldexp(1.0, ilogb(m));
-      atomicOr(flag, 1u);
-    }
-    rowscale[i] = sc;
-  }
+  if ((threadIdx.x & 63) == 0 && mn < __builtin_inf()) atomicMin(out, (unsigned long long)__double_as_longlong(mn));
 }
 
-hipError_t launch_bw_rowscale(const double* a, int nstates, double* rowscale, unsigned* flag, hipStream_t stream) {
-  hipLaunchKernelGGL(bw_rowscale, dim3((unsigned)nstates), dim3(256), 0, stream, a, nstates, rowscale, flag);
+__global__ __launch_bounds__(256) void bw_scale(const double* __restrict__ src, double* __restrict__ dst, int64_t n,
+                                                double scale) {
+  for (int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x; k < n; k += (int64_t)gridDim.x * 256) dst[k] = src[k] * scale;
+}
+
+hipError_t launch_bw_amin(const double* a, int64_t n, unsigned long long* out, hipStream_t stream) {
+  const unsigned blocks = (unsigned)std::max<int64_t>(1, std::min<int64_t>(2048, (n + 255) / 256));
+  hipLaunchKernelGGL(bw_amin, dim3(blocks), dim3(256), 0, stream, a, n, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_bw_scale(const double* src, double* dst, int64_t n, double scale, hipStream_t stream) {
+  const unsigned blocks = (unsigned)std::max<int64_t>(1, std::min<int64_t>(2048, (n + 255) / 256));
+  hipLaunchKernelGGL(bw_scale, dim3(blocks), dim3(256), 0, stream, src, dst, n, scale);
   return hipGetLastError();
 }
 
@@ -1550,15 +1531,11 @@ __global__ __launch_bounds__(256) void bw_mstep_pa(MstepArgs m) {
     // The factored sum S = sum_t alpha_t u_t+1 / c_t can exceed DBL_MAX exactly where A is 0
     // or subnormal (each xi_t entry A alpha u / c is <= 1, hmm.rs:135-141, so alpha u / c <=
     // 1 / A): a == 0 takes no term (the reference's entries are 0 there; 0 * inf would be NaN),
-    // and S is clamped to DBL_MAX (finite for a subnormal a; never reached for a normal one
-    // unless ~1/a summed over steps overflows)
-    // ... unless the row was rescaled (m.rowscale): a tiny arc's count then comes from the
-    // second pass's sum S' = rowscale[i] S, which stays in range: (a / rowscale[i]) S'
-    const double rsc = m.rowscale ? m.rowscale[i] : 0.0;
-    const double cnt = (m.xs2 && rsc > 0.0 && m.a[k] != 0.0 && m.a[k] < kBwTinyArc)
-                           ? (m.a[k] / rsc) * m.xs2[k]
-                           : (m.a[k] != 0.0 ? m.a[k] * fmin(xs[k], 1.7976931348623157e308) : 0.0);
-    const double na = (cnt + zu) / a_den[i];
+    // and S is clamped to DBL_MAX as a last guard.  While A has an arc below kBwTinyArc the
+    // E-step runs on A 2^K (m.ascale = 2^K, every arc >= kBwTinyArc there), which leaves
+    // S' = S / 2^K in range, so the count is (a 2^K) S' -- exact scalings of the same products
+    const double ak = m.ascale != 0.0 ? m.a[k] * m.ascale : m.a[k];
+    const double na = ((m.a[k] != 0.0 ? ak * fmin(xs[k], 1.7976931348623157e308) : 0.0) + zu) / a_den[i];
     d += fabs(na - m.a[k]);
     m.a[k] = na;
     m.at[(size_t)j * N + i] = na;
@@ -1699,21 +1676,12 @@ hipError_t launch_bw_estep(const BwArgs& g, int64_t nseq, int64_t max_waves, hip
     const int64_t parts2 = std::max<int64_t>(1, std::min<int64_t>(512 / (nt * nt), (nrows + 255) / 256));
     const int64_t per2 = ((nrows + parts2 - 1) / parts2 + kGemmKB - 1) / kGemmKB * kGemmKB;
     const int64_t np2 = (nrows + per2 - 1) / per2;
-    BwArgs g0 = g;
-    g0.rowscale = nullptr;  // the plain sum first
-    hipLaunchKernelGGL(bw_xi_gemm_lds, dim3((unsigned)((np2 + 7) / 8 * 8 * nt * nt)), dim3(256), 0, stream, g0, nrows,
+    hipLaunchKernelGGL(bw_xi_gemm_lds, dim3((unsigned)((np2 + 7) / 8 * 8 * nt * nt)), dim3(256), 0, stream, g, nrows,
                        per2);
-    if (g.rowscale) {  // the row-scaled second pass (tiny arcs) into xi_s2
-      BwArgs gs = g;
-      gs.xi_s = g.xi_s2;
-      hipLaunchKernelGGL(bw_xi_gemm_lds, dim3((unsigned)((np2 + 7) / 8 * 8 * nt * nt)), dim3(256), 0, stream, gs,
-                         nrows, per2);
-    }
     return hipGetLastError();
   }
   const bool mm = bw_estep_mm(g.nstates);
-  // tiny arcs (g.rowscale): the GEMM path at any N, so the row-scaled second pass has rows to read
-  if (g.nstates > kBwLdsStates || mm || g.rowscale || bw_gemm_path()) {  // the xi sum as R^T U on the matrix cores
+  if (g.nstates > kBwLdsStates || mm || bw_gemm_path()) {  // the xi sum as R^T U on the matrix cores
     BwArgs gg = g;
     if (!mm) gg.rscale = nullptr;  // the per-sequence kernels store R over alpha
     if (mm) {  // 16 MT sequences per workgroup, the step products on the matrix cores
@@ -1737,11 +1705,6 @@ hipError_t launch_bw_estep(const BwArgs& g, int64_t nseq, int64_t max_waves, hip
       hipLaunchKernelGGL(bw_backward, dim3((unsigned)nseq), dim3(256), 0, stream, g);
       hipLaunchKernelGGL(bw_stats_rows, dim3((unsigned)nseq), dim3(256), 0, stream, g);
     }
-    // the GEMM, then (tiny arcs) its row-scaled second pass into xi_s2
-    for (int pass = 0; pass < (g.rowscale ? 2 : 1); ++pass) {
-    if (pass == 1) gg.xi_s = g.xi_s2;
-    else gg.rowscale = nullptr;
-    if (pass == 1) gg.rowscale = g.rowscale;
     // 64 x 64 tiles per wave above 128 states (32 x 32 below); ~4,096 waves: row ranges of a
     // multiple of 4 rows per output tile
     const bool t64 = g.nstates > 128 && !gemm32();
@@ -1765,7 +1728,6 @@ hipError_t launch_bw_estep(const BwArgs& g, int64_t nseq, int64_t max_waves, hip
       hipLaunchKernelGGL((bw_xi_gemm<4, 1>), grid, block, 0, stream, gg, nrows, per);
     else
       hipLaunchKernelGGL((bw_xi_gemm<2, 1>), grid, block, 0, stream, gg, nrows, per);
-    }
     return hipGetLastError();
   }
   if (g.nstates <= kBwWaveStates) {

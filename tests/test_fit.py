@@ -257,8 +257,9 @@ def test_gpu_train_tiny_arcs_forced(gpu, n):
     """Arcs far below DBL_MIN's square root that tags force through: a 1e-306 arc
     p -> q and a subnormal 5e-320 arc p2 -> q2, each taken ~1,200 times by fully tagged
     sequences, so every step's xi is one-hot there and the factored sum sum_t r_t u_{t+1}
-    (~1 / a per step) leaves the f64 range.  The row-scaled second xi pass keeps those counts
-    exact: two EM iterations against the oracle (per-entry xi, hmm.rs:133-143)."""
+    (~1 / a per step) leaves the f64 range, and the subnormal arc's step normaliser c_t = fl(a u)
+    keeps ~13 bits.  The E-step on A 2^K keeps those counts exact: two EM iterations against
+    the oracle (per-entry xi, hmm.rs:133-143)."""
     import cviterbi as cv
 
     v = 23
