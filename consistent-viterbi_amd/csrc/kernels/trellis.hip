@@ -1428,8 +1428,12 @@ __global__ __launch_bounds__(1024) void generic_fwd_ms(GenericFwdArgs<REAL> args
   const int assoc = args.assoc;
   const REAL ninf = -__builtin_inf();
   // candidate loops unrolled for one- and two-sequence workgroups in psi mode only (see
-  // CVK_GEN_UNROLL): a rolled walk waits out one L2 latency per candidate
-  constexpr int kCandUnroll = (S <= 2 && !ROWS) ? CVK_GEN_UNROLL : 1;
+  // CVK_GEN_UNROLL): a rolled walk waits out one L2 latency per candidate.  A/B builds:
+  // -DCVK_GEN_UNROLL_S=4 unrolls the four-sequence psi walk too
+#ifndef CVK_GEN_UNROLL_S
+#define CVK_GEN_UNROLL_S 2
+#endif
+  constexpr int kCandUnroll = (S <= CVK_GEN_UNROLL_S && !ROWS) ? CVK_GEN_UNROLL : 1;
   int64_t e0[S], slot[S], seq[S];
   int T[S];
   int Tmax = 0;
