@@ -1427,11 +1427,12 @@ __global__ __launch_bounds__(1024) void generic_fwd_ms(GenericFwdArgs<REAL> args
   const int V = args.nobs;
   const int assoc = args.assoc;
   const REAL ninf = -__builtin_inf();
-  // candidate loops unrolled for one- and two-sequence workgroups in psi mode only (see
-  // CVK_GEN_UNROLL): a rolled walk waits out one L2 latency per candidate.  A/B builds:
-  // -DCVK_GEN_UNROLL_S=4 unrolls the four-sequence psi walk too
+  // candidate loops unrolled in psi mode only (see CVK_GEN_UNROLL): a rolled walk waits out one
+  // L2 latency per candidate.  Four-sequence workgroups too since round 5: psi CP at N = 300,
+  // 8,192 x 128, forward 28.6 -> 25.5 ms; the chain's speculative batch at S = 4 21.0 -> 12.1
+  // ms (profiles/r05_ab_unroll_s4.txt).  A/B builds: -DCVK_GEN_UNROLL_S=2 (or 1)
 #ifndef CVK_GEN_UNROLL_S
-#define CVK_GEN_UNROLL_S 2
+#define CVK_GEN_UNROLL_S 4
 #endif
   constexpr int kCandUnroll = (S <= CVK_GEN_UNROLL_S && !ROWS) ? CVK_GEN_UNROLL : 1;
   int64_t e0[S], slot[S], seq[S];
