@@ -286,8 +286,6 @@ struct cv_hmm {
   hipStream_t copy_stream = nullptr;
   hipEvent_t paths_ev = nullptr;
   PinnedHost chain_pin;  // the chain's scores, statuses and certificates on their way to the host
-  PinnedHost copy_pin;   // two 16 MiB chunks of the chain's paths on their way to the host
-  hipEvent_t copy_ev[2] = {nullptr, nullptr};
 
   ~cv_hmm() {
     for (auto e : ev) (void)hipEventDestroy(e);
@@ -303,8 +301,6 @@ struct cv_hmm {
     if (stream) (void)hipStreamDestroy(stream);
     if (bt_stream) (void)hipStreamDestroy(bt_stream);
     if (copy_stream) (void)hipStreamDestroy(copy_stream);
-    for (auto e : copy_ev)
-      if (e) (void)hipEventDestroy(e);
     if (paths_ev) (void)hipEventDestroy(paths_ev);
   }
 };
@@ -3071,47 +3067,6 @@ cv_status superseq_cp_wg(cv_hmm* h, int64_t L, const int32_t* obs, const std::ve
 // Knobs (bit-identical): CV_CHAIN_PAR=0 (serial chain), CV_CHAIN_PAR_FORCE=m (every m-th
 // non-empty sequence taken as uncertified: exercises speculation and the runs), CV_CHAIN_SPEC=0
 // (no speculation: every uncertified sequence through the serial chain kernel).
-// Device -> pageable host copy of `bytes` on h->copy_stream (behind whatever it waits for)
-// through two pinned 16 MiB chunks: each chunk's DMA runs while the host threads move the
-// previous one into `dst`.  The runtime's own pageable copy of the config-4-sized paths (134 MB)
-// ran at ~12 GB/s, its last staging chunks 2 ms apart (profiles/r05_chain_api_timeline.txt).
-// Returns with the copy complete (false: no pinned memory -- the caller copies as before).
-bool d2h_pinned_chunks(cv_hmm* h, void* dst, const void* src, size_t bytes) {
-  constexpr size_t kCh = (size_t)16 << 20;
-  if (!h->copy_pin.ensure(2 * kCh)) return false;
-  for (auto& e : h->copy_ev)
-    if (!e && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
-      (void)hipGetLastError();
-      return false;
-    }
-  unsigned char* pin = h->copy_pin.as<unsigned char>();
-  const size_t n = (bytes + kCh - 1) / kCh;
-  auto enqueue = [&](size_t i) {
-    const size_t off = i * kCh, sz = std::min(kCh, bytes - off);
-    return hipMemcpyAsync(pin + (i & 1) * kCh, static_cast<const unsigned char*>(src) + off, sz, hipMemcpyDeviceToHost,
-                          h->copy_stream) == hipSuccess &&
-           hipEventRecord(h->copy_ev[i & 1], h->copy_stream) == hipSuccess;
-  };
-  bool ok = n == 0 || enqueue(0);
-  for (size_t i = 0; ok && i < n; ++i) {
-    if (i + 1 < n) ok = enqueue(i + 1);  // its buffer's previous chunk (i - 1) is already out
-    if (!ok || hipEventSynchronize(h->copy_ev[i & 1]) != hipSuccess) {
-      ok = false;
-      break;
-    }
-    const size_t off = i * kCh, sz = std::min(kCh, bytes - off);
-    const unsigned char* from = pin + (i & 1) * kCh;
-    unsigned char* to = static_cast<unsigned char*>(dst) + off;
-    parallel_ranges((int64_t)sz, [&](int, int64_t a, int64_t b) { std::memcpy(to + a, from + a, (size_t)(b - a)); },
-                    (int64_t)1 << 20);
-  }
-  if (!ok) {
-    (void)hipStreamSynchronize(h->copy_stream);
-    (void)hipGetLastError();
-  }
-  return ok;
-}
-
 cv_status superseq_cp_par(cv_hmm* h, int64_t nseq, const int64_t* offsets, const int32_t* obs, int32_t* path_out,
                           double* objective_out, bool* applied) {
   *applied = false;
@@ -3185,13 +3140,8 @@ cv_status superseq_cp_par(cv_hmm* h, int64_t nseq, const int64_t* offsets, const
   } copy_join{h->copy_stream, false};
   if (paths_rec) {
     HIP_TRY(hipStreamWaitEvent(h->copy_stream, h->paths_ev, 0));
-    // through pinned chunks while the certificate pass runs (CV_CHAIN_PIN_COPY=0: the
-    // runtime's pageable copy, A/B knob)
-    const char* pc = getenv("CV_CHAIN_PIN_COPY");
-    if ((pc && *pc == '0') || !d2h_pinned_chunks(h, path_out, d_path.p, (size_t)L * 4)) {
-      HIP_TRY(hipMemcpyAsync(path_out, d_path.p, (size_t)L * 4, hipMemcpyDeviceToHost, h->copy_stream));
-      copy_join.on = true;
-    }
+    HIP_TRY(hipMemcpyAsync(path_out, d_path.p, (size_t)L * 4, hipMemcpyDeviceToHost, h->copy_stream));
+    copy_join.on = true;
   } else {
     HIP_TRY(hipMemcpyAsync(path_out, d_path.p, (size_t)L * 4, hipMemcpyDeviceToHost, stream));
   }

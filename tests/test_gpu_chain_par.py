@@ -297,12 +297,10 @@ def test_chain_par_wide_speculation(gpu, monkeypatch, n):
     assert obj == robj and np.array_equal(path, rp), st
 
 
-@pytest.mark.parametrize("n,nseq", [(256, 2048), (256, 20000), (300, 120)])
+@pytest.mark.parametrize("n,nseq", [(256, 2048), (300, 120)])
 def test_chain_par_copy_overlap_knob(gpu, monkeypatch, n, nseq):
     """The paths' host copy runs on its own stream behind the last backtrack, beside the
-    certificate pass, through two pinned 16 MiB chunks (default; 2,048 x 512 at N = 256 is one
-    partial chunk, 20,000 x 512 three, the last partial) or the runtime's pageable copy
-    (CV_CHAIN_PIN_COPY=0); CV_CHAIN_COPY_OVERLAP=0 copies after the certificates on the
+    certificate pass (default); CV_CHAIN_COPY_OVERLAP=0 copies after the certificates on the
     decode's stream.  Both return the same paths and objective (f64 trellis at N = 256, the
     generic rows mode's plain-row certificates at N = 300)."""
     if n == 256:
@@ -313,10 +311,6 @@ def test_chain_par_copy_overlap_knob(gpu, monkeypatch, n, nseq):
     h = cv.HMM(pi, a, b)
     (path, obj), st = _par(h, off, obs)
     assert st["parallel"], st
-    monkeypatch.setenv("CV_CHAIN_PIN_COPY", "0")  # the runtime's pageable copy on that stream
-    (pp, op), stp = _par(h, off, obs)
-    assert stp["parallel"], stp
-    assert obj == op and np.array_equal(path, pp)
     monkeypatch.setenv("CV_CHAIN_COPY_OVERLAP", "0")
     (p0, o0), st0 = _par(h, off, obs)
     assert st0["parallel"], st0
