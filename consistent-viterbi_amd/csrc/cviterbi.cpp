@@ -279,9 +279,8 @@ struct cv_hmm {
   // the parallel chain's per-call device arrays, kept between calls (grow-only): a
   // config-4-sized call allocated and freed ~0.4 GB of them each time (hipFree synchronises)
   struct ChainBufs {
-    DevBuf off, obs, path, res, cert, ebin, q, path8;
+    DevBuf off, obs, path, res, cert, ebin, q;
   } chainb;
-  PinnedHost path_pin;  // the chain's u8 paths on their way to the host (N <= 256)
   // the parallel chain's path copy: on its own stream, behind the last backtrack (paths_ev),
   // beside the certificate pass
   hipStream_t copy_stream = nullptr;
@@ -3150,31 +3149,8 @@ cv_status superseq_cp_par(cv_hmm* h, int64_t nseq, const int64_t* offsets, const
         std::memset(reinterpret_cast<unsigned char*>(path_out) + a, 0, (size_t)(b - a));
       }, (int64_t)1 << 22);
     HIP_TRY(hipStreamWaitEvent(h->copy_stream, h->paths_ev, 0));
-    // N <= 256: the states cross PCIe as bytes (narrowed on the device, widened by the host
-    // threads into the prefaulted output) -- a quarter of the DMA, which ran at ~12 GB/s and
-    // ended ~6 ms after the certificate pass (profiles/r05_chain_api_timeline.txt); A/B knob
-    // CV_CHAIN_U8=0
-    const char* u8e = getenv("CV_CHAIN_U8");
-    bool u8 = W <= 256 && !(u8e && *u8e == '0');
-    if (u8 && (h->chainb.path8.ensure((size_t)L) != CV_OK || !h->path_pin.ensure((size_t)L))) {
-      u8 = false;
-      g_err.clear();
-    }
-    if (u8) {
-      const hipError_t e = cvk::launch_narrow_u8(d_path.as<int32_t>(), h->chainb.path8.as<uint8_t>(), L, h->copy_stream);
-      if (e != hipSuccess) return set_err(CV_EDEVICE, "path narrowing failed: %s", hipGetErrorString(e));
-      HIP_TRY(hipMemcpyAsync(h->path_pin.p, h->chainb.path8.p, (size_t)L, hipMemcpyDeviceToHost, h->copy_stream));
-      copy_join.on = true;
-      HIP_TRY(hipStreamSynchronize(h->copy_stream));
-      copy_join.on = false;
-      const uint8_t* p8 = h->path_pin.as<uint8_t>();
-      parallel_ranges(L, [&](int, int64_t a, int64_t b) {
-        for (int64_t k = a; k < b; ++k) path_out[k] = p8[k];
-      }, (int64_t)1 << 20);
-    } else {
-      HIP_TRY(hipMemcpyAsync(path_out, d_path.p, (size_t)L * 4, hipMemcpyDeviceToHost, h->copy_stream));
-      copy_join.on = true;
-    }
+    HIP_TRY(hipMemcpyAsync(path_out, d_path.p, (size_t)L * 4, hipMemcpyDeviceToHost, h->copy_stream));
+    copy_join.on = true;
   } else {
     HIP_TRY(hipMemcpyAsync(path_out, d_path.p, (size_t)L * 4, hipMemcpyDeviceToHost, stream));
   }

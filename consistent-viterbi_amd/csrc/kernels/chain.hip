@@ -531,28 +531,6 @@ hipError_t launch_cp_cert_plain(const CpCert64Args& a, hipStream_t stream) {
   return hipGetLastError();
 }
 
-// states < 256 as bytes: the parallel chain's paths cross PCIe as u8 (a quarter of the bytes)
-__global__ __launch_bounds__(256) void narrow_u8(const int32_t* __restrict__ src, uint8_t* __restrict__ dst, int64_t n) {
-  const int64_t k0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
-  for (int64_t k = k0; k < n; k += (int64_t)gridDim.x * 1024) {
-    if (k + 4 <= n) {
-      const int4 v = *reinterpret_cast<const int4*>(src + k);
-      const uint32_t w = (uint32_t)(v.x & 255) | (uint32_t)(v.y & 255) << 8 | (uint32_t)(v.z & 255) << 16 |
-                         (uint32_t)(v.w & 255) << 24;
-      *reinterpret_cast<uint32_t*>(dst + k) = w;
-    } else {
-      for (int64_t q = k; q < n; ++q) dst[q] = (uint8_t)src[q];
-    }
-  }
-}
-
-hipError_t launch_narrow_u8(const int32_t* src, uint8_t* dst, int64_t n, hipStream_t stream) {
-  if (n <= 0) return hipSuccess;
-  const unsigned blocks = (unsigned)std::max<int64_t>(1, std::min<int64_t>(4096, (n + 1023) / 1024));
-  hipLaunchKernelGGL(narrow_u8, dim3(blocks), dim3(256), 0, stream, src, dst, n);
-  return hipGetLastError();
-}
-
 hipError_t launch_cp_quant(const CpQuant64Args& a, hipStream_t stream) {
   if (a.nseq <= 0) return hipSuccess;
   hipLaunchKernelGGL(cp_quant_f64, dim3((unsigned)((a.nseq + 3) / 4)), dim3(256), 0, stream, a);

@@ -174,8 +174,6 @@ struct CpQuant64Args {
   uint8_t* tie;            // [nseq] 1: a tie or out-of-range arc (fold element by element)
 };
 hipError_t launch_cp_quant(const CpQuant64Args& a, hipStream_t stream);
-// dst[k] = (uint8_t)src[k], k < n (the parallel chain's paths for N <= 256 across PCIe)
-hipError_t launch_narrow_u8(const int32_t* src, uint8_t* dst, int64_t n, hipStream_t stream);
 
 // CPSolver's super-sequence decode chained exactly over the whole batch (cp_superseq_chain).
 struct CpChainArgs {

@@ -300,9 +300,8 @@ def test_chain_par_wide_speculation(gpu, monkeypatch, n):
 @pytest.mark.parametrize("n,nseq", [(256, 2048), (300, 120)])
 def test_chain_par_copy_overlap_knob(gpu, monkeypatch, n, nseq):
     """The paths' host copy runs on its own stream behind the last backtrack, beside the
-    certificate pass (default; N <= 256: as bytes widened on the host, CV_CHAIN_U8=0: as int32;
-    the output prefaulted during the forward, CV_CHAIN_PREFAULT=0: not); CV_CHAIN_COPY_OVERLAP=0
-    copies after the certificates on the decode's stream.  Both return the same paths and objective (f64 trellis at N = 256, the
+    certificate pass (default); CV_CHAIN_COPY_OVERLAP=0 copies after the certificates on the
+    decode's stream.  Both return the same paths and objective (f64 trellis at N = 256, the
     generic rows mode's plain-row certificates at N = 300)."""
     if n == 256:
         c = synth.config("c4", nseq)
@@ -316,10 +315,6 @@ def test_chain_par_copy_overlap_knob(gpu, monkeypatch, n, nseq):
     (pp, op), stp = _par(h, off, obs)
     assert stp["parallel"], stp
     assert obj == op and np.array_equal(path, pp)
-    monkeypatch.setenv("CV_CHAIN_U8", "0")  # N <= 256: the int32 paths across PCIe, not bytes
-    (pu, ou), stu = _par(h, off, obs)
-    assert stu["parallel"], stu
-    assert obj == ou and np.array_equal(path, pu)
     monkeypatch.setenv("CV_CHAIN_COPY_OVERLAP", "0")
     (p0, o0), st0 = _par(h, off, obs)
     assert st0["parallel"], st0
