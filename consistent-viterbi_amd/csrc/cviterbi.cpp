@@ -3139,15 +3139,6 @@ cv_status superseq_cp_par(cv_hmm* h, int64_t nseq, const int64_t* offsets, const
     }
   } copy_join{h->copy_stream, false};
   if (paths_rec) {
-    // the caller's output is typically freshly allocated: its first touch (page faults, ~5 ms
-    // for the 134 MB of a config-4-sized call) is taken by the host threads here, while the
-    // forward pass runs, instead of by the copy behind the certificate pass (A/B knob:
-    // CV_CHAIN_PREFAULT=0)
-    const char* pf = getenv("CV_CHAIN_PREFAULT");
-    if (!(pf && *pf == '0'))
-      parallel_ranges((int64_t)L * 4, [&](int, int64_t a, int64_t b) {
-        std::memset(reinterpret_cast<unsigned char*>(path_out) + a, 0, (size_t)(b - a));
-      }, (int64_t)1 << 22);
     HIP_TRY(hipStreamWaitEvent(h->copy_stream, h->paths_ev, 0));
     HIP_TRY(hipMemcpyAsync(path_out, d_path.p, (size_t)L * 4, hipMemcpyDeviceToHost, h->copy_stream));
     copy_join.on = true;
