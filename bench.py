@@ -32,6 +32,7 @@ Rank 0 prints ONE JSON line.
 from __future__ import annotations
 
 import argparse
+import contextlib
 import json
 import os
 import sys
@@ -254,7 +255,7 @@ def bench_superseq_cp(dev):
                     "for this input"}
 
 
-def c5_sharded(dev, world, rank, dist, backend, nseq, reps):
+def c5_sharded(dev, world, rank, dist, backend, nseq, reps, ph):
     """BASELINE config 5 (consistency-constrained decode, "8x MI355X") across the ranks:
     cviterbi.dist.constrained_decode_sharded -- each rank's contiguous shard through
     cv_decode_constrained_exchange (terms pass, ONE all-reduce of exact integer partials, the
@@ -273,16 +274,19 @@ def c5_sharded(dev, world, rank, dist, backend, nseq, reps):
     h = cv.HMM(c["pi"], c["a"], c["b"].reshape(N_STATES, 32, 32), device=dev.index)
     device = dev if backend == "nccl" else None
     call = (h, c["offsets"], c["obs"], c["component"], 7, dist)
-    got = cvd.constrained_decode_sharded(*call, device=device)  # warmup
-    dist.barrier()
-    t0 = time.perf_counter()
-    for _ in range(reps):
-        got = cvd.constrained_decode_sharded(*call, device=device)
-    dist.barrier()
+    with ph("c5_sharded: all_reduce of the exact partials + packed gather (warmup call)"):
+        got = cvd.constrained_decode_sharded(*call, device=device)  # warmup
+        dist.barrier()
+    with ph("c5_sharded: all_reduce of the exact partials + packed gather (timed calls)"):
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            got = cvd.constrained_decode_sharded(*call, device=device)
+        dist.barrier()
     el = (time.perf_counter() - t0) / reps
     traced = cv.last_suffix_traced(h)  # this rank's shard, before rank 0's reference decode below
     tt = torch.tensor([el], dtype=torch.float64, device="cpu" if backend == "gloo" else dev)
-    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    with ph("c5_sharded: all_reduce MAX of the call times"):
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
     el = float(tt.item())
     out = None
     if rank == 0:
@@ -296,7 +300,8 @@ def c5_sharded(dev, world, rank, dist, backend, nseq, reps):
                "check": {"what": "gathered paths/scores/statuses, component states and objective == rank 0's "
                                  "single-process cv_decode_constrained of the global batch, bit for bit",
                          "equal": bool(equal)}}
-    dist.barrier()
+    with ph("c5_sharded: barrier after rank 0's single-process check"):
+        dist.barrier()
     del h
     return out
 
@@ -319,16 +324,22 @@ def main():
     local = local % max(torch.cuda.device_count(), 1)  # == LOCAL_RANK on a node with one GPU per rank
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
-        if args.backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
-        else:
-            dist.init_process_group("gloo")
-
     from cviterbi import dist as cvd
 
+    watch = None
+    if world > 1:
+        # finite collective timeout (180 s, async error handling for RCCL) and a watchdog that
+        # names the collective a rank is stuck in: a hang exits non-zero with that message well
+        # inside the driver's 600 s limit instead of being killed there silently
+        cvd.init_process_group(dist, args.backend, dev if args.backend == "nccl" else None)
+        watch = cvd.CollectiveWatch(rank)
+
+    def ph(name, timeout_s=None):
+        return watch.phase(name, timeout_s) if watch else contextlib.nullcontext()
+
     if world > 1:  # RCCL first-run readiness: one known-value gather + one int64 all-reduce
-        ok, msg = cvd.preflight(dist, dev if args.backend == "nccl" else None, N_STATES)
+        with ph("preflight: gather_packed_to_root + int64 all_reduce"):
+            ok, msg = cvd.preflight(dist, dev if args.backend == "nccl" else None, N_STATES)
         if not ok:
             print(f"bench.py rank {rank}: collective pre-flight failed ({args.backend}): {msg}", file=sys.stderr, flush=True)
             dist.destroy_process_group()
@@ -393,16 +404,18 @@ def main():
         # timed region: barrier + sync on both sides, exactly K steps; kernel times summed from
         # HIP events recorded around each launch on the decode stream (read after the region)
         if world > 1:
-            dist.barrier()
+            with ph("barrier before the timed region"):
+                dist.barrier()
         torch.cuda.synchronize(dev)
         cv.timing_begin(h)
-        t0 = time.perf_counter()
-        for _ in range(steps):
-            step(dtype)
-        torch.cuda.synchronize(dev)
-        if world > 1:
-            dist.barrier()
-        el = time.perf_counter() - t0
+        with ph("timed steps: per-step gather_packed_to_root to rank 0 + closing barrier"):
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                step(dtype)
+            torch.cuda.synchronize(dev)
+            if world > 1:
+                dist.barrier()
+            el = time.perf_counter() - t0
         kt = cv.timing_end(h)
         per_rank = [el]
         if world > 1:  # every rank's time (the SCALE record shows imbalance); the max is the job's
@@ -413,7 +426,8 @@ def main():
     def all_gather_floats(vals):
         t = torch.tensor(vals, dtype=torch.float64, device="cpu" if args.backend == "gloo" else dev)
         parts = [torch.zeros_like(t) for _ in range(world)]
-        dist.all_gather(parts, t)
+        with ph("all_gather of per-rank timings"):
+            dist.all_gather(parts, t)
         return [p.cpu().tolist() for p in parts]
 
     el, kt, per_rank_s = timed(args.dtype, args.steps, args.warmup)
@@ -456,7 +470,8 @@ def main():
             verify = {"what": "last step's gathered paths/scores/statuses (all ranks) == rank 0's single-GPU "
                               "decode of the same global batch, bit for bit", "sequences": B, "equal": ok}
             del obs_g, rp, rs, rst
-        dist.barrier()
+        with ph("barrier after rank 0's verify decode"):
+            dist.barrier()
 
     f32_extra = None
     if f64 and not args.no_f32_extra:
@@ -478,7 +493,7 @@ def main():
 
     c5s = None
     if world > 1 and not args.no_c5_sharded:
-        c5s = c5_sharded(dev, world, rank, dist, args.backend, args.c5_batch, 2)
+        c5s = c5_sharded(dev, world, rank, dist, args.backend, args.c5_batch, 2, ph)
 
     # per-rank peak device memory: torch's tensors + the library's tables and workspaces
     mem = [torch.cuda.max_memory_allocated(dev) / 1e9, cv.device_memory()["peak"] / 1e9]
@@ -585,7 +600,8 @@ def main():
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
-        dist.barrier()
+        with ph("final barrier (rank 0's CPU baseline and configs)"):
+            dist.barrier()
         dist.destroy_process_group()
     if rank == 0 and checks and not all(checks):
         raise SystemExit("bench.py: the decoded result failed its check (see multi_gpu_check / cpu_baseline.check)")

@@ -36,10 +36,16 @@
 #include "kernels/fit.h"
 #include "kernels/trellis.h"
 #include "kernels/trellis64.h"
+#include "tuning.h"
 
 namespace {
 
 thread_local std::string g_err;
+
+// the handle's lock plus its tuning snapshot as the calling thread's current tuning (tuning.h)
+#define CV_LOCK(h)                             \
+  std::lock_guard<std::mutex> lk((h)->mu);     \
+  cvk::TuningScope tuning_scope((h)->tuning)
 
 cv_status set_err(cv_status st, const char* fmt, ...) {
   char buf[512];
@@ -198,6 +204,9 @@ struct cv_hmm {
   hipStream_t stream = nullptr;     // default stream of the handle
   hipStream_t bt_stream = nullptr;  // backtrack stream (overlaps the next chunk's forward)
   std::mutex mu;
+  // tuning keys and test hooks (tuning.h): the environment at cv_hmm_create, then
+  // cv_hmm_set_tuning only; every locked host API call makes it the thread's current tuning
+  cvk::Tuning tuning;
 
   // trellis kernel tables (f32, padded to NP)
   int np = 0;
@@ -218,6 +227,8 @@ struct cv_hmm {
   DevBuf q_at32;            // f32(a^T), uploaded when t64_nonpos
   bool t64_nonpos = false;  // every finite pi/a/b entry in [-2^80, 0] (NONPOS backtrack test)
   int nonpos_cache = -1;    // model_nonpos(): the same predicate without the t64 tables (any N)
+  double arc_max = -1.0;    // max finite |pi| or |a|, plus max finite |b| (< 0: not computed yet)
+  double cert_rho_cap = 0.0;  // the parallel chain's certified backtrack (T64BtArgs::rho_cap)
   DevBuf q_pi0;  // the reversed (suffix) pass: pi = 0 for the N states, -inf padding
   // f32 generic tables
   bool g32_ready = false;
@@ -450,14 +461,11 @@ cv_status ensure_at32(cv_hmm* h) {
 }
 
 // Every finite pi/a/b entry in [-2^80, 0] (log-probabilities): the NONPOS backtrack test and the
-// parallel chain's certificates hold for such models.  The CV_T64_NONPOS=0 knob forces the
+// parallel chain's certificates hold for such models.  Tuning key t64_nonpos = 0 forces the
 // general f64 interval test (same paths, bit for bit) and turns the parallel chain off.
 bool model_nonpos(cv_hmm* h) {
   if (h->nonpos_cache >= 0) return h->nonpos_cache != 0;
-  static const bool nonpos_knob = [] {
-    const char* e = getenv("CV_T64_NONPOS");
-    return !(e && e[0] == '0');
-  }();
+  const bool nonpos_knob = h->tuning.t64_nonpos != 0;
   auto nonpos = [](const std::vector<double>& v) {
     for (double x : v)
       if (std::isfinite(x) && !(x <= 0.0 && x >= -0x1p80)) return false;
@@ -559,18 +567,13 @@ cv_status make_hmm(int N, const std::vector<int64_t>& bdims, const double* pi, c
   std::transform(a, a + (size_t)N * N, h->a.begin(), canon);
   std::transform(b, b + (size_t)N * V, h->b.begin(), canon);
   h->device = device;
+  h->tuning = cvk::tuning_from_env();  // the handle's snapshot: no later environment read
   *out = h.release();
   return CV_OK;
 }
 
-// CV_TRACE=1: host-side phase timestamps of the constrained decode on stderr (profiling aid).
-bool trace_on() {
-  static const bool on = [] {
-    const char* e = getenv("CV_TRACE");
-    return e && *e && *e != '0';
-  }();
-  return on;
-}
+// tuning key trace (CV_TRACE=1): host-side phase timestamps on stderr (profiling aid).
+bool trace_on() { return cvk::tuning().trace != 0; }
 void trace_mark(const char* what) {
   if (!trace_on()) return;
   static thread_local auto last = std::chrono::steady_clock::now();
@@ -580,14 +583,11 @@ void trace_mark(const char* what) {
 }
 
 // Host worker threads for the O(elements) loops of the host API (validation, constraint
-// bookkeeping, exact accumulation): min(16, hardware threads), CV_HOST_THREADS overrides.
+// bookkeeping, exact accumulation): min(16, hardware threads), tuning key host_threads overrides.
 int host_threads() {
-  static const int n = [] {
-    const char* e = getenv("CV_HOST_THREADS");
-    int v = e ? atoi(e) : (int)std::thread::hardware_concurrency();
-    return std::max(1, std::min(v > 0 ? v : 1, 16));
-  }();
-  return n;
+  static const int hw = (int)std::thread::hardware_concurrency();
+  const int v = cvk::tuning().host_threads > 0 ? cvk::tuning().host_threads : hw;
+  return std::max(1, std::min(v > 0 ? v : 1, 16));
 }
 
 // f(t, lo, hi) over [0, n) split into contiguous ranges, one per worker (t = worker index).
@@ -711,8 +711,7 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
   // What the f64 trellis SUPPORTS (an explicit CV_KERNEL_TRELLIS_F64 request gets it) is wider
   // than what AUTO picks: 256 < N <= 512 only for N >= 384 or >= 8,192 sequences, 512 < N <=
   // 1,024 only above N = 724 (cvk::t64_batch_states; the generic kernels win below)
-  const char* t512_env = getenv("CV_T64_512");
-  const bool t512_pick = (t512_env && t512_env[0] == '1') || h->N >= 384 || nseq >= 8192;
+  const bool t512_pick = h->tuning.t64_512 == 1 || h->N >= 384 || nseq >= 8192;
   const bool small_ok = (o.assoc == CV_ASSOC_VITERBI || o.assoc == CV_ASSOC_DECODE || o.assoc == CV_ASSOC_CP ||
                          o.assoc == CV_ASSOC_DP) &&
                         (!(o.forced || resume_rows) || o.assoc == CV_ASSOC_VITERBI) && cvk::t64_padded_states(h->N) != 0;
@@ -783,12 +782,11 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
                                          : default_workspace_cap(w_main.bytes, use_t64 ? kDefaultWorkspaceT64 : kDefaultWorkspace);
   // generic kernels: rows mode (the delta rows, argmax recomputed along the path) for every
   // association but CP (whose values need the argmax in the forward pass); A/B knob
-  // CV_GENERIC_ROWS=0 (psi mode, bit-identical), read per call.  4,096 x 128 sequences:
+  // tuning key generic_rows = 0 (psi mode, bit-identical).  4,096 x 128 sequences:
   // N = 300 14.9 -> 11.5 ms, N = 512 28.7 -> 21.5 ms, N = 1,024 163 -> 139 ms
   // (profiles/r04_large_n.txt)
-  const char* gr_env = getenv("CV_GENERIC_ROWS");
   const bool gen_rows =
-      !use_trellis && !use_t64 && !gen_global && o.assoc != CV_ASSOC_CP && !(gr_env && *gr_env == '0');
+      !use_trellis && !use_t64 && !gen_global && o.assoc != CV_ASSOC_CP && h->tuning.generic_rows != 0;
   if (cp_cert && !use_t64 && !(gen_rows && o.dtype == CV_DTYPE_F64))
     return set_err(CV_EUNSUPPORTED, "chain certificates need the f64 trellis or the generic kernels' rows mode");
   if (gen_rows && (st = o.dtype == CV_DTYPE_F64 ? ensure_at64(h) : ensure_at32(h)) != CV_OK) return st;
@@ -805,27 +803,18 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
   // t64 runs serial: its 212-VGPR forward waves fill each SIMD exactly twice per launch and
   // saturate the VALU; a co-running backtrack cost more than it hid (config 4: 159.8 ms with a
   // persistent one-wave-per-SIMD backtrack vs 152.4 ms serial, profiles/r02_ab_t64_overlap.txt)
-  static const bool t64_overlap = [] {  // A/B knob (bit-identical): CV_T64_OVERLAP=0/1
-    const char* e = getenv("CV_T64_OVERLAP");
-    return e != nullptr && e[0] == '1';
-  }();
-  const bool serial = (o.flags & CV_FLAG_SERIAL) != 0 || wave || (use_t64 && !t64_overlap) || side_ws;
+  const bool serial = (o.flags & CV_FLAG_SERIAL) != 0 || wave || use_t64 || side_ws;
   // Sequences per forward workgroup: 2 (trellis_fwd2_f32, equal-length pairs; default) or 1
   // (trellis_fwd_f32: leftovers, N not a multiple of 64).
   const bool plain = use_trellis && !wave && cvk::trellis_pair_supported(h->np);
   const int group = (!plain || (o.flags & CV_FLAG_NO_PAIR)) ? 1 : 2;
-  static const uint64_t max_chunks = [] {  // A/B knob (bit-identical): pipeline depth
-    const char* e = getenv("CV_MAX_CHUNKS");
-    const long v = e ? atol(e) : 8;
+  const uint64_t max_chunks = [&] {  // tuning key max_chunks (bit-identical): pipeline depth
+    const int v = h->tuning.max_chunks;
     return (uint64_t)(v >= 1 && v <= 64 ? v : 8);
   }();
   const uint64_t half_cap = std::max<uint64_t>(serial ? cap : cap / 2, per_elem);
   uint64_t nchunks = std::max<uint64_t>(1, (total_elems * per_elem + half_cap - 1) / half_cap);
-  // t64: chunks of >= 8 sequences x 2 waves x 4 SIMDs x CUs so every chunk runs S = 8
-  if (!serial)
-    nchunks = std::max<uint64_t>(
-        nchunks, use_t64 ? std::min<uint64_t>(4, (uint64_t)(nseq / (64 * (int64_t)std::max(h->cus, 1))))
-                         : std::min<uint64_t>(max_chunks, (uint64_t)(nseq / 2048)));
+  if (!serial) nchunks = std::max<uint64_t>(nchunks, std::min<uint64_t>(max_chunks, (uint64_t)(nseq / 2048)));
   const uint64_t target = std::max<uint64_t>(1, (total_elems + nchunks - 1) / nchunks);
   const uint64_t elem_cap = std::max<uint64_t>(half_cap / per_elem, 1);
   std::vector<std::pair<int64_t, int64_t>> chunks;
@@ -960,7 +949,6 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
   for (size_t ci = 0; ci < chunks.size(); ++ci) {
     const auto& c = chunks[ci];
     const int64_t n = c.second - c.first;
-    bool fused_chunk = false;  // the forward launch also backtracked the chunk
     const int buf = nbuf == 2 ? (int)(ci % 2) : 0;
     unsigned char* wsb = w_main.as<unsigned char>() + buf * buf_bytes;
     unsigned char* lrb = w_last.as<unsigned char>() + buf * last_bytes;
@@ -1032,10 +1020,6 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
           tmax = std::max(tmax, T);
         }
         fa.wg_ok = (8 * tmin >= 7 * tmax || n >= 2 * 64 * (int64_t)std::max(h->cus, 1)) ? 1 : 0;
-        if (side_ws) {  // A/B knob CV_SIDE_WG=0: the config-5 side decode in one-wave workgroups
-          const char* e = getenv("CV_SIDE_WG");
-          if (e && *e == '0') fa.wg_ok = 0;
-        }
       }
       if (t64cp) {
         fa.nstates = h->N;
@@ -1045,10 +1029,7 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
         fa.cp_last = cp_last;
         err = cvk::launch_t64_cp_fwd(h->np64, spw, fa, n, stream);
       } else {
-        const cvk::T64BtArgs ba = t64_bt_args(c, wsb);
-        fused_chunk = !cp_cert && cvk::t64_wave_fusable(h->np64, fa, ba);
-        err = fused_chunk ? cvk::launch_t64_wave_fused(fa, ba, n, stream)  // N <= 64: backtrack fused
-                          : cvk::launch_t64_fwd(h->np64, spw, fa, n, stream);
+        err = cvk::launch_t64_fwd(h->np64, spw, fa, n, stream);
       }
     } else if (o.dtype == CV_DTYPE_F64) {
       cvk::GenericFwdArgs<double> fa{};
@@ -1131,17 +1112,22 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
         err = cvk::launch_rescore_f64(ra, n, bts, reserve);
       }
     } else if (use_t64 && !t64cp) {
-      // overlap mode: one persistent workgroup per CU while the next chunk's forward runs (one
-      // 60-VGPR wave per SIMD beside its two 212-VGPR waves); the last chunk at full occupancy
-      err = fused_chunk ? hipSuccess
-                        : cvk::launch_t64_bt(h->np64, t64_bt_args(c, wsb), n, bts,
-                                             (serial || ci + 1 == chunks.size()) ? 0 : std::max(h->cus, 1));
+      cvk::T64BtArgs ba = t64_bt_args(c, wsb);
+      // the parallel chain's certificates inside the backtrack (NONPOS row A0, NP <= 256): no
+      // second pass over every row (tuning key chain_cert_fused = 0: the cp_cert_f64 pass)
+      const bool fused_cert = cp_cert && ba.at32 && !ba.dp_assoc && !ba.decode_bt && h->np64 <= 256 &&
+                              h->tuning.chain_cert_fused != 0;
+      if (fused_cert) {
+        ba.cert = cp_cert;
+        ba.rho_cap = h->cert_rho_cap;
+      }
+      err = cvk::launch_t64_bt(h->np64, ba, n, bts);
       if (err == hipSuccess && cp_cert && paths_ev_rec && ci + 1 == chunks.size()) {
         if (!h->paths_ev) HIP_TRY(hipEventCreateWithFlags(&h->paths_ev, hipEventDisableTiming));
         HIP_TRY(hipEventRecord(h->paths_ev, bts));
         *paths_ev_rec = true;
       }
-      if (err == hipSuccess && cp_cert) {
+      if (err == hipSuccess && cp_cert && !fused_cert) {
         cvk::CpCert64Args ca{};
         ca.delta = reinterpret_cast<const double*>(wsb);
         ca.delta_elem_base = offsets_host[c.first];
@@ -1316,6 +1302,23 @@ CV_API void cv_hmm_destroy(cv_hmm* h) {
   delete h;
 }
 
+CV_API cv_status cv_hmm_set_tuning(cv_hmm* h, const char* key, int64_t value) {
+  if (!h || !key) return set_err(CV_EINVAL, "bad argument");
+  std::lock_guard<std::mutex> lk(h->mu);
+  if (!cvk::tuning_set(h->tuning, key, value)) return set_err(CV_EINVAL, "unknown tuning key '%s' or value out of range", key);
+  if (std::strcmp(key, "t64_nonpos") == 0) {  // model_nonpos reads it: rebuild the f64 trellis tables
+    h->nonpos_cache = -1;
+    h->t64_ready = false;
+  }
+  return CV_OK;
+}
+CV_API cv_status cv_hmm_get_tuning(const cv_hmm* h, const char* key, int64_t* value) {
+  if (!h || !key || !value) return set_err(CV_EINVAL, "bad argument");
+  std::lock_guard<std::mutex> lk(const_cast<cv_hmm*>(h)->mu);
+  if (!cvk::tuning_get(h->tuning, key, value)) return set_err(CV_EINVAL, "unknown tuning key '%s'", key);
+  return CV_OK;
+}
+CV_API const char* cv_tuning_key(int32_t i) { return cvk::tuning_key(i); }
 CV_API int32_t cv_hmm_nstates(const cv_hmm* h) { return h ? h->N : -1; }
 CV_API int64_t cv_hmm_nobs(const cv_hmm* h) { return h ? h->V : -1; }
 CV_API int32_t cv_hmm_ndims(const cv_hmm* h) { return h ? h->D : -1; }
@@ -1376,7 +1379,7 @@ CV_API cv_status cv_decode_batch_device(cv_hmm* h, int64_t nseq, const int64_t* 
   if (!h) return set_err(CV_EINVAL, "null handle");
   if (nseq > 0 && (!offsets_dev || !obs_dev || !path_dev || !score_dev || !status_dev))
     return set_err(CV_EINVAL, "null device buffer");
-  std::lock_guard<std::mutex> lk(h->mu);
+  CV_LOCK(h);
   cv_status st = set_device(h);
   if (st != CV_OK) return st;
   const cv_opts o = opts ? *opts : default_opts();
@@ -1442,7 +1445,7 @@ CV_API cv_status cv_decode_batch(cv_hmm* h, int64_t nseq, const int64_t* offsets
   if (!h) return set_err(CV_EINVAL, "null handle");
   if (nseq < 0 || (nseq > 0 && (!offsets || !obs || !path_out || !score_out || !status_out)))
     return set_err(CV_EINVAL, "null argument");
-  std::lock_guard<std::mutex> lk(h->mu);
+  CV_LOCK(h);
   cv_status st = set_device(h);
   if (st != CV_OK) return st;
   return decode_host_locked(h, nseq, offsets, obs, opts ? *opts : default_opts(), path_out, score_out, status_out);
@@ -1583,32 +1586,17 @@ struct PrefixKeep {
 };
 
 // The certified suffix trace (suffix_trace_f64) replaces the resume flow's second forward pass
-// for one-position sequences: f64, models whose finite entries are all in [-2^80, 0].  A/B knob
-// (bit-identical): CV_NO_TRACE=1.
-bool trace_supported(const cv_hmm* h) {
-  const char* e = getenv("CV_NO_TRACE");  // read per call: tests flip it within one process
-  return !(e && *e && *e != '0') && h->t64_nonpos;
-}
+// for one-position sequences: f64, models whose finite entries are all in [-2^80, 0].  Tuning key
+// (bit-identical): no_trace = 1.
+bool trace_supported(const cv_hmm* h) { return h->tuning.no_trace == 0 && h->t64_nonpos; }
 
 // The resume flow covers f32 N > 64 with NP % 64 == 0 (pair kernel + backtrack_v) and every f64
 // N <= 256; its stored rows must fit 4x the workspace cap (32 GiB by default: config 5 needs
 // 8.6 GB of f32 rows; f64 rows are twice that, within the f64 trellis's 64 GiB cap x 4).
 bool resume_supported(const cv_hmm* h, bool f64) {
-  const char* e = getenv("CV_NO_RESUME");
-  if (e && *e && *e != '0') return false;
+  if (h->tuning.no_resume != 0) return false;  // tuning key (bit-identical)
   if (f64) return cvk::t64_padded_states(h->N) != 0;  // trellis_fwd_f64 EXT + prefix_backtrack_f64
   return h->N > 64 && (h->np == 128 || h->np == 192 || h->np == 256);
-}
-
-// A/B knob (bit-identical): CV_T64_WG_TERMS=1 runs the terms pass in eight-wave workgroups
-// from two rounds on; off: neutral at config 5 (185.2 vs 185.9 ms, profiles/r03_ab_c5_terms.txt
-// -- the faster prefix/suffix passes leave the side decode less room)
-bool terms_wg() {
-  static const bool on = [] {
-    const char* e = getenv("CV_T64_WG_TERMS");
-    return e && e[0] == '1';
-  }();
-  return on;
 }
 
 cv_status constrained_partials_locked(cv_hmm* h, int64_t nseq, const int64_t* offsets, const int32_t* obs,
@@ -1870,7 +1858,10 @@ cv_status constrained_partials_locked(cv_hmm* h, int64_t nseq, const int64_t* of
     fa.queue = h->cs_queue.as<int>();
     // prefix / suffix passes: longest-first ranges; with CV_T64_WG_TERMS=1 and at least two
     // rounds of eight-wave workgroups, that layout
-    fa.wg_ok = (terms_wg() && nc >= 2 * 64 * (int64_t)std::max(h->cus, 1)) ? 1 : 0;
+    // one-wave workgroups: the eight-wave layout measured neutral here (CV_T64_WG_TERMS, round 3:
+    // 185.2 vs 185.9 ms -- the faster prefix/suffix passes leave the side decode less room;
+    // removed in round 6)
+    fa.wg_ok = 0;
     err = cvk::launch_t64_fwd(np, cvk::t64_seqs_per_wave(nc, h->cus), fa, nc, stream);
     // suffixes: the same recurrence on a^T with pi = 0, reversed (its last row = g_{t_m+1})
     if (err == hipSuccess) {
@@ -1906,9 +1897,8 @@ cv_status constrained_partials_locked(cv_hmm* h, int64_t nseq, const int64_t* of
     return set_err(CV_EINVAL, "a constrained-decode term is outside the exact unit's range (|score| >= 2^32): "
                               "check the model's log-probabilities (null, not a huge negative, for impossible)");
   };
-  // CV_HOST_SUMS=1 takes the host loop (tests compare the two; same integers by construction)
-  const char* hs = getenv("CV_HOST_SUMS");
-  const bool host_sums = hs && *hs && *hs != '0';
+  // tuning key host_sums = 1 takes the host loop (tests compare the two; same integers by construction)
+  const bool host_sums = h->tuning.host_sums != 0;
   if (!host_sums && ncomp <= cvx::kUnarySumMaxComp && N <= 256) {
     // exact unary sums on the device (kernels/exact.hip): only the ncomp x uw words come back
     std::vector<int32_t> cc((size_t)2 * nc);
@@ -2231,18 +2221,9 @@ cv_status side_decode_launch(cv_hmm* h, int64_t nseq, const int64_t* offsets_hos
     return CV_OK;
   }
   // the side stream starts behind everything the caller had queued on its stream when the
-  // constrained decode began (h->side.start, recorded then), not behind the term launches;
-  // A/B knob CV_SIDE_AFTER=1: behind the term launches (the terms pass alone on the device,
-  // then the side decode beside the search and the suffix trace)
-  const char* after_env = getenv("CV_SIDE_AFTER");
-  if (after_env && *after_env == '1') {
-    if (!sd.after && hipEventCreateWithFlags(&sd.after, hipEventDisableTiming) != hipSuccess)
-      return set_err(CV_EDEVICE, "hipEventCreate failed");
-    HIP_TRY(hipEventRecord(sd.after, stream));
-    HIP_TRY(hipStreamWaitEvent(sd.stream, sd.after, 0));
-  } else {
-    HIP_TRY(hipStreamWaitEvent(sd.stream, sd.start, 0));
-  }
+  // constrained decode began (h->side.start, recorded then), not behind the term launches
+  // (round 4 measured every other order slower: DESIGN.md §3, rejected variants)
+  HIP_TRY(hipStreamWaitEvent(sd.stream, sd.start, 0));
   HIP_TRY(hipMemcpyAsync(sd.idx.p, sd.idx_host.data(), sd.idx_host.size() * 8, hipMemcpyHostToDevice, sd.stream));
   const int64_t* cstart_d = sd.idx.as<int64_t>();
   const int64_t* cseq_d = cstart_d + nu;
@@ -2256,13 +2237,6 @@ cv_status side_decode_launch(cv_hmm* h, int64_t nseq, const int64_t* offsets_hos
   cv_opts o2 = o;
   o2.forced = nullptr;
   o2.rescore_f64 = 0;  // f64: the decode's score is the reference's
-  {  // A/B knob CV_SIDE_CHUNKS=k: the side decode in k chunks (each chunk's backtrack runs
-     // beside the next chunk's forward and the constrained work; the last one is shorter)
-    const char* e = getenv("CV_SIDE_CHUNKS");
-    const int k = e ? atoi(e) : 1;
-    if (k > 1 && cvk::t64_padded_states(h->N))
-      o2.workspace_bytes = ((uint64_t)total2 * h->np64 * 8 + (uint64_t)k - 1) / (uint64_t)k + 4096;
-  }
   if ((st = decode_device(h, nu, off2, off2_d, sd.obs2.as<int32_t>(), o2, sd.path2.as<int32_t>(), score2, status2,
                           sd.stream, nullptr, /*side_ws=*/true)) != CV_OK) {
     if (st != CV_ENOMEM) return st;
@@ -2303,21 +2277,8 @@ cv_status side_streams(cv_hmm* h) {
       (void)hipGetLastError();
       least = greatest = 0;
     }
-    const char* e = getenv("CV_SIDE_PRIO");
-    if (e && *e == '0') greatest = least;
-    if (e && *e == '2') std::swap(least, greatest);  // A/B: the side decode first, the terms pass in its gaps
-    // A/B knob CV_SIDE_CUMASK=p (1..7): the side stream on the CUs i with i % 8 < p, the
-    // constrained stream on the others (disjoint halves instead of shared CUs)
-    const char* cm = getenv("CV_SIDE_CUMASK");
-    const int p = cm ? atoi(cm) : 0;
-    if (p >= 1 && p <= 7 && h->cus > 0) {
-      std::vector<uint32_t> ms((size_t)(h->cus + 31) / 32, 0u), mh(ms.size(), 0u);
-      for (int i = 0; i < h->cus; ++i) ((i % 8) < p ? ms : mh)[(size_t)i / 32] |= 1u << (i % 32);
-      if (hipExtStreamCreateWithCUMask(&sd.stream, (uint32_t)ms.size(), ms.data()) != hipSuccess ||
-          hipExtStreamCreateWithCUMask(&sd.hi, (uint32_t)mh.size(), mh.data()) != hipSuccess)
-        return set_err(CV_EDEVICE, "hipExtStreamCreateWithCUMask failed");
-    } else if (hipStreamCreateWithPriority(&sd.stream, hipStreamNonBlocking, least) != hipSuccess ||
-               hipStreamCreateWithPriority(&sd.hi, hipStreamNonBlocking, greatest) != hipSuccess)
+    if (hipStreamCreateWithPriority(&sd.stream, hipStreamNonBlocking, least) != hipSuccess ||
+        hipStreamCreateWithPriority(&sd.hi, hipStreamNonBlocking, greatest) != hipSuccess)
       return set_err(CV_EDEVICE, "hipStreamCreateWithPriority failed");
   }
   if (!sd.start && hipEventCreateWithFlags(&sd.start, hipEventDisableTiming) != hipSuccess)
@@ -2385,13 +2346,6 @@ cv_status forced_decode_resume(cv_hmm* h, int64_t nseq, const int64_t* offsets_h
     ta.score = score_dev;
     ta.status = status_dev;
     ta.cert = cert_d;
-    // A/B knob CV_TRACE_AFTER_SIDE=1: the trace waits for the side decode (it then runs alone on
-    // the chip instead of beside the side decode's tail)
-    static const bool after_side = [] {
-      const char* e = getenv("CV_TRACE_AFTER_SIDE");
-      return e && *e == '1';
-    }();
-    if (after_side && constrained_only) HIP_TRY(hipStreamWaitEvent(stream, h->side.done, 0));
     const hipError_t e = cvk::launch_t64_suffix_trace(np, ta, n1, stream);
     if (e != hipSuccess) return set_err(CV_EDEVICE, "suffix trace failed: %s", hipGetErrorString(e));
     HIP_TRY(hipMemcpyAsync(cert.data(), cert_d, (size_t)n1, hipMemcpyDeviceToHost, stream));
@@ -2614,7 +2568,7 @@ CV_API cv_status cv_constrained_partials(cv_hmm* h, int64_t nseq, const int64_t*
       (ncomp > 0 && !partials_out) || (npairs > 0 && !pairs))
     return set_err(CV_EINVAL, "null argument");
   if (!pairs_sorted(pairs, npairs, ncomp)) return set_err(CV_EINVAL, "pairs must be sorted (c1 < c2) and unique");
-  std::lock_guard<std::mutex> lk(h->mu);
+  CV_LOCK(h);
   cv_status st = set_device(h);
   if (st != CV_OK) return st;
   cv_opts o = opts ? *opts : default_opts();
@@ -2639,7 +2593,7 @@ CV_API cv_status cv_decode_constrained(cv_hmm* h, int64_t nseq, const int64_t* o
   if (nseq < 0 || ncomp < 0 || (nseq > 0 && (!offsets || !obs || !component || !path_out || !score_out ||
                                              !status_out)) || (ncomp > 0 && !comp_state_out))
     return set_err(CV_EINVAL, "null argument");
-  std::lock_guard<std::mutex> lk(h->mu);
+  CV_LOCK(h);
   cv_status st = set_device(h);
   if (st != CV_OK) return st;
   cv_opts o = opts ? *opts : default_opts();
@@ -2677,7 +2631,7 @@ CV_API cv_status cv_decode_forced_components(cv_hmm* h, int64_t nseq, const int6
   if (nseq < 0 || ncomp < 0 || (nseq > 0 && (!offsets || !obs || !component || !path_out || !score_out ||
                                              !status_out)) || (ncomp > 0 && !comp_state))
     return set_err(CV_EINVAL, "null argument");
-  std::lock_guard<std::mutex> lk(h->mu);
+  CV_LOCK(h);
   cv_status st = set_device(h);
   if (st != CV_OK) return st;
   cv_opts o = opts ? *opts : default_opts();
@@ -2709,7 +2663,7 @@ CV_API cv_status cv_decode_constrained_device(cv_hmm* h, int64_t nseq, const int
   if (nseq < 0 || ncomp < 0 || (nseq > 0 && (!offsets_host || !offsets_dev || !obs_dev || !component || !path_dev ||
                                              !score_dev || !status_dev)) || (ncomp > 0 && !comp_state_out))
     return set_err(CV_EINVAL, "null argument");
-  std::lock_guard<std::mutex> lk(h->mu);
+  CV_LOCK(h);
   cv_status st = set_device(h);
   if (st != CV_OK) return st;
   cv_opts o = opts ? *opts : default_opts();
@@ -2743,10 +2697,9 @@ CV_API cv_status cv_decode_constrained_device(cv_hmm* h, int64_t nseq, const int
   if (first_bad_obs != ~0ull)
     return set_err(CV_EINVAL, "obs[%llu] out of range [0,%lld)", first_bad_obs, (long long)h->V);
   trace_mark("device constrained: checks + constrained list");
-  // the unconstrained sequences beside the terms pass (A/B knob, bit-identical: CV_NO_SIDE=1)
+  // the unconstrained sequences beside the terms pass (tuning key, bit-identical: no_side = 1)
   SideJoin side{h};
-  const char* no_side = getenv("CV_NO_SIDE");
-  const bool side_off = no_side && *no_side && *no_side != '0';
+  const bool side_off = h->tuning.no_side != 0;
   if (!side_off && o.dtype == CV_DTYPE_F64 && resume_supported(h, true) && !cs.empty()) {
     // the constrained work moves to a highest-priority stream (behind the caller's stream), the
     // side decode gets the lowest: its waves take the slots the constrained work leaves free
@@ -2827,7 +2780,7 @@ CV_API cv_status cv_decode_constrained_exchange(cv_hmm* h, int64_t nseq, const i
       (ncomp > 0 && !comp_state_out) || (npairs > 0 && !pairs))
     return set_err(CV_EINVAL, "null argument");
   if (!pairs_sorted(pairs, npairs, ncomp)) return set_err(CV_EINVAL, "pairs must be sorted (c1 < c2) and unique");
-  std::lock_guard<std::mutex> lk(h->mu);
+  CV_LOCK(h);
   cv_status st = set_device(h);
   if (st != CV_OK) return st;
   cv_opts o = opts ? *opts : default_opts();
@@ -2891,7 +2844,7 @@ CV_API cv_status cv_last_suffix_traced(const cv_hmm* h, int64_t* out) {
 
 CV_API cv_status cv_last_timing(cv_hmm* h, cv_timing* out) {
   if (!h || !out) return set_err(CV_EINVAL, "null argument");
-  std::lock_guard<std::mutex> lk(h->mu);
+  CV_LOCK(h);
   std::memset(out, 0, sizeof *out);
   out->launches = h->last_launches;
   out->kernel = h->last_kernel;
@@ -2902,7 +2855,7 @@ CV_API cv_status cv_last_timing(cv_hmm* h, cv_timing* out) {
 
 CV_API cv_status cv_timing_begin(cv_hmm* h) {
   if (!h) return set_err(CV_EINVAL, "null argument");
-  std::lock_guard<std::mutex> lk(h->mu);
+  CV_LOCK(h);
   h->acc_on = true;
   h->acc_overflow = false;
   h->acc_used = 0;
@@ -2911,7 +2864,7 @@ CV_API cv_status cv_timing_begin(cv_hmm* h) {
 
 CV_API cv_status cv_timing_end(cv_hmm* h, cv_timing* out) {
   if (!h || !out) return set_err(CV_EINVAL, "null argument");
-  std::lock_guard<std::mutex> lk(h->mu);
+  CV_LOCK(h);
   std::memset(out, 0, sizeof *out);
   const bool was_on = h->acc_on, overflow = h->acc_overflow;
   const size_t used = h->acc_used;
@@ -3104,6 +3057,19 @@ cv_status superseq_cp_par(cv_hmm* h, int64_t nseq, const int64_t* offsets, const
   }
   double* d_score = d_res.as<double>();
   uint8_t* d_status = reinterpret_cast<uint8_t*>(d_score + nseq);
+  // the certified backtrack's rho_cap (T64BtArgs): above every U = 2^-52 (|M| + |S_k| + 16) the
+  // walk can test -- |M| and every |S_k| are at most L w, w the largest finite arc magnitude
+  // |pi| or |a| plus |b| (every term <= 0) -- so its certificates decide like the exact ones
+  if (h->arc_max < 0.0) {
+    auto fmax_abs = [](const std::vector<double>& v) {
+      double m = 0.0;
+      for (double x : v)
+        if (std::isfinite(x)) m = std::max(m, std::fabs(x));
+      return m;
+    };
+    h->arc_max = std::max(fmax_abs(h->pi), fmax_abs(h->a)) + fmax_abs(h->b);
+  }
+  h->cert_rho_cap = 0x1p-52 * (2.0 * (double)L * h->arc_max + 16.0) * (1.0 + 0x1p-20);
   cv_opts o = default_opts();
   o.dtype = CV_DTYPE_F64;
   o.assoc = CV_ASSOC_VITERBI;
@@ -3111,10 +3077,9 @@ cv_status superseq_cp_par(cv_hmm* h, int64_t nseq, const int64_t* offsets, const
   o.rescore_f64 = 0;
   o.stream = stream;
   // the paths' copy to the host (4 B per element) runs on its own stream beside the
-  // certificate pass, which reads every row (A/B knob: CV_CHAIN_COPY_OVERLAP=0)
-  const char* cov = getenv("CV_CHAIN_COPY_OVERLAP");
+  // certificate pass, which reads every row (tuning key chain_copy_overlap = 0: after it)
   bool paths_rec = false;
-  const bool overlap_copy = !(cov && *cov == '0') && !trace_on();
+  const bool overlap_copy = h->tuning.chain_copy_overlap != 0 && !trace_on();
   if (overlap_copy && !h->copy_stream) HIP_TRY(hipStreamCreateWithFlags(&h->copy_stream, hipStreamNonBlocking));
   st = decode_device(h, nseq, off.data(), d_off.as<int64_t>(), d_obs.as<int32_t>(), o, d_path.as<int32_t>(), d_score,
                      d_status, stream, nullptr, false, d_cert.as<double>(), nullptr, nullptr,
@@ -3215,14 +3180,8 @@ cv_status superseq_cp_par(cv_hmm* h, int64_t nseq, const int64_t* offsets, const
   double pimax = 0.0;
   for (double x : h->pi)
     if (std::isfinite(x)) pimax = std::max(pimax, std::fabs(x));
-  const int force_m = [] {
-    const char* e = getenv("CV_CHAIN_PAR_FORCE");
-    return e ? std::max(0, atoi(e)) : 0;
-  }();
-  const bool spec_env = [] {  // A/B knob: CV_CHAIN_SPEC=0 re-runs every uncertified sequence serially
-    const char* e = getenv("CV_CHAIN_SPEC");
-    return !(e && *e == '0');
-  }();
+  const int force_m = std::max(0, h->tuning.chain_par_force);
+  const bool spec_env = h->tuning.chain_spec != 0;  // 0: every uncertified sequence re-run serially
   const int32_t* P = path_out;  // the row-A0 paths (element index relative to base)
   const int32_t* ob = obs + base;
   auto fold_elems = [&](int64_t k, double M) {  // the CP fold of sequence k's path from M
@@ -3451,10 +3410,9 @@ cv_status superseq_cp_par(cv_hmm* h, int64_t nseq, const int64_t* offsets, const
     oc.dtype = CV_DTYPE_F64;
     oc.assoc = CV_ASSOC_CP;
     // generic_fwd_ms (psi, one state per thread, one sequence per workgroup) or, N <= 256,
-    // trellis_cp_f64 by CV_CHAIN_SPEC_KERNEL=trellis (read per call: A/B knob, bit-identical):
-    // config-4 size, 620 sequences, the batch 15-17 vs 17-17.7 ms (profiles/r05_spec_ab.txt)
-    const char* sk = getenv("CV_CHAIN_SPEC_KERNEL");
-    const bool spec_generic = !small || !(sk && *sk == 't');
+    // trellis_cp_f64 by tuning key chain_spec_kernel = 1 (bit-identical): config-4 size, 620
+    // sequences, the batch 15-17 vs 17-17.7 ms (profiles/r05_spec_ab.txt)
+    const bool spec_generic = !small || h->tuning.chain_spec_kernel != 1;
     oc.kernel = spec_generic ? CV_KERNEL_GENERIC : CV_KERNEL_TRELLIS_F64;
     oc.rescore_f64 = 0;
     oc.stream = stream;
@@ -3558,7 +3516,7 @@ CV_API cv_status cv_decode_superseq_cp(cv_hmm* h, int64_t nseq, const int64_t* o
   if (nseq == 0) return CV_OK;
   if (h->N > cvk::kChainMaxStates)
     return set_err(CV_EUNSUPPORTED, "super-sequence chain covers N <= %d (N=%d)", cvk::kChainMaxStates, h->N);
-  std::lock_guard<std::mutex> lk(h->mu);
+  CV_LOCK(h);
   cv_status st = set_device(h);
   if (st != CV_OK) return st;
   if ((st = check_batch(h, nseq, offsets)) != CV_OK) return st;
@@ -3573,11 +3531,10 @@ CV_API cv_status cv_decode_superseq_cp(cv_hmm* h, int64_t nseq, const int64_t* o
   // one-workgroup chain with the candidates split over its waves and A on chip
   // (kernels/chain.hip), N > 256 (or CV_CHAIN_OLD=1, an A/B knob, bit-identical) one thread per
   // state (cp_superseq_chain); both then the parallel segmented backtrack
-  const char* old_env = getenv("CV_CHAIN_OLD");
-  const char* par_env = getenv("CV_CHAIN_PAR");  // read per call: tests flip it within one process
+  const bool chain_old = h->tuning.chain_old == 1;
   h->last_chain[0] = 0;
   for (int q = 1; q < 7; ++q) h->last_chain[q] = 0;
-  if (!(old_env && *old_env == '1') && !(par_env && *par_env == '0')) {
+  if (!chain_old && h->tuning.chain_par != 0) {
     bool applied = false;
     st = superseq_cp_par(h, nseq, offsets, obs, path_out, objective_out, &applied);
     if (st != CV_OK || applied) return st;
@@ -3587,7 +3544,7 @@ CV_API cv_status cv_decode_superseq_cp(cv_hmm* h, int64_t nseq, const int64_t* o
   std::vector<uint8_t> first((size_t)L, 0);
   for (int64_t q = 0; q < nseq; ++q)
     if (offsets[q + 1] > offsets[q]) first[(size_t)(offsets[q] - base)] = 1;
-  if (cvk::t64_padded_states(h->N) && !(old_env && *old_env == '1'))
+  if (cvk::t64_padded_states(h->N) && !chain_old)
     return superseq_cp_wg(h, L, obs + base, first, path_out, objective_out);
   if ((st = ensure_f64_tables(h)) != CV_OK) return st;
   hipStream_t stream = h->stream;
@@ -3861,7 +3818,7 @@ CV_API cv_status cv_solver_write_cfn(cv_solver* s, const char* path, uint64_t* c
   jobs.push_back({0, f_time, 0, cvcfn::kCfnStart});
   std::vector<double> rows(jobs.size() * (size_t)N);
   {
-    std::lock_guard<std::mutex> lk(h->mu);
+    CV_LOCK(h);
     cv_status st = set_device(h);
     if (st != CV_OK) return st;
     if ((st = ensure_f64_tables(h)) != CV_OK) return st;
@@ -4093,12 +4050,12 @@ CV_API cv_status cv_hmm_fit_train(int32_t nstates, int64_t nobs, int64_t nseq, c
   cv_status st = fit_validate(N, V, nseq, offsets, obs, tags, false, pi, a, b);
   if (st != CV_OK) return st;
   if (N > cvf::kBwMaxStates) return set_err(CV_EUNSUPPORTED, "Baum-Welch covers N <= %d (N=%d)", cvf::kBwMaxStates, N);
+  // no handle: the environment's tuning keys for this call (tuning.h)
+  const cvk::Tuning tun = cvk::tuning_from_env();
+  cvk::TuningScope tuning_scope(tun);
   // the strided kernels' vectors in global scratch: above kBwLdsMaxStates, or from N = 257
-  // with CV_BW_GLOBAL=1 (A/B knob and tests)
-  const bool bw_global = N > cvf::kBwLdsMaxStates || (N > cvf::kBwMmStates && [] {
-                           const char* e = getenv("CV_BW_GLOBAL");
-                           return e && *e == '1';
-                         }());
+  // with tuning key bw_global = 1 (A/B and tests)
+  const bool bw_global = N > cvf::kBwLdsMaxStates || (N > cvf::kBwMmStates && tun.bw_global == 1);
   if (max_iter < 0) return set_err(CV_EINVAL, "max_iter < 0");
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) {
@@ -4180,29 +4137,12 @@ CV_API cv_status cv_hmm_fit_train(int32_t nstates, int64_t nobs, int64_t nseq, c
   m.part = d.cnt.as<double>();
   m.parts_a = parts_a;
   std::vector<double> part((size_t)(parts_a + kPartsB));
-  // The E-step pipeline (64 < N <= 256): each chunk's sequences in P contiguous parts on their
-  // own streams, part p's forward behind part p - 1's, so one part's backward and xi GEMM run
-  // beside the next part's forward (the kernels' per-step phases without matrix products
-  // leave the matrix cores to the other kernel's workgroups on the CU).  CV_BW_PIPE=P (1..4;
-  // 1: one launch of each kernel per chunk).  Same sums up to the atomics' order.
-  const int pipe = [&] {
-    if (!cvf::bw_estep_mm(N)) return 1;
-    const char* e = getenv("CV_BW_PIPE");
-    const int v = e ? atoi(e) : 1;
-    return std::max(1, std::min(v, 4));
-  }();
-  // parts: contiguous sequence ranges of a chunk with about equal element counts
+  // (Round 5 measured an E-step pipeline -- each chunk in P parts on P streams so one part's
+  // backward and xi GEMM run beside the next part's forward -- and rejected it: the iteration got
+  // longer, 262.5 ms at P = 1 vs 285.3 at P = 4, profiles/r05_ab_bw_pipe.txt; removed in round 6.)
+  // parts: one per chunk
   std::vector<std::vector<std::pair<int64_t, int64_t>>> parts(chunks.size());
-  for (size_t ci = 0; ci < chunks.size(); ++ci) {
-    const int64_t s0 = chunks[ci].first, s1 = chunks[ci].second, E = off0[s1] - off0[s0];
-    int64_t a = s0;
-    for (int p = 1; p <= pipe && a < s1; ++p) {
-      int64_t b = a + 1;
-      while (b < s1 && (p == pipe || off0[b] - off0[s0] < E * p / pipe)) ++b;
-      parts[ci].emplace_back(a, b);
-      a = b;
-    }
-  }
+  for (size_t ci = 0; ci < chunks.size(); ++ci) parts[ci].emplace_back(chunks[ci].first, chunks[ci].second);
   {
     // longest sequences first within each part (indices relative to the part)
     std::vector<int64_t> ord((size_t)nseq);
@@ -4215,23 +4155,6 @@ CV_API cv_status cv_hmm_fit_train(int32_t nstates, int64_t nobs, int64_t nseq, c
         });
       }
     if ((st = upload(d.ord, ord.data(), ord.size() * 8)) != CV_OK) return st;
-  }
-  struct PipeStreams {
-    hipStream_t s[4] = {};
-    hipEvent_t ev[5] = {};  // [0..3] forward done per part, [4] the accumulators zeroed
-    ~PipeStreams() {
-      for (auto x : s)
-        if (x) (void)hipStreamDestroy(x);
-      for (auto x : ev)
-        if (x) (void)hipEventDestroy(x);
-    }
-  } ps;
-  if (pipe > 1) {
-    for (int p = 0; p < pipe; ++p)
-      if (hipStreamCreateWithFlags(&ps.s[p], hipStreamNonBlocking) != hipSuccess)
-        return set_err(CV_EDEVICE, "hipStreamCreate failed");
-    for (auto& x : ps.ev)
-      if (hipEventCreateWithFlags(&x, hipEventDisableTiming) != hipSuccess) return set_err(CV_EDEVICE, "hipEventCreate failed");
   }
   // Arcs below cvf::kBwTinyArc (A's smallest positive entry, checked on the device before every
   // E-step): the E-step then runs on A 2^K and A^T 2^K, K the least that lifts every arc to
@@ -4273,15 +4196,6 @@ CV_API cv_status cv_hmm_fit_train(int32_t nstates, int64_t nobs, int64_t nseq, c
       // earlier parts, so the parts' rows never overlap)
       const int64_t row0 = off0[c.first] - off0[chunks[ci].first];
       hipStream_t ss = nullptr;
-      if (pipe > 1) {
-        ss = ps.s[pi_];
-        if (pi_ == 0) {  // behind the zeroed accumulators and the previous chunk (null stream)
-          HIP_TRY(hipEventRecord(ps.ev[4], nullptr));
-          for (int p = 0; p < pipe; ++p) HIP_TRY(hipStreamWaitEvent(ps.s[p], ps.ev[4], 0));
-        } else {
-          HIP_TRY(hipStreamWaitEvent(ss, ps.ev[pi_ - 1], 0));
-        }
-      }
       cvf::BwArgs g{};
       g.offsets = d.off.as<int64_t>() + c.first;
       g.obs = d.obs.as<int32_t>();
@@ -4304,14 +4218,9 @@ CV_API cv_status cv_hmm_fit_train(int32_t nstates, int64_t nobs, int64_t nseq, c
       g.b_num = A + 3 * N;
       g.xi_s = g.b_num + (size_t)V * N;
       g.xi_zero = g.xi_s + (size_t)N * N;
-      const hipError_t e = cvf::launch_bw_estep(g, c.second - c.first, max_waves, ss, off0[c.second] - off0[c.first],
-                                                pipe > 1 ? ps.ev[pi_] : nullptr);
+      const hipError_t e =
+          cvf::launch_bw_estep(g, c.second - c.first, max_waves, ss, off0[c.second] - off0[c.first], nullptr);
       if (e != hipSuccess) return set_err(CV_EDEVICE, "Baum-Welch launch failed: %s", hipGetErrorString(e));
-      if (pipe > 1 && pi_ + 1 == parts[ci].size())  // the chunk's parts joined on the null stream
-        for (size_t p = 0; p < parts[ci].size(); ++p) {
-          HIP_TRY(hipEventRecord(ps.ev[p], ps.s[p]));
-          HIP_TRY(hipStreamWaitEvent(nullptr, ps.ev[p], 0));
-        }
     }
     // M-step (hmm.rs:145-170) on the device: new_pi = sum gamma_0 / R; new_a = sum xi / a_den
     // (row); new_b = sum gamma at o / b_den; sum_t xi_t = A o S + z / N^2 (see bw_stats);

@@ -42,7 +42,7 @@ struct BwArgs {
   double* beta;         // [elements][N] workspace
   double* rscale;       // [elements] N > 64 matrix-core path: row t of R = alpha_t * rscale[t]
                         // (1 / (c_t 2^k), 0 where c_t = 0 or t = T - 1); null: R is stored over alpha
-  double* gscratch;     // [kBwScratchSeqs][4 N] N > kBwLdsMaxStates (or CV_BW_GLOBAL=1 above 256):
+  double* gscratch;     // [kBwScratchSeqs][4 N] N > kBwLdsMaxStates (or tuning key bw_global above 256):
                         // the strided kernels' per-sequence vectors in global memory
   double* dump;         // [kBwDumpWaves][64] N <= 64 kernels: target of the stores / atomic adds
                         // of lanes without a state (one row per wave: no shared hot line)
@@ -83,12 +83,14 @@ hipError_t launch_mle_counts(const MleArgs& g, int64_t nseq, hipStream_t stream)
 // backward kernel runs at most max_waves waves (each walks several sequences)
 // nrows: the chunk's elements (alpha / beta rows from elem_base), for the GEMM path (N > 128)
 // fwd_done (64 < N <= 256, the matrix-core kernels): recorded on `stream` right after the
-// forward launch (the E-step pipeline of cv_hmm_fit_train staggers its parts on it)
+// forward launch when non-null
 hipError_t launch_bw_estep(const BwArgs& g, int64_t nseq, int64_t max_waves, hipStream_t stream, int64_t nrows,
                            hipEvent_t fwd_done = nullptr);
-// the E-step sequences per pipeline part have the matrix-core kernels (64 < N <= 256)
+// the E-step runs the matrix-core kernels (64 < N <= 256; tuning key bw_perseq = 1: not)
 bool bw_estep_mm(int nstates);
-// CV_BW_GEMM_PATH=1: the per-sequence kernels + xi GEMM at every N (what tiny arcs select)
+// tuning key bw_gemm_path = 1: the per-sequence kernels + xi GEMM at every N (A/B and tests;
+// tiny arcs no longer select it: since round 5 the E-step runs on A 2^K on whichever path N
+// picks, cv_hmm_fit_train)
 bool bw_gemm_path();
 // *out = the bits of the smallest positive a[k], k < n (*out preset to +inf's bits by the caller)
 hipError_t launch_bw_amin(const double* a, int64_t n, unsigned long long* out, hipStream_t stream);

@@ -17,6 +17,7 @@
 #include <algorithm>
 
 #include "fit.h"
+#include "../tuning.h"
 
 namespace cvf {
 
@@ -1573,17 +1574,11 @@ static void launch_wave_estep(const BwArgs& g, int64_t nseq, int64_t nwaves, hip
                      nwaves);
 }
 
-// sequences per workgroup of the 64 < N <= 256 kernels: 16 MT; MT = 2 (default) runs two
-// workgroups per CU, so one's reductions and barriers overlap the other's matrix products;
-// CV_BW_MT=4: one workgroup of 64 per CU
-static int bw_mt() {
-  static const int v = [] {
-    const char* e = getenv("CV_BW_MT");
-    return (e && e[0] == '4') ? 4 : 2;
-  }();
-  return v;
-}
-
+// sequences per workgroup of the 64 < N <= 256 kernels: 16 MT; MT = 2 runs two workgroups per
+// CU, so one's reductions and barriers overlap the other's matrix products (MT = 4, one
+// workgroup of 64 per CU, and eight forward waves per workgroup -- 82.4 vs 79.2 ms at config 4
+// -- measured slower in round 4 and removed in round 6 with the GEMM's one-wave-tile,
+// double-buffered and 32 x 32 variants)
 template <int NP, int MT, int WVF, int WVB>
 static void launch_mm(const BwArgs& g, int64_t nseq, hipStream_t stream, hipEvent_t fwd_done) {
   const dim3 grid((unsigned)((nseq + 16 * MT - 1) / (16 * MT)));
@@ -1592,58 +1587,13 @@ static void launch_mm(const BwArgs& g, int64_t nseq, hipStream_t stream, hipEven
   hipLaunchKernelGGL((bw_bwd_mm<NP, MT, WVB>), grid, dim3(64 * WVB), 0, stream, g, nseq);
 }
 
-// waves per workgroup of the 64 < N <= 256 forward: 4, or with CV_BW_WV=8 eight (two 16-column
-// tiles per wave at 256 states, four waves per SIMD: 82.4 vs 79.2 ms at config 4)
-static int bw_wv() {
-  static const int v = [] {
-    const char* e = getenv("CV_BW_WV");
-    return (e && e[0] == '8') ? 8 : 4;
-  }();
-  return v;
-}
-
-static bool gemm_wave() {  // A/B knob: CV_BW_GEMM_WAVE=1 keeps one wave per 64 x 64 tile
-  static const bool v = [] {
-    const char* e = getenv("CV_BW_GEMM_WAVE");
-    return e && e[0] == '1';
-  }();
-  return v;
-}
-
-static bool gemm_st2() {  // A/B knob: CV_BW_GEMM_ST2=1 double-buffers the GEMM's loads
-  static const bool v = [] {
-    const char* e = getenv("CV_BW_GEMM_ST2");
-#ifdef CVF_GEMM_ST2_DEFAULT
-    return !(e && e[0] == '0');
-#else
-    return e && e[0] == '1';
-#endif
-  }();
-  return v;
-}
-
-static bool gemm32() {  // A/B knob: CV_BW_GEMM32=1 keeps 32 x 32 tiles at every N
-  static const bool v = [] {
-    const char* e = getenv("CV_BW_GEMM32");
-    return e && e[0] == '1';
-  }();
-  return v;
-}
-
-static bool bw_per_seq() {  // A/B knob: CV_BW_PERSEQ=1 keeps one workgroup per sequence
-  static const bool v = [] {
-    const char* e = getenv("CV_BW_PERSEQ");
-    return e && e[0] == '1';
-  }();
-  return v;
-}
+// tuning key bw_perseq = 1 keeps one workgroup per sequence (A/B and tests)
+static bool bw_per_seq() { return cvk::tuning().bw_perseq == 1; }
 
 bool bw_estep_mm(int nstates) { return nstates > kBwWaveStates && nstates <= kBwMmStates && !bw_per_seq(); }
 
-bool bw_gemm_path() {  // A/B knob and tests: CV_BW_GEMM_PATH=1 takes the xi GEMM path at every N
-  const char* e = getenv("CV_BW_GEMM_PATH");  // read per call
-  return e && e[0] == '1';
-}
+// tuning key bw_gemm_path = 1 takes the xi GEMM path at every N (A/B and tests)
+bool bw_gemm_path() { return cvk::tuning().bw_gemm_path == 1; }
 
 hipError_t launch_bw_estep(const BwArgs& g, int64_t nseq, int64_t max_waves, hipStream_t stream, int64_t nrows,
                            hipEvent_t fwd_done) {
@@ -1687,19 +1637,9 @@ hipError_t launch_bw_estep(const BwArgs& g, int64_t nseq, int64_t max_waves, hip
     if (mm) {  // 16 MT sequences per workgroup, the step products on the matrix cores
       // waves per workgroup: forward / backward (the backward's per-step state needs the
       // registers of four waves at 256 states)
-      if (bw_mt() == 4) {
-        if (g.nstates <= 128) launch_mm<128, 4, 4, 4>(g, nseq, stream, fwd_done);
-        else if (g.nstates <= 192) launch_mm<192, 4, 4, 4>(g, nseq, stream, fwd_done);
-        else launch_mm<256, 4, 4, 4>(g, nseq, stream, fwd_done);
-      } else if (bw_wv() == 4) {
-        if (g.nstates <= 128) launch_mm<128, 2, 4, 4>(g, nseq, stream, fwd_done);
-        else if (g.nstates <= 192) launch_mm<192, 2, 4, 4>(g, nseq, stream, fwd_done);
-        else launch_mm<256, 2, 4, 4>(g, nseq, stream, fwd_done);
-      } else {
-        if (g.nstates <= 128) launch_mm<128, 2, 8, 4>(g, nseq, stream, fwd_done);
-        else if (g.nstates <= 192) launch_mm<192, 2, 4, 4>(g, nseq, stream, fwd_done);  // 12 tiles: four waves
-        else launch_mm<256, 2, 8, 4>(g, nseq, stream, fwd_done);
-      }
+      if (g.nstates <= 128) launch_mm<128, 2, 4, 4>(g, nseq, stream, fwd_done);
+      else if (g.nstates <= 192) launch_mm<192, 2, 4, 4>(g, nseq, stream, fwd_done);
+      else launch_mm<256, 2, 4, 4>(g, nseq, stream, fwd_done);
     } else {
       hipLaunchKernelGGL(bw_forward, dim3((unsigned)nseq), dim3(256), 0, stream, g);
       hipLaunchKernelGGL(bw_backward, dim3((unsigned)nseq), dim3(256), 0, stream, g);
@@ -1707,14 +1647,14 @@ hipError_t launch_bw_estep(const BwArgs& g, int64_t nseq, int64_t max_waves, hip
     }
     // 64 x 64 tiles per wave above 128 states (32 x 32 below); ~4,096 waves: row ranges of a
     // multiple of 4 rows per output tile
-    const bool t64 = g.nstates > 128 && !gemm32();
+    const bool t64 = g.nstates > 128;
     const int ts = t64 ? 64 : 32, ntt = (g.nstates + ts - 1) / ts;
     const int64_t parts = std::max<int64_t>(1, std::min<int64_t>(4096 / (ntt * ntt), (nrows + 255) / 256));
     const int64_t per = ((nrows + parts - 1) / parts + 3) / 4 * 4;
     const int64_t np = (nrows + per - 1) / per;
     // a multiple of 8 row ranges (empty ones exit): the XCD-aware block mapping of bw_xi_gemm
     const dim3 grid((unsigned)((np + 7) / 8 * 8 * ntt * ntt)), block(64);
-    if (t64 && !gemm_wave()) {
+    if (t64) {
       // 128 x 128 per workgroup: ~2 workgroups per CU over 256 CUs
       const int nt = (g.nstates + 127) / 128;
       const int64_t parts2 = std::max<int64_t>(1, std::min<int64_t>(512 / (nt * nt), (nrows + 255) / 256));
@@ -1722,12 +1662,9 @@ hipError_t launch_bw_estep(const BwArgs& g, int64_t nseq, int64_t max_waves, hip
       const int64_t np2 = (nrows + per2 - 1) / per2;
       hipLaunchKernelGGL(bw_xi_gemm_lds, dim3((unsigned)((np2 + 7) / 8 * 8 * nt * nt)), dim3(256), 0, stream, gg, nrows,
                          per2);
-    } else if (t64 && gemm_st2())
-      hipLaunchKernelGGL((bw_xi_gemm<4, 2>), grid, block, 0, stream, gg, nrows, per);
-    else if (t64)
-      hipLaunchKernelGGL((bw_xi_gemm<4, 1>), grid, block, 0, stream, gg, nrows, per);
-    else
+    } else {
       hipLaunchKernelGGL((bw_xi_gemm<2, 1>), grid, block, 0, stream, gg, nrows, per);
+    }
     return hipGetLastError();
   }
   if (g.nstates <= kBwWaveStates) {

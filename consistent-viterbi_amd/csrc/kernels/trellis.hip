@@ -36,6 +36,7 @@
 #include <algorithm>
 
 #include "trellis.h"
+#include "../tuning.h"
 
 namespace cvk {
 
@@ -1367,20 +1368,19 @@ __global__ __launch_bounds__(256) void generic_wide_step(GenericFwdArgs<REAL> ar
 }
 
 // slots per wide workgroup: 4 once that still gives >= one workgroup per CU (256 CUs), else 1
-// (S = 2 was never the fastest: profiles/r05_wide_crossover.txt); CV_WIDE_S=k sets it (1, 2 or
-// 4; read per launch: A/B knob and tests, bit-identical)
+// (S = 2 was never the fastest: profiles/r05_wide_crossover.txt); tuning key wide_s = k sets it
+// (1, 2 or 4; A/B and tests, bit-identical)
 inline int generic_wide_seqs(int n, int64_t nseq) {
-  if (const char* e = getenv("CV_WIDE_S")) return atoi(e) >= 4 ? 4 : atoi(e) >= 2 ? 2 : 1;
+  if (const int k = tuning().wide_s; k > 0) return k >= 4 ? 4 : k >= 2 ? 2 : 1;
   return (nseq + 3) / 4 * ((n + 255) / 256) >= 256 ? 4 : 1;
 }
 
 template <typename REAL, int S>
 hipError_t launch_generic_wide_s(const GenericFwdArgs<REAL>& fa, int64_t nseq, hipStream_t stream) {
   const int nblk = (fa.nstates + 255) / 256;
-  // XCD-aware column blocks when they come in eights (CV_WIDE_XCD=0: never; A/B knob, read per
-  // launch, bit-identical)
-  const char* xe = getenv("CV_WIDE_XCD");
-  const int xcd = (nblk % 8 == 0 && !(xe && *xe == '0')) ? 1 : 0;
+  // XCD-aware column blocks when they come in eights (no measurable difference at N = 10,240,
+  // 273.5 vs 273.3 ms; the CV_WIDE_XCD A/B knob was removed in round 6)
+  const int xcd = nblk % 8 == 0 ? 1 : 0;
   const int64_t grid = (nseq + S - 1) / S * nblk;
   if (grid > (int64_t)INT32_MAX) return hipErrorInvalidValue;
   for (int64_t t = 0; t < fa.wide_steps; ++t) {
@@ -1404,8 +1404,8 @@ hipError_t launch_generic_wide(const GenericFwdArgs<REAL>& fa, int64_t nseq, hip
 
 bool generic_wide(int n, int real_bytes, int64_t nseq, bool cp) {
   if (n > generic_max_states(real_bytes)) return true;
-  if (const char* e = getenv("CV_GENERIC_WIDE_MIN"); e && *e) return n >= atoi(e);
-  if (const char* e = getenv("CV_GENERIC_WIDE"); e && *e == '0') return false;
+  if (const int m = tuning().generic_wide_min; m > 0) return n >= m;  // tuning keys (A/B and tests)
+  if (tuning().generic_wide == 0) return false;
   return n > 1024 && (cp || nseq < 4096 || n > 3072);
 }
 
@@ -2146,9 +2146,8 @@ static hipError_t trellis_fwd2_np(const TrellisFwdArgs& fa, int64_t npairs, hipS
     return hipErrorInvalidValue;
   } else {
     if (fa.ranges || fa.reverse || fa.last_row || fa.start || !fa.delta) return hipErrorInvalidValue;
-    // A/B knob CV_F32_ONEBAR=0/1 (bit-identical; read per launch)
-    const char* e = getenv("CV_F32_ONEBAR");
-    const bool onebar = e ? e[0] == '1' : kF32OneBarDefault;
+    // tuning key f32_onebar = 0 / 1 (bit-identical)
+    const bool onebar = kF32OneBarDefault && tuning().f32_onebar != 0;
     const dim3 grid((unsigned)npairs), block(NP * 4);
     if (fa.forced && onebar)
       hipLaunchKernelGGL((trellis_fwd2_f32<NP, true, true>), grid, block, 0, stream, fa);
@@ -2212,13 +2211,13 @@ hipError_t launch_trellis_bt(int np, const BacktrackArgs& ba, int64_t nseq, hipS
 }
 
 // sequences per workgroup of generic_fwd_ms: 4 while their rows fit the LDS and the launch
-// keeps >= 2 workgroups per CU (256 CUs), else fewer; 1 = generic_fwd.  CV_GENERIC_S=k sets it
-// (1, 2 or 4 where the rows fit; read per launch: A/B knob and tests, bit-identical)
+// keeps >= 2 workgroups per CU (256 CUs), else fewer; 1 = generic_fwd.  Tuning key generic_s = k
+// sets it (1, 2 or 4 where the rows fit; A/B and tests, bit-identical)
 template <typename REAL>
 int generic_seqs_per_wg(int n, int64_t nseq) {
   auto fits = [&](int s) { return 2 * (size_t)s * n * sizeof(REAL) <= 160 * 1024; };
-  if (const char* e = getenv("CV_GENERIC_S")) {
-    int s = atoi(e) >= 4 ? 4 : atoi(e) >= 2 ? 2 : 1;
+  if (const int k = tuning().generic_s; k > 0) {
+    int s = k >= 4 ? 4 : k >= 2 ? 2 : 1;
     while (s > 1 && !fits(s)) s /= 2;
     return s;
   }
@@ -2252,10 +2251,13 @@ hipError_t launch_generic_fwd(const GenericFwdArgs<REAL>& fa, int64_t nseq, hipS
     }
   }
   int s = generic_seqs_per_wg<REAL>(fa.nstates, nseq);
-  // psi mode from 256 sequences on: two per workgroup (each A load serves both, the walk
+  // CP psi mode from 256 sequences on: two per workgroup (each A load serves both, the walk
   // unrolled) -- the chain's speculative batch (~620 sequences at N = 256) 11.9 -> 8.5 ms
-  // (profiles/r05_ab_spec_s2.txt); below, one per workgroup keeps more of them in flight
-  if (s == 1 && nseq >= 256 && !getenv("CV_GENERIC_S") && 4 * (size_t)fa.nstates * sizeof(REAL) <= 160 * 1024) s = 2;
+  // (profiles/r05_ab_spec_s2.txt); below, one per workgroup keeps more of them in flight.  The
+  // CP association only: the case that was measured
+  if (s == 1 && nseq >= 256 && fa.assoc == CVK_ASSOC_CP && tuning().generic_s == 0 &&
+      4 * (size_t)fa.nstates * sizeof(REAL) <= 160 * 1024)
+    s = 2;
   switch (s) {
     case 4: return launch_generic_ms<REAL, 4, false>(fa, nseq, stream);
     case 2: return launch_generic_ms<REAL, 2, false>(fa, nseq, stream);
@@ -2264,18 +2266,16 @@ hipError_t launch_generic_fwd(const GenericFwdArgs<REAL>& fa, int64_t nseq, hipS
   // one sequence per workgroup: one thread per state up to N = 1,024 (64 ceil(N / 64) threads;
   // generic_fwd's 256 threads walk 4 states each at N = 1,024 -- a handful of sequences, e.g.
   // the parallel chain's speculative re-decodes, then ran latency-bound on a few CUs).
-  // CV_GENERIC_SPLIT=1 (A/B knob, read per launch, bit-identical): K threads per state split
+  // tuning key generic_split = 1 (A/B and tests, bit-identical): K threads per state split
   // each state's candidates (generic_fwd_split) -- measured neutral on the chain's speculative
   // batch (12.4 vs 12.2 ms, profiles/r05_ab_spec_s.txt), so off by default
   {
     const int nt = (fa.nstates + 63) / 64 * 64;
-    const char* se = getenv("CV_GENERIC_SPLIT");
-    const bool split = se && *se == '1';
+    const bool split = tuning().generic_split == 1;
     // K: at most 512 threads per workgroup, so four workgroups fit a CU and a batch of ~1,000
     // sequences runs in one round (1,024-thread workgroups: two per CU, a second round at 620
-    // sequences); CV_GENERIC_SPLIT_K=2/4/8 sets it (A/B knob)
-    const char* ke = getenv("CV_GENERIC_SPLIT_K");
-    int K = ke && *ke ? atoi(ke) : 512 / nt;
+    // sequences); tuning key generic_split_k = 2 / 4 / 8 sets it
+    int K = tuning().generic_split_k > 0 ? tuning().generic_split_k : 512 / nt;
     K = K >= 8 ? 8 : K >= 4 ? 4 : K >= 2 ? 2 : 1;
     while (K > 1 && nt * K > 1024) K /= 2;
     if (split && K >= 2 && fa.nstates <= 512) {
@@ -2437,8 +2437,8 @@ __global__ __launch_bounds__(256) void generic_ext_wide_step(GenericExtArgs g, i
 
 bool generic_ext_wide(int n) {
   if (n > generic_max_states(8)) return true;
-  const char* e = getenv("CV_EXT_WIDE_MIN");
-  return e && *e && n >= atoi(e);
+  const int m = tuning().ext_wide_min;  // tuning key (A/B and tests)
+  return m > 0 && n >= m;
 }
 
 hipError_t launch_generic_ext(const GenericExtArgs& g, int64_t nslots, hipStream_t stream) {

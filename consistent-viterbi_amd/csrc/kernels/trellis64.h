@@ -73,6 +73,9 @@ struct T64BtArgs {
                            // all in [-2^80, 0]: the NONPOS interval test (null: f64 test)
   int only_infeasible;     // set by launch_t64_bt: the general kernel's viterbi::decode pass over
                            // the infeasible sequences the NONPOS kernel left (their DEC chain)
+  double* cert;            // non-null (NONPOS row A0, NP <= 256): the parallel chain's certificate
+                           // (rho, gF) per sequence [2 nseq], as cp_cert_f64 computes it
+  double rho_cap;          // steps whose estimated certificate term reaches it skip the exact gap
 };
 
 // Delta rows of the f64 trellis (forward -> backtrack, resume-flow prefix rows) use a
@@ -202,16 +205,16 @@ constexpr int kChainMaxStates = 65535;
 constexpr int kChainLdsMaxStates = 10240;
 // the wide chain runs above N = 1,024 (one workgroup then strides its states: 0.18 vs 0.08 ms
 // per element at N = 1,100, 17 vs 1.1 ms at 10,240 -- profiles/r05_wide_crossover.txt); read
-// per call (A/B knobs and tests, bit-identical): CV_CHAIN_WIDE=0 only above N = 10,240,
-// CV_CHAIN_WIDE_MIN=n from n states
+// (tuning keys, bit-identical): chain_wide = 0 only above N = 10,240, chain_wide_min = n from n
+// states
 bool cp_chain_wide(int n);
 hipError_t launch_cp_superseq_chain(const CpChainArgs& g, hipStream_t stream);
 
 // NP = 64 * ceil(N / 64) for 1 <= N <= 256, else 0 (no f64 trellis kernel)
 int t64_padded_states(int n);
 // the batch decode's NP under CV_KERNEL_AUTO: t64_padded_states, 512 for 256 < N <= 512
-// (column-split pairs of waves), 1,024 for 724 < N <= 1,024 (quads; CV_T64_512 / CV_T64_1024
-// knobs); 0 = the generic kernels
+// (column-split pairs of waves), 1,024 for 724 < N <= 1,024 (quads; tuning keys t64_512 /
+// t64_1024); 0 = the generic kernels
 int t64_batch_states(int n);
 // every NP the kernels support at this N (64..256 padded, 512, 1,024; 0 above): what an
 // explicit CV_KERNEL_TRELLIS_F64 request gets and what the handle's t64 tables are padded to
@@ -219,15 +222,10 @@ int t64_support_states(int n);
 // sequences per forward wave (2, 4 or 8) for a launch of nseq sequences on `cus` CUs
 int t64_seqs_per_wave(int64_t nseq, int cus, int np = 0);
 hipError_t launch_t64_fwd(int np, int s, const T64FwdArgs& fa, int64_t nseq, hipStream_t stream);
-// N <= 64 row-A0 decodes of NONPOS models: forward and backtrack in one launch (each wave
-// backtracks its own sequence after its forward pass); t64_wave_fusable says when it applies
-bool t64_wave_fusable(int np, const T64FwdArgs& fa, const T64BtArgs& ba);
-hipError_t launch_t64_wave_fused(const T64FwdArgs& fa, const T64BtArgs& ba, int64_t nseq, hipStream_t stream);
 // CP association (cp.rs:70-79): psi and the CP value d[psi] + (a[psi,j] + b[j,o]) in the forward
 // sequences per wave the CP forward launches for a requested s and batch size
 int t64_cp_seqs_per_wave(int s, int64_t nseq);
 hipError_t launch_t64_cp_fwd(int np, int s, const T64FwdArgs& fa, int64_t nseq, hipStream_t stream);
-// max_wgs > 0: at most that many 4-wave workgroups, each looping over the slots (persistent)
-hipError_t launch_t64_bt(int np, const T64BtArgs& ba, int64_t nseq, hipStream_t stream, int max_wgs = 0);
+hipError_t launch_t64_bt(int np, const T64BtArgs& ba, int64_t nseq, hipStream_t stream);
 
 }  // namespace cvk

@@ -32,6 +32,7 @@
 #include "trellis64.h"
 #include "wave64.h"
 #include "wide.h"
+#include "../tuning.h"
 
 namespace cvk {
 
@@ -1147,11 +1148,24 @@ __device__ __forceinline__ int first_argmax_d(const double (&s)[KP], const bool 
 // inside the remaining slack.  Half the L2 bytes of the f64 a^T column, a DPP wave max in
 // place of six ds_bpermute rounds, and no per-candidate bound arithmetic.  |x| < 2^112 for
 // T < 2^31, so no estimate overflows f32.
-template <int KP, int PF, bool DEC = false, bool NONPOS = false>
+//
+// CERT (NONPOS row A0 only, the parallel CPSolver chain): the backtrack also reduces the path's
+// gaps to the chain certificate rho of cp_cert_f64 (kernels/chain.hip), so no second pass
+// re-reads every row.  gap_t = s_path - max_{i != path} s_i is bounded BELOW from the step's f32
+// estimates -- s_path >= x_path (1 + c') and s_i <= x_i (1 - c') with c' = 1.5 * 2^-20 > c, both
+// <= 0 -- and the step's term r_t = (gap_t - (4t + 1) u0) / (3t + 1) taken from that bound when
+// it already reaches rho_cap; below it the lo plane is read and the exact f64 gap used, as
+// cp_cert_f64 does.  So the returned rho equals cp_cert_f64's exact rho whenever that is below
+// rho_cap, and is >= rho_cap otherwise: the host's tests rho > U agree with the exact
+// certificate for every U <= rho_cap (the host sizes rho_cap above the largest U it can test).
+template <int KP, int PF, bool DEC = false, bool NONPOS = false, bool CERT = false>
 __device__ __forceinline__ void bt_chain_f64(const uint32_t* __restrict__ rows, int T, int cur, int32_t* __restrict__ path,
                                              const double* __restrict__ at, const double* __restrict__ et,
                                              const int32_t* __restrict__ obs, int dp_assoc, int N, int lane,
-                                             const float* __restrict__ at32 = nullptr) {
+                                             const float* __restrict__ at32 = nullptr, double* rho_io = nullptr,
+                                             double u0 = 0.0, double rho_cap = 0.0) {
+  static_assert(!CERT || (NONPOS && !DEC), "certificates: the NONPOS row-A0 chain");
+  double rho = CERT ? *rho_io : 0.0;
   constexpr int NP = 64 * KP;
   constexpr uint32_t NINF_HI = 0xFFF00000u;  // hi word of -inf (lo word 0)
   bool valid[KP];
@@ -1214,9 +1228,25 @@ __device__ __forceinline__ void bt_chain_f64(const uint32_t* __restrict__ rows, 
           cnt += __builtin_popcountll(mask);
           if (mask) idx = 64 * k + __builtin_ctzll(mask);
         }
-        if (cnt == 1) {
+        bool exact = cnt != 1;
+        if constexpr (CERT) {
+          if (!exact) {  // the gap's lower bound from the estimates (x_path = M: the unique survivor)
+            float lo = -__builtin_inff();
+#pragma unroll
+            for (int k = 0; k < KP; ++k) lo = __builtin_fmaxf(lo, (64 * k + lane == idx) ? -__builtin_inff() : x[k]);
+            const double O = (double)wave_max_f32(lo), Md = (double)M;
+            const double lb = Md * (1.0 + 0x3p-21) - O * (1.0 - 0x3p-21) - __builtin_fabs(Md) * 0x1p-50 - 0x1p-99;
+            const double r = (lb - (double)(4 * t + 1) * u0) / (double)(3 * t + 1);
+            if (r >= rho_cap) {
+              rho = fmin(rho, r);
+            } else {
+              exact = true;
+            }
+          }
+        }
+        if (!exact) {
           cur = idx;
-        } else {  // near tie: the exact f64 sums of this row decide (first index)
+        } else {  // near tie (or a certificate step below rho_cap): the exact f64 sums decide (first index)
           const double* acol = at + (size_t)cur * NP + lane;
           uint32_t lw[KP];
           load_lo(t - 1, lw);
@@ -1228,6 +1258,14 @@ __device__ __forceinline__ void bt_chain_f64(const uint32_t* __restrict__ rows, 
                              : ninf_d();
           double Md;
           cur = first_argmax_d<KP>(sx, valid, Md);
+          if constexpr (CERT) {  // the exact gap: the path's candidate minus the best other one
+            double o = ninf_d();
+#pragma unroll
+            for (int k = 0; k < KP; ++k) o = fmax(o, (64 * k + lane == cur) ? ninf_d() : sx[k]);
+            const double m2 = wave_max_d(o);
+            rho = fmin(rho, (Md - m2 - (double)(4 * t + 1) * u0) / (double)(3 * t + 1));
+            if (!(Md > ninf_d())) rho = -1.0;
+          }
         }
         const int tp = t - 1;
         if (lane == (tp & 63)) pathreg = cur;
@@ -1284,6 +1322,7 @@ __device__ __forceinline__ void bt_chain_f64(const uint32_t* __restrict__ rows, 
 #pragma unroll
     for (int u = 0; u < PF; ++u) load_hi(base - PF - 1 - u, ring[u]);
   }
+  if constexpr (CERT) *rho_io = rho;
 }
 
 // NONPOS: the kernel holds only the NONPOS chain (fewer VGPRs, more waves per SIMD); the
@@ -1291,7 +1330,9 @@ __device__ __forceinline__ void bt_chain_f64(const uint32_t* __restrict__ rows, 
 // g.at32 is set.
 // prior_in >= 0: the sequence's status as its forward pass left it, passed in registers (the
 // fused N <= 64 kernel: a uniform load of g.status could come from a stale scalar-cache line)
-template <int KP, int PF, bool NONPOS>
+// CERT: the chain certificate (rho, gF) of cp_cert_f64 into g.cert[2 seq], computed along the way
+// (bt_chain_f64 CERT); -1 for sequences that are not OK.
+template <int KP, int PF, bool NONPOS, bool CERT = false>
 __device__ __forceinline__ void backtrack_one_f64(const T64BtArgs& g, int64_t slot, int lane, int prior_in = -1) {
   constexpr int NP = 64 * KP;
   const int64_t seq = g.order ? (int64_t)g.order[slot] : slot;
@@ -1302,6 +1343,7 @@ __device__ __forceinline__ void backtrack_one_f64(const T64BtArgs& g, int64_t sl
     if (lane == 0) {
       g.score[seq] = 0.0;
       g.status[seq] = CVK_SEQ_EMPTY;
+      if constexpr (CERT) g.cert[2 * seq] = -1.0, g.cert[2 * seq + 1] = -1.0;
     }
     return;
   }
@@ -1312,6 +1354,7 @@ __device__ __forceinline__ void backtrack_one_f64(const T64BtArgs& g, int64_t sl
   for (int k = 0; k < KP; ++k) valid[k] = (lane + 64 * k) < N;
   double bv;
   int cur;
+  double gF = -1.0, rho = -1.0, u0 = 0.0;
   {
     double last[KP];
 #pragma unroll
@@ -1321,6 +1364,15 @@ __device__ __forceinline__ void backtrack_one_f64(const T64BtArgs& g, int64_t sl
                          : ninf_d();
     }
     cur = first_argmax_d<KP>(last, valid, bv);  // cp.rs:86
+    if constexpr (CERT) {  // the last row's top-2 gap (cp_cert_f64's gapF)
+      double o = ninf_d();
+#pragma unroll
+      for (int k = 0; k < KP; ++k) o = fmax(o, (64 * k + lane == cur) ? ninf_d() : last[k]);
+      const double m2 = wave_max_d(o);
+      u0 = (__builtin_fabs(bv) + 16.0) * 0x1p-51;
+      gF = bv - m2 - 4.0 * (double)T * u0;  // +inf when the row has one finite entry
+      rho = gF / (double)(3 * T + 2);
+    }
   }
   const uint8_t prior = prior_in >= 0 ? (uint8_t)prior_in : g.status[seq];
   if (!(bv > ninf_d()) || prior == CVK_SEQ_BADOBS) {
@@ -1334,17 +1386,27 @@ __device__ __forceinline__ void backtrack_one_f64(const T64BtArgs& g, int64_t sl
     if (lane == 0) {
       g.score[seq] = ninf_d();
       g.status[seq] = prior == CVK_SEQ_BADOBS ? CVK_SEQ_BADOBS : CVK_SEQ_INFEASIBLE;
+      if constexpr (CERT) g.cert[2 * seq] = -1.0, g.cert[2 * seq + 1] = -1.0;
     }
     return;
   }
   if (!NONPOS && g.only_infeasible) return;  // feasible: done by the NONPOS kernel
-  if constexpr (NONPOS)
+  if constexpr (CERT)
+    bt_chain_f64<KP, PF, false, true, true>(rows, T, cur, path, g.at, g.et, g.obs + e0, g.dp_assoc, N, lane, g.at32,
+                                            &rho, u0, g.rho_cap);
+  else if constexpr (NONPOS)
     bt_chain_f64<KP, PF, false, true>(rows, T, cur, path, g.at, g.et, g.obs + e0, g.dp_assoc, N, lane, g.at32);
   else
     bt_chain_f64<KP, PF>(rows, T, cur, path, g.at, g.et, g.obs + e0, g.dp_assoc, N, lane);
   if (lane == 0) {
     g.score[seq] = bv;
     g.status[seq] = CVK_SEQ_OK;
+    if constexpr (CERT) {
+      // the divisions and subtractions round: a relative 2^-50 covers them (as cp_cert_f64)
+      const bool pass = rho > 0.0;
+      g.cert[2 * seq] = pass ? rho * (1.0 - 0x1p-50) : -1.0;
+      g.cert[2 * seq + 1] = pass ? gF * (1.0 - 0x1p-50) : -1.0;
+    }
   }
 }
 
@@ -1354,7 +1416,7 @@ __device__ __forceinline__ void backtrack_one_f64(const T64BtArgs& g, int64_t sl
 // NONPOS at NP = 64: the f32 a^T (16 KiB) is staged in LDS, so the one dependent read of each
 // chain step is an LDS round trip instead of an L2 one (the longest chains set the makespan
 // of ragged batches, config 3).
-template <int KP, int PF, bool NONPOS = false, bool PERSIST = false>
+template <int KP, int PF, bool NONPOS = false, bool CERT = false>
 __global__ __launch_bounds__(256) void backtrack_f64(T64BtArgs g) {
   constexpr bool LDS_AT = NONPOS && KP == 1;
   __shared__ float at_lds[LDS_AT ? 64 * 64 : 1];
@@ -1365,12 +1427,7 @@ __global__ __launch_bounds__(256) void backtrack_f64(T64BtArgs g) {
   }
   const int lane = threadIdx.x & 63;
   const int64_t slot0 = g.seq_begin + (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if constexpr (PERSIST) {  // the loop costs VGPRs (60 -> 76 at NP = 256): overlap mode only
-    const int64_t stride = (int64_t)gridDim.x * 4;
-    for (int64_t slot = slot0; slot < g.seq_end; slot += stride) backtrack_one_f64<KP, PF, NONPOS>(g, slot, lane);
-  } else if (slot0 < g.seq_end) {
-    backtrack_one_f64<KP, PF, NONPOS>(g, slot0, lane);
-  }
+  if (slot0 < g.seq_end) backtrack_one_f64<KP, PF, NONPOS, CERT>(g, slot0, lane);
 }
 
 // Resume flow (f64): the prefix [offsets[seq], t1] of every constrained sequence backtracked
@@ -1534,31 +1591,17 @@ __global__ void resume_rows_f64(const double* last, const int32_t* state, int np
   if (j < np) out[i * np + j] = (j == state[i]) ? last[i * np + j] : ninf_d();
 }
 
-// test knob: CV_T64_WG_FORCE=1 takes the eight-wave layout whatever the batch (T64FwdArgs::wg_ok)
-bool wg_force() {
-  static const bool f = [] {
-    const char* e = getenv("CV_T64_WG_FORCE");
-    return e && e[0] == '1';
-  }();
-  return f;
-}
+// tuning key t64_wg_force = 1 takes the eight-wave layout whatever the batch (T64FwdArgs::wg_ok)
+bool wg_force() { return tuning().t64_wg_force != 0; }
 
 // S sequences over a PAIR of waves (C = 2 each, N = 256): the small-batch layout
 template <int S>
 hipError_t fwd_w2(const T64FwdArgs& fa, int64_t nseq, bool ext, hipStream_t stream) {
   const dim3 grid((unsigned)((nseq + S - 1) / S)), block(128);
-  static const bool ldsfirst = [] {  // A/B knob (bit-identical), as in fwd_cs
-    const char* e = getenv("CV_T64_LDSFIRST");
-    return !(e && e[0] == '0');
-  }();
-  static const bool rs_mode = [] {  // A/B knob (bit-identical): CV_T64_RS=0 keeps the column split
-    const char* e = getenv("CV_T64_RS");
-    return !(e && e[0] == '0');
-  }();
-  static const int wg_mode = [] {  // A/B knob (bit-identical), as in fwd_cs: 0 = one pair per workgroup
-    const char* e = getenv("CV_T64_WG");
-    return e ? atoi(e) : 4;
-  }();
+  // tuning keys (bit-identical): t64_rs = 0 keeps the column split, t64_wg = 0 one pair per
+  // workgroup
+  const bool rs_mode = tuning().t64_rs != 0;
+  const bool wg_mode = tuning().t64_wg != 0;
   if (ext) {
     hipLaunchKernelGGL((trellis_fwd_f64<2, S, 8, false, true, 2>), grid, block, 0, stream, fa);
     return hipGetLastError();
@@ -1572,66 +1615,33 @@ hipError_t fwd_w2(const T64FwdArgs& fa, int64_t nseq, bool ext, hipStream_t stre
       return hipGetLastError();
     }
   }
-  if (wg_mode > 0 && (fa.wg_ok || wg_force())) {
+  if (wg_mode && (fa.wg_ok || wg_force())) {
     // four pairs per workgroup (the CU's eight waves), SIMD partners trade priority
     T64FwdArgs f4 = fa;
     f4.balance = 0;
     hipLaunchKernelGGL((trellis_fwd_f64<2, S, 8, false, false, 2, true, 2, 1, true, 4, 2>),
                        dim3((unsigned)((nseq + 4 * S - 1) / (4 * S))), dim3(512), 0, stream, f4);
-  } else if (!ldsfirst)
-    hipLaunchKernelGGL((trellis_fwd_f64<2, S, 8, false, false, 2, true, 2, 1, false>), grid, block, 0, stream, fa);
-  else
+  } else {
     hipLaunchKernelGGL((trellis_fwd_f64<2, S, 8, false, false, 2>), grid, block, 0, stream, fa);
+  }
   return hipGetLastError();
 }
 
-// A/B knob CV_T64_PERSIST=1: the constrained passes from a work queue (persistent waves) instead
-// of one workgroup per unit.  Rejected: config 5 160.5 vs 154.9 ms (profiles/r04_ab_c5_persist.txt)
-// -- 4,096 units over 2,048 waves is two units a wave, so the queue cannot even out the ragged tail
-bool persist_ext() {
-  static const bool on = [] {
-    const char* e = getenv("CV_T64_PERSIST");
-    return e && e[0] == '1';
-  }();
-  return on;
-}
-
-// compute units of the current device (queried once)
-int device_cus() {
-  static const int n = [] {
-    int dev = 0, cus = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) {
-      (void)hipGetLastError();
-      cus = 256;
-    }
-    return cus > 0 ? cus : 256;
-  }();
-  return n;
-}
+// (Round 4 also ran the constrained passes from a work queue of persistent waves, CV_T64_PERSIST:
+// config 5 160.5 vs 154.9 ms, profiles/r04_ab_c5_persist.txt -- 4,096 units over 2,048 waves is
+// two units a wave, so the queue cannot even out the ragged tail.  Removed in round 6, with the
+// deferred delta stores (DEFST, +1.4%), the compiler-placed delta reads (LDSFIRST = false), the
+// 4-row A ring and the partial eight-wave mechanisms (CV_T64_WG = 1..3).)
 
 template <int C, int S>
 hipError_t fwd_cs(const T64FwdArgs& fa, int64_t nseq, hipStream_t stream) {
   const int64_t blocks = (nseq + S - 1) / S;
-  static const int pf = [] {  // tuning knob (bit-identical): A rows in flight, 8 (default) or 4
-    const char* e = getenv("CV_T64_PF");
-    return e ? atoi(e) : 8;
-  }();
-  static const bool ldsfirst = [] {  // A/B knob (bit-identical): CV_T64_LDSFIRST=0, compiler-placed delta reads
-    const char* e = getenv("CV_T64_LDSFIRST");
-    return !(e && e[0] == '0');
-  }();
-  // A/B knob (bit-identical): CV_T64_WG = 1 + SYNC bits (1: barrier per step, 2: SIMD-pair
-  // priority trade) runs the batch decode as eight independent waves per workgroup; default 4
-  // (both), 0 = one wave per workgroup with the global SIMD balancing (round-2 layout).  Config
-  // 4 forward 136.4 -> 131.4 ms, 8,192 sequences 18.6 -> 17.7 ms (profiles/r03_ab_wg.txt)
-  static const int wg_mode = [] {
-    const char* e = getenv("CV_T64_WG");
-    return e ? atoi(e) : 4;
-  }();
-  static const bool w2 = [] {  // A/B knob (bit-identical): CV_T64_W2=0 keeps one wave per group
-    const char* e = getenv("CV_T64_W2");
-    return !(e && e[0] == '0');
-  }();
+  // tuning key t64_wg (bit-identical): 1 runs the batch decode as eight independent waves per
+  // workgroup with a barrier per step and the SIMD-pair priority trade (default), 0 = one wave
+  // per workgroup with the global SIMD balancing (round-2 layout).  Config 4 forward 136.4 ->
+  // 131.4 ms, 8,192 sequences 18.6 -> 17.7 ms (profiles/r03_ab_wg.txt)
+  const bool wg_mode = tuning().t64_wg != 0;
+  const bool w2 = tuning().t64_w2 != 0;  // tuning key t64_w2 = 0 keeps one wave per group
   const bool ext = fa.forced || fa.ranges || fa.reverse || fa.start || fa.row_base || fa.resume_rows ||
                    fa.slot_order || fa.last_row;
   // S = 6: three waves per SIMD (<= 168 VGPRs, 12.3 KiB of LDS each), batch decode only
@@ -1651,34 +1661,16 @@ hipError_t fwd_cs(const T64FwdArgs& fa, int64_t nseq, hipStream_t stream) {
   // C >= 3 only: at C <= 2 the one-wave workgroups fit three or more waves per SIMD, which beat
   // two aligned ones (N = 128: 37.7 vs 38.1 ms; N = 192: 84.4 -> 81.1 ms; profiles/r03_ab_wg.txt)
   if constexpr (S == 8 && C >= 3) {
-    static const bool defst = [] {  // A/B knob (bit-identical): CV_T64_DEFST=1, deferred delta stores
-      const char* e = getenv("CV_T64_DEFST");
-      return e && e[0] == '1';
-    }();
-    static const bool wg_ext = [] {  // A/B knob (bit-identical): CV_T64_WG_EXT=1, the constrained passes too
-      const char* e = getenv("CV_T64_WG_EXT");
-      return e && e[0] == '1';
-    }();
-    if (wg_mode > 0 && !fa.dp_assoc && (ext ? (wg_ext || fa.wg_ok != 0) : (fa.wg_ok != 0 || wg_force()))) {
+    // the constrained passes (EXT) take it too from two rounds of workgroups on (fa.wg_ok)
+    if (wg_mode && !fa.dp_assoc && (fa.wg_ok != 0 || wg_force())) {
       // eight independent waves per workgroup (two per SIMD), A-row reads kept together
       const dim3 g8((unsigned)((nseq + 8 * S - 1) / (8 * S))), b8(512);
       T64FwdArgs f8 = fa;
       f8.balance = 0;
-      if (ext) {
+      if (ext)
         hipLaunchKernelGGL((trellis_fwd_f64<C, S, 8, false, true, 1, false, 2, 1, true, 8, 3>), g8, b8, 0, stream, f8);
-        return hipGetLastError();
-      }
-      switch (wg_mode - 1) {
-        case 1: hipLaunchKernelGGL((trellis_fwd_f64<C, S, 8, false, false, 1, false, 2, 1, true, 8, 1>), g8, b8, 0, stream, f8); break;
-        case 2: hipLaunchKernelGGL((trellis_fwd_f64<C, S, 8, false, false, 1, false, 2, 1, true, 8, 2>), g8, b8, 0, stream, f8); break;
-        case 3:
-          if (defst)
-            hipLaunchKernelGGL((trellis_fwd_f64<C, S, 8, false, false, 1, false, 2, 1, true, 8, 3, true>), g8, b8, 0, stream, f8);
-          else
-            hipLaunchKernelGGL((trellis_fwd_f64<C, S, 8, false, false, 1, false, 2, 1, true, 8, 3>), g8, b8, 0, stream, f8);
-          break;
-        default: hipLaunchKernelGGL((trellis_fwd_f64<C, S, 8, false, false, 1, false, 2, 1, true, 8, 0>), g8, b8, 0, stream, f8); break;
-      }
+      else
+        hipLaunchKernelGGL((trellis_fwd_f64<C, S, 8, false, false, 1, false, 2, 1, true, 8, 3>), g8, b8, 0, stream, f8);
       return hipGetLastError();
     }
   }
@@ -1688,20 +1680,8 @@ hipError_t fwd_cs(const T64FwdArgs& fa, int64_t nseq, hipStream_t stream) {
       hipLaunchKernelGGL((trellis_fwd_f64<C, S, 8, true, false>), grid, block, 0, stream, fa);
     else
       return hipErrorInvalidValue;
-  } else if (ext && fa.queue && persist_ext()) {
-    // the ragged constrained passes from a work queue: two waves per SIMD, each taking units
-    const int64_t units = (nseq + S - 1) / S;
-    const int64_t waves = std::min<int64_t>(units, 2 * 4 * (int64_t)device_cus());
-    hipError_t e = hipMemsetAsync(fa.queue, 0, sizeof(int), stream);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((trellis_fwd_f64<C, S, 8, false, true, 1, false, 2, 1, true, 1, 0, false, true>),
-                       dim3((unsigned)waves), block, 0, stream, fa);
   } else if (ext) {
     hipLaunchKernelGGL((trellis_fwd_f64<C, S, 8, false, true>), grid, block, 0, stream, fa);
-  } else if (pf == 4) {
-    hipLaunchKernelGGL((trellis_fwd_f64<C, S, 4, false, false>), grid, block, 0, stream, fa);
-  } else if (!ldsfirst) {
-    hipLaunchKernelGGL((trellis_fwd_f64<C, S, 8, false, false, 1, false, 2, 1, false>), grid, block, 0, stream, fa);
   } else {
     hipLaunchKernelGGL((trellis_fwd_f64<C, S, 8, false, false>), grid, block, 0, stream, fa);
   }
@@ -1734,22 +1714,12 @@ __device__ __forceinline__ double dpp_f64(double v, int ctrl_is_xor2) {
   return from_words((uint32_t)hi, (uint32_t)lo);
 }
 
-// FUSE (knob CV_T64_FUSE=1, off: slower, see t64_wave_fusable): the wave backtracks its own
-// sequence right after its forward pass (backtrack_one_f64,
-// NONPOS test, a^T in f32 staged in LDS as backtrack_f64 does at NP = 64): the chains of the
-// long sequences, scheduled first, run while other waves still compute forward passes instead
-// of after the whole grid (config 3: their 1,024-step chains set the separate backtrack's
-// makespan).  Row-A0 decodes of NONPOS models only (the host checks).
-template <bool ZI, bool FUSE = false>
-__global__ __launch_bounds__(256) void trellis_wave_f64(T64FwdArgs g, T64BtArgs bt) {
+// (Round 3 also had a FUSE variant whose wave backtracked its own sequence right after the
+// forward pass: slower -- config 3 3.46 vs 3.22 ms -- and removed in round 6.)
+template <bool ZI>
+__global__ __launch_bounds__(256) void trellis_wave_f64(T64FwdArgs g) {
   constexpr int NPW = 64, C = 4, R = 16, LS = R + 2;
   __shared__ __attribute__((aligned(16))) double lds_all[4][2][4 * LS];
-  __shared__ float at_lds[FUSE ? 64 * 64 : 1];
-  if constexpr (FUSE) {  // before any wave leaves: every wave takes part in the barrier
-    for (int k = threadIdx.x; k < 64 * 64; k += 256) at_lds[k] = bt.at32[k];
-    __syncthreads();
-    bt.at32 = at_lds;
-  }
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
   const int rg = lane & 3, cq = lane >> 2;
@@ -1760,10 +1730,7 @@ __global__ __launch_bounds__(256) void trellis_wave_f64(T64FwdArgs g, T64BtArgs 
   const int64_t seq = g.order ? (int64_t)g.order[slot] : slot;
   const int64_t e0 = g.offsets[seq];
   const int T = (int)(g.offsets[seq + 1] - e0);
-  if (T <= 0) {  // the backtrack reports empty sequences
-    if constexpr (FUSE) backtrack_one_f64<1, 32, true>(bt, slot, lane, 0);
-    return;
-  }
+  if (T <= 0) return;  // the backtrack reports empty sequences
   double(*lds)[4 * LS] = lds_all[wv];
   const sptr<int32_t> obs = scalar_view(g.obs + e0);
   uint32_t* __restrict__ rows = reinterpret_cast<uint32_t*>(g.delta) + (e0 - g.delta_elem_base) * (2 * NPW);
@@ -1839,23 +1806,15 @@ __global__ __launch_bounds__(256) void trellis_wave_f64(T64FwdArgs g, T64BtArgs 
       so[k] = obs_s(min(t + 8, Tm1));          // observation of step t+8
     }
   }
-  if constexpr (FUSE) {
-    // this wave's rows are in L2 before it reads them back (no other wave touches them, so no
-    // L1 line of them can be stale); the status stays in registers
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    backtrack_one_f64<1, 32, true>(bt, slot, lane, bad ? (int)CVK_SEQ_BADOBS : 0);
-  } else {
-    if (bad && lane == 0) g.status[seq] = CVK_SEQ_BADOBS;
-  }
+  if (bad && lane == 0) g.status[seq] = CVK_SEQ_BADOBS;
 }
 
 hipError_t launch_t64_wave(const T64FwdArgs& fa, int64_t nseq, hipStream_t stream) {
   const dim3 grid((unsigned)((nseq + 3) / 4)), block(256);
-  const T64BtArgs none{};
   if (fa.zero_init)
-    hipLaunchKernelGGL(trellis_wave_f64<true>, grid, block, 0, stream, fa, none);
+    hipLaunchKernelGGL(trellis_wave_f64<true>, grid, block, 0, stream, fa);
   else
-    hipLaunchKernelGGL(trellis_wave_f64<false>, grid, block, 0, stream, fa, none);
+    hipLaunchKernelGGL(trellis_wave_f64<false>, grid, block, 0, stream, fa);
   return hipGetLastError();
 }
 
@@ -1887,8 +1846,8 @@ hipError_t cp_c(const T64FwdArgs& fa, int s, int64_t nseq, hipStream_t stream) {
 int t64_cp_seqs_per_wave(int s, int64_t nseq) {
   s = s > 4 ? 4 : s;  // the argmax state (idx) costs registers: at most 4 sequences per wave
   // a batch that leaves SIMDs idle at two sequences per wave: one per wave (the sequences are
-  // independent, so the results are the same); CV_T64_CP_S=1/2/4 sets it (A/B knob, per launch)
-  if (const char* e = getenv("CV_T64_CP_S"); e && *e) return atoi(e) >= 4 ? 4 : atoi(e) >= 2 ? 2 : 1;
+  // independent, so the results are the same); tuning key t64_cp_s = 1 / 2 / 4 sets it
+  if (const int k = tuning().t64_cp_s; k > 0) return k >= 4 ? 4 : k >= 2 ? 2 : 1;
   return nseq <= 1024 ? 1 : s;
 }
 
@@ -1911,48 +1870,21 @@ extern "C" __attribute__((visibility("default"))) int cv_debug_t64_probe(uint64_
 }
 #endif
 
-bool t64_wave_fusable(int np, const T64FwdArgs& fa, const T64BtArgs& ba) {
-  // A/B knob (bit-identical): CV_T64_FUSE=1.  Off by default: measured slower (config 3 3.46
-  // vs 3.22 ms, config 2 0.189 vs 0.179 ms; profiles/r03_ab_fuse.txt) -- the chains run at the
-  // forward's two waves per SIMD (184 VGPRs held) instead of the separate kernel's eight, so
-  // their HBM latency is exposed
-  static const bool fuse = [] {
-    const char* e = getenv("CV_T64_FUSE");
-    return e && e[0] == '1';
-  }();
-  static const bool wave = [] {  // as launch_t64_fwd's CV_T64_WAVE
-    const char* e = getenv("CV_T64_WAVE");
-    return !(e && e[0] == '0');
-  }();
-  const bool ext = fa.forced || fa.ranges || fa.reverse || fa.start || fa.row_base || fa.resume_rows ||
-                   fa.slot_order || fa.last_row;
-  return fuse && wave && np == 64 && !ext && !fa.dp_assoc && !fa.zero_init && !ba.dp_assoc && !ba.decode_bt &&
-         ba.at32 != nullptr;
-}
-
-hipError_t launch_t64_wave_fused(const T64FwdArgs& fa, const T64BtArgs& ba, int64_t nseq, hipStream_t stream) {
-  if (nseq <= 0) return hipSuccess;
-  hipLaunchKernelGGL((trellis_wave_f64<false, true>), dim3((unsigned)((nseq + 3) / 4)), dim3(256), 0, stream, fa, ba);
-  return hipGetLastError();
-}
-
 int t64_padded_states(int n) { return (n >= 1 && n <= 256) ? 64 * ((n + 63) / 64) : 0; }
 
 // The batch decode's f64 trellis (VITERBI / DECODE rows, no forced states) also covers
 // 256 < N <= 512: NP = 512 as PAIRS of C = 4 waves splitting the columns (the W = 2 layout of
 // the small-batch kernel with the full batch's C), four pairs per workgroup, and backtrack_f64
-// at KP = 8.  A/B knob CV_T64_512=0 (read per call): the generic kernels (bit-identical).
+// at KP = 8.  Tuning key t64_512 = 0: the generic kernels (bit-identical).
 int t64_batch_states(int n) {
   if (n <= 256) return t64_padded_states(n);
-  const char* e = getenv("CV_T64_512");
-  if (n <= 512) return !(e && e[0] == '0') ? 512 : 0;
+  if (n <= 512) return tuning().t64_512 != 0 ? 512 : 0;
   // 512 < N <= 1,024: QUADS of C = 4 waves, where A (N^2 f64) outgrows an XCD's 4 MiB L2
   // (N > 724) and the generic kernels turn HBM-bound: 16,384 x 128 at N = 800 188 vs 455 ms,
   // N = 1,024 191 vs 552 ms; at N = 600 the padding loses (179 vs 139 ms;
-  // profiles/r04_large_n.txt).  A/B knob CV_T64_1024=0 / =1 (read per call): never / always
+  // profiles/r04_large_n.txt).  Tuning key t64_1024 = 0 / 1: never / always
   if (n > 1024) return 0;
-  const char* q = getenv("CV_T64_1024");
-  if (q && (q[0] == '0' || q[0] == '1')) return q[0] == '1' ? 1024 : 0;
+  if (const int k = tuning().t64_1024; k == 0 || k == 1) return k == 1 ? 1024 : 0;
   return n > 724 ? 1024 : 0;
 }
 
@@ -2011,10 +1943,7 @@ int t64_seqs_per_wave(int64_t nseq, int cus, int np) {
   // over the same S sequences (W = NP / 256 waves each), so W times fewer sequences fill the
   // chip: at NP = 1,024, where A (8 MiB) streams from beyond an XCD's L2 every step, S = 2
   // doubled that stream (4,096 x 512 at N = 1,024: ~0.8 s forward at S = 2)
-  if (const char* e = getenv("CV_T64_S")) {  // tuning knob (bit-identical for every value)
-    const int s = atoi(e);
-    if (s == 2 || s == 4 || s == 6 || s == 8) return s;
-  }
+  if (const int s = tuning().t64_s; s == 2 || s == 4 || s == 6 || s == 8) return s;  // tuning key (bit-identical)
   const int64_t w = np >= 512 ? np / 256 : 1;
   const int64_t simd_waves = 2 * 4 * (int64_t)(cus > 0 ? cus : 256);
   if (nseq * w >= 8 * simd_waves) return 8;
@@ -2024,23 +1953,13 @@ int t64_seqs_per_wave(int64_t nseq, int cus, int np) {
 
 hipError_t launch_t64_fwd(int np, int s, const T64FwdArgs& fa_in, int64_t nseq, hipStream_t stream) {
   if (nseq <= 0) return hipSuccess;
-  static const int balance = [] {  // A/B knob (bit-identical): CV_T64_BAL = steps between SIMD balancing, 0 = off
-    const char* e = getenv("CV_T64_BAL");
-    return e ? atoi(e) : 8;
-  }();
+  const int balance = tuning().t64_bal;  // tuning key (bit-identical): steps between SIMD balancing, 0 = off
   T64FwdArgs fa = fa_in;
   // the batch decode only: the constrained decode's passes (EXT, 2 sequences per wave, two
   // streams) ran ~2% slower balanced (profiles/r02_t64_simd_balance.txt)
-  static const bool bal_ext = [] {  // A/B knob (bit-identical): CV_T64_BAL_EXT=1 balances the EXT passes too
-    const char* e = getenv("CV_T64_BAL_EXT");
-    return e && e[0] == '1';
-  }();
-  fa.balance = ((fa.forced || fa.ranges || fa.reverse || fa.start || fa.row_base || fa.resume_rows ||
-                 fa.slot_order || fa.last_row) && !bal_ext) ? 0 : balance;
-  static const bool wave = [] {  // A/B knob (bit-identical): CV_T64_WAVE=0 keeps the lock-step layout
-    const char* e = getenv("CV_T64_WAVE");
-    return !(e && e[0] == '0');
-  }();
+  fa.balance = (fa.forced || fa.ranges || fa.reverse || fa.start || fa.row_base || fa.resume_rows ||
+                fa.slot_order || fa.last_row) ? 0 : balance;
+  const bool wave = tuning().t64_wave != 0;  // tuning key t64_wave = 0 keeps the lock-step layout
   const bool ext = fa.forced || fa.ranges || fa.reverse || fa.start || fa.row_base || fa.resume_rows ||
                    fa.slot_order || fa.last_row;
   if (np == 64 && wave && !fa.dp_assoc && !ext) return launch_t64_wave(fa, nseq, stream);
@@ -2069,26 +1988,26 @@ hipError_t launch_t64_fwd(int np, int s, const T64FwdArgs& fa_in, int64_t nseq, 
   }
 }
 
-template <int PF, bool NONPOS, bool PERSIST>
+template <int PF, bool NONPOS>
 hipError_t bt_pf_np(int np, const T64BtArgs& ba, dim3 grid, dim3 block, hipStream_t stream) {
   if constexpr (PF == 32) {  // NP = 64 only (launch_t64_bt)
     if (np != 64) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((backtrack_f64<1, PF, NONPOS, PERSIST>), grid, block, 0, stream, ba);
+    hipLaunchKernelGGL((backtrack_f64<1, PF, NONPOS>), grid, block, 0, stream, ba);
   } else {
     switch (np) {
-      case 64: hipLaunchKernelGGL((backtrack_f64<1, PF, NONPOS, PERSIST>), grid, block, 0, stream, ba); break;
-      case 128: hipLaunchKernelGGL((backtrack_f64<2, PF, NONPOS, PERSIST>), grid, block, 0, stream, ba); break;
-      case 192: hipLaunchKernelGGL((backtrack_f64<3, PF, NONPOS, PERSIST>), grid, block, 0, stream, ba); break;
-      case 256: hipLaunchKernelGGL((backtrack_f64<4, PF, NONPOS, PERSIST>), grid, block, 0, stream, ba); break;
+      case 64: hipLaunchKernelGGL((backtrack_f64<1, PF, NONPOS>), grid, block, 0, stream, ba); break;
+      case 128: hipLaunchKernelGGL((backtrack_f64<2, PF, NONPOS>), grid, block, 0, stream, ba); break;
+      case 192: hipLaunchKernelGGL((backtrack_f64<3, PF, NONPOS>), grid, block, 0, stream, ba); break;
+      case 256: hipLaunchKernelGGL((backtrack_f64<4, PF, NONPOS>), grid, block, 0, stream, ba); break;
       case 512:
         if constexpr (PF <= 8) {
-          hipLaunchKernelGGL((backtrack_f64<8, PF, NONPOS, PERSIST>), grid, block, 0, stream, ba);
+          hipLaunchKernelGGL((backtrack_f64<8, PF, NONPOS>), grid, block, 0, stream, ba);
           break;
         }
         return hipErrorInvalidValue;
       case 1024:
         if constexpr (PF <= 4) {
-          hipLaunchKernelGGL((backtrack_f64<16, PF, NONPOS, PERSIST>), grid, block, 0, stream, ba);
+          hipLaunchKernelGGL((backtrack_f64<16, PF, NONPOS>), grid, block, 0, stream, ba);
           break;
         }
         return hipErrorInvalidValue;
@@ -2098,46 +2017,46 @@ hipError_t bt_pf_np(int np, const T64BtArgs& ba, dim3 grid, dim3 block, hipStrea
   return hipGetLastError();
 }
 
-template <int PF, bool NONPOS>
-hipError_t bt_pf_np(int np, const T64BtArgs& ba, dim3 grid, dim3 block, hipStream_t stream, bool persist) {
-  return persist ? bt_pf_np<PF, NONPOS, true>(np, ba, grid, block, stream)
-                 : bt_pf_np<PF, NONPOS, false>(np, ba, grid, block, stream);
-}
-
 template <int PF>
-hipError_t bt_pf(int np, const T64BtArgs& ba, dim3 grid, dim3 block, hipStream_t stream, bool persist) {
+hipError_t bt_pf(int np, const T64BtArgs& ba, dim3 grid, dim3 block, hipStream_t stream) {
+  if (ba.cert) {  // the parallel chain's certified backtrack (NONPOS row A0, N <= 256)
+    if (!ba.at32 || ba.dp_assoc || ba.decode_bt) return hipErrorInvalidValue;
+    switch (np) {
+      case 64: hipLaunchKernelGGL((backtrack_f64<1, PF, true, true>), grid, block, 0, stream, ba); break;
+      case 128: hipLaunchKernelGGL((backtrack_f64<2, PF, true, true>), grid, block, 0, stream, ba); break;
+      case 192: hipLaunchKernelGGL((backtrack_f64<3, PF, true, true>), grid, block, 0, stream, ba); break;
+      case 256: hipLaunchKernelGGL((backtrack_f64<4, PF, true, true>), grid, block, 0, stream, ba); break;
+      default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+  }
   if (ba.at32) {
-    hipError_t e = bt_pf_np<PF, true>(np, ba, grid, block, stream, persist);
+    hipError_t e = bt_pf_np<PF, true>(np, ba, grid, block, stream);
     if (e == hipSuccess && ba.decode_bt) {  // viterbi::decode: the infeasible sequences' DEC chains
       T64BtArgs b2 = ba;
       b2.only_infeasible = 1;
-      e = bt_pf_np<PF, false>(np, b2, grid, block, stream, persist);
+      e = bt_pf_np<PF, false>(np, b2, grid, block, stream);
     }
     return e;
   }
-  return bt_pf_np<PF, false>(np, ba, grid, block, stream, persist);
+  return bt_pf_np<PF, false>(np, ba, grid, block, stream);
 }
 
-hipError_t launch_t64_bt(int np, const T64BtArgs& ba, int64_t nseq, hipStream_t stream, int max_wgs) {
+hipError_t launch_t64_bt(int np, const T64BtArgs& ba, int64_t nseq, hipStream_t stream) {
   if (nseq <= 0) return hipSuccess;
-  int64_t wgs = (nseq + 3) / 4;
-  if (max_wgs > 0 && wgs > max_wgs) wgs = max_wgs;
-  const dim3 grid((unsigned)wgs), block(256);
-  static const int pf_env = [] {  // tuning knob (bit-identical): 2, 4, 8, 16 or 32 rows in flight
-    const char* e = getenv("CV_T64_BT_PF");
-    return e ? atoi(e) : 0;
-  }();
+  const dim3 grid((unsigned)((nseq + 3) / 4)), block(256);
   // NP = 64 (configs 2/3): the longest chains set the makespan and each step's hi row (256 B)
   // comes from HBM: 32 rows in flight, config 3 backtrack 0.615 -> 0.51 ms (16: 0.54)
-  // (profiles/r02_ab_bt_pf_c3.txt); N = 256: occupancy matters more (2 rows, 8 waves/SIMD)
-  const int pf = pf_env ? pf_env : np >= 192 ? 2 : np == 64 ? 32 : 8;
-  const bool persist = max_wgs > 0 && (nseq + 3) / 4 > max_wgs;
+  // (profiles/r02_ab_bt_pf_c3.txt); N = 256: occupancy matters more (2 rows, 8 waves/SIMD);
+  // tuning key t64_bt_pf (bit-identical) sets 2, 4, 8, 16 or 32
+  const int pf_key = tuning().t64_bt_pf;
+  const int pf = pf_key ? pf_key : np >= 192 ? 2 : np == 64 ? 32 : 8;
   switch (pf) {
-    case 2: return bt_pf<2>(np, ba, grid, block, stream, persist);
-    case 4: return bt_pf<4>(np, ba, grid, block, stream, persist);
-    case 16: return bt_pf<16>(np, ba, grid, block, stream, persist);
-    case 32: return np == 64 ? bt_pf<32>(np, ba, grid, block, stream, persist) : hipErrorInvalidValue;
-    default: return bt_pf<8>(np, ba, grid, block, stream, persist);
+    case 2: return bt_pf<2>(np, ba, grid, block, stream);
+    case 4: return bt_pf<4>(np, ba, grid, block, stream);
+    case 16: return bt_pf<16>(np, ba, grid, block, stream);
+    case 32: return np == 64 ? bt_pf<32>(np, ba, grid, block, stream) : hipErrorInvalidValue;
+    default: return bt_pf<8>(np, ba, grid, block, stream);
   }
 }
 
@@ -2336,8 +2255,8 @@ __global__ __launch_bounds__(1024) void cp_chain_wide_finish(CpChainArgs g) {
 
 bool cp_chain_wide(int n) {
   if (n > kChainLdsMaxStates) return true;
-  if (const char* e = getenv("CV_CHAIN_WIDE_MIN"); e && *e) return n >= atoi(e);
-  if (const char* e = getenv("CV_CHAIN_WIDE"); e && *e == '0') return false;
+  if (const int m = tuning().chain_wide_min; m > 0) return n >= m;
+  if (tuning().chain_wide == 0) return false;
   return n > 1024;
 }
 

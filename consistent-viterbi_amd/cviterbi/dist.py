@@ -14,7 +14,72 @@ exact search and decodes its own shard.
 """
 from __future__ import annotations
 
+import os
+import sys
+import threading
+import time
+from contextlib import contextmanager
+from datetime import timedelta
+
 import numpy as np
+
+# collective timeout of bench.py's process group: well inside the driver's 600 s bench limit,
+# far above any legitimate wait (rank 0's verify decode is a few seconds)
+COLLECTIVE_TIMEOUT_S = 180.0
+
+
+def init_process_group(dist, backend, device=None, timeout_s=COLLECTIVE_TIMEOUT_S, **kw):
+    """init_process_group with a finite collective timeout and, for "nccl" (RCCL), async error
+    handling on: a collective that never completes raises (gloo) or tears the process down
+    (the RCCL watchdog) after `timeout_s` instead of the default 10 minutes."""
+    if backend == "nccl":
+        os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
+        dist.init_process_group("nccl", device_id=device, timeout=timedelta(seconds=timeout_s), **kw)
+    else:
+        dist.init_process_group(backend, timeout=timedelta(seconds=timeout_s), **kw)
+
+
+class CollectiveWatch:
+    """Names the collective a rank is stuck in and ends the process when it overruns.
+
+    `with watch.phase("gather_packed_to_root (step results)"):` marks the code between as one
+    collective phase; a daemon thread checks every `poll_s`, and when a phase has run longer
+    than `timeout_s` it prints "<who> rank R: collective '<phase>' did not complete within N s"
+    to stderr and exits the process with `exit_code` (os._exit: a rank blocked inside a
+    collective cannot unwind).  A collective that FAILS instead raises inside the phase; the
+    phase re-raises it as RuntimeError with the same naming.  Works for gloo and nccl alike,
+    independent of the backend's own timeout (which `init_process_group` above also sets)."""
+
+    def __init__(self, rank, timeout_s=COLLECTIVE_TIMEOUT_S, who="bench.py", exit_code=4, poll_s=1.0):
+        self.rank, self.timeout_s, self.who, self.exit_code = rank, float(timeout_s), who, exit_code
+        self._cur = None  # (name, start, limit)
+        self._lock = threading.Lock()
+        self._t = threading.Thread(target=self._run, args=(poll_s,), daemon=True)
+        self._t.start()
+
+    def _run(self, poll_s):
+        while True:
+            time.sleep(poll_s)
+            with self._lock:
+                cur = self._cur
+            if cur and time.monotonic() - cur[1] > cur[2]:
+                print(f"{self.who} rank {self.rank}: collective '{cur[0]}' did not complete within "
+                      f"{cur[2]:.0f} s (a peer rank never entered it or the transport hangs); exiting",
+                      file=sys.stderr, flush=True)
+                os._exit(self.exit_code)
+
+    @contextmanager
+    def phase(self, name, timeout_s=None):
+        """timeout_s: this phase's own limit (default: the watch's)."""
+        with self._lock:
+            self._cur = (name, time.monotonic(), float(timeout_s or self.timeout_s))
+        try:
+            yield
+        except Exception as e:  # a backend error (gloo timeout, RCCL abort): say which collective
+            raise RuntimeError(f"{self.who} rank {self.rank}: collective '{name}' failed: {e}") from e
+        finally:
+            with self._lock:
+                self._cur = None
 
 
 def shard_range(total: int, world: int, rank: int):

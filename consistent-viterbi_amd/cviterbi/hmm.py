@@ -64,6 +64,36 @@ class HMM:
     def handle(self):
         return self._h
 
+    # ---- tuning keys (include/cviterbi.h): per-handle layout / schedule / A-B choices --------
+    def set_tuning(self, **keys):
+        """cv_hmm_set_tuning for each key=value (bit-identical in results; see cviterbi.h).
+        The handle's snapshot was taken from the CV_<KEY> environment at creation; later
+        environment changes do not reach it, this does."""
+        for k, v in keys.items():
+            L.check(L.lib().cv_hmm_set_tuning(self._h, k.encode(), int(v)))
+
+    def tuning(self, key) -> int:
+        """cv_hmm_get_tuning: the handle's current value of one tuning key."""
+        v = ctypes.c_int64()
+        L.check(L.lib().cv_hmm_get_tuning(self._h, key.encode(), ctypes.byref(v)))
+        return v.value
+
+    def tuned(self, **keys):
+        """Context manager: the given tuning keys for the block, the previous values after it."""
+        import contextlib
+
+        @contextlib.contextmanager
+        def cm():
+            old = {k: self.tuning(k) for k in keys}
+            self.set_tuning(**keys)
+            try:
+                yield self
+            finally:
+                self.set_tuning(**old)
+
+        return cm()
+
+
     # ---- shape -----------------------------------------------------------------------
     def nstates(self) -> int:
         """HMM::nstates (hmm.rs:207-209)."""
@@ -111,3 +141,14 @@ class HMM:
         out = np.zeros(self.nstates())
         L.check(L.lib().cv_hmm_emit_probs(self._h, self.flat(obs), _p(out)))
         return out
+
+
+def tuning_keys():
+    """Every tuning key the library knows (cv_tuning_key)."""
+    out, i = [], 0
+    while True:
+        k = L.lib().cv_tuning_key(i)
+        if not k:
+            return out
+        out.append(k.decode())
+        i += 1

@@ -61,7 +61,7 @@ enum { CV_ASSOC_VITERBI = 0, CV_ASSOC_CP = 1, CV_ASSOC_DP = 2, CV_ASSOC_DECODE =
  * VITERBI only; one wave per 2/4/8 sequences, A streamed from L2.  Above 256, VITERBI /
  * DECODE / DP without forced states (VITERBI with them) as pairs of waves at NP = 512 or quads
  * at NP = 1,024; AUTO takes NP = 512 for N >= 384 or >= 8,192 sequences and NP = 1,024 for
- * N > 724, knobs CV_T64_512 / CV_T64_1024; an explicit TRELLIS_F64 gets it for any N <= 1,024),
+ * N > 724, tuning keys t64_512 / t64_1024; an explicit TRELLIS_F64 gets it for any N <= 1,024),
  * else GENERIC (f32/f64, any association, N <= 65535: one workgroup per sequence with two rows
  * of N in LDS, or above N = 1024 -- always above 20480 f32 / 10240 f64 -- wide: one launch per
  * step, each sequence's states over ceil(N / 256) workgroups, rows in global memory). */
@@ -150,6 +150,51 @@ CV_API cv_status cv_hmm_from_json(const char* path, int32_t device, cv_hmm** out
 CV_API cv_status cv_hmm_write_json(const cv_hmm* h, const char* path);
 CV_API void cv_hmm_destroy(cv_hmm* h);
 /* HMM::nstates (hmm.rs:207-209). */
+/* ---- tuning keys (per handle) ------------------------------------------------------------
+ * Layout, schedule and A/B choices of the kernels, and the test hooks that force a code path.
+ * None changes a result: every key is bit-identical in paths, scores and statuses.  Each handle
+ * holds ONE snapshot, taken at cv_hmm_create / cv_hmm_from_json from the environment
+ * (variable CV_<KEY> in upper case, e.g. CV_T64_S=4 for "t64_s"; integers) over the defaults
+ * below, and changed afterwards only by cv_hmm_set_tuning: an environment variable set after
+ * the handle exists changes nothing, and no kernel launch reads the environment.  The
+ * handle-less cv_hmm_fit_* read the environment once per call.
+ *   trace 0               1: host phase stamps on stderr
+ *   host_threads 0        host worker threads (0: min(16, hardware threads))
+ *   t64_nonpos 1          0: the general f64 backtrack interval test (and no parallel chain)
+ *   generic_rows 1        0: generic kernels in psi mode (inline argmax) instead of rows mode
+ *   max_chunks 8          f32 trellis pipeline depth (1..64)
+ *   host_sums 0           1: the constrained decode's exact unary sums on the host
+ *   no_trace / no_resume / no_side 0   1: no certified suffix trace / resume flow / side-stream decode
+ *   chain_par 1           0: cv_decode_superseq_cp runs the serial chain kernel
+ *   chain_old 0           1: the one-thread-per-state chain kernel at any N
+ *   chain_par_force 0     m > 0: every m-th sequence of the parallel chain taken as uncertified
+ *   chain_spec 1          0: no speculative re-decode in the parallel chain
+ *   chain_spec_kernel 0   1: speculation on trellis_cp_f64 instead of the generic CP kernel
+ *   chain_copy_overlap 1  0: the parallel chain's path copy after its certificate pass
+ *   t64_s 0               f64 trellis sequences per wave 2 / 4 / 6 / 8 (0: by batch)
+ *   t64_512 / t64_1024 -1 NP = 512 / 1,024 batch kernel: -1 auto, 0 never, 1 always
+ *   t64_wg 1              0: one wave per workgroup instead of eight-wave units
+ *   t64_wg_force 0        1: eight-wave units whatever the batch's lengths
+ *   t64_rs 1 / t64_w2 1   0: no row-split / no pair-of-waves small-batch layout
+ *   t64_wave 1            0: N <= 64 on the lock-step kernel, not one wave per sequence
+ *   t64_bal 8             steps between SIMD-balancing updates (0: off)
+ *   t64_cp_s 0            trellis_cp_f64 sequences per wave 1 / 2 / 4 (0: by batch)
+ *   t64_bt_pf 0           backtrack_f64 rows in flight 2 / 4 / 8 / 16 / 32 (0: by NP)
+ *   generic_s 0           generic kernels' sequences per workgroup 1 / 2 / 4 (0: by batch)
+ *   generic_split 0, generic_split_k 0   1: K threads per state (generic_fwd_split), its K
+ *   generic_wide 1, generic_wide_min 0   0: never wide / > 0: wide from this N
+ *   wide_s 0              wide decode sequences per workgroup 1 / 2 / 4 (0: by batch)
+ *   ext_wide_min 0        > 0: the constrained terms passes wide from this N
+ *   chain_wide 1, chain_wide_min 0       the wide serial chain step: 0 never / from this N
+ *   f32_onebar 1          0: two barriers per step in the f32 pair trellis
+ *   bw_global 0, bw_perseq 0, bw_gemm_path 0   Baum-Welch: global scratch from N = 257 /
+ *                         per-sequence E-step kernels / the xi GEMM path at every N
+ * Unknown keys and values outside int32 are CV_EINVAL.  cv_tuning_key(i) lists the keys
+ * (NULL past the last). */
+CV_API cv_status cv_hmm_set_tuning(cv_hmm* h, const char* key, int64_t value);
+CV_API cv_status cv_hmm_get_tuning(const cv_hmm* h, const char* key, int64_t* value);
+CV_API const char* cv_tuning_key(int32_t i);
+
 CV_API int32_t cv_hmm_nstates(const cv_hmm* h);
 CV_API int64_t cv_hmm_nobs(const cv_hmm* h);                   /* V = prod(bdims) */
 CV_API int32_t cv_hmm_ndims(const cv_hmm* h);
@@ -230,7 +275,7 @@ CV_API cv_status cv_decode_constrained_device(cv_hmm* h, int64_t nseq, const int
  * took from the certified suffix trace (f64, one constrained element, log-probability models:
  * the path after t1 read off the terms pass's suffix rows, with a rounding-error margin that
  * proves it is the forced decode's own path) instead of a second forward pass; 0 when the
- * trace was off (CV_NO_TRACE=1, f32, no kept rows). */
+ * trace was off (tuning key no_trace, f32, no kept rows). */
 CV_API cv_status cv_last_suffix_traced(const cv_hmm* h, int64_t* out);
 /* The same decode split at its one exchange step, for a batch sharded over processes/GPUs:
  * 0. cv_constrained_pairs (host only) on the FULL batch: the sorted component pairs (c1 < c2)

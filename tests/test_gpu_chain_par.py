@@ -2,7 +2,7 @@
 super-sequence of utils.rs:62-103).  Every sequence is decoded on its own by the f64 trellis,
 certified to be the chain's own path at the chain's running total, and folded on the host;
 uncertified sequences re-run through the serial chain kernel.  The result must equal the serial
-chain (CV_CHAIN_PAR=0) and the C oracle's chained restatement (cvo_cp_superseq_f64) bit for bit:
+chain (tuning key chain_par = 0) and the C oracle's chained restatement (cvo_cp_superseq_f64) bit for bit:
 every element of the path and the objective."""
 import os
 
@@ -17,34 +17,16 @@ pytestmark = pytest.mark.gpu
 
 
 def _serial(h, off, obs):
-    old = os.environ.get("CV_CHAIN_PAR")
-    os.environ["CV_CHAIN_PAR"] = "0"
-    try:
+    with h.tuned(chain_par=0):  # tuning key (cviterbi.h): the serial chain kernel
         out = cv.decode_superseq_cp(h, off, obs)
         assert not cv.last_superseq_stats(h)["parallel"]
         return out
-    finally:
-        if old is None:
-            del os.environ["CV_CHAIN_PAR"]
-        else:
-            os.environ["CV_CHAIN_PAR"] = old
 
 
 def _par(h, off, obs, force=None, spec=True):
-    env = {"CV_CHAIN_PAR_FORCE": None if force is None else str(force), "CV_CHAIN_SPEC": None if spec else "0"}
-    old = {k: os.environ.get(k) for k in env}
-    for k, v in env.items():
-        if v is not None:
-            os.environ[k] = v
-    try:
+    with h.tuned(chain_par_force=0 if force is None else int(force), chain_spec=1 if spec else 0):
         out = cv.decode_superseq_cp(h, off, obs)
         return out, cv.last_superseq_stats(h)
-    finally:
-        for k, v in old.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
 
 
 def _case(n, v, nseq, tlo, thi, seed, scale=1.0, zeros=(), ones=()):
@@ -270,7 +252,7 @@ def test_chain_par_beyond_1024_equals_oracle(gpu, n):
 def test_chain_par_wide_runs(gpu, monkeypatch, n, force):
     """The wide chain (cp_chain_wide_step: one launch per element, the states over workgroups,
     the rows in global memory; what runs above N = 10,240) as the parallel chain's serial runs
-    from a start row (CV_CHAIN_WIDE_MIN=1 brings it down to these N), and the whole serial chain
+    from a start row (tuning key chain_wide_min = 1 brings it down to these N), and the whole serial chain
     with the segmented backtrack: the oracle's chain either way."""
     monkeypatch.setenv("CV_CHAIN_WIDE_MIN", "1")
     pi, a, b, off, obs = _case(n, 11, 16, 1, 30, seed=5000 + n + force, zeros=(2,), ones=(7,))
@@ -286,7 +268,7 @@ def test_chain_par_wide_runs(gpu, monkeypatch, n, force):
 @pytest.mark.parametrize("n", [300, 1100])
 def test_chain_par_wide_speculation(gpu, monkeypatch, n):
     """Speculative re-decodes through the wide generic CP kernel (start offsets cp_init, last
-    rows cp_last by sequence id; CV_GENERIC_WIDE_MIN=1 -- the certificates keep the rows mode):
+    rows cp_last by sequence id; tuning key generic_wide_min = 1 -- the certificates keep the rows mode):
     the oracle's chain."""
     monkeypatch.setenv("CV_GENERIC_WIDE_MIN", "1")
     pi, a, b, off, obs = _case(n, 11, 16, 1, 30, seed=5100 + n, zeros=(2,), ones=(7,))
@@ -300,7 +282,7 @@ def test_chain_par_wide_speculation(gpu, monkeypatch, n):
 @pytest.mark.parametrize("n,nseq", [(256, 2048), (300, 120)])
 def test_chain_par_copy_overlap_knob(gpu, monkeypatch, n, nseq):
     """The paths' host copy runs on its own stream behind the last backtrack, beside the
-    certificate pass (default); CV_CHAIN_COPY_OVERLAP=0 copies after the certificates on the
+    certificate pass (default); tuning key chain_copy_overlap = 0 copies after the certificates on the
     decode's stream.  Both return the same paths and objective (f64 trellis at N = 256, the
     generic rows mode's plain-row certificates at N = 300)."""
     if n == 256:
@@ -311,10 +293,30 @@ def test_chain_par_copy_overlap_knob(gpu, monkeypatch, n, nseq):
     h = cv.HMM(pi, a, b)
     (path, obj), st = _par(h, off, obs)
     assert st["parallel"], st
-    monkeypatch.setenv("CV_CHAIN_COPY_OVERLAP", "0")
+    h.set_tuning(chain_copy_overlap=0)
     (p0, o0), st0 = _par(h, off, obs)
     assert st0["parallel"], st0
     assert obj == o0 and np.array_equal(path, p0)
     if n == 300:
         rp, robj = O.cp_superseq_f64(pi, a, b, off, obs)
         assert obj == robj and np.array_equal(path, rp)
+
+
+@pytest.mark.parametrize("nseq,force", [(4096, None), (1024, 3)])
+def test_chain_cert_fused_vs_pass(gpu, nseq, force):
+    """The certificates computed inside the backtrack (backtrack_f64 CERT: estimated gap bounds,
+    exact gaps below rho_cap) vs the separate cp_cert_f64 pass (tuning key chain_cert_fused = 0,
+    exact gaps at every step): the same chain -- every element and the objective -- and the same
+    certification decisions (rho_cap is above every U the walk tests)."""
+    c = synth.config("c4", nseq)
+    pi, a, b, off, obs = c["pi"], c["a"], c["b"], c["offsets"], c["obs"]
+    h = cv.HMM(pi, a, b)
+    (p1, o1), s1 = _par(h, off, obs, force=force)
+    with h.tuned(chain_cert_fused=0):
+        (p0, o0), s0 = _par(h, off, obs, force=force)
+    assert s1["parallel"] and s0["parallel"], (s1, s0)
+    assert o1 == o0 and np.array_equal(p1, p0)
+    assert s1 == s0, (s1, s0)
+    sp, sobj = _serial(h, off[:257], obs[:int(off[256])])
+    (pp, op), _ = _par(h, off[:257], obs[:int(off[256])])
+    assert op == sobj and np.array_equal(pp, sp)

@@ -446,7 +446,7 @@ def test_cli_cfn(gpu, tmp_path):
 @pytest.mark.parametrize("n,seed", [(7, 1), (64, 2), (256, 3)])
 def test_device_exact_sums_equal_host(gpu, monkeypatch, n, seed, dtype):
     """The unary terms summed exactly on the device (kernels/exact.hip) give the same int64
-    words as the host loop (CV_HOST_SUMS=1): single- and multi-position sequences, -inf
+    words as the host loop (tuning key host_sums = 1): single- and multi-position sequences, -inf
     terms, several components."""
     pi, a, b = synth.random_hmm(n, 13, seed=seed, zero_frac=0.05)
     rng = np.random.default_rng(seed)
@@ -461,7 +461,7 @@ def test_device_exact_sums_equal_host(gpu, monkeypatch, n, seed, dtype):
     h = cv.HMM(pi, a, b)
     pairs = cv.constrained_pairs(off, comp, 5)
     dev = cv.constrained_partials(h, off, obs, comp, 5, pairs, dtype=dtype)
-    monkeypatch.setenv("CV_HOST_SUMS", "1")
+    h.set_tuning(host_sums=1)
     host = cv.constrained_partials(h, off, obs, comp, 5, pairs, dtype=dtype)
     assert np.array_equal(dev, host)
 
@@ -536,16 +536,16 @@ def _resume_case(n, seed, nseq=48, tmax=40, bad_obs=False):
                                         (130, 5, True), (200, 6, False), (40, 7, True)])
 def test_constrained_resume_equals_full(gpu, monkeypatch, n, seed, bad, dtype):
     """Resume flow (stored prefix rows, decode of [t_1, end), prefix backtrack from the forced
-    state) == the full forced decode (CV_NO_RESUME=1), host and device APIs, bit for bit;
+    state) == the full forced decode (tuning key no_resume = 1), host and device APIs, bit for bit;
     f32: N = 200 (NP 224) and N = 40 are outside the resume flow and run the full decode both
     times; f64 resumes at every N <= 256."""
     import torch
     pi, a, b, off, obs, comp = _resume_case(n, seed, bad_obs=bad)
     h = cv.HMM(pi, a, b)
     for f64 in ((False, True) if dtype == "f32" else (False,)):  # f32 scores see the resumed row itself
-        monkeypatch.setenv("CV_NO_RESUME", "1")
+        h.set_tuning(no_resume=1)
         ref = cv.decode_constrained(h, off, obs, comp, ncomp=5, rescore_f64=f64, dtype=dtype)
-        monkeypatch.setenv("CV_NO_RESUME", "0")
+        h.set_tuning(no_resume=0)
         got = cv.decode_constrained(h, off, obs, comp, ncomp=5, rescore_f64=f64, dtype=dtype)
         for x, y, what in zip(got, ref, ("path", "score", "status", "states", "objective")):
             assert np.array_equal(np.asarray(x), np.asarray(y)), (what, f64)
@@ -643,7 +643,7 @@ def test_constrained_sharded_two_processes(gpu):
 @pytest.mark.parametrize("nseq,T", [(4096, 64), (300, 33)])
 def test_constrained_device_side_decode_bit_identical(gpu, monkeypatch, nseq, T):
     """The device API decodes the unconstrained sequences on a side stream beside the terms
-    pass: bit-identical to the same call with CV_NO_SIDE=1 and to the host API
+    pass: bit-identical to the same call with tuning key no_side = 1 and to the host API
     (which does not use the side stream)."""
     import torch
 
@@ -657,7 +657,7 @@ def test_constrained_device_side_decode_bit_identical(gpu, monkeypatch, nseq, T)
     o_d, ob_d = torch.from_numpy(off).to(dev), torch.from_numpy(obs).to(dev)
     res = []
     for side in ("0", "1"):
-        monkeypatch.setenv("CV_NO_SIDE", side)
+        h.set_tuning(no_side=int(side))
         outs = (torch.full((nseq * T,), 9, dtype=torch.int32, device=dev),
                 torch.empty(nseq, dtype=torch.float64, device=dev), torch.empty(nseq, dtype=torch.uint8, device=dev))
         states, obj = cv.decode_constrained_device(h, off, o_d, ob_d, comp, *outs, ncomp=5, dtype="f64")
@@ -691,10 +691,10 @@ def test_full_config5_device_equals_host(gpu):
 
 @pytest.mark.parametrize("n", [256, 192])
 def test_constrained_ext_workgroup_units_bit_identical(gpu, tmp_path, n):
-    """The constrained passes in eight-wave workgroups (the terms pass takes them from two
-    rounds on; CV_T64_WG_EXT=1 forces them for every EXT launch: prefix, suffix, segment
-    tables, resume decode) decode the same bits as one-wave workgroups: ragged lengths, multi-
-    position sequences (segment tables), empty sequences."""
+    """The constrained passes in eight-wave workgroups (the resume decode takes them from two
+    rounds on; tuning key t64_wg_force = 1 forces them for every EXT launch: prefix, suffix,
+    segment tables, resume decode) decode the same bits as one-wave workgroups: ragged
+    lengths, multi-position sequences (segment tables), empty sequences."""
     import os
     import subprocess
     import sys
@@ -714,7 +714,7 @@ def test_constrained_ext_workgroup_units_bit_identical(gpu, tmp_path, n):
         "d = np.load(sys.argv[2]); h = cv.HMM(d['pi'], d['a'], d['b']); "
         "p, s, st, states, obj = cv.decode_constrained(h, d['off'], d['obs'], d['comp'], ncomp=4, dtype='f64'); "
         "np.savez(sys.argv[3], p=p, s=s, st=st, states=np.asarray(states), obj=np.asarray(obj))")
-    env = dict(os.environ, CV_T64_WG_EXT="1", CV_T64_S="8")
+    env = dict(os.environ, CV_T64_WG_FORCE="1", CV_T64_S="8")
     subprocess.run([sys.executable, "-c", code, pkg, str(tmp_path / "in.npz"), str(tmp_path / "out.npz")],
                    env=env, check=True, timeout=180)
     got = np.load(tmp_path / "out.npz")

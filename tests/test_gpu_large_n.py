@@ -536,9 +536,10 @@ def test_generic_split_golden(gpu, monkeypatch, split, name):
 @pytest.mark.parametrize("assoc", ["cp", "viterbi"])
 @pytest.mark.parametrize("n", [100, 300])
 def test_generic_psi_two_per_workgroup_default(gpu, monkeypatch, assoc, n):
-    """psi mode from 256 sequences on runs two sequences per workgroup by default (the walk
-    unrolled): 300 ragged sequences against the oracle and against one per workgroup
-    (CV_GENERIC_S=1), bit for bit."""
+    """CP psi mode from 256 sequences on runs two sequences per workgroup by default (the walk
+    unrolled; the other associations' psi mode keeps one -- ADVICE r5: only the CP batch was
+    measured): 300 ragged sequences against the oracle and against one per workgroup (tuning
+    key generic_s = 1), bit for bit."""
     monkeypatch.setenv("CV_GENERIC_ROWS", "0")
     monkeypatch.delenv("CV_GENERIC_S", raising=False)
     pi, a, b = synth.random_hmm(n, 13, seed=n + 404, zero_frac=0.05)
@@ -553,7 +554,7 @@ def test_generic_psi_two_per_workgroup_default(gpu, monkeypatch, assoc, n):
     ok = got[2] == 0
     assert np.array_equal(got[1][ok], ref[1][ok])
     assert np.array_equal(got[0], ref[0])
-    monkeypatch.setenv("CV_GENERIC_S", "1")
+    h.set_tuning(generic_s=1)
     one = cv.decode_batch(h, off, obs, dtype="f64", assoc=assoc, kernel="generic", rescore_f64=False)
     for x, y in zip(got, one):
         assert np.array_equal(x, y)

@@ -27,9 +27,12 @@ SCRIPT = textwrap.dedent(r"""
 
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
-    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    # bench.py's init: 180 s collective timeout, RCCL async error handling, a named-phase watch
+    cvd.init_process_group(dist, "nccl", dev, rank=0, world_size=1)
     assert dist.get_backend() == "nccl"
-    ok, msg = cvd.preflight(dist, dev, 256)
+    watch = cvd.CollectiveWatch(0, who="rccl-single")
+    with watch.phase("preflight: gather_packed_to_root + int64 all_reduce"):
+        ok, msg = cvd.preflight(dist, dev, 256)
     assert ok, msg
     # a real decode on the device, gathered as bench.py does (its own stream)
     pi, a, b = synth.random_hmm(256, 64, seed=11)

@@ -48,13 +48,13 @@ def _one_position(off, comp):
 
 def _both(h, off, obs, comp, ncomp, monkeypatch):
     """(trace on, trace off) results of the host API, plus the trace count of the first."""
-    monkeypatch.setenv("CV_NO_TRACE", "0")
+    h.set_tuning(no_trace=0)
     got = cv.decode_constrained(h, off, obs, comp, ncomp=ncomp, dtype="f64")
     traced = cv.last_suffix_traced(h)
-    monkeypatch.setenv("CV_NO_TRACE", "1")
+    h.set_tuning(no_trace=1)
     ref = cv.decode_constrained(h, off, obs, comp, ncomp=ncomp, dtype="f64")
     assert cv.last_suffix_traced(h) == 0
-    monkeypatch.setenv("CV_NO_TRACE", "0")
+    h.set_tuning(no_trace=0)
     return got, ref, traced
 
 
@@ -141,9 +141,9 @@ def test_trace_config5_full(gpu, monkeypatch):
     c = synth.config("c5")
     pi, a, b, off, obs, comp = c["pi"], c["a"], c["b"], c["offsets"], c["obs"], c["component"]
     h = cv.HMM(pi, a, b.reshape(256, 32, 32))
-    monkeypatch.setenv("CV_NO_TRACE", "1")
+    h.set_tuning(no_trace=1)
     ref = _device(h, off, obs, comp, 7)
-    monkeypatch.setenv("CV_NO_TRACE", "0")
+    h.set_tuning(no_trace=0)
     got = _device(h, off, obs, comp, 7)
     traced = cv.last_suffix_traced(h)
     _same(got, ref)

@@ -1,0 +1,124 @@
+"""Tuning keys (include/cviterbi.h): one snapshot per handle, no environment read afterwards.
+
+VERDICT r5 #5: the library's layout / schedule / A-B choices used to be read from 61 CV_*
+environment variables, several on every launch, so a caller's stray variable silently changed
+kernels.  Now csrc/tuning.cpp holds the only environment read (tuning_from_env, at
+cv_hmm_create), every launcher reads the handle's snapshot, and cv_hmm_set_tuning is the only
+way to change it.  CPU tests here (handle creation needs no GPU); the GPU test checks that an
+environment change after creation does not change the kernel layout a decode reports.
+"""
+import os
+import re
+
+import numpy as np
+import pytest
+
+import cviterbi as cv
+from conftest import ROOT
+
+CSRC = os.path.join(ROOT, "consistent-viterbi_amd", "csrc")
+
+
+def _hmm(n=8, v=5, seed=0):
+    rng = np.random.default_rng(seed)
+    pi = np.log10(rng.dirichlet(np.ones(n)))
+    a = np.log10(rng.dirichlet(np.ones(n), size=n))
+    b = np.log10(rng.dirichlet(np.ones(v), size=n))
+    return cv.HMM(pi, a, b)
+
+
+def test_snapshot_at_create_then_env_ignored(monkeypatch):
+    monkeypatch.setenv("CV_T64_S", "4")
+    monkeypatch.setenv("CV_CHAIN_SPEC", "0")
+    h1 = _hmm()
+    assert h1.tuning("t64_s") == 4 and h1.tuning("chain_spec") == 0
+    # set after the handle exists: h1 keeps its snapshot, a new handle takes the new value
+    monkeypatch.setenv("CV_T64_S", "2")
+    monkeypatch.delenv("CV_CHAIN_SPEC")
+    assert h1.tuning("t64_s") == 4 and h1.tuning("chain_spec") == 0
+    h2 = _hmm()
+    assert h2.tuning("t64_s") == 2 and h2.tuning("chain_spec") == 1
+    # the API is the only way to change a handle's value
+    h1.set_tuning(t64_s=8, chain_spec=1)
+    assert h1.tuning("t64_s") == 8 and h1.tuning("chain_spec") == 1
+    assert h2.tuning("t64_s") == 2
+    with h1.tuned(t64_s=6):
+        assert h1.tuning("t64_s") == 6
+    assert h1.tuning("t64_s") == 8
+
+
+def test_defaults_and_unknown_keys(monkeypatch):
+    for k in cv.tuning_keys():
+        monkeypatch.delenv("CV_" + k.upper(), raising=False)
+    h = _hmm()
+    want = {"t64_s": 0, "t64_wg": 1, "t64_bal": 8, "t64_512": -1, "chain_par": 1, "chain_cert_fused": 1,
+            "generic_rows": 1, "max_chunks": 8, "no_trace": 0, "trace": 0}
+    for k, v in want.items():
+        assert h.tuning(k) == v, k
+    with pytest.raises(cv.CVError, match="EINVAL"):
+        h.set_tuning(no_such_key=1)
+    with pytest.raises(cv.CVError, match="EINVAL"):
+        h.tuning("CV_T64_S")  # keys are the lower-case names, not the variables
+    with pytest.raises(cv.CVError, match="EINVAL"):
+        h.set_tuning(t64_s=1 << 40)
+
+
+def test_every_key_round_trips_through_its_variable(monkeypatch):
+    keys = cv.tuning_keys()
+    assert len(keys) == len(set(keys)) >= 30
+    for i, k in enumerate(keys):
+        monkeypatch.setenv("CV_" + k.upper(), str(100 + i))
+    h = _hmm()
+    for i, k in enumerate(keys):
+        assert h.tuning(k) == 100 + i, k
+
+
+def test_no_environment_read_outside_tuning_from_env():
+    """grep: every getenv of the library's sources is in tuning.cpp's tuning_from_env."""
+    calls = []
+    for dirpath, _, files in os.walk(CSRC):
+        if os.sep + "build" in dirpath:
+            continue
+        for f in files:
+            if f.endswith((".cpp", ".hip", ".h", ".hpp")):
+                src = open(os.path.join(dirpath, f)).read()
+                for m in re.finditer(r"\bgetenv\s*\(", src):
+                    line = src[: m.start()].count("\n") + 1
+                    calls.append((f, line, src))
+    assert 1 <= len(calls) <= 15, [(c[0], c[1]) for c in calls]
+    for f, line, src in calls:
+        assert f == "tuning.cpp", (f, line)
+        # inside tuning_from_env's body
+        start = src.index("Tuning tuning_from_env()")
+        end = src.index("\n}\n", start)
+        off = sum(len(x) + 1 for x in src.split("\n")[: line - 1])
+        assert start < off < end, (f, line)
+
+
+@pytest.mark.gpu
+def test_env_after_create_does_not_change_kernel(gpu, monkeypatch):
+    """A CV_* variable set after cv_hmm_create changes neither the layout last_timing reports
+    nor the result; a handle created afterwards takes it."""
+    from cviterbi import synth
+
+    for k in ("CV_T64_S", "CV_T64_WAVE", "CV_T64_W2"):
+        monkeypatch.delenv(k, raising=False)
+    pi, a, b = synth.random_hmm(256, 64, seed=5)
+    nseq, T = 4096, 24
+    off = np.arange(nseq + 1, dtype=np.int64) * T
+    obs = synth.iid_obs(64, nseq * T, 5)
+    h = cv.HMM(pi, a, b)
+    ref = cv.decode_batch(h, off, obs, rescore_f64=False)
+    t0 = cv.last_timing(h)
+    assert t0["kernel"] == "trellis_f64" and t0["seqs_per_wave"] == 2, t0  # 4,096 sequences: S = 2
+    monkeypatch.setenv("CV_T64_S", "4")
+    got = cv.decode_batch(h, off, obs, rescore_f64=False)
+    t1 = cv.last_timing(h)
+    assert (t1["kernel"], t1["seqs_per_wave"]) == (t0["kernel"], t0["seqs_per_wave"]), (t0, t1)
+    for x, y in zip(got, ref):
+        np.testing.assert_array_equal(x, y)
+    h2 = cv.HMM(pi, a, b)  # created after: the variable's value
+    got2 = cv.decode_batch(h2, off, obs, rescore_f64=False)
+    assert cv.last_timing(h2)["seqs_per_wave"] == 4
+    for x, y in zip(got2, ref):
+        np.testing.assert_array_equal(x, y)

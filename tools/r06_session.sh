@@ -1,0 +1,50 @@
+#!/bin/bash
+# Round-6 GPU session driver: named steps, each under its own time limit, chained so that the
+# first failure ends the call.  STEPS selects them (default: roof chain c2):
+#   roof   tools/microbench/valu_roof_f64.hip: the f64 VALU roof per SIMD at 1-4 waves/SIMD
+#   chain  the config-4-sized gpu-cp chain: CV_TRACE phase stamps + a kernel / copy trace
+#   c2     bench_configs c2f64 (and c3f64)
+#   tests  the full GPU suite;  smoke  __graft_entry__.smoke();  bench  bench.py
+#   prof   rocprofv3 --kernel-trace --stats of bench.py
+#   c5     bench_configs c5
+# TAG names the output directory under gpurun_out/.
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+O=$R/gpurun_out/${TAG:-r06_s1}
+mkdir -p $O
+cd $R
+export TMPDIR=/tmp
+step() {
+  local name=$1 t=$2
+  shift 2
+  echo "== $name $(date +%T)"
+  timeout -k 10 $t "$@" > $O/$name.log 2>&1
+  local rc=$?
+  tail -4 $O/$name.log | cut -c1-300
+  echo "== $name rc=$rc"
+  return $rc
+}
+run() {
+  case $1 in
+    roof)
+      hipcc --offload-arch=gfx950 -O3 -o /tmp/valu_roof_f64 tools/microbench/valu_roof_f64.hip > $O/roof_build.log 2>&1 &&
+        step roof 180 /tmp/valu_roof_f64 ;;
+    chain)
+      CV_TRACE=1 step chain_phases 240 python3 -u tools/bench_chain.py 65536 256 &&
+        (cd /tmp && SERIAL=0 step chain_trace 300 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv \
+          -d $O/kt -o kt -- python3 $R/tools/bench_chain_large_n.py 256 256 65536) &&
+        python3 tools/trace_timeline.py $O/kt trellis_fwd_f64 > $O/chain_timeline.txt ;;
+    c2) REPS=20 step c2 200 python3 -u tools/bench_configs.py c2f64 c3f64 ;;
+    c5) step c5 300 python3 -u tools/bench_configs.py c5 ;;
+    tests) step tests 900 python3 -u -m pytest -q --maxfail=25 --timeout 200 --timeout-method thread -m gpu tests ;;
+    chainq) step chainq 240 python3 -u tools/bench_chain.py 65536 256 ;;
+    smoke) step smoke 200 python3 -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" ;;
+    bench) step bench 400 python3 -u bench.py ;;
+    prof)
+      (cd /tmp && step prof 400 rocprofv3 --kernel-trace --stats -d $O/prof -o prof -- python3 $R/bench.py --no-f32-extra) ;;
+    *) echo "unknown step $1"; return 2 ;;
+  esac
+}
+for s in ${STEPS:-roof chain c2}; do
+  run $s || exit $?
+done
