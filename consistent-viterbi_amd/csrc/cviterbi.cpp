@@ -286,16 +286,18 @@ struct cv_hmm {
   // the last cv_decode_superseq_cp: parallel chain ran (1/0), sequences certified, sequences in
   // serial-chain runs, runs, certified folds done by the quantised sum, sequences taken from
   // speculative parallel re-decodes, such batches
-  int64_t last_chain[7] = {0, 0, 0, 0, 0, 0, 0};
+  // speculative parallel re-decodes, such batches, candidate paths fetched packed for the walk,
+  // walk steps that waited for the whole path copy
+  int64_t last_chain[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
   // the parallel chain's per-call device arrays, kept between calls (grow-only): a
   // config-4-sized call allocated and freed ~0.4 GB of them each time (hipFree synchronises)
   struct ChainBufs {
-    DevBuf off, obs, path, res, cert, ebin, q;
+    DevBuf off, obs, path, res, cert, ebin, q, ends, gid, gpath;
   } chainb;
-  // the parallel chain's path copy: on its own stream, behind the last backtrack (paths_ev),
-  // beside the certificate pass
+  // the parallel chain's path copy: per decode chunk, behind that chunk's backtrack (chunk_ev),
+  // on a non-blocking stream of its own, from a host thread of its own
+  std::vector<hipEvent_t> chunk_ev;
   hipStream_t copy_stream = nullptr;
-  hipEvent_t paths_ev = nullptr;
   PinnedHost chain_pin;  // the chain's scores, statuses and certificates on their way to the host
 
   ~cv_hmm() {
@@ -311,8 +313,8 @@ struct cv_hmm {
     if (side.ws_done) (void)hipEventDestroy(side.ws_done);
     if (stream) (void)hipStreamDestroy(stream);
     if (bt_stream) (void)hipStreamDestroy(bt_stream);
+    for (auto e : chunk_ev) (void)hipEventDestroy(e);
     if (copy_stream) (void)hipStreamDestroy(copy_stream);
-    if (paths_ev) (void)hipEventDestroy(paths_ev);
   }
 };
 
@@ -668,11 +670,12 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
                         const int32_t* obs_dev, const cv_opts& o, int32_t* path_dev, double* score_dev,
                         uint8_t* status_dev, hipStream_t stream, const void* resume_rows = nullptr,
                         bool side_ws = false, double* cp_cert = nullptr, const double* cp_init = nullptr,
-                        double* cp_last = nullptr, bool* paths_ev_rec = nullptr) {
-  // cp_cert (the parallel CPSolver chain, row-A0 f64 trellis only): after each chunk's
-  // backtrack, cp_cert_f64 reads the chunk's rows and paths -> [nseq][2] certificates;
-  // paths_ev_rec: h->paths_ev is recorded after the last chunk's backtrack (every path written),
-  // before its certificate pass, and *paths_ev_rec set
+                        double* cp_last = nullptr,
+                        std::vector<std::pair<int64_t, int64_t>>* chunks_out = nullptr) {
+  // cp_cert (the parallel CPSolver chain, row-A0 f64 trellis only): each chunk's backtrack
+  // computes its certificates (or cp_cert_f64 reads the chunk's rows and paths) -> [nseq][2];
+  // chunks_out: h->chunk_ev[i] is recorded after chunk i's backtrack (its paths written,
+  // before any certificate pass) and its sequence range [s0, s1) appended
   // side_ws: the handle's second workspace (h->side), no timing / last-call bookkeeping -- a
   // decode running beside another decode_device call of the same handle on another stream
   DevBuf& w_main = side_ws ? h->side.main : h->ws_main;
@@ -1029,6 +1032,7 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
         fa.cp_last = cp_last;
         err = cvk::launch_t64_cp_fwd(h->np64, spw, fa, n, stream);
       } else {
+        fa.nstates = h->N;  // the N <= 48 one-wave kernel
         err = cvk::launch_t64_fwd(h->np64, spw, fa, n, stream);
       }
     } else if (o.dtype == CV_DTYPE_F64) {
@@ -1122,10 +1126,11 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
         ba.rho_cap = h->cert_rho_cap;
       }
       err = cvk::launch_t64_bt(h->np64, ba, n, bts);
-      if (err == hipSuccess && cp_cert && paths_ev_rec && ci + 1 == chunks.size()) {
-        if (!h->paths_ev) HIP_TRY(hipEventCreateWithFlags(&h->paths_ev, hipEventDisableTiming));
-        HIP_TRY(hipEventRecord(h->paths_ev, bts));
-        *paths_ev_rec = true;
+      if (err == hipSuccess && chunks_out) {
+        hipEvent_t ce = get_event(h->chunk_ev, chunks_out->size());
+        if (!ce) return set_err(CV_EDEVICE, "hipEventCreate failed");
+        HIP_TRY(hipEventRecord(ce, bts));
+        chunks_out->push_back(c);
       }
       if (err == hipSuccess && cp_cert && !fused_cert) {
         cvk::CpCert64Args ca{};
@@ -1169,10 +1174,11 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
         ba.nobs = (int)h->V;
       }
       err = gen_rows ? cvk::launch_generic_bt_rows<double>(ba, n, bts) : cvk::launch_generic_bt<double>(ba, n, bts);
-      if (err == hipSuccess && cp_cert && paths_ev_rec && ci + 1 == chunks.size()) {
-        if (!h->paths_ev) HIP_TRY(hipEventCreateWithFlags(&h->paths_ev, hipEventDisableTiming));
-        HIP_TRY(hipEventRecord(h->paths_ev, bts));
-        *paths_ev_rec = true;
+      if (err == hipSuccess && chunks_out) {
+        hipEvent_t ce = get_event(h->chunk_ev, chunks_out->size());
+        if (!ce) return set_err(CV_EDEVICE, "hipEventCreate failed");
+        HIP_TRY(hipEventRecord(ce, bts));
+        chunks_out->push_back(c);
       }
       if (err == hipSuccess && cp_cert) {  // the parallel chain (N > 256): certificates over the plain rows
         cvk::CpCert64Args ca{};
@@ -2832,7 +2838,7 @@ cv_status sum_timing(cv_hmm* h, size_t eb, int64_t launches, cv_timing* out) {
 
 CV_API cv_status cv_last_superseq_stats(const cv_hmm* h, int64_t* out) {
   if (!h || !out) return set_err(CV_EINVAL, "null argument");
-  for (int q = 0; q < 7; ++q) out[q] = h->last_chain[q];
+  for (int q = 0; q < 9; ++q) out[q] = h->last_chain[q];
   return CV_OK;
 }
 
@@ -3020,6 +3026,10 @@ cv_status superseq_cp_wg(cv_hmm* h, int64_t L, const int32_t* obs, const std::ve
 // Knobs (bit-identical): CV_CHAIN_PAR=0 (serial chain), CV_CHAIN_PAR_FORCE=m (every m-th
 // non-empty sequence taken as uncertified: exercises speculation and the runs), CV_CHAIN_SPEC=0
 // (no speculation: every uncertified sequence through the serial chain kernel).
+// the parallel chain's decode in two chunks (their path copies beside the next chunk's forward
+// and the walk) from this many elements on
+constexpr int64_t kChainCopyChunkMin = 1 << 22;
+
 cv_status superseq_cp_par(cv_hmm* h, int64_t nseq, const int64_t* offsets, const int32_t* obs, int32_t* path_out,
                           double* objective_out, bool* applied) {
   *applied = false;
@@ -3076,59 +3086,87 @@ cv_status superseq_cp_par(cv_hmm* h, int64_t nseq, const int64_t* offsets, const
   o.kernel = small ? CV_KERNEL_TRELLIS_F64 : CV_KERNEL_AUTO;  // N > 256: the batch path's own pick
   o.rescore_f64 = 0;
   o.stream = stream;
-  // the paths' copy to the host (4 B per element) runs on its own stream beside the
-  // certificate pass, which reads every row (tuning key chain_copy_overlap = 0: after it)
-  bool paths_rec = false;
-  const bool overlap_copy = h->tuning.chain_copy_overlap != 0 && !trace_on();
-  if (overlap_copy && !h->copy_stream) HIP_TRY(hipStreamCreateWithFlags(&h->copy_stream, hipStreamNonBlocking));
-  st = decode_device(h, nseq, off.data(), d_off.as<int64_t>(), d_obs.as<int32_t>(), o, d_path.as<int32_t>(), d_score,
-                     d_status, stream, nullptr, false, d_cert.as<double>(), nullptr, nullptr,
-                     overlap_copy ? &paths_rec : nullptr);
-  if (st == CV_EUNSUPPORTED && !small) return CV_OK;  // no rows to certify (CV_GENERIC_ROWS=0): serial chain
-  if (st != CV_OK) {
-    if (paths_rec) (void)hipStreamSynchronize(h->copy_stream);
-    return st;
+  // The paths reach the caller's (pageable) buffer from a host thread of their own, one copy
+  // per decode chunk behind that chunk's backtrack (a pageable D2H blocks its calling thread):
+  // the first chunk's copy runs beside the next chunk's forward, the last one beside the walk
+  // below, which needs only the end states and the paths of the few sequences it may fold
+  // element by element (fetched packed).  Two chunks at config-4 size (tuning key
+  // chain_copy_overlap = 0: one chunk, the copy before the walk).
+  const bool overlap_copy = h->tuning.chain_copy_overlap != 0;
+  if (overlap_copy && small) {
+    const uint64_t rows = (uint64_t)L * (uint64_t)h->np64 * 8;
+    if (L >= 2 * (int64_t)kChainCopyChunkMin) o.workspace_bytes = (rows + 1) / 2 + ((uint64_t)h->np64 * 8 << 10);
   }
+  std::vector<std::pair<int64_t, int64_t>> dchunks;
+  st = decode_device(h, nseq, off.data(), d_off.as<int64_t>(), d_obs.as<int32_t>(), o, d_path.as<int32_t>(), d_score,
+                     d_status, stream, nullptr, false, d_cert.as<double>(), nullptr, nullptr, &dchunks);
+  if (st == CV_EUNSUPPORTED && !small) return CV_OK;  // no rows to certify (generic_rows = 0): serial chain
+  if (st != CV_OK) return st;
   std::vector<double> score((size_t)nseq), cert((size_t)nseq * 2);
   std::vector<uint8_t> status((size_t)nseq);
+  std::vector<int32_t> ends((size_t)nseq);
   if (trace_on()) {
     HIP_TRY(hipStreamSynchronize(stream));
     trace_mark("chain: row-A0 decode + certificates (device)");
   }
-  // an early return below must not leave the copy writing into the caller's buffer
-  struct CopyJoin {
-    hipStream_t s;
-    bool on;
-    ~CopyJoin() {
-      if (on) (void)hipStreamSynchronize(s);
+  // the copy thread; any return below joins it first (it writes into the caller's buffer)
+  struct CopyThread {
+    std::thread t;
+    hipError_t err = hipSuccess;
+    ~CopyThread() { join(); }
+    void join() {
+      if (t.joinable()) t.join();
     }
-  } copy_join{h->copy_stream, false};
-  if (paths_rec) {
-    HIP_TRY(hipStreamWaitEvent(h->copy_stream, h->paths_ev, 0));
-    HIP_TRY(hipMemcpyAsync(path_out, d_path.p, (size_t)L * 4, hipMemcpyDeviceToHost, h->copy_stream));
-    copy_join.on = true;
-  } else {
-    HIP_TRY(hipMemcpyAsync(path_out, d_path.p, (size_t)L * 4, hipMemcpyDeviceToHost, stream));
+  } copy;
+  if (!h->copy_stream) HIP_TRY(hipStreamCreateWithFlags(&h->copy_stream, hipStreamNonBlocking));
+  {
+    const int dev = h->device;
+    hipStream_t cs = h->copy_stream;
+    std::vector<hipEvent_t> evs(h->chunk_ev.begin(), h->chunk_ev.begin() + (ptrdiff_t)dchunks.size());
+    int32_t* dp = d_path.as<int32_t>();
+    auto run_copies = [&copy, dev, cs, evs, dchunks, off, path_out, dp]() {
+      if ((copy.err = hipSetDevice(dev)) != hipSuccess) return;
+      for (size_t i = 0; i < dchunks.size(); ++i) {
+        const int64_t e0 = off[(size_t)dchunks[i].first], e1 = off[(size_t)dchunks[i].second];
+        if ((copy.err = hipStreamWaitEvent(cs, evs[i], 0)) != hipSuccess) return;
+        if (e1 > e0 &&
+            (copy.err = hipMemcpyAsync(path_out + e0, dp + e0, (size_t)(e1 - e0) * 4, hipMemcpyDeviceToHost, cs)) !=
+                hipSuccess)
+          return;
+      }
+      copy.err = hipStreamSynchronize(cs);
+    };
+    if (overlap_copy)
+      copy.t = std::thread(run_copies);
+    else
+      run_copies();
   }
-  // scores, certificates and statuses through one pinned buffer (d_res holds scores then
-  // statuses contiguously)
-  if (h->chain_pin.ensure((size_t)nseq * 25)) {
+  if (!overlap_copy && copy.err != hipSuccess)
+    return set_err(CV_EDEVICE, "chain path copy failed: %s", hipGetErrorString(copy.err));
+  // end states, scores, statuses and certificates through one pinned buffer (d_res holds
+  // scores then statuses contiguously)
+  DevBuf& d_ends = h->chainb.ends;
+  if ((st = d_ends.ensure((size_t)nseq * 4)) != CV_OK) return st;
+  {
+    const hipError_t e = cvk::launch_cp_seq_ends(d_path.as<int32_t>(), d_off.as<int64_t>(), nseq, d_ends.as<int32_t>(), stream);
+    if (e != hipSuccess) return set_err(CV_EDEVICE, "chain end states failed: %s", hipGetErrorString(e));
+  }
+  if (h->chain_pin.ensure((size_t)nseq * 29)) {
     unsigned char* pin = h->chain_pin.as<unsigned char>();
     HIP_TRY(hipMemcpyAsync(pin, d_res.p, (size_t)nseq * 9, hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipMemcpyAsync(pin + (size_t)nseq * 9, d_cert.p, (size_t)nseq * 16, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipMemcpyAsync(pin + (size_t)nseq * 25, d_ends.p, (size_t)nseq * 4, hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipStreamSynchronize(stream));
     std::memcpy(score.data(), pin, (size_t)nseq * 8);
     std::memcpy(status.data(), pin + (size_t)nseq * 8, (size_t)nseq);
     std::memcpy(cert.data(), pin + (size_t)nseq * 9, (size_t)nseq * 16);
+    std::memcpy(ends.data(), pin + (size_t)nseq * 25, (size_t)nseq * 4);
   } else {
     HIP_TRY(hipMemcpyAsync(score.data(), d_score, (size_t)nseq * 8, hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipMemcpyAsync(status.data(), d_status, (size_t)nseq, hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipMemcpyAsync(cert.data(), d_cert.p, (size_t)nseq * 16, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipMemcpyAsync(ends.data(), d_ends.p, (size_t)nseq * 4, hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipStreamSynchronize(stream));
-  }
-  if (paths_rec) {
-    copy_join.on = false;
-    HIP_TRY(hipStreamSynchronize(h->copy_stream));
   }
   trace_mark("chain: paths, scores, certificates D2H");
   for (int64_t k = 0; k < nseq; ++k)
@@ -3182,19 +3220,90 @@ cv_status superseq_cp_par(cv_hmm* h, int64_t nseq, const int64_t* offsets, const
     if (std::isfinite(x)) pimax = std::max(pimax, std::fabs(x));
   const int force_m = std::max(0, h->tuning.chain_par_force);
   const bool spec_env = h->tuning.chain_spec != 0;  // 0: every uncertified sequence re-run serially
-  const int32_t* P = path_out;  // the row-A0 paths (element index relative to base)
   const int32_t* ob = obs + base;
+  // The row-A0 paths the walk folds element by element: the sequences whose certificate may
+  // fail at the running maximum the walk will see (predicted from the optima, with a 2x margin
+  // on every bound), those without a quantised fold, and each one's successor, fetched packed
+  // while the copy thread fills the caller's buffer; any other sequence the walk needs waits
+  // for that copy (counted in path_waits).
+  std::vector<int32_t> gpath;
+  std::vector<int64_t> gpos((size_t)nseq, -1);
+  bool copy_joined = !overlap_copy;
+  int64_t path_waits = 0, gathered = 0;
+  {
+    double smax = 0.0;
+    for (double x : score) smax = std::max(smax, std::fabs(x));
+    std::vector<int64_t> gids, gdst;
+    double mp = 0.0;
+    bool prev_cand = false;
+    int64_t x = 0, tot = 0;
+    for (int64_t k = 0; k < nseq; ++k) {
+      const int64_t T = off[(size_t)k + 1] - off[(size_t)k];
+      if (T == 0) continue;
+      const double S = std::fabs(score[(size_t)k]);
+      const double Up = 0x1p-52 * (mp * (1.0 + 0x1p-8) + S + 16.0);
+      const double Up1 = 0x1p-52 * ((mp + S) * (1.0 + 0x1p-8) + smax + pimax + 16.0);
+      const double rho = cert[(size_t)k * 2], gF = cert[(size_t)k * 2 + 1];
+      const bool cand = !(rho > 2.0 * Up) || !(gF - 6.0 * (double)T * Up > 4.0 * Up1) || tie[(size_t)k] ||
+                        ebin[(size_t)k] == cvk::CVK_NO_BINADE ||
+                        (force_m > 0 && (int64_t)(x % (int64_t)force_m) == force_m - 1);
+      if (cand || prev_cand) {
+        gids.push_back(k);
+        gdst.push_back(tot);
+        gpos[(size_t)k] = tot;
+        tot += T;
+      }
+      prev_cand = cand;
+      mp += S;
+      ++x;
+    }
+    gathered = (int64_t)gids.size();
+    if (!copy_joined && !gids.empty()) {
+      DevBuf &d_gid = h->chainb.gid, &d_gpath = h->chainb.gpath;
+      if ((st = d_gid.ensure(gids.size() * 16)) != CV_OK || (st = d_gpath.ensure((size_t)tot * 4)) != CV_OK) return st;
+      gids.insert(gids.end(), gdst.begin(), gdst.end());
+      HIP_TRY(hipMemcpyAsync(d_gid.p, gids.data(), gids.size() * 8, hipMemcpyHostToDevice, stream));
+      const hipError_t e = cvk::launch_cp_gather_paths(d_path.as<int32_t>(), d_off.as<int64_t>(), d_gid.as<int64_t>(),
+                                                       d_gid.as<int64_t>() + gathered, gathered, d_gpath.as<int32_t>(),
+                                                       stream);
+      if (e != hipSuccess) return set_err(CV_EDEVICE, "chain path gather failed: %s", hipGetErrorString(e));
+      gpath.resize((size_t)tot);
+      HIP_TRY(hipMemcpyAsync(gpath.data(), d_gpath.p, (size_t)tot * 4, hipMemcpyDeviceToHost, stream));
+      HIP_TRY(hipStreamSynchronize(stream));
+    }
+    trace_mark("chain: candidate paths gathered");
+  }
+  auto join_copy = [&]() -> cv_status {
+    if (copy_joined) return CV_OK;
+    copy.join();
+    copy_joined = true;
+    if (copy.err != hipSuccess) return set_err(CV_EDEVICE, "chain path copy failed: %s", hipGetErrorString(copy.err));
+    return CV_OK;
+  };
+  cv_status path_st = CV_OK;
+  auto seq_path = [&](int64_t k) -> const int32_t* {  // sequence k's row-A0 path
+    if (!copy_joined && gpos[(size_t)k] >= 0) return gpath.data() + gpos[(size_t)k];
+    if (!copy_joined) {
+      ++path_waits;
+      if (path_st == CV_OK) path_st = join_copy();
+    }
+    return path_out + off[(size_t)k];
+  };
   auto fold_elems = [&](int64_t k, double M) {  // the CP fold of sequence k's path from M
     const int64_t e0 = off[(size_t)k], T = off[(size_t)k + 1] - e0;
-    int32_t p = P[e0];
+    const int32_t* P = seq_path(k);
+    int32_t p = P[0];
     double d = M + (h->pi[(size_t)p] + h->b[(size_t)p * V + ob[e0]]);
     for (int64_t t = 1; t < T; ++t) {
-      const int32_t c = P[e0 + t];
+      const int32_t c = P[t];
       d = d + (h->a[(size_t)p * N + c] + h->b[(size_t)c * V + ob[e0 + t]]);
       p = c;
     }
     return d;
   };
+  // writes into the caller's buffer that must land after the copy thread's (serial runs,
+  // accepted speculative decodes): applied once it has joined
+  std::vector<std::pair<int64_t, std::vector<int32_t>>> deferred;
   // the fold of a certified path: M + q 2^(e-52) when M and the sequence's values share the
   // predicted binade 2^e (cp_quant_f64), else element by element
   auto fold = [&](int64_t k, double M, bool* quant) {
@@ -3266,8 +3375,10 @@ cv_status superseq_cp_par(cv_hmm* h, int64_t nseq, const int64_t* offsets, const
     if ((st = d_rpath.ensure((size_t)run_len * 4)) != CV_OK) return st;
     if ((st = chain_backtrack(W, d_rpsi.as<uint16_t>(), run_len, end_state, d_rpath.as<int32_t>(), stream)) != CV_OK)
       return st;
-    HIP_TRY(hipMemcpyAsync(path_out + run_e0, d_rpath.p, (size_t)run_len * 4, hipMemcpyDeviceToHost, stream));
+    std::vector<int32_t> rp((size_t)run_len);
+    HIP_TRY(hipMemcpyAsync(rp.data(), d_rpath.p, (size_t)run_len * 4, hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipStreamSynchronize(stream));
+    deferred.emplace_back(run_e0, std::move(rp));
     in_run = false;
     return CV_OK;
   };
@@ -3445,7 +3556,7 @@ cv_status superseq_cp_par(cv_hmm* h, int64_t nseq, const int64_t* offsets, const
       if (in_run && (st = end_run(row_arg)) != CV_OK) return st;  // clean: the run ends in its argmax
       M = Mn;
       prev = CERT;
-      prev_end = P[e0 + T - 1];
+      prev_end = ends[(size_t)k];
       ++ncert;
       nquant += qd ? 1 : 0;
       ++x;
@@ -3463,7 +3574,8 @@ cv_status superseq_cp_par(cv_hmm* h, int64_t nseq, const int64_t* offsets, const
       const double m1 = lr[arg];
       if (m1 > -INFINITY && (x + 1 >= ks.size() || row_clean(lr, arg, m1, score_of(x + 1) + pimax + 16.0))) {
         if (in_run && (st = end_run(row_arg)) != CV_OK) return st;
-        std::memcpy(path_out + e0, spec_path.data() + spec_off[(size_t)si], (size_t)T * 4);
+        const int32_t* sp = spec_path.data() + spec_off[(size_t)si];
+        deferred.emplace_back(e0, std::vector<int32_t>(sp, sp + T));
         std::copy(lr, lr + N, row_host.begin());
         std::fill(row_host.begin() + N, row_host.end(), -INFINITY);
         row_dev = nullptr;
@@ -3490,7 +3602,13 @@ cv_status superseq_cp_par(cv_hmm* h, int64_t nseq, const int64_t* offsets, const
     ++x;
   }
   if (in_run && (st = end_run(row_arg)) != CV_OK) return st;  // cp.rs:86: first argmax of the last row
+  if (path_st != CV_OK) return path_st;
   trace_mark("chain: walk + runs");
+  if ((st = join_copy()) != CV_OK) return st;
+  for (const auto& d : deferred) std::memcpy(path_out + d.first, d.second.data(), d.second.size() * 4);
+  trace_mark("chain: path copy joined");
+  h->last_chain[7] = gathered;
+  h->last_chain[8] = path_waits;
   h->last_chain[0] = 1;
   h->last_chain[1] = ncert;
   h->last_chain[2] = run_seqs;
@@ -3532,8 +3650,7 @@ CV_API cv_status cv_decode_superseq_cp(cv_hmm* h, int64_t nseq, const int64_t* o
   // (kernels/chain.hip), N > 256 (or CV_CHAIN_OLD=1, an A/B knob, bit-identical) one thread per
   // state (cp_superseq_chain); both then the parallel segmented backtrack
   const bool chain_old = h->tuning.chain_old == 1;
-  h->last_chain[0] = 0;
-  for (int q = 1; q < 7; ++q) h->last_chain[q] = 0;
+  for (int q = 0; q < 9; ++q) h->last_chain[q] = 0;
   if (!chain_old && h->tuning.chain_par != 0) {
     bool applied = false;
     st = superseq_cp_par(h, nseq, offsets, obs, path_out, objective_out, &applied);

@@ -531,6 +531,42 @@ hipError_t launch_cp_cert_plain(const CpCert64Args& a, hipStream_t stream) {
   return hipGetLastError();
 }
 
+// the parallel chain's host walk without the whole path on the host: every sequence's end
+// state (its last element; -1 for an empty sequence) ...
+__global__ void cp_seq_ends(const int32_t* __restrict__ path, const int64_t* __restrict__ offsets, int64_t nseq,
+                            int32_t* __restrict__ out) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= nseq) return;
+  const int64_t e1 = offsets[k + 1];
+  out[k] = e1 > offsets[k] ? path[e1 - 1] : -1;
+}
+
+// ... and the paths of the sequences it may fold element by element, packed: sequence ids[i]'s
+// path to out[dst[i] ..] (one workgroup per sequence, coalesced)
+__global__ __launch_bounds__(256) void cp_gather_paths(const int32_t* __restrict__ path,
+                                                       const int64_t* __restrict__ offsets,
+                                                       const int64_t* __restrict__ ids, const int64_t* __restrict__ dst,
+                                                       int32_t* __restrict__ out) {
+  const int64_t k = ids[blockIdx.x];
+  const int64_t e0 = offsets[k], T = offsets[k + 1] - e0, d = dst[blockIdx.x];
+  for (int64_t t = threadIdx.x; t < T; t += 256) out[d + t] = path[e0 + t];
+}
+
+hipError_t launch_cp_seq_ends(const int32_t* path, const int64_t* offsets, int64_t nseq, int32_t* out,
+                              hipStream_t stream) {
+  if (nseq <= 0) return hipSuccess;
+  hipLaunchKernelGGL(cp_seq_ends, dim3((unsigned)((nseq + 255) / 256)), dim3(256), 0, stream, path, offsets, nseq, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_cp_gather_paths(const int32_t* path, const int64_t* offsets, const int64_t* ids, const int64_t* dst,
+                                  int64_t n, int32_t* out, hipStream_t stream) {
+  if (n <= 0) return hipSuccess;
+  if (n > (int64_t)INT32_MAX) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(cp_gather_paths, dim3((unsigned)n), dim3(256), 0, stream, path, offsets, ids, dst, out);
+  return hipGetLastError();
+}
+
 hipError_t launch_cp_quant(const CpQuant64Args& a, hipStream_t stream) {
   if (a.nseq <= 0) return hipSuccess;
   hipLaunchKernelGGL(cp_quant_f64, dim3((unsigned)((a.nseq + 3) / 4)), dim3(256), 0, stream, a);

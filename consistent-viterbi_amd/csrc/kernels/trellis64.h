@@ -177,6 +177,12 @@ struct CpQuant64Args {
   uint8_t* tie;            // [nseq] 1: a tie or out-of-range arc (fold element by element)
 };
 hipError_t launch_cp_quant(const CpQuant64Args& a, hipStream_t stream);
+// out[k] = path[offsets[k+1] - 1] (-1 for an empty sequence), k < nseq
+hipError_t launch_cp_seq_ends(const int32_t* path, const int64_t* offsets, int64_t nseq, int32_t* out,
+                              hipStream_t stream);
+// out[dst[i] + t] = path[offsets[ids[i]] + t], t < T(ids[i]), i < n
+hipError_t launch_cp_gather_paths(const int32_t* path, const int64_t* offsets, const int64_t* ids, const int64_t* dst,
+                                  int64_t n, int32_t* out, hipStream_t stream);
 
 // CPSolver's super-sequence decode chained exactly over the whole batch (cp_superseq_chain).
 struct CpChainArgs {

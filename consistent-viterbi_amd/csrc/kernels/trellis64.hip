@@ -1809,9 +1809,120 @@ __global__ __launch_bounds__(256) void trellis_wave_f64(T64FwdArgs g) {
   if (bad && lane == 0) g.status[seq] = CVK_SEQ_BADOBS;
 }
 
+// trellis_wave48_f64<ZI>: N <= 48 (config 2's N = 45) -- one wave per sequence like
+// trellis_wave_f64, on the 48 states that exist instead of 64 padded ones (1.8x fewer pairs),
+// in at most 128 VGPRs so FOUR waves share a SIMD (one round of 4,096 sequences on the chip,
+// workgroups of the longest-first order spread one per quartile onto every CU).  Lane
+// l = 4 cq + rg holds A[12 rg + r][3 cq + k] (r < 12, k < 3: 72 VGPRs) and walks its 12 rows for
+// its 3 columns (36 pairs, one v_add_f64 + one v_max_f64 each); the 4 row groups' partial
+// maxima meet in LDS (part[col][rg], written and read back by the same wave: LDS executes a
+// wave's operations in order), lane j < 48 takes the max of its column's 4 partials and adds
+// the emission.  Max is exact and order-free, so values, rows and results are those of
+// trellis_wave_f64 bit for bit.  Rows go to HBM split-plane, 64 wide, for backtrack_f64
+// (columns >= N are never read: the backtrack masks candidates >= N).
+template <bool ZI>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void trellis_wave48_f64(T64FwdArgs g) {
+  constexpr int NPW = 64, NC = 48, C = 3, R = 12, LS = NC + 4;
+  __shared__ __attribute__((aligned(16))) double dl_all[4][2][LS];    // delta_{t-1} / delta_t per wave
+  __shared__ __attribute__((aligned(16))) double part_all[4][NC][4];  // [col][rg] partial maxima
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+  const int rg = lane & 3, cq = lane >> 2;
+  const bool owner = lane < NC;  // lane j < 48 owns column j after the fold
+  const int64_t slot = g.seq_begin + 4 * (int64_t)blockIdx.x + wv;
+  if (slot >= g.seq_begin + g.nslots) return;
+  const int64_t seq = g.order ? (int64_t)g.order[slot] : slot;
+  const int64_t e0 = g.offsets[seq];
+  const int T = (int)(g.offsets[seq + 1] - e0);
+  if (T <= 0) return;  // the backtrack reports empty sequences
+  double(*dl)[LS] = dl_all[wv];
+  double(*part)[4] = part_all[wv];
+  const sptr<int32_t> obs = scalar_view(g.obs + e0);
+  uint32_t* __restrict__ rows = reinterpret_cast<uint32_t*>(g.delta) + (e0 - g.delta_elem_base) * (2 * NPW);
+  const unsigned V = (unsigned)g.nobs;
+  double a_reg[R * C];  // a_reg[C r + k] = A[R rg + r][C cq + k]
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const double* src = g.a + (size_t)(R * rg + r) * NPW + C * cq;
+#pragma unroll
+    for (int k = 0; k < C; ++k) a_reg[C * r + k] = src[k];
+  }
+  unsigned bad = 0;
+  auto obs_s = [&](int t) -> unsigned {
+    const unsigned o = (unsigned)obs[t];
+    bad |= (o >= V);
+    return o < V ? o : 0u;
+  };
+  const int jw = owner ? lane : 0;
+  auto put = [&](int t, double v) {
+    if (owner) {
+      uint32_t* r = rows + (size_t)t * (2 * NPW) + jw;
+      __builtin_nontemporal_store(hi_word(v), r);
+      __builtin_nontemporal_store(lo_word(v), r + NPW);
+    }
+  };
+  {
+    const double d0 = ZI ? 0.0 : g.pi[jw] + g.et[(size_t)obs_s(0) * NPW + jw];  // cp.rs:66-68
+    if (owner) dl[0][jw] = d0;
+    __builtin_amdgcn_wave_barrier();
+    put(0, d0);
+  }
+  const int Tm1 = T - 1;
+  unsigned so[2];
+  double pe[2];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    pe[k] = g.et[(size_t)obs_s(min(1 + k, Tm1)) * NPW + jw];  // steps 1..2
+    so[k] = obs_s(min(3 + k, Tm1));                           // observations of steps 3..4
+  }
+  for (int t0 = 1; t0 < T; t0 += 2) {
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int t = t0 + k;
+      if (t >= T) break;
+      const double* src = &dl[(t - 1) & 1][R * rg];
+      f64x2 d[R / 2];
+#pragma unroll
+      for (int b = 0; b < R / 2; ++b) d[b] = *reinterpret_cast<const f64x2*>(src + 2 * b);
+#pragma unroll
+      for (int kc = 0; kc < C; ++kc) {
+        double m = d[0].x + a_reg[kc];  // s_i = d[i] + a[i,j]  (viterbi.rs:15)
+        m = __builtin_fmax(m, d[0].y + a_reg[C + kc]);
+#pragma unroll
+        for (int b = 1; b < R / 2; ++b) {
+          m = __builtin_fmax(m, d[b].x + a_reg[(2 * b) * C + kc]);
+          m = __builtin_fmax(m, d[b].y + a_reg[(2 * b + 1) * C + kc]);
+        }
+        part[C * cq + kc][rg] = m;
+      }
+      __builtin_amdgcn_wave_barrier();  // the partials are other lanes' (LDS: in wave order)
+      double dn = 0.0;
+      if (owner) {
+        const f64x2 p01 = *reinterpret_cast<const f64x2*>(&part[jw][0]);
+        const f64x2 p23 = *reinterpret_cast<const f64x2*>(&part[jw][2]);
+        const double m = __builtin_fmax(__builtin_fmax(p01.x, p01.y), __builtin_fmax(p23.x, p23.y));
+        dn = m + pe[k];  // (d + a) + b -- viterbi.rs:15-17
+        dl[t & 1][jw] = dn;
+      }
+      __builtin_amdgcn_wave_barrier();  // delta_t before the next step's reads
+      put(t, dn);
+      pe[k] = g.et[(size_t)so[k] * NPW + jw];  // step t+2
+      so[k] = obs_s(min(t + 4, Tm1));          // observation of step t+4
+    }
+  }
+  if (bad && lane == 0) g.status[seq] = CVK_SEQ_BADOBS;
+}
+
 hipError_t launch_t64_wave(const T64FwdArgs& fa, int64_t nseq, hipStream_t stream) {
   const dim3 grid((unsigned)((nseq + 3) / 4)), block(256);
-  if (fa.zero_init)
+  // N <= 48: the 48-state layout at four waves per SIMD (tuning key t64_wave = 2: always the
+  // 64-state one)
+  const bool w48 = fa.nstates > 0 && fa.nstates <= 48 && tuning().t64_wave != 2;
+  if (w48 && fa.zero_init)
+    hipLaunchKernelGGL(trellis_wave48_f64<true>, grid, block, 0, stream, fa);
+  else if (w48)
+    hipLaunchKernelGGL(trellis_wave48_f64<false>, grid, block, 0, stream, fa);
+  else if (fa.zero_init)
     hipLaunchKernelGGL(trellis_wave_f64<true>, grid, block, 0, stream, fa);
   else
     hipLaunchKernelGGL(trellis_wave_f64<false>, grid, block, 0, stream, fa);

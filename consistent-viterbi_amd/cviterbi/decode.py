@@ -257,10 +257,10 @@ def last_superseq_stats(hmm: HMM) -> dict:
     """How the last decode_superseq_cp ran (cv_last_superseq_stats): parallel (the certified
     per-sequence decode + host fold) or the serial chain, and how many sequences certified /
     re-ran through the serial chain kernel."""
-    out = (ctypes.c_int64 * 7)()
+    out = (ctypes.c_int64 * 9)()
     L.check(L.lib().cv_last_superseq_stats(hmm.handle, out))
     return dict(parallel=bool(out[0]), certified=out[1], rerun=out[2], runs=out[3], quantised=out[4],
-                speculated=out[5], spec_batches=out[6])
+                speculated=out[5], spec_batches=out[6], gathered=out[7], path_waits=out[8])
 
 
 def device_memory() -> dict:

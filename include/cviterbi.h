@@ -339,13 +339,15 @@ CV_API cv_status cv_viterbi_decode(cv_hmm* h, int64_t T, const int32_t* obs, int
  * CV_EINFEASIBLE when the maximum is -inf. */
 CV_API cv_status cv_decode_superseq_cp(cv_hmm* h, int64_t nseq, const int64_t* offsets, const int32_t* obs,
                                        int32_t* path_out, double* objective_out);
-/* How the last cv_decode_superseq_cp on this handle ran (out[7]): out[0] = 1 when the PARALLEL
+/* How the last cv_decode_superseq_cp on this handle ran (out[9]): out[0] = 1 when the PARALLEL
  * chain ran (every finite entry of the model in [-2^80, 0], every sequence feasible:
  * each sequence decoded on its own by the f64 trellis and certified to be the chain's own path
  * at the chain's running total), 0 for the serial chain; out[1] = sequences
  * certified, out[2] = sequences the serial chain kernel re-ran, out[3] = such runs, out[4] =
  * certified sequences folded by one quantised add, out[5] = uncertified sequences settled by
- * the parallel re-decode from their exact offsets (speculation), out[6] = such batches. */
+ * the parallel re-decode from their exact offsets (speculation), out[6] = such batches, out[7] =
+ * sequences whose paths the host walk fetched packed while the whole path copy ran beside it,
+ * out[8] = walk steps that had to wait for that copy (a prediction miss; 0 when it held). */
 CV_API cv_status cv_last_superseq_stats(const cv_hmm* h, int64_t* out);
 
 /* ---- trait Solver (viterbi_solver.rs:11-16) -------------------------------------------

@@ -316,7 +316,8 @@ def test_chain_cert_fused_vs_pass(gpu, nseq, force):
         (p0, o0), s0 = _par(h, off, obs, force=force)
     assert s1["parallel"] and s0["parallel"], (s1, s0)
     assert o1 == o0 and np.array_equal(p1, p0)
-    assert s1 == s0, (s1, s0)
+    drop = ("gathered", "path_waits")
+    assert {k: v for k, v in s1.items() if k not in drop} == {k: v for k, v in s0.items() if k not in drop}, (s1, s0)
     sp, sobj = _serial(h, off[:257], obs[:int(off[256])])
     (pp, op), _ = _par(h, off[:257], obs[:int(off[256])])
     assert op == sobj and np.array_equal(pp, sp)

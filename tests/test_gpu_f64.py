@@ -425,3 +425,29 @@ def test_t64_cp_seqs_per_wave(gpu, monkeypatch, s, n):
     h2 = cv.HMM(pi2, a2, b2)
     _assert_same(cv.decode_batch(h2, off2, obs2, dtype="f64", assoc="cp", rescore_f64=False),
                  O.decode_batch(pi2, a2, b2, off2, obs2, O.CP, np.float64), f"cp random S={s} N={n}")
+
+
+@pytest.mark.parametrize("assoc", ["viterbi", "decode"])
+@pytest.mark.parametrize("n", [5, 17, 33, 45, 48, 49])
+def test_t64_wave48_vs_wave64_and_oracle(gpu, n, assoc):
+    """N <= 48: trellis_wave48_f64 (48 states, 3 columns x 12 rows per lane, the four row groups'
+    maxima through LDS, four waves per SIMD) == trellis_wave_f64 on 64 padded states (tuning key
+    t64_wave = 2) == the oracle, bit for bit: ragged, empty and infeasible sequences, -inf
+    transitions, viterbi::decode's row 0 = 0 (ZI).  N = 49 keeps the 64-state kernel."""
+    pi, a, b = synth.random_hmm(n, 40, seed=480 + n, zero_frac=0.1)
+    b = b.copy()
+    b[:, 39] = -np.inf  # observation 39: no state emits it
+    rng = np.random.default_rng(480 + n)
+    lengths = rng.integers(0, 140, size=3000)
+    off = synth.offsets_from_lengths(lengths)
+    obs = rng.integers(0, 39, size=int(off[-1])).astype(np.int32)
+    obs[rng.integers(0, len(obs), size=4)] = 39
+    h = cv.HMM(pi, a, b)
+    got = cv.decode_batch(h, off, obs, dtype="f64", assoc=assoc, rescore_f64=False)
+    assert cv.last_timing(h)["kernel"] == "trellis_f64"
+    with h.tuned(t64_wave=2):
+        ref64 = cv.decode_batch(h, off, obs, dtype="f64", assoc=assoc, rescore_f64=False)
+    _assert_same(got, ref64, f"wave48 vs wave64 N={n} {assoc}")
+    ref = O.decode_batch(pi, a, b, off, obs, O.VITERBI if assoc == "viterbi" else O.DECODE, np.float64)
+    _assert_same(got, ref, f"wave48 vs oracle N={n} {assoc}")
+    assert np.any(got[2] == 1) and np.any(got[2] == 2)  # infeasible, empty
