@@ -48,6 +48,14 @@ HBM_PEAK = 8.0e12            # B/s, MI355X_MICROARCH.md chip table (spec)
 VALU_PAIR_PEAK = 3.93e13     # f32 (from,to) pairs/s: 256 CU x 4 SIMD x 32 lanes x 2.4 GHz / 2 VALU slots per pair
 F64_PAIR_PEAK = 1.966e13     # f64 (from,to) pairs/s: 256 CU x 64 lanes x 2.4 GHz / (v_add_f64 + v_max_f64)
 NOMINAL_GHZ = 2.4
+# measured f64 VALU roof (tools/microbench/valu_roof_f64.hip, profiles/r06_valu_roof.txt): lane-
+# pairs per clock per SIMD, each SIMD timed from its first wave's start to its last wave's end
+# (s_memtime), clock from s_memtime / s_memrealtime; pure add+max pairs at 2 waves / SIMD (the
+# forward's occupancy) and at 4, and the forward's own issue mix (2 dwordx4 A-row loads + 4
+# ds_read_b128 broadcasts per 32 pairs) at 2 waves
+VALU_ROOF_F64 = {"pairs_2w": 7.772, "pairs_4w": 7.884, "fwd_mix_2w": 7.006, "nominal": 8.0,
+                 "clock_ghz": 2.393, "source": "profiles/r06_valu_roof.txt"}
+SIMDS = 1024
 WORKSPACE = 48 << 30         # delta workspace cap: one forward launch per step at N=1 (34.4 GB)
 WORKSPACE_F64 = 80 << 30     # f64: one launch per step too (68.7 GB of f64 delta rows)
 PMC_F64 = "profiles/pmc_trellis_fwd_f64_c4.json"   # committed rocprofv3 PMC summary (traffic, clock)
@@ -528,6 +536,17 @@ def main():
     if pmc and pmc.get("clock_ghz"):
         valu.update({"clock_ghz_pmc": pmc["clock_ghz"], "frac_at_pmc_clock": valu_frac * NOMINAL_GHZ / pmc["clock_ghz"],
                      "clock_source": pmc["source"] + ": GRBM_GUI_ACTIVE / 8 XCDs over the kernel duration"})
+        if f64:  # against the MEASURED roof, per clock
+            per_clk = pairs_per_launch / fwd_launch_s / (SIMDS * pmc["clock_ghz"] * 1e9)
+            valu["measured_roof"] = {
+                "achieved_lane_pairs_per_clk_per_simd": per_clk,
+                "roof_lane_pairs_per_clk_per_simd": VALU_ROOF_F64["pairs_2w"],
+                "frac": per_clk / VALU_ROOF_F64["pairs_2w"],
+                "frac_of_4_wave_roof": per_clk / VALU_ROOF_F64["pairs_4w"],
+                "frac_of_fwd_mix_roof": per_clk / VALU_ROOF_F64["fwd_mix_2w"],
+                "basis": "pure v_add_f64 + v_max_f64 pairs at 2 waves per SIMD (the forward's occupancy), per-SIMD "
+                         "first-start to last-end s_memtime spans; the kernel's rate per clock at the PMC clock",
+                "source": VALU_ROOF_F64["source"]}
     out = {
         "metric": "trellis cells/s (N*T*batch), N=256 T=512 batch=65536",
         "value": value,

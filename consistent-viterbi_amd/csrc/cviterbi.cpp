@@ -1011,7 +1011,7 @@ cv_status decode_device(cv_hmm* h, int64_t nseq, const int64_t* offsets_host, co
       const int spw = cvk::t64_seqs_per_wave(n, h->cus, h->np64);
       // the S actually launched: CP / DP, NP = 1,024 and forced NP = 512 run S <= 4 (launch_t64_fwd)
       if (!side_ws)
-        h->last_mt = t64cp ? cvk::t64_cp_seqs_per_wave(spw, n)
+        h->last_mt = t64cp ? cvk::t64_cp_seqs_per_wave(spw, n, cvk::t64_cp_waves(h->np64, n))
                            : (fa.dp_assoc || h->np64 == 1024 || (h->np64 == 512 && o.forced)) ? std::min(spw, 4) : spw;
       {  // eight-wave workgroups: equal lengths (within 1/8), or >= 2 rounds of 64 x CUs
          // (ragged T in [32, 1024], chunks of 32,768: 158 vs 168 ms; one round, 16,384: 65.5

@@ -229,8 +229,10 @@ int t64_support_states(int n);
 int t64_seqs_per_wave(int64_t nseq, int cus, int np = 0);
 hipError_t launch_t64_fwd(int np, int s, const T64FwdArgs& fa, int64_t nseq, hipStream_t stream);
 // CP association (cp.rs:70-79): psi and the CP value d[psi] + (a[psi,j] + b[j,o]) in the forward
-// sequences per wave the CP forward launches for a requested s and batch size
-int t64_cp_seqs_per_wave(int s, int64_t nseq);
+// the CP forward's layout for a batch: waves per workgroup splitting the columns, then
+// sequences per workgroup for a requested s
+int t64_cp_waves(int np, int64_t nseq);
+int t64_cp_seqs_per_wave(int s, int64_t nseq, int w = 1);
 hipError_t launch_t64_cp_fwd(int np, int s, const T64FwdArgs& fa, int64_t nseq, hipStream_t stream);
 hipError_t launch_t64_bt(int np, const T64BtArgs& ba, int64_t nseq, hipStream_t stream);
 

@@ -906,9 +906,14 @@ __global__ __launch_bounds__(512) void trellis_fwd_f64_rs(T64FwdArgs g) {
 // layout as trellis_fwd_f64 (S sequences per wave, A rows streamed through a register ring).
 // S = 1 (round 5): one sequence per wave for small batches (the parallel chain's speculative
 // re-decodes, ~620 sequences at config-4 size), so every sequence has a SIMD of its own.
-template <int C, int S, int PF>
-__global__ __launch_bounds__(64) void trellis_cp_f64(T64FwdArgs g) {
-  constexpr int NP = 64 * C;
+// W > 1 (round 6): the workgroup's W waves split the columns (C per lane, NP = 64 C W) of the
+// same S sequences, delta_{t-1} shared in LDS behind the step's two workgroup barriers: each
+// A element streamed from L2 serves S sequences while a wave's per-step walk (256 rows x C
+// columns x S sequences x 4 VALU) stays short -- the chain's speculative batch is a few
+// hundred sequences, each step of which every sequence must finish before its next.
+template <int C, int S, int PF, int W = 1>
+__global__ __launch_bounds__(64 * W) void trellis_cp_f64(T64FwdArgs g) {
+  constexpr int NP = 64 * C * W;
   static_assert((S == 1 || S % 2 == 0) && PF % 2 == 0, "one sequence or pairs of sequences / rows");
   __shared__ __attribute__((aligned(16))) double dl[NP * S];  // delta_{t-1}: [row][S]
   const int lane = threadIdx.x;
@@ -1942,29 +1947,49 @@ hipError_t fwd_c(const T64FwdArgs& fa, int s, int64_t nseq, hipStream_t stream) 
 
 }  // namespace
 
-template <int C>
+template <int C, int W = 1>
 hipError_t cp_c(const T64FwdArgs& fa, int s, int64_t nseq, hipStream_t stream) {
-  const dim3 block(64);
+  const dim3 block(64 * W);
   switch (s) {
-    case 1: hipLaunchKernelGGL((trellis_cp_f64<C, 1, 4>), dim3((unsigned)nseq), block, 0, stream, fa); break;
-    case 2: hipLaunchKernelGGL((trellis_cp_f64<C, 2, 4>), dim3((unsigned)((nseq + 1) / 2)), block, 0, stream, fa); break;
-    case 4: hipLaunchKernelGGL((trellis_cp_f64<C, 4, 4>), dim3((unsigned)((nseq + 3) / 4)), block, 0, stream, fa); break;
+    case 1: hipLaunchKernelGGL((trellis_cp_f64<C, 1, 4, W>), dim3((unsigned)nseq), block, 0, stream, fa); break;
+    case 2: hipLaunchKernelGGL((trellis_cp_f64<C, 2, 4, W>), dim3((unsigned)((nseq + 1) / 2)), block, 0, stream, fa); break;
+    case 4: hipLaunchKernelGGL((trellis_cp_f64<C, 4, 4, W>), dim3((unsigned)((nseq + 3) / 4)), block, 0, stream, fa); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
 }
 
-int t64_cp_seqs_per_wave(int s, int64_t nseq) {
+// waves per workgroup splitting the columns (trellis_cp_f64's W): NP / 64 for the batches of at
+// most 4,096 sequences (the parallel chain's speculative re-decodes), else 1; tuning key
+// t64_cp_w = 1 keeps one wave per workgroup, > 1 forces the split
+int t64_cp_waves(int np, int64_t nseq) {
+  const int k = tuning().t64_cp_w;
+  if (k == 1 || np < 128) return 1;
+  return (k > 1 || nseq <= 4096) ? np / 64 : 1;
+}
+
+int t64_cp_seqs_per_wave(int s, int64_t nseq, int w) {
   s = s > 4 ? 4 : s;  // the argmax state (idx) costs registers: at most 4 sequences per wave
   // a batch that leaves SIMDs idle at two sequences per wave: one per wave (the sequences are
-  // independent, so the results are the same); tuning key t64_cp_s = 1 / 2 / 4 sets it
+  // independent, so the results are the same); tuning key t64_cp_s = 1 / 2 / 4 sets it; split
+  // columns (w > 1): 4 sequences share each A element
   if (const int k = tuning().t64_cp_s; k > 0) return k >= 4 ? 4 : k >= 2 ? 2 : 1;
+  if (w > 1) return 4;
   return nseq <= 1024 ? 1 : s;
 }
 
 hipError_t launch_t64_cp_fwd(int np, int s, const T64FwdArgs& fa, int64_t nseq, hipStream_t stream) {
   if (nseq <= 0) return hipSuccess;
-  s = t64_cp_seqs_per_wave(s, nseq);
+  const int w = t64_cp_waves(np, nseq);
+  s = t64_cp_seqs_per_wave(s, nseq, w);
+  if (w > 1) {
+    switch (np) {
+      case 128: return cp_c<1, 2>(fa, s, nseq, stream);
+      case 192: return cp_c<1, 3>(fa, s, nseq, stream);
+      case 256: return cp_c<1, 4>(fa, s, nseq, stream);
+      default: return hipErrorInvalidValue;
+    }
+  }
   switch (np) {
     case 64: return cp_c<1>(fa, s, nseq, stream);
     case 128: return cp_c<2>(fa, s, nseq, stream);

@@ -170,7 +170,8 @@ CV_API void cv_hmm_destroy(cv_hmm* h);
  *   chain_par_force 0     m > 0: every m-th sequence of the parallel chain taken as uncertified
  *   chain_spec 1          0: no speculative re-decode in the parallel chain
  *   chain_spec_kernel 0   1: speculation on trellis_cp_f64 instead of the generic CP kernel
- *   chain_copy_overlap 1  0: the parallel chain's path copy after its certificate pass
+ *   chain_copy_overlap 1  0: the parallel chain in one decode chunk, its path copy before the walk
+ *   chain_cert_fused 1    0: the chain's certificates by their own pass (cp_cert_f64), not the backtrack
  *   t64_s 0               f64 trellis sequences per wave 2 / 4 / 6 / 8 (0: by batch)
  *   t64_512 / t64_1024 -1 NP = 512 / 1,024 batch kernel: -1 auto, 0 never, 1 always
  *   t64_wg 1              0: one wave per workgroup instead of eight-wave units
@@ -179,6 +180,8 @@ CV_API void cv_hmm_destroy(cv_hmm* h);
  *   t64_wave 1            0: N <= 64 on the lock-step kernel, not one wave per sequence
  *   t64_bal 8             steps between SIMD-balancing updates (0: off)
  *   t64_cp_s 0            trellis_cp_f64 sequences per wave 1 / 2 / 4 (0: by batch)
+ *   t64_cp_w 0            trellis_cp_f64 waves splitting the columns: 1 never, > 1 always (0: up to
+ *                         4,096 sequences, NP >= 128)
  *   t64_bt_pf 0           backtrack_f64 rows in flight 2 / 4 / 8 / 16 / 32 (0: by NP)
  *   generic_s 0           generic kernels' sequences per workgroup 1 / 2 / 4 (0: by batch)
  *   generic_split 0, generic_split_k 0   1: K threads per state (generic_fwd_split), its K

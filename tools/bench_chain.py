@@ -1,7 +1,7 @@
 """CPSolver chained super-sequence decode (cv_decode_superseq_cp = solver kind gpu-cp, what
 main.rs:120 runs): wall time of the PARALLEL chain (per-sequence f64 trellis + certificates +
 host fold + serial re-runs of the uncertified sequences) on config-4-shaped inputs, with the
-serial chain kernel (CV_CHAIN_PAR=0) on a smaller slice for comparison; every parallel result
+serial chain kernel (tuning key chain_par = 0) on a smaller slice for comparison; every parallel result
 is checked against the serial chain where both run.
 
   python tools/bench_chain.py [nseq_full=65536] [nseq_cmp=2048]
@@ -18,14 +18,10 @@ from cviterbi import synth  # noqa: E402
 
 
 def run(h, off, obs, serial=False):
-    if serial:
-        os.environ["CV_CHAIN_PAR"] = "0"
-    try:
+    with h.tuned(chain_par=0 if serial else 1):  # tuning key: the serial chain kernel
         t0 = time.perf_counter()
         path, obj = cv.decode_superseq_cp(h, off, obs)
         el = time.perf_counter() - t0
-    finally:
-        os.environ.pop("CV_CHAIN_PAR", None)
     return path, obj, el, cv.last_superseq_stats(h)
 
 

@@ -1,6 +1,6 @@
 """The parallel CPSolver chain above N = 256 (cv_decode_superseq_cp = solver kind gpu-cp, what
 main.rs:120 runs; cp.rs:63-93 over utils.rs:24-38): wall time of the parallel chain vs the
-serial chain kernel (cp_superseq_chain, CV_CHAIN_PAR=0) on config-4-shaped inputs at N states
+serial chain kernel (cp_superseq_chain, tuning key chain_par = 0) on config-4-shaped inputs at N states
 (Dirichlet(1) log10 model, V = 1,024, T = 512), bit for bit (every element and the objective).
 
   python tools/bench_chain_large_n.py N [nseq=4096] [nseq_par_only=0]
@@ -21,8 +21,7 @@ from cviterbi import synth  # noqa: E402
 
 
 def run(h, off, obs, serial=False):
-    if serial:
-        os.environ["CV_CHAIN_PAR"] = "0"
+    h.set_tuning(chain_par=0 if serial else 1)  # tuning key: the serial chain kernel
     stop = threading.Event()
 
     def beat():  # the serial chain runs minutes in one library call (ctypes releases the GIL)
@@ -39,7 +38,7 @@ def run(h, off, obs, serial=False):
     finally:
         stop.set()
         hb.join()
-        os.environ.pop("CV_CHAIN_PAR", None)
+        h.set_tuning(chain_par=1)
     return path, obj, el, cv.last_superseq_stats(h)
 
 

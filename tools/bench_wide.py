@@ -40,7 +40,7 @@ def main():
     ap.add_argument("--nseq", default="4,64,1024")
     ap.add_argument("--T", type=int, default=8)
     ap.add_argument("--chain-len", type=int, default=64)
-    ap.add_argument("--wide-s", default="auto", help="CV_WIDE_S values for the wide runs, e.g. auto,1,2,4")
+    ap.add_argument("--wide-s", default="auto", help="tuning key wide_s values for the wide runs, e.g. auto,1,2,4")
     ap.add_argument("--assocs", default="viterbi,cp")
     args = ap.parse_args()
     threading.Thread(target=_beat, daemon=True).start()
@@ -53,13 +53,8 @@ def main():
             res = {}
             modes = (["lds"] if n <= 10240 else []) + ["wide" + x for x in args.wide_s.split(",")]
             for mode in modes:
-                os.environ.pop("CV_WIDE_S", None)
-                if mode.startswith("wide"):
-                    os.environ["CV_GENERIC_WIDE_MIN"] = "1"
-                    if mode != "wideauto":
-                        os.environ["CV_WIDE_S"] = mode[4:]
-                else:
-                    os.environ.pop("CV_GENERIC_WIDE_MIN", None)
+                h.set_tuning(wide_s=0 if mode in ("lds", "wideauto") else int(mode[4:]),
+                             generic_wide_min=1 if mode.startswith("wide") else 0)
                 for assoc in args.assocs.split(","):
                     ms, out = _time(lambda: cv.decode_batch(h, off, obs, dtype="f64", assoc=assoc, kernel="generic",
                                                             rescore_f64=False))
@@ -69,25 +64,20 @@ def main():
                     gbs = steps * n * n * 8 / (t["fwd_ms"] * 1e-3) / 1e9
                     print(f"N={n} nseq={nseq} T={args.T} {mode:8s} {assoc:7s} wall {ms:9.2f} ms  fwd {t['fwd_ms']:9.2f} ms "
                           f"bt {t['bt_ms']:6.2f} ms  table stream {gbs:7.1f} GB/s", flush=True)
-            os.environ.pop("CV_GENERIC_WIDE_MIN", None)
-            os.environ.pop("CV_WIDE_S", None)
+            h.set_tuning(wide_s=0, generic_wide_min=0)
             for (mode, assoc), out in res.items():
                 for x, y in zip(res[(modes[0], assoc)], out):
                     assert np.array_equal(x, y), (n, nseq, mode, assoc)
         # the serial chain
         off = synth.offsets_from_lengths(np.full(max(args.chain_len // 8, 1), 8))
         obs = synth.iid_obs(16, int(off[-1]), n)
-        os.environ["CV_CHAIN_PAR"] = "0"
+        h.set_tuning(chain_par=0)
         outs = {}
         for mode in (("lds", "wide") if n <= 10240 else ("wide",)):
-            if mode == "wide":
-                os.environ["CV_CHAIN_WIDE_MIN"] = "1"
-            else:
-                os.environ.pop("CV_CHAIN_WIDE_MIN", None)
+            h.set_tuning(chain_wide_min=1 if mode == "wide" else 0)
             ms, outs[mode] = _time(lambda: cv.decode_superseq_cp(h, off, obs), reps=1)
             print(f"N={n} chain L={int(off[-1])} {mode:4s} {ms:9.2f} ms  ({ms / int(off[-1]):.3f} ms per element)", flush=True)
-        os.environ.pop("CV_CHAIN_WIDE_MIN", None)
-        os.environ.pop("CV_CHAIN_PAR", None)
+        h.set_tuning(chain_wide_min=0, chain_par=1)
         if len(outs) == 2:
             assert outs["lds"][1] == outs["wide"][1] and np.array_equal(outs["lds"][0], outs["wide"][0])
         del h
