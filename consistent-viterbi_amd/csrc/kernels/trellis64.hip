@@ -1825,16 +1825,25 @@ __global__ __launch_bounds__(256) void trellis_wave_f64(T64FwdArgs g) {
 // the emission.  Max is exact and order-free, so values, rows and results are those of
 // trellis_wave_f64 bit for bit.  Rows go to HBM split-plane, 64 wide, for backtrack_f64
 // (columns >= N are never read: the backtrack masks candidates >= N).
-template <bool ZI>
+// Workgroups go to the CUs round-robin (block b and b + 256 share a CU), so a grid of four
+// rounds puts one workgroup of each quarter of the longest-first order on every CU; the odd
+// quarters run reversed (the block of rank r takes slots of rank 255 - r there), so every CU
+// and SIMD gets long with short sequences: equal sums instead of the longest of each quarter.
+template <bool ZI, int PD = 4>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void trellis_wave48_f64(T64FwdArgs g) {
-  constexpr int NPW = 64, NC = 48, C = 3, R = 12, LS = NC + 4;
+  constexpr int NPW = 64, NC = 48, C = 3, R = 12, LS = NC + 4, P = 256;
   __shared__ __attribute__((aligned(16))) double dl_all[4][2][LS];    // delta_{t-1} / delta_t per wave
   __shared__ __attribute__((aligned(16))) double part_all[4][NC][4];  // [col][rg] partial maxima
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
   const int rg = lane & 3, cq = lane >> 2;
   const bool owner = lane < NC;  // lane j < 48 owns column j after the fold
-  const int64_t slot = g.seq_begin + 4 * (int64_t)blockIdx.x + wv;
+  int blk = (int)blockIdx.x;
+  {
+    const int q = blk / P, r = blk % P;
+    if ((q & 1) && (q + 1) * P <= (int)gridDim.x) blk = q * P + (P - 1 - r);
+  }
+  const int64_t slot = g.seq_begin + 4 * (int64_t)blk + wv;
   if (slot >= g.seq_begin + g.nslots) return;
   const int64_t seq = g.order ? (int64_t)g.order[slot] : slot;
   const int64_t e0 = g.offsets[seq];
@@ -1873,16 +1882,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void t
     put(0, d0);
   }
   const int Tm1 = T - 1;
-  unsigned so[2];
-  double pe[2];
+  // emissions PD steps ahead (V = 50,000 at config 2: a 25.6 MB table, beyond L2)
+  unsigned so[PD];
+  double pe[PD];
 #pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    pe[k] = g.et[(size_t)obs_s(min(1 + k, Tm1)) * NPW + jw];  // steps 1..2
-    so[k] = obs_s(min(3 + k, Tm1));                           // observations of steps 3..4
+  for (int k = 0; k < PD; ++k) {
+    pe[k] = g.et[(size_t)obs_s(min(1 + k, Tm1)) * NPW + jw];  // steps 1..PD
+    so[k] = obs_s(min(PD + 1 + k, Tm1));                      // observations of steps PD+1..2PD
   }
-  for (int t0 = 1; t0 < T; t0 += 2) {
+  for (int t0 = 1; t0 < T; t0 += PD) {
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {
+    for (int k = 0; k < PD; ++k) {
       const int t = t0 + k;
       if (t >= T) break;
       const double* src = &dl[(t - 1) & 1][R * rg];
@@ -1911,8 +1921,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void t
       }
       __builtin_amdgcn_wave_barrier();  // delta_t before the next step's reads
       put(t, dn);
-      pe[k] = g.et[(size_t)so[k] * NPW + jw];  // step t+2
-      so[k] = obs_s(min(t + 4, Tm1));          // observation of step t+4
+      pe[k] = g.et[(size_t)so[k] * NPW + jw];  // step t+PD
+      so[k] = obs_s(min(t + 2 * PD, Tm1));     // observation of step t+2PD
     }
   }
   if (bad && lane == 0) g.status[seq] = CVK_SEQ_BADOBS;
@@ -1947,13 +1957,15 @@ hipError_t fwd_c(const T64FwdArgs& fa, int s, int64_t nseq, hipStream_t stream) 
 
 }  // namespace
 
-template <int C, int W = 1>
+// PF: A rows in flight per wave.  Split columns (W > 1, C = 1): a wave's step is 256 dependent
+// row loads of 8 B per lane from L2, so the ring must cover the L2 latency (PF = 32: 64 VGPRs)
+template <int C, int W = 1, int PF = 4>
 hipError_t cp_c(const T64FwdArgs& fa, int s, int64_t nseq, hipStream_t stream) {
   const dim3 block(64 * W);
   switch (s) {
-    case 1: hipLaunchKernelGGL((trellis_cp_f64<C, 1, 4, W>), dim3((unsigned)nseq), block, 0, stream, fa); break;
-    case 2: hipLaunchKernelGGL((trellis_cp_f64<C, 2, 4, W>), dim3((unsigned)((nseq + 1) / 2)), block, 0, stream, fa); break;
-    case 4: hipLaunchKernelGGL((trellis_cp_f64<C, 4, 4, W>), dim3((unsigned)((nseq + 3) / 4)), block, 0, stream, fa); break;
+    case 1: hipLaunchKernelGGL((trellis_cp_f64<C, 1, PF, W>), dim3((unsigned)nseq), block, 0, stream, fa); break;
+    case 2: hipLaunchKernelGGL((trellis_cp_f64<C, 2, PF, W>), dim3((unsigned)((nseq + 1) / 2)), block, 0, stream, fa); break;
+    case 4: hipLaunchKernelGGL((trellis_cp_f64<C, 4, PF, W>), dim3((unsigned)((nseq + 3) / 4)), block, 0, stream, fa); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
@@ -1983,10 +1995,11 @@ hipError_t launch_t64_cp_fwd(int np, int s, const T64FwdArgs& fa, int64_t nseq, 
   const int w = t64_cp_waves(np, nseq);
   s = t64_cp_seqs_per_wave(s, nseq, w);
   if (w > 1) {
+    const bool pf16 = tuning().t64_cp_pf == 16;  // A/B: 16 rows in flight instead of 32
     switch (np) {
-      case 128: return cp_c<1, 2>(fa, s, nseq, stream);
-      case 192: return cp_c<1, 3>(fa, s, nseq, stream);
-      case 256: return cp_c<1, 4>(fa, s, nseq, stream);
+      case 128: return pf16 ? cp_c<1, 2, 16>(fa, s, nseq, stream) : cp_c<1, 2, 32>(fa, s, nseq, stream);
+      case 192: return pf16 ? cp_c<1, 3, 16>(fa, s, nseq, stream) : cp_c<1, 3, 32>(fa, s, nseq, stream);
+      case 256: return pf16 ? cp_c<1, 4, 16>(fa, s, nseq, stream) : cp_c<1, 4, 32>(fa, s, nseq, stream);
       default: return hipErrorInvalidValue;
     }
   }

@@ -43,6 +43,7 @@ struct Tuning {
   int t64_wave = 1;            // 0: N <= 64 on the lock-step kernel instead of one wave per sequence
   int t64_bal = 8;             // steps between SIMD-balancing updates (0: off)
   int t64_cp_s = 0;            // trellis_cp_f64 sequences per wave 1 / 2 / 4 (0: by batch)
+  int t64_cp_pf = 0;           // split-column trellis_cp_f64 A rows in flight: 16 (0: 32)
   int t64_cp_w = 0;            // trellis_cp_f64 waves splitting the columns: 1 never, > 1 always (0: by batch)
   int t64_bt_pf = 0;           // backtrack_f64 rows in flight (0: by NP)
   // ---- generic and wide kernels (kernels/trellis.hip) ----

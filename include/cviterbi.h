@@ -181,7 +181,7 @@ CV_API void cv_hmm_destroy(cv_hmm* h);
  *   t64_bal 8             steps between SIMD-balancing updates (0: off)
  *   t64_cp_s 0            trellis_cp_f64 sequences per wave 1 / 2 / 4 (0: by batch)
  *   t64_cp_w 0            trellis_cp_f64 waves splitting the columns: 1 never, > 1 always (0: up to
- *                         4,096 sequences, NP >= 128)
+ *                         4,096 sequences, NP >= 128); t64_cp_pf 0: its A rows in flight 32 (16)
  *   t64_bt_pf 0           backtrack_f64 rows in flight 2 / 4 / 8 / 16 / 32 (0: by NP)
  *   generic_s 0           generic kernels' sequences per workgroup 1 / 2 / 4 (0: by batch)
  *   generic_split 0, generic_split_k 0   1: K threads per state (generic_fwd_split), its K

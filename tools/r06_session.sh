@@ -38,11 +38,14 @@ run() {
     c5) step c5 300 python3 -u tools/bench_configs.py c5 ;;
     tests) step tests 900 python3 -u -m pytest -q --maxfail=25 --timeout 200 --timeout-method thread -m gpu tests ;;
     chainq) step chainq 240 python3 -u tools/bench_chain.py 65536 256 ;;
-    chainab)  # the speculative batch's kernel: generic (default) / trellis_cp_f64 split columns S=4 / S=2
+    chainab)  # the speculative batch's kernel: generic / trellis_cp_f64 split columns (S, rows in flight)
       step chainab_gen 240 python3 -u tools/bench_chain.py 65536 256 &&
         CV_CHAIN_SPEC_KERNEL=1 step chainab_cp4 240 python3 -u tools/bench_chain.py 65536 256 &&
+        CV_CHAIN_SPEC_KERNEL=1 CV_T64_CP_PF=16 step chainab_cp4pf16 240 python3 -u tools/bench_chain.py 65536 256 &&
         CV_CHAIN_SPEC_KERNEL=1 CV_T64_CP_S=2 step chainab_cp2 240 python3 -u tools/bench_chain.py 65536 256 &&
-        CV_TRACE=1 CV_CHAIN_SPEC_KERNEL=1 step chainab_phases 240 python3 -u tools/bench_chain.py 65536 256 ;;
+        (cd /tmp && CV_CHAIN_SPEC_KERNEL=1 SERIAL=0 step chainab_trace 300 rocprofv3 --kernel-trace --memory-copy-trace \
+          --output-format csv -d $O/kt -o kt -- python3 $R/tools/bench_chain_large_n.py 256 256 65536) &&
+        python3 tools/trace_timeline.py $O/kt trellis_fwd_f64 > $O/chain_timeline.txt ;;
     chaintests) step chaintests 600 python3 -u -m pytest -q -x --timeout 200 --timeout-method thread -m gpu \
       tests/test_gpu_chain_par.py tests/test_gpu_f64.py -k "chain or cp_seqs or wave48" ;;
     smoke) step smoke 200 python3 -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" ;;
