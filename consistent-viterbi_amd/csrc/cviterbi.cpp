@@ -20,6 +20,7 @@
 #include <cstring>
 #include <memory>
 #include <functional>
+#include <limits>
 #include <mutex>
 #include <numeric>
 #include <string>
@@ -46,6 +47,17 @@ thread_local std::string g_err;
 #define CV_LOCK(h)                             \
   std::lock_guard<std::mutex> lk((h)->mu);     \
   cvk::TuningScope tuning_scope((h)->tuning)
+
+inline uint64_t dbits(double x) {
+  uint64_t b;
+  std::memcpy(&b, &x, 8);
+  return b;
+}
+inline double from_dbits(uint64_t b) {
+  double x;
+  std::memcpy(&x, &b, 8);
+  return x;
+}
 
 cv_status set_err(cv_status st, const char* fmt, ...) {
   char buf[512];
@@ -3229,7 +3241,7 @@ cv_status superseq_cp_par(cv_hmm* h, int64_t nseq, const int64_t* offsets, const
   std::vector<int32_t> gpath;
   std::vector<int64_t> gpos((size_t)nseq, -1);
   bool copy_joined = !overlap_copy;
-  int64_t path_waits = 0, gathered = 0;
+  int64_t path_waits = 0, gathered = 0, memo_hits = 0;
   {
     double smax = 0.0;
     for (double x : score) smax = std::max(smax, std::fabs(x));
@@ -3306,13 +3318,21 @@ cv_status superseq_cp_par(cv_hmm* h, int64_t nseq, const int64_t* offsets, const
   std::vector<std::pair<int64_t, std::vector<int32_t>>> deferred;
   // the fold of a certified path: M + q 2^(e-52) when M and the sequence's values share the
   // predicted binade 2^e (cp_quant_f64), else element by element
+  // the binade of a normal nonzero double from its exponent bits (std::ilogb otherwise)
+  auto ilogb_fast = [](double x) {
+    const uint64_t b = dbits(x);
+    const int be = (int)((b >> 52) & 0x7FF);
+    return (be != 0 && be != 0x7FF) ? be - 1023 : std::ilogb(x);
+  };
   auto fold = [&](int64_t k, double M, bool* quant) {
     *quant = false;
     const int e = ebin[(size_t)k];
-    if (e != cvk::CVK_NO_BINADE && !tie[(size_t)k] && M != 0.0 && std::ilogb(std::fabs(M)) == e &&
-        std::fabs((double)qv[(size_t)k]) < 0x1p53) {
-      const double Mn = M + std::ldexp((double)qv[(size_t)k], e - 52);
-      if (std::ilogb(std::fabs(Mn)) == e) {
+    if (e != cvk::CVK_NO_BINADE && !tie[(size_t)k] && M != 0.0 && ilogb_fast(M) == e &&
+        std::fabs((double)qv[(size_t)k]) < 0x1p53 && e - 52 > -1022 && e - 52 < 1023) {
+      // q 2^(e-52): |q| < 2^53 and a normal power of two, so the product is exact (= ldexp)
+      const double g2 = from_dbits((uint64_t)(e - 52 + 1023) << 52);
+      const double Mn = M + (double)qv[(size_t)k] * g2;
+      if (ilogb_fast(Mn) == e) {
         *quant = true;
         return Mn;
       }
@@ -3481,6 +3501,12 @@ cv_status superseq_cp_par(cv_hmm* h, int64_t nseq, const int64_t* offsets, const
   size_t spec_from = SIZE_MAX;  // position a batch was last launched from
   constexpr int64_t kSpecMax = 16384;
   DevBuf d_soff, d_sobs, d_spath, d_sres, d_sinit, d_slast;
+  // the prediction walk's certify() results, reused by the exact walk wherever it arrives at a
+  // sequence after a certified one with the same running maximum, bit for bit (certify is a
+  // function of the sequence, the maximum and the predecessor's kind): memo_in[x] = that
+  // maximum, memo_out[x] = the fold (NaN: not certified), memo_q[x] = quantised (2 = no memo)
+  std::vector<double> memo_in(ks.size()), memo_out(ks.size());
+  std::vector<uint8_t> memo_q(ks.size(), 2);
   auto speculate = [&](size_t x0) -> cv_status {
     std::vector<int64_t> F;
     std::vector<double> G;
@@ -3489,7 +3515,14 @@ cv_status superseq_cp_par(cv_hmm* h, int64_t nseq, const int64_t* offsets, const
     for (size_t y = x0; y < ks.size() && (int64_t)F.size() < kSpecMax; ++y) {
       double Mn;
       bool qd;
-      if (certify(y, Ms, y == x0 ? pk : CERT, &Mn, &qd)) {
+      const Kind ky = y == x0 ? pk : CERT;
+      const bool ok = certify(y, Ms, ky, &Mn, &qd);
+      if (ky == CERT) {
+        memo_in[y] = Ms;
+        memo_out[y] = ok ? Mn : std::numeric_limits<double>::quiet_NaN();
+        memo_q[y] = qd ? 1 : 0;
+      }
+      if (ok) {
         Ms = Mn;
         continue;
       }
@@ -3552,7 +3585,16 @@ cv_status superseq_cp_par(cv_hmm* h, int64_t nseq, const int64_t* offsets, const
     const int64_t e0 = off[(size_t)k], T = off[(size_t)k + 1] - e0;
     double Mn;
     bool qd;
-    if (certify(x, M, prev, &Mn, &qd)) {
+    bool ok;
+    if (prev == CERT && memo_q[x] != 2 && dbits(memo_in[x]) == dbits(M)) {
+      ok = !std::isnan(memo_out[x]);  // the prediction walk's decision at this very maximum
+      Mn = memo_out[x];
+      qd = memo_q[x] == 1;
+      ++memo_hits;
+    } else {
+      ok = certify(x, M, prev, &Mn, &qd);
+    }
+    if (ok) {
       if (in_run && (st = end_run(row_arg)) != CV_OK) return st;  // clean: the run ends in its argmax
       M = Mn;
       prev = CERT;
@@ -3603,7 +3645,11 @@ cv_status superseq_cp_par(cv_hmm* h, int64_t nseq, const int64_t* offsets, const
   }
   if (in_run && (st = end_run(row_arg)) != CV_OK) return st;  // cp.rs:86: first argmax of the last row
   if (path_st != CV_OK) return path_st;
-  trace_mark("chain: walk + runs");
+  if (trace_on()) {
+    char msg[96];
+    snprintf(msg, sizeof msg, "chain: walk + runs (%lld memo hits)", (long long)memo_hits);
+    trace_mark(msg);
+  }
   if ((st = join_copy()) != CV_OK) return st;
   for (const auto& d : deferred) std::memcpy(path_out + d.first, d.second.data(), d.second.size() * 4);
   trace_mark("chain: path copy joined");
