@@ -143,8 +143,11 @@ struct PinnedHost {
   PinnedHost() = default;
   PinnedHost(const PinnedHost&) = delete;
   PinnedHost& operator=(const PinnedHost&) = delete;
-  ~PinnedHost() {
+  ~PinnedHost() { release(); }
+  void release() {
     if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
   }
   bool ensure(size_t bytes) {
     if (cap >= bytes && p) return true;
@@ -1328,6 +1331,28 @@ CV_API cv_status cv_hmm_set_tuning(cv_hmm* h, const char* key, int64_t value) {
     h->nonpos_cache = -1;
     h->t64_ready = false;
   }
+  return CV_OK;
+}
+CV_API cv_status cv_hmm_release_workspaces(cv_hmm* h) {
+  if (!h) return set_err(CV_EINVAL, "null handle");
+  CV_LOCK(h);
+  cv_status st = set_device(h);
+  if (st != CV_OK) return st;
+  // every stream the workspaces were used on has drained before the memory goes
+  for (hipStream_t s : {h->stream, h->bt_stream, h->side.stream, h->side.hi, h->copy_stream})
+    if (s) HIP_TRY(hipStreamSynchronize(s));
+  for (DevBuf* b : {&h->ws_main, &h->ws_last, &h->ws_order, &h->side.main, &h->side.last, &h->side.order,
+                    &h->side.idx, &h->side.obs2, &h->side.path2, &h->side.res2, &h->st_off, &h->st_obs, &h->st_path,
+                    &h->st_score, &h->st_status, &h->st_forced, &h->cs_ranges, &h->cs_delta, &h->cs_g, &h->cs_mu,
+                    &h->cs_start, &h->cs_zero, &h->cs_queue, &h->cs_wrows, &h->cs_comp, &h->cs_words, &h->cs_flag,
+                    &h->cs_seg, &h->rs_rows, &h->rs_rowbase, &h->rs_resume, &h->rs_start, &h->rs_off2, &h->rs_ridx,
+                    &h->rs_slot, &h->rs_obs2, &h->rs_frc2, &h->rs_path2, &h->rs_srows, &h->rs_srowbase, &h->rs_cert,
+                    &h->chainb.off, &h->chainb.obs, &h->chainb.path, &h->chainb.res, &h->chainb.cert, &h->chainb.ebin,
+                    &h->chainb.q, &h->chainb.ends, &h->chainb.gid, &h->chainb.gpath})
+    b->release();
+  h->ws_rec = false;
+  h->side.ws_rec = false;
+  h->chain_pin.release();
   return CV_OK;
 }
 CV_API cv_status cv_hmm_get_tuning(const cv_hmm* h, const char* key, int64_t* value) {
@@ -3112,7 +3137,10 @@ cv_status superseq_cp_par(cv_hmm* h, int64_t nseq, const int64_t* offsets, const
   std::vector<std::pair<int64_t, int64_t>> dchunks;
   st = decode_device(h, nseq, off.data(), d_off.as<int64_t>(), d_obs.as<int32_t>(), o, d_path.as<int32_t>(), d_score,
                      d_status, stream, nullptr, false, d_cert.as<double>(), nullptr, nullptr, &dchunks);
-  if (st == CV_EUNSUPPORTED && !small) return CV_OK;  // no rows to certify (generic_rows = 0): serial chain
+  if (st == CV_EUNSUPPORTED && !small) {  // no rows to certify (generic_rows = 0): the serial chain
+    g_err.clear();                         // runs, and the public call succeeds
+    return CV_OK;
+  }
   if (st != CV_OK) return st;
   std::vector<double> score((size_t)nseq), cert((size_t)nseq * 2);
   std::vector<uint8_t> status((size_t)nseq);

@@ -41,7 +41,7 @@ EXPORTS = [
     "cv_solver_create", "cv_solver_solve", "cv_solver_get_solution", "cv_solver_get_objective",
     "cv_solver_get_name", "cv_solver_get_explored_nodes", "cv_solver_destroy",
     "cv_hmm_fit_mle", "cv_hmm_fit_train", "cv_solver_write_cfn",
-    "cv_hmm_set_tuning", "cv_hmm_get_tuning", "cv_tuning_key",
+    "cv_hmm_set_tuning", "cv_hmm_get_tuning", "cv_tuning_key", "cv_hmm_release_workspaces",
 ]
 
 
@@ -105,6 +105,7 @@ def lib():
         "cv_hmm_set_tuning": ([P, ctypes.c_char_p, I64], S),
         "cv_hmm_get_tuning": ([P, ctypes.c_char_p, P], S),
         "cv_tuning_key": ([I32], ctypes.c_char_p),
+        "cv_hmm_release_workspaces": ([P], S),
         "cv_hmm_nstates": ([P], I32),
         "cv_hmm_nobs": ([P], I64),
         "cv_hmm_ndims": ([P], I32),

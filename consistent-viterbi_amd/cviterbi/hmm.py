@@ -72,6 +72,10 @@ class HMM:
         for k, v in keys.items():
             L.check(L.lib().cv_hmm_set_tuning(self._h, k.encode(), int(v)))
 
+    def release_workspaces(self):
+        """cv_hmm_release_workspaces: free the decode workspaces this handle keeps between calls."""
+        L.check(L.lib().cv_hmm_release_workspaces(self._h))
+
     def tuning(self, key) -> int:
         """cv_hmm_get_tuning: the handle's current value of one tuning key."""
         v = ctypes.c_int64()

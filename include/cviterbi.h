@@ -194,6 +194,12 @@ CV_API void cv_hmm_destroy(cv_hmm* h);
  *                         per-sequence E-step kernels / the xi GEMM path at every N
  * Unknown keys and values outside int32 are CV_EINVAL.  cv_tuning_key(i) lists the keys
  * (NULL past the last). */
+/* Frees the handle's decode workspaces (delta rows, the constrained decode's and the parallel
+ * chain's per-call buffers, pinned staging), which are otherwise kept grow-only between calls
+ * so repeated calls do not reallocate: e.g. ~0.4 GB of chain buffers plus the 34-69 GB delta
+ * workspace after a config-4-sized cv_decode_superseq_cp / cv_decode_batch.  The model tables
+ * stay; the next call allocates what it needs again.  Waits for the handle's streams. */
+CV_API cv_status cv_hmm_release_workspaces(cv_hmm* h);
 CV_API cv_status cv_hmm_set_tuning(cv_hmm* h, const char* key, int64_t value);
 CV_API cv_status cv_hmm_get_tuning(const cv_hmm* h, const char* key, int64_t* value);
 CV_API const char* cv_tuning_key(int32_t i);

@@ -451,3 +451,21 @@ def test_t64_wave48_vs_wave64_and_oracle(gpu, n, assoc):
     ref = O.decode_batch(pi, a, b, off, obs, O.VITERBI if assoc == "viterbi" else O.DECODE, np.float64)
     _assert_same(got, ref, f"wave48 vs oracle N={n} {assoc}")
     assert np.any(got[2] == 1) and np.any(got[2] == 2)  # infeasible, empty
+
+
+def test_release_workspaces(gpu):
+    """cv_hmm_release_workspaces frees the grow-only decode workspaces (the parallel
+    chain's ~0.4 GB of per-call buffers stayed for the handle's life); the next decode
+    allocates again and returns the same bits."""
+    c = synth.config("c4", 2048)
+    pi, a, b, off, obs = c["pi"], c["a"], c["b"], c["offsets"], c["obs"]
+    h = cv.HMM(pi, a, b)
+    p0, o0 = cv.decode_superseq_cp(h, off, obs)
+    ref = cv.decode_batch(h, off, obs, dtype="f64", rescore_f64=False)
+    held = cv.device_memory()["current"]
+    h.release_workspaces()
+    after = cv.device_memory()["current"]
+    assert after < held - 2048 * 512 * 256 * 8, (held, after)  # at least the delta rows went
+    p1, o1 = cv.decode_superseq_cp(h, off, obs)
+    assert o1 == o0 and np.array_equal(p1, p0)
+    _assert_same(cv.decode_batch(h, off, obs, dtype="f64", rescore_f64=False), ref, "after release")
