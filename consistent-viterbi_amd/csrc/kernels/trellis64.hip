@@ -1849,6 +1849,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void t
   const int64_t e0 = g.offsets[seq];
   const int T = (int)(g.offsets[seq + 1] - e0);
   if (T <= 0) return;  // the backtrack reports empty sequences
+  // issue priority by length (all waves start together, so the longest has the most left
+  // throughout): a SIMD's longest sequence runs near its one-wave pace while the shorter ones
+  // fill its latency gaps, instead of finishing alone at the end (tuning key t64_bal = 0: off)
+  if (g.balance) {
+    const int tq = T >> 5;  // 32-step bands
+    if (tq >= 3)
+      __builtin_amdgcn_s_setprio(3);
+    else if (tq == 2)
+      __builtin_amdgcn_s_setprio(2);
+    else if (tq == 1)
+      __builtin_amdgcn_s_setprio(1);
+  }
   double(*dl)[LS] = dl_all[wv];
   double(*part)[4] = part_all[wv];
   const sptr<int32_t> obs = scalar_view(g.obs + e0);
@@ -1928,153 +1940,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void t
   if (bad && lane == 0) g.status[seq] = CVK_SEQ_BADOBS;
 }
 
-// trellis_wave48x2_f64<ZI>: the same 48-state lane layout with TWO sequences per wave (slots
-// 2w and 2w + 1 of the longest-first order: near-equal lengths), in lock step up to the longer
-// one.  Each A fragment in registers serves both, and each step's two LDS round trips (the
-// partial maxima, then delta_t) are shared by twice the VALU work, so fewer waves hide them:
-// 3 waves per SIMD (<= 168 VGPRs), 2,048 waves for config 2's 4,096 sequences.  Same values,
-// bit for bit (max is exact and order-free).
-template <bool ZI, int PD = 2>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void trellis_wave48x2_f64(T64FwdArgs g) {
-  constexpr int NPW = 64, NC = 48, C = 3, R = 12, LS = NC + 4, P = 256, S = 2;
-  __shared__ __attribute__((aligned(16))) double dl_all[4][S][2][LS];
-  __shared__ __attribute__((aligned(16))) double part_all[4][S][NC][4];
-  const int lane = threadIdx.x & 63;
-  const int wv = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
-  const int rg = lane & 3, cq = lane >> 2;
-  const bool owner = lane < NC;
-  const int jw = owner ? lane : 0;
-  int blk = (int)blockIdx.x;
-  {
-    const int q = blk / P, r = blk % P;
-    if ((q & 1) && (q + 1) * P <= (int)gridDim.x) blk = q * P + (P - 1 - r);
-  }
-  const int64_t slot0 = g.seq_begin + S * (4 * (int64_t)blk + wv);
-  const int64_t slot_end = g.seq_begin + g.nslots;
-  if (slot0 >= slot_end) return;
-  int64_t seq[S], e0[S];
-  int T[S];
-  int Tmax = 0;
-#pragma unroll
-  for (int q = 0; q < S; ++q) {
-    seq[q] = -1;
-    e0[q] = 0;
-    T[q] = 0;
-    if (slot0 + q < slot_end) {
-      seq[q] = g.order ? (int64_t)g.order[slot0 + q] : slot0 + q;
-      e0[q] = g.offsets[seq[q]];
-      T[q] = (int)(g.offsets[seq[q] + 1] - e0[q]);
-    }
-    Tmax = T[q] > Tmax ? T[q] : Tmax;
-  }
-  if (Tmax <= 0) return;  // the backtrack reports empty sequences
-  const unsigned V = (unsigned)g.nobs;
-  double a_reg[R * C];
-#pragma unroll
-  for (int r = 0; r < R; ++r) {
-    const double* src = g.a + (size_t)(R * rg + r) * NPW + C * cq;
-#pragma unroll
-    for (int k = 0; k < C; ++k) a_reg[C * r + k] = src[k];
-  }
-  unsigned bad = 0;
-  auto obs_s = [&](int q, int t) -> unsigned {  // observation t of sequence q (clamped, checked)
-    if (t >= T[q]) return 0u;
-    const unsigned o = (unsigned)g.obs[e0[q] + t];
-    bad |= (o >= V) ? (1u << q) : 0u;
-    return o < V ? o : 0u;
-  };
-  auto put = [&](int q, int t, double v) {
-    if (owner) {
-      uint32_t* r = reinterpret_cast<uint32_t*>(g.delta) + (e0[q] - g.delta_elem_base + t) * (2 * NPW) + jw;
-      __builtin_nontemporal_store(hi_word(v), r);
-      __builtin_nontemporal_store(lo_word(v), r + NPW);
-    }
-  };
-#pragma unroll
-  for (int q = 0; q < S; ++q) {
-    if (T[q] > 0) {
-      const double d0 = ZI ? 0.0 : g.pi[jw] + g.et[(size_t)obs_s(q, 0) * NPW + jw];  // cp.rs:66-68
-      if (owner) dl_all[wv][q][0][jw] = d0;
-      put(q, 0, d0);
-    }
-  }
-  __builtin_amdgcn_wave_barrier();
-  unsigned so[S][PD];
-  double pe[S][PD];
-#pragma unroll
-  for (int q = 0; q < S; ++q)
-#pragma unroll
-    for (int k = 0; k < PD; ++k) {
-      pe[q][k] = g.et[(size_t)obs_s(q, 1 + k) * NPW + jw];
-      so[q][k] = obs_s(q, PD + 1 + k);
-    }
-  for (int t0 = 1; t0 < Tmax; t0 += PD) {
-#pragma unroll
-    for (int k = 0; k < PD; ++k) {
-      const int t = t0 + k;
-      if (t >= Tmax) break;
-      f64x2 d[S][R / 2];
-#pragma unroll
-      for (int q = 0; q < S; ++q) {
-        const double* src = &dl_all[wv][q][(t - 1) & 1][R * rg];
-#pragma unroll
-        for (int b = 0; b < R / 2; ++b) d[q][b] = *reinterpret_cast<const f64x2*>(src + 2 * b);
-      }
-#pragma unroll
-      for (int kc = 0; kc < C; ++kc) {
-        double m[S];
-#pragma unroll
-        for (int q = 0; q < S; ++q) {
-          m[q] = d[q][0].x + a_reg[kc];  // s_i = d[i] + a[i,j]  (viterbi.rs:15)
-          m[q] = __builtin_fmax(m[q], d[q][0].y + a_reg[C + kc]);
-        }
-#pragma unroll
-        for (int b = 1; b < R / 2; ++b)
-#pragma unroll
-          for (int q = 0; q < S; ++q) {
-            m[q] = __builtin_fmax(m[q], d[q][b].x + a_reg[(2 * b) * C + kc]);
-            m[q] = __builtin_fmax(m[q], d[q][b].y + a_reg[(2 * b + 1) * C + kc]);
-          }
-#pragma unroll
-        for (int q = 0; q < S; ++q) part_all[wv][q][C * cq + kc][rg] = m[q];
-      }
-      __builtin_amdgcn_wave_barrier();  // the partials are other lanes' (LDS: in wave order)
-      double dn[S] = {};
-#pragma unroll
-      for (int q = 0; q < S; ++q)
-        if (owner) {
-          const f64x2 p01 = *reinterpret_cast<const f64x2*>(&part_all[wv][q][jw][0]);
-          const f64x2 p23 = *reinterpret_cast<const f64x2*>(&part_all[wv][q][jw][2]);
-          const double mm = __builtin_fmax(__builtin_fmax(p01.x, p01.y), __builtin_fmax(p23.x, p23.y));
-          dn[q] = mm + pe[q][k];  // (d + a) + b -- viterbi.rs:15-17
-          dl_all[wv][q][t & 1][jw] = dn[q];
-        }
-      __builtin_amdgcn_wave_barrier();  // delta_t before the next step's reads
-#pragma unroll
-      for (int q = 0; q < S; ++q) {
-        if (t < T[q]) put(q, t, dn[q]);  // a finished sequence keeps stepping in LDS only
-        pe[q][k] = g.et[(size_t)so[q][k] * NPW + jw];
-        so[q][k] = obs_s(q, t + 2 * PD);
-      }
-    }
-  }
-  if (lane == 0) {
-#pragma unroll
-    for (int q = 0; q < S; ++q)
-      if (bad & (1u << q)) g.status[seq[q]] = CVK_SEQ_BADOBS;
-  }
-}
-
 hipError_t launch_t64_wave(const T64FwdArgs& fa, int64_t nseq, hipStream_t stream) {
-  // N <= 48, tuning key t64_wave48_s = 2 (default) / 1: two / one sequences per wave
-  if (fa.nstates > 0 && fa.nstates <= 48 && tuning().t64_wave != 2 && tuning().t64_wave48_s != 1) {
-    const dim3 grid2((unsigned)((nseq + 7) / 8)), block2(256);
-    if (fa.zero_init)
-      hipLaunchKernelGGL(trellis_wave48x2_f64<true>, grid2, block2, 0, stream, fa);
-    else
-      hipLaunchKernelGGL(trellis_wave48x2_f64<false>, grid2, block2, 0, stream, fa);
-    return hipGetLastError();
-  }
+  // (a two-sequences-per-wave variant, three waves per SIMD, measured 0.153 vs 0.070 ms at
+  // config 2 and was removed)
   const dim3 grid((unsigned)((nseq + 3) / 4)), block(256);
   // N <= 48: the 48-state layout at four waves per SIMD (tuning key t64_wave = 2: always the
   // 64-state one)

@@ -23,7 +23,7 @@ const Key kKeys[] = {
     CVK_KEY(chain_spec),     CVK_KEY(chain_spec_kernel), CVK_KEY(chain_copy_overlap), CVK_KEY(chain_cert_fused),
     CVK_KEY(t64_s),
     CVK_KEY(t64_512),        CVK_KEY(t64_1024),          CVK_KEY(t64_wg),            CVK_KEY(t64_wg_force),
-    CVK_KEY(t64_rs),         CVK_KEY(t64_w2),            CVK_KEY(t64_wave),          CVK_KEY(t64_wave48_s),          CVK_KEY(t64_bal),
+    CVK_KEY(t64_rs),         CVK_KEY(t64_w2),            CVK_KEY(t64_wave),          CVK_KEY(t64_bal),
     CVK_KEY(t64_cp_s),       CVK_KEY(t64_cp_w),          CVK_KEY(t64_cp_pf),          CVK_KEY(t64_bt_pf),         CVK_KEY(generic_s),         CVK_KEY(generic_split),
     CVK_KEY(generic_split_k), CVK_KEY(generic_wide),     CVK_KEY(generic_wide_min),  CVK_KEY(wide_s),
     CVK_KEY(ext_wide_min),   CVK_KEY(chain_wide),        CVK_KEY(chain_wide_min),    CVK_KEY(f32_onebar),

@@ -40,7 +40,6 @@ struct Tuning {
   int t64_wg_force = 0;        // 1: the eight-wave layouts whatever the batch's lengths
   int t64_rs = 1;              // 0: small batches' column-split pairs instead of the row split
   int t64_w2 = 1;              // 0: no pair-of-waves small-batch layout
-  int t64_wave48_s = 0;        // N <= 48 one-wave kernel: 1 or 2 (0: 2) sequences per wave
   int t64_wave = 1;            // 0: N <= 64 on the lock-step kernel instead of one wave per sequence
   int t64_bal = 8;             // steps between SIMD-balancing updates (0: off)
   int t64_cp_s = 0;            // trellis_cp_f64 sequences per wave 1 / 2 / 4 (0: by batch)

@@ -178,8 +178,7 @@ CV_API void cv_hmm_destroy(cv_hmm* h);
  *   t64_wg_force 0        1: eight-wave units whatever the batch's lengths
  *   t64_rs 1 / t64_w2 1   0: no row-split / no pair-of-waves small-batch layout
  *   t64_wave 1            0: N <= 64 on the lock-step kernel, not one wave per sequence; 2: N <= 48
- *                         on the 64-state one-wave kernel; t64_wave48_s 0: the 48-state kernel's
- *                         sequences per wave 2 (1)
+ *                         on the 64-state one-wave kernel
  *   t64_bal 8             steps between SIMD-balancing updates (0: off)
  *   t64_cp_s 0            trellis_cp_f64 sequences per wave 1 / 2 / 4 (0: by batch)
  *   t64_cp_w 0            trellis_cp_f64 waves splitting the columns: 1 never, > 1 always (0: up to

@@ -430,9 +430,8 @@ def test_t64_cp_seqs_per_wave(gpu, monkeypatch, s, n):
 @pytest.mark.parametrize("assoc", ["viterbi", "decode"])
 @pytest.mark.parametrize("n", [5, 17, 33, 45, 48, 49])
 def test_t64_wave48_vs_wave64_and_oracle(gpu, n, assoc):
-    """N <= 48: trellis_wave48x2_f64 (two sequences per wave, the default) and trellis_wave48_f64
-    (one; 48 states, 3 columns x 12 rows per lane, the four row groups' maxima through LDS) ==
-    trellis_wave_f64 on 64 padded states (tuning key
+    """N <= 48: trellis_wave48_f64 (48 states, 3 columns x 12 rows per lane, the four row groups'
+    maxima through LDS, four waves per SIMD) == trellis_wave_f64 on 64 padded states (tuning key
     t64_wave = 2) == the oracle, bit for bit: ragged, empty and infeasible sequences, -inf
     transitions, viterbi::decode's row 0 = 0 (ZI).  N = 49 keeps the 64-state kernel."""
     pi, a, b = synth.random_hmm(n, 40, seed=480 + n, zero_frac=0.1)
@@ -449,9 +448,6 @@ def test_t64_wave48_vs_wave64_and_oracle(gpu, n, assoc):
     with h.tuned(t64_wave=2):
         ref64 = cv.decode_batch(h, off, obs, dtype="f64", assoc=assoc, rescore_f64=False)
     _assert_same(got, ref64, f"wave48 vs wave64 N={n} {assoc}")
-    with h.tuned(t64_wave48_s=1):  # one sequence per wave (the default runs two)
-        one = cv.decode_batch(h, off, obs, dtype="f64", assoc=assoc, rescore_f64=False)
-    _assert_same(one, ref64, f"wave48 S=1 vs wave64 N={n} {assoc}")
     ref = O.decode_batch(pi, a, b, off, obs, O.VITERBI if assoc == "viterbi" else O.DECODE, np.float64)
     _assert_same(got, ref, f"wave48 vs oracle N={n} {assoc}")
     assert np.any(got[2] == 1) and np.any(got[2] == 2)  # infeasible, empty

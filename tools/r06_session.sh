@@ -35,6 +35,9 @@ run() {
           -d $O/kt -o kt -- python3 $R/tools/bench_chain_large_n.py 256 256 65536) &&
         python3 tools/trace_timeline.py $O/kt trellis_fwd_f64 > $O/chain_timeline.txt ;;
     c2) REPS=20 step c2 200 python3 -u tools/bench_configs.py c2f64 c3f64 ;;
+    c2ab) REPS=50 step c2ab_on 200 python3 -u tools/bench_configs.py c2f64 &&
+      REPS=50 CV_T64_BAL=0 step c2ab_off 200 python3 -u tools/bench_configs.py c2f64 &&
+      REPS=50 CV_T64_WAVE=2 step c2ab_w64 200 python3 -u tools/bench_configs.py c2f64 ;;
     c5) step c5 300 python3 -u tools/bench_configs.py c5 ;;
     tests) step tests 900 python3 -u -m pytest -q --maxfail=25 --timeout 200 --timeout-method thread -m gpu tests ;;
     chainq) step chainq 240 python3 -u tools/bench_chain.py 65536 256 ;;
