@@ -1831,13 +1831,12 @@ __global__ __launch_bounds__(256) void trellis_wave_f64(T64FwdArgs g) {
 // and SIMD gets long with short sequences: equal sums instead of the longest of each quarter.
 template <bool ZI, int PD = 4>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void trellis_wave48_f64(T64FwdArgs g) {
-  constexpr int NPW = 64, NC = 48, C = 3, R = 12, LS = NC + 4, P = 256;
-  __shared__ __attribute__((aligned(16))) double dl_all[4][2][LS];    // delta_{t-1} / delta_t per wave
-  __shared__ __attribute__((aligned(16))) double part_all[4][NC][4];  // [col][rg] partial maxima
+  constexpr int NPW = 64, C = 3, R = 12, LS = NPW + 4, P = 256;
+  __shared__ __attribute__((aligned(16))) double dl_all[4][2][LS];     // delta_{t-1} / delta_t per wave
+  __shared__ __attribute__((aligned(16))) double part_all[4][NPW][4];  // [col][rg] partial maxima
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
   const int rg = lane & 3, cq = lane >> 2;
-  const bool owner = lane < NC;  // lane j < 48 owns column j after the fold
   int blk = (int)blockIdx.x;
   {
     const int q = blk / P, r = blk % P;
@@ -1849,21 +1848,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void t
   const int64_t e0 = g.offsets[seq];
   const int T = (int)(g.offsets[seq + 1] - e0);
   if (T <= 0) return;  // the backtrack reports empty sequences
-  // issue priority by length (all waves start together, so the longest has the most left
-  // throughout): a SIMD's longest sequence runs near its one-wave pace while the shorter ones
-  // fill its latency gaps, instead of finishing alone at the end (tuning key t64_bal = 0: off)
-  if (g.balance) {
-    const int tq = T >> 5;  // 32-step bands
-    if (tq >= 3)
-      __builtin_amdgcn_s_setprio(3);
-    else if (tq == 2)
-      __builtin_amdgcn_s_setprio(2);
-    else if (tq == 1)
-      __builtin_amdgcn_s_setprio(1);
-  }
   double(*dl)[LS] = dl_all[wv];
   double(*part)[4] = part_all[wv];
-  const sptr<int32_t> obs = scalar_view(g.obs + e0);
+  // Every lane runs every instruction of a step (lanes >= 48 fold columns 48..63, which no
+  // partial reaches: their rows land in the 64-wide rows' padding, which the backtrack masks),
+  // so no branch splits the step's memory operations and the waits before each use count only
+  // what is outstanding; observations come through per-lane (vector) loads of one uniform
+  // address, so no scalar load shares the LDS reads' counter.
+  int vz;
+  asm volatile("v_mov_b32 %0, 0" : "=v"(vz));  // a per-lane zero: keeps the observation loads on the vector path
+  const int32_t* __restrict__ obs = g.obs + e0 + vz;
   uint32_t* __restrict__ rows = reinterpret_cast<uint32_t*>(g.delta) + (e0 - g.delta_elem_base) * (2 * NPW);
   const unsigned V = (unsigned)g.nobs;
   double a_reg[R * C];  // a_reg[C r + k] = A[R rg + r][C cq + k]
@@ -1873,71 +1867,72 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void t
 #pragma unroll
     for (int k = 0; k < C; ++k) a_reg[C * r + k] = src[k];
   }
+  part[lane][0] = part[lane][1] = part[lane][2] = part[lane][3] = 0.0;  // columns 48..63 stay 0
   unsigned bad = 0;
-  auto obs_s = [&](int t) -> unsigned {
-    const unsigned o = (unsigned)obs[t];
+  auto eaddr = [&](unsigned o) -> const double* {
     bad |= (o >= V);
-    return o < V ? o : 0u;
+    return g.et + (size_t)(o < V ? o : 0u) * NPW + lane;
   };
-  const int jw = owner ? lane : 0;
   auto put = [&](int t, double v) {
-    if (owner) {
-      uint32_t* r = rows + (size_t)t * (2 * NPW) + jw;
-      __builtin_nontemporal_store(hi_word(v), r);
-      __builtin_nontemporal_store(lo_word(v), r + NPW);
-    }
+    uint32_t* r = rows + (size_t)t * (2 * NPW) + lane;
+    __builtin_nontemporal_store(hi_word(v), r);
+    __builtin_nontemporal_store(lo_word(v), r + NPW);
   };
   {
-    const double d0 = ZI ? 0.0 : g.pi[jw] + g.et[(size_t)obs_s(0) * NPW + jw];  // cp.rs:66-68
-    if (owner) dl[0][jw] = d0;
+    const double d0 = ZI ? 0.0 : g.pi[lane] + *eaddr((unsigned)obs[0]);  // cp.rs:66-68
+    dl[0][lane] = d0;
     __builtin_amdgcn_wave_barrier();
     put(0, d0);
   }
   const int Tm1 = T - 1;
-  // emissions PD steps ahead (V = 50,000 at config 2: a 25.6 MB table, beyond L2)
+  // emissions PD steps ahead (V = 50,000 at config 2: a 25.6 MB table, beyond L2), their
+  // observations PD steps before that
   unsigned so[PD];
   double pe[PD];
 #pragma unroll
   for (int k = 0; k < PD; ++k) {
-    pe[k] = g.et[(size_t)obs_s(min(1 + k, Tm1)) * NPW + jw];  // steps 1..PD
-    so[k] = obs_s(min(PD + 1 + k, Tm1));                      // observations of steps PD+1..2PD
+    pe[k] = *eaddr((unsigned)obs[min(1 + k, Tm1)]);  // steps 1..PD
+    so[k] = (unsigned)obs[min(PD + 1 + k, Tm1)];     // observations of steps PD+1..2PD
   }
-  for (int t0 = 1; t0 < T; t0 += PD) {
+  auto step = [&](int t, int k) {
+    const double* src = &dl[(t - 1) & 1][R * rg];
+    // row-major: each pair of delta rows is consumed by the 3 columns as it arrives, so few
+    // delta VGPRs are live beside A's 72 (four waves per SIMD leave 128)
+    double m[C];
 #pragma unroll
-    for (int k = 0; k < PD; ++k) {
-      const int t = t0 + k;
-      if (t >= T) break;
-      const double* src = &dl[(t - 1) & 1][R * rg];
-      f64x2 d[R / 2];
-#pragma unroll
-      for (int b = 0; b < R / 2; ++b) d[b] = *reinterpret_cast<const f64x2*>(src + 2 * b);
+    for (int b = 0; b < R / 2; ++b) {
+      const f64x2 d = *reinterpret_cast<const f64x2*>(src + 2 * b);
 #pragma unroll
       for (int kc = 0; kc < C; ++kc) {
-        double m = d[0].x + a_reg[kc];  // s_i = d[i] + a[i,j]  (viterbi.rs:15)
-        m = __builtin_fmax(m, d[0].y + a_reg[C + kc]);
-#pragma unroll
-        for (int b = 1; b < R / 2; ++b) {
-          m = __builtin_fmax(m, d[b].x + a_reg[(2 * b) * C + kc]);
-          m = __builtin_fmax(m, d[b].y + a_reg[(2 * b + 1) * C + kc]);
-        }
-        part[C * cq + kc][rg] = m;
+        const double x = d.x + a_reg[2 * b * C + kc];  // s_i = d[i] + a[i,j]  (viterbi.rs:15)
+        m[kc] = b == 0 ? x : __builtin_fmax(m[kc], x);
+        m[kc] = __builtin_fmax(m[kc], d.y + a_reg[(2 * b + 1) * C + kc]);
       }
-      __builtin_amdgcn_wave_barrier();  // the partials are other lanes' (LDS: in wave order)
-      double dn = 0.0;
-      if (owner) {
-        const f64x2 p01 = *reinterpret_cast<const f64x2*>(&part[jw][0]);
-        const f64x2 p23 = *reinterpret_cast<const f64x2*>(&part[jw][2]);
-        const double m = __builtin_fmax(__builtin_fmax(p01.x, p01.y), __builtin_fmax(p23.x, p23.y));
-        dn = m + pe[k];  // (d + a) + b -- viterbi.rs:15-17
-        dl[t & 1][jw] = dn;
-      }
-      __builtin_amdgcn_wave_barrier();  // delta_t before the next step's reads
-      put(t, dn);
-      pe[k] = g.et[(size_t)so[k] * NPW + jw];  // step t+PD
-      so[k] = obs_s(min(t + 2 * PD, Tm1));     // observation of step t+2PD
     }
+#pragma unroll
+    for (int kc = 0; kc < C; ++kc) part[C * cq + kc][rg] = m[kc];
+    __builtin_amdgcn_wave_barrier();  // the partials are other lanes' (LDS: in wave order)
+    const f64x2 p01 = *reinterpret_cast<const f64x2*>(&part[lane][0]);
+    const f64x2 p23 = *reinterpret_cast<const f64x2*>(&part[lane][2]);
+    const double mx = __builtin_fmax(__builtin_fmax(p01.x, p01.y), __builtin_fmax(p23.x, p23.y));
+    const double dn = mx + pe[k];  // (d + a) + b -- viterbi.rs:15-17
+    dl[t & 1][lane] = dn;
+    __builtin_amdgcn_wave_barrier();  // delta_t before the next step's reads
+    put(t, dn);
+    pe[k] = *eaddr(so[k]);                        // step t+PD
+    so[k] = (unsigned)obs[min(t + 2 * PD, Tm1)];  // observation of step t+2PD
+  };
+  // whole blocks of PD steps with no exit inside, so the loop's back edge carries one count of
+  // outstanding loads and the wait for a step's emission covers only loads issued PD steps ago
+  int t0 = 1;
+  for (; t0 + PD <= T; t0 += PD) {
+#pragma unroll
+    for (int k = 0; k < PD; ++k) step(t0 + k, k);
   }
-  if (bad && lane == 0) g.status[seq] = CVK_SEQ_BADOBS;
+#pragma unroll
+  for (int k = 0; k < PD - 1; ++k)
+    if (t0 + k < T) step(t0 + k, k);
+  if (bad) g.status[seq] = CVK_SEQ_BADOBS;
 }
 
 hipError_t launch_t64_wave(const T64FwdArgs& fa, int64_t nseq, hipStream_t stream) {

@@ -51,6 +51,16 @@ run() {
         python3 tools/trace_timeline.py $O/kt trellis_fwd_f64 > $O/chain_timeline.txt ;;
     chaintests) step chaintests 600 python3 -u -m pytest -q -x --timeout 200 --timeout-method thread -m gpu \
       tests/test_gpu_chain_par.py tests/test_gpu_f64.py -k "chain or cp_seqs or wave48" ;;
+    w48t) step w48t 400 python3 -u -m pytest -q -x --timeout 200 --timeout-method thread -m gpu \
+      tests/test_gpu_f64.py tests/test_gpu_configs_oracle.py -k "wave48 or c2 or golden or wave" ;;
+    c2pmc)  # where trellis_wave48_f64's waves spend their cycles
+      (cd /tmp && REPS=3 step c2pmc1 120 rocprofv3 --kernel-include-regex wave48 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES \
+        SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_VALU -d $O/pmc1 -o pmc1 --output-format csv \
+        -- python3 $R/tools/bench_configs.py c2f64) &&
+      (cd /tmp && REPS=3 step c2pmc2 120 rocprofv3 --kernel-include-regex wave48 --pmc SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_ANY \
+        SQ_INST_CYCLES_VMEM SQ_WAIT_INST_LDS SQ_INSTS_LDS SQ_INSTS_VMEM GRBM_GUI_ACTIVE -d $O/pmc2 -o pmc2 --output-format csv \
+        -- python3 $R/tools/bench_configs.py c2f64) ;;
+    spec) step spec 300 python3 -u tools/bench_spec.py 573 64 ;;
     smoke) step smoke 200 python3 -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" ;;
     bench) step bench 400 python3 -u bench.py ;;
     prof)
