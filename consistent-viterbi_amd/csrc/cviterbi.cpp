@@ -308,7 +308,15 @@ struct cv_hmm {
   // config-4-sized call allocated and freed ~0.4 GB of them each time (hipFree synchronises)
   struct ChainBufs {
     DevBuf off, obs, path, res, cert, ebin, q, ends, gid, gpath;
+    // serial runs and speculative batches (kept, so no hipFree -- a device-wide sync -- lands
+    // while the second part's forward pass runs)
+    DevBuf first, rpsi, rows, small, rpath, soff, sobs, spath, sres, sinit, slast;
   } chainb;
+  // the chain's own stream (high priority: its walk-side kernels -- end states, quantised folds,
+  // gathers, runs, speculative batches -- run beside the second part's forward pass) and the
+  // events closing each part's decode
+  hipStream_t chain_stream = nullptr;
+  std::vector<hipEvent_t> part_ev;
   // the parallel chain's path copy: per decode chunk, behind that chunk's backtrack (chunk_ev),
   // on a non-blocking stream of its own, from a host thread of its own
   std::vector<hipEvent_t> chunk_ev;
@@ -329,7 +337,9 @@ struct cv_hmm {
     if (stream) (void)hipStreamDestroy(stream);
     if (bt_stream) (void)hipStreamDestroy(bt_stream);
     for (auto e : chunk_ev) (void)hipEventDestroy(e);
+    for (auto e : part_ev) (void)hipEventDestroy(e);
     if (copy_stream) (void)hipStreamDestroy(copy_stream);
+    if (chain_stream) (void)hipStreamDestroy(chain_stream);
   }
 };
 
@@ -1339,7 +1349,7 @@ CV_API cv_status cv_hmm_release_workspaces(cv_hmm* h) {
   cv_status st = set_device(h);
   if (st != CV_OK) return st;
   // every stream the workspaces were used on has drained before the memory goes
-  for (hipStream_t s : {h->stream, h->bt_stream, h->side.stream, h->side.hi, h->copy_stream})
+  for (hipStream_t s : {h->stream, h->bt_stream, h->side.stream, h->side.hi, h->copy_stream, h->chain_stream})
     if (s) HIP_TRY(hipStreamSynchronize(s));
   for (DevBuf* b : {&h->ws_main, &h->ws_last, &h->ws_order, &h->side.main, &h->side.last, &h->side.order,
                     &h->side.idx, &h->side.obs2, &h->side.path2, &h->side.res2, &h->st_off, &h->st_obs, &h->st_path,
@@ -1348,7 +1358,9 @@ CV_API cv_status cv_hmm_release_workspaces(cv_hmm* h) {
                     &h->cs_seg, &h->rs_rows, &h->rs_rowbase, &h->rs_resume, &h->rs_start, &h->rs_off2, &h->rs_ridx,
                     &h->rs_slot, &h->rs_obs2, &h->rs_frc2, &h->rs_path2, &h->rs_srows, &h->rs_srowbase, &h->rs_cert,
                     &h->chainb.off, &h->chainb.obs, &h->chainb.path, &h->chainb.res, &h->chainb.cert, &h->chainb.ebin,
-                    &h->chainb.q, &h->chainb.ends, &h->chainb.gid, &h->chainb.gpath})
+                    &h->chainb.q, &h->chainb.ends, &h->chainb.gid, &h->chainb.gpath, &h->chainb.first,
+                    &h->chainb.rpsi, &h->chainb.rows, &h->chainb.small, &h->chainb.rpath, &h->chainb.soff,
+                    &h->chainb.sobs, &h->chainb.spath, &h->chainb.sres, &h->chainb.sinit, &h->chainb.slast})
     b->release();
   h->ws_rec = false;
   h->side.ws_rec = false;
@@ -3063,9 +3075,6 @@ cv_status superseq_cp_wg(cv_hmm* h, int64_t L, const int32_t* obs, const std::ve
 // Knobs (bit-identical): CV_CHAIN_PAR=0 (serial chain), CV_CHAIN_PAR_FORCE=m (every m-th
 // non-empty sequence taken as uncertified: exercises speculation and the runs), CV_CHAIN_SPEC=0
 // (no speculation: every uncertified sequence through the serial chain kernel).
-// the parallel chain's decode in two chunks (their path copies beside the next chunk's forward
-// and the walk) from this many elements on
-constexpr int64_t kChainCopyChunkMin = 1 << 22;
 
 cv_status superseq_cp_par(cv_hmm* h, int64_t nseq, const int64_t* offsets, const int32_t* obs, int32_t* path_out,
                           double* objective_out, bool* applied) {
@@ -3088,7 +3097,11 @@ cv_status superseq_cp_par(cv_hmm* h, int64_t nseq, const int64_t* offsets, const
   int64_t maxT = 0;
   for (int64_t k = 0; k <= nseq; ++k) off[(size_t)k] = offsets[k] - base;
   for (int64_t k = 0; k < nseq; ++k) maxT = std::max(maxT, off[(size_t)k + 1] - off[(size_t)k]);
-  // 1. the per-sequence row-A0 decode with certificates
+  // 1. the per-sequence row-A0 decode with certificates -- in two parts where N <= 256 and the
+  // batch spans several forward rounds: the walk over the first part (its end states,
+  // quantised folds, gathered paths, runs and speculative batches, all on the chain stream)
+  // runs while the second part's forward pass holds the chip, so only the second part's share
+  // of that work follows the last forward (tuning key chain_parts = 0: one part)
   DevBuf &d_off = h->chainb.off, &d_obs = h->chainb.obs, &d_path = h->chainb.path, &d_res = h->chainb.res,
          &d_cert = h->chainb.cert;
   if ((st = d_off.ensure((size_t)(nseq + 1) * 8)) != CV_OK) return st;
@@ -3096,12 +3109,6 @@ cv_status superseq_cp_par(cv_hmm* h, int64_t nseq, const int64_t* offsets, const
   if ((st = d_path.ensure((size_t)L * 4)) != CV_OK) return st;
   if ((st = d_res.ensure((size_t)nseq * 9)) != CV_OK) return st;
   if ((st = d_cert.ensure((size_t)nseq * 16)) != CV_OK) return st;
-  HIP_TRY(hipMemcpyAsync(d_off.p, off.data(), off.size() * 8, hipMemcpyHostToDevice, stream));
-  HIP_TRY(hipMemcpyAsync(d_obs.p, obs + base, (size_t)L * 4, hipMemcpyHostToDevice, stream));
-  if (trace_on()) {  // phase split (CV_TRACE only: the syncs cost overlap)
-    HIP_TRY(hipStreamSynchronize(stream));
-    trace_mark("chain: obs H2D");
-  }
   double* d_score = d_res.as<double>();
   uint8_t* d_status = reinterpret_cast<uint8_t*>(d_score + nseq);
   // the certified backtrack's rho_cap (T64BtArgs): above every U = 2^-52 (|M| + |S_k| + 16) the
@@ -3124,31 +3131,65 @@ cv_status superseq_cp_par(cv_hmm* h, int64_t nseq, const int64_t* offsets, const
   o.rescore_f64 = 0;
   o.stream = stream;
   // The paths reach the caller's (pageable) buffer from a host thread of their own, one copy
-  // per decode chunk behind that chunk's backtrack (a pageable D2H blocks its calling thread):
-  // the first chunk's copy runs beside the next chunk's forward, the last one beside the walk
-  // below, which needs only the end states and the paths of the few sequences it may fold
-  // element by element (fetched packed).  Two chunks at config-4 size (tuning key
-  // chain_copy_overlap = 0: one chunk, the copy before the walk).
+  // per decode chunk behind that chunk's backtrack (a pageable D2H blocks its calling thread),
+  // beside the later forward passes and the walk, which needs only the end states and the
+  // paths of the few sequences it may fold element by element (fetched packed).  Tuning key
+  // chain_copy_overlap = 0: one part, the copy before the walk.
   const bool overlap_copy = h->tuning.chain_copy_overlap != 0;
-  if (overlap_copy && small) {
-    const uint64_t rows = (uint64_t)L * (uint64_t)h->np64 * 8;
-    if (L >= 2 * (int64_t)kChainCopyChunkMin) o.workspace_bytes = (rows + 1) / 2 + ((uint64_t)h->np64 * 8 << 10);
+  // the parts: one forward round each (64 sequences per CU at eight per wave), the last one
+  // taking the remainder; part p's walk runs beside part p + 1's forward pass, part p + 1's
+  // observations cross during part p's
+  std::vector<int64_t> pb{0};
+  if (small && overlap_copy && h->tuning.chain_parts != 0) {
+    const int64_t unit = 64 * (int64_t)std::max(h->cus, 1);
+    for (int64_t s = unit; s + unit <= nseq; s += unit) pb.push_back(s);
   }
+  pb.push_back(nseq);
+  const int nparts = (int)pb.size() - 1;
+  if (!h->chain_stream) {
+    int least = 0, greatest = 0;
+    HIP_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
+    HIP_TRY(hipStreamCreateWithPriority(&h->chain_stream, hipStreamNonBlocking, greatest));
+  }
+  hipStream_t cs = h->chain_stream;
+  // events: [0, nparts) each part's decode done, [nparts, 2 nparts) each part's observations in
+  std::vector<hipEvent_t> part_done((size_t)nparts), obs_in((size_t)nparts);
+  for (int p = 0; p < nparts; ++p) {
+    part_done[(size_t)p] = get_event(h->part_ev, (size_t)p);
+    obs_in[(size_t)p] = get_event(h->part_ev, (size_t)(nparts + p));
+    if (!part_done[(size_t)p] || !obs_in[(size_t)p]) return set_err(CV_EDEVICE, "hipEventCreate failed");
+  }
+  if (!h->copy_stream) HIP_TRY(hipStreamCreateWithFlags(&h->copy_stream, hipStreamNonBlocking));
+  HIP_TRY(hipMemcpyAsync(d_off.p, off.data(), off.size() * 8, hipMemcpyHostToDevice, stream));
   std::vector<std::pair<int64_t, int64_t>> dchunks;
-  st = decode_device(h, nseq, off.data(), d_off.as<int64_t>(), d_obs.as<int32_t>(), o, d_path.as<int32_t>(), d_score,
-                     d_status, stream, nullptr, false, d_cert.as<double>(), nullptr, nullptr, &dchunks);
-  if (st == CV_EUNSUPPORTED && !small) {  // no rows to certify (generic_rows = 0): the serial chain
-    g_err.clear();                         // runs, and the public call succeeds
-    return CV_OK;
+  for (int p = 0; p < nparts; ++p) {
+    const int64_t s0 = pb[p], s1 = pb[p + 1], e0 = off[(size_t)s0], e1 = off[(size_t)s1];
+    // the second part's observations cross on the copy stream while the first part's forward runs
+    hipStream_t hs = p == 0 ? stream : h->copy_stream;
+    HIP_TRY(hipMemcpyAsync(d_obs.as<int32_t>() + e0, obs + base + e0, (size_t)(e1 - e0) * 4, hipMemcpyHostToDevice, hs));
+    if (p > 0) {
+      HIP_TRY(hipEventRecord(obs_in[(size_t)p], hs));
+      HIP_TRY(hipStreamWaitEvent(stream, obs_in[(size_t)p], 0));
+    }
+    if (trace_on() && p == 0) {  // phase split (CV_TRACE only: the syncs cost overlap)
+      HIP_TRY(hipStreamSynchronize(stream));
+      trace_mark("chain: obs H2D (first part)");
+    }
+    const size_t c0 = dchunks.size();
+    st = decode_device(h, s1 - s0, off.data() + s0, d_off.as<int64_t>() + s0, d_obs.as<int32_t>(), o,
+                       d_path.as<int32_t>(), d_score + s0, d_status + s0, stream, nullptr, false,
+                       d_cert.as<double>() + 2 * s0, nullptr, nullptr, &dchunks);
+    if (st == CV_EUNSUPPORTED && !small) {  // no rows to certify (generic_rows = 0): the serial chain
+      g_err.clear();                         // runs, and the public call succeeds
+      return CV_OK;
+    }
+    if (st != CV_OK) return st;
+    for (size_t i = c0; i < dchunks.size(); ++i) dchunks[i] = {dchunks[i].first + s0, dchunks[i].second + s0};
+    HIP_TRY(hipEventRecord(part_done[(size_t)p], stream));
   }
-  if (st != CV_OK) return st;
   std::vector<double> score((size_t)nseq), cert((size_t)nseq * 2);
   std::vector<uint8_t> status((size_t)nseq);
   std::vector<int32_t> ends((size_t)nseq);
-  if (trace_on()) {
-    HIP_TRY(hipStreamSynchronize(stream));
-    trace_mark("chain: row-A0 decode + certificates (device)");
-  }
   // the copy thread; any return below joins it first (it writes into the caller's buffer)
   struct CopyThread {
     std::thread t;
@@ -3158,23 +3199,22 @@ cv_status superseq_cp_par(cv_hmm* h, int64_t nseq, const int64_t* offsets, const
       if (t.joinable()) t.join();
     }
   } copy;
-  if (!h->copy_stream) HIP_TRY(hipStreamCreateWithFlags(&h->copy_stream, hipStreamNonBlocking));
   {
     const int dev = h->device;
-    hipStream_t cs = h->copy_stream;
+    hipStream_t cps = h->copy_stream;
     std::vector<hipEvent_t> evs(h->chunk_ev.begin(), h->chunk_ev.begin() + (ptrdiff_t)dchunks.size());
     int32_t* dp = d_path.as<int32_t>();
-    auto run_copies = [&copy, dev, cs, evs, dchunks, off, path_out, dp]() {
+    auto run_copies = [&copy, dev, cps, evs, dchunks, off, path_out, dp]() {
       if ((copy.err = hipSetDevice(dev)) != hipSuccess) return;
       for (size_t i = 0; i < dchunks.size(); ++i) {
         const int64_t e0 = off[(size_t)dchunks[i].first], e1 = off[(size_t)dchunks[i].second];
-        if ((copy.err = hipStreamWaitEvent(cs, evs[i], 0)) != hipSuccess) return;
+        if ((copy.err = hipStreamWaitEvent(cps, evs[i], 0)) != hipSuccess) return;
         if (e1 > e0 &&
-            (copy.err = hipMemcpyAsync(path_out + e0, dp + e0, (size_t)(e1 - e0) * 4, hipMemcpyDeviceToHost, cs)) !=
+            (copy.err = hipMemcpyAsync(path_out + e0, dp + e0, (size_t)(e1 - e0) * 4, hipMemcpyDeviceToHost, cps)) !=
                 hipSuccess)
           return;
       }
-      copy.err = hipStreamSynchronize(cs);
+      copy.err = hipStreamSynchronize(cps);
     };
     if (overlap_copy)
       copy.t = std::thread(run_copies);
@@ -3183,84 +3223,42 @@ cv_status superseq_cp_par(cv_hmm* h, int64_t nseq, const int64_t* offsets, const
   }
   if (!overlap_copy && copy.err != hipSuccess)
     return set_err(CV_EDEVICE, "chain path copy failed: %s", hipGetErrorString(copy.err));
-  // end states, scores, statuses and certificates through one pinned buffer (d_res holds
-  // scores then statuses contiguously)
-  DevBuf& d_ends = h->chainb.ends;
+  // every buffer the walk may need, sized now: growing one later would free the old one, a
+  // device-wide synchronisation that would wait for the second part's forward pass
+  constexpr int64_t kSpecMax = 16384;  // sequences per speculative batch
+  DevBuf &d_ends = h->chainb.ends, &d_ebin = h->chainb.ebin, &d_q = h->chainb.q, &d_gid = h->chainb.gid,
+         &d_gpath = h->chainb.gpath;
   if ((st = d_ends.ensure((size_t)nseq * 4)) != CV_OK) return st;
-  {
-    const hipError_t e = cvk::launch_cp_seq_ends(d_path.as<int32_t>(), d_off.as<int64_t>(), nseq, d_ends.as<int32_t>(), stream);
-    if (e != hipSuccess) return set_err(CV_EDEVICE, "chain end states failed: %s", hipGetErrorString(e));
-  }
-  if (h->chain_pin.ensure((size_t)nseq * 29)) {
-    unsigned char* pin = h->chain_pin.as<unsigned char>();
-    HIP_TRY(hipMemcpyAsync(pin, d_res.p, (size_t)nseq * 9, hipMemcpyDeviceToHost, stream));
-    HIP_TRY(hipMemcpyAsync(pin + (size_t)nseq * 9, d_cert.p, (size_t)nseq * 16, hipMemcpyDeviceToHost, stream));
-    HIP_TRY(hipMemcpyAsync(pin + (size_t)nseq * 25, d_ends.p, (size_t)nseq * 4, hipMemcpyDeviceToHost, stream));
-    HIP_TRY(hipStreamSynchronize(stream));
-    std::memcpy(score.data(), pin, (size_t)nseq * 8);
-    std::memcpy(status.data(), pin + (size_t)nseq * 8, (size_t)nseq);
-    std::memcpy(cert.data(), pin + (size_t)nseq * 9, (size_t)nseq * 16);
-    std::memcpy(ends.data(), pin + (size_t)nseq * 25, (size_t)nseq * 4);
-  } else {
-    HIP_TRY(hipMemcpyAsync(score.data(), d_score, (size_t)nseq * 8, hipMemcpyDeviceToHost, stream));
-    HIP_TRY(hipMemcpyAsync(status.data(), d_status, (size_t)nseq, hipMemcpyDeviceToHost, stream));
-    HIP_TRY(hipMemcpyAsync(cert.data(), d_cert.p, (size_t)nseq * 16, hipMemcpyDeviceToHost, stream));
-    HIP_TRY(hipMemcpyAsync(ends.data(), d_ends.p, (size_t)nseq * 4, hipMemcpyDeviceToHost, stream));
-    HIP_TRY(hipStreamSynchronize(stream));
-  }
-  trace_mark("chain: paths, scores, certificates D2H");
-  for (int64_t k = 0; k < nseq; ++k)
-    if (status[(size_t)k] != CV_SEQ_OK && status[(size_t)k] != CV_SEQ_EMPTY) return CV_OK;  // serial chain
-  // 2a. predicted binades and the quantised folds of every path
-  std::vector<int32_t> ebin((size_t)nseq, cvk::CVK_NO_BINADE);
-  {
-    double mp = 0.0;
-    for (int64_t k = 0; k < nseq; ++k) {
-      if (off[(size_t)k + 1] == off[(size_t)k]) continue;
-      const double em = std::fabs(mp), sk = std::fabs(score[(size_t)k]);
-      if (em >= 0x1p12) {
-        const int e = std::ilogb(em);
-        // the prediction is off by far less than 2^-20 relative: both ends of the sequence's
-        // value range stay in the binade with that margin
-        if (std::ilogb(em * (1.0 - 0x1p-20)) == e && std::ilogb((em + sk + 16.0) * (1.0 + 0x1p-20)) == e)
-          ebin[(size_t)k] = e;
-      }
-      mp -= sk;
-    }
-  }
-  DevBuf &d_ebin = h->chainb.ebin, &d_q = h->chainb.q;
   if ((st = d_ebin.ensure((size_t)nseq * 4)) != CV_OK) return st;
   if ((st = d_q.ensure((size_t)nseq * 9)) != CV_OK) return st;
-  HIP_TRY(hipMemcpyAsync(d_ebin.p, ebin.data(), (size_t)nseq * 4, hipMemcpyHostToDevice, stream));
-  {
-    cvk::CpQuant64Args qa{};
-    qa.a = small ? h->q_a.as<double>() : h->d_a64.as<double>();
-    qa.pi = small ? h->q_pi.as<double>() : h->d_pi64.as<double>();
-    qa.et = small ? h->q_et.as<double>() : h->d_et64.as<double>();
-    qa.np = W;
-    qa.offsets = d_off.as<int64_t>();
-    qa.obs = d_obs.as<int32_t>();
-    qa.path = d_path.as<int32_t>();
-    qa.ebin = d_ebin.as<int32_t>();
-    qa.nseq = nseq;
-    qa.q = d_q.as<long long>();
-    qa.tie = reinterpret_cast<uint8_t*>(d_q.as<long long>() + nseq);
-    const hipError_t err = cvk::launch_cp_quant(qa, stream);
-    if (err != hipSuccess) return set_err(CV_EDEVICE, "chain quantised folds failed: %s", hipGetErrorString(err));
+  if ((st = d_gid.ensure((size_t)nseq * 16)) != CV_OK) return st;
+  DevBuf &d_first = h->chainb.first, &d_rpsi = h->chainb.rpsi, &d_rows = h->chainb.rows, &d_small = h->chainb.small,
+         &d_rpath = h->chainb.rpath;
+  DevBuf &d_soff = h->chainb.soff, &d_sobs = h->chainb.sobs, &d_spath = h->chainb.spath, &d_sres = h->chainb.sres,
+         &d_sinit = h->chainb.sinit, &d_slast = h->chainb.slast;
+  if (nparts > 1) {
+    const int64_t nspec = std::min<int64_t>(nseq, kSpecMax), lspec = std::min<int64_t>(L, nspec * maxT);
+    if ((st = d_gpath.ensure((size_t)L * 4)) != CV_OK) return st;
+    if ((st = d_soff.ensure((size_t)(nspec + 1) * 8)) != CV_OK) return st;
+    if ((st = d_sobs.ensure((size_t)lspec * 4)) != CV_OK) return st;
+    if ((st = d_spath.ensure((size_t)lspec * 4)) != CV_OK) return st;
+    if ((st = d_sres.ensure((size_t)nspec * 9)) != CV_OK) return st;
+    if ((st = d_sinit.ensure((size_t)nspec * 8)) != CV_OK) return st;
+    if ((st = d_slast.ensure((size_t)nspec * N * 8)) != CV_OK) return st;
+    if ((st = d_rpsi.ensure((size_t)std::max<int64_t>(4 * maxT, 1) * W * 2)) != CV_OK) return st;
+    if ((st = d_rpath.ensure((size_t)std::max<int64_t>(4 * maxT, 1) * 4)) != CV_OK) return st;
   }
-  std::vector<long long> qv((size_t)nseq);
-  std::vector<uint8_t> tie((size_t)nseq);
-  HIP_TRY(hipMemcpyAsync(qv.data(), d_q.p, (size_t)nseq * 8, hipMemcpyDeviceToHost, stream));
-  HIP_TRY(hipMemcpyAsync(tie.data(), d_q.as<long long>() + nseq, (size_t)nseq, hipMemcpyDeviceToHost, stream));
-  HIP_TRY(hipStreamSynchronize(stream));
-  trace_mark("chain: quantised folds");
-  // 2b/3. the walk
+  if (!h->chain_pin.ensure((size_t)nseq * 29)) return set_err(CV_ENOMEM, "pinned chain staging failed");
+  unsigned char* pin = h->chain_pin.as<unsigned char>();
   double pimax = 0.0;
   for (double x : h->pi)
     if (std::isfinite(x)) pimax = std::max(pimax, std::fabs(x));
   const int force_m = std::max(0, h->tuning.chain_par_force);
   const bool spec_env = h->tuning.chain_spec != 0;  // 0: every uncertified sequence re-run serially
   const int32_t* ob = obs + base;
+  std::vector<int32_t> ebin((size_t)nseq, cvk::CVK_NO_BINADE);
+  std::vector<long long> qv((size_t)nseq);
+  std::vector<uint8_t> tie((size_t)nseq);
   // The row-A0 paths the walk folds element by element: the sequences whose certificate may
   // fail at the running maximum the walk will see (predicted from the optima, with a 2x margin
   // on every bound), those without a quantised fold, and each one's successor, fetched packed
@@ -3270,49 +3268,128 @@ cv_status superseq_cp_par(cv_hmm* h, int64_t nseq, const int64_t* offsets, const
   std::vector<int64_t> gpos((size_t)nseq, -1);
   bool copy_joined = !overlap_copy;
   int64_t path_waits = 0, gathered = 0, memo_hits = 0;
-  {
-    double smax = 0.0;
-    for (double x : score) smax = std::max(smax, std::fabs(x));
+  std::vector<int64_t> ks;  // the non-empty sequences, in order (the walk's positions)
+  // the prediction walk's certify() results, reused by the exact walk wherever it arrives at a
+  // sequence after a certified one with the same running maximum, bit for bit (certify is a
+  // function of the sequence, the maximum and the predecessor's kind): memo_in[x] = that
+  // maximum, memo_out[x] = the fold (NaN: not certified), memo_q[x] = quantised (2 = no memo)
+  std::vector<double> memo_in, memo_out;
+  std::vector<uint8_t> memo_q;
+  double mp_bin = 0.0, mp_cand = 0.0, smax = 0.0;  // running sums of |score| (binades, candidates)
+  bool prev_cand = false, fallback = false;
+  int64_t xc = 0;
+  // 2. one part's end states, scores, statuses and certificates (through the pinned buffer),
+  // predicted binades, quantised folds and gathered candidate paths, on the chain stream behind
+  // the part's decode
+  auto prep = [&](int p) -> cv_status {
+    const int64_t s0 = pb[p], s1 = pb[p + 1], n = s1 - s0;
+    HIP_TRY(hipStreamWaitEvent(cs, part_done[(size_t)p], 0));
+    {
+      const hipError_t e = cvk::launch_cp_seq_ends(d_path.as<int32_t>(), d_off.as<int64_t>() + s0, n,
+                                                   d_ends.as<int32_t>() + s0, cs);
+      if (e != hipSuccess) return set_err(CV_EDEVICE, "chain end states failed: %s", hipGetErrorString(e));
+    }
+    HIP_TRY(hipMemcpyAsync(pin + s0 * 8, d_score + s0, (size_t)n * 8, hipMemcpyDeviceToHost, cs));
+    HIP_TRY(hipMemcpyAsync(pin + nseq * 8 + s0, d_status + s0, (size_t)n, hipMemcpyDeviceToHost, cs));
+    HIP_TRY(hipMemcpyAsync(pin + nseq * 9 + s0 * 16, d_cert.as<double>() + 2 * s0, (size_t)n * 16,
+                           hipMemcpyDeviceToHost, cs));
+    HIP_TRY(hipMemcpyAsync(pin + nseq * 25 + s0 * 4, d_ends.as<int32_t>() + s0, (size_t)n * 4, hipMemcpyDeviceToHost,
+                           cs));
+    HIP_TRY(hipStreamSynchronize(cs));
+    std::memcpy(score.data() + s0, pin + s0 * 8, (size_t)n * 8);
+    std::memcpy(status.data() + s0, pin + nseq * 8 + s0, (size_t)n);
+    std::memcpy(cert.data() + 2 * s0, pin + nseq * 9 + s0 * 16, (size_t)n * 16);
+    std::memcpy(ends.data() + s0, pin + nseq * 25 + s0 * 4, (size_t)n * 4);
+    trace_mark("chain: part's scores, certificates, end states D2H");
+    for (int64_t k = s0; k < s1; ++k)
+      if (status[(size_t)k] != CV_SEQ_OK && status[(size_t)k] != CV_SEQ_EMPTY) {
+        fallback = true;  // the serial chain
+        return CV_OK;
+      }
+    // predicted binades and the quantised folds of every path
+    for (int64_t k = s0; k < s1; ++k) {
+      if (off[(size_t)k + 1] == off[(size_t)k]) continue;
+      const double em = std::fabs(mp_bin), sk = std::fabs(score[(size_t)k]);
+      if (em >= 0x1p12) {
+        const int e = std::ilogb(em);
+        // the prediction is off by far less than 2^-20 relative: both ends of the sequence's
+        // value range stay in the binade with that margin
+        if (std::ilogb(em * (1.0 - 0x1p-20)) == e && std::ilogb((em + sk + 16.0) * (1.0 + 0x1p-20)) == e)
+          ebin[(size_t)k] = e;
+      }
+      mp_bin -= sk;
+    }
+    HIP_TRY(hipMemcpyAsync(d_ebin.as<int32_t>() + s0, ebin.data() + s0, (size_t)n * 4, hipMemcpyHostToDevice, cs));
+    {
+      cvk::CpQuant64Args qa{};
+      qa.a = small ? h->q_a.as<double>() : h->d_a64.as<double>();
+      qa.pi = small ? h->q_pi.as<double>() : h->d_pi64.as<double>();
+      qa.et = small ? h->q_et.as<double>() : h->d_et64.as<double>();
+      qa.np = W;
+      qa.offsets = d_off.as<int64_t>() + s0;
+      qa.obs = d_obs.as<int32_t>();
+      qa.path = d_path.as<int32_t>();
+      qa.ebin = d_ebin.as<int32_t>() + s0;
+      qa.nseq = n;
+      qa.q = d_q.as<long long>() + s0;
+      qa.tie = reinterpret_cast<uint8_t*>(d_q.as<long long>() + nseq) + s0;
+      const hipError_t err = cvk::launch_cp_quant(qa, cs);
+      if (err != hipSuccess) return set_err(CV_EDEVICE, "chain quantised folds failed: %s", hipGetErrorString(err));
+    }
+    HIP_TRY(hipMemcpyAsync(qv.data() + s0, d_q.as<long long>() + s0, (size_t)n * 8, hipMemcpyDeviceToHost, cs));
+    HIP_TRY(hipMemcpyAsync(tie.data() + s0, reinterpret_cast<uint8_t*>(d_q.as<long long>() + nseq) + s0, (size_t)n,
+                           hipMemcpyDeviceToHost, cs));
+    HIP_TRY(hipStreamSynchronize(cs));
+    trace_mark("chain: quantised folds");
+    const size_t x0 = ks.size();
+    for (int64_t k = s0; k < s1; ++k) {
+      if (off[(size_t)k + 1] > off[(size_t)k]) ks.push_back(k);
+      smax = std::max(smax, std::fabs(score[(size_t)k]));
+    }
+    memo_in.resize(ks.size());
+    memo_out.resize(ks.size());
+    memo_q.resize(ks.size(), 2);
+    // candidates (the successor of the part's last candidate is the next part's first sequence:
+    // prev_cand carries over)
     std::vector<int64_t> gids, gdst;
-    double mp = 0.0;
-    bool prev_cand = false;
-    int64_t x = 0, tot = 0;
-    for (int64_t k = 0; k < nseq; ++k) {
+    const int64_t gbase = (int64_t)gpath.size();
+    int64_t tot = 0;
+    for (size_t xi = x0; xi < ks.size(); ++xi) {
+      const int64_t k = ks[xi];
       const int64_t T = off[(size_t)k + 1] - off[(size_t)k];
-      if (T == 0) continue;
       const double S = std::fabs(score[(size_t)k]);
-      const double Up = 0x1p-52 * (mp * (1.0 + 0x1p-8) + S + 16.0);
-      const double Up1 = 0x1p-52 * ((mp + S) * (1.0 + 0x1p-8) + smax + pimax + 16.0);
+      const double Up = 0x1p-52 * (mp_cand * (1.0 + 0x1p-8) + S + 16.0);
+      const double Up1 = 0x1p-52 * ((mp_cand + S) * (1.0 + 0x1p-8) + smax + pimax + 16.0);
       const double rho = cert[(size_t)k * 2], gF = cert[(size_t)k * 2 + 1];
       const bool cand = !(rho > 2.0 * Up) || !(gF - 6.0 * (double)T * Up > 4.0 * Up1) || tie[(size_t)k] ||
                         ebin[(size_t)k] == cvk::CVK_NO_BINADE ||
-                        (force_m > 0 && (int64_t)(x % (int64_t)force_m) == force_m - 1);
+                        (force_m > 0 && (int64_t)(xc % (int64_t)force_m) == force_m - 1);
       if (cand || prev_cand) {
         gids.push_back(k);
         gdst.push_back(tot);
-        gpos[(size_t)k] = tot;
+        gpos[(size_t)k] = gbase + tot;
         tot += T;
       }
       prev_cand = cand;
-      mp += S;
-      ++x;
+      mp_cand += S;
+      ++xc;
     }
-    gathered = (int64_t)gids.size();
+    gathered += (int64_t)gids.size();
     if (!copy_joined && !gids.empty()) {
-      DevBuf &d_gid = h->chainb.gid, &d_gpath = h->chainb.gpath;
-      if ((st = d_gid.ensure(gids.size() * 16)) != CV_OK || (st = d_gpath.ensure((size_t)tot * 4)) != CV_OK) return st;
+      const int64_t ng = (int64_t)gids.size();
+      if ((st = d_gid.ensure((size_t)ng * 16)) != CV_OK || (st = d_gpath.ensure((size_t)tot * 4)) != CV_OK) return st;
       gids.insert(gids.end(), gdst.begin(), gdst.end());
-      HIP_TRY(hipMemcpyAsync(d_gid.p, gids.data(), gids.size() * 8, hipMemcpyHostToDevice, stream));
+      HIP_TRY(hipMemcpyAsync(d_gid.p, gids.data(), gids.size() * 8, hipMemcpyHostToDevice, cs));
       const hipError_t e = cvk::launch_cp_gather_paths(d_path.as<int32_t>(), d_off.as<int64_t>(), d_gid.as<int64_t>(),
-                                                       d_gid.as<int64_t>() + gathered, gathered, d_gpath.as<int32_t>(),
-                                                       stream);
+                                                       d_gid.as<int64_t>() + ng, ng, d_gpath.as<int32_t>(), cs);
       if (e != hipSuccess) return set_err(CV_EDEVICE, "chain path gather failed: %s", hipGetErrorString(e));
-      gpath.resize((size_t)tot);
-      HIP_TRY(hipMemcpyAsync(gpath.data(), d_gpath.p, (size_t)tot * 4, hipMemcpyDeviceToHost, stream));
-      HIP_TRY(hipStreamSynchronize(stream));
+      gpath.resize((size_t)(gbase + tot));
+      HIP_TRY(hipMemcpyAsync(gpath.data() + gbase, d_gpath.p, (size_t)tot * 4, hipMemcpyDeviceToHost, cs));
+      HIP_TRY(hipStreamSynchronize(cs));
     }
     trace_mark("chain: candidate paths gathered");
-  }
+    return CV_OK;
+  };
   auto join_copy = [&]() -> cv_status {
     if (copy_joined) return CV_OK;
     copy.join();
@@ -3367,9 +3444,6 @@ cv_status superseq_cp_par(cv_hmm* h, int64_t nseq, const int64_t* offsets, const
     }
     return fold_elems(k, M);
   };
-  std::vector<int64_t> ks;
-  for (int64_t k = 0; k < nseq; ++k)
-    if (off[(size_t)k + 1] > off[(size_t)k]) ks.push_back(k);
   auto score_of = [&](size_t x) { return x < ks.size() ? std::fabs(score[(size_t)ks[x]]) : 0.0; };
 
   // The state of the chain before the sequence at hand: NONE (first sequence), CERT (a certified
@@ -3390,7 +3464,8 @@ cv_status superseq_cp_par(cv_hmm* h, int64_t nseq, const int64_t* offsets, const
     return true;
   };
   // sequence ks[x] certified at running maximum Mc after a predecessor of kind pk (the row test
-  // against row_host when pk == ROW); *Mn = its fold
+  // against row_host when pk == ROW); *Mn = its fold.  ks[x + 1] must be known (the walk of a
+  // part stops before its last sequence until the next part's scores are in).
   auto certify = [&](size_t x, double Mc, Kind pk, double* Mn, bool* quant) {
     const int64_t k = ks[x];
     const int64_t T = off[(size_t)k + 1] - off[(size_t)k];
@@ -3406,10 +3481,9 @@ cv_status superseq_cp_par(cv_hmm* h, int64_t nseq, const int64_t* offsets, const
   };
 
   // ---- runs: the serial chain kernel over consecutive uncertified sequences ----
-  DevBuf d_first, d_rpsi, d_rows, d_small, d_rpath;
   if ((st = d_first.ensure((size_t)std::max<int64_t>(maxT, 1))) != CV_OK) return st;
-  HIP_TRY(hipMemsetAsync(d_first.p, 0, (size_t)std::max<int64_t>(maxT, 1), stream));
-  HIP_TRY(hipMemsetAsync(d_first.p, 1, 1, stream));  // one sequence per launch: its element 0 starts it
+  HIP_TRY(hipMemsetAsync(d_first.p, 0, (size_t)std::max<int64_t>(maxT, 1), cs));
+  HIP_TRY(hipMemsetAsync(d_first.p, 1, 1, cs));  // one sequence per launch: its element 0 starts it
   if ((st = d_rows.ensure((size_t)W * 8 * 3)) != CV_OK) return st;
   // objective, final state (+ the wide chain's two rows, CV_CHAIN_WIDE_MIN)
   if ((st = d_small.ensure(16 + (!small && cvk::cp_chain_wide(N) ? (size_t)N * 16 : 0))) != CV_OK) return st;
@@ -3418,14 +3492,14 @@ cv_status superseq_cp_par(cv_hmm* h, int64_t nseq, const int64_t* offsets, const
   double* row_b = row_a + W;
   bool in_run = false;
   int64_t run_e0 = 0, run_len = 0, runs = 0, run_seqs = 0, ncert = 0, nquant = 0, spec_acc = 0, spec_batches = 0;
-  int64_t psi_cap = 0;
+  int64_t psi_cap = (int64_t)(d_rpsi.bytes / ((size_t)W * 2));
   auto end_run = [&](int32_t end_state) -> cv_status {
     if ((st = d_rpath.ensure((size_t)run_len * 4)) != CV_OK) return st;
-    if ((st = chain_backtrack(W, d_rpsi.as<uint16_t>(), run_len, end_state, d_rpath.as<int32_t>(), stream)) != CV_OK)
+    if ((st = chain_backtrack(W, d_rpsi.as<uint16_t>(), run_len, end_state, d_rpath.as<int32_t>(), cs)) != CV_OK)
       return st;
     std::vector<int32_t> rp((size_t)run_len);
-    HIP_TRY(hipMemcpyAsync(rp.data(), d_rpath.p, (size_t)run_len * 4, hipMemcpyDeviceToHost, stream));
-    HIP_TRY(hipStreamSynchronize(stream));
+    HIP_TRY(hipMemcpyAsync(rp.data(), d_rpath.p, (size_t)run_len * 4, hipMemcpyDeviceToHost, cs));
+    HIP_TRY(hipStreamSynchronize(cs));
     deferred.emplace_back(run_e0, std::move(rp));
     in_run = false;
     return CV_OK;
@@ -3436,11 +3510,11 @@ cv_status superseq_cp_par(cv_hmm* h, int64_t nseq, const int64_t* offsets, const
     if (prev == CERT) {  // what a clean boundary after a certified sequence sees
       std::fill(syn.begin(), syn.end(), -INFINITY);
       syn[(size_t)prev_end] = M;
-      HIP_TRY(hipMemcpyAsync(row_in, syn.data(), (size_t)W * 8, hipMemcpyHostToDevice, stream));
+      HIP_TRY(hipMemcpyAsync(row_in, syn.data(), (size_t)W * 8, hipMemcpyHostToDevice, cs));
       init = row_in;
     } else if (prev == ROW) {
       if (!row_dev) {  // a speculative decode's last row: the exact row, uploaded
-        HIP_TRY(hipMemcpyAsync(row_in, row_host.data(), (size_t)W * 8, hipMemcpyHostToDevice, stream));
+        HIP_TRY(hipMemcpyAsync(row_in, row_host.data(), (size_t)W * 8, hipMemcpyHostToDevice, cs));
         row_dev = row_in;
       }
       init = row_dev;
@@ -3456,13 +3530,13 @@ cv_status superseq_cp_par(cv_hmm* h, int64_t nseq, const int64_t* offsets, const
       DevBuf nb;
       if ((st = nb.ensure((size_t)cap * W * 2)) != CV_OK) return st;
       if (run_len > 0)
-        HIP_TRY(hipMemcpyAsync(nb.p, d_rpsi.p, (size_t)run_len * W * 2, hipMemcpyDeviceToDevice, stream));
-      HIP_TRY(hipStreamSynchronize(stream));
+        HIP_TRY(hipMemcpyAsync(nb.p, d_rpsi.p, (size_t)run_len * W * 2, hipMemcpyDeviceToDevice, cs));
+      HIP_TRY(hipStreamSynchronize(cs));
       std::swap(nb.p, d_rpsi.p);
       std::swap(nb.bytes, d_rpsi.bytes);
       psi_cap = cap;
     }
-    if (!init) HIP_TRY(hipMemsetAsync(d_rpsi.as<uint16_t>() + run_len * W, 0, (size_t)W * 2, stream));
+    if (!init) HIP_TRY(hipMemsetAsync(d_rpsi.as<uint16_t>() + run_len * W, 0, (size_t)W * 2, cs));
     double* out_row = init == row_a ? row_b : row_a;
     hipError_t err;
     if (small) {
@@ -3479,7 +3553,7 @@ cv_status superseq_cp_par(cv_hmm* h, int64_t nseq, const int64_t* offsets, const
       g.final_state = reinterpret_cast<int32_t*>(d_small.as<double>() + 1);
       g.init_row = init;
       g.final_row = out_row;
-      err = cvk::launch_cp_chain_wg(W, g, stream);
+      err = cvk::launch_cp_chain_wg(W, g, cs);
     } else {  // N > 256: one thread per state (cp_superseq_chain), the unpadded f64 tables
       cvk::CpChainArgs g{};
       g.pi = h->d_pi64.as<double>();
@@ -3497,13 +3571,13 @@ cv_status superseq_cp_par(cv_hmm* h, int64_t nseq, const int64_t* offsets, const
       g.init_row = init;
       g.final_row = out_row;
       if (cvk::cp_chain_wide(N)) g.grows = d_small.as<double>() + 2;
-      err = cvk::launch_cp_superseq_chain(g, stream);
+      err = cvk::launch_cp_superseq_chain(g, cs);
     }
     if (err != hipSuccess) return set_err(CV_EDEVICE, "chain run launch failed: %s", hipGetErrorString(err));
     double out[2];
-    HIP_TRY(hipMemcpyAsync(out, d_small.p, 16, hipMemcpyDeviceToHost, stream));
-    HIP_TRY(hipMemcpyAsync(row_host.data(), out_row, (size_t)W * 8, hipMemcpyDeviceToHost, stream));
-    HIP_TRY(hipStreamSynchronize(stream));
+    HIP_TRY(hipMemcpyAsync(out, d_small.p, 16, hipMemcpyDeviceToHost, cs));
+    HIP_TRY(hipMemcpyAsync(row_host.data(), out_row, (size_t)W * 8, hipMemcpyDeviceToHost, cs));
+    HIP_TRY(hipStreamSynchronize(cs));
     row_dev = out_row;
     M = out[0];
     std::memcpy(&row_arg, &out[1], 4);
@@ -3519,28 +3593,22 @@ cv_status superseq_cp_par(cv_hmm* h, int64_t nseq, const int64_t* offsets, const
   // maximum and its start clean; a prediction goes wrong only after an earlier uncertified
   // sequence's path changed, so one batch resolves the fallbacks up to there, and the next
   // batch (from the exact maximum) the ones after.  Batches that resolve little (tie-heavy
-  // models) switch speculation off: the serial runs take over.
+  // models) switch speculation off: the serial runs take over.  A batch covers positions
+  // below x_lim (the walk's limit: the sequences whose successors' scores are in).
   std::vector<int64_t> spec_idx((size_t)nseq, -1);
+  bool beside_fwd = false;  // the walk runs beside the last part's forward pass
   std::vector<double> spec_guess, spec_last;
   std::vector<int64_t> spec_off;
   std::vector<int32_t> spec_path;
   bool spec_on = spec_env;
   int64_t batch_acc = 0, batch_size = 0;
   size_t spec_from = SIZE_MAX;  // position a batch was last launched from
-  constexpr int64_t kSpecMax = 16384;
-  DevBuf d_soff, d_sobs, d_spath, d_sres, d_sinit, d_slast;
-  // the prediction walk's certify() results, reused by the exact walk wherever it arrives at a
-  // sequence after a certified one with the same running maximum, bit for bit (certify is a
-  // function of the sequence, the maximum and the predecessor's kind): memo_in[x] = that
-  // maximum, memo_out[x] = the fold (NaN: not certified), memo_q[x] = quantised (2 = no memo)
-  std::vector<double> memo_in(ks.size()), memo_out(ks.size());
-  std::vector<uint8_t> memo_q(ks.size(), 2);
-  auto speculate = [&](size_t x0) -> cv_status {
+  auto speculate = [&](size_t x0, size_t x_lim) -> cv_status {
     std::vector<int64_t> F;
     std::vector<double> G;
     double Ms = M;
     Kind pk = prev;
-    for (size_t y = x0; y < ks.size() && (int64_t)F.size() < kSpecMax; ++y) {
+    for (size_t y = x0; y < x_lim && (int64_t)F.size() < kSpecMax; ++y) {
       double Mn;
       bool qd;
       const Kind ky = y == x0 ? pk : CERT;
@@ -3575,9 +3643,9 @@ cv_status superseq_cp_par(cv_hmm* h, int64_t nseq, const int64_t* offsets, const
     if ((st = d_sres.ensure((size_t)nf * 9)) != CV_OK) return st;
     if ((st = d_sinit.ensure((size_t)nf * 8)) != CV_OK) return st;
     if ((st = d_slast.ensure((size_t)nf * N * 8)) != CV_OK) return st;
-    HIP_TRY(hipMemcpyAsync(d_soff.p, so.data(), so.size() * 8, hipMemcpyHostToDevice, stream));
-    HIP_TRY(hipMemcpyAsync(d_sobs.p, sob.data(), sob.size() * 4, hipMemcpyHostToDevice, stream));
-    HIP_TRY(hipMemcpyAsync(d_sinit.p, G.data(), (size_t)nf * 8, hipMemcpyHostToDevice, stream));
+    HIP_TRY(hipMemcpyAsync(d_soff.p, so.data(), so.size() * 8, hipMemcpyHostToDevice, cs));
+    HIP_TRY(hipMemcpyAsync(d_sobs.p, sob.data(), sob.size() * 4, hipMemcpyHostToDevice, cs));
+    HIP_TRY(hipMemcpyAsync(d_sinit.p, G.data(), (size_t)nf * 8, hipMemcpyHostToDevice, cs));
     cv_opts oc = default_opts();
     oc.dtype = CV_DTYPE_F64;
     oc.assoc = CV_ASSOC_CP;
@@ -3587,17 +3655,25 @@ cv_status superseq_cp_par(cv_hmm* h, int64_t nseq, const int64_t* offsets, const
     const bool spec_generic = !small || h->tuning.chain_spec_kernel != 1;
     oc.kernel = spec_generic ? CV_KERNEL_GENERIC : CV_KERNEL_TRELLIS_F64;
     oc.rescore_f64 = 0;
-    oc.stream = stream;
+    oc.stream = cs;
     double* sc = d_sres.as<double>();
+    // beside the last part's forward pass (two waves of 224 VGPRs per SIMD, 31.5 KiB of LDS per
+    // CU left): one sequence per workgroup, whose 58-VGPR waves fit the 64 VGPRs left, instead
+    // of the two-sequence kernel's 78, which waited for the forward pass to drain
+    cvk::TuningOverride one_seq(&cvk::Tuning::generic_s, beside_fwd && h->tuning.generic_s == 0 ? 1 : h->tuning.generic_s);
+    // ... and at issue priority 3: a latency-bound walk that takes few issue slots, which the
+    // forward's waves (priority 2-3) would otherwise leave it only when they stall
+    cvk::TuningOverride prio(&cvk::Tuning::generic_prio, beside_fwd ? 1 : h->tuning.generic_prio);
+    // the side workspace: the main one may still hold the last part's forward pass
     if ((st = decode_device(h, nf, so.data(), d_soff.as<int64_t>(), d_sobs.as<int32_t>(), oc, d_spath.as<int32_t>(), sc,
-                            reinterpret_cast<uint8_t*>(sc + nf), stream, nullptr, false, nullptr,
-                            d_sinit.as<double>(), d_slast.as<double>())) != CV_OK)
+                            reinterpret_cast<uint8_t*>(sc + nf), cs, nullptr, true, nullptr, d_sinit.as<double>(),
+                            d_slast.as<double>())) != CV_OK)
       return st;
     spec_path.resize((size_t)Ls);
     spec_last.resize((size_t)nf * N);
-    HIP_TRY(hipMemcpyAsync(spec_path.data(), d_spath.p, (size_t)Ls * 4, hipMemcpyDeviceToHost, stream));
-    HIP_TRY(hipMemcpyAsync(spec_last.data(), d_slast.p, (size_t)nf * N * 8, hipMemcpyDeviceToHost, stream));
-    HIP_TRY(hipStreamSynchronize(stream));
+    HIP_TRY(hipMemcpyAsync(spec_path.data(), d_spath.p, (size_t)Ls * 4, hipMemcpyDeviceToHost, cs));
+    HIP_TRY(hipMemcpyAsync(spec_last.data(), d_slast.p, (size_t)nf * N * 8, hipMemcpyDeviceToHost, cs));
+    HIP_TRY(hipStreamSynchronize(cs));
     trace_mark("chain: speculative batch (pack, decode, D2H)");
     spec_off = std::move(so);
     spec_guess = std::move(G);
@@ -3608,68 +3684,83 @@ cv_status superseq_cp_par(cv_hmm* h, int64_t nseq, const int64_t* offsets, const
     return CV_OK;
   };
 
-  for (size_t x = 0; x < ks.size();) {
-    const int64_t k = ks[x];
-    const int64_t e0 = off[(size_t)k], T = off[(size_t)k + 1] - e0;
-    double Mn;
-    bool qd;
-    bool ok;
-    if (prev == CERT && memo_q[x] != 2 && dbits(memo_in[x]) == dbits(M)) {
-      ok = !std::isnan(memo_out[x]);  // the prediction walk's decision at this very maximum
-      Mn = memo_out[x];
-      qd = memo_q[x] == 1;
-      ++memo_hits;
-    } else {
-      ok = certify(x, M, prev, &Mn, &qd);
-    }
-    if (ok) {
-      if (in_run && (st = end_run(row_arg)) != CV_OK) return st;  // clean: the run ends in its argmax
-      M = Mn;
-      prev = CERT;
-      prev_end = ends[(size_t)k];
-      ++ncert;
-      nquant += qd ? 1 : 0;
-      ++x;
-      continue;
-    }
-    const double S = score_of(x);
-    const bool start_clean = prev != ROW || row_clean(row_host.data(), row_arg, M, S + pimax + 16.0);
-    const int64_t si = spec_idx[(size_t)k];
-    if (si >= 0 && start_clean && spec_guess[(size_t)si] == M && std::signbit(spec_guess[(size_t)si]) == std::signbit(M)) {
-      // the speculative decode started from the chain's exact state: it IS the chain there
-      const double* lr = spec_last.data() + (size_t)si * N;
-      int32_t arg = 0;
-      for (int32_t i = 1; i < N; ++i)
-        if (lr[i] > lr[arg]) arg = i;
-      const double m1 = lr[arg];
-      if (m1 > -INFINITY && (x + 1 >= ks.size() || row_clean(lr, arg, m1, score_of(x + 1) + pimax + 16.0))) {
-        if (in_run && (st = end_run(row_arg)) != CV_OK) return st;
-        const int32_t* sp = spec_path.data() + spec_off[(size_t)si];
-        deferred.emplace_back(e0, std::vector<int32_t>(sp, sp + T));
-        std::copy(lr, lr + N, row_host.begin());
-        std::fill(row_host.begin() + N, row_host.end(), -INFINITY);
-        row_dev = nullptr;
-        row_arg = arg;
-        M = m1;
-        prev = ROW;
-        ++spec_acc;
-        ++batch_acc;
+  // 3. the walk over positions [x, x_lim)
+  size_t x = 0;
+  auto walk = [&](size_t x_lim) -> cv_status {
+    while (x < x_lim) {
+      const int64_t k = ks[x];
+      const int64_t e0 = off[(size_t)k], T = off[(size_t)k + 1] - e0;
+      double Mn;
+      bool qd;
+      bool ok;
+      if (prev == CERT && memo_q[x] != 2 && dbits(memo_in[x]) == dbits(M)) {
+        ok = !std::isnan(memo_out[x]);  // the prediction walk's decision at this very maximum
+        Mn = memo_out[x];
+        qd = memo_q[x] == 1;
+        ++memo_hits;
+      } else {
+        ok = certify(x, M, prev, &Mn, &qd);
+      }
+      if (ok) {
+        if (in_run && (st = end_run(row_arg)) != CV_OK) return st;  // clean: the run ends in its argmax
+        M = Mn;
+        prev = CERT;
+        prev_end = ends[(size_t)k];
+        ++ncert;
+        nquant += qd ? 1 : 0;
         ++x;
         continue;
       }
-      // its end state could differ from its argmax (an unclean boundary): the serial chain
-    } else if (spec_on && start_clean && spec_from != x) {
-      // no valid speculation for this sequence (none yet, or an earlier path changed): a new
-      // batch from the exact state here, unless the last one resolved too little
-      if (spec_batches > 0 && batch_acc < 4 && batch_acc * 4 < batch_size) spec_on = false;
-      if (spec_on) {
-        spec_from = x;
-        if ((st = speculate(x)) != CV_OK) return st;
-        continue;  // retry x with the new batch
+      const double S = score_of(x);
+      const bool start_clean = prev != ROW || row_clean(row_host.data(), row_arg, M, S + pimax + 16.0);
+      const int64_t si = spec_idx[(size_t)k];
+      if (si >= 0 && start_clean && spec_guess[(size_t)si] == M &&
+          std::signbit(spec_guess[(size_t)si]) == std::signbit(M)) {
+        // the speculative decode started from the chain's exact state: it IS the chain there
+        const double* lr = spec_last.data() + (size_t)si * N;
+        int32_t arg = 0;
+        for (int32_t i = 1; i < N; ++i)
+          if (lr[i] > lr[arg]) arg = i;
+        const double m1 = lr[arg];
+        if (m1 > -INFINITY && (x + 1 >= ks.size() || row_clean(lr, arg, m1, score_of(x + 1) + pimax + 16.0))) {
+          if (in_run && (st = end_run(row_arg)) != CV_OK) return st;
+          const int32_t* sp = spec_path.data() + spec_off[(size_t)si];
+          deferred.emplace_back(e0, std::vector<int32_t>(sp, sp + T));
+          std::copy(lr, lr + N, row_host.begin());
+          std::fill(row_host.begin() + N, row_host.end(), -INFINITY);
+          row_dev = nullptr;
+          row_arg = arg;
+          M = m1;
+          prev = ROW;
+          ++spec_acc;
+          ++batch_acc;
+          ++x;
+          continue;
+        }
+        // its end state could differ from its argmax (an unclean boundary): the serial chain
+      } else if (spec_on && start_clean && spec_from != x) {
+        // no valid speculation for this sequence (none yet, or an earlier path changed): a new
+        // batch from the exact state here, unless the last one resolved too little
+        if (spec_batches > 0 && batch_acc < 4 && batch_acc * 4 < batch_size) spec_on = false;
+        if (spec_on) {
+          spec_from = x;
+          if ((st = speculate(x, x_lim)) != CV_OK) return st;
+          continue;  // retry x with the new batch
+        }
       }
+      if ((st = run_step(k)) != CV_OK) return st;
+      ++x;
     }
-    if ((st = run_step(k)) != CV_OK) return st;
-    ++x;
+    return CV_OK;
+  };
+  for (int p = 0; p < nparts; ++p) {
+    if ((st = prep(p)) != CV_OK) return st;
+    if (fallback) return CV_OK;
+    // all but the part's last sequence (its boundary test needs the next part's first score)
+    const size_t x_lim = p + 1 < nparts ? (ks.empty() ? 0 : ks.size() - 1) : ks.size();
+    beside_fwd = p + 1 < nparts;
+    if ((st = walk(x_lim)) != CV_OK) return st;
+    if (p + 1 < nparts) trace_mark("chain: part walked");
   }
   if (in_run && (st = end_run(row_arg)) != CV_OK) return st;  // cp.rs:86: first argmax of the last row
   if (path_st != CV_OK) return path_st;

@@ -106,6 +106,10 @@ struct GenericFwdArgs {
   // one launch per step, each sequence's states spread over ceil(N / 256) workgroups
   REAL* grows;
   int64_t wide_steps;
+  // 1: the waves run at issue priority 3 (set by launch_generic_fwd from tuning key
+  // generic_prio: the parallel chain's speculative batch beside a forward pass, whose waves
+  // otherwise take issue slots only where the forward's leave one)
+  int prio;
 };
 
 template <typename REAL>

@@ -1453,6 +1453,7 @@ __global__ __launch_bounds__(1024) void generic_fwd_ms(GenericFwdArgs<REAL> args
     Tmax = T[s] > Tmax ? T[s] : Tmax;
   }
   if (Tmax <= 0) return;
+  if (args.prio) __builtin_amdgcn_s_setprio(3);
   auto row = [&](int buf, int s) -> REAL* { return dbuf + ((size_t)buf * S + s) * N; };
   auto grow = [&](int s, int t) -> REAL* { return args.rows + (e0[s] + t - args.psi_elem_base) * (int64_t)N; };
   int bad = 0;  // bit s: sequence s saw an observation outside [0, V)
@@ -2239,8 +2240,10 @@ hipError_t launch_generic_ms(const GenericFwdArgs<REAL>& fa, int64_t nseq, hipSt
 }
 
 template <typename REAL>
-hipError_t launch_generic_fwd(const GenericFwdArgs<REAL>& fa, int64_t nseq, hipStream_t stream) {
+hipError_t launch_generic_fwd(const GenericFwdArgs<REAL>& fa_in, int64_t nseq, hipStream_t stream) {
   if (nseq <= 0) return hipSuccess;
+  GenericFwdArgs<REAL> fa = fa_in;
+  fa.prio = tuning().generic_prio == 1 ? 1 : 0;  // tuning key (issue priority only: bit-identical)
   if (fa.grows) return launch_generic_wide<REAL>(fa, nseq, stream);
   if (fa.rows) {  // rows mode: the maximum only (VITERBI / DECODE / DP)
     if (fa.assoc == CVK_ASSOC_CP || fa.nstates > generic_max_states((int)sizeof(REAL))) return hipErrorInvalidValue;

@@ -1163,6 +1163,9 @@ __device__ __forceinline__ int first_argmax_d(const double (&s)[KP], const bool 
 // cp_cert_f64 does.  So the returned rho equals cp_cert_f64's exact rho whenever that is below
 // rho_cap, and is >= rho_cap otherwise: the host's tests rho > U agree with the exact
 // certificate for every U <= rho_cap (the host sizes rho_cap above the largest U it can test).
+#ifndef CVK_BT_ROLL
+#define CVK_BT_ROLL 0
+#endif
 template <int KP, int PF, bool DEC = false, bool NONPOS = false, bool CERT = false>
 __device__ __forceinline__ void bt_chain_f64(const uint32_t* __restrict__ rows, int T, int cur, int32_t* __restrict__ path,
                                              const double* __restrict__ at, const double* __restrict__ et,
@@ -1323,9 +1326,14 @@ __device__ __forceinline__ void bt_chain_f64(const uint32_t* __restrict__ rows, 
         if (lane == (tp & 63)) pathreg = cur;
         if ((tp & 63) == 0 && tp + lane < T) path[tp + lane] = pathreg;
       }
+#if CVK_BT_ROLL
+      load_hi(t - PF - 1, ring[u]);  // the row of step t - PF, PF steps ahead
+#endif
     }
+#if !CVK_BT_ROLL
 #pragma unroll
     for (int u = 0; u < PF; ++u) load_hi(base - PF - 1 - u, ring[u]);
+#endif
   }
   if constexpr (CERT) *rho_io = rho;
 }

@@ -32,6 +32,7 @@ struct Tuning {
   int chain_spec_kernel = 0;   // 1: speculation on trellis_cp_f64 instead of the generic CP kernel
   int chain_copy_overlap = 1;  // 0: the chain's path copy after the certificate pass
   int chain_cert_fused = 1;    // 0: the chain's certificates by their own pass (cp_cert_f64), not the backtrack
+  int chain_parts = 1;         // 0: the chain's decode in one part (no walk beside the last part's forward)
   // ---- f64 trellis (kernels/trellis64.hip) ----
   int t64_s = 0;               // sequences per wave 2 / 4 / 6 / 8 (0: by batch)
   int t64_512 = -1;            // NP = 512 batch kernel: -1 auto, 0 never, 1 whenever supported
@@ -51,7 +52,8 @@ struct Tuning {
   int generic_split = 0;       // 1: generic_fwd_split (K threads per state)
   int generic_split_k = 0;     // its K (0: by N)
   int generic_wide = 1;        // 0: never the wide (one launch per step) decode
-  int generic_wide_min = 0;    // > 0: the wide decode from this N on
+  int generic_wide_min = 0;
+  int generic_prio = 0;  // 1: generic_fwd_ms waves at issue priority 3 (the chain sets it beside a forward)    // > 0: the wide decode from this N on
   int wide_s = 0;              // wide decode sequences per workgroup 1 / 2 / 4 (0: by batch)
   int ext_wide_min = 0;        // > 0: the constrained terms passes wide from this N on
   int chain_wide = 1;          // 0: never the wide serial chain step
@@ -68,6 +70,19 @@ const Tuning& tuning();
 // makes `t` the calling thread's current tuning until the matching tuning_leave
 void tuning_enter(const Tuning& t);
 void tuning_leave();
+// one key of the calling thread's current tuning (inside a TuningScope) set to `value` until
+// destroyed; nothing outside a scope
+struct TuningOverride {
+  TuningOverride(int Tuning::*field, int value);
+  ~TuningOverride();
+  TuningOverride(const TuningOverride&) = delete;
+  TuningOverride& operator=(const TuningOverride&) = delete;
+
+ private:
+  int Tuning::*field_;
+  int saved_;
+  bool on_;
+};
 struct TuningScope {
   explicit TuningScope(const Tuning& t) { tuning_enter(t); }
   ~TuningScope() { tuning_leave(); }

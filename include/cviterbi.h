@@ -172,6 +172,9 @@ CV_API void cv_hmm_destroy(cv_hmm* h);
  *   chain_spec_kernel 0   1: speculation on trellis_cp_f64 instead of the generic CP kernel
  *   chain_copy_overlap 1  0: the parallel chain in one decode chunk, its path copy before the walk
  *   chain_cert_fused 1    0: the chain's certificates by their own pass (cp_cert_f64), not the backtrack
+ *   chain_parts 1         0: the parallel chain's decode in one part (1: two parts where N <= 256 and
+ *                         the batch spans several forward rounds; the walk over the first part runs
+ *                         beside the second part's forward pass)
  *   t64_s 0               f64 trellis sequences per wave 2 / 4 / 6 / 8 (0: by batch)
  *   t64_512 / t64_1024 -1 NP = 512 / 1,024 batch kernel: -1 auto, 0 never, 1 always
  *   t64_wg 1              0: one wave per workgroup instead of eight-wave units
@@ -187,6 +190,8 @@ CV_API void cv_hmm_destroy(cv_hmm* h);
  *   generic_s 0           generic kernels' sequences per workgroup 1 / 2 / 4 (0: by batch)
  *   generic_split 0, generic_split_k 0   1: K threads per state (generic_fwd_split), its K
  *   generic_wide 1, generic_wide_min 0   0: never wide / > 0: wide from this N
+ *   generic_prio 0        1: generic_fwd_ms waves at issue priority 3 (the parallel chain sets it
+ *                         for its speculative batch beside the last part's forward pass)
  *   wide_s 0              wide decode sequences per workgroup 1 / 2 / 4 (0: by batch)
  *   ext_wide_min 0        > 0: the constrained terms passes wide from this N
  *   chain_wide 1, chain_wide_min 0       the wide serial chain step: 0 never / from this N

@@ -18,13 +18,15 @@ VARIANTS = [
     ("generic s=1", "generic", {"generic_s": 1}),
     ("generic s=2", "generic", {"generic_s": 2}),
     ("generic s=4", "generic", {"generic_s": 4}),
+    ("generic split k=2", "generic", {"generic_split": 1, "generic_split_k": 2}),
+    ("generic split k=4", "generic", {"generic_split": 1, "generic_split_k": 4}),
     ("trellis_cp auto", "trellis_f64", {}),
     ("trellis_cp w=1", "trellis_f64", {"t64_cp_w": 1}),
 ]
 
 
 def main():
-    sizes = [int(x) for x in sys.argv[1:]] or [573]
+    sizes = [int(x) for x in sys.argv[1:]] or [573, 143]
     c = synth.config("c4", max(sizes))
     h = cv.HMM(c["pi"], c["a"], c["b"])
     off, obs = c["offsets"], c["obs"]

@@ -60,7 +60,19 @@ run() {
       (cd /tmp && REPS=3 step c2pmc2 120 rocprofv3 --kernel-include-regex wave48 --pmc SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_ANY \
         SQ_INST_CYCLES_VMEM SQ_WAIT_INST_LDS SQ_INSTS_LDS SQ_INSTS_VMEM GRBM_GUI_ACTIVE -d $O/pmc2 -o pmc2 --output-format csv \
         -- python3 $R/tools/bench_configs.py c2f64) ;;
-    spec) step spec 300 python3 -u tools/bench_spec.py 573 64 ;;
+    spec) step spec 300 python3 -u tools/bench_spec.py 573 143 64 ;;
+    specu16) CV_LIB_PATH=$R/tools/_ab/libcv_u16.so step specu16 300 python3 -u tools/bench_spec.py 573 143 ;;
+    btpf)  # the backtrack's rows in flight (tuning key t64_bt_pf): config 4 and the chain
+      for pf in 2 4 8; do
+        REPS=3 CV_T64_BT_PF=$pf step btpf_c4_$pf 200 python3 -u tools/bench_configs.py c4f64 &&
+          CV_T64_BT_PF=$pf step btpf_chain_$pf 240 python3 -u tools/bench_chain.py 65536 256 || return $?
+      done ;;
+    btab)  # block-refilled vs rolling backtrack row ring, rows in flight 2 / 4 / 8 (config 4)
+      for pf in 2 4 8; do
+        REPS=3 CV_T64_BT_PF=$pf step btab_main_$pf 200 python3 -u tools/bench_configs.py c4f64 &&
+          REPS=3 CV_T64_BT_PF=$pf CV_LIB_PATH=$R/tools/_ab/libcv_roll.so step btab_roll_$pf 200 \
+            python3 -u tools/bench_configs.py c4f64 || return $?
+      done ;;
     smoke) step smoke 200 python3 -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" ;;
     bench) step bench 400 python3 -u bench.py ;;
     prof)

@@ -1,8 +1,9 @@
 """Timeline of the last call in a rocprofv3 --kernel-trace [--memory-copy-trace] csv directory.
 
-  python tools/trace_timeline.py <trace dir> <kernel-name substring marking the call's start>
+  python tools/trace_timeline.py <trace dir> <kernel-name substring marking the call's start> [k]
 
-Prints every kernel dispatch and copy from the LAST dispatch whose name contains the marker on,
+Prints every kernel dispatch and copy from the LAST (k = -1, or the k-th from the end) dispatch
+whose name contains the marker on,
 in start order, in ms relative to that dispatch, with the gap after the previous item's end.
 """
 import csv
@@ -25,7 +26,7 @@ def main():
     starts = [i for i, r in enumerate(rows) if marker in r[2]]
     if not starts:
         raise SystemExit(f"no dispatch matches {marker!r}")
-    i0 = starts[-1]
+    i0 = starts[int(sys.argv[3]) if len(sys.argv) > 3 else -1]
     t0 = rows[i0][0]
     prev = None
     for s, e, k in rows[i0:]:
