@@ -310,7 +310,7 @@ struct cv_hmm {
     DevBuf off, obs, path, res, cert, ebin, q, ends, gid, gpath;
     // serial runs and speculative batches (kept, so no hipFree -- a device-wide sync -- lands
     // while the second part's forward pass runs)
-    DevBuf first, rpsi, rows, small, rpath, soff, sobs, spath, sres, sinit, slast;
+    DevBuf first, rpsi, rows, small, rpath, soff, sobs, spath, sres, sinit, slast, spsi;
   } chainb;
   // the chain's own stream (high priority: its walk-side kernels -- end states, quantised folds,
   // gathers, runs, speculative batches -- run beside the second part's forward pass) and the
@@ -3097,11 +3097,11 @@ cv_status superseq_cp_par(cv_hmm* h, int64_t nseq, const int64_t* offsets, const
   int64_t maxT = 0;
   for (int64_t k = 0; k <= nseq; ++k) off[(size_t)k] = offsets[k] - base;
   for (int64_t k = 0; k < nseq; ++k) maxT = std::max(maxT, off[(size_t)k + 1] - off[(size_t)k]);
-  // 1. the per-sequence row-A0 decode with certificates -- in two parts where N <= 256 and the
-  // batch spans several forward rounds: the walk over the first part (its end states,
-  // quantised folds, gathered paths, runs and speculative batches, all on the chain stream)
-  // runs while the second part's forward pass holds the chip, so only the second part's share
-  // of that work follows the last forward (tuning key chain_parts = 0: one part)
+  // 1. the per-sequence row-A0 decode with certificates -- in parts where N <= 256 and the
+  // batch spans more than a forward round: the walk over each part (its end states, quantised
+  // folds, gathered paths, runs and speculative batches, all on the chain stream) runs while
+  // the next part's forward pass holds the chip, so only the last part's share of that work
+  // follows the last forward (tuning key chain_parts = 0: one part)
   DevBuf &d_off = h->chainb.off, &d_obs = h->chainb.obs, &d_path = h->chainb.path, &d_res = h->chainb.res,
          &d_cert = h->chainb.cert;
   if ((st = d_off.ensure((size_t)(nseq + 1) * 8)) != CV_OK) return st;
@@ -3136,13 +3136,24 @@ cv_status superseq_cp_par(cv_hmm* h, int64_t nseq, const int64_t* offsets, const
   // paths of the few sequences it may fold element by element (fetched packed).  Tuning key
   // chain_copy_overlap = 0: one part, the copy before the walk.
   const bool overlap_copy = h->tuning.chain_copy_overlap != 0;
-  // the parts: one forward round each (64 sequences per CU at eight per wave), the last one
-  // taking the remainder; part p's walk runs beside part p + 1's forward pass, part p + 1's
-  // observations cross during part p's
+  // the parts: part p's walk runs beside part p + 1's forward pass, part p + 1's observations
+  // cross during part p's.  A forward round is 64 sequences per CU (eight per wave); a launch
+  // of one round pays its own fill and drain (one round alone: 36.8 ms vs 33.5 ms per round of
+  // a four-round launch), while half a round runs at four per wave in half the time.  Tuning key
+  // chain_parts = 1 (default): one large first part, then chain_tail parts of a round /
+  // chain_tail_div each (config 4: 49,152 + 8,192 + 8,192), so only a small part's work follows
+  // the last forward; 2: one round per part
   std::vector<int64_t> pb{0};
   if (small && overlap_copy && h->tuning.chain_parts != 0) {
     const int64_t unit = 64 * (int64_t)std::max(h->cus, 1);
-    for (int64_t s = unit; s + unit <= nseq; s += unit) pb.push_back(s);
+    if (h->tuning.chain_parts == 2) {
+      for (int64_t s = unit; s + unit <= nseq; s += unit) pb.push_back(s);
+    } else {
+      const int64_t ntail = std::max(0, h->tuning.chain_tail);
+      const int64_t tsz = std::max<int64_t>(1, unit / std::max(1, h->tuning.chain_tail_div));
+      if (ntail > 0 && nseq >= unit + ntail * tsz)
+        for (int64_t i = ntail; i >= 1; --i) pb.push_back(nseq - i * tsz);
+    }
   }
   pb.push_back(nseq);
   const int nparts = (int)pb.size() - 1;
@@ -3646,6 +3657,26 @@ cv_status superseq_cp_par(cv_hmm* h, int64_t nseq, const int64_t* offsets, const
     HIP_TRY(hipMemcpyAsync(d_soff.p, so.data(), so.size() * 8, hipMemcpyHostToDevice, cs));
     HIP_TRY(hipMemcpyAsync(d_sobs.p, sob.data(), sob.size() * 4, hipMemcpyHostToDevice, cs));
     HIP_TRY(hipMemcpyAsync(d_sinit.p, G.data(), (size_t)nf * 8, hipMemcpyHostToDevice, cs));
+    // N <= 256 after the last forward pass (the chip is free): the serial chain kernel's
+    // layout, one sequence per workgroup and CU (A on chip, ~3.5 us per element; tuning key
+    // chain_spec_kernel = 0), its path backtracked in the same workgroup
+    if (small && !beside_fwd && h->tuning.chain_spec_kernel == 0) {
+      DevBuf& d_spsi = h->chainb.spsi;
+      if ((st = d_spsi.ensure((size_t)Ls * W * 2)) != CV_OK) return st;
+      cvk::CpChainWgArgs g{};
+      g.pi = h->q_pi.as<double>();
+      g.a = h->q_a.as<double>();
+      g.et = h->q_et.as<double>();
+      g.obs = d_sobs.as<int32_t>();
+      g.nstates = N;
+      g.psi = d_spsi.as<uint16_t>();
+      g.final_row = d_slast.as<double>();
+      g.soff = d_soff.as<int64_t>();
+      g.sinit = d_sinit.as<double>();
+      g.path = d_spath.as<int32_t>();
+      const hipError_t e = cvk::launch_cp_chain_wg_batch(W, g, nf, cs);
+      if (e != hipSuccess) return set_err(CV_EDEVICE, "chain speculative batch failed: %s", hipGetErrorString(e));
+    } else {
     cv_opts oc = default_opts();
     oc.dtype = CV_DTYPE_F64;
     oc.assoc = CV_ASSOC_CP;
@@ -3669,6 +3700,7 @@ cv_status superseq_cp_par(cv_hmm* h, int64_t nseq, const int64_t* offsets, const
                             reinterpret_cast<uint8_t*>(sc + nf), cs, nullptr, true, nullptr, d_sinit.as<double>(),
                             d_slast.as<double>())) != CV_OK)
       return st;
+    }
     spec_path.resize((size_t)Ls);
     spec_last.resize((size_t)nf * N);
     HIP_TRY(hipMemcpyAsync(spec_path.data(), d_spath.p, (size_t)Ls * 4, hipMemcpyDeviceToHost, cs));

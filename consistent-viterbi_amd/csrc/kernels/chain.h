@@ -25,9 +25,21 @@ struct CpChainWgArgs {
   // [NP] receives the last row.  Both null: the whole chain (row 0 = init_probs, cp.rs:66-68).
   const double* init_row;
   double* final_row;
+  // BATCH (launch_cp_chain_wg_batch, the parallel chain's speculative re-decodes after the
+  // forward passes): workgroup i decodes sequence i of a packed batch on its own, elements
+  // [soff[i], soff[i + 1]) of obs, row 0 = sinit[i] + (pi + b) (the chain's start value at
+  // offset sinit[i] after a clean boundary, utils.rs:32-35), psi rows at psi + soff[i] * np;
+  // its last row to final_row + i * nstates and its path (first argmax of the last row,
+  // cp.rs:86, then psi) to path + soff[i]
+  const int64_t* soff;
+  const double* sinit;
+  int32_t* path;
 };
 // forward of the whole chain on ONE workgroup; np = 64 * ceil(N / 64) <= 256
 hipError_t launch_cp_chain_wg(int np, const CpChainWgArgs& g, hipStream_t stream);
+// nseq such sequences at once, one workgroup (one CU) each: A on chip, ~3.5 us per element at
+// N = 256, against ~17 us for the one-thread-per-state kernels that stream A from L2
+hipError_t launch_cp_chain_wg_batch(int np, const CpChainWgArgs& g, int64_t nseq, hipStream_t stream);
 // LDS bytes launch_cp_chain_wg asks for at this np (0: unsupported)
 size_t cp_chain_wg_lds(int np);
 

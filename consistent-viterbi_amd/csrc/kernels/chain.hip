@@ -30,6 +30,11 @@ namespace {
 // AFULL: a full copy of A in LDS after the row slices (NP <= 128), so the value's a[psi][j]
 // is an LDS read instead of an L2 round trip on the element's critical path.
 template <int NP, int G, int RREG, int RLDS, int RGLB, bool AFULL>
+constexpr size_t chain_lds_bytes() {
+  return (size_t)(2 * NP + G * NP + G * NP / 2 + G * RLDS * NP + (AFULL ? NP * NP : 0)) * sizeof(double);
+}
+
+template <int NP, int G, int RREG, int RLDS, int RGLB, bool AFULL, bool BATCH = false>
 __global__ __launch_bounds__(NP * G) void cp_chain_wg(CpChainWgArgs g) {
   constexpr int R = NP / G;
   static_assert(RREG + RLDS + RGLB == R, "every candidate row has one home");
@@ -44,6 +49,17 @@ __global__ __launch_bounds__(NP * G) void cp_chain_wg(CpChainWgArgs g) {
   const int tid = threadIdx.x;
   const int c = tid % NP;
   const int grp = __builtin_amdgcn_readfirstlane(tid / NP);  // wave-uniform (NP % 64 == 0)
+  const int32_t* obs = g.obs;
+  uint16_t* psi = g.psi;
+  int64_t L = g.len;
+  int64_t e0 = 0;
+  if constexpr (BATCH) {
+    e0 = g.soff[blockIdx.x];
+    L = g.soff[blockIdx.x + 1] - e0;
+    obs += e0;
+    psi += e0 * NP;
+    if (L <= 0) return;  // uniform over the workgroup
+  }
   const int i0 = grp * R;
   double areg[RREG > 0 ? RREG : 1];
 #pragma unroll
@@ -52,13 +68,18 @@ __global__ __launch_bounds__(NP * G) void cp_chain_wg(CpChainWgArgs g) {
   const double* aglb = g.a + (size_t)(i0 + RREG + RLDS) * NP + c;
   if constexpr (AFULL)
     for (int k = tid; k < NP * NP; k += NP * G) afull[k] = g.a[k];
-  if (grp == 0)  // init_probs (cp.rs:66-68), or the row before this part of the chain
-    prev[c] = g.init_row ? g.init_row[c] : g.pi[c] + g.et[(size_t)g.obs[0] * NP + c];
+  if (grp == 0) {  // init_probs (cp.rs:66-68), or the row before this part of the chain
+    if constexpr (BATCH)
+      prev[c] = g.sinit[blockIdx.x] + (g.pi[c] + g.et[(size_t)obs[0] * NP + c]);
+    else
+      prev[c] = g.init_row ? g.init_row[c] : g.pi[c] + g.et[(size_t)obs[0] * NP + c];
+  }
   __syncthreads();
-  const int64_t L = g.len;
-  for (int64_t t = g.init_row ? 0 : 1; t < L; ++t) {
-    const bool first = g.first[t] != 0;
-    const int o = g.obs[t];
+  for (int64_t t = (!BATCH && g.init_row) ? 0 : 1; t < L; ++t) {
+    // BATCH passes first = nullptr: the branch stays (without it the compiler's schedule of the
+    // candidate loop spills 42 VGPRs at N = 256)
+    const bool first = BATCH ? (g.first && g.first[t] != 0) : g.first[t] != 0;
+    const int o = obs[t];
     double m;
     int arg;
     if (first) {  // transitions = the constant pi[j] (utils.rs:32-35)
@@ -120,12 +141,50 @@ __global__ __launch_bounds__(NP * G) void cp_chain_wg(CpChainWgArgs g) {
       }
       const double tr = first ? g.pi[c] : AFULL ? afull[A * NP + c] : g.a[(size_t)A * NP + c];
       cur[c] = prev[A] + (tr + g.et[(size_t)o * NP + c]);  // cp.rs:75-77
-      g.psi[(size_t)t * NP + c] = (uint16_t)A;
+      psi[(size_t)t * NP + c] = (uint16_t)A;
     }
     __syncthreads();
     double* tmp = prev;
     prev = cur;
     cur = tmp;
+  }
+  if constexpr (BATCH) {
+    if (grp == 0 && c < g.nstates) g.final_row[(size_t)blockIdx.x * g.nstates + c] = prev[c];
+    // the path: first argmax of the last row (cp.rs:86), then psi back to element 0, the psi
+    // rows staged through the LDS the A rows no longer need (after both row buffers), walked by
+    // one thread (a dependent LDS read per element instead of an L2 round trip)
+    constexpr int64_t kCap = (int64_t)((chain_lds_bytes<NP, G, RREG, RLDS, RGLB, AFULL>() - 2 * NP * sizeof(double)) /
+                                       (NP * sizeof(uint16_t))) / 8 * 8;
+    static_assert(kCap >= 8, "psi staging rows");
+    uint16_t* ps = reinterpret_cast<uint16_t*>(sm + 2 * NP);
+    int32_t* path = g.path + e0;
+    int cs = 0;
+    if (tid == 0) {
+      double m = prev[0];
+      for (int i = 1; i < g.nstates; ++i)
+        if (prev[i] > m) {
+          m = prev[i];
+          cs = i;
+        }
+      path[L - 1] = cs;
+    }
+    __threadfence();  // this workgroup's psi stores, read back below
+    __syncthreads();
+    for (int64_t hi = L; hi > 1;) {  // rows [lo, hi) hold psi for elements lo .. hi - 1
+      const int64_t lo = hi - 1 > kCap ? hi - kCap : 1;
+      const uint4* src = reinterpret_cast<const uint4*>(psi + lo * NP);
+      uint4* dst = reinterpret_cast<uint4*>(ps);
+      for (int64_t q = tid; q < (hi - lo) * NP / 8; q += NP * G) dst[q] = src[q];
+      __syncthreads();
+      if (tid == 0)
+        for (int64_t t = hi - 1; t >= lo; --t) {
+          cs = ps[(t - lo) * NP + cs];
+          path[t - 1] = cs;
+        }
+      __syncthreads();
+      hi = lo;
+    }
+    return;
   }
   if (g.final_row && grp == 0) g.final_row[c] = prev[c];
   if (tid == 0) {  // cp.rs:86 / 140: first argmax and max of the last row
@@ -143,16 +202,17 @@ __global__ __launch_bounds__(NP * G) void cp_chain_wg(CpChainWgArgs g) {
 
 template <int NP, int G, int RREG, int RLDS, int RGLB, bool AFULL>
 size_t chain_lds() {
-  return (size_t)(2 * NP + G * NP + G * NP / 2 + G * RLDS * NP + (AFULL ? NP * NP : 0)) * sizeof(double);
+  return chain_lds_bytes<NP, G, RREG, RLDS, RGLB, AFULL>();
 }
 
-template <int NP, int G, int RREG, int RLDS, int RGLB, bool AFULL>
-hipError_t chain_launch(const CpChainWgArgs& g, hipStream_t stream) {
+template <int NP, int G, int RREG, int RLDS, int RGLB, bool AFULL, bool BATCH = false>
+hipError_t chain_launch(const CpChainWgArgs& g, hipStream_t stream, int64_t nblocks = 1) {
   const size_t lds = chain_lds<NP, G, RREG, RLDS, RGLB, AFULL>();
   if (lds > 64 * 1024)
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&cp_chain_wg<NP, G, RREG, RLDS, RGLB, AFULL>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&cp_chain_wg<NP, G, RREG, RLDS, RGLB, AFULL, BATCH>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL((cp_chain_wg<NP, G, RREG, RLDS, RGLB, AFULL>), dim3(1), dim3(NP * G), lds, stream, g);
+  hipLaunchKernelGGL((cp_chain_wg<NP, G, RREG, RLDS, RGLB, AFULL, BATCH>), dim3((unsigned)nblocks), dim3(NP * G), lds,
+                     stream, g);
   return hipGetLastError();
 }
 
@@ -474,6 +534,18 @@ hipError_t launch_cp_chain_wg(int np, const CpChainWgArgs& g, hipStream_t stream
     case 128: return chain_launch<128, 4, 32, 0, 0, true>(g, stream);
     case 192: return chain_launch<192, 4, 32, 16, 0, false>(g, stream);
     case 256: return chain_launch<256, 4, 47, 17, 0, false>(g, stream);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+hipError_t launch_cp_chain_wg_batch(int np, const CpChainWgArgs& g, int64_t nseq, hipStream_t stream) {
+  if (nseq <= 0) return hipSuccess;
+  if (!g.soff || !g.sinit || !g.path || !g.final_row || nseq > 0x7fffffff) return hipErrorInvalidValue;
+  switch (np) {
+    case 64: return chain_launch<64, 4, 16, 0, 0, true, true>(g, stream, nseq);
+    case 128: return chain_launch<128, 4, 32, 0, 0, true, true>(g, stream, nseq);
+    case 192: return chain_launch<192, 4, 32, 16, 0, false, true>(g, stream, nseq);
+    case 256: return chain_launch<256, 4, 47, 17, 0, false, true>(g, stream, nseq);
     default: return hipErrorInvalidValue;
   }
 }

@@ -29,10 +29,14 @@ struct Tuning {
   int chain_old = 0;           // 1: the one-thread-per-state chain kernel at any N
   int chain_par_force = 0;     // m > 0: every m-th sequence of the parallel chain taken as uncertified
   int chain_spec = 1;          // 0: no speculative re-decode (uncertified sequences run serially)
-  int chain_spec_kernel = 0;   // 1: speculation on trellis_cp_f64 instead of the generic CP kernel
+  int chain_spec_kernel = 0;   // speculation: 0 the batched chain kernel after the forward passes (N <= 256),
+                               // else the generic CP kernel; 1 trellis_cp_f64; 2 the generic CP kernel
   int chain_copy_overlap = 1;  // 0: the chain's path copy after the certificate pass
   int chain_cert_fused = 1;    // 0: the chain's certificates by their own pass (cp_cert_f64), not the backtrack
-  int chain_parts = 1;         // 0: the chain's decode in one part (no walk beside the last part's forward)
+  int chain_parts = 1;         // 0: the chain's decode in one part; 1: a large first part, then chain_tail
+                               // parts of one forward round / chain_tail_div; 2: one forward round per part
+  int chain_tail = 2;          // chain_parts = 1: the small parts after the first
+  int chain_tail_div = 2;      // chain_parts = 1: a small part is one forward round / this
   // ---- f64 trellis (kernels/trellis64.hip) ----
   int t64_s = 0;               // sequences per wave 2 / 4 / 6 / 8 (0: by batch)
   int t64_512 = -1;            // NP = 512 batch kernel: -1 auto, 0 never, 1 whenever supported
@@ -52,8 +56,8 @@ struct Tuning {
   int generic_split = 0;       // 1: generic_fwd_split (K threads per state)
   int generic_split_k = 0;     // its K (0: by N)
   int generic_wide = 1;        // 0: never the wide (one launch per step) decode
-  int generic_wide_min = 0;
-  int generic_prio = 0;  // 1: generic_fwd_ms waves at issue priority 3 (the chain sets it beside a forward)    // > 0: the wide decode from this N on
+  int generic_wide_min = 0;    // > 0: the wide decode from this N on
+  int generic_prio = 0;        // 1: generic_fwd_ms waves at issue priority 3 (the chain sets it beside a forward)
   int wide_s = 0;              // wide decode sequences per workgroup 1 / 2 / 4 (0: by batch)
   int ext_wide_min = 0;        // > 0: the constrained terms passes wide from this N on
   int chain_wide = 1;          // 0: never the wide serial chain step

@@ -169,12 +169,16 @@ CV_API void cv_hmm_destroy(cv_hmm* h);
  *   chain_old 0           1: the one-thread-per-state chain kernel at any N
  *   chain_par_force 0     m > 0: every m-th sequence of the parallel chain taken as uncertified
  *   chain_spec 1          0: no speculative re-decode in the parallel chain
- *   chain_spec_kernel 0   1: speculation on trellis_cp_f64 instead of the generic CP kernel
+ *   chain_spec_kernel 0   the parallel chain's speculative re-decodes: 0 the serial chain kernel's
+ *                         layout batched (one sequence per CU) after the forward passes where N <= 256,
+ *                         the generic CP kernel beside them; 1 trellis_cp_f64; 2 the generic CP kernel
  *   chain_copy_overlap 1  0: the parallel chain in one decode chunk, its path copy before the walk
  *   chain_cert_fused 1    0: the chain's certificates by their own pass (cp_cert_f64), not the backtrack
- *   chain_parts 1         0: the parallel chain's decode in one part (1: two parts where N <= 256 and
- *                         the batch spans several forward rounds; the walk over the first part runs
- *                         beside the second part's forward pass)
+ *   chain_parts 1         0: the parallel chain's decode in one part; 1: where N <= 256 and the batch
+ *                         spans more than a forward round, a large first part then chain_tail small
+ *                         parts (each walked beside the next part's forward pass); 2: one round each
+ *   chain_tail 2, chain_tail_div 2       chain_parts = 1: the number of small parts, and a small
+ *                         part's size as a forward round (64 sequences per CU) / chain_tail_div
  *   t64_s 0               f64 trellis sequences per wave 2 / 4 / 6 / 8 (0: by batch)
  *   t64_512 / t64_1024 -1 NP = 512 / 1,024 batch kernel: -1 auto, 0 never, 1 always
  *   t64_wg 1              0: one wave per workgroup instead of eight-wave units

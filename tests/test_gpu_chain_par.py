@@ -321,3 +321,46 @@ def test_chain_cert_fused_vs_pass(gpu, nseq, force):
     sp, sobj = _serial(h, off[:257], obs[:int(off[256])])
     (pp, op), _ = _par(h, off[:257], obs[:int(off[256])])
     assert op == sobj and np.array_equal(pp, sp)
+
+
+@pytest.mark.parametrize("force", [None, 97])
+def test_chain_parts_schedules(gpu, force):
+    """The parallel chain decodes a batch that spans more than a forward round (64 sequences per
+    CU) in parts, each part's walk beside the next part's forward (tuning key chain_parts: 1 =
+    one large part then chain_tail parts of a round / chain_tail_div, 2 = one round per part,
+    0 = one part).  Every schedule returns the serial chain's path and objective; forced runs
+    (every 97th sequence uncertified) put speculative batches and runs on every part boundary."""
+    nseq = 40000  # > 2 rounds on 256 CUs: three parts at the default schedule
+    pi, a, b, off, obs = _case(256, 31, nseq, 4, 40, seed=5100, zeros=(16383, 16384, 32767), ones=(24575, 24576))
+    h = cv.HMM(pi, a, b)
+    sp, sobj = _serial(h, off, obs)
+    for keys in ({}, {"chain_parts": 0}, {"chain_parts": 2}, {"chain_tail": 3, "chain_tail_div": 4}):
+        with h.tuned(**keys):
+            (path, obj), st = _par(h, off, obs, force=force)
+        assert st["parallel"], (keys, st)
+        if force:
+            assert st["speculated"] + st["rerun"] >= nseq // 97 - 1, (keys, st)
+        assert obj == sobj, (keys, obj, sobj)
+        bad = np.nonzero(path != sp)[0]
+        assert bad.size == 0, (keys, bad[:10], st)
+
+
+@pytest.mark.parametrize("n", [3, 64, 100, 128, 150, 192, 256])
+def test_chain_spec_batched_chain_kernel(gpu, n):
+    """Speculative re-decodes after the forward passes run the serial chain kernel's layout
+    batched, one sequence per workgroup (cp_chain_wg BATCH: row 0 at the predicted offset, the
+    path backtracked through LDS-staged psi rows in the same workgroup), at every padded width;
+    tuning key chain_spec_kernel = 2 keeps the generic CP kernel.  Every 2nd / 3rd sequence
+    forced uncertified, ragged lengths with empty and one-element sequences and sequences longer
+    than one psi staging block (> 296 rows at N = 256): both equal the oracle's chain."""
+    pi, a, b, off, obs = _case(n, 21, 36, 1, 700, seed=5200 + n, zeros=(4,), ones=(9, 10))
+    h = cv.HMM(pi, a, b)
+    rp, robj = O.cp_superseq_f64(pi, a, b, off, obs)
+    for force in (2, 3):
+        for kern in (0, 2):
+            with h.tuned(chain_spec_kernel=kern):
+                (path, obj), st = _par(h, off, obs, force=force)
+            assert st["parallel"] and st["speculated"] >= 1, (kern, st)
+            assert obj == robj, (kern, force, obj, robj)
+            bad = np.nonzero(path != rp)[0]
+            assert bad.size == 0, (kern, force, bad[:10], st)
