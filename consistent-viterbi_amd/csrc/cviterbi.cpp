@@ -322,6 +322,7 @@ struct cv_hmm {
   std::vector<hipEvent_t> chunk_ev;
   hipStream_t copy_stream = nullptr;
   PinnedHost chain_pin;  // the chain's scores, statuses and certificates on their way to the host
+  PinnedHost chain_gpin;  // the chain's gathered candidate paths and speculative results (16 MiB)
 
   ~cv_hmm() {
     for (auto e : ev) (void)hipEventDestroy(e);
@@ -1365,6 +1366,7 @@ CV_API cv_status cv_hmm_release_workspaces(cv_hmm* h) {
   h->ws_rec = false;
   h->side.ws_rec = false;
   h->chain_pin.release();
+  h->chain_gpin.release();
   return CV_OK;
 }
 CV_API cv_status cv_hmm_get_tuning(const cv_hmm* h, const char* key, int64_t* value) {
@@ -3261,6 +3263,20 @@ cv_status superseq_cp_par(cv_hmm* h, int64_t nseq, const int64_t* offsets, const
   }
   if (!h->chain_pin.ensure((size_t)nseq * 29)) return set_err(CV_ENOMEM, "pinned chain staging failed");
   unsigned char* pin = h->chain_pin.as<unsigned char>();
+  // the walk's small D2H copies (gathered paths, speculative paths and last rows) through pinned
+  // memory: a pageable copy is staged by the runtime and queued behind the path copy's
+  constexpr size_t kGpin = (size_t)16 << 20;
+  unsigned char* gpin = h->chain_gpin.ensure(kGpin) ? h->chain_gpin.as<unsigned char>() : nullptr;
+  auto d2h_small = [&](void* dst, const void* src, size_t bytes, size_t pin_off) -> hipError_t {
+    if (gpin && pin_off + bytes <= kGpin) {
+      hipError_t e = hipMemcpyAsync(gpin + pin_off, src, bytes, hipMemcpyDeviceToHost, cs);
+      if (e == hipSuccess) e = hipStreamSynchronize(cs);
+      if (e == hipSuccess) std::memcpy(dst, gpin + pin_off, bytes);
+      return e;
+    }
+    hipError_t e = hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, cs);
+    return e == hipSuccess ? hipStreamSynchronize(cs) : e;
+  };
   double pimax = 0.0;
   for (double x : h->pi)
     if (std::isfinite(x)) pimax = std::max(pimax, std::fabs(x));
@@ -3312,6 +3328,13 @@ cv_status superseq_cp_par(cv_hmm* h, int64_t nseq, const int64_t* offsets, const
     std::memcpy(cert.data() + 2 * s0, pin + nseq * 9 + s0 * 16, (size_t)n * 16);
     std::memcpy(ends.data() + s0, pin + nseq * 25 + s0 * 4, (size_t)n * 4);
     trace_mark("chain: part's scores, certificates, end states D2H");
+    for (int64_t k = s0; k < s1; ++k)
+      if (status[(size_t)k] == CV_SEQ_BADOBS) {  // the caller's observations were not scanned on the host
+        const int64_t V = h->V;
+        const int64_t e = first_bad(base, offsets[nseq], [&](int64_t i) { return obs[i] < 0 || obs[i] >= V; });
+        return set_err(CV_EINVAL, "obs[%lld] = %d out of range [0,%lld)", (long long)e, e >= 0 ? obs[e] : 0,
+                       (long long)V);
+      }
     for (int64_t k = s0; k < s1; ++k)
       if (status[(size_t)k] != CV_SEQ_OK && status[(size_t)k] != CV_SEQ_EMPTY) {
         fallback = true;  // the serial chain
@@ -3386,6 +3409,7 @@ cv_status superseq_cp_par(cv_hmm* h, int64_t nseq, const int64_t* offsets, const
       ++xc;
     }
     gathered += (int64_t)gids.size();
+    trace_mark("chain: candidates listed");
     if (!copy_joined && !gids.empty()) {
       const int64_t ng = (int64_t)gids.size();
       if ((st = d_gid.ensure((size_t)ng * 16)) != CV_OK || (st = d_gpath.ensure((size_t)tot * 4)) != CV_OK) return st;
@@ -3395,8 +3419,7 @@ cv_status superseq_cp_par(cv_hmm* h, int64_t nseq, const int64_t* offsets, const
                                                        d_gid.as<int64_t>() + ng, ng, d_gpath.as<int32_t>(), cs);
       if (e != hipSuccess) return set_err(CV_EDEVICE, "chain path gather failed: %s", hipGetErrorString(e));
       gpath.resize((size_t)(gbase + tot));
-      HIP_TRY(hipMemcpyAsync(gpath.data() + gbase, d_gpath.p, (size_t)tot * 4, hipMemcpyDeviceToHost, cs));
-      HIP_TRY(hipStreamSynchronize(cs));
+      HIP_TRY(d2h_small(gpath.data() + gbase, d_gpath.p, (size_t)tot * 4, 0));
     }
     trace_mark("chain: candidate paths gathered");
     return CV_OK;
@@ -3638,6 +3661,7 @@ cv_status superseq_cp_par(cv_hmm* h, int64_t nseq, const int64_t* offsets, const
       G.push_back(Ms);
       Ms = fold_elems(ks[y], Ms);  // predicted: the chain keeps the row-A0 path
     }
+    trace_mark("chain: speculation predicted");
     std::fill(spec_idx.begin(), spec_idx.end(), -1);
     spec_guess.clear();
     if (F.empty()) return CV_OK;
@@ -3657,6 +3681,7 @@ cv_status superseq_cp_par(cv_hmm* h, int64_t nseq, const int64_t* offsets, const
     HIP_TRY(hipMemcpyAsync(d_soff.p, so.data(), so.size() * 8, hipMemcpyHostToDevice, cs));
     HIP_TRY(hipMemcpyAsync(d_sobs.p, sob.data(), sob.size() * 4, hipMemcpyHostToDevice, cs));
     HIP_TRY(hipMemcpyAsync(d_sinit.p, G.data(), (size_t)nf * 8, hipMemcpyHostToDevice, cs));
+    trace_mark("chain: speculative batch packed");
     // N <= 256 after the last forward pass (the chip is free): the serial chain kernel's
     // layout, one sequence per workgroup and CU (A on chip, ~3.5 us per element; tuning key
     // chain_spec_kernel = 0), its path backtracked in the same workgroup
@@ -3694,7 +3719,8 @@ cv_status superseq_cp_par(cv_hmm* h, int64_t nseq, const int64_t* offsets, const
     cvk::TuningOverride one_seq(&cvk::Tuning::generic_s, beside_fwd && h->tuning.generic_s == 0 ? 1 : h->tuning.generic_s);
     // ... and at issue priority 3: a latency-bound walk that takes few issue slots, which the
     // forward's waves (priority 2-3) would otherwise leave it only when they stall
-    cvk::TuningOverride prio(&cvk::Tuning::generic_prio, beside_fwd ? 1 : h->tuning.generic_prio);
+    cvk::TuningOverride prio(&cvk::Tuning::generic_prio,
+                             beside_fwd && h->tuning.chain_spec_prio ? 1 : h->tuning.generic_prio);
     // the side workspace: the main one may still hold the last part's forward pass
     if ((st = decode_device(h, nf, so.data(), d_soff.as<int64_t>(), d_sobs.as<int32_t>(), oc, d_spath.as<int32_t>(), sc,
                             reinterpret_cast<uint8_t*>(sc + nf), cs, nullptr, true, nullptr, d_sinit.as<double>(),
@@ -3703,9 +3729,8 @@ cv_status superseq_cp_par(cv_hmm* h, int64_t nseq, const int64_t* offsets, const
     }
     spec_path.resize((size_t)Ls);
     spec_last.resize((size_t)nf * N);
-    HIP_TRY(hipMemcpyAsync(spec_path.data(), d_spath.p, (size_t)Ls * 4, hipMemcpyDeviceToHost, cs));
-    HIP_TRY(hipMemcpyAsync(spec_last.data(), d_slast.p, (size_t)nf * N * 8, hipMemcpyDeviceToHost, cs));
-    HIP_TRY(hipStreamSynchronize(cs));
+    HIP_TRY(d2h_small(spec_last.data(), d_slast.p, (size_t)nf * N * 8, 0));
+    HIP_TRY(d2h_small(spec_path.data(), d_spath.p, (size_t)Ls * 4, (size_t)nf * N * 8));
     trace_mark("chain: speculative batch (pack, decode, D2H)");
     spec_off = std::move(so);
     spec_guess = std::move(G);
@@ -3837,11 +3862,12 @@ CV_API cv_status cv_decode_superseq_cp(cv_hmm* h, int64_t nseq, const int64_t* o
   if ((st = check_batch(h, nseq, offsets)) != CV_OK) return st;
   const int64_t base = offsets[0], L = offsets[nseq] - base;
   if (L <= 0) return CV_OK;
-  {
+  auto check_obs = [&]() -> cv_status {
     const int64_t V = h->V;
     const int64_t k = first_bad(base, offsets[nseq], [&](int64_t i) { return obs[i] < 0 || obs[i] >= V; });
     if (k >= 0) return set_err(CV_EINVAL, "obs[%lld] = %d out of range [0,%lld)", (long long)k, obs[k], (long long)V);
-  }
+    return CV_OK;
+  };
   // The parallel chain (any N, log-probability models); else serially: N <= 256 the
   // one-workgroup chain with the candidates split over its waves and A on chip
   // (kernels/chain.hip), N > 256 (or CV_CHAIN_OLD=1, an A/B knob, bit-identical) one thread per
@@ -3849,10 +3875,13 @@ CV_API cv_status cv_decode_superseq_cp(cv_hmm* h, int64_t nseq, const int64_t* o
   const bool chain_old = h->tuning.chain_old == 1;
   for (int q = 0; q < 9; ++q) h->last_chain[q] = 0;
   if (!chain_old && h->tuning.chain_par != 0) {
+    // the parallel chain range-checks the observations on the device (its trellis statuses,
+    // CV_SEQ_BADOBS -> CV_EINVAL with the host scan's message), not by a host scan first
     bool applied = false;
     st = superseq_cp_par(h, nseq, offsets, obs, path_out, objective_out, &applied);
     if (st != CV_OK || applied) return st;
   }
+  if ((st = check_obs()) != CV_OK) return st;
   // the serial chain's sequence-start flags (MetaElements t == 0), built only when it runs (the
   // parallel chain never reads them: 33.5 MB zeroed and walked at config-4 size)
   std::vector<uint8_t> first((size_t)L, 0);

@@ -179,6 +179,8 @@ CV_API void cv_hmm_destroy(cv_hmm* h);
  *                         parts (each walked beside the next part's forward pass); 2: one round each
  *   chain_tail 2, chain_tail_div 2       chain_parts = 1: the number of small parts, and a small
  *                         part's size as a forward round (64 sequences per CU) / chain_tail_div
+ *   chain_spec_prio 1     0: the chain's speculative batches beside a forward pass at the default
+ *                         issue priority (1: priority 3)
  *   t64_s 0               f64 trellis sequences per wave 2 / 4 / 6 / 8 (0: by batch)
  *   t64_512 / t64_1024 -1 NP = 512 / 1,024 batch kernel: -1 auto, 0 never, 1 always
  *   t64_wg 1              0: one wave per workgroup instead of eight-wave units

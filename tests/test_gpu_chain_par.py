@@ -364,3 +364,23 @@ def test_chain_spec_batched_chain_kernel(gpu, n):
             assert obj == robj, (kern, force, obj, robj)
             bad = np.nonzero(path != rp)[0]
             assert bad.size == 0, (kern, force, bad[:10], st)
+
+
+@pytest.mark.parametrize("n,nseq", [(64, 50), (256, 40000)])
+def test_chain_bad_obs_rejected(gpu, n, nseq):
+    """An observation outside [0, V) fails the call with CV_EINVAL naming the first bad element,
+    on the parallel chain (range-checked by the trellis on the device: CV_SEQ_BADOBS, no host
+    scan first; at 40,000 sequences the bad element sits in a later part) and on the serial chain
+    (host scan), like the reference's index panic (hmm.rs:224)."""
+    pi, a, b, off, obs = _case(n, 13, nseq, 2, 30, seed=5300 + n)
+    h = cv.HMM(pi, a, b)
+    for k in (nseq - 3, nseq // 2):
+        bad = obs.copy()
+        e = int(off[k]) + 1
+        bad[e] = 13
+        for par in (1, 0):
+            with h.tuned(chain_par=par):
+                with pytest.raises(cv.CVError, match=rf"obs\[{e}\] = 13 out of range"):
+                    cv.decode_superseq_cp(h, off, bad)
+    (path, obj), st = _par(h, off, obs)  # the handle still decodes
+    assert st["parallel"]
