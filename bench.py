@@ -248,7 +248,7 @@ def bench_superseq_cp(dev):
     h = cv.HMM(c["pi"], c["a"], c["b"].reshape(N_STATES, 32, 32), device=dev.index)
     cv.decode_superseq_cp(h, c["offsets"][:3], c["obs"][:2 * T_LEN])  # tables
     times = []
-    for _ in range(2):
+    for _ in range(3):  # the first full-size call also sizes the handle's chain buffers
         t0 = time.perf_counter()
         _, obj = cv.decode_superseq_cp(h, c["offsets"], c["obs"])
         times.append(time.perf_counter() - t0)

@@ -323,8 +323,15 @@ struct cv_hmm {
   hipStream_t copy_stream = nullptr;
   PinnedHost chain_pin;  // the chain's scores, statuses and certificates on their way to the host
   PinnedHost chain_gpin;  // the chain's gathered candidate paths and speculative results (16 MiB)
+  // the chain's later parts' observations and its path copy's two-chunk ring, staged through
+  // pinned memory: the DMA engines move them, where a pageable copy runs blit kernels beside
+  // the forward passes (tuning keys chain_pin_obs / chain_pin_path)
+  PinnedHost chain_obs_pin, chain_ring[2];
+  hipEvent_t ring_ev[2] = {nullptr, nullptr};
 
   ~cv_hmm() {
+    for (auto e : ring_ev)
+      if (e) (void)hipEventDestroy(e);
     for (auto e : ev) (void)hipEventDestroy(e);
     for (auto e : side.ev) (void)hipEventDestroy(e);
     if (side.start) (void)hipEventDestroy(side.start);
@@ -1367,6 +1374,9 @@ CV_API cv_status cv_hmm_release_workspaces(cv_hmm* h) {
   h->side.ws_rec = false;
   h->chain_pin.release();
   h->chain_gpin.release();
+  h->chain_obs_pin.release();
+  h->chain_ring[0].release();
+  h->chain_ring[1].release();
   return CV_OK;
 }
 CV_API cv_status cv_hmm_get_tuning(const cv_hmm* h, const char* key, int64_t* value) {
@@ -3174,12 +3184,25 @@ cv_status superseq_cp_par(cv_hmm* h, int64_t nseq, const int64_t* offsets, const
   }
   if (!h->copy_stream) HIP_TRY(hipStreamCreateWithFlags(&h->copy_stream, hipStreamNonBlocking));
   HIP_TRY(hipMemcpyAsync(d_off.p, off.data(), off.size() * 8, hipMemcpyHostToDevice, stream));
+  // the later parts' observations through pinned memory (host threads fill it while the first
+  // part's forward runs; a pageable copy would run the runtime's blit kernels beside it)
+  const int64_t eo = off[(size_t)pb[std::min(1, nparts)]];
+  int32_t* obs_pin = nullptr;
+  if (nparts > 1 && h->tuning.chain_pin_obs != 0 && h->chain_obs_pin.ensure((size_t)(L - eo) * 4))
+    obs_pin = h->chain_obs_pin.as<int32_t>();
   std::vector<std::pair<int64_t, int64_t>> dchunks;
   for (int p = 0; p < nparts; ++p) {
     const int64_t s0 = pb[p], s1 = pb[p + 1], e0 = off[(size_t)s0], e1 = off[(size_t)s1];
     // the second part's observations cross on the copy stream while the first part's forward runs
     hipStream_t hs = p == 0 ? stream : h->copy_stream;
-    HIP_TRY(hipMemcpyAsync(d_obs.as<int32_t>() + e0, obs + base + e0, (size_t)(e1 - e0) * 4, hipMemcpyHostToDevice, hs));
+    if (p > 0 && obs_pin) {
+      int32_t* dst = obs_pin + (e0 - eo);
+      const int32_t* src = obs + base + e0;
+      parallel_ranges(e1 - e0, [&](int, int64_t a, int64_t b) { std::memcpy(dst + a, src + a, (size_t)(b - a) * 4); });
+      HIP_TRY(hipMemcpyAsync(d_obs.as<int32_t>() + e0, dst, (size_t)(e1 - e0) * 4, hipMemcpyHostToDevice, hs));
+    } else {
+      HIP_TRY(hipMemcpyAsync(d_obs.as<int32_t>() + e0, obs + base + e0, (size_t)(e1 - e0) * 4, hipMemcpyHostToDevice, hs));
+    }
     if (p > 0) {
       HIP_TRY(hipEventRecord(obs_in[(size_t)p], hs));
       HIP_TRY(hipStreamWaitEvent(stream, obs_in[(size_t)p], 0));
@@ -3217,17 +3240,61 @@ cv_status superseq_cp_par(cv_hmm* h, int64_t nseq, const int64_t* offsets, const
     hipStream_t cps = h->copy_stream;
     std::vector<hipEvent_t> evs(h->chunk_ev.begin(), h->chunk_ev.begin() + (ptrdiff_t)dchunks.size());
     int32_t* dp = d_path.as<int32_t>();
-    auto run_copies = [&copy, dev, cps, evs, dchunks, off, path_out, dp]() {
+    // pinned two-chunk ring (tuning key chain_pin_path): chunk j's DMA into ring[j % 2] while the
+    // thread moves chunk j - 1 into the caller's buffer
+    static constexpr int64_t kRing = (int64_t)4 << 20;  // elements per ring chunk (16 MiB)
+    int32_t* ring[2] = {nullptr, nullptr};
+    if (h->tuning.chain_pin_path != 0 && h->chain_ring[0].ensure((size_t)kRing * 4) &&
+        h->chain_ring[1].ensure((size_t)kRing * 4)) {
+      for (int b = 0; b < 2; ++b)
+        if (!h->ring_ev[b] && hipEventCreateWithFlags(&h->ring_ev[b], hipEventDisableTiming) != hipSuccess) {
+          (void)hipGetLastError();
+          h->ring_ev[b] = nullptr;
+        }
+      if (h->ring_ev[0] && h->ring_ev[1]) {
+        ring[0] = h->chain_ring[0].as<int32_t>();
+        ring[1] = h->chain_ring[1].as<int32_t>();
+      }
+    }
+    hipEvent_t rev[2] = {h->ring_ev[0], h->ring_ev[1]};
+    auto run_copies = [&copy, dev, cps, evs, dchunks, off, path_out, dp, ring, rev]() {
       if ((copy.err = hipSetDevice(dev)) != hipSuccess) return;
+      if (!ring[0]) {
+        for (size_t i = 0; i < dchunks.size(); ++i) {
+          const int64_t e0 = off[(size_t)dchunks[i].first], e1 = off[(size_t)dchunks[i].second];
+          if ((copy.err = hipStreamWaitEvent(cps, evs[i], 0)) != hipSuccess) return;
+          if (e1 > e0 &&
+              (copy.err = hipMemcpyAsync(path_out + e0, dp + e0, (size_t)(e1 - e0) * 4, hipMemcpyDeviceToHost, cps)) !=
+                  hipSuccess)
+            return;
+        }
+        copy.err = hipStreamSynchronize(cps);
+        return;
+      }
+      int64_t pend[2][2] = {{0, 0}, {0, 0}};  // [buffer] = {first element, count} in flight
+      int j = 0;
+      auto drain = [&](int b) -> bool {
+        if (pend[b][1] == 0) return true;
+        if ((copy.err = hipEventSynchronize(rev[b])) != hipSuccess) return false;
+        std::memcpy(path_out + pend[b][0], ring[b], (size_t)pend[b][1] * 4);
+        pend[b][1] = 0;
+        return true;
+      };
       for (size_t i = 0; i < dchunks.size(); ++i) {
         const int64_t e0 = off[(size_t)dchunks[i].first], e1 = off[(size_t)dchunks[i].second];
         if ((copy.err = hipStreamWaitEvent(cps, evs[i], 0)) != hipSuccess) return;
-        if (e1 > e0 &&
-            (copy.err = hipMemcpyAsync(path_out + e0, dp + e0, (size_t)(e1 - e0) * 4, hipMemcpyDeviceToHost, cps)) !=
-                hipSuccess)
-          return;
+        for (int64_t a = e0; a < e1; a += kRing, ++j) {
+          const int b = j & 1;
+          const int64_t n = std::min(kRing, e1 - a);
+          if (!drain(b)) return;
+          if ((copy.err = hipMemcpyAsync(ring[b], dp + a, (size_t)n * 4, hipMemcpyDeviceToHost, cps)) != hipSuccess ||
+              (copy.err = hipEventRecord(rev[b], cps)) != hipSuccess)
+            return;
+          pend[b][0] = a;
+          pend[b][1] = n;
+        }
       }
-      copy.err = hipStreamSynchronize(cps);
+      if (drain(j & 1)) drain((j + 1) & 1);
     };
     if (overlap_copy)
       copy.t = std::thread(run_copies);

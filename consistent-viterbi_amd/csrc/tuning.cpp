@@ -21,7 +21,7 @@ const Key kKeys[] = {
     CVK_KEY(max_chunks), CVK_KEY(host_sums), CVK_KEY(no_trace), CVK_KEY(no_resume),
     CVK_KEY(no_side), CVK_KEY(chain_par), CVK_KEY(chain_old), CVK_KEY(chain_par_force),
     CVK_KEY(chain_spec), CVK_KEY(chain_spec_kernel), CVK_KEY(chain_copy_overlap), CVK_KEY(chain_cert_fused),
-    CVK_KEY(chain_parts), CVK_KEY(chain_tail), CVK_KEY(chain_tail_div), CVK_KEY(chain_spec_prio), CVK_KEY(t64_s),
+    CVK_KEY(chain_parts), CVK_KEY(chain_tail), CVK_KEY(chain_tail_div), CVK_KEY(chain_spec_prio), CVK_KEY(chain_pin_obs), CVK_KEY(chain_pin_path), CVK_KEY(t64_s),
     CVK_KEY(t64_512), CVK_KEY(t64_1024), CVK_KEY(t64_wg), CVK_KEY(t64_wg_force),
     CVK_KEY(t64_rs), CVK_KEY(t64_w2), CVK_KEY(t64_wave), CVK_KEY(t64_bal),
     CVK_KEY(t64_cp_s), CVK_KEY(t64_cp_w), CVK_KEY(t64_cp_pf), CVK_KEY(t64_bt_pf),

@@ -328,13 +328,16 @@ def test_chain_parts_schedules(gpu, force):
     """The parallel chain decodes a batch that spans more than a forward round (64 sequences per
     CU) in parts, each part's walk beside the next part's forward (tuning key chain_parts: 1 =
     one large part then chain_tail parts of a round / chain_tail_div, 2 = one round per part,
-    0 = one part).  Every schedule returns the serial chain's path and objective; forced runs
-    (every 97th sequence uncertified) put speculative batches and runs on every part boundary."""
+    0 = one part), with the later parts' observations and the path copy through pinned staging or
+    pageable copies (chain_pin_obs / chain_pin_path).  Every schedule returns the serial chain's
+    path and objective; forced runs (every 97th sequence uncertified) put speculative batches and
+    runs on every part boundary."""
     nseq = 40000  # > 2 rounds on 256 CUs: three parts at the default schedule
     pi, a, b, off, obs = _case(256, 31, nseq, 4, 40, seed=5100, zeros=(16383, 16384, 32767), ones=(24575, 24576))
     h = cv.HMM(pi, a, b)
     sp, sobj = _serial(h, off, obs)
-    for keys in ({}, {"chain_parts": 0}, {"chain_parts": 2}, {"chain_tail": 3, "chain_tail_div": 4}):
+    for keys in ({}, {"chain_parts": 0}, {"chain_parts": 2}, {"chain_tail": 3, "chain_tail_div": 4},
+                 {"chain_pin_obs": 0, "chain_pin_path": 0}):
         with h.tuned(**keys):
             (path, obj), st = _par(h, off, obs, force=force)
         assert st["parallel"], (keys, st)
@@ -384,3 +387,29 @@ def test_chain_bad_obs_rejected(gpu, n, nseq):
                     cv.decode_superseq_cp(h, off, bad)
     (path, obj), st = _par(h, off, obs)  # the handle still decodes
     assert st["parallel"]
+
+
+def test_chain_config4_size(gpu):
+    """The config-4-sized chain (65,536 x 512 = 33.5 M elements, N = 256: what main.rs:120 runs
+    on BASELINE config 4's data) on the default schedule (parts, pinned copies through a ring of
+    16 MiB chunks, speculation beside the forward passes and after them) equals the most
+    conservative parallel schedule (one part, pageable copies, the generic speculation kernel,
+    the separate certificate pass) bit for bit, and its first 2,048 sequences equal the serial
+    chain's (the prefix's last element aside: the prefix ends its own chain there).
+    CV_TEST_FULL_SERIAL=1 also runs the serial chain over the whole input (~2 minutes)."""
+    c = synth.config("c4")
+    off, obs = c["offsets"], c["obs"]
+    h = cv.HMM(c["pi"], c["a"], c["b"])
+    (p1, o1), s1 = _par(h, off, obs)
+    assert s1["parallel"] and s1["certified"] > 60000, s1
+    with h.tuned(chain_parts=0, chain_pin_obs=0, chain_pin_path=0, chain_spec_kernel=2, chain_cert_fused=0):
+        (p0, o0), s0 = _par(h, off, obs)
+    assert o1 == o0, (o1, o0)
+    bad = np.nonzero(p1 != p0)[0]
+    assert bad.size == 0, (bad[:10], s1, s0)
+    k = 2048
+    sp, _ = _serial(h, off[:k + 1], obs[:int(off[k])])
+    assert np.array_equal(p1[:int(off[k]) - 1], sp[:-1])
+    if os.environ.get("CV_TEST_FULL_SERIAL") == "1":
+        fp, fo = _serial(h, off, obs)
+        assert fo == o1 and np.array_equal(fp, p1)
