@@ -1238,18 +1238,25 @@ __device__ __forceinline__ void bt_chain_f64(const uint32_t* __restrict__ rows, 
         }
         bool exact = cnt != 1;
         if constexpr (CERT) {
-          if (!exact) {  // the gap's lower bound from the estimates (x_path = M: the unique survivor)
-            float lo = -__builtin_inff();
+          if (!exact) {
+            // the gap's lower bound from the estimates (x_path = M: the unique survivor), O = the
+            // best other estimate: lb = M (1 + 3 2^-21) - O (1 - 3 2^-21) - |M| 2^-50 - 2^-99, and
+            // the step's term r = (lb - (4t + 1) u0) / (3t + 1) reaches rho_cap iff
+            // O <= theta = (M (1 + 3 2^-21) - |M| 2^-50 - 2^-99 - rho_cap (3t + 1) - (4t + 1) u0)
+            //              / (1 - 3 2^-21)
+            // (theta <= 0: times 1 + 2^-19 > 1 / (1 - 3 2^-21), less |theta| 2^-48 for its own
+            // roundings, only makes the test stricter).  So one ballot per candidate block
+            // replaces the wave maximum of O; a step that reaches the cap leaves rho alone (the
+            // returned rho is then >= rho_cap, which is all the host's tests need), one below
+            // takes the exact gap
+            const double Md = (double)M;
+            const double need = rho_cap * (double)(3 * t + 1) + (double)(4 * t + 1) * u0;
+            double th = (Md * (1.0 + 0x3p-21) - __builtin_fabs(Md) * 0x1p-50 - 0x1p-99 - need) * (1.0 + 0x1p-19);
+            th -= __builtin_fabs(th) * 0x1p-48;
+            bool over = false;
 #pragma unroll
-            for (int k = 0; k < KP; ++k) lo = __builtin_fmaxf(lo, (64 * k + lane == idx) ? -__builtin_inff() : x[k]);
-            const double O = (double)wave_max_f32(lo), Md = (double)M;
-            const double lb = Md * (1.0 + 0x3p-21) - O * (1.0 - 0x3p-21) - __builtin_fabs(Md) * 0x1p-50 - 0x1p-99;
-            const double r = (lb - (double)(4 * t + 1) * u0) / (double)(3 * t + 1);
-            if (r >= rho_cap) {
-              rho = fmin(rho, r);
-            } else {
-              exact = true;
-            }
+            for (int k = 0; k < KP; ++k) over |= __ballot((double)x[k] > th && 64 * k + lane != idx) != 0;
+            exact = over;
           }
         }
         if (!exact) {
