@@ -3306,6 +3306,7 @@ cv_status superseq_cp_par(cv_hmm* h, int64_t nseq, const int64_t* offsets, const
   // every buffer the walk may need, sized now: growing one later would free the old one, a
   // device-wide synchronisation that would wait for the second part's forward pass
   constexpr int64_t kSpecMax = 16384;  // sequences per speculative batch
+  constexpr int64_t kSpecBeside = 2048;  // ... beside a forward pass (cp_spec_psi's psi rows, sized up front)
   DevBuf &d_ends = h->chainb.ends, &d_ebin = h->chainb.ebin, &d_q = h->chainb.q, &d_gid = h->chainb.gid,
          &d_gpath = h->chainb.gpath;
   if ((st = d_ends.ensure((size_t)nseq * 4)) != CV_OK) return st;
@@ -3327,6 +3328,11 @@ cv_status superseq_cp_par(cv_hmm* h, int64_t nseq, const int64_t* offsets, const
     if ((st = d_slast.ensure((size_t)nspec * N * 8)) != CV_OK) return st;
     if ((st = d_rpsi.ensure((size_t)std::max<int64_t>(4 * maxT, 1) * W * 2)) != CV_OK) return st;
     if ((st = d_rpath.ensure((size_t)std::max<int64_t>(4 * maxT, 1) * 4)) != CV_OK) return st;
+    // psi rows of the speculative batches beside a forward (cp_spec_psi): up to kSpecBeside
+    // sequences' worth (a batch beside a forward stops there)
+    if (small && (st = h->chainb.spsi.ensure((size_t)std::min<int64_t>(L, kSpecBeside * std::max<int64_t>(maxT, 1)) * W *
+                                             2)) != CV_OK)
+      return st;
   }
   if (!h->chain_pin.ensure((size_t)nseq * 29)) return set_err(CV_ENOMEM, "pinned chain staging failed");
   unsigned char* pin = h->chain_pin.as<unsigned char>();
@@ -3709,6 +3715,10 @@ cv_status superseq_cp_par(cv_hmm* h, int64_t nseq, const int64_t* offsets, const
     std::vector<double> G;
     double Ms = M;
     Kind pk = prev;
+    // beside a forward, on cp_spec_psi: as many sequences as its psi rows hold
+    const bool spec_psi = small && beside_fwd && h->tuning.chain_spec_kernel == 0;
+    const int64_t psi_rows = spec_psi ? (int64_t)(h->chainb.spsi.bytes / ((size_t)W * 2)) : INT64_MAX;
+    int64_t rows_used = 0;
     for (size_t y = x0; y < x_lim && (int64_t)F.size() < kSpecMax; ++y) {
       double Mn;
       bool qd;
@@ -3724,6 +3734,9 @@ cv_status superseq_cp_par(cv_hmm* h, int64_t nseq, const int64_t* offsets, const
         continue;
       }
       if (y == x0 && pk == ROW && !row_clean(row_host.data(), row_arg, Ms, score_of(y) + pimax + 16.0)) break;
+      const int64_t Ty = off[(size_t)ks[y] + 1] - off[(size_t)ks[y]];
+      if (rows_used + Ty > psi_rows) break;
+      rows_used += Ty;
       F.push_back(ks[y]);
       G.push_back(Ms);
       Ms = fold_elems(ks[y], Ms);  // predicted: the chain keeps the row-A0 path
@@ -3752,7 +3765,25 @@ cv_status superseq_cp_par(cv_hmm* h, int64_t nseq, const int64_t* offsets, const
     // N <= 256 after the last forward pass (the chip is free): the serial chain kernel's
     // layout, one sequence per workgroup and CU (A on chip, ~3.5 us per element; tuning key
     // chain_spec_kernel = 0), its path backtracked in the same workgroup
-    if (small && !beside_fwd && h->tuning.chain_spec_kernel == 0) {
+    if (spec_psi) {
+      // beside a forward pass: cp_spec_psi (4 VALU per candidate, A by buffer loads, ~20 KiB of
+      // LDS), its psi rows sized up front (no reallocation -- a device-wide synchronisation --
+      // while the forward runs)
+      cvk::CpSpecArgs g{};
+      g.pi = h->q_pi.as<double>();
+      g.a = h->q_a.as<double>();
+      g.et = h->q_et.as<double>();
+      g.obs = d_sobs.as<int32_t>();
+      g.soff = d_soff.as<int64_t>();
+      g.sinit = d_sinit.as<double>();
+      g.nstates = N;
+      g.prio = h->tuning.chain_spec_prio != 0 ? 1 : 0;
+      g.psi = h->chainb.spsi.as<uint16_t>();
+      g.last = d_slast.as<double>();
+      g.path = d_spath.as<int32_t>();
+      const hipError_t e = cvk::launch_cp_spec_psi(W, g, nf, cs);
+      if (e != hipSuccess) return set_err(CV_EDEVICE, "chain speculative batch failed: %s", hipGetErrorString(e));
+    } else if (small && !beside_fwd && h->tuning.chain_spec_kernel == 0) {
       DevBuf& d_spsi = h->chainb.spsi;
       if ((st = d_spsi.ensure((size_t)Ls * W * 2)) != CV_OK) return st;
       cvk::CpChainWgArgs g{};

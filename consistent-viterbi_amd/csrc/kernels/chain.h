@@ -40,6 +40,27 @@ hipError_t launch_cp_chain_wg(int np, const CpChainWgArgs& g, hipStream_t stream
 // nseq such sequences at once, one workgroup (one CU) each: A on chip, ~3.5 us per element at
 // N = 256, against ~17 us for the one-thread-per-state kernels that stream A from L2
 hipError_t launch_cp_chain_wg_batch(int np, const CpChainWgArgs& g, int64_t nseq, hipStream_t stream);
+
+// The parallel chain's speculative re-decodes BESIDE a forward pass (N <= 256): one sequence per
+// workgroup, thread j = state j, A through buffer loads with a scalar row offset, the candidate
+// walk at 4 VALU per candidate (add, compare, max, index select), row 0 = sinit + (pi + b) like
+// the batched kernel; psi [soff[i] + t][np], the last row to last[i nstates ..], the path (first
+// argmax of the last row, then psi through LDS-staged rows) to path + soff[i].  ~20 KiB of LDS
+// and few VGPRs: it fits beside two forward waves per SIMD.
+struct CpSpecArgs {
+  const double* pi;    // [np] -inf padded
+  const double* a;     // [np][np] from-major, -inf padded
+  const double* et;    // [V][np] -inf padded
+  const int32_t* obs;  // packed batch observations
+  const int64_t* soff;
+  const double* sinit;
+  int nstates;
+  int prio;            // 1: issue priority 3
+  uint16_t* psi;
+  double* last;
+  int32_t* path;
+};
+hipError_t launch_cp_spec_psi(int np, const CpSpecArgs& g, int64_t nseq, hipStream_t stream);
 // LDS bytes launch_cp_chain_wg asks for at this np (0: unsupported)
 size_t cp_chain_wg_lds(int np);
 

@@ -550,6 +550,86 @@ hipError_t launch_cp_chain_wg_batch(int np, const CpChainWgArgs& g, int64_t nseq
   }
 }
 
+template <int NP>
+__global__ __launch_bounds__(NP) void cp_spec_psi(CpSpecArgs g) {
+  constexpr int kRows = 32;  // psi rows per LDS staging block of the path walk
+  __shared__ __attribute__((aligned(16))) double dl[2][NP];
+  __shared__ __attribute__((aligned(16))) uint16_t ps[kRows * NP];
+  const int j = threadIdx.x;
+  const int64_t b = blockIdx.x;
+  const int64_t e0 = g.soff[b], T = g.soff[b + 1] - e0;
+  if (T <= 0) return;  // uniform over the workgroup
+  if (g.prio) __builtin_amdgcn_s_setprio(3);
+  const int32_t* obs = g.obs + e0;
+  uint16_t* psi = g.psi + e0 * NP;
+  const __amdgpu_buffer_rsrc_t ra =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(g.a), 0, NP * NP * 8, 0x00020000);
+  auto aload = [&](int i) {  // a[i][j]: the row offset in a scalar register, no per-lane address math
+    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(ra, (uint32_t)j * 8u, (uint32_t)i * NP * 8u, 0));
+  };
+  dl[0][j] = g.sinit[b] + (g.pi[j] + g.et[(size_t)obs[0] * NP + j]);  // utils.rs:32-35 after a clean boundary
+  __syncthreads();
+  for (int64_t t = 1; t < T; ++t) {
+    const double* dp = dl[(t - 1) & 1];
+    const double e = g.et[(size_t)obs[t] * NP + j];
+    double best = dp[0] + aload(0);
+    int arg = 0;
+#pragma unroll 8
+    for (int i = 1; i < NP; ++i) {
+      const double x = dp[i] + aload(i);
+      arg = x > best ? i : arg;  // strict: the first argmax (cp.rs:70-79)
+      best = __builtin_fmax(best, x);
+    }
+    const double v = dp[arg] + (aload(arg) + e);  // cp.rs:75-77
+    psi[t * NP + j] = (uint16_t)arg;
+    dl[t & 1][j] = v;
+    __syncthreads();
+  }
+  const double* lr = dl[(T - 1) & 1];
+  if (j < g.nstates) g.last[b * g.nstates + j] = lr[j];
+  int32_t* path = g.path + e0;
+  int cs = 0;
+  if (j == 0) {  // cp.rs:86
+    double m = lr[0];
+    for (int i = 1; i < g.nstates; ++i)
+      if (lr[i] > m) {
+        m = lr[i];
+        cs = i;
+      }
+    path[T - 1] = cs;
+  }
+  __threadfence();  // this workgroup's psi stores, read back below
+  __syncthreads();
+  for (int64_t hi = T; hi > 1;) {  // rows [lo, hi) hold psi for elements lo .. hi - 1
+    const int64_t lo = hi - 1 > kRows ? hi - kRows : 1;
+    const uint4* src = reinterpret_cast<const uint4*>(psi + lo * NP);
+    uint4* dst = reinterpret_cast<uint4*>(ps);
+    for (int64_t q = j; q < (hi - lo) * NP / 8; q += NP) dst[q] = src[q];
+    __syncthreads();
+    if (j == 0)
+      for (int64_t t = hi - 1; t >= lo; --t) {
+        cs = ps[(t - lo) * NP + cs];
+        path[t - 1] = cs;
+      }
+    __syncthreads();
+    hi = lo;
+  }
+}
+
+hipError_t launch_cp_spec_psi(int np, const CpSpecArgs& g, int64_t nseq, hipStream_t stream) {
+  if (nseq <= 0) return hipSuccess;
+  if (nseq > 0x7fffffff) return hipErrorInvalidValue;
+  const dim3 grid((unsigned)nseq);
+  switch (np) {
+    case 64: hipLaunchKernelGGL(cp_spec_psi<64>, grid, dim3(64), 0, stream, g); break;
+    case 128: hipLaunchKernelGGL(cp_spec_psi<128>, grid, dim3(128), 0, stream, g); break;
+    case 192: hipLaunchKernelGGL(cp_spec_psi<192>, grid, dim3(192), 0, stream, g); break;
+    case 256: hipLaunchKernelGGL(cp_spec_psi<256>, grid, dim3(256), 0, stream, g); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
 hipError_t launch_cp_chain_seg_map(const CpChainBtArgs& g, hipStream_t stream) {
   if (g.nseg <= 1) return hipSuccess;
   const dim3 grid((unsigned)(g.nseg - 1));

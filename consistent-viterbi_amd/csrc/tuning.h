@@ -29,8 +29,9 @@ struct Tuning {
   int chain_old = 0;           // 1: the one-thread-per-state chain kernel at any N
   int chain_par_force = 0;     // m > 0: every m-th sequence of the parallel chain taken as uncertified
   int chain_spec = 1;          // 0: no speculative re-decode (uncertified sequences run serially)
-  int chain_spec_kernel = 0;   // speculation: 0 the batched chain kernel after the forward passes (N <= 256),
-                               // else the generic CP kernel; 1 trellis_cp_f64; 2 the generic CP kernel
+  int chain_spec_kernel = 0;   // speculation (N <= 256): 0 cp_spec_psi beside a forward pass, the batched
+                               // chain kernel after the forward passes; 1 trellis_cp_f64; 2 the generic
+                               // CP kernel (N > 256: always the generic kernel)
   int chain_copy_overlap = 1;  // 0: the chain's path copy after the certificate pass
   int chain_cert_fused = 1;    // 0: the chain's certificates by their own pass (cp_cert_f64), not the backtrack
   int chain_parts = 1;         // 0: the chain's decode in one part; 1: a large first part, then chain_tail

@@ -169,9 +169,10 @@ CV_API void cv_hmm_destroy(cv_hmm* h);
  *   chain_old 0           1: the one-thread-per-state chain kernel at any N
  *   chain_par_force 0     m > 0: every m-th sequence of the parallel chain taken as uncertified
  *   chain_spec 1          0: no speculative re-decode in the parallel chain
- *   chain_spec_kernel 0   the parallel chain's speculative re-decodes: 0 the serial chain kernel's
- *                         layout batched (one sequence per CU) after the forward passes where N <= 256,
- *                         the generic CP kernel beside them; 1 trellis_cp_f64; 2 the generic CP kernel
+ *   chain_spec_kernel 0   the parallel chain's speculative re-decodes where N <= 256: 0 the serial chain
+ *                         kernel's layout batched (one sequence per CU) after the forward passes and
+ *                         cp_spec_psi (one sequence per workgroup, ~20 KiB of LDS) beside them;
+ *                         1 trellis_cp_f64; 2 the generic CP kernel (always so above N = 256)
  *   chain_copy_overlap 1  0: the parallel chain in one decode chunk, its path copy before the walk
  *   chain_cert_fused 1    0: the chain's certificates by their own pass (cp_cert_f64), not the backtrack
  *   chain_parts 1         0: the parallel chain's decode in one part; 1: where N <= 256 and the batch

@@ -323,17 +323,18 @@ def test_chain_cert_fused_vs_pass(gpu, nseq, force):
     assert op == sobj and np.array_equal(pp, sp)
 
 
-@pytest.mark.parametrize("force", [None, 97])
-def test_chain_parts_schedules(gpu, force):
+@pytest.mark.parametrize("n,force", [(256, None), (256, 97), (100, 53)])
+def test_chain_parts_schedules(gpu, n, force):
     """The parallel chain decodes a batch that spans more than a forward round (64 sequences per
     CU) in parts, each part's walk beside the next part's forward (tuning key chain_parts: 1 =
     one large part then chain_tail parts of a round / chain_tail_div, 2 = one round per part,
     0 = one part), with the later parts' observations and the path copy through pinned staging or
     pageable copies (chain_pin_obs / chain_pin_path).  Every schedule returns the serial chain's
     path and objective; forced runs (every 97th sequence uncertified) put speculative batches and
-    runs on every part boundary."""
+    runs on every part boundary; beside a forward the speculation runs cp_spec_psi (NP = 256 and
+    128 here)."""
     nseq = 40000  # > 2 rounds on 256 CUs: three parts at the default schedule
-    pi, a, b, off, obs = _case(256, 31, nseq, 4, 40, seed=5100, zeros=(16383, 16384, 32767), ones=(24575, 24576))
+    pi, a, b, off, obs = _case(n, 31, nseq, 4, 40, seed=5100 + n, zeros=(16383, 16384, 32767), ones=(24575, 24576))
     h = cv.HMM(pi, a, b)
     sp, sobj = _serial(h, off, obs)
     for keys in ({}, {"chain_parts": 0}, {"chain_parts": 2}, {"chain_tail": 3, "chain_tail_div": 4},
