@@ -550,6 +550,10 @@ hipError_t launch_cp_chain_wg_batch(int np, const CpChainWgArgs& g, int64_t nseq
   }
 }
 
+// A loads in flight per thread (16: 78 VGPRs, measured no faster beside the forward)
+#ifndef CVK_SPEC_UNROLL
+#define CVK_SPEC_UNROLL 8
+#endif
 template <int NP>
 __global__ __launch_bounds__(NP) void cp_spec_psi(CpSpecArgs g) {
   constexpr int kRows = 32;  // psi rows per LDS staging block of the path walk
@@ -574,7 +578,7 @@ __global__ __launch_bounds__(NP) void cp_spec_psi(CpSpecArgs g) {
     const double e = g.et[(size_t)obs[t] * NP + j];
     double best = dp[0] + aload(0);
     int arg = 0;
-#pragma unroll 8
+#pragma unroll CVK_SPEC_UNROLL
     for (int i = 1; i < NP; ++i) {
       const double x = dp[i] + aload(i);
       arg = x > best ? i : arg;  // strict: the first argmax (cp.rs:70-79)

@@ -13,6 +13,6 @@ IFS=';' read -ra VS <<< "${VARIANTS:-;CV_CHAIN_PIN_OBS=0,CV_CHAIN_PIN_PATH=0;CV_
 for rep in 1 2; do
   for v in "${VS[@]}"; do
     echo "== ${v:-default}"
-    env ${v//,/ } timeout -k 10 200 python3 -u tools/bench_chain.py 65536 256 2>&1 | grep "65536 seqs" | cut -c1-110 || exit 1
+    env ${v//,/ } timeout -k 10 200 python3 -u tools/chain_reps.py 2>&1 | grep "chain ms" || exit 1
   done
 done
