@@ -1844,7 +1844,10 @@ __global__ __launch_bounds__(256) void trellis_wave_f64(T64FwdArgs g) {
 // rounds puts one workgroup of each quarter of the longest-first order on every CU; the odd
 // quarters run reversed (the block of rank r takes slots of rank 255 - r there), so every CU
 // and SIMD gets long with short sequences: equal sums instead of the longest of each quarter.
-template <bool ZI, int PD = 4>
+#ifndef CVK_W48_PD
+#define CVK_W48_PD 4  // emission rows prefetched this many steps ahead (A/B builds: -DCVK_W48_PD=n)
+#endif
+template <bool ZI, int PD = CVK_W48_PD>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void trellis_wave48_f64(T64FwdArgs g) {
   constexpr int NPW = 64, C = 3, R = 12, LS = NPW + 4, P = 256;
   __shared__ __attribute__((aligned(16))) double dl_all[4][2][LS];     // delta_{t-1} / delta_t per wave
