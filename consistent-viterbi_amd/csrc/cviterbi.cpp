@@ -3762,9 +3762,6 @@ cv_status superseq_cp_par(cv_hmm* h, int64_t nseq, const int64_t* offsets, const
     HIP_TRY(hipMemcpyAsync(d_sobs.p, sob.data(), sob.size() * 4, hipMemcpyHostToDevice, cs));
     HIP_TRY(hipMemcpyAsync(d_sinit.p, G.data(), (size_t)nf * 8, hipMemcpyHostToDevice, cs));
     trace_mark("chain: speculative batch packed");
-    // N <= 256 after the last forward pass (the chip is free): the serial chain kernel's
-    // layout, one sequence per workgroup and CU (A on chip, ~3.5 us per element; tuning key
-    // chain_spec_kernel = 0), its path backtracked in the same workgroup
     if (spec_psi) {
       // beside a forward pass: cp_spec_psi (4 VALU per candidate, A by buffer loads, ~20 KiB of
       // LDS), its psi rows sized up front (no reallocation -- a device-wide synchronisation --
@@ -3784,6 +3781,9 @@ cv_status superseq_cp_par(cv_hmm* h, int64_t nseq, const int64_t* offsets, const
       const hipError_t e = cvk::launch_cp_spec_psi(W, g, nf, cs);
       if (e != hipSuccess) return set_err(CV_EDEVICE, "chain speculative batch failed: %s", hipGetErrorString(e));
     } else if (small && !beside_fwd && h->tuning.chain_spec_kernel == 0) {
+      // N <= 256 after the last forward pass (the chip is free): the serial chain kernel's
+      // layout, one sequence per workgroup and CU (A on chip, ~3.5 us per element), its path
+      // backtracked in the same workgroup
       DevBuf& d_spsi = h->chainb.spsi;
       if ((st = d_spsi.ensure((size_t)Ls * W * 2)) != CV_OK) return st;
       cvk::CpChainWgArgs g{};
