@@ -39,8 +39,8 @@ struct Tuning {
   int chain_tail = 2;          // chain_parts = 1: the small parts after the first
   int chain_tail_div = 2;      // chain_parts = 1: a small part is one forward round / this
   int chain_spec_prio = 1;     // 0: speculative batches beside a forward pass at the default issue priority
-  int chain_pin_obs = 1;       // 0: the later parts' observations by pageable copies (blit kernels)
-  int chain_pin_path = 1;      // 0: the path copy by pageable copies instead of a pinned two-chunk ring
+  int chain_pin_obs = 0;       // 1: the later parts' observations through pinned staging (measured neutral)
+  int chain_pin_path = 0;      // 1: the path copy through a pinned two-chunk ring (measured neutral)
   // ---- f64 trellis (kernels/trellis64.hip) ----
   int t64_s = 0;               // sequences per wave 2 / 4 / 6 / 8 (0: by batch)
   int t64_512 = -1;            // NP = 512 batch kernel: -1 auto, 0 never, 1 whenever supported

@@ -182,9 +182,10 @@ CV_API void cv_hmm_destroy(cv_hmm* h);
  *                         part's size as a forward round (64 sequences per CU) / chain_tail_div
  *   chain_spec_prio 1     0: the chain's speculative batches beside a forward pass at the default
  *                         issue priority (1: priority 3)
- *   chain_pin_obs 1, chain_pin_path 1   0: the parallel chain's later parts' observations / its
- *                         path copy by pageable copies (the runtime's blit kernels beside the forward
- *                         passes) instead of pinned staging (the DMA engines)
+ *   chain_pin_obs 0, chain_pin_path 0   1: the parallel chain's later parts' observations / its
+ *                         path copy through pinned staging (82 MiB of pinned host memory per handle)
+ *                         instead of the runtime's pageable copies (measured neutral; the pageable
+ *                         default keeps a first call ~20-70 ms shorter)
  *   t64_s 0               f64 trellis sequences per wave 2 / 4 / 6 / 8 (0: by batch)
  *   t64_512 / t64_1024 -1 NP = 512 / 1,024 batch kernel: -1 auto, 0 never, 1 always
  *   t64_wg 1              0: one wave per workgroup instead of eight-wave units

@@ -338,7 +338,7 @@ def test_chain_parts_schedules(gpu, n, force):
     h = cv.HMM(pi, a, b)
     sp, sobj = _serial(h, off, obs)
     for keys in ({}, {"chain_parts": 0}, {"chain_parts": 2}, {"chain_tail": 3, "chain_tail_div": 4},
-                 {"chain_pin_obs": 0, "chain_pin_path": 0}):
+                 {"chain_pin_obs": 1, "chain_pin_path": 1}):
         with h.tuned(**keys):
             (path, obj), st = _par(h, off, obs, force=force)
         assert st["parallel"], (keys, st)
