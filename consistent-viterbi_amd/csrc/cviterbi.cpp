@@ -3774,7 +3774,7 @@ cv_status superseq_cp_par(cv_hmm* h, int64_t nseq, const int64_t* offsets, const
       g.soff = d_soff.as<int64_t>();
       g.sinit = d_sinit.as<double>();
       g.nstates = N;
-      g.prio = h->tuning.chain_spec_prio != 0 ? 1 : 0;
+      g.prio = std::min(std::max(h->tuning.chain_spec_prio, 0), 3);
       g.psi = h->chainb.spsi.as<uint16_t>();
       g.last = d_slast.as<double>();
       g.path = d_spath.as<int32_t>();

@@ -55,7 +55,7 @@ struct CpSpecArgs {
   const int64_t* soff;
   const double* sinit;
   int nstates;
-  int prio;            // 1: issue priority 3
+  int prio;            // issue priority 1..3 (0: the default)
   uint16_t* psi;
   double* last;
   int32_t* path;

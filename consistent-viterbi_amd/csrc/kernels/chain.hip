@@ -563,7 +563,9 @@ __global__ __launch_bounds__(NP) void cp_spec_psi(CpSpecArgs g) {
   const int64_t b = blockIdx.x;
   const int64_t e0 = g.soff[b], T = g.soff[b + 1] - e0;
   if (T <= 0) return;  // uniform over the workgroup
-  if (g.prio) __builtin_amdgcn_s_setprio(3);
+  if (g.prio == 1) __builtin_amdgcn_s_setprio(1);
+  if (g.prio == 2) __builtin_amdgcn_s_setprio(2);
+  if (g.prio >= 3) __builtin_amdgcn_s_setprio(3);
   const int32_t* obs = g.obs + e0;
   uint16_t* psi = g.psi + e0 * NP;
   const __amdgpu_buffer_rsrc_t ra =

@@ -38,7 +38,7 @@ struct Tuning {
                                // parts of one forward round / chain_tail_div; 2: one forward round per part
   int chain_tail = 2;          // chain_parts = 1: the small parts after the first
   int chain_tail_div = 2;      // chain_parts = 1: a small part is one forward round / this
-  int chain_spec_prio = 1;     // 0: speculative batches beside a forward pass at the default issue priority
+  int chain_spec_prio = 3;     // issue priority of the speculative batches beside a forward pass (0: default)
   int chain_pin_obs = 0;       // 1: the later parts' observations through pinned staging (measured neutral)
   int chain_pin_path = 0;      // 1: the path copy through a pinned two-chunk ring (measured neutral)
   // ---- f64 trellis (kernels/trellis64.hip) ----

@@ -180,8 +180,8 @@ CV_API void cv_hmm_destroy(cv_hmm* h);
  *                         parts (each walked beside the next part's forward pass); 2: one round each
  *   chain_tail 2, chain_tail_div 2       chain_parts = 1: the number of small parts, and a small
  *                         part's size as a forward round (64 sequences per CU) / chain_tail_div
- *   chain_spec_prio 1     0: the chain's speculative batches beside a forward pass at the default
- *                         issue priority (1: priority 3)
+ *   chain_spec_prio 3     issue priority (s_setprio 1..3; 0 the default) of the parallel chain's
+ *                         speculative batches beside a forward pass
  *   chain_pin_obs 0, chain_pin_path 0   1: the parallel chain's later parts' observations / its
  *                         path copy through pinned staging (82 MiB of pinned host memory per handle)
  *                         instead of the runtime's pageable copies (measured neutral; the pageable
