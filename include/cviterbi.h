@@ -213,8 +213,9 @@ CV_API void cv_hmm_destroy(cv_hmm* h);
  * (NULL past the last). */
 /* Frees the handle's decode workspaces (delta rows, the constrained decode's and the parallel
  * chain's per-call buffers, pinned staging), which are otherwise kept grow-only between calls
- * so repeated calls do not reallocate: e.g. ~0.4 GB of chain buffers plus the 34-69 GB delta
- * workspace after a config-4-sized cv_decode_superseq_cp / cv_decode_batch.  The model tables
+ * so repeated calls do not reallocate: e.g. ~1 GB of chain buffers (observations, paths, the
+ * speculative batches' psi rows) and 18 MiB of pinned staging plus the 34-69 GB delta workspace
+ * after a config-4-sized cv_decode_superseq_cp / cv_decode_batch.  The model tables
  * stay; the next call allocates what it needs again.  Waits for the handle's streams. */
 CV_API cv_status cv_hmm_release_workspaces(cv_hmm* h);
 CV_API cv_status cv_hmm_set_tuning(cv_hmm* h, const char* key, int64_t value);
