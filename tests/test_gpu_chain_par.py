@@ -323,7 +323,7 @@ def test_chain_cert_fused_vs_pass(gpu, nseq, force):
     assert op == sobj and np.array_equal(pp, sp)
 
 
-@pytest.mark.parametrize("n,force", [(256, None), (256, 97), (100, 53)])
+@pytest.mark.parametrize("n,force", [(256, None), (256, 97), (100, 53), (150, 61), (40, 59)])
 def test_chain_parts_schedules(gpu, n, force):
     """The parallel chain decodes a batch that spans more than a forward round (64 sequences per
     CU) in parts, each part's walk beside the next part's forward (tuning key chain_parts: 1 =
@@ -331,8 +331,8 @@ def test_chain_parts_schedules(gpu, n, force):
     0 = one part), with the later parts' observations and the path copy through pinned staging or
     pageable copies (chain_pin_obs / chain_pin_path).  Every schedule returns the serial chain's
     path and objective; forced runs (every 97th sequence uncertified) put speculative batches and
-    runs on every part boundary; beside a forward the speculation runs cp_spec_psi (NP = 256 and
-    128 here)."""
+    runs on every part boundary; beside a forward the speculation runs cp_spec_psi (NP = 256,
+    192, 128 and 64 here)."""
     nseq = 40000  # > 2 rounds on 256 CUs: three parts at the default schedule
     pi, a, b, off, obs = _case(n, 31, nseq, 4, 40, seed=5100 + n, zeros=(16383, 16384, 32767), ones=(24575, 24576))
     h = cv.HMM(pi, a, b)
