@@ -76,7 +76,7 @@ run() {
     smoke) step smoke 200 python3 -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" ;;
     bench) step bench 400 python3 -u bench.py ;;
     prof)
-      (cd /tmp && step prof 400 rocprofv3 --kernel-trace --stats -d $O/prof -o prof -- python3 $R/bench.py --no-f32-extra) ;;
+      (cd /tmp && step prof 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o prof -- python3 $R/bench.py --no-f32-extra) ;;
     *) echo "unknown step $1"; return 2 ;;
   esac
 }
