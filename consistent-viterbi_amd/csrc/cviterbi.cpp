@@ -2754,9 +2754,11 @@ CV_API cv_status cv_decode_constrained_device(cv_hmm* h, int64_t nseq, const int
     if (err != hipSuccess) return set_err(CV_EDEVICE, "observation check failed: %s", hipGetErrorString(err));
     HIP_TRY(hipMemcpyAsync(&first_bad_obs, h->cs_zero.p, 8, hipMemcpyDeviceToHost, stream));
   }
+  trace_mark("device constrained: entry, observation check enqueued");
   // components checked and the constrained list built in one host pass
   std::vector<ConSeq> cs;
   const int64_t bad_comp = build_conseq_checked(nseq, offsets_host, component, ncomp, cs);
+  trace_mark("device constrained: host scan of component");
   HIP_TRY(hipStreamSynchronize(stream));  // first_bad_obs is a local the copy writes
   if (bad_comp >= 0)
     return set_err(CV_EINVAL, "component[%lld] = %d out of range [-1,%d)", (long long)bad_comp, component[bad_comp],
