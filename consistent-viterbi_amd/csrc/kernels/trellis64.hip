@@ -1847,12 +1847,21 @@ __global__ __launch_bounds__(256) void trellis_wave_f64(T64FwdArgs g) {
 #ifndef CVK_W48_PD
 #define CVK_W48_PD 4  // emission rows prefetched this many steps ahead (A/B builds: -DCVK_W48_PD=n)
 #endif
+#ifdef CVK_W48_PROBE
+// Probe build only (tools/w48_probe.py): per sequence s_memrealtime (100 MHz) after the
+// sequence's offsets, at the end, at entry, after delta_0, after the first PD-step block (0 if
+// none), HW_ID, XCC_ID, T -- written by lanes 0..7 with vector stores.
+__device__ unsigned long long cvk_w48_probe[8192][8];
+#endif
 template <bool ZI, int PD = CVK_W48_PD>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void trellis_wave48_f64(T64FwdArgs g) {
   constexpr int NPW = 64, C = 3, R = 12, LS = NPW + 4, P = 256;
   __shared__ __attribute__((aligned(16))) double dl_all[4][2][LS];     // delta_{t-1} / delta_t per wave
   __shared__ __attribute__((aligned(16))) double part_all[4][NPW][4];  // [col][rg] partial maxima
   const int lane = threadIdx.x & 63;
+#ifdef CVK_W48_PROBE
+  const unsigned long long pre = __builtin_amdgcn_s_memrealtime();
+#endif
   const int wv = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
   const int rg = lane & 3, cq = lane >> 2;
   int blk = (int)blockIdx.x;
@@ -1868,6 +1877,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void t
   if (T <= 0) return;  // the backtrack reports empty sequences
   double(*dl)[LS] = dl_all[wv];
   double(*part)[4] = part_all[wv];
+#ifdef CVK_W48_PROBE
+  const unsigned long long pr0 = __builtin_amdgcn_s_memrealtime();
+  unsigned long long prd0 = 0, prb1 = 0;
+#endif
   // Every lane runs every instruction of a step (lanes >= 48 fold columns 48..63, which no
   // partial reaches: their rows land in the 64-wide rows' padding, which the backtrack masks),
   // so no branch splits the step's memory operations and the waits before each use count only
@@ -1878,6 +1891,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void t
   const int32_t* __restrict__ obs = g.obs + e0 + vz;
   uint32_t* __restrict__ rows = reinterpret_cast<uint32_t*>(g.delta) + (e0 - g.delta_elem_base) * (2 * NPW);
   const unsigned V = (unsigned)g.nobs;
+  const int Tm1 = T - 1;
+  // Start-up: the observations of steps 0..2PD (and pi) in one batch, then A (L2), then the
+  // emissions of steps 0..PD in one batch -- the chain before step 1 is offsets -> observations
+  // -> emissions with the A loads beside it, not two observation -> emission round trips
+  // queued behind the A loads (V = 50,000 at config 2: a 25.6 MB emission table, beyond L2)
+  const unsigned ob0 = (unsigned)obs[0];
+  const double pil = ZI ? 0.0 : g.pi[lane];
+  unsigned sp[PD], so[PD];
+#pragma unroll
+  for (int k = 0; k < PD; ++k) {
+    sp[k] = (unsigned)obs[min(1 + k, Tm1)];       // observations of steps 1..PD
+    so[k] = (unsigned)obs[min(PD + 1 + k, Tm1)];  // observations of steps PD+1..2PD
+  }
   double a_reg[R * C];  // a_reg[C r + k] = A[R rg + r][C cq + k]
 #pragma unroll
   for (int r = 0; r < R; ++r) {
@@ -1896,21 +1922,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void t
     __builtin_nontemporal_store(hi_word(v), r);
     __builtin_nontemporal_store(lo_word(v), r + NPW);
   };
+  const double e0v = ZI ? 0.0 : *eaddr(ob0);
+  double pe[PD];  // emissions PD steps ahead
+#pragma unroll
+  for (int k = 0; k < PD; ++k) pe[k] = *eaddr(sp[k]);  // steps 1..PD
   {
-    const double d0 = ZI ? 0.0 : g.pi[lane] + *eaddr((unsigned)obs[0]);  // cp.rs:66-68
+    const double d0 = ZI ? 0.0 : pil + e0v;  // cp.rs:66-68
     dl[0][lane] = d0;
     __builtin_amdgcn_wave_barrier();
     put(0, d0);
-  }
-  const int Tm1 = T - 1;
-  // emissions PD steps ahead (V = 50,000 at config 2: a 25.6 MB table, beyond L2), their
-  // observations PD steps before that
-  unsigned so[PD];
-  double pe[PD];
-#pragma unroll
-  for (int k = 0; k < PD; ++k) {
-    pe[k] = *eaddr((unsigned)obs[min(1 + k, Tm1)]);  // steps 1..PD
-    so[k] = (unsigned)obs[min(PD + 1 + k, Tm1)];     // observations of steps PD+1..2PD
+#ifdef CVK_W48_PROBE
+    prd0 = __builtin_amdgcn_s_memrealtime() + (unsigned long long)(d0 == 12345.0);  // after delta_0
+#endif
   }
   auto step = [&](int t, int k) {
     const double* src = &dl[(t - 1) & 1][R * rg];
@@ -1946,13 +1969,38 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void t
   for (; t0 + PD <= T; t0 += PD) {
 #pragma unroll
     for (int k = 0; k < PD; ++k) step(t0 + k, k);
+#ifdef CVK_W48_PROBE
+    if (t0 == 1) prb1 = __builtin_amdgcn_s_memrealtime();
+#endif
   }
 #pragma unroll
   for (int k = 0; k < PD - 1; ++k)
     if (t0 + k < T) step(t0 + k, k);
   if (bad) g.status[seq] = CVK_SEQ_BADOBS;
+#ifdef CVK_W48_PROBE
+  {
+    const unsigned long long pr1 = __builtin_amdgcn_s_memrealtime();
+    const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4), xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);
+    if (lane < 8 && seq < 8192) {  // lane-indexed: a vector store per lane
+      const unsigned long long v[8] = {pr0, pr1, pre, prd0, hw, xcc, (unsigned long long)T, prb1};
+      unsigned long long x = 0;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) x = lane == i ? v[i] : x;
+      cvk_w48_probe[seq][lane] = x;
+    }
+  }
+#endif
 }
 
+#ifdef CVK_W48_PROBE
+}  // namespace
+}  // namespace cvk
+extern "C" int cvk_w48_probe_read(void* dst, size_t bytes) {
+  return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(cvk::cvk_w48_probe), bytes, 0, hipMemcpyDeviceToHost);
+}
+namespace cvk {
+namespace {
+#endif
 hipError_t launch_t64_wave(const T64FwdArgs& fa, int64_t nseq, hipStream_t stream) {
   // (a two-sequences-per-wave variant, three waves per SIMD, measured 0.153 vs 0.070 ms at
   // config 2 and was removed)
