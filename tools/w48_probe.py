@@ -1,7 +1,11 @@
 """Per-wave timeline of trellis_wave48_f64 at config 2 (probe build: CVK_W48_PROBE, loaded with
 CV_LIB_PATH=tools/_ab/lib_probe.so).  Each sequence's wave records s_memrealtime (100 MHz) and
 s_memtime at start and end, HW_ID and XCC_ID; this groups them by SIMD and prints where the
-makespan goes: the longest sequences' per-step time, alone and shared."""
+makespan goes: the longest sequences' per-step time, alone and shared.
+Build the probe library first (in this container; it travels to the GPU box with the tree):
+  make -C consistent-viterbi_amd/csrc BUILD=build_probe OUT=../../tools/_ab/lib_probe.so \
+       T64FLAGS="-fno-honor-nans -DCVK_W48_PROBE"
+(the `build_probe` objects are git- and gpurun-ignored; `tools/_ab/` is git-ignored)."""
 import ctypes
 import os
 import sys
