@@ -96,3 +96,18 @@ for i in range(len(uk)):
         alone.append(((r1[j] - last_mate) * 10, T[j]))
 print(f"longest waves running alone at their end: {len(alone)} SIMDs, median alone time"
       f" {np.median([a for a, _ in alone]) / 1e3 if alone else 0:.2f} us")
+# SIMD end time by its composition (sorted lengths of its four waves)
+comp = []
+for i in range(len(uk)):
+    m = np.where(inv == i)[0]
+    comp.append((tuple(sorted((int(T[j]) for j in m), reverse=True)), ends[i]))
+comp.sort(key=lambda c: c[1])
+print("SIMD compositions, earliest and latest ends:")
+for c, e in comp[:6] + comp[-6:]:
+    print(f"  {c}: end {e:.2f} us")
+lmax = np.array([c[0][0] for c in comp]); l2 = np.array([c[0][1] for c in comp]); en = np.array([c[1] for c in comp])
+for lo, hi in ((0, 100), (100, 116), (116, 129)):
+    for a, b in ((0, 48), (48, 80), (80, 129)):
+        sel = (lmax >= lo) & (lmax < hi) & (l2 >= a) & (l2 < b)
+        if sel.any():
+            print(f"  longest [{lo},{hi}) second [{a},{b}): {sel.sum():4d} SIMDs, end p50 {np.median(en[sel]):.2f} max {en[sel].max():.2f} us")
